@@ -1,0 +1,180 @@
+#!/usr/bin/env python3
+"""Headline benchmark: embeds/sec + top-k QPS, all-MiniLM-L6-v2 / 100M x 384 index, 1..8 MI355X.
+
+One STEP = the system's ingest+search cycle on every rank (one process per GPU):
+  1. H2D of the next synthetic tokenized batch on a copy stream (overlaps the previous search)
+  2. encode B=256 sentences x S=128 tokens with the HIP MiniLM-L6 encoder (bf16, varlen-packed)
+  3. upsert the 256 unit embeddings into this rank's HBM index shard
+  4. semantic search: the 256 new embeddings are the queries; all_gather the queries of all
+     ranks, fused MFMA scan + top-10 over the rank's shard of the 100M x 384 corpus, all_to_all
+     the partial top-k back to each query's owner and merge.
+So every step embeds 256*N sentences AND answers 256*N top-10 queries over the full 100M-row
+corpus: value = embeds/s = top-k QPS (whole job).  Per-rank work is constant in N ("weak").
+
+Data: synthetic token ids, random-init weights (real MiniLM-L6 architecture), random unit
+index rows -- there is no network for checkpoints or datasets.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = ("embeds/sec + top-k QPS, all-MiniLM-L6-v2 / 100M×384 index at 1/2/4/8 MI355X")
+DERIVED_REF_EMBEDS_PER_SEC = 225.0  # BASELINE.md derived estimate (not a published number)
+
+
+def log(info, *a):
+    if info.rank == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--seq", type=int, default=128)
+    ap.add_argument("--index-rows", type=int, default=100_000_000)
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--model", default="minilm-l6")
+    ap.add_argument("--mode", choices=["full", "embed", "search"], default="full")
+    args = ap.parse_args()
+
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+    from codename_symbiont_amd.models import get_config
+    from codename_symbiont_amd.models.encoder import HipEncoder, synthetic_batch
+    from codename_symbiont_amd.parallel import dist as D
+    from codename_symbiont_amd.parallel.sharded import ShardedSearcher
+
+    info = D.init()
+    if info.world != args.gpus:
+        log(info, f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={info.world}")
+    dev = info.device
+    torch.manual_seed(1234 + info.rank)
+    cfg = get_config(args.model)
+    B, S, K, W = args.batch, args.seq, args.steps, args.warmup
+
+    t0 = time.time()
+    enc = HipEncoder(cfg, seed=0, device=dev)
+    rows_per_rank = args.index_rows // info.world
+    extra = (K + W + 4) * B
+    shard = HbmIndexShard(cfg.hidden, rows_per_rank + extra, device=dev)
+    if args.mode != "embed":
+        shard.fill_random(rows_per_rank, seed=100 + info.rank)
+    searcher = ShardedSearcher(shard, info)
+    torch.cuda.synchronize(dev)
+    log(info, f"[bench] setup {time.time() - t0:.1f}s: {cfg.model_name}, shard {rows_per_rank} "
+              f"rows x {cfg.hidden} bf16 = {rows_per_rank * cfg.hidden * 2 / 1e9:.1f} GB/rank")
+
+    # host batches (pinned) rotated through two device buffers filled on a copy stream
+    NB = 4
+    host = [synthetic_batch(cfg, B, S, seed=1000 * info.rank + i) for i in range(NB)]
+    host = [type(h)(h.ids.pin_memory(), h.pos.pin_memory(), None, h.cu_seqlens.pin_memory(),
+                    h.max_len) for h in host]
+    dbuf = [host[0].to(dev), host[1].to(dev)]
+    copy_stream = torch.cuda.Stream(dev)
+    compute = torch.cuda.current_stream(dev)
+    copy_done = [torch.cuda.Event(), torch.cuda.Event()]
+    consumed = [torch.cuda.Event(), torch.cuda.Event()]
+    out_f32 = torch.empty(B, cfg.hidden, device=dev)
+    out_unit = torch.empty(B, cfg.hidden, dtype=torch.bfloat16, device=dev)
+    q_fixed = torch.nn.functional.normalize(torch.randn(B, cfg.hidden, device=dev), dim=-1).bfloat16()
+
+    def prefetch(i: int) -> None:
+        slot = i % 2
+        with torch.cuda.stream(copy_stream):
+            if i >= 2:
+                copy_stream.wait_event(consumed[slot])
+            h, d = host[i % NB], dbuf[slot]
+            d.ids.copy_(h.ids, non_blocking=True)
+            d.pos.copy_(h.pos, non_blocking=True)
+            d.cu_seqlens.copy_(h.cu_seqlens, non_blocking=True)
+            d.max_len = h.max_len
+            copy_done[slot].record(copy_stream)
+
+    def step(i: int, ev=None) -> None:
+        slot = i % 2
+        if ev:
+            ev[0].record(compute)
+        if args.mode != "search":
+            compute.wait_event(copy_done[slot])
+            enc.forward_packed(dbuf[slot], out_f32, out_unit)
+            consumed[slot].record(compute)
+            prefetch(i + 1)
+            shard.append_unit(out_unit)
+            q = out_unit
+        else:
+            q = q_fixed
+        if ev:
+            ev[1].record(compute)
+        if args.mode != "embed":
+            searcher.search(q, args.k)
+        if ev:
+            ev[2].record(compute)
+
+    prefetch(0)
+    for i in range(W):
+        step(i)
+    torch.cuda.synchronize(dev)
+    D.barrier(info)
+    torch.cuda.synchronize(dev)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(K)]
+    t_start = time.perf_counter()
+    for j in range(K):
+        step(W + j, evs[j])
+    torch.cuda.synchronize(dev)
+    D.barrier(info)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t_start
+    elapsed = D.allreduce_max(info, elapsed)
+    e_ms = sum(a.elapsed_time(b) for a, b, _ in evs) / K
+    s_ms = sum(b.elapsed_time(c) for _, b, c in evs) / K
+
+    ms = elapsed * 1000.0 / K
+    total = B * info.world * K / elapsed
+    if info.rank == 0:
+        res = {
+            "metric": METRIC,
+            "value": round(total, 2),
+            "unit": "embeds/s (whole job; every embedded sentence is also answered as a top-10 "
+                    "query over the 100M x 384 corpus, so this equals top-k QPS)"
+                    if args.mode == "full" else ("embeds/s" if args.mode == "embed" else "queries/s"),
+            "n_gpus": info.world,
+            "steps": K,
+            "warmup": W,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic token ids, random-init weights, random unit index rows",
+            "config": {
+                "model": "all-MiniLM-L6-v2", "global_batch": B * info.world, "seq_len": S,
+                "parallelism": f"dp{info.world}+index_shard{info.world}",
+                "index_rows": args.index_rows, "dim": cfg.hidden, "top_k": args.k,
+                "mode": args.mode,
+            },
+            "embeds_per_sec": round(total, 2) if args.mode != "search" else 0.0,
+            "topk_qps": round(total, 2) if args.mode != "embed" else 0.0,
+            "embed_ms_per_step_rank0": round(e_ms, 3),
+            "search_ms_per_step_rank0": round(s_ms, 3),
+            "vs_derived_reference_estimate": round(total / DERIVED_REF_EMBEDS_PER_SEC, 1),
+        }
+        print(json.dumps(res), flush=True)
+    D.shutdown(info)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,220 @@
+"""In-HBM brute-force cosine index shard (the Qdrant replacement of vector_memory_service).
+
+Reference behaviour (services/vector_memory_service/src/main.rs):
+* collection ``symbiont_document_embeddings``, Distance::Cosine (:19-22, :36): scores are cosine
+  similarities in [-1, 1], results sorted descending, fewer than k if the collection is small;
+* upsert one point per sentence with a fresh UUIDv4 id and a 6-field payload (:142-177).
+
+Layout here: one contiguous bf16 slab ``rows[capacity_pad, D]`` of UNIT vectors (cosine ==
+dot product), sized up front for the shard (288 GB of HBM per MI355X holds 100M x 384 bf16 =
+76.8 GB with room to spare), rows appended in place; the fused HIP scan (``_hip.index_scan``)
+streams the slab once per query batch and never materialises scores.  Point ids and payloads
+live host-side in a columnar ``PayloadStore`` indexed by row.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+
+TILE_ROWS = 32
+
+
+def _round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+@dataclass
+class Payload:
+    original_document_id: str = ""
+    source_url: str = ""
+    sentence_text: str = ""
+    sentence_order: int = 0
+    model_name: str = ""
+    processed_at_ms: int = 0
+
+
+class PayloadStore:
+    """Columnar host store: row -> (point id, payload fields).  Rows without payload are allowed
+    (synthetic benchmark rows) and decode to the reference's defaults ("" / 0, main.rs:337-390)."""
+
+    FIELDS = ("original_document_id", "source_url", "sentence_text", "sentence_order",
+              "model_name", "processed_at_ms")
+
+    def __init__(self):
+        self.point_ids: list[str | None] = []
+        self.cols: dict[str, list] = {f: [] for f in self.FIELDS}
+        self.id_to_row: dict[str, int] = {}
+
+    def __len__(self):
+        return len(self.point_ids)
+
+    def extend_empty(self, n: int) -> None:
+        self.point_ids.extend([None] * n)
+        for f in self.FIELDS:
+            self.cols[f].extend([None] * n)
+
+    def set(self, row: int, point_id: str | None, payload: Payload | None) -> None:
+        old = self.point_ids[row]
+        if old is not None and self.id_to_row.get(old) == row:
+            del self.id_to_row[old]
+        self.point_ids[row] = point_id
+        if point_id is not None:
+            self.id_to_row[point_id] = row
+        for f in self.FIELDS:
+            self.cols[f][row] = getattr(payload, f) if payload is not None else None
+
+    def get(self, row: int) -> tuple[str | None, Payload]:
+        vals = {}
+        for f in self.FIELDS:
+            v = self.cols[f][row]
+            if v is None:
+                v = 0 if f in ("sentence_order", "processed_at_ms") else ""
+            vals[f] = v
+        return self.point_ids[row], Payload(**vals)
+
+
+class HbmIndexShard:
+    def __init__(self, dim: int, capacity: int, device="cuda", kmax: int = 16):
+        self.dim = dim
+        self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self.capacity = int(capacity)
+        self.rows = torch.empty(_round_up(max(self.capacity, 1), TILE_ROWS), dim,
+                                dtype=torch.bfloat16, device=self.device)
+        self.count = 0
+        self.payloads = PayloadStore()
+        self._ws: dict = {}
+
+    # ------------------------------------------------------------------ inserts
+    def _reserve(self, n: int) -> int:
+        if self.count + n > self.capacity:
+            raise MemoryError(f"index shard full ({self.count}+{n} > {self.capacity})")
+        r0 = self.count
+        self.count += n
+        self.payloads.extend_empty(n)
+        return r0
+
+    def append_unit(self, unit_bf16: torch.Tensor) -> int:
+        """Append already unit-norm bf16 rows (e.g. the encoder's pooled+normalised output)."""
+        n = unit_bf16.shape[0]
+        r0 = self._reserve(n)
+        self.rows[r0:r0 + n].copy_(unit_bf16, non_blocking=True)
+        return r0
+
+    def append_f32(self, vecs: torch.Tensor) -> int:
+        """Append raw float vectors (wire embeddings); normalised + cast by the l2norm_cast kernel."""
+        n = vecs.shape[0]
+        if vecs.shape[1] != self.dim:
+            raise ValueError(f"dimension mismatch: got {vecs.shape[1]}, index is {self.dim}")
+        r0 = self._reserve(n)
+        self.write_f32(r0, vecs)
+        return r0
+
+    def write_f32(self, r0: int, vecs: torch.Tensor) -> None:
+        vecs = vecs.to(self.device, torch.float32).contiguous()
+        if self.device.type == "cuda":
+            from ..ops.kernels import l2norm_cast
+
+            l2norm_cast(vecs, self.rows[r0:r0 + vecs.shape[0]])
+        else:
+            self.rows[r0:r0 + vecs.shape[0]] = torch.nn.functional.normalize(vecs, dim=-1).bfloat16()
+
+    def upsert(self, point_ids: list[str], vecs: torch.Tensor, payloads: list[Payload]) -> list[int]:
+        """Qdrant-style upsert: existing ids are overwritten in place, new ids appended."""
+        rows = []
+        new_pos = [i for i, pid in enumerate(point_ids) if pid not in self.payloads.id_to_row]
+        old_pos = [i for i, pid in enumerate(point_ids) if pid in self.payloads.id_to_row]
+        out = [0] * len(point_ids)
+        if new_pos:
+            r0 = self.append_f32(vecs[new_pos])
+            for j, i in enumerate(new_pos):
+                out[i] = r0 + j
+        for i in old_pos:
+            r = self.payloads.id_to_row[point_ids[i]]
+            self.write_f32(r, vecs[i:i + 1])
+            out[i] = r
+        for i, r in enumerate(out):
+            self.payloads.set(r, point_ids[i], payloads[i])
+        rows.extend(out)
+        return rows
+
+    def fill_random(self, n: int, seed: int = 0, chunk: int = 1 << 20) -> None:
+        """Synthetic unit rows straight into HBM (benchmark corpus; no payloads)."""
+        g = torch.Generator(device=self.device)
+        g.manual_seed(seed)
+        r0 = self._reserve(n)
+        for s in range(0, n, chunk):
+            e = min(n, s + chunk)
+            x = torch.randn(e - s, self.dim, generator=g, device=self.device, dtype=torch.float32)
+            if self.device.type == "cuda":
+                from ..ops.kernels import l2norm_cast
+
+                l2norm_cast(x, self.rows[r0 + s:r0 + e])
+            else:
+                self.rows[r0 + s:r0 + e] = torch.nn.functional.normalize(x, dim=-1).bfloat16()
+
+    # ------------------------------------------------------------------ search
+    def search(self, q_unit: torch.Tensor, k: int, n_cus: int | None = None):
+        """Top-k cosine over this shard for unit bf16 queries [NQ, D].
+
+        Returns (scores f32 [NQ, k], rows int32 [NQ, k]); missing slots are (-inf, -1)."""
+        NQ = q_unit.shape[0]
+        k = int(k)
+        if NQ == 0 or k <= 0:
+            return (torch.empty(NQ, max(k, 0), device=self.device),
+                    torch.empty(NQ, max(k, 0), dtype=torch.int32, device=self.device))
+        if self.device.type != "cuda" or k > 32:
+            return self._search_matmul(q_unit, k)
+        from ..ops._ext import hip, stream_handle
+
+        q_unit = q_unit.to(torch.bfloat16).contiguous()
+        kmax = 16 if k <= 16 else 32
+        lists, qpb = hip().topk_geometry(self.dim, kmax)
+        n_qblk = math.ceil(NQ / qpb)
+        if n_cus is None:
+            n_cus = torch.cuda.get_device_properties(self.device).multi_processor_count
+        n = self.count
+        n_rblk = max(1, min(math.ceil(n / (TILE_ROWS * 16)), max(1, round(n_cus / n_qblk))))
+        rows_per_blk = _round_up(max(1, math.ceil(n / n_rblk)), TILE_ROWS)
+        n_rblk = max(1, math.ceil(n / rows_per_blk))
+        ncand = n_rblk * lists * kmax
+        key = (NQ, ncand)
+        ws = self._ws.get(key)
+        if ws is None:
+            ws = (torch.empty(NQ, ncand, device=self.device),
+                  torch.empty(NQ, ncand, dtype=torch.int32, device=self.device))
+            self._ws = {key: ws}
+        cs, ci = ws
+        out_s = torch.empty(NQ, k, device=self.device)
+        out_i = torch.empty(NQ, k, dtype=torch.int32, device=self.device)
+        st = stream_handle(self.device)
+        h = hip()
+        h.index_scan(self.rows.data_ptr(), n, self.dim, rows_per_blk, n_rblk, q_unit.data_ptr(),
+                     NQ, kmax, cs.data_ptr(), ci.data_ptr(), st)
+        h.topk_merge(cs.data_ptr(), ci.data_ptr(), NQ, ncand, kmax, k, out_s.data_ptr(),
+                     out_i.data_ptr(), 0, 0, st)
+        return out_s, out_i
+
+    def _search_matmul(self, q_unit: torch.Tensor, k: int, chunk: int = 1 << 22):
+        """Chunked exact fallback (CPU backend, or k > 32 on GPU)."""
+        NQ = q_unit.shape[0]
+        best_s = torch.full((NQ, k), -math.inf, device=self.device)
+        best_i = torch.full((NQ, k), -1, dtype=torch.int64, device=self.device)
+        q = q_unit.to(self.device).float()
+        for s in range(0, self.count, chunk):
+            e = min(self.count, s + chunk)
+            sc = q @ self.rows[s:e].float().t()
+            kk = min(k, e - s)
+            ts, ti = torch.topk(sc, kk, dim=1)
+            cat_s = torch.cat([best_s, ts], 1)
+            cat_i = torch.cat([best_i, ti + s], 1)
+            best_s, idx = torch.topk(cat_s, k, dim=1)
+            best_i = torch.gather(cat_i, 1, idx)
+        best_i = torch.where(torch.isfinite(best_s), best_i, torch.full_like(best_i, -1))
+        return best_s, best_i.to(torch.int32)
+
+    def unit_rows(self) -> torch.Tensor:
+        return self.rows[:self.count]

@@ -1,0 +1,188 @@
+"""Sentence-transformer encoder: packed varlen batches through the native HIP runtime.
+
+Reference hot path (replaced): EmbeddingGenerator::generate_sentence_embeddings
+(services/preprocessing_service/src/embedding_generator.rs:134-223) -- chunks of 8, each sentence
+padded to 514 tokens, F32 candle BertModel, mask-weighted mean pool, synchronous D2H per chunk.
+
+Here:
+* sentences are packed back to back (``cu_seqlens``), so compute scales with real tokens;
+* one ``EncoderRuntime.forward`` call (C++) issues the whole network on the current HIP stream;
+* batches are formed by a token budget, not a fixed count of 8;
+* H2D of the next batch's token ids can overlap the current forward (see ``EncodePipeline``).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from ..ops import reference as R
+from .config import EncoderConfig
+from .weights import load_params, to_device
+
+
+@dataclass
+class PackedBatch:
+    ids: torch.Tensor        # int32 [T]
+    pos: torch.Tensor        # int32 [T]
+    type_ids: torch.Tensor | None
+    cu_seqlens: torch.Tensor  # int32 [B+1]
+    max_len: int
+
+    @property
+    def num_seqs(self) -> int:
+        return self.cu_seqlens.numel() - 1
+
+    @property
+    def num_tokens(self) -> int:
+        return self.ids.numel()
+
+    def to(self, device, non_blocking=False) -> "PackedBatch":
+        mv = lambda t: None if t is None else t.to(device, non_blocking=non_blocking)  # noqa: E731
+        return PackedBatch(mv(self.ids), mv(self.pos), mv(self.type_ids), mv(self.cu_seqlens),
+                           self.max_len)
+
+
+def _resolve(device) -> torch.device:
+    d = torch.device(device)
+    if d.type == "cuda" and d.index is None:
+        d = torch.device("cuda", torch.cuda.current_device())
+    return d
+
+
+def pack_token_ids(token_lists, cfg: EncoderConfig, pin: bool = False) -> PackedBatch:
+    """Concatenate per-sentence id lists into one varlen batch (no padding anywhere)."""
+    lens = np.fromiter((len(t) for t in token_lists), dtype=np.int64, count=len(token_lists))
+    cu = np.zeros(len(token_lists) + 1, dtype=np.int32)
+    np.cumsum(lens, out=cu[1:])
+    T = int(cu[-1])
+    ids = np.empty(T, dtype=np.int32)
+    pos = np.empty(T, dtype=np.int32)
+    for i, t in enumerate(token_lists):
+        s = cu[i]
+        ids[s:s + len(t)] = t
+        pos[s:s + len(t)] = np.arange(cfg.position_offset, cfg.position_offset + len(t),
+                                      dtype=np.int32)
+    mk = lambda a: torch.from_numpy(a).pin_memory() if pin else torch.from_numpy(a)  # noqa: E731
+    return PackedBatch(mk(ids), mk(pos), None, mk(cu), int(lens.max()) if len(lens) else 0)
+
+
+def synthetic_batch(cfg: EncoderConfig, batch: int, seq_len: int, seed: int = 0,
+                    varlen: bool = False) -> PackedBatch:
+    """Random token ids with [CLS] ... [SEP] framing (ids 101/102 for BERT vocabularies)."""
+    rng = np.random.default_rng(seed)
+    if varlen:
+        lens = rng.integers(max(4, seq_len // 4), seq_len + 1, size=batch)
+    else:
+        lens = np.full(batch, seq_len)
+    toks = []
+    for L in lens:
+        t = rng.integers(1000, cfg.vocab_size, size=int(L)).astype(np.int32)
+        t[0], t[-1] = (101, 102) if cfg.vocab_size > 30000 and cfg.pad_token_id == 0 else (0, 2)
+        toks.append(t)
+    return pack_token_ids(toks, cfg)
+
+
+class HipEncoder:
+    """bf16 weights on device + the native C++ ``EncoderRuntime`` (gfx950 kernels)."""
+
+    backend = "hip"
+
+    def __init__(self, cfg: EncoderConfig, params: dict | None = None, device="cuda", seed=0):
+        from ..ops._ext import hip
+
+        self.cfg = cfg
+        self.device = _resolve(device)
+        if params is None:
+            params = load_params(cfg, seed=seed, device=self.device)
+        self.params = to_device(params, self.device, mat_dtype=torch.bfloat16)
+        p = self.params
+        self.rt = hip().EncoderRuntime(cfg.hidden, cfg.heads, cfg.ffn, float(cfg.ln_eps),
+                                       p["wemb"].data_ptr(), p["pemb"].data_ptr(),
+                                       p["temb"].data_ptr(), p["eln_g"].data_ptr(),
+                                       p["eln_b"].data_ptr())
+        for L in p["layers"]:
+            self.rt.add_layer([L[k].data_ptr() for k in (
+                "wqkv", "bqkv", "wo", "bo", "ln1_g", "ln1_b", "wi", "bi", "wo2", "bo2", "ln2_g",
+                "ln2_b")])
+        self._ws_tokens = 0
+        self._ws: list[torch.Tensor] = []
+
+    def _workspace(self, T: int) -> list[int]:
+        if T > self._ws_tokens:
+            cap = max(T, int(self._ws_tokens * 1.5), 4096)
+            H, F = self.cfg.hidden, self.cfg.ffn
+            mk = lambda n: torch.empty(cap, n, dtype=torch.bfloat16, device=self.device)  # noqa
+            self._ws = [mk(H), mk(H), mk(3 * H), mk(H), mk(F), mk(H)]
+            self._ws_tokens = cap
+        return [t.data_ptr() for t in self._ws]
+
+    def last_hidden(self) -> torch.Tensor:
+        return self._ws[0]
+
+    def forward_packed(self, b: PackedBatch, out_f32: torch.Tensor | None = None,
+                       out_unit: torch.Tensor | None = None, pool: bool = True):
+        """Encode a device-resident packed batch.  Returns (pooled_f32 [B,H], unit_bf16 [B,H])."""
+        T, B = b.num_tokens, b.num_seqs
+        if T == 0:
+            z = torch.zeros(0, self.cfg.hidden, device=self.device)
+            return z, z.bfloat16()
+        for t in (b.ids, b.pos, b.cu_seqlens):
+            if t.device != self.device or t.dtype != torch.int32:
+                raise ValueError("packed batch must be int32 on the encoder device")
+        if b.max_len > self.cfg.max_position - self.cfg.position_offset:
+            raise ValueError("sequence longer than the position table")
+        ws = self._workspace(T)
+        H = self.cfg.hidden
+        if pool:
+            if out_f32 is None:
+                out_f32 = torch.empty(B, H, dtype=torch.float32, device=self.device)
+            if out_unit is None:
+                out_unit = torch.empty(B, H, dtype=torch.bfloat16, device=self.device)
+        self.rt.forward(b.ids.data_ptr(), b.pos.data_ptr(),
+                        0 if b.type_ids is None else b.type_ids.data_ptr(),
+                        b.cu_seqlens.data_ptr(), T, B, int(b.max_len), ws,
+                        0 if self.cfg.pooling == "mean" else 1, 1 if self.cfg.normalize else 0,
+                        out_f32.data_ptr() if pool else 0, out_unit.data_ptr() if pool else 0,
+                        torch.cuda.current_stream(self.device).cuda_stream)
+        return out_f32, out_unit
+
+    def encode(self, token_lists) -> torch.Tensor:
+        b = pack_token_ids(token_lists, self.cfg).to(self.device)
+        return self.forward_packed(b)[0]
+
+
+class TorchEncoder:
+    """fp32 PyTorch execution of the same network (CPU backend / numerics oracle)."""
+
+    backend = "torch"
+
+    def __init__(self, cfg: EncoderConfig, params: dict | None = None, device="cpu", seed=0):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        if params is None:
+            params = load_params(cfg, seed=seed, device="cpu")
+        self.params = to_device(params, self.device)
+
+    @torch.no_grad()
+    def forward_packed(self, b: PackedBatch, out_f32=None, out_unit=None, pool=True):
+        b = b.to(self.device)
+        h = R.encoder_ref(self.params, self.cfg, b.ids, b.pos, b.type_ids, b.cu_seqlens)
+        self._last = h
+        pooled = R.pool_ref(h, b.cu_seqlens, self.cfg.pooling, self.cfg.normalize)
+        unit = torch.nn.functional.normalize(pooled, dim=-1)
+        return pooled, unit.to(torch.bfloat16)
+
+    def last_hidden(self):
+        return self._last
+
+    def encode(self, token_lists) -> torch.Tensor:
+        return self.forward_packed(pack_token_ids(token_lists, self.cfg))[0]
+
+
+def make_encoder(cfg: EncoderConfig, force_cpu: bool = False, seed: int = 0, device=None):
+    """GPU present -> HIP encoder (extension mandatory); otherwise the fp32 CPU backend."""
+    if not force_cpu and torch.cuda.is_available():
+        return HipEncoder(cfg, seed=seed, device=device or "cuda")
+    return TorchEncoder(cfg, seed=seed)

@@ -1,0 +1,134 @@
+"""Typed torch-tensor front-ends for the CDNA4 HIP kernels.
+
+Each wrapper validates shapes/dtypes/devices on the host BEFORE launching (a malformed launch of a
+hand-written kernel can fault the GPU), then calls the native launcher with raw pointers on the
+current HIP stream.  Numerics of every op are pinned against the fp32 PyTorch oracles in
+``codename_symbiont_amd.ops.reference`` by ``tests/test_kernels_gpu.py``.
+"""
+from __future__ import annotations
+
+import torch
+
+from ._ext import hip, stream_handle
+
+EPI_BIAS, EPI_GELU, EPI_RES, EPI_RES_LN = 0, 1, 2, 3
+SUPPORTED_H = (384, 768, 1024)
+
+
+def _ptr(t: torch.Tensor | None) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def _chk(t: torch.Tensor, dtype: torch.dtype, name: str, ndim: int | None = None) -> None:
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_cuda:
+        raise ValueError(f"{name}: must be a device tensor")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    if ndim is not None and t.dim() != ndim:
+        raise ValueError(f"{name}: expected {ndim}-d, got {tuple(t.shape)}")
+
+
+def embed_ln(ids, pos, type_ids, wemb, pemb, temb, gamma, beta, eps, out=None):
+    T = ids.numel()
+    H = wemb.shape[1]
+    if H not in SUPPORTED_H:
+        raise ValueError(f"hidden {H} unsupported")
+    for t, n in ((ids, "ids"), (pos, "pos")):
+        _chk(t, torch.int32, n, 1)
+    if type_ids is not None:
+        _chk(type_ids, torch.int32, "type_ids", 1)
+    for t, n in ((wemb, "wemb"), (pemb, "pemb"), (temb, "temb")):
+        _chk(t, torch.bfloat16, n, 2)
+    _chk(gamma, torch.float32, "gamma", 1)
+    _chk(beta, torch.float32, "beta", 1)
+    if out is None:
+        out = torch.empty(T, H, dtype=torch.bfloat16, device=ids.device)
+    hip().embed_ln(_ptr(ids), _ptr(pos), _ptr(type_ids), _ptr(wemb), _ptr(pemb), _ptr(temb),
+                   _ptr(gamma), _ptr(beta), float(eps), _ptr(out), T, H, stream_handle())
+    return out
+
+
+def add_ln(x, res, gamma, beta, eps, out=None):
+    _chk(x, torch.bfloat16, "x", 2)
+    T, H = x.shape
+    if H not in SUPPORTED_H:
+        raise ValueError(f"hidden {H} unsupported")
+    if res is not None:
+        _chk(res, torch.bfloat16, "res", 2)
+        assert res.shape == x.shape
+    if out is None:
+        out = torch.empty_like(x)
+    hip().add_ln(_ptr(x), _ptr(res), _ptr(gamma), _ptr(beta), float(eps), _ptr(out), T, H,
+                 stream_handle())
+    return out
+
+
+def gemm(a, w, bias, epi=EPI_BIAS, residual=None, gamma=None, beta=None, eps=1e-12, out=None):
+    """out = epi(a @ w.T + bias) with a:[M,K] bf16, w:[N,K] bf16, bias:[N] fp32."""
+    _chk(a, torch.bfloat16, "a", 2)
+    _chk(w, torch.bfloat16, "w", 2)
+    _chk(bias, torch.float32, "bias", 1)
+    M, K = a.shape
+    N, K2 = w.shape
+    if K != K2:
+        raise ValueError(f"K mismatch {K} vs {K2}")
+    if K % 64:
+        raise ValueError("K must be a multiple of 64")
+    if epi == EPI_RES_LN:
+        if N != 384:
+            raise ValueError("fused LayerNorm epilogue needs N == 384 (use EPI_RES + add_ln)")
+    elif N % 128:
+        raise ValueError("N must be a multiple of 128")
+    if epi in (EPI_RES, EPI_RES_LN):
+        _chk(residual, torch.bfloat16, "residual", 2)
+        assert residual.shape == (M, N)
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
+    hip().gemm(epi, _ptr(a), K, _ptr(w), K, _ptr(bias), _ptr(residual), N, _ptr(gamma),
+               _ptr(beta), float(eps), _ptr(out), N, M, N, K, stream_handle())
+    return out
+
+
+def attention(qkv, cu_seqlens, max_len, n_heads, head_dim, out=None):
+    """Varlen attention over packed [T, 3H] QKV rows -> [T, H]."""
+    _chk(qkv, torch.bfloat16, "qkv", 2)
+    _chk(cu_seqlens, torch.int32, "cu_seqlens", 1)
+    T, H3 = qkv.shape
+    H = n_heads * head_dim
+    if H3 != 3 * H or head_dim not in (32, 64):
+        raise ValueError("bad attention geometry")
+    B = cu_seqlens.numel() - 1
+    if out is None:
+        out = torch.empty(T, H, dtype=torch.bfloat16, device=qkv.device)
+    hip().attention(_ptr(qkv), H3, _ptr(cu_seqlens), B, int(max_len), n_heads, head_dim,
+                    _ptr(out), H, stream_handle())
+    return out
+
+
+def pool(hidden, cu_seqlens, mode="mean", normalize=False, want_normed_bf16=True):
+    """Returns (pooled_f32 [B,H], unit_bf16 [B,H] or None)."""
+    _chk(hidden, torch.bfloat16, "hidden", 2)
+    _chk(cu_seqlens, torch.int32, "cu_seqlens", 1)
+    T, H = hidden.shape
+    B = cu_seqlens.numel() - 1
+    out = torch.empty(B, H, dtype=torch.float32, device=hidden.device)
+    normed = torch.empty(B, H, dtype=torch.bfloat16, device=hidden.device) if want_normed_bf16 else None
+    hip().pool(_ptr(hidden), _ptr(cu_seqlens), B, H, 0 if mode == "mean" else 1,
+               1 if normalize else 0, _ptr(out), _ptr(normed), stream_handle())
+    return out, normed
+
+
+def l2norm_cast(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Unit-normalise f32 rows into bf16 rows (out may be a row-slice of an index slab)."""
+    _chk(x, torch.float32, "x", 2)
+    n, D = x.shape
+    if D % 4:
+        raise ValueError("D must be a multiple of 4")
+    if out is None:
+        out = torch.empty(n, D, dtype=torch.bfloat16, device=x.device)
+    if out.dtype != torch.bfloat16 or out.shape[0] < n or out.shape[1] != D or out.stride(1) != 1:
+        raise ValueError("bad l2norm_cast output")
+    hip().l2norm_cast(_ptr(x), _ptr(out), n, D, out.stride(0), stream_handle())
+    return out

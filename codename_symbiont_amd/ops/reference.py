@@ -1,0 +1,97 @@
+"""Plain-PyTorch fp32 oracles for every HIP kernel (and the CPU execution backend).
+
+These are deliberately written as the straightforward textbook math of the reference pipeline:
+BERT embeddings + LayerNorm, per-layer self-attention / GELU-FFN with post-LN residuals, and the
+masked mean pool of services/preprocessing_service/src/embedding_generator.rs:201-207
+(sum(h * mask) / (sum(mask) + 1e-9)).  They operate on the same packed (varlen) layout as the
+HIP kernels so tests compare like with like.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+
+def embed_ln_ref(ids, pos, type_ids, wemb, pemb, temb, gamma, beta, eps):
+    x = wemb.float()[ids.long()] + pemb.float()[pos.long()]
+    tt = type_ids.long() if type_ids is not None else torch.zeros_like(ids, dtype=torch.long)
+    x = x + temb.float()[tt]
+    return F.layer_norm(x, (x.shape[-1],), gamma.float(), beta.float(), eps)
+
+
+def add_ln_ref(x, res, gamma, beta, eps):
+    y = x.float() + (res.float() if res is not None else 0.0)
+    return F.layer_norm(y, (y.shape[-1],), gamma.float(), beta.float(), eps)
+
+
+def gemm_ref(a, w, bias, epi=0, residual=None, gamma=None, beta=None, eps=1e-12):
+    y = a.float() @ w.float().t() + bias.float()
+    if epi == 1:
+        y = F.gelu(y)  # erf form, as BERT
+    elif epi == 2:
+        y = y + residual.float()
+    elif epi == 3:
+        y = F.layer_norm(y + residual.float(), (y.shape[-1],), gamma.float(), beta.float(), eps)
+    return y
+
+
+def attention_ref(qkv, cu_seqlens, n_heads, head_dim):
+    """Varlen bidirectional attention over packed [T, 3H] rows -> [T, H] (fp32)."""
+    H = n_heads * head_dim
+    qkv = qkv.float()
+    out = torch.empty(qkv.shape[0], H, dtype=torch.float32, device=qkv.device)
+    cu = cu_seqlens.tolist()
+    for b in range(len(cu) - 1):
+        s, e = cu[b], cu[b + 1]
+        if e <= s:
+            continue
+        blk = qkv[s:e]
+        q = blk[:, :H].view(-1, n_heads, head_dim).transpose(0, 1)
+        k = blk[:, H:2 * H].view(-1, n_heads, head_dim).transpose(0, 1)
+        v = blk[:, 2 * H:].view(-1, n_heads, head_dim).transpose(0, 1)
+        p = torch.softmax(q @ k.transpose(1, 2) / math.sqrt(head_dim), dim=-1)
+        out[s:e] = (p @ v).transpose(0, 1).reshape(e - s, H)
+    return out
+
+
+def pool_ref(hidden, cu_seqlens, mode="mean", normalize=False):
+    h = hidden.float()
+    cu = cu_seqlens.tolist()
+    outs = []
+    for b in range(len(cu) - 1):
+        s, e = cu[b], cu[b + 1]
+        if mode == "cls":
+            v = h[s] if e > s else torch.zeros(h.shape[1], device=h.device)
+        else:
+            v = h[s:e].sum(0) / (float(e - s) + 1e-9)
+        outs.append(v)
+    out = torch.stack(outs) if outs else torch.zeros(0, h.shape[1], device=h.device)
+    if normalize:
+        out = F.normalize(out, dim=-1)
+    return out
+
+
+def encoder_ref(params: dict, cfg, ids, pos, type_ids, cu_seqlens):
+    """Full fp32 encoder forward on packed tokens -> last hidden state [T, H]."""
+    H, nh = cfg.hidden, cfg.heads
+    hd = H // nh
+    h = embed_ln_ref(ids, pos, type_ids, params["wemb"], params["pemb"], params["temb"],
+                     params["eln_g"], params["eln_b"], cfg.ln_eps)
+    for L in params["layers"]:
+        qkv = h @ L["wqkv"].float().t() + L["bqkv"].float()
+        ctx = attention_ref(qkv, cu_seqlens, nh, hd)
+        a = ctx @ L["wo"].float().t() + L["bo"].float()
+        h2 = F.layer_norm(a + h, (H,), L["ln1_g"].float(), L["ln1_b"].float(), cfg.ln_eps)
+        f = F.gelu(h2 @ L["wi"].float().t() + L["bi"].float())
+        o = f @ L["wo2"].float().t() + L["bo2"].float()
+        h = F.layer_norm(o + h2, (H,), L["ln2_g"].float(), L["ln2_b"].float(), cfg.ln_eps)
+    return h
+
+
+def topk_ref(index_rows: torch.Tensor, queries: torch.Tensor, k: int):
+    """Exact cosine top-k of unit rows (fp32 math on the same bf16 data)."""
+    s = queries.float() @ index_rows.float().t()
+    k = min(k, index_rows.shape[0])
+    return torch.topk(s, k, dim=1)

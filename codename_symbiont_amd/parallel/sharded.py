@@ -1,0 +1,67 @@
+"""Corpus-sharded top-k search across the GPUs of one node (RCCL over xGMI).
+
+Replaces Qdrant's single-node HNSW (services/vector_memory_service/src/main.rs:261-308, which has
+``shard_number: None`` at :50) with the retrieval analogue of context parallelism:
+
+    queries of every rank --all_gather--> every rank scans ITS shard with the fused MFMA kernel
+    --> per-rank top-k [world*nq, k] --all_to_all--> each query's owner --> k-way merge.
+
+Message sizes are tiny (nq x D bf16 queries, nq x k x (f32+i64) results) and xGMI is a full mesh
+of point-to-point links, so all_gather / all_to_all (direct, α-dominated) are used and
+all_reduce is avoided entirely.  Global point ids are ``rank << 40 | row``.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from ..index.shard import HbmIndexShard
+from .dist import DistInfo
+
+RANK_SHIFT = 40
+
+
+def encode_gid(rank: int, rows: torch.Tensor) -> torch.Tensor:
+    r = rows.long()
+    return torch.where(r >= 0, (rank << RANK_SHIFT) | r, torch.full_like(r, -1))
+
+
+def decode_gid(gid: int) -> tuple[int, int]:
+    return gid >> RANK_SHIFT, gid & ((1 << RANK_SHIFT) - 1)
+
+
+class ShardedSearcher:
+    def __init__(self, shard: HbmIndexShard, info: DistInfo, group=None):
+        self.shard = shard
+        self.info = info
+        self.group = group
+        # gloo has no bf16 collectives on every build: ship queries as f32 there
+        self.wire_dtype = torch.bfloat16 if info.backend == "nccl" else torch.float32
+
+    def search(self, q_local: torch.Tensor, k: int):
+        """Every rank calls this collectively with its own [nq, D] unit queries (same nq on all
+        ranks).  Returns (scores f32 [nq, k], global ids int64 [nq, k]) for the LOCAL queries."""
+        info = self.info
+        if info.world == 1:
+            s, r = self.shard.search(q_local, k)
+            return s, encode_gid(0, r)
+        nq, D = q_local.shape
+        q_send = q_local.to(self.wire_dtype).contiguous()
+        q_all = torch.empty(info.world * nq, D, dtype=self.wire_dtype, device=q_send.device)
+        dist.all_gather_into_tensor(q_all, q_send, group=self.group)
+        s, r = self.shard.search(q_all.to(torch.bfloat16), k)
+        gid = encode_gid(info.rank, r)
+        s_recv = torch.empty_like(s)
+        g_recv = torch.empty_like(gid)
+        dist.all_to_all_single(s_recv, s.contiguous(), group=self.group)
+        dist.all_to_all_single(g_recv, gid.contiguous(), group=self.group)
+        return merge_ranked(s_recv.view(info.world, nq, k), g_recv.view(info.world, nq, k), k)
+
+
+def merge_ranked(scores: torch.Tensor, gids: torch.Tensor, k: int):
+    """[world, nq, k] per-rank sorted lists -> [nq, k] global top-k (ties: lower rank first)."""
+    W, nq, kk = scores.shape
+    s = scores.permute(1, 0, 2).reshape(nq, W * kk)
+    g = gids.permute(1, 0, 2).reshape(nq, W * kk)
+    top_s, idx = torch.topk(s, min(k, W * kk), dim=1, sorted=True)
+    return top_s, torch.gather(g, 1, idx)

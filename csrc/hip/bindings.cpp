@@ -1,0 +1,200 @@
+// Python bindings + native encoder runtime for the HIP kernels (module codename_symbiont_amd._hip).
+//
+// Pointers cross the boundary as integers (torch tensors' data_ptr()) and streams as the raw
+// hipStream_t handle of torch.cuda.current_stream().  The module links the same libamdhip64.so.7
+// as torch (SONAME match), so torch's allocator, streams and our launches share one HIP runtime.
+//
+// EncoderRuntime::forward is the native replacement of the reference's
+// EmbeddingGenerator::generate_sentence_embeddings hot loop
+// (services/preprocessing_service/src/embedding_generator.rs:134-223): one call issues the whole
+// varlen encoder (embed+LN, L x {QKV GEMM, attention, out-proj+res+LN, FFN1+GELU, FFN2+res+LN},
+// pool) on one stream with no host synchronisation, so it can be captured in a hipGraph.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace py = pybind11;
+
+// ---- kernel launchers (defined in the .hip translation units) ----
+int symb_embed_ln(const int32_t* ids, const int32_t* pos, const int32_t* tt, const void* wemb,
+                  const void* pemb, const void* temb, const float* g, const float* b, float eps,
+                  void* out, int T, int H, hipStream_t st);
+int symb_add_ln(const void* x, const void* res, const float* g, const float* b, float eps,
+                void* out, int T, int H, hipStream_t st);
+int symb_pool(const void* hidden, const int32_t* cu, int B, int H, int mode, int normalize_f32,
+              float* out_f32, void* out_norm, hipStream_t st);
+int symb_l2norm_cast(const float* x, void* out, int n, int D, int ld_out, hipStream_t st);
+int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const float* bias,
+              const void* R, int ldr, const float* gamma, const float* beta, float eps, void* C,
+              int ldc, int M, int N, int K, hipStream_t st);
+int symb_attention(const void* qkv, int ld_qkv, const int32_t* cu, int B, int max_len,
+                   int n_heads, int head_dim, void* out, int ld_out, hipStream_t st);
+int symb_topk_geometry(int D, int kmax, int* lists, int* queries_per_blk);
+int symb_index_scan(const void* X, int n_valid, int D, int rows_per_blk, int n_rblk,
+                    const void* Q, int NQ, int kmax, float* cand_s, int* cand_i, hipStream_t st);
+int symb_topk_merge(const float* cand_s, const int* cand_i, int NQ, int n_cand_per_query,
+                    int kmax, int k, float* out_s, int* out_i, int64_t id_offset,
+                    int64_t* out_id64, hipStream_t st);
+
+namespace {
+
+using uptr = uintptr_t;
+template <class T>
+inline T* P(uptr p) { return reinterpret_cast<T*>(p); }
+inline hipStream_t S(uptr s) { return reinterpret_cast<hipStream_t>(s); }
+
+void check(int rc, const char* what) {
+  if (rc == 0) return;
+  if (rc < 0) throw std::invalid_argument(std::string(what) + ": unsupported shape/config");
+  throw std::runtime_error(std::string(what) + ": " + hipGetErrorString((hipError_t)rc));
+}
+
+enum { EPI_BIAS = 0, EPI_GELU = 1, EPI_RES = 2, EPI_RES_LN = 3 };
+
+struct LayerWeights {
+  uptr wqkv, bqkv, wo, bo, ln1_g, ln1_b, wi, bi, wo2, bo2, ln2_g, ln2_b;
+};
+
+class EncoderRuntime {
+ public:
+  EncoderRuntime(int hidden, int n_heads, int ffn, float eps, uptr wemb, uptr pemb, uptr temb,
+                 uptr eln_g, uptr eln_b)
+      : H_(hidden), nh_(n_heads), hd_(hidden / n_heads), FF_(ffn), eps_(eps), wemb_(wemb),
+        pemb_(pemb), temb_(temb), eln_g_(eln_g), eln_b_(eln_b) {
+    if (H_ % n_heads) throw std::invalid_argument("hidden % heads != 0");
+  }
+  void add_layer(const std::vector<uptr>& w) {
+    if (w.size() != 12) throw std::invalid_argument("layer needs 12 pointers");
+    layers_.push_back(LayerWeights{w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], w[8], w[9],
+                                   w[10], w[11]});
+  }
+  int num_layers() const { return (int)layers_.size(); }
+
+  // ws: {h, h2, qkv, ctx, ff, tmp} device buffers sized for T tokens.
+  void forward(uptr ids, uptr pos, uptr tt, uptr cu, int T, int B, int max_len,
+               const std::vector<uptr>& ws, int pool_mode, int normalize_f32, uptr out_f32,
+               uptr out_norm, uptr stream) {
+    if (ws.size() != 6) throw std::invalid_argument("workspace needs 6 buffers");
+    hipStream_t st = S(stream);
+    const int H = H_;
+    uptr h = ws[0], h2 = ws[1], qkv = ws[2], ctx = ws[3], ff = ws[4], tmp = ws[5];
+    check(symb_embed_ln(P<int32_t>(ids), P<int32_t>(pos), P<int32_t>(tt), P<void>(wemb_),
+                        P<void>(pemb_), P<void>(temb_), P<float>(eln_g_), P<float>(eln_b_), eps_,
+                        P<void>(h), T, H, st),
+          "embed_ln");
+    const bool fuse_ln = (H == 384);
+    for (const auto& L : layers_) {
+      check(symb_gemm(EPI_BIAS, P<void>(h), H, P<void>(L.wqkv), H, P<float>(L.bqkv), nullptr, 0,
+                      nullptr, nullptr, 0.f, P<void>(qkv), 3 * H, T, 3 * H, H, st),
+            "qkv gemm");
+      check(symb_attention(P<void>(qkv), 3 * H, P<int32_t>(cu), B, max_len, nh_, hd_,
+                           P<void>(ctx), H, st),
+            "attention");
+      if (fuse_ln) {
+        check(symb_gemm(EPI_RES_LN, P<void>(ctx), H, P<void>(L.wo), H, P<float>(L.bo),
+                        P<void>(h), H, P<float>(L.ln1_g), P<float>(L.ln1_b), eps_, P<void>(h2),
+                        H, T, H, H, st),
+              "out-proj+LN gemm");
+      } else {
+        check(symb_gemm(EPI_RES, P<void>(ctx), H, P<void>(L.wo), H, P<float>(L.bo), P<void>(h),
+                        H, nullptr, nullptr, 0.f, P<void>(tmp), H, T, H, H, st),
+              "out-proj gemm");
+        check(symb_add_ln(P<void>(tmp), nullptr, P<float>(L.ln1_g), P<float>(L.ln1_b), eps_,
+                          P<void>(h2), T, H, st),
+              "ln1");
+      }
+      check(symb_gemm(EPI_GELU, P<void>(h2), H, P<void>(L.wi), H, P<float>(L.bi), nullptr, 0,
+                      nullptr, nullptr, 0.f, P<void>(ff), FF_, T, FF_, H, st),
+            "ffn1 gemm");
+      if (fuse_ln) {
+        check(symb_gemm(EPI_RES_LN, P<void>(ff), FF_, P<void>(L.wo2), FF_, P<float>(L.bo2),
+                        P<void>(h2), H, P<float>(L.ln2_g), P<float>(L.ln2_b), eps_, P<void>(h),
+                        H, T, H, FF_, st),
+              "ffn2+LN gemm");
+      } else {
+        check(symb_gemm(EPI_RES, P<void>(ff), FF_, P<void>(L.wo2), FF_, P<float>(L.bo2),
+                        P<void>(h2), H, nullptr, nullptr, 0.f, P<void>(tmp), H, T, H, FF_, st),
+              "ffn2 gemm");
+        check(symb_add_ln(P<void>(tmp), nullptr, P<float>(L.ln2_g), P<float>(L.ln2_b), eps_,
+                          P<void>(h), T, H, st),
+              "ln2");
+      }
+    }
+    if (out_f32)
+      check(symb_pool(P<void>(h), P<int32_t>(cu), B, H, pool_mode, normalize_f32, P<float>(out_f32),
+                      P<void>(out_norm), st),
+            "pool");
+  }
+
+ private:
+  int H_, nh_, hd_, FF_;
+  float eps_;
+  uptr wemb_, pemb_, temb_, eln_g_, eln_b_;
+  std::vector<LayerWeights> layers_;
+};
+
+}  // namespace
+
+PYBIND11_MODULE(_hip, m) {
+  m.doc() = "CDNA4 (gfx950) HIP kernels of codename_symbiont_amd";
+  m.def("arch", []() { return std::string("gfx950"); });
+  m.def("embed_ln", [](uptr ids, uptr pos, uptr tt, uptr wemb, uptr pemb, uptr temb, uptr g,
+                       uptr b, float eps, uptr out, int T, int H, uptr st) {
+    check(symb_embed_ln(P<int32_t>(ids), P<int32_t>(pos), P<int32_t>(tt), P<void>(wemb),
+                        P<void>(pemb), P<void>(temb), P<float>(g), P<float>(b), eps, P<void>(out),
+                        T, H, S(st)),
+          "embed_ln");
+  });
+  m.def("add_ln", [](uptr x, uptr res, uptr g, uptr b, float eps, uptr out, int T, int H, uptr st) {
+    check(symb_add_ln(P<void>(x), P<void>(res), P<float>(g), P<float>(b), eps, P<void>(out), T, H,
+                      S(st)),
+          "add_ln");
+  });
+  m.def("pool", [](uptr hidden, uptr cu, int B, int H, int mode, int normalize_f32, uptr out_f32,
+                   uptr out_norm, uptr st) {
+    check(symb_pool(P<void>(hidden), P<int32_t>(cu), B, H, mode, normalize_f32, P<float>(out_f32),
+                    P<void>(out_norm), S(st)),
+          "pool");
+  });
+  m.def("l2norm_cast", [](uptr x, uptr out, int n, int D, int ld_out, uptr st) {
+    check(symb_l2norm_cast(P<float>(x), P<void>(out), n, D, ld_out, S(st)), "l2norm_cast");
+  });
+  m.def("gemm", [](int epi, uptr A, int lda, uptr W, int ldw, uptr bias, uptr R, int ldr, uptr g,
+                   uptr b, float eps, uptr C, int ldc, int M, int N, int K, uptr st) {
+    check(symb_gemm(epi, P<void>(A), lda, P<void>(W), ldw, P<float>(bias), P<void>(R), ldr,
+                    P<float>(g), P<float>(b), eps, P<void>(C), ldc, M, N, K, S(st)),
+          "gemm");
+  });
+  m.def("attention", [](uptr qkv, int ld_qkv, uptr cu, int B, int max_len, int n_heads,
+                        int head_dim, uptr out, int ld_out, uptr st) {
+    check(symb_attention(P<void>(qkv), ld_qkv, P<int32_t>(cu), B, max_len, n_heads, head_dim,
+                         P<void>(out), ld_out, S(st)),
+          "attention");
+  });
+  m.def("topk_geometry", [](int D, int kmax) {
+    int lists = 0, qpb = 0;
+    check(symb_topk_geometry(D, kmax, &lists, &qpb), "topk_geometry");
+    return py::make_tuple(lists, qpb);
+  });
+  m.def("index_scan", [](uptr X, int n_valid, int D, int rows_per_blk, int n_rblk, uptr Q, int NQ,
+                         int kmax, uptr cand_s, uptr cand_i, uptr st) {
+    check(symb_index_scan(P<void>(X), n_valid, D, rows_per_blk, n_rblk, P<void>(Q), NQ, kmax,
+                          P<float>(cand_s), P<int>(cand_i), S(st)),
+          "index_scan");
+  });
+  m.def("topk_merge", [](uptr cand_s, uptr cand_i, int NQ, int n_cand, int kmax, int k,
+                         uptr out_s, uptr out_i, int64_t id_offset, uptr out_id64, uptr st) {
+    check(symb_topk_merge(P<float>(cand_s), P<int>(cand_i), NQ, n_cand, kmax, k, P<float>(out_s),
+                          P<int>(out_i), id_offset, P<int64_t>(out_id64), S(st)),
+          "topk_merge");
+  });
+  py::class_<EncoderRuntime>(m, "EncoderRuntime")
+      .def(py::init<int, int, int, float, uptr, uptr, uptr, uptr, uptr>())
+      .def("add_layer", &EncoderRuntime::add_layer)
+      .def("num_layers", &EncoderRuntime::num_layers)
+      .def("forward", &EncoderRuntime::forward);
+}

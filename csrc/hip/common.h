@@ -1,0 +1,66 @@
+// Shared device helpers for the CDNA4 (gfx950 / MI355X) kernels of codename_symbiont_amd.
+//
+// Everything here is written for 64-lane wavefronts, MFMA matrix cores and the 160 KiB LDS of a
+// gfx950 CU.  No CUDA, no dual paths: hard-coded wave width 64, OCP bf16/fp8 types.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace symb {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;   // MFMA A/B operand (4 VGPRs)
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;     // 16x16 MFMA accumulator
+typedef __attribute__((ext_vector_type(16))) float f32x16;   // 32x32 MFMA accumulator
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;  // raw 16-byte vector
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float bf2f(__bf16 h) { return (float)h; }
+__device__ __forceinline__ __bf16 f2bf(float f) { return (__bf16)f; }  // RNE, v_cvt_pk_bf16_f32
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m, 64));
+  return v;
+}
+
+// 8 bf16 <-> 8 f32 through one 16-byte access.
+__device__ __forceinline__ void load8(const __bf16* p, float (&o)[8]) {
+  bf16x8 v = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = (float)v[i];
+}
+__device__ __forceinline__ void store8(__bf16* p, const float (&o)[8]) {
+  bf16x8 v;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = (__bf16)o[i];
+  *reinterpret_cast<bf16x8*>(p) = v;
+}
+
+__device__ __forceinline__ float gelu_erf(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}
+
+// Bijective XCD-aware remap of a linear workgroup id (MI355X deals workgroups round-robin over
+// 8 XCDs): consecutive logical tiles land on the same XCD so their shared operand panels hit the
+// same private L2.  Speed only, never correctness.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
+
+// Async global->LDS copy of 16 bytes per lane (global_load_lds_dwordx4).  The LDS destination is
+// the wave-uniform base; lane l lands at base + 16*l.
+__device__ __forceinline__ void glds16(const void* gsrc, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(
+      (const __attribute__((address_space(1))) void*)gsrc,
+      (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+}  // namespace symb

@@ -1,0 +1,330 @@
+// Fused brute-force cosine scan + top-k over an HBM-resident index shard (replaces Qdrant's
+// HNSW search, services/vector_memory_service/src/main.rs:261-308).
+//
+//   scores = X[rows] · Q^T   (X: unit-norm bf16 rows, Q: unit-norm bf16 queries)  -> per-query
+//   top-KMAX candidates, without ever writing the [rows x queries] score matrix to HBM.
+//
+// CDNA4 design (one 512-thread workgroup per CU, 2 waves per SIMD):
+//  * The queries live in REGISTERS as MFMA B fragments: every wave owns 32 queries (D=384,
+//    v_mfma_f32_32x32x16_bf16, 24 fragments = 96 VGPRs) or 16 queries (D=768/1024,
+//    v_mfma_f32_16x16x32_bf16).  A workgroup therefore scores 256 (or 128) queries at once.
+//  * Index rows stream HBM -> LDS in 32-row tiles by global_load_lds_dwordx4 (no VGPR staging)
+//    through a 4-deep LDS ring with a COUNTED `s_waitcnt vmcnt(6)` and a raw s_barrier, so two
+//    tiles are always in flight across the barrier (a __syncthreads would drain vmcnt to 0).
+//    Every tile read from HBM once feeds 8 waves x their queries.
+//  * Bank conflicts: the image stays lane-linear for the DMA; the 16-byte chunk index is XORed
+//    with (row & 15) on the global source address and on the ds_read_b128 address.
+//  * Top-k: with X as the A operand, a lane's accumulator column IS one query, so the running
+//    per-query threshold lives in a register and the sorted top-KMAX list in statically indexed
+//    registers; the insertion path runs only for lanes whose new scores beat their threshold
+//    (rare once the list is warm).
+//  * A second small kernel merges the per-workgroup candidate lists into the final top-k.
+#include "common.h"
+
+namespace symb {
+
+constexpr int TOPK_NS = 4;       // LDS ring depth (tiles)
+constexpr int TOPK_WAVES = 8;
+
+template <int KMAX>
+__device__ __forceinline__ void topk_insert(float (&tv)[KMAX], int (&ti)[KMAX], float s, int id) {
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) {
+    const bool sw = s > tv[i];
+    const float ov = tv[i];
+    const int oi = ti[i];
+    tv[i] = sw ? s : ov;
+    ti[i] = sw ? id : oi;
+    s = sw ? ov : s;
+    id = sw ? oi : id;
+  }
+}
+
+// MFMA_32 = true : D = 384 path (32x32x16, 32 queries per wave, 2 lists per query per wave)
+// MFMA_32 = false: D = 768/1024 path (16x16x32, 16 queries per wave, 4 lists per query per wave)
+template <int D, bool MFMA_32, int KMAX>
+__global__ __launch_bounds__(512) void index_scan_topk_kernel(
+    const __bf16* __restrict__ X, int n_valid, int rows_per_blk, const __bf16* __restrict__ Q,
+    int NQ, int n_qblk, float* __restrict__ cand_s, int* __restrict__ cand_i) {
+  constexpr int CPR = D / 8;                          // 16-byte chunks per row
+  constexpr int TR = MFMA_32 ? 32 : 16;               // rows per LDS tile (<= 32 KiB per tile)
+  constexpr int TILE_BYTES = TR * D * 2;
+  constexpr int LOADS = TILE_BYTES / (1024 * TOPK_WAVES);  // glds per wave per tile
+  static_assert(TILE_BYTES % (1024 * TOPK_WAVES) == 0, "tile must split evenly over waves");
+  static_assert(LOADS == 3 || LOADS == 4, "vmcnt literal table");
+  static_assert(TOPK_NS * TILE_BYTES <= 160 * 1024, "LDS ring exceeds the CU's 160 KiB");
+  constexpr int QW = MFMA_32 ? 32 : 16;               // queries per wave
+  constexpr int NKS = MFMA_32 ? D / 16 : D / 32;      // MFMA k-steps over D
+  constexpr int LISTS = MFMA_32 ? 2 : 4;
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int qb = blockIdx.x % n_qblk, rb = blockIdx.x / n_qblk;
+  const int row_begin = rb * rows_per_blk;
+  const int row_end = min(row_begin + rows_per_blk, n_valid);
+  const int n_tiles = row_end > row_begin ? (row_end - row_begin + TR - 1) / TR : 0;
+
+  // ---- query fragments (B operand) ----
+  const int qlocal = MFMA_32 ? (lane & 31) : (lane & 15);
+  const int query = qb * (QW * TOPK_WAVES) + wave * QW + qlocal;
+  const __bf16* qp = Q + (size_t)min(query, NQ - 1) * D;
+  bf16x8 qf[NKS];
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
+    const int k0 = MFMA_32 ? ks * 16 + (lane >> 5) * 8 : ks * 32 + (lane >> 4) * 8;
+    qf[ks] = *reinterpret_cast<const bf16x8*>(qp + k0);
+  }
+
+  // ---- per-thread DMA source offsets within a tile (identical for every tile) ----
+  uint32_t goff[LOADS];
+#pragma unroll
+  for (int i = 0; i < LOADS; ++i) {
+    const int s = (i * TOPK_WAVES + wave) * 64 + lane;  // LDS 16-byte slot this lane fills
+    const int row = s / CPR, pc = s % CPR;
+    const int c = pc ^ (row & 15);
+    goff[i] = (uint32_t)(row * D + c * 8);
+  }
+  auto issue = [&](int t) {
+    const int tt = min(t, n_tiles - 1);  // past the end: re-load the last tile (keeps vmcnt exact)
+    const __bf16* base = X + (size_t)(row_begin + tt * TR) * D;
+    char* dst = smem + (t % TOPK_NS) * TILE_BYTES;
+#pragma unroll
+    for (int i = 0; i < LOADS; ++i) glds16(base + goff[i], dst + ((i * TOPK_WAVES + wave) * 64) * 16);
+  };
+
+  float tv[KMAX];
+  int ti[KMAX];
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) {
+    tv[i] = -INFINITY;
+    ti[i] = -1;
+  }
+  float thr = -INFINITY;
+
+  if (n_tiles > 0) {
+#pragma unroll
+    for (int p = 0; p < TOPK_NS - 1; ++p) issue(p);
+  }
+  for (int t = 0; t < n_tiles; ++t) {
+    // tile t landed for this wave once only the (NS-2) younger tiles' loads remain
+    static_assert(TOPK_NS == 4, "vmcnt literals assume 2 younger tiles in flight");
+    if constexpr (LOADS == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    if constexpr (LOADS == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    issue(t + TOPK_NS - 1);
+    const char* tile = smem + (t % TOPK_NS) * TILE_BYTES;
+    const int tile_row0 = row_begin + t * TR;
+    const bool partial = tile_row0 + TR > row_end;
+
+    if constexpr (MFMA_32) {
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      const int arow = lane & 31;
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        const int c = ks * 2 + (lane >> 5);
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(tile + arow * (D * 2) + ((c ^ (arow & 15)) << 4));
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[ks], acc, 0, 0, 0);
+      }
+      const int rbase = tile_row0 + 4 * (lane >> 5);
+      if (partial) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (rbase + (r & 3) + 8 * (r >> 2) >= row_end) acc[r] = -INFINITY;
+      }
+      float mx = acc[0];
+#pragma unroll
+      for (int r = 1; r < 16; ++r) mx = fmaxf(mx, acc[r]);
+      if (mx > thr) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          if (acc[r] > thr) {
+            topk_insert<KMAX>(tv, ti, acc[r], rbase + (r & 3) + 8 * (r >> 2));
+            thr = tv[KMAX - 1];
+          }
+        }
+      }
+    } else {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int arow = lane & 15;
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        const int c = ks * 4 + (lane >> 4);
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(tile + arow * (D * 2) + ((c ^ arow) << 4));
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[ks], acc, 0, 0, 0);
+      }
+      const int rbase = tile_row0 + (lane >> 4) * 4;
+      if (partial) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (rbase + r >= row_end) acc[r] = -INFINITY;
+      }
+      const float mx = fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3]));
+      if (mx > thr) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (acc[r] > thr) {
+            topk_insert<KMAX>(tv, ti, acc[r], rbase + r);
+            thr = tv[KMAX - 1];
+          }
+        }
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the tail prefetches before exit
+
+  if (query < NQ) {
+    const int list = MFMA_32 ? (lane >> 5) : (lane >> 4);
+    const int n_rblk = gridDim.x / n_qblk;
+    const size_t base = (((size_t)query * n_rblk + rb) * LISTS + list) * KMAX;
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i) {
+      cand_s[base + i] = tv[i];
+      cand_i[base + i] = ti[i];
+    }
+  }
+}
+
+// Merge the candidate lists of one query (contiguous: [n_rblk][lists][KMAX]) into the final
+// top-k.  One workgroup per query: strided local top-KMAX, then an LDS tree of pairwise merges.
+template <int KMAX, int NTH>
+__global__ __launch_bounds__(NTH) void topk_merge_kernel(const float* __restrict__ cand_s,
+                                                         const int* __restrict__ cand_i,
+                                                         int n_cand_per_query, int k,
+                                                         float* __restrict__ out_s,
+                                                         int* __restrict__ out_i,
+                                                         int64_t id_offset,
+                                                         int64_t* __restrict__ out_id64) {
+  __shared__ float ls[NTH * KMAX];
+  __shared__ int li[NTH * KMAX];
+  const int q = blockIdx.x, tid = threadIdx.x;
+  const float* cs = cand_s + (size_t)q * n_cand_per_query;
+  const int* ci = cand_i + (size_t)q * n_cand_per_query;
+  float tv[KMAX];
+  int ti[KMAX];
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) {
+    tv[i] = -INFINITY;
+    ti[i] = -1;
+  }
+  for (int c = tid; c < n_cand_per_query; c += NTH) {
+    const float s = cs[c];
+    if (s > tv[KMAX - 1]) topk_insert<KMAX>(tv, ti, s, ci[c]);
+  }
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) {
+    ls[tid * KMAX + i] = tv[i];
+    li[tid * KMAX + i] = ti[i];
+  }
+  __syncthreads();
+  for (int half = NTH / 2; half >= 1; half >>= 1) {
+    if (tid < half) {
+      const float* as = ls + tid * KMAX;
+      const int* ai = li + tid * KMAX;
+      const float* bs = ls + (tid + half) * KMAX;
+      const int* bi = li + (tid + half) * KMAX;
+      int pa = 0, pb = 0;
+#pragma unroll
+      for (int i = 0; i < KMAX; ++i) {
+        const bool take_a = as[pa] >= bs[pb];
+        tv[i] = take_a ? as[pa] : bs[pb];
+        ti[i] = take_a ? ai[pa] : bi[pb];
+        pa += take_a ? 1 : 0;
+        pb += take_a ? 0 : 1;
+        pa = min(pa, KMAX - 1);
+        pb = min(pb, KMAX - 1);
+      }
+    }
+    __syncthreads();
+    if (tid < half) {
+#pragma unroll
+      for (int i = 0; i < KMAX; ++i) {
+        ls[tid * KMAX + i] = tv[i];
+        li[tid * KMAX + i] = ti[i];
+      }
+    }
+    __syncthreads();
+  }
+  if (tid < k) {
+    const float s = tid < KMAX ? ls[tid] : -INFINITY;
+    const int i = tid < KMAX ? li[tid] : -1;
+    out_s[(size_t)q * k + tid] = s;
+    out_i[(size_t)q * k + tid] = i;
+    if (out_id64) out_id64[(size_t)q * k + tid] = i >= 0 ? id_offset + i : -1;
+  }
+}
+
+}  // namespace symb
+
+using namespace symb;
+
+// Candidate-buffer geometry the host must allocate: [n_rblk][NQ][lists][kmax] floats and ints.
+int symb_topk_geometry(int D, int kmax, int* lists, int* queries_per_blk) {
+  if (kmax != 16 && kmax != 32) return -1;
+  if (D == 384) {
+    *lists = 2;
+    *queries_per_blk = 256;
+  } else if (D == 768 || D == 1024) {
+    *lists = 4;
+    *queries_per_blk = 128;
+  } else {
+    return -1;
+  }
+  return 0;
+}
+
+template <int D, bool M32, int KMAX>
+static int launch_scan(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
+                       int NQ, int n_qblk, float* cs, int* ci, hipStream_t st) {
+  auto kern = index_scan_topk_kernel<D, M32, KMAX>;
+  constexpr int lds = TOPK_NS * (M32 ? 32 : 16) * D * 2;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(n_rblk * n_qblk), dim3(512), lds, st, (const __bf16*)X, n_valid,
+                     rows_per_blk, (const __bf16*)Q, NQ, n_qblk, cs, ci);
+  return (int)hipGetLastError();
+}
+
+// X: [>= round_up(n_valid, 32), D] bf16 unit rows; Q: [NQ, D] bf16 unit rows.
+// rows_per_blk must be a multiple of 32; n_rblk * rows_per_blk >= n_valid.
+int symb_index_scan(const void* X, int n_valid, int D, int rows_per_blk, int n_rblk,
+                    const void* Q, int NQ, int kmax, float* cand_s, int* cand_i, hipStream_t st) {
+  if (NQ <= 0 || n_rblk <= 0) return 0;
+  if (rows_per_blk % 32) return -1;
+  int lists, qpb;
+  if (symb_topk_geometry(D, kmax, &lists, &qpb)) return -1;
+  const int n_qblk = (NQ + qpb - 1) / qpb;
+#define SYMB_SCAN(DD, M32)                                                                     \
+  return kmax == 16 ? launch_scan<DD, M32, 16>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, n_qblk, \
+                                               cand_s, cand_i, st)                              \
+                    : launch_scan<DD, M32, 32>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, n_qblk, \
+                                               cand_s, cand_i, st);
+  if (D == 384) { SYMB_SCAN(384, true) }
+  if (D == 768) { SYMB_SCAN(768, false) }
+  if (D == 1024) { SYMB_SCAN(1024, false) }
+#undef SYMB_SCAN
+  return -1;
+}
+
+// cand_* laid out [NQ][n_cand_per_query] -- exactly the scan's [NQ][n_rblk][lists][kmax] output.
+// Also merges gathered per-rank top-k lists ([NQ][world*k], padded to kmax) in the sharded path.
+int symb_topk_merge(const float* cand_s, const int* cand_i, int NQ, int n_cand_per_query,
+                    int kmax, int k, float* out_s, int* out_i, int64_t id_offset,
+                    int64_t* out_id64, hipStream_t st) {
+  if (NQ <= 0) return 0;
+  if (k > kmax) return -1;
+  if (kmax == 16)
+    hipLaunchKernelGGL((topk_merge_kernel<16, 256>), dim3(NQ), dim3(256), 0, st, cand_s, cand_i,
+                       n_cand_per_query, k, out_s, out_i, id_offset, out_id64);
+  else if (kmax == 32)
+    hipLaunchKernelGGL((topk_merge_kernel<32, 128>), dim3(NQ), dim3(128), 0, st, cand_s, cand_i,
+                       n_cand_per_query, k, out_s, out_i, id_offset, out_id64);
+  else
+    return -1;
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,227 @@
+// Python-object side of the JSON codec: dumps(obj) -> bytes and loads(bytes) -> obj.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "json.h"
+
+namespace py = pybind11;
+
+namespace symbn {
+
+static void dump_value(std::string& out, PyObject* o, int depth);
+
+static void dump_value(std::string& out, PyObject* o, int depth) {
+  if (depth > 128) throw std::runtime_error("recursion limit exceeded");
+  if (o == Py_None) {
+    out += "null";
+  } else if (o == Py_True) {
+    out += "true";
+  } else if (o == Py_False) {
+    out += "false";
+  } else if (PyLong_Check(o)) {
+    PyObject* s = PyObject_Str(o);
+    if (!s) throw py::error_already_set();
+    Py_ssize_t n;
+    const char* c = PyUnicode_AsUTF8AndSize(s, &n);
+    out.append(c, n);
+    Py_DECREF(s);
+  } else if (PyFloat_Check(o)) {
+    append_f32(out, (float)PyFloat_AS_DOUBLE(o));
+  } else if (PyUnicode_Check(o)) {
+    Py_ssize_t n;
+    const char* c = PyUnicode_AsUTF8AndSize(o, &n);
+    if (!c) throw py::error_already_set();
+    append_json_string(out, c, (size_t)n);
+  } else if (PyDict_Check(o)) {
+    out.push_back('{');
+    PyObject *k, *v;
+    Py_ssize_t pos = 0;
+    bool first = true;
+    while (PyDict_Next(o, &pos, &k, &v)) {
+      if (!PyUnicode_Check(k)) throw std::runtime_error("key must be a string");
+      if (!first) out.push_back(',');
+      first = false;
+      Py_ssize_t n;
+      const char* c = PyUnicode_AsUTF8AndSize(k, &n);
+      append_json_string(out, c, (size_t)n);
+      out.push_back(':');
+      dump_value(out, v, depth + 1);
+    }
+    out.push_back('}');
+  } else if (PyList_Check(o) || PyTuple_Check(o)) {
+    PyObject* seq = o;
+    const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+    PyObject** items = PySequence_Fast_ITEMS(seq);
+    out.push_back('[');
+    for (Py_ssize_t i = 0; i < n; ++i) {
+      if (i) out.push_back(',');
+      dump_value(out, items[i], depth + 1);
+    }
+    out.push_back(']');
+  } else if (py::isinstance<py::array>(py::handle(o))) {
+    auto arr = py::array_t<float, py::array::c_style | py::array::forcecast>::ensure(py::handle(o));
+    if (!arr) throw std::runtime_error("array not convertible to float32");
+    if (arr.ndim() != 1) throw std::runtime_error("only 1-d arrays are serialisable");
+    append_f32_array(out, arr.data(), (size_t)arr.size());
+  } else if (PyObject_HasAttrString(o, "__float__") && !PyObject_HasAttrString(o, "__index__")) {
+    const double d = PyFloat_AsDouble(o);
+    if (PyErr_Occurred()) throw py::error_already_set();
+    append_f32(out, (float)d);
+  } else if (PyObject_HasAttrString(o, "__index__")) {
+    PyObject* i = PyNumber_Index(o);
+    if (!i) throw py::error_already_set();
+    dump_value(out, i, depth + 1);
+    Py_DECREF(i);
+  } else {
+    throw std::runtime_error(std::string("unserialisable type: ") + Py_TYPE(o)->tp_name);
+  }
+}
+
+py::bytes dumps(py::handle obj) {
+  std::string out;
+  out.reserve(256);
+  dump_value(out, obj.ptr(), 0);
+  return py::bytes(out);
+}
+
+py::bytes dumps_f32_array(py::array_t<float, py::array::c_style | py::array::forcecast> a) {
+  std::string out;
+  out.reserve((size_t)a.size() * 12 + 2);
+  append_f32_array(out, a.data(), (size_t)a.size());
+  return py::bytes(out);
+}
+
+// --------------------------------------------------------------------------- loads
+struct Loader {
+  Parser p;
+  bool f32_arrays;
+  Loader(const char* s, size_t n, bool f32) : p(s, n), f32_arrays(f32) {}
+
+  py::object number_obj(const Number& n) {
+    if (!n.is_float) {
+      PyObject* o = PyLong_FromString(n.text.c_str(), nullptr, 10);
+      if (!o) throw py::error_already_set();
+      return py::reinterpret_steal<py::object>(o);
+    }
+    return py::float_(std::strtod(n.text.c_str(), nullptr));
+  }
+
+  py::object value(int depth) {
+    if (depth > 128) p.fail("recursion limit exceeded");
+    const char c = p.peek();
+    if (c == '{') {
+      p.advance();
+      py::dict d;
+      if (p.peek() == '}') {
+        p.advance();
+        return std::move(d);
+      }
+      for (;;) {
+        if (p.peek() != '"') p.fail("key must be a string");
+        std::string k = p.string();
+        if (p.peek() != ':') p.fail("expected `:`");
+        p.advance();
+        py::object v = value(depth + 1);
+        d[py::str(k)] = v;
+        const char t = p.peek();
+        if (t == ',') {
+          p.advance();
+          continue;
+        }
+        if (t == '}') {
+          p.advance();
+          return std::move(d);
+        }
+        p.fail("expected `,` or `}`");
+      }
+    }
+    if (c == '[') {
+      p.advance();
+      if (p.peek() == ']') {
+        p.advance();
+        return py::list();
+      }
+      // fast path: an all-number array becomes a float32 numpy buffer when requested
+      std::vector<py::object> items;
+      std::vector<Number> raw;     // numbers seen before the first non-number element
+      bool all_num = f32_arrays;
+      for (;;) {
+        const char t = p.peek();
+        if (all_num && (t == '-' || (t >= '0' && t <= '9'))) {
+          raw.push_back(p.number());
+        } else {
+          if (all_num) {  // demote: materialise the numbers parsed so far
+            for (const Number& n : raw) items.push_back(number_obj(n));
+            raw.clear();
+            all_num = false;
+          }
+          items.push_back(value(depth + 1));
+        }
+        const char s = p.peek();
+        if (s == ',') {
+          p.advance();
+          continue;
+        }
+        if (s == ']') {
+          p.advance();
+          break;
+        }
+        p.fail("expected `,` or `]`");
+      }
+      if (all_num) {
+        py::array_t<float> arr((py::ssize_t)raw.size());
+        float* dst = arr.mutable_data();
+        for (size_t i = 0; i < raw.size(); ++i) dst[i] = std::strtof(raw[i].text.c_str(), nullptr);
+        return std::move(arr);
+      }
+      py::list l(items.size());
+      for (size_t i = 0; i < items.size(); ++i) l[i] = items[i];
+      return std::move(l);
+    }
+    if (c == '"') return py::str(p.string());
+    if (c == 't') {
+      p.expect_lit("true");
+      return py::bool_(true);
+    }
+    if (c == 'f') {
+      p.expect_lit("false");
+      return py::bool_(false);
+    }
+    if (c == 'n') {
+      p.expect_lit("null");
+      return py::none();
+    }
+    if (c == '-' || (c >= '0' && c <= '9')) return number_obj(p.number());
+    p.fail("expected value");
+  }
+};
+
+py::object loads(py::bytes data, bool f32_arrays) {
+  char* buf;
+  Py_ssize_t n;
+  PyBytes_AsStringAndSize(data.ptr(), &buf, &n);
+  Loader L(buf, (size_t)n, f32_arrays);
+  py::object v = L.value(0);
+  if (!L.p.at_end()) L.p.fail("trailing characters");
+  return v;
+}
+
+std::string format_f32(float f) {
+  std::string s;
+  append_f32(s, f);
+  return s;
+}
+
+void register_json(py::module_& m) {
+  py::register_exception<JsonError>(m, "JsonError", PyExc_ValueError);
+  m.def("json_dumps", &dumps, "serde_json-compatible compact encoding (floats as f32)");
+  m.def("json_dumps_f32_array", &dumps_f32_array);
+  m.def("json_loads", &loads, py::arg("data"), py::arg("f32_arrays") = false);
+  m.def("format_f32", &format_f32);
+}
+
+}  // namespace symbn

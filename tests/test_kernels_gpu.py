@@ -1,0 +1,175 @@
+"""Numerics of every HIP kernel against its plain-PyTorch fp32 oracle (ops/reference.py).
+
+Inputs are random and ASYMMETRIC (a transposed C-write or swapped operand fails), shapes include
+ragged tails (M not a multiple of the tile, odd sequence lengths) so the masked paths run.
+"""
+import math
+
+import pytest
+import torch
+
+from codename_symbiont_amd.ops import reference as R
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _bf(*shape, scale=1.0, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(torch.bfloat16).to(DEV)
+
+
+def _f(*shape, scale=1.0, seed=0, offset=0.0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale + offset).to(DEV)
+
+
+def _close(out, ref, atol, rtol=0.0, what=""):
+    out = out.float()
+    ref = ref.float()
+    err = (out - ref).abs()
+    bound = atol + rtol * ref.abs()
+    bad = (err > bound).sum().item()
+    assert bad == 0, f"{what}: {bad} elems off, max err {err.max().item():.4g}"
+
+
+def test_extension_is_native_gfx950():
+    from codename_symbiont_amd.ops._ext import hip
+
+    h = hip()
+    assert h.arch() == "gfx950"
+    assert h.__file__.endswith(".so")
+
+
+@pytest.mark.parametrize("H", [384, 768, 1024])
+def test_embed_ln(H):
+    from codename_symbiont_amd.ops.kernels import embed_ln
+
+    V, P, T = 1000, 128, 333
+    w, p, t = _bf(V, H, seed=1), _bf(P, H, seed=2), _bf(2, H, seed=3)
+    g, b = _f(H, scale=0.1, offset=1.0, seed=4), _f(H, scale=0.1, seed=5)
+    ids = torch.randint(0, V, (T,), dtype=torch.int32, device=DEV)
+    pos = torch.randint(0, P, (T,), dtype=torch.int32, device=DEV)
+    tt = torch.randint(0, 2, (T,), dtype=torch.int32, device=DEV)
+    out = embed_ln(ids, pos, tt, w, p, t, g, b, 1e-12)
+    ref = R.embed_ln_ref(ids, pos, tt, w, p, t, g, b, 1e-12)
+    _close(out, ref, atol=3e-2, rtol=1e-2, what="embed_ln")
+
+
+@pytest.mark.parametrize("H", [384, 768, 1024])
+def test_add_ln(H):
+    from codename_symbiont_amd.ops.kernels import add_ln
+
+    x, r = _bf(257, H, seed=1), _bf(257, H, seed=2)
+    g, b = _f(H, scale=0.1, offset=1.0, seed=4), _f(H, scale=0.1, seed=5)
+    _close(add_ln(x, r, g, b, 1e-5), R.add_ln_ref(x, r, g, b, 1e-5), 3e-2, 1e-2, "add_ln")
+    _close(add_ln(x, None, g, b, 1e-5), R.add_ln_ref(x, None, g, b, 1e-5), 3e-2, 1e-2, "ln")
+
+
+@pytest.mark.parametrize("M,N,K,epi", [
+    (300, 1152, 384, 0), (129, 1536, 384, 1), (517, 384, 384, 2), (517, 384, 384, 3),
+    (300, 384, 1536, 3), (64, 768, 768, 2), (1000, 2304, 768, 0), (77, 1024, 4096, 2),
+])
+def test_gemm(M, N, K, epi):
+    from codename_symbiont_amd.ops.kernels import gemm
+
+    a = _bf(M, K, seed=1)
+    w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=2)
+    bias = _f(N, scale=0.5, seed=3)
+    res = _bf(M, N, seed=4) if epi in (2, 3) else None
+    g = _f(N, scale=0.1, offset=1.0, seed=5) if epi == 3 else None
+    b = _f(N, scale=0.1, seed=6) if epi == 3 else None
+    out = gemm(a, w, bias, epi, res, g, b, 1e-12)
+    ref = R.gemm_ref(a, w, bias, epi, res, g, b, 1e-12)
+    _close(out, ref, atol=4e-2, rtol=2e-2, what=f"gemm epi={epi}")
+
+
+@pytest.mark.parametrize("D,nh", [(32, 12), (64, 12), (64, 16)])
+def test_attention_varlen(D, nh):
+    from codename_symbiont_amd.ops.kernels import attention
+
+    lens = [1, 7, 64, 65, 128, 200, 3, 511]
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
+    T = int(cu[-1])
+    H = nh * D
+    qkv = _bf(T, 3 * H, seed=7)
+    out = attention(qkv, cu, max(lens), nh, D)
+    ref = R.attention_ref(qkv, cu, nh, D)
+    _close(out, ref, atol=2e-2, rtol=2e-2, what="attention")
+
+
+@pytest.mark.parametrize("H,mode,norm", [(384, "mean", True), (768, "cls", True),
+                                         (1024, "mean", False)])
+def test_pool(H, mode, norm):
+    from codename_symbiont_amd.ops.kernels import pool
+
+    lens = [5, 1, 64, 33, 200]
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
+    h = _bf(int(cu[-1]), H, seed=9)
+    out, unit = pool(h, cu, mode, norm)
+    ref = R.pool_ref(h, cu, mode, norm)
+    _close(out, ref, atol=1e-3, rtol=1e-3, what="pool")
+    _close(unit, torch.nn.functional.normalize(ref, dim=-1), atol=1e-2, what="pool unit")
+
+
+def test_l2norm_cast_into_slab():
+    from codename_symbiont_amd.ops.kernels import l2norm_cast
+
+    x = _f(100, 384, seed=3)
+    slab = torch.zeros(128, 384, dtype=torch.bfloat16, device=DEV)
+    l2norm_cast(x, slab[10:110])
+    _close(slab[10:110], torch.nn.functional.normalize(x, dim=-1), atol=8e-3, what="l2norm")
+    assert slab[:10].abs().sum() == 0 and slab[110:].abs().sum() == 0
+
+
+@pytest.mark.parametrize("model", ["minilm-l6", "bge-base"])
+def test_encoder_matches_fp32_oracle(model):
+    from codename_symbiont_amd.models import get_config
+    from codename_symbiont_amd.models.encoder import (HipEncoder, TorchEncoder,
+                                                      synthetic_batch)
+    from codename_symbiont_amd.models.weights import random_params
+
+    cfg = get_config(model)
+    params = random_params(cfg, seed=3)
+    hip_enc = HipEncoder(cfg, params=params)
+    ref_enc = TorchEncoder(cfg, params=params)
+    b = synthetic_batch(cfg, 24, 96, seed=1, varlen=True)
+    out, unit = hip_enc.forward_packed(b.to(DEV))
+    ref, _ = ref_enc.forward_packed(b)
+    cos = torch.nn.functional.cosine_similarity(out.float().cpu(), ref.float(), dim=-1)
+    assert cos.min().item() > 0.999, cos
+
+
+@pytest.mark.parametrize("D,k,n,nq", [(384, 10, 10_007, 300), (384, 20, 5000, 17),
+                                      (768, 5, 9000, 130), (1024, 16, 4133, 64)])
+def test_index_scan_topk_exact(D, k, n, nq):
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+
+    shard = HbmIndexShard(D, n + 100)
+    shard.fill_random(n, seed=5)
+    q = torch.nn.functional.normalize(_f(nq, D, seed=11), dim=-1).bfloat16()
+    s, r = shard.search(q, k)
+    ref_s, ref_i = R.topk_ref(shard.unit_rows(), q, k)
+    torch.cuda.synchronize()
+    # scores agree to bf16-input / fp32-accumulate rounding
+    _close(s, ref_s, atol=2e-3, what="topk scores")
+    # recall@k == 1 up to near-ties
+    hits = 0
+    for i in range(nq):
+        hits += len(set(r[i].tolist()) & set(ref_i[i].tolist()))
+    assert hits / (nq * k) > 0.995
+    # every returned row's true score equals the returned score
+    true = (q.float() @ shard.unit_rows().float().t()).gather(1, r.long())
+    _close(s, true, atol=2e-3, what="returned rows")
+
+
+def test_index_scan_small_and_partial():
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+
+    shard = HbmIndexShard(384, 64)
+    shard.fill_random(3, seed=1)
+    q = torch.nn.functional.normalize(_f(2, 384, seed=2), dim=-1).bfloat16()
+    s, r = shard.search(q, 5)
+    assert (r[:, 3:] == -1).all() and torch.isinf(s[:, 3:]).all()
+    assert sorted(r[0, :3].tolist()) == [0, 1, 2]
