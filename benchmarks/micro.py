@@ -1,0 +1,184 @@
+#!/usr/bin/env python3
+"""Kernel micro-benchmarks on one MI355X (interleaved A/B rounds in ONE process).
+
+  python benchmarks/micro.py scan   [--rows 100000000] [--nq 256]   fused scan+top-k variants
+  python benchmarks/micro.py gemm                                   encoder GEMMs vs torch (hipBLASLt)
+  python benchmarks/micro.py encoder [--batch 256 --seq 128]        whole encoder forward
+  python benchmarks/micro.py attn                                   varlen attention
+
+Prints one JSON line per measurement (median / min over rounds).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def timeit(fn, iters=10):
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def ab(variants: dict, rounds=5, iters=10):
+    for f in variants.values():  # warm
+        f()
+    torch.cuda.synchronize()
+    res = {k: [] for k in variants}
+    for _ in range(rounds):
+        for k, f in variants.items():
+            res[k].append(timeit(f, iters))
+    return {k: (statistics.median(v), min(v)) for k, v in res.items()}
+
+
+def cmd_scan(a):
+    from codename_symbiont_amd.index.shard import HbmIndexShard, _round_up
+    from codename_symbiont_amd.ops._ext import hip, stream_handle
+
+    D = a.dim
+    shard = HbmIndexShard(D, a.rows, device="cuda")
+    shard.fill_random(a.rows, seed=1)
+    q = torch.nn.functional.normalize(torch.randn(a.nq, D, device="cuda"), dim=-1).bfloat16()
+    h = hip()
+    kmax = 16
+    lists, qpb = h.topk_geometry(D, kmax)
+    n_qblk = math.ceil(a.nq / qpb)
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    out = {}
+    for mult in (1, 2):
+        n_rblk = max(1, round(ncu * mult / n_qblk))
+        rpb = _round_up(math.ceil(a.rows / n_rblk), 64)
+        n_rblk = math.ceil(a.rows / rpb)
+        ncand = n_rblk * lists * kmax
+        cs = torch.empty(a.nq, ncand, device="cuda")
+        ci = torch.empty(a.nq, ncand, dtype=torch.int32, device="cuda")
+        st = stream_handle()
+        variants = {}
+        for ns in ((2, 3) if D == 384 else (0,)):
+            for aux in (0, 2):
+                def f(ns=ns, aux=aux):
+                    h.index_scan(shard.rows.data_ptr(), a.rows, D, rpb, n_rblk, q.data_ptr(), a.nq,
+                                 kmax, cs.data_ptr(), ci.data_ptr(), st, ns, aux)
+                variants[f"blk{mult}x_ns{ns}_aux{aux}"] = f
+        r = ab(variants, rounds=a.rounds, iters=a.iters)
+        for k, (med, mn) in r.items():
+            gbs = a.rows * D * 2 / (med / 1e3) / 1e9
+            tf = 2 * a.rows * D * a.nq / (med / 1e3) / 1e12
+            out[k] = dict(ms=round(med, 3), min_ms=round(mn, 3), GBps=round(gbs), TFLOPs=round(tf))
+    print(json.dumps({"bench": "scan", "rows": a.rows, "dim": D, "nq": a.nq, "results": out}))
+
+
+def cmd_scanabl(a):
+    """DMA-only vs compute-only vs full scan (D=384), plus a plain torch streaming read."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard, _round_up
+    from codename_symbiont_amd.ops._ext import hip, stream_handle
+
+    D = 384
+    shard = HbmIndexShard(D, a.rows, device="cuda")
+    shard.fill_random(a.rows, seed=1)
+    q = torch.nn.functional.normalize(torch.randn(a.nq, D, device="cuda"), dim=-1).bfloat16()
+    h = hip()
+    n_qblk = math.ceil(a.nq / 256)
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    n_rblk = max(1, round(ncu / n_qblk))
+    rpb = _round_up(math.ceil(a.rows / n_rblk), 64)
+    n_rblk = math.ceil(a.rows / rpb)
+    cs = torch.empty(a.nq, n_rblk * 2 * 16, device="cuda")
+    ci = torch.empty(a.nq, n_rblk * 2 * 16, dtype=torch.int32, device="cuda")
+    st = stream_handle()
+    flat = shard.rows[:a.rows].view(torch.int64)
+    variants = {f"abl{m}": (lambda m=m: h.index_scan_ablate(shard.rows.data_ptr(), a.rows, rpb, n_rblk,
+                                                            q.data_ptr(), a.nq, cs.data_ptr(),
+                                                            ci.data_ptr(), st, m)) for m in (0, 1, 2)}
+    variants["torch_int64_sum"] = lambda: flat.sum()
+    r = ab(variants, rounds=a.rounds, iters=a.iters)
+    out = {k: dict(ms=round(m, 3), GBps=round(a.rows * D * 2 / (m / 1e3) / 1e9)) for k, (m, _) in r.items()}
+    print(json.dumps({"bench": "scan_ablation", "rows": a.rows, "nq": a.nq, "results": out}))
+
+
+def cmd_gemm(a):
+    from codename_symbiont_amd.ops import kernels as K
+
+    M = a.batch * a.seq
+    shapes = [("qkv", 1152, 384, K.EPI_BIAS), ("out+ln", 384, 384, K.EPI_RES_LN),
+              ("ffn1", 1536, 384, K.EPI_GELU), ("ffn2+ln", 384, 1536, K.EPI_RES_LN)]
+    out = {}
+    for name, N, Kd, epi in shapes:
+        x = torch.randn(M, Kd, device="cuda").bfloat16()
+        w = (torch.randn(N, Kd, device="cuda") / math.sqrt(Kd)).bfloat16()
+        b = torch.randn(N, device="cuda")
+        r = torch.randn(M, N, device="cuda").bfloat16()
+        g = torch.ones(N, device="cuda")
+        be = torch.zeros(N, device="cuda")
+        y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        res = ab({
+            "hip_fused": lambda: K.gemm(x, w, b, epi, r if epi >= 2 else None, g, be, 1e-12, out=y),
+            "torch_matmul_only": lambda: torch.matmul(x, w.t(), out=y),
+        }, rounds=a.rounds, iters=a.iters)
+        fl = 2 * M * N * Kd
+        out[name] = {k: dict(ms=round(m, 4), TFLOPs=round(fl / (m / 1e3) / 1e12)) for k, (m, _) in res.items()}
+    print(json.dumps({"bench": "gemm", "M": M, "results": out}))
+
+
+def cmd_encoder(a):
+    from codename_symbiont_amd.models import get_config
+    from codename_symbiont_amd.models.encoder import HipEncoder, synthetic_batch
+
+    cfg = get_config(a.model)
+    enc = HipEncoder(cfg, seed=0)
+    b = synthetic_batch(cfg, a.batch, a.seq, seed=0).to("cuda")
+    o1 = torch.empty(a.batch, cfg.hidden, device="cuda")
+    o2 = torch.empty(a.batch, cfg.hidden, device="cuda", dtype=torch.bfloat16)
+    res = ab({"forward": lambda: enc.forward_packed(b, o1, o2)}, rounds=a.rounds, iters=a.iters)
+    m = res["forward"][0]
+    toks = a.batch * a.seq
+    fl = cfg.flops_per_token(a.seq) * toks
+    print(json.dumps({"bench": "encoder", "model": a.model, "batch": a.batch, "seq": a.seq,
+                      "ms": round(m, 3), "embeds_per_s": round(a.batch / (m / 1e3)),
+                      "TFLOPs": round(fl / (m / 1e3) / 1e12)}))
+
+
+def cmd_attn(a):
+    from codename_symbiont_amd.ops import kernels as K
+
+    nh, hd = 12, a.head_dim
+    cu = torch.arange(0, (a.batch + 1) * a.seq, a.seq, dtype=torch.int32, device="cuda")
+    qkv = torch.randn(a.batch * a.seq, 3 * nh * hd, device="cuda").bfloat16()
+    out = torch.empty(a.batch * a.seq, nh * hd, device="cuda", dtype=torch.bfloat16)
+    res = ab({"attn": lambda: K.attention(qkv, cu, a.seq, nh, hd, out=out)}, a.rounds, a.iters)
+    m = res["attn"][0]
+    fl = 4 * a.batch * nh * a.seq * a.seq * hd
+    print(json.dumps({"bench": "attn", "ms": round(m, 4), "TFLOPs": round(fl / (m / 1e3) / 1e12)}))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("cmd", choices=["scan", "scanabl", "gemm", "encoder", "attn"])
+    ap.add_argument("--rows", type=int, default=100_000_000)
+    ap.add_argument("--dim", type=int, default=384)
+    ap.add_argument("--nq", type=int, default=256)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--seq", type=int, default=128)
+    ap.add_argument("--head-dim", type=int, default=32)
+    ap.add_argument("--model", default="minilm-l6")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=5)
+    a = ap.parse_args()
+    {"scan": cmd_scan, "scanabl": cmd_scanabl, "gemm": cmd_gemm, "encoder": cmd_encoder, "attn": cmd_attn}[a.cmd](a)
+
+
+if __name__ == "__main__":
+    main()

@@ -18,7 +18,7 @@ from dataclasses import dataclass
 
 import torch
 
-TILE_ROWS = 32
+TILE_ROWS = 64  # scan tile: 2 MFMA sub-tiles per barrier interval
 
 
 def _round_up(x: int, m: int) -> int:
@@ -87,6 +87,8 @@ class HbmIndexShard:
         self.count = 0
         self.payloads = PayloadStore()
         self._ws: dict = {}
+        self.scan_ns = 0     # LDS ring depth of the fused scan (0 = kernel default)
+        self.scan_aux = -1   # index-stream cache policy (-1 = auto: non-temporal when read once)
 
     # ------------------------------------------------------------------ inserts
     def _reserve(self, n: int) -> int:
@@ -193,7 +195,7 @@ class HbmIndexShard:
         st = stream_handle(self.device)
         h = hip()
         h.index_scan(self.rows.data_ptr(), n, self.dim, rows_per_blk, n_rblk, q_unit.data_ptr(),
-                     NQ, kmax, cs.data_ptr(), ci.data_ptr(), st)
+                     NQ, kmax, cs.data_ptr(), ci.data_ptr(), st, self.scan_ns, self.scan_aux)
         h.topk_merge(cs.data_ptr(), ci.data_ptr(), NQ, ncand, kmax, k, out_s.data_ptr(),
                      out_i.data_ptr(), 0, 0, st)
         return out_s, out_i

@@ -35,7 +35,10 @@ int symb_attention(const void* qkv, int ld_qkv, const int32_t* cu, int B, int ma
                    int n_heads, int head_dim, void* out, int ld_out, hipStream_t st);
 int symb_topk_geometry(int D, int kmax, int* lists, int* queries_per_blk);
 int symb_index_scan(const void* X, int n_valid, int D, int rows_per_blk, int n_rblk,
-                    const void* Q, int NQ, int kmax, float* cand_s, int* cand_i, hipStream_t st);
+                    const void* Q, int NQ, int kmax, float* cand_s, int* cand_i, hipStream_t st,
+                    int ns, int aux);
+int symb_index_scan_ablate(const void* X, int n_valid, int rows_per_blk, int n_rblk,
+                           const void* Q, int NQ, float* cs, int* ci, hipStream_t st, int abl);
 int symb_topk_merge(const float* cand_s, const int* cand_i, int NQ, int n_cand_per_query,
                     int kmax, int k, float* out_s, int* out_i, int64_t id_offset,
                     int64_t* out_id64, hipStream_t st);
@@ -181,10 +184,18 @@ PYBIND11_MODULE(_hip, m) {
     return py::make_tuple(lists, qpb);
   });
   m.def("index_scan", [](uptr X, int n_valid, int D, int rows_per_blk, int n_rblk, uptr Q, int NQ,
-                         int kmax, uptr cand_s, uptr cand_i, uptr st) {
+                         int kmax, uptr cand_s, uptr cand_i, uptr st, int ns, int aux) {
     check(symb_index_scan(P<void>(X), n_valid, D, rows_per_blk, n_rblk, P<void>(Q), NQ, kmax,
-                          P<float>(cand_s), P<int>(cand_i), S(st)),
+                          P<float>(cand_s), P<int>(cand_i), S(st), ns, aux),
           "index_scan");
+  }, py::arg("X"), py::arg("n_valid"), py::arg("D"), py::arg("rows_per_blk"), py::arg("n_rblk"),
+     py::arg("Q"), py::arg("NQ"), py::arg("kmax"), py::arg("cand_s"), py::arg("cand_i"),
+     py::arg("stream"), py::arg("ns") = 0, py::arg("aux") = -1);
+  m.def("index_scan_ablate", [](uptr X, int n_valid, int rows_per_blk, int n_rblk, uptr Q, int NQ,
+                                uptr cs, uptr ci, uptr st, int abl) {
+    check(symb_index_scan_ablate(P<void>(X), n_valid, rows_per_blk, n_rblk, P<void>(Q), NQ,
+                                 P<float>(cs), P<int>(ci), S(st), abl),
+          "index_scan_ablate");
   });
   m.def("topk_merge", [](uptr cand_s, uptr cand_i, int NQ, int n_cand, int kmax, int k,
                          uptr out_s, uptr out_i, int64_t id_offset, uptr out_id64, uptr st) {

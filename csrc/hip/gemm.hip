@@ -207,7 +207,7 @@ static int launch_cfg(const __bf16* A, int lda, const __bf16* W, int ldw, const 
   constexpr int lds = main_bytes > epi_bytes ? main_bytes : epi_bytes;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr_set = true;
   }
   const int nwg = ((M + BM - 1) / BM) * (N / BN);

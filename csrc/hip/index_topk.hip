@@ -21,10 +21,68 @@
 //  * A second small kernel merges the per-workgroup candidate lists into the final top-k.
 #include "common.h"
 
+#include <type_traits>
+
 namespace symb {
 
-constexpr int TOPK_NS = 4;       // LDS ring depth (tiles)
 constexpr int TOPK_WAVES = 8;
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+template <int AUX>
+__device__ __forceinline__ void glds16_aux(const void* gsrc, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(
+      (const __attribute__((address_space(1))) void*)gsrc,
+      (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, AUX);
+}
+
+// ---- hand-counted LDS fragment pipeline -------------------------------------------------------
+// hipcc will not count ds_reads around the DMA ring (it drains lgkmcnt(0) before every few MFMAs),
+// so the A fragments are read by inline asm and each MFMA waits with a counted lgkmcnt(N) whose
+// asm names the fragment as "+v" (the MFMA depends on it and cannot be hoisted above the wait).
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
+}
+
+template <int OFF>
+__device__ __forceinline__ void ds_read16(bf16x8& dst, uint32_t addr) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(addr), "i"(OFF));
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait(bf16x8& v) {
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(v) : "i"(N));
+}
+
+// Fragment ks lives at  base + voff[ks % M] + (ks / M) * 256  (the XOR swizzle only touches the
+// low 4 bits of the 16-byte chunk index, so the per-lane part repeats every M k-steps).
+template <int KS, int NKS, int PF, int M, bool M32>
+struct FragChain {
+  static constexpr int R = PF + 1;  // ring slots: a slot is refilled one MFMA after its last use
+  template <class Acc>
+  __device__ __forceinline__ static void run(Acc& acc, bf16x8 (&a)[R], const bf16x8 (&qf)[NKS],
+                                             const uint32_t (&voff)[M], uint32_t base) {
+    constexpr int outstanding = (NKS - KS < PF) ? (NKS - KS) : PF;
+    lgkm_wait<outstanding - 1>(a[KS % R]);
+    if constexpr (M32)
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[KS % R], qf[KS], acc, 0, 0, 0);
+    else
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[KS % R], qf[KS], acc, 0, 0, 0);
+    if constexpr (KS + PF < NKS)
+      ds_read16<((KS + PF) / M) * 256>(a[(KS + PF) % R], base + voff[(KS + PF) % M]);
+    if constexpr (KS + 1 < NKS) FragChain<KS + 1, NKS, PF, M, M32>::run(acc, a, qf, voff, base);
+  }
+};
+
+template <int J, int PF, int M, int R>
+__device__ __forceinline__ void frag_prologue(bf16x8 (&a)[R], const uint32_t (&voff)[M],
+                                              uint32_t base) {
+  ds_read16<(J / M) * 256>(a[J % R], base + voff[J % M]);
+  if constexpr (J + 1 < PF) frag_prologue<J + 1, PF, M, R>(a, voff, base);
+}
 
 template <int KMAX>
 __device__ __forceinline__ void topk_insert(float (&tv)[KMAX], int (&ti)[KMAX], float s, int id) {
@@ -42,20 +100,32 @@ __device__ __forceinline__ void topk_insert(float (&tv)[KMAX], int (&ti)[KMAX], 
 
 // MFMA_32 = true : D = 384 path (32x32x16, 32 queries per wave, 2 lists per query per wave)
 // MFMA_32 = false: D = 768/1024 path (16x16x32, 16 queries per wave, 4 lists per query per wave)
-template <int D, bool MFMA_32, int KMAX>
+// A barrier interval covers one TILE = 2 sub-tiles (2 x 32 rows, or 2 x 16 rows); the second
+// sub-tile's fragment reads are issued before the first sub-tile's top-k VALU work so LDS latency
+// and the VALU tail overlap, and the per-barrier fixed cost is paid once per 2 MFMA chains.
+// NS  : LDS ring depth in tiles (NS-2 tiles stay in flight across every barrier)
+// AUX : cache policy of the index stream (0 = default, 2 = non-temporal: rows read once)
+// ABL (profiling builds only): 0 = full kernel, 1 = DMA ring only (no MFMA / top-k),
+// 2 = compute only (no DMA; fragments come from whatever the LDS holds).
+template <int D, bool MFMA_32, int KMAX, int NS, int AUX, int ABL = 0>
 __global__ __launch_bounds__(512) void index_scan_topk_kernel(
     const __bf16* __restrict__ X, int n_valid, int rows_per_blk, const __bf16* __restrict__ Q,
     int NQ, int n_qblk, float* __restrict__ cand_s, int* __restrict__ cand_i) {
   constexpr int CPR = D / 8;                          // 16-byte chunks per row
-  constexpr int TR = MFMA_32 ? 32 : 16;               // rows per LDS tile (<= 32 KiB per tile)
+  constexpr int SUB = MFMA_32 ? 32 : 16;              // rows per MFMA chain (sub-tile)
+  constexpr int TR = 2 * SUB;                         // rows per barrier interval
   constexpr int TILE_BYTES = TR * D * 2;
+  constexpr int SUB_BYTES = SUB * D * 2;
   constexpr int LOADS = TILE_BYTES / (1024 * TOPK_WAVES);  // glds per wave per tile
   static_assert(TILE_BYTES % (1024 * TOPK_WAVES) == 0, "tile must split evenly over waves");
-  static_assert(LOADS == 3 || LOADS == 4, "vmcnt literal table");
-  static_assert(TOPK_NS * TILE_BYTES <= 160 * 1024, "LDS ring exceeds the CU's 160 KiB");
+  static_assert(NS >= 2 && NS * TILE_BYTES <= 160 * 1024, "LDS ring exceeds the CU's 160 KiB");
   constexpr int QW = MFMA_32 ? 32 : 16;               // queries per wave
   constexpr int NKS = MFMA_32 ? D / 16 : D / 32;      // MFMA k-steps over D
   constexpr int LISTS = MFMA_32 ? 2 : 4;
+  constexpr int M = MFMA_32 ? 8 : 4;                  // period of the per-lane fragment offsets
+  constexpr int PF = 6;                               // fragment reads in flight
+  using Acc = typename std::conditional<MFMA_32, f32x16, f32x4>::type;
+  constexpr int NR = MFMA_32 ? 16 : 4;                // accumulator registers per lane
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -87,10 +157,24 @@ __global__ __launch_bounds__(512) void index_scan_topk_kernel(
   auto issue = [&](int t) {
     const int tt = min(t, n_tiles - 1);  // past the end: re-load the last tile (keeps vmcnt exact)
     const __bf16* base = X + (size_t)(row_begin + tt * TR) * D;
-    char* dst = smem + (t % TOPK_NS) * TILE_BYTES;
+    char* dst = smem + (t % NS) * TILE_BYTES;
 #pragma unroll
-    for (int i = 0; i < LOADS; ++i) glds16(base + goff[i], dst + ((i * TOPK_WAVES + wave) * 64) * 16);
+    for (int i = 0; i < LOADS; ++i)
+      glds16_aux<AUX>(base + goff[i], dst + ((i * TOPK_WAVES + wave) * 64) * 16);
   };
+
+  // ---- per-lane LDS fragment offsets within a sub-tile (see FragChain) ----
+  const uint32_t lds_smem = lds_addr(smem);
+  uint32_t voff[M];
+  if constexpr (MFMA_32) {
+    const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int m = 0; m < M; ++m) voff[m] = (uint32_t)(r * D * 2 + (((2 * m + h) ^ (r & 15)) << 4));
+  } else {
+    const int r = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int m = 0; m < M; ++m) voff[m] = (uint32_t)(r * D * 2 + (((4 * m + g) ^ r) << 4));
+  }
 
   float tv[KMAX];
   int ti[KMAX];
@@ -101,77 +185,59 @@ __global__ __launch_bounds__(512) void index_scan_topk_kernel(
   }
   float thr = -INFINITY;
 
-  if (n_tiles > 0) {
+  // row of accumulator register r for this lane (relative to the sub-tile)
+  auto acc_row = [&](int r) {
+    return MFMA_32 ? (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5) : (lane >> 4) * 4 + r;
+  };
+  auto topk_update = [&](Acc& acc, int row0) {
+    if (row0 + SUB > row_end) {
 #pragma unroll
-    for (int p = 0; p < TOPK_NS - 1; ++p) issue(p);
-  }
-  for (int t = 0; t < n_tiles; ++t) {
-    // tile t landed for this wave once only the (NS-2) younger tiles' loads remain
-    static_assert(TOPK_NS == 4, "vmcnt literals assume 2 younger tiles in flight");
-    if constexpr (LOADS == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    if constexpr (LOADS == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    issue(t + TOPK_NS - 1);
-    const char* tile = smem + (t % TOPK_NS) * TILE_BYTES;
-    const int tile_row0 = row_begin + t * TR;
-    const bool partial = tile_row0 + TR > row_end;
-
-    if constexpr (MFMA_32) {
-      f32x16 acc;
+      for (int r = 0; r < NR; ++r)
+        if (row0 + acc_row(r) >= row_end) acc[r] = -INFINITY;
+    }
+    float mx = acc[0];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      const int arow = lane & 31;
+    for (int r = 1; r < NR; ++r) mx = fmaxf(mx, acc[r]);
+    if (mx > thr) {
 #pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) {
-        const int c = ks * 2 + (lane >> 5);
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(tile + arow * (D * 2) + ((c ^ (arow & 15)) << 4));
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[ks], acc, 0, 0, 0);
-      }
-      const int rbase = tile_row0 + 4 * (lane >> 5);
-      if (partial) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (rbase + (r & 3) + 8 * (r >> 2) >= row_end) acc[r] = -INFINITY;
-      }
-      float mx = acc[0];
-#pragma unroll
-      for (int r = 1; r < 16; ++r) mx = fmaxf(mx, acc[r]);
-      if (mx > thr) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          if (acc[r] > thr) {
-            topk_insert<KMAX>(tv, ti, acc[r], rbase + (r & 3) + 8 * (r >> 2));
-            thr = tv[KMAX - 1];
-          }
-        }
-      }
-    } else {
-      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-      const int arow = lane & 15;
-#pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) {
-        const int c = ks * 4 + (lane >> 4);
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(tile + arow * (D * 2) + ((c ^ arow) << 4));
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[ks], acc, 0, 0, 0);
-      }
-      const int rbase = tile_row0 + (lane >> 4) * 4;
-      if (partial) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (rbase + r >= row_end) acc[r] = -INFINITY;
-      }
-      const float mx = fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3]));
-      if (mx > thr) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          if (acc[r] > thr) {
-            topk_insert<KMAX>(tv, ti, acc[r], rbase + r);
-            thr = tv[KMAX - 1];
-          }
+      for (int r = 0; r < NR; ++r) {
+        if (acc[r] > thr) {
+          topk_insert<KMAX>(tv, ti, acc[r], row0 + acc_row(r));
+          thr = tv[KMAX - 1];
         }
       }
     }
+  };
+
+  if (n_tiles > 0 && ABL != 2) {
+#pragma unroll
+    for (int p = 0; p < NS - 1; ++p) issue(p);
+  }
+  constexpr int R = PF + 1;
+  bf16x8 a[R];
+  for (int t = 0; t < n_tiles; ++t) {
+    // tile t landed for this wave once only the (NS-2) younger tiles' loads remain
+    if constexpr (ABL != 2) wait_vmcnt<LOADS * (NS - 2)>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if constexpr (ABL != 2) issue(t + NS - 1);
+    if constexpr (ABL == 1) continue;
+    const uint32_t base0 = lds_smem + (uint32_t)((t % NS) * TILE_BYTES);
+    const uint32_t base1 = base0 + SUB_BYTES;
+    const int row0 = row_begin + t * TR;
+
+    Acc acc0, acc1;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      acc0[r] = 0.f;
+      acc1[r] = 0.f;
+    }
+    frag_prologue<0, PF, M, R>(a, voff, base0);
+    FragChain<0, NKS, PF, M, MFMA_32>::run(acc0, a, qf, voff, base0);
+    frag_prologue<0, PF, M, R>(a, voff, base1);   // sub-tile 1 reads fly during top-k of sub 0
+    topk_update(acc0, row0);
+    FragChain<0, NKS, PF, M, MFMA_32>::run(acc1, a, qf, voff, base1);
+    topk_update(acc1, row0 + SUB);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the tail prefetches before exit
 
@@ -275,14 +341,14 @@ int symb_topk_geometry(int D, int kmax, int* lists, int* queries_per_blk) {
   return 0;
 }
 
-template <int D, bool M32, int KMAX>
+template <int D, bool M32, int KMAX, int NS, int AUX>
 static int launch_scan(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                        int NQ, int n_qblk, float* cs, int* ci, hipStream_t st) {
-  auto kern = index_scan_topk_kernel<D, M32, KMAX>;
-  constexpr int lds = TOPK_NS * (M32 ? 32 : 16) * D * 2;
+  auto kern = index_scan_topk_kernel<D, M32, KMAX, NS, AUX>;
+  constexpr int lds = NS * (M32 ? 64 : 32) * D * 2;
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
   hipLaunchKernelGGL(kern, dim3(n_rblk * n_qblk), dim3(512), lds, st, (const __bf16*)X, n_valid,
@@ -290,24 +356,66 @@ static int launch_scan(const void* X, int n_valid, int rows_per_blk, int n_rblk,
   return (int)hipGetLastError();
 }
 
+// Profiling-only entry: time the DMA ring alone (abl=1) or the compute alone (abl=2), D=384.
+int symb_index_scan_ablate(const void* X, int n_valid, int rows_per_blk, int n_rblk,
+                           const void* Q, int NQ, float* cs, int* ci, hipStream_t st, int abl) {
+  const int n_qblk = (NQ + 255) / 256;
+  auto go = [&](auto kern) {
+    constexpr int lds = 3 * 64 * 384 * 2;
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipLaunchKernelGGL(kern, dim3(n_rblk * n_qblk), dim3(512), lds, st, (const __bf16*)X, n_valid,
+                       rows_per_blk, (const __bf16*)Q, NQ, n_qblk, cs, ci);
+    return (int)hipGetLastError();
+  };
+  if (abl == 1) return go(index_scan_topk_kernel<384, true, 16, 3, 0, 1>);
+  if (abl == 2) return go(index_scan_topk_kernel<384, true, 16, 3, 0, 2>);
+  return go(index_scan_topk_kernel<384, true, 16, 3, 0, 0>);
+}
+
+// Default ring depth per D: as many 24-32 KiB tiles in flight as the 160 KiB LDS allows.
+template <int D> struct ScanCfg;
+template <> struct ScanCfg<384> { static constexpr bool M32 = true; static constexpr int NS = 3; };
+template <> struct ScanCfg<768> { static constexpr bool M32 = false; static constexpr int NS = 3; };
+template <> struct ScanCfg<1024> { static constexpr bool M32 = false; static constexpr int NS = 2; };
+
+template <int D, int NS>
+static int dispatch_k(int kmax, int aux, const void* X, int n_valid, int rows_per_blk, int n_rblk,
+                      const void* Q, int NQ, int n_qblk, float* cs, int* ci, hipStream_t st) {
+  constexpr bool M32 = ScanCfg<D>::M32;
+  if (kmax == 16)
+    return aux ? launch_scan<D, M32, 16, NS, 2>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, n_qblk, cs, ci, st)
+               : launch_scan<D, M32, 16, NS, 0>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, n_qblk, cs, ci, st);
+  return aux ? launch_scan<D, M32, 32, NS, 2>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, n_qblk, cs, ci, st)
+             : launch_scan<D, M32, 32, NS, 0>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, n_qblk, cs, ci, st);
+}
+
 // X: [>= round_up(n_valid, 32), D] bf16 unit rows; Q: [NQ, D] bf16 unit rows.
-// rows_per_blk must be a multiple of 32; n_rblk * rows_per_blk >= n_valid.
+// rows_per_blk must be a multiple of 64; n_rblk * rows_per_blk >= n_valid.
+// ns = 0 -> default ring depth; aux = -1 -> non-temporal iff each index row is read by one block.
 int symb_index_scan(const void* X, int n_valid, int D, int rows_per_blk, int n_rblk,
-                    const void* Q, int NQ, int kmax, float* cand_s, int* cand_i, hipStream_t st) {
+                    const void* Q, int NQ, int kmax, float* cand_s, int* cand_i, hipStream_t st,
+                    int ns, int aux) {
   if (NQ <= 0 || n_rblk <= 0) return 0;
-  if (rows_per_blk % 32) return -1;
+  if (rows_per_blk % 64) return -1;
   int lists, qpb;
   if (symb_topk_geometry(D, kmax, &lists, &qpb)) return -1;
   const int n_qblk = (NQ + qpb - 1) / qpb;
-#define SYMB_SCAN(DD, M32)                                                                     \
-  return kmax == 16 ? launch_scan<DD, M32, 16>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, n_qblk, \
-                                               cand_s, cand_i, st)                              \
-                    : launch_scan<DD, M32, 32>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, n_qblk, \
-                                               cand_s, cand_i, st);
-  if (D == 384) { SYMB_SCAN(384, true) }
-  if (D == 768) { SYMB_SCAN(768, false) }
-  if (D == 1024) { SYMB_SCAN(1024, false) }
-#undef SYMB_SCAN
+  if (aux < 0) aux = n_qblk == 1 ? 2 : 0;
+#define SYMB_ARGS kmax, aux, X, n_valid, rows_per_blk, n_rblk, Q, NQ, n_qblk, cand_s, cand_i, st
+  if (D == 384) {
+    if (ns == 0 || ns == 3) return dispatch_k<384, 3>(SYMB_ARGS);
+    if (ns == 2) return dispatch_k<384, 2>(SYMB_ARGS);
+    return -1;
+  }
+  if (D == 768) {
+    if (ns == 0 || ns == 3) return dispatch_k<768, 3>(SYMB_ARGS);
+    return -1;
+  }
+  if (D == 1024) {
+    if (ns == 0 || ns == 2) return dispatch_k<1024, 2>(SYMB_ARGS);
+    return -1;
+  }
+#undef SYMB_ARGS
   return -1;
 }
 
