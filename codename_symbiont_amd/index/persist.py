@@ -1,0 +1,148 @@
+"""Checkpoint / resume of an HBM index shard: snapshot + append-only WAL.
+
+The reference persists through Qdrant (on-disk vectors + payload, vector_memory_service/src/main.rs
+:39,52; docker volume ./data/qdrant_storage).  The HBM index is volatile, so each shard keeps:
+
+  <dir>/snapshot/meta.json        {"dim", "count", "format": 1}
+  <dir>/snapshot/vectors.npy      count x dim bf16 bit patterns (uint16 .npy, memory-mappable)
+  <dir>/snapshot/payloads.jsonl   one [point_id, doc_id, url, text, order, model, ts] per row
+  <dir>/wal.log                   records appended (and fsync'd) per upsert batch
+
+WAL record: magic u32 | n u32 | body_len u32 | crc32(body) u32 | body, body = n x
+(u16 id_len, id, u32 payload_len, payload JSON, f32[dim]).  A torn tail record (crash mid-write)
+fails its length/CRC check and is dropped on replay.  Boot = mmap snapshot -> HBM, replay WAL.
+"""
+from __future__ import annotations
+
+import json
+import os
+import struct
+import zlib
+
+import numpy as np
+import torch
+
+from .shard import HbmIndexShard, Payload
+
+MAGIC = 0x53594D42  # "SYMB"
+_HDR = struct.Struct("<IIII")
+
+
+class Wal:
+    def __init__(self, path: str, dim: int):
+        self.path = path
+        self.dim = dim
+        os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+        self._f = open(path, "ab")
+
+    def append(self, point_ids: list[str], payloads: list[Payload], vecs: np.ndarray) -> None:
+        vecs = np.ascontiguousarray(vecs, dtype=np.float32)
+        assert vecs.shape == (len(point_ids), self.dim)
+        parts = []
+        for pid, p, v in zip(point_ids, payloads, vecs):
+            b = pid.encode()
+            pj = json.dumps([p.original_document_id, p.source_url, p.sentence_text,
+                             p.sentence_order, p.model_name, p.processed_at_ms],
+                            ensure_ascii=False).encode()
+            parts += [struct.pack("<H", len(b)), b, struct.pack("<I", len(pj)), pj, v.tobytes()]
+        body = b"".join(parts)
+        self._f.write(_HDR.pack(MAGIC, len(point_ids), len(body), zlib.crc32(body)) + body)
+        self._f.flush()
+        os.fsync(self._f.fileno())
+
+    def truncate(self) -> None:
+        self._f.close()
+        self._f = open(self.path, "wb")
+        self._f.flush()
+        os.fsync(self._f.fileno())
+
+    def close(self) -> None:
+        self._f.close()
+
+    @staticmethod
+    def replay(path: str, dim: int):
+        """Yields (point_ids, payloads, vecs) per intact record."""
+        if not os.path.exists(path):
+            return
+        with open(path, "rb") as f:
+            data = f.read()
+        off = 0
+        while off + _HDR.size <= len(data):
+            magic, n, blen, crc = _HDR.unpack_from(data, off)
+            body = data[off + _HDR.size: off + _HDR.size + blen]
+            if magic != MAGIC or len(body) != blen or zlib.crc32(body) != crc:
+                break  # torn / corrupt tail
+            off += _HDR.size + blen
+            ids, pls, vs = [], [], []
+            o = 0
+            for _ in range(n):
+                (lb,) = struct.unpack_from("<H", body, o)
+                o += 2
+                ids.append(body[o:o + lb].decode())
+                o += lb
+                (lp,) = struct.unpack_from("<I", body, o)
+                o += 4
+                a = json.loads(body[o:o + lp])
+                o += lp
+                pls.append(Payload(*a))
+                vs.append(np.frombuffer(body, dtype=np.float32, count=dim, offset=o))
+                o += 4 * dim
+            yield ids, pls, np.stack(vs) if vs else np.zeros((0, dim), np.float32)
+
+
+def save_snapshot(shard: HbmIndexShard, directory: str, chunk: int = 1 << 20) -> None:
+    snap = os.path.join(directory, "snapshot")
+    tmp = snap + ".tmp"
+    os.makedirs(tmp, exist_ok=True)
+    n, D = shard.count, shard.dim
+    mm = np.lib.format.open_memmap(os.path.join(tmp, "vectors.npy"), mode="w+",
+                                   dtype=np.uint16, shape=(n, D)) if n else None
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        mm[s:e] = shard.rows[s:e].view(torch.int16).cpu().numpy().view(np.uint16)
+    if mm is not None:
+        mm.flush()
+        del mm
+    with open(os.path.join(tmp, "payloads.jsonl"), "w", encoding="utf-8") as f:
+        ps = shard.payloads
+        for r in range(n):
+            pid, p = ps.get(r)
+            f.write(json.dumps([pid, p.original_document_id, p.source_url, p.sentence_text,
+                                p.sentence_order, p.model_name, p.processed_at_ms],
+                               ensure_ascii=False) + "\n")
+    with open(os.path.join(tmp, "meta.json"), "w") as f:
+        json.dump({"dim": D, "count": n, "format": 1}, f)
+    if os.path.exists(snap):
+        old = snap + ".old"
+        os.replace(snap, old)
+        os.replace(tmp, snap)
+        for fn in os.listdir(old):
+            os.remove(os.path.join(old, fn))
+        os.rmdir(old)
+    else:
+        os.replace(tmp, snap)
+
+
+def load_snapshot(shard: HbmIndexShard, directory: str, chunk: int = 1 << 20) -> int:
+    snap = os.path.join(directory, "snapshot")
+    meta_p = os.path.join(snap, "meta.json")
+    if not os.path.exists(meta_p):
+        return 0
+    with open(meta_p) as f:
+        meta = json.load(f)
+    if meta["dim"] != shard.dim:
+        raise ValueError(f"snapshot dim {meta['dim']} != index dim {shard.dim}")
+    n = meta["count"]
+    if n == 0:
+        return 0
+    mm = np.load(os.path.join(snap, "vectors.npy"), mmap_mode="r")
+    r0 = shard._reserve(n)
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        t = torch.from_numpy(np.ascontiguousarray(mm[s:e]).view(np.int16)).view(torch.bfloat16)
+        shard.rows[r0 + s:r0 + e].copy_(t.to(shard.device))
+    with open(os.path.join(snap, "payloads.jsonl"), encoding="utf-8") as f:
+        for r, line in enumerate(f):
+            a = json.loads(line)
+            shard.payloads.set(r0 + r, a[0], Payload(*a[1:]))
+    return n

@@ -1,0 +1,112 @@
+"""VectorStore: the Qdrant-collection replacement used by vector_memory_service.
+
+One HBM shard (or, with ``group``, the rank-0 view of a multi-GPU IndexGroup) + host payload
+store + durability (WAL per upsert batch, periodic snapshots).  API mirrors what the reference
+does with qdrant-client (vector_memory_service/src/main.rs): ``upsert`` points with UUID ids
+and 6-field payloads (wait=true semantics: durable + searchable on return) and ``search``
+(limit=top_k, payload on, vectors off, no filter / threshold), returning cosine scores sorted
+descending with fewer than k results when the collection is small.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import threading
+
+import numpy as np
+import torch
+
+from .persist import Wal, load_snapshot, save_snapshot
+from .shard import HbmIndexShard, Payload
+
+log = logging.getLogger("symbiont.index")
+
+
+class DimensionError(ValueError):
+    pass
+
+
+class VectorStore:
+    def __init__(self, dim: int, capacity: int, device=None, snapshot_dir: str = "",
+                 snapshot_every: int = 100_000, group=None):
+        if device is None:
+            device = "cuda" if torch.cuda.is_available() else "cpu"
+        self.dim = dim
+        self.group = group
+        self.shard = group.shard if group is not None else HbmIndexShard(dim, capacity, device)
+        self.dir = snapshot_dir
+        self.snapshot_every = snapshot_every
+        self._since_snapshot = 0
+        self._lock = threading.Lock()
+        self.wal = None
+        if snapshot_dir:
+            os.makedirs(snapshot_dir, exist_ok=True)
+            n = load_snapshot(self.shard, snapshot_dir)
+            m = 0
+            for ids, pls, vecs in Wal.replay(os.path.join(snapshot_dir, "wal.log"), dim):
+                self._upsert_nolog(ids, vecs, pls)
+                m += len(ids)
+            log.info("[INDEX_RESTORE] snapshot rows=%d, WAL replayed=%d", n, m)
+            self.wal = Wal(os.path.join(snapshot_dir, "wal.log"), dim)
+
+    @property
+    def count(self) -> int:
+        return self.shard.count
+
+    def _upsert_nolog(self, point_ids, vecs, payloads):
+        t = torch.as_tensor(np.ascontiguousarray(vecs, dtype=np.float32))
+        if self.group is not None:
+            return self.group.upsert(point_ids, t, payloads)
+        return self.shard.upsert(point_ids, t, payloads)
+
+    def upsert(self, point_ids: list[str], vecs: np.ndarray, payloads: list[Payload]) -> None:
+        vecs = np.asarray(vecs, dtype=np.float32)
+        if vecs.ndim != 2 or vecs.shape[1] != self.dim:
+            got = vecs.shape[-1] if vecs.ndim else 0
+            raise DimensionError(f"Wrong input: Vector dimension error: expected dim: {self.dim}, got {got}")
+        with self._lock:
+            if self.wal is not None:
+                self.wal.append(point_ids, payloads, vecs)
+            self._upsert_nolog(point_ids, vecs, payloads)
+            if self.shard.device.type == "cuda":
+                torch.cuda.synchronize(self.shard.device)  # wait=true: searchable on return
+            self._since_snapshot += len(point_ids)
+            if self.wal is not None and self._since_snapshot >= self.snapshot_every:
+                self.snapshot()
+
+    def snapshot(self) -> None:
+        if not self.dir:
+            return
+        save_snapshot(self.shard, self.dir)
+        if self.wal is not None:
+            self.wal.truncate()
+        self._since_snapshot = 0
+
+    def search(self, queries: np.ndarray, k: int):
+        """queries f32 [nq, D] (any norm) -> (scores f32 [nq, k'], rows int64 [nq, k']); -1 = empty."""
+        q = np.asarray(queries, dtype=np.float32)
+        if q.ndim == 1:
+            q = q[None]
+        if q.shape[1] != self.dim:
+            raise DimensionError(f"Wrong input: Vector dimension error: expected dim: {self.dim}, "
+                                 f"got {q.shape[1]}")
+        k = int(k)
+        if k <= 0 or self.count == 0:
+            return np.zeros((q.shape[0], 0), np.float32), np.zeros((q.shape[0], 0), np.int64)
+        qt = torch.nn.functional.normalize(torch.from_numpy(q).to(self.shard.device), dim=-1)
+        qt = qt.to(torch.bfloat16)
+        if self.group is not None:
+            s, r = self.group.search(qt, k)
+        else:
+            s, r = self.shard.search(qt, k)
+        return s.float().cpu().numpy(), r.long().cpu().numpy()
+
+    def lookup(self, gid: int):
+        if self.group is not None:
+            return self.group.payload(gid)
+        return self.shard.payloads.get(int(gid))
+
+    def close(self) -> None:
+        if self.wal is not None:
+            self.snapshot()
+            self.wal.close()

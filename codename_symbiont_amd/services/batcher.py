@@ -1,0 +1,172 @@
+"""Dynamic micro-batchers in front of the GPU.
+
+The reference encodes each message's sentences in fixed chunks of 8 padded to 514 tokens and
+handles every query with its own B=1 forward (embedding_generator.rs:146, preprocessing main.rs
+:205-246), blocking a tokio worker meanwhile.  Here concurrent requests from
+any number of handlers are coalesced (up to a token budget / a short window) into ONE packed
+varlen launch executed off the event loop, and the results are scattered back to the callers.
+The same pattern batches concurrent semantic searches into one fused index scan.
+"""
+from __future__ import annotations
+
+import asyncio
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+
+@dataclass
+class _Req:
+    texts: list
+    fut: asyncio.Future
+    t0: float = field(default_factory=time.perf_counter)
+
+
+class EmbedBatcher:
+    def __init__(self, encoder, tokenizer, token_budget: int = 65536, window_ms: float = 2.0,
+                 max_seqs: int = 4096, metrics=None):
+        self.encoder = encoder
+        self.tok = tokenizer
+        self.token_budget = token_budget
+        self.window = window_ms / 1000.0
+        self.max_seqs = max_seqs
+        self.metrics = metrics
+        self._q: asyncio.Queue = asyncio.Queue()
+        self._task: asyncio.Task | None = None
+        self._lock = asyncio.Lock()
+
+    def start(self) -> None:
+        if self._task is None:
+            self._task = asyncio.create_task(self._run())
+
+    async def embed(self, texts: list[str]) -> np.ndarray:
+        """-> float32 [len(texts), H] pooled embeddings (the wire representation)."""
+        if not texts:
+            return np.zeros((0, self.encoder.cfg.hidden), np.float32)
+        self.start()
+        fut = asyncio.get_running_loop().create_future()
+        await self._q.put(_Req(list(texts), fut))
+        return await fut
+
+    async def _run(self) -> None:
+        loop = asyncio.get_running_loop()
+        while True:
+            first = await self._q.get()
+            batch = [first]
+            n = len(first.texts)
+            deadline = loop.time() + self.window
+            while n < self.max_seqs:
+                timeout = deadline - loop.time()
+                if timeout <= 0:
+                    break
+                try:
+                    r = await asyncio.wait_for(self._q.get(), timeout)
+                except asyncio.TimeoutError:
+                    break
+                batch.append(r)
+                n += len(r.texts)
+            texts = [t for r in batch for t in r.texts]
+            try:
+                out = await loop.run_in_executor(None, self._encode_all, texts)
+            except Exception as e:  # propagate to every waiter
+                for r in batch:
+                    if not r.fut.done():
+                        r.fut.set_exception(e)
+                continue
+            o = 0
+            for r in batch:
+                if not r.fut.done():
+                    r.fut.set_result(out[o:o + len(r.texts)])
+                o += len(r.texts)
+                if self.metrics is not None:
+                    self.metrics.observe("embed.request", (time.perf_counter() - r.t0) * 1e3)
+            if self.metrics is not None:
+                self.metrics.inc("embed.sentences", len(texts))
+                self.metrics.inc("embed.launch_groups")
+
+    def _encode_all(self, texts: list[str]) -> np.ndarray:
+        """Tokenize (native, GIL released) and run token-budgeted packed forwards."""
+        from ..models.encoder import PackedBatch
+
+        cfg = self.encoder.cfg
+        ids, cu = self.tok.encode_packed(texts)
+        lens = np.diff(cu)
+        outs = []
+        s = 0
+        dev = getattr(self.encoder, "device", torch.device("cpu"))
+        while s < len(texts):
+            e, tok = s, 0
+            while e < len(texts) and (e == s or tok + lens[e] <= self.token_budget):
+                tok += int(lens[e])
+                e += 1
+            a, b = int(cu[s]), int(cu[e])
+            sub_ids = ids[a:b]
+            sub_cu = (cu[s:e + 1] - cu[s]).astype(np.int32)
+            pos = np.concatenate([np.arange(cfg.position_offset, cfg.position_offset + int(L),
+                                            dtype=np.int32) for L in lens[s:e]])
+            pb = PackedBatch(torch.from_numpy(np.ascontiguousarray(sub_ids)), torch.from_numpy(pos),
+                             None, torch.from_numpy(sub_cu), int(lens[s:e].max()))
+            if dev.type == "cuda":
+                pb = pb.to(dev, non_blocking=False)
+            pooled, _unit = self.encoder.forward_packed(pb)
+            outs.append(pooled.float().cpu().numpy())
+            s = e
+        return np.concatenate(outs, 0) if outs else np.zeros((0, cfg.hidden), np.float32)
+
+
+@dataclass
+class _SReq:
+    q: np.ndarray
+    k: int
+    fut: asyncio.Future
+
+
+class SearchBatcher:
+    """Coalesce concurrent searches into one fused scan (Q up to ``max_q`` queries per launch)."""
+
+    def __init__(self, search_fn, window_ms: float = 1.0, max_q: int = 256, metrics=None):
+        self.search_fn = search_fn  # (np.ndarray [nq, D] f32, k) -> (scores [nq,k], ids [nq,k])
+        self.window = window_ms / 1000.0
+        self.max_q = max_q
+        self.metrics = metrics
+        self._q: asyncio.Queue = asyncio.Queue()
+        self._task = None
+
+    async def search(self, q: np.ndarray, k: int):
+        if self._task is None:
+            self._task = asyncio.create_task(self._run())
+        fut = asyncio.get_running_loop().create_future()
+        await self._q.put(_SReq(np.asarray(q, np.float32).reshape(1, -1), int(k), fut))
+        return await fut
+
+    async def _run(self) -> None:
+        loop = asyncio.get_running_loop()
+        while True:
+            first = await self._q.get()
+            batch = [first]
+            deadline = loop.time() + self.window
+            while len(batch) < self.max_q:
+                timeout = deadline - loop.time()
+                if timeout <= 0:
+                    break
+                try:
+                    batch.append(await asyncio.wait_for(self._q.get(), timeout))
+                except asyncio.TimeoutError:
+                    break
+            kmax = max(r.k for r in batch)
+            qs = np.concatenate([r.q for r in batch], 0)
+            try:
+                s, i = await loop.run_in_executor(None, self.search_fn, qs, kmax)
+            except Exception as e:
+                for r in batch:
+                    if not r.fut.done():
+                        r.fut.set_exception(e)
+                continue
+            for j, r in enumerate(batch):
+                if not r.fut.done():
+                    r.fut.set_result((s[j, :r.k], i[j, :r.k]))
+            if self.metrics is not None:
+                self.metrics.inc("search.batched_queries", len(batch))
+                self.metrics.inc("search.launches")

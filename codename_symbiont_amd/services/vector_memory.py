@@ -1,0 +1,144 @@
+"""vector_memory_service: storage + semantic search over the in-HBM index
+(services/vector_memory_service/src/main.rs, with Qdrant replaced by index.store.VectorStore).
+
+* ``data.text.with_embeddings`` -> one point per sentence: fresh UUIDv4 id and the 6-field
+  payload {original_document_id, source_url, sentence_text, sentence_order (index within the
+  message, + ``sentence_order_offset`` when the producer chunked), model_name, processed_at_ms
+  (= message timestamp)} (main.rs:142-177); upsert is durable (WAL) before returning (wait=true).
+* ``tasks.search.semantic.request`` request/reply -> SemanticSearchNatsResult; concurrent
+  requests are coalesced into one fused MFMA scan by the SearchBatcher.  Error replies keep the
+  reference's texts ("Failed to deserialize SemanticSearchNatsTask: ...", request_id "unknown";
+  "Qdrant search failed for request_id <id>: <error>").
+"""
+from __future__ import annotations
+
+import asyncio
+import uuid
+
+import numpy as np
+
+from ..index.shard import Payload
+from ..index.store import VectorStore
+from ..models.config import get_config
+from ..ops._ext import native
+from ..utils import log as ulog
+from ..wire import (QdrantPointPayload, SemanticSearchNatsResult, SemanticSearchNatsTask,
+                    SemanticSearchResultItem, TextWithEmbeddingsMessage, WireError, subjects)
+from .base import Service
+from .batcher import SearchBatcher
+
+
+class VectorMemoryService(Service):
+    name = "vector_memory_service"
+
+    def __init__(self, *a, store: VectorStore | None = None, **kw):
+        super().__init__(*a, **kw)
+        dim = self.cfg.index_dim or get_config(self.cfg.model).hidden
+        self.store = store or VectorStore(dim, self.cfg.index_capacity,
+                                          device="cpu" if self.cfg.force_cpu else None,
+                                          snapshot_dir=self.cfg.snapshot_dir)
+        self.log.info("[INDEX_SETUP] collection '%s': dim %d, capacity %d, device %s, %d points",
+                      self.cfg.collection, dim, self.store.shard.capacity, self.store.shard.device,
+                      self.store.count)
+        self.searcher = SearchBatcher(self.store.search, metrics=self.metrics)
+
+    async def setup(self) -> None:
+        await self.subscribe_loop(subjects.TEXT_WITH_EMBEDDINGS, self.handle_store)
+        await self.subscribe_loop(subjects.SEARCH_SEMANTIC_REQUEST, self.handle_search)
+
+    # ------------------------------------------------------------------ storage
+    async def handle_store(self, nmsg) -> None:
+        try:
+            msg = TextWithEmbeddingsMessage.from_json(nmsg.data)
+        except WireError as e:
+            self.log.warning("[TASK_DESERIALIZE_FAIL] Failed to deserialize TextWithEmbeddingsMessage: %s", e)
+            return
+        offset = 0
+        try:  # extra field added by our chunking producer; absent from reference producers
+            offset = int(native().json_loads(bytes(nmsg.data), False).get("sentence_order_offset", 0))
+        except Exception:
+            offset = 0
+        self.log.info("[QDRANT_HANDLER] Received TextWithEmbeddingsMessage (original_id: %s), %d "
+                      "embeddings from model '%s'.", msg.original_id, len(msg.embeddings_data),
+                      msg.model_name)
+        if not msg.embeddings_data:
+            self.log.warning("[QDRANT_HANDLER] No embeddings data found in message for original_id: %s. "
+                             "Skipping.", msg.original_id)
+            return
+        ids = [str(uuid.uuid4()) for _ in msg.embeddings_data]
+        pls = [Payload(msg.original_id, msg.source_url, se.sentence_text, offset + i, msg.model_name,
+                       msg.timestamp_ms) for i, se in enumerate(msg.embeddings_data)]
+        try:
+            vecs = np.stack([np.asarray(se.embedding, np.float32) for se in msg.embeddings_data])
+        except ValueError as e:
+            self.log.error("[QDRANT_HANDLER_ERROR] ragged embeddings for original_id %s: %s",
+                           msg.original_id, e)
+            return
+        loop = asyncio.get_running_loop()
+        try:
+            await loop.run_in_executor(None, self.store.upsert, ids, vecs, pls)
+        except Exception as e:
+            self.log.error("[QDRANT_HANDLER_ERROR] Failed to upsert points for original_id %s: %s",
+                           msg.original_id, e)
+            self.metrics.inc("upsert_errors")
+            return
+        self.metrics.inc("points_upserted", len(ids))
+        self.log.info("[QDRANT_HANDLER] Successfully upserted %d points for original_id: %s",
+                      len(ids), msg.original_id)
+
+    # ------------------------------------------------------------------ search
+    async def reply(self, nmsg, res: SemanticSearchNatsResult) -> None:
+        if nmsg.reply:
+            await self.nc.publish(nmsg.reply, res.to_json())
+        else:
+            self.log.warning("[SEARCH_HANDLER] No reply subject provided for search task_id %s. "
+                             "Results not sent.", res.request_id)
+
+    async def handle_search(self, nmsg) -> None:
+        try:
+            task = SemanticSearchNatsTask.from_json(nmsg.data)
+        except WireError as e:
+            err = f"Failed to deserialize SemanticSearchNatsTask: {e}"
+            self.log.error("[SEARCH_HANDLER_DESERIALIZE_FAIL] %s", err)
+            await self.reply(nmsg, SemanticSearchNatsResult("unknown", [], err))
+            return
+        self.log.info("[SEARCH_HANDLER] Processing SemanticSearchNatsTask (request_id: %s, top_k: %d)",
+                      task.request_id, task.top_k)
+        try:
+            q = np.asarray(task.query_embedding, np.float32)
+            if q.shape[0] != self.store.dim:
+                raise ValueError(f"Wrong input: Vector dimension error: expected dim: {self.store.dim}, "
+                                 f"got {q.shape[0]}")
+            scores, rows = await self.searcher.search(q, task.top_k)
+        except Exception as e:
+            err = f"Qdrant search failed for request_id {task.request_id}: {e}"
+            self.log.error("[SEARCH_HANDLER_QDRANT_FAIL] %s", err)
+            await self.reply(nmsg, SemanticSearchNatsResult(task.request_id, [], err))
+            return
+        items = []
+        for s, r in zip(scores.tolist(), rows.tolist()):
+            if r < 0:
+                continue
+            pid, p = self.store.lookup(r)
+            if pid is None:
+                self.log.warning("[SEARCH_HANDLER] Found point with missing or unexpected ID format. Skipping.")
+                continue
+            items.append(SemanticSearchResultItem(pid, float(s), QdrantPointPayload(
+                p.original_document_id, p.source_url, p.sentence_text, int(p.sentence_order) & 0xFFFFFFFF,
+                p.model_name, int(p.processed_at_ms))))
+        await self.reply(nmsg, SemanticSearchNatsResult(task.request_id, items, None))
+        self.log.info("[SEARCH_HANDLER] Sent %d search results for request_id %s", len(items),
+                      task.request_id)
+
+    async def stop(self) -> None:
+        await super().stop()
+        self.store.close()
+
+
+def main() -> None:
+    ulog.setup(VectorMemoryService.name, "info")
+    asyncio.run(VectorMemoryService().run_forever())
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,141 @@
+"""WordPiece tokenizer front-end (native core: csrc/native/text.cpp).
+
+The reference downloads ``tokenizer.json`` from the HF Hub (embedding_generator.rs:25-58) and pads
+every input to max_position_embeddings (:75-91).  Offline, this module builds a DETERMINISTIC
+synthetic vocabulary with the real special-token layout of each family (BERT: [PAD]=0, [UNK]=100,
+[CLS]=101, [SEP]=102, [MASK]=103; XLM-R: <s>=0, <pad>=1, </s>=2, <unk>=3) and the real vocab size,
+or loads a real ``vocab.txt`` when ``SYMB_VOCAB`` points at one.  No padding is produced: outputs
+are packed varlen batches (ids + cu_seqlens) for the HIP encoder.
+"""
+from __future__ import annotations
+
+import functools
+import os
+
+import numpy as np
+
+from ..models.config import EncoderConfig
+from ..ops._ext import native
+
+_EN_WORDS = """the of and to in a is that for it as was with be by on not he i this are or his from at
+which but have an they you were her she there one all we their been has would when who will more no
+if out so said what up its about into than them can only other new some could time these two may
+then do first any my now such like our over man me even most made after also did many before must
+through back years where much your way well down should because each just those people how too
+little state good very make world still own see men work long get here between both life being under
+never day same another know while last might us great old year off come since against go came right
+used take three himself few house use during without again place around however home small found
+mrs thought went say part once general high upon school every does got united left number course war
+until always away something fact though water less public put think almost hand enough far took head
+yet government system better set told nothing night end why called didn find going look asked later
+knew point next program city business give group toward young days let room president side social
+given present several order national possible rather second face per among form important often
+things looked early white case john become large big need four within felt along children saw best
+church ever least power development light thing seemed family interest want members mind country area
+others done turned although open god service problem certain kind different thus began door help sense
+whole matter perhaps itself york times law human line above name example action company hands local
+show whether five history gave today either act feet across taken past quite anything seen having death
+week experience body word half really field am car words already themselves information tell together
+college shall money period held keep sure free seems real behind cannot miss political air question
+making office brought whose special heard major problems ago became federal moment study available
+known result street economic boy position reason change south board individual job society areas west
+close turn love community true court force full seem am semantic search vector index graph model text
+data embedding query document sentence token search gpu memory service api neural network learning""".split()
+
+_RU_WORDS = """и в не на я быть он с что а по это она этот к но они мы как из у который то за свой
+весь год от так о для ты же все тот мочь вы человек такой его сказать только или еще бы себя один
+когда уже до время если сам другой вот говорить наш мой знать стать при чтобы дело жизнь кто первый
+очень два день ее новый рука даже во со раз где там под можно ну какой после их работа без самый
+потом надо хотеть ли слово идти большой должен место иметь ничто пошел гулять парк увидел собаку
+собака была веселая решил ней поиграть дом город страна мир вопрос сторона дети голова друг система
+поиск текст документ модель данные граф память запрос""".split()
+
+_SUBWORDS = """s es ed ing ly er ers est tion tions ment ness able ible al ial ous ive ize ise ful less
+un re in dis pre de non over mis sub inter trans ity ism ist ance ence ant ent ary ory ic ical""".split()
+
+
+def _chars() -> list[str]:
+    cs = [chr(c) for c in range(33, 127) if not chr(c).isupper()]
+    cs += [chr(c) for c in range(0xDF, 0x100) if chr(c).islower()]
+    cs += [chr(c) for c in range(0x430, 0x450)] + ["ё", "і", "ї", "є", "ґ"]
+    cs += [chr(c) for c in range(0x3B1, 0x3CA)]
+    cs += [chr(c) for c in range(0x4E00, 0x4E00 + 512)]  # a slice of CJK ideographs
+    cs += ["¡", "§", "«", "¶", "·", "»", "¿", "–", "—", "‘", "’", "“", "”", "…", "€"]
+    seen, out = set(), []
+    for c in cs:
+        if c not in seen:
+            seen.add(c)
+            out.append(c)
+    return out
+
+
+@functools.lru_cache(maxsize=None)
+def synthetic_vocab(size: int, family: str = "bert", cased: bool = False) -> tuple[str, ...]:
+    if family == "xlmr":
+        vocab = ["<s>", "<pad>", "</s>", "<unk>"]
+    else:
+        vocab = ["[PAD]"] + [f"[unused{i}]" for i in range(99)] + ["[UNK]", "[CLS]", "[SEP]",
+                                                                     "[MASK]"]
+        vocab += [f"[unused{i}]" for i in range(99, 99 + 999 - len(vocab))]
+    chars = _chars()
+    if cased:
+        chars += [c.upper() for c in chars if c.upper() != c and len(c.upper()) == 1]
+    words = _EN_WORDS + _RU_WORDS
+    if cased:
+        words = words + [w.capitalize() for w in words]
+    base = list(dict.fromkeys(chars + ["##" + c for c in chars] + words +
+                              ["##" + s for s in _SUBWORDS] + _SUBWORDS))
+    seen = set(vocab)
+    for t in base:
+        if t not in seen:
+            vocab.append(t)
+            seen.add(t)
+    # deterministic filler: syllable pairs, then numbered pieces
+    rng = np.random.default_rng(12345)
+    syl = ["ba", "ko", "ri", "ne", "tu", "sa", "mi", "lo", "de", "pa", "ve", "zu", "ch", "st",
+           "ar", "en", "on", "in", "ta", "ro"]
+    i = 0
+    while len(vocab) < size:
+        if i < 8000:
+            a, b, c = rng.integers(0, len(syl), 3)
+            t = syl[a] + syl[b] + (syl[c] if i % 3 == 0 else "")
+            t = ("##" + t) if i % 2 else t
+        else:
+            t = f"##p{i}" if i % 2 else f"p{i}"
+        i += 1
+        if t not in seen:
+            vocab.append(t)
+            seen.add(t)
+    return tuple(vocab[:size])
+
+
+class Tokenizer:
+    """BERT BasicTokenizer + WordPiece in C++, configured for an encoder family."""
+
+    def __init__(self, cfg: EncoderConfig, vocab_file: str | None = None):
+        self.cfg = cfg
+        vocab_file = vocab_file if vocab_file is not None else os.environ.get("SYMB_VOCAB", "")
+        if vocab_file:
+            with open(vocab_file, encoding="utf-8") as f:
+                vocab = [line.rstrip("\n") for line in f]
+        else:
+            fam = "xlmr" if cfg.special["cls"] == "<s>" else "bert"
+            vocab = list(synthetic_vocab(cfg.vocab_size, fam, cased=not cfg.lowercase))
+        self.vocab = vocab
+        sp = cfg.special
+        self._wp = native().WordPiece(vocab, cfg.lowercase, sp["unk"], sp["cls"], sp["sep"], 100)
+        if self._wp.unk_id < 0 or self._wp.cls_id < 0 or self._wp.sep_id < 0:
+            raise ValueError("vocabulary lacks the special tokens of " + cfg.key)
+
+    def __len__(self):
+        return len(self.vocab)
+
+    def tokenize(self, text: str) -> list[str]:
+        return self._wp.tokenize(text)
+
+    def encode(self, text: str, max_len: int | None = None) -> list[int]:
+        return self._wp.encode(text, max_len or self.cfg.max_seq_len, True)
+
+    def encode_packed(self, texts: list[str], max_len: int | None = None):
+        """-> (ids int32 [T], cu_seqlens int32 [B+1]); truncation keeps [CLS] ... [SEP]."""
+        return self._wp.encode_packed(list(texts), max_len or self.cfg.max_seq_len)

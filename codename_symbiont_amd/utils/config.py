@@ -1,0 +1,74 @@
+"""Typed configuration: the reference's env-var surface plus the knobs it hard-codes.
+
+Compatible names: NATS_URL, API_SERVER_HOST, API_SERVER_PORT, NEO4J_URI, NEO4J_USER,
+NEO4J_PASSWORD, FORCE_CPU, RUST_LOG.  New (SYMB_*): model family, batch token budget, index
+dimension/capacity, snapshot dir, timeouts, world size...  Qdrant's QDRANT_URI is accepted and
+ignored (the vector store is the in-HBM index now).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field
+
+
+def _env(name: str, default: str) -> str:
+    v = os.environ.get(name)
+    return default if v is None or v == "" else v
+
+
+def _int(name: str, default: int) -> int:
+    try:
+        return int(_env(name, str(default)))
+    except ValueError:
+        return default
+
+
+def _float(name: str, default: float) -> float:
+    try:
+        return float(_env(name, str(default)))
+    except ValueError:
+        return default
+
+
+def _bool(name: str, default: bool) -> bool:
+    v = os.environ.get(name)
+    if v is None:
+        return default
+    return v == "1" or v.lower() == "true"
+
+
+@dataclass
+class Config:
+    # --- reference-compatible ---
+    nats_url: str = field(default_factory=lambda: _env("NATS_URL", "nats://localhost:4222"))
+    api_host: str = field(default_factory=lambda: _env("API_SERVER_HOST", "0.0.0.0"))
+    api_port: int = field(default_factory=lambda: _int("API_SERVER_PORT", 8080))  # parse fail -> 8080
+    neo4j_uri: str = field(default_factory=lambda: _env("NEO4J_URI", "bolt://localhost:7687"))
+    neo4j_user: str = field(default_factory=lambda: _env("NEO4J_USER", "neo4j"))
+    neo4j_password: str = field(default_factory=lambda: _env("NEO4J_PASSWORD", ""))
+    neo4j_db: str = "neo4j"
+    force_cpu: bool = field(default_factory=lambda: _bool("FORCE_CPU", False))
+    # --- hard-coded in the reference, configurable here ---
+    model: str = field(default_factory=lambda: _env("SYMB_MODEL", "mpnet-multi"))
+    model_seed: int = field(default_factory=lambda: _int("SYMB_MODEL_SEED", 0))
+    vocab_file: str = field(default_factory=lambda: _env("SYMB_VOCAB", ""))
+    batch_tokens: int = field(default_factory=lambda: _int("SYMB_BATCH_TOKENS", 65536))
+    batch_window_ms: float = field(default_factory=lambda: _float("SYMB_BATCH_WINDOW_MS", 2.0))
+    index_dim: int = field(default_factory=lambda: _int("SYMB_INDEX_DIM", 0))  # 0 -> model hidden
+    index_capacity: int = field(default_factory=lambda: _int("SYMB_INDEX_CAPACITY", 1 << 22))
+    snapshot_dir: str = field(default_factory=lambda: _env("SYMB_SNAPSHOT_DIR", ""))
+    collection: str = "symbiont_document_embeddings"
+    embed_timeout_s: float = field(default_factory=lambda: _float("SYMB_EMBED_TIMEOUT_S", 15.0))
+    search_timeout_s: float = field(default_factory=lambda: _float("SYMB_SEARCH_TIMEOUT_S", 20.0))
+    nats_request_timeout_s: float = field(default_factory=lambda: _float("SYMB_NATS_REQUEST_TIMEOUT_S", 10.0))
+    sse_capacity: int = field(default_factory=lambda: _int("SYMB_SSE_CAPACITY", 32))
+    sse_keepalive_s: float = field(default_factory=lambda: _float("SYMB_SSE_KEEPALIVE_S", 15.0))
+    max_length_limit: int = 1000
+    markov_corpus: str = field(default_factory=lambda: _env(
+        "SYMB_MARKOV_CORPUS",
+        "я пошел гулять в парк и увидел там собаку собака была очень веселая и я решил с ней поиграть"))
+    scrape_timeout_s: float = field(default_factory=lambda: _float("SYMB_SCRAPE_TIMEOUT_S", 15.0))
+    user_agent: str = "CodenameSymbiontBot/0.1 (+https://makkenzo.com)"
+    publish_tokenized: bool = field(default_factory=lambda: _bool("SYMB_PUBLISH_TOKENIZED", True))
+    queue_group: str = field(default_factory=lambda: _env("SYMB_QUEUE_GROUP", ""))
+    fault_spec: str = field(default_factory=lambda: _env("SYMB_FAULT", ""))

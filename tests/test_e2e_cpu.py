@@ -1,0 +1,139 @@
+"""End-to-end flows on CPU (gloo-free, no GPU): broker + services + HTTP/SSE gateway.
+
+* Markov over NATS (BASELINE config #1): POST /api/generate-text -> text_generator -> SSE event
+* ingest: raw text -> preprocessing (fp32 CPU encoder) -> vector_memory -> POST /api/search/semantic
+* gateway error contract: 400s, 503 "no responders", CORS.
+"""
+import asyncio
+import json
+
+import httpx
+import pytest
+
+from codename_symbiont_amd.services.api import ApiService
+from codename_symbiont_amd.services.preprocessing import PreprocessingService
+from codename_symbiont_amd.services.text_generator import TextGeneratorService
+from codename_symbiont_amd.services.vector_memory import VectorMemoryService
+from codename_symbiont_amd.wire import RawTextMessage, subjects
+
+from helpers import broker, cpu_config, start_api, stop_api
+
+
+def run(coro):
+    return asyncio.run(asyncio.wait_for(coro, 120))
+
+
+async def _read_sse_event(client, url, trigger):
+    async with client.stream("GET", url + "/api/events") as r:
+        assert r.headers["content-type"].startswith("text/event-stream")
+        await trigger()
+        async for line in r.aiter_lines():
+            if line.startswith("data: "):
+                return json.loads(line[6:])
+
+
+def test_generate_text_to_sse():
+    async def main():
+        async with broker() as b:
+            cfg = cpu_config(b.url)
+            gen = await TextGeneratorService(cfg, seed=1).start()
+            api = ApiService(cfg)
+            url, t = await start_api(api)
+            async with httpx.AsyncClient(timeout=10) as c:
+                async def trigger():
+                    await asyncio.sleep(0.2)
+                    r = await c.post(url + "/api/generate-text",
+                                     json={"task_id": "t-1", "prompt": "hi", "max_length": 12})
+                    assert r.status_code == 200
+                    assert r.json() == {"message": "Text generation task (id: t-1) submitted successfully.",
+                                        "task_id": "t-1"}
+                ev = await asyncio.wait_for(_read_sse_event(c, url, trigger), 20)
+            assert ev["original_task_id"] == "t-1"
+            words = ev["generated_text"].split()
+            assert 1 <= len(words) <= 12 and words[0] == "я"   # reference starter quirk
+            assert set(ev) == {"original_task_id", "generated_text", "timestamp_ms"}
+            await stop_api(api, t)
+            await gen.stop()
+    run(main())
+
+
+def test_gateway_validation_and_no_responders():
+    async def main():
+        async with broker() as b:
+            cfg = cpu_config(b.url)
+            api = ApiService(cfg)
+            url, t = await start_api(api)
+            async with httpx.AsyncClient(timeout=10) as c:
+                r = await c.post(url + "/api/submit-url", json={"url": "   "})
+                assert r.status_code == 400 and r.json() == {"message": "URL cannot be empty", "task_id": None}
+                r = await c.post(url + "/api/submit-url", json={"url": " http://x.org/a "})
+                assert r.status_code == 200
+                assert r.json()["message"] == "Task to scrape URL 'http://x.org/a' submitted successfully."
+                r = await c.post(url + "/api/generate-text", json={"task_id": " ", "max_length": 5})
+                assert r.status_code == 400 and r.json()["message"] == "task_id cannot be empty"
+                r = await c.post(url + "/api/generate-text", json={"task_id": "a", "max_length": 0})
+                assert r.status_code == 400
+                assert r.json() == {"message": "max_length must be between 1 and 1000", "task_id": "a"}
+                r = await c.post(url + "/api/generate-text", json={"task_id": "a", "max_length": 1001})
+                assert r.status_code == 400
+                r = await c.post(url + "/api/generate-text", content=b"{}",
+                                 headers={"content-type": "application/json"})
+                assert r.status_code == 400 and r.text.startswith("Json deserialize error: missing field")
+                r = await c.post(url + "/api/generate-text", content=b"x", headers={"content-type": "text/plain"})
+                assert r.status_code == 400 and r.text == "Content type error"
+                # nobody serves tasks.embedding.for_query -> fast 503 (no responders)
+                r = await c.post(url + "/api/search/semantic", json={"query_text": "q", "top_k": 3})
+                assert r.status_code == 503
+                body = r.json()
+                assert body["results"] == [] and body["error_message"] == \
+                    "Failed to get embedding from preprocessing service: no responders"
+                assert len(body["search_request_id"]) == 36
+                # CORS
+                r = await c.options(url + "/api/search/semantic", headers={
+                    "origin": "http://localhost:3000", "access-control-request-method": "POST"})
+                assert r.status_code == 200
+                assert r.headers["access-control-allow-origin"] == "http://localhost:3000"
+                assert r.headers["access-control-max-age"] == "3600"
+                r = await c.post(url + "/api/submit-url", json={"url": "u"},
+                                 headers={"origin": "http://evil.example"})
+                assert r.status_code == 400
+            await stop_api(api, t)
+    run(main())
+
+
+def test_ingest_then_semantic_search_cpu():
+    async def main():
+        async with broker() as b:
+            cfg = cpu_config(b.url)
+            pre = await PreprocessingService(cfg).start()
+            vm = await VectorMemoryService(cfg).start()
+            api = ApiService(cfg)
+            url, t = await start_api(api)
+            text = ("The GPU index keeps every vector in HBM.   It answers cosine queries! "
+                    "Markov chains generate text? Neo4j stores the graph")
+            raw = RawTextMessage("doc-1", "http://example.org/p", text, 123)
+            await api.nc.publish(subjects.RAW_TEXT_DISCOVERED, raw.to_json())
+            for _ in range(200):
+                if vm.store.count >= 4:
+                    break
+                await asyncio.sleep(0.05)
+            assert vm.store.count == 4
+            async with httpx.AsyncClient(timeout=30) as c:
+                r = await c.post(url + "/api/search/semantic",
+                                 json={"query_text": "It answers cosine queries!", "top_k": 3})
+            assert r.status_code == 200, r.text
+            body = r.json()
+            assert body["error_message"] is None and len(body["results"]) == 3
+            top = body["results"][0]
+            assert top["payload"]["sentence_text"] == "It answers cosine queries!"
+            assert top["payload"]["sentence_order"] == 1
+            assert top["payload"]["original_document_id"] == "doc-1"
+            assert top["payload"]["source_url"] == "http://example.org/p"
+            assert top["payload"]["model_name"] == "sentence-transformers/all-MiniLM-L6-v2"
+            assert top["score"] > 0.999
+            scores = [x["score"] for x in body["results"]]
+            assert scores == sorted(scores, reverse=True)
+            await stop_api(api, t)
+            await pre.stop()
+            await vm.stop()
+    run(main())
