@@ -137,3 +137,53 @@ def test_ingest_then_semantic_search_cpu():
             await pre.stop()
             await vm.stop()
     run(main())
+
+
+def test_url_to_search_pipeline_with_fixture_site():
+    """POST /api/submit-url -> perception (local fixture site) -> preprocessing -> vector_memory
+    -> POST /api/search/semantic, plus the restored tokenized feed."""
+    from aiohttp import web
+
+    from codename_symbiont_amd.services.perception import PerceptionService
+    from codename_symbiont_amd.wire import TokenizedTextMessage
+
+    page = ("<html><body><nav><p>menu</p></nav><article><h1>Vector search on MI355X</h1>"
+            "<p>The fused kernel scans rows in HBM. It keeps the top scores per query.</p>"
+            "<li>Queries are batched</li></article></body></html>")
+
+    async def main():
+        app = web.Application()
+        app.router.add_get("/doc", lambda r: web.Response(text=page, content_type="text/html"))
+        runner = web.AppRunner(app)
+        await runner.setup()
+        site = web.TCPSite(runner, "127.0.0.1", 0)
+        await site.start()
+        port = site._server.sockets[0].getsockname()[1]
+        async with broker() as b:
+            cfg = cpu_config(b.url)
+            per = await PerceptionService(cfg).start()
+            pre = await PreprocessingService(cfg).start()
+            vm = await VectorMemoryService(cfg).start()
+            api = ApiService(cfg)
+            url, t = await start_api(api)
+            tok_sub = await api.nc.subscribe(subjects.PROCESSED_TEXT_TOKENIZED)
+            async with httpx.AsyncClient(timeout=30) as c:
+                r = await c.post(url + "/api/submit-url", json={"url": f"http://127.0.0.1:{port}/doc"})
+                assert r.status_code == 200
+                for _ in range(300):
+                    if vm.store.count >= 3:
+                        break
+                    await asyncio.sleep(0.05)
+                assert vm.store.count == 3   # "Vector search on MI355X The fused ... HBM." / "It keeps..." / "Queries are batched"
+                tm = TokenizedTextMessage.from_json((await tok_sub.next_msg(5)).data)
+                assert "MI355X" in tm.tokens and len(tm.sentences) == 3
+                r = await c.post(url + "/api/search/semantic",
+                                 json={"query_text": "It keeps the top scores per query.", "top_k": 2})
+            res = r.json()["results"]
+            assert res[0]["payload"]["sentence_text"] == "It keeps the top scores per query."
+            assert res[0]["payload"]["source_url"] == f"http://127.0.0.1:{port}/doc"
+            await stop_api(api, t)
+            for s in (per, pre, vm):
+                await s.stop()
+        await runner.cleanup()
+    run(main())
