@@ -60,6 +60,27 @@ class Wal:
         self._f.close()
 
     @staticmethod
+    def repair(path: str) -> int:
+        """Truncate a torn / corrupt tail so later appends stay reachable; returns valid bytes."""
+        if not os.path.exists(path):
+            return 0
+        with open(path, "rb") as f:
+            data = f.read()
+        off = 0
+        while off + _HDR.size <= len(data):
+            magic, _n, blen, crc = _HDR.unpack_from(data, off)
+            body = data[off + _HDR.size: off + _HDR.size + blen]
+            if magic != MAGIC or len(body) != blen or zlib.crc32(body) != crc:
+                break
+            off += _HDR.size + blen
+        if off != len(data):
+            with open(path, "r+b") as f:
+                f.truncate(off)
+                f.flush()
+                os.fsync(f.fileno())
+        return off
+
+    @staticmethod
     def replay(path: str, dim: int):
         """Yields (point_ids, payloads, vecs) per intact record."""
         if not os.path.exists(path):
@@ -139,7 +160,7 @@ def load_snapshot(shard: HbmIndexShard, directory: str, chunk: int = 1 << 20) ->
     r0 = shard._reserve(n)
     for s in range(0, n, chunk):
         e = min(n, s + chunk)
-        t = torch.from_numpy(np.ascontiguousarray(mm[s:e]).view(np.int16)).view(torch.bfloat16)
+        t = torch.from_numpy(np.array(mm[s:e]).view(np.int16)).view(torch.bfloat16)
         shard.rows[r0 + s:r0 + e].copy_(t.to(shard.device))
     with open(os.path.join(snap, "payloads.jsonl"), encoding="utf-8") as f:
         for r, line in enumerate(f):

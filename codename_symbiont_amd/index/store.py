@@ -41,8 +41,10 @@ class VectorStore:
         self.wal = None
         if snapshot_dir:
             os.makedirs(snapshot_dir, exist_ok=True)
-            n = load_snapshot(self.shard, snapshot_dir)
+            # a group re-distributes the WAL over its ranks; single shards also have snapshots
+            n = load_snapshot(self.shard, snapshot_dir) if group is None else 0
             m = 0
+            Wal.repair(os.path.join(snapshot_dir, "wal.log"))
             for ids, pls, vecs in Wal.replay(os.path.join(snapshot_dir, "wal.log"), dim):
                 self._upsert_nolog(ids, vecs, pls)
                 m += len(ids)
@@ -51,7 +53,7 @@ class VectorStore:
 
     @property
     def count(self) -> int:
-        return self.shard.count
+        return self.group.count if self.group is not None else self.shard.count
 
     def _upsert_nolog(self, point_ids, vecs, payloads):
         t = torch.as_tensor(np.ascontiguousarray(vecs, dtype=np.float32))
@@ -75,7 +77,7 @@ class VectorStore:
                 self.snapshot()
 
     def snapshot(self) -> None:
-        if not self.dir:
+        if not self.dir or self.group is not None:  # group mode: WAL-only durability
             return
         save_snapshot(self.shard, self.dir)
         if self.wal is not None:

@@ -1,0 +1,154 @@
+"""IndexGroup: one logical vector collection sharded over all GPUs of a node.
+
+Process model (one process per GPU): rank 0 hosts vector_memory_service (NATS, payloads, WAL);
+ranks 1..N-1 run ``serve()``, a loop that executes the operations rank 0 broadcasts.  Every op is
+a short, fixed sequence of collectives, so all ranks stay in lockstep:
+
+  SEARCH : header -> broadcast queries [nq, D] -> every rank: fused MFMA scan of ITS shard ->
+           all_gather of the per-rank top-k (f32 scores, i64 global ids) -> rank 0 merges.
+  UPSERT : header -> broadcast vectors [n, D] f32 + (owner rank, target row) -> owners write rows.
+  STOP   : header only.
+Owner assignment is least-loaded-first, so shards stay balanced (the reference's Qdrant has a
+single shard: vector_memory_service/src/main.rs:50).  Global id = rank << 40 | row.
+Payloads (and the point-id -> gid map) live on rank 0 only; other ranks hold vectors only.
+"""
+from __future__ import annotations
+
+import logging
+import threading
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..index.shard import HbmIndexShard, Payload
+from .dist import DistInfo
+from .sharded import RANK_SHIFT, encode_gid, merge_ranked
+
+log = logging.getLogger("symbiont.index_group")
+
+OP_STOP, OP_SEARCH, OP_UPSERT = 0, 1, 2
+
+
+class IndexGroup:
+    def __init__(self, info: DistInfo, dim: int, capacity_per_rank: int, group=None):
+        self.info = info
+        self.dim = dim
+        self.group = group
+        dev = info.device
+        self.shard = HbmIndexShard(dim, capacity_per_rank, dev)
+        self.comm_device = dev if info.backend == "nccl" else torch.device("cpu")
+        # rank-0 bookkeeping; ops may arrive from several executor threads, but the collective
+        # sequence of one op must never interleave with another's
+        self._op_lock = threading.Lock()
+        self.counts = [0] * info.world
+        self.payload_by_gid: dict[int, tuple[str, Payload]] = {}
+        self.gid_by_pid: dict[str, int] = {}
+
+    # ------------------------------------------------------------------ plumbing
+    def _bcast(self, t: torch.Tensor) -> torch.Tensor:
+        if self.info.world > 1:
+            dist.broadcast(t, src=0, group=self.group)
+        return t
+
+    def _header(self, op: int, a: int = 0, b: int = 0) -> torch.Tensor:
+        h = torch.tensor([op, a, b, 0], dtype=torch.int64, device=self.comm_device)
+        return self._bcast(h)
+
+    @property
+    def count(self) -> int:
+        return sum(self.counts) if self.info.is_root else self.shard.count
+
+    # ------------------------------------------------------------------ ops (collective bodies)
+    def _do_search(self, q: torch.Tensor, k: int):
+        info = self.info
+        s, r = self.shard.search(q.to(self.shard.device, torch.bfloat16), k)
+        gid = encode_gid(info.rank, r.to(torch.int64))
+        s = s.to(self.comm_device).contiguous()
+        gid = gid.to(self.comm_device).contiguous()
+        if info.world == 1:
+            return s, gid
+        s_all = [torch.empty_like(s) for _ in range(info.world)]
+        g_all = [torch.empty_like(gid) for _ in range(info.world)]
+        dist.all_gather(s_all, s, group=self.group)
+        dist.all_gather(g_all, gid, group=self.group)
+        return merge_ranked(torch.stack(s_all), torch.stack(g_all), k)
+
+    def _do_upsert(self, vecs: torch.Tensor, owner: torch.Tensor, target: torch.Tensor) -> None:
+        mine = (owner == self.info.rank).nonzero().flatten()
+        if mine.numel() == 0:
+            return
+        v = vecs[mine].to(self.shard.device, torch.float32)
+        tg = target[mine].tolist()
+        new = [i for i, t in enumerate(tg) if t < 0]
+        if new:
+            self.shard.append_f32(v[new])
+        for i, t in enumerate(tg):
+            if t >= 0:
+                self.shard.write_f32(int(t), v[i:i + 1])
+
+    # ------------------------------------------------------------------ rank-0 API
+    def search(self, q_unit: torch.Tensor, k: int):
+        assert self.info.is_root
+        nq = q_unit.shape[0]
+        with self._op_lock:
+            self._header(OP_SEARCH, nq, k)
+            q = self._bcast(q_unit.to(self.comm_device, torch.float32).contiguous())
+            return self._do_search(q, k)
+
+    def upsert(self, point_ids: list[str], vecs: torch.Tensor, payloads: list[Payload]) -> list[int]:
+        assert self.info.is_root
+        with self._op_lock:
+            return self._upsert_locked(point_ids, vecs, payloads)
+
+    def _upsert_locked(self, point_ids, vecs, payloads) -> list[int]:
+        n = len(point_ids)
+        owner = np.empty(n, np.int64)
+        target = np.full(n, -1, np.int64)
+        gids = []
+        counts = list(self.counts)
+        for i, pid in enumerate(point_ids):
+            g = self.gid_by_pid.get(pid)
+            if g is not None:  # overwrite in place
+                owner[i], target[i] = g >> RANK_SHIFT, g & ((1 << RANK_SHIFT) - 1)
+                gids.append(g)
+            else:
+                r = int(np.argmin(counts))
+                owner[i] = r
+                gids.append((r << RANK_SHIFT) | counts[r])
+                counts[r] += 1
+        self._header(OP_UPSERT, n)
+        v = self._bcast(vecs.to(self.comm_device, torch.float32).contiguous())
+        ot = self._bcast(torch.from_numpy(np.stack([owner, target])).to(self.comm_device))
+        self._do_upsert(v, ot[0], ot[1])
+        self.counts = counts
+        for pid, g, p in zip(point_ids, gids, payloads):
+            self.payload_by_gid[g] = (pid, p)
+            self.gid_by_pid[pid] = g
+        return gids
+
+    def payload(self, gid: int) -> tuple[str | None, Payload]:
+        return self.payload_by_gid.get(int(gid), (None, Payload()))
+
+    def stop(self) -> None:
+        if self.info.is_root and self.info.world > 1:
+            with self._op_lock:
+                self._header(OP_STOP)
+
+    # ------------------------------------------------------------------ ranks 1..N-1
+    def serve(self) -> None:
+        assert not self.info.is_root
+        while True:
+            h = self._header(OP_STOP).tolist()
+            op, a, b = h[0], h[1], h[2]
+            if op == OP_STOP:
+                return
+            if op == OP_SEARCH:
+                q = self._bcast(torch.empty(a, self.dim, dtype=torch.float32, device=self.comm_device))
+                self._do_search(q, b)
+            elif op == OP_UPSERT:
+                v = self._bcast(torch.empty(a, self.dim, dtype=torch.float32, device=self.comm_device))
+                ot = self._bcast(torch.empty(2, a, dtype=torch.int64, device=self.comm_device))
+                self._do_upsert(v, ot[0], ot[1])
+            else:
+                raise RuntimeError(f"unknown index op {op}")

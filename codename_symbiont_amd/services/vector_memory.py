@@ -136,8 +136,33 @@ class VectorMemoryService(Service):
 
 
 def main() -> None:
+    """Single GPU: ``python -m ...vector_memory``.  A node: launch one process per GPU
+    (``torch.distributed.run --nproc-per-node N -m codename_symbiont_amd.services.vector_memory``):
+    rank 0 serves NATS over an IndexGroup, the other ranks execute its collective ops."""
+    import os
+
     ulog.setup(VectorMemoryService.name, "info")
-    asyncio.run(VectorMemoryService().run_forever())
+    if int(os.environ.get("WORLD_SIZE", "1")) <= 1:
+        asyncio.run(VectorMemoryService().run_forever())
+        return
+    from ..parallel import dist as D
+    from ..parallel.index_group import IndexGroup
+
+    from ..utils.config import Config
+
+    cfg = Config()
+    info = D.init()
+    dim = cfg.index_dim or get_config(cfg.model).hidden
+    group = IndexGroup(info, dim, cfg.index_capacity // info.world + 1)
+    try:
+        if info.is_root:
+            store = VectorStore(dim, 0, snapshot_dir=cfg.snapshot_dir, group=group)
+            asyncio.run(VectorMemoryService(cfg, store=store).run_forever())
+        else:
+            group.serve()
+    finally:
+        group.stop()
+        D.shutdown(info)
 
 
 if __name__ == "__main__":

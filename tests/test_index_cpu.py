@@ -1,0 +1,65 @@
+"""Index shard semantics + checkpoint/resume (snapshot + WAL) on CPU."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from codename_symbiont_amd.index.persist import Wal
+from codename_symbiont_amd.index.shard import HbmIndexShard, Payload
+from codename_symbiont_amd.index.store import DimensionError, VectorStore
+
+
+def _vecs(n, d, seed=0):
+    return np.random.default_rng(seed).standard_normal((n, d)).astype(np.float32)
+
+
+def test_shard_search_exact_and_small():
+    sh = HbmIndexShard(16, 100, device="cpu")
+    v = _vecs(50, 16)
+    sh.append_f32(torch.from_numpy(v))
+    q = torch.nn.functional.normalize(torch.from_numpy(v[[3, 7]]), dim=-1).bfloat16()
+    s, r = sh.search(q, 3)
+    assert r[:, 0].tolist() == [3, 7] and torch.all(s[:, 0] > 0.99)
+    s, r = sh.search(q, 80)                     # k > rows: trailing slots empty
+    assert (r[:, 50:] == -1).all() and torch.isinf(s[:, 50:]).all()
+    with pytest.raises(MemoryError):
+        sh.append_f32(torch.zeros(51, 16))
+
+
+def test_upsert_overwrites_existing_ids():
+    st = VectorStore(8, 10, device="cpu")
+    v = _vecs(3, 8)
+    st.upsert(["a", "b", "c"], v, [Payload("d", "u", t) for t in "abc"])
+    st.upsert(["b"], -v[1:2], [Payload("d", "u", "B")])
+    assert st.count == 3
+    s, r = st.search(-v[1], 1)
+    pid, p = st.lookup(r[0, 0])
+    assert pid == "b" and p.sentence_text == "B"
+    with pytest.raises(DimensionError, match="expected dim: 8, got 5"):
+        st.upsert(["x"], _vecs(1, 5), [Payload()])
+
+
+def test_snapshot_wal_resume_and_torn_tail(tmp_path):
+    d = str(tmp_path / "idx")
+    st = VectorStore(8, 1000, device="cpu", snapshot_dir=d, snapshot_every=10)
+    v = _vecs(25, 8, 1)
+    for i in range(0, 25, 5):   # 25 points: snapshot at 10 and 20, 5 rows left in the WAL
+        st.upsert([f"p{j}" for j in range(i, i + 5)], v[i:i + 5],
+                  [Payload(f"doc{j}", "u", f"s{j}", j, "m", 100 + j) for j in range(i, i + 5)])
+    assert os.path.exists(os.path.join(d, "snapshot", "vectors.npy"))
+    st.wal.close()  # crash: no close() snapshot
+    with open(os.path.join(d, "wal.log"), "ab") as f:   # torn record at the tail
+        f.write(b"SYMB\x05\x00\x00\x00garbage")
+    st2 = VectorStore(8, 1000, device="cpu", snapshot_dir=d)
+    assert st2.count == 25
+    s, r = st2.search(v[22], 1)
+    pid, p = st2.lookup(r[0, 0])
+    assert pid == "p22" and p.sentence_order == 22 and p.processed_at_ms == 122
+    # the torn tail was dropped, new writes still append and replay
+    st2.upsert(["z"], v[:1] * 3, [Payload("dz")])
+    st2.wal.close()
+    recs = list(Wal.replay(os.path.join(d, "wal.log"), 8))
+    assert sum(len(ids) for ids, _, _ in recs) >= 1
+    st3 = VectorStore(8, 1000, device="cpu", snapshot_dir=d)
+    assert st3.count == 26

@@ -1,0 +1,101 @@
+"""Multi-process (gloo, world_size 2-4) tests of the distributed paths on CPU:
+ShardedSearcher (all_gather queries -> local scan -> all_to_all partial top-k -> merge) and the
+IndexGroup driven by rank 0 (lockstep broadcast ops, least-loaded owners, global ids)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _init(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from codename_symbiont_amd.parallel import dist as D
+    return D.init(backend="gloo", device_type="cpu")
+
+
+def _sharded_worker(rank, world, port, out):
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+    from codename_symbiont_amd.parallel import dist as D
+    from codename_symbiont_amd.parallel.sharded import ShardedSearcher
+    info = _init(rank, world, port)
+    D_, n, nq, k = 64, 500, 7, 5
+    g = torch.Generator().manual_seed(0)
+    all_rows = torch.nn.functional.normalize(torch.randn(world * n, D_, generator=g), dim=-1)
+    all_q = torch.nn.functional.normalize(torch.randn(world * nq, D_, generator=g), dim=-1)
+    shard = HbmIndexShard(D_, n, device="cpu")
+    shard.append_unit(all_rows[rank * n:(rank + 1) * n].bfloat16())
+    s, gid = ShardedSearcher(shard, info).search(all_q[rank * nq:(rank + 1) * nq].bfloat16(), k)
+    out[rank] = (s.numpy(), gid.numpy())
+    D.barrier(info)
+    D.shutdown(info)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_searcher_matches_global_topk(world):
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.start_processes(_sharded_worker, args=(world, _free_port(), out), nprocs=world, join=True,
+                       start_method="spawn")
+    D_, n, nq, k = 64, 500, 7, 5
+    g = torch.Generator().manual_seed(0)
+    all_rows = torch.nn.functional.normalize(torch.randn(world * n, D_, generator=g), dim=-1).bfloat16().float()
+    all_q = torch.nn.functional.normalize(torch.randn(world * nq, D_, generator=g), dim=-1).bfloat16().float()
+    ref_s, ref_i = torch.topk(all_q @ all_rows.t(), k, dim=1)
+    for r in range(world):
+        s, gid = out[r]
+        rows = (gid >> 40) * n + (gid & ((1 << 40) - 1))
+        np.testing.assert_array_equal(rows, ref_i[r * nq:(r + 1) * nq].numpy())
+        np.testing.assert_allclose(s, ref_s[r * nq:(r + 1) * nq].numpy(), atol=1e-5)
+
+
+def _group_worker(rank, world, port, out):
+    from codename_symbiont_amd.index.shard import Payload
+    from codename_symbiont_amd.index.store import VectorStore
+    from codename_symbiont_amd.parallel import dist as D
+    from codename_symbiont_amd.parallel.index_group import IndexGroup
+    info = _init(rank, world, port)
+    grp = IndexGroup(info, dim=32, capacity_per_rank=1000)
+    if rank != 0:
+        grp.serve()
+        out[rank] = grp.shard.count
+    else:
+        store = VectorStore(32, 0, group=grp)
+        rng = np.random.default_rng(1)
+        vecs = rng.standard_normal((300, 32)).astype(np.float32)
+        ids = [f"p{i}" for i in range(300)]
+        for s in range(0, 300, 70):
+            store.upsert(ids[s:s + 70], vecs[s:s + 70], [Payload(f"d{i}", "u", f"t{i}", i) for i in range(s, min(300, s + 70))])
+        vecs[5] = -vecs[5]                                    # overwrite one point in place
+        store.upsert(["p5"], vecs[5:6], [Payload("d5", "u", "t5-new", 5)])
+        q = vecs[[5, 17, 299]]
+        sc, gids = store.search(q, 4)
+        unit = vecs / np.linalg.norm(vecs, axis=1, keepdims=True)
+        ref = np.argsort(-(q / np.linalg.norm(q, axis=1, keepdims=True)) @ unit.T, axis=1)[:, :4]
+        got = [[int(store.lookup(g)[1].sentence_text.split("-")[0][1:]) for g in row] for row in gids]
+        out[0] = (got, ref.tolist(), store.count, store.lookup(gids[0][0])[1].sentence_text)
+        grp.stop()
+    D.shutdown(info)
+
+
+def test_index_group_upsert_search_overwrite():
+    world = 3
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.start_processes(_group_worker, args=(world, _free_port(), out), nprocs=world, join=True,
+                       start_method="spawn")
+    got, ref, count, text = out[0]
+    assert got == ref
+    assert count == 300 and text == "t5-new"
+    assert out[1] == 100 and out[2] == 100          # least-loaded placement balances the shards
