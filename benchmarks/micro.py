@@ -73,6 +73,15 @@ def cmd_scan(a):
                     h.index_scan(shard.rows.data_ptr(), a.rows, D, rpb, n_rblk, q.data_ptr(), a.nq,
                                  kmax, cs.data_ptr(), ci.data_ptr(), st, ns, aux)
                 variants[f"blk{mult}x_ns{ns}_aux{aux}"] = f
+        if mult == 1:
+            def srch(seed):
+                shard.seed_threshold = seed
+                return shard.search(q, 10)
+            ref = srch(False)
+            got = srch(True)
+            out["seeded_matches_unseeded"] = bool(torch.equal(ref[1], got[1]))
+            variants["search_k10_seeded"] = lambda: srch(True)
+            variants["search_k10_unseeded"] = lambda: srch(False)
         r = ab(variants, rounds=a.rounds, iters=a.iters)
         for k, (med, mn) in r.items():
             gbs = a.rows * D * 2 / (med / 1e3) / 1e9
@@ -100,13 +109,62 @@ def cmd_scanabl(a):
     ci = torch.empty(a.nq, n_rblk * 2 * 16, dtype=torch.int32, device="cuda")
     st = stream_handle()
     flat = shard.rows[:a.rows].view(torch.int64)
+    pre_s, _ = shard._scan(a.rows // 64, q, 16, 10, None, None)
+    thr = torch.nextafter(pre_s[:, 9].contiguous(), torch.tensor(-math.inf, device="cuda"))
+    tp = thr.data_ptr() if a.seed else 0
     variants = {f"abl{m}": (lambda m=m: h.index_scan_ablate(shard.rows.data_ptr(), a.rows, rpb, n_rblk,
                                                             q.data_ptr(), a.nq, cs.data_ptr(),
-                                                            ci.data_ptr(), st, m)) for m in (0, 1, 2)}
+                                                            ci.data_ptr(), st, m, tp)) for m in (0, 1, 2, 3, 4, 5)}
     variants["torch_int64_sum"] = lambda: flat.sum()
+    # correctness: the 8-wave (abl0) and the wide 4-wave (abl3) kernels give the same merged top-k
+    merged = {}
+    for m in (0, 3, 4):
+        variants[f"abl{m}"]()
+        os_ = torch.empty(a.nq, 10, device="cuda")
+        oi = torch.empty(a.nq, 10, dtype=torch.int32, device="cuda")
+        h.topk_merge(cs.data_ptr(), ci.data_ptr(), a.nq, cs.shape[1], 16, 10, os_.data_ptr(),
+                     oi.data_ptr(), 0, 0, st)
+        torch.cuda.synchronize()
+        merged[m] = (os_.clone(), oi.clone())
+    same_var = {m: bool(torch.equal(merged[0][1], merged[m][1])) for m in (3, 4)}
     r = ab(variants, rounds=a.rounds, iters=a.iters)
     out = {k: dict(ms=round(m, 3), GBps=round(a.rows * D * 2 / (m / 1e3) / 1e9)) for k, (m, _) in r.items()}
-    print(json.dumps({"bench": "scan_ablation", "rows": a.rows, "nq": a.nq, "results": out}))
+    print(json.dumps({"bench": "scan_ablation", "rows": a.rows, "nq": a.nq, "seeded": bool(a.seed), "variants_match_abl0": same_var,
+                      "results": out}))
+
+
+def cmd_scanstamp(a):
+    """Per-segment s_memtime stamps of the D=384 scan (diagnostic builds: full, L2-source, compute)."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard, _round_up
+    from codename_symbiont_amd.ops._ext import hip, stream_handle
+
+    D = 384
+    shard = HbmIndexShard(D, a.rows, device="cuda")
+    shard.fill_random(a.rows, seed=1)
+    q = torch.nn.functional.normalize(torch.randn(a.nq, D, device="cuda"), dim=-1).bfloat16()
+    h = hip()
+    n_rblk = max(1, round(torch.cuda.get_device_properties(0).multi_processor_count / math.ceil(a.nq / 256)))
+    rpb = _round_up(math.ceil(a.rows / n_rblk), 64)
+    n_rblk = math.ceil(a.rows / rpb)
+    cs = torch.zeros(a.nq, n_rblk * 2 * 16, device="cuda")
+    ci = torch.empty(a.nq, n_rblk * 2 * 16, dtype=torch.int32, device="cuda")
+    st = stream_handle()
+    names = ["vmcnt_wait", "barrier", "chain0+dma", "pro1+topk0", "chain1", "topk1", "cyc_per_tile", "GHz"]
+    out = {}
+    pre_s, _ = shard._scan(a.rows // 64, q, 16, 10, None, None)
+    thr = torch.nextafter(pre_s[:, 9].contiguous(), torch.tensor(-math.inf, device="cuda"))
+    for m, label, tp in ((8, "full", 0), (8, "full_seeded", thr.data_ptr()), (9, "l2_source", 0),
+                         (10, "compute_only", 0)):
+        run = lambda: h.index_scan_ablate(shard.rows.data_ptr(), a.rows, rpb, n_rblk, q.data_ptr(), a.nq,
+                                          cs.data_ptr(), ci.data_ptr(), st, m, tp)
+        ms = timeit(run, 20)  # also warms the clock
+        run()
+        torch.cuda.synchronize()
+        v = cs.view(-1)[: n_rblk * 8 * 8].view(n_rblk, 8, 8)
+        med = v.median(dim=0).values  # [wave, seg]
+        out[label] = dict(ms=round(ms, 3), per_wave={f"w{w}": [round(float(x), 1) for x in med[w]] for w in range(8)},
+                          mean={n: round(float(v[:, :, i].mean()), 1) for i, n in enumerate(names)})
+    print(json.dumps({"bench": "scan_stamps", "rows": a.rows, "segments": names, "results": out}))
 
 
 def cmd_gemm(a):
@@ -166,7 +224,7 @@ def cmd_attn(a):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("cmd", choices=["scan", "scanabl", "gemm", "encoder", "attn"])
+    ap.add_argument("cmd", choices=["scan", "scanabl", "scanstamp", "gemm", "encoder", "attn"])
     ap.add_argument("--rows", type=int, default=100_000_000)
     ap.add_argument("--dim", type=int, default=384)
     ap.add_argument("--nq", type=int, default=256)
@@ -174,10 +232,11 @@ def main():
     ap.add_argument("--seq", type=int, default=128)
     ap.add_argument("--head-dim", type=int, default=32)
     ap.add_argument("--model", default="minilm-l6")
+    ap.add_argument("--seed", type=int, default=1, help="scanabl: seed per-query thresholds")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=5)
     a = ap.parse_args()
-    {"scan": cmd_scan, "scanabl": cmd_scanabl, "gemm": cmd_gemm, "encoder": cmd_encoder, "attn": cmd_attn}[a.cmd](a)
+    {"scan": cmd_scan, "scanabl": cmd_scanabl, "scanstamp": cmd_scanstamp, "gemm": cmd_gemm, "encoder": cmd_encoder, "attn": cmd_attn}[a.cmd](a)
 
 
 if __name__ == "__main__":

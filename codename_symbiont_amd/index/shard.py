@@ -89,6 +89,7 @@ class HbmIndexShard:
         self._ws: dict = {}
         self.scan_ns = 0     # LDS ring depth of the fused scan (0 = kernel default)
         self.scan_aux = -1   # index-stream cache policy (-1 = auto: non-temporal when read once)
+        self.seed_threshold = True  # sample pre-pass seeds per-query top-k thresholds
 
     # ------------------------------------------------------------------ inserts
     def _reserve(self, n: int) -> int:
@@ -170,15 +171,35 @@ class HbmIndexShard:
                     torch.empty(NQ, max(k, 0), dtype=torch.int32, device=self.device))
         if self.device.type != "cuda" or k > 32:
             return self._search_matmul(q_unit, k)
-        from ..ops._ext import hip, stream_handle
-
         q_unit = q_unit.to(torch.bfloat16).contiguous()
         kmax = 16 if k <= 16 else 32
+        n = self.count
+        thr = None
+        m = self._seed_rows(n, k)
+        if m:
+            # threshold seeding: the k-th best score over the first m rows lower-bounds the final
+            # k-th score, so the full scan may drop anything below it (exact; see the kernel note)
+            pre_s, _ = self._scan(m, q_unit, kmax, k, None, n_cus)
+            thr = torch.nextafter(pre_s[:, k - 1].contiguous(),
+                                  torch.tensor(-math.inf, device=self.device))
+        return self._scan(n, q_unit, kmax, k, thr, n_cus)
+
+    SEED_DIV = 64            # sample = first n/64 rows (~1.6% extra scan work)
+    SEED_MIN_ROWS = 1 << 20  # below this the record-breaking inserts are cheap anyway
+
+    def _seed_rows(self, n: int, k: int) -> int:
+        if not self.seed_threshold or n < self.SEED_MIN_ROWS:
+            return 0
+        return max(_round_up(n // self.SEED_DIV, TILE_ROWS), _round_up(k, TILE_ROWS))
+
+    def _scan(self, n: int, q_unit: torch.Tensor, kmax: int, k: int, thr, n_cus):
+        from ..ops._ext import hip, stream_handle
+
+        NQ = q_unit.shape[0]
         lists, qpb = hip().topk_geometry(self.dim, kmax)
         n_qblk = math.ceil(NQ / qpb)
         if n_cus is None:
             n_cus = torch.cuda.get_device_properties(self.device).multi_processor_count
-        n = self.count
         n_rblk = max(1, min(math.ceil(n / (TILE_ROWS * 16)), max(1, round(n_cus / n_qblk))))
         rows_per_blk = _round_up(max(1, math.ceil(n / n_rblk)), TILE_ROWS)
         n_rblk = max(1, math.ceil(n / rows_per_blk))
@@ -188,14 +209,17 @@ class HbmIndexShard:
         if ws is None:
             ws = (torch.empty(NQ, ncand, device=self.device),
                   torch.empty(NQ, ncand, dtype=torch.int32, device=self.device))
-            self._ws = {key: ws}
+            if len(self._ws) >= 4:
+                self._ws.clear()
+            self._ws[key] = ws
         cs, ci = ws
         out_s = torch.empty(NQ, k, device=self.device)
         out_i = torch.empty(NQ, k, dtype=torch.int32, device=self.device)
         st = stream_handle(self.device)
         h = hip()
         h.index_scan(self.rows.data_ptr(), n, self.dim, rows_per_blk, n_rblk, q_unit.data_ptr(),
-                     NQ, kmax, cs.data_ptr(), ci.data_ptr(), st, self.scan_ns, self.scan_aux)
+                     NQ, kmax, cs.data_ptr(), ci.data_ptr(), st, self.scan_ns, self.scan_aux,
+                     0 if thr is None else thr.data_ptr())
         h.topk_merge(cs.data_ptr(), ci.data_ptr(), NQ, ncand, kmax, k, out_s.data_ptr(),
                      out_i.data_ptr(), 0, 0, st)
         return out_s, out_i

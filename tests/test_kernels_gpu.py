@@ -173,3 +173,25 @@ def test_index_scan_small_and_partial():
     s, r = shard.search(q, 5)
     assert (r[:, 3:] == -1).all() and torch.isinf(s[:, 3:]).all()
     assert sorted(r[0, :3].tolist()) == [0, 1, 2]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D", [384, 768])
+def test_index_scan_seeded_threshold_is_exact(D):
+    """The sample pre-pass threshold (k-th best over the first n/64 rows, one ulp down) must not
+    change the answer: same rows as the unseeded scan, and as the fp32 oracle up to near-ties."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+
+    n, nq, k = (1 << 20) + 4096, 300, 10
+    shard = HbmIndexShard(D, n)
+    shard.fill_random(n, seed=9)
+    q = torch.nn.functional.normalize(_f(nq, D, seed=3), dim=-1).bfloat16()
+    assert shard._seed_rows(n, k) > 0
+    shard.seed_threshold = False
+    s0, r0 = shard.search(q, k)
+    shard.seed_threshold = True
+    s1, r1 = shard.search(q, k)
+    torch.cuda.synchronize()
+    assert torch.equal(r0, r1) and torch.equal(s0, s1)
+    ref_s, _ = R.topk_ref(shard.unit_rows(), q, k)
+    _close(s1, ref_s, atol=2e-3, what="seeded topk scores")
