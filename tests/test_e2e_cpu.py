@@ -57,6 +57,23 @@ def test_generate_text_to_sse():
     run(main())
 
 
+def test_gateway_serves_ui_page():
+    """C9: the gateway serves the single-page client with the reference's three features."""
+    async def main():
+        async with broker() as b:
+            api = ApiService(cpu_config(b.url))
+            url, t = await start_api(api)
+            async with httpx.AsyncClient(timeout=10) as c:
+                r = await c.get(url + "/")
+            assert r.status_code == 200 and r.headers["content-type"].startswith("text/html")
+            html = r.text
+            for needle in ('id="url-form"', 'id="gen-form"', 'id="search-form"', "/submit-url",
+                           "/generate-text", "/search/semantic", "EventSource", "Codename: Symbiont UI"):
+                assert needle in html, needle
+            await stop_api(api, t)
+    run(main())
+
+
 def test_gateway_validation_and_no_responders():
     async def main():
         async with broker() as b:
