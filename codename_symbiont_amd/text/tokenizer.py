@@ -1,4 +1,4 @@
-"""WordPiece tokenizer front-end (native core: csrc/native/text.cpp).
+"""Tokenizer front-end: WordPiece and SentencePiece-Unigram (native cores: csrc/native/text.cpp).
 
 The reference downloads ``tokenizer.json`` from the HF Hub (embedding_generator.rs:25-58) and pads
 every input to max_position_embeddings (:75-91).  Offline, this module builds a DETERMINISTIC
@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import functools
 import os
+import unicodedata
 
 import numpy as np
 
@@ -109,33 +110,113 @@ def synthetic_vocab(size: int, family: str = "bert", cased: bool = False) -> tup
     return tuple(vocab[:size])
 
 
+META = "\u2581"
+
+
+def synthetic_unigram(size: int) -> tuple[list[str], list[float]]:
+    """Deterministic SentencePiece-style vocabulary with the XLM-R layout (<s>, <pad>, </s>, <unk>
+    first, <mask> last) and strictly decreasing log-prob scores (no Viterbi ties)."""
+    pieces = ["<s>", "<pad>", "</s>", "<unk>", META]
+    words = _EN_WORDS + _RU_WORDS
+    words = words + [w.capitalize() for w in words]
+    chars = _chars()
+    chars = chars + [c.upper() for c in chars if c.upper() != c and len(c.upper()) == 1]
+    base = [META + w for w in words] + words + _SUBWORDS + [META + c for c in chars] + chars
+    seen = set(pieces)
+    for t in base:
+        if t not in seen:
+            pieces.append(t)
+            seen.add(t)
+    rng = np.random.default_rng(54321)
+    syl = ["ba", "ko", "ri", "ne", "tu", "sa", "mi", "lo", "de", "pa", "ve", "zu", "ch", "st",
+           "ar", "en", "on", "in", "ta", "ro", "ми", "на", "ко", "ст", "ра"]
+    i = 0
+    while len(pieces) < size - 1:
+        if i < 20000:
+            a, b, c = rng.integers(0, len(syl), 3)
+            t = syl[a] + syl[b] + (syl[c] if i % 3 == 0 else "")
+            t = (META + t) if i % 2 else t
+        else:
+            t = f"{META}q{i}" if i % 2 else f"q{i}"
+        i += 1
+        if t not in seen:
+            pieces.append(t)
+            seen.add(t)
+    pieces = pieces[:size - 1] + ["<mask>"]
+    n = len(pieces)
+    scores = [0.0] * 4 + [-1.5 - 14.0 * r / n for r in range(4, n - 1)] + [0.0]
+    return pieces, scores
+
+
+def _load_tokenizer_json(path: str):
+    """HF tokenizer.json (Unigram or WordPiece model) -> ("unigram", pieces, scores, unk_id) or
+    ("wordpiece", vocab list)."""
+    import json
+
+    with open(path, encoding="utf-8") as f:
+        m = json.load(f)["model"]
+    if m["type"] == "Unigram":
+        return "unigram", [p for p, _ in m["vocab"]], [float(s) for _, s in m["vocab"]], m.get("unk_id", 3)
+    if m["type"] == "WordPiece":
+        inv = sorted(m["vocab"].items(), key=lambda kv: kv[1])
+        return "wordpiece", [t for t, _ in inv]
+    raise ValueError(f"unsupported tokenizer model {m['type']!r} in {path}")
+
+
 class Tokenizer:
-    """BERT BasicTokenizer + WordPiece in C++, configured for an encoder family."""
+    """Native tokenizer front-end for an encoder family: BERT BasicTokenizer + WordPiece, or (XLM-R
+    family) NFKC + Metaspace + SentencePiece-Unigram Viterbi.  Sources, in order: ``vocab_file``
+    argument / ``SYMB_TOKENIZER`` (a HF tokenizer.json) / ``SYMB_VOCAB`` (a BERT vocab.txt), else
+    the deterministic synthetic vocabulary of the family (real special-token layout and size)."""
 
     def __init__(self, cfg: EncoderConfig, vocab_file: str | None = None):
         self.cfg = cfg
-        vocab_file = vocab_file if vocab_file is not None else os.environ.get("SYMB_VOCAB", "")
-        if vocab_file:
-            with open(vocab_file, encoding="utf-8") as f:
-                vocab = [line.rstrip("\n") for line in f]
-        else:
-            fam = "xlmr" if cfg.special["cls"] == "<s>" else "bert"
-            vocab = list(synthetic_vocab(cfg.vocab_size, fam, cased=not cfg.lowercase))
-        self.vocab = vocab
         sp = cfg.special
-        self._wp = native().WordPiece(vocab, cfg.lowercase, sp["unk"], sp["cls"], sp["sep"], 100)
-        if self._wp.unk_id < 0 or self._wp.cls_id < 0 or self._wp.sep_id < 0:
-            raise ValueError("vocabulary lacks the special tokens of " + cfg.key)
+        self.kind = "unigram" if sp["cls"] == "<s>" else "wordpiece"
+        path = vocab_file if vocab_file is not None else (os.environ.get("SYMB_TOKENIZER", "")
+                                                          or os.environ.get("SYMB_VOCAB", ""))
+        pieces = scores = None
+        unk_id = 3
+        if path.endswith(".json"):
+            loaded = _load_tokenizer_json(path)
+            self.kind = loaded[0]
+            if self.kind == "unigram":
+                _, pieces, scores, unk_id = loaded
+            else:
+                pieces = loaded[1]
+        elif path:
+            with open(path, encoding="utf-8") as f:
+                pieces = [line.rstrip("\n") for line in f]
+            self.kind = "wordpiece"
+        if self.kind == "unigram":
+            if pieces is None:
+                pieces, scores = synthetic_unigram(cfg.vocab_size)
+            self.vocab = pieces
+            ids = {p: i for i, p in enumerate(pieces)}
+            if sp["cls"] not in ids or sp["sep"] not in ids:
+                raise ValueError("vocabulary lacks the special tokens of " + cfg.key)
+            self._tk = native().Unigram(pieces, scores, unk_id, ids[sp["cls"]], ids[sp["sep"]])
+        else:
+            if pieces is None:
+                pieces = list(synthetic_vocab(cfg.vocab_size, "bert", cased=not cfg.lowercase))
+            self.vocab = pieces
+            self._tk = native().WordPiece(pieces, cfg.lowercase, sp["unk"], sp["cls"], sp["sep"], 100)
+            if self._tk.unk_id < 0 or self._tk.cls_id < 0 or self._tk.sep_id < 0:
+                raise ValueError("vocabulary lacks the special tokens of " + cfg.key)
 
     def __len__(self):
         return len(self.vocab)
 
+    def _norm(self, text: str) -> str:
+        # XLM-R's precompiled SentencePiece charsmap is an NFKC variant; WordPiece normalises in C++
+        return unicodedata.normalize("NFKC", text) if self.kind == "unigram" else text
+
     def tokenize(self, text: str) -> list[str]:
-        return self._wp.tokenize(text)
+        return self._tk.tokenize(self._norm(text))
 
     def encode(self, text: str, max_len: int | None = None) -> list[int]:
-        return self._wp.encode(text, max_len or self.cfg.max_seq_len, True)
+        return self._tk.encode(self._norm(text), max_len or self.cfg.max_seq_len, True)
 
     def encode_packed(self, texts: list[str], max_len: int | None = None):
-        """-> (ids int32 [T], cu_seqlens int32 [B+1]); truncation keeps [CLS] ... [SEP]."""
-        return self._wp.encode_packed(list(texts), max_len or self.cfg.max_seq_len)
+        """-> (ids int32 [T], cu_seqlens int32 [B+1]); truncation keeps <cls> ... <sep>."""
+        return self._tk.encode_packed([self._norm(t) for t in texts], max_len or self.cfg.max_seq_len)

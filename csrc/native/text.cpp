@@ -14,7 +14,9 @@
 #include <pybind11/stl.h>
 
 #include <algorithm>
+#include <limits>
 #include <random>
+#include <stdexcept>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -268,15 +270,16 @@ static bool is_mn(uint32_t c) {
 }
 
 // Base letter of a precomposed char after NFD + Mn removal (Latin-1, Latin Ext-A, Cyrillic й/ё).
+// Tables generated from unicodedata (NFD, drop category Mn); '.' = unchanged.
 static uint32_t strip_accent(uint32_t c) {
   static const char* latin1 =  // U+00C0..U+00FF ('.' = no decomposition)
-      "AAAAAA.CEEEEIIII.NOOOOO.OUUUUY..aaaaaa.ceeeeiiii.nooooo.ouuuuy.y";
+      "AAAAAA.CEEEEIIII.NOOOOO..UUUUY..aaaaaa.ceeeeiiii.nooooo..uuuuy.y";
   if (c >= 0xC0 && c <= 0xFF) {
     const char b = latin1[c - 0xC0];
     return b == '.' ? c : (uint32_t)b;
   }
   static const char* extA =  // U+0100..U+017F
-      "AaAaAaCcCcCcCcDd..EeEeEeEeEeGgGgGgGgHh..IiIiIiIiI..JjKk.LlLlLl..NnNnNn...OoOoOo..RrRrRrSsSsSsSsTtTt..UuUuUuUuUuUuWwYyYZzZzZz.";
+      "AaAaAaCcCcCcCcDd..EeEeEeEeEeGgGgGgGgHh..IiIiIiIiI...JjKk.LlLlLl....NnNnNn...OoOoOo..RrRrRrSsSsSsSsTtTt..UuUuUuUuUuUuWwYyYZzZzZz.";
   if (c >= 0x100 && c <= 0x17F) {
     const char b = extA[c - 0x100];
     return b == '.' ? c : (uint32_t)b;
@@ -307,6 +310,23 @@ static uint32_t to_lower(uint32_t c) {
   if (c >= 0x460 && c <= 0x4FF && !(c & 1) && !(c >= 0x482 && c <= 0x489)) return c + 1;
   if (c >= 0x531 && c <= 0x556) return c + 48;
   return c;
+}
+
+// Pack per-sequence id lists into (ids int32[T], cu_seqlens int32[B+1]) numpy arrays.
+static py::tuple pack_varlen(const std::vector<std::vector<int>>& all) {
+  size_t T = 0;
+  for (auto& v : all) T += v.size();
+  py::array_t<int32_t> ids((py::ssize_t)T), cu((py::ssize_t)all.size() + 1);
+  int32_t* pi = ids.mutable_data();
+  int32_t* pc = cu.mutable_data();
+  pc[0] = 0;
+  size_t o = 0;
+  for (size_t b = 0; b < all.size(); ++b) {
+    std::copy(all[b].begin(), all[b].end(), pi + o);
+    o += all[b].size();
+    pc[b + 1] = (int32_t)o;
+  }
+  return py::make_tuple(ids, cu);
 }
 
 class WordPiece {
@@ -407,19 +427,7 @@ class WordPiece {
       py::gil_scoped_release nogil;
       for (const auto& t : texts) all.push_back(encode(t, max_len, true));
     }
-    size_t T = 0;
-    for (auto& v : all) T += v.size();
-    py::array_t<int32_t> ids((py::ssize_t)T), cu((py::ssize_t)all.size() + 1);
-    int32_t* pi = ids.mutable_data();
-    int32_t* pc = cu.mutable_data();
-    pc[0] = 0;
-    size_t o = 0;
-    for (size_t b = 0; b < all.size(); ++b) {
-      std::copy(all[b].begin(), all[b].end(), pi + o);
-      o += all[b].size();
-      pc[b + 1] = (int32_t)o;
-    }
-    return py::make_tuple(ids, cu);
+    return pack_varlen(all);
   }
 
   std::vector<std::string> tokenize(const std::string& text) const {
@@ -443,6 +451,145 @@ class WordPiece {
   int unk_ = -1, cls_ = -1, sep_ = -1;
 };
 
+// SentencePiece-Unigram segmentation (XLM-R family: paraphrase-multilingual-mpnet-base-v2, the
+// reference's model, preprocessing_service/src/main.rs:305; its tokenizer.json is fetched from
+// the Hub in embedding_generator.rs:25-58).  Input is NFKC-normalised by the caller.  Pipeline, as
+// HF tokenizers runs it: strip trailing whitespace, collapse runs of >= 2 spaces, Metaspace
+// (' ' -> U+2581, prepend one to the
+// text, split before every U+2581), then per piece a Viterbi over the lattice of vocabulary pieces
+// maximising the summed log-probabilities.  A character no single-character piece covers becomes
+// an <unk> node scored min_score - 10; consecutive <unk>s are fused into one.
+class Unigram {
+ public:
+  Unigram(const std::vector<std::string>& pieces, const std::vector<double>& scores, int unk_id,
+          int bos_id, int eos_id)
+      : pieces_(pieces), scores_(scores), unk_(unk_id), bos_(bos_id), eos_(eos_id) {
+    if (pieces.size() != scores.size()) throw std::invalid_argument("pieces/scores length mismatch");
+    double mn = 0.0;
+    for (size_t i = 0; i < pieces.size(); ++i) {
+      ids_.emplace(pieces[i], (int)i);
+      mn = std::min(mn, scores[i]);
+      max_chars_ = std::max(max_chars_, (int)utf8_decode(pieces[i]).size());
+    }
+    unk_score_ = mn - 10.0;
+  }
+
+  // Metaspace pre-tokenisation of already-normalised text.
+  std::vector<std::u32string> pretokenize(const std::string& text) const {
+    std::u32string u = utf8_decode(text), m;
+    while (!u.empty() && is_ws(u.back())) u.pop_back();  // Strip(right)
+    m.reserve(u.size() + 1);
+    for (size_t i = 0; i < u.size(); ++i) {
+      if (u[i] == U' ' && i + 1 < u.size() && u[i + 1] == U' ') continue;  // " {2,}" -> " "
+      m.push_back(u[i] == U' ' ? kMeta : u[i]);
+    }
+    std::vector<std::u32string> words;
+    if (m.empty()) return words;
+    if (m[0] != kMeta) m.insert(m.begin(), kMeta);
+    size_t st = 0;
+    for (size_t i = 1; i <= m.size(); ++i) {
+      if (i == m.size() || m[i] == kMeta) {
+        words.emplace_back(m.substr(st, i - st));
+        st = i;
+      }
+    }
+    return words;
+  }
+
+  void segment(const std::u32string& w, std::vector<int>& out) const {
+    const int n = (int)w.size();
+    std::vector<size_t> boff(n + 1, 0);  // utf-8 byte offset of each char boundary
+    std::string u8;
+    for (int i = 0; i < n; ++i) {
+      boff[i] = u8.size();
+      utf8_put(u8, w[i]);
+    }
+    boff[n] = u8.size();
+    std::vector<double> best(n + 1, -std::numeric_limits<double>::infinity());
+    std::vector<int> prev(n + 1, -1), pid(n + 1, -1);
+    best[0] = 0.0;
+    std::string key;
+    for (int i = 0; i < n; ++i) {
+      if (best[i] == -std::numeric_limits<double>::infinity()) continue;
+      bool single = false;
+      const int lmax = std::min(max_chars_, n - i);
+      for (int l = 1; l <= lmax; ++l) {
+        key.assign(u8, boff[i], boff[i + l] - boff[i]);
+        auto it = ids_.find(key);
+        if (it == ids_.end()) continue;
+        if (l == 1) single = true;
+        const double c = best[i] + scores_[it->second];
+        if (c > best[i + l]) {
+          best[i + l] = c;
+          prev[i + l] = i;
+          pid[i + l] = it->second;
+        }
+      }
+      if (!single) {
+        const double c = best[i] + unk_score_;
+        if (c > best[i + 1]) {
+          best[i + 1] = c;
+          prev[i + 1] = i;
+          pid[i + 1] = unk_;
+        }
+      }
+    }
+    std::vector<int> rev;
+    for (int p = n; p > 0; p = prev[p]) rev.push_back(pid[p]);
+    bool prev_unk = false;  // fuse runs of <unk> within this piece (HF fuse_unk)
+    for (auto it = rev.rbegin(); it != rev.rend(); ++it) {
+      const bool u = *it == unk_;
+      if (!(u && prev_unk)) out.push_back(*it);
+      prev_unk = u;
+    }
+  }
+
+  std::vector<int> encode(const std::string& text, int max_len, bool add_special) const {
+    std::vector<int> ids;
+    if (add_special) ids.push_back(bos_);
+    for (const auto& w : pretokenize(text)) segment(w, ids);
+    if (add_special) {
+      if (max_len > 0 && (int)ids.size() + 1 > max_len) ids.resize(std::max(1, max_len - 1));
+      ids.push_back(eos_);
+    } else if (max_len > 0 && (int)ids.size() > max_len) {
+      ids.resize(max_len);
+    }
+    return ids;
+  }
+
+  py::tuple encode_packed(const std::vector<std::string>& texts, int max_len) const {
+    std::vector<std::vector<int>> all;
+    all.reserve(texts.size());
+    {
+      py::gil_scoped_release nogil;
+      for (const auto& t : texts) all.push_back(encode(t, max_len, true));
+    }
+    return pack_varlen(all);
+  }
+
+  std::vector<std::string> tokenize(const std::string& text) const {
+    std::vector<int> ids = encode(text, 0, false);
+    std::vector<std::string> out;
+    for (int i : ids) out.push_back(pieces_[i]);
+    return out;
+  }
+
+  int id_of(const std::string& t) const {
+    auto it = ids_.find(t);
+    return it == ids_.end() ? -1 : it->second;
+  }
+  size_t size() const { return pieces_.size(); }
+
+ private:
+  static constexpr char32_t kMeta = U'\u2581';
+  std::vector<std::string> pieces_;
+  std::vector<double> scores_;
+  std::unordered_map<std::string, int> ids_;
+  int unk_, bos_, eos_;
+  int max_chars_ = 1;
+  double unk_score_ = -10.0;
+};
+
 void register_text(py::module_& m) {
   m.def("normalize_whitespace", &normalize_whitespace);
   m.def("split_sentences", &split_sentences);
@@ -455,6 +602,16 @@ void register_text(py::module_& m) {
       .def("num_states", &MarkovModel::num_states)
       .def("starters", &MarkovModel::starters)
       .def("successors", &MarkovModel::successors);
+  py::class_<Unigram>(m, "Unigram")
+      .def(py::init<const std::vector<std::string>&, const std::vector<double>&, int, int, int>(),
+           py::arg("pieces"), py::arg("scores"), py::arg("unk_id"), py::arg("bos_id"),
+           py::arg("eos_id"))
+      .def("tokenize", &Unigram::tokenize)
+      .def("encode", &Unigram::encode, py::arg("text"), py::arg("max_len") = 0,
+           py::arg("add_special") = true)
+      .def("encode_packed", &Unigram::encode_packed)
+      .def("id_of", &Unigram::id_of)
+      .def("__len__", &Unigram::size);
   py::class_<WordPiece>(m, "WordPiece")
       .def(py::init<std::vector<std::string>, bool, std::string, std::string, std::string, int>(),
            py::arg("vocab"), py::arg("lowercase") = true, py::arg("unk") = "[UNK]",
