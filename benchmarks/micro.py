@@ -167,6 +167,30 @@ def cmd_scanstamp(a):
     print(json.dumps({"bench": "scan_stamps", "rows": a.rows, "segments": names, "results": out}))
 
 
+def cmd_scanfp8(a):
+    """fp8 (e4m3) index scan, D=1024 by default (BASELINE config #5 geometry), seeded top-10."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+
+    D = a.dim if a.dim != 384 else 1024
+    shard = HbmIndexShard(D, a.rows, device="cuda", dtype="fp8")
+    shard.fill_random(a.rows, seed=1)
+    q = torch.nn.functional.normalize(torch.randn(a.nq, D, device="cuda"), dim=-1).bfloat16()
+    out = {}
+
+    def run(variant, seed):
+        shard.scan_variant, shard.seed_threshold = variant, seed
+        return shard.search(q, 10)
+
+    ref = run(0, False)
+    out["variants_match"] = all(torch.equal(ref[1], run(v, sd)[1]) for v in (0, 1) for sd in (0, 1))
+    variants = {f"v{v}_seed{sd}": (lambda v=v, sd=sd: run(v, sd)) for v in (0, 1) for sd in (False, True)}
+    r = ab(variants, rounds=a.rounds, iters=a.iters)
+    for k, (med, mn) in r.items():
+        out[k] = dict(ms=round(med, 3), GBps=round(a.rows * D / (med / 1e3) / 1e9),
+                      TFLOPs=round(2 * a.rows * D * a.nq / (med / 1e3) / 1e12))
+    print(json.dumps({"bench": "scan_fp8", "rows": a.rows, "dim": D, "nq": a.nq, "results": out}))
+
+
 def cmd_gemm(a):
     from codename_symbiont_amd.ops import kernels as K
 
@@ -224,7 +248,7 @@ def cmd_attn(a):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("cmd", choices=["scan", "scanabl", "scanstamp", "gemm", "encoder", "attn"])
+    ap.add_argument("cmd", choices=["scan", "scanabl", "scanstamp", "scanfp8", "gemm", "encoder", "attn"])
     ap.add_argument("--rows", type=int, default=100_000_000)
     ap.add_argument("--dim", type=int, default=384)
     ap.add_argument("--nq", type=int, default=256)
@@ -236,7 +260,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=5)
     a = ap.parse_args()
-    {"scan": cmd_scan, "scanabl": cmd_scanabl, "scanstamp": cmd_scanstamp, "gemm": cmd_gemm, "encoder": cmd_encoder, "attn": cmd_attn}[a.cmd](a)
+    {"scan": cmd_scan, "scanabl": cmd_scanabl, "scanstamp": cmd_scanstamp, "scanfp8": cmd_scanfp8, "gemm": cmd_gemm, "encoder": cmd_encoder, "attn": cmd_attn}[a.cmd](a)
 
 
 if __name__ == "__main__":

@@ -4,7 +4,8 @@ The reference persists through Qdrant (on-disk vectors + payload, vector_memory_
 :39,52; docker volume ./data/qdrant_storage).  The HBM index is volatile, so each shard keeps:
 
   <dir>/snapshot/meta.json        {"dim", "count", "format": 1}
-  <dir>/snapshot/vectors.npy      count x dim bf16 bit patterns (uint16 .npy, memory-mappable)
+  <dir>/snapshot/vectors.npy      count x dim bf16 bit patterns (uint16 .npy, memory-mappable),
+                                  or e4m3 bytes (uint8) for an fp8 shard (meta "dtype")
   <dir>/snapshot/payloads.jsonl   one [point_id, doc_id, url, text, order, model, ts] per row
   <dir>/wal.log                   records appended (and fsync'd) per upsert batch
 
@@ -116,11 +117,15 @@ def save_snapshot(shard: HbmIndexShard, directory: str, chunk: int = 1 << 20) ->
     tmp = snap + ".tmp"
     os.makedirs(tmp, exist_ok=True)
     n, D = shard.count, shard.dim
+    fp8 = getattr(shard, "dtype", "bf16") == "fp8"
     mm = np.lib.format.open_memmap(os.path.join(tmp, "vectors.npy"), mode="w+",
-                                   dtype=np.uint16, shape=(n, D)) if n else None
+                                   dtype=np.uint8 if fp8 else np.uint16, shape=(n, D)) if n else None
     for s in range(0, n, chunk):
         e = min(n, s + chunk)
-        mm[s:e] = shard.rows[s:e].view(torch.int16).cpu().numpy().view(np.uint16)
+        if fp8:
+            mm[s:e] = shard.rows[s:e].cpu().numpy()
+        else:
+            mm[s:e] = shard.rows[s:e].view(torch.int16).cpu().numpy().view(np.uint16)
     if mm is not None:
         mm.flush()
         del mm
@@ -132,7 +137,7 @@ def save_snapshot(shard: HbmIndexShard, directory: str, chunk: int = 1 << 20) ->
                                 p.sentence_order, p.model_name, p.processed_at_ms],
                                ensure_ascii=False) + "\n")
     with open(os.path.join(tmp, "meta.json"), "w") as f:
-        json.dump({"dim": D, "count": n, "format": 1}, f)
+        json.dump({"dim": D, "count": n, "format": 1, "dtype": "fp8" if fp8 else "bf16"}, f)
     if os.path.exists(snap):
         old = snap + ".old"
         os.replace(snap, old)
@@ -153,6 +158,9 @@ def load_snapshot(shard: HbmIndexShard, directory: str, chunk: int = 1 << 20) ->
         meta = json.load(f)
     if meta["dim"] != shard.dim:
         raise ValueError(f"snapshot dim {meta['dim']} != index dim {shard.dim}")
+    fp8 = meta.get("dtype", "bf16") == "fp8"
+    if fp8 != (getattr(shard, "dtype", "bf16") == "fp8"):
+        raise ValueError(f"snapshot dtype {meta.get('dtype', 'bf16')} != index dtype {shard.dtype}")
     n = meta["count"]
     if n == 0:
         return 0
@@ -160,7 +168,10 @@ def load_snapshot(shard: HbmIndexShard, directory: str, chunk: int = 1 << 20) ->
     r0 = shard._reserve(n)
     for s in range(0, n, chunk):
         e = min(n, s + chunk)
-        t = torch.from_numpy(np.array(mm[s:e]).view(np.int16)).view(torch.bfloat16)
+        if fp8:
+            t = torch.from_numpy(np.array(mm[s:e]))
+        else:
+            t = torch.from_numpy(np.array(mm[s:e]).view(np.int16)).view(torch.bfloat16)
         shard.rows[r0 + s:r0 + e].copy_(t.to(shard.device))
     with open(os.path.join(snap, "payloads.jsonl"), encoding="utf-8") as f:
         for r, line in enumerate(f):

@@ -75,21 +75,34 @@ class PayloadStore:
         return self.point_ids[row], Payload(**vals)
 
 
+FP8_SCALE = 256.0  # == ops.kernels.FP8_SCALE (kept import-free for CPU-only users)
+
+
 class HbmIndexShard:
-    def __init__(self, dim: int, capacity: int, device="cuda", kmax: int = 16):
+    """``dtype="bf16"`` (default) or ``"fp8"``: OCP e4m3 rows of FP8_SCALE * x (half the HBM bytes
+    and twice the MFMA rate; BASELINE config #5).  Scores returned are cosines either way."""
+
+    def __init__(self, dim: int, capacity: int, device="cuda", kmax: int = 16, dtype: str = "bf16"):
+        if dtype not in ("bf16", "fp8"):
+            raise ValueError(f"index dtype must be bf16 or fp8, got {dtype!r}")
+        if dtype == "fp8" and dim % 256:
+            raise ValueError("fp8 index rows must be a multiple of 256 wide (512/768/1024)")
         self.dim = dim
+        self.dtype = dtype
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
         self.capacity = int(capacity)
         self.rows = torch.empty(_round_up(max(self.capacity, 1), TILE_ROWS), dim,
-                                dtype=torch.bfloat16, device=self.device)
+                                dtype=torch.uint8 if dtype == "fp8" else torch.bfloat16,
+                                device=self.device)
         self.count = 0
         self.payloads = PayloadStore()
         self._ws: dict = {}
         self.scan_ns = 0     # LDS ring depth of the fused scan (0 = kernel default)
         self.scan_aux = -1   # index-stream cache policy (-1 = auto: non-temporal when read once)
         self.seed_threshold = True  # sample pre-pass seeds per-query top-k thresholds
+        self.scan_variant = 0        # fp8 scan ring geometry (0 = default)
 
     # ------------------------------------------------------------------ inserts
     def _reserve(self, n: int) -> int:
@@ -104,8 +117,31 @@ class HbmIndexShard:
         """Append already unit-norm bf16 rows (e.g. the encoder's pooled+normalised output)."""
         n = unit_bf16.shape[0]
         r0 = self._reserve(n)
-        self.rows[r0:r0 + n].copy_(unit_bf16, non_blocking=True)
+        if self.dtype == "fp8":
+            self._store(r0, unit_bf16.to(self.device), normalize=False)
+        else:
+            self.rows[r0:r0 + n].copy_(unit_bf16, non_blocking=True)
         return r0
+
+    def _store(self, r0: int, x: torch.Tensor, normalize: bool) -> None:
+        """Write rows (f32 or bf16 on self.device) at r0, unit-normalising them if asked."""
+        n = x.shape[0]
+        dst = self.rows[r0:r0 + n]
+        if self.device.type == "cuda":
+            from ..ops import kernels as K
+
+            if self.dtype == "fp8":
+                K.quant_fp8(x.contiguous(), dst, FP8_SCALE, normalize)
+            elif normalize:
+                K.l2norm_cast(x.float().contiguous(), dst)
+            else:
+                dst.copy_(x)
+            return
+        y = torch.nn.functional.normalize(x.float(), dim=-1) if normalize else x.float()
+        if self.dtype == "fp8":
+            dst.copy_((y * FP8_SCALE).to(torch.float8_e4m3fn).view(torch.uint8))
+        else:
+            dst.copy_(y.bfloat16())
 
     def append_f32(self, vecs: torch.Tensor) -> int:
         """Append raw float vectors (wire embeddings); normalised + cast by the l2norm_cast kernel."""
@@ -117,13 +153,7 @@ class HbmIndexShard:
         return r0
 
     def write_f32(self, r0: int, vecs: torch.Tensor) -> None:
-        vecs = vecs.to(self.device, torch.float32).contiguous()
-        if self.device.type == "cuda":
-            from ..ops.kernels import l2norm_cast
-
-            l2norm_cast(vecs, self.rows[r0:r0 + vecs.shape[0]])
-        else:
-            self.rows[r0:r0 + vecs.shape[0]] = torch.nn.functional.normalize(vecs, dim=-1).bfloat16()
+        self._store(r0, vecs.to(self.device, torch.float32).contiguous(), normalize=True)
 
     def upsert(self, point_ids: list[str], vecs: torch.Tensor, payloads: list[Payload]) -> list[int]:
         """Qdrant-style upsert: existing ids are overwritten in place, new ids appended."""
@@ -152,12 +182,7 @@ class HbmIndexShard:
         for s in range(0, n, chunk):
             e = min(n, s + chunk)
             x = torch.randn(e - s, self.dim, generator=g, device=self.device, dtype=torch.float32)
-            if self.device.type == "cuda":
-                from ..ops.kernels import l2norm_cast
-
-                l2norm_cast(x, self.rows[r0 + s:r0 + e])
-            else:
-                self.rows[r0 + s:r0 + e] = torch.nn.functional.normalize(x, dim=-1).bfloat16()
+            self._store(r0 + s, x, normalize=True)
 
     # ------------------------------------------------------------------ search
     def search(self, q_unit: torch.Tensor, k: int, n_cus: int | None = None):
@@ -173,6 +198,10 @@ class HbmIndexShard:
             return self._search_matmul(q_unit, k)
         q_unit = q_unit.to(torch.bfloat16).contiguous()
         kmax = 16 if k <= 16 else 32
+        if self.dtype == "fp8":
+            from ..ops.kernels import quant_fp8
+
+            q_unit = quant_fp8(q_unit, scale=FP8_SCALE)  # scores come back as S^2 * cosine
         n = self.count
         thr = None
         m = self._seed_rows(n, k)
@@ -182,7 +211,10 @@ class HbmIndexShard:
             pre_s, _ = self._scan(m, q_unit, kmax, k, None, n_cus)
             thr = torch.nextafter(pre_s[:, k - 1].contiguous(),
                                   torch.tensor(-math.inf, device=self.device))
-        return self._scan(n, q_unit, kmax, k, thr, n_cus)
+        out_s, out_i = self._scan(n, q_unit, kmax, k, thr, n_cus)
+        if self.dtype == "fp8":
+            out_s.mul_(1.0 / (FP8_SCALE * FP8_SCALE))
+        return out_s, out_i
 
     SEED_DIV = 64            # sample = first n/64 rows (~1.6% extra scan work)
     SEED_MIN_ROWS = 1 << 20  # below this the record-breaking inserts are cheap anyway
@@ -196,7 +228,10 @@ class HbmIndexShard:
         from ..ops._ext import hip, stream_handle
 
         NQ = q_unit.shape[0]
-        lists, qpb = hip().topk_geometry(self.dim, kmax)
+        if self.dtype == "fp8":
+            lists, qpb = 2, 256
+        else:
+            lists, qpb = hip().topk_geometry(self.dim, kmax)
         n_qblk = math.ceil(NQ / qpb)
         if n_cus is None:
             n_cus = torch.cuda.get_device_properties(self.device).multi_processor_count
@@ -217,9 +252,15 @@ class HbmIndexShard:
         out_i = torch.empty(NQ, k, dtype=torch.int32, device=self.device)
         st = stream_handle(self.device)
         h = hip()
-        h.index_scan(self.rows.data_ptr(), n, self.dim, rows_per_blk, n_rblk, q_unit.data_ptr(),
-                     NQ, kmax, cs.data_ptr(), ci.data_ptr(), st, self.scan_ns, self.scan_aux,
-                     0 if thr is None else thr.data_ptr())
+        thr_p = 0 if thr is None else thr.data_ptr()
+        if self.dtype == "fp8":
+            h.index_scan_fp8(self.rows.data_ptr(), n, self.dim, rows_per_blk, n_rblk,
+                             q_unit.data_ptr(), NQ, kmax, cs.data_ptr(), ci.data_ptr(), st,
+                             self.scan_aux, thr_p, self.scan_variant)
+        else:
+            h.index_scan(self.rows.data_ptr(), n, self.dim, rows_per_blk, n_rblk, q_unit.data_ptr(),
+                         NQ, kmax, cs.data_ptr(), ci.data_ptr(), st, self.scan_ns, self.scan_aux,
+                         thr_p)
         h.topk_merge(cs.data_ptr(), ci.data_ptr(), NQ, ncand, kmax, k, out_s.data_ptr(),
                      out_i.data_ptr(), 0, 0, st)
         return out_s, out_i
@@ -232,7 +273,7 @@ class HbmIndexShard:
         q = q_unit.to(self.device).float()
         for s in range(0, self.count, chunk):
             e = min(self.count, s + chunk)
-            sc = q @ self.rows[s:e].float().t()
+            sc = q @ self._rows_f32(s, e).t()
             kk = min(k, e - s)
             ts, ti = torch.topk(sc, kk, dim=1)
             cat_s = torch.cat([best_s, ts], 1)
@@ -242,5 +283,14 @@ class HbmIndexShard:
         best_i = torch.where(torch.isfinite(best_s), best_i, torch.full_like(best_i, -1))
         return best_s, best_i.to(torch.int32)
 
+    def _rows_f32(self, s: int, e: int) -> torch.Tensor:
+        r = self.rows[s:e]
+        if self.dtype == "fp8":
+            return r.view(torch.float8_e4m3fn).float() / FP8_SCALE
+        return r.float()
+
     def unit_rows(self) -> torch.Tensor:
+        """The stored rows as bf16 (fp8 shards: decoded, a copy)."""
+        if self.dtype == "fp8":
+            return self._rows_f32(0, self.count).bfloat16()
         return self.rows[:self.count]

@@ -132,3 +132,31 @@ def l2norm_cast(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tenso
         raise ValueError("bad l2norm_cast output")
     hip().l2norm_cast(_ptr(x), _ptr(out), n, D, out.stride(0), stream_handle())
     return out
+
+
+FP8_SCALE = 256.0  # global index/query scale: unit vectors -> |S x_i| <= 256 < 448 (e4m3 max)
+
+
+def quant_fp8(x: torch.Tensor, out: torch.Tensor | None = None, scale: float = FP8_SCALE,
+              normalize: bool = False) -> torch.Tensor:
+    """Rows (f32 or bf16) -> OCP e4m3 bytes of scale * x (optionally unit-normalised first).
+    ``out`` is a uint8 [n, D] tensor (may be a row-slice of an fp8 index slab)."""
+    if x.dtype not in (torch.float32, torch.bfloat16) or x.dim() != 2 or x.stride(1) != 1:
+        raise ValueError("quant_fp8 expects a row-major f32/bf16 matrix")
+    if not x.is_cuda:
+        raise ValueError("quant_fp8 runs on the GPU")
+    n, D = x.shape
+    if D % 8 or D > 1024:
+        raise ValueError("D must be a multiple of 8 and <= 1024")
+    if out is None:
+        out = torch.empty(n, D, dtype=torch.uint8, device=x.device)
+    if out.dtype != torch.uint8 or out.shape[0] < n or out.shape[1] != D or out.stride(1) != 1:
+        raise ValueError("bad quant_fp8 output")
+    hip().quant_fp8(_ptr(x), x.dtype == torch.float32, x.stride(0), _ptr(out), out.stride(0), n, D,
+                    float(scale), bool(normalize), stream_handle())
+    return out
+
+
+def fp8_to_float(b: torch.Tensor, scale: float = FP8_SCALE) -> torch.Tensor:
+    """Reference decode of e4m3 bytes (torch float8_e4m3fn == gfx950's OCP format)."""
+    return b.view(torch.float8_e4m3fn).float() / scale

@@ -31,12 +31,13 @@ OP_STOP, OP_SEARCH, OP_UPSERT = 0, 1, 2
 
 
 class IndexGroup:
-    def __init__(self, info: DistInfo, dim: int, capacity_per_rank: int, group=None):
+    def __init__(self, info: DistInfo, dim: int, capacity_per_rank: int, group=None,
+                 dtype: str = "bf16"):
         self.info = info
         self.dim = dim
         self.group = group
         dev = info.device
-        self.shard = HbmIndexShard(dim, capacity_per_rank, dev)
+        self.shard = HbmIndexShard(dim, capacity_per_rank, dev, dtype=dtype)
         self.comm_device = dev if info.backend == "nccl" else torch.device("cpu")
         # rank-0 bookkeeping; ops may arrive from several executor threads, but the collective
         # sequence of one op must never interleave with another's

@@ -36,7 +36,8 @@ class VectorMemoryService(Service):
         dim = self.cfg.index_dim or get_config(self.cfg.model).hidden
         self.store = store or VectorStore(dim, self.cfg.index_capacity,
                                           device="cpu" if self.cfg.force_cpu else None,
-                                          snapshot_dir=self.cfg.snapshot_dir)
+                                          snapshot_dir=self.cfg.snapshot_dir,
+                                          dtype=self.cfg.index_dtype)
         self.log.info("[INDEX_SETUP] collection '%s': dim %d, capacity %d, device %s, %d points",
                       self.cfg.collection, dim, self.store.shard.capacity, self.store.shard.device,
                       self.store.count)
@@ -153,7 +154,7 @@ def main() -> None:
     cfg = Config()
     info = D.init()
     dim = cfg.index_dim or get_config(cfg.model).hidden
-    group = IndexGroup(info, dim, cfg.index_capacity // info.world + 1)
+    group = IndexGroup(info, dim, cfg.index_capacity // info.world + 1, dtype=cfg.index_dtype)
     try:
         if info.is_root:
             store = VectorStore(dim, 0, snapshot_dir=cfg.snapshot_dir, group=group)

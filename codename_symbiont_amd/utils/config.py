@@ -56,6 +56,8 @@ class Config:
     batch_window_ms: float = field(default_factory=lambda: _float("SYMB_BATCH_WINDOW_MS", 2.0))
     index_dim: int = field(default_factory=lambda: _int("SYMB_INDEX_DIM", 0))  # 0 -> model hidden
     index_capacity: int = field(default_factory=lambda: _int("SYMB_INDEX_CAPACITY", 1 << 22))
+    # "bf16" (default) or "fp8" (OCP e4m3 rows; needs a dim that is a multiple of 256)
+    index_dtype: str = field(default_factory=lambda: os.environ.get("SYMB_INDEX_DTYPE", "bf16"))
     snapshot_dir: str = field(default_factory=lambda: _env("SYMB_SNAPSHOT_DIR", ""))
     collection: str = "symbiont_document_embeddings"
     embed_timeout_s: float = field(default_factory=lambda: _float("SYMB_EMBED_TIMEOUT_S", 15.0))

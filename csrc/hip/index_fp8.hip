@@ -1,0 +1,333 @@
+// fp8 (OCP e4m3) index: quantiser + fused scan/top-k (BASELINE config #5:
+// e5-large-v2 fp8 + 1B-vector index; a 1B x 1024 index is 1.02 TB, i.e. 128-256 GB per MI355X).
+//
+// Storage: row r holds e4m3(S * x_r) for the unit vector x_r with ONE global scale S = 256.
+// |x_i| <= 1 so S*|x_i| <= 256 < 448 (never saturates) and a typical component (1/sqrt(D) ~ 0.03)
+// lands at ~8, well inside e4m3's normal range: per-component relative error = the 3-bit mantissa,
+// with no per-row scale to fetch in the scan.  Queries are quantised the same way, so
+// acc = S^2 * <x, q> and the host divides the final scores by S^2 (top-k order is unchanged).
+//
+// Scan design (gfx950): 4 waves / CU, one per SIMD (up to 512 VGPR+AGPR per lane).  Each wave
+// owns 64 queries as two 32-query B-fragment sets RESIDENT IN AGPRs (D=1024: 2 x 16 fragments x
+// 8 regs = 256 AGPRs), so one A fragment read from LDS (32 B per lane) feeds TWO
+// v_mfma_f32_32x32x64_f8f6f4 (hand-issued: the builtin form makes the compiler copy AGPR
+// operands to VGPRs around every MFMA).  A 256-thread workgroup scores 256 queries per pass over
+// the index; rows stream HBM -> LDS by global_load_lds_dwordx4 (16 pieces/wave/tile at D=1024)
+// issued one per k-step inside the first sub-tile's MFMA chain, with an XOR-swizzled image
+// (16-byte chunk ^ (row & 15)) that keeps the ds_read_b128 fragment reads conflict-free.
+// Top-k, candidate layout and per-query threshold seeding are those of the bf16 scan
+// (index_topk.hip); the candidates merge with symb_topk_merge.
+#include "scan_common.h"
+
+namespace symb {
+
+typedef __attribute__((ext_vector_type(8))) int i32x8;  // fp8 MFMA operand: 32 bytes per lane
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+
+// ---- quantiser: one wave per row, D <= 1024, D % 8 == 0 -----------------------------------------
+template <bool IN_F32>
+__global__ __launch_bounds__(256) void quant_fp8_kernel(const void* __restrict__ in, int ld_in,
+                                                        uint8_t* __restrict__ out, int ld_out,
+                                                        int n, int D, float scale, int normalize) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n) return;
+  float v[2][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int col = (c * 64 + lane) * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
+    if (col < D) {
+      if constexpr (IN_F32) {
+        const float* p = (const float*)in + (size_t)row * ld_in + col;
+        const float4 a = *reinterpret_cast<const float4*>(p);
+        const float4 b = *reinterpret_cast<const float4*>(p + 4);
+        v[c][0] = a.x; v[c][1] = a.y; v[c][2] = a.z; v[c][3] = a.w;
+        v[c][4] = b.x; v[c][5] = b.y; v[c][6] = b.z; v[c][7] = b.w;
+      } else {
+        load8((const __bf16*)in + (size_t)row * ld_in + col, v[c]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[c][j] * v[c][j];
+    }
+  }
+  float mul = scale;
+  if (normalize) mul = scale / fmaxf(sqrtf(wave_sum(ss)), 1e-12f);
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (col >= D) continue;
+    int lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[c][0] * mul, v[c][1] * mul, 0, false);
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[c][2] * mul, v[c][3] * mul, lo, true);
+    int hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[c][4] * mul, v[c][5] * mul, 0, false);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[c][6] * mul, v[c][7] * mul, hi, true);
+    *reinterpret_cast<int2*>(out + (size_t)row * ld_out + col) = make_int2(lo, hi);
+  }
+}
+
+// ---- scan -------------------------------------------------------------------------------------
+template <int OFF>
+__device__ __forceinline__ void ds_read16_i(i32x4& dst, uint32_t addr) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(addr), "i"(OFF));
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait2(i32x4& a, i32x4& b) {
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "i"(N));
+}
+
+// fragment ks of a sub-tile: row r = lane & 31 holds bytes [64 ks + 32 h, +32), h = lane >> 5,
+// i.e. 16-byte chunks c = 4 ks + 2 h + j (j = 0, 1), stored at chunk c ^ (r & 15): the per-lane
+// part repeats every 4 k-steps (voff[ks & 3][j]) and the rest is the immediate (ks >> 2) * 256.
+template <int J, int PF, int R>
+__device__ __forceinline__ void fp8_prologue(i32x4 (&lo)[R], i32x4 (&hi)[R],
+                                             const uint32_t (&voff)[8], uint32_t base) {
+  ds_read16_i<(J >> 2) * 256>(lo[J % R], base + voff[(J & 3) * 2]);
+  ds_read16_i<(J >> 2) * 256>(hi[J % R], base + voff[(J & 3) * 2 + 1]);
+  if constexpr (J + 1 < PF) fp8_prologue<J + 1, PF, R>(lo, hi, voff, base);
+}
+
+template <int KS, int NKS, int PF, int DMA_PIECES>
+struct Fp8Chain {
+  static constexpr int R = PF + 1;
+  template <class Dma>
+  __device__ __forceinline__ static void run(f32x16& acc0, f32x16& acc1, i32x4 (&lo)[R],
+                                             i32x4 (&hi)[R], const i32x8 (&q0)[NKS],
+                                             const i32x8 (&q1)[NKS], const uint32_t (&voff)[8],
+                                             uint32_t base, const Dma& dma) {
+    if constexpr (KS < DMA_PIECES) dma(KS);
+    constexpr int in_flight = (NKS - KS < PF) ? (NKS - KS) : PF;  // fragments incl. this one
+    lgkm_wait2<2 * (in_flight - 1)>(lo[KS % R], hi[KS % R]);
+    const i32x8 a = __builtin_shufflevector(lo[KS % R], hi[KS % R], 0, 1, 2, 3, 4, 5, 6, 7);
+    if constexpr (KS == 0) {
+      asm volatile("v_mfma_f32_32x32x64_f8f6f4 %0, %1, %2, 0" : "=&v"(acc0) : "v"(a), "a"(q0[0]));
+      asm volatile("v_mfma_f32_32x32x64_f8f6f4 %0, %1, %2, 0" : "=&v"(acc1) : "v"(a), "a"(q1[0]));
+    } else {
+      asm volatile("v_mfma_f32_32x32x64_f8f6f4 %0, %1, %2, %0" : "+v"(acc0) : "v"(a), "a"(q0[KS]));
+      asm volatile("v_mfma_f32_32x32x64_f8f6f4 %0, %1, %2, %0" : "+v"(acc1) : "v"(a), "a"(q1[KS]));
+    }
+    if constexpr (KS + 1 == NKS)  // XDL write -> VALU read of the accumulators (16-pass: 19 states)
+      asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+    if constexpr (KS + PF < NKS) {
+      constexpr int J = KS + PF;
+      ds_read16_i<(J >> 2) * 256>(lo[J % R], base + voff[(J & 3) * 2]);
+      ds_read16_i<(J >> 2) * 256>(hi[J % R], base + voff[(J & 3) * 2 + 1]);
+    }
+    if constexpr (KS + 1 < NKS)
+      Fp8Chain<KS + 1, NKS, PF, DMA_PIECES>::run(acc0, acc1, lo, hi, q0, q1, voff, base, dma);
+  }
+};
+
+template <int D, int KMAX, int NS, int SUBS, int AUX>
+__global__ __launch_bounds__(256, 1) void index_scan_fp8_kernel(
+    const uint8_t* __restrict__ X, int n_valid, int rows_per_blk, const uint8_t* __restrict__ Q,
+    int NQ, int n_qblk, const float* __restrict__ thr_init, float* __restrict__ cand_s,
+    int* __restrict__ cand_i) {
+  constexpr int CPR = D / 16, SUB = 32, TR = 32 * SUBS, NW = 4;
+  constexpr int TILE_BYTES = TR * D, SUB_BYTES = SUB * D;
+  constexpr int LOADS = TILE_BYTES / (1024 * NW);  // DMA pieces per wave per tile
+  constexpr int NKS = D / 64, PF = 4, R = PF + 1;
+  static_assert(D % 256 == 0 && TILE_BYTES % (1024 * NW) == 0, "fp8 scan geometry");
+  static_assert(NS >= 2 && NS * TILE_BYTES <= 160 * 1024, "LDS ring exceeds the CU's 160 KiB");
+  static_assert(LOADS <= NKS, "DMA pieces must fit the first chain");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int qb = blockIdx.x % n_qblk, rb = blockIdx.x / n_qblk;
+  const int row_begin = rb * rows_per_blk;
+  const int row_end = min(row_begin + rows_per_blk, n_valid);
+  const int n_tiles = row_end > row_begin ? (row_end - row_begin + TR - 1) / TR : 0;
+  const int h = lane >> 5;
+
+  const int query0 = qb * 256 + wave * 64 + (lane & 31);
+  const int query1 = query0 + 32;
+  i32x8 q0[NKS], q1[NKS];
+  {
+    const uint8_t* p0 = Q + (size_t)min(query0, NQ - 1) * D + h * 32;
+    const uint8_t* p1 = Q + (size_t)min(query1, NQ - 1) * D + h * 32;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      q0[ks] = *reinterpret_cast<const i32x8*>(p0 + ks * 64);
+      q1[ks] = *reinterpret_cast<const i32x8*>(p1 + ks * 64);
+    }
+  }
+  uint32_t goff[LOADS];
+#pragma unroll
+  for (int i = 0; i < LOADS; ++i) {
+    const int s = (i * NW + wave) * 64 + lane;  // 16-byte LDS slot this lane fills
+    const int row = s / CPR, pc = s % CPR;
+    goff[i] = (uint32_t)(row * D + (((pc & ~15) | ((pc & 15) ^ (row & 15))) << 4));
+  }
+  auto issue_piece = [&](int t, int i) {
+    const int tt = min(t, n_tiles - 1);  // past the end: re-load the last tile (keeps vmcnt exact)
+    const uint8_t* base = X + (size_t)(row_begin + tt * TR) * D;
+    char* dst = smem + (t % NS) * TILE_BYTES;
+    glds16_aux<AUX>(base + goff[i], dst + (i * NW + wave) * 1024);
+  };
+  const uint32_t lds_smem = lds_addr(smem);
+  uint32_t voff[8];
+  {
+    const int r = lane & 31;
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        voff[m * 2 + j] = (uint32_t)(r * D + (((4 * m + 2 * h + j) ^ (r & 15)) << 4));
+  }
+
+  float tv0[KMAX], tv1[KMAX];
+  int ti0[KMAX], ti1[KMAX];
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) {
+    tv0[i] = tv1[i] = -INFINITY;
+    ti0[i] = ti1[i] = -1;
+  }
+  float thr0 = thr_init ? thr_init[min(query0, NQ - 1)] : -INFINITY;
+  float thr1 = thr_init ? thr_init[min(query1, NQ - 1)] : -INFINITY;
+  auto update = [&](f32x16& acc, float (&tv)[KMAX], int (&ti)[KMAX], float& thr, int row0) {
+    const int rb4 = row0 + 4 * h;
+    if (row0 + SUB > row_end) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (rb4 + (r & 3) + 8 * (r >> 2) >= row_end) acc[r] = -INFINITY;
+    }
+    float mx = acc[0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, acc[r]);
+    if (mx > thr) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (acc[r] > thr) {
+          topk_insert_par<KMAX>(tv, ti, acc[r], rb4 + (r & 3) + 8 * (r >> 2));
+          thr = fmaxf(thr, tv[KMAX - 1]);
+        }
+      }
+    }
+  };
+
+  if (n_tiles > 0) {
+    for (int p = 0; p < NS - 1; ++p)
+#pragma unroll
+      for (int i = 0; i < LOADS; ++i) issue_piece(p, i);
+  }
+  i32x4 lo[R], hi[R];
+  for (int t = 0; t < n_tiles; ++t) {
+    wait_vmcnt<LOADS * (NS - 2)>();  // tile t landed for this wave
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const uint32_t tbase = lds_smem + (uint32_t)((t % NS) * TILE_BYTES);
+    const int row0 = row_begin + t * TR;
+    const int tnext = t + NS - 1;
+    auto dma = [&](int i) { issue_piece(tnext, i); };
+#pragma unroll
+    for (int sub = 0; sub < SUBS; ++sub) {
+      const uint32_t base = tbase + sub * SUB_BYTES;
+      f32x16 acc0, acc1;
+      if (sub == 0) {
+        fp8_prologue<0, PF, R>(lo, hi, voff, base);
+        Fp8Chain<0, NKS, PF, LOADS>::run(acc0, acc1, lo, hi, q0, q1, voff, base, dma);
+      } else {
+        Fp8Chain<0, NKS, PF, 0>::run(acc0, acc1, lo, hi, q0, q1, voff, base, NoDma());
+      }
+      if (sub + 1 < SUBS)  // next sub-tile's first fragments fly during this top-k
+        fp8_prologue<0, PF, R>(lo, hi, voff, base + SUB_BYTES);
+      update(acc0, tv0, ti0, thr0, row0 + sub * SUB);
+      update(acc1, tv1, ti1, thr1, row0 + sub * SUB);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the tail prefetches before exit
+
+  const int n_rblk = gridDim.x / n_qblk;
+  if (query0 < NQ) {
+    const size_t base = (((size_t)query0 * n_rblk + rb) * 2 + h) * KMAX;
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i) {
+      cand_s[base + i] = tv0[i];
+      cand_i[base + i] = ti0[i];
+    }
+  }
+  if (query1 < NQ) {
+    const size_t base = (((size_t)query1 * n_rblk + rb) * 2 + h) * KMAX;
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i) {
+      cand_s[base + i] = tv1[i];
+      cand_i[base + i] = ti1[i];
+    }
+  }
+}
+
+}  // namespace symb
+
+using namespace symb;
+
+int symb_quant_fp8(const void* in, int in_f32, int ld_in, uint8_t* out, int ld_out, int n, int D,
+                   float scale, int normalize, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (D % 8 || D > 1024) return -1;
+  const dim3 grid((n + 3) / 4), block(256);
+  if (in_f32)
+    hipLaunchKernelGGL(quant_fp8_kernel<true>, grid, block, 0, st, in, ld_in, out, ld_out, n, D,
+                       scale, normalize);
+  else
+    hipLaunchKernelGGL(quant_fp8_kernel<false>, grid, block, 0, st, in, ld_in, out, ld_out, n, D,
+                       scale, normalize);
+  return (int)hipGetLastError();
+}
+
+template <int D, int KMAX, int NS, int SUBS, int AUX>
+static int launch_fp8(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
+                      int NQ, int n_qblk, const float* thr, float* cs, int* ci, hipStream_t st) {
+  auto kern = index_scan_fp8_kernel<D, KMAX, NS, SUBS, AUX>;
+  constexpr int lds = NS * 32 * SUBS * D;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(n_rblk * n_qblk), dim3(256), lds, st, (const uint8_t*)X, n_valid,
+                     rows_per_blk, (const uint8_t*)Q, NQ, n_qblk, thr, cs, ci);
+  return (int)hipGetLastError();
+}
+
+// Ring geometry per D: SUBS sub-tiles of 32 rows per barrier, NS tiles in the LDS ring.
+template <int D> struct Fp8Cfg;
+template <> struct Fp8Cfg<1024> { static constexpr int SUBS = 2, NS = 2; };  // 2 x 64 KiB
+template <> struct Fp8Cfg<768> { static constexpr int SUBS = 1, NS = 6; };   // 6 x 24 KiB
+template <> struct Fp8Cfg<512> { static constexpr int SUBS = 2, NS = 4; };   // 4 x 32 KiB
+
+template <int D>
+static int dispatch_fp8(int kmax, int aux, int variant, const void* X, int n_valid,
+                        int rows_per_blk, int n_rblk, const void* Q, int NQ, int n_qblk,
+                        const float* thr, float* cs, int* ci, hipStream_t st) {
+  constexpr int SUBS = Fp8Cfg<D>::SUBS, NS = Fp8Cfg<D>::NS;
+#define SYMB_F(K, NS_, SUBS_, A) \
+  launch_fp8<D, K, NS_, SUBS_, A>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, n_qblk, thr, cs, ci, st)
+  if constexpr (D == 1024)  // variant 1: one sub-tile per barrier, 4-deep ring (-4 % at 100M rows)
+    if (variant == 1) return aux ? SYMB_F(16, 4, 1, 2) : SYMB_F(16, 4, 1, 0);
+  if (kmax == 16) return aux ? SYMB_F(16, NS, SUBS, 2) : SYMB_F(16, NS, SUBS, 0);
+  if (kmax == 32) return aux ? SYMB_F(32, NS, SUBS, 2) : SYMB_F(32, NS, SUBS, 0);
+#undef SYMB_F
+  return -1;
+}
+
+// X: [>= round_up(n_valid, 64), D] e4m3 rows (scale S), Q: [NQ, D] e4m3 queries (scale S).
+// Candidates: [NQ][n_rblk][2][kmax] raw accumulators (S^2 * cosine); thr_init in the same units.
+// variant: 0 = default ring geometry, 1 = D=1024 with 1 sub-tile/barrier and a 4-deep ring.
+int symb_index_scan_fp8(const void* X, int n_valid, int D, int rows_per_blk, int n_rblk,
+                        const void* Q, int NQ, int kmax, float* cand_s, int* cand_i,
+                        hipStream_t st, int aux, const float* thr_init, int variant) {
+  if (NQ <= 0 || n_rblk <= 0) return 0;
+  if (rows_per_blk % 64) return -1;
+  const int n_qblk = (NQ + 255) / 256;
+  if (aux < 0) aux = n_qblk == 1 ? 2 : 0;
+#define SYMB_ARGS kmax, aux, variant, X, n_valid, rows_per_blk, n_rblk, Q, NQ, n_qblk, thr_init, \
+                  cand_s, cand_i, st
+  switch (D) {
+    case 512: return dispatch_fp8<512>(SYMB_ARGS);
+    case 768: return dispatch_fp8<768>(SYMB_ARGS);
+    case 1024: return dispatch_fp8<1024>(SYMB_ARGS);
+  }
+#undef SYMB_ARGS
+  return -1;
+}

@@ -19,7 +19,7 @@
 //    registers; the insertion path runs only for lanes whose new scores beat their threshold
 //    (rare once the list is warm).
 //  * A second small kernel merges the per-workgroup candidate lists into the final top-k.
-#include "common.h"
+#include "scan_common.h"
 
 #include <type_traits>
 
@@ -27,27 +27,10 @@ namespace symb {
 
 constexpr int TOPK_WAVES = 8;
 
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
-}
-
-template <int AUX>
-__device__ __forceinline__ void glds16_aux(const void* gsrc, void* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds(
-      (const __attribute__((address_space(1))) void*)gsrc,
-      (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, AUX);
-}
-
 // ---- hand-counted LDS fragment pipeline -------------------------------------------------------
 // hipcc will not count ds_reads around the DMA ring (it drains lgkmcnt(0) before every few MFMAs),
 // so the A fragments are read by inline asm and each MFMA waits with a counted lgkmcnt(N) whose
 // asm names the fragment as "+v" (the MFMA depends on it and cannot be hoisted above the wait).
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
-}
-
 template <int OFF>
 __device__ __forceinline__ void ds_read16(bf16x8& dst, uint32_t addr) {
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(addr), "i"(OFF));
@@ -61,9 +44,6 @@ __device__ __forceinline__ void lgkm_wait(bf16x8& v) {
 // low 4 bits of the 16-byte chunk index, so the per-lane part repeats every M k-steps).
 // DMA (functor, may be a no-op): DMA(i) issues LDS-DMA piece i of the next tile; pieces are
 // spread one per DMA_EVERY MFMAs so the waves' DMA issue interleaves with their matrix work.
-struct NoDma {
-  __device__ __forceinline__ void operator()(int) const {}
-};
 template <int KS, int NKS, int PF, int M, bool M32, int DMA_EVERY = 0, int DMA_PIECES = 0>
 struct FragChain {
   static constexpr int R = PF + 1;  // ring slots: a slot is refilled one MFMA after its last use
@@ -91,42 +71,6 @@ __device__ __forceinline__ void frag_prologue(bf16x8 (&a)[R], const uint32_t (&v
                                               uint32_t base) {
   ds_read16<(J / M) * 256>(a[J % R], base + voff[J % M]);
   if constexpr (J + 1 < PF) frag_prologue<J + 1, PF, M, R>(a, voff, base);
-}
-
-template <int KMAX>
-__device__ __forceinline__ void topk_insert(float (&tv)[KMAX], int (&ti)[KMAX], float s, int id) {
-#pragma unroll
-  for (int i = 0; i < KMAX; ++i) {
-    const bool sw = s > tv[i];
-    const float ov = tv[i];
-    const int oi = ti[i];
-    tv[i] = sw ? s : ov;
-    ti[i] = sw ? id : oi;
-    s = sw ? ov : s;
-    id = sw ? oi : id;
-  }
-}
-
-// Same result as topk_insert but with no serial chain: every slot decides from the ORIGINAL
-// sorted list (monotone "s > tv[i]" flags), so the 16 compare/select pairs issue back to back.
-template <int KMAX>
-__device__ __forceinline__ void topk_insert_par(float (&tv)[KMAX], int (&ti)[KMAX], float s, int id) {
-  float nv[KMAX];
-  int ni[KMAX];
-  nv[0] = s > tv[0] ? s : tv[0];
-  ni[0] = s > tv[0] ? id : ti[0];
-#pragma unroll
-  for (int i = 1; i < KMAX; ++i) {
-    const float shv = s > tv[i - 1] ? tv[i - 1] : s;   // value slot i takes if s beats it
-    const int shi = s > tv[i - 1] ? ti[i - 1] : id;
-    nv[i] = s > tv[i] ? shv : tv[i];
-    ni[i] = s > tv[i] ? shi : ti[i];
-  }
-#pragma unroll
-  for (int i = 0; i < KMAX; ++i) {
-    tv[i] = nv[i];
-    ti[i] = ni[i];
-  }
 }
 
 // MFMA_32 = true : D = 384 path (32x32x16, 32 queries per wave, 2 lists per query per wave)
@@ -388,8 +332,8 @@ struct FragChain2 {
     // hand-issued so the 192 query registers stay resident in AGPRs as the B operand (the builtin
     // form makes the compiler shuttle them AGPR->VGPR around every MFMA); step 0 zero-inits C.
     if constexpr (KS == 0) {
-      asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=v"(acc0) : "v"(a[0]), "a"(q0[0]));
-      asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=v"(acc1) : "v"(a[0]), "a"(q1[0]));
+      asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(acc0) : "v"(a[0]), "a"(q0[0]));
+      asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(acc1) : "v"(a[0]), "a"(q1[0]));
     } else {
       asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc0) : "v"(a[KS % R]), "a"(q0[KS]));
       asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc1) : "v"(a[KS % R]), "a"(q1[KS]));

@@ -63,3 +63,27 @@ def test_snapshot_wal_resume_and_torn_tail(tmp_path):
     assert sum(len(ids) for ids, _, _ in recs) >= 1
     st3 = VectorStore(8, 1000, device="cpu", snapshot_dir=d)
     assert st3.count == 26
+
+
+def test_fp8_shard_cpu_path_and_snapshot(tmp_path):
+    """fp8 storage on CPU (torch float8_e4m3fn == gfx950 OCP e4m3): search ranks like fp32 up to
+    e4m3 rounding; snapshots keep the raw bytes and refuse a dtype mismatch."""
+    from codename_symbiont_amd.index.persist import load_snapshot, save_snapshot
+
+    D = 256
+    v = _vecs(500, D, 3)
+    sh = HbmIndexShard(D, 600, device="cpu", dtype="fp8")
+    sh.append_f32(torch.from_numpy(v))
+    assert sh.rows.dtype == torch.uint8
+    q = torch.nn.functional.normalize(torch.from_numpy(v[[5, 77, 300]]), dim=-1)
+    s, r = sh.search(q.bfloat16(), 4)
+    assert r[:, 0].tolist() == [5, 77, 300]
+    assert torch.allclose(s[:, 0], torch.ones(3), atol=0.03)   # self-similarity through e4m3
+    save_snapshot(sh, str(tmp_path))
+    sh2 = HbmIndexShard(D, 600, device="cpu", dtype="fp8")
+    assert load_snapshot(sh2, str(tmp_path)) == 500
+    assert torch.equal(sh2.rows[:500], sh.rows[:500])
+    with pytest.raises(ValueError, match="dtype"):
+        load_snapshot(HbmIndexShard(D, 600, device="cpu"), str(tmp_path))
+    with pytest.raises(ValueError, match="multiple of 256"):
+        HbmIndexShard(384, 10, device="cpu", dtype="fp8")

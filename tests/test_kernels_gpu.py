@@ -195,3 +195,63 @@ def test_index_scan_seeded_threshold_is_exact(D):
     assert torch.equal(r0, r1) and torch.equal(s0, s1)
     ref_s, _ = R.topk_ref(shard.unit_rows(), q, k)
     _close(s1, ref_s, atol=2e-3, what="seeded topk scores")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("src", [torch.float32, torch.bfloat16])
+def test_quant_fp8_matches_torch_e4m3(src):
+    from codename_symbiont_amd.ops import kernels as K
+
+    x = torch.nn.functional.normalize(_f(1000, 768, seed=4).float(), dim=-1).to(src)
+    got = K.quant_fp8(x, scale=K.FP8_SCALE)
+    ref = (x.float() * K.FP8_SCALE).to(torch.float8_e4m3fn).view(torch.uint8)
+    torch.cuda.synchronize()
+    assert (got == ref).float().mean().item() > 0.999
+    _close(K.fp8_to_float(got), K.fp8_to_float(ref), atol=1e-3, what="e4m3 decode")
+    # normalize=True on raw rows == quantising the normalised rows
+    raw = _f(64, 1024, seed=6).float() * 3.0
+    a = K.quant_fp8(raw, normalize=True)
+    b = K.quant_fp8(torch.nn.functional.normalize(raw, dim=-1))
+    assert (a == b).float().mean().item() > 0.999
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D,k,n,nq", [(1024, 10, 20_011, 300), (768, 5, 9000, 70),
+                                      (512, 20, 7777, 33), (1024, 16, 64, 256)])
+def test_index_scan_fp8_exact_on_decoded_rows(D, k, n, nq):
+    """fp8 scan == fp32 top-k over the DECODED e4m3 rows and queries (the MFMA sums exact e4m3
+    products in fp32), and ranks like the bf16 cosine up to e4m3 rounding."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+    from codename_symbiont_amd.ops import kernels as K
+
+    shard = HbmIndexShard(D, n + 64, dtype="fp8")
+    shard.fill_random(n, seed=7)
+    q = torch.nn.functional.normalize(_f(nq, D, seed=8).float(), dim=-1).bfloat16()
+    s, r = shard.search(q, k)
+    qd = K.fp8_to_float(K.quant_fp8(q))
+    ref_s, ref_i = R.topk_ref(shard.unit_rows().float(), qd, k)
+    torch.cuda.synchronize()
+    _close(s, ref_s.float(), atol=2e-3, what="fp8 topk scores")
+    hits = sum(len(set(r[i].tolist()) & set(ref_i[i].tolist())) for i in range(nq))
+    assert hits / (nq * min(k, n)) > 0.99
+    true = (qd @ shard.unit_rows().float().t()).gather(1, r.long())
+    _close(s, true, atol=2e-3, what="fp8 returned rows")
+
+
+@pytest.mark.gpu
+def test_index_scan_fp8_seeded_matches_unseeded():
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+
+    n, D, nq, k = (1 << 20) + 999, 1024, 256, 10
+    shard = HbmIndexShard(D, n, dtype="fp8")
+    shard.fill_random(n, seed=2)
+    q = torch.nn.functional.normalize(_f(nq, D, seed=1).float(), dim=-1).bfloat16()
+    shard.seed_threshold = False
+    s0, r0 = shard.search(q, k)
+    shard.seed_threshold = True
+    s1, r1 = shard.search(q, k)
+    shard.scan_variant = 1       # 1 sub-tile per barrier, 4-deep ring
+    s2, r2 = shard.search(q, k)
+    torch.cuda.synchronize()
+    assert torch.equal(r0, r1) and torch.equal(s0, s1)
+    assert torch.equal(r0, r2) and torch.equal(s0, s2)
