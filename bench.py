@@ -16,6 +16,15 @@ index rows -- there is no network for checkpoints or datasets.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+
+The other BASELINE.json configs run through the same step (benchmarks/suite.py drives them):
+  --mode embed                                   all-MiniLM-L6-v2 bf16 embedding, batch 256
+  --mode search                                  100M x 384 sharded cosine top-k
+  --model bge-base --mode embed                  bge-base-en-v1.5 DP embedding
+  --model e5-large --index-dtype fp8 --index-rows 1000000000
+                                                 e5-large-v2 + 1B-vector fp8 index (1B/N rows
+                                                 per rank: needs N >= 4 for 1 TB; smaller N
+                                                 takes --index-rows that fit)
 """
 from __future__ import annotations
 
@@ -50,6 +59,7 @@ def main() -> None:
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--model", default="minilm-l6")
     ap.add_argument("--mode", choices=["full", "embed", "search"], default="full")
+    ap.add_argument("--index-dtype", choices=["bf16", "fp8"], default="bf16")
     args = ap.parse_args()
 
     from codename_symbiont_amd.index.shard import HbmIndexShard
@@ -70,13 +80,14 @@ def main() -> None:
     enc = HipEncoder(cfg, seed=0, device=dev)
     rows_per_rank = args.index_rows // info.world
     extra = (K + W + 4) * B
-    shard = HbmIndexShard(cfg.hidden, rows_per_rank + extra, device=dev)
+    shard = HbmIndexShard(cfg.hidden, rows_per_rank + extra, device=dev, dtype=args.index_dtype)
     if args.mode != "embed":
         shard.fill_random(rows_per_rank, seed=100 + info.rank)
     searcher = ShardedSearcher(shard, info)
     torch.cuda.synchronize(dev)
+    row_bytes = cfg.hidden * (1 if args.index_dtype == "fp8" else 2)
     log(info, f"[bench] setup {time.time() - t0:.1f}s: {cfg.model_name}, shard {rows_per_rank} "
-              f"rows x {cfg.hidden} bf16 = {rows_per_rank * cfg.hidden * 2 / 1e9:.1f} GB/rank")
+              f"rows x {cfg.hidden} {args.index_dtype} = {rows_per_rank * row_bytes / 1e9:.1f} GB/rank")
 
     # host batches (pinned) rotated through two device buffers filled on a copy stream
     NB = 4
@@ -144,12 +155,21 @@ def main() -> None:
 
     ms = elapsed * 1000.0 / K
     total = B * info.world * K / elapsed
+    headline = (args.model in ("minilm-l6", "minilm", "all-MiniLM-L6-v2") and args.mode == "full"
+                and args.index_rows == 100_000_000 and args.index_dtype == "bf16")
+    short = cfg.model_name.split("/")[-1]
+    rows_txt = f"{args.index_rows / 1e6:g}M" if args.index_rows < 10**9 else f"{args.index_rows / 1e9:g}B"
+    metric = METRIC if headline else {
+        "full": f"embeds/sec + top-k QPS, {short} / {rows_txt}x{cfg.hidden} {args.index_dtype} index",
+        "embed": f"embeds/sec, {short} ({cfg.key}) bf16, batch {B} x seq {S}",
+        "search": f"top-{args.k} QPS, {rows_txt}x{cfg.hidden} {args.index_dtype} index, {B} queries/rank",
+    }[args.mode]
     if info.rank == 0:
         res = {
-            "metric": METRIC,
+            "metric": metric,
             "value": round(total, 2),
-            "unit": "embeds/s (whole job; every embedded sentence is also answered as a top-10 "
-                    "query over the 100M x 384 corpus, so this equals top-k QPS)"
+            "unit": f"embeds/s (whole job; every embedded sentence is also answered as a top-{args.k} "
+                    f"query over the {rows_txt} x {cfg.hidden} corpus, so this equals top-k QPS)"
                     if args.mode == "full" else ("embeds/s" if args.mode == "embed" else "queries/s"),
             "n_gpus": info.world,
             "steps": K,
@@ -159,9 +179,10 @@ def main() -> None:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
+            "index_dtype": args.index_dtype,
             "data": "synthetic token ids, random-init weights, random unit index rows",
             "config": {
-                "model": "all-MiniLM-L6-v2", "global_batch": B * info.world, "seq_len": S,
+                "model": short, "global_batch": B * info.world, "seq_len": S,
                 "parallelism": f"dp{info.world}+index_shard{info.world}",
                 "index_rows": args.index_rows, "dim": cfg.hidden, "top_k": args.k,
                 "mode": args.mode,
@@ -170,7 +191,8 @@ def main() -> None:
             "topk_qps": round(total, 2) if args.mode != "embed" else 0.0,
             "embed_ms_per_step_rank0": round(e_ms, 3),
             "search_ms_per_step_rank0": round(s_ms, 3),
-            "vs_derived_reference_estimate": round(total / DERIVED_REF_EMBEDS_PER_SEC, 1),
+            "vs_derived_reference_estimate": (round(total / DERIVED_REF_EMBEDS_PER_SEC, 1)
+                                              if args.mode != "search" else None),
         }
         print(json.dumps(res), flush=True)
     D.shutdown(info)
