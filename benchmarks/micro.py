@@ -122,8 +122,8 @@ def cmd_scanabl(a):
         variants[f"abl{m}"]()
         os_ = torch.empty(a.nq, 10, device="cuda")
         oi = torch.empty(a.nq, 10, dtype=torch.int32, device="cuda")
-        h.topk_merge(cs.data_ptr(), ci.data_ptr(), a.nq, cs.shape[1], 16, 10, os_.data_ptr(),
-                     oi.data_ptr(), 0, 0, st)
+        h.topk_merge(cs.data_ptr(), ci.data_ptr(), a.nq, n_rblk * 2 * 16, 16, 10,
+                     os_.data_ptr(), oi.data_ptr(), 0, 0, st)
         torch.cuda.synchronize()
         merged[m] = (os_.clone(), oi.clone())
     same_var = {m: bool(torch.equal(merged[0][1], merged[m][1])) for m in (3, 4)}
