@@ -96,6 +96,8 @@ class EmbedBatcher:
         outs = []
         s = 0
         dev = getattr(self.encoder, "device", torch.device("cpu"))
+        if dev.type == "cuda":
+            return self._encode_all_gpu(ids, cu, lens, dev)
         while s < len(texts):
             e, tok = s, 0
             while e < len(texts) and (e == s or tok + lens[e] <= self.token_budget):
@@ -114,6 +116,52 @@ class EmbedBatcher:
             outs.append(pooled.float().cpu().numpy())
             s = e
         return np.concatenate(outs, 0) if outs else np.zeros((0, cfg.hidden), np.float32)
+
+
+    def _encode_all_gpu(self, ids, cu, lens, dev) -> np.ndarray:
+        """K0/K19 pipeline: pinned host staging, H2D of sub-batch i+1 on a copy
+        stream while sub-batch i computes, async D2H of every pooled block into one pinned output,
+        ONE host sync per group (the reference syncs per chunk of 8, embedding_generator.rs:214)."""
+        from ..models.encoder import PackedBatch
+
+        cfg = self.encoder.cfg
+        n = len(lens)
+        out = torch.empty((n, cfg.hidden), dtype=torch.float32, pin_memory=True)
+        compute = torch.cuda.current_stream(dev)
+        copy = self._copy_stream(dev)
+        keep = []   # host/device tensors that must outlive their async copies
+        s = 0
+        while s < n:
+            e, tok = s, 0
+            while e < n and (e == s or tok + lens[e] <= self.token_budget):
+                tok += int(lens[e])
+                e += 1
+            a, b = int(cu[s]), int(cu[e])
+            sub_cu = (cu[s:e + 1] - cu[s]).astype(np.int32)
+            pos = np.concatenate([np.arange(cfg.position_offset, cfg.position_offset + int(L),
+                                            dtype=np.int32) for L in lens[s:e]])
+            host = [torch.from_numpy(np.ascontiguousarray(x)).pin_memory()
+                    for x in (ids[a:b], pos, sub_cu)]
+            with torch.cuda.stream(copy):
+                d = [h.to(dev, non_blocking=True) for h in host]
+                ready = torch.cuda.Event()
+                ready.record(copy)
+            compute.wait_event(ready)
+            for t in d:
+                t.record_stream(compute)
+            pb = PackedBatch(d[0], d[1], None, d[2], int(lens[s:e].max()))
+            pooled, _unit = self.encoder.forward_packed(pb)
+            out[s:e].copy_(pooled.float(), non_blocking=True)
+            keep.append((host, pooled))
+            s = e
+        compute.synchronize()
+        return out.numpy()
+
+    def _copy_stream(self, dev):
+        st = getattr(self, "_cs", None)
+        if st is None:
+            st = self._cs = torch.cuda.Stream(dev)
+        return st
 
 
 @dataclass

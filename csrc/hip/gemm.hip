@@ -42,6 +42,8 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
   constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
   constexpr int RM = WTM / 16, RN = WTN / 16;
   constexpr int TILE_BYTES = (BM + BN) * 128;
+  // RES_LN tiles too tall to stage in fp32 at once are normalised one wave-row band at a time
+  constexpr int EPI_PASSES = (EPI == EPI_RES_LN && BM * (BN + 4) * 4 > 160 * 1024) ? WAVES_M : 1;
   static_assert((BM * 8) % NT == 0 && (BN * 8) % NT == 0, "tile rows must cover the DMA waves");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -72,87 +74,14 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
     }
   };
 
-  f32x4 acc[RM][RN];
-#pragma unroll
-  for (int i = 0; i < RM; ++i)
-#pragma unroll
-    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  stage(0, 0);
-  for (int kt = 0; kt < KT; ++kt) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (kt + 1 < KT) stage(kt + 1, (kt + 1) & 1);
-    const char* sA = smem + (kt & 1) * TILE_BYTES;
-    const char* sB = sA + BM * 128;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int chunk = kk * 4 + (lane >> 4);
-      bf16x8 a[RM], b[RN];
-#pragma unroll
-      for (int i = 0; i < RM; ++i)
-        a[i] = *reinterpret_cast<const bf16x8*>(sA + swz_off(wm * WTM + i * 16 + (lane & 15), chunk));
-#pragma unroll
-      for (int j = 0; j < RN; ++j)
-        b[j] = *reinterpret_cast<const bf16x8*>(sB + swz_off(wn * WTN + j * 16 + (lane & 15), chunk));
-#pragma unroll
-      for (int i = 0; i < RM; ++i)
-#pragma unroll
-        for (int j = 0; j < RN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-    }
-  }
-
-  // ---- epilogue: fp32 tile -> LDS (padded rows) -> row-contiguous 16-byte stores ----
-  constexpr int CS = BN + 4;
-  float* Cs = reinterpret_cast<float*>(smem);
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < RM; ++i)
-#pragma unroll
-    for (int j = 0; j < RN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wm * WTM + i * 16 + (lane >> 4) * 4 + r;
-        const int col = wn * WTN + j * 16 + (lane & 15);
-        Cs[row * CS + col] = acc[i][j][r];
-      }
-  __syncthreads();
-
-  if constexpr (EPI != EPI_RES_LN) {
-    constexpr int VPR = BN / 8;
-    for (int v = tid; v < BM * VPR; v += NT) {
-      const int row = v / VPR, c8 = (v % VPR) * 8;
-      const int grow = m0 + row;
-      if (grow >= M) continue;
-      const f32x4 x0 = *reinterpret_cast<const f32x4*>(Cs + row * CS + c8);
-      const f32x4 x1 = *reinterpret_cast<const f32x4*>(Cs + row * CS + c8 + 4);
-      const f32x4 b0 = *reinterpret_cast<const f32x4*>(bias + n0 + c8);
-      const f32x4 b1 = *reinterpret_cast<const f32x4*>(bias + n0 + c8 + 4);
-      float y[8];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        y[e] = x0[e] + b0[e];
-        y[e + 4] = x1[e] + b1[e];
-      }
-      if constexpr (EPI == EPI_GELU) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) y[e] = gelu_erf(y[e]);
-      }
-      if constexpr (EPI == EPI_RES) {
-        float r[8];
-        load8(R + (size_t)grow * ldr + n0 + c8, r);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) y[e] += r[e];
-      }
-      store8(C + (size_t)grow * ldc + n0 + c8, y);
-    }
-  } else {
-    // Row-complete tile (n0 == 0, BN == N): one wave per row, lane owns 8 consecutive columns.
+  // LayerNorm(+ bias + residual) of `rows` staged fp32 rows (row-complete: n0 == 0, BN == N);
+  // one wave per row, lane owns 8 consecutive columns.
+  auto res_ln_rows = [&](const float* Cs, int rows, int grow0) {
+    constexpr int CS = BN + 4;
     constexpr int NV = BN / 8;
     constexpr int PER = (NV + 63) / 64;
-    for (int row = wave; row < BM; row += NW) {
-      const int grow = m0 + row;
+    for (int row = wave; row < rows; row += NW) {
+      const int grow = grow0 + row;
       if (grow >= M) break;
       float x[PER][8];
       float s = 0.f;
@@ -194,6 +123,106 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
         }
       }
     }
+  };
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  stage(0, 0);
+  for (int kt = 0; kt < KT; ++kt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt + 1 < KT) stage(kt + 1, (kt + 1) & 1);
+    const char* sA = smem + (kt & 1) * TILE_BYTES;
+    const char* sB = sA + BM * 128;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int chunk = kk * 4 + (lane >> 4);
+      bf16x8 a[RM], b[RN];
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+        a[i] = *reinterpret_cast<const bf16x8*>(sA + swz_off(wm * WTM + i * 16 + (lane & 15), chunk));
+#pragma unroll
+      for (int j = 0; j < RN; ++j)
+        b[j] = *reinterpret_cast<const bf16x8*>(sB + swz_off(wn * WTN + j * 16 + (lane & 15), chunk));
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  // ---- epilogue: fp32 tile -> LDS (padded rows) -> row-contiguous 16-byte stores ----
+  constexpr int CS = BN + 4;
+  float* Cs = reinterpret_cast<float*>(smem);
+  __syncthreads();
+  if constexpr (EPI == EPI_RES_LN && EPI_PASSES > 1) {
+    // the fp32 row-complete tile does not fit LDS at once: stage one wave-row band per pass
+    for (int p = 0; p < EPI_PASSES; ++p) {
+      if (wm == p) {
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int j = 0; j < RN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int row = i * 16 + (lane >> 4) * 4 + r;
+              const int col = wn * WTN + j * 16 + (lane & 15);
+              Cs[row * CS + col] = acc[i][j][r];
+            }
+      }
+      __syncthreads();
+      res_ln_rows(Cs, WTM, m0 + p * WTM);
+      __syncthreads();
+    }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * WTM + i * 16 + (lane >> 4) * 4 + r;
+        const int col = wn * WTN + j * 16 + (lane & 15);
+        Cs[row * CS + col] = acc[i][j][r];
+      }
+  __syncthreads();
+
+  if constexpr (EPI != EPI_RES_LN) {
+    constexpr int VPR = BN / 8;
+    for (int v = tid; v < BM * VPR; v += NT) {
+      const int row = v / VPR, c8 = (v % VPR) * 8;
+      const int grow = m0 + row;
+      if (grow >= M) continue;
+      const f32x4 x0 = *reinterpret_cast<const f32x4*>(Cs + row * CS + c8);
+      const f32x4 x1 = *reinterpret_cast<const f32x4*>(Cs + row * CS + c8 + 4);
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(bias + n0 + c8);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(bias + n0 + c8 + 4);
+      float y[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        y[e] = x0[e] + b0[e];
+        y[e + 4] = x1[e] + b1[e];
+      }
+      if constexpr (EPI == EPI_GELU) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) y[e] = gelu_erf(y[e]);
+      }
+      if constexpr (EPI == EPI_RES) {
+        float r[8];
+        load8(R + (size_t)grow * ldr + n0 + c8, r);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) y[e] += r[e];
+      }
+      store8(C + (size_t)grow * ldc + n0 + c8, y);
+    }
+  } else {
+    res_ln_rows(Cs, BM, m0);
   }
 }
 
@@ -203,7 +232,8 @@ static int launch_cfg(const __bf16* A, int lda, const __bf16* W, int ldw, const 
                       __bf16* C, int ldc, int M, int N, int K, hipStream_t st) {
   auto kern = gemm_bf16_kernel<BM, BN, WM, WN, EPI>;
   constexpr int main_bytes = 2 * (BM + BN) * 128;
-  constexpr int epi_bytes = BM * (BN + 4) * 4;
+  constexpr int full_epi = BM * (BN + 4) * 4;
+  constexpr int epi_bytes = full_epi > 160 * 1024 ? (BM / WM) * (BN + 4) * 4 : full_epi;
   constexpr int lds = main_bytes > epi_bytes ? main_bytes : epi_bytes;
   static bool attr_set = false;
   if (!attr_set) {
@@ -220,6 +250,14 @@ static int launch_cfg(const __bf16* A, int lda, const __bf16* W, int ldw, const 
 
 using namespace symb;
 
+// Tile height of the row-complete RES_LN GEMM (64 or 128); a tuning knob, see symb_gemm_config.
+static int g_resln_bm = 128;
+int symb_gemm_config(int resln_bm) {
+  if (resln_bm != 64 && resln_bm != 128) return -1;
+  g_resln_bm = resln_bm;
+  return 0;
+}
+
 // Returns 0 on success, a HIP error code, or -1 for an unsupported shape.
 int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const float* bias,
               const void* R, int ldr, const float* gamma, const float* beta, float eps, void* C,
@@ -231,6 +269,9 @@ int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const flo
   auto r = (const __bf16*)R;
   auto c = (__bf16*)C;
   if (epi == EPI_RES_LN) {
+    if (N == 384 && g_resln_bm == 128)
+      return launch_cfg<128, 384, 2, 4, EPI_RES_LN>(a, lda, w, ldw, bias, r, ldr, gamma, beta,
+                                                    eps, c, ldc, M, N, K, st);
     if (N == 384)
       return launch_cfg<64, 384, 2, 4, EPI_RES_LN>(a, lda, w, ldw, bias, r, ldr, gamma, beta, eps,
                                                    c, ldc, M, N, K, st);
