@@ -207,14 +207,17 @@ def cmd_gemm(a):
         be = torch.zeros(N, device="cuda")
         y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         from codename_symbiont_amd.ops._ext import hip as _hip
-        var = {"hip_fused_bm64": lambda: (_hip().gemm_config(64),
-                                     K.gemm(x, w, b, epi, r if epi >= 2 else None, g, be, 1e-12, out=y)),
-               "torch_matmul_only": lambda: torch.matmul(x, w.t(), out=y)}
+        rr = r if epi >= 2 else None
+        var = {"torch_matmul_only": lambda: torch.matmul(x, w.t(), out=y)}
         if epi == K.EPI_RES_LN:
-            var["hip_fused_bm128"] = lambda: (_hip().gemm_config(128),
-                                              K.gemm(x, w, b, epi, r, g, be, 1e-12, out=y))
+            var["hip_bm64"] = lambda: (_hip().gemm_config(64, 0), K.gemm(x, w, b, epi, rr, g, be, 1e-12, out=y))
+            var["hip_bm128"] = lambda: (_hip().gemm_config(128, 0), K.gemm(x, w, b, epi, rr, g, be, 1e-12, out=y))
+        else:
+            var["hip_128x128"] = lambda: (_hip().gemm_config(128, 0), K.gemm(x, w, b, epi, rr, g, be, 1e-12, out=y))
+            var["hip_256x128_3st"] = lambda: (_hip().gemm_config(128, 1),
+                                              K.gemm(x, w, b, epi, rr, g, be, 1e-12, out=y))
         res = ab(var, rounds=a.rounds, iters=a.iters)
-        _hip().gemm_config(128)
+        _hip().gemm_config(128, 0)
         fl = 2 * M * N * Kd
         out[name] = {k: dict(ms=round(m, 4), TFLOPs=round(fl / (m / 1e3) / 1e12)) for k, (m, _) in res.items()}
     print(json.dumps({"bench": "gemm", "M": M, "results": out}))

@@ -40,7 +40,7 @@ int symb_index_scan(const void* X, int n_valid, int D, int rows_per_blk, int n_r
 int symb_index_scan_ablate(const void* X, int n_valid, int rows_per_blk, int n_rblk,
                            const void* Q, int NQ, float* cs, int* ci, hipStream_t st, int abl,
                            const float* thr);
-int symb_gemm_config(int resln_bm);
+int symb_gemm_config(int resln_bm, int tile);
 int symb_quant_fp8(const void* in, int in_f32, int ld_in, uint8_t* out, int ld_out, int n, int D,
                    float scale, int normalize, hipStream_t st);
 int symb_index_scan_fp8(const void* X, int n_valid, int D, int rows_per_blk, int n_rblk,
@@ -206,8 +206,9 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("X"), py::arg("n_valid"), py::arg("rows_per_blk"), py::arg("n_rblk"), py::arg("Q"),
      py::arg("NQ"), py::arg("cs"), py::arg("ci"), py::arg("stream"), py::arg("abl"),
      py::arg("thr") = 0);
-  m.def("gemm_config", [](int resln_bm) { check(symb_gemm_config(resln_bm), "gemm_config"); },
-        py::arg("resln_bm"));
+  m.def("gemm_config", [](int resln_bm, int tile) {
+    check(symb_gemm_config(resln_bm, tile), "gemm_config");
+  }, py::arg("resln_bm") = 128, py::arg("tile") = 0);
   m.def("quant_fp8", [](uptr in, bool in_f32, int ld_in, uptr out, int ld_out, int n, int D,
                         float scale, bool normalize, uptr st) {
     check(symb_quant_fp8(P<void>(in), in_f32, ld_in, P<uint8_t>(out), ld_out, n, D, scale,

@@ -31,7 +31,7 @@ __device__ __forceinline__ int swz_off(int row, int chunk) {
   return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
 }
 
-template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI>
+template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, int NSTAGE = 2>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
     const __bf16* __restrict__ A, int lda, const __bf16* __restrict__ W, int ldw,
     const float* __restrict__ bias, const __bf16* __restrict__ R, int ldr,
@@ -131,12 +131,27 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
 #pragma unroll
     for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  constexpr int LOADS = (BM * 8) / NT + (BN * 8) / NT;  // glds per thread per stage
   stage(0, 0);
+  if (NSTAGE > 2 && KT > 1) stage(1, 1);
   for (int kt = 0; kt < KT; ++kt) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (kt + 1 < KT) stage(kt + 1, (kt + 1) & 1);
-    const char* sA = smem + (kt & 1) * TILE_BYTES;
+    if constexpr (NSTAGE == 2) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (kt + 1 < KT) stage(kt + 1, (kt + 1) & 1);
+    } else {
+      // tile kt landed once only tile kt+1's loads remain; a raw barrier (no vmcnt(0) drain)
+      // keeps that next tile in flight across it, and it also retires every wave's reads of the
+      // buffer that stage(kt+2) refills (read in iteration kt-1)
+      if (kt + 1 < KT)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(LOADS) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (kt + 2 < KT) stage(kt + 2, (kt + 2) % NSTAGE);
+    }
+    const char* sA = smem + (kt % NSTAGE) * TILE_BYTES;
     const char* sB = sA + BM * 128;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -226,12 +241,12 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
   }
 }
 
-template <int BM, int BN, int WM, int WN, int EPI>
+template <int BM, int BN, int WM, int WN, int EPI, int NSTAGE = 2>
 static int launch_cfg(const __bf16* A, int lda, const __bf16* W, int ldw, const float* bias,
                       const __bf16* R, int ldr, const float* g, const float* b, float eps,
                       __bf16* C, int ldc, int M, int N, int K, hipStream_t st) {
-  auto kern = gemm_bf16_kernel<BM, BN, WM, WN, EPI>;
-  constexpr int main_bytes = 2 * (BM + BN) * 128;
+  auto kern = gemm_bf16_kernel<BM, BN, WM, WN, EPI, NSTAGE>;
+  constexpr int main_bytes = NSTAGE * (BM + BN) * 128;
   constexpr int full_epi = BM * (BN + 4) * 4;
   constexpr int epi_bytes = full_epi > 160 * 1024 ? (BM / WM) * (BN + 4) * 4 : full_epi;
   constexpr int lds = main_bytes > epi_bytes ? main_bytes : epi_bytes;
@@ -252,9 +267,14 @@ using namespace symb;
 
 // Tile height of the row-complete RES_LN GEMM (64 or 128); a tuning knob, see symb_gemm_config.
 static int g_resln_bm = 128;
-int symb_gemm_config(int resln_bm) {
+// Tile of the bias / GELU / residual GEMMs: 0 = 128x128 (4 waves, 2-stage ring),
+// 1 = 256x128 (8 waves, 3-stage ring with a tile in flight across each barrier).
+static int g_tile = 0;
+int symb_gemm_config(int resln_bm, int tile) {
   if (resln_bm != 64 && resln_bm != 128) return -1;
+  if (tile != 0 && tile != 1) return -1;
   g_resln_bm = resln_bm;
+  g_tile = tile;
   return 0;
 }
 
@@ -278,6 +298,17 @@ int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const flo
     return -1;  // wider rows: EPI_RES + symb_add_ln
   }
   if (N % 128 != 0) return -1;
+  if (g_tile == 1) {
+#define SYMB_G(E) launch_cfg<256, 128, 4, 2, E, 3>(a, lda, w, ldw, bias, r, ldr, gamma, beta, eps, \
+                                                 c, ldc, M, N, K, st)
+    switch (epi) {
+      case EPI_BIAS: return SYMB_G(EPI_BIAS);
+      case EPI_GELU: return SYMB_G(EPI_GELU);
+      case EPI_RES: return SYMB_G(EPI_RES);
+    }
+#undef SYMB_G
+    return -1;
+  }
   switch (epi) {
     case EPI_BIAS:
       return launch_cfg<128, 128, 2, 2, EPI_BIAS>(a, lda, w, ldw, bias, r, ldr, gamma, beta, eps,

@@ -67,12 +67,17 @@ def test_add_ln(H):
     _close(add_ln(x, None, g, b, 1e-5), R.add_ln_ref(x, None, g, b, 1e-5), 3e-2, 1e-2, "ln")
 
 
+@pytest.mark.parametrize("tile", [0, 1])
 @pytest.mark.parametrize("M,N,K,epi", [
     (300, 1152, 384, 0), (129, 1536, 384, 1), (517, 384, 384, 2), (517, 384, 384, 3),
     (300, 384, 1536, 3), (64, 768, 768, 2), (1000, 2304, 768, 0), (77, 1024, 4096, 2),
+    (4099, 1536, 384, 1), (700, 384, 1536, 3),
 ])
-def test_gemm(M, N, K, epi):
+def test_gemm(M, N, K, epi, tile):
+    from codename_symbiont_amd.ops._ext import hip
     from codename_symbiont_amd.ops.kernels import gemm
+
+    hip().gemm_config(64 if tile else 128, tile)   # tile=1: 256x128 3-stage / 64-row RES_LN
 
     a = _bf(M, K, seed=1)
     w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=2)
@@ -80,7 +85,10 @@ def test_gemm(M, N, K, epi):
     res = _bf(M, N, seed=4) if epi in (2, 3) else None
     g = _f(N, scale=0.1, offset=1.0, seed=5) if epi == 3 else None
     b = _f(N, scale=0.1, seed=6) if epi == 3 else None
-    out = gemm(a, w, bias, epi, res, g, b, 1e-12)
+    try:
+        out = gemm(a, w, bias, epi, res, g, b, 1e-12)
+    finally:
+        hip().gemm_config(128, 0)
     ref = R.gemm_ref(a, w, bias, epi, res, g, b, 1e-12)
     _close(out, ref, atol=4e-2, rtol=2e-2, what=f"gemm epi={epi}")
 
