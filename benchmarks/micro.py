@@ -241,6 +241,22 @@ def cmd_encoder(a):
                       "TFLOPs": round(fl / (m / 1e3) / 1e12)}))
 
 
+def cmd_latency(a):
+    """Small-batch (query path) encoder latency: eager launches vs the captured hipGraph."""
+    from codename_symbiont_amd.models import get_config
+    from codename_symbiont_amd.models.encoder import HipEncoder, synthetic_batch
+
+    cfg = get_config(a.model)
+    enc = HipEncoder(cfg, seed=0)
+    out = {}
+    for B, S in ((1, 16), (1, 64), (8, 32), (32, 48)):
+        b = synthetic_batch(cfg, B, S, seed=1).to("cuda")
+        r = ab({"eager": lambda: enc.forward_packed(b), "graph": lambda: enc.forward_graphed(b)},
+               rounds=a.rounds, iters=50)
+        out[f"B{B}xS{S}"] = {k: round(m * 1e3, 1) for k, (m, _) in r.items()}
+    print(json.dumps({"bench": "encoder_latency_us", "model": a.model, "results": out}))
+
+
 def cmd_attn(a):
     from codename_symbiont_amd.ops import kernels as K
 
@@ -256,7 +272,7 @@ def cmd_attn(a):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("cmd", choices=["scan", "scanabl", "scanstamp", "scanfp8", "gemm", "encoder", "attn"])
+    ap.add_argument("cmd", choices=["scan", "scanabl", "scanstamp", "scanfp8", "gemm", "encoder", "attn", "latency"])
     ap.add_argument("--rows", type=int, default=100_000_000)
     ap.add_argument("--dim", type=int, default=384)
     ap.add_argument("--nq", type=int, default=256)
@@ -268,7 +284,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=5)
     a = ap.parse_args()
-    {"scan": cmd_scan, "scanabl": cmd_scanabl, "scanstamp": cmd_scanstamp, "scanfp8": cmd_scanfp8, "gemm": cmd_gemm, "encoder": cmd_encoder, "attn": cmd_attn}[a.cmd](a)
+    {"scan": cmd_scan, "scanabl": cmd_scanabl, "scanstamp": cmd_scanstamp, "scanfp8": cmd_scanfp8, "gemm": cmd_gemm, "encoder": cmd_encoder, "attn": cmd_attn, "latency": cmd_latency}[a.cmd](a)
 
 
 if __name__ == "__main__":

@@ -152,6 +152,81 @@ class HipEncoder:
         b = pack_token_ids(token_lists, self.cfg).to(self.device)
         return self.forward_packed(b)[0]
 
+    # ---------------------------------------------------------------- HIP graphs (small batches)
+    # A B=1..32 query-embedding forward is ~6 launches per layer of microsecond kernels, i.e.
+    # launch-bound.  Each (token bucket, sequence bucket) is captured once into a hipGraph over
+    # static buffers; a batch is copied in, padded with one trailing dummy sequence that owns the
+    # spare tokens (its pooled row is dropped; zero-length fillers for the spare sequence slots),
+    # and the graph replays.
+    GRAPH_MAX_TOKENS = 2048
+    GRAPH_MAX_SEQS = 32
+    use_graphs = True
+
+    def forward_auto(self, b: PackedBatch):
+        """forward_packed, through a captured graph when the batch is small enough."""
+        if (not self.use_graphs or b.num_tokens == 0 or b.num_tokens > self.GRAPH_MAX_TOKENS
+                or b.num_seqs > self.GRAPH_MAX_SEQS):
+            return self.forward_packed(b)
+        return self.forward_graphed(b)
+
+    @staticmethod
+    def _bucket(x: int, lo: int) -> int:
+        v = lo
+        while v < x:
+            v *= 2
+        return v
+
+    def forward_graphed(self, b: PackedBatch):
+        T, B = b.num_tokens, b.num_seqs
+        Tb = self._bucket(T + 1, 64)        # +1: the dummy sequence always owns >= 1 token
+        Bb = self._bucket(B, 1)
+        g = self._graph(Tb, Bb)
+        # real tokens first; rows [T, Tb) keep whatever valid ids/positions they last held and
+        # form the dummy sequence (cu[Bb + 1] == Tb is fixed at capture)
+        g["ids"][:T].copy_(b.ids, non_blocking=True)
+        g["pos"][:T].copy_(b.pos, non_blocking=True)
+        g["cu"][:B + 1].copy_(b.cu_seqlens, non_blocking=True)
+        g["cu"][B + 1:Bb + 1].fill_(T)      # zero-length fillers, then the dummy [T, Tb)
+        g["graph"].replay()
+        return g["f32"][:B], g["unit"][:B]
+
+    def _graph(self, Tb: int, Bb: int):
+        if not hasattr(self, "_graphs"):
+            self._graphs = {}
+        key = (Tb, Bb)
+        if key in self._graphs:
+            return self._graphs[key]
+        cfg, dev, H = self.cfg, self.device, self.cfg.hidden
+        ids = torch.full((Tb,), cfg.pad_token_id, dtype=torch.int32, device=dev)
+        pos = (torch.arange(Tb, dtype=torch.int32, device=dev) % 64) + cfg.position_offset
+        cu = torch.zeros(Bb + 2, dtype=torch.int32, device=dev)
+        cu[-1] = Tb
+        mk = lambda n: torch.empty(Tb, n, dtype=torch.bfloat16, device=dev)  # noqa: E731
+        ws = [mk(H), mk(H), mk(3 * H), mk(H), mk(cfg.ffn), mk(H)]
+        f32 = torch.empty(Bb + 1, H, dtype=torch.float32, device=dev)
+        unit = torch.empty(Bb + 1, H, dtype=torch.bfloat16, device=dev)
+        max_len = min(Tb, cfg.max_position - cfg.position_offset)
+
+        def launch():
+            self.rt.forward(ids.data_ptr(), pos.data_ptr(), 0, cu.data_ptr(), Tb, Bb + 1, max_len,
+                            [t.data_ptr() for t in ws], 0 if cfg.pooling == "mean" else 1,
+                            1 if cfg.normalize else 0, f32.data_ptr(), unit.data_ptr(),
+                            torch.cuda.current_stream(dev).cuda_stream)
+
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            launch()                        # warm-up (kernel attributes, code objects)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            launch()
+        g = dict(graph=graph, ids=ids, pos=pos, cu=cu, ws=ws, f32=f32, unit=unit)
+        if len(self._graphs) >= 24:
+            self._graphs.clear()
+        self._graphs[key] = g
+        return g
+
 
 class TorchEncoder:
     """fp32 PyTorch execution of the same network (CPU backend / numerics oracle)."""

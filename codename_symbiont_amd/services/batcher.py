@@ -150,7 +150,8 @@ class EmbedBatcher:
             for t in d:
                 t.record_stream(compute)
             pb = PackedBatch(d[0], d[1], None, d[2], int(lens[s:e].max()))
-            pooled, _unit = self.encoder.forward_packed(pb)
+            fwd = getattr(self.encoder, "forward_auto", self.encoder.forward_packed)
+            pooled, _unit = fwd(pb)   # small groups replay a captured hipGraph
             out[s:e].copy_(pooled.float(), non_blocking=True)
             keep.append((host, pooled))
             s = e

@@ -12,8 +12,10 @@
 // Parsing: a tolerant tokenizer + open-element stack with the HTML auto-closing rules that
 // matter for these selectors (p closed by block starts, li by li, void elements, raw-text
 // script/style/textarea/title, comments, doctype, character references).
+#ifndef SYMB_NO_PYTHON
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
+#endif
 
 #include <algorithm>
 #include <cctype>
@@ -23,7 +25,9 @@
 #include <unordered_set>
 #include <vector>
 
+#ifndef SYMB_NO_PYTHON
 namespace py = pybind11;
+#endif
 
 namespace symbn {
 
@@ -48,7 +52,7 @@ static void put_utf8(std::string& s, uint32_t cp) {
   }
 }
 
-static std::string decode_entities(const std::string& s) {
+std::string decode_entities(const std::string& s) {
   static const std::unordered_map<std::string, uint32_t> named = {
       {"amp", '&'}, {"lt", '<'}, {"gt", '>'}, {"quot", '"'}, {"apos", '\''}, {"nbsp", 0xA0},
       {"copy", 0xA9}, {"reg", 0xAE}, {"trade", 0x2122}, {"hellip", 0x2026}, {"mdash", 0x2014},
@@ -335,7 +339,8 @@ static std::string trim_ws(const std::string& s) {
   return s.substr(b, e - b);
 }
 
-py::tuple extract_text(const std::string& html) {
+// -> (text, container selector); pure C++ core (the sanitizer self-test links it directly)
+std::pair<std::string, std::string> extract_text_core(const std::string& html) {
   Document doc(html);
   struct Sel { const char* tag; const char* cls; const char* attr; const char* val; const char* name; };
   static const Sel containers[] = {
@@ -392,13 +397,17 @@ py::tuple extract_text(const std::string& html) {
     if (e == joined.size()) break;
     pos = e + 1;
   }
-  return py::make_tuple(out, used);
+  return {out, used};
 }
 
+#ifndef SYMB_NO_PYTHON
 void register_html(py::module_& m) {
-  m.def("html_extract_text", &extract_text,
-        "Reference-compatible main-content text extraction -> (text, container selector)");
+  m.def("html_extract_text", [](const std::string& html) {
+    auto r = extract_text_core(html);
+    return py::make_tuple(r.first, r.second);
+  }, "Reference-compatible main-content text extraction -> (text, container selector)");
   m.def("html_decode_entities", &decode_entities);
 }
+#endif
 
 }  // namespace symbn

@@ -9,9 +9,11 @@
 //  * WordPiece -- BERT BasicTokenizer (clean, CJK split, lowercase + accent strip, punctuation
 //    split) + greedy longest-match-first WordPiece with "##" continuations, replacing the HF
 //    `tokenizers` crate used by embedding_generator.rs:161-164.
+#ifndef SYMB_NO_PYTHON
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
+#endif
 
 #include <algorithm>
 #include <limits>
@@ -21,7 +23,9 @@
 #include <unordered_map>
 #include <vector>
 
+#ifndef SYMB_NO_PYTHON
 namespace py = pybind11;
+#endif
 
 namespace symbn {
 
@@ -312,6 +316,7 @@ static uint32_t to_lower(uint32_t c) {
   return c;
 }
 
+#ifndef SYMB_NO_PYTHON
 // Pack per-sequence id lists into (ids int32[T], cu_seqlens int32[B+1]) numpy arrays.
 static py::tuple pack_varlen(const std::vector<std::vector<int>>& all) {
   size_t T = 0;
@@ -328,6 +333,7 @@ static py::tuple pack_varlen(const std::vector<std::vector<int>>& all) {
   }
   return py::make_tuple(ids, cu);
 }
+#endif
 
 class WordPiece {
  public:
@@ -420,6 +426,7 @@ class WordPiece {
   }
 
   // Batch encode straight into a packed varlen layout: (ids int32[T], cu_seqlens int32[B+1]).
+#ifndef SYMB_NO_PYTHON
   py::tuple encode_packed(const std::vector<std::string>& texts, int max_len) const {
     std::vector<std::vector<int>> all;
     all.reserve(texts.size());
@@ -429,6 +436,7 @@ class WordPiece {
     }
     return pack_varlen(all);
   }
+#endif
 
   std::vector<std::string> tokenize(const std::string& text) const {
     std::vector<int> ids;
@@ -557,6 +565,7 @@ class Unigram {
     return ids;
   }
 
+#ifndef SYMB_NO_PYTHON
   py::tuple encode_packed(const std::vector<std::string>& texts, int max_len) const {
     std::vector<std::vector<int>> all;
     all.reserve(texts.size());
@@ -566,6 +575,7 @@ class Unigram {
     }
     return pack_varlen(all);
   }
+#endif
 
   std::vector<std::string> tokenize(const std::string& text) const {
     std::vector<int> ids = encode(text, 0, false);
@@ -590,6 +600,7 @@ class Unigram {
   double unk_score_ = -10.0;
 };
 
+#ifndef SYMB_NO_PYTHON
 void register_text(py::module_& m) {
   m.def("normalize_whitespace", &normalize_whitespace);
   m.def("split_sentences", &split_sentences);
@@ -627,5 +638,7 @@ void register_text(py::module_& m) {
       .def_property_readonly("cls_id", &WordPiece::cls_id)
       .def_property_readonly("sep_id", &WordPiece::sep_id);
 }
+
+#endif
 
 }  // namespace symbn

@@ -263,3 +263,23 @@ def test_index_scan_fp8_seeded_matches_unseeded():
     torch.cuda.synchronize()
     assert torch.equal(r0, r1) and torch.equal(s0, s1)
     assert torch.equal(r0, r2) and torch.equal(s0, s2)
+
+
+@pytest.mark.gpu
+def test_encoder_graph_replay_matches_eager():
+    """hipGraph path (bucketed, dummy-padded) == eager forward, across buckets and re-use."""
+    from codename_symbiont_amd.models import get_config
+    from codename_symbiont_amd.models.encoder import HipEncoder, synthetic_batch
+
+    cfg = get_config("minilm-l6")
+    enc = HipEncoder(cfg, seed=4)
+    for B, S, seed in [(1, 9, 0), (3, 40, 1), (1, 200, 2), (8, 30, 3), (3, 17, 4), (32, 50, 5)]:
+        b = synthetic_batch(cfg, B, S, seed=seed, varlen=True).to(DEV)
+        e32, eu = enc.forward_packed(b)
+        e32, eu = e32.clone(), eu.clone()
+        g32, gu = enc.forward_graphed(b)
+        torch.cuda.synchronize()
+        assert g32.shape == e32.shape
+        _close(g32, e32, atol=1e-5, what=f"graph f32 B={B} S={S}")
+        assert torch.equal(gu, eu)
+    assert len(enc._graphs) >= 4
