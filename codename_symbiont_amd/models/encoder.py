@@ -158,9 +158,13 @@ class HipEncoder:
     # static buffers; a batch is copied in, padded with one trailing dummy sequence that owns the
     # spare tokens (its pooled row is dropped; zero-length fillers for the spare sequence slots),
     # and the graph replays.
+    # Measured (profiles/r1_gemm/latency.log, MiniLM-L6): eager 386 / 458 / 575 / 593 us vs graph
+    # 475 / 577 / 656 / 766 us at B x S = 1x16, 1x64, 8x32, 32x48 -- these forwards are bound by
+    # the small-M GEMMs' k-loop latency on the GPU, not by launches, and the bucket padding adds
+    # work, so replay is opt-in (set use_graphs = True) until a small-M GEMM path exists.
     GRAPH_MAX_TOKENS = 2048
     GRAPH_MAX_SEQS = 32
-    use_graphs = True
+    use_graphs = False
 
     def forward_auto(self, b: PackedBatch):
         """forward_packed, through a captured graph when the batch is small enough."""
