@@ -113,6 +113,20 @@ class HbmIndexShard:
         self.payloads.extend_empty(n)
         return r0
 
+    def truncate(self, n: int) -> None:
+        """Forget rows >= n (their payload slots too)."""
+        if n >= self.count:
+            return
+        ps = self.payloads
+        for r in range(n, self.count):
+            pid = ps.point_ids[r]
+            if pid is not None and ps.id_to_row.get(pid) == r:
+                del ps.id_to_row[pid]
+        del ps.point_ids[n:]
+        for f in ps.FIELDS:
+            del ps.cols[f][n:]
+        self.count = n
+
     def append_unit(self, unit_bf16: torch.Tensor) -> int:
         """Append already unit-norm bf16 rows (e.g. the encoder's pooled+normalised output)."""
         n = unit_bf16.shape[0]

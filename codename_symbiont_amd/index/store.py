@@ -42,8 +42,8 @@ class VectorStore:
         self.wal = None
         if snapshot_dir:
             os.makedirs(snapshot_dir, exist_ok=True)
-            # a group re-distributes the WAL over its ranks; single shards also have snapshots
-            n = load_snapshot(self.shard, snapshot_dir) if group is None else 0
+            # a group restores every rank's shard collectively, then re-applies the WAL over it
+            n = load_snapshot(self.shard, snapshot_dir) if group is None else group.load(snapshot_dir)
             m = 0
             Wal.repair(os.path.join(snapshot_dir, "wal.log"))
             for ids, pls, vecs in Wal.replay(os.path.join(snapshot_dir, "wal.log"), dim):
@@ -78,9 +78,12 @@ class VectorStore:
                 self.snapshot()
 
     def snapshot(self) -> None:
-        if not self.dir or self.group is not None:  # group mode: WAL-only durability
+        if not self.dir:
             return
-        save_snapshot(self.shard, self.dir)
+        if self.group is not None:
+            self.group.snapshot(self.dir)
+        else:
+            save_snapshot(self.shard, self.dir)
         if self.wal is not None:
             self.wal.truncate()
         self._since_snapshot = 0

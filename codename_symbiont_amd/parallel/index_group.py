@@ -7,6 +7,9 @@ a short, fixed sequence of collectives, so all ranks stay in lockstep:
   SEARCH : header -> broadcast queries [nq, D] -> every rank: fused MFMA scan of ITS shard ->
            all_gather of the per-rank top-k (f32 scores, i64 global ids) -> rank 0 merges.
   UPSERT : header -> broadcast vectors [n, D] f32 + (owner rank, target row) -> owners write rows.
+  SNAPSHOT / LOAD : header -> every rank saves / loads its own shard under <dir>/rank<r>/ (raw rows,
+           index/persist.py format); rank 0 adds group.json (world, per-rank counts) and the
+           gid -> (point id, payload) table.  A load requires the same world size.
   STOP   : header only.
 Owner assignment is least-loaded-first, so shards stay balanced (the reference's Qdrant has a
 single shard: vector_memory_service/src/main.rs:50).  Global id = rank << 40 | row.
@@ -14,7 +17,9 @@ Payloads (and the point-id -> gid map) live on rank 0 only; other ranks hold vec
 """
 from __future__ import annotations
 
+import json
 import logging
+import os
 import threading
 
 import numpy as np
@@ -27,7 +32,7 @@ from .sharded import RANK_SHIFT, encode_gid, merge_ranked
 
 log = logging.getLogger("symbiont.index_group")
 
-OP_STOP, OP_SEARCH, OP_UPSERT = 0, 1, 2
+OP_STOP, OP_SEARCH, OP_UPSERT, OP_SNAPSHOT, OP_LOAD = 0, 1, 2, 3, 4
 
 
 class IndexGroup:
@@ -45,6 +50,7 @@ class IndexGroup:
         self.counts = [0] * info.world
         self.payload_by_gid: dict[int, tuple[str, Payload]] = {}
         self.gid_by_pid: dict[str, int] = {}
+        self.snapshot_root: str | None = None   # shared snapshot directory (all ranks)
 
     # ------------------------------------------------------------------ plumbing
     def _bcast(self, t: torch.Tensor) -> torch.Tensor:
@@ -88,7 +94,80 @@ class IndexGroup:
             if t >= 0:
                 self.shard.write_f32(int(t), v[i:i + 1])
 
+    def _rank_dir(self, directory: str) -> str:
+        return os.path.join(directory, f"rank{self.info.rank}")
+
+    def _do_snapshot(self, directory: str) -> None:
+        from ..index.persist import save_snapshot
+
+        d = self._rank_dir(directory)
+        os.makedirs(d, exist_ok=True)
+        save_snapshot(self.shard, d)
+        if self.info.world > 1:
+            dist.barrier(group=self.group)   # every shard durable before rank 0 commits group.json
+
+    def _do_load(self, directory: str, counts: torch.Tensor) -> int:
+        """Load this rank's shard, cut to the row count group.json committed: a crash between
+        the per-rank saves and the group.json commit leaves newer rank snapshots whose extra rows
+        the WAL (truncated only after the commit) re-applies."""
+        from ..index.persist import load_snapshot
+
+        load_snapshot(self.shard, self._rank_dir(directory))
+        self.shard.truncate(min(self.shard.count, int(counts[self.info.rank])))
+        if self.info.world > 1:
+            dist.barrier(group=self.group)
+        return self.shard.count
+
     # ------------------------------------------------------------------ rank-0 API
+    def snapshot(self, directory: str) -> None:
+        """Collective checkpoint of every shard + rank 0's payload table (atomic group.json)."""
+        assert self.info.is_root
+        with self._op_lock:
+            self._header(OP_SNAPSHOT)
+            self._do_snapshot(directory)
+            tmp = os.path.join(directory, "group_payloads.jsonl.tmp")
+            with open(tmp, "w", encoding="utf-8") as f:
+                for g, (pid, p) in self.payload_by_gid.items():
+                    f.write(json.dumps([g, pid, p.original_document_id, p.source_url, p.sentence_text,
+                                        p.sentence_order, p.model_name, p.processed_at_ms],
+                                       ensure_ascii=False) + "\n")
+            os.replace(tmp, os.path.join(directory, "group_payloads.jsonl"))
+            meta = {"world": self.info.world, "counts": self.counts, "dim": self.dim, "format": 1}
+            tmp = os.path.join(directory, "group.json.tmp")
+            with open(tmp, "w") as f:
+                json.dump(meta, f)
+                f.flush()
+                os.fsync(f.fileno())
+            os.replace(tmp, os.path.join(directory, "group.json"))
+
+    def load(self, directory: str) -> int:
+        """Collective restore written by ``snapshot``; returns the number of points (0 if none)."""
+        assert self.info.is_root
+        meta_p = os.path.join(directory, "group.json")
+        if not os.path.exists(meta_p):
+            return 0
+        with open(meta_p) as f:
+            meta = json.load(f)
+        if meta["world"] != self.info.world or meta["dim"] != self.dim:
+            raise ValueError(f"group snapshot is for world={meta['world']} dim={meta['dim']}, "
+                             f"this group is world={self.info.world} dim={self.dim}")
+        with self._op_lock:
+            self._header(OP_LOAD)
+            c = self._bcast(torch.tensor(meta["counts"], dtype=torch.int64, device=self.comm_device))
+            self._do_load(directory, c)
+        self.counts = list(meta["counts"])
+        self.payload_by_gid.clear()
+        self.gid_by_pid.clear()
+        with open(os.path.join(directory, "group_payloads.jsonl"), encoding="utf-8") as f:
+            for line in f:
+                a = json.loads(line)
+                self.payload_by_gid[a[0]] = (a[1], Payload(*a[2:]))
+                self.gid_by_pid[a[1]] = a[0]
+        return sum(self.counts)
+
+    def snapshot_dir_exists(self, directory: str) -> bool:
+        return os.path.exists(os.path.join(directory, "group.json"))
+
     def search(self, q_unit: torch.Tensor, k: int):
         assert self.info.is_root
         nq = q_unit.shape[0]
@@ -151,5 +230,14 @@ class IndexGroup:
                 v = self._bcast(torch.empty(a, self.dim, dtype=torch.float32, device=self.comm_device))
                 ot = self._bcast(torch.empty(2, a, dtype=torch.int64, device=self.comm_device))
                 self._do_upsert(v, ot[0], ot[1])
+            elif op in (OP_SNAPSHOT, OP_LOAD):
+                if self.snapshot_root is None:
+                    raise RuntimeError("index rank has no snapshot directory (SYMB_SNAPSHOT_DIR)")
+                if op == OP_SNAPSHOT:
+                    self._do_snapshot(self.snapshot_root)
+                else:
+                    c = self._bcast(torch.empty(self.info.world, dtype=torch.int64,
+                                                device=self.comm_device))
+                    self._do_load(self.snapshot_root, c)
             else:
                 raise RuntimeError(f"unknown index op {op}")

@@ -155,6 +155,7 @@ def main() -> None:
     info = D.init()
     dim = cfg.index_dim or get_config(cfg.model).hidden
     group = IndexGroup(info, dim, cfg.index_capacity // info.world + 1, dtype=cfg.index_dtype)
+    group.snapshot_root = cfg.snapshot_dir or None
     try:
         if info.is_root:
             store = VectorStore(dim, 0, snapshot_dir=cfg.snapshot_dir, group=group)

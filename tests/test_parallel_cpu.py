@@ -99,3 +99,52 @@ def test_index_group_upsert_search_overwrite():
     assert got == ref
     assert count == 300 and text == "t5-new"
     assert out[1] == 100 and out[2] == 100          # least-loaded placement balances the shards
+
+
+def _group_snapshot_worker(rank, world, port, snap, phase, out):
+    """phase 0: ingest, snapshot, ingest more (WAL only), crash.  phase 1: restore + search."""
+    from codename_symbiont_amd.index.shard import Payload
+    from codename_symbiont_amd.index.store import VectorStore
+    from codename_symbiont_amd.parallel import dist as D
+    from codename_symbiont_amd.parallel.index_group import IndexGroup
+    info = _init(rank, world, port)
+    grp = IndexGroup(info, dim=16, capacity_per_rank=500)
+    grp.snapshot_root = snap
+    rng = np.random.default_rng(7)
+    vecs = rng.standard_normal((200, 16)).astype(np.float32)
+    if rank != 0:
+        grp.serve()
+        out[(phase, rank)] = grp.shard.count
+    else:
+        store = VectorStore(16, 0, snapshot_dir=snap, snapshot_every=10**9, group=grp)
+        if phase == 0:
+            ids = [f"p{i}" for i in range(200)]
+            pls = [Payload(f"d{i}", "u", f"t{i}", i) for i in range(200)]
+            store.upsert(ids[:150], vecs[:150], pls[:150])
+            store.snapshot()                                   # collective checkpoint
+            store.upsert(ids[150:], vecs[150:], pls[150:])     # only in the WAL
+            store.upsert(["p3"], -vecs[3:4], [Payload("d3", "u", "t3-new", 3)])
+            out[(0, 0)] = store.count
+            store.wal.close()                                  # crash: no final snapshot
+        else:
+            out[(1, 0)] = store.count
+            q = np.concatenate([vecs[[10, 170]], -vecs[3:4]])
+            _, gids = store.search(q, 1)
+            out["texts"] = [store.lookup(int(g[0]))[1].sentence_text for g in gids]
+        grp.stop()
+    D.shutdown(info)
+
+
+def test_index_group_snapshot_restore(tmp_path):
+    world = 2
+    snap = str(tmp_path / "snap")
+    mgr = mp.Manager()
+    out = mgr.dict()
+    for phase in (0, 1):
+        mp.start_processes(_group_snapshot_worker, args=(world, _free_port(), snap, phase, out),
+                           nprocs=world, join=True, start_method="spawn")
+    assert os.path.exists(os.path.join(snap, "group.json"))
+    assert os.path.exists(os.path.join(snap, "rank1", "snapshot", "vectors.npy"))
+    assert out[(0, 0)] == 200 and out[(1, 0)] == 200      # 150 from the snapshot + 50 from the WAL
+    assert out[(1, 1)] == 100                             # rank 1's shard restored, then WAL rows
+    assert out["texts"] == ["t10", "t170", "t3-new"]
