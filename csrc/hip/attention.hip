@@ -6,142 +6,147 @@
 // K6-K11).  Sequences are packed back to back ([T, 3H] fused QKV rows, cu_seqlens offsets), so
 // no FLOP or byte is spent on padding and no mask tensor exists.
 //
-// Per workgroup: 64 query rows of one (sequence, head); 4 waves x 16 rows.
-//   S = Q K^T   : v_mfma_f32_16x16x32_bf16, Q fragments in registers, K tile row-major in LDS
-//   softmax     : online (running max / sum in fp32, exp2 with log2(e) folded into the scale)
-//   O += P V    : P goes through a wave-private LDS slab to become the A operand; V is stored
-//                 transposed in LDS so every B fragment is one ds_read_b128.
+// Per workgroup: 64 query rows of one (sequence, head); 4 waves x 16 queries.  gfx950 layout:
+//  * S^T = K Q^T (v_mfma_f32_16x16x32_bf16, K = A operand from LDS, Q = B operand in registers):
+//    a lane's accumulators are 4 keys x ONE query, so the softmax row statistics are lane-local
+//    up to a 4-lane (shfl 16/32) reduction, and the probabilities feed the PV MFMA straight from
+//    registers: P^T tiles n = 2t, 2t+1 (keys 4g+r and 16+4g+r of a 32-key step) ARE the B operand
+//    of O^T = V^T P^T under a fixed permutation of the k index -- no LDS round trip for P.
+//  * V stays row-major in LDS (16-byte staging writes) and the matching V^T A fragments come from
+//    two ds_read_b64_tr_b16 (4 keys x 16 head dims each, hardware transpose).
+//  * Bank conflicts: K rows XOR-swizzle their 16-byte chunk with (row >> 1); V rows are padded to
+//    D*2 + 32 bytes.  Both layouts are conflict-free for their reads (checked with the LDS lane-
+//    group rules, then SQ_LDS_BANK_CONFLICT).
+//  * Output O^T: a lane holds 4 consecutive head dims of one query -> 8-byte stores.
 #include "common.h"
 
 namespace symb {
 
-template <int D>
+template <int D, int KVT>
 __global__ __launch_bounds__(256) void attn_varlen_kernel(const __bf16* __restrict__ qkv,
                                                           int ld_qkv, const int32_t* __restrict__ cu,
                                                           int H, float scale_log2,
                                                           __bf16* __restrict__ out, int ld_out) {
-  constexpr int KVT = 64;          // keys per tile
-  constexpr int KP = D + 8;        // padded K row (elements)
-  constexpr int VP = KVT + 8;      // padded V^T row
-  constexpr int PP = KVT + 8;      // padded P row
-  constexpr int NKS = D / 32;      // k-steps of the QK^T product
-  constexpr int ND = D / 16;       // 16-wide output column tiles
-  __shared__ __attribute__((aligned(16))) __bf16 sm[KVT * KP + D * VP + 4 * 16 * PP];
+  static_assert(KVT % 32 == 0, "keys per tile");   // 128: a <=128-token sentence in ONE stage
+  constexpr int NT = KVT / 16;            // 16-key accumulator tiles
+  constexpr int CK = D / 8;               // 16-byte chunks per K/V row
+  constexpr int KRB = D * 2;              // K row bytes (unpadded, swizzled)
+  constexpr int VRB = D * 2 + 32;         // V row bytes (padded)
+  constexpr int NKS = D / 32;             // k-steps of the QK^T product
+  constexpr int ND = D / 16;              // 16-dim output tiles
+  typedef short s16x4 __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) char sm[KVT * KRB + KVT * VRB];
+  char* Ks = sm;
+  char* Vs = sm + KVT * KRB;
 
   const int b = blockIdx.z, h = blockIdx.y;
   const int s0 = cu[b], L = cu[b + 1] - s0;
   const int q0 = blockIdx.x * 64;
-  if (q0 >= L) return;
+  if (q0 >= L) return;                    // block-uniform: EXEC stays full for the tr reads
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  __bf16* Ks = sm;
-  __bf16* Vt = sm + KVT * KP;
-  __bf16* Ps = Vt + D * VP + wave * 16 * PP;
+  const int c16 = lane & 15, g = lane >> 4;
 
-  const int qrow = min(q0 + wave * 16 + (lane & 15), L - 1);
+  const int qrow = min(q0 + wave * 16 + c16, L - 1);
   const __bf16* qp = qkv + (size_t)(s0 + qrow) * ld_qkv + h * D;
   bf16x8 qf[NKS];
 #pragma unroll
-  for (int ks = 0; ks < NKS; ++ks)
-    qf[ks] = *reinterpret_cast<const bf16x8*>(qp + ks * 32 + (lane >> 4) * 8);
+  for (int ks = 0; ks < NKS; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qp + ks * 32 + g * 8);
+
+  // per-lane constant LDS offsets
+  uint32_t koff[NT][NKS];                 // A fragment of key tile n, k-step ks
+#pragma unroll
+  for (int n = 0; n < NT; ++n)
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const int r = n * 16 + c16, c = ks * 4 + g;
+      koff[n][ks] = (uint32_t)(r * KRB + ((c ^ ((r >> 1) & (CK - 1))) << 4));
+    }
+  // tr read: lane 4q+p of its 16-lane group gives row (4g + q), columns 4p..4p+3 of a 16-dim tile
+  const uint32_t vbase = (uint32_t)((4 * g + (c16 >> 2)) * VRB + (c16 & 3) * 8);
+  const uint32_t lds_k = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)Ks);
+  const uint32_t lds_v = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)Vs);
 
   f32x4 o[ND];
 #pragma unroll
   for (int d = 0; d < ND; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m[4], l[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    m[r] = -INFINITY;
-    l[r] = 0.f;
-  }
+  float m = -INFINITY, lsum = 0.f;        // running max / per-lane partial sum of this query
 
   for (int kv0 = 0; kv0 < L; kv0 += KVT) {
     __syncthreads();
-    for (int c = tid; c < KVT * (D / 8); c += 256) {
-      const int r = c / (D / 8), ch = c % (D / 8);
+    for (int c = tid; c < KVT * CK; c += 256) {
+      const int r = c / CK, ch = c % CK;
       const int kr = min(kv0 + r, L - 1);
       const __bf16* src = qkv + (size_t)(s0 + kr) * ld_qkv + h * D + ch * 8;
-      *reinterpret_cast<bf16x8*>(Ks + r * KP + ch * 8) =
+      *reinterpret_cast<bf16x8*>(Ks + r * KRB + ((ch ^ ((r >> 1) & (CK - 1))) << 4)) =
           *reinterpret_cast<const bf16x8*>(src + H);
-      const bf16x8 vv = *reinterpret_cast<const bf16x8*>(src + 2 * H);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) Vt[(ch * 8 + e) * VP + r] = vv[e];
+      *reinterpret_cast<bf16x8*>(Vs + r * VRB + ch * 16) =
+          *reinterpret_cast<const bf16x8*>(src + 2 * H);
     }
     __syncthreads();
 
-    f32x4 s[4];
+    f32x4 s[NT];
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
+    for (int n = 0; n < NT; ++n) {
       s[n] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
-        const bf16x8 kb = *reinterpret_cast<const bf16x8*>(Ks + (n * 16 + (lane & 15)) * KP +
-                                                           ks * 32 + (lane >> 4) * 8);
-        s[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[ks], kb, s[n], 0, 0, 0);
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + koff[n][ks]);
+        s[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], s[n], 0, 0, 0);
       }
     }
-    // scale + key mask (keys past the sequence end contribute exp2(-inf) = 0)
-    float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    // scale + key mask; s[n][r] is key kv0 + 16n + 4g + r of this lane's query
+    float mx = -INFINITY;
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      const bool valid = (kv0 + n * 16 + (lane & 15)) < L;
+    for (int n = 0; n < NT; ++n)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float v = valid ? s[n][r] * scale_log2 : -INFINITY;
+        const float v = (kv0 + n * 16 + 4 * g + r) < L ? s[n][r] * scale_log2 : -INFINITY;
         s[n][r] = v;
-        mx[r] = fmaxf(mx[r], v);
+        mx = fmaxf(mx, v);
       }
-    }
-    float alpha[4], rs[4];
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float alpha = exp2f(m - mn);
+    m = mn;
+    lsum *= alpha;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int d = 0; d < ND; ++d) o[d] *= alpha;
+    bf16x8 pb[NT / 2];
 #pragma unroll
-      for (int msk = 1; msk < 16; msk <<= 1) mx[r] = fmaxf(mx[r], __shfl_xor(mx[r], msk, 64));
-      const float mn = fmaxf(m[r], mx[r]);
-      alpha[r] = exp2f(m[r] - mn);
-      m[r] = mn;
-      rs[r] = 0.f;
-    }
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
+    for (int n = 0; n < NT; ++n)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = exp2f(s[n][r] - m[r]);
-        rs[r] += p;
-        Ps[((lane >> 4) * 4 + r) * PP + n * 16 + (lane & 15)] = (__bf16)p;
+        const float p = exp2f(s[n][r] - mn);
+        lsum += p;
+        pb[n >> 1][(n & 1) * 4 + r] = (__bf16)p;
       }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-#pragma unroll
-      for (int msk = 1; msk < 16; msk <<= 1) rs[r] += __shfl_xor(rs[r], msk, 64);
-      l[r] = l[r] * alpha[r] + rs[r];
-    }
-#pragma unroll
-    for (int d = 0; d < ND; ++d)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[d][r] *= alpha[r];
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8 pa =
-          *reinterpret_cast<const bf16x8*>(Ps + (lane & 15) * PP + ks * 32 + (lane >> 4) * 8);
+    for (int t = 0; t < NT / 2; ++t)
 #pragma unroll
       for (int d = 0; d < ND; ++d) {
-        const bf16x8 vb = *reinterpret_cast<const bf16x8*>(Vt + (d * 16 + (lane & 15)) * VP +
-                                                           ks * 32 + (lane >> 4) * 8);
-        o[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, o[d], 0, 0, 0);
+        const uint32_t a0 = lds_v + vbase + (uint32_t)(t * 32 * VRB + d * 32);
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(uintptr_t)a0);
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(uintptr_t)(a0 + 16 * VRB));
+        const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        o[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[t], o[d], 0, 0, 0);
       }
-    }
-    __builtin_amdgcn_wave_barrier();
   }
 
+  lsum += __shfl_xor(lsum, 16, 64);
+  lsum += __shfl_xor(lsum, 32, 64);
+  const int row = q0 + wave * 16 + c16;
+  if (row < L) {
+    const float inv = 1.0f / lsum;
+    __bf16* op = out + (size_t)(s0 + row) * ld_out + h * D + 4 * g;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int row = q0 + wave * 16 + (lane >> 4) * 4 + r;
-    if (row < L) {
-      const float inv = 1.0f / l[r];
-      __bf16* op = out + (size_t)(s0 + row) * ld_out + h * D + (lane & 15);
+    for (int d = 0; d < ND; ++d) {
+      bf16x4 v;
 #pragma unroll
-      for (int d = 0; d < ND; ++d) op[d * 16] = (__bf16)(o[d][r] * inv);
+      for (int r = 0; r < 4; ++r) v[r] = (__bf16)(o[d][r] * inv);
+      *reinterpret_cast<bf16x4*>(op + d * 16) = v;
     }
   }
 }
@@ -156,13 +161,17 @@ int symb_attention(const void* qkv, int ld_qkv, const int32_t* cu, int B, int ma
   const int H = n_heads * head_dim;
   const float scale_log2 = 1.4426950408889634f / sqrtf((float)head_dim);
   dim3 grid((max_len + 63) / 64, n_heads, B);
+  // 64-key tiles (a 128-key single-stage variant measured 9-12 % slower at S = 128:
+  // profiles/r1_attn/attn_kvt.log)
+#define SYMB_A(DD, KV) hipLaunchKernelGGL((attn_varlen_kernel<DD, KV>), grid, dim3(256), 0, st, \
+                                          (const __bf16*)qkv, ld_qkv, cu, H, scale_log2,      \
+                                          (__bf16*)out, ld_out)
   if (head_dim == 32)
-    hipLaunchKernelGGL(attn_varlen_kernel<32>, grid, dim3(256), 0, st, (const __bf16*)qkv, ld_qkv,
-                       cu, H, scale_log2, (__bf16*)out, ld_out);
+    SYMB_A(32, 64);
   else if (head_dim == 64)
-    hipLaunchKernelGGL(attn_varlen_kernel<64>, grid, dim3(256), 0, st, (const __bf16*)qkv, ld_qkv,
-                       cu, H, scale_log2, (__bf16*)out, ld_out);
+    SYMB_A(64, 64);
   else
     return -1;
+#undef SYMB_A
   return (int)hipGetLastError();
 }

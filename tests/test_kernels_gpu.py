@@ -94,10 +94,12 @@ def test_gemm(M, N, K, epi, tile):
 
 
 @pytest.mark.parametrize("D,nh", [(32, 12), (64, 12), (64, 16)])
-def test_attention_varlen(D, nh):
+@pytest.mark.parametrize("lens", [[1, 7, 64, 65, 128, 200, 3, 511],   # 64-key tiles
+                                  [1, 7, 64, 65, 100, 128, 3],        # <=128: one 128-key tile
+                                  [5, 33, 64]])                       # <=64
+def test_attention_varlen(D, nh, lens):
     from codename_symbiont_amd.ops.kernels import attention
 
-    lens = [1, 7, 64, 65, 128, 200, 3, 511]
     cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
     T = int(cu[-1])
     H = nh * D
