@@ -16,6 +16,8 @@ from dataclasses import dataclass, field
 import numpy as np
 import torch
 
+from ..utils.trace import stage
+
 
 @dataclass
 class _Req:
@@ -91,7 +93,8 @@ class EmbedBatcher:
         from ..models.encoder import PackedBatch
 
         cfg = self.encoder.cfg
-        ids, cu = self.tok.encode_packed(texts)
+        with stage("tokenize", self.metrics, n=len(texts)):
+            ids, cu = self.tok.encode_packed(texts)
         lens = np.diff(cu)
         outs = []
         s = 0
@@ -140,22 +143,25 @@ class EmbedBatcher:
             sub_cu = (cu[s:e + 1] - cu[s]).astype(np.int32)
             pos = np.concatenate([np.arange(cfg.position_offset, cfg.position_offset + int(L),
                                             dtype=np.int32) for L in lens[s:e]])
-            host = [torch.from_numpy(np.ascontiguousarray(x)).pin_memory()
-                    for x in (ids[a:b], pos, sub_cu)]
-            with torch.cuda.stream(copy):
-                d = [h.to(dev, non_blocking=True) for h in host]
-                ready = torch.cuda.Event()
-                ready.record(copy)
-            compute.wait_event(ready)
-            for t in d:
-                t.record_stream(compute)
+            with stage("h2d", self.metrics):
+                host = [torch.from_numpy(np.ascontiguousarray(x)).pin_memory()
+                        for x in (ids[a:b], pos, sub_cu)]
+                with torch.cuda.stream(copy):
+                    d = [h.to(dev, non_blocking=True) for h in host]
+                    ready = torch.cuda.Event()
+                    ready.record(copy)
+                compute.wait_event(ready)
+                for t in d:
+                    t.record_stream(compute)
             pb = PackedBatch(d[0], d[1], None, d[2], int(lens[s:e].max()))
             fwd = getattr(self.encoder, "forward_auto", self.encoder.forward_packed)
-            pooled, _unit = fwd(pb)   # small groups replay a captured hipGraph
+            with stage("encode_launch", self.metrics, tokens=b - a):
+                pooled, _unit = fwd(pb)   # small groups replay a captured hipGraph
             out[s:e].copy_(pooled.float(), non_blocking=True)
             keep.append((host, pooled))
             s = e
-        compute.synchronize()
+        with stage("encode_d2h_sync", self.metrics):
+            compute.synchronize()
         return out.numpy()
 
     def _copy_stream(self, dev):
@@ -190,6 +196,10 @@ class SearchBatcher:
         await self._q.put(_SReq(np.asarray(q, np.float32).reshape(1, -1), int(k), fut))
         return await fut
 
+    def _timed_search(self, qs, k):
+        with stage("index_search", self.metrics, nq=len(qs), k=k):
+            return self.search_fn(qs, k)
+
     async def _run(self) -> None:
         loop = asyncio.get_running_loop()
         while True:
@@ -207,7 +217,7 @@ class SearchBatcher:
             kmax = max(r.k for r in batch)
             qs = np.concatenate([r.q for r in batch], 0)
             try:
-                s, i = await loop.run_in_executor(None, self.search_fn, qs, kmax)
+                s, i = await loop.run_in_executor(None, self._timed_search, qs, kmax)
             except Exception as e:
                 for r in batch:
                     if not r.fut.done():

@@ -17,6 +17,7 @@ import uuid
 
 import numpy as np
 
+from ..utils.trace import stage
 from ..index.shard import Payload
 from ..index.store import VectorStore
 from ..models.config import get_config
@@ -77,7 +78,8 @@ class VectorMemoryService(Service):
             return
         loop = asyncio.get_running_loop()
         try:
-            await loop.run_in_executor(None, self.store.upsert, ids, vecs, pls)
+            with stage("upsert", self.metrics, trace_id=msg.original_id, n=len(ids)):
+                await loop.run_in_executor(None, self.store.upsert, ids, vecs, pls)
         except Exception as e:
             self.log.error("[QDRANT_HANDLER_ERROR] Failed to upsert points for original_id %s: %s",
                            msg.original_id, e)
@@ -110,7 +112,8 @@ class VectorMemoryService(Service):
             if q.shape[0] != self.store.dim:
                 raise ValueError(f"Wrong input: Vector dimension error: expected dim: {self.store.dim}, "
                                  f"got {q.shape[0]}")
-            scores, rows = await self.searcher.search(q, task.top_k)
+            with stage("search_request", self.metrics, trace_id=task.request_id, k=task.top_k):
+                scores, rows = await self.searcher.search(q, task.top_k)
         except Exception as e:
             err = f"Qdrant search failed for request_id {task.request_id}: {e}"
             self.log.error("[SEARCH_HANDLER_QDRANT_FAIL] %s", err)

@@ -87,3 +87,22 @@ def test_fp8_shard_cpu_path_and_snapshot(tmp_path):
         load_snapshot(HbmIndexShard(D, 600, device="cpu"), str(tmp_path))
     with pytest.raises(ValueError, match="multiple of 256"):
         HbmIndexShard(384, 10, device="cpu", dtype="fp8")
+
+
+def test_stage_tracing_records_metrics(caplog):
+    import logging
+
+    from codename_symbiont_amd.services.base import Metrics
+    from codename_symbiont_amd.utils import trace
+
+    m = Metrics()
+    trace._ENABLED = True
+    try:
+        with caplog.at_level(logging.INFO, logger="symbiont.trace"):
+            with trace.stage("unit", m, trace_id="req-1", n=3):
+                pass
+    finally:
+        trace._ENABLED = False
+    snap = m.snapshot()["latency_ms"]
+    assert snap["stage.unit"]["n"] == 1
+    assert any("[TRACE] stage=unit id=req-1" in r.message and "n=3" in r.message for r in caplog.records)
