@@ -60,6 +60,8 @@ def main() -> None:
     ap.add_argument("--model", default="minilm-l6")
     ap.add_argument("--mode", choices=["full", "embed", "search"], default="full")
     ap.add_argument("--index-dtype", choices=["bf16", "fp8"], default="bf16")
+    ap.add_argument("--encoder-dtype", choices=["bf16", "fp8"], default="bf16",
+                    help="fp8: e4m3 projection GEMMs (BASELINE config #5); the headline stays bf16")
     args = ap.parse_args()
 
     from codename_symbiont_amd.index.shard import HbmIndexShard
@@ -77,7 +79,7 @@ def main() -> None:
     B, S, K, W = args.batch, args.seq, args.steps, args.warmup
 
     t0 = time.time()
-    enc = HipEncoder(cfg, seed=0, device=dev)
+    enc = HipEncoder(cfg, seed=0, device=dev, precision=args.encoder_dtype)
     rows_per_rank = args.index_rows // info.world
     extra = (K + W + 4) * B
     shard = HbmIndexShard(cfg.hidden, rows_per_rank + extra, device=dev, dtype=args.index_dtype)
@@ -156,12 +158,13 @@ def main() -> None:
     ms = elapsed * 1000.0 / K
     total = B * info.world * K / elapsed
     headline = (args.model in ("minilm-l6", "minilm", "all-MiniLM-L6-v2") and args.mode == "full"
-                and args.index_rows == 100_000_000 and args.index_dtype == "bf16")
+                and args.index_rows == 100_000_000 and args.index_dtype == "bf16"
+                and args.encoder_dtype == "bf16")
     short = cfg.model_name.split("/")[-1]
     rows_txt = f"{args.index_rows / 1e6:g}M" if args.index_rows < 10**9 else f"{args.index_rows / 1e9:g}B"
     metric = METRIC if headline else {
         "full": f"embeds/sec + top-k QPS, {short} / {rows_txt}x{cfg.hidden} {args.index_dtype} index",
-        "embed": f"embeds/sec, {short} ({cfg.key}) bf16, batch {B} x seq {S}",
+        "embed": f"embeds/sec, {short} ({cfg.key}) {args.encoder_dtype}, batch {B} x seq {S}",
         "search": f"top-{args.k} QPS, {rows_txt}x{cfg.hidden} {args.index_dtype} index, {B} queries/rank",
     }[args.mode]
     if info.rank == 0:
@@ -178,7 +181,7 @@ def main() -> None:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": args.encoder_dtype,
             "index_dtype": args.index_dtype,
             "data": "synthetic token ids, random-init weights, random unit index rows",
             "config": {

@@ -228,17 +228,18 @@ def cmd_encoder(a):
     from codename_symbiont_amd.models.encoder import HipEncoder, synthetic_batch
 
     cfg = get_config(a.model)
-    enc = HipEncoder(cfg, seed=0)
     b = synthetic_batch(cfg, a.batch, a.seq, seed=0).to("cuda")
     o1 = torch.empty(a.batch, cfg.hidden, device="cuda")
     o2 = torch.empty(a.batch, cfg.hidden, device="cuda", dtype=torch.bfloat16)
-    res = ab({"forward": lambda: enc.forward_packed(b, o1, o2)}, rounds=a.rounds, iters=a.iters)
-    m = res["forward"][0]
+    encs = {p: HipEncoder(cfg, seed=0, precision=p) for p in a.precision.split(",")}
+    res = ab({p: (lambda e=e: e.forward_packed(b, o1, o2)) for p, e in encs.items()},
+             rounds=a.rounds, iters=a.iters)
     toks = a.batch * a.seq
     fl = cfg.flops_per_token(a.seq) * toks
+    out = {p: dict(ms=round(m, 3), embeds_per_s=round(a.batch / (m / 1e3)),
+                   TFLOPs=round(fl / (m / 1e3) / 1e12)) for p, (m, _) in res.items()}
     print(json.dumps({"bench": "encoder", "model": a.model, "batch": a.batch, "seq": a.seq,
-                      "ms": round(m, 3), "embeds_per_s": round(a.batch / (m / 1e3)),
-                      "TFLOPs": round(fl / (m / 1e3) / 1e12)}))
+                      "results": out}))
 
 
 def cmd_latency(a):
@@ -257,6 +258,42 @@ def cmd_latency(a):
     print(json.dumps({"bench": "encoder_latency_us", "model": a.model, "results": out}))
 
 
+def cmd_gemmfp8(a):
+    """e4m3 GEMM (row quantiser + fp8 MFMA GEMM) vs the bf16 GEMM on encoder shapes."""
+    from codename_symbiont_amd.models.encoder import quant_weight_fp8
+    from codename_symbiont_amd.ops import kernels as K
+    from codename_symbiont_amd.ops._ext import hip, stream_handle
+
+    M = a.batch * a.seq
+    shapes = [("e5.qkv", 3072, 1024, 0), ("e5.out", 1024, 1024, 2), ("e5.ffn1", 4096, 1024, 1),
+              ("e5.ffn2", 1024, 4096, 2), ("minilm.ffn1", 1536, 384, 1)]
+    out = {}
+    st = stream_handle()
+    for name, N, Kd, epi in shapes:
+        x = torch.randn(M, Kd, device="cuda").bfloat16()
+        w = (torch.randn(N, Kd, device="cuda") / math.sqrt(Kd)).bfloat16()
+        bias = torch.randn(N, device="cuda")
+        r = torch.randn(M, N, device="cuda").bfloat16()
+        y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        a8 = torch.empty(M, Kd, dtype=torch.uint8, device="cuda")
+        sa = torch.empty(M, device="cuda")
+        w8, sw = quant_weight_fp8(w)
+        h = hip()
+        rr = r.data_ptr() if epi == 2 else 0
+
+        def f8(with_quant=True):
+            if with_quant:
+                h.quant_rows_fp8(x.data_ptr(), Kd, a8.data_ptr(), Kd, sa.data_ptr(), M, Kd, st)
+            h.gemm_fp8(epi, a8.data_ptr(), Kd, w8.data_ptr(), Kd, sa.data_ptr(), sw.data_ptr(),
+                       bias.data_ptr(), rr, N, y.data_ptr(), N, M, N, Kd, st)
+        res = ab({"bf16": lambda: K.gemm(x, w, bias, epi, r if epi == 2 else None, out=y),
+                  "fp8_with_quant": lambda: f8(True), "fp8_gemm_only": lambda: f8(False)},
+                 rounds=a.rounds, iters=a.iters)
+        fl = 2 * M * N * Kd
+        out[name] = {k: dict(ms=round(m, 4), TFLOPs=round(fl / (m / 1e3) / 1e12)) for k, (m, _) in res.items()}
+    print(json.dumps({"bench": "gemm_fp8", "M": M, "results": out}))
+
+
 def cmd_attn(a):
     from codename_symbiont_amd.ops import kernels as K
 
@@ -272,7 +309,7 @@ def cmd_attn(a):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("cmd", choices=["scan", "scanabl", "scanstamp", "scanfp8", "gemm", "encoder", "attn", "latency"])
+    ap.add_argument("cmd", choices=["scan", "scanabl", "scanstamp", "scanfp8", "gemm", "encoder", "attn", "latency", "gemmfp8"])
     ap.add_argument("--rows", type=int, default=100_000_000)
     ap.add_argument("--dim", type=int, default=384)
     ap.add_argument("--nq", type=int, default=256)
@@ -281,10 +318,11 @@ def main():
     ap.add_argument("--head-dim", type=int, default=32)
     ap.add_argument("--model", default="minilm-l6")
     ap.add_argument("--seed", type=int, default=1, help="scanabl: seed per-query thresholds")
+    ap.add_argument("--precision", default="bf16", help="encoder: comma list of bf16,fp8")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=5)
     a = ap.parse_args()
-    {"scan": cmd_scan, "scanabl": cmd_scanabl, "scanstamp": cmd_scanstamp, "scanfp8": cmd_scanfp8, "gemm": cmd_gemm, "encoder": cmd_encoder, "attn": cmd_attn, "latency": cmd_latency}[a.cmd](a)
+    {"scan": cmd_scan, "scanabl": cmd_scanabl, "scanstamp": cmd_scanstamp, "scanfp8": cmd_scanfp8, "gemm": cmd_gemm, "encoder": cmd_encoder, "attn": cmd_attn, "latency": cmd_latency, "gemmfp8": cmd_gemmfp8}[a.cmd](a)
 
 
 if __name__ == "__main__":

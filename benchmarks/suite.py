@@ -62,7 +62,7 @@ def main():
         ("index-100m", launch + common + ["--mode", "search"], 900),
         ("bge-dp", launch + common + ["--model", "bge-base", "--mode", "embed"], 600),
         ("e5-fp8", launch + common + ["--model", "e5-large", "--index-dtype", "fp8",
-                                      "--index-rows", str(fp8_rows)], 1200),
+                                      "--encoder-dtype", "fp8", "--index-rows", str(fp8_rows)], 1200),
         ("headline", launch + common, 900),
     ]
     only = set(filter(None, a.only.split(",")))

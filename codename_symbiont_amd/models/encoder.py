@@ -84,15 +84,29 @@ def synthetic_batch(cfg: EncoderConfig, batch: int, seq_len: int, seed: int = 0,
     return pack_token_ids(toks, cfg)
 
 
+def quant_weight_fp8(w: torch.Tensor):
+    """[N, K] weights -> (e4m3 bytes [N, K], per-output-channel scale f32 [N]); w ~= q * s."""
+    wf = w.float()
+    s = wf.abs().amax(dim=1).clamp_min(1e-12) / 448.0
+    q = (wf / s[:, None]).to(torch.float8_e4m3fn).view(torch.uint8).contiguous()
+    return q, s.contiguous()
+
+
 class HipEncoder:
     """bf16 weights on device + the native C++ ``EncoderRuntime`` (gfx950 kernels)."""
 
     backend = "hip"
 
-    def __init__(self, cfg: EncoderConfig, params: dict | None = None, device="cuda", seed=0):
+    def __init__(self, cfg: EncoderConfig, params: dict | None = None, device="cuda", seed=0,
+                 precision: str = "bf16"):
+        """precision "fp8": the four projection GEMMs of every layer run on e4m3 MFMAs with
+        per-output-channel weight scales and per-token activation scales (BASELINE config #5)."""
         from ..ops._ext import hip
 
+        if precision not in ("bf16", "fp8"):
+            raise ValueError(f"encoder precision must be bf16 or fp8, got {precision!r}")
         self.cfg = cfg
+        self.precision = precision
         self.device = _resolve(device)
         if params is None:
             params = load_params(cfg, seed=seed, device=self.device)
@@ -102,10 +116,21 @@ class HipEncoder:
                                        p["wemb"].data_ptr(), p["pemb"].data_ptr(),
                                        p["temb"].data_ptr(), p["eln_g"].data_ptr(),
                                        p["eln_b"].data_ptr())
+        keys = ("wqkv", "bqkv", "wo", "bo", "ln1_g", "ln1_b", "wi", "bi", "wo2", "bo2", "ln2_g",
+                "ln2_b")
+        self._fp8 = []
         for L in p["layers"]:
-            self.rt.add_layer([L[k].data_ptr() for k in (
-                "wqkv", "bqkv", "wo", "bo", "ln1_g", "ln1_b", "wi", "bi", "wo2", "bo2", "ln2_g",
-                "ln2_b")])
+            if precision == "bf16":
+                self.rt.add_layer([L[k].data_ptr() for k in keys])
+                continue
+            q = dict(L)
+            scales = []
+            for k in ("wqkv", "wo", "wi", "wo2"):
+                w8, s = quant_weight_fp8(L[k])
+                q[k] = w8
+                scales.append(s)
+            self._fp8.append((q, scales))      # keep the e4m3 weights and scales alive
+            self.rt.add_layer_fp8([q[k].data_ptr() for k in keys] + [s.data_ptr() for s in scales])
         self._ws_tokens = 0
         self._ws: list[torch.Tensor] = []
 
@@ -115,6 +140,9 @@ class HipEncoder:
             H, F = self.cfg.hidden, self.cfg.ffn
             mk = lambda n: torch.empty(cap, n, dtype=torch.bfloat16, device=self.device)  # noqa
             self._ws = [mk(H), mk(H), mk(3 * H), mk(H), mk(F), mk(H)]
+            if self.precision == "fp8":   # e4m3 activations + per-token scales
+                self._ws += [torch.empty(cap, max(H, F), dtype=torch.uint8, device=self.device),
+                             torch.empty(cap, dtype=torch.float32, device=self.device)]
             self._ws_tokens = cap
         return [t.data_ptr() for t in self._ws]
 
@@ -207,6 +235,9 @@ class HipEncoder:
         cu[-1] = Tb
         mk = lambda n: torch.empty(Tb, n, dtype=torch.bfloat16, device=dev)  # noqa: E731
         ws = [mk(H), mk(H), mk(3 * H), mk(H), mk(cfg.ffn), mk(H)]
+        if self.precision == "fp8":
+            ws += [torch.empty(Tb, max(H, cfg.ffn), dtype=torch.uint8, device=dev),
+                   torch.empty(Tb, dtype=torch.float32, device=dev)]
         f32 = torch.empty(Bb + 1, H, dtype=torch.float32, device=dev)
         unit = torch.empty(Bb + 1, H, dtype=torch.bfloat16, device=dev)
         max_len = min(Tb, cfg.max_position - cfg.position_offset)

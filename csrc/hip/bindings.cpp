@@ -41,6 +41,11 @@ int symb_index_scan_ablate(const void* X, int n_valid, int rows_per_blk, int n_r
                            const void* Q, int NQ, float* cs, int* ci, hipStream_t st, int abl,
                            const float* thr);
 int symb_gemm_config(int resln_bm, int tile);
+int symb_gemm_fp8(int epi, const void* A8, int lda, const void* W8, int ldw, const float* sa,
+                  const float* sw, const float* bias, const void* R, int ldr, void* C, int ldc,
+                  int M, int N, int K, hipStream_t st);
+int symb_quant_rows_fp8(const void* x, int ldx, void* out, int ldo, float* scale, int M, int K,
+                        hipStream_t st);
 int symb_quant_fp8(const void* in, int in_f32, int ld_in, uint8_t* out, int ld_out, int n, int D,
                    float scale, int normalize, hipStream_t st);
 int symb_index_scan_fp8(const void* X, int n_valid, int D, int rows_per_blk, int n_rblk,
@@ -67,6 +72,10 @@ enum { EPI_BIAS = 0, EPI_GELU = 1, EPI_RES = 2, EPI_RES_LN = 3 };
 
 struct LayerWeights {
   uptr wqkv, bqkv, wo, bo, ln1_g, ln1_b, wi, bi, wo2, bo2, ln2_g, ln2_b;
+  // fp8 layers: the four weight pointers above are e4m3 [N, K] and these are their per-output-
+  // channel scales (f32 [N]); activations are quantised per token right before each GEMM
+  bool fp8 = false;
+  uptr sw_qkv = 0, sw_o = 0, sw_i = 0, sw_o2 = 0;
 };
 
 class EncoderRuntime {
@@ -82,13 +91,27 @@ class EncoderRuntime {
     layers_.push_back(LayerWeights{w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], w[8], w[9],
                                    w[10], w[11]});
   }
+  void add_layer_fp8(const std::vector<uptr>& w) {
+    if (w.size() != 16) throw std::invalid_argument("fp8 layer needs 12 pointers + 4 scales");
+    if (H_ % 128 || FF_ % 128) throw std::invalid_argument("fp8 layers need hidden/ffn % 128 == 0");
+    LayerWeights L{w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], w[8], w[9], w[10], w[11]};
+    L.fp8 = true;
+    L.sw_qkv = w[12];
+    L.sw_o = w[13];
+    L.sw_i = w[14];
+    L.sw_o2 = w[15];
+    layers_.push_back(L);
+    any_fp8_ = true;
+  }
   int num_layers() const { return (int)layers_.size(); }
 
-  // ws: {h, h2, qkv, ctx, ff, tmp} device buffers sized for T tokens.
+  // ws: {h, h2, qkv, ctx, ff, tmp} device buffers sized for T tokens; fp8 layers add
+  // {a8 (T x max(H, FF) bytes), sa (T floats)}.
   void forward(uptr ids, uptr pos, uptr tt, uptr cu, int T, int B, int max_len,
                const std::vector<uptr>& ws, int pool_mode, int normalize_f32, uptr out_f32,
                uptr out_norm, uptr stream) {
-    if (ws.size() != 6) throw std::invalid_argument("workspace needs 6 buffers");
+    if (ws.size() != (any_fp8_ ? 8u : 6u))
+      throw std::invalid_argument(any_fp8_ ? "fp8 workspace needs 8 buffers" : "workspace needs 6 buffers");
     hipStream_t st = S(stream);
     const int H = H_;
     uptr h = ws[0], h2 = ws[1], qkv = ws[2], ctx = ws[3], ff = ws[4], tmp = ws[5];
@@ -98,6 +121,10 @@ class EncoderRuntime {
           "embed_ln");
     const bool fuse_ln = (H == 384);
     for (const auto& L : layers_) {
+      if (L.fp8) {
+        fp8_layer(L, ws, T, B, max_len, cu, st);
+        continue;
+      }
       check(symb_gemm(EPI_BIAS, P<void>(h), H, P<void>(L.wqkv), H, P<float>(L.bqkv), nullptr, 0,
                       nullptr, nullptr, 0.f, P<void>(qkv), 3 * H, T, 3 * H, H, st),
             "qkv gemm");
@@ -141,6 +168,45 @@ class EncoderRuntime {
   }
 
  private:
+  // e4m3 layer: per-token quantiser -> fp8 MFMA GEMM (scales folded into the epilogue) for each
+  // of the four projections; LayerNorms through symb_add_ln.
+  void fp8_layer(const LayerWeights& L, const std::vector<uptr>& ws, int T, int B, int max_len,
+                 uptr cu, hipStream_t st) {
+    const int H = H_;
+    uptr h = ws[0], h2 = ws[1], qkv = ws[2], ctx = ws[3], ff = ws[4], tmp = ws[5];
+    uptr a8 = ws[6];
+    float* sa = P<float>(ws[7]);
+    auto q8 = [&](uptr x, int K, const char* what) {
+      check(symb_quant_rows_fp8(P<void>(x), K, P<void>(a8), K, sa, T, K, st), what);
+    };
+    q8(h, H, "quant h");
+    check(symb_gemm_fp8(EPI_BIAS, P<void>(a8), H, P<void>(L.wqkv), H, sa, P<float>(L.sw_qkv),
+                        P<float>(L.bqkv), nullptr, 0, P<void>(qkv), 3 * H, T, 3 * H, H, st),
+          "qkv gemm fp8");
+    check(symb_attention(P<void>(qkv), 3 * H, P<int32_t>(cu), B, max_len, nh_, hd_, P<void>(ctx),
+                         H, st),
+          "attention");
+    q8(ctx, H, "quant ctx");
+    check(symb_gemm_fp8(EPI_RES, P<void>(a8), H, P<void>(L.wo), H, sa, P<float>(L.sw_o),
+                        P<float>(L.bo), P<void>(h), H, P<void>(tmp), H, T, H, H, st),
+          "out-proj gemm fp8");
+    check(symb_add_ln(P<void>(tmp), nullptr, P<float>(L.ln1_g), P<float>(L.ln1_b), eps_,
+                      P<void>(h2), T, H, st),
+          "ln1");
+    q8(h2, H, "quant h2");
+    check(symb_gemm_fp8(EPI_GELU, P<void>(a8), H, P<void>(L.wi), H, sa, P<float>(L.sw_i),
+                        P<float>(L.bi), nullptr, 0, P<void>(ff), FF_, T, FF_, H, st),
+          "ffn1 gemm fp8");
+    q8(ff, FF_, "quant ff");
+    check(symb_gemm_fp8(EPI_RES, P<void>(a8), FF_, P<void>(L.wo2), FF_, sa, P<float>(L.sw_o2),
+                        P<float>(L.bo2), P<void>(h2), H, P<void>(tmp), H, T, H, FF_, st),
+          "ffn2 gemm fp8");
+    check(symb_add_ln(P<void>(tmp), nullptr, P<float>(L.ln2_g), P<float>(L.ln2_b), eps_,
+                      P<void>(h), T, H, st),
+          "ln2");
+  }
+
+  bool any_fp8_ = false;
   int H_, nh_, hd_, FF_;
   float eps_;
   uptr wemb_, pemb_, temb_, eln_g_, eln_b_;
@@ -209,6 +275,16 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gemm_config", [](int resln_bm, int tile) {
     check(symb_gemm_config(resln_bm, tile), "gemm_config");
   }, py::arg("resln_bm") = 128, py::arg("tile") = 0);
+  m.def("gemm_fp8", [](int epi, uptr A8, int lda, uptr W8, int ldw, uptr sa, uptr sw, uptr bias,
+                       uptr R, int ldr, uptr C, int ldc, int M, int N, int K, uptr st) {
+    check(symb_gemm_fp8(epi, P<void>(A8), lda, P<void>(W8), ldw, P<float>(sa), P<float>(sw),
+                        P<float>(bias), P<void>(R), ldr, P<void>(C), ldc, M, N, K, S(st)),
+          "gemm_fp8");
+  });
+  m.def("quant_rows_fp8", [](uptr x, int ldx, uptr out, int ldo, uptr scale, int M, int K, uptr st) {
+    check(symb_quant_rows_fp8(P<void>(x), ldx, P<void>(out), ldo, P<float>(scale), M, K, S(st)),
+          "quant_rows_fp8");
+  });
   m.def("quant_fp8", [](uptr in, bool in_f32, int ld_in, uptr out, int ld_out, int n, int D,
                         float scale, bool normalize, uptr st) {
     check(symb_quant_fp8(P<void>(in), in_f32, ld_in, P<uint8_t>(out), ld_out, n, D, scale,
@@ -234,6 +310,7 @@ PYBIND11_MODULE(_hip, m) {
   py::class_<EncoderRuntime>(m, "EncoderRuntime")
       .def(py::init<int, int, int, float, uptr, uptr, uptr, uptr, uptr>())
       .def("add_layer", &EncoderRuntime::add_layer)
+      .def("add_layer_fp8", &EncoderRuntime::add_layer_fp8)
       .def("num_layers", &EncoderRuntime::num_layers)
       .def("forward", &EncoderRuntime::forward);
 }

@@ -31,12 +31,24 @@ __device__ __forceinline__ int swz_off(int row, int chunk) {
   return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
 }
 
-template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, int NSTAGE = 2>
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+
+// F8 = true: A, W are OCP e4m3 bytes and one k-tile is 128 elements (still 128-byte LDS rows, so
+// staging and swizzle are shared); v_mfma_f32_16x16x128_f8f6f4 consumes 32 bytes per lane (two
+// swizzled 16-byte chunks), and the epilogue rescales by sa[row] (per-token activation scale) x
+// sw[col] (per-output-channel weight scale) before bias / GELU / residual.
+template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, int NSTAGE = 2, bool F8 = false>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
-    const __bf16* __restrict__ A, int lda, const __bf16* __restrict__ W, int ldw,
+    const void* __restrict__ Av, int lda, const void* __restrict__ Wv, int ldw,
     const float* __restrict__ bias, const __bf16* __restrict__ R, int ldr,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
-    __bf16* __restrict__ C, int ldc, int M, int N, int K) {
+    __bf16* __restrict__ C, int ldc, int M, int N, int K, const float* __restrict__ sa,
+    const float* __restrict__ sw) {
+  constexpr int ES = F8 ? 1 : 2;               // bytes per element
+  constexpr int KTILE = 128 / ES;              // elements per 128-byte k-tile row
+  const char* A = reinterpret_cast<const char*>(Av);
+  const char* W = reinterpret_cast<const char*>(Wv);
   constexpr int NW = WAVES_M * WAVES_N;
   constexpr int NT = 64 * NW;
   constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
@@ -53,24 +65,24 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
   const int nwg = gridDim.x;
   const int tile = xcd_remap(blockIdx.x, nwg);
   const int m0 = (tile / n_tiles) * BM, n0 = (tile % n_tiles) * BN;
-  const int KT = K / GEMM_BK;
+  const int KT = K / KTILE;
 
   auto stage = [&](int kt, int buf) {
     char* sA = smem + buf * TILE_BYTES;
     char* sB = sA + BM * 128;
-    const int k0 = kt * GEMM_BK;
+    const size_t k0 = (size_t)kt * 128;         // byte offset of the k-tile
 #pragma unroll
     for (int i = 0; i < (BM * 8) / NT; ++i) {
       const int s = i * NT + tid;
       const int row = s >> 3, pc = s & 7, c = pc ^ ((row >> 1) & 7);
       const int grow = min(m0 + row, M - 1);
-      glds16(A + (size_t)grow * lda + k0 + c * 8, sA + (i * NT + wave * 64) * 16);
+      glds16(A + (size_t)grow * lda * ES + k0 + c * 16, sA + (i * NT + wave * 64) * 16);
     }
 #pragma unroll
     for (int i = 0; i < (BN * 8) / NT; ++i) {
       const int s = i * NT + tid;
       const int row = s >> 3, pc = s & 7, c = pc ^ ((row >> 1) & 7);
-      glds16(W + (size_t)(n0 + row) * ldw + k0 + c * 8, sB + (i * NT + wave * 64) * 16);
+      glds16(W + (size_t)(n0 + row) * ldw * ES + k0 + c * 16, sB + (i * NT + wave * 64) * 16);
     }
   };
 
@@ -153,6 +165,30 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
     }
     const char* sA = smem + (kt % NSTAGE) * TILE_BYTES;
     const char* sB = sA + BM * 128;
+    if constexpr (F8) {
+      const int g = lane >> 4;
+      i32x8 a[RM], b[RN];
+#pragma unroll
+      for (int i = 0; i < RM; ++i) {
+        const int row = wm * WTM + i * 16 + (lane & 15);
+        const i32x4 lo = *reinterpret_cast<const i32x4*>(sA + swz_off(row, 2 * g));
+        const i32x4 hi = *reinterpret_cast<const i32x4*>(sA + swz_off(row, 2 * g + 1));
+        a[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        const int row = wn * WTN + j * 16 + (lane & 15);
+        const i32x4 lo = *reinterpret_cast<const i32x4*>(sB + swz_off(row, 2 * g));
+        const i32x4 hi = *reinterpret_cast<const i32x4*>(sB + swz_off(row, 2 * g + 1));
+        b[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[i], b[j], acc[i][j], 0, 0,
+                                                                       0, 127, 0, 127);
+    } else {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int chunk = kk * 4 + (lane >> 4);
@@ -168,6 +204,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
 #pragma unroll
         for (int j = 0; j < RN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
     }
   }
 
@@ -204,7 +241,10 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
       for (int r = 0; r < 4; ++r) {
         const int row = wm * WTM + i * 16 + (lane >> 4) * 4 + r;
         const int col = wn * WTN + j * 16 + (lane & 15);
-        Cs[row * CS + col] = acc[i][j][r];
+        if constexpr (F8)
+          Cs[row * CS + col] = acc[i][j][r] * sa[min(m0 + row, M - 1)] * sw[n0 + col];
+        else
+          Cs[row * CS + col] = acc[i][j][r];
       }
   __syncthreads();
 
@@ -241,11 +281,12 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
   }
 }
 
-template <int BM, int BN, int WM, int WN, int EPI, int NSTAGE = 2>
-static int launch_cfg(const __bf16* A, int lda, const __bf16* W, int ldw, const float* bias,
+template <int BM, int BN, int WM, int WN, int EPI, int NSTAGE = 2, bool F8 = false>
+static int launch_cfg(const void* A, int lda, const void* W, int ldw, const float* bias,
                       const __bf16* R, int ldr, const float* g, const float* b, float eps,
-                      __bf16* C, int ldc, int M, int N, int K, hipStream_t st) {
-  auto kern = gemm_bf16_kernel<BM, BN, WM, WN, EPI, NSTAGE>;
+                      __bf16* C, int ldc, int M, int N, int K, hipStream_t st,
+                      const float* sa = nullptr, const float* sw = nullptr) {
+  auto kern = gemm_bf16_kernel<BM, BN, WM, WN, EPI, NSTAGE, F8>;
   constexpr int main_bytes = NSTAGE * (BM + BN) * 128;
   constexpr int full_epi = BM * (BN + 4) * 4;
   constexpr int epi_bytes = full_epi > 160 * 1024 ? (BM / WM) * (BN + 4) * 4 : full_epi;
@@ -257,7 +298,7 @@ static int launch_cfg(const __bf16* A, int lda, const __bf16* W, int ldw, const 
   }
   const int nwg = ((M + BM - 1) / BM) * (N / BN);
   hipLaunchKernelGGL(kern, dim3(nwg), dim3(64 * WM * WN), lds, st, A, lda, W, ldw, bias, R, ldr,
-                     g, b, eps, C, ldc, M, N, K);
+                     g, b, eps, C, ldc, M, N, K, sa, sw);
   return (int)hipGetLastError();
 }
 
@@ -321,4 +362,68 @@ int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const flo
                                                  ldc, M, N, K, st);
   }
   return -1;
+}
+
+// fp8 GEMM: C = epi((A8 . W8^T) * sa[m] * sw[n] + bias); A8 [M,K], W8 [N,K] OCP e4m3 bytes.
+// epi: EPI_BIAS / EPI_GELU / EPI_RES (row LayerNorms go through symb_add_ln).
+int symb_gemm_fp8(int epi, const void* A8, int lda, const void* W8, int ldw, const float* sa,
+                  const float* sw, const float* bias, const void* R, int ldr, void* C, int ldc,
+                  int M, int N, int K, hipStream_t st) {
+  if (M <= 0) return 0;
+  if (K % 128 != 0 || N % 128 != 0) return -1;
+  auto r = (const __bf16*)R;
+  auto c = (__bf16*)C;
+#define SYMB_G8(E) launch_cfg<128, 128, 2, 2, E, 2, true>(A8, lda, W8, ldw, bias, r, ldr, nullptr, \
+                                                           nullptr, 0.f, c, ldc, M, N, K, st, sa, sw)
+  switch (epi) {
+    case EPI_BIAS: return SYMB_G8(EPI_BIAS);
+    case EPI_GELU: return SYMB_G8(EPI_GELU);
+    case EPI_RES: return SYMB_G8(EPI_RES);
+  }
+#undef SYMB_G8
+  return -1;
+}
+
+// Per-row (token) activation quantiser for the fp8 GEMMs: scale[m] = amax(x[m, :]) / 448 and
+// out = e4m3(x / scale).  One wave per row; K <= 4096 and K % 8 == 0.
+__global__ __launch_bounds__(256) void quant_rows_fp8_kernel(const __bf16* __restrict__ x, int ldx,
+                                                             uint8_t* __restrict__ out, int ldo,
+                                                             float* __restrict__ scale, int M,
+                                                             int K) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  float v[8][8];
+  float amax = 0.f;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (col < K) {
+      load8(x + (size_t)row * ldx + col, v[c]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[c][e]));
+    }
+  }
+  amax = fmaxf(wave_max(amax), 1e-12f);
+  const float inv = 448.f / amax;
+  if (lane == 0) scale[row] = amax / 448.f;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (col >= K) continue;
+    int lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[c][0] * inv, v[c][1] * inv, 0, false);
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[c][2] * inv, v[c][3] * inv, lo, true);
+    int hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[c][4] * inv, v[c][5] * inv, 0, false);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[c][6] * inv, v[c][7] * inv, hi, true);
+    *reinterpret_cast<int2*>(out + (size_t)row * ldo + col) = make_int2(lo, hi);
+  }
+}
+
+int symb_quant_rows_fp8(const void* x, int ldx, void* out, int ldo, float* scale, int M, int K,
+                        hipStream_t st) {
+  if (M <= 0) return 0;
+  if (K % 8 || K > 4096) return -1;
+  hipLaunchKernelGGL(quant_rows_fp8_kernel, dim3((M + 3) / 4), dim3(256), 0, st,
+                     (const __bf16*)x, ldx, (uint8_t*)out, ldo, scale, M, K);
+  return (int)hipGetLastError();
 }

@@ -285,3 +285,59 @@ def test_encoder_graph_replay_matches_eager():
         _close(g32, e32, atol=1e-5, what=f"graph f32 B={B} S={S}")
         assert torch.equal(gu, eu)
     assert len(enc._graphs) >= 4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K,epi", [(300, 1152, 384, 0), (129, 1536, 384, 1), (517, 384, 1536, 2),
+                                      (1000, 3072, 1024, 1), (77, 1024, 4096, 2)])
+def test_gemm_fp8(M, N, K, epi):
+    """fp8 GEMM == fp32 product of the DECODED e4m3 operands, rescaled (+ the bf16 epilogue)."""
+    from codename_symbiont_amd.models.encoder import quant_weight_fp8
+    from codename_symbiont_amd.ops._ext import hip, stream_handle
+
+    a = _bf(M, K, seed=1)
+    w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=2)
+    bias = _f(N, scale=0.5, seed=3)
+    res = _bf(M, N, seed=4) if epi == 2 else None
+    a8 = torch.empty(M, K, dtype=torch.uint8, device=DEV)
+    sa = torch.empty(M, dtype=torch.float32, device=DEV)
+    st = stream_handle()
+    hip().quant_rows_fp8(a.data_ptr(), K, a8.data_ptr(), K, sa.data_ptr(), M, K, st)
+    w8, sw = quant_weight_fp8(w)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    hip().gemm_fp8(epi, a8.data_ptr(), K, w8.data_ptr(), K, sa.data_ptr(), sw.data_ptr(),
+                   bias.data_ptr(), 0 if res is None else res.data_ptr(), N, out.data_ptr(), N,
+                   M, N, K, st)
+    torch.cuda.synchronize()
+    # the row quantiser matches torch's e4m3 cast of x / scale
+    ref_a8 = (a.float() / sa[:, None]).to(torch.float8_e4m3fn).view(torch.uint8)
+    assert (a8 == ref_a8).float().mean().item() > 0.999
+    ad = a8.view(torch.float8_e4m3fn).float() * sa[:, None]
+    wd = w8.view(torch.float8_e4m3fn).float() * sw[:, None]
+    ref = R.gemm_ref(ad.bfloat16(), wd.bfloat16(), bias, epi, res, None, None, 1e-12)
+    exact = ad @ wd.t() + bias
+    if epi == 1:
+        exact = torch.nn.functional.gelu(exact)
+    elif epi == 2:
+        exact = exact + res.float()
+    _close(out, exact, atol=4e-2, rtol=2e-2, what=f"gemm_fp8 epi={epi}")
+    del ref
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model", ["minilm-l6", "bge-base"])
+def test_encoder_fp8_close_to_fp32_oracle(model):
+    """fp8 encoder (e4m3 GEMMs, per-channel / per-token scales) keeps cosine >= 0.99 vs fp32."""
+    from codename_symbiont_amd.models import get_config
+    from codename_symbiont_amd.models.encoder import HipEncoder, TorchEncoder, synthetic_batch
+    from codename_symbiont_amd.models.weights import load_params
+
+    cfg = get_config(model)
+    params = load_params(cfg, seed=5, device="cpu")
+    enc8 = HipEncoder(cfg, params=params, precision="fp8")
+    ref = TorchEncoder(cfg, params=params)
+    b = synthetic_batch(cfg, 16, 64, seed=2, varlen=True)
+    out8, _ = enc8.forward_packed(b.to(DEV))
+    outr, _ = ref.forward_packed(b)
+    cos = torch.nn.functional.cosine_similarity(out8.float().cpu(), outr.float(), dim=-1)
+    assert cos.min().item() > 0.99, cos
