@@ -243,7 +243,9 @@ class ApiService(Service):
         self.metrics.inc("search.requests")
         self.log.info("[API_SEARCH_HANDLER] Successfully received %d search results for client_req_id: %s",
                       len(sr.results), rid)
-        return _json_response(SemanticSearchApiResponse(rid, sr.results, None))
+        resp = _json_response(SemanticSearchApiResponse(rid, sr.results, None))
+        self.metrics.observe("search.handler", (time.perf_counter() - t0) * 1e3)
+        return resp
 
     async def metrics_ep(self, request):
         from starlette.responses import JSONResponse
@@ -285,12 +287,25 @@ class ApiService(Service):
     async def serve(self, host: str | None = None, port: int | None = None):
         import uvicorn
 
+        import socket
+
         config = uvicorn.Config(self.app(), host=host or self.cfg.api_host,
                                 port=self.cfg.api_port if port is None else port,
-                                log_level="warning", lifespan="off")
+                                log_level="warning", lifespan="off",
+                                # actix keeps connections 5 s like uvicorn; a longer idle keep-alive
+                                # avoids close-vs-reuse races with pooled clients under load
+                                timeout_keep_alive=75)
         self.server = uvicorn.Server(config)
         self.log.info("[HTTP_SERVER] Starting API HTTP server at http://%s:%s", config.host, config.port)
-        await self.server.serve()
+        if self.cfg.api_workers > 1:   # every worker binds the same port; the kernel balances
+            sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+            sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+            sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEPORT, 1)
+            sock.bind((config.host, config.port))
+            sock.listen(2048)
+            await self.server.serve(sockets=[sock])
+        else:
+            await self.server.serve()
 
     async def run_forever(self) -> None:
         await self.start()
@@ -352,11 +367,37 @@ async def _plain(send, status: int, body: bytes) -> None:
 
 
 def main() -> None:
+    import subprocess
+    import sys
+
     ulog.setup(ApiService.name, "info")
     cfg = ApiService().cfg
     if "NATS_URL" not in os.environ:
         cfg.nats_url = "nats://cs-nats:4222"  # the reference's api default (main.rs:519-524)
-    asyncio.run(ApiService(cfg).run_forever())
+    import signal
+
+    kids = []
+    if cfg.api_workers > 1 and not os.environ.get("SYMB_API_CHILD"):
+        # extra gateway workers as CHILD processes on the same SO_REUSEPORT port; they die with
+        # this process (PR_SET_PDEATHSIG) and SIGTERM unwinds through the cleanup below
+        def _die_with_parent():
+            import ctypes
+            ctypes.CDLL("libc.so.6").prctl(1, signal.SIGTERM)   # PR_SET_PDEATHSIG
+        env = dict(os.environ, SYMB_API_CHILD="1", NATS_URL=cfg.nats_url)
+        kids = [subprocess.Popen([sys.executable, "-m", "codename_symbiont_amd.services.api"], env=env,
+                                 preexec_fn=_die_with_parent)
+                for _ in range(cfg.api_workers - 1)]
+        signal.signal(signal.SIGTERM, lambda *_: sys.exit(0))
+    try:
+        asyncio.run(ApiService(cfg).run_forever())
+    finally:
+        for k in kids:
+            k.terminate()
+        for k in kids:
+            try:
+                k.wait(10)
+            except subprocess.TimeoutExpired:
+                k.kill()
 
 
 if __name__ == "__main__":

@@ -11,6 +11,7 @@ a metrics registry (exposed by the api service on ``GET /api/metrics`` and publi
 from __future__ import annotations
 
 import asyncio
+import os
 import json
 import logging
 import random
@@ -143,8 +144,9 @@ class Service:
         return self
 
     async def _metrics_loop(self) -> None:
+        interval = float(os.environ.get("SYMB_METRICS_INTERVAL", "10"))
         while True:
-            await asyncio.sleep(10.0)
+            await asyncio.sleep(interval)
             try:
                 await self.nc.publish(f"metrics.{self.name}", json.dumps(
                     {"service": self.name, "ts_ms": int(time.time() * 1000), **self.metrics.snapshot()}

@@ -39,6 +39,8 @@ class VectorMemoryService(Service):
                                           device="cpu" if self.cfg.force_cpu else None,
                                           snapshot_dir=self.cfg.snapshot_dir,
                                           dtype=self.cfg.index_dtype)
+        if self.cfg.index_fill_random and self.store.count == 0:
+            self.store.shard.fill_random(self.cfg.index_fill_random, seed=17)
         self.log.info("[INDEX_SETUP] collection '%s': dim %d, capacity %d, device %s, %d points",
                       self.cfg.collection, dim, self.store.shard.capacity, self.store.shard.device,
                       self.store.count)
@@ -120,16 +122,20 @@ class VectorMemoryService(Service):
             await self.reply(nmsg, SemanticSearchNatsResult(task.request_id, [], err))
             return
         items = []
+        skipped = 0
         for s, r in zip(scores.tolist(), rows.tolist()):
             if r < 0:
                 continue
             pid, p = self.store.lookup(r)
             if pid is None:
-                self.log.warning("[SEARCH_HANDLER] Found point with missing or unexpected ID format. Skipping.")
+                skipped += 1
                 continue
             items.append(SemanticSearchResultItem(pid, float(s), QdrantPointPayload(
                 p.original_document_id, p.source_url, p.sentence_text, int(p.sentence_order) & 0xFFFFFFFF,
                 p.model_name, int(p.processed_at_ms))))
+        if skipped:  # one line per request (the reference logs one per point)
+            self.log.warning("[SEARCH_HANDLER] Found %d point(s) with missing or unexpected ID format. "
+                             "Skipping.", skipped)
         await self.reply(nmsg, SemanticSearchNatsResult(task.request_id, items, None))
         self.log.info("[SEARCH_HANDLER] Sent %d search results for request_id %s", len(items),
                       task.request_id)

@@ -43,6 +43,9 @@ class Config:
     nats_url: str = field(default_factory=lambda: _env("NATS_URL", "nats://localhost:4222"))
     api_host: str = field(default_factory=lambda: _env("API_SERVER_HOST", "0.0.0.0"))
     api_port: int = field(default_factory=lambda: _int("API_SERVER_PORT", 8080))  # parse fail -> 8080
+    # gateway worker processes sharing the port (SO_REUSEPORT); each has its own NATS connection
+    # and SSE hub, and every worker receives every events.text.generated message
+    api_workers: int = field(default_factory=lambda: _int("SYMB_API_WORKERS", 1))
     neo4j_uri: str = field(default_factory=lambda: _env("NEO4J_URI", "bolt://localhost:7687"))
     neo4j_user: str = field(default_factory=lambda: _env("NEO4J_USER", "neo4j"))
     neo4j_password: str = field(default_factory=lambda: _env("NEO4J_PASSWORD", ""))
@@ -56,6 +59,8 @@ class Config:
     batch_window_ms: float = field(default_factory=lambda: _float("SYMB_BATCH_WINDOW_MS", 2.0))
     index_dim: int = field(default_factory=lambda: _int("SYMB_INDEX_DIM", 0))  # 0 -> model hidden
     index_capacity: int = field(default_factory=lambda: _int("SYMB_INDEX_CAPACITY", 1 << 22))
+    # benchmarking only: pre-fill the index with N random unit rows (no payloads) at startup
+    index_fill_random: int = field(default_factory=lambda: _int("SYMB_INDEX_FILL_RANDOM", 0))
     # "bf16" (default) or "fp8" (OCP e4m3 rows; needs a dim that is a multiple of 256)
     index_dtype: str = field(default_factory=lambda: os.environ.get("SYMB_INDEX_DTYPE", "bf16"))
     snapshot_dir: str = field(default_factory=lambda: _env("SYMB_SNAPSHOT_DIR", ""))
