@@ -8,17 +8,24 @@
 //  * The queries live in REGISTERS as MFMA B fragments: every wave owns 32 queries (D=384,
 //    v_mfma_f32_32x32x16_bf16, 24 fragments = 96 VGPRs) or 16 queries (D=768/1024,
 //    v_mfma_f32_16x16x32_bf16).  A workgroup therefore scores 256 (or 128) queries at once.
-//  * Index rows stream HBM -> LDS in 32-row tiles by global_load_lds_dwordx4 (no VGPR staging)
-//    through a 4-deep LDS ring with a COUNTED `s_waitcnt vmcnt(6)` and a raw s_barrier, so two
-//    tiles are always in flight across the barrier (a __syncthreads would drain vmcnt to 0).
-//    Every tile read from HBM once feeds 8 waves x their queries.
+//  * Index rows stream HBM -> LDS by global_load_lds_dwordx4 (no VGPR staging) in tiles of two
+//    MFMA sub-tiles (64 rows at D=384) through an NS-deep LDS ring (ScanCfg: 3 x 48 KiB at D=384)
+//    with a COUNTED `s_waitcnt vmcnt` and a raw s_barrier, so the next tile stays in flight across
+//    the barrier (a __syncthreads would drain vmcnt to 0).  The DMA pieces of tile t+NS-1 are
+//    issued inside sub-tile 0's MFMA chain of tile t.  Every tile read from HBM once feeds 8
+//    waves x their queries.
+//  * A fragments are read by hand-issued ds_read_b128 (inline asm) with counted lgkmcnt waits,
+//    6 in flight, so the compiler cannot serialise them behind lgkmcnt(0).
 //  * Bank conflicts: the image stays lane-linear for the DMA; the 16-byte chunk index is XORed
 //    with (row & 15) on the global source address and on the ds_read_b128 address.
 //  * Top-k: with X as the A operand, a lane's accumulator column IS one query, so the running
 //    per-query threshold lives in a register and the sorted top-KMAX list in statically indexed
-//    registers; the insertion path runs only for lanes whose new scores beat their threshold
-//    (rare once the list is warm).
+//    registers.  The threshold can be SEEDED (thr_init) with a lower bound on the final k-th
+//    score from a sample pre-pass, which removes the record-breaking inserts that otherwise hit
+//    nearly every sub-tile of a fresh 64-list wave (profiles/r1_scan/README.md).
 //  * A second small kernel merges the per-workgroup candidate lists into the final top-k.
+//  * Profiling-only variants (index_scan_ablate): DMA-only, compute-only, L2-sourced DMA,
+//    staggered top-k, s_memtime segment stamps, and a 4-wave AGPR-resident "wide" kernel.
 #include "scan_common.h"
 
 #include <type_traits>
