@@ -51,31 +51,43 @@ def _sentences(n: int, seed: int, model: str) -> list[str]:
 
 
 def _client(url: str, queries: list[str], conc: int, out, endpoint: str = "search") -> None:
-    import httpx
+    """Raw asyncio HTTP/1.1 keep-alive client (httpx's per-request cost capped the first version
+    of this benchmark at ~420 req/s even on /api/health; one gateway worker serves ~6.5k req/s
+    of that endpoint to this client)."""
+    host, port = url.split("//")[1].split(":")
+    port = int(port)
+
+    async def conn_loop(qs, lat):
+        r, w = await asyncio.open_connection(host, port)
+        for q in qs:
+            if endpoint == "health":
+                req = b"GET /api/health HTTP/1.1\r\nHost: bench\r\n\r\n"
+            else:
+                body = json.dumps({"query_text": q, "top_k": 10}).encode()
+                req = (b"POST /api/search/semantic HTTP/1.1\r\nHost: bench\r\n"
+                       b"Content-Type: application/json\r\nContent-Length: "
+                       + str(len(body)).encode() + b"\r\n\r\n" + body)
+            t = time.perf_counter()
+            w.write(req)
+            await w.drain()
+            head = await r.readuntil(b"\r\n\r\n")
+            status = int(head.split(b" ", 2)[1])
+            n = 0
+            for line in head.split(b"\r\n"):
+                if line[:15].lower() == b"content-length:":
+                    n = int(line[15:])
+            await r.readexactly(n)
+            if status != 200:
+                raise RuntimeError(f"HTTP {status}")
+            lat.append(time.perf_counter() - t)
+        w.close()
 
     async def main():
-        lat = []
-        sem = asyncio.Semaphore(conc)
-        lim = httpx.Limits(max_connections=conc, max_keepalive_connections=conc)
-        async with httpx.AsyncClient(timeout=120, limits=lim) as c:
-            async def one(q):
-                async with sem:
-                    s = time.perf_counter()
-                    async def call():
-                        if endpoint == "health":   # calibration: HTTP stack only, no NATS hops
-                            return await c.get(url + "/api/health")
-                        return await c.post(url + "/api/search/semantic",
-                                            json={"query_text": q, "top_k": 10})
-                    try:
-                        r = await call()
-                    except httpx.TransportError:   # pooled-connection race: retry once (idempotent)
-                        r = await call()
-                    if r.status_code != 200:
-                        raise RuntimeError(r.text)
-                    lat.append(time.perf_counter() - s)
-            t0 = time.perf_counter()
-            await asyncio.gather(*(one(q) for q in queries))
-            return lat, t0, time.perf_counter()
+        lat: list[float] = []
+        t0 = time.perf_counter()
+        await asyncio.gather(*(conn_loop(queries[i::conc], lat) for i in range(conc)))
+        return lat, t0, time.perf_counter()
+
     try:
         out.put(asyncio.run(main()))
     except BaseException as e:   # never leave the parent waiting on a dead client
