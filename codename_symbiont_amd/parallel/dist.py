@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import os
 from dataclasses import dataclass
+from datetime import timedelta
 
 import torch
 import torch.distributed as dist
@@ -45,7 +46,10 @@ def init(backend: str | None = None, device_type: str | None = None) -> DistInfo
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29512")
         kw = {"device_id": device} if backend == "nccl" else {}
-        dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
+        # bounded collectives: a dead peer (e.g. a crashed index rank) surfaces as an error on the
+        # survivors -- the search handler then replies with error_message -- instead of a hang
+        timeout = timedelta(seconds=float(os.environ.get("SYMB_COLLECTIVE_TIMEOUT_S", "300")))
+        dist.init_process_group(backend=backend, rank=rank, world_size=world, timeout=timeout, **kw)
     return DistInfo(rank, world, local, device, backend if world > 1 else "none")
 
 

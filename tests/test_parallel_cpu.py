@@ -148,3 +148,48 @@ def test_index_group_snapshot_restore(tmp_path):
     assert out[(0, 0)] == 200 and out[(1, 0)] == 200      # 150 from the snapshot + 50 from the WAL
     assert out[(1, 1)] == 100                             # rank 1's shard restored, then WAL rows
     assert out["texts"] == ["t10", "t170", "t3-new"]
+
+
+def _dead_rank_worker(rank, world, port, out):
+    """Rank 1 dies while rank 0 runs a search: rank 0 must get an error, not hang."""
+    os.environ["SYMB_COLLECTIVE_TIMEOUT_S"] = "20"
+    import time
+
+    from codename_symbiont_amd.index.store import VectorStore
+    from codename_symbiont_amd.parallel import dist as D
+    from codename_symbiont_amd.parallel.index_group import IndexGroup
+    info = _init(rank, world, port)
+    grp = IndexGroup(info, dim=8, capacity_per_rank=100)
+    if rank == 1:
+        h = grp._header(0).tolist()          # the UPSERT op runs normally ...
+        v = grp._bcast(torch.empty(h[1], 8))
+        ot = grp._bcast(torch.empty(2, h[1], dtype=torch.int64))
+        grp._do_upsert(v, ot[0], ot[1])
+        grp._header(0)                       # ... then the SEARCH header arrives and the rank dies
+        os._exit(3)
+    from codename_symbiont_amd.index.shard import Payload
+    store = VectorStore(8, 0, group=grp)
+    store.upsert(["a", "b", "c", "d"], np.eye(4, 8, dtype=np.float32), [Payload()] * 4)
+    t0 = time.time()
+    try:
+        store.search(np.ones((1, 8), np.float32), 3)
+        out["result"] = "returned"
+    except Exception as e:     # noqa: BLE001 - any collective error is the expected outcome
+        out["result"] = type(e).__name__
+    out["seconds"] = time.time() - t0
+    os._exit(0)
+
+
+def test_dead_index_rank_errors_instead_of_hanging():
+    mgr = mp.Manager()
+    out = mgr.dict()
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    ps = [ctx.Process(target=_dead_rank_worker, args=(r, 2, port, out)) for r in range(2)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(120)
+    assert not any(p.is_alive() for p in ps)
+    assert out.get("result") not in (None, "returned"), out
+    assert out["seconds"] < 60
