@@ -291,8 +291,10 @@ class TorchEncoder:
         return self.forward_packed(pack_token_ids(token_lists, self.cfg))[0]
 
 
-def make_encoder(cfg: EncoderConfig, force_cpu: bool = False, seed: int = 0, device=None):
-    """GPU present -> HIP encoder (extension mandatory); otherwise the fp32 CPU backend."""
+def make_encoder(cfg: EncoderConfig, force_cpu: bool = False, seed: int = 0, device=None,
+                 precision: str = "bf16"):
+    """GPU present -> HIP encoder (extension mandatory; bf16 or fp8 GEMMs); otherwise the fp32
+    CPU backend."""
     if not force_cpu and torch.cuda.is_available():
-        return HipEncoder(cfg, seed=seed, device=device or "cuda")
+        return HipEncoder(cfg, seed=seed, device=device or "cuda", precision=precision)
     return TorchEncoder(cfg, seed=seed)

@@ -38,7 +38,8 @@ class PreprocessingService(Service):
         self.log.info("[EMBED_INIT] Initializing encoder %s (force_cpu: %s)", self.model_cfg.model_name,
                       self.cfg.force_cpu)
         self.encoder = encoder or make_encoder(self.model_cfg, force_cpu=self.cfg.force_cpu,
-                                               seed=self.cfg.model_seed)
+                                               seed=self.cfg.model_seed,
+                                               precision=self.cfg.encoder_dtype)
         self.tokenizer = Tokenizer(self.model_cfg, self.cfg.vocab_file or None)
         self.batcher = EmbedBatcher(self.encoder, self.tokenizer, self.cfg.batch_tokens,
                                     self.cfg.batch_window_ms, metrics=self.metrics)

@@ -61,6 +61,8 @@ class Config:
     index_capacity: int = field(default_factory=lambda: _int("SYMB_INDEX_CAPACITY", 1 << 22))
     # benchmarking only: pre-fill the index with N random unit rows (no payloads) at startup
     index_fill_random: int = field(default_factory=lambda: _int("SYMB_INDEX_FILL_RANDOM", 0))
+    # encoder projection GEMMs: "bf16" (default) or "fp8" (e4m3, per-channel/per-token scales)
+    encoder_dtype: str = field(default_factory=lambda: os.environ.get("SYMB_ENCODER_DTYPE", "bf16"))
     # "bf16" (default) or "fp8" (OCP e4m3 rows; needs a dim that is a multiple of 256)
     index_dtype: str = field(default_factory=lambda: os.environ.get("SYMB_INDEX_DTYPE", "bf16"))
     snapshot_dir: str = field(default_factory=lambda: _env("SYMB_SNAPSHOT_DIR", ""))
