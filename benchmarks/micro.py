@@ -69,10 +69,11 @@ def cmd_scan(a):
         variants = {}
         for ns in ((2, 3) if D == 384 else (0,)):
             for aux in (0, 2):
-                def f(ns=ns, aux=aux):
-                    h.index_scan(shard.rows.data_ptr(), a.rows, D, rpb, n_rblk, q.data_ptr(), a.nq,
-                                 kmax, cs.data_ptr(), ci.data_ptr(), st, ns, aux)
-                variants[f"blk{mult}x_ns{ns}_aux{aux}"] = f
+                for xcd in ((0, 1) if n_qblk > 1 else (0,)):
+                    def f(ns=ns, aux=aux, xcd=xcd):
+                        h.index_scan(shard.rows.data_ptr(), a.rows, D, rpb, n_rblk, q.data_ptr(),
+                                     a.nq, kmax, cs.data_ptr(), ci.data_ptr(), st, ns, aux, 0, xcd)
+                    variants[f"blk{mult}x_ns{ns}_aux{aux}_xcd{xcd}"] = f
         if mult == 1:
             def srch(seed):
                 shard.seed_threshold = seed

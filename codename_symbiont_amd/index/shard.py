@@ -103,6 +103,9 @@ class HbmIndexShard:
         self.scan_aux = -1   # index-stream cache policy (-1 = auto: non-temporal when read once)
         self.seed_threshold = True  # sample pre-pass seeds per-query top-k thresholds
         self.scan_variant = 0        # fp8 scan ring geometry (0 = default)
+        # > 256 queries: put the query blocks of each row block on one XCD (row stream shared
+        # through that XCD's L2 instead of re-read from HBM once per query block)
+        self.scan_xcd = 1
 
     # ------------------------------------------------------------------ inserts
     def _reserve(self, n: int) -> int:
@@ -270,11 +273,11 @@ class HbmIndexShard:
         if self.dtype == "fp8":
             h.index_scan_fp8(self.rows.data_ptr(), n, self.dim, rows_per_blk, n_rblk,
                              q_unit.data_ptr(), NQ, kmax, cs.data_ptr(), ci.data_ptr(), st,
-                             self.scan_aux, thr_p, self.scan_variant)
+                             self.scan_aux, thr_p, self.scan_variant, self.scan_xcd)
         else:
             h.index_scan(self.rows.data_ptr(), n, self.dim, rows_per_blk, n_rblk, q_unit.data_ptr(),
                          NQ, kmax, cs.data_ptr(), ci.data_ptr(), st, self.scan_ns, self.scan_aux,
-                         thr_p)
+                         thr_p, self.scan_xcd)
         h.topk_merge(cs.data_ptr(), ci.data_ptr(), NQ, ncand, kmax, k, out_s.data_ptr(),
                      out_i.data_ptr(), 0, 0, st)
         return out_s, out_i

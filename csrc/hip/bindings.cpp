@@ -36,7 +36,7 @@ int symb_attention(const void* qkv, int ld_qkv, const int32_t* cu, int B, int ma
 int symb_topk_geometry(int D, int kmax, int* lists, int* queries_per_blk);
 int symb_index_scan(const void* X, int n_valid, int D, int rows_per_blk, int n_rblk,
                     const void* Q, int NQ, int kmax, float* cand_s, int* cand_i, hipStream_t st,
-                    int ns, int aux, const float* thr_init);
+                    int ns, int aux, const float* thr_init, int xcd);
 int symb_index_scan_ablate(const void* X, int n_valid, int rows_per_blk, int n_rblk,
                            const void* Q, int NQ, float* cs, int* ci, hipStream_t st, int abl,
                            const float* thr);
@@ -50,7 +50,7 @@ int symb_quant_fp8(const void* in, int in_f32, int ld_in, uint8_t* out, int ld_o
                    float scale, int normalize, hipStream_t st);
 int symb_index_scan_fp8(const void* X, int n_valid, int D, int rows_per_blk, int n_rblk,
                         const void* Q, int NQ, int kmax, float* cand_s, int* cand_i,
-                        hipStream_t st, int aux, const float* thr_init, int variant);
+                        hipStream_t st, int aux, const float* thr_init, int variant, int xcd);
 int symb_topk_merge(const float* cand_s, const int* cand_i, int NQ, int n_cand_per_query,
                     int kmax, int k, float* out_s, int* out_i, int64_t id_offset,
                     int64_t* out_id64, hipStream_t st);
@@ -257,13 +257,16 @@ PYBIND11_MODULE(_hip, m) {
     return py::make_tuple(lists, qpb);
   });
   m.def("index_scan", [](uptr X, int n_valid, int D, int rows_per_blk, int n_rblk, uptr Q, int NQ,
-                         int kmax, uptr cand_s, uptr cand_i, uptr st, int ns, int aux, uptr thr) {
+                         int kmax, uptr cand_s, uptr cand_i, uptr st, int ns, int aux, uptr thr,
+                         int xcd) {
     check(symb_index_scan(P<void>(X), n_valid, D, rows_per_blk, n_rblk, P<void>(Q), NQ, kmax,
-                          P<float>(cand_s), P<int>(cand_i), S(st), ns, aux, P<const float>(thr)),
+                          P<float>(cand_s), P<int>(cand_i), S(st), ns, aux, P<const float>(thr),
+                          xcd),
           "index_scan");
   }, py::arg("X"), py::arg("n_valid"), py::arg("D"), py::arg("rows_per_blk"), py::arg("n_rblk"),
      py::arg("Q"), py::arg("NQ"), py::arg("kmax"), py::arg("cand_s"), py::arg("cand_i"),
-     py::arg("stream"), py::arg("ns") = 0, py::arg("aux") = -1, py::arg("thr_init") = 0);
+     py::arg("stream"), py::arg("ns") = 0, py::arg("aux") = -1, py::arg("thr_init") = 0,
+     py::arg("xcd") = 1);
   m.def("index_scan_ablate", [](uptr X, int n_valid, int rows_per_blk, int n_rblk, uptr Q, int NQ,
                                 uptr cs, uptr ci, uptr st, int abl, uptr thr) {
     check(symb_index_scan_ablate(P<void>(X), n_valid, rows_per_blk, n_rblk, P<void>(Q), NQ,
@@ -293,14 +296,15 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("index_scan_fp8", [](uptr X, int n_valid, int D, int rows_per_blk, int n_rblk, uptr Q,
                              int NQ, int kmax, uptr cand_s, uptr cand_i, uptr st, int aux, uptr thr,
-                             int variant) {
+                             int variant, int xcd) {
     check(symb_index_scan_fp8(P<void>(X), n_valid, D, rows_per_blk, n_rblk, P<void>(Q), NQ, kmax,
                               P<float>(cand_s), P<int>(cand_i), S(st), aux, P<const float>(thr),
-                              variant),
+                              variant, xcd),
           "index_scan_fp8");
   }, py::arg("X"), py::arg("n_valid"), py::arg("D"), py::arg("rows_per_blk"), py::arg("n_rblk"),
      py::arg("Q"), py::arg("NQ"), py::arg("kmax"), py::arg("cand_s"), py::arg("cand_i"),
-     py::arg("stream"), py::arg("aux") = -1, py::arg("thr_init") = 0, py::arg("variant") = 0);
+     py::arg("stream"), py::arg("aux") = -1, py::arg("thr_init") = 0, py::arg("variant") = 0,
+     py::arg("xcd") = 1);
   m.def("topk_merge", [](uptr cand_s, uptr cand_i, int NQ, int n_cand, int kmax, int k,
                          uptr out_s, uptr out_i, int64_t id_offset, uptr out_id64, uptr st) {
     check(symb_topk_merge(P<float>(cand_s), P<int>(cand_i), NQ, n_cand, kmax, k, P<float>(out_s),

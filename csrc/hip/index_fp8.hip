@@ -122,7 +122,7 @@ struct Fp8Chain {
 template <int D, int KMAX, int NS, int SUBS, int AUX>
 __global__ __launch_bounds__(256, 1) void index_scan_fp8_kernel(
     const uint8_t* __restrict__ X, int n_valid, int rows_per_blk, const uint8_t* __restrict__ Q,
-    int NQ, int n_qblk, const float* __restrict__ thr_init, float* __restrict__ cand_s,
+    int NQ, int n_qblk, int xcd, const float* __restrict__ thr_init, float* __restrict__ cand_s,
     int* __restrict__ cand_i) {
   constexpr int CPR = D / 16, SUB = 32, TR = 32 * SUBS, NW = 4;
   constexpr int TILE_BYTES = TR * D, SUB_BYTES = SUB * D;
@@ -134,7 +134,8 @@ __global__ __launch_bounds__(256, 1) void index_scan_fp8_kernel(
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int qb = blockIdx.x % n_qblk, rb = blockIdx.x / n_qblk;
+  const int lb = xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;  // L2-shared row stream
+  const int qb = lb % n_qblk, rb = lb / n_qblk;
   const int row_begin = rb * rows_per_blk;
   const int row_end = min(row_begin + rows_per_blk, n_valid);
   const int n_tiles = row_end > row_begin ? (row_end - row_begin + TR - 1) / TR : 0;
@@ -277,7 +278,8 @@ int symb_quant_fp8(const void* in, int in_f32, int ld_in, uint8_t* out, int ld_o
 
 template <int D, int KMAX, int NS, int SUBS, int AUX>
 static int launch_fp8(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
-                      int NQ, int n_qblk, const float* thr, float* cs, int* ci, hipStream_t st) {
+                      int NQ, int n_qblk, int xcd, const float* thr, float* cs, int* ci,
+                      hipStream_t st) {
   auto kern = index_scan_fp8_kernel<D, KMAX, NS, SUBS, AUX>;
   constexpr int lds = NS * 32 * SUBS * D;
   static bool attr = false;
@@ -286,7 +288,7 @@ static int launch_fp8(const void* X, int n_valid, int rows_per_blk, int n_rblk, 
     attr = true;
   }
   hipLaunchKernelGGL(kern, dim3(n_rblk * n_qblk), dim3(256), lds, st, (const uint8_t*)X, n_valid,
-                     rows_per_blk, (const uint8_t*)Q, NQ, n_qblk, thr, cs, ci);
+                     rows_per_blk, (const uint8_t*)Q, NQ, n_qblk, xcd, thr, cs, ci);
   return (int)hipGetLastError();
 }
 
@@ -298,11 +300,11 @@ template <> struct Fp8Cfg<512> { static constexpr int SUBS = 2, NS = 4; };   // 
 
 template <int D>
 static int dispatch_fp8(int kmax, int aux, int variant, const void* X, int n_valid,
-                        int rows_per_blk, int n_rblk, const void* Q, int NQ, int n_qblk,
+                        int rows_per_blk, int n_rblk, const void* Q, int NQ, int n_qblk, int xcd,
                         const float* thr, float* cs, int* ci, hipStream_t st) {
   constexpr int SUBS = Fp8Cfg<D>::SUBS, NS = Fp8Cfg<D>::NS;
 #define SYMB_F(K, NS_, SUBS_, A) \
-  launch_fp8<D, K, NS_, SUBS_, A>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, n_qblk, thr, cs, ci, st)
+  launch_fp8<D, K, NS_, SUBS_, A>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, n_qblk, xcd, thr, cs, ci, st)
   if constexpr (D == 1024)  // variant 1: one sub-tile per barrier, 4-deep ring (-4 % at 100M rows)
     if (variant == 1) return aux ? SYMB_F(16, 4, 1, 2) : SYMB_F(16, 4, 1, 0);
   if (kmax == 16) return aux ? SYMB_F(16, NS, SUBS, 2) : SYMB_F(16, NS, SUBS, 0);
@@ -316,12 +318,12 @@ static int dispatch_fp8(int kmax, int aux, int variant, const void* X, int n_val
 // variant: 0 = default ring geometry, 1 = D=1024 with 1 sub-tile/barrier and a 4-deep ring.
 int symb_index_scan_fp8(const void* X, int n_valid, int D, int rows_per_blk, int n_rblk,
                         const void* Q, int NQ, int kmax, float* cand_s, int* cand_i,
-                        hipStream_t st, int aux, const float* thr_init, int variant) {
+                        hipStream_t st, int aux, const float* thr_init, int variant, int xcd) {
   if (NQ <= 0 || n_rblk <= 0) return 0;
   if (rows_per_blk % 64) return -1;
   const int n_qblk = (NQ + 255) / 256;
   if (aux < 0) aux = n_qblk == 1 ? 2 : 0;
-#define SYMB_ARGS kmax, aux, variant, X, n_valid, rows_per_blk, n_rblk, Q, NQ, n_qblk, thr_init, \
+#define SYMB_ARGS kmax, aux, variant, X, n_valid, rows_per_blk, n_rblk, Q, NQ, n_qblk, xcd, thr_init, \
                   cand_s, cand_i, st
   switch (D) {
     case 512: return dispatch_fp8<512>(SYMB_ARGS);

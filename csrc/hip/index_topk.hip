@@ -93,7 +93,7 @@ __device__ __forceinline__ void frag_prologue(bf16x8 (&a)[R], const uint32_t (&v
 template <int D, bool MFMA_32, int KMAX, int NS, int AUX, int ABLX = 0>
 __global__ __launch_bounds__(512) void index_scan_topk_kernel(
     const __bf16* __restrict__ X, int n_valid, int rows_per_blk, const __bf16* __restrict__ Q,
-    int NQ, int n_qblk, const float* __restrict__ thr_init, float* __restrict__ cand_s,
+    int NQ, int n_qblk, int xcd, const float* __restrict__ thr_init, float* __restrict__ cand_s,
     int* __restrict__ cand_i) {
   constexpr bool STAMP = ABLX >= 8;
   constexpr int ABL = ABLX == 8 ? 0 : ABLX == 9 ? 5 : ABLX == 10 ? 2 : ABLX;
@@ -129,7 +129,11 @@ __global__ __launch_bounds__(512) void index_scan_topk_kernel(
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int qb = blockIdx.x % n_qblk, rb = blockIdx.x / n_qblk;
+  // xcd != 0: the n_qblk query blocks of one row block are consecutive logical ids on ONE XCD, so
+  // the row block streams from HBM into that XCD's L2 once and feeds all of its query blocks
+  // (without it, round-robin dispatch puts them on n_qblk different XCDs: n_qblk HBM reads).
+  const int lb = xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int qb = lb % n_qblk, rb = lb / n_qblk;
   const int row_begin = rb * rows_per_blk;
   const int row_end = min(row_begin + rows_per_blk, n_valid);
   const int n_tiles = row_end > row_begin ? (row_end - row_begin + TR - 1) / TR : 0;
@@ -357,7 +361,7 @@ struct FragChain2 {
 template <int KMAX, int NS, int AUX>
 __global__ __launch_bounds__(256, 1) void index_scan_wide_kernel(
     const __bf16* __restrict__ X, int n_valid, int rows_per_blk, const __bf16* __restrict__ Q,
-    int NQ, int n_qblk, const float* __restrict__ thr_init, float* __restrict__ cand_s,
+    int NQ, int n_qblk, int xcd, const float* __restrict__ thr_init, float* __restrict__ cand_s,
     int* __restrict__ cand_i) {
   constexpr int D = 384, CPR = D / 8, SUB = 32, TR = 64, NW = 4;
   constexpr int TILE_BYTES = TR * D * 2, SUB_BYTES = SUB * D * 2;
@@ -368,7 +372,8 @@ __global__ __launch_bounds__(256, 1) void index_scan_wide_kernel(
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int qb = blockIdx.x % n_qblk, rb = blockIdx.x / n_qblk;
+  const int lb = xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int qb = lb % n_qblk, rb = lb / n_qblk;
   const int row_begin = rb * rows_per_blk;
   const int row_end = min(row_begin + rows_per_blk, n_valid);
   const int n_tiles = row_end > row_begin ? (row_end - row_begin + TR - 1) / TR : 0;
@@ -572,7 +577,8 @@ int symb_topk_geometry(int D, int kmax, int* lists, int* queries_per_blk) {
 
 template <int D, bool M32, int KMAX, int NS, int AUX>
 static int launch_scan(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
-                       int NQ, int n_qblk, const float* thr, float* cs, int* ci, hipStream_t st) {
+                       int NQ, int n_qblk, int xcd, const float* thr, float* cs, int* ci,
+                       hipStream_t st) {
   auto kern = index_scan_topk_kernel<D, M32, KMAX, NS, AUX>;
   constexpr int lds = NS * (M32 ? 64 : 32) * D * 2;
   static bool attr = false;
@@ -581,7 +587,7 @@ static int launch_scan(const void* X, int n_valid, int rows_per_blk, int n_rblk,
     attr = true;
   }
   hipLaunchKernelGGL(kern, dim3(n_rblk * n_qblk), dim3(512), lds, st, (const __bf16*)X, n_valid,
-                     rows_per_blk, (const __bf16*)Q, NQ, n_qblk, thr, cs, ci);
+                     rows_per_blk, (const __bf16*)Q, NQ, n_qblk, xcd, thr, cs, ci);
   return (int)hipGetLastError();
 }
 
@@ -594,7 +600,7 @@ int symb_index_scan_ablate(const void* X, int n_valid, int rows_per_blk, int n_r
     constexpr int lds = 3 * 64 * 384 * 2;
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipLaunchKernelGGL(kern, dim3(n_rblk * n_qblk), dim3(512), lds, st, (const __bf16*)X, n_valid,
-                       rows_per_blk, (const __bf16*)Q, NQ, n_qblk, thr, cs, ci);
+                       rows_per_blk, (const __bf16*)Q, NQ, n_qblk, 0, thr, cs, ci);
     return (int)hipGetLastError();
   };
   if (abl == 3) {
@@ -602,7 +608,7 @@ int symb_index_scan_ablate(const void* X, int n_valid, int rows_per_blk, int n_r
     constexpr int lds = 3 * 64 * 384 * 2;
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipLaunchKernelGGL(kern, dim3(n_rblk * n_qblk), dim3(256), lds, st, (const __bf16*)X, n_valid,
-                       rows_per_blk, (const __bf16*)Q, NQ, n_qblk, thr, cs, ci);
+                       rows_per_blk, (const __bf16*)Q, NQ, n_qblk, 0, thr, cs, ci);
     return (int)hipGetLastError();
   }
   if (abl == 1) return go(index_scan_topk_kernel<384, true, 16, 3, 0, 1>);
@@ -623,10 +629,10 @@ template <> struct ScanCfg<1024> { static constexpr bool M32 = false; static con
 
 template <int D, int NS>
 static int dispatch_k(int kmax, int aux, const void* X, int n_valid, int rows_per_blk, int n_rblk,
-                      const void* Q, int NQ, int n_qblk, const float* thr, float* cs, int* ci,
-                      hipStream_t st) {
+                      const void* Q, int NQ, int n_qblk, int xcd, const float* thr, float* cs,
+                      int* ci, hipStream_t st) {
   constexpr bool M32 = ScanCfg<D>::M32;
-#define SYMB_L(K, A) launch_scan<D, M32, K, NS, A>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, n_qblk, thr, cs, ci, st)
+#define SYMB_L(K, A) launch_scan<D, M32, K, NS, A>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, n_qblk, xcd, thr, cs, ci, st)
   if (kmax == 16) return aux ? SYMB_L(16, 2) : SYMB_L(16, 0);
   return aux ? SYMB_L(32, 2) : SYMB_L(32, 0);
 #undef SYMB_L
@@ -636,16 +642,17 @@ static int dispatch_k(int kmax, int aux, const void* X, int n_valid, int rows_pe
 // rows_per_blk must be a multiple of 64; n_rblk * rows_per_blk >= n_valid.
 // ns = 0 -> default ring depth; aux = -1 -> non-temporal iff each index row is read by one block.
 // thr_init: optional [NQ] per-query lower bounds on the final k-th score (nullptr = none).
+// xcd: group the query blocks of each row block on one XCD (L2-shared row stream; NQ > 256).
 int symb_index_scan(const void* X, int n_valid, int D, int rows_per_blk, int n_rblk,
                     const void* Q, int NQ, int kmax, float* cand_s, int* cand_i, hipStream_t st,
-                    int ns, int aux, const float* thr_init) {
+                    int ns, int aux, const float* thr_init, int xcd) {
   if (NQ <= 0 || n_rblk <= 0) return 0;
   if (rows_per_blk % 64) return -1;
   int lists, qpb;
   if (symb_topk_geometry(D, kmax, &lists, &qpb)) return -1;
   const int n_qblk = (NQ + qpb - 1) / qpb;
   if (aux < 0) aux = n_qblk == 1 ? 2 : 0;
-#define SYMB_ARGS kmax, aux, X, n_valid, rows_per_blk, n_rblk, Q, NQ, n_qblk, thr_init, cand_s, cand_i, st
+#define SYMB_ARGS kmax, aux, X, n_valid, rows_per_blk, n_rblk, Q, NQ, n_qblk, xcd, thr_init, cand_s, cand_i, st
   if (D == 384) {
     if (ns == 0 || ns == 3) return dispatch_k<384, 3>(SYMB_ARGS);
     if (ns == 2) return dispatch_k<384, 2>(SYMB_ARGS);
