@@ -23,13 +23,13 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 async def run(a) -> dict:
-    from codename_symbiont_amd.bus import Broker
+    from codename_symbiont_amd.bus.broker import BROKERS
     from codename_symbiont_amd.bus.client import NatsClient
     from codename_symbiont_amd.services.text_generator import TextGeneratorService
     from codename_symbiont_amd.utils.config import Config
     from codename_symbiont_amd.wire import GeneratedTextMessage, GenerateTextTask, subjects
 
-    b = await Broker().start()
+    b = await BROKERS[a.broker]().start()
     cfg = Config()
     cfg.nats_url = b.url
     cfg.fault_spec = ""
@@ -77,13 +77,14 @@ async def run(a) -> dict:
         "words_per_sec": round(words / elapsed, 1),
         "latency_ms": {"p50": round(1e3 * statistics.median(lat), 3),
                        "p99": round(1e3 * lat[int(0.99 * (len(lat) - 1))], 3)},
-        "config": {"model": "word-bigram Markov (reference corpus)", "transport": "in-process NATS broker, TCP loopback"},
+        "config": {"model": "word-bigram Markov (reference corpus)", "transport": f"in-process {a.broker} NATS broker, TCP loopback"},
     }
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tasks", type=int, default=20000)
+    ap.add_argument("--broker", choices=["native", "py"], default="native")
     ap.add_argument("--inflight", type=int, default=64)
     ap.add_argument("--max-length", type=int, default=50)
     a = ap.parse_args()

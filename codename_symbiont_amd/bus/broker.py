@@ -8,7 +8,15 @@ nats-server), and no-responders status messages (``NATS/1.0 503``) for requests 
 subscriber when the client negotiated headers + no_responders.  At-most-once, no persistence --
 exactly NATS core semantics (no JetStream in the reference).
 
-Run standalone: ``python -m codename_symbiont_amd.bus.broker --port 4222``.
+Two implementations with the same interface (``await start()``, ``url``, ``port``, ``stats``,
+``await stop()``):
+
+* ``NativeBroker`` (default, ``Broker``): the C++ epoll server in ``csrc/native/natsd.cpp``, run on
+  its own thread without the GIL -- what ``launch.py`` deploys.
+* ``PyBroker``: this asyncio implementation, kept as the executable specification the native
+  server is tested against (``tests/test_bus_cpu.py`` runs every bus test on both).
+
+Run standalone: ``python -m codename_symbiont_amd.bus.broker --port 4222 [--impl native|py]``.
 """
 from __future__ import annotations
 
@@ -66,7 +74,7 @@ class _Sub:
 class _Conn:
     _ids = itertools.count(1)
 
-    def __init__(self, broker: "Broker", reader, writer):
+    def __init__(self, broker: "PyBroker", reader, writer):
         self.id = next(self._ids)
         self.broker = broker
         self.reader = reader
@@ -101,7 +109,7 @@ class _Conn:
             pass
 
 
-class Broker:
+class PyBroker:
     def __init__(self, host: str = "127.0.0.1", port: int = 0, max_payload: int = 1 << 20):
         self.host = host
         self.port = port
@@ -118,7 +126,7 @@ class Broker:
     def url(self) -> str:
         return f"nats://{self.host}:{self.port}"
 
-    async def start(self) -> "Broker":
+    async def start(self) -> "PyBroker":
         self._server = await asyncio.start_server(self._handle, self.host, self.port)
         self.port = self._server.sockets[0].getsockname()[1]
         log.info("[BROKER] listening on %s", self.url)
@@ -180,7 +188,7 @@ class Broker:
                 "proto": 1, "go": "n/a", "host": self.host, "port": self.port, "headers": True,
                 "max_payload": self.max_payload, "client_id": c.id}
         c.send(b"INFO " + json.dumps(info, separators=(",", ":")).encode() + b"\r\n")
-        parser = native().NatsParser(4096, 64 << 20)
+        parser = native().NatsParser(4096, self.max_payload)  # size checked on the PUB line
         try:
             while not c.closed:
                 chunk = await reader.read(1 << 20)
@@ -223,9 +231,12 @@ class Broker:
             if not subject_valid(subject, wildcards=False):
                 c.send(b"-ERR 'Invalid Publish Subject'\r\n")
                 return
+            if c.verbose:
+                c.send(b"+OK\r\n")   # nats-server acks a verbose PUB before routing it
             self.stats["in_msgs"] += 1
             self.stats["in_bytes"] += len(payload)
             self.route(subject, reply, hdr, payload, c)
+            return
         elif op == "SUB":
             _, subject, queue, sid = ev
             if not subject_valid(subject, wildcards=True):
@@ -252,14 +263,55 @@ class Broker:
             c.send(b"+OK\r\n")
 
 
+class NativeBroker:
+    """The C++ NATS server (``_native.NatsServer``) behind the asyncio broker interface."""
+
+    def __init__(self, host: str = "127.0.0.1", port: int = 0, max_payload: int = 1 << 20,
+                 max_pending: int = 64 << 20):
+        self.host = host
+        self.port = port
+        self.max_payload = max_payload
+        self._srv = native().NatsServer(host, port, max_payload, max_pending)
+
+    @property
+    def url(self) -> str:
+        return f"nats://{self.host}:{self.port}"
+
+    @property
+    def stats(self) -> dict:
+        return self._srv.stats()
+
+    async def start(self) -> "NativeBroker":
+        self._srv.start()   # binds + listens synchronously (errors raise here), then loops on a thread
+        self.port = self._srv.port
+        log.info("[BROKER] native server listening on %s", self.url)
+        return self
+
+    async def stop(self) -> None:
+        self._srv.stop()
+
+    async def serve_forever(self) -> None:
+        await self.start()
+        try:
+            while self._srv.running:
+                await asyncio.sleep(3600)
+        finally:
+            await self.stop()
+
+
+Broker = NativeBroker
+BROKERS = {"native": NativeBroker, "py": PyBroker}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser(description="symbiont in-repo NATS broker")
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--port", type=int, default=4222)
     ap.add_argument("--max-payload", type=int, default=1 << 20)
+    ap.add_argument("--impl", choices=sorted(BROKERS), default="native")
     a = ap.parse_args()
     logging.basicConfig(level=logging.INFO)
-    asyncio.run(Broker(a.host, a.port, a.max_payload).serve_forever())
+    asyncio.run(BROKERS[a.impl](a.host, a.port, a.max_payload).serve_forever())
 
 
 if __name__ == "__main__":

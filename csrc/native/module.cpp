@@ -9,13 +9,16 @@ void register_nats(py::module_& m);
 void register_text(py::module_& m);
 void register_html(py::module_& m);
 void register_packstream(py::module_& m);
+void register_natsd(py::module_& m);
 }  // namespace symbn
 
 PYBIND11_MODULE(_native, m) {
-  m.doc() = "codename_symbiont_amd host cores: JSON wire codec, NATS protocol, text, HTML, PackStream";
+  m.doc() = "codename_symbiont_amd host cores: JSON wire codec, NATS protocol + server, text, HTML, "
+            "PackStream";
   symbn::register_json(m);
   symbn::register_nats(m);
   symbn::register_text(m);
   symbn::register_html(m);
   symbn::register_packstream(m);
+  symbn::register_natsd(m);
 }

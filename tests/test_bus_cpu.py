@@ -3,8 +3,15 @@ import asyncio
 
 import pytest
 
-from codename_symbiont_amd.bus import Broker, NatsClient, NoRespondersError, RequestTimeoutError
-from codename_symbiont_amd.bus.broker import subject_matches, subject_valid
+from codename_symbiont_amd.bus import NatsClient, NoRespondersError, RequestTimeoutError
+from codename_symbiont_amd.bus.broker import BROKERS, subject_matches, subject_valid
+from codename_symbiont_amd.ops._ext import native
+
+
+@pytest.fixture(params=sorted(BROKERS))
+def Broker(request):
+    """Every bus test runs against the native C++ server and the asyncio reference broker."""
+    return BROKERS[request.param]
 
 
 def run(coro):
@@ -17,9 +24,17 @@ def test_subject_rules():
     assert m("a.>", "a.b.c") and not m("a.>", "a") and m(">", "x")
     assert subject_valid("a.b", False) and not subject_valid("a.*", False) and subject_valid("a.*", True)
     assert not subject_valid("a..b", True) and not subject_valid("a.>.c", True)
+    # the native server applies the same rules
+    N = native()
+    for subj, wild in [("a.b", False), ("a.*", False), ("a.*", True), ("a..b", True),
+                       ("a.>.c", True), (">", True), ("a b", False), ("", True), ("a.", True)]:
+        assert N.nats_subject_valid(subj, wild) == subject_valid(subj, wild), (subj, wild)
+    for pat, subj in [("a.*.c", "a.b.c"), ("a.*.c", "a.b.d"), ("a.*", "a.b.c"), ("a.>", "a.b.c"),
+                      ("a.>", "a"), (">", "x"), ("a.b", "a.b"), ("a.b", "a.b.c")]:
+        assert N.nats_subject_matches(pat, subj) == subject_matches(pat.split("."), subj.split("."))
 
 
-def test_pubsub_queue_groups_request_reply():
+def test_pubsub_queue_groups_request_reply(Broker):
     async def main():
         b = await Broker().start()
         a = await NatsClient.connect(b.url)
@@ -75,7 +90,7 @@ def test_pubsub_queue_groups_request_reply():
     run(main())
 
 
-def test_max_payload_and_reconnect_resubscribe():
+def test_max_payload_and_reconnect_resubscribe(Broker):
     async def main():
         b = await Broker(max_payload=1000).start()
         port = b.port
@@ -101,4 +116,83 @@ def test_max_payload_and_reconnect_resubscribe():
         await a.close()
         await c.close()
         await b2.stop()
+    run(main())
+
+
+async def _raw(port):
+    r, w = await asyncio.open_connection("127.0.0.1", port)
+    info = await r.readline()
+    assert info.startswith(b"INFO {") and b'"headers":true' in info
+    return r, w
+
+
+def test_raw_protocol_semantics(Broker):
+    """Wire-level behaviour a NATS client relies on, identical on both brokers."""
+    async def main():
+        b = await Broker(max_payload=64).start()
+        r, w = await _raw(b.port)
+        w.write(b'CONNECT {"verbose":true,"headers":true,"no_responders":true,"name":"t",'
+                b'"opts":{"x":[1,2,{"y":null}]},"lang":"py"}\r\n')
+        assert await r.readline() == b"+OK\r\n"
+        w.write(b"PING\r\n")
+        assert await r.readline() == b"PONG\r\n"
+        w.write(b"SUB in.* 7\r\nPUB in.x rep 5\r\nhello\r\n")
+        assert await r.readline() == b"+OK\r\n"
+        assert await r.readline() == b"+OK\r\n"
+        assert await r.readline() == b"MSG in.x 7 rep 5\r\n"
+        assert await r.readline() == b"hello\r\n"
+        w.write(b"HPUB in.y 12 14\r\nNATS/1.0\r\n\r\nhi\r\n")
+        assert await r.readline() == b"+OK\r\n"
+        assert await r.readline() == b"HMSG in.y 7 12 14\r\n"
+        assert await r.readexactly(16) == b"NATS/1.0\r\n\r\nhi\r\n"
+        # request to nobody -> no-responders status on the reply subject
+        w.write(b"SUB _INBOX.q 9\r\nPUB nobody _INBOX.q 0\r\n\r\n")
+        assert await r.readline() == b"+OK\r\n"
+        assert await r.readline() == b"+OK\r\n"
+        assert await r.readline() == b"HMSG _INBOX.q 9 16 16\r\n"
+        assert await r.readexactly(18) == b"NATS/1.0 503\r\n\r\n\r\n"
+        w.write(b"PUB bad.* 1\r\nx\r\n")
+        assert await r.readline() == b"-ERR 'Invalid Publish Subject'\r\n"
+        w.write(b"PUB big 65\r\n")
+        assert await r.readline() == b"-ERR 'Maximum Payload Violation'\r\n"
+        assert await r.read() == b""                       # ... and the connection is closed
+        w.close()
+        r2, w2 = await _raw(b.port)
+        w2.write(b"BOGUS\r\n")
+        assert (await r2.readline()).startswith(b"-ERR 'Unknown Protocol Operation'")
+        w2.close()
+        await b.stop()
+    run(main())
+
+
+def test_native_broker_fanout_and_stats():
+    """Many publishers x subscribers through the C++ server: every plain subscriber sees every
+    message in publish order per publisher; queue-group members split the stream exactly."""
+    async def main():
+        b = await BROKERS["native"]().start()
+        subs_c = [await NatsClient.connect(b.url) for _ in range(4)]
+        pubs_c = [await NatsClient.connect(b.url) for _ in range(3)]
+        plain = [await c.subscribe("fan.>") for c in subs_c]
+        group = [await c.subscribe("fan.q", queue="g") for c in subs_c]
+        await asyncio.gather(*[c.flush() for c in subs_c])
+        N = 300
+        for i in range(N):
+            for j, p in enumerate(pubs_c):
+                await p.publish("fan.q", f"{j}:{i}".encode())
+        await asyncio.gather(*[p.flush() for p in pubs_c])
+        for s in plain:
+            got = [(await s.next_msg(5)).data.decode() for _ in range(N * len(pubs_c))]
+            for j in range(len(pubs_c)):
+                assert [int(x.split(":")[1]) for x in got if x.startswith(f"{j}:")] == list(range(N))
+        await asyncio.sleep(0.2)
+        assert sum(g._q.qsize() for g in group) == N * len(pubs_c)
+        st = b.stats
+        assert st["in_msgs"] == N * len(pubs_c)
+        assert st["out_msgs"] == N * len(pubs_c) * (len(plain) + 1)
+        assert st["connections"] == len(subs_c) + len(pubs_c)
+        for c in subs_c + pubs_c:
+            await c.close()
+        await asyncio.sleep(0.1)
+        assert b.stats["connections"] == 0 and b.stats["subscriptions"] == 0
+        await b.stop()
     run(main())
