@@ -26,6 +26,10 @@ namespace symb {
 enum { EPI_BIAS = 0, EPI_GELU = 1, EPI_RES = 2, EPI_RES_LN = 3 };
 
 constexpr int GEMM_BK = 64;  // bf16 elements per k-tile (128-byte rows)
+#ifndef SYMB_GEMM_SCHED
+#define SYMB_GEMM_SCHED 1
+#endif
+constexpr bool GEMM_SCHED = SYMB_GEMM_SCHED;  // pinned read/MFMA interleave (0: compiler's own)
 
 __device__ __forceinline__ int swz_off(int row, int chunk) {
   return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
@@ -189,22 +193,38 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
           acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[i], b[j], acc[i][j], 0, 0,
                                                                        0, 127, 0, 127);
     } else {
+      // Both k-halves' fragments are read up front and the schedule is pinned: the 8 reads of
+      // half 1 are interleaved with half 0's MFMAs (2 MFMAs per read), so only half 0's LDS
+      // latency is exposed after each barrier (the compiler's own schedule waited lgkmcnt(0)
+      // every 8 MFMAs; profiles/r1_gemm).
+      bf16x8 a[2][RM], b[2][RN];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int chunk = kk * 4 + (lane >> 4);
-      bf16x8 a[RM], b[RN];
+      for (int kk = 0; kk < 2; ++kk) {
+        const int chunk = kk * 4 + (lane >> 4);
 #pragma unroll
-      for (int i = 0; i < RM; ++i)
-        a[i] = *reinterpret_cast<const bf16x8*>(sA + swz_off(wm * WTM + i * 16 + (lane & 15), chunk));
-#pragma unroll
-      for (int j = 0; j < RN; ++j)
-        b[j] = *reinterpret_cast<const bf16x8*>(sB + swz_off(wn * WTN + j * 16 + (lane & 15), chunk));
-#pragma unroll
-      for (int i = 0; i < RM; ++i)
+        for (int i = 0; i < RM; ++i)
+          a[kk][i] = *reinterpret_cast<const bf16x8*>(sA + swz_off(wm * WTM + i * 16 + (lane & 15), chunk));
 #pragma unroll
         for (int j = 0; j < RN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-    }
+          b[kk][j] = *reinterpret_cast<const bf16x8*>(sB + swz_off(wn * WTN + j * 16 + (lane & 15), chunk));
+      }
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int j = 0; j < RN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kk][i], b[kk][j], acc[i][j], 0, 0, 0);
+      if constexpr (GEMM_SCHED) {
+        constexpr int NR = RM + RN, NM = RM * RN;
+        __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);        // half 0 reads
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          __builtin_amdgcn_sched_group_barrier(0x008, NM / NR, 0);  // half 0 MFMAs ...
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);        // ... with half 1 reads
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);         // half 1 MFMAs
+      }
     }
   }
 
