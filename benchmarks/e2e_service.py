@@ -122,6 +122,9 @@ def main():
     ap.add_argument("--clients", type=int, default=4)
     ap.add_argument("--concurrency", type=int, default=64, help="in-flight requests per client")
     ap.add_argument("--api-workers", type=int, default=4)
+    ap.add_argument("--api-impl", choices=["native", "py"], default="native",
+                    help="native: C++ gateway (worker threads); py: asyncio gateway (worker processes)")
+    ap.add_argument("--broker-impl", choices=["native", "py"], default="native")
     ap.add_argument("--endpoint", choices=["search", "health"], default="search")
     a = ap.parse_args()
     py = sys.executable
@@ -132,12 +135,13 @@ def main():
                SYMB_MODEL=a.model, SYMB_INDEX_FILL_RANDOM=str(a.index_rows),
                SYMB_INDEX_CAPACITY=str(a.index_rows + a.docs * a.sentences + 4096),
                SYMB_LOG="warning", RUST_LOG="warning", SYMB_METRICS_INTERVAL="0.1",
-               SYMB_API_WORKERS=str(a.api_workers),
+               SYMB_API_WORKERS=str(a.api_workers), SYMB_API_IMPL=a.api_impl,
                HSA_ENABLE_IPC_MODE_LEGACY="0")
     import signal
 
     signal.signal(signal.SIGTERM, lambda *_: sys.exit(1))   # a timeout still runs the cleanup
-    procs = [subprocess.Popen([py, "-m", "codename_symbiont_amd.bus.broker", "--port", str(bport)],
+    procs = [subprocess.Popen([py, "-m", "codename_symbiont_amd.bus.broker", "--port", str(bport),
+                               "--impl", a.broker_impl],
                               env=env, cwd=ROOT, start_new_session=True)]
     time.sleep(0.5)
     for s in ("preprocessing", "vector_memory", "api"):
@@ -220,8 +224,8 @@ def main():
         "config": {"model": a.model, "index_rows": a.index_rows + a.docs * a.sentences,
                    "docs": a.docs, "sentences_per_doc": a.sentences, "requests": len(lat),
                    "clients": a.clients, "concurrency_per_client": a.concurrency, "top_k": 10,
-                   "deployment": f"broker + preprocessing + vector_memory + {a.api_workers} api "
-                                 "worker processes"},
+                   "deployment": f"{a.broker_impl} broker + preprocessing + vector_memory + "
+                                 f"{a.api_impl} gateway x {a.api_workers} workers"},
         "endpoint": a.endpoint,
         "gateway_hops_ms": m.get("api_service", {}).get("latency_ms", {}),
         "data": "synthetic sentences over the synthetic vocabulary, random-init weights",

@@ -374,6 +374,12 @@ def main() -> None:
     cfg = ApiService().cfg
     if "NATS_URL" not in os.environ:
         cfg.nats_url = "nats://cs-nats:4222"  # the reference's api default (main.rs:519-524)
+    if os.environ.get("SYMB_API_IMPL", "native") == "native":
+        # the compiled gateway (csrc/native/gateway.cpp): api_workers epoll threads in-process
+        from .gateway_native import serve_forever
+
+        serve_forever(cfg)
+        return
     import signal
 
     kids = []

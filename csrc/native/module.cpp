@@ -10,6 +10,7 @@ void register_text(py::module_& m);
 void register_html(py::module_& m);
 void register_packstream(py::module_& m);
 void register_natsd(py::module_& m);
+void register_gateway(py::module_& m);
 }  // namespace symbn
 
 PYBIND11_MODULE(_native, m) {
@@ -21,4 +22,5 @@ PYBIND11_MODULE(_native, m) {
   symbn::register_html(m);
   symbn::register_packstream(m);
   symbn::register_natsd(m);
+  symbn::register_gateway(m);
 }

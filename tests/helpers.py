@@ -46,6 +46,29 @@ async def stop_api(svc, task):
 
 
 @contextlib.asynccontextmanager
+async def gateway(impl: str, cfg: Config):
+    """The api gateway under test: "py" (asyncio/starlette spec) or "native" (C++ epoll)."""
+    if impl == "py":
+        from codename_symbiont_amd.services.api import ApiService
+
+        api = ApiService(cfg)
+        url, task = await start_api(api)
+        try:
+            yield url
+        finally:
+            await stop_api(api, task)
+    else:
+        from codename_symbiont_amd.services.gateway_native import NativeGateway
+
+        gw = await NativeGateway(cfg, workers=2, log=False).start(host="127.0.0.1", port=0)
+        assert gw.stats["nats_connected"]
+        try:
+            yield gw.url
+        finally:
+            await gw.stop()
+
+
+@contextlib.asynccontextmanager
 async def broker():
     b = await Broker().start()
     try:

@@ -10,13 +10,13 @@ import json
 import httpx
 import pytest
 
-from codename_symbiont_amd.services.api import ApiService
+from codename_symbiont_amd.bus import NatsClient
 from codename_symbiont_amd.services.preprocessing import PreprocessingService
 from codename_symbiont_amd.services.text_generator import TextGeneratorService
 from codename_symbiont_amd.services.vector_memory import VectorMemoryService
 from codename_symbiont_amd.wire import RawTextMessage, subjects
 
-from helpers import broker, cpu_config, start_api, stop_api
+from helpers import broker, cpu_config, gateway
 
 
 def run(coro):
@@ -32,13 +32,15 @@ async def _read_sse_event(client, url, trigger):
                 return json.loads(line[6:])
 
 
-def test_generate_text_to_sse():
+@pytest.mark.parametrize("gw", ["py", "native"])
+def test_generate_text_to_sse(gw):
     async def main():
         async with broker() as b:
             cfg = cpu_config(b.url)
             gen = await TextGeneratorService(cfg, seed=1).start()
-            api = ApiService(cfg)
-            url, t = await start_api(api)
+            gwc = gateway(gw, cfg)
+            url = await gwc.__aenter__()
+            nc = await NatsClient.connect(b.url)
             async with httpx.AsyncClient(timeout=10) as c:
                 async def trigger():
                     await asyncio.sleep(0.2)
@@ -52,17 +54,20 @@ def test_generate_text_to_sse():
             words = ev["generated_text"].split()
             assert 1 <= len(words) <= 12 and words[0] == "я"   # reference starter quirk
             assert set(ev) == {"original_task_id", "generated_text", "timestamp_ms"}
-            await stop_api(api, t)
+            await gwc.__aexit__(None, None, None)
+            await nc.close()
             await gen.stop()
     run(main())
 
 
-def test_gateway_serves_ui_page():
+@pytest.mark.parametrize("gw", ["py", "native"])
+def test_gateway_serves_ui_page(gw):
     """C9: the gateway serves the single-page client with the reference's three features."""
     async def main():
         async with broker() as b:
-            api = ApiService(cpu_config(b.url))
-            url, t = await start_api(api)
+            gwc = gateway(gw, cpu_config(b.url))
+            url = await gwc.__aenter__()
+            nc = await NatsClient.connect(b.url)
             async with httpx.AsyncClient(timeout=10) as c:
                 r = await c.get(url + "/")
             assert r.status_code == 200 and r.headers["content-type"].startswith("text/html")
@@ -70,16 +75,19 @@ def test_gateway_serves_ui_page():
             for needle in ('id="url-form"', 'id="gen-form"', 'id="search-form"', "/submit-url",
                            "/generate-text", "/search/semantic", "EventSource", "Codename: Symbiont UI"):
                 assert needle in html, needle
-            await stop_api(api, t)
+            await gwc.__aexit__(None, None, None)
+            await nc.close()
     run(main())
 
 
-def test_gateway_validation_and_no_responders():
+@pytest.mark.parametrize("gw", ["py", "native"])
+def test_gateway_validation_and_no_responders(gw):
     async def main():
         async with broker() as b:
             cfg = cpu_config(b.url)
-            api = ApiService(cfg)
-            url, t = await start_api(api)
+            gwc = gateway(gw, cfg)
+            url = await gwc.__aenter__()
+            nc = await NatsClient.connect(b.url)
             async with httpx.AsyncClient(timeout=10) as c:
                 r = await c.post(url + "/api/submit-url", json={"url": "   "})
                 assert r.status_code == 400 and r.json() == {"message": "URL cannot be empty", "task_id": None}
@@ -114,22 +122,25 @@ def test_gateway_validation_and_no_responders():
                 r = await c.post(url + "/api/submit-url", json={"url": "u"},
                                  headers={"origin": "http://evil.example"})
                 assert r.status_code == 400
-            await stop_api(api, t)
+            await gwc.__aexit__(None, None, None)
+            await nc.close()
     run(main())
 
 
-def test_ingest_then_semantic_search_cpu():
+@pytest.mark.parametrize("gw", ["py", "native"])
+def test_ingest_then_semantic_search_cpu(gw):
     async def main():
         async with broker() as b:
             cfg = cpu_config(b.url)
             pre = await PreprocessingService(cfg).start()
             vm = await VectorMemoryService(cfg).start()
-            api = ApiService(cfg)
-            url, t = await start_api(api)
+            gwc = gateway(gw, cfg)
+            url = await gwc.__aenter__()
+            nc = await NatsClient.connect(b.url)
             text = ("The GPU index keeps every vector in HBM.   It answers cosine queries! "
                     "Markov chains generate text? Neo4j stores the graph")
             raw = RawTextMessage("doc-1", "http://example.org/p", text, 123)
-            await api.nc.publish(subjects.RAW_TEXT_DISCOVERED, raw.to_json())
+            await nc.publish(subjects.RAW_TEXT_DISCOVERED, raw.to_json())
             for _ in range(200):
                 if vm.store.count >= 4:
                     break
@@ -150,13 +161,15 @@ def test_ingest_then_semantic_search_cpu():
             assert top["score"] > 0.999
             scores = [x["score"] for x in body["results"]]
             assert scores == sorted(scores, reverse=True)
-            await stop_api(api, t)
+            await gwc.__aexit__(None, None, None)
+            await nc.close()
             await pre.stop()
             await vm.stop()
     run(main())
 
 
-def test_url_to_search_pipeline_with_fixture_site():
+@pytest.mark.parametrize("gw", ["py", "native"])
+def test_url_to_search_pipeline_with_fixture_site(gw):
     """POST /api/submit-url -> perception (local fixture site) -> preprocessing -> vector_memory
     -> POST /api/search/semantic, plus the restored tokenized feed."""
     from aiohttp import web
@@ -181,9 +194,10 @@ def test_url_to_search_pipeline_with_fixture_site():
             per = await PerceptionService(cfg).start()
             pre = await PreprocessingService(cfg).start()
             vm = await VectorMemoryService(cfg).start()
-            api = ApiService(cfg)
-            url, t = await start_api(api)
-            tok_sub = await api.nc.subscribe(subjects.PROCESSED_TEXT_TOKENIZED)
+            gwc = gateway(gw, cfg)
+            url = await gwc.__aenter__()
+            nc = await NatsClient.connect(b.url)
+            tok_sub = await nc.subscribe(subjects.PROCESSED_TEXT_TOKENIZED)
             async with httpx.AsyncClient(timeout=30) as c:
                 r = await c.post(url + "/api/submit-url", json={"url": f"http://127.0.0.1:{port}/doc"})
                 assert r.status_code == 200
@@ -199,7 +213,8 @@ def test_url_to_search_pipeline_with_fixture_site():
             res = r.json()["results"]
             assert res[0]["payload"]["sentence_text"] == "It keeps the top scores per query."
             assert res[0]["payload"]["source_url"] == f"http://127.0.0.1:{port}/doc"
-            await stop_api(api, t)
+            await gwc.__aexit__(None, None, None)
+            await nc.close()
             for s in (per, pre, vm):
                 await s.stop()
         await runner.cleanup()
