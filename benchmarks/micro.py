@@ -197,7 +197,9 @@ def cmd_gemm(a):
 
     M = a.batch * a.seq
     shapes = [("qkv", 1152, 384, K.EPI_BIAS), ("out+ln", 384, 384, K.EPI_RES_LN),
-              ("ffn1", 1536, 384, K.EPI_GELU), ("ffn2+ln", 384, 1536, K.EPI_RES_LN)]
+              ("ffn1", 1536, 384, K.EPI_GELU), ("ffn2+ln", 384, 1536, K.EPI_RES_LN),
+              ("bge.qkv", 2304, 768, K.EPI_BIAS), ("bge.out+res", 768, 768, K.EPI_RES),
+              ("bge.ffn1", 3072, 768, K.EPI_GELU), ("bge.ffn2+res", 768, 3072, K.EPI_RES)]
     out = {}
     for name, N, Kd, epi in shapes:
         x = torch.randn(M, Kd, device="cuda").bfloat16()

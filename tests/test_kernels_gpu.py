@@ -72,12 +72,15 @@ def test_add_ln(H):
     (300, 1152, 384, 0), (129, 1536, 384, 1), (517, 384, 384, 2), (517, 384, 384, 3),
     (300, 384, 1536, 3), (64, 768, 768, 2), (1000, 2304, 768, 0), (77, 1024, 4096, 2),
     (4099, 1536, 384, 1), (700, 384, 1536, 3),
+    # > 256 tiles: more tiles than CUs
+    (16384, 1152, 384, 0), (12800, 1536, 384, 1), (9000, 768, 3072, 2),
 ])
 def test_gemm(M, N, K, epi, tile):
     from codename_symbiont_amd.ops._ext import hip
     from codename_symbiont_amd.ops.kernels import gemm
 
-    hip().gemm_config(64 if tile else 128, tile)   # tile=1: 256x128 3-stage / 64-row RES_LN
+    # tile=1: 256x128 3-stage / 64-row RES_LN
+    hip().gemm_config(64 if tile else 128, tile)
 
     a = _bf(M, K, seed=1)
     w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=2)
