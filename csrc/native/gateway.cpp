@@ -26,7 +26,9 @@
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#ifndef SYMB_NO_PYTHON
 #include <pybind11/pybind11.h>
+#endif
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
@@ -51,7 +53,9 @@
 
 #include "json.h"
 
+#ifndef SYMB_NO_PYTHON
 namespace py = pybind11;
+#endif
 
 namespace symbn {
 namespace gw {
@@ -1402,6 +1406,8 @@ class Gateway {
   }
 
   int port() const { return port_; }
+  long long search_ok() const { return st_.search_ok.load(); }
+  long long sse_events() const { return st_.sse_events.load(); }
   bool nats_connected() const {
     for (auto& l : loops_)
       if (!l->nats_up()) return false;
@@ -1440,6 +1446,7 @@ class Gateway {
     return o;
   }
 
+#ifndef SYMB_NO_PYTHON
   py::dict stats() {
     py::dict d;
     d["requests"] = st_.requests.load();
@@ -1453,6 +1460,7 @@ class Gateway {
     d["nats_connected"] = nats_connected();
     return d;
   }
+#endif
 
  private:
   Config cfg_;
@@ -1465,6 +1473,7 @@ std::string Loop::gw_metrics() { return gw_->metrics_json(); }
 
 }  // namespace gw
 
+#ifndef SYMB_NO_PYTHON
 void register_gateway(py::module_& m) {
   using gw::Config;
   using gw::Gateway;
@@ -1493,5 +1502,7 @@ void register_gateway(py::module_& m) {
       .def("metrics_json", &Gateway::metrics_json);
   m.def("py_float_repr", &gw::py_float_repr);
 }
+
+#endif  // SYMB_NO_PYTHON
 
 }  // namespace symbn

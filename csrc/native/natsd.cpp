@@ -28,7 +28,9 @@
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#ifndef SYMB_NO_PYTHON
 #include <pybind11/pybind11.h>
+#endif
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
@@ -48,7 +50,9 @@
 
 #include "json.h"
 
+#ifndef SYMB_NO_PYTHON
 namespace py = pybind11;
+#endif
 
 namespace symbn {
 namespace natsd {
@@ -274,6 +278,15 @@ class Server {
   int port() const { return port_; }
   bool running() const { return running_; }
 
+  struct Counters {
+    long long in_msgs, out_msgs, in_bytes, out_bytes, connections, total_connections,
+        subscriptions, slow_consumers;
+  };
+  Counters counters() const {
+    return {in_msgs_.load(), out_msgs_.load(), in_bytes_.load(), out_bytes_.load(),
+            n_conns_.load(), total_conns_.load(), n_subs_.load(), slow_.load()};
+  }
+#ifndef SYMB_NO_PYTHON
   py::dict stats() const {
     py::dict d;
     d["in_msgs"] = in_msgs_.load();
@@ -286,6 +299,7 @@ class Server {
     d["slow_consumers"] = slow_.load();
     return d;
   }
+#endif
 
  private:
   [[noreturn]] void fail_close(const std::string& m) {
@@ -744,6 +758,7 @@ class Server {
 
 }  // namespace natsd
 
+#ifndef SYMB_NO_PYTHON
 void register_natsd(py::module_& m) {
   using natsd::Server;
   py::class_<Server>(m, "NatsServer")
@@ -762,5 +777,7 @@ void register_natsd(py::module_& m) {
     return natsd::subject_matches(natsd::split_dots(pat), natsd::split_dots(subj));
   });
 }
+
+#endif  // SYMB_NO_PYTHON
 
 }  // namespace symbn
