@@ -211,6 +211,28 @@ def test_index_scan_seeded_threshold_is_exact(D):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["bf16", "fp8"])
+def test_index_scan_xcd_grouping_is_exact(dtype):
+    """2048 gathered queries (the 8-rank shape): the XCD-grouped block order returns exactly the
+    rows and scores of the plain order, and matches the oracle."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+
+    n, nq, k, D = 300_001, 2048, 10, 384 if dtype == "bf16" else 768
+    shard = HbmIndexShard(D, n, dtype=dtype)
+    shard.fill_random(n, seed=21)
+    q = torch.nn.functional.normalize(_f(nq, D, seed=22), dim=-1).bfloat16()
+    shard.scan_xcd = 0
+    s0, r0 = shard.search(q, k)
+    shard.scan_xcd = 1
+    s1, r1 = shard.search(q, k)
+    torch.cuda.synchronize()
+    assert torch.equal(r0, r1) and torch.equal(s0, s1)
+    if dtype == "bf16":
+        ref_s, _ = R.topk_ref(shard.unit_rows(), q, k)
+        _close(s1, ref_s, atol=2e-3, what="xcd-grouped topk scores")
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("src", [torch.float32, torch.bfloat16])
 def test_quant_fp8_matches_torch_e4m3(src):
     from codename_symbiont_amd.ops import kernels as K
