@@ -304,10 +304,17 @@ def cmd_attn(a):
     cu = torch.arange(0, (a.batch + 1) * a.seq, a.seq, dtype=torch.int32, device="cuda")
     qkv = torch.randn(a.batch * a.seq, 3 * nh * hd, device="cuda").bfloat16()
     out = torch.empty(a.batch * a.seq, nh * hd, device="cuda", dtype=torch.bfloat16)
-    res = ab({"attn": lambda: K.attention(qkv, cu, a.seq, nh, hd, out=out)}, a.rounds, a.iters)
-    m = res["attn"][0]
+    from codename_symbiont_amd.ops._ext import hip
+
+    def run(w, kv):
+        hip().attention_config(w, kv)
+        return K.attention(qkv, cu, a.seq, nh, hd, out=out)
+    res = ab({f"waves{w}_kvt{kv}": (lambda w=w, kv=kv: run(w, kv)) for w in (4, 8) for kv in (64, 128)},
+             a.rounds, a.iters)
+    hip().attention_config(8, 64)
     fl = 4 * a.batch * nh * a.seq * a.seq * hd
-    print(json.dumps({"bench": "attn", "ms": round(m, 4), "TFLOPs": round(fl / (m / 1e3) / 1e12)}))
+    print(json.dumps({"bench": "attn", "head_dim": hd, "seq": a.seq, "results": {
+        k: {"ms": round(m, 4), "TFLOPs": round(fl / (m / 1e3) / 1e12)} for k, (m, _) in res.items()}}))
 
 
 def main():

@@ -6,7 +6,9 @@
 // K6-K11).  Sequences are packed back to back ([T, 3H] fused QKV rows, cu_seqlens offsets), so
 // no FLOP or byte is spent on padding and no mask tensor exists.
 //
-// Per workgroup: 64 query rows of one (sequence, head); 4 waves x 16 queries.  gfx950 layout:
+// Per workgroup: 16*NWAVE query rows of one (sequence, head); NWAVE waves x 16 queries (NWAVE = 8
+// covers a <=128-token sentence in ONE workgroup, so its K/V rows are read from HBM once instead of
+// once per 64-query block).  gfx950 layout:
 //  * S^T = K Q^T (v_mfma_f32_16x16x32_bf16, K = A operand from LDS, Q = B operand in registers):
 //    a lane's accumulators are 4 keys x ONE query, so the softmax row statistics are lane-local
 //    up to a 4-lane (shfl 16/32) reduction, and the probabilities feed the PV MFMA straight from
@@ -22,8 +24,8 @@
 
 namespace symb {
 
-template <int D, int KVT>
-__global__ __launch_bounds__(256) void attn_varlen_kernel(const __bf16* __restrict__ qkv,
+template <int D, int KVT, int NWAVE>
+__global__ __launch_bounds__(64 * NWAVE) void attn_varlen_kernel(const __bf16* __restrict__ qkv,
                                                           int ld_qkv, const int32_t* __restrict__ cu,
                                                           int H, float scale_log2,
                                                           __bf16* __restrict__ out, int ld_out) {
@@ -41,7 +43,8 @@ __global__ __launch_bounds__(256) void attn_varlen_kernel(const __bf16* __restri
 
   const int b = blockIdx.z, h = blockIdx.y;
   const int s0 = cu[b], L = cu[b + 1] - s0;
-  const int q0 = blockIdx.x * 64;
+  constexpr int NTH = 64 * NWAVE, QB = 16 * NWAVE;  // threads, query rows per workgroup
+  const int q0 = blockIdx.x * QB;
   if (q0 >= L) return;                    // block-uniform: EXEC stays full for the tr reads
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int c16 = lane & 15, g = lane >> 4;
@@ -73,7 +76,7 @@ __global__ __launch_bounds__(256) void attn_varlen_kernel(const __bf16* __restri
 
   for (int kv0 = 0; kv0 < L; kv0 += KVT) {
     __syncthreads();
-    for (int c = tid; c < KVT * CK; c += 256) {
+    for (int c = tid; c < KVT * CK; c += NTH) {
       const int r = c / CK, ch = c % CK;
       const int kr = min(kv0 + r, L - 1);
       const __bf16* src = qkv + (size_t)(s0 + kr) * ld_qkv + h * D + ch * 8;
@@ -155,23 +158,40 @@ __global__ __launch_bounds__(256) void attn_varlen_kernel(const __bf16* __restri
 
 using namespace symb;
 
+// 8 waves (one workgroup per <=128-token sentence and head) with 64-key tiles: 256 x 128 tokens,
+// 12 heads: D=32 40.5 -> 34.0 us, D=64 52.2 -> 43.1 us vs 4 waves (profiles/r1_attn/attn_waves.json)
+static int g_attn_waves = 8;  // 4: 64-query workgroups; 8: 128-query workgroups
+static int g_attn_kvt = 64;   // keys per LDS tile (64, or 128 = a <=128-token sentence at once)
+int symb_attention_config(int waves, int kvt) {
+  if ((waves != 4 && waves != 8) || (kvt != 64 && kvt != 128)) return -1;
+  g_attn_waves = waves;
+  g_attn_kvt = kvt;
+  return 0;
+}
+
 int symb_attention(const void* qkv, int ld_qkv, const int32_t* cu, int B, int max_len, int n_heads,
                    int head_dim, void* out, int ld_out, hipStream_t st) {
   if (B <= 0 || max_len <= 0) return 0;
   const int H = n_heads * head_dim;
   const float scale_log2 = 1.4426950408889634f / sqrtf((float)head_dim);
-  dim3 grid((max_len + 63) / 64, n_heads, B);
-  // 64-key tiles (a 128-key single-stage variant measured 9-12 % slower at S = 128:
-  // profiles/r1_attn/attn_kvt.log)
-#define SYMB_A(DD, KV) hipLaunchKernelGGL((attn_varlen_kernel<DD, KV>), grid, dim3(256), 0, st, \
-                                          (const __bf16*)qkv, ld_qkv, cu, H, scale_log2,      \
-                                          (__bf16*)out, ld_out)
-  if (head_dim == 32)
-    SYMB_A(32, 64);
-  else if (head_dim == 64)
-    SYMB_A(64, 64);
-  else
+  const int NW = g_attn_waves;
+  dim3 grid((max_len + 16 * NW - 1) / (16 * NW), n_heads, B);
+#define SYMB_A(DD, KV, W) hipLaunchKernelGGL((attn_varlen_kernel<DD, KV, W>), grid, dim3(64 * W), 0, \
+                                             st, (const __bf16*)qkv, ld_qkv, cu, H, scale_log2,     \
+                                             (__bf16*)out, ld_out)
+#define SYMB_AW(DD)                                             \
+  if (NW == 8 && g_attn_kvt == 128) SYMB_A(DD, 128, 8);         \
+  else if (NW == 8) SYMB_A(DD, 64, 8);                          \
+  else if (g_attn_kvt == 128) SYMB_A(DD, 128, 4);               \
+  else SYMB_A(DD, 64, 4);
+  if (head_dim == 32) {
+    SYMB_AW(32)
+  } else if (head_dim == 64) {
+    SYMB_AW(64)
+  } else {
     return -1;
+  }
+#undef SYMB_AW
 #undef SYMB_A
   return (int)hipGetLastError();
 }

@@ -100,14 +100,20 @@ def test_gemm(M, N, K, epi, tile):
 @pytest.mark.parametrize("lens", [[1, 7, 64, 65, 128, 200, 3, 511],   # 64-key tiles
                                   [1, 7, 64, 65, 100, 128, 3],        # <=128: one 128-key tile
                                   [5, 33, 64]])                       # <=64
-def test_attention_varlen(D, nh, lens):
+@pytest.mark.parametrize("waves,kvt", [(4, 64), (8, 64), (8, 128)])
+def test_attention_varlen(D, nh, lens, waves, kvt):
+    from codename_symbiont_amd.ops._ext import hip
     from codename_symbiont_amd.ops.kernels import attention
 
     cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
     T = int(cu[-1])
     H = nh * D
     qkv = _bf(T, 3 * H, seed=7)
-    out = attention(qkv, cu, max(lens), nh, D)
+    hip().attention_config(waves, kvt)
+    try:
+        out = attention(qkv, cu, max(lens), nh, D)
+    finally:
+        hip().attention_config(8, 64)
     ref = R.attention_ref(qkv, cu, nh, D)
     _close(out, ref, atol=2e-2, rtol=2e-2, what="attention")
 
