@@ -42,7 +42,7 @@ def _sharded_worker(rank, world, port, out):
     D.shutdown(info)
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])   # 8: the driver's N=8 rank count, rehearsed on gloo
 def test_sharded_searcher_matches_global_topk(world):
     mgr = mp.Manager()
     out = mgr.dict()
