@@ -26,6 +26,8 @@ class DimensionError(ValueError):
     pass
 
 
+from ..ops._ext import native as _native  # noqa: E402
+
 class VectorStore:
     def __init__(self, dim: int, capacity: int, device=None, snapshot_dir: str = "",
                  snapshot_every: int = 100_000, group=None, dtype: str = "bf16"):
@@ -39,6 +41,7 @@ class VectorStore:
         self.snapshot_every = snapshot_every
         self._since_snapshot = 0
         self._lock = threading.Lock()
+        self._frag: dict[int, tuple[bytes, bytes]] = {}
         self.wal = None
         if snapshot_dir:
             os.makedirs(snapshot_dir, exist_ok=True)
@@ -59,8 +62,12 @@ class VectorStore:
     def _upsert_nolog(self, point_ids, vecs, payloads):
         t = torch.as_tensor(np.ascontiguousarray(vecs, dtype=np.float32))
         if self.group is not None:
-            return self.group.upsert(point_ids, t, payloads)
-        return self.shard.upsert(point_ids, t, payloads)
+            out = self.group.upsert(point_ids, t, payloads)
+        else:
+            out = self.shard.upsert(point_ids, t, payloads)
+        for g in out or ():
+            self._frag.pop(int(g), None)   # (re)written rows: their cached result JSON is stale
+        return out
 
     def upsert(self, point_ids: list[str], vecs: np.ndarray, payloads: list[Payload]) -> None:
         vecs = np.asarray(vecs, dtype=np.float32)
@@ -111,6 +118,30 @@ class VectorStore:
         if self.group is not None:
             return self.group.payload(gid)
         return self.shard.payloads.get(int(gid))
+
+    FRAG_CACHE_MAX = 1 << 20
+
+    def result_fragments(self, gid: int):
+        """(prefix, suffix) JSON bytes of this point's SemanticSearchResultItem around its score,
+        cached per row (search results are encoded by concatenation, search_result_json);
+        None for rows without a point id."""
+        gid = int(gid)
+        f = self._frag.get(gid)
+        if f is None:
+            pid, p = self.lookup(gid)
+            if pid is None:
+                return None
+            from ..wire import QdrantPointPayload
+
+            pl = QdrantPointPayload(p.original_document_id, p.source_url, p.sentence_text,
+                                    int(p.sentence_order) & 0xFFFFFFFF, p.model_name,
+                                    int(p.processed_at_ms)).to_json()
+            f = (b'{"qdrant_point_id":' + _native().json_dumps(pid) + b',"score":',
+                 b',"payload":' + pl + b'}')
+            if len(self._frag) >= self.FRAG_CACHE_MAX:
+                self._frag.clear()
+            self._frag[gid] = f
+        return f
 
     def close(self) -> None:
         if self.wal is not None:

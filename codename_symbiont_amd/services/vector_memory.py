@@ -23,8 +23,8 @@ from ..index.store import VectorStore
 from ..models.config import get_config
 from ..ops._ext import native
 from ..utils import log as ulog
-from ..wire import (QdrantPointPayload, SemanticSearchNatsResult, SemanticSearchNatsTask,
-                    SemanticSearchResultItem, TextWithEmbeddingsMessage, WireError, subjects)
+from ..wire import (SemanticSearchNatsResult, SemanticSearchNatsTask, TextWithEmbeddingsMessage,
+                    WireError, subjects)
 from .base import Service
 from .batcher import SearchBatcher
 
@@ -121,23 +121,29 @@ class VectorMemoryService(Service):
             self.log.error("[SEARCH_HANDLER_QDRANT_FAIL] %s", err)
             await self.reply(nmsg, SemanticSearchNatsResult(task.request_id, [], err))
             return
-        items = []
+        # result JSON = per-point cached fragments around f32 scores (native concatenation; the
+        # same bytes as SemanticSearchNatsResult(...).to_json())
+        frags, keep = [], []
         skipped = 0
         for s, r in zip(scores.tolist(), rows.tolist()):
             if r < 0:
                 continue
-            pid, p = self.store.lookup(r)
-            if pid is None:
+            f = self.store.result_fragments(r)
+            if f is None:
                 skipped += 1
                 continue
-            items.append(SemanticSearchResultItem(pid, float(s), QdrantPointPayload(
-                p.original_document_id, p.source_url, p.sentence_text, int(p.sentence_order) & 0xFFFFFFFF,
-                p.model_name, int(p.processed_at_ms))))
+            frags.append(f)
+            keep.append(s)
         if skipped:  # one line per request (the reference logs one per point)
             self.log.warning("[SEARCH_HANDLER] Found %d point(s) with missing or unexpected ID format. "
                              "Skipping.", skipped)
-        await self.reply(nmsg, SemanticSearchNatsResult(task.request_id, items, None))
-        self.log.info("[SEARCH_HANDLER] Sent %d search results for request_id %s", len(items),
+        body = native().search_result_json(task.request_id, np.asarray(keep, np.float32), frags)
+        if nmsg.reply:
+            await self.nc.publish(nmsg.reply, body)
+        else:
+            self.log.warning("[SEARCH_HANDLER] No reply subject provided for search task_id %s. "
+                             "Results not sent.", task.request_id)
+        self.log.info("[SEARCH_HANDLER] Sent %d search results for request_id %s", len(frags),
                       task.request_id)
 
     async def stop(self) -> None:

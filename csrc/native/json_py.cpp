@@ -2,6 +2,7 @@
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 
+#include <charconv>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -175,7 +176,14 @@ struct Loader {
       if (all_num) {
         py::array_t<float> arr((py::ssize_t)raw.size());
         float* dst = arr.mutable_data();
-        for (size_t i = 0; i < raw.size(); ++i) dst[i] = std::strtof(raw[i].text.c_str(), nullptr);
+        // std::from_chars: correctly rounded like strtof, several times faster (a 384-float
+        // query embedding parsed 52 -> ~12 us)
+        for (size_t i = 0; i < raw.size(); ++i) {
+          const std::string& t = raw[i].text;
+          float f = 0.f;
+          const auto r = std::from_chars(t.data(), t.data() + t.size(), f);
+          dst[i] = r.ec == std::errc() ? f : std::strtof(t.c_str(), nullptr);  // (overflow: ±inf)
+        }
         return std::move(arr);
       }
       py::list l(items.size());
@@ -216,7 +224,39 @@ std::string format_f32(float f) {
   return s;
 }
 
+// SemanticSearchNatsResult bytes from per-point JSON fragments cached by the vector store:
+// frags[i] = (b'{"qdrant_point_id":"<id>","score":', b',"payload":{...}}'); scores are f32 and
+// formatted like serde_json.  Identical bytes to SemanticSearchNatsResult(...).to_json().
+py::bytes search_result_json(const std::string& request_id,
+                             py::array_t<float, py::array::c_style | py::array::forcecast> scores,
+                             py::list frags) {
+  const size_t n = (size_t)py::len(frags);
+  if ((size_t)scores.size() < n) throw std::runtime_error("fewer scores than fragments");
+  const float* sc = scores.data();
+  std::string out;
+  out.reserve(64 + n * 320);
+  out += "{\"request_id\":";
+  append_json_string(out, request_id.data(), request_id.size());
+  out += ",\"results\":[";
+  for (size_t i = 0; i < n; ++i) {
+    py::tuple t = frags[i].cast<py::tuple>();
+    char* a;
+    char* b;
+    Py_ssize_t na, nb;
+    if (PyBytes_AsStringAndSize(t[0].ptr(), &a, &na) || PyBytes_AsStringAndSize(t[1].ptr(), &b, &nb))
+      throw py::error_already_set();
+    if (i) out.push_back(',');
+    out.append(a, (size_t)na);
+    append_f32(out, sc[i]);
+    out.append(b, (size_t)nb);
+  }
+  out += "],\"error_message\":null}";
+  return py::bytes(out);
+}
+
 void register_json(py::module_& m) {
+  m.def("search_result_json", &search_result_json, py::arg("request_id"), py::arg("scores"),
+        py::arg("frags"));
   py::register_exception<JsonError>(m, "JsonError", PyExc_ValueError);
   m.def("json_dumps", &dumps, "serde_json-compatible compact encoding (floats as f32)");
   m.def("json_dumps_f32_array", &dumps_f32_array);

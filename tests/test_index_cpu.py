@@ -106,3 +106,35 @@ def test_stage_tracing_records_metrics(caplog):
     snap = m.snapshot()["latency_ms"]
     assert snap["stage.unit"]["n"] == 1
     assert any("[TRACE] stage=unit id=req-1" in r.message and "n=3" in r.message for r in caplog.records)
+
+
+def test_search_result_fragments_match_wire_encoding_and_follow_overwrites():
+    """vector_memory encodes replies by concatenating per-point cached JSON fragments; the bytes
+    must equal SemanticSearchNatsResult.to_json() and an overwrite must refresh the fragment."""
+    import numpy as np
+
+    from codename_symbiont_amd.index.shard import Payload
+    from codename_symbiont_amd.index.store import VectorStore
+    from codename_symbiont_amd.ops._ext import native
+    from codename_symbiont_amd.wire import (QdrantPointPayload, SemanticSearchNatsResult,
+                                            SemanticSearchResultItem)
+
+    st = VectorStore(8, 64, device="cpu")
+    rng = np.random.default_rng(0)
+    st.upsert(["a", "b\"ü"], rng.standard_normal((2, 8)).astype(np.float32),
+              [Payload("d1", "u1", "first \n one", 0, "m", 5), Payload("d2", "u2", "two", 1, "m", 6)])
+    scores, rows = st.search(rng.standard_normal((1, 8)).astype(np.float32), 2)
+    frags = [st.result_fragments(r) for r in rows[0]]
+    got = native().search_result_json("rid", scores[0], frags)
+    items = []
+    for s, r in zip(scores[0].tolist(), rows[0].tolist()):
+        pid, p = st.lookup(r)
+        items.append(SemanticSearchResultItem(pid, s, QdrantPointPayload(
+            p.original_document_id, p.source_url, p.sentence_text, p.sentence_order, p.model_name,
+            p.processed_at_ms)))
+    assert got == SemanticSearchNatsResult("rid", items, None).to_json()
+    row_a = st.shard.payloads.id_to_row["a"]
+    assert b'"first \\n one"' in st.result_fragments(row_a)[1]
+    st.upsert(["a"], rng.standard_normal((1, 8)).astype(np.float32), [Payload("d1", "u1", "new", 0, "m", 9)])
+    row_a = st.shard.payloads.id_to_row["a"]
+    assert b'"sentence_text":"new"' in st.result_fragments(row_a)[1]
