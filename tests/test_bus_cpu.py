@@ -196,3 +196,79 @@ def test_native_broker_fanout_and_stats():
         assert b.stats["connections"] == 0 and b.stats["subscriptions"] == 0
         await b.stop()
     run(main())
+
+
+# ---------------------------------------------------------------------------------------------
+# differential property test: random protocol scripts give byte-identical per-connection output
+# on the native server and on the asyncio reference broker
+from hypothesis import HealthCheck, given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+_TOK = st.sampled_from(["a", "b", "c"])
+_SUBJ = st.lists(_TOK, min_size=1, max_size=3).map(".".join)
+_PAT = st.lists(st.one_of(_TOK, st.just("*")), min_size=1, max_size=3).map(".".join) | \
+    st.lists(_TOK, min_size=0, max_size=2).map(lambda t: ".".join(t + [">"]))
+_OP = st.one_of(
+    st.tuples(st.just("sub"), st.integers(0, 2), _PAT, st.integers(1, 6)),
+    st.tuples(st.just("pub"), st.integers(0, 2), _SUBJ, st.binary(max_size=12)),
+    st.tuples(st.just("hpub"), st.integers(0, 2), _SUBJ, st.binary(max_size=6)),
+    st.tuples(st.just("unsub"), st.integers(0, 2), st.integers(1, 6), st.integers(0, 3)),
+    st.tuples(st.just("bad"), st.integers(0, 2), st.sampled_from(["a.*", "a..b", " "]), st.just(b"")),
+)
+
+
+async def _script_output(Broker, script):
+    b = await Broker(max_payload=4096).start()
+    conns = []
+    for _ in range(3):
+        r, w = await _raw(b.port)
+        w.write(b'CONNECT {"verbose":false,"headers":true,"no_responders":true}\r\nPING\r\n')
+        assert await r.readline() == b"PONG\r\n"
+        conns.append((r, w))
+    outs = [bytearray() for _ in conns]
+    closed: set[int] = set()
+
+    async def sync():
+        # a PING/PONG round trip on EVERY connection after each op makes the outputs
+        # deterministic (the broker handles one connection's bytes in order)
+        for i, (r, w) in enumerate(conns):
+            if i in closed:
+                continue
+            w.write(b"PING\r\n")
+            while True:
+                line = await asyncio.wait_for(r.readline(), 5)
+                if line == b"PONG\r\n":
+                    break
+                outs[i] += line
+                if not line:          # the server closed this connection (protocol error)
+                    closed.add(i)
+                    break
+    for op in script:
+        kind, c = op[0], op[1]
+        if c in closed:
+            continue
+        w = conns[c][1]
+        if kind == "sub":
+            w.write(f"SUB {op[2]} {op[3]}\r\n".encode())
+        elif kind == "pub":
+            w.write(f"PUB {op[2]} _INBOX.r {len(op[3])}\r\n".encode() + op[3] + b"\r\n")
+        elif kind == "hpub":
+            h = b"NATS/1.0\r\nk: v\r\n\r\n"
+            w.write(f"HPUB {op[2]} {len(h)} {len(h) + len(op[3])}\r\n".encode() + h + op[3] + b"\r\n")
+        elif kind == "unsub":
+            w.write(f"UNSUB {op[2]} {op[3]}\r\n".encode() if op[3] else f"UNSUB {op[2]}\r\n".encode())
+        else:
+            w.write(f"PUB {op[2]} 0\r\n\r\n".encode())
+        await sync()
+    for _, w in conns:
+        w.close()
+    await b.stop()
+    return [bytes(o) for o in outs]
+
+
+@settings(max_examples=40, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(st.lists(_OP, min_size=1, max_size=25))
+def test_native_broker_matches_reference_on_random_scripts(script):
+    py = run(_script_output(BROKERS["py"], script))
+    nat = run(_script_output(BROKERS["native"], script))
+    assert nat == py
