@@ -62,6 +62,10 @@ def main() -> None:
     ap.add_argument("--index-dtype", choices=["bf16", "fp8"], default="bf16")
     ap.add_argument("--encoder-dtype", choices=["bf16", "fp8"], default="bf16",
                     help="fp8: e4m3 projection GEMMs (BASELINE config #5); the headline stays bf16")
+    ap.add_argument("--embed-dp", choices=["replica", "group"], default="replica",
+                    help="--mode embed, N > 1: independent replicas, or ONE global batch of "
+                         "batch*N sentences per step split over the ranks and gathered back to "
+                         "rank 0 over RCCL (parallel/embed_group.py; BASELINE config #4 over xGMI)")
     args = ap.parse_args()
 
     from codename_symbiont_amd.index.shard import HbmIndexShard
@@ -91,9 +95,15 @@ def main() -> None:
     log(info, f"[bench] setup {time.time() - t0:.1f}s: {cfg.model_name}, shard {rows_per_rank} "
               f"rows x {cfg.hidden} {args.index_dtype} = {rows_per_rank * row_bytes / 1e9:.1f} GB/rank")
 
+    group_dp = args.mode == "embed" and args.embed_dp == "group" and info.world > 1
+    if group_dp:
+        from codename_symbiont_amd.parallel.embed_group import EmbedGroup
+
+        egroup = EmbedGroup(info, enc)
     # host batches (pinned) rotated through two device buffers filled on a copy stream
     NB = 4
-    host = [synthetic_batch(cfg, B, S, seed=1000 * info.rank + i) for i in range(NB)]
+    NBATCH = B * info.world if group_dp else B   # group mode: rank 0 holds the global batch
+    host = [synthetic_batch(cfg, NBATCH, S, seed=1000 * info.rank + i) for i in range(NB)]
     host = [type(h)(h.ids.pin_memory(), h.pos.pin_memory(), None, h.cu_seqlens.pin_memory(),
                     h.max_len) for h in host]
     dbuf = [host[0].to(dev), host[1].to(dev)]
@@ -121,7 +131,16 @@ def main() -> None:
         slot = i % 2
         if ev:
             ev[0].record(compute)
-        if args.mode != "search":
+        if group_dp:
+            if info.is_root:
+                compute.wait_event(copy_done[slot])
+                egroup.embed(dbuf[slot])
+                consumed[slot].record(compute)
+                prefetch(i + 1)
+            else:
+                egroup.embed(None)
+            q = None
+        elif args.mode != "search":
             compute.wait_event(copy_done[slot])
             enc.forward_packed(dbuf[slot], out_f32, out_unit)
             consumed[slot].record(compute)
@@ -186,7 +205,8 @@ def main() -> None:
             "data": "synthetic token ids, random-init weights, random unit index rows",
             "config": {
                 "model": short, "global_batch": B * info.world, "seq_len": S,
-                "parallelism": f"dp{info.world}+index_shard{info.world}",
+                "parallelism": (f"dp{info.world}-rccl-group" if group_dp
+                                else f"dp{info.world}+index_shard{info.world}"),
                 "index_rows": args.index_rows, "dim": cfg.hidden, "top_k": args.k,
                 "mode": args.mode,
             },

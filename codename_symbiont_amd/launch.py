@@ -6,7 +6,9 @@
 Starts the in-repo NATS broker and every service as child processes with the reference's env
 plumbing (NATS_URL, API_SERVER_*, NEO4J_*, ...).  GPU services scale with ``--gpus``:
 * preprocessing: N independent processes (one per GPU, HIP_VISIBLE_DEVICES pinned) in the NATS
-  queue group "preprocessing" -> data-parallel ingest, each message handled exactly once;
+  queue group "preprocessing" -> data-parallel ingest, each message handled exactly once; or, with
+  ``--embed-dp rccl``, ONE service over N ranks whose batches are split across the GPUs and
+  gathered back over RCCL (parallel/embed_group.py);
 * vector_memory: ONE logical index over N ranks (torch.distributed.run, RCCL), rank 0 on NATS.
 Unlike the reference compose file (no restart policies) crashed children are
 restarted with exponential backoff.  Children are started as subprocesses, never exec'd.
@@ -72,7 +74,12 @@ def build_children(a) -> list[Child]:
     for s in SERVICES:
         if s not in only:
             continue
-        if s == "preprocessing" and a.gpus > 1:
+        if s == "preprocessing" and a.gpus > 1 and a.embed_dp == "rccl":
+            kids.append(Child("preprocessing", [py, "-m", "torch.distributed.run", "--nnodes=1",
+                                                f"--nproc-per-node={a.gpus}", "--master-addr",
+                                                "127.0.0.1", "--master-port", str(a.dist_port + 1),
+                                                "-m", mod + s], base))
+        elif s == "preprocessing" and a.gpus > 1:
             for g in range(a.gpus):
                 env = dict(base, HIP_VISIBLE_DEVICES=str(g), SYMB_QUEUE_GROUP="preprocessing")
                 kids.append(Child(f"preprocessing[{g}]", [py, "-m", mod + s], env))
@@ -94,6 +101,8 @@ def main() -> None:
     ap.add_argument("--api-port", type=int, default=8080)
     ap.add_argument("--dist-port", type=int, default=29600)
     ap.add_argument("--no-broker", action="store_true")
+    ap.add_argument("--embed-dp", choices=["queue", "rccl"], default="queue",
+                    help="multi-GPU embedding: NATS queue-group replicas or one RCCL group")
     a = ap.parse_args()
     kids = build_children(a)
     stop = {"flag": False}

@@ -167,8 +167,35 @@ class PreprocessingService(Service):
 
 
 def main() -> None:
+    """One GPU: ``python -m ...preprocessing``.  A node with RCCL data parallelism:
+    ``torch.distributed.run --nproc-per-node N -m codename_symbiont_amd.services.preprocessing``
+    -- rank 0 serves NATS and spreads every packed batch over all ranks (parallel/embed_group.py);
+    the other ranks execute its collective ops.  (launch.py's default is N independent replicas in
+    a NATS queue group; ``--embed-dp rccl`` selects this mode.)"""
+    import os
+
     ulog.setup(PreprocessingService.name, "info,preprocessing_service=debug")
-    asyncio.run(PreprocessingService().run_forever())
+    if int(os.environ.get("WORLD_SIZE", "1")) <= 1:
+        asyncio.run(PreprocessingService().run_forever())
+        return
+    from ..models import get_config
+    from ..parallel import dist as D
+    from ..parallel.embed_group import EmbedGroup, GroupEncoder
+    from ..utils.config import Config
+
+    cfg = Config()
+    info = D.init()
+    enc = make_encoder(get_config(cfg.model), force_cpu=cfg.force_cpu, device=info.device,
+                       precision=cfg.encoder_dtype)
+    group = EmbedGroup(info, enc)
+    try:
+        if info.is_root:
+            asyncio.run(PreprocessingService(cfg, encoder=GroupEncoder(group)).run_forever())
+        else:
+            group.serve()
+    finally:
+        group.stop()
+        D.shutdown(info)
 
 
 if __name__ == "__main__":

@@ -445,7 +445,7 @@ class Loop {
     std::string in, out;
     size_t out_pos = 0;
     bool closing = false, close_after = false, busy = false, epollout = false;
-    bool sse = false;
+    bool sse = false, continued = false;
     std::deque<std::string> sse_backlog;
     double sse_last = 0;
     std::string origin;  // CORS origin of the in-flight request (allowed), echoed on the reply
@@ -657,7 +657,16 @@ class Loop {
                     std::to_string(JSON_LIMIT) + " bytes).", true);
         return;
       }
-      if (c->in.size() < he + 4 + clen) return;  // body not complete yet
+      if (c->in.size() < he + 4 + clen) {  // body not complete yet
+        // curl & co. hold bodies > 1 KiB back until "100 Continue" (or a 1 s timeout)
+        if (!c->continued && h.count("expect") && lower(h["expect"]) == "100-continue") {
+          c->out += "HTTP/1.1 100 Continue\r\n\r\n";
+          c->continued = true;
+          flush(c);
+        }
+        return;
+      }
+      c->continued = false;
       std::string body = c->in.substr(he + 4, clen);
       c->in.erase(0, he + 4 + clen);
       const std::string conn_h = lower(h.count("connection") ? h["connection"] : "");

@@ -99,6 +99,15 @@ def test_native_gateway_http_mechanics():
                 assert heads == [b"HTTP/1.1 200 OK"] * 3 + [b"HTTP/1.1 404 Not Found",
                                                              b"HTTP/1.1 405 Method Not Allowed"]
                 assert data.count(b"submitted successfully") == 3
+                # Expect: 100-continue (curl holds bodies > 1 KiB back until told to send)
+                r, w = await asyncio.open_connection("127.0.0.1", port)
+                w.write(b"POST /api/submit-url HTTP/1.1\r\nHost: x\r\nContent-Type: application/json\r\n"
+                        b"Expect: 100-continue\r\nContent-Length: %d\r\n\r\n" % len(body))
+                assert await asyncio.wait_for(r.readline(), 5) == b"HTTP/1.1 100 Continue\r\n"
+                assert await r.readline() == b"\r\n"
+                w.write(body)
+                assert (await asyncio.wait_for(r.readline(), 5)).startswith(b"HTTP/1.1 200")
+                w.close()
                 async with httpx.AsyncClient(timeout=10) as c:
                     h = (await c.get(url + "/api/health")).json()
                     assert h["status"] == "ok" and h["nats"] is True

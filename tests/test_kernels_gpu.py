@@ -372,3 +372,24 @@ def test_encoder_fp8_close_to_fp32_oracle(model):
     outr, _ = ref.forward_packed(b)
     cos = torch.nn.functional.cosine_similarity(out8.float().cpu(), outr.float(), dim=-1)
     assert cos.min().item() > 0.99, cos
+
+
+@pytest.mark.gpu
+def test_embed_group_single_rank_matches_encoder():
+    """EmbedGroup's slicing/reassembly path on the HIP encoder (world 1 on the GPU box; the
+    multi-rank collective path is covered with gloo in test_parallel_cpu.py)."""
+    from codename_symbiont_amd.models import get_config
+    from codename_symbiont_amd.models.encoder import HipEncoder, synthetic_batch
+    from codename_symbiont_amd.parallel.dist import DistInfo
+    from codename_symbiont_amd.parallel.embed_group import EmbedGroup, GroupEncoder
+
+    cfg = get_config("minilm-l6")
+    enc = HipEncoder(cfg, seed=0, device=DEV)
+    info = DistInfo(0, 1, 0, torch.device(DEV), "none")
+    genc = GroupEncoder(EmbedGroup(info, enc))
+    b = synthetic_batch(cfg, 37, 64, seed=3, varlen=True).to(DEV)
+    want, _ = enc.forward_packed(b)
+    got, unit = genc.forward_packed(b)
+    torch.cuda.synchronize()
+    _close(got, want, atol=1e-6, what="group embed")
+    assert unit.dtype == torch.bfloat16 and unit.shape == want.shape

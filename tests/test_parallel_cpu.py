@@ -60,6 +60,57 @@ def test_sharded_searcher_matches_global_topk(world):
         np.testing.assert_allclose(s, ref_s[r * nq:(r + 1) * nq].numpy(), atol=1e-5)
 
 
+_EMBED_LENS = [[5, 17, 3, 40, 9, 12, 2, 31, 8, 6], [7, 9]]   # the 2-sentence batch leaves ranks idle
+
+
+def _embed_batches(cfg):
+    from codename_symbiont_amd.models.encoder import pack_token_ids
+
+    rng = np.random.default_rng(4)
+    return [pack_token_ids([rng.integers(1000, cfg.vocab_size, size=L).astype(np.int32) for L in lens], cfg)
+            for lens in _EMBED_LENS]
+
+
+def _embed_worker(rank, world, port, out):
+    from codename_symbiont_amd.models import get_config
+    from codename_symbiont_amd.models.encoder import TorchEncoder
+    from codename_symbiont_amd.parallel import dist as D
+    from codename_symbiont_amd.parallel.embed_group import EmbedGroup, GroupEncoder
+    info = _init(rank, world, port)
+    cfg = get_config("minilm-l6")
+    group = EmbedGroup(info, TorchEncoder(cfg, seed=0))
+    if info.is_root:
+        enc = GroupEncoder(group)
+        out[0] = [enc.forward_packed(b)[0].numpy() for b in _embed_batches(cfg)]
+        group.stop()
+    else:
+        group.serve()
+    D.barrier(info)
+    D.shutdown(info)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_embed_group_matches_single_process(world):
+    """DP embedding over the group (token-balanced slices, all_gather back to rank 0) returns the
+    same pooled embeddings, in input order, as one process encoding the whole batch."""
+    from codename_symbiont_amd.models import get_config
+    from codename_symbiont_amd.models.encoder import TorchEncoder
+    from codename_symbiont_amd.parallel.embed_group import split_by_tokens
+
+    cu = np.array([0, 5, 22, 25, 65, 74], np.int32)
+    r = split_by_tokens(cu, 3)
+    assert r[0][0] == 0 and r[-1][1] == 5 and all(a <= b for a, b in r)
+    assert split_by_tokens(np.array([0, 7], np.int32), 4) == [(0, 1), (1, 1), (1, 1), (1, 1)]
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.start_processes(_embed_worker, args=(world, _free_port(), out), nprocs=world, join=True,
+                       start_method="spawn")
+    cfg = get_config("minilm-l6")
+    ref = TorchEncoder(cfg, seed=0)
+    for got, b in zip(out[0], _embed_batches(cfg)):
+        np.testing.assert_allclose(got, ref.forward_packed(b)[0].numpy(), rtol=1e-4, atol=1e-4)
+
+
 def _group_worker(rank, world, port, out):
     from codename_symbiont_amd.index.shard import Payload
     from codename_symbiont_amd.index.store import VectorStore
