@@ -242,9 +242,10 @@ class PyBroker:
             if not subject_valid(subject, wildcards=True):
                 c.send(b"-ERR 'Invalid Subject'\r\n")
                 return
-            s = _Sub(c, sid, subject, queue)
-            c.subs[sid] = s
-            self._subs.append(s)
+            if sid not in c.subs:   # nats-server keeps the existing subscription for a live sid
+                s = _Sub(c, sid, subject, queue)
+                c.subs[sid] = s
+                self._subs.append(s)
         elif op == "UNSUB":
             _, sid, max_msgs = ev
             s = c.subs.get(sid)
@@ -267,11 +268,17 @@ class NativeBroker:
     """The C++ NATS server (``_native.NatsServer``) behind the asyncio broker interface."""
 
     def __init__(self, host: str = "127.0.0.1", port: int = 0, max_payload: int = 1 << 20,
-                 max_pending: int = 64 << 20):
+                 max_pending: int = 64 << 20, monitor_port: int = -1):
+        """monitor_port >= 0 (0 = ephemeral): nats-server-style HTTP monitoring (GET /varz,
+        /connz, /subsz, /healthz) -- the reference compose publishes it on 8222."""
         self.host = host
         self.port = port
         self.max_payload = max_payload
-        self._srv = native().NatsServer(host, port, max_payload, max_pending)
+        self._srv = native().NatsServer(host, port, max_payload, max_pending, monitor_port)
+
+    @property
+    def monitor_port(self) -> int:
+        return self._srv.monitor_port
 
     @property
     def url(self) -> str:
@@ -309,9 +316,15 @@ def main() -> None:
     ap.add_argument("--port", type=int, default=4222)
     ap.add_argument("--max-payload", type=int, default=1 << 20)
     ap.add_argument("--impl", choices=sorted(BROKERS), default="native")
+    ap.add_argument("--http-port", type=int, default=-1,
+                    help="native server: HTTP monitoring port (nats-server -m; 8222 in the reference)")
     a = ap.parse_args()
     logging.basicConfig(level=logging.INFO)
-    asyncio.run(BROKERS[a.impl](a.host, a.port, a.max_payload).serve_forever())
+    if a.impl == "native":
+        b = NativeBroker(a.host, a.port, a.max_payload, monitor_port=a.http_port)
+    else:
+        b = PyBroker(a.host, a.port, a.max_payload)
+    asyncio.run(b.serve_forever())
 
 
 if __name__ == "__main__":

@@ -38,6 +38,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cerrno>
 #include <cstring>
 #include <memory>
@@ -214,8 +215,10 @@ static void parse_connect(Conn& c, const char* s, size_t n) {
 
 class Server {
  public:
-  Server(std::string host, int port, long long max_payload, long long max_pending)
-      : host_(std::move(host)), port_(port), max_payload_(max_payload), max_pending_(max_pending) {
+  Server(std::string host, int port, long long max_payload, long long max_pending,
+         int monitor_port = -1)
+      : host_(std::move(host)), port_(port), max_payload_(max_payload), max_pending_(max_pending),
+        mon_port_(monitor_port) {
     std::random_device rd;
     std::mt19937 g(rd());
     const char* al = "ABCDEFGHJKLMNPQRSTUVWXYZ234567";
@@ -254,6 +257,24 @@ class Server {
     wake_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
     add_fd(listen_fd_, EPOLLIN, nullptr);
     add_fd(wake_, EPOLLIN, &wake_tag_);
+    if (mon_port_ >= 0) {  // nats-server's HTTP monitoring port (8222 in the reference compose)
+      mon_fd_ = ::socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+      setsockopt(mon_fd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+      a.sin_port = htons((uint16_t)mon_port_);
+      if (::bind(mon_fd_, (sockaddr*)&a, sizeof a) < 0 || ::listen(mon_fd_, 64) < 0) {
+        const std::string m = strerror(errno);
+        ::close(mon_fd_);
+        mon_fd_ = -1;
+        ::close(ep_);
+        ::close(wake_);
+        fail_close("monitor bind :" + std::to_string(mon_port_) + ": " + m);
+      }
+      len = sizeof a;
+      getsockname(mon_fd_, (sockaddr*)&a, &len);
+      mon_port_ = ntohs(a.sin_port);
+      add_fd(mon_fd_, EPOLLIN, &mon_tag_);
+    }
+    start_time_ = std::chrono::steady_clock::now();
     running_ = true;
     thread_ = std::thread([this] { loop(); });
   }
@@ -266,6 +287,10 @@ class Server {
     thread_.join();
     for (auto& kv : conns_) ::close(kv.first);
     conns_.clear();
+    for (auto& kv : mons_) ::close(kv.second->fd);
+    mons_.clear();
+    if (mon_fd_ >= 0) ::close(mon_fd_);
+    mon_fd_ = -1;
     literal_.clear();
     wild_.clear();
     cache_.clear();
@@ -276,6 +301,7 @@ class Server {
   }
 
   int port() const { return port_; }
+  int monitor_port() const { return mon_fd_ >= 0 ? mon_port_ : -1; }
   bool running() const { return running_; }
 
   struct Counters {
@@ -334,6 +360,14 @@ class Server {
           accept_all();
           continue;
         }
+        if (tag == &mon_tag_) {
+          accept_monitor();
+          continue;
+        }
+        if (auto m = mons_.find(tag); m != mons_.end()) {
+          on_monitor(m->second.get());
+          continue;
+        }
         Conn* c = static_cast<Conn*>(tag);
         if (c->closing) continue;
         if (evs[i].events & (EPOLLERR | EPOLLHUP)) {
@@ -347,6 +381,92 @@ class Server {
       }
       flush_all();
       reap();
+    }
+  }
+
+  // ---- HTTP monitoring (GET /varz, /connz, /subsz, /healthz; one request per connection) ----
+  struct MonConn {
+    int fd;
+    std::string in;
+  };
+
+  void accept_monitor() {
+    for (;;) {
+      const int fd = accept4(mon_fd_, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
+      if (fd < 0) return;
+      auto m = std::make_unique<MonConn>();
+      m->fd = fd;
+      add_fd(fd, EPOLLIN, m.get());
+      mons_[m.get()] = std::move(m);
+    }
+  }
+
+  std::string monitor_body(const std::string& path, int& status) {
+    status = 200;
+    const auto up = std::chrono::duration<double>(std::chrono::steady_clock::now() - start_time_).count();
+    auto num = [](long long v) { return std::to_string(v); };
+    if (path == "/varz" || path == "/") {
+      return "{\"server_id\":\"" + server_id_ + "\",\"server_name\":\"symbiont-natsd\",\"version\":\"" +
+             VERSION + "\",\"host\":\"" + host_ + "\",\"port\":" + num(port_) +
+             ",\"max_payload\":" + num(max_payload_) + ",\"uptime_s\":" + num((long long)up) +
+             ",\"connections\":" + num(n_conns_) + ",\"total_connections\":" + num(total_conns_) +
+             ",\"subscriptions\":" + num(n_subs_) + ",\"slow_consumers\":" + num(slow_) +
+             ",\"in_msgs\":" + num(in_msgs_) + ",\"out_msgs\":" + num(out_msgs_) +
+             ",\"in_bytes\":" + num(in_bytes_) + ",\"out_bytes\":" + num(out_bytes_) + "}";
+    }
+    if (path == "/connz") {
+      std::string o = "{\"num_connections\":" + num((long long)conns_.size()) + ",\"connections\":[";
+      bool first = true;
+      for (auto& kv : conns_) {
+        const Conn* c = kv.second.get();
+        if (!first) o += ',';
+        first = false;
+        o += "{\"cid\":" + num((long long)c->id) + ",\"subscriptions\":" + num((long long)c->subs.size()) +
+             ",\"pending_bytes\":" + num((long long)(c->out.size() - c->out_pos)) + "}";
+      }
+      return o + "]}";
+    }
+    if (path == "/subsz") {
+      return "{\"num_subscriptions\":" + num(n_subs_) + ",\"num_literal_subjects\":" +
+             num((long long)literal_.size()) + ",\"num_wildcard\":" + num((long long)wild_.size()) +
+             ",\"num_cache\":" + num((long long)cache_.size()) + "}";
+    }
+    if (path == "/healthz") return "{\"status\":\"ok\"}";
+    status = 404;
+    return "{\"error\":\"not found\"}";
+  }
+
+  void on_monitor(MonConn* m) {
+    char buf[4096];
+    bool eof = false;
+    for (;;) {
+      const ssize_t r = ::read(m->fd, buf, sizeof buf);
+      if (r > 0) {
+        m->in.append(buf, (size_t)r);
+        if (m->in.size() > 16384) eof = true;
+        continue;
+      }
+      if (r == 0 || (errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR)) eof = true;
+      if (r < 0 && errno == EINTR) continue;
+      break;
+    }
+    if (m->in.find("\r\n\r\n") != std::string::npos) {
+      const size_t sp1 = m->in.find(' '), sp2 = m->in.find(' ', sp1 + 1);
+      std::string path = sp1 == std::string::npos ? "/" : m->in.substr(sp1 + 1, sp2 - sp1 - 1);
+      const size_t q = path.find('?');
+      if (q != std::string::npos) path.resize(q);
+      int status = 200;
+      const std::string body = monitor_body(path, status);
+      const std::string resp = std::string("HTTP/1.1 ") + (status == 200 ? "200 OK" : "404 Not Found") +
+                               "\r\nContent-Type: application/json\r\nContent-Length: " +
+                               std::to_string(body.size()) + "\r\nConnection: close\r\n\r\n" + body;
+      (void)!::send(m->fd, resp.data(), resp.size(), MSG_NOSIGNAL);  // small: fits the socket buffer
+      eof = true;
+    }
+    if (eof) {
+      epoll_ctl(ep_, EPOLL_CTL_DEL, m->fd, nullptr);
+      ::close(m->fd);
+      mons_.erase(m);
     }
   }
 
@@ -488,10 +608,11 @@ class Server {
       sub->toks = split_dots(a[0]);
       sub->wild = std::any_of(sub->toks.begin(), sub->toks.end(),
                               [](const std::string& t) { return t == "*" || t == ">"; });
-      auto old = c->subs.find(sub->sid);
-      if (old != c->subs.end()) unindex(old->second.get());
-      index(sub.get());
-      c->subs[sub->sid] = std::move(sub);
+      // nats-server keeps the existing subscription when a client reuses a live sid
+      if (c->subs.find(sub->sid) == c->subs.end()) {
+        index(sub.get());
+        c->subs[sub->sid] = std::move(sub);
+      }
       ok(c);
     } else if (op_is(s, sp, "UNSUB")) {
       auto a = split_ws(rest, rn);
@@ -729,6 +850,12 @@ class Server {
       for (auto& kv : c->subs) unindex(kv.second.get());
       c->subs.clear();
       epoll_ctl(ep_, EPOLL_CTL_DEL, c->fd, nullptr);
+      // FIN after the queued -ERR, and discard unread input first: closing a socket with unread
+      // bytes sends RST, which can destroy the -ERR line before the client reads it
+      ::shutdown(c->fd, SHUT_WR);
+      char sink[4096];
+      for (int i = 0; i < 256 && ::recv(c->fd, sink, sizeof sink, MSG_DONTWAIT) > 0; ++i) {
+      }
       ::close(c->fd);
       dirty_.erase(std::remove(dirty_.begin(), dirty_.end(), c), dirty_.end());
       conns_.erase(c->fd);
@@ -743,6 +870,9 @@ class Server {
   std::string server_id_;
   int listen_fd_ = -1, ep_ = -1, wake_ = -1;
   int wake_tag_ = 0;
+  int mon_port_ = -1, mon_fd_ = -1, mon_tag_ = 0;
+  std::unordered_map<void*, std::unique_ptr<MonConn>> mons_;
+  std::chrono::steady_clock::time_point start_time_;
   std::thread thread_;
   std::atomic<bool> running_{false};
   uint64_t next_id_ = 0;
@@ -762,9 +892,10 @@ class Server {
 void register_natsd(py::module_& m) {
   using natsd::Server;
   py::class_<Server>(m, "NatsServer")
-      .def(py::init<std::string, int, long long, long long>(), py::arg("host") = "127.0.0.1",
+      .def(py::init<std::string, int, long long, long long, int>(), py::arg("host") = "127.0.0.1",
            py::arg("port") = 0, py::arg("max_payload") = 1ll << 20,
-           py::arg("max_pending") = 64ll << 20)
+           py::arg("max_pending") = 64ll << 20, py::arg("monitor_port") = -1)
+      .def_property_readonly("monitor_port", &Server::monitor_port)
       .def("start", &Server::start)
       .def("stop", &Server::stop, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("port", &Server::port)

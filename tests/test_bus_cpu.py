@@ -266,9 +266,34 @@ async def _script_output(Broker, script):
     return [bytes(o) for o in outs]
 
 
-@settings(max_examples=40, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@settings(max_examples=100, deadline=None, suppress_health_check=[HealthCheck.too_slow])
 @given(st.lists(_OP, min_size=1, max_size=25))
 def test_native_broker_matches_reference_on_random_scripts(script):
     py = run(_script_output(BROKERS["py"], script))
     nat = run(_script_output(BROKERS["native"], script))
     assert nat == py
+
+
+def test_native_broker_http_monitoring():
+    """nats-server-style monitoring endpoints (the reference publishes :8222)."""
+    import httpx
+
+    async def main():
+        b = await BROKERS["native"](monitor_port=0).start()
+        a = await NatsClient.connect(b.url)
+        await a.subscribe("m.*")
+        await a.publish("m.x", b"123")
+        await a.flush()
+        base = f"http://127.0.0.1:{b.monitor_port}"
+        async with httpx.AsyncClient(timeout=5) as c:
+            v = (await c.get(base + "/varz")).json()
+            assert v["version"] == "2.10.7" and v["port"] == b.port and v["connections"] == 1
+            assert v["in_msgs"] == 1 and v["out_msgs"] == 1 and v["in_bytes"] == 3
+            cz = (await c.get(base + "/connz")).json()
+            assert cz["num_connections"] == 1 and cz["connections"][0]["subscriptions"] >= 1
+            assert (await c.get(base + "/subsz")).json()["num_wildcard"] >= 1
+            assert (await c.get(base + "/healthz")).json() == {"status": "ok"}
+            assert (await c.get(base + "/nope")).status_code == 404
+        await a.close()
+        await b.stop()
+    run(main())
