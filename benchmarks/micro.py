@@ -213,6 +213,9 @@ def cmd_gemm(a):
         rr = r if epi >= 2 else None
         var = {"torch_matmul_only": lambda: torch.matmul(x, w.t(), out=y)}
         if epi == K.EPI_RES_LN:
+            tmp = torch.empty_like(y)
+            var["hip_res+add_ln"] = lambda: (K.gemm(x, w, b, K.EPI_RES, rr, out=tmp),
+                                             K.add_ln(tmp, None, g, be, 1e-12, out=y))
             var["hip_bm64"] = lambda: (_hip().gemm_config(64, 0), K.gemm(x, w, b, epi, rr, g, be, 1e-12, out=y))
             var["hip_bm128"] = lambda: (_hip().gemm_config(128, 0), K.gemm(x, w, b, epi, rr, g, be, 1e-12, out=y))
         else:
