@@ -75,6 +75,8 @@ class VectorStore:
             got = vecs.shape[-1] if vecs.ndim else 0
             raise DimensionError(f"Wrong input: Vector dimension error: expected dim: {self.dim}, got {got}")
         with self._lock:
+            if self.group is not None:
+                self.group.check_alive()    # refuse before logging: a refused upsert never lands
             if self.wal is not None:
                 self.wal.append(point_ids, payloads, vecs)
             self._upsert_nolog(point_ids, vecs, payloads)

@@ -35,6 +35,10 @@ log = logging.getLogger("symbiont.index_group")
 OP_STOP, OP_SEARCH, OP_UPSERT, OP_SNAPSHOT, OP_LOAD = 0, 1, 2, 3, 4
 
 
+class RankUnavailableError(RuntimeError):
+    """A peer index rank stopped heart-beating: the op is refused before any collective starts."""
+
+
 class IndexGroup:
     def __init__(self, info: DistInfo, dim: int, capacity_per_rank: int, group=None,
                  dtype: str = "bf16"):
@@ -51,6 +55,13 @@ class IndexGroup:
         self.payload_by_gid: dict[int, tuple[str, Payload]] = {}
         self.gid_by_pid: dict[str, int] = {}
         self.snapshot_root: str | None = None   # shared snapshot directory (all ranks)
+        # rank 0: parallel/heartbeat.HeartbeatMonitor -- refuse ops while a peer is down
+        self.liveness = None
+        # SYMB_FAULT=kill_rank:<r>:<n>: rank r exits after serving n ops (failure tests)
+        from ..services.base import FaultInjector
+
+        self._kill_after = FaultInjector(os.environ.get("SYMB_FAULT", "")).kill_rank.get(info.rank)
+        self._served = 0
 
     # ------------------------------------------------------------------ plumbing
     def _bcast(self, t: torch.Tensor) -> torch.Tensor:
@@ -118,10 +129,20 @@ class IndexGroup:
             dist.barrier(group=self.group)
         return self.shard.count
 
+    def check_alive(self) -> None:
+        m = self.liveness
+        if m is None:
+            return
+        dead = m.dead_ranks()
+        if dead:
+            r, age = dead[0]
+            raise RankUnavailableError(f"index rank {r} unavailable: no heartbeat for {age:.1f}s")
+
     # ------------------------------------------------------------------ rank-0 API
     def snapshot(self, directory: str) -> None:
         """Collective checkpoint of every shard + rank 0's payload table (atomic group.json)."""
         assert self.info.is_root
+        self.check_alive()
         with self._op_lock:
             self._header(OP_SNAPSHOT)
             self._do_snapshot(directory)
@@ -171,6 +192,7 @@ class IndexGroup:
     def search(self, q_unit: torch.Tensor, k: int):
         assert self.info.is_root
         nq = q_unit.shape[0]
+        self.check_alive()
         with self._op_lock:
             self._header(OP_SEARCH, nq, k)
             q = self._bcast(q_unit.to(self.comm_device, torch.float32).contiguous())
@@ -178,6 +200,7 @@ class IndexGroup:
 
     def upsert(self, point_ids: list[str], vecs: torch.Tensor, payloads: list[Payload]) -> list[int]:
         assert self.info.is_root
+        self.check_alive()
         with self._op_lock:
             return self._upsert_locked(point_ids, vecs, payloads)
 
@@ -218,26 +241,36 @@ class IndexGroup:
     # ------------------------------------------------------------------ ranks 1..N-1
     def serve(self) -> None:
         assert not self.info.is_root
-        while True:
-            h = self._header(OP_STOP).tolist()
-            op, a, b = h[0], h[1], h[2]
-            if op == OP_STOP:
-                return
-            if op == OP_SEARCH:
-                q = self._bcast(torch.empty(a, self.dim, dtype=torch.float32, device=self.comm_device))
-                self._do_search(q, b)
-            elif op == OP_UPSERT:
-                v = self._bcast(torch.empty(a, self.dim, dtype=torch.float32, device=self.comm_device))
-                ot = self._bcast(torch.empty(2, a, dtype=torch.int64, device=self.comm_device))
-                self._do_upsert(v, ot[0], ot[1])
-            elif op in (OP_SNAPSHOT, OP_LOAD):
-                if self.snapshot_root is None:
-                    raise RuntimeError("index rank has no snapshot directory (SYMB_SNAPSHOT_DIR)")
-                if op == OP_SNAPSHOT:
-                    self._do_snapshot(self.snapshot_root)
-                else:
-                    c = self._bcast(torch.empty(self.info.world, dtype=torch.int64,
-                                                device=self.comm_device))
-                    self._do_load(self.snapshot_root, c)
+        while self.serve_one():
+            pass
+
+    def serve_one(self) -> bool:
+        """Receive and execute one op from rank 0; False once rank 0 sent OP_STOP."""
+        h = self._header(OP_STOP).tolist()
+        op, a, b = h[0], h[1], h[2]
+        if op == OP_STOP:
+            return False
+        if op == OP_SEARCH:
+            q = self._bcast(torch.empty(a, self.dim, dtype=torch.float32, device=self.comm_device))
+            self._do_search(q, b)
+        elif op == OP_UPSERT:
+            v = self._bcast(torch.empty(a, self.dim, dtype=torch.float32, device=self.comm_device))
+            ot = self._bcast(torch.empty(2, a, dtype=torch.int64, device=self.comm_device))
+            self._do_upsert(v, ot[0], ot[1])
+        elif op in (OP_SNAPSHOT, OP_LOAD):
+            if self.snapshot_root is None:
+                raise RuntimeError("index rank has no snapshot directory (SYMB_SNAPSHOT_DIR)")
+            if op == OP_SNAPSHOT:
+                self._do_snapshot(self.snapshot_root)
             else:
-                raise RuntimeError(f"unknown index op {op}")
+                c = self._bcast(torch.empty(self.info.world, dtype=torch.int64,
+                                            device=self.comm_device))
+                self._do_load(self.snapshot_root, c)
+        else:
+            raise RuntimeError(f"unknown index op {op}")
+        self._served += 1
+        if self._kill_after is not None and self._served >= self._kill_after:
+            log.error("[FAULT] kill_rank: index rank %d exits after %d ops", self.info.rank,
+                      self._served)
+            os._exit(137)
+        return True

@@ -6,7 +6,8 @@ Here: asyncio tasks per message (bounded by a semaphore so a burst cannot exhaus
 a metrics registry (exposed by the api service on ``GET /api/metrics`` and published on
 ``metrics.<service>``), and ``SYMB_FAULT`` injection for failure tests:
 
-    SYMB_FAULT="drop:<subject>:<prob>,delay:<subject>:<ms>,kill:<service>:<after_n_msgs>"
+    SYMB_FAULT="drop:<subject>:<prob>,delay:<subject>:<ms>,kill:<service>:<after_n_msgs>,
+                kill_rank:<index rank>:<after_n_ops>"
 """
 from __future__ import annotations
 
@@ -51,6 +52,7 @@ class FaultInjector:
         self.drop: dict[str, float] = {}
         self.delay: dict[str, float] = {}
         self.kill: dict[str, int] = {}
+        self.kill_rank: dict[int, int] = {}   # parallel/index_group.py: serve_one exits the rank
         for part in (p for p in spec.split(",") if p.strip()):
             kind, target, val = (part.split(":") + ["", ""])[:3]
             if kind == "drop":
@@ -59,6 +61,8 @@ class FaultInjector:
                 self.delay[target] = float(val or 0) / 1000.0
             elif kind == "kill":
                 self.kill[target] = int(val or 0)
+            elif kind == "kill_rank":
+                self.kill_rank[int(target)] = int(val or 0)
 
     async def on_publish(self, subject: str) -> bool:
         """Returns False when the message must be dropped."""

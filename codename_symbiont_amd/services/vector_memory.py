@@ -171,6 +171,15 @@ def main() -> None:
     dim = cfg.index_dim or get_config(cfg.model).hidden
     group = IndexGroup(info, dim, cfg.index_capacity // info.world + 1, dtype=cfg.index_dtype)
     group.snapshot_root = cfg.snapshot_dir or None
+    # liveness: every rank heart-beats on health.index.<rank>; rank 0 refuses ops while a peer is
+    # silent (fast error replies instead of a collective blocked until the RCCL timeout)
+    from ..parallel.heartbeat import Heartbeat, HeartbeatMonitor
+
+    hb = Heartbeat(cfg.nats_url, info.rank, count_fn=lambda: group.shard.count)
+    hb.start()
+    if info.is_root:
+        group.liveness = HeartbeatMonitor(cfg.nats_url, info.world)
+        group.liveness.start()
     try:
         if info.is_root:
             store = VectorStore(dim, 0, snapshot_dir=cfg.snapshot_dir, group=group)
@@ -178,6 +187,9 @@ def main() -> None:
         else:
             group.serve()
     finally:
+        hb.stop()
+        if group.liveness is not None:
+            group.liveness.stop()
         group.stop()
         D.shutdown(info)
 

@@ -244,3 +244,72 @@ def test_dead_index_rank_errors_instead_of_hanging():
     assert not any(p.is_alive() for p in ps)
     assert out.get("result") not in (None, "returned"), out
     assert out["seconds"] < 60
+
+
+def _heartbeat_worker(rank, world, port, nats_url, out):
+    """Rank 2 stops heart-beating (dies) after an upsert; rank 0 must refuse the next search at
+    once instead of entering a collective that would wait for the dead peer."""
+    os.environ["SYMB_COLLECTIVE_TIMEOUT_S"] = "15"
+    # rank 2 dies after the upsert and one healthy search (SYMB_FAULT hook): heartbeats stop
+    os.environ["SYMB_FAULT"] = "kill_rank:2:2"
+    import time
+
+    from codename_symbiont_amd.index.shard import Payload
+    from codename_symbiont_amd.index.store import VectorStore
+    from codename_symbiont_amd.parallel.heartbeat import Heartbeat, HeartbeatMonitor
+    from codename_symbiont_amd.parallel.index_group import IndexGroup, RankUnavailableError
+    info = _init(rank, world, port)
+    grp = IndexGroup(info, dim=8, capacity_per_rank=100)
+    hb = Heartbeat(nats_url, rank, interval=0.2)
+    hb.start()
+    if rank in (1, 2):
+        try:
+            grp.serve()
+        except Exception:  # noqa: BLE001 - the group is torn down under it
+            pass
+        os._exit(0)
+    mon = HeartbeatMonitor(nats_url, world, stale_after=1.0, grace=10.0)
+    mon.start()
+    grp.liveness = mon
+    for _ in range(100):                      # all three ranks heard from
+        if len(mon.last_seen) == world:
+            break
+        time.sleep(0.05)
+    store = VectorStore(8, 0, group=grp)
+    store.upsert(["a", "b", "c"], np.eye(3, 8, dtype=np.float32), [Payload()] * 3)
+    out["healthy_search"] = store.search(np.ones((1, 8), np.float32), 2)[0].shape[1]
+    time.sleep(2.0)                           # rank 2 has been silent for > stale_after
+    t0 = time.time()
+    try:
+        store.search(np.ones((1, 8), np.float32), 2)
+        out["result"] = "returned"
+    except RankUnavailableError as e:
+        out["result"] = str(e)
+    out["seconds"] = time.time() - t0
+    os._exit(0)
+
+
+def test_dead_rank_detected_by_heartbeat_fails_fast():
+    import asyncio
+
+    from codename_symbiont_amd.bus.broker import NativeBroker
+
+    async def start():
+        return await NativeBroker().start()
+    b = asyncio.run(start())
+    mgr = mp.Manager()
+    out = mgr.dict()
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    ps = [ctx.Process(target=_heartbeat_worker, args=(r, 3, port, b.url, out)) for r in range(3)]
+    for p in ps:
+        p.start()
+    ps[0].join(60)
+    for p in ps[1:]:
+        p.join(30)
+        if p.is_alive():
+            p.kill()
+    asyncio.run(b.stop())
+    assert out.get("healthy_search") == 2, dict(out)
+    assert "index rank 2 unavailable: no heartbeat" in out.get("result", ""), dict(out)
+    assert out["seconds"] < 1.0
