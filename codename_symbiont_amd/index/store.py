@@ -111,7 +111,12 @@ class VectorStore:
         qt = torch.nn.functional.normalize(torch.from_numpy(q).to(self.shard.device), dim=-1)
         qt = qt.to(torch.bfloat16)
         if self.group is not None:
-            s, r = self.group.search(qt, k)
+            try:
+                s, r = self.group.search(qt, k)
+            except Exception as e:
+                if hasattr(e, "take"):   # PartialSearchError: hand numpy arrays to the service
+                    e.scores, e.ids = e.scores.float().cpu().numpy(), e.ids.long().cpu().numpy()
+                raise
         else:
             s, r = self.shard.search(qt, k)
         return s.float().cpu().numpy(), r.long().cpu().numpy()

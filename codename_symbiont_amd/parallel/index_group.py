@@ -39,6 +39,19 @@ class RankUnavailableError(RuntimeError):
     """A peer index rank stopped heart-beating: the op is refused before any collective starts."""
 
 
+class PartialSearchError(RankUnavailableError):
+    """A search while a peer is down: carries rank 0's own-shard top-k (``scores``, global
+    ``ids``; -1 = empty) so the service can reply with partial results + an error_message."""
+
+    def __init__(self, msg: str, scores, ids):
+        super().__init__(msg)
+        self.scores, self.ids = scores, ids
+
+    def take(self, j: int, k: int) -> "PartialSearchError":
+        """Query ``j``'s slice (1-D, first ``k``) -- for a batch of coalesced requests."""
+        return PartialSearchError(str(self), self.scores[j, :k], self.ids[j, :k])
+
+
 class IndexGroup:
     def __init__(self, info: DistInfo, dim: int, capacity_per_rank: int, group=None,
                  dtype: str = "bf16"):
@@ -192,7 +205,13 @@ class IndexGroup:
     def search(self, q_unit: torch.Tensor, k: int):
         assert self.info.is_root
         nq = q_unit.shape[0]
-        self.check_alive()
+        try:
+            self.check_alive()
+        except RankUnavailableError as e:
+            # degrade: rank 0 scans its own shard (no collective) -> partial results
+            s, r = self.shard.search(q_unit.to(self.shard.device, torch.bfloat16), k)
+            raise PartialSearchError(f"{e}; partial results from index rank 0 only", s,
+                                     encode_gid(0, r.to(torch.int64))) from None
         with self._op_lock:
             self._header(OP_SEARCH, nq, k)
             q = self._bcast(q_unit.to(self.comm_device, torch.float32).contiguous())

@@ -219,9 +219,10 @@ class SearchBatcher:
             try:
                 s, i = await loop.run_in_executor(None, self._timed_search, qs, kmax)
             except Exception as e:
-                for r in batch:
+                for j, r in enumerate(batch):
                     if not r.fut.done():
-                        r.fut.set_exception(e)
+                        # a partial-result error carries per-query rows: give each its own slice
+                        r.fut.set_exception(e.take(j, r.k) if hasattr(e, "take") else e)
                 continue
             for j, r in enumerate(batch):
                 if not r.fut.done():

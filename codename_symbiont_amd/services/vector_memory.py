@@ -27,6 +27,7 @@ from ..wire import (SemanticSearchNatsResult, SemanticSearchNatsTask, TextWithEm
                     WireError, subjects)
 from .base import Service
 from .batcher import SearchBatcher
+from ..parallel.index_group import PartialSearchError
 
 
 class VectorMemoryService(Service):
@@ -116,11 +117,19 @@ class VectorMemoryService(Service):
                                  f"got {q.shape[0]}")
             with stage("search_request", self.metrics, trace_id=task.request_id, k=task.top_k):
                 scores, rows = await self.searcher.search(q, task.top_k)
+        except PartialSearchError as e:
+            # a peer index rank is down: rank 0's own shard still answers (partial results)
+            partial = f"Qdrant search failed for request_id {task.request_id}: {e}"
+            self.log.error("[SEARCH_HANDLER_QDRANT_FAIL] %s", partial)
+            self.metrics.inc("search.partial")
+            scores, rows = e.scores, e.ids
         except Exception as e:
             err = f"Qdrant search failed for request_id {task.request_id}: {e}"
             self.log.error("[SEARCH_HANDLER_QDRANT_FAIL] %s", err)
             await self.reply(nmsg, SemanticSearchNatsResult(task.request_id, [], err))
             return
+        else:
+            partial = None
         # result JSON = per-point cached fragments around f32 scores (native concatenation; the
         # same bytes as SemanticSearchNatsResult(...).to_json())
         frags, keep = [], []
@@ -137,7 +146,8 @@ class VectorMemoryService(Service):
         if skipped:  # one line per request (the reference logs one per point)
             self.log.warning("[SEARCH_HANDLER] Found %d point(s) with missing or unexpected ID format. "
                              "Skipping.", skipped)
-        body = native().search_result_json(task.request_id, np.asarray(keep, np.float32), frags)
+        body = native().search_result_json(task.request_id, np.asarray(keep, np.float32), frags,
+                                           partial)
         if nmsg.reply:
             await self.nc.publish(nmsg.reply, body)
         else:

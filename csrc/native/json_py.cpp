@@ -229,7 +229,7 @@ std::string format_f32(float f) {
 // formatted like serde_json.  Identical bytes to SemanticSearchNatsResult(...).to_json().
 py::bytes search_result_json(const std::string& request_id,
                              py::array_t<float, py::array::c_style | py::array::forcecast> scores,
-                             py::list frags) {
+                             py::list frags, py::object error_message) {
   const size_t n = (size_t)py::len(frags);
   if ((size_t)scores.size() < n) throw std::runtime_error("fewer scores than fragments");
   const float* sc = scores.data();
@@ -250,13 +250,20 @@ py::bytes search_result_json(const std::string& request_id,
     append_f32(out, sc[i]);
     out.append(b, (size_t)nb);
   }
-  out += "],\"error_message\":null}";
+  out += "],\"error_message\":";
+  if (error_message.is_none()) {
+    out += "null";
+  } else {
+    const std::string e = error_message.cast<std::string>();
+    append_json_string(out, e.data(), e.size());
+  }
+  out += "}";
   return py::bytes(out);
 }
 
 void register_json(py::module_& m) {
   m.def("search_result_json", &search_result_json, py::arg("request_id"), py::arg("scores"),
-        py::arg("frags"));
+        py::arg("frags"), py::arg("error_message") = py::none());
   py::register_exception<JsonError>(m, "JsonError", PyExc_ValueError);
   m.def("json_dumps", &dumps, "serde_json-compatible compact encoding (floats as f32)");
   m.def("json_dumps_f32_array", &dumps_f32_array);

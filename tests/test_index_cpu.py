@@ -133,6 +133,9 @@ def test_search_result_fragments_match_wire_encoding_and_follow_overwrites():
             p.original_document_id, p.source_url, p.sentence_text, p.sentence_order, p.model_name,
             p.processed_at_ms)))
     assert got == SemanticSearchNatsResult("rid", items, None).to_json()
+    err = 'index rank 1 unavailable: "x"'          # partial results carry an error_message
+    assert (native().search_result_json("rid", scores[0], frags, err)
+            == SemanticSearchNatsResult("rid", items, err).to_json())
     row_a = st.shard.payloads.id_to_row["a"]
     assert b'"first \\n one"' in st.result_fragments(row_a)[1]
     st.upsert(["a"], rng.standard_normal((1, 8)).astype(np.float32), [Payload("d1", "u1", "new", 0, "m", 9)])

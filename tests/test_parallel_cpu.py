@@ -285,6 +285,8 @@ def _heartbeat_worker(rank, world, port, nats_url, out):
         out["result"] = "returned"
     except RankUnavailableError as e:
         out["result"] = str(e)
+        out["partial_ranks"] = sorted({int(g) >> 40 for g in e.ids.ravel() if g >= 0})
+        out["partial_n"] = int((e.ids >= 0).sum())
     out["seconds"] = time.time() - t0
     os._exit(0)
 
@@ -312,4 +314,27 @@ def test_dead_rank_detected_by_heartbeat_fails_fast():
     asyncio.run(b.stop())
     assert out.get("healthy_search") == 2, dict(out)
     assert "index rank 2 unavailable: no heartbeat" in out.get("result", ""), dict(out)
+    assert "partial results from index rank 0 only" in out["result"]
+    assert out["partial_ranks"] == [0] and out["partial_n"] >= 1, dict(out)   # rank 0's shard
     assert out["seconds"] < 1.0
+
+
+def test_search_batcher_slices_partial_results():
+    """Coalesced requests each get their own query's partial rows + the error message."""
+    import asyncio
+
+    from codename_symbiont_amd.parallel.index_group import PartialSearchError
+    from codename_symbiont_amd.services.batcher import SearchBatcher
+
+    def search_fn(qs, k):
+        s = np.arange(len(qs) * k, dtype=np.float32).reshape(len(qs), k)
+        raise PartialSearchError("index rank 1 unavailable", s, s.astype(np.int64) + 100)
+
+    async def run():
+        b = SearchBatcher(search_fn, window_ms=20)
+        qs = [b.search(np.ones(4, np.float32), k) for k in (2, 3)]
+        return await asyncio.gather(*qs, return_exceptions=True)
+    e2, e3 = asyncio.run(run())
+    assert isinstance(e2, PartialSearchError) and isinstance(e3, PartialSearchError)
+    assert e2.scores.tolist() == [0, 1] and e3.scores.tolist() == [3, 4, 5]
+    assert e3.ids.tolist() == [103, 104, 105] and "rank 1 unavailable" in str(e3)
