@@ -103,6 +103,26 @@ class Subscription:
             raise StopAsyncIteration
         return m
 
+    async def next_batch(self, max_n: int = 256) -> list[Msg] | None:
+        """Wait for one message, then take whatever else is already queued (up to ``max_n``);
+        None once the subscription has ended."""
+        if self._closed and self._q.empty():
+            return None
+        m = await self._q.get()
+        if m is None:
+            return None
+        batch = [m]
+        while len(batch) < max_n:
+            try:
+                x = self._q.get_nowait()
+            except asyncio.QueueEmpty:
+                break
+            if x is None:              # end marker: deliver this batch, end on the next call
+                self._q.put_nowait(None)
+                break
+            batch.append(x)
+        return batch
+
     async def unsubscribe(self) -> None:
         await self._client._unsubscribe(self)
 
@@ -299,6 +319,17 @@ class NatsClient:
             raise NatsError(f"maximum payload exceeded ({len(payload)} > {self.max_payload})")
         hdr = native().nats_headers(None, None, headers) if headers else None
         await self._send(native().nats_pub(subject, reply, payload, hdr))
+
+    async def publish_many(self, msgs: list[tuple[str, bytes]]) -> None:
+        """Several PUBs in one socket write (replies to a batch of requests)."""
+        out = []
+        for subject, payload in msgs:
+            payload = bytes(payload)
+            if len(payload) > self.max_payload:
+                raise NatsError(f"maximum payload exceeded ({len(payload)} > {self.max_payload})")
+            out.append(native().nats_pub(subject, None, payload, None))
+        if out:
+            await self._send(b"".join(out))
 
     async def subscribe(self, subject: str, queue: str | None = None) -> Subscription:
         self._sid += 1

@@ -138,6 +138,33 @@ class Service:
 
         self._loops.append(asyncio.create_task(loop()))
 
+    async def subscribe_batches(self, subject: str, handler, max_batch: int = 256,
+                                queue: str | None = None) -> None:
+        """Subscribe and call ``await handler(list_of_msgs)`` with everything queued at once (one
+        message at least): under load a handler sees whole bursts, so per-message Python costs
+        (decode, task, reply write) become per-batch costs.  The handler runs in this loop; it
+        may hand work off (spawn) to overlap the next batch with the current one."""
+        sub = await self.nc.subscribe(subject, queue=queue or (self.cfg.queue_group or None))
+        self.log.info("Subscribed to subject: %s", subject)
+
+        async def loop():
+            while True:
+                batch = await sub.next_batch(max_batch)
+                if batch is None:
+                    break
+                self.metrics.inc(f"received.{subject}", len(batch))
+                for _ in batch:
+                    self._count_and_maybe_die()
+                try:
+                    await handler(batch)
+                except Exception:
+                    self.log.exception("[%s] batch handler failed", self.name.upper())
+                    self.metrics.inc("handler_errors")
+            self.log.info("[NATS_LOOP_END] subscription to %s ended.", subject)
+            self._stopped.set()
+
+        self._loops.append(asyncio.create_task(loop()))
+
     async def setup(self) -> None:  # pragma: no cover - overridden
         raise NotImplementedError
 

@@ -52,7 +52,8 @@ class PreprocessingService(Service):
 
     async def setup(self) -> None:
         await self.subscribe_loop(subjects.RAW_TEXT_DISCOVERED, self.handle_raw_text)
-        await self.subscribe_loop(subjects.EMBEDDING_FOR_QUERY, self.handle_query)
+        # query embeddings: whole drained bursts -> one EmbedBatcher request + one socket write
+        await self.subscribe_batches(subjects.EMBEDDING_FOR_QUERY, self.handle_query_batch)
 
     # ------------------------------------------------------------------ ingest
     async def process_text_and_embed(self, raw: RawTextMessage):
@@ -136,6 +137,42 @@ class PreprocessingService(Service):
                     await self.publish(subjects.PROCESSED_TEXT_TOKENIZED, n.json_dumps(obj))
 
     # ------------------------------------------------------------------ query embedding
+    async def handle_query_batch(self, msgs) -> None:
+        """A burst of QueryForEmbeddingTask requests -> one packed encode (through the
+        EmbedBatcher, so it also coalesces with ingest work) -> replies in one write.  Undecodable
+        messages get handle_query's error reply."""
+        tasks, good = [], []
+        for m in msgs:
+            try:
+                tasks.append(QueryForEmbeddingTask.from_json(m.data))
+                good.append(m)
+            except WireError:
+                self.spawn(self.handle_query(m))
+        if tasks:
+            self.log.info("[QUERY_EMBED_HANDLER] Processing %d QueryForEmbeddingTask(s) "
+                          "(request_ids %s..%s)", len(tasks), tasks[0].request_id,
+                          tasks[-1].request_id)
+            self.spawn(self._finish_query_batch(good, tasks))
+
+    async def _finish_query_batch(self, msgs, tasks) -> None:
+        try:
+            out = await self.batcher.embed([t.text_to_embed for t in tasks])
+            errs = [None] * len(tasks)
+        except Exception as e:
+            out = None
+            errs = [f"Failed to generate embedding for request_id {t.request_id}: {e}" for t in tasks]
+            self.log.error("[QUERY_EMBED_HANDLER_GENERATION_FAIL] %s", errs[0])
+        replies = []
+        for j, (m, t) in enumerate(zip(msgs, tasks)):
+            res = QueryEmbeddingResult(t.request_id, None if out is None else out[j],
+                                       self.model_name, errs[j])
+            if m.reply:
+                replies.append((m.reply, res.to_json()))
+            else:
+                self.log.warning("[QUERY_EMBED_HANDLER] No reply subject provided for query "
+                                 "embedding task_id %s. Result not sent.", t.request_id)
+        await self.nc.publish_many(replies)
+
     async def handle_query(self, nmsg) -> None:
         try:
             task = QueryForEmbeddingTask.from_json(nmsg.data)

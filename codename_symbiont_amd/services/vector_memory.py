@@ -46,10 +46,13 @@ class VectorMemoryService(Service):
                       self.cfg.collection, dim, self.store.shard.capacity, self.store.shard.device,
                       self.store.count)
         self.searcher = SearchBatcher(self.store.search, metrics=self.metrics)
+        self._inflight: asyncio.Semaphore | None = None
 
     async def setup(self) -> None:
         await self.subscribe_loop(subjects.TEXT_WITH_EMBEDDINGS, self.handle_store)
-        await self.subscribe_loop(subjects.SEARCH_SEMANTIC_REQUEST, self.handle_search)
+        # searches: whole drained bursts -> one native decode + one index scan + one socket write
+        await self.subscribe_batches(subjects.SEARCH_SEMANTIC_REQUEST, self.handle_search_batch,
+                                     max_batch=self.SEARCH_MAX_BATCH)
 
     # ------------------------------------------------------------------ storage
     async def handle_store(self, nmsg) -> None:
@@ -99,6 +102,86 @@ class VectorMemoryService(Service):
         else:
             self.log.warning("[SEARCH_HANDLER] No reply subject provided for search task_id %s. "
                              "Results not sent.", res.request_id)
+
+    SEARCH_MAX_BATCH = 256      # queries per fused scan launch
+    SEARCH_MAX_INFLIGHT = 2     # scans in flight: batch i+1 decodes/scans while i's replies encode
+
+    async def handle_search_batch(self, msgs) -> None:
+        """A burst of SemanticSearchNatsTask requests: the regular ones are decoded natively into
+        one [n, D] query matrix and answered from one scan; irregular ones (decode errors, wrong
+        dimension, extra keys) take ``handle_search``, which produces the reference's error
+        replies.  The scan runs in an executor thread while this loop goes back for the next
+        burst (at most SEARCH_MAX_INFLIGHT scans in flight)."""
+        ok, ids, topk, q = native().search_tasks_batch([bytes(m.data) for m in msgs], self.store.dim)
+        good = np.flatnonzero(ok)
+        if len(good) < len(msgs):
+            for i in np.flatnonzero(~ok):
+                self.spawn(self.handle_search(msgs[int(i)]))
+        if not len(good):
+            return
+        if self._inflight is None:
+            self._inflight = asyncio.Semaphore(self.SEARCH_MAX_INFLIGHT)
+        await self._inflight.acquire()
+        ks = topk[good]
+        fut = asyncio.get_running_loop().run_in_executor(None, self._batch_search, q[good],
+                                                         int(ks.max()))
+        self.spawn(self._finish_search_batch([msgs[int(i)] for i in good],
+                                             [ids[int(i)] for i in good], ks, fut))
+
+    def _batch_search(self, qs, k):
+        with stage("index_search", self.metrics, nq=len(qs), k=k):
+            return self.store.search(qs, k)
+
+    async def _finish_search_batch(self, msgs, rids, ks, fut) -> None:
+        try:
+            try:
+                scores, rows = await fut
+                errs = [None] * len(msgs)
+            except PartialSearchError as e:
+                scores, rows = e.scores, e.ids
+                errs = [f"Qdrant search failed for request_id {r}: {e}" for r in rids]
+                self.log.error("[SEARCH_HANDLER_QDRANT_FAIL] %s", errs[0])
+                self.metrics.inc("search.partial", len(msgs))
+            except Exception as e:
+                out = []
+                for m, r in zip(msgs, rids):
+                    err = f"Qdrant search failed for request_id {r}: {e}"
+                    self.log.error("[SEARCH_HANDLER_QDRANT_FAIL] %s", err)
+                    if m.reply:
+                        out.append((m.reply, SemanticSearchNatsResult(r, [], err).to_json()))
+                await self.nc.publish_many(out)
+                return
+        finally:
+            self._inflight.release()
+        self.metrics.inc("search.batched_queries", len(msgs))
+        self.metrics.inc("search.launches")
+        out, skipped, sent = [], 0, 0
+        frag = self.store.result_fragments
+        encode = native().search_result_json
+        for j, (m, rid, k) in enumerate(zip(msgs, rids, ks.tolist())):
+            frags, keep = [], []
+            if scores.shape[1]:
+                for sc, r in zip(scores[j, :k].tolist(), rows[j, :k].tolist()):
+                    if r < 0:
+                        continue
+                    f = frag(r)
+                    if f is None:
+                        skipped += 1
+                        continue
+                    frags.append(f)
+                    keep.append(sc)
+            if m.reply:
+                out.append((m.reply, encode(rid, np.asarray(keep, np.float32), frags, errs[j])))
+                sent += 1
+            else:
+                self.log.warning("[SEARCH_HANDLER] No reply subject provided for search task_id %s. "
+                                 "Results not sent.", rid)
+        if skipped:
+            self.log.warning("[SEARCH_HANDLER] Found %d point(s) with missing or unexpected ID format. "
+                             "Skipping.", skipped)
+        await self.nc.publish_many(out)
+        self.log.info("[SEARCH_HANDLER] Sent search results for %d request(s) (one scan, request_ids "
+                      "%s..%s)", sent, rids[0], rids[-1])
 
     async def handle_search(self, nmsg) -> None:
         try:

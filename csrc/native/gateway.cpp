@@ -252,7 +252,7 @@ static unsigned long long want_uint(const JVal& v, const char* name, unsigned lo
 static float want_f32(const JVal& v) {
   if (v.t != JVal::Int && v.t != JVal::Float)
     throw WireErr("invalid type: " + desc(v) + ", expected f32");
-  return (float)std::strtod(v.s.c_str(), nullptr);
+  return (float)parse_f64(v.s.data(), v.s.size());
 }
 
 static const JVal& want_obj(const JVal& v, const char* name) {

@@ -13,6 +13,8 @@
 // buffers to keep 384-1024-float embeddings off the Python object path.
 #include "json.h"
 
+#include <cstdlib>
+
 #include <charconv>
 #include <cmath>
 #include <cstring>
@@ -246,7 +248,9 @@ std::string Parser::string() {
   }
 }
 
-Number Parser::number() {
+static inline bool is_dig(char c) { return (unsigned)(c - '0') < 10u; }
+
+NumSpan Parser::number_span() {
   const size_t st = i_;
   bool is_float = false;
   if (p_[i_] == '-') ++i_;
@@ -254,26 +258,99 @@ Number Parser::number() {
   if (p_[i_] == '0') {
     ++i_;
   } else if (p_[i_] >= '1' && p_[i_] <= '9') {
-    while (i_ < n_ && isdigit((unsigned char)p_[i_])) ++i_;
+    while (i_ < n_ && is_dig(p_[i_])) ++i_;
   } else {
     fail("invalid number");
   }
   if (i_ < n_ && p_[i_] == '.') {
     is_float = true;
     ++i_;
-    if (i_ >= n_ || !isdigit((unsigned char)p_[i_])) fail("invalid number");
-    while (i_ < n_ && isdigit((unsigned char)p_[i_])) ++i_;
+    if (i_ >= n_ || !is_dig(p_[i_])) fail("invalid number");
+    while (i_ < n_ && is_dig(p_[i_])) ++i_;
   }
   if (i_ < n_ && (p_[i_] == 'e' || p_[i_] == 'E')) {
     is_float = true;
     ++i_;
     if (i_ < n_ && (p_[i_] == '+' || p_[i_] == '-')) ++i_;
-    if (i_ >= n_ || !isdigit((unsigned char)p_[i_])) fail("invalid number");
-    while (i_ < n_ && isdigit((unsigned char)p_[i_])) ++i_;
+    if (i_ >= n_ || !is_dig(p_[i_])) fail("invalid number");
+    while (i_ < n_ && is_dig(p_[i_])) ++i_;
   }
+  return NumSpan{st, i_ - st, is_float};
+}
+
+static const double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,
+                                  1e8,  1e9,  1e10, 1e11, 1e12, 1e13, 1e14, 1e15,
+                                  1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+
+double Parser::number_f64() {
+  // one pass: JSON number grammar (number_span's checks) + the decimal mantissa/exponent for
+  // parse_f64's fast path; strtod on the token when the fast path does not apply
+  const size_t st = i_;
+  const bool neg = p_[i_] == '-';
+  if (neg) ++i_;
+  if (i_ >= n_) fail("EOF while parsing a value");
+  // m accumulates every digit (leading zeros add nothing); the digit count from the first
+  // non-zero one decides the fast path (<= 15 significant digits: m < 2^53, exact)
+  const char* p = p_;
+  size_t i = i_;
+  const size_t n = n_;
+  uint64_t m = 0;
+  int e10 = 0;
+  size_t first_sig = SIZE_MAX, frac_digits = 0, int_end;
+  if (p[i] == '0') {
+    ++i;
+  } else if (p[i] >= '1' && p[i] <= '9') {
+    first_sig = i;
+    while (i < n && is_dig(p[i])) m = m * 10 + (uint64_t)(p[i++] - '0');
+  } else {
+    i_ = i;
+    fail("invalid number");
+  }
+  int_end = i;
+  size_t sig_digits = first_sig == SIZE_MAX ? 0 : int_end - first_sig;
+  if (i < n && p[i] == '.') {
+    ++i;
+    if (i >= n || !is_dig(p[i])) {
+      i_ = i;
+      fail("invalid number");
+    }
+    const size_t fs = i;
+    while (i < n && is_dig(p[i])) {
+      if (first_sig == SIZE_MAX && p[i] != '0') first_sig = i;
+      m = m * 10 + (uint64_t)(p[i++] - '0');
+    }
+    frac_digits = i - fs;
+    if (first_sig != SIZE_MAX) sig_digits = first_sig < fs ? (int_end - first_sig) + frac_digits
+                                                          : i - first_sig;
+  }
+  e10 = -(int)frac_digits;
+  bool fast = sig_digits <= 15;
+  i_ = i;
+  if (i_ < n_ && (p_[i_] == 'e' || p_[i_] == 'E')) {
+    ++i_;
+    bool eneg = false;
+    if (i_ < n_ && (p_[i_] == '+' || p_[i_] == '-')) eneg = p_[i_++] == '-';
+    if (i_ >= n_ || !is_dig(p_[i_])) fail("invalid number");
+    int x = 0, nd = 0;
+    while (i_ < n_ && is_dig(p_[i_])) {
+      if (++nd > 4) fast = false;
+      x = x * 10 + (p_[i_++] - '0');
+    }
+    e10 += eneg ? -x : x;
+  }
+  if (fast && m == 0) return neg ? -0.0 : 0.0;
+  if (fast && e10 >= -22 && e10 <= 22) {
+    const double d = e10 >= 0 ? (double)m * kPow10[e10] : (double)m / kPow10[-e10];
+    return neg ? -d : d;
+  }
+  return std::strtod(std::string(p_ + st, i_ - st).c_str(), nullptr);
+}
+
+Number Parser::number() {
+  const NumSpan sp = number_span();
   Number num;
-  num.is_float = is_float;
-  num.text.assign(p_ + st, i_ - st);
+  num.is_float = sp.is_float;
+  num.text.assign(p_ + sp.start, sp.len);
   return num;
 }
 
@@ -283,4 +360,55 @@ void Parser::expect_lit(const char* lit) {
   i_ += L;
 }
 
+
+static bool f64_fast(const char* s, size_t n, double& out) {
+  static const double kP10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,
+                                  1e8,  1e9,  1e10, 1e11, 1e12, 1e13, 1e14, 1e15,
+                                  1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+  size_t i = 0;
+  const bool neg = i < n && s[i] == '-';
+  if (neg) ++i;
+  uint64_t m = 0;
+  int sig = 0, e10 = 0;
+  bool any = false;
+  for (; i < n && s[i] >= '0' && s[i] <= '9'; ++i, any = true) {
+    if ((sig || s[i] != '0') && ++sig > 15) return false;
+    m = m * 10 + (uint64_t)(s[i] - '0');
+  }
+  if (i < n && s[i] == '.') {
+    for (++i; i < n && s[i] >= '0' && s[i] <= '9'; ++i, any = true) {
+      if ((sig || s[i] != '0') && ++sig > 15) return false;
+      m = m * 10 + (uint64_t)(s[i] - '0');
+      --e10;
+    }
+  }
+  if (!any) return false;
+  if (i < n && (s[i] == 'e' || s[i] == 'E')) {
+    ++i;
+    bool eneg = false;
+    if (i < n && (s[i] == '+' || s[i] == '-')) eneg = s[i++] == '-';
+    int x = 0, nd = 0;
+    for (; i < n && s[i] >= '0' && s[i] <= '9'; ++i) {
+      if (++nd > 4) return false;
+      x = x * 10 + (s[i] - '0');
+    }
+    if (!nd) return false;
+    e10 += eneg ? -x : x;
+  }
+  if (i != n) return false;
+  if (m == 0) {
+    out = neg ? -0.0 : 0.0;
+    return true;
+  }
+  if (e10 < -22 || e10 > 22) return false;
+  const double d = e10 >= 0 ? (double)m * kP10[e10] : (double)m / kP10[-e10];
+  out = neg ? -d : d;
+  return true;
+}
+
+double parse_f64(const char* s, size_t n) {
+  double d;
+  if (f64_fast(s, n, d)) return d;
+  return std::strtod(std::string(s, n).c_str(), nullptr);
+}
 }  // namespace symbn

@@ -108,7 +108,7 @@ struct Loader {
       if (!o) throw py::error_already_set();
       return py::reinterpret_steal<py::object>(o);
     }
-    return py::float_(std::strtod(n.text.c_str(), nullptr));
+    return py::float_(parse_f64(n.text.data(), n.text.size()));
   }
 
   py::object value(int depth) {
@@ -148,15 +148,16 @@ struct Loader {
       }
       // fast path: an all-number array becomes a float32 numpy buffer when requested
       std::vector<py::object> items;
-      std::vector<Number> raw;     // numbers seen before the first non-number element
+      std::vector<NumSpan> raw;    // numbers seen before the first non-number element
       bool all_num = f32_arrays;
       for (;;) {
         const char t = p.peek();
         if (all_num && (t == '-' || (t >= '0' && t <= '9'))) {
-          raw.push_back(p.number());
+          raw.push_back(p.number_span());
         } else {
           if (all_num) {  // demote: materialise the numbers parsed so far
-            for (const Number& n : raw) items.push_back(number_obj(n));
+            for (const NumSpan& n : raw)
+              items.push_back(number_obj(Number{n.is_float, std::string(p.data() + n.start, n.len)}));
             raw.clear();
             all_num = false;
           }
@@ -176,14 +177,10 @@ struct Loader {
       if (all_num) {
         py::array_t<float> arr((py::ssize_t)raw.size());
         float* dst = arr.mutable_data();
-        // std::from_chars: correctly rounded like strtof, several times faster (a 384-float
-        // query embedding parsed 52 -> ~12 us)
-        for (size_t i = 0; i < raw.size(); ++i) {
-          const std::string& t = raw[i].text;
-          float f = 0.f;
-          const auto r = std::from_chars(t.data(), t.data() + t.size(), f);
-          dst[i] = r.ec == std::errc() ? f : std::strtof(t.c_str(), nullptr);  // (overflow: ±inf)
-        }
+        // f64 then cast, as serde_json reads an f32 (fast path: a 384-float query embedding
+        // parses in a few us; libstdc++ 11's from_chars<float> goes through strtod)
+        for (size_t i = 0; i < raw.size(); ++i)
+          dst[i] = (float)parse_f64(p.data() + raw[i].start, raw[i].len);
         return std::move(arr);
       }
       py::list l(items.size());
@@ -261,10 +258,101 @@ py::bytes search_result_json(const std::string& request_id,
   return py::bytes(out);
 }
 
+
+// A batch of SemanticSearchNatsTask messages -> (ok[n], request_ids[n], top_k[n], queries[n, dim]).
+// Only the regular shape {"request_id": str, "query_embedding": [dim numbers], "top_k": int}
+// (keys in any order, each once) is decoded here; anything else -- malformed JSON, other keys,
+// wrong types, another length -- gets ok = false and the caller decodes that message with the
+// wire model, which produces serde's exact error text.  vector_memory answers a whole drained
+// batch of search requests with one call and one index scan.
+static py::tuple search_tasks_batch(py::list msgs, int dim) {
+  const size_t n = (size_t)py::len(msgs);
+  py::array_t<bool> ok((py::ssize_t)n);
+  py::array_t<int64_t> topk((py::ssize_t)n);
+  py::array_t<float> q({(py::ssize_t)n, (py::ssize_t)dim});
+  py::list ids(n);
+  bool* okp = ok.mutable_data();
+  int64_t* kp = topk.mutable_data();
+  float* qp = q.mutable_data();
+  for (size_t m = 0; m < n; ++m) {
+    okp[m] = false;
+    kp[m] = 0;
+    ids[m] = py::none();
+    char* buf;
+    Py_ssize_t len;
+    if (PyBytes_AsStringAndSize(msgs[m].ptr(), &buf, &len)) {
+      PyErr_Clear();
+      continue;
+    }
+    Parser p(buf, (size_t)len);
+    float* row = qp + m * (size_t)dim;
+    try {
+      if (p.peek() != '{') continue;
+      p.advance();
+      int seen = 0;  // bit 0 request_id, 1 query_embedding, 2 top_k
+      bool good = true;
+      std::string rid;
+      for (;;) {
+        if (p.peek() != '"') { good = false; break; }
+        const std::string key = p.string();
+        if (p.peek() != ':') { good = false; break; }
+        p.advance();
+        const char c = p.peek();
+        if (key == "request_id" && !(seen & 1) && c == '"') {
+          rid = p.string();
+          seen |= 1;
+        } else if (key == "query_embedding" && !(seen & 2) && c == '[') {
+          p.advance();
+          int cnt = 0;
+          if (p.peek() == ']') {
+            p.advance();
+          } else {
+            for (;;) {
+              const char t = p.peek();
+              if (!(t == '-' || (t >= '0' && t <= '9')) || cnt >= dim) { good = false; break; }
+              row[cnt++] = (float)p.number_f64();
+              const char sep = p.peek();
+              p.advance();
+              if (sep == ']') break;
+              if (sep != ',') { good = false; break; }
+            }
+          }
+          if (!good || cnt != dim) { good = false; break; }
+          seen |= 2;
+        } else if (key == "top_k" && !(seen & 4) && c >= '0' && c <= '9') {
+          const NumSpan sp = p.number_span();
+          if (sp.is_float || sp.len > 10) { good = false; break; }
+          int64_t v = 0;
+          for (size_t i = 0; i < sp.len; ++i) v = v * 10 + (p.data()[sp.start + i] - '0');
+          if (v > 0xFFFFFFFFll) { good = false; break; }  // u32, like the wire model
+          kp[m] = v;
+          seen |= 4;
+        } else {
+          good = false;
+          break;
+        }
+        const char sep = p.peek();
+        p.advance();
+        if (sep == '}') break;
+        if (sep != ',') { good = false; break; }
+      }
+      if (!good || seen != 7 || !p.at_end()) continue;
+      ids[m] = py::str(rid);  // same conversion as json_loads
+      okp[m] = true;
+    } catch (const JsonError&) {
+      continue;
+    } catch (const py::error_already_set&) {
+      continue;
+    }
+  }
+  return py::make_tuple(ok, ids, topk, q);
+}
+
 void register_json(py::module_& m) {
   m.def("search_result_json", &search_result_json, py::arg("request_id"), py::arg("scores"),
         py::arg("frags"), py::arg("error_message") = py::none());
   py::register_exception<JsonError>(m, "JsonError", PyExc_ValueError);
+  m.def("search_tasks_batch", &search_tasks_batch, py::arg("msgs"), py::arg("dim"));
   m.def("json_dumps", &dumps, "serde_json-compatible compact encoding (floats as f32)");
   m.def("json_dumps_f32_array", &dumps_f32_array);
   m.def("json_loads", &loads, py::arg("data"), py::arg("f32_arrays") = false);

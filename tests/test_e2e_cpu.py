@@ -8,6 +8,7 @@ import asyncio
 import json
 
 import httpx
+import numpy as np
 import pytest
 
 from codename_symbiont_amd.bus import NatsClient
@@ -218,4 +219,59 @@ def test_url_to_search_pipeline_with_fixture_site(gw):
             for s in (per, pre, vm):
                 await s.stop()
         await runner.cleanup()
+    run(main())
+
+
+def test_search_and_query_embedding_bursts_are_answered_per_request():
+    """Bursts of concurrent requests are decoded, scanned/encoded and answered as batches
+    (vector_memory / preprocessing batch handlers); each reply must still be its own request's,
+    with its own top_k, and malformed requests in the same burst get their error replies."""
+    from codename_symbiont_amd.wire import (QueryEmbeddingResult, QueryForEmbeddingTask,
+                                            SemanticSearchNatsResult, SemanticSearchNatsTask)
+
+    async def main():
+        async with broker() as b:
+            cfg = cpu_config(b.url)
+            pre = await PreprocessingService(cfg).start()
+            vm = await VectorMemoryService(cfg).start()
+            nc = await NatsClient.connect(b.url)
+            sents = ["Alpha beta gamma.", "Delta epsilon zeta!", "Eta theta iota?", "Kappa lambda mu"]
+            raw = RawTextMessage("doc-b", "http://example.org/b", " ".join(sents), 1)
+            await nc.publish(subjects.RAW_TEXT_DISCOVERED, raw.to_json())
+            for _ in range(200):
+                if vm.store.count >= 4:
+                    break
+                await asyncio.sleep(0.05)
+            assert vm.store.count == 4
+
+            async def embed(i):
+                t = QueryForEmbeddingTask(f"q{i}", sents[i % 4])
+                m = await nc.request(subjects.EMBEDDING_FOR_QUERY, t.to_json(), timeout=30)
+                return QueryEmbeddingResult.from_json(m.data)
+            embs = await asyncio.gather(*[embed(i) for i in range(48)])
+            for i, e in enumerate(embs):
+                assert e.request_id == f"q{i}" and e.error_message is None
+            bad = await nc.request(subjects.EMBEDDING_FOR_QUERY, b'{"request_id": 5}', timeout=30)
+            assert "Failed to deserialize QueryForEmbeddingTask" in \
+                QueryEmbeddingResult.from_json(bad.data).error_message
+
+            async def search(i):
+                if i % 16 == 15:   # wrong dimension inside the burst
+                    t = SemanticSearchNatsTask(f"s{i}", np.ones(7, np.float32), 2)
+                else:
+                    t = SemanticSearchNatsTask(f"s{i}", embs[i].embedding, 1 + i % 4)
+                m = await nc.request(subjects.SEARCH_SEMANTIC_REQUEST, t.to_json(), timeout=30)
+                return SemanticSearchNatsResult.from_json(m.data)
+            res = await asyncio.gather(*[search(i) for i in range(48)])
+            for i, r in enumerate(res):
+                assert r.request_id == f"s{i}"
+                if i % 16 == 15:
+                    assert "Vector dimension error" in r.error_message and not r.results
+                    continue
+                assert r.error_message is None and len(r.results) == 1 + i % 4
+                assert r.results[0].payload.sentence_text == sents[i % 4]
+            assert vm.metrics.snapshot()["counters"].get("search.launches", 0) >= 1
+            await nc.close()
+            await pre.stop()
+            await vm.stop()
     run(main())

@@ -121,3 +121,76 @@ def test_roundtrip_embeddings_exact(vals):
     m = SemanticSearchNatsTask("r", v, 3)
     back = SemanticSearchNatsTask.from_json(m.to_json())
     assert np.array_equal(back.query_embedding, v)
+
+
+_NUM_TEXT = st.one_of(
+    st.floats(allow_nan=False, allow_infinity=False, width=32).map(lambda v: str(np.float32(v))),
+    st.floats(allow_nan=False, allow_infinity=False).map(repr),
+    st.tuples(st.floats(allow_nan=False, allow_infinity=False, min_value=-1e30, max_value=1e30),
+              st.integers(0, 20)).map(lambda t: f"{t[0]:.{t[1]}e}"),
+    st.tuples(st.floats(allow_nan=False, allow_infinity=False, min_value=-1e6, max_value=1e6),
+              st.integers(0, 12)).map(lambda t: f"{t[0]:.{t[1]}f}"),
+    st.integers(-(1 << 60), 1 << 60).map(str),
+    st.sampled_from(["0", "-0", "-0.0", "0e5", "16777217", "16777219", "33554434.0", "1e22",
+                     "1e23", "1e-22", "1e-23", "123456789012345", "1234567890123456",
+                     "0.000000000000000000001", "3.4028235e38", "3.4028236e38", "1E+2", "5e-324"]))
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.lists(_NUM_TEXT, min_size=1, max_size=40))
+def test_number_parsing_matches_serde_semantics(texts):
+    """Floats parse to strtod's double (Python's float()); f32 arrays are that double cast to f32
+    (serde_json's f32 = f64-then-cast), including the fast decimal path's edge cases."""
+    doc = ("[" + ",".join(texts) + "]").encode()
+    got32 = native().json_loads(doc, True)
+    want64 = np.array([float(t) for t in texts], np.float64)
+    with np.errstate(over="ignore"):
+        want32 = want64.astype(np.float32)
+    assert got32.dtype == np.float32
+    assert got32.tobytes() == want32.tobytes(), (texts, got32, want32)
+    got64 = native().json_loads(doc, False)
+    for t, g in zip(texts, got64):
+        v = float(t)
+        if isinstance(g, float):
+            assert g == v and np.signbit(g) == np.signbit(v), (t, g)
+        else:
+            assert g == int(t), (t, g)
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.lists(_NUM_TEXT, min_size=4, max_size=4), st.integers(0, (1 << 32) + 5),
+       st.text(max_size=8))
+def test_search_tasks_batch_matches_wire_model(texts, k, rid):
+    """vector_memory's batch decoder: regular messages decode exactly as SemanticSearchNatsTask
+    (same f32 bits), everything irregular is flagged for the wire-model path."""
+    import json
+
+    from codename_symbiont_amd.wire import SemanticSearchNatsTask, WireError
+    emb = "[" + ",".join(texts) + "]"
+    rid_j = json.dumps(rid)
+    msgs = [
+        f'{{"request_id":{rid_j},"query_embedding":{emb},"top_k":{k}}}',
+        f'{{ "top_k" : {k} , "query_embedding" : {emb}, "request_id" : {rid_j} }}',
+        f'{{"request_id":{rid_j},"query_embedding":{emb},"top_k":{k},"x":1}}',   # extra key
+        f'{{"request_id":{rid_j},"query_embedding":{emb}}}',                     # missing top_k
+        f'{{"request_id":{rid_j},"query_embedding":[1,2,3],"top_k":{k}}}',       # other dim
+        f'{{"request_id":{rid_j},"query_embedding":{emb},"top_k":{k}',           # truncated
+        f'{{"request_id":{rid_j},"query_embedding":{emb},"top_k":-1}}',
+    ]
+    raw = [m.encode() for m in msgs]
+    ok, ids, topk, q = native().search_tasks_batch(raw, 4)
+    for i, m in enumerate(raw):
+        try:
+            t = SemanticSearchNatsTask.from_json(m)
+        except WireError:
+            assert not ok[i], msgs[i]
+            continue
+        if len(t.query_embedding) != 4:
+            assert not ok[i]
+            continue
+        if i >= 2:   # irregular shape: left to the wire model even when it parses
+            assert not ok[i], msgs[i]
+            continue
+        assert ok[i], msgs[i]
+        assert ids[i] == t.request_id and topk[i] == t.top_k
+        assert q[i].tobytes() == np.asarray(t.query_embedding, np.float32).tobytes()
