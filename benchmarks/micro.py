@@ -217,13 +217,20 @@ def cmd_gemm(a):
             var["hip_res+add_ln"] = lambda: (K.gemm(x, w, b, K.EPI_RES, rr, out=tmp),
                                              K.add_ln(tmp, None, g, be, 1e-12, out=y))
             var["hip_bm64"] = lambda: (_hip().gemm_config(64, 0), K.gemm(x, w, b, epi, rr, g, be, 1e-12, out=y))
-            var["hip_bm128"] = lambda: (_hip().gemm_config(128, 0), K.gemm(x, w, b, epi, rr, g, be, 1e-12, out=y))
+            var["hip_bm128"] = lambda: (_hip().gemm_config(128, 3), K.gemm(x, w, b, epi, rr, g, be, 1e-12, out=y))
         else:
-            var["hip_128x128"] = lambda: (_hip().gemm_config(128, 0), K.gemm(x, w, b, epi, rr, g, be, 1e-12, out=y))
-            var["hip_256x128_3st"] = lambda: (_hip().gemm_config(128, 1),
+            var["hip_128x128"] = lambda: (_hip().gemm_config(128, 0, 8), K.gemm(x, w, b, epi, rr, g, be, 1e-12, out=y))
+            var["hip_128x128_rowmajor"] = lambda: (_hip().gemm_config(128, 0, 0),
+                                                   K.gemm(x, w, b, epi, rr, g, be, 1e-12, out=y))
+            var["hip_128x128_g16"] = lambda: (_hip().gemm_config(128, 0, 16),
+                                              K.gemm(x, w, b, epi, rr, g, be, 1e-12, out=y))
+            var["hip_256x128_3st"] = lambda: (_hip().gemm_config(128, 1, 8),
+                                              K.gemm(x, w, b, epi, rr, g, be, 1e-12, out=y))
+            if N % 256 == 0:
+                var["hip_256x256"] = lambda: (_hip().gemm_config(128, 2, 8),
                                               K.gemm(x, w, b, epi, rr, g, be, 1e-12, out=y))
         res = ab(var, rounds=a.rounds, iters=a.iters)
-        _hip().gemm_config(128, 0)
+        _hip().gemm_config(128, 3, 8)
         fl = 2 * M * N * Kd
         out[name] = {k: dict(ms=round(m, 4), TFLOPs=round(fl / (m / 1e3) / 1e12)) for k, (m, _) in res.items()}
     print(json.dumps({"bench": "gemm", "M": M, "results": out}))
@@ -237,9 +244,17 @@ def cmd_encoder(a):
     b = synthetic_batch(cfg, a.batch, a.seq, seed=0).to("cuda")
     o1 = torch.empty(a.batch, cfg.hidden, device="cuda")
     o2 = torch.empty(a.batch, cfg.hidden, device="cuda", dtype=torch.bfloat16)
+    from codename_symbiont_amd.ops._ext import hip as _hip
+
     encs = {p: HipEncoder(cfg, seed=0, precision=p) for p in a.precision.split(",")}
-    res = ab({p: (lambda e=e: e.forward_packed(b, o1, o2)) for p, e in encs.items()},
-             rounds=a.rounds, iters=a.iters)
+    tiles = [int(t) for t in a.tiles.split(",")]
+    var = {}
+    for p, e in encs.items():
+        for t in tiles:
+            name = p if len(tiles) == 1 else f"{p}_tile{t}"
+            var[name] = (lambda e=e, t=t: (_hip().gemm_config(128, t, 8), e.forward_packed(b, o1, o2)))
+    res = ab(var, rounds=a.rounds, iters=a.iters)
+    _hip().gemm_config(128, 3, 8)
     toks = a.batch * a.seq
     fl = cfg.flops_per_token(a.seq) * toks
     out = {p: dict(ms=round(m, 3), embeds_per_s=round(a.batch / (m / 1e3)),
@@ -292,8 +307,26 @@ def cmd_gemmfp8(a):
                 h.quant_rows_fp8(x.data_ptr(), Kd, a8.data_ptr(), Kd, sa.data_ptr(), M, Kd, st)
             h.gemm_fp8(epi, a8.data_ptr(), Kd, w8.data_ptr(), Kd, sa.data_ptr(), sw.data_ptr(),
                        bias.data_ptr(), rr, N, y.data_ptr(), N, M, N, Kd, st)
+        # MX mode as the encoder uses it: GELU layers emit MX fp8 (EPI_GELU_MX8), the others take
+        # an MX-scaled A (E8M0 per 32 k through the MFMA's scale operand), no quantiser pass
+        aexp = torch.full((M, Kd // 32), 127, dtype=torch.uint8, device="cuda")
+        y8 = torch.empty(M, N, dtype=torch.uint8, device="cuda")
+        yexp = torch.empty(M, N // 32, dtype=torch.uint8, device="cuda")
+
+        def fmx():
+            if epi == 1:
+                h.gemm_fp8(4, a8.data_ptr(), Kd, w8.data_ptr(), Kd, sa.data_ptr(), sw.data_ptr(),
+                           bias.data_ptr(), 0, 0, y8.data_ptr(), N, M, N, Kd, st,
+                           cscale=yexp.data_ptr())
+            else:
+                h.gemm_fp8(epi, a8.data_ptr(), Kd, w8.data_ptr(), Kd, 0, sw.data_ptr(),
+                           bias.data_ptr(), rr, N, y.data_ptr(), N, M, N, Kd, st,
+                           ascale=aexp.data_ptr())
         res = ab({"bf16": lambda: K.gemm(x, w, bias, epi, r if epi == 2 else None, out=y),
-                  "fp8_with_quant": lambda: f8(True), "fp8_gemm_only": lambda: f8(False)},
+                  "fp8_with_quant": lambda: f8(True), "fp8_gemm_only": lambda: f8(False),
+                  "fp8_gemm_only_rowmajor": lambda: (h.gemm_config(128, 0, 0), f8(False),
+                                                     h.gemm_config(128, 3, 8)),
+                  "fp8_mx": lambda: fmx()},
                  rounds=a.rounds, iters=a.iters)
         fl = 2 * M * N * Kd
         out[name] = {k: dict(ms=round(m, 4), TFLOPs=round(fl / (m / 1e3) / 1e12)) for k, (m, _) in res.items()}
@@ -332,6 +365,7 @@ def main():
     ap.add_argument("--model", default="minilm-l6")
     ap.add_argument("--seed", type=int, default=1, help="scanabl: seed per-query thresholds")
     ap.add_argument("--precision", default="bf16", help="encoder: comma list of bf16,fp8")
+    ap.add_argument("--tiles", default="0", help="encoder: comma list of gemm_config tile modes")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=5)
     a = ap.parse_args()

@@ -24,7 +24,8 @@ int symb_embed_ln(const int32_t* ids, const int32_t* pos, const int32_t* tt, con
                   const void* pemb, const void* temb, const float* g, const float* b, float eps,
                   void* out, int T, int H, hipStream_t st);
 int symb_add_ln(const void* x, const void* res, const float* g, const float* b, float eps,
-                void* out, int T, int H, hipStream_t st);
+                void* out, int T, int H, hipStream_t st, void* out8 = nullptr,
+                float* scale8 = nullptr);
 int symb_pool(const void* hidden, const int32_t* cu, int B, int H, int mode, int normalize_f32,
               float* out_f32, void* out_norm, hipStream_t st);
 int symb_l2norm_cast(const float* x, void* out, int n, int D, int ld_out, hipStream_t st);
@@ -41,10 +42,11 @@ int symb_index_scan(const void* X, int n_valid, int D, int rows_per_blk, int n_r
 int symb_index_scan_ablate(const void* X, int n_valid, int rows_per_blk, int n_rblk,
                            const void* Q, int NQ, float* cs, int* ci, hipStream_t st, int abl,
                            const float* thr);
-int symb_gemm_config(int resln_bm, int tile);
+int symb_gemm_config(int resln_bm, int tile, int group_m);
 int symb_gemm_fp8(int epi, const void* A8, int lda, const void* W8, int ldw, const float* sa,
                   const float* sw, const float* bias, const void* R, int ldr, void* C, int ldc,
-                  int M, int N, int K, hipStream_t st);
+                  int M, int N, int K, hipStream_t st, const void* ascale = nullptr,
+                  void* cscale = nullptr);
 int symb_quant_rows_fp8(const void* x, int ldx, void* out, int ldo, float* scale, int M, int K,
                         hipStream_t st);
 int symb_quant_fp8(const void* in, int in_f32, int ld_in, uint8_t* out, int ld_out, int n, int D,
@@ -69,7 +71,7 @@ void check(int rc, const char* what) {
   throw std::runtime_error(std::string(what) + ": " + hipGetErrorString((hipError_t)rc));
 }
 
-enum { EPI_BIAS = 0, EPI_GELU = 1, EPI_RES = 2, EPI_RES_LN = 3 };
+enum { EPI_BIAS = 0, EPI_GELU = 1, EPI_RES = 2, EPI_RES_LN = 3, EPI_GELU_MX8 = 4 };
 
 struct LayerWeights {
   uptr wqkv, bqkv, wo, bo, ln1_g, ln1_b, wi, bi, wo2, bo2, ln2_g, ln2_b;
@@ -121,11 +123,16 @@ class EncoderRuntime {
                         P<void>(h), T, H, st),
           "embed_ln");
     const bool fuse_ln = (H == 384);
-    for (const auto& L : layers_) {
+    bool h_quantized = false;  // a8/sa hold the per-token e4m3 image of h (fp8 layers)
+    for (size_t li = 0; li < layers_.size(); ++li) {
+      const auto& L = layers_[li];
       if (L.fp8) {
-        fp8_layer(L, ws, T, B, max_len, cu, st);
+        const bool next_fp8 = li + 1 < layers_.size() && layers_[li + 1].fp8;
+        fp8_layer(L, ws, T, B, max_len, cu, st, h_quantized, next_fp8);
+        h_quantized = next_fp8;
         continue;
       }
+      h_quantized = false;
       check(symb_gemm(EPI_BIAS, P<void>(h), H, P<void>(L.wqkv), H, P<float>(L.bqkv), nullptr, 0,
                       nullptr, nullptr, 0.f, P<void>(qkv), 3 * H, T, 3 * H, H, st),
             "qkv gemm");
@@ -169,18 +176,25 @@ class EncoderRuntime {
   }
 
  private:
-  // e4m3 layer: per-token quantiser -> fp8 MFMA GEMM (scales folded into the epilogue) for each
-  // of the four projections; LayerNorms through symb_add_ln.
+  // e4m3 layer: every projection is an fp8 MFMA GEMM with its scales folded into the epilogue.
+  // Activation hand-offs (no separate quantiser pass except for the attention output):
+  //   h   --(previous layer's ln2, fused per-token quant, or quant_rows here)--> QKV
+  //   ctx --quant_rows--> out-proj --ln1 + fused per-token quant--> FFN1
+  //   FFN1 epilogue emits GELU as MX fp8 (E8M0 per 32 columns) --> FFN2's block-scaled MFMA
+  // h_quantized: a8/sa already hold h's quantisation; quantize_out: leave the output h quantised
+  // in a8/sa for the next (fp8) layer.
   void fp8_layer(const LayerWeights& L, const std::vector<uptr>& ws, int T, int B, int max_len,
-                 uptr cu, hipStream_t st) {
+                 uptr cu, hipStream_t st, bool h_quantized, bool quantize_out) {
     const int H = H_;
-    uptr h = ws[0], h2 = ws[1], qkv = ws[2], ctx = ws[3], ff = ws[4], tmp = ws[5];
+    uptr h = ws[0], h2 = ws[1], qkv = ws[2], ctx = ws[3], tmp = ws[5];
     uptr a8 = ws[6];
     float* sa = P<float>(ws[7]);
+    // the bf16 FFN buffer (T x FF x 2 bytes) holds the MX activation: T x FF e4m3 + T x FF/32 E8M0
+    uptr ff8 = ws[4], ffs = ws[4] + (uptr)T * FF_;
     auto q8 = [&](uptr x, int K, const char* what) {
       check(symb_quant_rows_fp8(P<void>(x), K, P<void>(a8), K, sa, T, K, st), what);
     };
-    q8(h, H, "quant h");
+    if (!h_quantized) q8(h, H, "quant h");
     check(symb_gemm_fp8(EPI_BIAS, P<void>(a8), H, P<void>(L.wqkv), H, sa, P<float>(L.sw_qkv),
                         P<float>(L.bqkv), nullptr, 0, P<void>(qkv), 3 * H, T, 3 * H, H, st),
           "qkv gemm fp8");
@@ -192,18 +206,19 @@ class EncoderRuntime {
                         P<float>(L.bo), P<void>(h), H, P<void>(tmp), H, T, H, H, st),
           "out-proj gemm fp8");
     check(symb_add_ln(P<void>(tmp), nullptr, P<float>(L.ln1_g), P<float>(L.ln1_b), eps_,
-                      P<void>(h2), T, H, st),
-          "ln1");
-    q8(h2, H, "quant h2");
-    check(symb_gemm_fp8(EPI_GELU, P<void>(a8), H, P<void>(L.wi), H, sa, P<float>(L.sw_i),
-                        P<float>(L.bi), nullptr, 0, P<void>(ff), FF_, T, FF_, H, st),
-          "ffn1 gemm fp8");
-    q8(ff, FF_, "quant ff");
-    check(symb_gemm_fp8(EPI_RES, P<void>(a8), FF_, P<void>(L.wo2), FF_, sa, P<float>(L.sw_o2),
-                        P<float>(L.bo2), P<void>(h2), H, P<void>(tmp), H, T, H, FF_, st),
-          "ffn2 gemm fp8");
+                      P<void>(h2), T, H, st, P<void>(a8), sa),
+          "ln1 + quant");
+    check(symb_gemm_fp8(EPI_GELU_MX8, P<void>(a8), H, P<void>(L.wi), H, sa, P<float>(L.sw_i),
+                        P<float>(L.bi), nullptr, 0, P<void>(ff8), FF_, T, FF_, H, st, nullptr,
+                        P<void>(ffs)),
+          "ffn1 gemm fp8 -> mx8");
+    check(symb_gemm_fp8(EPI_RES, P<void>(ff8), FF_, P<void>(L.wo2), FF_, nullptr,
+                        P<float>(L.sw_o2), P<float>(L.bo2), P<void>(h2), H, P<void>(tmp), H, T, H,
+                        FF_, st, P<void>(ffs), nullptr),
+          "ffn2 gemm mx8");
     check(symb_add_ln(P<void>(tmp), nullptr, P<float>(L.ln2_g), P<float>(L.ln2_b), eps_,
-                      P<void>(h), T, H, st),
+                      P<void>(h), T, H, st, quantize_out ? P<void>(a8) : nullptr,
+                      quantize_out ? sa : nullptr),
           "ln2");
   }
 
@@ -226,11 +241,13 @@ PYBIND11_MODULE(_hip, m) {
                         T, H, S(st)),
           "embed_ln");
   });
-  m.def("add_ln", [](uptr x, uptr res, uptr g, uptr b, float eps, uptr out, int T, int H, uptr st) {
+  m.def("add_ln", [](uptr x, uptr res, uptr g, uptr b, float eps, uptr out, int T, int H, uptr st,
+                     uptr out8, uptr scale8) {
     check(symb_add_ln(P<void>(x), P<void>(res), P<float>(g), P<float>(b), eps, P<void>(out), T, H,
-                      S(st)),
+                      S(st), P<void>(out8), P<float>(scale8)),
           "add_ln");
-  });
+  }, py::arg("x"), py::arg("res"), py::arg("g"), py::arg("b"), py::arg("eps"), py::arg("out"),
+     py::arg("T"), py::arg("H"), py::arg("st"), py::arg("out8") = 0, py::arg("scale8") = 0);
   m.def("pool", [](uptr hidden, uptr cu, int B, int H, int mode, int normalize_f32, uptr out_f32,
                    uptr out_norm, uptr st) {
     check(symb_pool(P<void>(hidden), P<int32_t>(cu), B, H, mode, normalize_f32, P<float>(out_f32),
@@ -279,15 +296,20 @@ PYBIND11_MODULE(_hip, m) {
   m.def("attention_config", [](int waves, int kvt) {
     check(symb_attention_config(waves, kvt), "attention_config");
   }, py::arg("waves") = 8, py::arg("kvt") = 64);
-  m.def("gemm_config", [](int resln_bm, int tile) {
-    check(symb_gemm_config(resln_bm, tile), "gemm_config");
-  }, py::arg("resln_bm") = 128, py::arg("tile") = 0);
+  m.def("gemm_config", [](int resln_bm, int tile, int group_m) {
+    check(symb_gemm_config(resln_bm, tile, group_m), "gemm_config");
+  }, py::arg("resln_bm") = 128, py::arg("tile") = 3, py::arg("group_m") = 8);
   m.def("gemm_fp8", [](int epi, uptr A8, int lda, uptr W8, int ldw, uptr sa, uptr sw, uptr bias,
-                       uptr R, int ldr, uptr C, int ldc, int M, int N, int K, uptr st) {
+                       uptr R, int ldr, uptr C, int ldc, int M, int N, int K, uptr st,
+                       uptr ascale, uptr cscale) {
     check(symb_gemm_fp8(epi, P<void>(A8), lda, P<void>(W8), ldw, P<float>(sa), P<float>(sw),
-                        P<float>(bias), P<void>(R), ldr, P<void>(C), ldc, M, N, K, S(st)),
+                        P<float>(bias), P<void>(R), ldr, P<void>(C), ldc, M, N, K, S(st),
+                        P<void>(ascale), P<void>(cscale)),
           "gemm_fp8");
-  });
+  }, py::arg("epi"), py::arg("A8"), py::arg("lda"), py::arg("W8"), py::arg("ldw"), py::arg("sa"),
+     py::arg("sw"), py::arg("bias"), py::arg("R"), py::arg("ldr"), py::arg("C"), py::arg("ldc"),
+     py::arg("M"), py::arg("N"), py::arg("K"), py::arg("st"), py::arg("ascale") = 0,
+     py::arg("cscale") = 0);
   m.def("quant_rows_fp8", [](uptr x, int ldx, uptr out, int ldo, uptr scale, int M, int K, uptr st) {
     check(symb_quant_rows_fp8(P<void>(x), ldx, P<void>(out), ldo, P<float>(scale), M, K, S(st)),
           "quant_rows_fp8");

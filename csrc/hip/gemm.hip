@@ -23,7 +23,7 @@
 
 namespace symb {
 
-enum { EPI_BIAS = 0, EPI_GELU = 1, EPI_RES = 2, EPI_RES_LN = 3 };
+enum { EPI_BIAS = 0, EPI_GELU = 1, EPI_RES = 2, EPI_RES_LN = 3, EPI_GELU_MX8 = 4 };
 
 constexpr int GEMM_BK = 64;  // bf16 elements per k-tile (128-byte rows)
 #ifndef SYMB_GEMM_SCHED
@@ -38,17 +38,53 @@ __device__ __forceinline__ int swz_off(int row, int chunk) {
 typedef __attribute__((ext_vector_type(8))) int i32x8;
 typedef __attribute__((ext_vector_type(4))) int i32x4;
 
+// MX block exponent of 32 values spread over 4 consecutive lanes (8 each, `quad` = lane & 3 of
+// the first): the smallest e with amax * 2^-e < 448 (e4m3's largest finite), as an int in
+// [-127, 127] (E8M0 byte = e + 127).  All 4 lanes must be active.
+__device__ __forceinline__ int mx_block_exponent(const float (&y)[8], int quad) {
+  (void)quad;
+  float amax = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(y[e]));
+  amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
+  amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
+  // amax/448 = m * 2^ex with m in [0.5, 1)  =>  amax * 2^-ex < 448
+  const int ex = __builtin_amdgcn_frexp_expf(amax * (1.0f / 448.0f));
+  return amax > 0.f ? max(-127, min(ex, 127)) : -127;
+}
+
+// 8 floats * 2^-ex -> 8 OCP e4m3 bytes (round to nearest even, saturating).
+__device__ __forceinline__ int2 pack_e4m3x8(const float (&y)[8], int ex) {
+  const float inv = __builtin_amdgcn_ldexpf(1.0f, -ex);
+  int lo = __builtin_amdgcn_cvt_pk_fp8_f32(y[0] * inv, y[1] * inv, 0, false);
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(y[2] * inv, y[3] * inv, lo, true);
+  int hi = __builtin_amdgcn_cvt_pk_fp8_f32(y[4] * inv, y[5] * inv, 0, false);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(y[6] * inv, y[7] * inv, hi, true);
+  return make_int2(lo, hi);
+}
+
 // F8 = true: A, W are OCP e4m3 bytes and one k-tile is 128 elements (still 128-byte LDS rows, so
-// staging and swizzle are shared); v_mfma_f32_16x16x128_f8f6f4 consumes 32 bytes per lane (two
-// swizzled 16-byte chunks), and the epilogue rescales by sa[row] (per-token activation scale) x
+// staging and swizzle are shared); v_mfma_scale_f32_16x16x128_f8f6f4 consumes 32 bytes per lane
+// (swizzled 16-byte chunks g and g + 4 of lane group g), and the epilogue rescales by sa[row] (per-token activation scale) x
 // sw[col] (per-output-channel weight scale) before bias / GELU / residual.
-template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, int NSTAGE = 2, bool F8 = false>
+// AMX = true (F8 only): A is MX-scaled instead -- one E8M0 exponent per 32 consecutive k of a row
+// (ascale[row * K/32 + k/32]).  The exponent goes straight into the block-scaled MFMA's scale_a
+// operand (the 32 k a lane feeds one v_mfma_scale_f32_16x16x128_f8f6f4 are exactly one block),
+// so no per-row rescale is left for the epilogue.
+// EPI_GELU_MX8 (F8 only): GELU(+ bias) emitted as MX fp8 -- e4m3 bytes in C plus one E8M0 scale
+// per 32 output columns in cscale -- which is the A operand format AMX consumes.  The FFN1 -> FFN2
+// hand-off then needs no separate quantiser pass over the 4H-wide activation.
+template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, int NSTAGE = 2, bool F8 = false,
+          bool AMX = false>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
     const void* __restrict__ Av, int lda, const void* __restrict__ Wv, int ldw,
     const float* __restrict__ bias, const __bf16* __restrict__ R, int ldr,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
     __bf16* __restrict__ C, int ldc, int M, int N, int K, const float* __restrict__ sa,
-    const float* __restrict__ sw) {
+    const float* __restrict__ sw, int group_m, const uint8_t* __restrict__ ascale,
+    uint8_t* __restrict__ cscale) {
+  static_assert(!AMX || (F8 && NSTAGE == 2), "MX activations are an fp8 2-stage mode");
+  static_assert(EPI != EPI_GELU_MX8 || (F8 && BN % 32 == 0), "MX output is an fp8 mode");
   constexpr int ES = F8 ? 1 : 2;               // bytes per element
   constexpr int KTILE = 128 / ES;              // elements per 128-byte k-tile row
   const char* A = reinterpret_cast<const char*>(Av);
@@ -58,8 +94,11 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
   constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
   constexpr int RM = WTM / 16, RN = WTN / 16;
   constexpr int TILE_BYTES = (BM + BN) * 128;
-  // RES_LN tiles too tall to stage in fp32 at once are normalised one wave-row band at a time
-  constexpr int EPI_PASSES = (EPI == EPI_RES_LN && BM * (BN + 4) * 4 > 160 * 1024) ? WAVES_M : 1;
+  // AMX: the A tile's E8M0 exponents (BM rows x 4 blocks of 32 k) ride the same LDS ring
+  constexpr int SC_BYTES = (F8 && AMX) ? BM * 4 : 0;
+  constexpr int STAGE_BYTES = TILE_BYTES + SC_BYTES;
+  // tiles too big to stage in fp32 at once are emitted one wave-row band at a time
+  constexpr int EPI_PASSES = (BM * (BN + 4) * 4 > 160 * 1024) ? WAVES_M : 1;
   static_assert((BM * 8) % NT == 0 && (BN * 8) % NT == 0, "tile rows must cover the DMA waves");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -68,11 +107,22 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
   const int n_tiles = N / BN;
   const int nwg = gridDim.x;
   const int tile = xcd_remap(blockIdx.x, nwg);
-  const int m0 = (tile / n_tiles) * BM, n0 = (tile % n_tiles) * BN;
+  // grouped tile order: consecutive tiles (one XCD's in-flight set after xcd_remap) walk a
+  // group_m-row band column by column, so both the A row panels and the W column panels they
+  // touch stay resident in that XCD's 4 MB L2 (row-major order re-streamed all of W per band)
+  int tm = tile / n_tiles, tn = tile % n_tiles;
+  if (group_m > 1) {
+    const int m_tiles = nwg / n_tiles, per_group = group_m * n_tiles;
+    const int g = tile / per_group, first = g * group_m;
+    const int gm = min(group_m, m_tiles - first), local = tile - g * per_group;
+    tm = first + local % gm;
+    tn = local / gm;
+  }
+  const int m0 = tm * BM, n0 = tn * BN;
   const int KT = K / KTILE;
 
   auto stage = [&](int kt, int buf) {
-    char* sA = smem + buf * TILE_BYTES;
+    char* sA = smem + buf * STAGE_BYTES;
     char* sB = sA + BM * 128;
     const size_t k0 = (size_t)kt * 128;         // byte offset of the k-tile
 #pragma unroll
@@ -87,6 +137,15 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
       const int s = i * NT + tid;
       const int row = s >> 3, pc = s & 7, c = pc ^ ((row >> 1) & 7);
       glds16(W + (size_t)(n0 + row) * ldw * ES + k0 + c * 16, sB + (i * NT + wave * 64) * 16);
+    }
+    if constexpr (SC_BYTES > 0) {
+      // one dword (the 4 block exponents of this k-tile) per A row; the first BM/64 waves
+      if (tid < BM) {
+        const int grow = min(m0 + tid, M - 1);
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(ascale + (size_t)grow * (K / 32) + kt * 4),
+            (__attribute__((address_space(3))) void*)(sB + BN * 128 + wave * 64 * 4), 4, 0, 0);
+      }
     }
   };
 
@@ -167,31 +226,43 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
       __builtin_amdgcn_s_barrier();
       if (kt + 2 < KT) stage(kt + 2, (kt + 2) % NSTAGE);
     }
-    const char* sA = smem + (kt % NSTAGE) * TILE_BYTES;
+    const char* sA = smem + (kt % NSTAGE) * STAGE_BYTES;
     const char* sB = sA + BM * 128;
     if constexpr (F8) {
+      // lane group g feeds the MFMA's k = 16g..16g+15 (VGPRs 0-3) and 64+16g.. (VGPRs 4-7), and
+      // the hardware applies lane group b's scale to k block 32b..32b+31 (measured:
+      // benchmarks/diag/mx_scale_map.hip), so reading 16-byte chunks g and g + 4 keeps the MFMA's
+      // k order equal to memory order and every MX block under its own exponent
       const int g = lane >> 4;
+      // AMX: this lane's exponent for each 16-row fragment -- row (lane & 15), k block g
+      int asc[AMX ? RM : 1] = {127};
+      if constexpr (AMX) {
+        const uint8_t* sS = reinterpret_cast<const uint8_t*>(sB + BN * 128);
+#pragma unroll
+        for (int i = 0; i < RM; ++i) asc[i] = sS[(wm * WTM + i * 16 + (lane & 15)) * 4 + g];
+      }
       i32x8 a[RM], b[RN];
 #pragma unroll
       for (int i = 0; i < RM; ++i) {
         const int row = wm * WTM + i * 16 + (lane & 15);
-        const i32x4 lo = *reinterpret_cast<const i32x4*>(sA + swz_off(row, 2 * g));
-        const i32x4 hi = *reinterpret_cast<const i32x4*>(sA + swz_off(row, 2 * g + 1));
+        const i32x4 lo = *reinterpret_cast<const i32x4*>(sA + swz_off(row, g));
+        const i32x4 hi = *reinterpret_cast<const i32x4*>(sA + swz_off(row, g + 4));
         a[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
       }
 #pragma unroll
       for (int j = 0; j < RN; ++j) {
         const int row = wn * WTN + j * 16 + (lane & 15);
-        const i32x4 lo = *reinterpret_cast<const i32x4*>(sB + swz_off(row, 2 * g));
-        const i32x4 hi = *reinterpret_cast<const i32x4*>(sB + swz_off(row, 2 * g + 1));
+        const i32x4 lo = *reinterpret_cast<const i32x4*>(sB + swz_off(row, g));
+        const i32x4 hi = *reinterpret_cast<const i32x4*>(sB + swz_off(row, g + 4));
         b[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
       }
 #pragma unroll
       for (int i = 0; i < RM; ++i)
 #pragma unroll
         for (int j = 0; j < RN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[i], b[j], acc[i][j], 0, 0,
-                                                                       0, 127, 0, 127);
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+              a[i], b[j], acc[i][j], 0, 0, 0, AMX ? asc[i] : 127, 0, 127);
+
     } else {
       // Both k-halves' fragments are read up front and the schedule is pinned: the 8 reads of
       // half 1 are interleaved with half 0's MFMAs (2 MFMAs per read), so only half 0's LDS
@@ -229,85 +300,88 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
   }
 
   // ---- epilogue: fp32 tile -> LDS (padded rows) -> row-contiguous 16-byte stores ----
+  // A tile whose fp32 image does not fit LDS (256-row tiles, row-complete LN tiles) is emitted
+  // one wave-row band per pass.
   constexpr int CS = BN + 4;
+  constexpr int PROWS = BM / EPI_PASSES;
   float* Cs = reinterpret_cast<float*>(smem);
   __syncthreads();
-  if constexpr (EPI == EPI_RES_LN && EPI_PASSES > 1) {
-    // the fp32 row-complete tile does not fit LDS at once: stage one wave-row band per pass
-    for (int p = 0; p < EPI_PASSES; ++p) {
-      if (wm == p) {
+#pragma unroll 1
+  for (int p = 0; p < EPI_PASSES; ++p) {
+    const int band0 = m0 + p * PROWS;  // first global row of this pass
+    if (EPI_PASSES == 1 || wm == p) {
 #pragma unroll
-        for (int i = 0; i < RM; ++i)
+      for (int i = 0; i < RM; ++i)
 #pragma unroll
-          for (int j = 0; j < RN; ++j)
+        for (int j = 0; j < RN; ++j)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int row = i * 16 + (lane >> 4) * 4 + r;
-              const int col = wn * WTN + j * 16 + (lane & 15);
+          for (int r = 0; r < 4; ++r) {
+            const int row = (EPI_PASSES == 1 ? wm * WTM : 0) + i * 16 + (lane >> 4) * 4 + r;
+            const int col = wn * WTN + j * 16 + (lane & 15);
+            if constexpr (F8 && AMX)
+              Cs[row * CS + col] = acc[i][j][r] * sw[n0 + col];
+            else if constexpr (F8)
+              Cs[row * CS + col] = acc[i][j][r] * sa[min(band0 + row, M - 1)] * sw[n0 + col];
+            else
               Cs[row * CS + col] = acc[i][j][r];
-            }
-      }
-      __syncthreads();
-      res_ln_rows(Cs, WTM, m0 + p * WTM);
-      __syncthreads();
+          }
     }
-    return;
-  }
+    __syncthreads();
+    if constexpr (EPI == EPI_RES_LN) {
+      res_ln_rows(Cs, PROWS, band0);
+    } else {
+      constexpr int VPR = BN / 8;
+      for (int v = tid; v < PROWS * VPR; v += NT) {
+        const int row = v / VPR, c8 = (v % VPR) * 8;
+        const int grow = band0 + row;
+        if (grow >= M) continue;
+        const f32x4 x0 = *reinterpret_cast<const f32x4*>(Cs + row * CS + c8);
+        const f32x4 x1 = *reinterpret_cast<const f32x4*>(Cs + row * CS + c8 + 4);
+        const f32x4 b0 = *reinterpret_cast<const f32x4*>(bias + n0 + c8);
+        const f32x4 b1 = *reinterpret_cast<const f32x4*>(bias + n0 + c8 + 4);
+        float y[8];
 #pragma unroll
-  for (int i = 0; i < RM; ++i)
+        for (int e = 0; e < 4; ++e) {
+          y[e] = x0[e] + b0[e];
+          y[e + 4] = x1[e] + b1[e];
+        }
+        if constexpr (EPI == EPI_GELU || EPI == EPI_GELU_MX8) {
 #pragma unroll
-    for (int j = 0; j < RN; ++j)
+          for (int e = 0; e < 8; ++e) y[e] = gelu_erf(y[e]);
+        }
+        if constexpr (EPI == EPI_GELU_MX8) {
+          // the 4 consecutive threads (tid & 3) of one row hold one 32-column MX block
+          uint8_t* C8 = reinterpret_cast<uint8_t*>(C);
+          const int ex = mx_block_exponent(y, tid & 3);
+          *reinterpret_cast<int2*>(C8 + (size_t)grow * ldc + n0 + c8) = pack_e4m3x8(y, ex);
+          if ((tid & 3) == 0) cscale[(size_t)grow * (N / 32) + (n0 + c8) / 32] = (uint8_t)(ex + 127);
+          continue;
+        }
+        if constexpr (EPI == EPI_RES) {
+          float r[8];
+          load8(R + (size_t)grow * ldr + n0 + c8, r);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wm * WTM + i * 16 + (lane >> 4) * 4 + r;
-        const int col = wn * WTN + j * 16 + (lane & 15);
-        if constexpr (F8)
-          Cs[row * CS + col] = acc[i][j][r] * sa[min(m0 + row, M - 1)] * sw[n0 + col];
-        else
-          Cs[row * CS + col] = acc[i][j][r];
+          for (int e = 0; e < 8; ++e) y[e] += r[e];
+        }
+        store8(C + (size_t)grow * ldc + n0 + c8, y);
       }
-  __syncthreads();
-
-  if constexpr (EPI != EPI_RES_LN) {
-    constexpr int VPR = BN / 8;
-    for (int v = tid; v < BM * VPR; v += NT) {
-      const int row = v / VPR, c8 = (v % VPR) * 8;
-      const int grow = m0 + row;
-      if (grow >= M) continue;
-      const f32x4 x0 = *reinterpret_cast<const f32x4*>(Cs + row * CS + c8);
-      const f32x4 x1 = *reinterpret_cast<const f32x4*>(Cs + row * CS + c8 + 4);
-      const f32x4 b0 = *reinterpret_cast<const f32x4*>(bias + n0 + c8);
-      const f32x4 b1 = *reinterpret_cast<const f32x4*>(bias + n0 + c8 + 4);
-      float y[8];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        y[e] = x0[e] + b0[e];
-        y[e + 4] = x1[e] + b1[e];
-      }
-      if constexpr (EPI == EPI_GELU) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) y[e] = gelu_erf(y[e]);
-      }
-      if constexpr (EPI == EPI_RES) {
-        float r[8];
-        load8(R + (size_t)grow * ldr + n0 + c8, r);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) y[e] += r[e];
-      }
-      store8(C + (size_t)grow * ldc + n0 + c8, y);
     }
-  } else {
-    res_ln_rows(Cs, BM, m0);
+    if (EPI_PASSES > 1) __syncthreads();
   }
 }
 
-template <int BM, int BN, int WM, int WN, int EPI, int NSTAGE = 2, bool F8 = false>
+// Rows of tiles per group in the grouped tile order (0/1: plain row-major); see symb_gemm_config.
+static int g_group_m = 8;
+
+template <int BM, int BN, int WM, int WN, int EPI, int NSTAGE = 2, bool F8 = false,
+          bool AMX = false>
 static int launch_cfg(const void* A, int lda, const void* W, int ldw, const float* bias,
                       const __bf16* R, int ldr, const float* g, const float* b, float eps,
                       __bf16* C, int ldc, int M, int N, int K, hipStream_t st,
-                      const float* sa = nullptr, const float* sw = nullptr) {
-  auto kern = gemm_bf16_kernel<BM, BN, WM, WN, EPI, NSTAGE, F8>;
-  constexpr int main_bytes = NSTAGE * (BM + BN) * 128;
+                      const float* sa = nullptr, const float* sw = nullptr,
+                      const uint8_t* ascale = nullptr, uint8_t* cscale = nullptr) {
+  auto kern = gemm_bf16_kernel<BM, BN, WM, WN, EPI, NSTAGE, F8, AMX>;
+  constexpr int main_bytes = NSTAGE * ((BM + BN) * 128 + (AMX ? BM * 4 : 0));
   constexpr int full_epi = BM * (BN + 4) * 4;
   constexpr int epi_bytes = full_epi > 160 * 1024 ? (BM / WM) * (BN + 4) * 4 : full_epi;
   constexpr int lds = main_bytes > epi_bytes ? main_bytes : epi_bytes;
@@ -318,7 +392,7 @@ static int launch_cfg(const void* A, int lda, const void* W, int ldw, const floa
   }
   const int nwg = ((M + BM - 1) / BM) * (N / BN);
   hipLaunchKernelGGL(kern, dim3(nwg), dim3(64 * WM * WN), lds, st, A, lda, W, ldw, bias, R, ldr,
-                     g, b, eps, C, ldc, M, N, K, sa, sw);
+                     g, b, eps, C, ldc, M, N, K, sa, sw, g_group_m, ascale, cscale);
   return (int)hipGetLastError();
 }
 
@@ -329,13 +403,24 @@ using namespace symb;
 // Tile height of the row-complete RES_LN GEMM (64 or 128); a tuning knob, see symb_gemm_config.
 static int g_resln_bm = 128;
 // Tile of the bias / GELU / residual GEMMs: 0 = 128x128 (4 waves, 2-stage ring),
-// 1 = 256x128 (8 waves, 3-stage ring with a tile in flight across each barrier).
-static int g_tile = 0;
-int symb_gemm_config(int resln_bm, int tile) {
+// 1 = 256x128 (8 waves, 3-stage ring with a tile in flight across each barrier),
+// 2 = 256x256 (8 waves of 128x64, 2-stage ring, one workgroup per CU) whenever N % 256 == 0,
+// 3 = auto: 256x256 when N % 256 == 0 and the grid fills whole waves of the 256 CUs (or is
+//     long enough that a partial last wave costs little), else 128x128.
+static int g_tile = 3;
+static bool use_big_tile(int tile, int M, int N) {
+  if (N % 256 != 0 || (tile != 2 && tile != 3)) return false;
+  if (tile == 2) return true;
+  const int tiles = ((M + 255) / 256) * (N / 256);
+  return tiles % 256 == 0 || tiles >= 4 * 256;
+}
+int symb_gemm_config(int resln_bm, int tile, int group_m) {
   if (resln_bm != 64 && resln_bm != 128) return -1;
-  if (tile != 0 && tile != 1) return -1;
+  if (tile < 0 || tile > 3) return -1;
+  if (group_m < 0 || group_m > 64) return -1;
   g_resln_bm = resln_bm;
   g_tile = tile;
+  g_group_m = group_m;
   return 0;
 }
 
@@ -359,6 +444,17 @@ int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const flo
     return -1;  // wider rows: EPI_RES + symb_add_ln
   }
   if (N % 128 != 0) return -1;
+  if (use_big_tile(g_tile, M, N)) {
+#define SYMB_G(E) launch_cfg<256, 256, 2, 4, E>(a, lda, w, ldw, bias, r, ldr, gamma, beta, eps, c, \
+                                               ldc, M, N, K, st)
+    switch (epi) {
+      case EPI_BIAS: return SYMB_G(EPI_BIAS);
+      case EPI_GELU: return SYMB_G(EPI_GELU);
+      case EPI_RES: return SYMB_G(EPI_RES);
+    }
+#undef SYMB_G
+    return -1;
+  }
   if (g_tile == 1) {
 #define SYMB_G(E) launch_cfg<256, 128, 4, 2, E, 3>(a, lda, w, ldw, bias, r, ldr, gamma, beta, eps, \
                                                  c, ldc, M, N, K, st)
@@ -385,20 +481,36 @@ int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const flo
 }
 
 // fp8 GEMM: C = epi((A8 . W8^T) * sa[m] * sw[n] + bias); A8 [M,K], W8 [N,K] OCP e4m3 bytes.
-// epi: EPI_BIAS / EPI_GELU / EPI_RES (row LayerNorms go through symb_add_ln).
+// epi: EPI_BIAS / EPI_GELU / EPI_RES (row LayerNorms go through symb_add_ln), or EPI_GELU_MX8
+// (C receives MX fp8: e4m3 bytes, ldc in bytes, plus E8M0 exponents in cscale [M, N/32]).
+// ascale != nullptr: A8 is MX-scaled (E8M0 per 32 k, [M, K/32]) and sa is unused.
 int symb_gemm_fp8(int epi, const void* A8, int lda, const void* W8, int ldw, const float* sa,
                   const float* sw, const float* bias, const void* R, int ldr, void* C, int ldc,
-                  int M, int N, int K, hipStream_t st) {
+                  int M, int N, int K, hipStream_t st, const void* ascale, void* cscale) {
   if (M <= 0) return 0;
   if (K % 128 != 0 || N % 128 != 0) return -1;
+  if (epi == EPI_GELU_MX8 && !cscale) return -1;
   auto r = (const __bf16*)R;
   auto c = (__bf16*)C;
-#define SYMB_G8(E) launch_cfg<128, 128, 2, 2, E, 2, true>(A8, lda, W8, ldw, bias, r, ldr, nullptr, \
-                                                           nullptr, 0.f, c, ldc, M, N, K, st, sa, sw)
+  auto as = (const uint8_t*)ascale;
+  auto cs = (uint8_t*)cscale;
+#define SYMB_G8(E, X) launch_cfg<128, 128, 2, 2, E, 2, true, X>(A8, lda, W8, ldw, bias, r, ldr,  \
+                                                                nullptr, nullptr, 0.f, c, ldc, M, \
+                                                                N, K, st, sa, sw, as, cs)
+  if (as) {
+    switch (epi) {
+      case EPI_BIAS: return SYMB_G8(EPI_BIAS, true);
+      case EPI_GELU: return SYMB_G8(EPI_GELU, true);
+      case EPI_RES: return SYMB_G8(EPI_RES, true);
+      case EPI_GELU_MX8: return SYMB_G8(EPI_GELU_MX8, true);
+    }
+    return -1;
+  }
   switch (epi) {
-    case EPI_BIAS: return SYMB_G8(EPI_BIAS);
-    case EPI_GELU: return SYMB_G8(EPI_GELU);
-    case EPI_RES: return SYMB_G8(EPI_RES);
+    case EPI_BIAS: return SYMB_G8(EPI_BIAS, false);
+    case EPI_GELU: return SYMB_G8(EPI_GELU, false);
+    case EPI_RES: return SYMB_G8(EPI_RES, false);
+    case EPI_GELU_MX8: return SYMB_G8(EPI_GELU_MX8, false);
   }
 #undef SYMB_G8
   return -1;

@@ -85,7 +85,7 @@ template <int H>
 __global__ __launch_bounds__(256) void add_ln_kernel(
     const __bf16* __restrict__ x_in, const __bf16* __restrict__ res,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
-    __bf16* __restrict__ out, int T) {
+    __bf16* __restrict__ out, int T, uint8_t* __restrict__ out8, float* __restrict__ scale8) {
   constexpr int NV = H / 8;
   constexpr int PER = (NV + 63) / 64;
   const int lane = threadIdx.x & 63;
@@ -121,14 +121,37 @@ __global__ __launch_bounds__(256) void add_ln_kernel(
         ss += d * d;
       }
   const float rstd = rsqrtf(wave_sum(ss) * (1.0f / H) + eps);
+  float amax = 0.f;
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int v = lane + 64 * i;
     if (v < NV) {
-      float y[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) y[e] = (x[i][e] - mean) * rstd * gamma[v * 8 + e] + beta[v * 8 + e];
-      store8(out + (size_t)t * H + v * 8, y);
+      for (int e = 0; e < 8; ++e) {
+        x[i][e] = (x[i][e] - mean) * rstd * gamma[v * 8 + e] + beta[v * 8 + e];
+        amax = fmaxf(amax, fabsf(x[i][e]));
+      }
+      store8(out + (size_t)t * H + v * 8, x[i]);
+    }
+  }
+  if (!out8) return;
+  // fused per-token e4m3 quantiser for the next fp8 GEMM (same scale rule as
+  // quant_rows_fp8_kernel: scale = amax / 448), from the fp32 LN output
+  amax = fmaxf(wave_max(amax), 1e-12f);
+  const float inv = 448.f / amax;
+  if (lane == 0) scale8[t] = amax / 448.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int v = lane + 64 * i;
+    if (v < NV) {
+      float q[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) q[e] = x[i][e] * inv;
+      int lo = __builtin_amdgcn_cvt_pk_fp8_f32(q[0], q[1], 0, false);
+      lo = __builtin_amdgcn_cvt_pk_fp8_f32(q[2], q[3], lo, true);
+      int hi = __builtin_amdgcn_cvt_pk_fp8_f32(q[4], q[5], 0, false);
+      hi = __builtin_amdgcn_cvt_pk_fp8_f32(q[6], q[7], hi, true);
+      *reinterpret_cast<int2*>(out8 + (size_t)t * H + v * 8) = make_int2(lo, hi);
     }
   }
 }
@@ -259,13 +282,15 @@ int symb_embed_ln(const int32_t* ids, const int32_t* pos, const int32_t* tt, con
   return (int)hipGetLastError();
 }
 
+// out8/scale8 (both or neither): also emit the per-token e4m3 quantisation of the output.
 int symb_add_ln(const void* x, const void* res, const float* g, const float* b, float eps,
-                void* out, int T, int H, hipStream_t st) {
+                void* out, int T, int H, hipStream_t st, void* out8, float* scale8) {
   if (T <= 0) return 0;
+  if ((out8 == nullptr) != (scale8 == nullptr)) return -1;
   dim3 grid((T + 3) / 4);
   SYMB_H_DISPATCH(H, hipLaunchKernelGGL(add_ln_kernel<HH>, grid, dim3(256), 0, st,
                                         (const __bf16*)x, (const __bf16*)res, g, b, eps,
-                                        (__bf16*)out, T));
+                                        (__bf16*)out, T, (uint8_t*)out8, scale8));
   return (int)hipGetLastError();
 }
 

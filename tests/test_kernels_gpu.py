@@ -67,20 +67,25 @@ def test_add_ln(H):
     _close(add_ln(x, None, g, b, 1e-5), R.add_ln_ref(x, None, g, b, 1e-5), 3e-2, 1e-2, "ln")
 
 
-@pytest.mark.parametrize("tile", [0, 1])
+@pytest.mark.parametrize("tile", [0, 1, 2])
 @pytest.mark.parametrize("M,N,K,epi", [
     (300, 1152, 384, 0), (129, 1536, 384, 1), (517, 384, 384, 2), (517, 384, 384, 3),
     (300, 384, 1536, 3), (64, 768, 768, 2), (1000, 2304, 768, 0), (77, 1024, 4096, 2),
     (4099, 1536, 384, 1), (700, 384, 1536, 3),
     # > 256 tiles: more tiles than CUs
     (16384, 1152, 384, 0), (12800, 1536, 384, 1), (9000, 768, 3072, 2),
+    # tile=2 (256x256, banded epilogue) on every epilogue, ragged last row tile
+    (2000, 3072, 768, 1), (4353, 768, 3072, 2), (999, 2304, 768, 0),
 ])
 def test_gemm(M, N, K, epi, tile):
     from codename_symbiont_amd.ops._ext import hip
     from codename_symbiont_amd.ops.kernels import gemm
 
-    # tile=1: 256x128 3-stage / 64-row RES_LN
-    hip().gemm_config(64 if tile else 128, tile)
+    # tile=1: 256x128 3-stage / 64-row RES_LN, and a grouped tile order whose last band is short
+    # (group_m=3 rarely divides the row-tile count); tile=0: the default 8-row bands;
+    # tile=2: 256x256 wherever N % 256 == 0 (others fall back to 128x128), row-major order;
+    # the default (3, auto) is covered by the encoder tests
+    hip().gemm_config(64 if tile == 1 else 128, tile, {0: 8, 1: 3, 2: 0}[tile])
 
     a = _bf(M, K, seed=1)
     w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=2)
@@ -91,7 +96,7 @@ def test_gemm(M, N, K, epi, tile):
     try:
         out = gemm(a, w, bias, epi, res, g, b, 1e-12)
     finally:
-        hip().gemm_config(128, 0)
+        hip().gemm_config(128, 3, 8)
     ref = R.gemm_ref(a, w, bias, epi, res, g, b, 1e-12)
     _close(out, ref, atol=4e-2, rtol=2e-2, what=f"gemm epi={epi}")
 
@@ -353,6 +358,117 @@ def test_gemm_fp8(M, N, K, epi):
         exact = exact + res.float()
     _close(out, exact, atol=4e-2, rtol=2e-2, what=f"gemm_fp8 epi={epi}")
     del ref
+
+
+def _mx_quant_ref(x, block=32):
+    """Host MX fp8 quantiser: E8M0 exponent e per 32 consecutive columns (smallest e with
+    amax * 2^-e < 448), e4m3 bytes of x * 2^-e.  Returns (bytes uint8 [M,K], exps int [M,K/32])."""
+    M, K = x.shape
+    xb = x.float().view(M, K // block, block)
+    amax = xb.abs().amax(-1)
+    _, ex = torch.frexp(amax / 448.0)
+    ex = torch.where(amax > 0, ex.clamp(-127, 127), torch.full_like(ex, -127))
+    q = (xb * torch.pow(2.0, -ex.float())[..., None]).to(torch.float8_e4m3fn)
+    return q.view(M, K).view(torch.uint8), ex
+
+
+def _mx_decode(q8, ex, block=32):
+    M, K = q8.shape
+    v = q8.view(torch.float8_e4m3fn).float().view(M, K // block, block)
+    return (v * torch.pow(2.0, ex.float())[..., None]).view(M, K)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(300, 1536, 384), (1000, 4096, 1024), (77, 3072, 768)])
+def test_gemm_fp8_mx_gelu_output(M, N, K):
+    """EPI_GELU_MX8: the FFN1 epilogue's MX fp8 output (e4m3 + E8M0 per 32 columns) decodes to
+    GELU(A8 W8^T * sa * sw + bias) within e4m3 rounding, and its exponents follow the MX rule."""
+    from codename_symbiont_amd.models.encoder import quant_weight_fp8
+    from codename_symbiont_amd.ops._ext import hip, stream_handle
+
+    a = _bf(M, K, seed=11)
+    w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=12)
+    bias = _f(N, scale=0.5, seed=13)
+    a8 = torch.empty(M, K, dtype=torch.uint8, device=DEV)
+    sa = torch.empty(M, dtype=torch.float32, device=DEV)
+    st = stream_handle()
+    hip().quant_rows_fp8(a.data_ptr(), K, a8.data_ptr(), K, sa.data_ptr(), M, K, st)
+    w8, sw = quant_weight_fp8(w)
+    out8 = torch.empty(M, N, dtype=torch.uint8, device=DEV)
+    oexp = torch.empty(M, N // 32, dtype=torch.uint8, device=DEV)
+    hip().gemm_fp8(4, a8.data_ptr(), K, w8.data_ptr(), K, sa.data_ptr(), sw.data_ptr(),
+                   bias.data_ptr(), 0, 0, out8.data_ptr(), N, M, N, K, st,
+                   cscale=oexp.data_ptr())
+    torch.cuda.synchronize()
+    ad = a8.view(torch.float8_e4m3fn).float() * sa[:, None]
+    wd = w8.view(torch.float8_e4m3fn).float() * sw[:, None]
+    exact = torch.nn.functional.gelu(ad @ wd.t() + bias)
+    ex = oexp.long() - 127
+    _, ref_ex = _mx_quant_ref(exact)
+    # exponents agree except where fp32 summation order moves a block max across a power of 2
+    assert (ex == ref_ex).float().mean().item() > 0.995
+    got = _mx_decode(out8, ex)
+    # e4m3 keeps 3 mantissa bits: |err| <= 2^-4 relative, plus the subnormal floor of the block
+    blk_scale = torch.pow(2.0, ex.float()).repeat_interleave(32, dim=1)
+    err = (got - exact).abs()
+    assert (err <= exact.abs() * 0.0625 + blk_scale * 2.0 ** -9 + 1e-3).float().mean().item() > 0.999
+    assert torch.isfinite(got).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K,epi", [(300, 384, 1536, 2), (1000, 1024, 4096, 2),
+                                       (129, 768, 3072, 0), (517, 1536, 384, 1)])
+def test_gemm_fp8_mx_input(M, N, K, epi):
+    """Block-scaled A (MX: E8M0 per 32 k fed to the MFMA's scale operand) == fp32 product of the
+    decoded operands."""
+    from codename_symbiont_amd.models.encoder import quant_weight_fp8
+    from codename_symbiont_amd.ops._ext import hip, stream_handle
+
+    x = torch.nn.functional.gelu(_bf(M, K, scale=2.0, seed=21).float())
+    x[:, : K // 2] *= 8.0        # blocks of different magnitudes -> different exponents
+    q8, ex = _mx_quant_ref(x)
+    a8, aexp = q8.contiguous(), (ex + 127).to(torch.uint8).contiguous()
+    w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=22)
+    bias = _f(N, scale=0.5, seed=23)
+    res = _bf(M, N, seed=24) if epi == 2 else None
+    w8, sw = quant_weight_fp8(w)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    st = stream_handle()
+    hip().gemm_fp8(epi, a8.data_ptr(), K, w8.data_ptr(), K, 0, sw.data_ptr(), bias.data_ptr(),
+                   0 if res is None else res.data_ptr(), N, out.data_ptr(), N, M, N, K, st,
+                   ascale=aexp.data_ptr())
+    torch.cuda.synchronize()
+    ad = _mx_decode(a8, ex)
+    wd = w8.view(torch.float8_e4m3fn).float() * sw[:, None]
+    exact = ad @ wd.t() + bias
+    if epi == 1:
+        exact = torch.nn.functional.gelu(exact)
+    elif epi == 2:
+        exact = exact + res.float()
+    _close(out, exact, atol=6e-2, rtol=2e-2, what=f"gemm_fp8 mx input epi={epi}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H", [768, 1024])
+def test_add_ln_fused_fp8_quant(H):
+    """add_ln's fused per-token e4m3 output == the row quantiser's rule applied to the fp32 LN."""
+    from codename_symbiont_amd.ops._ext import hip, stream_handle
+
+    T = 333
+    x, r = _bf(T, H, seed=31), _bf(T, H, seed=32)
+    g, b = _f(H, scale=0.1, offset=1.0, seed=33), _f(H, scale=0.1, seed=34)
+    out = torch.empty(T, H, dtype=torch.bfloat16, device=DEV)
+    o8 = torch.empty(T, H, dtype=torch.uint8, device=DEV)
+    sc = torch.empty(T, dtype=torch.float32, device=DEV)
+    hip().add_ln(x.data_ptr(), r.data_ptr(), g.data_ptr(), b.data_ptr(), 1e-5, out.data_ptr(), T, H,
+                 stream_handle(), out8=o8.data_ptr(), scale8=sc.data_ptr())
+    torch.cuda.synchronize()
+    y = R.add_ln_ref(x, r, g, b, 1e-5).float()
+    _close(out, y, 3e-2, 1e-2, "add_ln (bf16 out with fused quant)")
+    amax = y.abs().amax(-1)
+    assert torch.allclose(sc, amax / 448.0, rtol=1e-3)
+    ref8 = (y / sc[:, None]).to(torch.float8_e4m3fn).view(torch.uint8)
+    assert (o8 == ref8).float().mean().item() > 0.995
 
 
 @pytest.mark.gpu
