@@ -66,6 +66,9 @@ def main() -> None:
                     help="--mode embed, N > 1: independent replicas, or ONE global batch of "
                          "batch*N sentences per step split over the ranks and gathered back to "
                          "rank 0 over RCCL (parallel/embed_group.py; BASELINE config #4 over xGMI)")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="--mode full: run encode and search back to back on one stream instead of "
+                         "encoding batch i+1 on a second stream while batch i is searched")
     args = ap.parse_args()
 
     from codename_symbiont_amd.index.shard import HbmIndexShard
@@ -113,6 +116,16 @@ def main() -> None:
     consumed = [torch.cuda.Event(), torch.cuda.Event()]
     out_f32 = torch.empty(B, cfg.hidden, device=dev)
     out_unit = torch.empty(B, cfg.hidden, dtype=torch.bfloat16, device=dev)
+    # --mode full pipelines the two halves of a step across two streams: batch i+1 is encoded
+    # on enc_stream while batch i's queries are searched on the compute stream (the scan is
+    # power-bound; the encoder's small kernels fill its tail and launch gaps).  Every timed step
+    # still encodes one batch and searches one batch.
+    overlap = args.mode == "full" and not group_dp and not args.no_overlap
+    enc_stream = torch.cuda.Stream(dev)
+    outs = [(torch.empty(B, cfg.hidden, device=dev),
+             torch.empty(B, cfg.hidden, dtype=torch.bfloat16, device=dev)) for _ in range(2)]
+    enc_done = [torch.cuda.Event(), torch.cuda.Event()]
+    q_free = [torch.cuda.Event(), torch.cuda.Event()]
     q_fixed = torch.nn.functional.normalize(torch.randn(B, cfg.hidden, device=dev), dim=-1).bfloat16()
 
     def prefetch(i: int) -> None:
@@ -127,7 +140,39 @@ def main() -> None:
             d.max_len = h.max_len
             copy_done[slot].record(copy_stream)
 
+    def encode_async(i: int, ev=None) -> None:
+        """Encode batch i on enc_stream into outs[i % 2] (overlap mode)."""
+        slot = i % 2
+        with torch.cuda.stream(enc_stream):
+            enc_stream.wait_event(copy_done[slot])
+            if i >= 2:
+                enc_stream.wait_event(q_free[slot])   # batch i-2's queries are searched
+            if ev:
+                ev[0].record(enc_stream)
+            enc.forward_packed(dbuf[slot], *outs[slot])
+            if ev:
+                ev[1].record(enc_stream)
+            consumed[slot].record(enc_stream)
+            enc_done[slot].record(enc_stream)
+        prefetch(i + 1)
+
+    def step_overlap(i: int, ev=None) -> None:
+        """Search batch i (encoded by the previous step) while batch i+1 encodes."""
+        slot = i % 2
+        encode_async(i + 1, ev)
+        compute.wait_event(enc_done[slot])
+        if ev:
+            ev[2].record(compute)
+        q = outs[slot][1]
+        shard.append_unit(q)
+        searcher.search(q, args.k)
+        q_free[slot].record(compute)
+        if ev:
+            ev[3].record(compute)
+
     def step(i: int, ev=None) -> None:
+        if overlap:
+            return step_overlap(i, ev)
         slot = i % 2
         if ev:
             ev[0].record(compute)
@@ -151,18 +196,21 @@ def main() -> None:
             q = q_fixed
         if ev:
             ev[1].record(compute)
+            ev[2].record(compute)
         if args.mode != "embed":
             searcher.search(q, args.k)
         if ev:
-            ev[2].record(compute)
+            ev[3].record(compute)
 
     prefetch(0)
+    if overlap:
+        encode_async(0)
     for i in range(W):
         step(i)
     torch.cuda.synchronize(dev)
     D.barrier(info)
     torch.cuda.synchronize(dev)
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(K)]
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(K)]
     t_start = time.perf_counter()
     for j in range(K):
         step(W + j, evs[j])
@@ -171,8 +219,8 @@ def main() -> None:
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t_start
     elapsed = D.allreduce_max(info, elapsed)
-    e_ms = sum(a.elapsed_time(b) for a, b, _ in evs) / K
-    s_ms = sum(b.elapsed_time(c) for _, b, c in evs) / K
+    e_ms = sum(a.elapsed_time(b) for a, b, _, _ in evs) / K
+    s_ms = sum(c.elapsed_time(d) for _, _, c, d in evs) / K
 
     ms = elapsed * 1000.0 / K
     total = B * info.world * K / elapsed
@@ -209,6 +257,7 @@ def main() -> None:
                                 else f"dp{info.world}+index_shard{info.world}"),
                 "index_rows": args.index_rows, "dim": cfg.hidden, "top_k": args.k,
                 "mode": args.mode,
+                "encode_search_overlap": overlap,
             },
             "embeds_per_sec": round(total, 2) if args.mode != "search" else 0.0,
             "topk_qps": round(total, 2) if args.mode != "embed" else 0.0,

@@ -73,3 +73,27 @@ def test_ingest_and_search_on_gpu():
             await vm.stop()
     asyncio.run(asyncio.wait_for(main(), 300))
     torch.cuda.synchronize()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("extra", [[], ["--no-overlap"]])
+def test_bench_contract_small_index(extra):
+    """bench.py's driver contract (one JSON line, whole-job value, step timing) on a small index,
+    with and without the encode/search stream overlap."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "3",
+                          "--warmup", "2", "--index-rows", "2000000"] + extra,
+                         capture_output=True, text=True, timeout=300, cwd=root)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 1 and r["steps"] == 3 and r["warmup"] == 2
+    assert r["value"] > 0 and r["higher_is_better"] is True and r["dtype"] == "bf16"
+    assert abs(r["value"] - 256 * 1000.0 / r["ms_per_step"]) / r["value"] < 0.01
+    assert r["config"]["encode_search_overlap"] is (not extra)
