@@ -20,15 +20,20 @@
 //    D*2 + 32 bytes.  Both layouts are conflict-free for their reads (checked with the LDS lane-
 //    group rules, then SQ_LDS_BANK_CONFLICT).
 //  * Output O^T: a lane holds 4 consecutive head dims of one query -> 8-byte stores.
+//  * MX8 (fp8 encoder): the output is emitted as MX fp8 for the out-projection's block-scaled
+//    MFMA -- e4m3 bytes plus one E8M0 exponent per 32 head dims, computed across the 4 lanes that
+//    share a query (a 32-dim block is 2 of a lane's 16-dim output tiles) -- instead of bf16 rows
+//    that a per-token quantiser pass would re-read.
 #include "common.h"
 
 namespace symb {
 
-template <int D, int KVT, int NWAVE>
+template <int D, int KVT, int NWAVE, bool MX8 = false>
 __global__ __launch_bounds__(64 * NWAVE) void attn_varlen_kernel(const __bf16* __restrict__ qkv,
                                                           int ld_qkv, const int32_t* __restrict__ cu,
                                                           int H, float scale_log2,
-                                                          __bf16* __restrict__ out, int ld_out) {
+                                                          __bf16* __restrict__ out, int ld_out,
+                                                          uint8_t* __restrict__ oscale) {
   static_assert(KVT % 32 == 0, "keys per tile");   // 128: a <=128-token sentence in ONE stage
   constexpr int NT = KVT / 16;            // 16-key accumulator tiles
   constexpr int CK = D / 8;               // 16-byte chunks per K/V row
@@ -141,6 +146,34 @@ __global__ __launch_bounds__(64 * NWAVE) void attn_varlen_kernel(const __bf16* _
   lsum += __shfl_xor(lsum, 16, 64);
   lsum += __shfl_xor(lsum, 32, 64);
   const int row = q0 + wave * 16 + c16;
+  if constexpr (MX8) {
+    // block j (32 dims) = output tiles 2j, 2j+1 of the 4 lanes g = 0..3 of this query
+    const float inv = 1.0f / lsum;
+    uint8_t* op8 = reinterpret_cast<uint8_t*>(out) + (size_t)(s0 + min(row, L - 1)) * ld_out + h * D + 4 * g;
+#pragma unroll
+    for (int j = 0; j < D / 32; ++j) {
+      float amax = 0.f;
+#pragma unroll
+      for (int d = 2 * j; d < 2 * j + 2; ++d)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) amax = fmaxf(amax, fabsf(o[d][r] * inv));
+      amax = fmaxf(amax, __shfl_xor(amax, 16, 64));
+      amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+      const int e = __builtin_amdgcn_frexp_expf(amax * (1.0f / 448.0f));
+      const int ex = amax > 0.f ? max(-127, min(e, 127)) : -127;
+      const float sc = __builtin_amdgcn_ldexpf(inv, -ex);
+      if (row < L) {
+#pragma unroll
+        for (int d = 2 * j; d < 2 * j + 2; ++d) {
+          int w = __builtin_amdgcn_cvt_pk_fp8_f32(o[d][0] * sc, o[d][1] * sc, 0, false);
+          w = __builtin_amdgcn_cvt_pk_fp8_f32(o[d][2] * sc, o[d][3] * sc, w, true);
+          *reinterpret_cast<int*>(op8 + d * 16) = w;
+        }
+        if (g == 0) oscale[(size_t)(s0 + row) * (H / 32) + (h * D) / 32 + j] = (uint8_t)(ex + 127);
+      }
+    }
+    return;
+  }
   if (row < L) {
     const float inv = 1.0f / lsum;
     __bf16* op = out + (size_t)(s0 + row) * ld_out + h * D + 4 * g;
@@ -169,16 +202,34 @@ int symb_attention_config(int waves, int kvt) {
   return 0;
 }
 
+// oscale != nullptr: emit MX fp8 (out = e4m3 bytes with ld_out in bytes, oscale = E8M0 per 32
+// columns, [T, H/32]) instead of bf16.
 int symb_attention(const void* qkv, int ld_qkv, const int32_t* cu, int B, int max_len, int n_heads,
-                   int head_dim, void* out, int ld_out, hipStream_t st) {
+                   int head_dim, void* out, int ld_out, hipStream_t st, void* oscale) {
   if (B <= 0 || max_len <= 0) return 0;
+  if (oscale) {
+    const int H = n_heads * head_dim;
+    const float scale_log2 = 1.4426950408889634f / sqrtf((float)head_dim);
+    dim3 grid((max_len + 127) / 128, n_heads, B);
+    if (head_dim == 32)
+      hipLaunchKernelGGL((attn_varlen_kernel<32, 64, 8, true>), grid, dim3(512), 0, st,
+                         (const __bf16*)qkv, ld_qkv, cu, H, scale_log2, (__bf16*)out, ld_out,
+                         (uint8_t*)oscale);
+    else if (head_dim == 64)
+      hipLaunchKernelGGL((attn_varlen_kernel<64, 64, 8, true>), grid, dim3(512), 0, st,
+                         (const __bf16*)qkv, ld_qkv, cu, H, scale_log2, (__bf16*)out, ld_out,
+                         (uint8_t*)oscale);
+    else
+      return -1;
+    return (int)hipGetLastError();
+  }
   const int H = n_heads * head_dim;
   const float scale_log2 = 1.4426950408889634f / sqrtf((float)head_dim);
   const int NW = g_attn_waves;
   dim3 grid((max_len + 16 * NW - 1) / (16 * NW), n_heads, B);
 #define SYMB_A(DD, KV, W) hipLaunchKernelGGL((attn_varlen_kernel<DD, KV, W>), grid, dim3(64 * W), 0, \
                                              st, (const __bf16*)qkv, ld_qkv, cu, H, scale_log2,     \
-                                             (__bf16*)out, ld_out)
+                                             (__bf16*)out, ld_out, nullptr)
 #define SYMB_AW(DD)                                             \
   if (NW == 8 && g_attn_kvt == 128) SYMB_A(DD, 128, 8);         \
   else if (NW == 8) SYMB_A(DD, 64, 8);                          \

@@ -33,7 +33,8 @@ int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const flo
               const void* R, int ldr, const float* gamma, const float* beta, float eps, void* C,
               int ldc, int M, int N, int K, hipStream_t st);
 int symb_attention(const void* qkv, int ld_qkv, const int32_t* cu, int B, int max_len,
-                   int n_heads, int head_dim, void* out, int ld_out, hipStream_t st);
+                   int n_heads, int head_dim, void* out, int ld_out, hipStream_t st,
+                   void* oscale = nullptr);
 int symb_topk_geometry(int D, int kmax, int* lists, int* queries_per_blk);
 int symb_attention_config(int waves, int kvt);
 int symb_index_scan(const void* X, int n_valid, int D, int rows_per_blk, int n_rblk,
@@ -177,20 +178,24 @@ class EncoderRuntime {
 
  private:
   // e4m3 layer: every projection is an fp8 MFMA GEMM with its scales folded into the epilogue.
-  // Activation hand-offs (no separate quantiser pass except for the attention output):
+  // Activation hand-offs (no separate quantiser pass inside a run of fp8 layers):
   //   h   --(previous layer's ln2, fused per-token quant, or quant_rows here)--> QKV
-  //   ctx --quant_rows--> out-proj --ln1 + fused per-token quant--> FFN1
+  //   attention emits ctx as MX fp8 (E8M0 per 32 head dims) --> out-proj's block-scaled MFMA
+  //   out-proj --ln1 + fused per-token quant--> FFN1
   //   FFN1 epilogue emits GELU as MX fp8 (E8M0 per 32 columns) --> FFN2's block-scaled MFMA
   // h_quantized: a8/sa already hold h's quantisation; quantize_out: leave the output h quantised
   // in a8/sa for the next (fp8) layer.
   void fp8_layer(const LayerWeights& L, const std::vector<uptr>& ws, int T, int B, int max_len,
                  uptr cu, hipStream_t st, bool h_quantized, bool quantize_out) {
     const int H = H_;
-    uptr h = ws[0], h2 = ws[1], qkv = ws[2], ctx = ws[3], tmp = ws[5];
+    uptr h = ws[0], h2 = ws[1], qkv = ws[2], tmp = ws[5];
     uptr a8 = ws[6];
     float* sa = P<float>(ws[7]);
-    // the bf16 FFN buffer (T x FF x 2 bytes) holds the MX activation: T x FF e4m3 + T x FF/32 E8M0
-    uptr ff8 = ws[4], ffs = ws[4] + (uptr)T * FF_;
+    // the bf16 FFN buffer (T x FF x 2 bytes) holds the MX activations: T x FF e4m3 + T x FF/32
+    // E8M0 for FFN1 -> FFN2, then T x H/32 E8M0 for the attention output (its e4m3 bytes go to
+    // the bf16 ctx buffer, T x H x 2 bytes)
+    uptr ff8 = ws[4], ffs = ws[4] + (uptr)T * FF_, ctxs = ffs + (uptr)T * (FF_ / 32);
+    uptr ctx8 = ws[3];
     auto q8 = [&](uptr x, int K, const char* what) {
       check(symb_quant_rows_fp8(P<void>(x), K, P<void>(a8), K, sa, T, K, st), what);
     };
@@ -198,13 +203,13 @@ class EncoderRuntime {
     check(symb_gemm_fp8(EPI_BIAS, P<void>(a8), H, P<void>(L.wqkv), H, sa, P<float>(L.sw_qkv),
                         P<float>(L.bqkv), nullptr, 0, P<void>(qkv), 3 * H, T, 3 * H, H, st),
           "qkv gemm fp8");
-    check(symb_attention(P<void>(qkv), 3 * H, P<int32_t>(cu), B, max_len, nh_, hd_, P<void>(ctx),
-                         H, st),
-          "attention");
-    q8(ctx, H, "quant ctx");
-    check(symb_gemm_fp8(EPI_RES, P<void>(a8), H, P<void>(L.wo), H, sa, P<float>(L.sw_o),
-                        P<float>(L.bo), P<void>(h), H, P<void>(tmp), H, T, H, H, st),
-          "out-proj gemm fp8");
+    check(symb_attention(P<void>(qkv), 3 * H, P<int32_t>(cu), B, max_len, nh_, hd_, P<void>(ctx8),
+                         H, st, P<void>(ctxs)),
+          "attention -> mx8");
+    check(symb_gemm_fp8(EPI_RES, P<void>(ctx8), H, P<void>(L.wo), H, nullptr, P<float>(L.sw_o),
+                        P<float>(L.bo), P<void>(h), H, P<void>(tmp), H, T, H, H, st, P<void>(ctxs),
+                        nullptr),
+          "out-proj gemm mx8");
     check(symb_add_ln(P<void>(tmp), nullptr, P<float>(L.ln1_g), P<float>(L.ln1_b), eps_,
                       P<void>(h2), T, H, st, P<void>(a8), sa),
           "ln1 + quant");
@@ -264,11 +269,13 @@ PYBIND11_MODULE(_hip, m) {
           "gemm");
   });
   m.def("attention", [](uptr qkv, int ld_qkv, uptr cu, int B, int max_len, int n_heads,
-                        int head_dim, uptr out, int ld_out, uptr st) {
+                        int head_dim, uptr out, int ld_out, uptr st, uptr oscale) {
     check(symb_attention(P<void>(qkv), ld_qkv, P<int32_t>(cu), B, max_len, n_heads, head_dim,
-                         P<void>(out), ld_out, S(st)),
+                         P<void>(out), ld_out, S(st), P<void>(oscale)),
           "attention");
-  });
+  }, py::arg("qkv"), py::arg("ld_qkv"), py::arg("cu"), py::arg("B"), py::arg("max_len"),
+     py::arg("n_heads"), py::arg("head_dim"), py::arg("out"), py::arg("ld_out"), py::arg("st"),
+     py::arg("oscale") = 0);
   m.def("topk_geometry", [](int D, int kmax) {
     int lists = 0, qpb = 0;
     check(symb_topk_geometry(D, kmax, &lists, &qpb), "topk_geometry");

@@ -472,6 +472,32 @@ def test_add_ln_fused_fp8_quant(H):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("D,nh", [(32, 12), (64, 16)])
+def test_attention_mx8_output(D, nh):
+    """Attention's MX fp8 output (e4m3 + E8M0 per 32 head dims) decodes to the fp32 attention
+    within e4m3 rounding, with the MX exponent rule."""
+    from codename_symbiont_amd.ops._ext import hip, stream_handle
+
+    lens = [1, 7, 64, 65, 128, 3, 100]
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
+    T, H = int(cu[-1]), nh * D
+    qkv = _bf(T, 3 * H, seed=41)
+    o8 = torch.zeros(T, H, dtype=torch.uint8, device=DEV)
+    osc = torch.zeros(T, H // 32, dtype=torch.uint8, device=DEV)
+    hip().attention(qkv.data_ptr(), 3 * H, cu.data_ptr(), len(lens), max(lens), nh, D,
+                    o8.data_ptr(), H, stream_handle(), oscale=osc.data_ptr())
+    torch.cuda.synchronize()
+    ref = R.attention_ref(qkv, cu, nh, D).float()
+    ex = osc.long() - 127
+    _, ref_ex = _mx_quant_ref(ref)
+    assert (ex == ref_ex).float().mean().item() > 0.99
+    got = _mx_decode(o8, ex)
+    blk = torch.pow(2.0, ex.float()).repeat_interleave(32, dim=1)
+    err = (got - ref).abs()
+    assert (err <= ref.abs() * 0.07 + blk * 2.0 ** -8 + 2e-2).all(), err.max()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("model", ["minilm-l6", "bge-base"])
 def test_encoder_fp8_close_to_fp32_oracle(model):
     """fp8 encoder (e4m3 GEMMs, per-channel / per-token scales) keeps cosine >= 0.99 vs fp32."""
