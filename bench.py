@@ -126,6 +126,10 @@ def main() -> None:
              torch.empty(B, cfg.hidden, dtype=torch.bfloat16, device=dev)) for _ in range(2)]
     enc_done = [torch.cuda.Event(), torch.cuda.Event()]
     q_free = [torch.cuda.Event(), torch.cuda.Event()]
+    # SYMB_GPU_DEBUG=1: assert the host enqueue order the events above rely on
+    from codename_symbiont_amd.utils.gpu_debug import BufferRing
+
+    in_ring, out_ring = BufferRing(2, "bench.dbuf"), BufferRing(2, "bench.outs")
     q_fixed = torch.nn.functional.normalize(torch.randn(B, cfg.hidden, device=dev), dim=-1).bfloat16()
 
     def prefetch(i: int) -> None:
@@ -134,6 +138,8 @@ def main() -> None:
             if i >= 2:
                 copy_stream.wait_event(consumed[slot])
             h, d = host[i % NB], dbuf[slot]
+            if overlap:
+                in_ring.fill(slot)
             d.ids.copy_(h.ids, non_blocking=True)
             d.pos.copy_(h.pos, non_blocking=True)
             d.cu_seqlens.copy_(h.cu_seqlens, non_blocking=True)
@@ -149,6 +155,8 @@ def main() -> None:
                 enc_stream.wait_event(q_free[slot])   # batch i-2's queries are searched
             if ev:
                 ev[0].record(enc_stream)
+            in_ring.consume(slot)
+            out_ring.fill(slot)
             enc.forward_packed(dbuf[slot], *outs[slot])
             if ev:
                 ev[1].record(enc_stream)
@@ -166,6 +174,7 @@ def main() -> None:
         q = outs[slot][1]
         shard.append_unit(q)
         searcher.search(q, args.k)
+        out_ring.consume(slot)
         q_free[slot].record(compute)
         if ev:
             ev[3].record(compute)

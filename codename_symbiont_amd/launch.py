@@ -61,8 +61,10 @@ class Child:
 
 
 def build_children(a) -> list[Child]:
+    from .utils.gpu_debug import debug_env
+
     py = sys.executable
-    base = dict(os.environ)
+    base = debug_env()   # + AMD_SERIALIZE_KERNEL / HIP_LAUNCH_BLOCKING under SYMB_GPU_DEBUG=1
     base.setdefault("NATS_URL", f"nats://127.0.0.1:{a.broker_port}")
     base["API_SERVER_PORT"] = str(a.api_port)
     only = set(a.only.split(",")) if a.only else set(SERVICES)

@@ -22,12 +22,17 @@ class ExtensionMissing(RuntimeError):
 @functools.lru_cache(maxsize=None)
 def hip():
     try:
-        return importlib.import_module("codename_symbiont_amd._hip")
+        mod = importlib.import_module("codename_symbiont_amd._hip")
     except ImportError as e:  # pragma: no cover - exercised only on broken installs
         raise ExtensionMissing(
             "codename_symbiont_amd._hip is not built; run `python csrc/build.py` "
             "(hipcc --offload-arch=gfx950)"
         ) from e
+    from ..utils.gpu_debug import debug_enabled
+
+    # SYMB_GPU_DEBUG=1: every kernel launch is synchronized and checked (fault attribution)
+    mod.set_debug(debug_enabled())
+    return mod
 
 
 @functools.lru_cache(maxsize=None)

@@ -66,8 +66,20 @@ template <class T>
 inline T* P(uptr p) { return reinterpret_cast<T*>(p); }
 inline hipStream_t S(uptr s) { return reinterpret_cast<hipStream_t>(s); }
 
+// GPU debug mode (SYMB_GPU_DEBUG=1, ops/_ext.py): every launch is followed by a device-wide
+// synchronize, so an asynchronous fault (bad address, illegal instruction) is raised by the call
+// that launched the faulting kernel, named, instead of by some later unrelated sync point.
+static bool g_debug = false;
+
 void check(int rc, const char* what) {
-  if (rc == 0) return;
+  if (rc == 0) {
+    if (!g_debug) return;
+    rc = (int)hipDeviceSynchronize();
+    if (rc == 0) rc = (int)hipGetLastError();
+    if (rc == 0) return;
+    throw std::runtime_error(std::string(what) + " [serialized, SYMB_GPU_DEBUG]: " +
+                             hipGetErrorString((hipError_t)rc));
+  }
   if (rc < 0) throw std::invalid_argument(std::string(what) + ": unsupported shape/config");
   throw std::runtime_error(std::string(what) + ": " + hipGetErrorString((hipError_t)rc));
 }
@@ -239,6 +251,8 @@ class EncoderRuntime {
 PYBIND11_MODULE(_hip, m) {
   m.doc() = "CDNA4 (gfx950) HIP kernels of codename_symbiont_amd";
   m.def("arch", []() { return std::string("gfx950"); });
+  m.def("set_debug", [](bool on) { g_debug = on; }, py::arg("on"));
+  m.def("debug", []() { return g_debug; });
   m.def("embed_ln", [](uptr ids, uptr pos, uptr tt, uptr wemb, uptr pemb, uptr temb, uptr g,
                        uptr b, float eps, uptr out, int T, int H, uptr st) {
     check(symb_embed_ln(P<int32_t>(ids), P<int32_t>(pos), P<int32_t>(tt), P<void>(wemb),

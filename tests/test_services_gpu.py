@@ -76,8 +76,8 @@ def test_ingest_and_search_on_gpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("extra", [[], ["--no-overlap"]])
-def test_bench_contract_small_index(extra):
+@pytest.mark.parametrize("extra,debug", [([], False), (["--no-overlap"], False), ([], True)])
+def test_bench_contract_small_index(extra, debug):
     """bench.py's driver contract (one JSON line, whole-job value, step timing) on a small index,
     with and without the encode/search stream overlap."""
     import json
@@ -88,7 +88,8 @@ def test_bench_contract_small_index(extra):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "3",
                           "--warmup", "2", "--index-rows", "2000000"] + extra,
-                         capture_output=True, text=True, timeout=300, cwd=root)
+                         capture_output=True, text=True, timeout=300, cwd=root,
+                         env=dict(os.environ, SYMB_GPU_DEBUG="1" if debug else "0"))
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, out.stdout
@@ -97,3 +98,26 @@ def test_bench_contract_small_index(extra):
     assert r["value"] > 0 and r["higher_is_better"] is True and r["dtype"] == "bf16"
     assert abs(r["value"] - 256 * 1000.0 / r["ms_per_step"]) / r["value"] < 0.01
     assert r["config"]["encode_search_overlap"] is (not extra)
+
+
+@pytest.mark.gpu
+def test_gpu_debug_mode_serializes_and_matches():
+    """SYMB_GPU_DEBUG's launch serialization (sync + check after every kernel) leaves the
+    encoder's results bit-identical."""
+    from codename_symbiont_amd.models import get_config
+    from codename_symbiont_amd.models.encoder import HipEncoder, synthetic_batch
+    from codename_symbiont_amd.ops._ext import hip
+
+    cfg = get_config("minilm-l6")
+    enc = HipEncoder(cfg, seed=3)
+    b = synthetic_batch(cfg, 8, 40, seed=4, varlen=True).to("cuda")
+    ref, _ = enc.forward_packed(b)
+    was = hip().debug()
+    hip().set_debug(True)
+    try:
+        assert hip().debug()
+        out, _ = enc.forward_packed(b)
+    finally:
+        hip().set_debug(was)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
