@@ -84,6 +84,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
     const float* __restrict__ sw, int group_m, const uint8_t* __restrict__ ascale,
     uint8_t* __restrict__ cscale) {
   static_assert(!AMX || (F8 && NSTAGE == 2), "MX activations are an fp8 2-stage mode");
+  static_assert(NSTAGE >= 2 && NSTAGE <= 4, "LDS ring depth");
   static_assert(EPI != EPI_GELU_MX8 || (F8 && BN % 32 == 0), "MX output is an fp8 mode");
   constexpr int ES = F8 ? 1 : 2;               // bytes per element
   constexpr int KTILE = 128 / ES;              // elements per 128-byte k-tile row
@@ -208,23 +209,28 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
 
   constexpr int LOADS = (BM * 8) / NT + (BN * 8) / NT;  // glds per thread per stage
   stage(0, 0);
-  if (NSTAGE > 2 && KT > 1) stage(1, 1);
+#pragma unroll
+  for (int p = 1; p < NSTAGE - 1; ++p)
+    if (p < KT) stage(p, p);
   for (int kt = 0; kt < KT; ++kt) {
     if constexpr (NSTAGE == 2) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (kt + 1 < KT) stage(kt + 1, (kt + 1) & 1);
     } else {
-      // tile kt landed once only tile kt+1's loads remain; a raw barrier (no vmcnt(0) drain)
-      // keeps that next tile in flight across it, and it also retires every wave's reads of the
-      // buffer that stage(kt+2) refills (read in iteration kt-1)
-      if (kt + 1 < KT)
+      // tile kt landed once only the (up to NSTAGE-2) younger tiles' loads remain; a raw barrier
+      // (no vmcnt(0) drain) keeps those in flight across it, and it also retires every wave's
+      // reads of the buffer that stage(kt+NSTAGE-1) refills (read in iteration kt-1)
+      const int younger = min(NSTAGE - 2, KT - 1 - kt);
+      if (NSTAGE > 3 && younger >= 2)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * LOADS) : "memory");
+      else if (younger >= 1)
         asm volatile("s_waitcnt vmcnt(%0)" ::"i"(LOADS) : "memory");
       else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      if (kt + 2 < KT) stage(kt + 2, (kt + 2) % NSTAGE);
+      if (kt + NSTAGE - 1 < KT) stage(kt + NSTAGE - 1, (kt + NSTAGE - 1) % NSTAGE);
     }
     const char* sA = smem + (kt % NSTAGE) * STAGE_BYTES;
     const char* sB = sA + BM * 128;
@@ -406,7 +412,8 @@ static int g_resln_bm = 128;
 // 1 = 256x128 (8 waves, 3-stage ring with a tile in flight across each barrier),
 // 2 = 256x256 (8 waves of 128x64, 2-stage ring, one workgroup per CU) whenever N % 256 == 0,
 // 3 = auto: 256x256 when N % 256 == 0 and the grid fills whole waves of the 256 CUs (or is
-//     long enough that a partial last wave costs little), else 128x128.
+//     long enough that a partial last wave costs little), else 128x128;
+// 4 / 5 = 128x128 with a 3- / 4-deep ring at one workgroup per CU (A/B knobs).
 static int g_tile = 3;
 static bool use_big_tile(int tile, int M, int N) {
   if (N % 256 != 0 || (tile != 2 && tile != 3)) return false;
@@ -416,7 +423,7 @@ static bool use_big_tile(int tile, int M, int N) {
 }
 int symb_gemm_config(int resln_bm, int tile, int group_m) {
   if (resln_bm != 64 && resln_bm != 128) return -1;
-  if (tile < 0 || tile > 3) return -1;
+  if (tile < 0 || tile > 5) return -1;
   if (group_m < 0 || group_m > 64) return -1;
   g_resln_bm = resln_bm;
   g_tile = tile;
@@ -451,6 +458,20 @@ int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const flo
       case EPI_BIAS: return SYMB_G(EPI_BIAS);
       case EPI_GELU: return SYMB_G(EPI_GELU);
       case EPI_RES: return SYMB_G(EPI_RES);
+    }
+#undef SYMB_G
+    return -1;
+  }
+  if (g_tile == 4 || g_tile == 5) {
+    // 128x128, one workgroup per CU with a 3- or 4-deep ring (1-2 tiles in flight across each
+    // barrier) instead of two workgroups with 2-deep rings; A/B knob
+#define SYMB_G(E, NS) launch_cfg<128, 128, 2, 2, E, NS>(a, lda, w, ldw, bias, r, ldr, gamma, beta, \
+                                                       eps, c, ldc, M, N, K, st)
+    const bool four = g_tile == 5;
+    switch (epi) {
+      case EPI_BIAS: return four ? SYMB_G(EPI_BIAS, 4) : SYMB_G(EPI_BIAS, 3);
+      case EPI_GELU: return four ? SYMB_G(EPI_GELU, 4) : SYMB_G(EPI_GELU, 3);
+      case EPI_RES: return four ? SYMB_G(EPI_RES, 4) : SYMB_G(EPI_RES, 3);
     }
 #undef SYMB_G
     return -1;
