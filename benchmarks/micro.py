@@ -226,6 +226,10 @@ def cmd_gemm(a):
                                               K.gemm(x, w, b, epi, rr, g, be, 1e-12, out=y))
             var["hip_256x128_3st"] = lambda: (_hip().gemm_config(128, 1, 8),
                                               K.gemm(x, w, b, epi, rr, g, be, 1e-12, out=y))
+            var["hip_128x128_8w_32x64"] = lambda: (_hip().gemm_config(128, 6, 8),
+                                                   K.gemm(x, w, b, epi, rr, g, be, 1e-12, out=y))
+            var["hip_128x128_8w_64x32"] = lambda: (_hip().gemm_config(128, 7, 8),
+                                                   K.gemm(x, w, b, epi, rr, g, be, 1e-12, out=y))
             var["hip_128x128_3st"] = lambda: (_hip().gemm_config(128, 4, 8),
                                               K.gemm(x, w, b, epi, rr, g, be, 1e-12, out=y))
             var["hip_128x128_4st"] = lambda: (_hip().gemm_config(128, 5, 8),

@@ -412,8 +412,11 @@ static int g_resln_bm = 128;
 // 1 = 256x128 (8 waves, 3-stage ring with a tile in flight across each barrier),
 // 2 = 256x256 (8 waves of 128x64, 2-stage ring, one workgroup per CU) whenever N % 256 == 0,
 // 3 = auto: 256x256 when N % 256 == 0 and the grid fills whole waves of the 256 CUs (or is
-//     long enough that a partial last wave costs little), else 128x128;
-// 4 / 5 = 128x128 with a 3- / 4-deep ring at one workgroup per CU (A/B knobs).
+//     long enough that a partial last wave costs little), else 128x128 with 8 waves of 64x32
+//     (4 waves per SIMD at 2 workgroups per CU: +3-8 % over 4 waves of 64x64,
+//     profiles/r1_s4/gemm_8wave.json);
+// 4 / 5 = 128x128 with a 3- / 4-deep ring at one workgroup per CU (A/B knobs);
+// 6 / 7 = 128x128 with 8 waves of 32x64 / 64x32.
 static int g_tile = 3;
 static bool use_big_tile(int tile, int M, int N) {
   if (N % 256 != 0 || (tile != 2 && tile != 3)) return false;
@@ -423,7 +426,7 @@ static bool use_big_tile(int tile, int M, int N) {
 }
 int symb_gemm_config(int resln_bm, int tile, int group_m) {
   if (resln_bm != 64 && resln_bm != 128) return -1;
-  if (tile < 0 || tile > 5) return -1;
+  if (tile < 0 || tile > 7) return -1;
   if (group_m < 0 || group_m > 64) return -1;
   g_resln_bm = resln_bm;
   g_tile = tile;
@@ -458,6 +461,19 @@ int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const flo
       case EPI_BIAS: return SYMB_G(EPI_BIAS);
       case EPI_GELU: return SYMB_G(EPI_GELU);
       case EPI_RES: return SYMB_G(EPI_RES);
+    }
+#undef SYMB_G
+    return -1;
+  }
+  if (g_tile == 3 || g_tile == 6 || g_tile == 7) {
+    // 128x128 with 8 waves (32x64 or 64x32 wave tiles): 4 waves per SIMD at 2 workgroups per CU
+#define SYMB_G(E, WM_, WN_) launch_cfg<128, 128, WM_, WN_, E>(a, lda, w, ldw, bias, r, ldr, gamma, \
+                                                             beta, eps, c, ldc, M, N, K, st)
+    const bool tall = g_tile == 6;  // auto (3) takes the 64x32 wave tiles
+    switch (epi) {
+      case EPI_BIAS: return tall ? SYMB_G(EPI_BIAS, 4, 2) : SYMB_G(EPI_BIAS, 2, 4);
+      case EPI_GELU: return tall ? SYMB_G(EPI_GELU, 4, 2) : SYMB_G(EPI_GELU, 2, 4);
+      case EPI_RES: return tall ? SYMB_G(EPI_RES, 4, 2) : SYMB_G(EPI_RES, 2, 4);
     }
 #undef SYMB_G
     return -1;
