@@ -256,13 +256,18 @@ def cmd_encoder(a):
 
     encs = {p: HipEncoder(cfg, seed=0, precision=p) for p in a.precision.split(",")}
     tiles = [int(t) for t in a.tiles.split(",")]
+    fw = [int(t) for t in a.fp8_waves.split(",")]
     var = {}
     for p, e in encs.items():
         for t in tiles:
-            name = p if len(tiles) == 1 else f"{p}_tile{t}"
-            var[name] = (lambda e=e, t=t: (_hip().gemm_config(128, t, 8), e.forward_packed(b, o1, o2)))
+            for w in (fw if p == "fp8" else fw[:1]):
+                name = p + ("" if len(tiles) == 1 else f"_tile{t}") + ("" if len(fw) == 1 else f"_w{w}")
+                var[name] = (lambda e=e, t=t, w=w: (_hip().gemm_config(128, t, 8),
+                                                    _hip().gemm_fp8_config(w),
+                                                    e.forward_packed(b, o1, o2)))
     res = ab(var, rounds=a.rounds, iters=a.iters)
     _hip().gemm_config(128, 3, 8)
+    _hip().gemm_fp8_config(8)
     toks = a.batch * a.seq
     fl = cfg.flops_per_token(a.seq) * toks
     out = {p: dict(ms=round(m, 3), embeds_per_s=round(a.batch / (m / 1e3)),
@@ -334,7 +339,9 @@ def cmd_gemmfp8(a):
                   "fp8_with_quant": lambda: f8(True), "fp8_gemm_only": lambda: f8(False),
                   "fp8_gemm_only_rowmajor": lambda: (h.gemm_config(128, 0, 0), f8(False),
                                                      h.gemm_config(128, 3, 8)),
-                  "fp8_mx": lambda: fmx()},
+                  "fp8_mx": lambda: fmx(),
+                  "fp8_mx_4w": lambda: (h.gemm_fp8_config(4), fmx(), h.gemm_fp8_config(8)),
+                  "fp8_gemm_only_4w": lambda: (h.gemm_fp8_config(4), f8(False), h.gemm_fp8_config(8))},
                  rounds=a.rounds, iters=a.iters)
         fl = 2 * M * N * Kd
         out[name] = {k: dict(ms=round(m, 4), TFLOPs=round(fl / (m / 1e3) / 1e12)) for k, (m, _) in res.items()}
@@ -373,7 +380,8 @@ def main():
     ap.add_argument("--model", default="minilm-l6")
     ap.add_argument("--seed", type=int, default=1, help="scanabl: seed per-query thresholds")
     ap.add_argument("--precision", default="bf16", help="encoder: comma list of bf16,fp8")
-    ap.add_argument("--tiles", default="0", help="encoder: comma list of gemm_config tile modes")
+    ap.add_argument("--tiles", default="3", help="encoder: comma list of gemm_config tile modes")
+    ap.add_argument("--fp8-waves", default="8", help="encoder: comma list of fp8 GEMM wave counts")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=5)
     a = ap.parse_args()

@@ -378,6 +378,9 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
 
 // Rows of tiles per group in the grouped tile order (0/1: plain row-major); see symb_gemm_config.
 static int g_group_m = 8;
+// Waves of the 128x128 fp8 tile: 4 (64x64 wave tiles) or 8 (64x32, default: e5-large fp8
+// forward 18.2 -> 17.7 ms, profiles/r1_s4/fp8_waves/).
+static int g_fp8_waves = 8;
 
 template <int BM, int BN, int WM, int WN, int EPI, int NSTAGE = 2, bool F8 = false,
           bool AMX = false>
@@ -431,6 +434,12 @@ int symb_gemm_config(int resln_bm, int tile, int group_m) {
   g_resln_bm = resln_bm;
   g_tile = tile;
   g_group_m = group_m;
+  return 0;
+}
+
+int symb_gemm_fp8_config(int waves) {
+  if (waves != 4 && waves != 8) return -1;
+  g_fp8_waves = waves;
   return 0;
 }
 
@@ -531,9 +540,9 @@ int symb_gemm_fp8(int epi, const void* A8, int lda, const void* W8, int ldw, con
   auto c = (__bf16*)C;
   auto as = (const uint8_t*)ascale;
   auto cs = (uint8_t*)cscale;
-#define SYMB_G8(E, X) launch_cfg<128, 128, 2, 2, E, 2, true, X>(A8, lda, W8, ldw, bias, r, ldr,  \
-                                                                nullptr, nullptr, 0.f, c, ldc, M, \
-                                                                N, K, st, sa, sw, as, cs)
+#define SYMB_G8W(E, X, WN_) launch_cfg<128, 128, 2, WN_, E, 2, true, X>(                         \
+    A8, lda, W8, ldw, bias, r, ldr, nullptr, nullptr, 0.f, c, ldc, M, N, K, st, sa, sw, as, cs)
+#define SYMB_G8(E, X) (g_fp8_waves == 8 ? SYMB_G8W(E, X, 4) : SYMB_G8W(E, X, 2))
   if (as) {
     switch (epi) {
       case EPI_BIAS: return SYMB_G8(EPI_BIAS, true);
@@ -550,6 +559,7 @@ int symb_gemm_fp8(int epi, const void* A8, int lda, const void* W8, int ldw, con
     case EPI_GELU_MX8: return SYMB_G8(EPI_GELU_MX8, false);
   }
 #undef SYMB_G8
+#undef SYMB_G8W
   return -1;
 }
 
