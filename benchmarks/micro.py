@@ -218,6 +218,9 @@ def cmd_gemm(a):
                                              K.add_ln(tmp, None, g, be, 1e-12, out=y))
             var["hip_bm64"] = lambda: (_hip().gemm_config(64, 0), K.gemm(x, w, b, epi, rr, g, be, 1e-12, out=y))
             var["hip_bm128"] = lambda: (_hip().gemm_config(128, 3), K.gemm(x, w, b, epi, rr, g, be, 1e-12, out=y))
+            var["hip_bm128_8w"] = lambda: (_hip().gemm_config(128, 3), _hip().gemm_resln_config(8),
+                                           K.gemm(x, w, b, epi, rr, g, be, 1e-12, out=y),
+                                           _hip().gemm_resln_config(16))
         else:
             var["hip_128x128"] = lambda: (_hip().gemm_config(128, 0, 8), K.gemm(x, w, b, epi, rr, g, be, 1e-12, out=y))
             var["hip_128x128_rowmajor"] = lambda: (_hip().gemm_config(128, 0, 0),
@@ -230,6 +233,8 @@ def cmd_gemm(a):
                                                    K.gemm(x, w, b, epi, rr, g, be, 1e-12, out=y))
             var["hip_128x128_8w_64x32"] = lambda: (_hip().gemm_config(128, 7, 8),
                                                    K.gemm(x, w, b, epi, rr, g, be, 1e-12, out=y))
+            var["hip_128x128_16w"] = lambda: (_hip().gemm_config(128, 8, 8),
+                                              K.gemm(x, w, b, epi, rr, g, be, 1e-12, out=y))
             var["hip_128x128_3st"] = lambda: (_hip().gemm_config(128, 4, 8),
                                               K.gemm(x, w, b, epi, rr, g, be, 1e-12, out=y))
             var["hip_128x128_4st"] = lambda: (_hip().gemm_config(128, 5, 8),

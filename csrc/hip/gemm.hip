@@ -419,7 +419,7 @@ static int g_resln_bm = 128;
 //     (4 waves per SIMD at 2 workgroups per CU: +3-8 % over 4 waves of 64x64,
 //     profiles/r1_s4/gemm_8wave.json);
 // 4 / 5 = 128x128 with a 3- / 4-deep ring at one workgroup per CU (A/B knobs);
-// 6 / 7 = 128x128 with 8 waves of 32x64 / 64x32.
+// 6 / 7 = 128x128 with 8 waves of 32x64 / 64x32; 8 = 128x128 with 16 waves of 32x32.
 static int g_tile = 3;
 static bool use_big_tile(int tile, int M, int N) {
   if (N % 256 != 0 || (tile != 2 && tile != 3)) return false;
@@ -429,11 +429,21 @@ static bool use_big_tile(int tile, int M, int N) {
 }
 int symb_gemm_config(int resln_bm, int tile, int group_m) {
   if (resln_bm != 64 && resln_bm != 128) return -1;
-  if (tile < 0 || tile > 7) return -1;
+  if (tile < 0 || tile > 8) return -1;
   if (group_m < 0 || group_m > 64) return -1;
   g_resln_bm = resln_bm;
   g_tile = tile;
   g_group_m = group_m;
+  return 0;
+}
+
+// Waves of the row-complete 128x384 RES_LN tile: 8 (64x96 wave tiles) or 16 (32x96, default:
+// 4 waves per SIMD; MiniLM out-proj+LN 33.3 -> 27.7 us, FFN2+LN 56.3 -> 50.2 us,
+// profiles/r1_s4/resln_waves/).
+static int g_resln_waves = 16;
+int symb_gemm_resln_config(int waves) {
+  if (waves != 8 && waves != 16) return -1;
+  g_resln_waves = waves;
   return 0;
 }
 
@@ -454,6 +464,9 @@ int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const flo
   auto r = (const __bf16*)R;
   auto c = (__bf16*)C;
   if (epi == EPI_RES_LN) {
+    if (N == 384 && g_resln_bm == 128 && g_resln_waves == 16)
+      return launch_cfg<128, 384, 4, 4, EPI_RES_LN>(a, lda, w, ldw, bias, r, ldr, gamma, beta,
+                                                    eps, c, ldc, M, N, K, st);
     if (N == 384 && g_resln_bm == 128)
       return launch_cfg<128, 384, 2, 4, EPI_RES_LN>(a, lda, w, ldw, bias, r, ldr, gamma, beta,
                                                     eps, c, ldc, M, N, K, st);
@@ -465,6 +478,18 @@ int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const flo
   if (N % 128 != 0) return -1;
   if (use_big_tile(g_tile, M, N)) {
 #define SYMB_G(E) launch_cfg<256, 256, 2, 4, E>(a, lda, w, ldw, bias, r, ldr, gamma, beta, eps, c, \
+                                               ldc, M, N, K, st)
+    switch (epi) {
+      case EPI_BIAS: return SYMB_G(EPI_BIAS);
+      case EPI_GELU: return SYMB_G(EPI_GELU);
+      case EPI_RES: return SYMB_G(EPI_RES);
+    }
+#undef SYMB_G
+    return -1;
+  }
+  if (g_tile == 8) {
+    // 128x128 with 16 waves of 32x32 (A/B knob)
+#define SYMB_G(E) launch_cfg<128, 128, 4, 4, E>(a, lda, w, ldw, bias, r, ldr, gamma, beta, eps, c, \
                                                ldc, M, N, K, st)
     switch (epi) {
       case EPI_BIAS: return SYMB_G(EPI_BIAS);

@@ -67,7 +67,7 @@ def test_add_ln(H):
     _close(add_ln(x, None, g, b, 1e-5), R.add_ln_ref(x, None, g, b, 1e-5), 3e-2, 1e-2, "ln")
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 4, 5, 6, 7])
+@pytest.mark.parametrize("tile", [0, 1, 2, 4, 5, 6, 7, 8, 16])
 @pytest.mark.parametrize("M,N,K,epi", [
     (300, 1152, 384, 0), (129, 1536, 384, 1), (517, 384, 384, 2), (517, 384, 384, 3),
     (300, 384, 1536, 3), (64, 768, 768, 2), (1000, 2304, 768, 0), (77, 1024, 4096, 2),
@@ -86,7 +86,11 @@ def test_gemm(M, N, K, epi, tile):
     # tile=2: 256x256 wherever N % 256 == 0 (others fall back to 128x128), row-major order;
     # the default (3, auto) is covered by the encoder tests
     # tile=4/5: 128x128 with 3-/4-deep rings at one workgroup per CU
-    hip().gemm_config(64 if tile == 1 else 128, tile, {0: 8, 1: 3, 2: 0, 4: 8, 5: 5, 6: 8, 7: 2}[tile])
+    # tile=16: default tiles with the 8-wave (64x96 wave tiles) row-complete RES_LN tile
+    # (others: the default 16-wave one); tile=8: 16 waves of 32x32
+    hip().gemm_config(64 if tile == 1 else 128, 3 if tile == 16 else tile,
+                      {0: 8, 1: 3, 2: 0, 4: 8, 5: 5, 6: 8, 7: 2, 8: 8, 16: 8}[tile])
+    hip().gemm_resln_config(8 if tile == 16 else 16)
 
     a = _bf(M, K, seed=1)
     w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=2)
@@ -98,6 +102,7 @@ def test_gemm(M, N, K, epi, tile):
         out = gemm(a, w, bias, epi, res, g, b, 1e-12)
     finally:
         hip().gemm_config(128, 3, 8)
+        hip().gemm_resln_config(16)
     ref = R.gemm_ref(a, w, bias, epi, res, g, b, 1e-12)
     _close(out, ref, atol=4e-2, rtol=2e-2, what=f"gemm epi={epi}")
 
