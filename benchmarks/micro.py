@@ -346,7 +346,9 @@ def cmd_gemmfp8(a):
                                                      h.gemm_config(128, 3, 8)),
                   "fp8_mx": lambda: fmx(),
                   "fp8_mx_4w": lambda: (h.gemm_fp8_config(4), fmx(), h.gemm_fp8_config(8)),
-                  "fp8_gemm_only_4w": lambda: (h.gemm_fp8_config(4), f8(False), h.gemm_fp8_config(8))},
+                  "fp8_gemm_only_4w": lambda: (h.gemm_fp8_config(4), f8(False), h.gemm_fp8_config(8)),
+                  "fp8_mx_16w": lambda: (h.gemm_fp8_config(16), fmx(), h.gemm_fp8_config(8)),
+                  "fp8_gemm_only_16w": lambda: (h.gemm_fp8_config(16), f8(False), h.gemm_fp8_config(8))},
                  rounds=a.rounds, iters=a.iters)
         fl = 2 * M * N * Kd
         out[name] = {k: dict(ms=round(m, 4), TFLOPs=round(fl / (m / 1e3) / 1e12)) for k, (m, _) in res.items()}

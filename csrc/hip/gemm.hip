@@ -448,7 +448,7 @@ int symb_gemm_resln_config(int waves) {
 }
 
 int symb_gemm_fp8_config(int waves) {
-  if (waves != 4 && waves != 8) return -1;
+  if (waves != 4 && waves != 8 && waves != 16) return -1;
   g_fp8_waves = waves;
   return 0;
 }
@@ -565,9 +565,11 @@ int symb_gemm_fp8(int epi, const void* A8, int lda, const void* W8, int ldw, con
   auto c = (__bf16*)C;
   auto as = (const uint8_t*)ascale;
   auto cs = (uint8_t*)cscale;
-#define SYMB_G8W(E, X, WN_) launch_cfg<128, 128, 2, WN_, E, 2, true, X>(                         \
+#define SYMB_G8W(E, X, WM_, WN_) launch_cfg<128, 128, WM_, WN_, E, 2, true, X>(                   \
     A8, lda, W8, ldw, bias, r, ldr, nullptr, nullptr, 0.f, c, ldc, M, N, K, st, sa, sw, as, cs)
-#define SYMB_G8(E, X) (g_fp8_waves == 8 ? SYMB_G8W(E, X, 4) : SYMB_G8W(E, X, 2))
+#define SYMB_G8(E, X)                                                                 \
+  (g_fp8_waves == 16 ? SYMB_G8W(E, X, 4, 4)                                           \
+                     : g_fp8_waves == 8 ? SYMB_G8W(E, X, 2, 4) : SYMB_G8W(E, X, 2, 2))
   if (as) {
     switch (epi) {
       case EPI_BIAS: return SYMB_G8(EPI_BIAS, true);

@@ -385,7 +385,7 @@ def _mx_decode(q8, ex, block=32):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("waves", [4, 8])
+@pytest.mark.parametrize("waves", [4, 8, 16])
 @pytest.mark.parametrize("M,N,K", [(300, 1536, 384), (1000, 4096, 1024), (77, 3072, 768)])
 def test_gemm_fp8_mx_gelu_output(M, N, K, waves):
     """EPI_GELU_MX8: the FFN1 epilogue's MX fp8 output (e4m3 + E8M0 per 32 columns) decodes to
@@ -427,7 +427,7 @@ def test_gemm_fp8_mx_gelu_output(M, N, K, waves):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("waves", [4, 8])
+@pytest.mark.parametrize("waves", [4, 8, 16])
 @pytest.mark.parametrize("M,N,K,epi", [(300, 384, 1536, 2), (1000, 1024, 4096, 2),
                                        (129, 768, 3072, 0), (517, 1536, 384, 1)])
 def test_gemm_fp8_mx_input(M, N, K, epi, waves):
