@@ -414,16 +414,19 @@ static int g_resln_bm = 128;
 // Tile of the bias / GELU / residual GEMMs: 0 = 128x128 (4 waves, 2-stage ring),
 // 1 = 256x128 (8 waves, 3-stage ring with a tile in flight across each barrier),
 // 2 = 256x256 (8 waves of 128x64, 2-stage ring, one workgroup per CU) whenever N % 256 == 0,
-// 3 = auto: 256x256 when N % 256 == 0 and the grid fills whole waves of the 256 CUs (or is
-//     long enough that a partial last wave costs little), else 128x128 with 8 waves of 64x32
+// 3 = auto: 256x256 when N % 256 == 0, K >= 768 and the grid fills whole waves of the 256 CUs
+//     (or is long enough that a partial last wave costs little), else 128x128 with 8 waves of 64x32
 //     (4 waves per SIMD at 2 workgroups per CU: +3-8 % over 4 waves of 64x64,
 //     profiles/r1_s4/gemm_8wave.json);
 // 4 / 5 = 128x128 with a 3- / 4-deep ring at one workgroup per CU (A/B knobs);
 // 6 / 7 = 128x128 with 8 waves of 32x64 / 64x32; 8 = 128x128 with 16 waves of 32x32.
 static int g_tile = 3;
-static bool use_big_tile(int tile, int M, int N) {
+static bool use_big_tile(int tile, int M, int N, int K) {
   if (N % 256 != 0 || (tile != 2 && tile != 3)) return false;
   if (tile == 2) return true;
+  // short K (MiniLM's 384): the 256x256 tile's fill and epilogue outweigh its operand reuse
+  // (FFN1 32768x1536x384: 546 vs 585 TFLOP/s for the 8-wave 128x128 tile)
+  if (K < 768) return false;
   const int tiles = ((M + 255) / 256) * (N / 256);
   return tiles % 256 == 0 || tiles >= 4 * 256;
 }
@@ -476,7 +479,7 @@ int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const flo
     return -1;  // wider rows: EPI_RES + symb_add_ln
   }
   if (N % 128 != 0) return -1;
-  if (use_big_tile(g_tile, M, N)) {
+  if (use_big_tile(g_tile, M, N, K)) {
 #define SYMB_G(E) launch_cfg<256, 256, 2, 4, E>(a, lda, w, ldw, bias, r, ldr, gamma, beta, eps, c, \
                                                ldc, M, N, K, st)
     switch (epi) {
