@@ -267,8 +267,11 @@ def cmd_encoder(a):
         for t in tiles:
             for w in (fw if p == "fp8" else fw[:1]):
                 name = p + ("" if len(tiles) == 1 else f"_tile{t}") + ("" if len(fw) == 1 else f"_w{w}")
+                # w = 256 / 257: 8-wave fp8 tiles plus the 256x256 fp8 tile wherever the bf16
+                # rule takes it / where the fp8 auto rule does (the default); else no 256x256
                 var[name] = (lambda e=e, t=t, w=w: (_hip().gemm_config(128, t, 8),
-                                                    _hip().gemm_fp8_config(w),
+                                                    _hip().gemm_fp8_config(8 if w >= 256 else w,
+                                                                           {256: 1, 257: 2}.get(w, 0)),
                                                     e.forward_packed(b, o1, o2)))
     res = ab(var, rounds=a.rounds, iters=a.iters)
     _hip().gemm_config(128, 3, 8)
@@ -345,10 +348,11 @@ def cmd_gemmfp8(a):
                   "fp8_gemm_only_rowmajor": lambda: (h.gemm_config(128, 0, 0), f8(False),
                                                      h.gemm_config(128, 3, 8)),
                   "fp8_mx": lambda: fmx(),
-                  "fp8_mx_4w": lambda: (h.gemm_fp8_config(4), fmx(), h.gemm_fp8_config(8)),
-                  "fp8_gemm_only_4w": lambda: (h.gemm_fp8_config(4), f8(False), h.gemm_fp8_config(8)),
-                  "fp8_mx_16w": lambda: (h.gemm_fp8_config(16), fmx(), h.gemm_fp8_config(8)),
-                  "fp8_gemm_only_16w": lambda: (h.gemm_fp8_config(16), f8(False), h.gemm_fp8_config(8))},
+                  "fp8_mx_4w": lambda: (h.gemm_fp8_config(4, 0), fmx(), h.gemm_fp8_config(8)),
+                  "fp8_gemm_only_4w": lambda: (h.gemm_fp8_config(4, 0), f8(False), h.gemm_fp8_config(8)),
+                  "fp8_mx_128": lambda: (h.gemm_fp8_config(8, 0), fmx(), h.gemm_fp8_config(8)),
+                  "fp8_mx_256": lambda: (h.gemm_fp8_config(8, 1), fmx(), h.gemm_fp8_config(8)),
+                  "fp8_gemm_only_256": lambda: (h.gemm_fp8_config(8, 1), f8(False), h.gemm_fp8_config(8))},
                  rounds=a.rounds, iters=a.iters)
         fl = 2 * M * N * Kd
         out[name] = {k: dict(ms=round(m, 4), TFLOPs=round(fl / (m / 1e3) / 1e12)) for k, (m, _) in res.items()}

@@ -44,7 +44,7 @@ int symb_index_scan_ablate(const void* X, int n_valid, int rows_per_blk, int n_r
                            const void* Q, int NQ, float* cs, int* ci, hipStream_t st, int abl,
                            const float* thr);
 int symb_gemm_config(int resln_bm, int tile, int group_m);
-int symb_gemm_fp8_config(int waves);
+int symb_gemm_fp8_config(int waves, int big);
 int symb_gemm_resln_config(int waves);
 int symb_gemm_fp8(int epi, const void* A8, int lda, const void* W8, int ldw, const float* sa,
                   const float* sw, const float* bias, const void* R, int ldr, void* C, int ldc,
@@ -324,8 +324,9 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("resln_bm") = 128, py::arg("tile") = 3, py::arg("group_m") = 8);
   m.def("gemm_resln_config", [](int waves) { check(symb_gemm_resln_config(waves), "gemm_resln_config"); },
         py::arg("waves") = 16);
-  m.def("gemm_fp8_config", [](int waves) { check(symb_gemm_fp8_config(waves), "gemm_fp8_config"); },
-        py::arg("waves") = 8);
+  m.def("gemm_fp8_config", [](int waves, int big) {
+    check(symb_gemm_fp8_config(waves, big), "gemm_fp8_config");
+  }, py::arg("waves") = 8, py::arg("big") = 2);
   m.def("gemm_fp8", [](int epi, uptr A8, int lda, uptr W8, int ldw, uptr sa, uptr sw, uptr bias,
                        uptr R, int ldr, uptr C, int ldc, int M, int N, int K, uptr st,
                        uptr ascale, uptr cscale) {

@@ -450,9 +450,13 @@ int symb_gemm_resln_config(int waves) {
   return 0;
 }
 
-int symb_gemm_fp8_config(int waves) {
+// fp8 256x256 tiles (8 waves of 128x64): 0 off, 1 under the bf16 auto rule, 2 auto (default).
+static int g_fp8_big = 2;
+int symb_gemm_fp8_config(int waves, int big) {
   if (waves != 4 && waves != 8 && waves != 16) return -1;
   g_fp8_waves = waves;
+  if (big < 0 || big > 2) return -1;
+  g_fp8_big = big;
   return 0;
 }
 
@@ -568,11 +572,18 @@ int symb_gemm_fp8(int epi, const void* A8, int lda, const void* W8, int ldw, con
   auto c = (__bf16*)C;
   auto as = (const uint8_t*)ascale;
   auto cs = (uint8_t*)cscale;
-#define SYMB_G8W(E, X, WM_, WN_) launch_cfg<128, 128, WM_, WN_, E, 2, true, X>(                   \
+  // 256x256: g_fp8_big 1 = wherever the bf16 auto rule takes it; 2 (default) = only where it
+  // measured faster -- long-K or wide-N projections (e5 QKV 1337 -> 1458, FFN2 MX-in 1687 -> 1867
+  // TFLOP/s), not the square out-projection or the MX-emitting FFN1 (both slower),
+  // profiles/r1_s4/fp8_waves/gemmfp8_256.json
+  const bool big = g_fp8_big != 0 && use_big_tile(3, M, N, K) &&
+                   (g_fp8_big == 1 || (K >= 1024 && N != K && epi != EPI_GELU_MX8));
+#define SYMB_G8W(E, X, BMN, WM_, WN_) launch_cfg<BMN, BMN, WM_, WN_, E, 2, true, X>(              \
     A8, lda, W8, ldw, bias, r, ldr, nullptr, nullptr, 0.f, c, ldc, M, N, K, st, sa, sw, as, cs)
-#define SYMB_G8(E, X)                                                                 \
-  (g_fp8_waves == 16 ? SYMB_G8W(E, X, 4, 4)                                           \
-                     : g_fp8_waves == 8 ? SYMB_G8W(E, X, 2, 4) : SYMB_G8W(E, X, 2, 2))
+#define SYMB_G8(E, X)                                                                      \
+  (big ? SYMB_G8W(E, X, 256, 2, 4)                                                         \
+       : g_fp8_waves == 16 ? SYMB_G8W(E, X, 128, 4, 4)                                     \
+                           : g_fp8_waves == 8 ? SYMB_G8W(E, X, 128, 2, 4) : SYMB_G8W(E, X, 128, 2, 2))
   if (as) {
     switch (epi) {
       case EPI_BIAS: return SYMB_G8(EPI_BIAS, true);

@@ -385,8 +385,9 @@ def _mx_decode(q8, ex, block=32):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("waves", [4, 8, 16])
-@pytest.mark.parametrize("M,N,K", [(300, 1536, 384), (1000, 4096, 1024), (77, 3072, 768)])
+@pytest.mark.parametrize("waves", [4, 8, 16, 256])
+@pytest.mark.parametrize("M,N,K", [(300, 1536, 384), (1000, 4096, 1024), (77, 3072, 768),
+                                   (16300, 4096, 1024)])   # >= 1024 256x256 tiles, ragged M
 def test_gemm_fp8_mx_gelu_output(M, N, K, waves):
     """EPI_GELU_MX8: the FFN1 epilogue's MX fp8 output (e4m3 + E8M0 per 32 columns) decodes to
     GELU(A8 W8^T * sa * sw + bias) within e4m3 rounding, and its exponents follow the MX rule."""
@@ -403,13 +404,13 @@ def test_gemm_fp8_mx_gelu_output(M, N, K, waves):
     w8, sw = quant_weight_fp8(w)
     out8 = torch.empty(M, N, dtype=torch.uint8, device=DEV)
     oexp = torch.empty(M, N // 32, dtype=torch.uint8, device=DEV)
-    hip().gemm_fp8_config(waves)
+    hip().gemm_fp8_config(8 if waves == 256 else waves, 1 if waves == 256 else 0)  # 256: 256x256
     try:
         hip().gemm_fp8(4, a8.data_ptr(), K, w8.data_ptr(), K, sa.data_ptr(), sw.data_ptr(),
                        bias.data_ptr(), 0, 0, out8.data_ptr(), N, M, N, K, st,
                        cscale=oexp.data_ptr())
     finally:
-        hip().gemm_fp8_config(8)
+        hip().gemm_fp8_config(8, 2)
     torch.cuda.synchronize()
     ad = a8.view(torch.float8_e4m3fn).float() * sa[:, None]
     wd = w8.view(torch.float8_e4m3fn).float() * sw[:, None]
@@ -427,9 +428,10 @@ def test_gemm_fp8_mx_gelu_output(M, N, K, waves):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("waves", [4, 8, 16])
+@pytest.mark.parametrize("waves", [4, 8, 16, 256])
 @pytest.mark.parametrize("M,N,K,epi", [(300, 384, 1536, 2), (1000, 1024, 4096, 2),
-                                       (129, 768, 3072, 0), (517, 1536, 384, 1)])
+                                       (129, 768, 3072, 0), (517, 1536, 384, 1),
+                                       (16384, 1024, 4096, 2)])   # 256 tiles of 256x256
 def test_gemm_fp8_mx_input(M, N, K, epi, waves):
     """Block-scaled A (MX: E8M0 per 32 k fed to the MFMA's scale operand) == fp32 product of the
     decoded operands."""
@@ -446,13 +448,13 @@ def test_gemm_fp8_mx_input(M, N, K, epi, waves):
     w8, sw = quant_weight_fp8(w)
     out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
     st = stream_handle()
-    hip().gemm_fp8_config(waves)
+    hip().gemm_fp8_config(8 if waves == 256 else waves, 1 if waves == 256 else 0)  # 256: 256x256
     try:
         hip().gemm_fp8(epi, a8.data_ptr(), K, w8.data_ptr(), K, 0, sw.data_ptr(), bias.data_ptr(),
                        0 if res is None else res.data_ptr(), N, out.data_ptr(), N, M, N, K, st,
                        ascale=aexp.data_ptr())
     finally:
-        hip().gemm_fp8_config(8)
+        hip().gemm_fp8_config(8, 2)
     torch.cuda.synchronize()
     ad = _mx_decode(a8, ex)
     wd = w8.view(torch.float8_e4m3fn).float() * sw[:, None]
