@@ -286,6 +286,7 @@ def cmd_encoder(a):
 
 def cmd_latency(a):
     """Small-batch (query path) encoder latency: eager launches vs the captured hipGraph."""
+    from codename_symbiont_amd.ops._ext import hip
     from codename_symbiont_amd.models import get_config
     from codename_symbiont_amd.models.encoder import HipEncoder, synthetic_batch
 
@@ -294,7 +295,9 @@ def cmd_latency(a):
     out = {}
     for B, S in ((1, 16), (1, 64), (8, 32), (32, 48)):
         b = synthetic_batch(cfg, B, S, seed=1).to("cuda")
-        r = ab({"eager": lambda: enc.forward_packed(b), "graph": lambda: enc.forward_graphed(b)},
+        r = ab({"eager": lambda: enc.forward_packed(b), "graph": lambda: enc.forward_graphed(b),
+                "eager_no_small_m_ring": lambda: (hip().gemm_config(128, 7, 8), enc.forward_packed(b),
+                                                  hip().gemm_config(128, 3, 8))},
                rounds=a.rounds, iters=50)
         out[f"B{B}xS{S}"] = {k: round(m * 1e3, 1) for k, (m, _) in r.items()}
     print(json.dumps({"bench": "encoder_latency_us", "model": a.model, "results": out}))

@@ -417,7 +417,7 @@ static int g_resln_bm = 128;
 // 3 = auto: 256x256 when N % 256 == 0, K >= 768 and the grid fills whole waves of the 256 CUs
 //     (or is long enough that a partial last wave costs little), else 128x128 with 8 waves of 64x32
 //     (4 waves per SIMD at 2 workgroups per CU: +3-8 % over 4 waves of 64x64,
-//     profiles/r1_s4/gemm_8wave.json);
+//     profiles/r1_s4/gemm_8wave.json); grids smaller than the 256 CUs take a 4-deep ring;
 // 4 / 5 = 128x128 with a 3- / 4-deep ring at one workgroup per CU (A/B knobs);
 // 6 / 7 = 128x128 with 8 waves of 32x64 / 64x32; 8 = 128x128 with 16 waves of 32x32.
 static int g_tile = 3;
@@ -498,6 +498,19 @@ int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const flo
     // 128x128 with 16 waves of 32x32 (A/B knob)
 #define SYMB_G(E) launch_cfg<128, 128, 4, 4, E>(a, lda, w, ldw, bias, r, ldr, gamma, beta, eps, c, \
                                                ldc, M, N, K, st)
+    switch (epi) {
+      case EPI_BIAS: return SYMB_G(EPI_BIAS);
+      case EPI_GELU: return SYMB_G(EPI_GELU);
+      case EPI_RES: return SYMB_G(EPI_RES);
+    }
+#undef SYMB_G
+    return -1;
+  }
+  if (g_tile == 3 && ((M + 127) / 128) * (N / 128) < 256) {
+    // small M (query-path batches): fewer tiles than CUs, so occupancy is moot and each tile's
+    // serial k-loop is the latency -- a 4-deep ring keeps 3 k-tiles' loads in flight
+#define SYMB_G(E) launch_cfg<128, 128, 2, 4, E, 4>(a, lda, w, ldw, bias, r, ldr, gamma, beta, eps, \
+                                                  c, ldc, M, N, K, st)
     switch (epi) {
       case EPI_BIAS: return SYMB_G(EPI_BIAS);
       case EPI_GELU: return SYMB_G(EPI_GELU);
