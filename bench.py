@@ -223,6 +223,7 @@ def main() -> None:
     t_start = time.perf_counter()
     for j in range(K):
         step(W + j, evs[j])
+    host_ms = (time.perf_counter() - t_start) * 1000.0 / K   # host enqueue time per step
     torch.cuda.synchronize(dev)
     D.barrier(info)
     torch.cuda.synchronize(dev)
@@ -272,6 +273,7 @@ def main() -> None:
             "topk_qps": round(total, 2) if args.mode != "embed" else 0.0,
             "embed_ms_per_step_rank0": round(e_ms, 3),
             "search_ms_per_step_rank0": round(s_ms, 3),
+            "host_enqueue_ms_per_step_rank0": round(host_ms, 3),
             "vs_derived_reference_estimate": (round(total / DERIVED_REF_EMBEDS_PER_SEC, 1)
                                               if args.mode != "search" else None),
         }
