@@ -69,6 +69,9 @@ def main() -> None:
     ap.add_argument("--no-overlap", action="store_true",
                     help="--mode full: run encode and search back to back on one stream instead of "
                          "encoding batch i+1 on a second stream while batch i is searched")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="launch the encoder's kernels eagerly every step instead of replaying a "
+                         "captured hipGraph of the forward")
     args = ap.parse_args()
 
     from codename_symbiont_amd.index.shard import HbmIndexShard
@@ -146,6 +149,37 @@ def main() -> None:
             d.max_len = h.max_len
             copy_done[slot].record(copy_stream)
 
+    # The encoder forward is ~40 kernel launches; on a busy host their enqueue time (0.9-1.2 ms
+    # per step measured) approaches the GPU time (1.5 ms), so each (input slot, output buffers)
+    # pair is captured once into a hipGraph and replayed: one launch per forward.  Graphs bake
+    # pointers and shapes; every bench batch has the same shape and lives in dbuf[slot].
+    from codename_symbiont_amd.utils.gpu_debug import debug_enabled
+
+    # (SYMB_GPU_DEBUG syncs after every launch, which a stream capture forbids: eager there)
+    use_graph = (not args.no_graph and not group_dp and args.mode != "search"
+                 and not debug_enabled())
+    graphs = {}
+
+    def run_encoder(slot: int, o32: torch.Tensor, ou: torch.Tensor) -> None:
+        g = graphs.get((slot, o32.data_ptr())) if use_graph else None
+        if g is None:
+            enc.forward_packed(dbuf[slot], o32, ou)
+        else:
+            g.replay()
+
+    def capture_encoder(slot: int, o32: torch.Tensor, ou: torch.Tensor) -> None:
+        enc.forward_packed(dbuf[slot], o32, ou)   # first call: kernel attributes, workspace
+        torch.cuda.synchronize(dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            enc.forward_packed(dbuf[slot], o32, ou)
+        torch.cuda.synchronize(dev)
+        graphs[(slot, o32.data_ptr())] = g
+
+    if use_graph:   # before any pipelined work is in flight
+        for slot in range(2):
+            capture_encoder(slot, *(outs[slot] if overlap else (out_f32, out_unit)))
+
     def encode_async(i: int, ev=None) -> None:
         """Encode batch i on enc_stream into outs[i % 2] (overlap mode)."""
         slot = i % 2
@@ -157,7 +191,7 @@ def main() -> None:
                 ev[0].record(enc_stream)
             in_ring.consume(slot)
             out_ring.fill(slot)
-            enc.forward_packed(dbuf[slot], *outs[slot])
+            run_encoder(slot, *outs[slot])
             if ev:
                 ev[1].record(enc_stream)
             consumed[slot].record(enc_stream)
@@ -196,7 +230,7 @@ def main() -> None:
             q = None
         elif args.mode != "search":
             compute.wait_event(copy_done[slot])
-            enc.forward_packed(dbuf[slot], out_f32, out_unit)
+            run_encoder(slot, out_f32, out_unit)
             consumed[slot].record(compute)
             prefetch(i + 1)
             shard.append_unit(out_unit)
@@ -268,6 +302,7 @@ def main() -> None:
                 "index_rows": args.index_rows, "dim": cfg.hidden, "top_k": args.k,
                 "mode": args.mode,
                 "encode_search_overlap": overlap,
+                "encoder_hipgraph": use_graph,
             },
             "embeds_per_sec": round(total, 2) if args.mode != "search" else 0.0,
             "topk_qps": round(total, 2) if args.mode != "embed" else 0.0,
