@@ -155,8 +155,10 @@ def main() -> None:
     # pointers and shapes; every bench batch has the same shape and lives in dbuf[slot].
     from codename_symbiont_amd.utils.gpu_debug import debug_enabled
 
-    # (SYMB_GPU_DEBUG syncs after every launch, which a stream capture forbids: eager there)
-    use_graph = (not args.no_graph and not group_dp and args.mode != "search"
+    # (SYMB_GPU_DEBUG syncs after every launch, which a stream capture forbids: eager there).
+    # Only the embed-only step is launch-bound; the headline step is bound by the scan (same
+    # 13.2k with or without the graph), so it keeps eager launches.
+    use_graph = (not args.no_graph and not group_dp and args.mode == "embed"
                  and not debug_enabled())
     graphs = {}
 
@@ -171,7 +173,8 @@ def main() -> None:
         enc.forward_packed(dbuf[slot], o32, ou)   # first call: kernel attributes, workspace
         torch.cuda.synchronize(dev)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # thread_local: other threads' HIP calls (e.g. a process group's watchdog) stay legal
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             enc.forward_packed(dbuf[slot], o32, ou)
         torch.cuda.synchronize(dev)
         graphs[(slot, o32.data_ptr())] = g

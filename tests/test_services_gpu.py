@@ -77,8 +77,8 @@ def test_ingest_and_search_on_gpu():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("extra,debug", [([], False), (["--no-overlap"], False), ([], True),
-                                         (["--no-graph"], False),
-                                         (["--mode", "embed"], False)])
+                                         (["--mode", "embed"], False),
+                                         (["--mode", "embed", "--no-graph"], False)])
 def test_bench_contract_small_index(extra, debug):
     """bench.py's driver contract (one JSON line, whole-job value, step timing) on a small index,
     with and without the encode/search stream overlap."""
@@ -101,7 +101,8 @@ def test_bench_contract_small_index(extra, debug):
     assert abs(r["value"] - 256 * 1000.0 / r["ms_per_step"]) / r["value"] < 0.01
     assert r["config"]["encode_search_overlap"] is ("--no-overlap" not in extra
                                                     and "--mode" not in extra)
-    assert r["config"]["encoder_hipgraph"] is ("--no-graph" not in extra and not debug)
+    assert r["config"]["encoder_hipgraph"] is ("--mode" in extra and "--no-graph" not in extra
+                                               and not debug)
 
 
 @pytest.mark.gpu
