@@ -3,11 +3,16 @@
 The reference persists through Qdrant (on-disk vectors + payload, vector_memory_service/src/main.rs
 :39,52; docker volume ./data/qdrant_storage).  The HBM index is volatile, so each shard keeps:
 
-  <dir>/snapshot/meta.json        {"dim", "count", "format": 1}
-  <dir>/snapshot/vectors.npy      count x dim bf16 bit patterns (uint16 .npy, memory-mappable),
-                                  or e4m3 bytes (uint8) for an fp8 shard (meta "dtype")
-  <dir>/snapshot/payloads.jsonl   one [point_id, doc_id, url, text, order, model, ts] per row
-  <dir>/wal.log                   records appended (and fsync'd) per upsert batch
+  <dir>/CURRENT                        commit pointer: "snapshot.<gen>" (atomic replace + fsync)
+  <dir>/snapshot.<gen>/meta.json       {"dim", "count", "format": 1}
+  <dir>/snapshot.<gen>/vectors.npy     count x dim bf16 bit patterns (uint16 .npy, memory-
+                                       mappable), or e4m3 bytes (uint8) for an fp8 shard
+  <dir>/snapshot.<gen>/payloads.jsonl  one [point_id, doc_id, url, text, order, model, ts] per row
+  <dir>/wal.log                        records appended (and fsync'd) per upsert batch
+
+A snapshot is written to a fresh generation directory (files + directory fsync'd), committed by
+replacing CURRENT, and only then are older generations deleted and the WAL truncated -- a crash
+at any step boots from the previous committed generation + the untruncated WAL.
 
 WAL record: magic u32 | n u32 | body_len u32 | crc32(body) u32 | body, body = n x
 (u16 id_len, id, u32 payload_len, payload JSON, f32[dim]).  A torn tail record (crash mid-write)
@@ -112,10 +117,80 @@ class Wal:
             yield ids, pls, np.stack(vs) if vs else np.zeros((0, dim), np.float32)
 
 
-def save_snapshot(shard: HbmIndexShard, directory: str, chunk: int = 1 << 20) -> None:
-    snap = os.path.join(directory, "snapshot")
-    tmp = snap + ".tmp"
-    os.makedirs(tmp, exist_ok=True)
+CURRENT = "CURRENT"        # commit pointer: names the live snapshot.<gen> directory
+_SNAP_PREFIX = "snapshot."
+
+
+def fsync_dir(path: str) -> None:
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        os.fsync(fd)
+    finally:
+        os.close(fd)
+
+
+def fsync_file(path: str) -> None:
+    with open(path, "rb+") as f:
+        os.fsync(f.fileno())
+
+
+def write_atomic(path: str, data: bytes) -> None:
+    """tmp + fsync + rename + fsync(dir): after return ``path`` holds ``data`` durably, and a
+    crash at any point leaves either the old or the new content."""
+    tmp = path + ".tmp"
+    with open(tmp, "wb") as f:
+        f.write(data)
+        f.flush()
+        os.fsync(f.fileno())
+    os.replace(tmp, path)
+    fsync_dir(os.path.dirname(path) or ".")
+
+
+def _rmtree(path: str) -> None:
+    if not os.path.isdir(path):
+        return
+    for fn in os.listdir(path):
+        os.remove(os.path.join(path, fn))
+    os.rmdir(path)
+
+
+def _snap_gen(name: str) -> int:
+    tail = name[len(_SNAP_PREFIX):]
+    return int(tail) if name.startswith(_SNAP_PREFIX) and tail.isdigit() else -1
+
+
+def committed_snapshot(directory: str) -> str | None:
+    """Path of the committed snapshot directory, or None.  ``CURRENT`` names it; directories
+    written by the pre-pointer format (``snapshot/``, or ``snapshot.old`` left by a crash in its
+    two-rename swap) are still honoured when no pointer exists."""
+    cur = os.path.join(directory, CURRENT)
+    if os.path.exists(cur):
+        with open(cur, encoding="utf-8") as f:
+            name = f.read().strip()
+        p = os.path.join(directory, name)
+        if os.path.exists(os.path.join(p, "meta.json")):
+            return p
+        raise RuntimeError(f"snapshot pointer {cur} names {name!r}, which is incomplete")
+    for legacy in ("snapshot", "snapshot.old"):
+        p = os.path.join(directory, legacy)
+        if os.path.exists(os.path.join(p, "meta.json")):
+            return p
+    return None
+
+
+def save_snapshot(shard: HbmIndexShard, directory: str, chunk: int = 1 << 20,
+                  _crash_before_commit: bool = False) -> None:
+    """Write ``snapshot.<gen>/`` (every file fsync'd, then the directory), then commit it by
+    atomically replacing ``CURRENT``; only then are older generations removed.  A crash anywhere
+    leaves the previous committed snapshot (and the WAL, truncated by the caller only after
+    this returns) intact.  ``_crash_before_commit`` stops right before the pointer swap (tests)."""
+    os.makedirs(directory, exist_ok=True)
+    names = os.listdir(directory)
+    gen = max([_snap_gen(n) for n in names] + [0]) + 1
+    final = os.path.join(directory, f"{_SNAP_PREFIX}{gen}")
+    tmp = final + ".tmp"
+    _rmtree(tmp)
+    os.makedirs(tmp)
     n, D = shard.count, shard.dim
     fp8 = getattr(shard, "dtype", "bf16") == "fp8"
     mm = np.lib.format.open_memmap(os.path.join(tmp, "vectors.npy"), mode="w+",
@@ -129,6 +204,7 @@ def save_snapshot(shard: HbmIndexShard, directory: str, chunk: int = 1 << 20) ->
     if mm is not None:
         mm.flush()
         del mm
+        fsync_file(os.path.join(tmp, "vectors.npy"))
     with open(os.path.join(tmp, "payloads.jsonl"), "w", encoding="utf-8") as f:
         ps = shard.payloads
         for r in range(n):
@@ -136,24 +212,32 @@ def save_snapshot(shard: HbmIndexShard, directory: str, chunk: int = 1 << 20) ->
             f.write(json.dumps([pid, p.original_document_id, p.source_url, p.sentence_text,
                                 p.sentence_order, p.model_name, p.processed_at_ms],
                                ensure_ascii=False) + "\n")
+        f.flush()
+        os.fsync(f.fileno())
     with open(os.path.join(tmp, "meta.json"), "w") as f:
         json.dump({"dim": D, "count": n, "format": 1, "dtype": "fp8" if fp8 else "bf16"}, f)
-    if os.path.exists(snap):
-        old = snap + ".old"
-        os.replace(snap, old)
-        os.replace(tmp, snap)
-        for fn in os.listdir(old):
-            os.remove(os.path.join(old, fn))
-        os.rmdir(old)
-    else:
-        os.replace(tmp, snap)
+        f.flush()
+        os.fsync(f.fileno())
+    fsync_dir(tmp)
+    os.replace(tmp, final)
+    fsync_dir(directory)
+    if _crash_before_commit:
+        return
+    write_atomic(os.path.join(directory, CURRENT), f"{_SNAP_PREFIX}{gen}\n".encode())
+    # committed: drop older generations and the pre-pointer layout
+    for name in os.listdir(directory):
+        p = os.path.join(directory, name)
+        if name == f"{_SNAP_PREFIX}{gen}" or not os.path.isdir(p):
+            continue
+        if name in ("snapshot", "snapshot.old", "snapshot.tmp") or name.startswith(_SNAP_PREFIX):
+            _rmtree(p)
 
 
 def load_snapshot(shard: HbmIndexShard, directory: str, chunk: int = 1 << 20) -> int:
-    snap = os.path.join(directory, "snapshot")
-    meta_p = os.path.join(snap, "meta.json")
-    if not os.path.exists(meta_p):
+    snap = committed_snapshot(directory)
+    if snap is None:
         return 0
+    meta_p = os.path.join(snap, "meta.json")
     with open(meta_p) as f:
         meta = json.load(f)
     if meta["dim"] != shard.dim:

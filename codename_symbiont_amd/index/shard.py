@@ -25,6 +25,13 @@ def _round_up(x: int, m: int) -> int:
     return (x + m - 1) // m * m
 
 
+def dedupe_last(point_ids) -> list[int]:
+    """Input positions that survive a batch upsert: the LAST occurrence of each point id, in
+    input order."""
+    last = {pid: i for i, pid in enumerate(point_ids)}
+    return sorted(last.values())
+
+
 @dataclass
 class Payload:
     original_document_id: str = ""
@@ -98,7 +105,6 @@ class HbmIndexShard:
                                 device=self.device)
         self.count = 0
         self.payloads = PayloadStore()
-        self._ws: dict = {}
         self.scan_ns = 0     # LDS ring depth of the fused scan (0 = kernel default)
         self.scan_aux = -1   # index-stream cache policy (-1 = auto: non-temporal when read once)
         self.seed_threshold = True  # sample pre-pass seeds per-query top-k thresholds
@@ -173,23 +179,25 @@ class HbmIndexShard:
         self._store(r0, vecs.to(self.device, torch.float32).contiguous(), normalize=True)
 
     def upsert(self, point_ids: list[str], vecs: torch.Tensor, payloads: list[Payload]) -> list[int]:
-        """Qdrant-style upsert: existing ids are overwritten in place, new ids appended."""
-        rows = []
-        new_pos = [i for i, pid in enumerate(point_ids) if pid not in self.payloads.id_to_row]
-        old_pos = [i for i, pid in enumerate(point_ids) if pid in self.payloads.id_to_row]
-        out = [0] * len(point_ids)
+        """Qdrant-style upsert: existing ids are overwritten in place, new ids appended.  An id
+        repeated inside one batch is one point and its last occurrence wins (Qdrant semantics);
+        every input position gets that point's row."""
+        pos = list(dedupe_last(point_ids))
+        id_to_row = self.payloads.id_to_row
+        new_pos = [i for i in pos if point_ids[i] not in id_to_row]
+        old_pos = [i for i in pos if point_ids[i] in id_to_row]
+        row_of: dict[str, int] = {}
         if new_pos:
             r0 = self.append_f32(vecs[new_pos])
             for j, i in enumerate(new_pos):
-                out[i] = r0 + j
+                row_of[point_ids[i]] = r0 + j
         for i in old_pos:
-            r = self.payloads.id_to_row[point_ids[i]]
+            r = id_to_row[point_ids[i]]
             self.write_f32(r, vecs[i:i + 1])
-            out[i] = r
-        for i, r in enumerate(out):
-            self.payloads.set(r, point_ids[i], payloads[i])
-        rows.extend(out)
-        return rows
+            row_of[point_ids[i]] = r
+        for i in pos:
+            self.payloads.set(row_of[point_ids[i]], point_ids[i], payloads[i])
+        return [row_of[pid] for pid in point_ids]
 
     def fill_random(self, n: int, seed: int = 0, chunk: int = 1 << 20) -> None:
         """Synthetic unit rows straight into HBM (benchmark corpus; no payloads)."""
@@ -256,15 +264,10 @@ class HbmIndexShard:
         rows_per_blk = _round_up(max(1, math.ceil(n / n_rblk)), TILE_ROWS)
         n_rblk = max(1, math.ceil(n / rows_per_blk))
         ncand = n_rblk * lists * kmax
-        key = (NQ, ncand)
-        ws = self._ws.get(key)
-        if ws is None:
-            ws = (torch.empty(NQ, ncand, device=self.device),
-                  torch.empty(NQ, ncand, dtype=torch.int32, device=self.device))
-            if len(self._ws) >= 4:
-                self._ws.clear()
-            self._ws[key] = ws
-        cs, ci = ws
+        # candidate workspace per call: concurrent searches (service executor threads share the
+        # stream) must never read each other's candidates; the caching allocator makes this free
+        cs = torch.empty(NQ, ncand, device=self.device)
+        ci = torch.empty(NQ, ncand, dtype=torch.int32, device=self.device)
         out_s = torch.empty(NQ, k, device=self.device)
         out_i = torch.empty(NQ, k, dtype=torch.int32, device=self.device)
         st = stream_handle(self.device)

@@ -26,7 +26,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from ..index.shard import HbmIndexShard, Payload
+from ..index.shard import HbmIndexShard, Payload, dedupe_last
 from .dist import DistInfo
 from .sharded import RANK_SHIFT, encode_gid, merge_ranked
 
@@ -159,29 +159,49 @@ class IndexGroup:
         with self._op_lock:
             self._header(OP_SNAPSHOT)
             self._do_snapshot(directory)
-            tmp = os.path.join(directory, "group_payloads.jsonl.tmp")
-            with open(tmp, "w", encoding="utf-8") as f:
-                for g, (pid, p) in self.payload_by_gid.items():
-                    f.write(json.dumps([g, pid, p.original_document_id, p.source_url, p.sentence_text,
-                                        p.sentence_order, p.model_name, p.processed_at_ms],
-                                       ensure_ascii=False) + "\n")
-            os.replace(tmp, os.path.join(directory, "group_payloads.jsonl"))
-            meta = {"world": self.info.world, "counts": self.counts, "dim": self.dim, "format": 1}
-            tmp = os.path.join(directory, "group.json.tmp")
-            with open(tmp, "w") as f:
-                json.dump(meta, f)
-                f.flush()
-                os.fsync(f.fileno())
-            os.replace(tmp, os.path.join(directory, "group.json"))
+            self._commit_group(directory)
+
+    def _commit_group(self, directory: str, _crash_before_commit: bool = False) -> None:
+        """The payload table goes to a NEW versioned file (fsync'd) that group.json names; the
+        atomic group.json replace is the one commit point for counts + payloads together, so a
+        crash can never pair a new payload table with old per-rank counts."""
+        from ..index.persist import fsync_dir, write_atomic
+
+        prev = self._group_meta(directory)
+        gen = (prev or {}).get("gen", 0) + 1
+        name = f"group_payloads.{gen}.jsonl"
+        path = os.path.join(directory, name)
+        with open(path, "w", encoding="utf-8") as f:
+            for g, (pid, p) in self.payload_by_gid.items():
+                f.write(json.dumps([g, pid, p.original_document_id, p.source_url, p.sentence_text,
+                                    p.sentence_order, p.model_name, p.processed_at_ms],
+                                   ensure_ascii=False) + "\n")
+            f.flush()
+            os.fsync(f.fileno())
+        fsync_dir(directory)
+        if _crash_before_commit:
+            return
+        meta = {"world": self.info.world, "counts": self.counts, "dim": self.dim, "format": 2,
+                "gen": gen, "payloads": name}
+        write_atomic(os.path.join(directory, "group.json"), json.dumps(meta).encode())
+        for fn in os.listdir(directory):   # committed: older tables are garbage
+            if fn.startswith("group_payloads") and fn != name:
+                os.remove(os.path.join(directory, fn))
+
+    @staticmethod
+    def _group_meta(directory: str):
+        p = os.path.join(directory, "group.json")
+        if not os.path.exists(p):
+            return None
+        with open(p) as f:
+            return json.load(f)
 
     def load(self, directory: str) -> int:
         """Collective restore written by ``snapshot``; returns the number of points (0 if none)."""
         assert self.info.is_root
-        meta_p = os.path.join(directory, "group.json")
-        if not os.path.exists(meta_p):
+        meta = self._group_meta(directory)
+        if meta is None:
             return 0
-        with open(meta_p) as f:
-            meta = json.load(f)
         if meta["world"] != self.info.world or meta["dim"] != self.dim:
             raise ValueError(f"group snapshot is for world={meta['world']} dim={meta['dim']}, "
                              f"this group is world={self.info.world} dim={self.dim}")
@@ -192,11 +212,18 @@ class IndexGroup:
         self.counts = list(meta["counts"])
         self.payload_by_gid.clear()
         self.gid_by_pid.clear()
-        with open(os.path.join(directory, "group_payloads.jsonl"), encoding="utf-8") as f:
+        # format 1 (one unversioned table) is still read; either way entries past a rank's
+        # committed row count are dropped, so a table newer than the counts cannot leave gids
+        # pointing beyond a shard
+        name = meta.get("payloads", "group_payloads.jsonl")
+        with open(os.path.join(directory, name), encoding="utf-8") as f:
             for line in f:
                 a = json.loads(line)
-                self.payload_by_gid[a[0]] = (a[1], Payload(*a[2:]))
-                self.gid_by_pid[a[1]] = a[0]
+                g = a[0]
+                if (g & ((1 << RANK_SHIFT) - 1)) >= self.counts[g >> RANK_SHIFT]:
+                    continue
+                self.payload_by_gid[g] = (a[1], Payload(*a[2:]))
+                self.gid_by_pid[a[1]] = g
         return sum(self.counts)
 
     def snapshot_dir_exists(self, directory: str) -> bool:
@@ -224,6 +251,13 @@ class IndexGroup:
             return self._upsert_locked(point_ids, vecs, payloads)
 
     def _upsert_locked(self, point_ids, vecs, payloads) -> list[int]:
+        # an id repeated inside the batch is ONE point, last occurrence wins (HbmIndexShard.upsert)
+        pos = dedupe_last(point_ids)
+        if len(pos) != len(point_ids):
+            ids_u = [point_ids[i] for i in pos]
+            gids_u = self._upsert_locked(ids_u, vecs[pos], [payloads[i] for i in pos])
+            by_pid = dict(zip(ids_u, gids_u))
+            return [by_pid[pid] for pid in point_ids]
         n = len(point_ids)
         owner = np.empty(n, np.int64)
         target = np.full(n, -1, np.int64)

@@ -69,6 +69,7 @@ struct Sub {
   std::vector<std::string> toks;
   bool wild = false;
   long long max_msgs = -1, delivered = 0;
+  uint64_t seq = 0;  // creation order: deliveries follow it (as the Python spec broker does)
 };
 
 struct Conn {
@@ -662,6 +663,7 @@ class Server {
 
   // ---- subscription index ----
   void index(Sub* s) {
+    s->seq = ++sub_seq_;
     if (s->wild) wild_.push_back(s);
     else literal_[s->subject].push_back(s);
     cache_.clear();
@@ -692,8 +694,13 @@ class Server {
     if (lit != literal_.end()) m = lit->second;
     if (!wild_.empty()) {
       const auto toks = split_dots(subject);
+      const size_t n_lit = m.size();
       for (Sub* s : wild_)
         if (subject_matches(s->toks, toks)) m.push_back(s);
+      // literal and wildcard lists are each in creation order; merge them into one
+      if (n_lit && m.size() > n_lit)
+        std::inplace_merge(m.begin(), m.begin() + n_lit, m.end(),
+                           [](const Sub* a, const Sub* b) { return a->seq < b->seq; });
     }
     return cache_.emplace(subject, std::move(m)).first->second;
   }
@@ -879,6 +886,7 @@ class Server {
   std::unordered_map<int, std::unique_ptr<Conn>> conns_;
   std::unordered_map<std::string, std::vector<Sub*>> literal_;
   std::vector<Sub*> wild_;
+  uint64_t sub_seq_ = 0;
   std::unordered_map<std::string, std::vector<Sub*>> cache_;
   std::unordered_map<std::string, uint64_t> qrr_;
   std::vector<Conn*> dirty_, dead_;

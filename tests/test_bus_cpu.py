@@ -201,7 +201,7 @@ def test_native_broker_fanout_and_stats():
 # ---------------------------------------------------------------------------------------------
 # differential property test: random protocol scripts give byte-identical per-connection output
 # on the native server and on the asyncio reference broker
-from hypothesis import HealthCheck, given, settings  # noqa: E402
+from hypothesis import HealthCheck, example, given, settings  # noqa: E402
 from hypothesis import strategies as st  # noqa: E402
 
 _TOK = st.sampled_from(["a", "b", "c"])
@@ -268,6 +268,9 @@ async def _script_output(Broker, script):
 
 @settings(max_examples=100, deadline=None, suppress_health_check=[HealthCheck.too_slow])
 @given(st.lists(_OP, min_size=1, max_size=25))
+# a reused sid re-subscribed after a wildcard sub: delivery follows creation order, not sid order
+@example([("sub", 0, "a", 1), ("unsub", 0, 1, 0), ("sub", 0, "*.*.*", 2), ("sub", 1, "*", 1),
+          ("sub", 0, "a.b.b", 1), ("pub", 0, "a.b.b", b"")])
 def test_native_broker_matches_reference_on_random_scripts(script):
     py = run(_script_output(BROKERS["py"], script))
     nat = run(_script_output(BROKERS["native"], script))

@@ -47,7 +47,10 @@ def test_snapshot_wal_resume_and_torn_tail(tmp_path):
     for i in range(0, 25, 5):   # 25 points: snapshot at 10 and 20, 5 rows left in the WAL
         st.upsert([f"p{j}" for j in range(i, i + 5)], v[i:i + 5],
                   [Payload(f"doc{j}", "u", f"s{j}", j, "m", 100 + j) for j in range(i, i + 5)])
-    assert os.path.exists(os.path.join(d, "snapshot", "vectors.npy"))
+    from codename_symbiont_amd.index.persist import committed_snapshot
+
+    assert os.path.exists(os.path.join(committed_snapshot(d), "vectors.npy"))
+    assert sorted(n for n in os.listdir(d) if n.startswith("snapshot")) == ["snapshot.2"]
     st.wal.close()  # crash: no close() snapshot
     with open(os.path.join(d, "wal.log"), "ab") as f:   # torn record at the tail
         f.write(b"SYMB\x05\x00\x00\x00garbage")
@@ -63,6 +66,66 @@ def test_snapshot_wal_resume_and_torn_tail(tmp_path):
     assert sum(len(ids) for ids, _, _ in recs) >= 1
     st3 = VectorStore(8, 1000, device="cpu", snapshot_dir=d)
     assert st3.count == 26
+
+
+def _store_with(d, n, seed=1, snapshot_every=1 << 30):
+    st = VectorStore(8, 1000, device="cpu", snapshot_dir=d, snapshot_every=snapshot_every)
+    v = _vecs(n, 8, seed)
+    st.upsert([f"p{j}" for j in range(n)], v, [Payload(f"doc{j}", "u", f"s{j}", j) for j in range(n)])
+    return st, v
+
+
+def test_snapshot_crash_before_commit_keeps_previous_generation(tmp_path):
+    """A crash after the new generation is written but before CURRENT moves: the boot loads the
+    previous committed generation and replays the (untruncated) WAL -- nothing is lost, and the
+    next snapshot still succeeds over the leftover directory."""
+    from codename_symbiont_amd.index import persist
+
+    d = str(tmp_path / "idx")
+    st, v = _store_with(d, 10)
+    st.snapshot()                                     # gen 1 committed, WAL empty
+    more = _vecs(5, 8, 9)
+    st.upsert([f"q{j}" for j in range(5)], more, [Payload("dq")] * 5)   # in the WAL only
+    persist.save_snapshot(st.shard, d, _crash_before_commit=True)       # gen 2 uncommitted
+    st.wal.close()                                    # crash: WAL not truncated
+    assert open(os.path.join(d, "CURRENT")).read().strip() == "snapshot.1"
+    st2 = VectorStore(8, 1000, device="cpu", snapshot_dir=d)
+    assert st2.count == 15
+    s, r = st2.search(more[3], 1)
+    assert st2.lookup(r[0, 0])[0] == "q3"
+    st2.snapshot()                                    # gen 3 commits; 1 and 2 are removed
+    assert sorted(n for n in os.listdir(d) if n.startswith("snapshot")) == ["snapshot.3"]
+    st2.wal.close()
+    assert VectorStore(8, 1000, device="cpu", snapshot_dir=d).count == 15
+
+
+def test_snapshot_legacy_layout_and_interrupted_swap(tmp_path):
+    """Directories written by the old two-rename swap still load: ``snapshot/``, or only
+    ``snapshot.old`` when a crash hit between the two renames."""
+    from codename_symbiont_amd.index import persist
+
+    d = str(tmp_path / "idx")
+    sh = HbmIndexShard(8, 100, device="cpu")
+    sh.append_f32(torch.from_numpy(_vecs(7, 8)))
+    persist.save_snapshot(sh, d)
+    os.remove(os.path.join(d, "CURRENT"))
+    os.rename(os.path.join(d, "snapshot.1"), os.path.join(d, "snapshot.old"))
+    sh2 = HbmIndexShard(8, 100, device="cpu")
+    assert persist.load_snapshot(sh2, d) == 7
+    persist.save_snapshot(sh2, d)                     # stale .old no longer blocks a snapshot
+    assert not os.path.exists(os.path.join(d, "snapshot.old"))
+    assert persist.load_snapshot(HbmIndexShard(8, 100, device="cpu"), d) == 7
+
+
+def test_upsert_duplicate_ids_in_one_batch_last_wins():
+    st = VectorStore(8, 10, device="cpu")
+    v = _vecs(3, 8)
+    st.upsert(["a", "b", "a"], v, [Payload("d", "u", t) for t in ("a1", "b", "a2")])
+    assert st.count == 2
+    s, r = st.search(v[2], 2)
+    assert st.lookup(r[0, 0])[1].sentence_text == "a2"
+    assert st.lookup(r[0, 0])[0] == "a"
+    assert len(st.shard.payloads.id_to_row) == 2
 
 
 def test_fp8_shard_cpu_path_and_snapshot(tmp_path):

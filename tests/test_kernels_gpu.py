@@ -205,6 +205,43 @@ def test_index_scan_small_and_partial():
     assert sorted(r[0, :3].tolist()) == [0, 1, 2]
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "fp8"])
+def test_concurrent_searches_match_sequential(dtype):
+    """The service runs searches from several executor threads on one shard and one stream:
+    interleaved enqueues (A.scan, B.scan, A.merge, B.merge) must never mix candidates."""
+    import threading
+
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+
+    D, n, nq, k = (384 if dtype == "bf16" else 512), 200_003, 64, 10
+    shard = HbmIndexShard(D, n, dtype=dtype)
+    shard.fill_random(n, seed=21)
+    qs = [torch.nn.functional.normalize(_f(nq, D, seed=40 + t), dim=-1).bfloat16()
+          for t in range(4)]
+    seq = [shard.search(q, k) for q in qs]
+    torch.cuda.synchronize()
+    seq = [(s.cpu(), r.cpu()) for s, r in seq]
+    got = [None] * len(qs)
+    start = threading.Barrier(len(qs))
+
+    def run(t):
+        start.wait()
+        res = []
+        for _ in range(8):
+            res.append(shard.search(qs[t], k))
+        torch.cuda.synchronize()
+        got[t] = [(s.cpu(), r.cpu()) for s, r in res]
+
+    th = [threading.Thread(target=run, args=(t,)) for t in range(len(qs))]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(120)
+    for t in range(len(qs)):
+        for s, r in got[t]:
+            assert torch.equal(r, seq[t][1]) and torch.equal(s, seq[t][0]), t
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("D", [384, 768])
 def test_index_scan_seeded_threshold_is_exact(D):

@@ -152,7 +152,7 @@ def test_index_group_upsert_search_overwrite():
     assert out[1] == 100 and out[2] == 100          # least-loaded placement balances the shards
 
 
-def _group_snapshot_worker(rank, world, port, snap, phase, out):
+def _group_snapshot_worker(rank, world, port, snap, phase, out, crash_mid=False):
     """phase 0: ingest, snapshot, ingest more (WAL only), crash.  phase 1: restore + search."""
     from codename_symbiont_amd.index.shard import Payload
     from codename_symbiont_amd.index.store import VectorStore
@@ -176,6 +176,15 @@ def _group_snapshot_worker(rank, world, port, snap, phase, out):
             store.upsert(ids[150:], vecs[150:], pls[150:])     # only in the WAL
             store.upsert(["p3"], -vecs[3:4], [Payload("d3", "u", "t3-new", 3)])
             out[(0, 0)] = store.count
+            if crash_mid:
+                # crash INSIDE the next snapshot: every rank saved its shard and rank 0 wrote the
+                # new payload table, but group.json was never replaced
+                from codename_symbiont_amd.parallel.index_group import OP_SNAPSHOT
+
+                with grp._op_lock:
+                    grp._header(OP_SNAPSHOT)
+                    grp._do_snapshot(snap)
+                    grp._commit_group(snap, _crash_before_commit=True)
             store.wal.close()                                  # crash: no final snapshot
         else:
             out[(1, 0)] = store.count
@@ -186,16 +195,21 @@ def _group_snapshot_worker(rank, world, port, snap, phase, out):
     D.shutdown(info)
 
 
-def test_index_group_snapshot_restore(tmp_path):
+@pytest.mark.parametrize("crash_mid", [False, True], ids=["clean", "crash_mid_snapshot"])
+def test_index_group_snapshot_restore(tmp_path, crash_mid):
+    from codename_symbiont_amd.index.persist import committed_snapshot
+
     world = 2
     snap = str(tmp_path / "snap")
     mgr = mp.Manager()
     out = mgr.dict()
     for phase in (0, 1):
-        mp.start_processes(_group_snapshot_worker, args=(world, _free_port(), snap, phase, out),
+        mp.start_processes(_group_snapshot_worker,
+                           args=(world, _free_port(), snap, phase, out, crash_mid),
                            nprocs=world, join=True, start_method="spawn")
     assert os.path.exists(os.path.join(snap, "group.json"))
-    assert os.path.exists(os.path.join(snap, "rank1", "snapshot", "vectors.npy"))
+    assert os.path.exists(os.path.join(committed_snapshot(os.path.join(snap, "rank1")),
+                                       "vectors.npy"))
     assert out[(0, 0)] == 200 and out[(1, 0)] == 200      # 150 from the snapshot + 50 from the WAL
     assert out[(1, 1)] == 100                             # rank 1's shard restored, then WAL rows
     assert out["texts"] == ["t10", "t170", "t3-new"]
