@@ -242,6 +242,8 @@ def cmd_gemm(a):
             if N % 256 == 0:
                 var["hip_256x256"] = lambda: (_hip().gemm_config(128, 2, 8),
                                               K.gemm(x, w, b, epi, rr, g, be, 1e-12, out=y))
+                var["hip_256_8phase"] = lambda: (_hip().gemm_config(128, 9, 8),
+                                                 K.gemm(x, w, b, epi, rr, g, be, 1e-12, out=y))
         res = ab(var, rounds=a.rounds, iters=a.iters)
         _hip().gemm_config(128, 3, 8)
         fl = 2 * M * N * Kd

@@ -234,8 +234,10 @@ class HbmIndexShard:
             # threshold seeding: the k-th best score over the first m rows lower-bounds the final
             # k-th score, so the full scan may drop anything below it (exact; see the kernel note)
             pre_s, _ = self._scan(m, q_unit, kmax, k, None, n_cus)
-            thr = torch.nextafter(pre_s[:, k - 1].contiguous(),
-                                  torch.tensor(-math.inf, device=self.device))
+            kth = pre_s[:, k - 1].contiguous()
+            # (full_like, not torch.tensor(-inf, device=...): a pageable H2D copy would block the
+            # host on the stream every search and leave the GPU idle while the scan is enqueued)
+            thr = torch.nextafter(kth, torch.full_like(kth, -math.inf))
         out_s, out_i = self._scan(n, q_unit, kmax, k, thr, n_cus)
         if self.dtype == "fp8":
             out_s.mul_(1.0 / (FP8_SCALE * FP8_SCALE))
@@ -249,6 +251,12 @@ class HbmIndexShard:
             return 0
         return max(_round_up(n // self.SEED_DIV, TILE_ROWS), _round_up(k, TILE_ROWS))
 
+    def _n_cus(self) -> int:
+        n = getattr(self, "_cus", None)
+        if n is None:
+            n = self._cus = torch.cuda.get_device_properties(self.device).multi_processor_count
+        return n
+
     def _scan(self, n: int, q_unit: torch.Tensor, kmax: int, k: int, thr, n_cus):
         from ..ops._ext import hip, stream_handle
 
@@ -259,7 +267,7 @@ class HbmIndexShard:
             lists, qpb = hip().topk_geometry(self.dim, kmax)
         n_qblk = math.ceil(NQ / qpb)
         if n_cus is None:
-            n_cus = torch.cuda.get_device_properties(self.device).multi_processor_count
+            n_cus = self._n_cus()
         n_rblk = max(1, min(math.ceil(n / (TILE_ROWS * 16)), max(1, round(n_cus / n_qblk))))
         rows_per_blk = _round_up(max(1, math.ceil(n / n_rblk)), TILE_ROWS)
         n_rblk = max(1, math.ceil(n / rows_per_blk))

@@ -44,6 +44,7 @@ int symb_index_scan_ablate(const void* X, int n_valid, int rows_per_blk, int n_r
                            const void* Q, int NQ, float* cs, int* ci, hipStream_t st, int abl,
                            const float* thr);
 int symb_gemm_config(int resln_bm, int tile, int group_m);
+int symb_gemm256_ablate(int abl);
 int symb_gemm_fp8_config(int waves, int big);
 int symb_gemm_resln_config(int waves);
 int symb_gemm_fp8(int epi, const void* A8, int lda, const void* W8, int ldw, const float* sa,
@@ -319,6 +320,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("attention_config", [](int waves, int kvt) {
     check(symb_attention_config(waves, kvt), "attention_config");
   }, py::arg("waves") = 8, py::arg("kvt") = 64);
+  m.def("gemm256_ablate", [](int abl) { check(symb_gemm256_ablate(abl), "gemm256_ablate"); });
   m.def("gemm_config", [](int resln_bm, int tile, int group_m) {
     check(symb_gemm_config(resln_bm, tile, group_m), "gemm_config");
   }, py::arg("resln_bm") = 128, py::arg("tile") = 3, py::arg("group_m") = 8);

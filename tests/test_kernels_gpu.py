@@ -67,7 +67,7 @@ def test_add_ln(H):
     _close(add_ln(x, None, g, b, 1e-5), R.add_ln_ref(x, None, g, b, 1e-5), 3e-2, 1e-2, "ln")
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 4, 5, 6, 7, 8, 16])
+@pytest.mark.parametrize("tile", [0, 1, 2, 4, 5, 6, 7, 8, 9, 16])
 @pytest.mark.parametrize("M,N,K,epi", [
     (300, 1152, 384, 0), (129, 1536, 384, 1), (517, 384, 384, 2), (517, 384, 384, 3),
     (300, 384, 1536, 3), (64, 768, 768, 2), (1000, 2304, 768, 0), (77, 1024, 4096, 2),
@@ -76,6 +76,8 @@ def test_add_ln(H):
     (16384, 1152, 384, 0), (12800, 1536, 384, 1), (9000, 768, 3072, 2),
     # tile=2 (256x256, banded epilogue) on every epilogue, ragged last row tile
     (2000, 3072, 768, 1), (4353, 768, 3072, 2), (999, 2304, 768, 0),
+    # tile=9 (8-phase 256x256): one and two loop iterations, a single 256-wide column tile
+    (300, 512, 128, 0), (513, 256, 256, 2),
 ])
 def test_gemm(M, N, K, epi, tile):
     from codename_symbiont_amd.ops._ext import hip
@@ -87,9 +89,10 @@ def test_gemm(M, N, K, epi, tile):
     # the default (3, auto) is covered by the encoder tests
     # tile=4/5: 128x128 with 3-/4-deep rings at one workgroup per CU
     # tile=16: default tiles with the 8-wave (64x96 wave tiles) row-complete RES_LN tile
-    # (others: the default 16-wave one); tile=8: 16 waves of 32x32
+    # (others: the default 16-wave one); tile=8: 16 waves of 32x32; tile=9: the 8-phase
+    # 256x256 kernel (gemm256.hip) where N % 256 == 0 and K % 128 == 0
     hip().gemm_config(64 if tile == 1 else 128, 3 if tile == 16 else tile,
-                      {0: 8, 1: 3, 2: 0, 4: 8, 5: 5, 6: 8, 7: 2, 8: 8, 16: 8}[tile])
+                      {0: 8, 1: 3, 2: 0, 4: 8, 5: 5, 6: 8, 7: 2, 8: 8, 9: 8, 16: 8}[tile])
     hip().gemm_resln_config(8 if tile == 16 else 16)
 
     a = _bf(M, K, seed=1)
