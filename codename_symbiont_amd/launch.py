@@ -1,7 +1,7 @@
 """Supervisor: the docker-compose.yml replacement (no docker on MI355X boxes).
 
     python -m codename_symbiont_amd.launch [--gpus N] [--only api,preprocessing,...]
-           [--broker-port 4222] [--api-port 8080] [--no-broker]
+           [--broker-port 4222] [--api-port 8080] [--no-broker] [--env-file .env]
 
 Starts the in-repo NATS broker and every service as child processes with the reference's env
 plumbing (NATS_URL, API_SERVER_*, NEO4J_*, ...).  GPU services scale with ``--gpus``:
@@ -12,6 +12,10 @@ plumbing (NATS_URL, API_SERVER_*, NEO4J_*, ...).  GPU services scale with ``--gp
 * vector_memory: ONE logical index over N ranks (torch.distributed.run, RCCL), rank 0 on NATS.
 Unlike the reference compose file (no restart policies) crashed children are
 restarted with exponential backoff.  Children are started as subprocesses, never exec'd.
+
+Like ``docker compose``, a ``.env`` file in the working directory (or ``--env-file``) supplies
+variables (the reference's keys: NATS_URL, NEO4J_*, API_SERVER_PORT, ...; .env.example:1-12);
+variables already set in the launching shell take precedence over the file.
 """
 from __future__ import annotations
 
@@ -61,12 +65,20 @@ class Child:
 
 
 def build_children(a) -> list[Child]:
+    from .utils.config import read_env_file
     from .utils.gpu_debug import debug_env
 
     py = sys.executable
-    base = debug_env()   # + AMD_SERIALIZE_KERNEL / HIP_LAUNCH_BLOCKING under SYMB_GPU_DEBUG=1
+    env_file = getattr(a, "env_file", None)
+    if env_file is None and os.path.exists(".env"):
+        env_file = ".env"
+    # compose semantics: the shell's own variables win over the .env file
+    file_env = read_env_file(env_file) if env_file else {}
+    base = debug_env(dict(file_env, **os.environ))   # + AMD_SERIALIZE_KERNEL / HIP_LAUNCH_BLOCKING
     base.setdefault("NATS_URL", f"nats://127.0.0.1:{a.broker_port}")
-    base["API_SERVER_PORT"] = str(a.api_port)
+    if a.api_port is not None:
+        base["API_SERVER_PORT"] = str(a.api_port)
+    base.setdefault("API_SERVER_PORT", "8080")
     only = set(a.only.split(",")) if a.only else set(SERVICES)
     kids = []
     if not a.no_broker:
@@ -100,7 +112,9 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--only", default="")
     ap.add_argument("--broker-port", type=int, default=4222)
-    ap.add_argument("--api-port", type=int, default=8080)
+    ap.add_argument("--api-port", type=int, default=None,
+                    help="gateway port (default: API_SERVER_PORT from the env / .env, else 8080)")
+    ap.add_argument("--env-file", default=None, help="compose-style KEY=VALUE file (default .env)")
     ap.add_argument("--dist-port", type=int, default=29600)
     ap.add_argument("--no-broker", action="store_true")
     ap.add_argument("--embed-dp", choices=["queue", "rccl"], default="queue",

@@ -7,6 +7,7 @@ four BASELINE.json configurations.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 
 
@@ -30,6 +31,8 @@ class EncoderConfig:
     lowercase: bool = True
     special: dict = field(default_factory=lambda: {"cls": "[CLS]", "sep": "[SEP]", "pad": "[PAD]",
                                                    "unk": "[UNK]"})
+    # local HF snapshot (models/hub.py) the weights and tokenizer come from; "" = synthetic
+    source_dir: str = ""
 
     @property
     def head_dim(self) -> int:
@@ -73,9 +76,24 @@ ALIASES = {
 }
 
 
-def get_config(name: str) -> EncoderConfig:
+def get_config(name: str, revision: str | None = None) -> EncoderConfig:
+    """A built-in family (by key or HF id) or any BERT / XLM-R model found offline in the local
+    HF cache / a local directory (models/hub.py).  A built-in family whose real snapshot is in the
+    cache takes that snapshot's config, weights and tokenizer; otherwise its weights are seeded
+    random init and its vocabulary synthetic."""
+    from . import hub
+
+    revision = revision or os.environ.get("SYMB_MODEL_REVISION", "main")
     k = name.lower()
     k = ALIASES.get(k, k)
-    if k not in MODELS:
-        raise KeyError(f"unknown model {name!r}; known: {sorted(MODELS)}")
-    return MODELS[k]
+    if k in MODELS:
+        base = MODELS[k]
+        snap = hub.resolve_snapshot(base.model_name, revision)
+        if snap is None:
+            return base
+        return hub.config_from_dir(snap, base.model_name, key=k)
+    snap = hub.resolve_snapshot(name, revision)
+    if snap is None:
+        raise KeyError(f"unknown model {name!r}: not a built-in family {sorted(MODELS)} and no "
+                       f"local snapshot (HF cache: {[str(c) for c in hub.cache_dirs()]})")
+    return hub.config_from_dir(snap, "" if os.path.isdir(name) else name)

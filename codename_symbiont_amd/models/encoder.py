@@ -97,6 +97,16 @@ class HipEncoder:
 
     backend = "hip"
 
+    @staticmethod
+    def supports(cfg: EncoderConfig) -> str:
+        """'' if the gfx950 kernels take this architecture, else the reason they do not
+        (attention head dims 32 / 64; GEMM widths multiples of 128)."""
+        if cfg.head_dim not in (32, 64):
+            return f"head_dim {cfg.head_dim} (kernels: 32, 64)"
+        if cfg.hidden % 128 or cfg.ffn % 128:
+            return f"hidden {cfg.hidden} / ffn {cfg.ffn} not multiples of 128"
+        return ""
+
     def __init__(self, cfg: EncoderConfig, params: dict | None = None, device="cuda", seed=0,
                  precision: str = "bf16"):
         """precision "fp8": the four projection GEMMs of every layer run on e4m3 MFMAs with
@@ -105,6 +115,9 @@ class HipEncoder:
 
         if precision not in ("bf16", "fp8"):
             raise ValueError(f"encoder precision must be bf16 or fp8, got {precision!r}")
+        why = self.supports(cfg)
+        if why:
+            raise ValueError(f"{cfg.model_name}: unsupported by the HIP encoder: {why}")
         self.cfg = cfg
         self.precision = precision
         self.device = _resolve(device)
@@ -294,7 +307,15 @@ class TorchEncoder:
 def make_encoder(cfg: EncoderConfig, force_cpu: bool = False, seed: int = 0, device=None,
                  precision: str = "bf16"):
     """GPU present -> HIP encoder (extension mandatory; bf16 or fp8 GEMMs); otherwise the fp32
-    CPU backend."""
+    CPU backend.  A snapshot architecture the gfx950 kernels do not take (models/hub.py loads any
+    BERT / XLM-R) runs as the fp32 PyTorch network on the GPU, with a warning."""
     if not force_cpu and torch.cuda.is_available():
-        return HipEncoder(cfg, seed=seed, device=device or "cuda", precision=precision)
+        why = HipEncoder.supports(cfg)
+        if not why:
+            return HipEncoder(cfg, seed=seed, device=device or "cuda", precision=precision)
+        import logging
+
+        logging.getLogger("symbiont.encoder").warning(
+            "[EMBED_INIT] %s: %s -> fp32 PyTorch encoder on the GPU", cfg.model_name, why)
+        return TorchEncoder(cfg, seed=seed, device=device or "cuda")
     return TorchEncoder(cfg, seed=seed)

@@ -88,6 +88,8 @@ def params_from_state_dict(cfg: EncoderConfig, sd: dict) -> dict:
 
 
 def load_params(cfg: EncoderConfig, path: str | None = None, seed: int = 0, device="cpu") -> dict:
+    """Weights from ``path`` / ``SYMB_WEIGHTS`` (a safetensors file), else from the config's HF
+    snapshot (models/hub.py), else seeded random init."""
     path = path or os.environ.get("SYMB_WEIGHTS")
     if path:
         from safetensors.torch import load_file  # executes nothing from the file
@@ -95,6 +97,12 @@ def load_params(cfg: EncoderConfig, path: str | None = None, seed: int = 0, devi
         sd = load_file(path, device="cpu")
         p = params_from_state_dict(cfg, sd)
         return to_device(p, device)
+    if cfg.source_dir:
+        from pathlib import Path
+
+        from .hub import load_state_dict
+
+        return to_device(params_from_state_dict(cfg, load_state_dict(Path(cfg.source_dir))), device)
     return random_params(cfg, seed=seed, device=device)
 
 

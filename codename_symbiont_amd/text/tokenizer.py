@@ -166,15 +166,21 @@ def _load_tokenizer_json(path: str):
 class Tokenizer:
     """Native tokenizer front-end for an encoder family: BERT BasicTokenizer + WordPiece, or (XLM-R
     family) NFKC + Metaspace + SentencePiece-Unigram Viterbi.  Sources, in order: ``vocab_file``
-    argument / ``SYMB_TOKENIZER`` (a HF tokenizer.json) / ``SYMB_VOCAB`` (a BERT vocab.txt), else
-    the deterministic synthetic vocabulary of the family (real special-token layout and size)."""
+    argument / ``SYMB_TOKENIZER`` (a HF tokenizer.json) / ``SYMB_VOCAB`` (a BERT vocab.txt) / the
+    model's local HF snapshot (models/hub.py), else the deterministic synthetic vocabulary of the
+    family (real special-token layout and size)."""
 
     def __init__(self, cfg: EncoderConfig, vocab_file: str | None = None):
         self.cfg = cfg
         sp = cfg.special
         self.kind = "unigram" if sp["cls"] == "<s>" else "wordpiece"
-        path = vocab_file if vocab_file is not None else (os.environ.get("SYMB_TOKENIZER", "")
-                                                          or os.environ.get("SYMB_VOCAB", ""))
+        if vocab_file is not None:
+            path = vocab_file
+        else:
+            from ..models.hub import tokenizer_file
+
+            path = (os.environ.get("SYMB_TOKENIZER", "") or os.environ.get("SYMB_VOCAB", "")
+                    or tokenizer_file(cfg))
         pieces = scores = None
         unk_id = 3
         if path.endswith(".json"):

@@ -81,3 +81,31 @@ class Config:
     publish_tokenized: bool = field(default_factory=lambda: _bool("SYMB_PUBLISH_TOKENIZED", True))
     queue_group: str = field(default_factory=lambda: _env("SYMB_QUEUE_GROUP", ""))
     fault_spec: str = field(default_factory=lambda: _env("SYMB_FAULT", ""))
+
+
+def read_env_file(path: str) -> dict[str, str]:
+    """docker-compose ``.env`` syntax: KEY=VALUE per line, ``#`` comments and blank lines skipped,
+    an optional ``export`` prefix, single or double quotes around the value stripped (escapes in
+    double quotes: \\n, \\", \\\\), an unquoted value's trailing `` # comment`` dropped."""
+    out: dict[str, str] = {}
+    with open(path, encoding="utf-8") as f:
+        for raw in f:
+            line = raw.strip()
+            if not line or line.startswith("#"):
+                continue
+            if line.startswith("export "):
+                line = line[len("export "):].lstrip()
+            key, sep, val = line.partition("=")
+            key = key.strip()
+            if not sep or not key:
+                continue
+            val = val.strip()
+            if len(val) >= 2 and val[0] == val[-1] and val[0] in "'\"":
+                q, val = val[0], val[1:-1]
+                if q == '"':
+                    val = (val.replace("\\\\", "\0").replace("\\n", "\n").replace('\\"', '"')
+                           .replace("\0", "\\"))
+            else:
+                val = val.split(" #", 1)[0].rstrip()
+            out[key] = val
+    return out

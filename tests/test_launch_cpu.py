@@ -122,3 +122,36 @@ def test_supervisor_serves_restarts_and_stops():
     while any(_alive(p) for p in live.values()) and time.time() - t0 < 15:
         time.sleep(0.2)
     assert not any(_alive(p) for p in live.values()), "supervisor left children behind"
+
+
+def test_env_file_compose_semantics(tmp_path, monkeypatch):
+    """.env like docker compose: comments, export, quotes; the shell's variables win."""
+    import argparse
+
+    from codename_symbiont_amd.launch import build_children
+    from codename_symbiont_amd.utils.config import read_env_file
+
+    p = tmp_path / ".env"
+    p.write_text("# reference .env.example keys\n"
+                 "NATS_URL=nats://cs-nats:4222\n"
+                 "export NEO4J_USER=neo4j\n"
+                 "NEO4J_PASSWORD=\"pa ss\\\"word\"\n"
+                 "API_SERVER_PORT=7070   # gateway\n"
+                 "FRONTEND_PORT='3000'\n"
+                 "\n"
+                 "NOT_A_PAIR\n")
+    env = read_env_file(str(p))
+    assert env == {"NATS_URL": "nats://cs-nats:4222", "NEO4J_USER": "neo4j",
+                   "NEO4J_PASSWORD": 'pa ss"word', "API_SERVER_PORT": "7070",
+                   "FRONTEND_PORT": "3000"}
+    monkeypatch.setenv("NEO4J_USER", "from-shell")
+    monkeypatch.delenv("NATS_URL", raising=False)
+    monkeypatch.delenv("API_SERVER_PORT", raising=False)
+    a = argparse.Namespace(broker_port=4333, api_port=None, env_file=str(p), only="api",
+                           no_broker=True, gpus=1, embed_dp="queue", dist_port=29600)
+    (kid,) = build_children(a)
+    assert kid.env["NATS_URL"] == "nats://cs-nats:4222"       # from the file
+    assert kid.env["NEO4J_USER"] == "from-shell"               # shell wins
+    assert kid.env["API_SERVER_PORT"] == "7070"
+    a.api_port = 9999                                          # the flag wins over both
+    assert build_children(a)[0].env["API_SERVER_PORT"] == "9999"
