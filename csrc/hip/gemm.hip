@@ -420,15 +420,16 @@ static int g_resln_bm = 128;
 // Tile of the bias / GELU / residual GEMMs: 0 = 128x128 (4 waves, 2-stage ring),
 // 1 = 256x128 (8 waves, 3-stage ring with a tile in flight across each barrier),
 // 2 = 256x256 (8 waves of 128x64, 2-stage ring, one workgroup per CU) whenever N % 256 == 0,
-// 3 = auto: the 8-phase 256x256 kernel (gemm256.hip) when it gives every CU >= 3 tiles (see
-//     gemm256_auto); else 256x256 when N % 256 == 0, K >= 768 and the grid fills whole waves of the 256 CUs
+// 3 = auto: 256x256 when N % 256 == 0, K >= 768 and the grid fills whole waves of the 256 CUs
 //     (or is long enough that a partial last wave costs little), else 128x128 with 8 waves of 64x32
 //     (4 waves per SIMD at 2 workgroups per CU: +3-8 % over 4 waves of 64x64,
 //     profiles/r1_s4/gemm_8wave.json); grids smaller than the 256 CUs take a 4-deep ring;
 // 4 / 5 = 128x128 with a 3- / 4-deep ring at one workgroup per CU (A/B knobs);
 // 6 / 7 = 128x128 with 8 waves of 32x64 / 64x32; 8 = 128x128 with 16 waves of 32x32;
-// 9 = the 256x256 8-phase kernel (gemm256.hip) wherever it applies (N % 256, K % 128);
-// 10 = auto without the 8-phase kernel (the round-1 rule; A/B knob).
+// 9 = the 256x256 8-phase kernel (gemm256.hip) wherever it applies (N % 256, K % 128): faster
+//     in isolation (+3-8 % at K >= 768 with >= 3 tiles per CU) but not inside the encoders
+//     (bge-base 7.93 vs 7.73 ms, e5-large 23.09 vs 22.86 ms; profiles/r2_gemm), so opt-in;
+// 10 = same as 3 (kept for the A/B scripts).
 static int g_tile = 3;
 static bool use_big_tile(int tile, int M, int N, int K) {
   if (N % 256 != 0 || (tile != 2 && tile != 3)) return false;
@@ -439,25 +440,6 @@ static bool use_big_tile(int tile, int M, int N, int K) {
   const int tiles = ((M + 255) / 256) * (N / 256);
   return tiles % 256 == 0 || tiles >= 4 * 256;
 }
-// auto rule for the 8-phase kernel (profiles/r2_gemm): it beats the 2-stage 256x256 / 8-wave
-// 128x128 tiles by 3-8 % once every CU gets >= 3 of its persistent tiles and K >= 768 (K = 768:
-// 799 vs 758 TFLOP/s bias, 672 vs 654 GELU; K = 3072: 1073 vs 990), and loses on short grids
-// where the last partial round of 256x256 tiles dominates (N = 768, 384 tiles: 547 vs 754), at
-// K = 384 (MiniLM FFN1 466 vs 488) and with the residual epilogue
-static bool gemm256_auto(int M, int N, int K) {
-  static int n_cus = 0;
-  if (n_cus == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&n_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        n_cus <= 0)
-      n_cus = 256;
-  }
-  if (N % 256 != 0 || K % 128 != 0 || K < 768) return false;
-  const long tiles = (long)((M + 255) / 256) * (N / 256);
-  return tiles >= 3L * n_cus;
-}
-
 int symb_gemm_config(int resln_bm, int tile, int group_m) {
   if (resln_bm != 64 && resln_bm != 128) return -1;
   if (tile < 0 || tile > 10) return -1;
@@ -511,8 +493,7 @@ int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const flo
     return -1;  // wider rows: EPI_RES + symb_add_ln
   }
   if (N % 128 != 0) return -1;
-  if ((g_tile == 9 || (g_tile == 3 && epi != EPI_RES && gemm256_auto(M, N, K))) &&
-      symb_gemm256_supported(M, N, K))
+  if (g_tile == 9 && symb_gemm256_supported(M, N, K))
     return symb_gemm256(epi, A, lda, W, ldw, bias, R, ldr, C, ldc, M, N, K, g_group_m, st);
   const int tile_mode = g_tile == 10 ? 3 : g_tile;   // 10: auto without the 8-phase kernel (A/B)
   if (use_big_tile(tile_mode, M, N, K)) {
