@@ -261,4 +261,5 @@ def load_snapshot(shard: HbmIndexShard, directory: str, chunk: int = 1 << 20) ->
         for r, line in enumerate(f):
             a = json.loads(line)
             shard.payloads.set(r0 + r, a[0], Payload(*a[1:]))
+    shard.publish()
     return n

@@ -103,7 +103,11 @@ class HbmIndexShard:
         self.rows = torch.empty(_round_up(max(self.capacity, 1), TILE_ROWS), dim,
                                 dtype=torch.uint8 if dtype == "fp8" else torch.bfloat16,
                                 device=self.device)
-        self.count = 0
+        self.count = 0      # rows reserved (payload slots exist)
+        # rows searches may read: published only after their writes are ENQUEUED on the stream
+        # the scans share, so a search racing an upsert in another thread never scans a reserved
+        # but unwritten row (stream order then guarantees the write lands first)
+        self.visible = 0
         self.payloads = PayloadStore()
         self.scan_ns = 0     # LDS ring depth of the fused scan (0 = kernel default)
         self.scan_aux = -1   # index-stream cache policy (-1 = auto: non-temporal when read once)
@@ -135,6 +139,11 @@ class HbmIndexShard:
         for f in ps.FIELDS:
             del ps.cols[f][n:]
         self.count = n
+        self.visible = min(self.visible, n)
+
+    def publish(self) -> None:
+        """Make every reserved row searchable (call after its write is enqueued)."""
+        self.visible = self.count
 
     def append_unit(self, unit_bf16: torch.Tensor) -> int:
         """Append already unit-norm bf16 rows (e.g. the encoder's pooled+normalised output)."""
@@ -144,6 +153,7 @@ class HbmIndexShard:
             self._store(r0, unit_bf16.to(self.device), normalize=False)
         else:
             self.rows[r0:r0 + n].copy_(unit_bf16, non_blocking=True)
+        self.publish()
         return r0
 
     def _store(self, r0: int, x: torch.Tensor, normalize: bool) -> None:
@@ -173,6 +183,7 @@ class HbmIndexShard:
             raise ValueError(f"dimension mismatch: got {vecs.shape[1]}, index is {self.dim}")
         r0 = self._reserve(n)
         self.write_f32(r0, vecs)
+        self.publish()
         return r0
 
     def write_f32(self, r0: int, vecs: torch.Tensor) -> None:
@@ -197,6 +208,7 @@ class HbmIndexShard:
             row_of[point_ids[i]] = r
         for i in pos:
             self.payloads.set(row_of[point_ids[i]], point_ids[i], payloads[i])
+        self.publish()
         return [row_of[pid] for pid in point_ids]
 
     def fill_random(self, n: int, seed: int = 0, chunk: int = 1 << 20) -> None:
@@ -208,6 +220,7 @@ class HbmIndexShard:
             e = min(n, s + chunk)
             x = torch.randn(e - s, self.dim, generator=g, device=self.device, dtype=torch.float32)
             self._store(r0 + s, x, normalize=True)
+        self.publish()
 
     # ------------------------------------------------------------------ search
     def search(self, q_unit: torch.Tensor, k: int, n_cus: int | None = None):
@@ -227,7 +240,7 @@ class HbmIndexShard:
             from ..ops.kernels import quant_fp8
 
             q_unit = quant_fp8(q_unit, scale=FP8_SCALE)  # scores come back as S^2 * cosine
-        n = self.count
+        n = self.visible
         thr = None
         m = self._seed_rows(n, k)
         if m:
@@ -299,8 +312,9 @@ class HbmIndexShard:
         best_s = torch.full((NQ, k), -math.inf, device=self.device)
         best_i = torch.full((NQ, k), -1, dtype=torch.int64, device=self.device)
         q = q_unit.to(self.device).float()
-        for s in range(0, self.count, chunk):
-            e = min(self.count, s + chunk)
+        n = self.visible
+        for s in range(0, n, chunk):
+            e = min(n, s + chunk)
             sc = q @ self._rows_f32(s, e).t()
             kk = min(k, e - s)
             ts, ti = torch.topk(sc, kk, dim=1)

@@ -204,3 +204,21 @@ def test_search_result_fragments_match_wire_encoding_and_follow_overwrites():
     st.upsert(["a"], rng.standard_normal((1, 8)).astype(np.float32), [Payload("d1", "u1", "new", 0, "m", 9)])
     row_a = st.shard.payloads.id_to_row["a"]
     assert b'"sentence_text":"new"' in st.result_fragments(row_a)[1]
+
+
+def test_reserved_rows_stay_invisible_until_published():
+    """An upsert in another thread reserves rows before it writes them; a search racing it must
+    only scan rows whose writes were already enqueued (``visible``), never reserved garbage."""
+    sh = HbmIndexShard(8, 100, device="cpu")
+    v = _vecs(10, 8)
+    sh.append_f32(torch.from_numpy(v))
+    r0 = sh._reserve(5)                       # reserved, not yet written
+    sh.rows[r0:r0 + 5] = float("nan")
+    assert sh.count == 15 and sh.visible == 10
+    q = torch.nn.functional.normalize(torch.from_numpy(v[:3]), dim=-1).bfloat16()
+    s, r = sh.search(q, 12)
+    assert (r[:, 10:] == -1).all() and int(r.max()) < 10 and torch.isfinite(s[:, :10]).all()
+    sh.write_f32(r0, torch.from_numpy(_vecs(5, 8, 4)))
+    sh.publish()
+    s, r = sh.search(q, 15)
+    assert int(r.max()) == 14
