@@ -384,9 +384,49 @@ def cmd_attn(a):
         k: {"ms": round(m, 4), "TFLOPs": round(fl / (m / 1e3) / 1e12)} for k, (m, _) in res.items()}}))
 
 
+def cmd_prefilter(a):
+    """Exact bf16 scan vs fp8 prefilter + exact bf16 rescore on the SAME rows and queries:
+    time per search, recall@k of the prefilter against the exact scan, and whether every returned
+    score is the exact bf16 cosine.  --qmode random: isotropic queries; --qmode near: queries are
+    noisy copies of index rows (a real corpus: true neighbours well above the bulk)."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+
+    k = 10
+    sh = HbmIndexShard(a.dim, a.rows, device="cuda", prefilter="fp8")
+    sh.fill_random(a.rows, seed=3)
+    g = torch.Generator(device="cuda").manual_seed(4)
+    q = torch.randn(a.nq, a.dim, device="cuda", generator=g)
+    if a.qmode == "near":
+        idx = torch.randint(0, a.rows, (a.nq,), device="cuda", generator=g)
+        q = sh.rows[idx].float() + 0.6 * q / math.sqrt(a.dim)
+    q = torch.nn.functional.normalize(q, dim=-1).bfloat16()
+
+    def exact():
+        sh.prefilter = None
+        try:
+            return sh.search(q, k)
+        finally:
+            sh.prefilter = "fp8"
+
+    res = ab({"exact_bf16": exact, "prefilter_fp8": lambda: sh.search(q, k)}, rounds=a.rounds,
+             iters=a.iters)
+    es, ei = exact()
+    ps, pi = sh.search(q, k)
+    torch.cuda.synchronize()
+    hits = sum(len(set(pi[i].tolist()) & set(ei[i].tolist())) for i in range(a.nq))
+    true = torch.stack([(q[i].float() * sh.rows[pi[i].long()].float()).sum(-1) for i in range(a.nq)])
+    print(json.dumps({"bench": "prefilter", "rows": a.rows, "dim": a.dim, "nq": a.nq, "k": k,
+                      "qmode": a.qmode,
+                      "ms": {n: round(m, 3) for n, (m, _) in res.items()},
+                      "recall_at_k": round(hits / (a.nq * k), 5),
+                      "max_abs_score_err_vs_exact_recompute": float((ps - true).abs().max()),
+                      "top1_equal_frac": float((pi[:, 0] == ei[:, 0]).float().mean())}))
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("cmd", choices=["scan", "scanabl", "scanstamp", "scanfp8", "gemm", "encoder", "attn", "latency", "gemmfp8"])
+    ap.add_argument("cmd", choices=["scan", "scanabl", "scanstamp", "scanfp8", "gemm", "encoder", "attn", "latency", "gemmfp8", "prefilter"])
+    ap.add_argument("--qmode", choices=["random", "near"], default="random", help="prefilter: query kind")
     ap.add_argument("--rows", type=int, default=100_000_000)
     ap.add_argument("--dim", type=int, default=384)
     ap.add_argument("--nq", type=int, default=256)
@@ -401,7 +441,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=5)
     a = ap.parse_args()
-    {"scan": cmd_scan, "scanabl": cmd_scanabl, "scanstamp": cmd_scanstamp, "scanfp8": cmd_scanfp8, "gemm": cmd_gemm, "encoder": cmd_encoder, "attn": cmd_attn, "latency": cmd_latency, "gemmfp8": cmd_gemmfp8}[a.cmd](a)
+    {"scan": cmd_scan, "scanabl": cmd_scanabl, "scanstamp": cmd_scanstamp, "scanfp8": cmd_scanfp8, "gemm": cmd_gemm, "encoder": cmd_encoder, "attn": cmd_attn, "latency": cmd_latency, "gemmfp8": cmd_gemmfp8, "prefilter": cmd_prefilter}[a.cmd](a)
 
 
 if __name__ == "__main__":

@@ -257,6 +257,7 @@ def load_snapshot(shard: HbmIndexShard, directory: str, chunk: int = 1 << 20) ->
         else:
             t = torch.from_numpy(np.array(mm[s:e]).view(np.int16)).view(torch.bfloat16)
         shard.rows[r0 + s:r0 + e].copy_(t.to(shard.device))
+    shard.rows_written(r0, n)   # the fp8 prefilter image, if the shard keeps one
     with open(os.path.join(snap, "payloads.jsonl"), encoding="utf-8") as f:
         for r, line in enumerate(f):
             a = json.loads(line)

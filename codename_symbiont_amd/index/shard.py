@@ -83,17 +83,33 @@ class PayloadStore:
 
 
 FP8_SCALE = 256.0  # == ops.kernels.FP8_SCALE (kept import-free for CPU-only users)
+FP8_DIMS = (256, 384, 512, 768, 1024)   # row widths the fp8 scan kernel takes
 
 
 class HbmIndexShard:
     """``dtype="bf16"`` (default) or ``"fp8"``: OCP e4m3 rows of FP8_SCALE * x (half the HBM bytes
-    and twice the MFMA rate; BASELINE config #5).  Scores returned are cosines either way."""
+    and twice the MFMA rate; BASELINE config #5).  Scores returned are cosines either way.
 
-    def __init__(self, dim: int, capacity: int, device="cuda", kmax: int = 16, dtype: str = "bf16"):
+    ``prefilter="fp8"`` (bf16 shards only): the shard also keeps an e4m3 copy of every row and a
+    search scans THAT (half the bytes, twice the MFMA rate) for ``oversample * k`` candidates per
+    query, which are then re-scored exactly against the bf16 rows -- Qdrant's scalar quantization
+    with ``rescore`` + ``oversampling``.  Returned scores are the exact bf16 cosines; a true
+    neighbour is missed only if e4m3 rounding moves it below the candidate cut (recall measured in
+    tests/test_kernels_gpu.py and profiles/); the default (None) is the exact bf16 scan."""
+
+    def __init__(self, dim: int, capacity: int, device="cuda", kmax: int = 16, dtype: str = "bf16",
+                 prefilter: str | None = None, oversample: int = 3):
         if dtype not in ("bf16", "fp8"):
             raise ValueError(f"index dtype must be bf16 or fp8, got {dtype!r}")
-        if dtype == "fp8" and dim % 256:
-            raise ValueError("fp8 index rows must be a multiple of 256 wide (512/768/1024)")
+        if dtype == "fp8" and dim not in FP8_DIMS:
+            raise ValueError(f"fp8 index rows must be one of {FP8_DIMS} wide, got {dim}")
+        if prefilter not in (None, "", "fp8"):
+            raise ValueError(f"index prefilter must be fp8 or None, got {prefilter!r}")
+        prefilter = prefilter or None
+        if prefilter and (dtype != "bf16" or dim not in FP8_DIMS):
+            raise ValueError(f"an fp8 prefilter needs a bf16 shard of width {FP8_DIMS}")
+        self.prefilter = prefilter
+        self.oversample = int(oversample)
         self.dim = dim
         self.dtype = dtype
         self.device = torch.device(device)
@@ -103,6 +119,9 @@ class HbmIndexShard:
         self.rows = torch.empty(_round_up(max(self.capacity, 1), TILE_ROWS), dim,
                                 dtype=torch.uint8 if dtype == "fp8" else torch.bfloat16,
                                 device=self.device)
+        # e4m3 image of the bf16 rows for the prefilter scan (kept in step by every write)
+        self.rows8 = (torch.empty(self.rows.shape, dtype=torch.uint8, device=self.device)
+                      if prefilter else None)
         self.count = 0      # rows reserved (payload slots exist)
         # rows searches may read: published only after their writes are ENQUEUED on the stream
         # the scans share, so a search racing an upsert in another thread never scans a reserved
@@ -153,8 +172,22 @@ class HbmIndexShard:
             self._store(r0, unit_bf16.to(self.device), normalize=False)
         else:
             self.rows[r0:r0 + n].copy_(unit_bf16, non_blocking=True)
+            self.rows_written(r0, n)
         self.publish()
         return r0
+
+    def rows_written(self, r0: int, n: int) -> None:
+        """bf16 rows [r0, r0+n) changed: refresh their e4m3 prefilter image (no-op without one).
+        Callers that write ``rows`` directly (snapshot loads) must call this too."""
+        if self.rows8 is None or n <= 0:
+            return
+        src, dst = self.rows[r0:r0 + n], self.rows8[r0:r0 + n]
+        if self.device.type == "cuda":
+            from ..ops import kernels as K
+
+            K.quant_fp8(src, dst, FP8_SCALE, False)
+        else:
+            dst.copy_((src.float() * FP8_SCALE).to(torch.float8_e4m3fn).view(torch.uint8))
 
     def _store(self, r0: int, x: torch.Tensor, normalize: bool) -> None:
         """Write rows (f32 or bf16 on self.device) at r0, unit-normalising them if asked."""
@@ -169,12 +202,13 @@ class HbmIndexShard:
                 K.l2norm_cast(x.float().contiguous(), dst)
             else:
                 dst.copy_(x)
-            return
-        y = torch.nn.functional.normalize(x.float(), dim=-1) if normalize else x.float()
-        if self.dtype == "fp8":
-            dst.copy_((y * FP8_SCALE).to(torch.float8_e4m3fn).view(torch.uint8))
         else:
-            dst.copy_(y.bfloat16())
+            y = torch.nn.functional.normalize(x.float(), dim=-1) if normalize else x.float()
+            if self.dtype == "fp8":
+                dst.copy_((y * FP8_SCALE).to(torch.float8_e4m3fn).view(torch.uint8))
+            else:
+                dst.copy_(y.bfloat16())
+        self.rows_written(r0, n)
 
     def append_f32(self, vecs: torch.Tensor) -> int:
         """Append raw float vectors (wire embeddings); normalised + cast by the l2norm_cast kernel."""
@@ -235,8 +269,17 @@ class HbmIndexShard:
         if self.device.type != "cuda" or k > 32:
             return self._search_matmul(q_unit, k)
         q_unit = q_unit.to(torch.bfloat16).contiguous()
-        kmax = 16 if k <= 16 else 32
+        if self.prefilter and k < 32:
+            return self._search_prefilter(q_unit, k, n_cus)
+        out_s, out_i = self._search_scan(q_unit, k, self.rows, self.dtype, n_cus)
         if self.dtype == "fp8":
+            out_s.mul_(1.0 / (FP8_SCALE * FP8_SCALE))
+        return out_s, out_i
+
+    def _search_scan(self, q_unit, k: int, rows, dtype: str, n_cus):
+        """Seeded fused scan + merge over ``rows`` (bf16 slab, or e4m3 bytes for dtype fp8)."""
+        kmax = 16 if k <= 16 else 32
+        if dtype == "fp8":
             from ..ops.kernels import quant_fp8
 
             q_unit = quant_fp8(q_unit, scale=FP8_SCALE)  # scores come back as S^2 * cosine
@@ -246,15 +289,24 @@ class HbmIndexShard:
         if m:
             # threshold seeding: the k-th best score over the first m rows lower-bounds the final
             # k-th score, so the full scan may drop anything below it (exact; see the kernel note)
-            pre_s, _ = self._scan(m, q_unit, kmax, k, None, n_cus)
+            pre_s, _ = self._scan(m, q_unit, kmax, k, None, n_cus, rows, dtype)
             kth = pre_s[:, k - 1].contiguous()
             # (full_like, not torch.tensor(-inf, device=...): a pageable H2D copy would block the
             # host on the stream every search and leave the GPU idle while the scan is enqueued)
             thr = torch.nextafter(kth, torch.full_like(kth, -math.inf))
-        out_s, out_i = self._scan(n, q_unit, kmax, k, thr, n_cus)
-        if self.dtype == "fp8":
-            out_s.mul_(1.0 / (FP8_SCALE * FP8_SCALE))
-        return out_s, out_i
+        return self._scan(n, q_unit, kmax, k, thr, n_cus, rows, dtype)
+
+    def _search_prefilter(self, q_unit, k: int, n_cus):
+        """fp8 scan for oversample*k candidates, exact bf16 re-score, top-k (see the class doc)."""
+        kc = min(32, max(16, self.oversample * k))
+        _, cand = self._search_scan(q_unit, kc, self.rows8, "fp8", n_cus)    # [NQ, kc] rows
+        valid = cand >= 0
+        rows = self.rows[cand.clamp_min(0).long()]                           # [NQ, kc, D] bf16
+        exact = torch.bmm(rows.float(), q_unit.float().unsqueeze(-1)).squeeze(-1)
+        exact = torch.where(valid, exact, torch.full_like(exact, -math.inf))
+        top_s, j = torch.topk(exact, k, dim=1)
+        top_i = torch.gather(cand, 1, j)
+        return top_s, torch.where(torch.isfinite(top_s), top_i, torch.full_like(top_i, -1))
 
     SEED_DIV = 64            # sample = first n/64 rows (~1.6% extra scan work)
     SEED_MIN_ROWS = 1 << 20  # below this the record-breaking inserts are cheap anyway
@@ -270,11 +322,14 @@ class HbmIndexShard:
             n = self._cus = torch.cuda.get_device_properties(self.device).multi_processor_count
         return n
 
-    def _scan(self, n: int, q_unit: torch.Tensor, kmax: int, k: int, thr, n_cus):
+    def _scan(self, n: int, q_unit: torch.Tensor, kmax: int, k: int, thr, n_cus, rows=None,
+              dtype=None):
         from ..ops._ext import hip, stream_handle
 
+        rows = self.rows if rows is None else rows
+        dtype = dtype or self.dtype
         NQ = q_unit.shape[0]
-        if self.dtype == "fp8":
+        if dtype == "fp8":
             lists, qpb = 2, 256
         else:
             lists, qpb = hip().topk_geometry(self.dim, kmax)
@@ -294,12 +349,12 @@ class HbmIndexShard:
         st = stream_handle(self.device)
         h = hip()
         thr_p = 0 if thr is None else thr.data_ptr()
-        if self.dtype == "fp8":
-            h.index_scan_fp8(self.rows.data_ptr(), n, self.dim, rows_per_blk, n_rblk,
+        if dtype == "fp8":
+            h.index_scan_fp8(rows.data_ptr(), n, self.dim, rows_per_blk, n_rblk,
                              q_unit.data_ptr(), NQ, kmax, cs.data_ptr(), ci.data_ptr(), st,
                              self.scan_aux, thr_p, self.scan_variant, self.scan_xcd)
         else:
-            h.index_scan(self.rows.data_ptr(), n, self.dim, rows_per_blk, n_rblk, q_unit.data_ptr(),
+            h.index_scan(rows.data_ptr(), n, self.dim, rows_per_blk, n_rblk, q_unit.data_ptr(),
                          NQ, kmax, cs.data_ptr(), ci.data_ptr(), st, self.scan_ns, self.scan_aux,
                          thr_p, self.scan_xcd)
         h.topk_merge(cs.data_ptr(), ci.data_ptr(), NQ, ncand, kmax, k, out_s.data_ptr(),

@@ -39,7 +39,8 @@ class VectorMemoryService(Service):
         self.store = store or VectorStore(dim, self.cfg.index_capacity,
                                           device="cpu" if self.cfg.force_cpu else None,
                                           snapshot_dir=self.cfg.snapshot_dir,
-                                          dtype=self.cfg.index_dtype)
+                                          dtype=self.cfg.index_dtype,
+                                          prefilter=self.cfg.index_prefilter or None)
         if self.cfg.index_fill_random and self.store.count == 0:
             self.store.shard.fill_random(self.cfg.index_fill_random, seed=17)
         self.log.info("[INDEX_SETUP] collection '%s': dim %d, capacity %d, device %s, %d points",
@@ -262,7 +263,8 @@ def main() -> None:
     cfg = Config()
     info = D.init()
     dim = cfg.index_dim or get_config(cfg.model).hidden
-    group = IndexGroup(info, dim, cfg.index_capacity // info.world + 1, dtype=cfg.index_dtype)
+    group = IndexGroup(info, dim, cfg.index_capacity // info.world + 1, dtype=cfg.index_dtype,
+                       prefilter=cfg.index_prefilter or None)
     group.snapshot_root = cfg.snapshot_dir or None
     # liveness: every rank heart-beats on health.index.<rank>; rank 0 refuses ops while a peer is
     # silent (fast error replies instead of a collective blocked until the RCCL timeout)

@@ -65,6 +65,9 @@ class Config:
     encoder_dtype: str = field(default_factory=lambda: os.environ.get("SYMB_ENCODER_DTYPE", "bf16"))
     # "bf16" (default) or "fp8" (OCP e4m3 rows; needs a dim that is a multiple of 256)
     index_dtype: str = field(default_factory=lambda: os.environ.get("SYMB_INDEX_DTYPE", "bf16"))
+    # "fp8": bf16 index searched through an e4m3 prefilter + exact bf16 re-score (Qdrant's
+    # quantization + rescore); "" = exact bf16 scan
+    index_prefilter: str = field(default_factory=lambda: os.environ.get("SYMB_INDEX_PREFILTER", ""))
     snapshot_dir: str = field(default_factory=lambda: _env("SYMB_SNAPSHOT_DIR", ""))
     collection: str = "symbiont_document_embeddings"
     embed_timeout_s: float = field(default_factory=lambda: _float("SYMB_EMBED_TIMEOUT_S", 15.0))

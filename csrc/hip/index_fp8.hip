@@ -77,18 +77,31 @@ __device__ __forceinline__ void lgkm_wait2(i32x4& a, i32x4& b) {
   asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "i"(N));
 }
 
+// LDS image swizzle: within each group of G 16-byte chunks of a row, chunk c is stored at
+// c ^ f(row).  G = 16, f = row & 15 for rows of 512 / 768 / 1024 bytes (a multiple of 256 B);
+// D = 384 (24 chunks, rows 96 dwords ~ 32 mod 64 banks) uses G = 8, f = (row >> 1) & 7, which
+// keeps every 16-lane ds_read_b128 group of a 32-row fragment conflict-free (rows 2i and 2i+1
+// sit in opposite 128-byte halves of the bank row, and f separates the pairs).
+template <int D> struct Fp8Swz {
+  static constexpr int G = D % 256 == 0 ? 16 : 8;
+  __device__ __forceinline__ static int f(int row) { return G == 16 ? (row & 15) : ((row >> 1) & 7); }
+  __device__ __forceinline__ static int phys(int c, int row) { return (c & ~(G - 1)) | ((c & (G - 1)) ^ f(row)); }
+};
+
 // fragment ks of a sub-tile: row r = lane & 31 holds bytes [64 ks + 32 h, +32), h = lane >> 5,
-// i.e. 16-byte chunks c = 4 ks + 2 h + j (j = 0, 1), stored at chunk c ^ (r & 15): the per-lane
-// part repeats every 4 k-steps (voff[ks & 3][j]) and the rest is the immediate (ks >> 2) * 256.
-template <int J, int PF, int R>
+// i.e. 16-byte chunks c = 4 ks + 2 h + j (j = 0, 1), stored at Fp8Swz::phys(c, r): the per-lane
+// part repeats every P = G / 4 k-steps (voff[ks % P][j]) and the rest is the immediate
+// (ks / P) * 16 G bytes.
+template <int J, int PF, int R, int G>
 __device__ __forceinline__ void fp8_prologue(i32x4 (&lo)[R], i32x4 (&hi)[R],
                                              const uint32_t (&voff)[8], uint32_t base) {
-  ds_read16_i<(J >> 2) * 256>(lo[J % R], base + voff[(J & 3) * 2]);
-  ds_read16_i<(J >> 2) * 256>(hi[J % R], base + voff[(J & 3) * 2 + 1]);
-  if constexpr (J + 1 < PF) fp8_prologue<J + 1, PF, R>(lo, hi, voff, base);
+  constexpr int P = G / 4;
+  ds_read16_i<(J / P) * 16 * G>(lo[J % R], base + voff[(J % P) * 2]);
+  ds_read16_i<(J / P) * 16 * G>(hi[J % R], base + voff[(J % P) * 2 + 1]);
+  if constexpr (J + 1 < PF) fp8_prologue<J + 1, PF, R, G>(lo, hi, voff, base);
 }
 
-template <int KS, int NKS, int PF, int DMA_PIECES>
+template <int KS, int NKS, int PF, int DMA_PIECES, int G>
 struct Fp8Chain {
   static constexpr int R = PF + 1;
   template <class Dma>
@@ -110,12 +123,12 @@ struct Fp8Chain {
     if constexpr (KS + 1 == NKS)  // XDL write -> VALU read of the accumulators (16-pass: 19 states)
       asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
     if constexpr (KS + PF < NKS) {
-      constexpr int J = KS + PF;
-      ds_read16_i<(J >> 2) * 256>(lo[J % R], base + voff[(J & 3) * 2]);
-      ds_read16_i<(J >> 2) * 256>(hi[J % R], base + voff[(J & 3) * 2 + 1]);
+      constexpr int J = KS + PF, P = G / 4;
+      ds_read16_i<(J / P) * 16 * G>(lo[J % R], base + voff[(J % P) * 2]);
+      ds_read16_i<(J / P) * 16 * G>(hi[J % R], base + voff[(J % P) * 2 + 1]);
     }
     if constexpr (KS + 1 < NKS)
-      Fp8Chain<KS + 1, NKS, PF, DMA_PIECES>::run(acc0, acc1, lo, hi, q0, q1, voff, base, dma);
+      Fp8Chain<KS + 1, NKS, PF, DMA_PIECES, G>::run(acc0, acc1, lo, hi, q0, q1, voff, base, dma);
   }
 };
 
@@ -128,7 +141,9 @@ __global__ __launch_bounds__(256, 1) void index_scan_fp8_kernel(
   constexpr int TILE_BYTES = TR * D, SUB_BYTES = SUB * D;
   constexpr int LOADS = TILE_BYTES / (1024 * NW);  // DMA pieces per wave per tile
   constexpr int NKS = D / 64, PF = 4, R = PF + 1;
-  static_assert(D % 256 == 0 && TILE_BYTES % (1024 * NW) == 0, "fp8 scan geometry");
+  static_assert((D % 256 == 0 || D == 384) && TILE_BYTES % (1024 * NW) == 0, "fp8 scan geometry");
+  using Swz = Fp8Swz<D>;
+  constexpr int G = Swz::G;
   static_assert(NS >= 2 && NS * TILE_BYTES <= 160 * 1024, "LDS ring exceeds the CU's 160 KiB");
   static_assert(LOADS <= NKS, "DMA pieces must fit the first chain");
 
@@ -158,7 +173,7 @@ __global__ __launch_bounds__(256, 1) void index_scan_fp8_kernel(
   for (int i = 0; i < LOADS; ++i) {
     const int s = (i * NW + wave) * 64 + lane;  // 16-byte LDS slot this lane fills
     const int row = s / CPR, pc = s % CPR;
-    goff[i] = (uint32_t)(row * D + (((pc & ~15) | ((pc & 15) ^ (row & 15))) << 4));
+    goff[i] = (uint32_t)(row * D + (Swz::phys(pc, row) << 4));   // the swizzle is an involution
   }
   auto issue_piece = [&](int t, int i) {
     const int tt = min(t, n_tiles - 1);  // past the end: re-load the last tile (keeps vmcnt exact)
@@ -171,10 +186,10 @@ __global__ __launch_bounds__(256, 1) void index_scan_fp8_kernel(
   {
     const int r = lane & 31;
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
+    for (int m = 0; m < G / 4; ++m)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        voff[m * 2 + j] = (uint32_t)(r * D + (((4 * m + 2 * h + j) ^ (r & 15)) << 4));
+        voff[m * 2 + j] = (uint32_t)(r * D + (Swz::phys(4 * m + 2 * h + j, r) << 4));
   }
 
   float tv0[KMAX], tv1[KMAX];
@@ -226,13 +241,13 @@ __global__ __launch_bounds__(256, 1) void index_scan_fp8_kernel(
       const uint32_t base = tbase + sub * SUB_BYTES;
       f32x16 acc0, acc1;
       if (sub == 0) {
-        fp8_prologue<0, PF, R>(lo, hi, voff, base);
-        Fp8Chain<0, NKS, PF, LOADS>::run(acc0, acc1, lo, hi, q0, q1, voff, base, dma);
+        fp8_prologue<0, PF, R, G>(lo, hi, voff, base);
+        Fp8Chain<0, NKS, PF, LOADS, G>::run(acc0, acc1, lo, hi, q0, q1, voff, base, dma);
       } else {
-        Fp8Chain<0, NKS, PF, 0>::run(acc0, acc1, lo, hi, q0, q1, voff, base, NoDma());
+        Fp8Chain<0, NKS, PF, 0, G>::run(acc0, acc1, lo, hi, q0, q1, voff, base, NoDma());
       }
       if (sub + 1 < SUBS)  // next sub-tile's first fragments fly during this top-k
-        fp8_prologue<0, PF, R>(lo, hi, voff, base + SUB_BYTES);
+        fp8_prologue<0, PF, R, G>(lo, hi, voff, base + SUB_BYTES);
       update(acc0, tv0, ti0, thr0, row0 + sub * SUB);
       update(acc1, tv1, ti1, thr1, row0 + sub * SUB);
     }
@@ -297,6 +312,8 @@ template <int D> struct Fp8Cfg;
 template <> struct Fp8Cfg<1024> { static constexpr int SUBS = 2, NS = 2; };  // 2 x 64 KiB
 template <> struct Fp8Cfg<768> { static constexpr int SUBS = 1, NS = 6; };   // 6 x 24 KiB
 template <> struct Fp8Cfg<512> { static constexpr int SUBS = 2, NS = 4; };   // 4 x 32 KiB
+template <> struct Fp8Cfg<384> { static constexpr int SUBS = 2, NS = 5; };   // 5 x 24 KiB
+template <> struct Fp8Cfg<256> { static constexpr int SUBS = 2, NS = 6; };   // 6 x 16 KiB
 
 template <int D>
 static int dispatch_fp8(int kmax, int aux, int variant, const void* X, int n_valid,
@@ -326,6 +343,8 @@ int symb_index_scan_fp8(const void* X, int n_valid, int D, int rows_per_blk, int
 #define SYMB_ARGS kmax, aux, variant, X, n_valid, rows_per_blk, n_rblk, Q, NQ, n_qblk, xcd, thr_init, \
                   cand_s, cand_i, st
   switch (D) {
+    case 256: return dispatch_fp8<256>(SYMB_ARGS);
+    case 384: return dispatch_fp8<384>(SYMB_ARGS);
     case 512: return dispatch_fp8<512>(SYMB_ARGS);
     case 768: return dispatch_fp8<768>(SYMB_ARGS);
     case 1024: return dispatch_fp8<1024>(SYMB_ARGS);

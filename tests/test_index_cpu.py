@@ -148,8 +148,8 @@ def test_fp8_shard_cpu_path_and_snapshot(tmp_path):
     assert torch.equal(sh2.rows[:500], sh.rows[:500])
     with pytest.raises(ValueError, match="dtype"):
         load_snapshot(HbmIndexShard(D, 600, device="cpu"), str(tmp_path))
-    with pytest.raises(ValueError, match="multiple of 256"):
-        HbmIndexShard(384, 10, device="cpu", dtype="fp8")
+    with pytest.raises(ValueError, match="fp8 index rows"):
+        HbmIndexShard(320, 10, device="cpu", dtype="fp8")
 
 
 def test_stage_tracing_records_metrics(caplog):
@@ -222,3 +222,24 @@ def test_reserved_rows_stay_invisible_until_published():
     sh.publish()
     s, r = sh.search(q, 15)
     assert int(r.max()) == 14
+
+
+def test_prefilter_image_follows_every_write(tmp_path):
+    """The e4m3 prefilter image tracks appends, overwrites and snapshot loads (CPU path)."""
+    from codename_symbiont_amd.index.persist import load_snapshot, save_snapshot
+
+    D = 384
+    sh = HbmIndexShard(D, 64, device="cpu", prefilter="fp8")
+    st = VectorStore(D, 64, device="cpu", prefilter="fp8")
+    v = _vecs(20, D, 5)
+    st.upsert([f"p{i}" for i in range(20)], v, [Payload() for _ in range(20)])
+    st.upsert(["p3"], -v[3:4], [Payload()])
+    dec = lambda s: s.rows8[:s.count].view(torch.float8_e4m3fn).float() / 256.0  # noqa: E731
+    assert torch.allclose(dec(st.shard), st.shard.rows[:20].float(), atol=0.01)
+    sh.append_unit(st.shard.rows[:20])
+    save_snapshot(sh, str(tmp_path))
+    sh2 = HbmIndexShard(D, 64, device="cpu", prefilter="fp8")
+    load_snapshot(sh2, str(tmp_path))
+    assert torch.equal(sh2.rows8[:20], st.shard.rows8[:20])
+    with pytest.raises(ValueError, match="prefilter"):
+        HbmIndexShard(D, 8, device="cpu", dtype="fp8", prefilter="fp8")

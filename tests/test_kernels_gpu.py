@@ -245,6 +245,32 @@ def test_concurrent_searches_match_sequential(dtype):
             assert torch.equal(r, seq[t][1]) and torch.equal(s, seq[t][0]), t
 
 
+@pytest.mark.parametrize("D,nq", [(384, 300), (768, 64)])
+def test_prefilter_fp8_rescored_search(D, nq):
+    """bf16 index searched through its e4m3 image (3k candidates) and re-scored in bf16: every
+    returned score is the exact bf16 cosine of the returned row, and recall@10 vs the exact scan
+    is ~1 (a miss needs e4m3 rounding to push a true top-10 row below the 30th candidate)."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+
+    n, k = (1 << 20) + 333, 10
+    exact = HbmIndexShard(D, n + 300)
+    pre = HbmIndexShard(D, n + 300, prefilter="fp8")
+    for sh in (exact, pre):
+        sh.fill_random(n, seed=31)
+    q = torch.nn.functional.normalize(_f(nq, D, seed=32), dim=-1).bfloat16()
+    pre.append_unit(q[:5])          # a few queries are their own nearest neighbour
+    exact.append_unit(q[:5])
+    es, ei = exact.search(q, k)
+    ps, pi = pre.search(q, k)
+    torch.cuda.synchronize()
+    assert torch.equal(pre.rows[:pre.count], exact.rows[:exact.count])
+    assert pi[:5, 0].tolist() == list(range(n, n + 5))
+    true = (q.float() @ pre.unit_rows().float().t()).gather(1, pi.long())
+    _close(ps, true, atol=1e-4, what="rescored scores")
+    hits = sum(len(set(pi[i].tolist()) & set(ei[i].tolist())) for i in range(nq))
+    assert hits / (nq * k) >= 0.998, hits / (nq * k)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("D", [384, 768])
 def test_index_scan_seeded_threshold_is_exact(D):
@@ -309,7 +335,9 @@ def test_quant_fp8_matches_torch_e4m3(src):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("D,k,n,nq", [(1024, 10, 20_011, 300), (768, 5, 9000, 70),
-                                      (512, 20, 7777, 33), (1024, 16, 64, 256)])
+                                      (512, 20, 7777, 33), (1024, 16, 64, 256),
+                                      (384, 10, 30_001, 300), (384, 32, 5000, 17),
+                                      (256, 10, 9000, 100)])
 def test_index_scan_fp8_exact_on_decoded_rows(D, k, n, nq):
     """fp8 scan == fp32 top-k over the DECODED e4m3 rows and queries (the MFMA sums exact e4m3
     products in fp32), and ranks like the bf16 cosine up to e4m3 rounding."""
