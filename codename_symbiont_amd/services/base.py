@@ -180,7 +180,8 @@ class Service:
             await asyncio.sleep(interval)
             try:
                 await self.nc.publish(f"metrics.{self.name}", json.dumps(
-                    {"service": self.name, "ts_ms": int(time.time() * 1000), **self.metrics.snapshot()}
+                    {"service": self.name, "replica": os.environ.get("SYMB_REPLICA", ""),
+                     "ts_ms": int(time.time() * 1000), **self.metrics.snapshot()}
                 ).encode())
             except Exception:
                 pass

@@ -155,3 +155,54 @@ def test_env_file_compose_semantics(tmp_path, monkeypatch):
     assert kid.env["API_SERVER_PORT"] == "7070"
     a.api_port = 9999                                          # the flag wins over both
     assert build_children(a)[0].env["API_SERVER_PORT"] == "9999"
+
+
+def test_supervisor_health_checks_restart_stuck_children():
+    """Compose-style healthchecks: a child that is alive but stuck (SIGSTOP) stops reporting
+    metrics.<service> / answering /api/health; the supervisor kills and restarts it."""
+    bport, aport = _port(), _port()
+    env = dict(os.environ, SYMB_LOG="warning", SYMB_FORCE_CPU="1", API_SERVER_HOST="127.0.0.1",
+               NATS_URL=f"nats://127.0.0.1:{bport}", SYMB_API_WORKERS="1")
+    sup = subprocess.Popen([sys.executable, "-m", "codename_symbiont_amd.launch", "--only",
+                            "text_generator,api", "--broker-port", str(bport), "--api-port",
+                            str(aport), "--health-interval", "1", "--health-retries", "2",
+                            "--health-grace", "4"], cwd=ROOT, env=env, stderr=subprocess.PIPE,
+                           text=True, start_new_session=True)
+    log: list[str] = []
+    threading.Thread(target=lambda: [log.append(ln) for ln in sup.stderr], daemon=True).start()
+
+    def pids() -> dict:
+        out = {}
+        for ln in list(log):
+            m = re.search(r"\[launch\] started (\S+) pid=(\d+)", ln)
+            if m:
+                out[m.group(1)] = int(m.group(2))
+        return out
+
+    url = f"http://127.0.0.1:{aport}"
+    try:
+        t0 = time.time()
+        while True:
+            try:
+                if httpx.get(url + "/api/health", timeout=2).status_code == 200:
+                    break
+            except httpx.HTTPError:
+                pass
+            assert time.time() - t0 < 90, "services did not come up:\n" + "".join(log[-20:])
+            time.sleep(0.3)
+        time.sleep(6)                       # past the grace: healthy children are left alone
+        assert not any("unhealthy" in ln for ln in log), "".join(log[-20:])
+        for name in ("text_generator", "api"):
+            old = pids()[name]
+            os.killpg(old, signal.SIGSTOP)  # alive but stuck
+            t0 = time.time()
+            while pids()[name] == old:
+                assert time.time() - t0 < 45, f"{name} not restarted:\n" + "".join(log[-20:])
+                time.sleep(0.2)
+            assert any(f"{name} unhealthy" in ln for ln in log)
+            assert not _alive(old) or open(f"/proc/{old}/stat").read().split()[2] == "Z"
+        ev = _generate_retry(url, "health")      # the restarted pair serves again
+        assert ev["generated_text"].split()[0] == "я"
+    finally:
+        os.killpg(sup.pid, signal.SIGTERM)
+        sup.wait(30)
