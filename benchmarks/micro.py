@@ -91,6 +91,40 @@ def cmd_scan(a):
     print(json.dumps({"bench": "scan", "rows": a.rows, "dim": D, "nq": a.nq, "results": out}))
 
 
+def cmd_scanmq(a):
+    """512-query-per-workgroup emitting scan (index_mq.hip) vs the 256-query list kernel on the
+    per-rank shape of the sharded search (rows/N x 256*N queries), seeded top-10 searches."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+
+    D, k = 384, 10
+    shard = HbmIndexShard(D, a.rows + 8192, device="cuda")
+    shard.fill_random(a.rows, seed=1)
+    q = torch.nn.functional.normalize(torch.randn(a.nq, D, device="cuda"), dim=-1).bfloat16()
+    if a.qmode == "near":   # bench-like: fresh embeddings appended last, queries near them
+        near = torch.nn.functional.normalize(q.float() + 0.05 * torch.randn_like(q.float()), dim=-1)
+        shard.append_unit(near.bfloat16())
+
+    def srch(mq):
+        shard.scan_mq = mq
+        return shard.search(q, k)
+
+    ref = srch(False)
+    got = srch(True)
+    torch.cuda.synchronize()
+    cnt, ovf = shard._mq_last
+    ids_equal = float((ref[1] == got[1]).float().mean())
+    max_score_diff = float((ref[0] - got[0]).abs().max())
+    r = ab({"list256": lambda: srch(False), "mq512": lambda: srch(True)}, rounds=a.rounds,
+           iters=a.iters)
+    flop = 2 * shard.visible * D * a.nq
+    out = {n: dict(ms=round(m, 3), min_ms=round(mn, 3), TFLOPs=round(flop / (m / 1e3) / 1e12))
+           for n, (m, mn) in r.items()}
+    print(json.dumps({"bench": "scanmq", "rows": shard.visible, "nq": a.nq, "qmode": a.qmode,
+                      "ids_equal_frac": ids_equal, "max_score_diff": max_score_diff,
+                      "overflow": int(ovf.item()), "cand_mean": float(cnt.float().mean()),
+                      "cand_max": int(cnt.max()), "results": out}))
+
+
 def cmd_scanabl(a):
     """DMA-only vs compute-only vs full scan (D=384), plus a plain torch streaming read."""
     from codename_symbiont_amd.index.shard import HbmIndexShard, _round_up
@@ -425,7 +459,7 @@ def cmd_prefilter(a):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("cmd", choices=["scan", "scanabl", "scanstamp", "scanfp8", "gemm", "encoder", "attn", "latency", "gemmfp8", "prefilter"])
+    ap.add_argument("cmd", choices=["scan", "scanmq", "scanabl", "scanstamp", "scanfp8", "gemm", "encoder", "attn", "latency", "gemmfp8", "prefilter"])
     ap.add_argument("--qmode", choices=["random", "near"], default="random", help="prefilter: query kind")
     ap.add_argument("--rows", type=int, default=100_000_000)
     ap.add_argument("--dim", type=int, default=384)
@@ -441,7 +475,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=5)
     a = ap.parse_args()
-    {"scan": cmd_scan, "scanabl": cmd_scanabl, "scanstamp": cmd_scanstamp, "scanfp8": cmd_scanfp8, "gemm": cmd_gemm, "encoder": cmd_encoder, "attn": cmd_attn, "latency": cmd_latency, "gemmfp8": cmd_gemmfp8, "prefilter": cmd_prefilter}[a.cmd](a)
+    {"scan": cmd_scan, "scanmq": cmd_scanmq, "scanabl": cmd_scanabl, "scanstamp": cmd_scanstamp, "scanfp8": cmd_scanfp8, "gemm": cmd_gemm, "encoder": cmd_encoder, "attn": cmd_attn, "latency": cmd_latency, "gemmfp8": cmd_gemmfp8, "prefilter": cmd_prefilter}[a.cmd](a)
 
 
 if __name__ == "__main__":

@@ -135,6 +135,9 @@ class HbmIndexShard:
         # > 256 queries: put the query blocks of each row block on one XCD (row stream shared
         # through that XCD's L2 instead of re-read from HBM once per query block)
         self.scan_xcd = 1
+        # >= 512 seeded queries on a 384-wide bf16 shard (the per-rank shape of the sharded search
+        # at N >= 2 GPUs): the 512-query-per-workgroup candidate-emitting kernel (index_mq.hip)
+        self.scan_mq = True
 
     # ------------------------------------------------------------------ inserts
     def _reserve(self, n: int) -> int:
@@ -286,6 +289,17 @@ class HbmIndexShard:
         n = self.visible
         thr = None
         m = self._seed_rows(n, k)
+        mq = m and self._mq_ok(q_unit.shape[0], k, rows, dtype)
+        if m and mq:
+            # the emitting kernel keeps EVERY row above the threshold, so it needs a threshold
+            # near the true k-th score for any row order: one pseudo-random row per 64-row block
+            # (no row twice, so the sample's k-th best is a lower bound), not the first n/64 rows
+            # (rows appended last, e.g. fresh embeddings, are often the best matches).  The margin
+            # covers the two kernels' different fp32 summation orders (16x16x32 vs 32x32x16).
+            ms, sample = self._block_sample(n)
+            pre_s, _ = self._scan(ms, q_unit, kmax, k, None, n_cus, sample, dtype)
+            thr = pre_s[:, k - 1].contiguous() - self.MQ_THR_MARGIN
+            return self._scan_mq(n, q_unit, kmax, k, thr, n_cus)
         if m:
             # threshold seeding: the k-th best score over the first m rows lower-bounds the final
             # k-th score, so the full scan may drop anything below it (exact; see the kernel note)
@@ -295,6 +309,57 @@ class HbmIndexShard:
             # host on the stream every search and leave the GPU idle while the scan is enqueued)
             thr = torch.nextafter(kth, torch.full_like(kth, -math.inf))
         return self._scan(n, q_unit, kmax, k, thr, n_cus, rows, dtype)
+
+    MQ_CAP = 4096             # candidate slots per query (expected use ~64 k)
+    MQ_THR_MARGIN = 2.0 ** -12
+
+    def _mq_ok(self, NQ: int, k: int, rows, dtype: str) -> bool:
+        return (self.scan_mq and dtype == "bf16" and self.dim == 384 and rows is self.rows
+                and NQ >= 512 and k <= 16)
+
+    def _block_sample(self, n: int):
+        """Row sample for threshold seeding: row 64 i + h(i) of every full 64-row block i (h a
+        fixed hash into [0, 64)), gathered into a tile-padded buffer."""
+        m = n // self.SEED_DIV
+        cached = getattr(self, "_sample_idx", None)
+        if cached is None or cached[0] != m:
+            i = torch.arange(m, device=self.device, dtype=torch.int64)
+            self._sample_idx = (m, i * self.SEED_DIV + (((i * 0x9E3779B1) & 0xFFFFFFFF) >> 26))
+        buf = torch.empty(_round_up(m, TILE_ROWS), self.dim, dtype=self.rows.dtype,
+                          device=self.device)
+        torch.index_select(self.rows, 0, self._sample_idx[1], out=buf[:m])
+        return m, buf
+
+    def _scan_mq(self, n: int, q_unit: torch.Tensor, kmax: int, k: int, thr, n_cus):
+        """512-query-per-workgroup scan emitting every score above ``thr`` (index_mq.hip), top-k
+        of each query's candidates, and the exact 256-query kernel as a fallback that runs on the
+        GPU only if some query's candidate buffer overflowed (a device flag gates it)."""
+        from ..ops._ext import hip, stream_handle
+
+        h = hip()
+        NQ = q_unit.shape[0]
+        n_qblk = math.ceil(NQ / h.mq_queries_per_blk())
+        if n_cus is None:
+            n_cus = self._n_cus()
+        n_rblk = max(1, min(math.ceil(n / (TILE_ROWS * 16)), max(1, round(n_cus / n_qblk))))
+        rows_per_blk = _round_up(max(1, math.ceil(n / n_rblk)), TILE_ROWS)
+        n_rblk = max(1, math.ceil(n / rows_per_blk))
+        cap, dev = self.MQ_CAP, self.device
+        cs = torch.empty(NQ, cap, device=dev)
+        ci = torch.empty(NQ, cap, dtype=torch.int32, device=dev)
+        cnt = torch.empty(NQ, dtype=torch.int32, device=dev)
+        ovf = torch.empty(1, dtype=torch.int32, device=dev)
+        out_s = torch.empty(NQ, k, device=dev)
+        out_i = torch.empty(NQ, k, dtype=torch.int32, device=dev)
+        st = stream_handle(dev)
+        h.index_scan_mq(self.rows.data_ptr(), n, rows_per_blk, n_rblk, q_unit.data_ptr(), NQ,
+                        thr.data_ptr(), cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(), cap,
+                        self.scan_xcd, st)
+        h.topk_select_counted(cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(), cap, NQ, kmax, k,
+                              out_s.data_ptr(), out_i.data_ptr(), ovf.data_ptr(), st)
+        self._scan(n, q_unit, kmax, k, thr, n_cus, gate=ovf, out=(out_s, out_i))
+        self._mq_last = (cnt, ovf)   # candidate counts / overflow flag (tests, diagnostics)
+        return out_s, out_i
 
     def _search_prefilter(self, q_unit, k: int, n_cus):
         """fp8 scan for oversample*k candidates, exact bf16 re-score, top-k (see the class doc)."""
@@ -323,7 +388,9 @@ class HbmIndexShard:
         return n
 
     def _scan(self, n: int, q_unit: torch.Tensor, kmax: int, k: int, thr, n_cus, rows=None,
-              dtype=None):
+              dtype=None, gate=None, out=None):
+        """Fused 256-query scan + merge.  ``gate`` (int32 device flag): the kernels skip
+        themselves unless it is non-zero; ``out``: (scores, rows) tensors to write."""
         from ..ops._ext import hip, stream_handle
 
         rows = self.rows if rows is None else rows
@@ -344,8 +411,11 @@ class HbmIndexShard:
         # stream) must never read each other's candidates; the caching allocator makes this free
         cs = torch.empty(NQ, ncand, device=self.device)
         ci = torch.empty(NQ, ncand, dtype=torch.int32, device=self.device)
-        out_s = torch.empty(NQ, k, device=self.device)
-        out_i = torch.empty(NQ, k, dtype=torch.int32, device=self.device)
+        if out is None:
+            out = (torch.empty(NQ, k, device=self.device),
+                   torch.empty(NQ, k, dtype=torch.int32, device=self.device))
+        out_s, out_i = out
+        gate_p = 0 if gate is None else gate.data_ptr()
         st = stream_handle(self.device)
         h = hip()
         thr_p = 0 if thr is None else thr.data_ptr()
@@ -356,9 +426,9 @@ class HbmIndexShard:
         else:
             h.index_scan(rows.data_ptr(), n, self.dim, rows_per_blk, n_rblk, q_unit.data_ptr(),
                          NQ, kmax, cs.data_ptr(), ci.data_ptr(), st, self.scan_ns, self.scan_aux,
-                         thr_p, self.scan_xcd)
+                         thr_p, self.scan_xcd, gate_p)
         h.topk_merge(cs.data_ptr(), ci.data_ptr(), NQ, ncand, kmax, k, out_s.data_ptr(),
-                     out_i.data_ptr(), 0, 0, st)
+                     out_i.data_ptr(), 0, 0, st, gate_p)
         return out_s, out_i
 
     def _search_matmul(self, q_unit: torch.Tensor, k: int, chunk: int = 1 << 22):

@@ -39,7 +39,8 @@ int symb_topk_geometry(int D, int kmax, int* lists, int* queries_per_blk);
 int symb_attention_config(int waves, int kvt);
 int symb_index_scan(const void* X, int n_valid, int D, int rows_per_blk, int n_rblk,
                     const void* Q, int NQ, int kmax, float* cand_s, int* cand_i, hipStream_t st,
-                    int ns, int aux, const float* thr_init, int xcd);
+                    int ns, int aux, const float* thr_init, int xcd,
+                    const int* gate = nullptr);
 int symb_index_scan_ablate(const void* X, int n_valid, int rows_per_blk, int n_rblk,
                            const void* Q, int NQ, float* cs, int* ci, hipStream_t st, int abl,
                            const float* thr);
@@ -60,7 +61,14 @@ int symb_index_scan_fp8(const void* X, int n_valid, int D, int rows_per_blk, int
                         hipStream_t st, int aux, const float* thr_init, int variant, int xcd);
 int symb_topk_merge(const float* cand_s, const int* cand_i, int NQ, int n_cand_per_query,
                     int kmax, int k, float* out_s, int* out_i, int64_t id_offset,
-                    int64_t* out_id64, hipStream_t st);
+                    int64_t* out_id64, hipStream_t st, const int* gate = nullptr);
+int symb_mq_queries_per_blk();
+int symb_index_scan_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
+                       int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
+                       int xcd, hipStream_t st);
+int symb_topk_select_counted(const float* cand_s, const int* cand_i, const int* cand_n, int cap,
+                             int NQ, int kmax, int k, float* out_s, int* out_i, int* ovf,
+                             hipStream_t st);
 
 namespace {
 
@@ -300,15 +308,32 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("index_scan", [](uptr X, int n_valid, int D, int rows_per_blk, int n_rblk, uptr Q, int NQ,
                          int kmax, uptr cand_s, uptr cand_i, uptr st, int ns, int aux, uptr thr,
-                         int xcd) {
+                         int xcd, uptr gate) {
     check(symb_index_scan(P<void>(X), n_valid, D, rows_per_blk, n_rblk, P<void>(Q), NQ, kmax,
                           P<float>(cand_s), P<int>(cand_i), S(st), ns, aux, P<const float>(thr),
-                          xcd),
+                          xcd, P<const int>(gate)),
           "index_scan");
   }, py::arg("X"), py::arg("n_valid"), py::arg("D"), py::arg("rows_per_blk"), py::arg("n_rblk"),
      py::arg("Q"), py::arg("NQ"), py::arg("kmax"), py::arg("cand_s"), py::arg("cand_i"),
      py::arg("stream"), py::arg("ns") = 0, py::arg("aux") = -1, py::arg("thr_init") = 0,
-     py::arg("xcd") = 1);
+     py::arg("xcd") = 1, py::arg("gate") = 0);
+  // multi-query-block D=384 scan (index_mq.hip): candidates above the seeded thresholds
+  m.def("mq_queries_per_blk", []() { return symb_mq_queries_per_blk(); });
+  m.def("index_scan_mq", [](uptr X, int n_valid, int rows_per_blk, int n_rblk, uptr Q, int NQ,
+                            uptr thr, uptr cand_s, uptr cand_i, uptr cand_n, int cap, int xcd,
+                            uptr st) {
+    check(symb_index_scan_mq(P<void>(X), n_valid, rows_per_blk, n_rblk, P<void>(Q), NQ,
+                             P<const float>(thr), P<float>(cand_s), P<int>(cand_i), P<int>(cand_n),
+                             cap, xcd, S(st)),
+          "index_scan_mq");
+  });
+  m.def("topk_select_counted", [](uptr cand_s, uptr cand_i, uptr cand_n, int cap, int NQ,
+                                  int kmax, int k, uptr out_s, uptr out_i, uptr ovf, uptr st) {
+    check(symb_topk_select_counted(P<const float>(cand_s), P<const int>(cand_i),
+                                   P<const int>(cand_n), cap, NQ, kmax, k, P<float>(out_s),
+                                   P<int>(out_i), P<int>(ovf), S(st)),
+          "topk_select_counted");
+  });
   m.def("index_scan_ablate", [](uptr X, int n_valid, int rows_per_blk, int n_rblk, uptr Q, int NQ,
                                 uptr cs, uptr ci, uptr st, int abl, uptr thr) {
     check(symb_index_scan_ablate(P<void>(X), n_valid, rows_per_blk, n_rblk, P<void>(Q), NQ,
@@ -362,11 +387,15 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("stream"), py::arg("aux") = -1, py::arg("thr_init") = 0, py::arg("variant") = 0,
      py::arg("xcd") = 1);
   m.def("topk_merge", [](uptr cand_s, uptr cand_i, int NQ, int n_cand, int kmax, int k,
-                         uptr out_s, uptr out_i, int64_t id_offset, uptr out_id64, uptr st) {
+                         uptr out_s, uptr out_i, int64_t id_offset, uptr out_id64, uptr st,
+                         uptr gate) {
     check(symb_topk_merge(P<float>(cand_s), P<int>(cand_i), NQ, n_cand, kmax, k, P<float>(out_s),
-                          P<int>(out_i), id_offset, P<int64_t>(out_id64), S(st)),
+                          P<int>(out_i), id_offset, P<int64_t>(out_id64), S(st),
+                          P<const int>(gate)),
           "topk_merge");
-  });
+  }, py::arg("cand_s"), py::arg("cand_i"), py::arg("NQ"), py::arg("n_cand"), py::arg("kmax"),
+     py::arg("k"), py::arg("out_s"), py::arg("out_i"), py::arg("id_offset"), py::arg("out_id64"),
+     py::arg("stream"), py::arg("gate") = 0);
   py::class_<EncoderRuntime>(m, "EncoderRuntime")
       .def(py::init<int, int, int, float, uptr, uptr, uptr, uptr, uptr>())
       .def("add_layer", &EncoderRuntime::add_layer)

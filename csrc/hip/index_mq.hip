@@ -1,0 +1,358 @@
+// Multi-query-block fused scan for D = 384 bf16 shards: the per-rank shape of the sharded search
+// at N >= 2 GPUs (every rank scores the 256*N all-gathered queries against its 100M/N rows;
+// SURVEY.md §2.5 X2, §2.6 index sharding).  Complements index_topk.hip, whose kernel holds 256
+// queries per workgroup and keeps per-lane top-k lists in registers.
+//
+// Why a second kernel: at 512+ queries the 256-query kernel streams every row block once per
+// 256-query block (L2 -> LDS), issues 6 LDS-DMA pieces per 1536 MFMA cycles per wave and reads
+// one A fragment from LDS per MFMA.  Its compute-only ablation runs 13.1 ms on 12.5M x 2048 q and
+// the full kernel 17.0 ms (profiles/r2_wide/): the row stream, not the MFMAs, is what is left.
+//
+// This kernel holds 512 queries per workgroup (8 waves x 64 queries):
+//  * queries stay RESIDENT IN AGPRs as the B operand of hand-issued v_mfma_f32_16x16x32_bf16
+//    (4 sets of 16 queries x 12 k-steps x 4 registers = 192 AGPRs per lane), so one A fragment
+//    read from LDS feeds FOUR MFMAs and every row tile DMA'd into LDS feeds 512 queries: half
+//    the LDS-DMA issue, L2->LDS bytes and LDS read bytes per FLOP of the 256-query kernel;
+//  * the 16x16x32 shape holds a higher clock than 32x32x16 under the chip's power management at
+//    equal cycles per FLOP (MI355X_MICROARCH.md, DVFS give-back item 7);
+//  * with 192 of the 256 registers a wave may hold at 2 waves/SIMD spent on queries, no per-lane
+//    top-k list fits.  The kernel EMITS candidates instead: every score above the query's seeded
+//    threshold (a lower bound on its final k-th score, from a row sample: exact by construction)
+//    is appended to that query's candidate buffer with a vector atomic, and a select kernel takes
+//    the top-k of each buffer.  A sample of 1/64 of the rows puts ~64k candidates per query above
+//    the threshold (~640 for k = 10), rare events against 12.5M rows.  A buffer that overflows
+//    raises a device flag on which the 256-query kernel re-runs the whole batch (gated launches,
+//    no host sync), so the result is exact for any data.
+//
+// Ring, swizzle and barrier structure follow index_topk.hip: 64-row tiles (48 KiB) through a
+// 3-deep LDS ring by global_load_lds_dwordx4 with counted vmcnt and a raw s_barrier; A fragments
+// by hand-issued ds_read_b128 with counted lgkmcnt; chunk XOR (row & 15) on both sides.
+#include "scan_common.h"
+
+namespace symb {
+
+namespace mq {
+constexpr int D = 384;
+constexpr int WAVES = 8;
+constexpr int SETS = 4;                     // 16-query B-fragment sets per wave
+constexpr int QW = SETS * 16;               // queries per wave
+constexpr int QPB = WAVES * QW;             // queries per workgroup
+constexpr int SUB = 16;                     // rows per MFMA chain
+constexpr int TR = 64;                      // rows per barrier interval (tile)
+constexpr int NSUB = TR / SUB;
+constexpr int NS = 3;                       // LDS ring depth in tiles
+constexpr int CPR = D / 8;                  // 16-byte chunks per row
+constexpr int TILE_BYTES = TR * D * 2;      // 48 KiB
+constexpr int SUB_BYTES = SUB * D * 2;
+constexpr int LOADS = TILE_BYTES / (1024 * WAVES);  // LDS-DMA pieces per wave per tile (6)
+constexpr int NKS = D / 32;                 // 16x16x32 k-steps over D (12)
+constexpr int M = 4;                        // period of the per-lane fragment offsets
+constexpr int PF = 3;                       // fragment reads in flight
+constexpr int R = PF + 1;                   // fragment ring slots
+constexpr int DMA_EVERY = 2;                // k-steps between DMA pieces in sub-tile 0
+static_assert(TILE_BYTES % (1024 * WAVES) == 0, "tile must split evenly over waves");
+static_assert(LOADS * DMA_EVERY <= NKS, "DMA pieces must fit the first chain");
+static_assert(NS * TILE_BYTES <= 160 * 1024, "LDS ring exceeds the CU's 160 KiB");
+}  // namespace mq
+
+template <int OFF>
+__device__ __forceinline__ void mq_read16(bf16x8& dst, uint32_t addr) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(addr), "i"(OFF));
+}
+template <int N>
+__device__ __forceinline__ void mq_lgkm(bf16x8& v) {
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(v) : "i"(N));
+}
+
+// One 16x16x32 MFMA per query set.  Hand-issued so the 192 query registers stay put as the B
+// operand (VGPRs: naming them as AGPRs makes the compiler split the 256-register budget 128/128
+// and shuttle queries between the files).
+template <bool FIRST>
+__device__ __forceinline__ void mq_mfma(f32x4& acc, const bf16x8& a, const bf16x8& q) {
+  if constexpr (FIRST)
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(a), "v"(q));
+  else
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(q));
+}
+
+// k-step KS of one 16-row sub-tile: wait for its A fragment, 4 MFMAs (one per query set), then
+// refill the ring slot PF steps ahead.  DMA(i) issues LDS-DMA piece i of a later tile.
+template <int KS, int DMA_PIECES>
+struct MqChain {
+  template <class Dma>
+  __device__ __forceinline__ static void run(f32x4 (&acc)[mq::SETS], bf16x8 (&a)[mq::R],
+                                             const bf16x8 (&qf)[mq::SETS][mq::NKS],
+                                             const uint32_t (&voff)[mq::M], uint32_t base,
+                                             const Dma& dma) {
+    using namespace mq;
+    if constexpr (DMA_PIECES > 0 && KS % DMA_EVERY == 0 && KS / DMA_EVERY < DMA_PIECES)
+      dma(KS / DMA_EVERY);
+    constexpr int outstanding = (NKS - KS < PF) ? (NKS - KS) : PF;
+    mq_lgkm<outstanding - 1>(a[KS % R]);
+#pragma unroll
+    for (int s = 0; s < SETS; ++s) mq_mfma<KS == 0>(acc[s], a[KS % R], qf[s][KS]);
+    // XDL result -> VALU read (the emission test reads acc right after the chain): the compiler
+    // pads nothing inside asm, so cover the MFMA's result latency here.
+    if constexpr (KS + 1 == NKS) asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+    if constexpr (KS + PF < NKS)
+      mq_read16<((KS + PF) / M) * 256>(a[(KS + PF) % R], base + voff[(KS + PF) % M]);
+    if constexpr (KS + 1 < NKS) MqChain<KS + 1, DMA_PIECES>::run(acc, a, qf, voff, base, dma);
+  }
+};
+
+template <int J>
+__device__ __forceinline__ void mq_prologue(bf16x8 (&a)[mq::R], const uint32_t (&voff)[mq::M],
+                                            uint32_t base) {
+  mq_read16<(J / mq::M) * 256>(a[J % mq::R], base + voff[J % mq::M]);
+  if constexpr (J + 1 < mq::PF) mq_prologue<J + 1>(a, voff, base);
+}
+
+// X: [>= round_up(n_valid, 64), 384] bf16 unit rows; Q: [NQ, 384] bf16 unit queries.
+// thr[NQ]: per-query lower bounds on the final k-th score (required).
+// cand_s/cand_i: [NQ][cap]; cand_n[NQ] (zeroed): number of candidates each query emitted (may
+// exceed cap: the select kernel then raises the overflow flag).
+__global__ __launch_bounds__(512, 1) void index_scan_mq_kernel(
+    const __bf16* __restrict__ X, int n_valid, int rows_per_blk, const __bf16* __restrict__ Q,
+    int NQ, int n_qblk, int xcd, const float* __restrict__ thr_in, float* __restrict__ cand_s,
+    int* __restrict__ cand_i, int* __restrict__ cand_n, int cap) {
+  using namespace mq;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lb = xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int qb = lb % n_qblk, rb = lb / n_qblk;
+  const int row_begin = rb * rows_per_blk;
+  const int row_end = min(row_begin + rows_per_blk, n_valid);
+  const int n_tiles = row_end > row_begin ? (row_end - row_begin + TR - 1) / TR : 0;
+
+  // ---- query fragments (B operand, 16x16x32: lane holds Q[col = lane&15][k = 8*(lane>>4)+j]) --
+  const int qbase = qb * QPB + wave * QW + (lane & 15);
+  bf16x8 qf[SETS][NKS];
+  float thr[SETS];
+#pragma unroll
+  for (int s = 0; s < SETS; ++s) {
+    const int q = qbase + s * 16;
+    const __bf16* qp = Q + (size_t)min(q, NQ - 1) * D + (lane >> 4) * 8;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) qf[s][ks] = *reinterpret_cast<const bf16x8*>(qp + ks * 32);
+    thr[s] = q < NQ ? thr_in[q] : INFINITY;   // padding queries never emit
+  }
+  // consume the query/threshold loads here, before any LDS-DMA is in flight: the compiler waits
+  // for a load at its first use, and a first use inside the tile loop would be a vmcnt(0) that
+  // drains the DMA ring every tile
+#pragma unroll
+  for (int s = 0; s < SETS; ++s) {
+    asm volatile("" ::"v"(thr[s]));
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) asm volatile("" ::"v"(qf[s][ks]));
+  }
+
+  // ---- LDS-DMA pieces: piece i of a tile fills 16-byte LDS slot (i*WAVES + wave)*64 + lane with
+  // chunk (pc ^ (row & 15)) of its row (the swizzle lives on the global source address).  The
+  // per-lane source offsets are loop-invariant 32-bit registers, so every piece issues in the
+  // SGPR-base + VGPR-offset form and no register a pending LDS-DMA reads is ever rewritten (the
+  // compiler would drain vmcnt to 0 before such a write).
+  uint32_t goff[LOADS];
+#pragma unroll
+  for (int i = 0; i < LOADS; ++i) {
+    const int sl = (i * WAVES + wave) * 64 + lane;
+    const int row = sl / CPR, pc = sl % CPR;
+    goff[i] = (uint32_t)(row * D + (pc ^ (row & 15)) * 8);
+  }
+  auto issue_piece = [&](int t, int i) {
+    const int tt = min(t, n_tiles - 1);  // past the end: re-load the last tile (vmcnt stays exact)
+    const __bf16* base = X + (size_t)(row_begin + tt * TR) * D;
+    char* dst = smem + (t % NS) * TILE_BYTES;
+    glds16_aux<0>(base + goff[i], dst + ((i * WAVES + wave) * 64) * 16);
+  };
+
+  // ---- per-lane A-fragment LDS offsets (16x16x32: lane holds X[row lane&15][k 8*(lane>>4)+j]) --
+  const uint32_t lds_smem = lds_addr(smem);
+  uint32_t voff[M];
+  {
+    const int r = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int m = 0; m < M; ++m) voff[m] = (uint32_t)(r * D * 2 + (((4 * m + g) ^ r) << 4));
+  }
+
+  // candidate emission for one 16-row sub-tile: lane holds rows row0 + 4*(lane>>4) + r of the
+  // 16 queries of each set (column lane & 15)
+  auto emit = [&](f32x4 (&acc)[SETS], int row0) {
+    const int rl = row0 + 4 * (lane >> 4);
+    if (row0 + SUB > row_end) {
+#pragma unroll
+      for (int s = 0; s < SETS; ++s)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (rl + r >= row_end) acc[s][r] = -INFINITY;
+    }
+    bool hit = false;
+#pragma unroll
+    for (int s = 0; s < SETS; ++s)
+      hit |= fmaxf(fmaxf(acc[s][0], acc[s][1]), fmaxf(acc[s][2], acc[s][3])) > thr[s];
+    if (hit) {
+      // cold path: the candidate addresses are derived from an opaque copy of qbase here, so the
+      // compiler cannot hoist twelve 64-bit pointers out of the tile loop into the register budget
+      int qo = qbase;
+      asm volatile("" : "+v"(qo));
+#pragma unroll
+      for (int s = 0; s < SETS; ++s) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (acc[s][r] > thr[s]) {
+            const int q = qo + s * 16;
+            const int slot = atomicAdd(cand_n + q, 1);
+            if (slot < cap) {
+              cand_s[(size_t)q * cap + slot] = acc[s][r];
+              cand_i[(size_t)q * cap + slot] = rl + r;
+            }
+          }
+        }
+      }
+    }
+  };
+
+  if (n_tiles > 0) {
+#pragma unroll
+    for (int p = 0; p < NS - 1; ++p)
+#pragma unroll
+      for (int i = 0; i < LOADS; ++i) issue_piece(p, i);
+  }
+  bf16x8 a[R];
+  f32x4 acc[SETS];
+  for (int t = 0; t < n_tiles; ++t) {
+    // tile t landed for this wave once only the (NS-2) younger tiles' pieces remain; the barrier
+    // makes every wave's pieces visible and retires every wave's reads of slot (t-1) % NS
+    wait_vmcnt<LOADS * (NS - 2)>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const uint32_t tbase = lds_smem + (uint32_t)((t % NS) * TILE_BYTES);
+    const int row0 = row_begin + t * TR;
+    const int tnext = t + NS - 1;
+    auto dma = [&](int i) { issue_piece(tnext, i); };
+    mq_prologue<0>(a, voff, tbase);
+    MqChain<0, LOADS>::run(acc, a, qf, voff, tbase, dma);
+#pragma unroll
+    for (int j = 1; j < NSUB; ++j) {
+      // the next sub-tile's first reads fly while this wave tests the previous one's scores
+      mq_prologue<0>(a, voff, tbase + j * SUB_BYTES);
+      emit(acc, row0 + (j - 1) * SUB);
+      MqChain<0, 0>::run(acc, a, qf, voff, tbase + j * SUB_BYTES, NoDma());
+    }
+    emit(acc, row0 + (NSUB - 1) * SUB);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tail prefetches and emissions
+}
+
+// Top-k of each query's emitted candidates.  One workgroup per query: strided local top-KMAX,
+// then an LDS tree of pairwise merges.  A query whose buffer overflowed raises *ovf (the gated
+// 256-query kernel then recomputes the batch).
+template <int KMAX, int NTH>
+__global__ __launch_bounds__(NTH) void topk_select_counted_kernel(
+    const float* __restrict__ cand_s, const int* __restrict__ cand_i,
+    const int* __restrict__ cand_n, int cap, int k, float* __restrict__ out_s,
+    int* __restrict__ out_i, int* __restrict__ ovf) {
+  __shared__ float ls[NTH * KMAX];
+  __shared__ int li[NTH * KMAX];
+  const int q = blockIdx.x, tid = threadIdx.x;
+  const int cnt = cand_n[q];
+  const int n = min(cnt, cap);
+  if (tid == 0 && cnt > cap) *ovf = 1;
+  const float* cs = cand_s + (size_t)q * cap;
+  const int* ci = cand_i + (size_t)q * cap;
+  float tv[KMAX];
+  int ti[KMAX];
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) {
+    tv[i] = -INFINITY;
+    ti[i] = -1;
+  }
+  for (int c = tid; c < n; c += NTH) {
+    const float s = cs[c];
+    if (s > tv[KMAX - 1]) topk_insert<KMAX>(tv, ti, s, ci[c]);
+  }
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) {
+    ls[tid * KMAX + i] = tv[i];
+    li[tid * KMAX + i] = ti[i];
+  }
+  __syncthreads();
+  for (int half = NTH / 2; half >= 1; half >>= 1) {
+    if (tid < half) {
+      const float* as = ls + tid * KMAX;
+      const int* ai = li + tid * KMAX;
+      const float* bs = ls + (tid + half) * KMAX;
+      const int* bi = li + (tid + half) * KMAX;
+      int pa = 0, pb = 0;
+#pragma unroll
+      for (int i = 0; i < KMAX; ++i) {
+        const bool take_a = as[pa] >= bs[pb];
+        tv[i] = take_a ? as[pa] : bs[pb];
+        ti[i] = take_a ? ai[pa] : bi[pb];
+        pa += take_a ? 1 : 0;
+        pb += take_a ? 0 : 1;
+        pa = min(pa, KMAX - 1);
+        pb = min(pb, KMAX - 1);
+      }
+    }
+    __syncthreads();
+    if (tid < half) {
+#pragma unroll
+      for (int i = 0; i < KMAX; ++i) {
+        ls[tid * KMAX + i] = tv[i];
+        li[tid * KMAX + i] = ti[i];
+      }
+    }
+    __syncthreads();
+  }
+  if (tid < k) {
+    out_s[(size_t)q * k + tid] = tid < KMAX ? ls[tid] : -INFINITY;
+    out_i[(size_t)q * k + tid] = tid < KMAX ? li[tid] : -1;
+  }
+}
+
+}  // namespace symb
+
+using namespace symb;
+
+int symb_mq_queries_per_blk() { return mq::QPB; }
+
+// rows_per_blk must be a multiple of 64; n_rblk * rows_per_blk >= n_valid.  cand_n is zeroed here.
+int symb_index_scan_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
+                       int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
+                       int xcd, hipStream_t st) {
+  if (NQ <= 0) return 0;
+  if (rows_per_blk % mq::TR || n_rblk <= 0 || thr == nullptr || cap <= 0) return -1;
+  hipError_t e = hipMemsetAsync(cand_n, 0, sizeof(int) * (size_t)NQ, st);
+  if (e != hipSuccess) return (int)e;
+  const int n_qblk = (NQ + mq::QPB - 1) / mq::QPB;
+  constexpr int lds = mq::NS * mq::TILE_BYTES;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)index_scan_mq_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL(index_scan_mq_kernel, dim3(n_rblk * n_qblk), dim3(512), lds, st,
+                     (const __bf16*)X, n_valid, rows_per_blk, (const __bf16*)Q, NQ, n_qblk, xcd,
+                     thr, cand_s, cand_i, cand_n, cap);
+  return (int)hipGetLastError();
+}
+
+// ovf (one int) is zeroed here, then set by any query whose buffer overflowed.
+int symb_topk_select_counted(const float* cand_s, const int* cand_i, const int* cand_n, int cap,
+                             int NQ, int kmax, int k, float* out_s, int* out_i, int* ovf,
+                             hipStream_t st) {
+  if (NQ <= 0) return 0;
+  if (k > kmax) return -1;
+  hipError_t e = hipMemsetAsync(ovf, 0, sizeof(int), st);
+  if (e != hipSuccess) return (int)e;
+  if (kmax == 16)
+    hipLaunchKernelGGL((topk_select_counted_kernel<16, 256>), dim3(NQ), dim3(256), 0, st, cand_s,
+                       cand_i, cand_n, cap, k, out_s, out_i, ovf);
+  else if (kmax == 32)
+    hipLaunchKernelGGL((topk_select_counted_kernel<32, 128>), dim3(NQ), dim3(128), 0, st, cand_s,
+                       cand_i, cand_n, cap, k, out_s, out_i, ovf);
+  else
+    return -1;
+  return (int)hipGetLastError();
+}

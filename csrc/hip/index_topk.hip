@@ -94,7 +94,11 @@ template <int D, bool MFMA_32, int KMAX, int NS, int AUX, int ABLX = 0>
 __global__ __launch_bounds__(512) void index_scan_topk_kernel(
     const __bf16* __restrict__ X, int n_valid, int rows_per_blk, const __bf16* __restrict__ Q,
     int NQ, int n_qblk, int xcd, const float* __restrict__ thr_init, float* __restrict__ cand_s,
-    int* __restrict__ cand_i) {
+    int* __restrict__ cand_i, const int* __restrict__ gate) {
+  // gate (optional): run only if *gate != 0 -- the exact fallback of the multi-query-block scan
+  // (index_mq.hip) is enqueued unconditionally and skips itself unless a candidate buffer
+  // overflowed, so no host sync decides it
+  if (gate != nullptr && *gate == 0) return;
   constexpr bool STAMP = ABLX >= 8;
   constexpr int ABL = ABLX == 8 ? 0 : ABLX == 9 ? 5 : ABLX == 10 ? 2 : ABLX;
   uint64_t seg[6] = {0, 0, 0, 0, 0, 0};
@@ -496,7 +500,9 @@ __global__ __launch_bounds__(NTH) void topk_merge_kernel(const float* __restrict
                                                          float* __restrict__ out_s,
                                                          int* __restrict__ out_i,
                                                          int64_t id_offset,
-                                                         int64_t* __restrict__ out_id64) {
+                                                         int64_t* __restrict__ out_id64,
+                                                         const int* __restrict__ gate) {
+  if (gate != nullptr && *gate == 0) return;   // see index_scan_topk_kernel
   __shared__ float ls[NTH * KMAX];
   __shared__ int li[NTH * KMAX];
   const int q = blockIdx.x, tid = threadIdx.x;
@@ -578,7 +584,7 @@ int symb_topk_geometry(int D, int kmax, int* lists, int* queries_per_blk) {
 template <int D, bool M32, int KMAX, int NS, int AUX>
 static int launch_scan(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                        int NQ, int n_qblk, int xcd, const float* thr, float* cs, int* ci,
-                       hipStream_t st) {
+                       hipStream_t st, const int* gate) {
   auto kern = index_scan_topk_kernel<D, M32, KMAX, NS, AUX>;
   constexpr int lds = NS * (M32 ? 64 : 32) * D * 2;
   static bool attr = false;
@@ -587,7 +593,7 @@ static int launch_scan(const void* X, int n_valid, int rows_per_blk, int n_rblk,
     attr = true;
   }
   hipLaunchKernelGGL(kern, dim3(n_rblk * n_qblk), dim3(512), lds, st, (const __bf16*)X, n_valid,
-                     rows_per_blk, (const __bf16*)Q, NQ, n_qblk, xcd, thr, cs, ci);
+                     rows_per_blk, (const __bf16*)Q, NQ, n_qblk, xcd, thr, cs, ci, gate);
   return (int)hipGetLastError();
 }
 
@@ -600,7 +606,7 @@ int symb_index_scan_ablate(const void* X, int n_valid, int rows_per_blk, int n_r
     constexpr int lds = 3 * 64 * 384 * 2;
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipLaunchKernelGGL(kern, dim3(n_rblk * n_qblk), dim3(512), lds, st, (const __bf16*)X, n_valid,
-                       rows_per_blk, (const __bf16*)Q, NQ, n_qblk, 0, thr, cs, ci);
+                       rows_per_blk, (const __bf16*)Q, NQ, n_qblk, 0, thr, cs, ci, nullptr);
     return (int)hipGetLastError();
   };
   if (abl == 3) {
@@ -630,9 +636,9 @@ template <> struct ScanCfg<1024> { static constexpr bool M32 = false; static con
 template <int D, int NS>
 static int dispatch_k(int kmax, int aux, const void* X, int n_valid, int rows_per_blk, int n_rblk,
                       const void* Q, int NQ, int n_qblk, int xcd, const float* thr, float* cs,
-                      int* ci, hipStream_t st) {
+                      int* ci, hipStream_t st, const int* gate) {
   constexpr bool M32 = ScanCfg<D>::M32;
-#define SYMB_L(K, A) launch_scan<D, M32, K, NS, A>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, n_qblk, xcd, thr, cs, ci, st)
+#define SYMB_L(K, A) launch_scan<D, M32, K, NS, A>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, n_qblk, xcd, thr, cs, ci, st, gate)
   if (kmax == 16) return aux ? SYMB_L(16, 2) : SYMB_L(16, 0);
   return aux ? SYMB_L(32, 2) : SYMB_L(32, 0);
 #undef SYMB_L
@@ -645,14 +651,14 @@ static int dispatch_k(int kmax, int aux, const void* X, int n_valid, int rows_pe
 // xcd: group the query blocks of each row block on one XCD (L2-shared row stream; NQ > 256).
 int symb_index_scan(const void* X, int n_valid, int D, int rows_per_blk, int n_rblk,
                     const void* Q, int NQ, int kmax, float* cand_s, int* cand_i, hipStream_t st,
-                    int ns, int aux, const float* thr_init, int xcd) {
+                    int ns, int aux, const float* thr_init, int xcd, const int* gate) {
   if (NQ <= 0 || n_rblk <= 0) return 0;
   if (rows_per_blk % 64) return -1;
   int lists, qpb;
   if (symb_topk_geometry(D, kmax, &lists, &qpb)) return -1;
   const int n_qblk = (NQ + qpb - 1) / qpb;
   if (aux < 0) aux = n_qblk == 1 ? 2 : 0;
-#define SYMB_ARGS kmax, aux, X, n_valid, rows_per_blk, n_rblk, Q, NQ, n_qblk, xcd, thr_init, cand_s, cand_i, st
+#define SYMB_ARGS kmax, aux, X, n_valid, rows_per_blk, n_rblk, Q, NQ, n_qblk, xcd, thr_init, cand_s, cand_i, st, gate
   if (D == 384) {
     if (ns == 0 || ns == 3) return dispatch_k<384, 3>(SYMB_ARGS);
     if (ns == 2) return dispatch_k<384, 2>(SYMB_ARGS);
@@ -674,15 +680,15 @@ int symb_index_scan(const void* X, int n_valid, int D, int rows_per_blk, int n_r
 // Also merges gathered per-rank top-k lists ([NQ][world*k], padded to kmax) in the sharded path.
 int symb_topk_merge(const float* cand_s, const int* cand_i, int NQ, int n_cand_per_query,
                     int kmax, int k, float* out_s, int* out_i, int64_t id_offset,
-                    int64_t* out_id64, hipStream_t st) {
+                    int64_t* out_id64, hipStream_t st, const int* gate) {
   if (NQ <= 0) return 0;
   if (k > kmax) return -1;
   if (kmax == 16)
     hipLaunchKernelGGL((topk_merge_kernel<16, 256>), dim3(NQ), dim3(256), 0, st, cand_s, cand_i,
-                       n_cand_per_query, k, out_s, out_i, id_offset, out_id64);
+                       n_cand_per_query, k, out_s, out_i, id_offset, out_id64, gate);
   else if (kmax == 32)
     hipLaunchKernelGGL((topk_merge_kernel<32, 128>), dim3(NQ), dim3(128), 0, st, cand_s, cand_i,
-                       n_cand_per_query, k, out_s, out_i, id_offset, out_id64);
+                       n_cand_per_query, k, out_s, out_i, id_offset, out_id64, gate);
   else
     return -1;
   return (int)hipGetLastError();

@@ -315,6 +315,55 @@ def test_index_scan_xcd_grouping_is_exact(dtype):
         _close(s1, ref_s, atol=2e-3, what="xcd-grouped topk scores")
 
 
+@pytest.mark.parametrize("nq", [512, 1100, 2048])
+def test_index_scan_mq_exact(nq):
+    """The 512-query emitting scan (the per-rank shape at N >= 2 GPUs) returns the rows of the
+    256-query list kernel and of the fp32 oracle; no candidate buffer overflows on random data."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+
+    n, k, D = (1 << 20) + 777, 10, 384
+    shard = HbmIndexShard(D, n + 4096)
+    shard.fill_random(n, seed=31)
+    q = torch.nn.functional.normalize(_f(nq, D, seed=32), dim=-1).bfloat16()
+    assert shard._seed_rows(n, k) and shard._mq_ok(nq, k, shard.rows, "bf16")
+    shard.scan_mq = False
+    s0, r0 = shard.search(q, k)
+    shard.scan_mq = True
+    s1, r1 = shard.search(q, k)
+    cnt, ovf = shard._mq_last
+    torch.cuda.synchronize()
+    assert int(ovf.item()) == 0
+    assert 0 < cnt.float().mean().item() < 8 * 64 * k
+    # different fp32 summation orders (16x16x32 vs 32x32x16 MFMA): scores agree to ~1e-6
+    _close(s1, s0, atol=1e-5, what="mq vs list scores")
+    assert (r0 == r1).float().mean().item() > 0.999
+    ref_s, _ = R.topk_ref(shard.unit_rows(), q, k)
+    _close(s1, ref_s, atol=2e-3, what="mq topk scores")
+    true = (q.float() @ shard.unit_rows().float().t()).gather(1, r1.long())
+    _close(s1, true, atol=2e-3, what="mq returned rows")
+
+
+def test_index_scan_mq_overflow_falls_back_exact():
+    """6000 copies of query 0 in the shard overflow its candidate buffer: the gated 256-query
+    kernel re-runs the batch on the GPU and the answer stays exact."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+
+    n, dup, nq, k = (1 << 20) + 100, 6000, 512, 10
+    shard = HbmIndexShard(384, n + dup)
+    shard.fill_random(n, seed=41)
+    q = torch.nn.functional.normalize(_f(nq, 384, seed=42), dim=-1).bfloat16()
+    shard.append_unit(q[:1].expand(dup, -1).contiguous())
+    s1, r1 = shard.search(q, k)
+    cnt, ovf = shard._mq_last
+    shard.scan_mq = False
+    s0, r0 = shard.search(q, k)
+    torch.cuda.synchronize()
+    assert int(ovf.item()) == 1 and int(cnt[0].item()) > shard.MQ_CAP
+    assert torch.equal(s0, s1)
+    assert torch.equal(r0[1:], r1[1:])
+    assert (r1[0] >= n).all()   # query 0's top-k are copies of itself
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("src", [torch.float32, torch.bfloat16])
 def test_quant_fp8_matches_torch_e4m3(src):
