@@ -125,6 +125,49 @@ def cmd_scanmq(a):
                       "cand_max": int(cnt.max()), "results": out}))
 
 
+def cmd_scanmqabl(a):
+    """index_scan_mq_kernel ablations (abl 0 full, 1 no DMA, 2 no emission test) and its in-kernel
+    clock (abl 3 stamps), same thresholds and grid as shard.search."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard, TILE_ROWS, _round_up
+    from codename_symbiont_amd.ops._ext import hip, stream_handle
+
+    D, k = 384, 10
+    shard = HbmIndexShard(D, a.rows, device="cuda")
+    shard.fill_random(a.rows, seed=1)
+    q = torch.nn.functional.normalize(torch.randn(a.nq, D, device="cuda"), dim=-1).bfloat16()
+    h = hip()
+    n = shard.visible
+    ms, sample = shard._block_sample(n)
+    pre_s, _ = shard._scan(ms, q, 16, k, None, None, sample, "bf16")
+    thr = pre_s[:, k - 1].contiguous() - shard.MQ_THR_MARGIN
+    n_qblk = math.ceil(a.nq / h.mq_queries_per_blk())
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    n_rblk = max(1, round(ncu / n_qblk))
+    rpb = _round_up(math.ceil(n / n_rblk), TILE_ROWS)
+    n_rblk = math.ceil(n / rpb)
+    cap = shard.MQ_CAP
+    cs = torch.zeros(a.nq, cap, device="cuda")
+    ci = torch.empty(a.nq, cap, dtype=torch.int32, device="cuda")
+    cnt = torch.empty(a.nq, dtype=torch.int32, device="cuda")
+    st = stream_handle()
+
+    def run(abl):
+        h.index_scan_mq_ablate(shard.rows.data_ptr(), n, rpb, n_rblk, q.data_ptr(), a.nq,
+                               thr.data_ptr(), cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(), cap,
+                               1, st, abl)
+    r = ab({f"abl{m}": (lambda m=m: run(m)) for m in (0, 1, 2)}, rounds=a.rounds, iters=a.iters)
+    flop = 2 * n * D * a.nq
+    out = {nm: dict(ms=round(m, 3), TFLOPs=round(flop / (m / 1e3) / 1e12)) for nm, (m, _) in r.items()}
+    timeit(lambda: run(3), 10)
+    run(3)
+    torch.cuda.synchronize()
+    st_ = cs.view(-1)[: 2 * n_rblk * n_qblk].view(-1, 2).double()
+    ghz = (st_[:, 0] / st_[:, 1] * 0.1).median().item()
+    out["in_kernel_clock_GHz"] = round(ghz, 3)
+    out["cycles_per_tile"] = round((st_[:, 0] / math.ceil(rpb / TILE_ROWS)).median().item(), 1)
+    print(json.dumps({"bench": "scanmq_ablation", "rows": n, "nq": a.nq, "results": out}))
+
+
 def cmd_scanabl(a):
     """DMA-only vs compute-only vs full scan (D=384), plus a plain torch streaming read."""
     from codename_symbiont_amd.index.shard import HbmIndexShard, _round_up
@@ -459,7 +502,7 @@ def cmd_prefilter(a):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("cmd", choices=["scan", "scanmq", "scanabl", "scanstamp", "scanfp8", "gemm", "encoder", "attn", "latency", "gemmfp8", "prefilter"])
+    ap.add_argument("cmd", choices=["scan", "scanmq", "scanmqabl", "scanabl", "scanstamp", "scanfp8", "gemm", "encoder", "attn", "latency", "gemmfp8", "prefilter"])
     ap.add_argument("--qmode", choices=["random", "near"], default="random", help="prefilter: query kind")
     ap.add_argument("--rows", type=int, default=100_000_000)
     ap.add_argument("--dim", type=int, default=384)
@@ -475,7 +518,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=5)
     a = ap.parse_args()
-    {"scan": cmd_scan, "scanmq": cmd_scanmq, "scanabl": cmd_scanabl, "scanstamp": cmd_scanstamp, "scanfp8": cmd_scanfp8, "gemm": cmd_gemm, "encoder": cmd_encoder, "attn": cmd_attn, "latency": cmd_latency, "gemmfp8": cmd_gemmfp8, "prefilter": cmd_prefilter}[a.cmd](a)
+    {"scan": cmd_scan, "scanmq": cmd_scanmq, "scanmqabl": cmd_scanmqabl, "scanabl": cmd_scanabl, "scanstamp": cmd_scanstamp, "scanfp8": cmd_scanfp8, "gemm": cmd_gemm, "encoder": cmd_encoder, "attn": cmd_attn, "latency": cmd_latency, "gemmfp8": cmd_gemmfp8, "prefilter": cmd_prefilter}[a.cmd](a)
 
 
 if __name__ == "__main__":

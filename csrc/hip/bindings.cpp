@@ -66,6 +66,9 @@ int symb_mq_queries_per_blk();
 int symb_index_scan_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                        int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
                        int xcd, hipStream_t st);
+int symb_index_scan_mq_ablate(const void* X, int n_valid, int rows_per_blk, int n_rblk,
+                              const void* Q, int NQ, const float* thr, float* cand_s, int* cand_i,
+                              int* cand_n, int cap, int xcd, hipStream_t st, int abl);
 int symb_topk_select_counted(const float* cand_s, const int* cand_i, const int* cand_n, int cap,
                              int NQ, int kmax, int k, float* out_s, int* out_i, int* ovf,
                              hipStream_t st);
@@ -326,6 +329,14 @@ PYBIND11_MODULE(_hip, m) {
                              P<const float>(thr), P<float>(cand_s), P<int>(cand_i), P<int>(cand_n),
                              cap, xcd, S(st)),
           "index_scan_mq");
+  });
+  m.def("index_scan_mq_ablate", [](uptr X, int n_valid, int rows_per_blk, int n_rblk, uptr Q,
+                                   int NQ, uptr thr, uptr cand_s, uptr cand_i, uptr cand_n,
+                                   int cap, int xcd, uptr st, int abl) {
+    check(symb_index_scan_mq_ablate(P<void>(X), n_valid, rows_per_blk, n_rblk, P<void>(Q), NQ,
+                                    P<const float>(thr), P<float>(cand_s), P<int>(cand_i),
+                                    P<int>(cand_n), cap, xcd, S(st), abl),
+          "index_scan_mq_ablate");
   });
   m.def("topk_select_counted", [](uptr cand_s, uptr cand_i, uptr cand_n, int cap, int NQ,
                                   int kmax, int k, uptr out_s, uptr out_i, uptr ovf, uptr st) {

@@ -24,9 +24,15 @@
 //    raises a device flag on which the 256-query kernel re-runs the whole batch (gated launches,
 //    no host sync), so the result is exact for any data.
 //
-// Ring, swizzle and barrier structure follow index_topk.hip: 64-row tiles (48 KiB) through a
-// 3-deep LDS ring by global_load_lds_dwordx4 with counted vmcnt and a raw s_barrier; A fragments
-// by hand-issued ds_read_b128 with counted lgkmcnt; chunk XOR (row & 15) on both sides.
+// Ring and barrier structure follow index_topk.hip: 64-row tiles (48 KiB) through a 3-deep LDS
+// ring by global_load_lds_dwordx4 with counted vmcnt and a raw s_barrier; A fragments by
+// hand-issued ds_read_b128 with counted lgkmcnt.  The LDS image of a tile is 48 1-KiB PIECES, one
+// per (16-row sub-tile j, 32-column k-step ks): piece j*12 + ks holds rows 16j..16j+15 x 64 bytes,
+// so one LDS-DMA instruction fills one piece and one ds_read_b128 per lane reads one MFMA A
+// fragment.  Lane l of a piece holds row l>>2, 16-byte slot l&3 = chunk (l&3) ^ f(row), and the
+// A-fragment read of lane (r = lane&15, g = lane>>4) takes slot g ^ f(r), f(r) = (r>>1) & 2: every
+// 16-lane ds_read_b128 group then covers all 16 slots of a 256-byte bank row once (conflict-free),
+// and both the DMA source offset and the fragment offset are ONE per-lane register each.
 #include "scan_common.h"
 
 namespace symb {
@@ -46,13 +52,20 @@ constexpr int TILE_BYTES = TR * D * 2;      // 48 KiB
 constexpr int SUB_BYTES = SUB * D * 2;
 constexpr int LOADS = TILE_BYTES / (1024 * WAVES);  // LDS-DMA pieces per wave per tile (6)
 constexpr int NKS = D / 32;                 // 16x16x32 k-steps over D (12)
-constexpr int M = 4;                        // period of the per-lane fragment offsets
+constexpr int PIECE = 1024;                 // LDS bytes per (sub-tile, k-step) piece
 constexpr int PF = 3;                       // fragment reads in flight
 constexpr int R = PF + 1;                   // fragment ring slots
 constexpr int DMA_EVERY = 2;                // k-steps between DMA pieces in sub-tile 0
 static_assert(TILE_BYTES % (1024 * WAVES) == 0, "tile must split evenly over waves");
+static_assert(NSUB * NKS * PIECE == TILE_BYTES, "a tile is NSUB x NKS pieces");
 static_assert(LOADS * DMA_EVERY <= NKS, "DMA pieces must fit the first chain");
 static_assert(NS * TILE_BYTES <= 160 * 1024, "LDS ring exceeds the CU's 160 KiB");
+// per-wave candidate stage in LDS after the ring: score f32, row i32, query-in-wave u16
+constexpr int STW = 192;                    // staged candidates per wave (flushed past STW - 64)
+constexpr int STAGE_BYTES = STW * 10;
+constexpr int LDS_BYTES = NS * TILE_BYTES + WAVES * STAGE_BYTES;
+static_assert(LDS_BYTES <= 160 * 1024, "ring + stages exceed the CU's 160 KiB");
+static_assert(NKS % R == 0, "cross-chain prefetch: fragment j of the next chain must use slot j % R");
 }  // namespace mq
 
 template <int OFF>
@@ -76,41 +89,58 @@ __device__ __forceinline__ void mq_mfma(f32x4& acc, const bf16x8& a, const bf16x
 }
 
 // k-step KS of one 16-row sub-tile: wait for its A fragment, 4 MFMAs (one per query set), then
-// refill the ring slot PF steps ahead.  DMA(i) issues LDS-DMA piece i of a later tile.
-template <int KS, int DMA_PIECES>
+// refill the ring slot PF steps ahead -- in the last PF steps with the first fragments of the
+// NEXT sub-tile (at ``next``, when NEXT), so its chain starts without an LDS round trip.
+// DMA(i) issues LDS-DMA piece i of a later tile.
+template <int KS, int DMA_PIECES, bool NEXT>
 struct MqChain {
   template <class Dma>
   __device__ __forceinline__ static void run(f32x4 (&acc)[mq::SETS], bf16x8 (&a)[mq::R],
                                              const bf16x8 (&qf)[mq::SETS][mq::NKS],
-                                             const uint32_t (&voff)[mq::M], uint32_t base,
-                                             const Dma& dma) {
+                                             uint32_t base, uint32_t next, const Dma& dma) {
     using namespace mq;
     if constexpr (DMA_PIECES > 0 && KS % DMA_EVERY == 0 && KS / DMA_EVERY < DMA_PIECES)
       dma(KS / DMA_EVERY);
-    constexpr int outstanding = (NKS - KS < PF) ? (NKS - KS) : PF;
+    constexpr int outstanding = (NEXT || NKS - KS >= PF) ? PF : (NKS - KS);
     mq_lgkm<outstanding - 1>(a[KS % R]);
 #pragma unroll
     for (int s = 0; s < SETS; ++s) mq_mfma<KS == 0>(acc[s], a[KS % R], qf[s][KS]);
     // XDL result -> VALU read (the emission test reads acc right after the chain): the compiler
     // pads nothing inside asm, so cover the MFMA's result latency here.
     if constexpr (KS + 1 == NKS) asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+    // base / next: this lane's fragment address in piece 0 of this / the next sub-tile
     if constexpr (KS + PF < NKS)
-      mq_read16<((KS + PF) / M) * 256>(a[(KS + PF) % R], base + voff[(KS + PF) % M]);
-    if constexpr (KS + 1 < NKS) MqChain<KS + 1, DMA_PIECES>::run(acc, a, qf, voff, base, dma);
+      mq_read16<(KS + PF) * PIECE>(a[(KS + PF) % R], base);
+    else if constexpr (NEXT)  // fragment KS + PF - NKS of the next sub-tile, same ring slot order
+      mq_read16<(KS + PF - NKS) * PIECE>(a[(KS + PF) % R], next);
+    if constexpr (KS + 1 < NKS)
+      MqChain<KS + 1, DMA_PIECES, NEXT>::run(acc, a, qf, base, next, dma);
   }
 };
 
+// A pointer the compiler must treat as wave-uniform (SGPR pair): with it the LDS-DMA issues in the
+// SGPR-base + 32-bit VGPR-offset form instead of a per-piece 64-bit VGPR address.
+__device__ __forceinline__ const char* mq_uniform(const char* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return reinterpret_cast<const char*>(((uint64_t)hi << 32) | lo);
+}
+
 template <int J>
-__device__ __forceinline__ void mq_prologue(bf16x8 (&a)[mq::R], const uint32_t (&voff)[mq::M],
-                                            uint32_t base) {
-  mq_read16<(J / mq::M) * 256>(a[J % mq::R], base + voff[J % mq::M]);
-  if constexpr (J + 1 < mq::PF) mq_prologue<J + 1>(a, voff, base);
+__device__ __forceinline__ void mq_prologue(bf16x8 (&a)[mq::R], uint32_t base) {
+  mq_read16<J * mq::PIECE>(a[J % mq::R], base);
+  if constexpr (J + 1 < mq::PF) mq_prologue<J + 1>(a, base);
 }
 
 // X: [>= round_up(n_valid, 64), 384] bf16 unit rows; Q: [NQ, 384] bf16 unit queries.
 // thr[NQ]: per-query lower bounds on the final k-th score (required).
 // cand_s/cand_i: [NQ][cap]; cand_n[NQ] (zeroed): number of candidates each query emitted (may
 // exceed cap: the select kernel then raises the overflow flag).
+// ABL (profiling entry symb_index_scan_mq_ablate only): 1 = no LDS-DMA (compute on whatever the
+// ring holds), 2 = no emission test, 3 = full kernel + per-workgroup s_memtime / s_memrealtime
+// around the tile loop written to cand_s[2 * blockIdx.x + {0, 1}] (in-kernel clock).
+template <int ABL = 0>
 __global__ __launch_bounds__(512, 1) void index_scan_mq_kernel(
     const __bf16* __restrict__ X, int n_valid, int rows_per_blk, const __bf16* __restrict__ Q,
     int NQ, int n_qblk, int xcd, const float* __restrict__ thr_in, float* __restrict__ cand_s,
@@ -146,72 +176,105 @@ __global__ __launch_bounds__(512, 1) void index_scan_mq_kernel(
     for (int ks = 0; ks < NKS; ++ks) asm volatile("" ::"v"(qf[s][ks]));
   }
 
-  // ---- LDS-DMA pieces: piece i of a tile fills 16-byte LDS slot (i*WAVES + wave)*64 + lane with
-  // chunk (pc ^ (row & 15)) of its row (the swizzle lives on the global source address).  The
-  // per-lane source offsets are loop-invariant 32-bit registers, so every piece issues in the
-  // SGPR-base + VGPR-offset form and no register a pending LDS-DMA reads is ever rewritten (the
-  // compiler would drain vmcnt to 0 before such a write).
-  uint32_t goff[LOADS];
-#pragma unroll
-  for (int i = 0; i < LOADS; ++i) {
-    const int sl = (i * WAVES + wave) * 64 + lane;
-    const int row = sl / CPR, pc = sl % CPR;
-    goff[i] = (uint32_t)(row * D + (pc ^ (row & 15)) * 8);
-  }
+  // ---- LDS-DMA: wave w fills pieces p = i*WAVES + w (i < LOADS) of a tile.  Lane l fetches row
+  // l>>2 of the piece, chunk (l&3) ^ f(l>>2): one loop-invariant per-lane offset for every piece
+  // (SGPR base + VGPR offset form; a pending LDS-DMA's registers are never rewritten, which would
+  // make the compiler drain vmcnt to 0).
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const uint32_t loff = (uint32_t)((lane >> 2) * D * 2 + (((lane & 3) ^ ((lane >> 3) & 2)) * 16));
   auto issue_piece = [&](int t, int i) {
     const int tt = min(t, n_tiles - 1);  // past the end: re-load the last tile (vmcnt stays exact)
-    const __bf16* base = X + (size_t)(row_begin + tt * TR) * D;
-    char* dst = smem + (t % NS) * TILE_BYTES;
-    glds16_aux<0>(base + goff[i], dst + ((i * WAVES + wave) * 64) * 16);
+    const int p = i * WAVES + wave_u, j = p / NKS, ks = p % NKS;
+    const char* base = reinterpret_cast<const char*>(X + (size_t)(row_begin + tt * TR + j * SUB) * D
+                                                     + ks * 32);
+    char* dst = smem + (t % NS) * TILE_BYTES + p * PIECE;
+    glds16_aux<0>(mq_uniform(base) + loff, dst);
   };
 
-  // ---- per-lane A-fragment LDS offsets (16x16x32: lane holds X[row lane&15][k 8*(lane>>4)+j]) --
+  // ---- per-lane A-fragment offset within a piece (lane holds X[row r][k 8g..8g+7] of the k-step)
   const uint32_t lds_smem = lds_addr(smem);
-  uint32_t voff[M];
-  {
-    const int r = lane & 15, g = lane >> 4;
-#pragma unroll
-    for (int m = 0; m < M; ++m) voff[m] = (uint32_t)(r * D * 2 + (((4 * m + g) ^ r) << 4));
-  }
+  const uint32_t foff = (uint32_t)((lane & 15) * 64 + (((lane >> 4) ^ ((lane >> 1) & 2)) * 16));
 
-  // candidate emission for one 16-row sub-tile: lane holds rows row0 + 4*(lane>>4) + r of the
-  // 16 queries of each set (column lane & 15)
+  // ---- candidate emission -------------------------------------------------------------------
+  // A hit is staged in this wave's LDS stage at a slot from a wave-wide ballot prefix count (no
+  // atomics, no waits), and the stage moves to the per-query global buffers (vector atomics whose
+  // returned slot the compiler must wait for, i.e. vmcnt(0), draining the LDS-DMA ring) only when
+  // it fills: ~once per 130 candidates instead of once per candidate.
+  char* stage = smem + NS * TILE_BYTES + wave_u * STAGE_BYTES;
+  float* st_s = reinterpret_cast<float*>(stage);
+  int* st_r = reinterpret_cast<int*>(stage + STW * 4);
+  uint16_t* st_q = reinterpret_cast<uint16_t*>(stage + STW * 8);
+  int nst = 0;  // staged entries (wave-uniform)
+  auto flush = [&]() {
+    // the candidate addresses derive from an opaque copy of the wave's first query so the
+    // compiler cannot hoist 64-bit pointers out of the tile loop into the register budget
+    int qw = qb * QPB + wave_u * QW;
+    asm volatile("" : "+v"(qw));
+    for (int e = lane; e < nst; e += 64) {
+      const int q = qw + st_q[e];
+      const int slot = atomicAdd(cand_n + q, 1);
+      if (slot < cap) {
+        cand_s[(size_t)q * cap + slot] = st_s[e];
+        cand_i[(size_t)q * cap + slot] = st_r[e];
+      }
+    }
+    nst = 0;
+  };
+  // one 16-row sub-tile: lane holds rows row0 + 4*(lane>>4) + r of the 16 queries of each set
+  // (column lane & 15)
   auto emit = [&](f32x4 (&acc)[SETS], int row0) {
-    const int rl = row0 + 4 * (lane >> 4);
-    if (row0 + SUB > row_end) {
+    if constexpr (ABL == 2) {
+#pragma unroll
+      for (int s = 0; s < SETS; ++s) asm volatile("" ::"v"(acc[s]));
+      return;
+    }
+    if (row0 + SUB > row_end) {   // last tile of the block: mask rows past its end
+      const int rl = row0 + 4 * (lane >> 4);
 #pragma unroll
       for (int s = 0; s < SETS; ++s)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           if (rl + r >= row_end) acc[s][r] = -INFINITY;
     }
-    bool hit = false;
+    // max of each set's 4 scores by two v_max3 (fmaxf would add NaN-canonicalising maxes)
+    float mx[SETS];
 #pragma unroll
     for (int s = 0; s < SETS; ++s)
-      hit |= fmaxf(fmaxf(acc[s][0], acc[s][1]), fmaxf(acc[s][2], acc[s][3])) > thr[s];
-    if (hit) {
-      // cold path: the candidate addresses are derived from an opaque copy of qbase here, so the
-      // compiler cannot hoist twelve 64-bit pointers out of the tile loop into the register budget
-      int qo = qbase;
-      asm volatile("" : "+v"(qo));
+      asm volatile("v_max3_f32 %0, %1, %2, %3\n\tv_max3_f32 %0, %0, %4, %4"
+                   : "=&v"(mx[s]) : "v"(acc[s][0]), "v"(acc[s][1]), "v"(acc[s][2]), "v"(acc[s][3]));
+    bool hit = false;
+#pragma unroll
+    for (int s = 0; s < SETS; ++s) hit |= mx[s] > thr[s];
+    if (__builtin_amdgcn_ballot_w64(hit)) {
+      // cold path: per-lane values come from opaque copies made here, so nothing it derives can
+      // be hoisted out of the tile loop into the (full) register budget
+      int lo = lane;
+      asm volatile("" : "+v"(lo));
+      const int lrow = row0 + 4 * (lo >> 4), lq = lo & 15;
 #pragma unroll
       for (int s = 0; s < SETS; ++s) {
+        if (!__builtin_amdgcn_ballot_w64(mx[s] > thr[s])) continue;   // usually one set hits
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          if (acc[s][r] > thr[s]) {
-            const int q = qo + s * 16;
-            const int slot = atomicAdd(cand_n + q, 1);
-            if (slot < cap) {
-              cand_s[(size_t)q * cap + slot] = acc[s][r];
-              cand_i[(size_t)q * cap + slot] = rl + r;
+          const bool p = acc[s][r] > thr[s];
+          const uint64_t m = __builtin_amdgcn_ballot_w64(p);
+          if (m) {
+            if (nst > STW - 64) flush();
+            const int idx = nst + (int)__builtin_amdgcn_mbcnt_hi(
+                                      (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+            if (p) {
+              st_s[idx] = acc[s][r];
+              st_r[idx] = lrow + r;
+              st_q[idx] = (uint16_t)(s * 16 + lq);
             }
+            nst += __builtin_popcountll(m);
           }
         }
       }
     }
   };
 
-  if (n_tiles > 0) {
+  if (n_tiles > 0 && ABL != 1) {
 #pragma unroll
     for (int p = 0; p < NS - 1; ++p)
 #pragma unroll
@@ -219,28 +282,56 @@ __global__ __launch_bounds__(512, 1) void index_scan_mq_kernel(
   }
   bf16x8 a[R];
   f32x4 acc[SETS];
+  // The two waves sharing a SIMD (w, w + 4) run in phase after every barrier, so their emission
+  // tests (VALU + branch, ~8 % of the loop) would idle the SIMD together.  The second wave tests
+  // its last sub-tile AFTER the barrier, under its partner's first MFMAs: the pair stays half a
+  // test apart and each test overlaps the other wave's chain.
+  const bool late = wave_u >= WAVES / 2;
+  uint64_t c0 = 0, r0t = 0;
+  if constexpr (ABL == 3) {
+    c0 = __builtin_amdgcn_s_memtime();
+    r0t = __builtin_amdgcn_s_memrealtime();
+  }
   for (int t = 0; t < n_tiles; ++t) {
     // tile t landed for this wave once only the (NS-2) younger tiles' pieces remain; the barrier
     // makes every wave's pieces visible and retires every wave's reads of slot (t-1) % NS
-    wait_vmcnt<LOADS * (NS - 2)>();
+    if constexpr (ABL != 1) wait_vmcnt<LOADS * (NS - 2)>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     const uint32_t tbase = lds_smem + (uint32_t)((t % NS) * TILE_BYTES);
     const int row0 = row_begin + t * TR;
     const int tnext = t + NS - 1;
-    auto dma = [&](int i) { issue_piece(tnext, i); };
-    mq_prologue<0>(a, voff, tbase);
-    MqChain<0, LOADS>::run(acc, a, qf, voff, tbase, dma);
+    auto dma = [&](int i) {
+      if constexpr (ABL != 1) issue_piece(tnext, i);
+    };
+    const uint32_t fb = tbase + foff;   // this lane's fragment in piece 0 of sub-tile 0
+    mq_prologue<0>(a, fb);
+    if (late && t > 0) emit(acc, row0 - SUB);
+    MqChain<0, LOADS, true>::run(acc, a, qf, fb, fb + NKS * PIECE, dma);
 #pragma unroll
     for (int j = 1; j < NSUB; ++j) {
-      // the next sub-tile's first reads fly while this wave tests the previous one's scores
-      mq_prologue<0>(a, voff, tbase + j * SUB_BYTES);
+      // sub-tile j's first fragments were read by the previous chain's tail and fly while this
+      // wave tests the previous sub-tile's scores
       emit(acc, row0 + (j - 1) * SUB);
-      MqChain<0, 0>::run(acc, a, qf, voff, tbase + j * SUB_BYTES, NoDma());
+      if (j + 1 < NSUB)
+        MqChain<0, 0, true>::run(acc, a, qf, fb + j * NKS * PIECE, fb + (j + 1) * NKS * PIECE,
+                                 NoDma());
+      else
+        MqChain<0, 0, false>::run(acc, a, qf, fb + j * NKS * PIECE, 0, NoDma());
     }
-    emit(acc, row0 + (NSUB - 1) * SUB);
+    if (!late) emit(acc, row0 + (NSUB - 1) * SUB);
   }
+  if (late && n_tiles > 0) emit(acc, row_begin + n_tiles * TR - SUB);
+  if (nst) flush();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tail prefetches and emissions
+  if constexpr (ABL == 3) {
+    const uint64_t cyc = __builtin_amdgcn_s_memtime() - c0;
+    const uint64_t rt = __builtin_amdgcn_s_memrealtime() - r0t;
+    if (tid == 0) {
+      cand_s[2 * blockIdx.x] = (float)cyc;
+      cand_s[2 * blockIdx.x + 1] = (float)rt;
+    }
+  }
 }
 
 // Top-k of each query's emitted candidates.  One workgroup per query: strided local top-KMAX,
@@ -325,17 +416,43 @@ int symb_index_scan_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk,
   hipError_t e = hipMemsetAsync(cand_n, 0, sizeof(int) * (size_t)NQ, st);
   if (e != hipSuccess) return (int)e;
   const int n_qblk = (NQ + mq::QPB - 1) / mq::QPB;
-  constexpr int lds = mq::NS * mq::TILE_BYTES;
+  constexpr int lds = mq::LDS_BYTES;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)index_scan_mq_kernel,
+    (void)hipFuncSetAttribute((const void*)index_scan_mq_kernel<0>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
-  hipLaunchKernelGGL(index_scan_mq_kernel, dim3(n_rblk * n_qblk), dim3(512), lds, st,
+  hipLaunchKernelGGL(index_scan_mq_kernel<0>, dim3(n_rblk * n_qblk), dim3(512), lds, st,
                      (const __bf16*)X, n_valid, rows_per_blk, (const __bf16*)Q, NQ, n_qblk, xcd,
                      thr, cand_s, cand_i, cand_n, cap);
   return (int)hipGetLastError();
+}
+
+// Profiling-only entry: the ablations of index_scan_mq_kernel (ABL above), same arguments.
+int symb_index_scan_mq_ablate(const void* X, int n_valid, int rows_per_blk, int n_rblk,
+                              const void* Q, int NQ, const float* thr, float* cand_s, int* cand_i,
+                              int* cand_n, int cap, int xcd, hipStream_t st, int abl) {
+  if (NQ <= 0) return 0;
+  if (rows_per_blk % mq::TR || n_rblk <= 0 || thr == nullptr || cap <= 0) return -1;
+  hipError_t e = hipMemsetAsync(cand_n, 0, sizeof(int) * (size_t)NQ, st);
+  if (e != hipSuccess) return (int)e;
+  const int n_qblk = (NQ + mq::QPB - 1) / mq::QPB;
+  constexpr int lds = mq::LDS_BYTES;
+  auto go = [&](auto kern) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipLaunchKernelGGL(kern, dim3(n_rblk * n_qblk), dim3(512), lds, st, (const __bf16*)X,
+                       n_valid, rows_per_blk, (const __bf16*)Q, NQ, n_qblk, xcd, thr, cand_s,
+                       cand_i, cand_n, cap);
+    return (int)hipGetLastError();
+  };
+  switch (abl) {
+    case 0: return go(index_scan_mq_kernel<0>);
+    case 1: return go(index_scan_mq_kernel<1>);
+    case 2: return go(index_scan_mq_kernel<2>);
+    case 3: return go(index_scan_mq_kernel<3>);
+    default: return -1;
+  }
 }
 
 // ovf (one int) is zeroed here, then set by any query whose buffer overflowed.
