@@ -297,7 +297,15 @@ class HbmIndexShard:
             # (rows appended last, e.g. fresh embeddings, are often the best matches).  The margin
             # covers the two kernels' different fp32 summation orders (16x16x32 vs 32x32x16).
             ms, sample = self._block_sample(n)
-            pre_s, _ = self._scan(ms, q_unit, kmax, k, None, n_cus, sample, dtype)
+            # the sample is scanned the same way, seeded from ITS first 1/64 (a uniform
+            # sub-sample; the 256-query kernel over the whole sample took ~6 % of the search)
+            m2 = _round_up(max(ms // self.SEED_DIV, k), TILE_ROWS)
+            if m2 < ms:
+                s0, _ = self._scan(m2, q_unit, kmax, k, None, n_cus, sample, dtype)
+                thr0 = s0[:, k - 1].contiguous() - self.MQ_THR_MARGIN
+                pre_s, _ = self._scan_mq(ms, q_unit, kmax, k, thr0, n_cus, rows=sample)
+            else:
+                pre_s, _ = self._scan(ms, q_unit, kmax, k, None, n_cus, sample, dtype)
             thr = pre_s[:, k - 1].contiguous() - self.MQ_THR_MARGIN
             return self._scan_mq(n, q_unit, kmax, k, thr, n_cus)
         if m:
@@ -330,7 +338,7 @@ class HbmIndexShard:
         torch.index_select(self.rows, 0, self._sample_idx[1], out=buf[:m])
         return m, buf
 
-    def _scan_mq(self, n: int, q_unit: torch.Tensor, kmax: int, k: int, thr, n_cus):
+    def _scan_mq(self, n: int, q_unit: torch.Tensor, kmax: int, k: int, thr, n_cus, rows=None):
         """512-query-per-workgroup scan emitting every score above ``thr`` (index_mq.hip), top-k
         of each query's candidates, and the exact 256-query kernel as a fallback that runs on the
         GPU only if some query's candidate buffer overflowed (a device flag gates it)."""
@@ -344,6 +352,7 @@ class HbmIndexShard:
         n_rblk = max(1, min(math.ceil(n / (TILE_ROWS * 16)), max(1, round(n_cus / n_qblk))))
         rows_per_blk = _round_up(max(1, math.ceil(n / n_rblk)), TILE_ROWS)
         n_rblk = max(1, math.ceil(n / rows_per_blk))
+        rows = self.rows if rows is None else rows
         cap, dev = self.MQ_CAP, self.device
         cs = torch.empty(NQ, cap, device=dev)
         ci = torch.empty(NQ, cap, dtype=torch.int32, device=dev)
@@ -352,12 +361,12 @@ class HbmIndexShard:
         out_s = torch.empty(NQ, k, device=dev)
         out_i = torch.empty(NQ, k, dtype=torch.int32, device=dev)
         st = stream_handle(dev)
-        h.index_scan_mq(self.rows.data_ptr(), n, rows_per_blk, n_rblk, q_unit.data_ptr(), NQ,
+        h.index_scan_mq(rows.data_ptr(), n, rows_per_blk, n_rblk, q_unit.data_ptr(), NQ,
                         thr.data_ptr(), cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(), cap,
                         self.scan_xcd, st)
         h.topk_select_counted(cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(), cap, NQ, kmax, k,
                               out_s.data_ptr(), out_i.data_ptr(), ovf.data_ptr(), st)
-        self._scan(n, q_unit, kmax, k, thr, n_cus, gate=ovf, out=(out_s, out_i))
+        self._scan(n, q_unit, kmax, k, thr, n_cus, rows, gate=ovf, out=(out_s, out_i))
         self._mq_last = (cnt, ovf)   # candidate counts / overflow flag (tests, diagnostics)
         return out_s, out_i
 
