@@ -102,6 +102,7 @@ def main() -> None:
     if args.mode != "embed":
         shard.fill_random(rows_per_rank, seed=100 + info.rank)
     searcher = ShardedSearcher(shard, info)
+    shard.mq_stats = os.environ.get("SYMB_MQ_STATS", "0") not in ("", "0")
     torch.cuda.synchronize(dev)
     row_bytes = cfg.hidden * (1 if args.index_dtype == "fp8" else 2)
     log(info, f"[bench] setup {time.time() - t0:.1f}s: {cfg.model_name}, shard {rows_per_rank} "
@@ -289,6 +290,10 @@ def main() -> None:
         "search": f"top-{args.k} QPS, {rows_txt}x{cfg.hidden} {args.index_dtype} index, {B} queries/rank"
                   + (" (fp8 prefilter + exact bf16 rescore)" if prefilter else ""),
     }[args.mode]
+    if shard._mq_tot is not None:
+        print(f"[bench] rank {info.rank} emitting-scan searches: {int(shard._mq_tot[0].item())} "
+              f"overflowed, max {int(shard._mq_tot[1].item())} candidates per query "
+              f"(cap {shard.MQ_CAP})", file=sys.stderr, flush=True)
     if info.rank == 0:
         res = {
             "metric": metric,

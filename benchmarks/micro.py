@@ -104,6 +104,8 @@ def cmd_scanmq(a):
         near = torch.nn.functional.normalize(q.float() + 0.05 * torch.randn_like(q.float()), dim=-1)
         shard.append_unit(near.bfloat16())
 
+    shard.mq_min_nq = min(shard.mq_min_nq, a.nq)
+
     def srch(mq):
         shard.scan_mq = mq
         return shard.search(q, k)

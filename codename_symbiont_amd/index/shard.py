@@ -138,6 +138,9 @@ class HbmIndexShard:
         # >= 512 seeded queries on a 384-wide bf16 shard (the per-rank shape of the sharded search
         # at N >= 2 GPUs): the 512-query-per-workgroup candidate-emitting kernel (index_mq.hip)
         self.scan_mq = True
+        self.mq_min_nq = 256   # smallest batch for the emitting kernel (< 512: its 2-set form)
+        self.mq_stats = False  # accumulate overflow count / max candidates (diagnostics)
+        self._mq_tot = None
 
     # ------------------------------------------------------------------ inserts
     def _reserve(self, n: int) -> int:
@@ -290,6 +293,30 @@ class HbmIndexShard:
         thr = None
         m = self._seed_rows(n, k)
         mq = m and self._mq_ok(q_unit.shape[0], k, rows, dtype)
+        group = TILE_ROWS << self.MQ_TILE_SHIFT               # rows per 1-in-64 tile group
+        g_end = (n - self.MQ_TAIL_ROWS) // group if n > self.MQ_TAIL_ROWS else 0
+        if m and mq and g_end >= self.SEED_DIV:
+            # Threshold sample = one pseudo-random 64-row tile of every 64 in groups [0, g_end),
+            # scanned IN PLACE by the emitting kernel (gathering n/64 rows cost 0.45 ms at 100M),
+            # plus every row after them -- the last 4096..8191 rows, where fresh inserts (often
+            # a query's best matches) sit -- by the 256-query kernel.  Disjoint real rows, so the
+            # k-th best of the union lower-bounds the final k-th score.
+            ts = self.MQ_TILE_SHIFT
+            nv = g_end                                         # one sampled tile per group
+            # virtual tile v reads physical tile (v << ts) + h(v) < nv << ts: inside the rows
+            assert (nv << ts) * TILE_ROWS <= n, "tile sample past the visible rows"
+            v = torch.arange(0, nv, self.SEED_DIV, device=self.device, dtype=torch.int64)
+            ph = (v << ts) + (((v * 0x9E3779B1) & 0xFFFFFFFF) >> (32 - ts))   # == kernel's h
+            idx = (ph[:, None] * TILE_ROWS + torch.arange(TILE_ROWS, device=self.device)).reshape(-1)
+            sub = torch.index_select(self.rows, 0, idx)       # whole tiles: already tile-padded
+            s0, _ = self._scan(sub.shape[0], q_unit, kmax, k, None, n_cus, sub, dtype)
+            thr0 = s0[:, k - 1].contiguous() - self.MQ_THR_MARGIN
+            pre_s, _ = self._scan_mq(nv * TILE_ROWS, q_unit, kmax, k, thr0, n_cus, tshift=ts)
+            t0 = g_end * group
+            tail_s, _ = self._scan(n - t0, q_unit, kmax, k, None, n_cus, self.rows[t0:], dtype)
+            kth = torch.topk(torch.cat([pre_s, tail_s], 1), k, dim=1).values[:, k - 1]
+            thr = kth.contiguous() - self.MQ_THR_MARGIN
+            return self._scan_mq(n, q_unit, kmax, k, thr, n_cus)
         if m and mq:
             # the emitting kernel keeps EVERY row above the threshold, so it needs a threshold
             # near the true k-th score for any row order: one pseudo-random row per 64-row block
@@ -320,10 +347,12 @@ class HbmIndexShard:
 
     MQ_CAP = 4096             # candidate slots per query (expected use ~64 k)
     MQ_THR_MARGIN = 2.0 ** -12
+    MQ_TILE_SHIFT = 6         # threshold sample: one 64-row tile in 2^6
+    MQ_TAIL_ROWS = 4096       # ... plus at least the last 4096 rows
 
     def _mq_ok(self, NQ: int, k: int, rows, dtype: str) -> bool:
         return (self.scan_mq and dtype == "bf16" and self.dim == 384 and rows is self.rows
-                and NQ >= 512 and k <= 16)
+                and NQ >= self.mq_min_nq and k <= 16)
 
     def _block_sample(self, n: int):
         """Row sample for threshold seeding: row 64 i + h(i) of every full 64-row block i (h a
@@ -338,15 +367,19 @@ class HbmIndexShard:
         torch.index_select(self.rows, 0, self._sample_idx[1], out=buf[:m])
         return m, buf
 
-    def _scan_mq(self, n: int, q_unit: torch.Tensor, kmax: int, k: int, thr, n_cus, rows=None):
+    def _scan_mq(self, n: int, q_unit: torch.Tensor, kmax: int, k: int, thr, n_cus, rows=None,
+                 tshift: int = 0):
         """512-query-per-workgroup scan emitting every score above ``thr`` (index_mq.hip), top-k
         of each query's candidates, and the exact 256-query kernel as a fallback that runs on the
-        GPU only if some query's candidate buffer overflowed (a device flag gates it)."""
+        GPU only if some query's candidate buffer overflowed (a device flag gates it).
+        ``tshift`` > 0: ``n`` virtual rows of the in-place 1-in-2^tshift tile sample; its
+        fallback scans every row (the exact top-k of all rows is a valid threshold too)."""
         from ..ops._ext import hip, stream_handle
 
         h = hip()
         NQ = q_unit.shape[0]
-        n_qblk = math.ceil(NQ / h.mq_queries_per_blk())
+        sets = 4 if NQ >= 512 else 2   # 512 or 256 queries per workgroup
+        n_qblk = math.ceil(NQ / h.mq_queries_per_blk(sets))
         if n_cus is None:
             n_cus = self._n_cus()
         n_rblk = max(1, min(math.ceil(n / (TILE_ROWS * 16)), max(1, round(n_cus / n_qblk))))
@@ -363,11 +396,20 @@ class HbmIndexShard:
         st = stream_handle(dev)
         h.index_scan_mq(rows.data_ptr(), n, rows_per_blk, n_rblk, q_unit.data_ptr(), NQ,
                         thr.data_ptr(), cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(), cap,
-                        self.scan_xcd, st)
+                        self.scan_xcd, st, sets, tshift)
         h.topk_select_counted(cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(), cap, NQ, kmax, k,
                               out_s.data_ptr(), out_i.data_ptr(), ovf.data_ptr(), st)
-        self._scan(n, q_unit, kmax, k, thr, n_cus, rows, gate=ovf, out=(out_s, out_i))
+        if tshift:
+            self._scan(self.visible, q_unit, kmax, k, thr, n_cus, gate=ovf, out=(out_s, out_i))
+        else:
+            self._scan(n, q_unit, kmax, k, thr, n_cus, rows, gate=ovf, out=(out_s, out_i))
         self._mq_last = (cnt, ovf)   # candidate counts / overflow flag (tests, diagnostics)
+        if self.mq_stats:            # running totals (two tiny kernels per search; off by default)
+            if self._mq_tot is None:
+                self._mq_tot = (torch.zeros(1, dtype=torch.int32, device=dev),
+                                torch.zeros(1, dtype=torch.int32, device=dev))
+            self._mq_tot[0].add_(ovf)
+            torch.maximum(self._mq_tot[1], cnt.max().view(1), out=self._mq_tot[1])
         return out_s, out_i
 
     def _search_prefilter(self, q_unit, k: int, n_cus):

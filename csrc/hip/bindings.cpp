@@ -62,10 +62,10 @@ int symb_index_scan_fp8(const void* X, int n_valid, int D, int rows_per_blk, int
 int symb_topk_merge(const float* cand_s, const int* cand_i, int NQ, int n_cand_per_query,
                     int kmax, int k, float* out_s, int* out_i, int64_t id_offset,
                     int64_t* out_id64, hipStream_t st, const int* gate = nullptr);
-int symb_mq_queries_per_blk();
+int symb_mq_queries_per_blk(int sets);
 int symb_index_scan_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                        int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
-                       int xcd, hipStream_t st);
+                       int xcd, hipStream_t st, int sets, int tshift);
 int symb_index_scan_mq_ablate(const void* X, int n_valid, int rows_per_blk, int n_rblk,
                               const void* Q, int NQ, const float* thr, float* cand_s, int* cand_i,
                               int* cand_n, int cap, int xcd, hipStream_t st, int abl);
@@ -321,15 +321,19 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("stream"), py::arg("ns") = 0, py::arg("aux") = -1, py::arg("thr_init") = 0,
      py::arg("xcd") = 1, py::arg("gate") = 0);
   // multi-query-block D=384 scan (index_mq.hip): candidates above the seeded thresholds
-  m.def("mq_queries_per_blk", []() { return symb_mq_queries_per_blk(); });
+  m.def("mq_queries_per_blk", [](int sets) { return symb_mq_queries_per_blk(sets); },
+        py::arg("sets") = 4);
   m.def("index_scan_mq", [](uptr X, int n_valid, int rows_per_blk, int n_rblk, uptr Q, int NQ,
                             uptr thr, uptr cand_s, uptr cand_i, uptr cand_n, int cap, int xcd,
-                            uptr st) {
+                            uptr st, int sets, int tshift) {
     check(symb_index_scan_mq(P<void>(X), n_valid, rows_per_blk, n_rblk, P<void>(Q), NQ,
                              P<const float>(thr), P<float>(cand_s), P<int>(cand_i), P<int>(cand_n),
-                             cap, xcd, S(st)),
+                             cap, xcd, S(st), sets, tshift),
           "index_scan_mq");
-  });
+  }, py::arg("X"), py::arg("n_valid"), py::arg("rows_per_blk"), py::arg("n_rblk"), py::arg("Q"),
+     py::arg("NQ"), py::arg("thr"), py::arg("cand_s"), py::arg("cand_i"), py::arg("cand_n"),
+     py::arg("cap"), py::arg("xcd"), py::arg("stream"), py::arg("sets") = 4,
+     py::arg("tshift") = 0);
   m.def("index_scan_mq_ablate", [](uptr X, int n_valid, int rows_per_blk, int n_rblk, uptr Q,
                                    int NQ, uptr thr, uptr cand_s, uptr cand_i, uptr cand_n,
                                    int cap, int xcd, uptr st, int abl) {

@@ -40,9 +40,8 @@ namespace symb {
 namespace mq {
 constexpr int D = 384;
 constexpr int WAVES = 8;
-constexpr int SETS = 4;                     // 16-query B-fragment sets per wave
-constexpr int QW = SETS * 16;               // queries per wave
-constexpr int QPB = WAVES * QW;             // queries per workgroup
+// query sets (16 queries each) per wave: a kernel template parameter NSET, 4 (512 queries per
+// workgroup: 192 registers of queries) or 2 (256 per workgroup, for 256-query batches)
 constexpr int SUB = 16;                     // rows per MFMA chain
 constexpr int TR = 64;                      // rows per barrier interval (tile)
 constexpr int NSUB = TR / SUB;
@@ -92,11 +91,11 @@ __device__ __forceinline__ void mq_mfma(f32x4& acc, const bf16x8& a, const bf16x
 // refill the ring slot PF steps ahead -- in the last PF steps with the first fragments of the
 // NEXT sub-tile (at ``next``, when NEXT), so its chain starts without an LDS round trip.
 // DMA(i) issues LDS-DMA piece i of a later tile.
-template <int KS, int DMA_PIECES, bool NEXT>
+template <int KS, int DMA_PIECES, bool NEXT, int SETS>
 struct MqChain {
   template <class Dma>
-  __device__ __forceinline__ static void run(f32x4 (&acc)[mq::SETS], bf16x8 (&a)[mq::R],
-                                             const bf16x8 (&qf)[mq::SETS][mq::NKS],
+  __device__ __forceinline__ static void run(f32x4 (&acc)[SETS], bf16x8 (&a)[mq::R],
+                                             const bf16x8 (&qf)[SETS][mq::NKS],
                                              uint32_t base, uint32_t next, const Dma& dma) {
     using namespace mq;
     if constexpr (DMA_PIECES > 0 && KS % DMA_EVERY == 0 && KS / DMA_EVERY < DMA_PIECES)
@@ -114,7 +113,7 @@ struct MqChain {
     else if constexpr (NEXT)  // fragment KS + PF - NKS of the next sub-tile, same ring slot order
       mq_read16<(KS + PF - NKS) * PIECE>(a[(KS + PF) % R], next);
     if constexpr (KS + 1 < NKS)
-      MqChain<KS + 1, DMA_PIECES, NEXT>::run(acc, a, qf, base, next, dma);
+      MqChain<KS + 1, DMA_PIECES, NEXT, SETS>::run(acc, a, qf, base, next, dma);
   }
 };
 
@@ -140,12 +139,13 @@ __device__ __forceinline__ void mq_prologue(bf16x8 (&a)[mq::R], uint32_t base) {
 // ABL (profiling entry symb_index_scan_mq_ablate only): 1 = no LDS-DMA (compute on whatever the
 // ring holds), 2 = no emission test, 3 = full kernel + per-workgroup s_memtime / s_memrealtime
 // around the tile loop written to cand_s[2 * blockIdx.x + {0, 1}] (in-kernel clock).
-template <int ABL = 0>
+template <int NSET, int ABL = 0>
 __global__ __launch_bounds__(512, 1) void index_scan_mq_kernel(
     const __bf16* __restrict__ X, int n_valid, int rows_per_blk, const __bf16* __restrict__ Q,
     int NQ, int n_qblk, int xcd, const float* __restrict__ thr_in, float* __restrict__ cand_s,
-    int* __restrict__ cand_i, int* __restrict__ cand_n, int cap) {
+    int* __restrict__ cand_i, int* __restrict__ cand_n, int cap, int tshift) {
   using namespace mq;
+  constexpr int SETS = NSET, QW = SETS * 16, QPB = WAVES * QW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lb = xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
@@ -153,6 +153,14 @@ __global__ __launch_bounds__(512, 1) void index_scan_mq_kernel(
   const int row_begin = rb * rows_per_blk;
   const int row_end = min(row_begin + rows_per_blk, n_valid);
   const int n_tiles = row_end > row_begin ? (row_end - row_begin + TR - 1) / TR : 0;
+  // Row numbers above are VIRTUAL.  tshift = 0: virtual = physical.  tshift > 0 (a row sample for
+  // threshold seeding, scanned in place): virtual 64-row tile v is physical tile
+  // (v << tshift) + h(v), one pseudo-random tile of every 2^tshift (h: top tshift bits of
+  // v * 0x9E3779B1; index/shard.py builds the matching sub-sample).
+  auto phys_tile = [&](int v) -> int {
+    if (tshift == 0) return v;
+    return (v << tshift) + (int)(((uint32_t)v * 0x9E3779B1u) >> (32 - tshift));
+  };
 
   // ---- query fragments (B operand, 16x16x32: lane holds Q[col = lane&15][k = 8*(lane>>4)+j]) --
   const int qbase = qb * QPB + wave * QW + (lane & 15);
@@ -185,8 +193,8 @@ __global__ __launch_bounds__(512, 1) void index_scan_mq_kernel(
   auto issue_piece = [&](int t, int i) {
     const int tt = min(t, n_tiles - 1);  // past the end: re-load the last tile (vmcnt stays exact)
     const int p = i * WAVES + wave_u, j = p / NKS, ks = p % NKS;
-    const char* base = reinterpret_cast<const char*>(X + (size_t)(row_begin + tt * TR + j * SUB) * D
-                                                     + ks * 32);
+    const int prow = phys_tile(row_begin / TR + tt) * TR;
+    const char* base = reinterpret_cast<const char*>(X + (size_t)(prow + j * SUB) * D + ks * 32);
     char* dst = smem + (t % NS) * TILE_BYTES + p * PIECE;
     glds16_aux<0>(mq_uniform(base) + loff, dst);
   };
@@ -220,9 +228,9 @@ __global__ __launch_bounds__(512, 1) void index_scan_mq_kernel(
     }
     nst = 0;
   };
-  // one 16-row sub-tile: lane holds rows row0 + 4*(lane>>4) + r of the 16 queries of each set
-  // (column lane & 15)
-  auto emit = [&](f32x4 (&acc)[SETS], int row0) {
+  // one 16-row sub-tile at virtual row row0 / physical row prow0: lane holds rows
+  // 4*(lane>>4) + r of it for the 16 queries of each set (column lane & 15)
+  auto emit = [&](f32x4 (&acc)[SETS], int row0, int prow0) {
     if constexpr (ABL == 2) {
 #pragma unroll
       for (int s = 0; s < SETS; ++s) asm volatile("" ::"v"(acc[s]));
@@ -250,7 +258,7 @@ __global__ __launch_bounds__(512, 1) void index_scan_mq_kernel(
       // be hoisted out of the tile loop into the (full) register budget
       int lo = lane;
       asm volatile("" : "+v"(lo));
-      const int lrow = row0 + 4 * (lo >> 4), lq = lo & 15;
+      const int lrow = prow0 + 4 * (lo >> 4), lq = lo & 15;
 #pragma unroll
       for (int s = 0; s < SETS; ++s) {
         if (!__builtin_amdgcn_ballot_w64(mx[s] > thr[s])) continue;   // usually one set hits
@@ -287,6 +295,7 @@ __global__ __launch_bounds__(512, 1) void index_scan_mq_kernel(
   // its last sub-tile AFTER the barrier, under its partner's first MFMAs: the pair stays half a
   // test apart and each test overlaps the other wave's chain.
   const bool late = wave_u >= WAVES / 2;
+  int prow_last = 0;   // physical first row of the previous tile
   uint64_t c0 = 0, r0t = 0;
   if constexpr (ABL == 3) {
     c0 = __builtin_amdgcn_s_memtime();
@@ -300,28 +309,30 @@ __global__ __launch_bounds__(512, 1) void index_scan_mq_kernel(
     __builtin_amdgcn_s_barrier();
     const uint32_t tbase = lds_smem + (uint32_t)((t % NS) * TILE_BYTES);
     const int row0 = row_begin + t * TR;
+    const int prow0 = phys_tile(row0 / TR) * TR;
     const int tnext = t + NS - 1;
     auto dma = [&](int i) {
       if constexpr (ABL != 1) issue_piece(tnext, i);
     };
     const uint32_t fb = tbase + foff;   // this lane's fragment in piece 0 of sub-tile 0
     mq_prologue<0>(a, fb);
-    if (late && t > 0) emit(acc, row0 - SUB);
-    MqChain<0, LOADS, true>::run(acc, a, qf, fb, fb + NKS * PIECE, dma);
+    if (late && t > 0) emit(acc, row0 - SUB, prow_last + TR - SUB);
+    prow_last = prow0;
+    MqChain<0, LOADS, true, SETS>::run(acc, a, qf, fb, fb + NKS * PIECE, dma);
 #pragma unroll
     for (int j = 1; j < NSUB; ++j) {
       // sub-tile j's first fragments were read by the previous chain's tail and fly while this
       // wave tests the previous sub-tile's scores
-      emit(acc, row0 + (j - 1) * SUB);
+      emit(acc, row0 + (j - 1) * SUB, prow0 + (j - 1) * SUB);
       if (j + 1 < NSUB)
-        MqChain<0, 0, true>::run(acc, a, qf, fb + j * NKS * PIECE, fb + (j + 1) * NKS * PIECE,
+        MqChain<0, 0, true, SETS>::run(acc, a, qf, fb + j * NKS * PIECE, fb + (j + 1) * NKS * PIECE,
                                  NoDma());
       else
-        MqChain<0, 0, false>::run(acc, a, qf, fb + j * NKS * PIECE, 0, NoDma());
+        MqChain<0, 0, false, SETS>::run(acc, a, qf, fb + j * NKS * PIECE, 0, NoDma());
     }
-    if (!late) emit(acc, row0 + (NSUB - 1) * SUB);
+    if (!late) emit(acc, row0 + (NSUB - 1) * SUB, prow0 + (NSUB - 1) * SUB);
   }
-  if (late && n_tiles > 0) emit(acc, row_begin + n_tiles * TR - SUB);
+  if (late && n_tiles > 0) emit(acc, row_begin + n_tiles * TR - SUB, prow_last + TR - SUB);
   if (nst) flush();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tail prefetches and emissions
   if constexpr (ABL == 3) {
@@ -405,28 +416,41 @@ __global__ __launch_bounds__(NTH) void topk_select_counted_kernel(
 
 using namespace symb;
 
-int symb_mq_queries_per_blk() { return mq::QPB; }
+int symb_mq_queries_per_blk(int sets) { return mq::WAVES * 16 * sets; }
 
 // rows_per_blk must be a multiple of 64; n_rblk * rows_per_blk >= n_valid.  cand_n is zeroed here.
-int symb_index_scan_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
-                       int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
-                       int xcd, hipStream_t st) {
-  if (NQ <= 0) return 0;
-  if (rows_per_blk % mq::TR || n_rblk <= 0 || thr == nullptr || cap <= 0) return -1;
-  hipError_t e = hipMemsetAsync(cand_n, 0, sizeof(int) * (size_t)NQ, st);
-  if (e != hipSuccess) return (int)e;
-  const int n_qblk = (NQ + mq::QPB - 1) / mq::QPB;
+template <int NSET>
+static int launch_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
+                     int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
+                     int xcd, hipStream_t st, int tshift) {
+  const int n_qblk = (NQ + mq::WAVES * 16 * NSET - 1) / (mq::WAVES * 16 * NSET);
   constexpr int lds = mq::LDS_BYTES;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)index_scan_mq_kernel<0>,
+    (void)hipFuncSetAttribute((const void*)index_scan_mq_kernel<NSET, 0>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
-  hipLaunchKernelGGL(index_scan_mq_kernel<0>, dim3(n_rblk * n_qblk), dim3(512), lds, st,
+  hipLaunchKernelGGL((index_scan_mq_kernel<NSET, 0>), dim3(n_rblk * n_qblk), dim3(512), lds, st,
                      (const __bf16*)X, n_valid, rows_per_blk, (const __bf16*)Q, NQ, n_qblk, xcd,
-                     thr, cand_s, cand_i, cand_n, cap);
+                     thr, cand_s, cand_i, cand_n, cap, tshift);
   return (int)hipGetLastError();
+}
+
+// tshift: 0 = rows [0, n_valid); k > 0 = virtual rows of a 1-in-2^k tile sample (kernel note).
+// sets: 16-query sets per wave, 4 (512 queries per workgroup) or 2 (256).
+int symb_index_scan_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
+                       int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
+                       int xcd, hipStream_t st, int sets, int tshift) {
+  if (NQ <= 0) return 0;
+  if (rows_per_blk % mq::TR || n_rblk <= 0 || thr == nullptr || cap <= 0) return -1;
+  if ((sets != 2 && sets != 4) || tshift < 0 || tshift > 12) return -1;
+  hipError_t e = hipMemsetAsync(cand_n, 0, sizeof(int) * (size_t)NQ, st);
+  if (e != hipSuccess) return (int)e;
+  return sets == 4 ? launch_mq<4>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, thr, cand_s, cand_i,
+                                  cand_n, cap, xcd, st, tshift)
+                   : launch_mq<2>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, thr, cand_s, cand_i,
+                                  cand_n, cap, xcd, st, tshift);
 }
 
 // Profiling-only entry: the ablations of index_scan_mq_kernel (ABL above), same arguments.
@@ -437,20 +461,20 @@ int symb_index_scan_mq_ablate(const void* X, int n_valid, int rows_per_blk, int 
   if (rows_per_blk % mq::TR || n_rblk <= 0 || thr == nullptr || cap <= 0) return -1;
   hipError_t e = hipMemsetAsync(cand_n, 0, sizeof(int) * (size_t)NQ, st);
   if (e != hipSuccess) return (int)e;
-  const int n_qblk = (NQ + mq::QPB - 1) / mq::QPB;
+  const int n_qblk = (NQ + mq::WAVES * 64 - 1) / (mq::WAVES * 64);
   constexpr int lds = mq::LDS_BYTES;
   auto go = [&](auto kern) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipLaunchKernelGGL(kern, dim3(n_rblk * n_qblk), dim3(512), lds, st, (const __bf16*)X,
                        n_valid, rows_per_blk, (const __bf16*)Q, NQ, n_qblk, xcd, thr, cand_s,
-                       cand_i, cand_n, cap);
+                       cand_i, cand_n, cap, 0);
     return (int)hipGetLastError();
   };
   switch (abl) {
-    case 0: return go(index_scan_mq_kernel<0>);
-    case 1: return go(index_scan_mq_kernel<1>);
-    case 2: return go(index_scan_mq_kernel<2>);
-    case 3: return go(index_scan_mq_kernel<3>);
+    case 0: return go(index_scan_mq_kernel<4, 0>);
+    case 1: return go(index_scan_mq_kernel<4, 1>);
+    case 2: return go(index_scan_mq_kernel<4, 2>);
+    case 3: return go(index_scan_mq_kernel<4, 3>);
     default: return -1;
   }
 }

@@ -315,7 +315,7 @@ def test_index_scan_xcd_grouping_is_exact(dtype):
         _close(s1, ref_s, atol=2e-3, what="xcd-grouped topk scores")
 
 
-@pytest.mark.parametrize("nq", [512, 1100, 2048])
+@pytest.mark.parametrize("nq", [300, 512, 1100, 2048])
 def test_index_scan_mq_exact(nq):
     """The 512-query emitting scan (the per-rank shape at N >= 2 GPUs) returns the rows of the
     256-query list kernel and of the fp32 oracle; no candidate buffer overflows on random data."""
@@ -324,6 +324,7 @@ def test_index_scan_mq_exact(nq):
     n, k, D = (1 << 20) + 777, 10, 384
     shard = HbmIndexShard(D, n + 4096)
     shard.fill_random(n, seed=31)
+    shard.mq_min_nq = 256     # < 512 queries: the 2-set (256 queries per workgroup) kernel
     q = torch.nn.functional.normalize(_f(nq, D, seed=32), dim=-1).bfloat16()
     assert shard._seed_rows(n, k) and shard._mq_ok(nq, k, shard.rows, "bf16")
     shard.scan_mq = False
