@@ -48,6 +48,7 @@ int symb_gemm_config(int resln_bm, int tile, int group_m);
 int symb_gemm256_ablate(int abl);
 int symb_gemm_fp8_config(int waves, int big);
 int symb_gemm_resln_config(int waves);
+int symb_gemm_gelu_config(int poly);
 int symb_gemm_fp8(int epi, const void* A8, int lda, const void* W8, int ldw, const float* sa,
                   const float* sw, const float* bias, const void* R, int ldr, void* C, int ldc,
                   int M, int N, int K, hipStream_t st, const void* ascale = nullptr,
@@ -366,6 +367,8 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("resln_bm") = 128, py::arg("tile") = 3, py::arg("group_m") = 8);
   m.def("gemm_resln_config", [](int waves) { check(symb_gemm_resln_config(waves), "gemm_resln_config"); },
         py::arg("waves") = 16);
+  m.def("gemm_gelu_config", [](int poly) { check(symb_gemm_gelu_config(poly), "gemm_gelu_config"); },
+        py::arg("poly"));
   m.def("gemm_fp8_config", [](int waves, int big) {
     check(symb_gemm_fp8_config(waves, big), "gemm_fp8_config");
   }, py::arg("waves") = 8, py::arg("big") = 2);

@@ -62,6 +62,35 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f));
 }
 
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+
+// GELU(erf) of a PAIR of values with no transcendental: erf(y) = y * P(y^2) on |y| <= 3 (degree-8
+// minimax-weighted fit in y^2, |erf error| < 1.7e-5), inputs clamped to |x| <= 3 sqrt(2) (erfc(3)
+// = 2.2e-5).  |GELU error| < 5e-5 absolute and 1.1e-5 relative for large |x|: below the bf16
+// rounding of the GEMM output except in the far negative tail (|y| ~ 1e-4..1e-3, a few tens of
+// bf16 ulps there).  The polynomial runs on packed f32 pairs (v_pk_fma_f32 / v_pk_mul_f32): ~8
+// issue slots per element against ~22 for gelu_erf, which made the GELU epilogue the largest
+// part of MiniLM's K = 384 FFN1 GEMM.
+__device__ __forceinline__ f32x2 gelu2_poly(f32x2 x) {
+  constexpr float lim = 4.24264068711928515f;   // 3 sqrt(2)
+  f32x2 xc;
+  xc.x = __builtin_amdgcn_fmed3f(x.x, -lim, lim);
+  xc.y = __builtin_amdgcn_fmed3f(x.y, -lim, lim);
+  const f32x2 y = xc * 0.70710678118654752f;
+  const f32x2 t = y * y;
+  f32x2 p = 4.074636806e-08f;
+  p = p * t + -1.944968972e-06f;
+  p = p * t + 4.106253982e-05f;
+  p = p * t + -5.110510974e-04f;
+  p = p * t + 4.235480912e-03f;
+  p = p * t + -2.510295995e-02f;
+  p = p * t + 1.110793948e-01f;
+  p = p * t + -3.753148317e-01f;
+  p = p * t + 1.128268361e+00f;
+  const f32x2 h = x * 0.5f;
+  return h * (y * p) + h;
+}
+
 // Bijective XCD-aware remap of a linear workgroup id (MI355X deals workgroups round-robin over
 // 8 XCDs): consecutive logical tiles land on the same XCD so their shared operand panels hit the
 // same private L2.  Speed only, never correctness.

@@ -352,8 +352,17 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
           y[e + 4] = x1[e] + b1[e];
         }
         if constexpr (EPI == EPI_GELU || EPI == EPI_GELU_MX8) {
+          if (eps != 0.f) {   // GELU epilogues take eps (LayerNorm-only) as the form switch
 #pragma unroll
-          for (int e = 0; e < 8; ++e) y[e] = gelu_erf(y[e]);
+            for (int e = 0; e < 8; e += 2) {
+              const f32x2 v = gelu2_poly(f32x2{y[e], y[e + 1]});
+              y[e] = v.x;
+              y[e + 1] = v.y;
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) y[e] = gelu_erf(y[e]);
+          }
         }
         if constexpr (EPI == EPI_GELU_MX8) {
           // the 4 consecutive threads (tid & 3) of one row hold one 32-column MX block
@@ -381,6 +390,12 @@ static int g_group_m = 8;
 // Waves of the 128x128 fp8 tile: 4 (64x64 wave tiles) or 8 (64x32, default: e5-large fp8
 // forward 18.2 -> 17.7 ms, profiles/r1_s4/fp8_waves/).
 static int g_fp8_waves = 8;
+// GELU epilogue form: 0 = gelu_erf (A&S erf, one rcp + one exp per value), 1 = gelu2_poly
+// (packed-pair polynomial, no transcendental).  Passed to the kernel in its eps argument, which
+// only the LayerNorm epilogue otherwise reads.
+// Measured (profiles/r2_gelu/ab.json, one process): MiniLM FFN1 52.2 -> 47.1 us, bge FFN1 133.9 ->
+// 123.9 us (bias-only epilogue: 40.3 / 111.4), same max error vs the fp32 oracle (bf16-bound).
+static int g_gelu_poly = 1;
 
 template <int BM, int BN, int WM, int WN, int EPI, int NSTAGE = 2, bool F8 = false,
           bool AMX = false>
@@ -475,6 +490,7 @@ int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const flo
               const void* R, int ldr, const float* gamma, const float* beta, float eps, void* C,
               int ldc, int M, int N, int K, hipStream_t st) {
   if (M <= 0) return 0;
+  if (epi == EPI_GELU) eps = g_gelu_poly ? 1.f : 0.f;
   if (K % GEMM_BK != 0) return -1;
   auto a = (const __bf16*)A;
   auto w = (const __bf16*)W;
@@ -605,7 +621,8 @@ int symb_gemm_fp8(int epi, const void* A8, int lda, const void* W8, int ldw, con
   const bool big = g_fp8_big != 0 && use_big_tile(3, M, N, K) &&
                    (g_fp8_big == 1 || (K >= 1024 && N != K && epi != EPI_GELU_MX8));
 #define SYMB_G8W(E, X, BMN, WM_, WN_) launch_cfg<BMN, BMN, WM_, WN_, E, 2, true, X>(              \
-    A8, lda, W8, ldw, bias, r, ldr, nullptr, nullptr, 0.f, c, ldc, M, N, K, st, sa, sw, as, cs)
+    A8, lda, W8, ldw, bias, r, ldr, nullptr, nullptr, g_gelu_poly ? 1.f : 0.f, c, ldc, M, N, K, \
+    st, sa, sw, as, cs)
 #define SYMB_G8(E, X)                                                                      \
   (big ? SYMB_G8W(E, X, 256, 2, 4)                                                         \
        : g_fp8_waves == 16 ? SYMB_G8W(E, X, 128, 4, 4)                                     \
@@ -672,4 +689,10 @@ int symb_quant_rows_fp8(const void* x, int ldx, void* out, int ldo, float* scale
   hipLaunchKernelGGL(quant_rows_fp8_kernel, dim3((M + 3) / 4), dim3(256), 0, st,
                      (const __bf16*)x, ldx, (uint8_t*)out, ldo, scale, M, K);
   return (int)hipGetLastError();
+}
+
+int symb_gemm_gelu_config(int poly) {
+  if (poly != 0 && poly != 1) return -1;
+  g_gelu_poly = poly;
+  return 0;
 }
