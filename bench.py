@@ -73,6 +73,9 @@ def main() -> None:
     ap.add_argument("--no-overlap", action="store_true",
                     help="--mode full: run encode and search back to back on one stream instead of "
                          "encoding batch i+1 on a second stream while batch i is searched")
+    ap.add_argument("--scan-cus", type=int, default=0,
+                    help="spread the index scans over this many CUs (0 = all), leaving the rest to "
+                         "the encoder running beside them on the second stream")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch the encoder's kernels eagerly every step instead of replaying a "
                          "captured hipGraph of the forward")
@@ -103,6 +106,7 @@ def main() -> None:
         shard.fill_random(rows_per_rank, seed=100 + info.rank)
     searcher = ShardedSearcher(shard, info)
     shard.mq_stats = os.environ.get("SYMB_MQ_STATS", "0") not in ("", "0")
+    shard.scan_cus = args.scan_cus
     torch.cuda.synchronize(dev)
     row_bytes = cfg.hidden * (1 if args.index_dtype == "fp8" else 2)
     log(info, f"[bench] setup {time.time() - t0:.1f}s: {cfg.model_name}, shard {rows_per_rank} "

@@ -137,6 +137,7 @@ class HbmIndexShard:
         self.scan_xcd = 1
         # >= 512 seeded queries on a 384-wide bf16 shard (the per-rank shape of the sharded search
         # at N >= 2 GPUs): the 512-query-per-workgroup candidate-emitting kernel (index_mq.hip)
+        self.scan_cus = 0      # 0 = every CU (see _n_cus)
         self.scan_mq = True
         self.mq_min_nq = 256   # smallest batch for the emitting kernel (< 512: its 2-set form)
         self.mq_stats = False  # accumulate overflow count / max candidates (diagnostics)
@@ -435,10 +436,12 @@ class HbmIndexShard:
         return max(_round_up(n // self.SEED_DIV, TILE_ROWS), _round_up(k, TILE_ROWS))
 
     def _n_cus(self) -> int:
+        """Workgroups (CUs) a scan spreads over: all of them unless ``scan_cus`` leaves some to
+        work running beside the search on another stream (e.g. the next batch's encoder)."""
         n = getattr(self, "_cus", None)
         if n is None:
             n = self._cus = torch.cuda.get_device_properties(self.device).multi_processor_count
-        return n
+        return min(n, self.scan_cus) if self.scan_cus else n
 
     def _scan(self, n: int, q_unit: torch.Tensor, kmax: int, k: int, thr, n_cus, rows=None,
               dtype=None, gate=None, out=None):
