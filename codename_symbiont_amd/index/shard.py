@@ -305,7 +305,8 @@ class HbmIndexShard:
             ts = self.MQ_TILE_SHIFT
             nv = g_end                                         # one sampled tile per group
             # virtual tile v reads physical tile (v << ts) + h(v) < nv << ts: inside the rows
-            assert (nv << ts) * TILE_ROWS <= n, "tile sample past the visible rows"
+            if (nv << ts) * TILE_ROWS > n:   # (a launch past the rows would fault the GPU)
+                raise RuntimeError("tile sample past the visible rows")
             v = torch.arange(0, nv, self.SEED_DIV, device=self.device, dtype=torch.int64)
             ph = (v << ts) + (((v * 0x9E3779B1) & 0xFFFFFFFF) >> (32 - ts))   # == kernel's h
             idx = (ph[:, None] * TILE_ROWS + torch.arange(TILE_ROWS, device=self.device)).reshape(-1)
