@@ -294,27 +294,18 @@ class HbmIndexShard:
         thr = None
         m = self._seed_rows(n, k)
         mq = m and self._mq_ok(q_unit.shape[0], k, rows, dtype)
-        group = TILE_ROWS << self.MQ_TILE_SHIFT               # rows per 1-in-64 tile group
-        g_end = (n - self.MQ_TAIL_ROWS) // group if n > self.MQ_TAIL_ROWS else 0
-        if m and mq and g_end >= self.SEED_DIV:
-            # Threshold sample = one pseudo-random 64-row tile of every 64 in groups [0, g_end),
+        plan = self._tile_sample_plan(n) if (m and mq) else None
+        if plan is not None:
+            # Threshold sample = one pseudo-random 64-row tile of every 64 in the first nv groups,
             # scanned IN PLACE by the emitting kernel (gathering n/64 rows cost 0.45 ms at 100M),
             # plus every row after them -- the last 4096..8191 rows, where fresh inserts (often
             # a query's best matches) sit -- by the 256-query kernel.  Disjoint real rows, so the
             # k-th best of the union lower-bounds the final k-th score.
-            ts = self.MQ_TILE_SHIFT
-            nv = g_end                                         # one sampled tile per group
-            # virtual tile v reads physical tile (v << ts) + h(v) < nv << ts: inside the rows
-            if (nv << ts) * TILE_ROWS > n:   # (a launch past the rows would fault the GPU)
-                raise RuntimeError("tile sample past the visible rows")
-            v = torch.arange(0, nv, self.SEED_DIV, device=self.device, dtype=torch.int64)
-            ph = (v << ts) + (((v * 0x9E3779B1) & 0xFFFFFFFF) >> (32 - ts))   # == kernel's h
-            idx = (ph[:, None] * TILE_ROWS + torch.arange(TILE_ROWS, device=self.device)).reshape(-1)
+            ts, nv, t0, idx = plan
             sub = torch.index_select(self.rows, 0, idx)       # whole tiles: already tile-padded
             s0, _ = self._scan(sub.shape[0], q_unit, kmax, k, None, n_cus, sub, dtype)
             thr0 = s0[:, k - 1].contiguous() - self.MQ_THR_MARGIN
             pre_s, _ = self._scan_mq(nv * TILE_ROWS, q_unit, kmax, k, thr0, n_cus, tshift=ts)
-            t0 = g_end * group
             # (seeded with thr0 too: a tail row below it cannot enter the union's top k, whose
             # k-th best is the sample's, >= thr0; unseeded this small scan took 0.2 ms)
             tail_s, _ = self._scan(n - t0, q_unit, kmax, k, thr0, n_cus, self.rows[t0:], dtype)
@@ -353,6 +344,27 @@ class HbmIndexShard:
     MQ_THR_MARGIN = 2.0 ** -12
     MQ_TILE_SHIFT = 6         # threshold sample: one 64-row tile in 2^6
     MQ_TAIL_ROWS = 4096       # ... plus at least the last 4096 rows
+
+    def _tile_sample_plan(self, n: int):
+        """In-place threshold sample over n visible rows, or None when n is too small.
+
+        Returns (ts, nv, t0, idx): the emitting kernel's virtual tile v < nv reads physical tile
+        (v << ts) + h(v) (h = top ts bits of v * 0x9E3779B1, as in index_mq.hip), i.e. one tile
+        of each group of 2^ts; rows [t0, n) (4096..8191 of them) are the exact tail; idx are the
+        rows of every SEED_DIV-th sampled tile (the sub-sample that seeds the sample scan, a
+        subset of the sample).  Every sampled row lies below t0 <= n - MQ_TAIL_ROWS."""
+        ts = self.MQ_TILE_SHIFT
+        group = TILE_ROWS << ts                                # rows per tile group
+        nv = (n - self.MQ_TAIL_ROWS) // group if n > self.MQ_TAIL_ROWS else 0
+        if nv < self.SEED_DIV:
+            return None
+        t0 = nv * group
+        if t0 > n:   # (a launch past the rows would fault the GPU)
+            raise RuntimeError("tile sample past the visible rows")
+        v = torch.arange(0, nv, self.SEED_DIV, device=self.device, dtype=torch.int64)
+        ph = (v << ts) + (((v * 0x9E3779B1) & 0xFFFFFFFF) >> (32 - ts))
+        idx = (ph[:, None] * TILE_ROWS + torch.arange(TILE_ROWS, device=self.device)).reshape(-1)
+        return ts, nv, t0, idx
 
     def _mq_ok(self, NQ: int, k: int, rows, dtype: str) -> bool:
         return (self.scan_mq and dtype == "bf16" and self.dim == 384 and rows is self.rows

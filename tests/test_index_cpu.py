@@ -243,3 +243,32 @@ def test_prefilter_image_follows_every_write(tmp_path):
     assert torch.equal(sh2.rows8[:20], st.shard.rows8[:20])
     with pytest.raises(ValueError, match="prefilter"):
         HbmIndexShard(D, 8, device="cpu", dtype="fp8", prefilter="fp8")
+
+
+def test_tile_sample_plan_invariants():
+    """The emitting scan's in-place threshold sample (index/shard.py _tile_sample_plan, mirrored
+    by index_mq.hip's phys_tile): every sampled tile lies inside the rows and below the exact
+    tail, no tile is sampled twice (the sample's k-th best must be a lower bound), the gathered
+    sub-sample is a subset of the sample, and the tail holds 4096..8191 rows.  A violation here
+    is an out-of-bounds GPU read or an inexact search."""
+    import torch
+
+    from codename_symbiont_amd.index.shard import TILE_ROWS, HbmIndexShard
+
+    shard = HbmIndexShard(384, 64, device="cpu")
+    assert shard._tile_sample_plan(100_000) is None          # too small: gather-sample path
+    for n in (1 << 20, (1 << 20) + 777, (1 << 20) + 4096, 12_500_000, 12_502_048, 50_000_000,
+              100_000_000, 100_007_424, 2 ** 31 - 2 ** 20):
+        ts, nv, t0, idx = shard._tile_sample_plan(n)
+        assert ts == shard.MQ_TILE_SHIFT and nv >= shard.SEED_DIV
+        assert shard.MQ_TAIL_ROWS <= n - t0 < shard.MQ_TAIL_ROWS + (TILE_ROWS << ts)
+        v = torch.arange(nv, dtype=torch.int64)
+        # the kernel's mapping, in 32-bit arithmetic as on the GPU
+        h = ((v * 0x9E3779B1) & 0xFFFFFFFF) >> (32 - ts)
+        phys = (v << ts) + h
+        assert int(phys.min()) >= 0 and int(phys.max() + 1) * TILE_ROWS <= t0
+        assert len(torch.unique(phys)) == nv                  # one distinct tile per group
+        assert bool(((phys >> ts) == v).all())                # tile v stays in group v
+        sub_tiles = torch.unique(idx // TILE_ROWS)
+        assert idx.numel() == sub_tiles.numel() * TILE_ROWS
+        assert bool(torch.isin(sub_tiles, phys).all())        # sub-sample within the sample
