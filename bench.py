@@ -323,6 +323,12 @@ def main() -> None:
                 "index_rows": args.index_rows, "dim": cfg.hidden, "top_k": args.k,
                 "mode": args.mode,
                 "encode_search_overlap": overlap,
+                # per-rank scan kernel: the emitting MFMA scan (csrc/hip/index_mq.hip) for >= 256
+                # seeded queries (512 per workgroup at >= 512), else the 256-query list kernel
+                "index_scan": ("emitting-512q" if B * info.world >= 512 else "emitting-256q")
+                              if (shard.scan_mq and args.index_dtype == "bf16" and cfg.hidden == 384
+                                  and B * info.world >= shard.mq_min_nq and args.k <= 16)
+                              else "list-256q",
                 "encoder_hipgraph": use_graph,
             },
             "embeds_per_sec": round(total, 2) if args.mode != "search" else 0.0,
