@@ -81,78 +81,87 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(
 // add_ln: out[t] = LN(x[t] (+ res[t])) * gamma + beta.  Used after the MFMA GEMMs whose row is
 // too wide (H >= 768) for the GEMM's own fused LayerNorm epilogue.
 // ---------------------------------------------------------------------------------------------
+// LPT lanes per token (16 at H = 384, 32 at 768 / 1024): every lane holds exactly PER 16-byte
+// chunks of its token -- with one 64-lane wave per token, 768 / 1024-wide rows left half the lanes
+// idle on the last chunk (2.9 TB/s at bge's 32768 x 768).  Sums reduce over the token's LPT lanes.
 template <int H>
 __global__ __launch_bounds__(256) void add_ln_kernel(
     const __bf16* __restrict__ x_in, const __bf16* __restrict__ res,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
     __bf16* __restrict__ out, int T, uint8_t* __restrict__ out8, float* __restrict__ scale8) {
-  constexpr int NV = H / 8;
-  constexpr int PER = (NV + 63) / 64;
-  const int lane = threadIdx.x & 63;
-  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (t >= T) return;
+  constexpr int NV = H / 8;                          // 16-byte chunks per row
+  constexpr int LPT = H == 384 ? 16 : 32;
+  constexpr int PER = NV / LPT;
+  static_assert(NV % LPT == 0, "row must split evenly over the token's lanes");
+  const int sl = threadIdx.x & (LPT - 1);
+  const int t = (blockIdx.x * 256 + threadIdx.x) / LPT;
+  if (t >= T) return;                                // whole token groups leave together
+  auto group_sum = [](float v) {
+#pragma unroll
+    for (int m = LPT / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+    return v;
+  };
   float x[PER][8];
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
-    const int v = lane + 64 * i;
+    const int v = sl + LPT * i;
+    load8(x_in + (size_t)t * H + v * 8, x[i]);
+    if (res) {
+      float r[8];
+      load8(res + (size_t)t * H + v * 8, r);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) x[i][e] = 0.f;
-    if (v < NV) {
-      load8(x_in + (size_t)t * H + v * 8, x[i]);
-      if (res) {
-        float r[8];
-        load8(res + (size_t)t * H + v * 8, r);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) x[i][e] += r[e];
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) s += x[i][e];
+      for (int e = 0; e < 8; ++e) x[i][e] += r[e];
     }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += x[i][e];
   }
-  const float mean = wave_sum(s) * (1.0f / H);
+  const float mean = group_sum(s) * (1.0f / H);
   float ss = 0.f;
 #pragma unroll
   for (int i = 0; i < PER; ++i)
-    if (lane + 64 * i < NV)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float d = x[i][e] - mean;
-        ss += d * d;
-      }
-  const float rstd = rsqrtf(wave_sum(ss) * (1.0f / H) + eps);
+    for (int e = 0; e < 8; ++e) {
+      const float d = x[i][e] - mean;
+      ss += d * d;
+    }
+  const float rstd = rsqrtf(group_sum(ss) * (1.0f / H) + eps);
   float amax = 0.f;
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
-    const int v = lane + 64 * i;
-    if (v < NV) {
+    const int v = sl + LPT * i;
+    const f32x4 g0 = *reinterpret_cast<const f32x4*>(gamma + v * 8);
+    const f32x4 g1 = *reinterpret_cast<const f32x4*>(gamma + v * 8 + 4);
+    const f32x4 b0 = *reinterpret_cast<const f32x4*>(beta + v * 8);
+    const f32x4 b1 = *reinterpret_cast<const f32x4*>(beta + v * 8 + 4);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        x[i][e] = (x[i][e] - mean) * rstd * gamma[v * 8 + e] + beta[v * 8 + e];
-        amax = fmaxf(amax, fabsf(x[i][e]));
-      }
-      store8(out + (size_t)t * H + v * 8, x[i]);
+    for (int e = 0; e < 4; ++e) {
+      x[i][e] = (x[i][e] - mean) * rstd * g0[e] + b0[e];
+      x[i][e + 4] = (x[i][e + 4] - mean) * rstd * g1[e] + b1[e];
     }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(x[i][e]));
+    store8(out + (size_t)t * H + v * 8, x[i]);
   }
   if (!out8) return;
   // fused per-token e4m3 quantiser for the next fp8 GEMM (same scale rule as
   // quant_rows_fp8_kernel: scale = amax / 448), from the fp32 LN output
-  amax = fmaxf(wave_max(amax), 1e-12f);
+#pragma unroll
+  for (int m = LPT / 2; m >= 1; m >>= 1) amax = fmaxf(amax, __shfl_xor(amax, m, 64));
+  amax = fmaxf(amax, 1e-12f);
   const float inv = 448.f / amax;
-  if (lane == 0) scale8[t] = amax / 448.f;
+  if (sl == 0) scale8[t] = amax / 448.f;
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
-    const int v = lane + 64 * i;
-    if (v < NV) {
-      float q[8];
+    const int v = sl + LPT * i;
+    float q[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) q[e] = x[i][e] * inv;
-      int lo = __builtin_amdgcn_cvt_pk_fp8_f32(q[0], q[1], 0, false);
-      lo = __builtin_amdgcn_cvt_pk_fp8_f32(q[2], q[3], lo, true);
-      int hi = __builtin_amdgcn_cvt_pk_fp8_f32(q[4], q[5], 0, false);
-      hi = __builtin_amdgcn_cvt_pk_fp8_f32(q[6], q[7], hi, true);
-      *reinterpret_cast<int2*>(out8 + (size_t)t * H + v * 8) = make_int2(lo, hi);
-    }
+    for (int e = 0; e < 8; ++e) q[e] = x[i][e] * inv;
+    int lo = __builtin_amdgcn_cvt_pk_fp8_f32(q[0], q[1], 0, false);
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(q[2], q[3], lo, true);
+    int hi = __builtin_amdgcn_cvt_pk_fp8_f32(q[4], q[5], 0, false);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(q[6], q[7], hi, true);
+    *reinterpret_cast<int2*>(out8 + (size_t)t * H + v * 8) = make_int2(lo, hi);
   }
 }
 
@@ -287,7 +296,8 @@ int symb_add_ln(const void* x, const void* res, const float* g, const float* b, 
                 void* out, int T, int H, hipStream_t st, void* out8, float* scale8) {
   if (T <= 0) return 0;
   if ((out8 == nullptr) != (scale8 == nullptr)) return -1;
-  dim3 grid((T + 3) / 4);
+  const int tpb = 256 / (H == 384 ? 16 : 32);   // tokens per block (add_ln_kernel's LPT)
+  dim3 grid((T + tpb - 1) / tpb);
   SYMB_H_DISPATCH(H, hipLaunchKernelGGL(add_ln_kernel<HH>, grid, dim3(256), 0, st,
                                         (const __bf16*)x, (const __bf16*)res, g, b, eps,
                                         (__bf16*)out, T, (uint8_t*)out8, scale8));
