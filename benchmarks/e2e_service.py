@@ -50,6 +50,35 @@ def _sentences(n: int, seed: int, model: str) -> list[str]:
             for _ in range(n)]
 
 
+def _requests(queries: list[str], endpoint: str) -> list[bytes]:
+    out = []
+    for q in queries:
+        if endpoint == "health":
+            out.append(b"GET /api/health HTTP/1.1\r\nHost: bench\r\n\r\n")
+            continue
+        body = json.dumps({"query_text": q, "top_k": 10}).encode()
+        out.append(b"POST /api/search/semantic HTTP/1.1\r\nHost: bench\r\n"
+                   b"Content-Type: application/json\r\nContent-Length: "
+                   + str(len(body)).encode() + b"\r\n\r\n" + body)
+    return out
+
+
+def _client_native(url: str, queries: list[str], conc: int, out, endpoint: str = "search") -> None:
+    """C++ epoll client (csrc/native/loadgen.cpp, GIL released): requests pre-built, one in flight
+    per keep-alive connection, latency from first byte written to last byte read."""
+    try:
+        sys.path.insert(0, ROOT)
+        from codename_symbiont_amd.ops._ext import native
+
+        host, port = url.split("//")[1].split(":")
+        r = native().http_load(host, int(port), _requests(queries, endpoint), conc, 300.0)
+        if r["errors"] or r["non200"]:
+            raise RuntimeError(f"{r['errors']} transport errors, {r['non200']} non-200 replies")
+        out.put((list(r["latency_s"]), r["t_start"], r["t_end"]))
+    except BaseException as e:   # never leave the parent waiting on a dead client
+        out.put(("error", repr(e)))
+
+
 def _client(url: str, queries: list[str], conc: int, out, endpoint: str = "search") -> None:
     """Raw asyncio HTTP/1.1 keep-alive client (httpx's per-request cost capped the first version
     of this benchmark at ~420 req/s even on /api/health; one gateway worker serves ~6.5k req/s
@@ -126,6 +155,8 @@ def main():
                     help="native: C++ gateway (worker threads); py: asyncio gateway (worker processes)")
     ap.add_argument("--broker-impl", choices=["native", "py"], default="native")
     ap.add_argument("--endpoint", choices=["search", "health"], default="search")
+    ap.add_argument("--client", choices=["native", "py"], default="native",
+                    help="load generator: C++ epoll (csrc/native/loadgen.cpp) or asyncio")
     a = ap.parse_args()
     py = sys.executable
     bport, aport = _port(), _port()
@@ -181,8 +212,9 @@ def main():
         # ---------------- search
         q = mp.get_context("spawn").Queue()
         per = [queries[i::a.clients] for i in range(a.clients)]
-        cl = [mp.get_context("spawn").Process(target=_client, args=(api, p, a.concurrency, q,
-                                                                     a.endpoint))
+        target = _client_native if a.client == "native" else _client
+        cl = [mp.get_context("spawn").Process(target=target, args=(api, p, a.concurrency, q,
+                                                                    a.endpoint))
               for p in per]
         for p in cl:
             p.start()
@@ -223,7 +255,8 @@ def main():
                               "p99": round(1e3 * lat[int(0.99 * (len(lat) - 1))], 2)},
         "config": {"model": a.model, "index_rows": a.index_rows + a.docs * a.sentences,
                    "docs": a.docs, "sentences_per_doc": a.sentences, "requests": len(lat),
-                   "clients": a.clients, "concurrency_per_client": a.concurrency, "top_k": 10,
+                   "clients": a.clients, "client_impl": a.client,
+                   "concurrency_per_client": a.concurrency, "top_k": 10,
                    "deployment": f"{a.broker_impl} broker + preprocessing + vector_memory + "
                                  f"{a.api_impl} gateway x {a.api_workers} workers"},
         "endpoint": a.endpoint,

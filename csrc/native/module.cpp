@@ -11,6 +11,7 @@ void register_html(py::module_& m);
 void register_packstream(py::module_& m);
 void register_natsd(py::module_& m);
 void register_gateway(py::module_& m);
+void register_loadgen(py::module_& m);
 }  // namespace symbn
 
 PYBIND11_MODULE(_native, m) {
@@ -23,4 +24,5 @@ PYBIND11_MODULE(_native, m) {
   symbn::register_packstream(m);
   symbn::register_natsd(m);
   symbn::register_gateway(m);
+  symbn::register_loadgen(m);
 }

@@ -146,3 +146,47 @@ def test_html_priority_and_body_fallback():
     assert t == "Заголовок\nПривет"
     t, _ = extract_html_text("<div role='main'><ul><li>a<li>b</ul><p>x <span>y</span></p></div>")
     assert t.split("\n") == ["x y", "a", "b", "y"]
+
+
+def test_http_load_generator_frames_keepalive_responses():
+    """csrc/native/loadgen.cpp (the e2e benchmark's client): every pre-built request is answered
+    over keep-alive connections, responses are framed by Content-Length (bodies split across
+    reads), non-200 replies are counted, not timed."""
+    import asyncio
+    import threading
+
+    from codename_symbiont_amd.ops._ext import native
+
+    ready = threading.Event()
+    port_box = {}
+
+    async def handle(reader, writer):
+        try:
+            while True:
+                head = await reader.readuntil(b"\r\n\r\n")
+                status = b"404 Not Found" if b"/missing" in head else b"200 OK"
+                body = b'{"pad":"' + b"x" * 70000 + b'"}'   # larger than one 64 KiB read
+                writer.write(b"HTTP/1.1 " + status + b"\r\nContent-Length: "
+                             + str(len(body)).encode() + b"\r\n\r\n" + body[:1000])
+                await writer.drain()
+                writer.write(body[1000:])
+                await writer.drain()
+        except (asyncio.IncompleteReadError, ConnectionError):
+            writer.close()
+
+    def serve():
+        loop = asyncio.new_event_loop()
+        srv = loop.run_until_complete(asyncio.start_server(handle, "127.0.0.1", 0))
+        port_box["port"] = srv.sockets[0].getsockname()[1]
+        port_box["loop"] = loop
+        ready.set()
+        loop.run_forever()
+
+    threading.Thread(target=serve, daemon=True).start()
+    assert ready.wait(10)
+    reqs = [b"GET /ok HTTP/1.1\r\nHost: t\r\n\r\n"] * 300 + [b"GET /missing HTTP/1.1\r\nHost: t\r\n\r\n"] * 5
+    r = native().http_load("127.0.0.1", port_box["port"], reqs, 7, 30.0)
+    port_box["loop"].call_soon_threadsafe(port_box["loop"].stop)
+    assert r["errors"] == 0 and r["non200"] == 5
+    assert len(r["latency_s"]) == 300 and min(r["latency_s"]) > 0
+    assert r["t_end"] >= r["t_start"]
