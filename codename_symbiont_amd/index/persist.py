@@ -207,7 +207,16 @@ def save_snapshot(shard: HbmIndexShard, directory: str, chunk: int = 1 << 20,
         fsync_file(os.path.join(tmp, "vectors.npy"))
     with open(os.path.join(tmp, "payloads.jsonl"), "w", encoding="utf-8") as f:
         ps = shard.payloads
+        empty = None
         for r in range(n):
+            if r not in ps.fields and r not in ps.point_ids:   # row without point (synthetic)
+                if empty is None:
+                    pid, p = ps.get(r)
+                    empty = json.dumps([pid, p.original_document_id, p.source_url,
+                                        p.sentence_text, p.sentence_order, p.model_name,
+                                        p.processed_at_ms], ensure_ascii=False) + "\n"
+                f.write(empty)
+                continue
             pid, p = ps.get(r)
             f.write(json.dumps([pid, p.original_document_id, p.source_url, p.sentence_text,
                                 p.sentence_order, p.model_name, p.processed_at_ms],
@@ -259,8 +268,14 @@ def load_snapshot(shard: HbmIndexShard, directory: str, chunk: int = 1 << 20) ->
         shard.rows[r0 + s:r0 + e].copy_(t.to(shard.device))
     shard.rows_written(r0, n)   # the fp8 prefilter image, if the shard keeps one
     with open(os.path.join(snap, "payloads.jsonl"), encoding="utf-8") as f:
+        empty = None
         for r, line in enumerate(f):
+            if line == empty:          # a row without point id or payload: nothing to store
+                continue
             a = json.loads(line)
+            if a[0] is None and a[1:] == ["", "", "", 0, "", 0]:
+                empty = line
+                continue
             shard.payloads.set(r0 + r, a[0], Payload(*a[1:]))
     shard.publish()
     return n

@@ -43,43 +43,64 @@ class Payload:
 
 
 class PayloadStore:
-    """Columnar host store: row -> (point id, payload fields).  Rows without payload are allowed
-    (synthetic benchmark rows) and decode to the reference's defaults ("" / 0, main.rs:337-390)."""
+    """Host store: row -> (point id, payload fields), SPARSE -- only rows that carry a point id
+    or a payload are held (dicts keyed by row).  Rows without payload (synthetic benchmark rows,
+    often the bulk of a 100M-row shard) cost nothing here and decode to the reference's defaults
+    ("" / 0, main.rs:337-390).  A dense layout kept 7 Python lists of n slots: 560 MB of list
+    pointers per 10M rows, traversed by every full GC pass of the service process (the e2e
+    benchmark's ~100 ms tail)."""
 
     FIELDS = ("original_document_id", "source_url", "sentence_text", "sentence_order",
               "model_name", "processed_at_ms")
 
     def __init__(self):
-        self.point_ids: list[str | None] = []
-        self.cols: dict[str, list] = {f: [] for f in self.FIELDS}
+        self.n = 0
+        self.point_ids: dict[int, str] = {}          # row -> point id
+        self.fields: dict[int, tuple] = {}           # row -> payload field tuple (FIELDS order)
         self.id_to_row: dict[str, int] = {}
 
     def __len__(self):
-        return len(self.point_ids)
+        return self.n
 
     def extend_empty(self, n: int) -> None:
-        self.point_ids.extend([None] * n)
-        for f in self.FIELDS:
-            self.cols[f].extend([None] * n)
+        self.n += n
 
     def set(self, row: int, point_id: str | None, payload: Payload | None) -> None:
-        old = self.point_ids[row]
+        if not 0 <= row < self.n:
+            raise IndexError(f"row {row} outside the store ({self.n} rows)")
+        old = self.point_ids.pop(row, None)
         if old is not None and self.id_to_row.get(old) == row:
             del self.id_to_row[old]
-        self.point_ids[row] = point_id
         if point_id is not None:
+            self.point_ids[row] = point_id
             self.id_to_row[point_id] = row
-        for f in self.FIELDS:
-            self.cols[f][row] = getattr(payload, f) if payload is not None else None
+        if payload is not None:
+            self.fields[row] = tuple(getattr(payload, f) for f in self.FIELDS)
+        else:
+            self.fields.pop(row, None)
 
     def get(self, row: int) -> tuple[str | None, Payload]:
+        t = self.fields.get(row)
+        if t is None:
+            return self.point_ids.get(row), Payload()
         vals = {}
-        for f in self.FIELDS:
-            v = self.cols[f][row]
+        for f, v in zip(self.FIELDS, t):
             if v is None:
                 v = 0 if f in ("sentence_order", "processed_at_ms") else ""
             vals[f] = v
-        return self.point_ids[row], Payload(**vals)
+        return self.point_ids.get(row), Payload(**vals)
+
+    def truncate(self, n: int) -> None:
+        """Forget rows >= n."""
+        if n >= self.n:
+            return
+        for r in [r for r in self.point_ids if r >= n]:
+            pid = self.point_ids.pop(r)
+            if self.id_to_row.get(pid) == r:
+                del self.id_to_row[pid]
+        for r in [r for r in self.fields if r >= n]:
+            del self.fields[r]
+        self.n = n
 
 
 FP8_SCALE = 256.0  # == ops.kernels.FP8_SCALE (kept import-free for CPU-only users)
@@ -156,14 +177,7 @@ class HbmIndexShard:
         """Forget rows >= n (their payload slots too)."""
         if n >= self.count:
             return
-        ps = self.payloads
-        for r in range(n, self.count):
-            pid = ps.point_ids[r]
-            if pid is not None and ps.id_to_row.get(pid) == r:
-                del ps.id_to_row[pid]
-        del ps.point_ids[n:]
-        for f in ps.FIELDS:
-            del ps.cols[f][n:]
+        self.payloads.truncate(n)
         self.count = n
         self.visible = min(self.visible, n)
 

@@ -12,6 +12,7 @@ a metrics registry (exposed by the api service on ``GET /api/metrics`` and publi
 from __future__ import annotations
 
 import asyncio
+import gc
 import os
 import json
 import logging
@@ -200,6 +201,12 @@ class Service:
 
     async def run_forever(self) -> None:
         await self.start()
+        # (service processes only) everything allocated while booting -- model weights' Python
+        # wrappers, tokenizer tables, the index's host state -- lives as long as the process:
+        # move it out of the collector's generations so full collections during serving only
+        # walk per-request garbage
+        gc.collect()
+        gc.freeze()
         try:
             await self.wait()
         finally:
