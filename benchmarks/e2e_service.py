@@ -63,15 +63,19 @@ def _requests(queries: list[str], endpoint: str) -> list[bytes]:
     return out
 
 
-def _client_native(url: str, queries: list[str], conc: int, out, endpoint: str = "search") -> None:
+def _client_native(url: str, queries: list[str], conc: int, out, endpoint: str = "search",
+                   warmup: int = 0) -> None:
     """C++ epoll client (csrc/native/loadgen.cpp, GIL released): requests pre-built, one in flight
-    per keep-alive connection, latency from first byte written to last byte read."""
+    per keep-alive connection, latency from first byte written to last byte read.  The first
+    ``warmup`` requests run untimed (first full-size bursts: allocator growth, cold caches)."""
     try:
         sys.path.insert(0, ROOT)
         from codename_symbiont_amd.ops._ext import native
 
         host, port = url.split("//")[1].split(":")
-        r = native().http_load(host, int(port), _requests(queries, endpoint), conc, 300.0)
+        if warmup:
+            native().http_load(host, int(port), _requests(queries[:warmup], endpoint), conc, 300.0)
+        r = native().http_load(host, int(port), _requests(queries[warmup:], endpoint), conc, 300.0)
         if r["errors"] or r["non200"]:
             raise RuntimeError(f"{r['errors']} transport errors, {r['non200']} non-200 replies")
         out.put((list(r["latency_s"]), r["t_start"], r["t_end"]))
@@ -157,6 +161,8 @@ def main():
     ap.add_argument("--endpoint", choices=["search", "health"], default="search")
     ap.add_argument("--client", choices=["native", "py"], default="native",
                     help="load generator: C++ epoll (csrc/native/loadgen.cpp) or asyncio")
+    ap.add_argument("--warmup-requests", type=int, default=2000,
+                    help="native client: untimed requests first (split over the clients)")
     a = ap.parse_args()
     py = sys.executable
     bport, aport = _port(), _port()
@@ -194,7 +200,8 @@ def main():
             time.sleep(1.0)
         print(f"[e2e] services up in {time.time() - t_boot:.1f}s", file=sys.stderr, flush=True)
         # ---------------- ingest
-        sents = _sentences(a.docs * a.sentences + a.requests, 0, a.model)
+        warm = a.warmup_requests if a.client == "native" else 0
+        sents = _sentences(a.docs * a.sentences + a.requests + warm, 0, a.model)
         docs = [" ".join(sents[i * a.sentences:(i + 1) * a.sentences]) for i in range(a.docs)]
         queries = sents[a.docs * a.sentences:]
         t0 = time.perf_counter()
@@ -212,10 +219,14 @@ def main():
         # ---------------- search
         q = mp.get_context("spawn").Queue()
         per = [queries[i::a.clients] for i in range(a.clients)]
-        target = _client_native if a.client == "native" else _client
-        cl = [mp.get_context("spawn").Process(target=target, args=(api, p, a.concurrency, q,
-                                                                    a.endpoint))
-              for p in per]
+        if a.client == "native":
+            cl = [mp.get_context("spawn").Process(
+                target=_client_native, args=(api, p, a.concurrency, q, a.endpoint,
+                                             warm // a.clients)) for p in per]
+        else:
+            cl = [mp.get_context("spawn").Process(target=_client, args=(api, p, a.concurrency, q,
+                                                                        a.endpoint))
+                  for p in per]
         for p in cl:
             p.start()
         res = []
@@ -255,7 +266,7 @@ def main():
                               "p99": round(1e3 * lat[int(0.99 * (len(lat) - 1))], 2)},
         "config": {"model": a.model, "index_rows": a.index_rows + a.docs * a.sentences,
                    "docs": a.docs, "sentences_per_doc": a.sentences, "requests": len(lat),
-                   "clients": a.clients, "client_impl": a.client,
+                   "clients": a.clients, "client_impl": a.client, "warmup_requests": warm,
                    "concurrency_per_client": a.concurrency, "top_k": 10,
                    "deployment": f"{a.broker_impl} broker + preprocessing + vector_memory + "
                                  f"{a.api_impl} gateway x {a.api_workers} workers"},
