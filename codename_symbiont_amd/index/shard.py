@@ -9,7 +9,7 @@ Layout here: one contiguous bf16 slab ``rows[capacity_pad, D]`` of UNIT vectors 
 dot product), sized up front for the shard (288 GB of HBM per MI355X holds 100M x 384 bf16 =
 76.8 GB with room to spare), rows appended in place; the fused HIP scan (``_hip.index_scan``)
 streams the slab once per query batch and never materialises scores.  Point ids and payloads
-live host-side in a columnar ``PayloadStore`` indexed by row.
+live host-side in a sparse ``PayloadStore`` keyed by row (rows without a point cost nothing).
 """
 from __future__ import annotations
 
