@@ -163,6 +163,8 @@ def main():
                     help="load generator: C++ epoll (csrc/native/loadgen.cpp) or asyncio")
     ap.add_argument("--warmup-requests", type=int, default=2000,
                     help="native client: untimed requests first (split over the clients)")
+    ap.add_argument("--idle-requests", type=int, default=300,
+                    help="after the load phase: this many requests one at a time (unloaded latency)")
     a = ap.parse_args()
     py = sys.executable
     bport, aport = _port(), _port()
@@ -246,6 +248,17 @@ def main():
         lat = sorted(x for r in res for x in r[0])
         t_search = max(r[2] for r in res) - min(r[1] for r in res)
         m = _metrics(api)
+        # ---------------- unloaded latency: one connection, one request in flight
+        idle = []
+        if a.idle_requests:
+            from codename_symbiont_amd.ops._ext import native
+
+            host, port = api.split("//")[1].split(":")
+            r = native().http_load(host, int(port),
+                                   _requests(queries[:a.idle_requests], a.endpoint), 1, 300.0)
+            if r["errors"] or r["non200"]:
+                raise RuntimeError(f"idle phase: {r['errors']} errors, {r['non200']} non-200")
+            idle = sorted(r["latency_s"])
     finally:   # each service leads its own process group (gateway workers included)
         for p in reversed(procs):
             try:
@@ -264,6 +277,9 @@ def main():
         "ingest_sentences_per_s": round(a.docs * a.sentences / t_ingest, 1),
         "search_latency_ms": {"p50": round(1e3 * statistics.median(lat), 2),
                               "p99": round(1e3 * lat[int(0.99 * (len(lat) - 1))], 2)},
+        "idle_latency_ms": ({"p50": round(1e3 * statistics.median(idle), 2),
+                             "p99": round(1e3 * idle[int(0.99 * (len(idle) - 1))], 2),
+                             "n": len(idle)} if idle else None),
         "config": {"model": a.model, "index_rows": a.index_rows + a.docs * a.sentences,
                    "docs": a.docs, "sentences_per_doc": a.sentences, "requests": len(lat),
                    "clients": a.clients, "client_impl": a.client, "warmup_requests": warm,

@@ -6,6 +6,10 @@ handles every query with its own B=1 forward (embedding_generator.rs:146, prepro
 any number of handlers are coalesced (up to a token budget / a short window) into ONE packed
 varlen launch executed off the event loop, and the results are scattered back to the callers.
 The same pattern batches concurrent semantic searches into one fused index scan.
+
+The collection window only applies under load: a request that finds the batcher idle (no launch
+ended within the last window) goes out with whatever is already queued, so an unloaded query pays
+no batching delay.  Under load the next batch forms while the previous launch runs anyway.
 """
 from __future__ import annotations
 
@@ -26,6 +30,27 @@ class _Req:
     t0: float = field(default_factory=time.perf_counter)
 
 
+async def _collect(q: asyncio.Queue, first, window: float, last_end: float, full) -> list:
+    """``first`` plus everything already queued; then, if a launch ended less than ``window`` ago
+    (the batcher is busy), keep collecting until ``window`` after ``first`` or ``full(batch)``."""
+    loop = asyncio.get_running_loop()
+    batch = [first]
+    while not full(batch) and not q.empty():
+        batch.append(q.get_nowait())
+    if loop.time() - last_end >= window:
+        return batch
+    deadline = loop.time() + window
+    while not full(batch):
+        timeout = deadline - loop.time()
+        if timeout <= 0:
+            break
+        try:
+            batch.append(await asyncio.wait_for(q.get(), timeout))
+        except asyncio.TimeoutError:
+            break
+    return batch
+
+
 class EmbedBatcher:
     def __init__(self, encoder, tokenizer, token_budget: int = 65536, window_ms: float = 2.0,
                  max_seqs: int = 4096, metrics=None):
@@ -38,6 +63,7 @@ class EmbedBatcher:
         self._q: asyncio.Queue = asyncio.Queue()
         self._task: asyncio.Task | None = None
         self._lock = asyncio.Lock()
+        self._last_end = float("-inf")   # loop time the last launch finished
 
     def start(self) -> None:
         if self._task is None:
@@ -56,27 +82,18 @@ class EmbedBatcher:
         loop = asyncio.get_running_loop()
         while True:
             first = await self._q.get()
-            batch = [first]
-            n = len(first.texts)
-            deadline = loop.time() + self.window
-            while n < self.max_seqs:
-                timeout = deadline - loop.time()
-                if timeout <= 0:
-                    break
-                try:
-                    r = await asyncio.wait_for(self._q.get(), timeout)
-                except asyncio.TimeoutError:
-                    break
-                batch.append(r)
-                n += len(r.texts)
+            batch = await _collect(self._q, first, self.window, self._last_end,
+                                   lambda b: sum(len(r.texts) for r in b) >= self.max_seqs)
             texts = [t for r in batch for t in r.texts]
             try:
                 out = await loop.run_in_executor(None, self._encode_all, texts)
             except Exception as e:  # propagate to every waiter
+                self._last_end = loop.time()
                 for r in batch:
                     if not r.fut.done():
                         r.fut.set_exception(e)
                 continue
+            self._last_end = loop.time()
             o = 0
             for r in batch:
                 if not r.fut.done():
@@ -188,6 +205,7 @@ class SearchBatcher:
         self.metrics = metrics
         self._q: asyncio.Queue = asyncio.Queue()
         self._task = None
+        self._last_end = float("-inf")
 
     async def search(self, q: np.ndarray, k: int):
         if self._task is None:
@@ -204,26 +222,20 @@ class SearchBatcher:
         loop = asyncio.get_running_loop()
         while True:
             first = await self._q.get()
-            batch = [first]
-            deadline = loop.time() + self.window
-            while len(batch) < self.max_q:
-                timeout = deadline - loop.time()
-                if timeout <= 0:
-                    break
-                try:
-                    batch.append(await asyncio.wait_for(self._q.get(), timeout))
-                except asyncio.TimeoutError:
-                    break
+            batch = await _collect(self._q, first, self.window, self._last_end,
+                                   lambda b: len(b) >= self.max_q)
             kmax = max(r.k for r in batch)
             qs = np.concatenate([r.q for r in batch], 0)
             try:
                 s, i = await loop.run_in_executor(None, self._timed_search, qs, kmax)
             except Exception as e:
+                self._last_end = loop.time()
                 for j, r in enumerate(batch):
                     if not r.fut.done():
                         # a partial-result error carries per-query rows: give each its own slice
                         r.fut.set_exception(e.take(j, r.k) if hasattr(e, "take") else e)
                 continue
+            self._last_end = loop.time()
             for j, r in enumerate(batch):
                 if not r.fut.done():
                     r.fut.set_result((s[j, :r.k], i[j, :r.k]))

@@ -127,3 +127,32 @@ def test_embed_batcher_failure_reaches_every_waiter():
     res, ok = asyncio.run(asyncio.wait_for(main(), 10))
     assert all(isinstance(r, RuntimeError) and "encoder failed" in str(r) for r in res)
     assert ok[0].shape == (0, 8)
+
+
+def test_idle_request_skips_window_busy_requests_coalesce():
+    """An unloaded request goes out at once (no batching delay); one that arrives while a launch
+    just ended waits the window and is coalesced with the requests behind it."""
+    import time
+
+    launches = []
+
+    def search_fn(q, k):
+        launches.append(len(q))
+        return np.zeros((len(q), k), np.float32), np.zeros((len(q), k), np.int64)
+
+    async def main():
+        b = SearchBatcher(search_fn, window_ms=300.0, max_q=64)
+        t0 = time.perf_counter()
+        await b.search(np.ones(4, np.float32), 1)          # idle: no 300 ms wait
+        idle_s = time.perf_counter() - t0
+
+        async def late(d):
+            await asyncio.sleep(d)
+            return await b.search(np.ones(4, np.float32), 1)
+        # right after a launch ended: the first waits the window, the later two join it
+        await asyncio.gather(late(0.0), late(0.05), late(0.1))
+        b._task.cancel()
+        return idle_s
+    idle_s = asyncio.run(asyncio.wait_for(main(), 10))
+    assert idle_s < 0.2
+    assert launches == [1, 3]
