@@ -106,8 +106,9 @@ def cmd_scanmq(a):
 
     shard.mq_min_nq = min(shard.mq_min_nq, a.nq)
 
-    def srch(mq):
+    def srch(mq, rsplit=True):
         shard.scan_mq = mq
+        shard.mq_rsplit = rsplit
         return shard.search(q, k)
 
     ref = srch(False)
@@ -116,8 +117,14 @@ def cmd_scanmq(a):
     cnt, ovf = shard._mq_last
     ids_equal = float((ref[1] == got[1]).float().mean())
     max_score_diff = float((ref[0] - got[0]).abs().max())
-    r = ab({"list256": lambda: srch(False), "mq512": lambda: srch(True)}, rounds=a.rounds,
-           iters=a.iters)
+    variants = {"list256": lambda: srch(False), "mq512": lambda: srch(True)}
+    if a.nq < 512:   # the two 256-query forms: row-split 4-set ("mq512") and 2-set
+        got2 = srch(True, False)
+        torch.cuda.synchronize()
+        ids_equal = min(ids_equal, float((ref[1] == got2[1]).float().mean()))
+        max_score_diff = max(max_score_diff, float((ref[0] - got2[0]).abs().max()))
+        variants["mq_2set"] = lambda: srch(True, False)
+    r = ab(variants, rounds=a.rounds, iters=a.iters)
     flop = 2 * shard.visible * D * a.nq
     out = {n: dict(ms=round(m, 3), min_ms=round(mn, 3), TFLOPs=round(flop / (m / 1e3) / 1e12))
            for n, (m, mn) in r.items()}
@@ -142,7 +149,7 @@ def cmd_scanmqabl(a):
     ms, sample = shard._block_sample(n)
     pre_s, _ = shard._scan(ms, q, 16, k, None, None, sample, "bf16")
     thr = pre_s[:, k - 1].contiguous() - shard.MQ_THR_MARGIN
-    n_qblk = math.ceil(a.nq / h.mq_queries_per_blk())
+    n_qblk = math.ceil(a.nq / h.mq_queries_per_blk(a.sets, a.rsplit))
     ncu = torch.cuda.get_device_properties(0).multi_processor_count
     n_rblk = max(1, round(ncu / n_qblk))
     rpb = _round_up(math.ceil(n / n_rblk), TILE_ROWS)
@@ -156,10 +163,14 @@ def cmd_scanmqabl(a):
     def run(abl):
         h.index_scan_mq_ablate(shard.rows.data_ptr(), n, rpb, n_rblk, q.data_ptr(), a.nq,
                                thr.data_ptr(), cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(), cap,
-                               1, st, abl)
-    r = ab({f"abl{m}": (lambda m=m: run(m)) for m in (0, 1, 2)}, rounds=a.rounds, iters=a.iters)
+                               1, st, abl, a.sets, a.rsplit)
+    variants = {f"abl{m}": (lambda m=m: run(m)) for m in (0, 1, 2, 4)}
+    flat = shard.rows[:n].view(torch.int64)
+    variants["torch_int64_sum"] = lambda: flat.sum()   # plain streaming read of the same bytes
+    r = ab(variants, rounds=a.rounds, iters=a.iters)
     flop = 2 * n * D * a.nq
-    out = {nm: dict(ms=round(m, 3), TFLOPs=round(flop / (m / 1e3) / 1e12)) for nm, (m, _) in r.items()}
+    out = {nm: dict(ms=round(m, 3), TFLOPs=round(flop / (m / 1e3) / 1e12),
+                    TBps=round(n * D * 2 / (m / 1e3) / 1e12, 2)) for nm, (m, _) in r.items()}
     timeit(lambda: run(3), 10)
     run(3)
     torch.cuda.synchronize()
@@ -167,7 +178,8 @@ def cmd_scanmqabl(a):
     ghz = (st_[:, 0] / st_[:, 1] * 0.1).median().item()
     out["in_kernel_clock_GHz"] = round(ghz, 3)
     out["cycles_per_tile"] = round((st_[:, 0] / math.ceil(rpb / TILE_ROWS)).median().item(), 1)
-    print(json.dumps({"bench": "scanmq_ablation", "rows": n, "nq": a.nq, "results": out}))
+    print(json.dumps({"bench": "scanmq_ablation", "rows": n, "nq": a.nq, "sets": a.sets, "rsplit": a.rsplit,
+                      "n_rblk": n_rblk, "n_qblk": n_qblk, "results": out}))
 
 
 def cmd_scanabl(a):
@@ -517,6 +529,8 @@ def main():
     ap.add_argument("--precision", default="bf16", help="encoder: comma list of bf16,fp8")
     ap.add_argument("--tiles", default="3", help="encoder: comma list of gemm_config tile modes")
     ap.add_argument("--fp8-waves", default="8", help="encoder: comma list of fp8 GEMM wave counts")
+    ap.add_argument("--sets", type=int, default=4, help="scanmqabl: 16-query sets per wave (2 or 4)")
+    ap.add_argument("--rsplit", type=int, default=1, help="scanmqabl: waves per query group (1, 2)")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=5)
     a = ap.parse_args()

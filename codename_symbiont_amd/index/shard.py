@@ -160,7 +160,10 @@ class HbmIndexShard:
         # at N >= 2 GPUs): the 512-query-per-workgroup candidate-emitting kernel (index_mq.hip)
         self.scan_cus = 0      # 0 = every CU (see _n_cus)
         self.scan_mq = True
-        self.mq_min_nq = 256   # smallest batch for the emitting kernel (< 512: its 2-set form)
+        self.mq_min_nq = 256   # smallest batch for the emitting kernel (< 512: a 256-query form)
+        # 256-query form: True = 4 query sets per wave, waves w / w + 4 splitting each tile's rows
+        # (half the LDS fragment reads per tile); False = 2 sets per wave, every wave all rows
+        self.mq_rsplit = True
         self.mq_stats = False  # accumulate overflow count / max candidates (diagnostics)
         self._mq_tot = None
 
@@ -408,8 +411,9 @@ class HbmIndexShard:
 
         h = hip()
         NQ = q_unit.shape[0]
-        sets = 4 if NQ >= 512 else 2   # 512 or 256 queries per workgroup
-        n_qblk = math.ceil(NQ / h.mq_queries_per_blk(sets))
+        # 512 queries per workgroup, or 256 (row-split 4-set or 2-set form)
+        sets, rsplit = (4, 1) if NQ >= 512 else ((4, 2) if self.mq_rsplit else (2, 1))
+        n_qblk = math.ceil(NQ / h.mq_queries_per_blk(sets, rsplit))
         if n_cus is None:
             n_cus = self._n_cus()
         n_rblk = max(1, min(math.ceil(n / (TILE_ROWS * 16)), max(1, round(n_cus / n_qblk))))
@@ -426,7 +430,7 @@ class HbmIndexShard:
         st = stream_handle(dev)
         h.index_scan_mq(rows.data_ptr(), n, rows_per_blk, n_rblk, q_unit.data_ptr(), NQ,
                         thr.data_ptr(), cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(), cap,
-                        self.scan_xcd, st, sets, tshift)
+                        self.scan_xcd, st, sets, tshift, rsplit)
         h.topk_select_counted(cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(), cap, NQ, kmax, k,
                               out_s.data_ptr(), out_i.data_ptr(), ovf.data_ptr(), st)
         if tshift:

@@ -63,13 +63,14 @@ int symb_index_scan_fp8(const void* X, int n_valid, int D, int rows_per_blk, int
 int symb_topk_merge(const float* cand_s, const int* cand_i, int NQ, int n_cand_per_query,
                     int kmax, int k, float* out_s, int* out_i, int64_t id_offset,
                     int64_t* out_id64, hipStream_t st, const int* gate = nullptr);
-int symb_mq_queries_per_blk(int sets);
+int symb_mq_queries_per_blk(int sets, int rsplit);
 int symb_index_scan_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                        int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
-                       int xcd, hipStream_t st, int sets, int tshift);
+                       int xcd, hipStream_t st, int sets, int tshift, int rsplit);
 int symb_index_scan_mq_ablate(const void* X, int n_valid, int rows_per_blk, int n_rblk,
                               const void* Q, int NQ, const float* thr, float* cand_s, int* cand_i,
-                              int* cand_n, int cap, int xcd, hipStream_t st, int abl);
+                              int* cand_n, int cap, int xcd, hipStream_t st, int abl, int sets,
+                              int rsplit);
 int symb_topk_select_counted(const float* cand_s, const int* cand_i, const int* cand_n, int cap,
                              int NQ, int kmax, int k, float* out_s, int* out_i, int* ovf,
                              hipStream_t st);
@@ -322,27 +323,30 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("stream"), py::arg("ns") = 0, py::arg("aux") = -1, py::arg("thr_init") = 0,
      py::arg("xcd") = 1, py::arg("gate") = 0);
   // multi-query-block D=384 scan (index_mq.hip): candidates above the seeded thresholds
-  m.def("mq_queries_per_blk", [](int sets) { return symb_mq_queries_per_blk(sets); },
-        py::arg("sets") = 4);
+  m.def("mq_queries_per_blk", [](int sets, int rsplit) { return symb_mq_queries_per_blk(sets, rsplit); },
+        py::arg("sets") = 4, py::arg("rsplit") = 1);
   m.def("index_scan_mq", [](uptr X, int n_valid, int rows_per_blk, int n_rblk, uptr Q, int NQ,
                             uptr thr, uptr cand_s, uptr cand_i, uptr cand_n, int cap, int xcd,
-                            uptr st, int sets, int tshift) {
+                            uptr st, int sets, int tshift, int rsplit) {
     check(symb_index_scan_mq(P<void>(X), n_valid, rows_per_blk, n_rblk, P<void>(Q), NQ,
                              P<const float>(thr), P<float>(cand_s), P<int>(cand_i), P<int>(cand_n),
-                             cap, xcd, S(st), sets, tshift),
+                             cap, xcd, S(st), sets, tshift, rsplit),
           "index_scan_mq");
   }, py::arg("X"), py::arg("n_valid"), py::arg("rows_per_blk"), py::arg("n_rblk"), py::arg("Q"),
      py::arg("NQ"), py::arg("thr"), py::arg("cand_s"), py::arg("cand_i"), py::arg("cand_n"),
      py::arg("cap"), py::arg("xcd"), py::arg("stream"), py::arg("sets") = 4,
-     py::arg("tshift") = 0);
+     py::arg("tshift") = 0, py::arg("rsplit") = 1);
   m.def("index_scan_mq_ablate", [](uptr X, int n_valid, int rows_per_blk, int n_rblk, uptr Q,
                                    int NQ, uptr thr, uptr cand_s, uptr cand_i, uptr cand_n,
-                                   int cap, int xcd, uptr st, int abl) {
+                                   int cap, int xcd, uptr st, int abl, int sets, int rsplit) {
     check(symb_index_scan_mq_ablate(P<void>(X), n_valid, rows_per_blk, n_rblk, P<void>(Q), NQ,
                                     P<const float>(thr), P<float>(cand_s), P<int>(cand_i),
-                                    P<int>(cand_n), cap, xcd, S(st), abl),
+                                    P<int>(cand_n), cap, xcd, S(st), abl, sets, rsplit),
           "index_scan_mq_ablate");
-  });
+  }, py::arg("X"), py::arg("n_valid"), py::arg("rows_per_blk"), py::arg("n_rblk"), py::arg("Q"),
+     py::arg("NQ"), py::arg("thr"), py::arg("cand_s"), py::arg("cand_i"), py::arg("cand_n"),
+     py::arg("cap"), py::arg("xcd"), py::arg("stream"), py::arg("abl"), py::arg("sets") = 4,
+     py::arg("rsplit") = 1);
   m.def("topk_select_counted", [](uptr cand_s, uptr cand_i, uptr cand_n, int cap, int NQ,
                                   int kmax, int k, uptr out_s, uptr out_i, uptr ovf, uptr st) {
     check(symb_topk_select_counted(P<const float>(cand_s), P<const int>(cand_i),

@@ -138,14 +138,24 @@ __device__ __forceinline__ void mq_prologue(bf16x8 (&a)[mq::R], uint32_t base) {
 // exceed cap: the select kernel then raises the overflow flag).
 // ABL (profiling entry symb_index_scan_mq_ablate only): 1 = no LDS-DMA (compute on whatever the
 // ring holds), 2 = no emission test, 3 = full kernel + per-workgroup s_memtime / s_memrealtime
-// around the tile loop written to cand_s[2 * blockIdx.x + {0, 1}] (in-kernel clock).
-template <int NSET, int ABL = 0>
+// around the tile loop written to cand_s[2 * blockIdx.x + {0, 1}] (in-kernel clock), 4 = LDS-DMA
+// ring only (same waits and barriers, no MFMA chains, no emission test: the row stream's rate).
+//
+// RSPLIT = 2 (the 256-query form of the 1-GPU shape): waves w and w + 4 hold the SAME 64 queries
+// (4 sets) and split each tile's rows, w the first two 16-row sub-tiles and w + 4 the last two.
+// Against the 2-set form (8 waves x 32 queries, every wave reading the whole tile) that halves
+// the LDS fragment reads per tile (192 KiB instead of 384) and the chain ends per MFMA, at the
+// same MFMA cycles per SIMD: at 256 queries the scan is bound by the chip's power limit (HBM
+// streaming + MFMAs hold the in-kernel clock near 1.5 GHz), so bytes moved per FLOP count.
+template <int NSET, int ABL = 0, int RSPLIT = 1>
 __global__ __launch_bounds__(512, 1) void index_scan_mq_kernel(
     const __bf16* __restrict__ X, int n_valid, int rows_per_blk, const __bf16* __restrict__ Q,
     int NQ, int n_qblk, int xcd, const float* __restrict__ thr_in, float* __restrict__ cand_s,
     int* __restrict__ cand_i, int* __restrict__ cand_n, int cap, int tshift) {
   using namespace mq;
-  constexpr int SETS = NSET, QW = SETS * 16, QPB = WAVES * QW;
+  constexpr int SETS = NSET, QW = SETS * 16, QWAVES = WAVES / RSPLIT, QPB = QWAVES * QW;
+  constexpr int NSW = NSUB / RSPLIT;          // 16-row sub-tiles per wave per tile
+  static_assert(RSPLIT == 1 || RSPLIT == 2, "row split");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lb = xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
@@ -163,7 +173,9 @@ __global__ __launch_bounds__(512, 1) void index_scan_mq_kernel(
   };
 
   // ---- query fragments (B operand, 16x16x32: lane holds Q[col = lane&15][k = 8*(lane>>4)+j]) --
-  const int qbase = qb * QPB + wave * QW + (lane & 15);
+  const int qwave = wave % QWAVES;                 // this wave's query group
+  const int j0 = (wave / QWAVES) * NSW;             // this wave's first sub-tile of a tile
+  const int qbase = qb * QPB + qwave * QW + (lane & 15);
   bf16x8 qf[SETS][NKS];
   float thr[SETS];
 #pragma unroll
@@ -216,7 +228,7 @@ __global__ __launch_bounds__(512, 1) void index_scan_mq_kernel(
   auto flush = [&]() {
     // the candidate addresses derive from an opaque copy of the wave's first query so the
     // compiler cannot hoist 64-bit pointers out of the tile loop into the register budget
-    int qw = qb * QPB + wave_u * QW;
+    int qw = qb * QPB + (wave_u % QWAVES) * QW;
     asm volatile("" : "+v"(qw));
     for (int e = lane; e < nst; e += 64) {
       const int q = qw + st_q[e];
@@ -231,7 +243,7 @@ __global__ __launch_bounds__(512, 1) void index_scan_mq_kernel(
   // one 16-row sub-tile at virtual row row0 / physical row prow0: lane holds rows
   // 4*(lane>>4) + r of it for the 16 queries of each set (column lane & 15)
   auto emit = [&](f32x4 (&acc)[SETS], int row0, int prow0) {
-    if constexpr (ABL == 2) {
+    if constexpr (ABL == 2 || ABL == 4) {
 #pragma unroll
       for (int s = 0; s < SETS; ++s) asm volatile("" ::"v"(acc[s]));
       return;
@@ -315,24 +327,38 @@ __global__ __launch_bounds__(512, 1) void index_scan_mq_kernel(
       if constexpr (ABL != 1) issue_piece(tnext, i);
     };
     const uint32_t fb = tbase + foff;   // this lane's fragment in piece 0 of sub-tile 0
-    mq_prologue<0>(a, fb);
-    if (late && t > 0) emit(acc, row0 - SUB, prow_last + TR - SUB);
-    prow_last = prow0;
-    MqChain<0, LOADS, true, SETS>::run(acc, a, qf, fb, fb + NKS * PIECE, dma);
+    if constexpr (ABL == 4) {
 #pragma unroll
-    for (int j = 1; j < NSUB; ++j) {
+      for (int i = 0; i < LOADS; ++i) dma(i);
+      continue;
+    }
+    mq_prologue<0>(a, fb + j0 * NKS * PIECE);
+    // (this wave's sub-tiles are j0 .. j0 + NSW - 1; ``last`` = row offset of its last one)
+    const int last = (j0 + NSW - 1) * SUB;
+    if (late && t > 0) emit(acc, row0 - TR + last, prow_last + last);
+    prow_last = prow0;
+    const uint32_t fw = fb + j0 * NKS * PIECE;
+    if constexpr (NSW > 1)
+      MqChain<0, LOADS, true, SETS>::run(acc, a, qf, fw, fw + NKS * PIECE, dma);
+    else
+      MqChain<0, LOADS, false, SETS>::run(acc, a, qf, fw, 0, dma);
+#pragma unroll
+    for (int j = 1; j < NSW; ++j) {
       // sub-tile j's first fragments were read by the previous chain's tail and fly while this
       // wave tests the previous sub-tile's scores
-      emit(acc, row0 + (j - 1) * SUB, prow0 + (j - 1) * SUB);
-      if (j + 1 < NSUB)
-        MqChain<0, 0, true, SETS>::run(acc, a, qf, fb + j * NKS * PIECE, fb + (j + 1) * NKS * PIECE,
+      emit(acc, row0 + (j0 + j - 1) * SUB, prow0 + (j0 + j - 1) * SUB);
+      if (j + 1 < NSW)
+        MqChain<0, 0, true, SETS>::run(acc, a, qf, fw + j * NKS * PIECE, fw + (j + 1) * NKS * PIECE,
                                  NoDma());
       else
-        MqChain<0, 0, false, SETS>::run(acc, a, qf, fb + j * NKS * PIECE, 0, NoDma());
+        MqChain<0, 0, false, SETS>::run(acc, a, qf, fw + j * NKS * PIECE, 0, NoDma());
     }
-    if (!late) emit(acc, row0 + (NSUB - 1) * SUB, prow0 + (NSUB - 1) * SUB);
+    if (!late) emit(acc, row0 + last, prow0 + last);
   }
-  if (late && n_tiles > 0) emit(acc, row_begin + n_tiles * TR - SUB, prow_last + TR - SUB);
+  if (late && n_tiles > 0) {
+    const int last = (j0 + NSW - 1) * SUB;
+    emit(acc, row_begin + (n_tiles - 1) * TR + last, prow_last + last);
+  }
   if (nst) flush();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tail prefetches and emissions
   if constexpr (ABL == 3) {
@@ -416,52 +442,62 @@ __global__ __launch_bounds__(NTH) void topk_select_counted_kernel(
 
 using namespace symb;
 
-int symb_mq_queries_per_blk(int sets) { return mq::WAVES * 16 * sets; }
+int symb_mq_queries_per_blk(int sets, int rsplit) { return mq::WAVES / rsplit * 16 * sets; }
 
 // rows_per_blk must be a multiple of 64; n_rblk * rows_per_blk >= n_valid.  cand_n is zeroed here.
-template <int NSET>
+template <int NSET, int RSPLIT>
 static int launch_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                      int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
                      int xcd, hipStream_t st, int tshift) {
-  const int n_qblk = (NQ + mq::WAVES * 16 * NSET - 1) / (mq::WAVES * 16 * NSET);
+  constexpr int qpb = mq::WAVES / RSPLIT * 16 * NSET;
+  const int n_qblk = (NQ + qpb - 1) / qpb;
   constexpr int lds = mq::LDS_BYTES;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)index_scan_mq_kernel<NSET, 0>,
+    (void)hipFuncSetAttribute((const void*)index_scan_mq_kernel<NSET, 0, RSPLIT>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
-  hipLaunchKernelGGL((index_scan_mq_kernel<NSET, 0>), dim3(n_rblk * n_qblk), dim3(512), lds, st,
+  hipLaunchKernelGGL((index_scan_mq_kernel<NSET, 0, RSPLIT>), dim3(n_rblk * n_qblk), dim3(512), lds, st,
                      (const __bf16*)X, n_valid, rows_per_blk, (const __bf16*)Q, NQ, n_qblk, xcd,
                      thr, cand_s, cand_i, cand_n, cap, tshift);
   return (int)hipGetLastError();
 }
 
 // tshift: 0 = rows [0, n_valid); k > 0 = virtual rows of a 1-in-2^k tile sample (kernel note).
-// sets: 16-query sets per wave, 4 (512 queries per workgroup) or 2 (256).
+// sets: 16-query sets per wave, 4 or 2; rsplit: waves sharing each query group (1, or 2 = the
+// row-split form, sets 4 only).  Queries per workgroup: 8 / rsplit * 16 * sets (512 or 256).
 int symb_index_scan_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                        int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
-                       int xcd, hipStream_t st, int sets, int tshift) {
+                       int xcd, hipStream_t st, int sets, int tshift, int rsplit) {
   if (NQ <= 0) return 0;
   if (rows_per_blk % mq::TR || n_rblk <= 0 || thr == nullptr || cap <= 0) return -1;
   if ((sets != 2 && sets != 4) || tshift < 0 || tshift > 12) return -1;
+  if (rsplit != 1 && !(rsplit == 2 && sets == 4)) return -1;
   hipError_t e = hipMemsetAsync(cand_n, 0, sizeof(int) * (size_t)NQ, st);
   if (e != hipSuccess) return (int)e;
-  return sets == 4 ? launch_mq<4>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, thr, cand_s, cand_i,
-                                  cand_n, cap, xcd, st, tshift)
-                   : launch_mq<2>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, thr, cand_s, cand_i,
-                                  cand_n, cap, xcd, st, tshift);
+  if (rsplit == 2)
+    return launch_mq<4, 2>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, thr, cand_s, cand_i, cand_n,
+                           cap, xcd, st, tshift);
+  return sets == 4 ? launch_mq<4, 1>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, thr, cand_s, cand_i,
+                                     cand_n, cap, xcd, st, tshift)
+                   : launch_mq<2, 1>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, thr, cand_s, cand_i,
+                                     cand_n, cap, xcd, st, tshift);
 }
 
 // Profiling-only entry: the ablations of index_scan_mq_kernel (ABL above), same arguments.
 int symb_index_scan_mq_ablate(const void* X, int n_valid, int rows_per_blk, int n_rblk,
                               const void* Q, int NQ, const float* thr, float* cand_s, int* cand_i,
-                              int* cand_n, int cap, int xcd, hipStream_t st, int abl) {
+                              int* cand_n, int cap, int xcd, hipStream_t st, int abl, int sets,
+                              int rsplit) {
   if (NQ <= 0) return 0;
   if (rows_per_blk % mq::TR || n_rblk <= 0 || thr == nullptr || cap <= 0) return -1;
+  if (sets != 2 && sets != 4) return -1;
+  if (rsplit != 1 && !(rsplit == 2 && sets == 4)) return -1;
   hipError_t e = hipMemsetAsync(cand_n, 0, sizeof(int) * (size_t)NQ, st);
   if (e != hipSuccess) return (int)e;
-  const int n_qblk = (NQ + mq::WAVES * 64 - 1) / (mq::WAVES * 64);
+  const int qpb = mq::WAVES / rsplit * 16 * sets;
+  const int n_qblk = (NQ + qpb - 1) / qpb;
   constexpr int lds = mq::LDS_BYTES;
   auto go = [&](auto kern) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
@@ -470,11 +506,22 @@ int symb_index_scan_mq_ablate(const void* X, int n_valid, int rows_per_blk, int 
                        cand_i, cand_n, cap, 0);
     return (int)hipGetLastError();
   };
-  switch (abl) {
+  switch (abl + 8 * (sets == 2) + 16 * (rsplit == 2)) {
     case 0: return go(index_scan_mq_kernel<4, 0>);
     case 1: return go(index_scan_mq_kernel<4, 1>);
     case 2: return go(index_scan_mq_kernel<4, 2>);
     case 3: return go(index_scan_mq_kernel<4, 3>);
+    case 4: return go(index_scan_mq_kernel<4, 4>);
+    case 8: return go(index_scan_mq_kernel<2, 0>);
+    case 9: return go(index_scan_mq_kernel<2, 1>);
+    case 10: return go(index_scan_mq_kernel<2, 2>);
+    case 11: return go(index_scan_mq_kernel<2, 3>);
+    case 12: return go(index_scan_mq_kernel<2, 4>);
+    case 16: return go(index_scan_mq_kernel<4, 0, 2>);
+    case 17: return go(index_scan_mq_kernel<4, 1, 2>);
+    case 18: return go(index_scan_mq_kernel<4, 2, 2>);
+    case 19: return go(index_scan_mq_kernel<4, 3, 2>);
+    case 20: return go(index_scan_mq_kernel<4, 4, 2>);
     default: return -1;
   }
 }

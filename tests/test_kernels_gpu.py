@@ -315,16 +315,19 @@ def test_index_scan_xcd_grouping_is_exact(dtype):
         _close(s1, ref_s, atol=2e-3, what="xcd-grouped topk scores")
 
 
-@pytest.mark.parametrize("nq", [300, 512, 1100, 2048])
-def test_index_scan_mq_exact(nq):
-    """The 512-query emitting scan (the per-rank shape at N >= 2 GPUs) returns the rows of the
-    256-query list kernel and of the fp32 oracle; no candidate buffer overflows on random data."""
+@pytest.mark.parametrize("nq,rsplit", [(300, True), (300, False), (256, True), (512, True),
+                                       (1100, True), (2048, True)])
+def test_index_scan_mq_exact(nq, rsplit):
+    """The 512-query emitting scan (the per-rank shape at N >= 2 GPUs) and its 256-query forms
+    (row-split 4-set, 2-set) return the rows of the 256-query list kernel and of the fp32 oracle;
+    no candidate buffer overflows on random data."""
     from codename_symbiont_amd.index.shard import HbmIndexShard
 
     n, k, D = (1 << 20) + 777, 10, 384
     shard = HbmIndexShard(D, n + 4096)
     shard.fill_random(n, seed=31)
-    shard.mq_min_nq = 256     # < 512 queries: the 2-set (256 queries per workgroup) kernel
+    shard.mq_min_nq = 256     # < 512 queries: a 256-query-per-workgroup form
+    shard.mq_rsplit = rsplit
     q = torch.nn.functional.normalize(_f(nq, D, seed=32), dim=-1).bfloat16()
     assert shard._seed_rows(n, k) and shard._mq_ok(nq, k, shard.rows, "bf16")
     shard.scan_mq = False
