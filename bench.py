@@ -76,6 +76,11 @@ def main() -> None:
     ap.add_argument("--scan-cus", type=int, default=0,
                     help="spread the index scans over this many CUs (0 = all), leaving the rest to "
                          "the encoder running beside them on the second stream")
+    ap.add_argument("--search-priority", action="store_true",
+                    help="run the search (and the step's bookkeeping) on a high-priority stream so "
+                         "its short latency-bound kernels dispatch ahead of the encoder's")
+    ap.add_argument("--scan-min-tiles", type=int, default=16,
+                    help="smallest row block (64-row tiles) of the small list scans")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch the encoder's kernels eagerly every step instead of replaying a "
                          "captured hipGraph of the forward")
@@ -107,6 +112,7 @@ def main() -> None:
     searcher = ShardedSearcher(shard, info)
     shard.mq_stats = os.environ.get("SYMB_MQ_STATS", "0") not in ("", "0")
     shard.scan_cus = args.scan_cus
+    shard.scan_min_tiles = args.scan_min_tiles
     torch.cuda.synchronize(dev)
     row_bytes = cfg.hidden * (1 if args.index_dtype == "fp8" else 2)
     log(info, f"[bench] setup {time.time() - t0:.1f}s: {cfg.model_name}, shard {rows_per_rank} "
@@ -126,6 +132,10 @@ def main() -> None:
     dbuf = [host[0].to(dev), host[1].to(dev)]
     copy_stream = torch.cuda.Stream(dev)
     compute = torch.cuda.current_stream(dev)
+    if args.search_priority:
+        torch.cuda.synchronize(dev)
+        compute = torch.cuda.Stream(dev, priority=-1)
+        torch.cuda.set_stream(compute)
     copy_done = [torch.cuda.Event(), torch.cuda.Event()]
     consumed = [torch.cuda.Event(), torch.cuda.Event()]
     out_f32 = torch.empty(B, cfg.hidden, device=dev)
@@ -330,6 +340,8 @@ def main() -> None:
                                   and B * info.world >= shard.mq_min_nq and args.k <= 16)
                               else "list-256q",
                 "encoder_hipgraph": use_graph,
+                "search_priority": args.search_priority,
+                "scan_min_tiles": args.scan_min_tiles,
             },
             "embeds_per_sec": round(total, 2) if args.mode != "search" else 0.0,
             "topk_qps": round(total, 2) if args.mode != "embed" else 0.0,

@@ -118,6 +118,19 @@ def cmd_scanmq(a):
     ids_equal = float((ref[1] == got[1]).float().mean())
     max_score_diff = float((ref[0] - got[0]).abs().max())
     variants = {"list256": lambda: srch(False), "mq512": lambda: srch(True)}
+    from codename_symbiont_amd.ops._ext import hip
+
+    def srch_nt():   # non-temporal row stream
+        hip().mq_config(2)
+        try:
+            return srch(True)
+        finally:
+            hip().mq_config(0)
+
+    got3 = srch_nt()
+    torch.cuda.synchronize()
+    ids_equal = min(ids_equal, float((ref[1] == got3[1]).float().mean()))
+    variants["mq_nt"] = srch_nt
     if a.nq < 512:   # the two 256-query forms: row-split 4-set ("mq512") and 2-set
         got2 = srch(True, False)
         torch.cuda.synchronize()

@@ -150,6 +150,9 @@ class HbmIndexShard:
         self.visible = 0
         self.payloads = PayloadStore()
         self.scan_ns = 0     # LDS ring depth of the fused scan (0 = kernel default)
+        # smallest row block (in 64-row tiles) of the 256-query list scan: small scans (threshold
+        # seeding, the fresh-row tail) are latency-bound, so fewer tiles per block = more CUs
+        self.scan_min_tiles = 16
         self.scan_aux = -1   # index-stream cache policy (-1 = auto: non-temporal when read once)
         self.seed_threshold = True  # sample pre-pass seeds per-query top-k thresholds
         self.scan_variant = 0        # fp8 scan ring geometry (0 = default)
@@ -490,7 +493,8 @@ class HbmIndexShard:
         n_qblk = math.ceil(NQ / qpb)
         if n_cus is None:
             n_cus = self._n_cus()
-        n_rblk = max(1, min(math.ceil(n / (TILE_ROWS * 16)), max(1, round(n_cus / n_qblk))))
+        n_rblk = max(1, min(math.ceil(n / (TILE_ROWS * self.scan_min_tiles)),
+                            max(1, round(n_cus / n_qblk))))
         rows_per_blk = _round_up(max(1, math.ceil(n / n_rblk)), TILE_ROWS)
         n_rblk = max(1, math.ceil(n / rows_per_blk))
         ncand = n_rblk * lists * kmax

@@ -147,7 +147,8 @@ __device__ __forceinline__ void mq_prologue(bf16x8 (&a)[mq::R], uint32_t base) {
 // the LDS fragment reads per tile (192 KiB instead of 384) and the chain ends per MFMA, at the
 // same MFMA cycles per SIMD: at 256 queries the scan is bound by the chip's power limit (HBM
 // streaming + MFMAs hold the in-kernel clock near 1.5 GHz), so bytes moved per FLOP count.
-template <int NSET, int ABL = 0, int RSPLIT = 1>
+// AUX: cache policy bits of the row stream's LDS-DMA (0 = default, 2 = non-temporal).
+template <int NSET, int ABL = 0, int RSPLIT = 1, int AUX = 0>
 __global__ __launch_bounds__(512, 1) void index_scan_mq_kernel(
     const __bf16* __restrict__ X, int n_valid, int rows_per_blk, const __bf16* __restrict__ Q,
     int NQ, int n_qblk, int xcd, const float* __restrict__ thr_in, float* __restrict__ cand_s,
@@ -208,7 +209,7 @@ __global__ __launch_bounds__(512, 1) void index_scan_mq_kernel(
     const int prow = phys_tile(row_begin / TR + tt) * TR;
     const char* base = reinterpret_cast<const char*>(X + (size_t)(prow + j * SUB) * D + ks * 32);
     char* dst = smem + (t % NS) * TILE_BYTES + p * PIECE;
-    glds16_aux<0>(mq_uniform(base) + loff, dst);
+    glds16_aux<AUX>(mq_uniform(base) + loff, dst);
   };
 
   // ---- per-lane A-fragment offset within a piece (lane holds X[row r][k 8g..8g+7] of the k-step)
@@ -445,8 +446,16 @@ using namespace symb;
 int symb_mq_queries_per_blk(int sets, int rsplit) { return mq::WAVES / rsplit * 16 * sets; }
 
 // rows_per_blk must be a multiple of 64; n_rblk * rows_per_blk >= n_valid.  cand_n is zeroed here.
-template <int NSET, int RSPLIT>
-static int launch_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
+// cache policy of the row stream (symb_mq_config): 0 default, 2 non-temporal
+static int g_mq_aux = 0;
+int symb_mq_config(int aux) {
+  if (aux != 0 && aux != 2) return -1;
+  g_mq_aux = aux;
+  return 0;
+}
+
+template <int NSET, int RSPLIT, int AUX>
+static int launch_mq_aux(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                      int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
                      int xcd, hipStream_t st, int tshift) {
   constexpr int qpb = mq::WAVES / RSPLIT * 16 * NSET;
@@ -454,14 +463,25 @@ static int launch_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk, c
   constexpr int lds = mq::LDS_BYTES;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)index_scan_mq_kernel<NSET, 0, RSPLIT>,
+    (void)hipFuncSetAttribute((const void*)index_scan_mq_kernel<NSET, 0, RSPLIT, AUX>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
-  hipLaunchKernelGGL((index_scan_mq_kernel<NSET, 0, RSPLIT>), dim3(n_rblk * n_qblk), dim3(512), lds, st,
-                     (const __bf16*)X, n_valid, rows_per_blk, (const __bf16*)Q, NQ, n_qblk, xcd,
-                     thr, cand_s, cand_i, cand_n, cap, tshift);
+  hipLaunchKernelGGL((index_scan_mq_kernel<NSET, 0, RSPLIT, AUX>), dim3(n_rblk * n_qblk), dim3(512),
+                     lds, st, (const __bf16*)X, n_valid, rows_per_blk, (const __bf16*)Q, NQ, n_qblk,
+                     xcd, thr, cand_s, cand_i, cand_n, cap, tshift);
   return (int)hipGetLastError();
+}
+
+template <int NSET, int RSPLIT>
+static int launch_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
+                     int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
+                     int xcd, hipStream_t st, int tshift) {
+  return g_mq_aux == 2
+             ? launch_mq_aux<NSET, RSPLIT, 2>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, thr, cand_s,
+                                             cand_i, cand_n, cap, xcd, st, tshift)
+             : launch_mq_aux<NSET, RSPLIT, 0>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, thr, cand_s,
+                                             cand_i, cand_n, cap, xcd, st, tshift);
 }
 
 // tshift: 0 = rows [0, n_valid); k > 0 = virtual rows of a 1-in-2^k tile sample (kernel note).
