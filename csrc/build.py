@@ -26,7 +26,8 @@ PKG = ROOT / "codename_symbiont_amd"
 BUILD = ROOT / "build"
 ARCH = os.environ.get("SYMB_OFFLOAD_ARCH", "gfx950")
 EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
-HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+HIPCC = os.environ.get("HIPCC", f"{ROCM}/bin/hipcc")
 CXX = os.environ.get("CXX", "g++")
 
 
@@ -78,6 +79,12 @@ def build_hip(force: bool = False, nproc: int = 8) -> Path:
         obj = obj_dir / (src.stem + ".o")
         jobs.append((common + ["-c", str(src), "-o", str(obj)], src, obj, hdr_mtime))
         objs.append(obj)
+    # host-only C++ (the hipBLASLt plan cache for the plain projections)
+    lt = src_dir / "gemm_lt.cpp"
+    lt_obj = obj_dir / "gemm_lt.o"
+    jobs.append(([HIPCC, "-O2", "-std=c++17", "-fPIC", "-fvisibility=hidden", f"-I{src_dir}",
+                  "-D__HIP_PLATFORM_AMD__", "-c", str(lt), "-o", str(lt_obj)], lt, lt_obj, hdr_mtime))
+    objs.append(lt_obj)
     bind = src_dir / "bindings.cpp"
     bind_obj = obj_dir / "bindings.o"
     jobs.append(
@@ -92,7 +99,8 @@ def build_hip(force: bool = False, nproc: int = 8) -> Path:
     changed = _compile_all(jobs, nproc, force)
     out = PKG / f"_hip{EXT_SUFFIX}"
     if changed or force or not out.exists() or out.stat().st_mtime < _newest(objs):
-        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(out)])
+        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs),
+              f"-L{ROCM}/lib", "-lhipblaslt", f"-Wl,-rpath,{ROCM}/lib", "-o", str(out)])
     return out
 
 

@@ -64,6 +64,7 @@ int symb_topk_merge(const float* cand_s, const int* cand_i, int NQ, int n_cand_p
                     int kmax, int k, float* out_s, int* out_i, int64_t id_offset,
                     int64_t* out_id64, hipStream_t st, const int* gate = nullptr);
 int symb_mq_queries_per_blk(int sets, int rsplit);
+int symb_gemm_lt_config(int mode);
 int symb_mq_config(int aux);
 int symb_index_scan_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                        int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
@@ -324,6 +325,8 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("stream"), py::arg("ns") = 0, py::arg("aux") = -1, py::arg("thr_init") = 0,
      py::arg("xcd") = 1, py::arg("gate") = 0);
   // multi-query-block D=384 scan (index_mq.hip): candidates above the seeded thresholds
+  m.def("gemm_lt_config", [](int mode) { check(symb_gemm_lt_config(mode), "gemm_lt_config"); },
+        py::arg("mode"));
   m.def("mq_config", [](int aux) { check(symb_mq_config(aux), "mq_config"); }, py::arg("aux"));
   m.def("mq_queries_per_blk", [](int sets, int rsplit) { return symb_mq_queries_per_blk(sets, rsplit); },
         py::arg("sets") = 4, py::arg("rsplit") = 1);

@@ -485,6 +485,18 @@ int symb_gemm_fp8_config(int waves, int big) {
   return 0;
 }
 
+// hipBLASLt for the plain bias / bias + residual projections (gemm_lt.cpp): 0 = never, 1 = auto
+// (K >= 768 and N >= 768 and M >= 4096: the bge-base / e5-large shapes, where the library's
+// kernels are faster; MiniLM's K = 384 projections stay here), 2 = every bias / residual GEMM.
+int symb_gemm_lt(int epi, const void* A, int lda, const void* W, int ldw, const float* bias,
+                 const void* R, int ldr, void* C, int ldc, int M, int N, int K, hipStream_t st);
+static int g_gemm_lt = 1;
+int symb_gemm_lt_config(int mode) {
+  if (mode < 0 || mode > 2) return -1;
+  g_gemm_lt = mode;
+  return 0;
+}
+
 // Returns 0 on success, a HIP error code, or -1 for an unsupported shape.
 int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const float* bias,
               const void* R, int ldr, const float* gamma, const float* beta, float eps, void* C,
@@ -509,6 +521,9 @@ int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const flo
     return -1;  // wider rows: EPI_RES + symb_add_ln
   }
   if (N % 128 != 0) return -1;
+  if ((epi == EPI_BIAS || epi == EPI_RES) &&
+      (g_gemm_lt == 2 || (g_gemm_lt == 1 && K >= 768 && N >= 768 && M >= 4096)))
+    return symb_gemm_lt(epi, A, lda, W, ldw, bias, R, ldr, C, ldc, M, N, K, st);
   if (g_tile == 9 && symb_gemm256_supported(M, N, K))
     return symb_gemm256(epi, A, lda, W, ldw, bias, R, ldr, C, ldc, M, N, K, g_group_m, st);
   const int tile_mode = g_tile == 10 ? 3 : g_tile;   // 10: auto without the 8-phase kernel (A/B)

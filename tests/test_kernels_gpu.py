@@ -94,6 +94,7 @@ def test_gemm(M, N, K, epi, tile):
     hip().gemm_config(64 if tile == 1 else 128, 3 if tile == 16 else tile,
                       {0: 8, 1: 3, 2: 0, 4: 8, 5: 5, 6: 8, 7: 2, 8: 8, 9: 8, 16: 8}[tile])
     hip().gemm_resln_config(8 if tile == 16 else 16)
+    hip().gemm_lt_config(0)   # gemm.hip's own tiles (the hipBLASLt route has its own test)
 
     a = _bf(M, K, seed=1)
     w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=2)
@@ -106,8 +107,30 @@ def test_gemm(M, N, K, epi, tile):
     finally:
         hip().gemm_config(128, 3, 8)
         hip().gemm_resln_config(16)
+        hip().gemm_lt_config(1)
     ref = R.gemm_ref(a, w, bias, epi, res, g, b, 1e-12)
     _close(out, ref, atol=4e-2, rtol=2e-2, what=f"gemm epi={epi}")
+
+
+@pytest.mark.parametrize("M,N,K,epi", [(300, 1152, 384, 0), (4100, 768, 3072, 2), (999, 2304, 768, 0),
+                                      (77, 1024, 4096, 2)])
+def test_gemm_hipblaslt_route(M, N, K, epi):
+    """symb_gemm's hipBLASLt route for the plain projections (bias, bias + residual through
+    beta * C) matches the fp32 oracle."""
+    from codename_symbiont_amd.ops._ext import hip
+    from codename_symbiont_amd.ops.kernels import gemm
+
+    a = _bf(M, K, seed=1)
+    w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=2)
+    bias = _f(N, scale=0.5, seed=3)
+    res = _bf(M, N, seed=4) if epi == 2 else None
+    hip().gemm_lt_config(2)
+    try:
+        out = gemm(a, w, bias, epi, res)
+    finally:
+        hip().gemm_lt_config(1)
+    ref = R.gemm_ref(a, w, bias, epi, res, None, None, 1e-12)
+    _close(out, ref, atol=4e-2, rtol=2e-2, what=f"hipblaslt gemm epi={epi}")
 
 
 @pytest.mark.parametrize("D,nh", [(32, 12), (64, 12), (64, 16)])
