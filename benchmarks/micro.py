@@ -481,12 +481,12 @@ def cmd_attn(a):
     out = torch.empty(a.batch * a.seq, nh * hd, device="cuda", dtype=torch.bfloat16)
     from codename_symbiont_amd.ops._ext import hip
 
-    def run(w, kv):
-        hip().attention_config(w, kv)
+    def run(w, kv, x):
+        hip().attention_config(w, kv, x)
         return K.attention(qkv, cu, a.seq, nh, hd, out=out)
-    res = ab({f"waves{w}_kvt{kv}": (lambda w=w, kv=kv: run(w, kv)) for w in (4, 8) for kv in (64, 128)},
-             a.rounds, a.iters)
-    hip().attention_config(8, 64)
+    res = ab({f"waves{w}_kvt{kv}_xcd{x}": (lambda w=w, kv=kv, x=x: run(w, kv, x))
+              for w in (4, 8) for kv in (64, 128) for x in (0, 1)}, a.rounds, a.iters)
+    hip().attention_config(8, 64, 2)
     fl = 4 * a.batch * nh * a.seq * a.seq * hd
     print(json.dumps({"bench": "attn", "head_dim": hd, "seq": a.seq, "results": {
         k: {"ms": round(m, 4), "TFLOPs": round(fl / (m / 1e3) / 1e12)} for k, (m, _) in res.items()}}))
@@ -544,7 +544,8 @@ def main():
     ap.add_argument("--model", default="minilm-l6")
     ap.add_argument("--seed", type=int, default=1, help="scanabl: seed per-query thresholds")
     ap.add_argument("--precision", default="bf16", help="encoder: comma list of bf16,fp8")
-    ap.add_argument("--tiles", default="3", help="encoder: comma list of gemm_config tile modes")
+    ap.add_argument("--tiles", default="12", help="encoder: comma list of gemm_config tile modes "
+                    "(12 = the default: auto tiles + the hipBLASLt route; 3 = auto tiles only)")
     ap.add_argument("--fp8-waves", default="8", help="encoder: comma list of fp8 GEMM wave counts")
     ap.add_argument("--sets", type=int, default=4, help="scanmqabl: 16-query sets per wave (2 or 4)")
     ap.add_argument("--rsplit", type=int, default=1, help="scanmqabl: waves per query group (1, 2)")

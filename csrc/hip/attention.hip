@@ -33,7 +33,7 @@ __global__ __launch_bounds__(64 * NWAVE) void attn_varlen_kernel(const __bf16* _
                                                           int ld_qkv, const int32_t* __restrict__ cu,
                                                           int H, float scale_log2,
                                                           __bf16* __restrict__ out, int ld_out,
-                                                          uint8_t* __restrict__ oscale) {
+                                                          uint8_t* __restrict__ oscale, int xcd) {
   static_assert(KVT % 32 == 0, "keys per tile");   // 128: a <=128-token sentence in ONE stage
   constexpr int NT = KVT / 16;            // 16-key accumulator tiles
   constexpr int CK = D / 8;               // 16-byte chunks per K/V row
@@ -46,10 +46,21 @@ __global__ __launch_bounds__(64 * NWAVE) void attn_varlen_kernel(const __bf16* _
   char* Ks = sm;
   char* Vs = sm + KVT * KRB;
 
-  const int b = blockIdx.z, h = blockIdx.y;
+  // xcd: workgroups walk (sequence, head, query block) in XCD-contiguous order, so the heads of
+  // one sequence run on ONE XCD.  Its K/V/Q rows then share that XCD's L2 lines: a d = 32 head is
+  // 64 of a 128-byte line whose other half is the neighbouring head, and with the default
+  // round-robin placement the two halves were fetched into two different XCDs' L2s.
+  int bx = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  if (xcd) {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int lid = xcd_remap(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gridDim.z);
+    bx = lid % gx;
+    h = (lid / gx) % gy;
+    b = lid / (gx * gy);
+  }
   const int s0 = cu[b], L = cu[b + 1] - s0;
   constexpr int NTH = 64 * NWAVE, QB = 16 * NWAVE;  // threads, query rows per workgroup
-  const int q0 = blockIdx.x * QB;
+  const int q0 = bx * QB;
   if (q0 >= L) return;                    // block-uniform: EXEC stays full for the tr reads
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int c16 = lane & 15, g = lane >> 4;
@@ -195,10 +206,15 @@ using namespace symb;
 // 12 heads: D=32 40.5 -> 34.0 us, D=64 52.2 -> 43.1 us vs 4 waves (profiles/r1_attn/attn_waves.json)
 static int g_attn_waves = 8;  // 4: 64-query workgroups; 8: 128-query workgroups
 static int g_attn_kvt = 64;   // keys per LDS tile (64, or 128 = a <=128-token sentence at once)
-int symb_attention_config(int waves, int kvt) {
-  if ((waves != 4 && waves != 8) || (kvt != 64 && kvt != 128)) return -1;
+// XCD-contiguous (sequence, head) order (kernel note): 0 off, 1 on, 2 auto = head_dim 32 only.
+// Measured (profiles/r2_attn_xcd/, 256 x 128 tokens, 12 heads, 8 waves): d = 32 35.2 -> 32.0 us,
+// d = 64 45.6 -> 47.0 us (a 64-dim head row is a whole 128-byte line: nothing to share).
+static int g_attn_xcd = 2;
+int symb_attention_config(int waves, int kvt, int xcd) {
+  if ((waves != 4 && waves != 8) || (kvt != 64 && kvt != 128) || xcd < 0 || xcd > 2) return -1;
   g_attn_waves = waves;
   g_attn_kvt = kvt;
+  g_attn_xcd = xcd;
   return 0;
 }
 
@@ -207,6 +223,7 @@ int symb_attention_config(int waves, int kvt) {
 int symb_attention(const void* qkv, int ld_qkv, const int32_t* cu, int B, int max_len, int n_heads,
                    int head_dim, void* out, int ld_out, hipStream_t st, void* oscale) {
   if (B <= 0 || max_len <= 0) return 0;
+  const int xcd = g_attn_xcd == 2 ? (head_dim == 32) : g_attn_xcd;
   if (oscale) {
     const int H = n_heads * head_dim;
     const float scale_log2 = 1.4426950408889634f / sqrtf((float)head_dim);
@@ -214,11 +231,11 @@ int symb_attention(const void* qkv, int ld_qkv, const int32_t* cu, int B, int ma
     if (head_dim == 32)
       hipLaunchKernelGGL((attn_varlen_kernel<32, 64, 8, true>), grid, dim3(512), 0, st,
                          (const __bf16*)qkv, ld_qkv, cu, H, scale_log2, (__bf16*)out, ld_out,
-                         (uint8_t*)oscale);
+                         (uint8_t*)oscale, xcd);
     else if (head_dim == 64)
       hipLaunchKernelGGL((attn_varlen_kernel<64, 64, 8, true>), grid, dim3(512), 0, st,
                          (const __bf16*)qkv, ld_qkv, cu, H, scale_log2, (__bf16*)out, ld_out,
-                         (uint8_t*)oscale);
+                         (uint8_t*)oscale, xcd);
     else
       return -1;
     return (int)hipGetLastError();
@@ -229,7 +246,7 @@ int symb_attention(const void* qkv, int ld_qkv, const int32_t* cu, int B, int ma
   dim3 grid((max_len + 16 * NW - 1) / (16 * NW), n_heads, B);
 #define SYMB_A(DD, KV, W) hipLaunchKernelGGL((attn_varlen_kernel<DD, KV, W>), grid, dim3(64 * W), 0, \
                                              st, (const __bf16*)qkv, ld_qkv, cu, H, scale_log2,     \
-                                             (__bf16*)out, ld_out, nullptr)
+                                             (__bf16*)out, ld_out, nullptr, xcd)
 #define SYMB_AW(DD)                                             \
   if (NW == 8 && g_attn_kvt == 128) SYMB_A(DD, 128, 8);         \
   else if (NW == 8) SYMB_A(DD, 64, 8);                          \

@@ -36,7 +36,7 @@ int symb_attention(const void* qkv, int ld_qkv, const int32_t* cu, int B, int ma
                    int n_heads, int head_dim, void* out, int ld_out, hipStream_t st,
                    void* oscale = nullptr);
 int symb_topk_geometry(int D, int kmax, int* lists, int* queries_per_blk);
-int symb_attention_config(int waves, int kvt);
+int symb_attention_config(int waves, int kvt, int xcd);
 int symb_index_scan(const void* X, int n_valid, int D, int rows_per_blk, int n_rblk,
                     const void* Q, int NQ, int kmax, float* cand_s, int* cand_i, hipStream_t st,
                     int ns, int aux, const float* thr_init, int xcd,
@@ -367,9 +367,9 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("X"), py::arg("n_valid"), py::arg("rows_per_blk"), py::arg("n_rblk"), py::arg("Q"),
      py::arg("NQ"), py::arg("cs"), py::arg("ci"), py::arg("stream"), py::arg("abl"),
      py::arg("thr") = 0);
-  m.def("attention_config", [](int waves, int kvt) {
-    check(symb_attention_config(waves, kvt), "attention_config");
-  }, py::arg("waves") = 8, py::arg("kvt") = 64);
+  m.def("attention_config", [](int waves, int kvt, int xcd) {
+    check(symb_attention_config(waves, kvt, xcd), "attention_config");
+  }, py::arg("waves") = 8, py::arg("kvt") = 64, py::arg("xcd") = 2);
   m.def("gemm256_ablate", [](int abl) { check(symb_gemm256_ablate(abl), "gemm256_ablate"); });
   m.def("gemm_config", [](int resln_bm, int tile, int group_m) {
     check(symb_gemm_config(resln_bm, tile, group_m), "gemm_config");

@@ -137,8 +137,8 @@ def test_gemm_hipblaslt_route(M, N, K, epi):
 @pytest.mark.parametrize("lens", [[1, 7, 64, 65, 128, 200, 3, 511],   # 64-key tiles
                                   [1, 7, 64, 65, 100, 128, 3],        # <=128: one 128-key tile
                                   [5, 33, 64]])                       # <=64
-@pytest.mark.parametrize("waves,kvt", [(4, 64), (8, 64), (8, 128)])
-def test_attention_varlen(D, nh, lens, waves, kvt):
+@pytest.mark.parametrize("waves,kvt,xcd", [(4, 64, 1), (8, 64, 1), (8, 128, 1), (8, 64, 0)])
+def test_attention_varlen(D, nh, lens, waves, kvt, xcd):
     from codename_symbiont_amd.ops._ext import hip
     from codename_symbiont_amd.ops.kernels import attention
 
@@ -146,11 +146,11 @@ def test_attention_varlen(D, nh, lens, waves, kvt):
     T = int(cu[-1])
     H = nh * D
     qkv = _bf(T, 3 * H, seed=7)
-    hip().attention_config(waves, kvt)
+    hip().attention_config(waves, kvt, xcd)
     try:
         out = attention(qkv, cu, max(lens), nh, D)
     finally:
-        hip().attention_config(8, 64)
+        hip().attention_config(8, 64, 2)
     ref = R.attention_ref(qkv, cu, nh, D)
     _close(out, ref, atol=2e-2, rtol=2e-2, what="attention")
 
