@@ -522,8 +522,10 @@ int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const flo
   }
   if (N % 128 != 0) return -1;
   if ((epi == EPI_BIAS || epi == EPI_RES) &&
-      (g_gemm_lt == 2 || (g_gemm_lt == 1 && K >= 768 && N >= 768 && M >= 4096)))
-    return symb_gemm_lt(epi, A, lda, W, ldw, bias, R, ldr, C, ldc, M, N, K, st);
+      (g_gemm_lt == 2 || (g_gemm_lt == 1 && K >= 768 && N >= 768 && M >= 4096))) {
+    const int rc = symb_gemm_lt(epi, A, lda, W, ldw, bias, R, ldr, C, ldc, M, N, K, st);
+    if (rc != -1 && rc != -2) return rc;   // 0, or a HIP error; else this file's kernels
+  }
   if (g_tile == 9 && symb_gemm256_supported(M, N, K))
     return symb_gemm256(epi, A, lda, W, ldw, bias, R, ldr, C, ldc, M, N, K, g_group_m, st);
   const int tile_mode = g_tile == 10 ? 3 : g_tile;   // 10: auto without the 8-phase kernel (A/B)

@@ -81,7 +81,8 @@ int make_plan(DeviceState& ds, Plan& p, bool res, int M, int N, int K, int lda, 
 }  // namespace
 
 // epi: 0 = + bias, 2 = + bias + R (gemm.hip's EPI_BIAS / EPI_RES).  Returns 0, a HIP error, -1
-// (no algorithm for the shape) or -2 (hipBLASLt call failed).
+// (no algorithm for the shape, or a first use inside a stream capture) or -2 (a hipBLASLt call
+// failed before anything was enqueued); on -1 / -2 symb_gemm falls back to its own kernels.
 int symb_gemm_lt(int epi, const void* A, int lda, const void* W, int ldw, const float* bias,
                  const void* R, int ldr, void* C, int ldc, int M, int N, int K, hipStream_t st) {
   if (M <= 0) return 0;
@@ -93,13 +94,24 @@ int symb_gemm_lt(int epi, const void* A, int lda, const void* W, int ldw, const 
   if (e != hipSuccess) return (int)e;
   std::lock_guard<std::mutex> lk(g_mu);
   DeviceState& ds = g_dev[dev];
-  if (ds.handle == nullptr) {
-    LT_TRY(hipblasLtCreate(&ds.handle));
-    e = hipMalloc(&ds.ws, kWorkspace);
-    if (e != hipSuccess) return (int)e;
-  }
   const auto key = std::make_tuple(epi, M, N, K, lda, ldw, res ? ldr : 0, ldc);
   auto it = ds.plans.find(key);
+  if (ds.handle == nullptr || it == ds.plans.end()) {
+    // first use of this device / shape allocates (workspace) and queries heuristics, neither of
+    // which belongs inside a stream capture: decline, the caller runs gemm.hip's kernel instead
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return -1;
+  }
+  if (ds.handle == nullptr) {
+    if (ds.ws == nullptr) {
+      e = hipMalloc(&ds.ws, kWorkspace);
+      if (e != hipSuccess) {
+        ds.ws = nullptr;
+        return -2;
+      }
+    }
+    LT_TRY(hipblasLtCreate(&ds.handle));
+  }
   if (it == ds.plans.end()) {
     Plan p;
     const int rc = make_plan(ds, p, res, M, N, K, lda, ldw, ldr, ldc);
