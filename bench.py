@@ -64,6 +64,11 @@ def main() -> None:
                     help="fp8: search the bf16 index through an e4m3 copy for 3k candidates and "
                          "re-score them exactly in bf16 (Qdrant quantization + rescore); the "
                          "headline default is the exact bf16 scan")
+    ap.add_argument("--index-prune", choices=["none", "i8"], default="none",
+                    help="i8: EXACT search through an int8 image of the bf16 rows -- rows whose "
+                         "int8 score cannot reach the query's k-th best (a proven error bound) are "
+                         "pruned, the rest re-scored in bf16 (csrc/hip/index_i8.hip); same top-k "
+                         "as the full bf16 scan")
     ap.add_argument("--encoder-dtype", choices=["bf16", "fp8"], default="bf16",
                     help="fp8: e4m3 projection GEMMs (BASELINE config #5); the headline stays bf16")
     ap.add_argument("--embed-dp", choices=["replica", "group"], default="replica",
@@ -105,8 +110,9 @@ def main() -> None:
     rows_per_rank = args.index_rows // info.world
     extra = (K + W + 4) * B
     prefilter = None if args.index_prefilter == "none" else args.index_prefilter
+    prune = None if args.index_prune == "none" else args.index_prune
     shard = HbmIndexShard(cfg.hidden, rows_per_rank + extra, device=dev, dtype=args.index_dtype,
-                          prefilter=prefilter)
+                          prefilter=prefilter, prune=prune)
     if args.mode != "embed":
         shard.fill_random(rows_per_rank, seed=100 + info.rank)
     searcher = ShardedSearcher(shard, info)
@@ -325,6 +331,8 @@ def main() -> None:
             "dtype": args.encoder_dtype,
             "index_dtype": args.index_dtype,
             "index_prefilter": prefilter,
+            "index_search": ("exact: int8 bound-pruned scan + bf16 re-score" if prune
+                             else ("fp8 prefilter + bf16 re-score" if prefilter else "exact bf16 scan")),
             "data": "synthetic token ids, random-init weights, random unit index rows",
             "config": {
                 "model": short, "global_batch": B * info.world, "seq_len": S,

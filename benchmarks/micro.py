@@ -97,7 +97,7 @@ def cmd_scanmq(a):
     from codename_symbiont_amd.index.shard import HbmIndexShard
 
     D, k = 384, 10
-    shard = HbmIndexShard(D, a.rows + 8192, device="cuda")
+    shard = HbmIndexShard(D, a.rows + 8192, device="cuda", prune="i8" if a.prune else None)
     shard.fill_random(a.rows, seed=1)
     q = torch.nn.functional.normalize(torch.randn(a.nq, D, device="cuda"), dim=-1).bfloat16()
     if a.qmode == "near":   # bench-like: fresh embeddings appended last, queries near them
@@ -106,9 +106,12 @@ def cmd_scanmq(a):
 
     shard.mq_min_nq = min(shard.mq_min_nq, a.nq)
 
-    def srch(mq, rsplit=True):
+    prune = shard.prune
+
+    def srch(mq, rsplit=True, pr=False):
         shard.scan_mq = mq
         shard.mq_rsplit = rsplit
+        shard.prune = prune if pr else None
         return shard.search(q, k)
 
     ref = srch(False)
@@ -118,6 +121,13 @@ def cmd_scanmq(a):
     ids_equal = float((ref[1] == got[1]).float().mean())
     max_score_diff = float((ref[0] - got[0]).abs().max())
     variants = {"list256": lambda: srch(False), "mq512": lambda: srch(True)}
+    if prune:   # exact int8 bound-pruned scan + bf16 re-score (index_i8.hip)
+        got4 = srch(True, True, True)
+        torch.cuda.synchronize()
+        pc, po = shard._mq_last
+        ids_equal = min(ids_equal, float((ref[1] == got4[1]).float().mean()))
+        max_score_diff = max(max_score_diff, float((ref[0] - got4[0]).abs().max()))
+        variants["pruned_i8"] = lambda: srch(True, True, True)
     from codename_symbiont_amd.ops._ext import hip
 
     def srch_nt():   # non-temporal row stream
@@ -141,7 +151,11 @@ def cmd_scanmq(a):
     flop = 2 * shard.visible * D * a.nq
     out = {n: dict(ms=round(m, 3), min_ms=round(mn, 3), TFLOPs=round(flop / (m / 1e3) / 1e12))
            for n, (m, mn) in r.items()}
-    print(json.dumps({"bench": "scanmq", "rows": shard.visible, "nq": a.nq, "qmode": a.qmode,
+    extra = {}
+    if prune:
+        extra = {"pruned_overflow": int(po.item()), "pruned_cand_mean": float(pc.float().mean()),
+                 "pruned_cand_max": int(pc.max()), "i8_bounds": [float(v) for v in shard.i8_bounds]}
+    print(json.dumps({"bench": "scanmq", "rows": shard.visible, "nq": a.nq, "qmode": a.qmode, **extra,
                       "ids_equal_frac": ids_equal, "max_score_diff": max_score_diff,
                       "overflow": int(ovf.item()), "cand_mean": float(cnt.float().mean()),
                       "cand_max": int(cnt.max()), "results": out}))
@@ -549,6 +563,7 @@ def main():
     ap.add_argument("--fp8-waves", default="8", help="encoder: comma list of fp8 GEMM wave counts")
     ap.add_argument("--sets", type=int, default=4, help="scanmqabl: 16-query sets per wave (2 or 4)")
     ap.add_argument("--rsplit", type=int, default=1, help="scanmqabl: waves per query group (1, 2)")
+    ap.add_argument("--prune", action="store_true", help="scanmq: also the exact int8-pruned search")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=5)
     a = ap.parse_args()

@@ -119,7 +119,7 @@ class HbmIndexShard:
     tests/test_kernels_gpu.py and profiles/); the default (None) is the exact bf16 scan."""
 
     def __init__(self, dim: int, capacity: int, device="cuda", kmax: int = 16, dtype: str = "bf16",
-                 prefilter: str | None = None, oversample: int = 3):
+                 prefilter: str | None = None, oversample: int = 3, prune: str | None = None):
         if dtype not in ("bf16", "fp8"):
             raise ValueError(f"index dtype must be bf16 or fp8, got {dtype!r}")
         if dtype == "fp8" and dim not in FP8_DIMS:
@@ -131,6 +131,12 @@ class HbmIndexShard:
             raise ValueError(f"an fp8 prefilter needs a bf16 shard of width {FP8_DIMS}")
         self.prefilter = prefilter
         self.oversample = int(oversample)
+        prune = prune or None
+        if prune not in (None, "i8"):
+            raise ValueError(f"index prune must be i8 or None, got {prune!r}")
+        if prune and (dtype != "bf16" or dim != 384):
+            raise ValueError("the int8 pruned search needs a 384-wide bf16 shard")
+        self.prune = prune
         self.dim = dim
         self.dtype = dtype
         self.device = torch.device(device)
@@ -143,6 +149,14 @@ class HbmIndexShard:
         # e4m3 image of the bf16 rows for the prefilter scan (kept in step by every write)
         self.rows8 = (torch.empty(self.rows.shape, dtype=torch.uint8, device=self.device)
                       if prefilter else None)
+        # prune="i8": int8 image of the bf16 rows (per-row scale) for the EXACT bound-pruned
+        # search (csrc/hip/index_i8.hip), plus the two global maxima its error bound needs:
+        # E = max |x - x~| and X = max |x~| over every row ever written (monotone, so conservative)
+        self.rows_i8 = self.sx_i8 = self.i8_bounds = None
+        if prune:
+            self.rows_i8 = torch.empty(self.rows.shape, dtype=torch.int8, device=self.device)
+            self.sx_i8 = torch.ones(self.rows.shape[0], dtype=torch.float32, device=self.device)
+            self.i8_bounds = torch.zeros(2, dtype=torch.float32, device=self.device)
         self.count = 0      # rows reserved (payload slots exist)
         # rows searches may read: published only after their writes are ENQUEUED on the stream
         # the scans share, so a search racing an upsert in another thread never scans a reserved
@@ -204,8 +218,12 @@ class HbmIndexShard:
         return r0
 
     def rows_written(self, r0: int, n: int) -> None:
-        """bf16 rows [r0, r0+n) changed: refresh their e4m3 prefilter image (no-op without one).
-        Callers that write ``rows`` directly (snapshot loads) must call this too."""
+        """bf16 rows [r0, r0+n) changed: refresh their e4m3 prefilter image and their int8
+        pruning image (no-ops without them).  Callers that write ``rows`` directly (snapshot loads)
+        must call this too."""
+        if self.rows_i8 is not None and n > 0:
+            self._quant_i8(self.rows[r0:r0 + n], self.rows_i8[r0:r0 + n], self.sx_i8[r0:r0 + n],
+                           self.i8_bounds)
         if self.rows8 is None or n <= 0:
             return
         src, dst = self.rows[r0:r0 + n], self.rows8[r0:r0 + n]
@@ -215,6 +233,27 @@ class HbmIndexShard:
             K.quant_fp8(src, dst, FP8_SCALE, False)
         else:
             dst.copy_((src.float() * FP8_SCALE).to(torch.float8_e4m3fn).view(torch.uint8))
+
+    def _quant_i8(self, src, dst8, scale, bounds=None):
+        """Per-row int8 image of bf16 rows (index_i8.hip quant_rows_i8); returns the per-row
+        |x - x~| and |x~|, and folds their maxima into ``bounds`` (E, X) when given."""
+        n = src.shape[0]
+        if self.device.type == "cuda":
+            from ..ops._ext import hip, stream_handle
+
+            err = torch.empty(n, dtype=torch.float32, device=self.device)
+            xtn = torch.empty(n, dtype=torch.float32, device=self.device)
+            hip().quant_rows_i8(src.data_ptr(), n, self.dim, dst8.data_ptr(), scale.data_ptr(),
+                                err.data_ptr(), xtn.data_ptr(), stream_handle(self.device))
+        else:
+            from ..ops.reference import quant_rows_i8_ref
+
+            q8, sc, err, xtn = quant_rows_i8_ref(src)
+            dst8.copy_(q8)
+            scale.copy_(sc)
+        if bounds is not None:
+            torch.maximum(bounds, torch.stack([err.max(), xtn.max()]), out=bounds)
+        return err, xtn
 
     def _store(self, r0: int, x: torch.Tensor, normalize: bool) -> None:
         """Write rows (f32 or bf16 on self.device) at r0, unit-normalising them if asked."""
@@ -298,6 +337,10 @@ class HbmIndexShard:
         q_unit = q_unit.to(torch.bfloat16).contiguous()
         if self.prefilter and k < 32:
             return self._search_prefilter(q_unit, k, n_cus)
+        if self.prune and k <= 16 and NQ >= self.mq_min_nq and self._seed_rows(self.visible, k):
+            out = self._search_pruned(q_unit, k, n_cus)
+            if out is not None:
+                return out
         out_s, out_i = self._search_scan(q_unit, k, self.rows, self.dtype, n_cus)
         if self.dtype == "fp8":
             out_s.mul_(1.0 / (FP8_SCALE * FP8_SCALE))
@@ -365,7 +408,7 @@ class HbmIndexShard:
     MQ_TILE_SHIFT = 6         # threshold sample: one 64-row tile in 2^6
     MQ_TAIL_ROWS = 4096       # ... plus at least the last 4096 rows
 
-    def _tile_sample_plan(self, n: int):
+    def _tile_sample_plan(self, n: int, ts: int | None = None):
         """In-place threshold sample over n visible rows, or None when n is too small.
 
         Returns (ts, nv, t0, idx): the emitting kernel's virtual tile v < nv reads physical tile
@@ -373,7 +416,7 @@ class HbmIndexShard:
         of each group of 2^ts; rows [t0, n) (4096..8191 of them) are the exact tail; idx are the
         rows of every SEED_DIV-th sampled tile (the sub-sample that seeds the sample scan, a
         subset of the sample).  Every sampled row lies below t0 <= n - MQ_TAIL_ROWS."""
-        ts = self.MQ_TILE_SHIFT
+        ts = self.MQ_TILE_SHIFT if ts is None else ts
         group = TILE_ROWS << ts                                # rows per tile group
         nv = (n - self.MQ_TAIL_ROWS) // group if n > self.MQ_TAIL_ROWS else 0
         if nv < self.SEED_DIV:
@@ -442,6 +485,70 @@ class HbmIndexShard:
             self._scan(n, q_unit, kmax, k, thr, n_cus, rows, gate=ovf, out=(out_s, out_i))
         self._mq_last = (cnt, ovf)   # candidate counts / overflow flag (tests, diagnostics)
         if self.mq_stats:            # running totals (two tiny kernels per search; off by default)
+            if self._mq_tot is None:
+                self._mq_tot = (torch.zeros(1, dtype=torch.int32, device=dev),
+                                torch.zeros(1, dtype=torch.int32, device=dev))
+            self._mq_tot[0].add_(ovf)
+            torch.maximum(self._mq_tot[1], cnt.max().view(1), out=self._mq_tot[1])
+        return out_s, out_i
+
+    PRUNE_TILE_SHIFT = 5      # pruned search: its exact threshold sample is 1 tile in 2^5
+    PRUNE_CAP = 8192          # candidate slots per query (expected ~1-2k at 100M x 384)
+
+    def _search_pruned(self, q_unit, k: int, n_cus):
+        """EXACT top-k through the int8 image (index_i8.hip has the bound): an exact bf16 sample
+        gives T <= each query's final k-th score; every row whose int8 score reaches T - margin is
+        emitted, re-scored in bf16 and the top-k of those is returned.  A query whose candidates
+        overflow PRUNE_CAP raises the flag that gates the exact bf16 list scan."""
+        from ..ops._ext import hip, stream_handle
+
+        n, NQ, kmax = self.visible, q_unit.shape[0], 16
+        plan = self._tile_sample_plan(n, self.PRUNE_TILE_SHIFT)
+        if plan is None:
+            return None
+        if n_cus is None:
+            n_cus = self._n_cus()
+        # 1. T: the k-th best exact score of a sample of real rows (1 tile in 2^ts, plus the last
+        #    4096+ rows where fresh inserts sit), as in _search_scan
+        ts, nv, t0, idx = plan
+        sub = torch.index_select(self.rows, 0, idx)
+        s0, _ = self._scan(sub.shape[0], q_unit, kmax, k, None, n_cus, sub, "bf16")
+        thr0 = s0[:, k - 1].contiguous() - self.MQ_THR_MARGIN
+        pre_s, _ = self._scan_mq(nv * TILE_ROWS, q_unit, kmax, k, thr0, n_cus, tshift=ts)
+        tail_s, _ = self._scan(n - t0, q_unit, kmax, k, thr0, n_cus, self.rows[t0:], "bf16")
+        T = torch.topk(torch.cat([pre_s, tail_s], 1), k, dim=1).values[:, k - 1] - self.MQ_THR_MARGIN
+        # 2. int8 queries and the per-query margin |q| E + |q - q~| X (+ fp32 slack)
+        q8 = torch.empty(NQ, self.dim, dtype=torch.int8, device=self.device)
+        sq = torch.empty(NQ, dtype=torch.float32, device=self.device)
+        eq, _ = self._quant_i8(q_unit, q8, sq)
+        E, X = self.i8_bounds[0], self.i8_bounds[1]
+        margin = q_unit.float().norm(dim=1) * E + eq * X + 1e-5
+        thr = ((T - margin) / sq).contiguous()
+        # 3. emit every row with (q8 . x8) * sx >= thr, 4. exact bf16 re-score, 5. top-k
+        h, dev, cap = hip(), self.device, self.PRUNE_CAP
+        rsplit = 2 if NQ < 512 else 1
+        n_qblk = math.ceil(NQ / h.i8_queries_per_blk(rsplit))
+        n_rblk = max(1, min(math.ceil(n / (TILE_ROWS * 16)), max(1, round(n_cus / n_qblk))))
+        rows_per_blk = _round_up(max(1, math.ceil(n / n_rblk)), TILE_ROWS)
+        n_rblk = max(1, math.ceil(n / rows_per_blk))
+        cs = torch.empty(NQ, cap, device=dev)
+        ci = torch.empty(NQ, cap, dtype=torch.int32, device=dev)
+        cnt = torch.empty(NQ, dtype=torch.int32, device=dev)
+        ovf = torch.empty(1, dtype=torch.int32, device=dev)
+        out_s = torch.empty(NQ, k, device=dev)
+        out_i = torch.empty(NQ, k, dtype=torch.int32, device=dev)
+        st = stream_handle(dev)
+        h.index_scan_i8(self.rows_i8.data_ptr(), self.sx_i8.data_ptr(), n, rows_per_blk, n_rblk,
+                        q8.data_ptr(), NQ, thr.data_ptr(), cs.data_ptr(), ci.data_ptr(),
+                        cnt.data_ptr(), cap, self.scan_xcd, st, rsplit)
+        h.rescore_bf16(self.rows.data_ptr(), q_unit.data_ptr(), NQ, self.dim, ci.data_ptr(),
+                       cnt.data_ptr(), cap, cs.data_ptr(), st)
+        h.topk_select_counted(cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(), cap, NQ, kmax, k,
+                              out_s.data_ptr(), out_i.data_ptr(), ovf.data_ptr(), st)
+        # overflow (some query had more than cap candidates): the exact bf16 scan, seeded with T
+        self._scan(n, q_unit, kmax, k, T.contiguous(), n_cus, gate=ovf, out=(out_s, out_i))
+        self._mq_last = (cnt, ovf)
+        if self.mq_stats:
             if self._mq_tot is None:
                 self._mq_tot = (torch.zeros(1, dtype=torch.int32, device=dev),
                                 torch.zeros(1, dtype=torch.int32, device=dev))

@@ -95,3 +95,14 @@ def topk_ref(index_rows: torch.Tensor, queries: torch.Tensor, k: int):
     s = queries.float() @ index_rows.float().t()
     k = min(k, index_rows.shape[0])
     return torch.topk(s, k, dim=1)
+
+
+def quant_rows_i8_ref(x: torch.Tensor):
+    """Per-row int8 image of bf16 rows (index_i8.hip quant_rows_i8): scale = max|x| / 127,
+    x8 = round-half-even(x / scale) clamped to +-127; returns (x8, scale, |x - x~|, |x~|)."""
+    xf = x.float()
+    amax = xf.abs().amax(dim=1)
+    sc = torch.where(amax > 0, amax / 127.0, torch.ones_like(amax))
+    q = torch.round(xf / sc[:, None]).clamp_(-127, 127)
+    xt = q * sc[:, None]
+    return q.to(torch.int8), sc, (xf - xt).norm(dim=1), xt.norm(dim=1)

@@ -64,6 +64,14 @@ int symb_topk_merge(const float* cand_s, const int* cand_i, int NQ, int n_cand_p
                     int kmax, int k, float* out_s, int* out_i, int64_t id_offset,
                     int64_t* out_id64, hipStream_t st, const int* gate = nullptr);
 int symb_mq_queries_per_blk(int sets, int rsplit);
+int symb_i8_queries_per_blk(int rsplit);
+int symb_index_scan_i8(const void* X8, const float* sx, int n_valid, int rows_per_blk, int n_rblk,
+                       const void* Q8, int NQ, const float* thr, float* cand_s, int* cand_i,
+                       int* cand_n, int cap, int xcd, hipStream_t st, int rsplit);
+int symb_rescore_bf16(const void* X, const void* Q, int NQ, int dim, const int* cand_i,
+                      const int* cand_n, int cap, float* cand_s, hipStream_t st);
+int symb_quant_rows_i8(const void* X, int n, int dim, void* X8, float* sx, float* err, float* xtn,
+                       hipStream_t st);
 int symb_gemm_lt_config(int mode);
 int symb_mq_config(int aux);
 int symb_index_scan_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
@@ -325,6 +333,27 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("stream"), py::arg("ns") = 0, py::arg("aux") = -1, py::arg("thr_init") = 0,
      py::arg("xcd") = 1, py::arg("gate") = 0);
   // multi-query-block D=384 scan (index_mq.hip): candidates above the seeded thresholds
+  m.def("i8_queries_per_blk", [](int rsplit) { return symb_i8_queries_per_blk(rsplit); },
+        py::arg("rsplit") = 2);
+  m.def("index_scan_i8", [](uptr X8, uptr sx, int n_valid, int rows_per_blk, int n_rblk, uptr Q8,
+                            int NQ, uptr thr, uptr cand_s, uptr cand_i, uptr cand_n, int cap,
+                            int xcd, uptr st, int rsplit) {
+    check(symb_index_scan_i8(P<void>(X8), P<const float>(sx), n_valid, rows_per_blk, n_rblk,
+                             P<void>(Q8), NQ, P<const float>(thr), P<float>(cand_s), P<int>(cand_i),
+                             P<int>(cand_n), cap, xcd, S(st), rsplit),
+          "index_scan_i8");
+  });
+  m.def("rescore_bf16", [](uptr X, uptr Q, int NQ, int dim, uptr cand_i, uptr cand_n, int cap,
+                           uptr cand_s, uptr st) {
+    check(symb_rescore_bf16(P<void>(X), P<void>(Q), NQ, dim, P<const int>(cand_i),
+                            P<const int>(cand_n), cap, P<float>(cand_s), S(st)),
+          "rescore_bf16");
+  });
+  m.def("quant_rows_i8", [](uptr X, int n, int dim, uptr X8, uptr sx, uptr err, uptr xtn, uptr st) {
+    check(symb_quant_rows_i8(P<void>(X), n, dim, P<void>(X8), P<float>(sx), P<float>(err),
+                             P<float>(xtn), S(st)),
+          "quant_rows_i8");
+  });
   m.def("gemm_lt_config", [](int mode) { check(symb_gemm_lt_config(mode), "gemm_lt_config"); },
         py::arg("mode"));
   m.def("mq_config", [](int aux) { check(symb_mq_config(aux), "mq_config"); }, py::arg("aux"));

@@ -1,0 +1,444 @@
+// EXACT bf16 top-k through an int8 image of the index: a bound-pruned candidate scan followed by an
+// exact bf16 re-score (SURVEY.md §2.5 X2/X3 for the 384-wide headline shard).
+//
+// Why: at 256 queries the bf16 emitting scan (index_mq.hip) is bound by the chip's power limit,
+// streaming 768 bytes and 2 x 256 x 384 bf16 MFMA FLOP per row (profiles/r2_rsplit/).  An int8
+// image of the rows is half the bytes and v_mfma_i32_16x16x64_i8 runs at twice the bf16 rate, so
+// the same row stream costs about half.  int8 scores are only approximate, so they are used to
+// PRUNE, never to rank:
+//
+//   x~ = sx * x8 (per-row scale sx = max|x| / 127, x8 = round(x / sx)), q~ = sq * q8 likewise,
+//   s = q . x (the bf16 cosine), s~ = q~ . x~ = sq * sx * (q8 . x8) (exact integer dot).
+//   |s - s~| = |q . (x - x~) + (q - q~) . x~| <= |q| * E + |q - q~| * X        (Cauchy-Schwarz)
+//   with E = max over rows of |x - x~| and X = max over rows of |x~| (tracked at every write) and
+//   |q - q~| computed per query.  If T lower-bounds the query's final k-th score (an exact sample,
+//   index/shard.py), every row of the true top-k has s >= T, hence s~ >= T - margin.
+//
+// So this kernel EMITS every row with s~ >= T - margin (a superset of the true top-k), the
+// re-score kernel replaces each candidate's score by its exact bf16 dot product, and the select
+// kernel (index_mq.hip) takes the top-k of those: the same rows and the same scores (up to fp32
+// summation order) as scanning every row in bf16.  A query whose candidate buffer overflows raises
+// the device flag on which the exact bf16 list scan re-runs the batch (gated, no host sync).
+//
+// Scan geometry: the emitting design of index_mq.hip at half the row bytes.  A 64-row tile is
+// 24 KiB; a 16-row x 64-byte piece (one k-step of one 16-row sub-tile) is exactly the bf16
+// kernel's 1 KiB piece, so the LDS image, the LDS-DMA source offsets, the conflict-free fragment
+// offsets and the candidate stages are the same.  8 waves x 64 queries (4 sets x 6 k-steps x 4
+// registers = 96 VGPRs of queries as B operands); RSPLIT = 2: waves w and w + 4 hold the same
+// queries and split each tile's rows (256 queries per workgroup), RSPLIT = 1: 512.  The tile's
+// 64 row scales ride the ring as one extra 4-byte-per-lane LDS-DMA issued by wave 0.
+#include "scan_common.h"
+
+namespace symb {
+
+namespace i8s {
+constexpr int D = 384;                      // int8 bytes per row
+constexpr int WAVES = 8;
+constexpr int SETS = 4;                     // 16-query sets per wave
+constexpr int SUB = 16;
+constexpr int TR = 64;
+constexpr int NSUB = TR / SUB;
+constexpr int NS = 5;                       // LDS ring depth in tiles
+constexpr int TILE_BYTES = TR * D;          // 24 KiB
+constexpr int LOADS = TILE_BYTES / (1024 * WAVES);  // 3 LDS-DMA pieces per wave per tile
+constexpr int NKS = D / 64;                 // 6 k-steps of v_mfma_i32_16x16x64_i8
+constexpr int PIECE = 1024;
+constexpr int PF = 2;                       // fragment reads in flight
+constexpr int R = PF + 1;
+constexpr int DMA_EVERY = 2;
+constexpr int SC_BYTES = TR * 4;            // one tile's row scales
+constexpr int STW = 192;                    // staged candidates per wave
+constexpr int STAGE_BYTES = STW * 10;
+constexpr int LDS_BYTES = NS * TILE_BYTES + NS * SC_BYTES + WAVES * STAGE_BYTES;
+static_assert(TILE_BYTES % (1024 * WAVES) == 0, "tile must split evenly over waves");
+static_assert(NSUB * NKS * PIECE == TILE_BYTES, "a tile is NSUB x NKS pieces");
+static_assert(LOADS * DMA_EVERY <= NKS, "DMA pieces must fit the first chain");
+static_assert(NKS % R == 0, "cross-chain prefetch: fragment j of the next chain uses slot j % R");
+static_assert(LDS_BYTES <= 160 * 1024, "ring + scales + stages exceed the CU's 160 KiB");
+}  // namespace i8s
+
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+
+template <int OFF>
+__device__ __forceinline__ void i8_read16(i32x4& dst, uint32_t addr) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(addr), "i"(OFF));
+}
+template <int N>
+__device__ __forceinline__ void i8_lgkm(i32x4& v) {
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(v) : "i"(N));
+}
+template <bool FIRST>
+__device__ __forceinline__ void i8_mfma(i32x4& acc, const i32x4& a, const i32x4& q) {
+  if constexpr (FIRST)
+    asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, 0" : "=&v"(acc) : "v"(a), "v"(q));
+  else
+    asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(q));
+}
+
+// k-step KS of one 16-row sub-tile (index_mq.hip MqChain, int8 operands).
+template <int KS, int DMA_PIECES, bool NEXT>
+struct I8Chain {
+  template <class Dma>
+  __device__ __forceinline__ static void run(i32x4 (&acc)[i8s::SETS], i32x4 (&a)[i8s::R],
+                                             const i32x4 (&qf)[i8s::SETS][i8s::NKS],
+                                             uint32_t base, uint32_t next, const Dma& dma) {
+    using namespace i8s;
+    if constexpr (DMA_PIECES > 0 && KS % DMA_EVERY == 0 && KS / DMA_EVERY < DMA_PIECES)
+      dma(KS / DMA_EVERY);
+    constexpr int outstanding = (NEXT || NKS - KS >= PF) ? PF : (NKS - KS);
+    i8_lgkm<outstanding - 1>(a[KS % R]);
+#pragma unroll
+    for (int s = 0; s < SETS; ++s) i8_mfma<KS == 0>(acc[s], a[KS % R], qf[s][KS]);
+    if constexpr (KS + 1 == NKS) asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+    if constexpr (KS + PF < NKS)
+      i8_read16<(KS + PF) * PIECE>(a[(KS + PF) % R], base);
+    else if constexpr (NEXT)
+      i8_read16<(KS + PF - NKS) * PIECE>(a[(KS + PF) % R], next);
+    if constexpr (KS + 1 < NKS) I8Chain<KS + 1, DMA_PIECES, NEXT>::run(acc, a, qf, base, next, dma);
+  }
+};
+
+template <int J>
+__device__ __forceinline__ void i8_prologue(i32x4 (&a)[i8s::R], uint32_t base) {
+  i8_read16<J * i8s::PIECE>(a[J % i8s::R], base);
+  if constexpr (J + 1 < i8s::PF) i8_prologue<J + 1>(a, base);
+}
+
+__device__ __forceinline__ const char* i8_uniform(const char* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return reinterpret_cast<const char*>(((uint64_t)hi << 32) | lo);
+}
+
+// X8: [>= round_up(n_valid, 64), 384] int8 rows; sx: their scales (f32, same padding);
+// Q8: [NQ, 384] int8 queries; thr[NQ]: emit a row iff (q8 . x8) * sx >= thr (already divided by
+// the query's scale).  cand_s/cand_i: [NQ][cap]; cand_n[NQ] zeroed by the host entry.
+template <int RSPLIT>
+__global__ __launch_bounds__(512, 1) void index_scan_i8_kernel(
+    const int8_t* __restrict__ X8, const float* __restrict__ sx, int n_valid, int rows_per_blk,
+    const int8_t* __restrict__ Q8, int NQ, int n_qblk, int xcd, const float* __restrict__ thr_in,
+    float* __restrict__ cand_s, int* __restrict__ cand_i, int* __restrict__ cand_n, int cap) {
+  using namespace i8s;
+  constexpr int QW = SETS * 16, QWAVES = WAVES / RSPLIT, QPB = QWAVES * QW;
+  constexpr int NSW = NSUB / RSPLIT;
+  static_assert(RSPLIT == 1 || RSPLIT == 2, "row split");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lb = xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int qb = lb % n_qblk, rb = lb / n_qblk;
+  const int row_begin = rb * rows_per_blk;
+  const int row_end = min(row_begin + rows_per_blk, n_valid);
+  const int n_tiles = row_end > row_begin ? (row_end - row_begin + TR - 1) / TR : 0;
+
+  // ---- query fragments (B operand: lane holds query lane&15, k-bytes 16*(lane>>4) .. +16) ----
+  const int qwave = wave % QWAVES;
+  const int j0 = (wave / QWAVES) * NSW;
+  const int qbase = qb * QPB + qwave * QW + (lane & 15);
+  i32x4 qf[SETS][NKS];
+  float thr[SETS];
+#pragma unroll
+  for (int s = 0; s < SETS; ++s) {
+    const int q = qbase + s * 16;
+    const int8_t* qp = Q8 + (size_t)min(q, NQ - 1) * D + (lane >> 4) * 16;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) qf[s][ks] = *reinterpret_cast<const i32x4*>(qp + ks * 64);
+    thr[s] = q < NQ ? thr_in[q] : INFINITY;
+  }
+#pragma unroll
+  for (int s = 0; s < SETS; ++s) {
+    asm volatile("" ::"v"(thr[s]));
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) asm volatile("" ::"v"(qf[s][ks]));
+  }
+
+  // ---- LDS-DMA (index_mq.hip layout): lane l fetches row l>>2 of a piece, chunk (l&3)^f ------
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const uint32_t loff = (uint32_t)((lane >> 2) * D + (((lane & 3) ^ ((lane >> 3) & 2)) * 16));
+  char* scl = smem + NS * TILE_BYTES;   // NS x 64 row scales
+  auto issue_tile = [&](int t, int i) {  // piece i of tile t (+ the scales: wave 0, piece 0)
+    const int tt = min(t, n_tiles - 1);   // past the end: re-load the last tile (vmcnt stays exact)
+    const int p = i * WAVES + wave_u, j = p / NKS, ks = p % NKS;
+    const int prow = row_begin + tt * TR;
+    const char* base = reinterpret_cast<const char*>(X8 + (size_t)(prow + j * SUB) * D + ks * 64);
+    glds16_aux<0>(i8_uniform(base) + loff, smem + (t % NS) * TILE_BYTES + p * PIECE);
+    if (wave_u == 0 && i == 0)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(sx + prow + lane),
+          (__attribute__((address_space(3))) void*)(scl + (t % NS) * SC_BYTES), 4, 0, 0);
+  };
+  const uint32_t lds_smem = lds_addr(smem);
+  const uint32_t foff = (uint32_t)((lane & 15) * 64 + (((lane >> 4) ^ ((lane >> 1) & 2)) * 16));
+
+  // ---- candidate emission (index_mq.hip: per-wave LDS stage, ballot slots, rare flushes) ------
+  char* stage = smem + NS * TILE_BYTES + NS * SC_BYTES + wave_u * STAGE_BYTES;
+  float* st_s = reinterpret_cast<float*>(stage);
+  int* st_r = reinterpret_cast<int*>(stage + STW * 4);
+  uint16_t* st_q = reinterpret_cast<uint16_t*>(stage + STW * 8);
+  int nst = 0;
+  auto flush = [&]() {
+    int qw = qb * QPB + (wave_u % QWAVES) * QW;
+    asm volatile("" : "+v"(qw));
+    for (int e = lane; e < nst; e += 64) {
+      const int q = qw + st_q[e];
+      const int slot = atomicAdd(cand_n + q, 1);
+      if (slot < cap) {
+        cand_s[(size_t)q * cap + slot] = st_s[e];
+        cand_i[(size_t)q * cap + slot] = st_r[e];
+      }
+    }
+    nst = 0;
+  };
+  // this lane's 4 row scales of sub-tile jj in ring slot `slot`
+  auto scales = [&](int slot, int jj) {
+    return *reinterpret_cast<const f32x4*>(scl + slot * SC_BYTES + (jj * SUB + 4 * (lane >> 4)) * 4);
+  };
+  // one 16-row sub-tile at row0 with this lane's row scales s4
+  auto emit = [&](i32x4 (&acc)[SETS], int row0, const f32x4 s4) {
+    const int rl = row0 + 4 * (lane >> 4);
+    float v[SETS][4];
+    float mx[SETS];
+#pragma unroll
+    for (int s = 0; s < SETS; ++s) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[s][r] = (float)acc[s][r] * s4[r];
+        if (rl + r >= row_end) v[s][r] = -INFINITY;
+      }
+      mx[s] = fmaxf(fmaxf(v[s][0], v[s][1]), fmaxf(v[s][2], v[s][3]));
+    }
+    bool hit = false;
+#pragma unroll
+    for (int s = 0; s < SETS; ++s) hit |= mx[s] >= thr[s];
+    if (__builtin_amdgcn_ballot_w64(hit)) {
+      int lo = lane;
+      asm volatile("" : "+v"(lo));
+      const int lrow = row0 + 4 * (lo >> 4), lq = lo & 15;
+#pragma unroll
+      for (int s = 0; s < SETS; ++s) {
+        if (!__builtin_amdgcn_ballot_w64(mx[s] >= thr[s])) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool p = v[s][r] >= thr[s];
+          const uint64_t m = __builtin_amdgcn_ballot_w64(p);
+          if (m) {
+            if (nst > STW - 64) flush();
+            const int idx = nst + (int)__builtin_amdgcn_mbcnt_hi(
+                                      (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+            if (p) {
+              st_s[idx] = v[s][r];
+              st_r[idx] = lrow + r;
+              st_q[idx] = (uint16_t)(s * 16 + lq);
+            }
+            nst += __builtin_popcountll(m);
+          }
+        }
+      }
+    }
+  };
+
+  // wave 0 carries one extra vector-memory op per tile (the scale DMA)
+  constexpr int W0X = 1;
+  if (n_tiles > 0) {
+#pragma unroll
+    for (int p = 0; p < NS - 1; ++p)
+#pragma unroll
+      for (int i = 0; i < LOADS; ++i) issue_tile(p, i);
+  }
+  i32x4 a[R];
+  i32x4 acc[SETS];
+  const bool late = wave_u >= WAVES / 2;   // partner waves (w, w + 4) stay half a test apart
+  // the late wave tests its last sub-tile after the NEXT barrier, when wave 0 may already be
+  // refilling that tile's scale slot: its scales are read into registers before the barrier
+  f32x4 s4_last = {0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < n_tiles; ++t) {
+    if (wave_u == 0)
+      wait_vmcnt<(LOADS + W0X) * (NS - 2)>();
+    else
+      wait_vmcnt<LOADS * (NS - 2)>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const int slot = t % NS;
+    const uint32_t tbase = lds_smem + (uint32_t)(slot * TILE_BYTES);
+    const int row0 = row_begin + t * TR;
+    const int tnext = t + NS - 1;
+    auto dma = [&](int i) { issue_tile(tnext, i); };
+    const uint32_t fw = tbase + foff + j0 * NKS * PIECE;
+    const int last = (j0 + NSW - 1) * SUB;
+    i8_prologue<0>(a, fw);
+    if (late && t > 0) emit(acc, row0 - TR + last, s4_last);
+    if constexpr (NSW > 1)
+      I8Chain<0, LOADS, true>::run(acc, a, qf, fw, fw + NKS * PIECE, dma);
+    else
+      I8Chain<0, LOADS, false>::run(acc, a, qf, fw, 0, dma);
+#pragma unroll
+    for (int j = 1; j < NSW; ++j) {
+      emit(acc, row0 + (j0 + j - 1) * SUB, scales(slot, j0 + j - 1));
+      if (j + 1 < NSW)
+        I8Chain<0, 0, true>::run(acc, a, qf, fw + j * NKS * PIECE, fw + (j + 1) * NKS * PIECE, NoDma());
+      else
+        I8Chain<0, 0, false>::run(acc, a, qf, fw + j * NKS * PIECE, 0, NoDma());
+    }
+    if (!late)
+      emit(acc, row0 + last, scales(slot, j0 + NSW - 1));
+    else
+      s4_last = scales(slot, j0 + NSW - 1);
+  }
+  if (late && n_tiles > 0) emit(acc, row_begin + (n_tiles - 1) * TR + (j0 + NSW - 1) * SUB, s4_last);
+  if (nst) flush();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// Exact re-score of every candidate: cand_s[q][c] = <Q[q], X[cand_i[q][c]]> over the bf16 rows
+// (fp32 accumulation).  One workgroup per query, one wave per candidate, 6 elements per lane.
+__global__ __launch_bounds__(256) void rescore_bf16_kernel(
+    const __bf16* __restrict__ X, const __bf16* __restrict__ Q, const int* __restrict__ cand_i,
+    const int* __restrict__ cand_n, int cap, float* __restrict__ cand_s) {
+  constexpr int D = 384, PER = D / 64;
+  const int q = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = min(cand_n[q], cap);
+  float qv[PER];
+  {
+    const uint32_t* qp = reinterpret_cast<const uint32_t*>(Q + (size_t)q * D + PER * lane);
+#pragma unroll
+    for (int i = 0; i < PER / 2; ++i) {
+      const uint32_t w = qp[i];
+      qv[2 * i] = __uint_as_float(w << 16);
+      qv[2 * i + 1] = __uint_as_float(w & 0xffff0000u);
+    }
+  }
+  const int* ci = cand_i + (size_t)q * cap;
+  float* cs = cand_s + (size_t)q * cap;
+  constexpr int U = 4;   // candidates in flight per wave
+  for (int c0 = wave * U; c0 < n; c0 += 4 * U) {
+    uint32_t w[U][PER / 2];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = min(c0 + u, n - 1);
+      const uint32_t* xp = reinterpret_cast<const uint32_t*>(X + (size_t)ci[c] * D + PER * lane);
+#pragma unroll
+      for (int i = 0; i < PER / 2; ++i) w[u][i] = xp[i];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float d = 0.f;
+#pragma unroll
+      for (int i = 0; i < PER / 2; ++i) {
+        d = fmaf(qv[2 * i], __uint_as_float(w[u][i] << 16), d);
+        d = fmaf(qv[2 * i + 1], __uint_as_float(w[u][i] & 0xffff0000u), d);
+      }
+      d = wave_sum(d);
+      if (lane == 0 && c0 + u < n) cs[c0 + u] = d;
+    }
+  }
+}
+
+// Per-row int8 quantiser of 384-wide bf16 rows: sx = max|x| / 127, x8 = round(x / sx), and the
+// per-row |x - sx * x8| (err) and |sx * x8| (xtn) the pruning bound needs.  One wave per row.
+__global__ __launch_bounds__(256) void quant_rows_i8_kernel(const __bf16* __restrict__ X, int n,
+                                                            int8_t* __restrict__ X8,
+                                                            float* __restrict__ sx,
+                                                            float* __restrict__ err,
+                                                            float* __restrict__ xtn) {
+  constexpr int D = 384, PER = D / 64;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n) return;
+  float x[PER];
+  const uint32_t* xp = reinterpret_cast<const uint32_t*>(X + (size_t)row * D + PER * lane);
+#pragma unroll
+  for (int i = 0; i < PER / 2; ++i) {
+    const uint32_t w = xp[i];
+    x[2 * i] = __uint_as_float(w << 16);
+    x[2 * i + 1] = __uint_as_float(w & 0xffff0000u);
+  }
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) amax = fmaxf(amax, fabsf(x[i]));
+  amax = wave_max(amax);
+  const float s = amax > 0.f ? amax / 127.f : 1.f;
+  const float inv = 1.f / s;
+  float e2 = 0.f, n2 = 0.f;
+  int qv[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    qv[i] = max(-127, min(127, (int)rintf(x[i] * inv)));
+    const float xt = (float)qv[i] * s;
+    e2 += (x[i] - xt) * (x[i] - xt);
+    n2 += xt * xt;
+  }
+  e2 = wave_sum(e2);
+  n2 = wave_sum(n2);
+  uint16_t* op = reinterpret_cast<uint16_t*>(X8 + (size_t)row * D + PER * lane);
+#pragma unroll
+  for (int i = 0; i < PER / 2; ++i)
+    op[i] = (uint16_t)((qv[2 * i] & 0xff) | ((qv[2 * i + 1] & 0xff) << 8));
+  if (lane == 0) {
+    sx[row] = s;
+    err[row] = sqrtf(e2);
+    xtn[row] = sqrtf(n2);
+  }
+}
+
+}  // namespace symb
+
+using namespace symb;
+
+int symb_i8_queries_per_blk(int rsplit) { return i8s::WAVES / rsplit * 16 * i8s::SETS; }
+
+template <int RSPLIT>
+static int launch_i8(const void* X8, const float* sx, int n_valid, int rows_per_blk, int n_rblk,
+                     const void* Q8, int NQ, const float* thr, float* cand_s, int* cand_i,
+                     int* cand_n, int cap, int xcd, hipStream_t st) {
+  constexpr int qpb = i8s::WAVES / RSPLIT * 16 * i8s::SETS;
+  const int n_qblk = (NQ + qpb - 1) / qpb;
+  constexpr int lds = i8s::LDS_BYTES;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)index_scan_i8_kernel<RSPLIT>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL((index_scan_i8_kernel<RSPLIT>), dim3(n_rblk * n_qblk), dim3(512), lds, st,
+                     (const int8_t*)X8, sx, n_valid, rows_per_blk, (const int8_t*)Q8, NQ, n_qblk,
+                     xcd, thr, cand_s, cand_i, cand_n, cap);
+  return (int)hipGetLastError();
+}
+
+// rows_per_blk % 64 == 0, n_rblk * rows_per_blk >= n_valid, X8 / sx padded to a whole last
+// tile (the DMA reads whole tiles).  rsplit 2 = 256 queries per workgroup, 1 = 512.
+int symb_index_scan_i8(const void* X8, const float* sx, int n_valid, int rows_per_blk, int n_rblk,
+                       const void* Q8, int NQ, const float* thr, float* cand_s, int* cand_i,
+                       int* cand_n, int cap, int xcd, hipStream_t st, int rsplit) {
+  if (NQ <= 0) return 0;
+  if (rows_per_blk % i8s::TR || n_rblk <= 0 || thr == nullptr || cap <= 0 || n_valid <= 0)
+    return -1;
+  if ((long long)n_rblk * rows_per_blk < n_valid) return -1;
+  hipError_t e = hipMemsetAsync(cand_n, 0, sizeof(int) * (size_t)NQ, st);
+  if (e != hipSuccess) return (int)e;
+  if (rsplit == 2)
+    return launch_i8<2>(X8, sx, n_valid, rows_per_blk, n_rblk, Q8, NQ, thr, cand_s, cand_i, cand_n,
+                        cap, xcd, st);
+  if (rsplit == 1)
+    return launch_i8<1>(X8, sx, n_valid, rows_per_blk, n_rblk, Q8, NQ, thr, cand_s, cand_i, cand_n,
+                        cap, xcd, st);
+  return -1;
+}
+
+int symb_rescore_bf16(const void* X, const void* Q, int NQ, int dim, const int* cand_i,
+                      const int* cand_n, int cap, float* cand_s, hipStream_t st) {
+  if (NQ <= 0) return 0;
+  if (dim != 384 || cap <= 0) return -1;
+  hipLaunchKernelGGL(rescore_bf16_kernel, dim3(NQ), dim3(256), 0, st, (const __bf16*)X,
+                     (const __bf16*)Q, cand_i, cand_n, cap, cand_s);
+  return (int)hipGetLastError();
+}
+
+int symb_quant_rows_i8(const void* X, int n, int dim, void* X8, float* sx, float* err, float* xtn,
+                       hipStream_t st) {
+  if (n <= 0) return 0;
+  if (dim != 384) return -1;
+  hipLaunchKernelGGL(quant_rows_i8_kernel, dim3((n + 3) / 4), dim3(256), 0, st, (const __bf16*)X,
+                     n, (int8_t*)X8, sx, err, xtn);
+  return (int)hipGetLastError();
+}

@@ -370,6 +370,68 @@ def test_index_scan_mq_exact(nq, rsplit):
     _close(s1, true, atol=2e-3, what="mq returned rows")
 
 
+def test_quant_rows_i8_matches_reference():
+    """index_i8.hip's per-row int8 quantiser == the torch reference (scale, codes, error norms)."""
+    from codename_symbiont_amd.ops._ext import hip, stream_handle
+
+    x = torch.nn.functional.normalize(_f(5003, 384, seed=61), dim=-1).bfloat16()
+    x[7] = 0   # a zero row keeps scale 1 and codes 0
+    q8 = torch.empty(5003, 384, dtype=torch.int8, device=DEV)
+    sc = torch.empty(5003, device=DEV)
+    err = torch.empty(5003, device=DEV)
+    xtn = torch.empty(5003, device=DEV)
+    hip().quant_rows_i8(x.data_ptr(), 5003, 384, q8.data_ptr(), sc.data_ptr(), err.data_ptr(),
+                        xtn.data_ptr(), stream_handle())
+    r8, rs, rerr, rxtn = R.quant_rows_i8_ref(x)
+    torch.cuda.synchronize()
+    _close(sc, rs, atol=0, rtol=1e-6, what="i8 scales")
+    assert ((q8.int() - r8.int()).abs() <= 1).all()
+    assert (q8 == r8).float().mean().item() > 0.999      # x * (1/s) vs x / s at exact halves
+    # the error norms the pruning bound uses are those of the codes actually stored
+    xt = q8.float() * sc[:, None]
+    _close(err, (x.float() - xt).norm(dim=1), atol=1e-6, what="i8 |x - x~|")
+    _close(xtn, xt.norm(dim=1), atol=1e-5, what="i8 |x~|")
+
+
+@pytest.mark.parametrize("nq,data", [(256, "random"), (300, "random"), (512, "random"),
+                                     (1100, "random"), (256, "clustered"), (512, "near")])
+def test_index_pruned_search_is_exact(nq, data):
+    """prune="i8" (int8 bound-pruned scan + exact bf16 re-score) returns the rows and scores of the
+    exact bf16 scan: random data, tight clusters (near-ties everywhere: candidate overflow takes
+    the gated exact path) and queries that are noisy copies of stored rows."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+
+    n, k, D = (1 << 20) + 777, 10, 384
+    g = torch.Generator(device=DEV).manual_seed(71)
+    if data == "clustered":
+        centers = torch.randn(64, D, device=DEV, generator=g)
+        x = centers[torch.randint(0, 64, (n,), device=DEV, generator=g)]
+        x = x + 0.05 * torch.randn(n, D, device=DEV, generator=g)
+    else:
+        x = torch.randn(n, D, device=DEV, generator=g)
+    ref = HbmIndexShard(D, n + 4096)
+    shard = HbmIndexShard(D, n + 4096, prune="i8")
+    for sh in (ref, shard):
+        sh.append_f32(x)
+    if data == "random":
+        q = torch.randn(nq, D, device=DEV, generator=g)
+    else:
+        q = x[torch.randint(0, n, (nq,), device=DEV, generator=g)].clone()
+        q += (0.02 if data == "clustered" else 0.5 / math.sqrt(D)) * torch.randn_like(q)
+    q = torch.nn.functional.normalize(q, dim=-1).bfloat16()
+    s0, r0 = ref.search(q, k)
+    s1, r1 = shard.search(q, k)
+    cnt, ovf = shard._mq_last
+    torch.cuda.synchronize()
+    if data != "clustered":
+        assert int(ovf.item()) == 0, "random / near data must not overflow the candidate buffer"
+        assert cnt.float().mean().item() < shard.PRUNE_CAP / 2
+    _close(s1, s0, atol=2e-5, what="pruned vs exact scores")
+    assert (r0 == r1).float().mean().item() > 0.999
+    true = (q.float() @ shard.unit_rows().float().t()).gather(1, r1.long())
+    _close(s1, true, atol=2e-3, what="pruned returned rows")
+
+
 def test_index_scan_mq_overflow_falls_back_exact():
     """6000 copies of query 0 in the shard overflow its candidate buffer: the gated 256-query
     kernel re-runs the batch on the GPU and the answer stays exact."""
