@@ -104,6 +104,18 @@ class PayloadStore:
 
 
 FP8_SCALE = 256.0  # == ops.kernels.FP8_SCALE (kept import-free for CPU-only users)
+
+
+def resolve_prune(mode: str | None, dtype: str = "bf16", dim: int = 384,
+                  prefilter: str | None = None) -> str | None:
+    """``SYMB_INDEX_PRUNE``: "auto" (default) = the exact int8-pruned search wherever it applies
+    (384-wide bf16 shards without an fp8 prefilter), "i8" = require it, "" / "none" = plain scan."""
+    mode = (mode or "").strip().lower()
+    if mode in ("", "none", "0", "off"):
+        return None
+    if mode == "auto":
+        return "i8" if (dtype == "bf16" and dim == 384 and not prefilter) else None
+    return mode
 FP8_DIMS = (256, 384, 512, 768, 1024)   # row widths the fp8 scan kernel takes
 
 

@@ -31,14 +31,15 @@ from ..ops._ext import native as _native  # noqa: E402
 class VectorStore:
     def __init__(self, dim: int, capacity: int, device=None, snapshot_dir: str = "",
                  snapshot_every: int = 100_000, group=None, dtype: str = "bf16",
-                 prefilter: str | None = None):
+                 prefilter: str | None = None, prune: str | None = None):
         if device is None:
             device = "cuda" if torch.cuda.is_available() else "cpu"
         self.dim = dim
         self.group = group
         self.shard = group.shard if group is not None else HbmIndexShard(dim, capacity, device,
                                                                             dtype=dtype,
-                                                                            prefilter=prefilter)
+                                                                            prefilter=prefilter,
+                                                                            prune=prune)
         self.dir = snapshot_dir
         self.snapshot_every = snapshot_every
         self._since_snapshot = 0

@@ -54,12 +54,13 @@ class PartialSearchError(RankUnavailableError):
 
 class IndexGroup:
     def __init__(self, info: DistInfo, dim: int, capacity_per_rank: int, group=None,
-                 dtype: str = "bf16", prefilter: str | None = None):
+                 dtype: str = "bf16", prefilter: str | None = None, prune: str | None = None):
         self.info = info
         self.dim = dim
         self.group = group
         dev = info.device
-        self.shard = HbmIndexShard(dim, capacity_per_rank, dev, dtype=dtype, prefilter=prefilter)
+        self.shard = HbmIndexShard(dim, capacity_per_rank, dev, dtype=dtype, prefilter=prefilter,
+                                   prune=prune)
         self.comm_device = dev if info.backend == "nccl" else torch.device("cpu")
         # rank-0 bookkeeping; ops may arrive from several executor threads, but the collective
         # sequence of one op must never interleave with another's

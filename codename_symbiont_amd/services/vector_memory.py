@@ -18,7 +18,7 @@ import uuid
 import numpy as np
 
 from ..utils.trace import stage
-from ..index.shard import Payload
+from ..index.shard import Payload, resolve_prune
 from ..index.store import VectorStore
 from ..models.config import get_config
 from ..ops._ext import native
@@ -40,7 +40,10 @@ class VectorMemoryService(Service):
                                           device="cpu" if self.cfg.force_cpu else None,
                                           snapshot_dir=self.cfg.snapshot_dir,
                                           dtype=self.cfg.index_dtype,
-                                          prefilter=self.cfg.index_prefilter or None)
+                                          prefilter=self.cfg.index_prefilter or None,
+                                          prune=resolve_prune(self.cfg.index_prune,
+                                                              self.cfg.index_dtype, dim,
+                                                              self.cfg.index_prefilter))
         if self.cfg.index_fill_random and self.store.count == 0:
             self.store.shard.fill_random(self.cfg.index_fill_random, seed=17)
         self.log.info("[INDEX_SETUP] collection '%s': dim %d, capacity %d, device %s, %d points",
@@ -264,7 +267,9 @@ def main() -> None:
     info = D.init()
     dim = cfg.index_dim or get_config(cfg.model).hidden
     group = IndexGroup(info, dim, cfg.index_capacity // info.world + 1, dtype=cfg.index_dtype,
-                       prefilter=cfg.index_prefilter or None)
+                       prefilter=cfg.index_prefilter or None,
+                       prune=resolve_prune(cfg.index_prune, cfg.index_dtype, dim,
+                                           cfg.index_prefilter))
     group.snapshot_root = cfg.snapshot_dir or None
     # liveness: every rank heart-beats on health.index.<rank>; rank 0 refuses ops while a peer is
     # silent (fast error replies instead of a collective blocked until the RCCL timeout)

@@ -68,6 +68,10 @@ class Config:
     # "fp8": bf16 index searched through an e4m3 prefilter + exact bf16 re-score (Qdrant's
     # quantization + rescore); "" = exact bf16 scan
     index_prefilter: str = field(default_factory=lambda: os.environ.get("SYMB_INDEX_PREFILTER", ""))
+    # "auto" (default): EXACT search through an int8 image of the bf16 rows where it applies
+    # (384-wide bf16 shards): rows whose int8 score provably cannot reach a query's k-th best are
+    # pruned, the rest re-scored in bf16 (csrc/hip/index_i8.hip); "none": scan every row in bf16
+    index_prune: str = field(default_factory=lambda: os.environ.get("SYMB_INDEX_PRUNE", "auto"))
     snapshot_dir: str = field(default_factory=lambda: _env("SYMB_SNAPSHOT_DIR", ""))
     collection: str = "symbiont_document_embeddings"
     embed_timeout_s: float = field(default_factory=lambda: _float("SYMB_EMBED_TIMEOUT_S", 15.0))
