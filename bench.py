@@ -6,8 +6,13 @@ One STEP = the system's ingest+search cycle on every rank (one process per GPU):
   2. encode B=256 sentences x S=128 tokens with the HIP MiniLM-L6 encoder (bf16, varlen-packed)
   3. upsert the 256 unit embeddings into this rank's HBM index shard
   4. semantic search: the 256 new embeddings are the queries; all_gather the queries of all
-     ranks, fused MFMA scan + top-10 over the rank's shard of the 100M x 384 corpus, all_to_all
-     the partial top-k back to each query's owner and merge.
+     ranks, EXACT top-10 over the rank's shard of the 100M x 384 bf16 corpus, all_to_all the
+     partial top-k back to each query's owner and merge.  The exact top-10 is found by an int8
+     MFMA scan of an int8 image of the rows that prunes only rows whose score provably cannot
+     reach the query's k-th best (Cauchy-Schwarz bound on the quantisation error, tracked at
+     every write), and the survivors are re-scored in bf16 (csrc/hip/index_i8.hip): the same
+     rows and scores as scanning every row in bf16 (GPU tests compare them); --index-prune none
+     runs that full bf16 scan.
 So every step embeds 256*N sentences AND answers 256*N top-10 queries over the full 100M-row
 corpus: value = embeds/s = top-k QPS (whole job).  Per-rank work is constant in N ("weak").
 
@@ -64,7 +69,7 @@ def main() -> None:
                     help="fp8: search the bf16 index through an e4m3 copy for 3k candidates and "
                          "re-score them exactly in bf16 (Qdrant quantization + rescore); the "
                          "headline default is the exact bf16 scan")
-    ap.add_argument("--index-prune", choices=["none", "i8"], default="none",
+    ap.add_argument("--index-prune", choices=["none", "i8"], default="i8",
                     help="i8: EXACT search through an int8 image of the bf16 rows -- rows whose "
                          "int8 score cannot reach the query's k-th best (a proven error bound) are "
                          "pruned, the rest re-scored in bf16 (csrc/hip/index_i8.hip); same top-k "
@@ -110,7 +115,11 @@ def main() -> None:
     rows_per_rank = args.index_rows // info.world
     extra = (K + W + 4) * B
     prefilter = None if args.index_prefilter == "none" else args.index_prefilter
-    prune = None if args.index_prune == "none" else args.index_prune
+    from codename_symbiont_amd.index.shard import resolve_prune
+
+    # exact either way; i8 applies to 384-wide bf16 shards without a prefilter (else: plain scan)
+    prune = resolve_prune("auto" if args.index_prune == "i8" else "none", args.index_dtype,
+                          cfg.hidden, prefilter)
     shard = HbmIndexShard(cfg.hidden, rows_per_rank + extra, device=dev, dtype=args.index_dtype,
                           prefilter=prefilter, prune=prune)
     if args.mode != "embed":

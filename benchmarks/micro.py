@@ -209,6 +209,50 @@ def cmd_scanmqabl(a):
                       "n_rblk": n_rblk, "n_qblk": n_qblk, "results": out}))
 
 
+def cmd_scani8abl(a):
+    """Exact int8-pruned search (index_i8.hip): its parts (whole search, scan kernel, re-score)
+    and the scan kernel's ablations (0 full, 1 no DMA, 2 no emission test, 4 DMA ring only) plus
+    its in-kernel clock (3), on the grid and thresholds shard.search uses."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard, TILE_ROWS
+    from codename_symbiont_amd.ops._ext import hip, stream_handle
+
+    D, k = 384, 10
+    shard = HbmIndexShard(D, a.rows + 8192, device="cuda", prune="i8")
+    shard.fill_random(a.rows, seed=1)
+    q = torch.nn.functional.normalize(torch.randn(a.nq, D, device="cuda"), dim=-1).bfloat16()
+    shard.search(q, k)
+    torch.cuda.synchronize()
+    P = shard._pruned_last
+    h, st, n = hip(), stream_handle(), shard.visible
+
+    def scan(abl):
+        h.index_scan_i8_ablate(shard.rows_i8.data_ptr(), shard.sx_i8.data_ptr(), n,
+                               P["rows_per_blk"], P["n_rblk"], P["q8"].data_ptr(), a.nq,
+                               P["thr"].data_ptr(), P["cs"].data_ptr(), P["ci"].data_ptr(),
+                               P["cnt"].data_ptr(), P["cap"], 1, st, abl)
+
+    ci0, cnt0, cs0 = P["ci"].clone(), P["cnt"].clone(), torch.empty_like(P["cs"])
+
+    def rescore():   # on the first search's candidates (the ablations overwrite P's buffers)
+        h.rescore_bf16(shard.rows.data_ptr(), P["q"].data_ptr(), a.nq, D, ci0.data_ptr(),
+                       cnt0.data_ptr(), P["cap"], cs0.data_ptr(), st)
+
+    variants = {"search": lambda: shard.search(q, k), "rescore": rescore}
+    variants.update({f"abl{m}": (lambda m=m: scan(m)) for m in (0, 1, 2, 4)})
+    r = ab(variants, rounds=a.rounds, iters=a.iters)
+    out = {nm: dict(ms=round(m, 3), TBps=round(n * D / (m / 1e3) / 1e12, 2)) for nm, (m, _) in r.items()}
+    cnt = cnt0
+    timeit(lambda: scan(3), 10)
+    scan(3)
+    torch.cuda.synchronize()
+    nb = P["n_rblk"] * math.ceil(a.nq / 256)
+    st_ = P["cs"].view(-1)[: 2 * nb].view(-1, 2).double()
+    out["in_kernel_clock_GHz"] = round((st_[:, 0] / st_[:, 1] * 0.1).median().item(), 3)
+    out["cycles_per_tile"] = round((st_[:, 0] / math.ceil(P["rows_per_blk"] / TILE_ROWS)).median().item(), 1)
+    print(json.dumps({"bench": "scani8_ablation", "rows": n, "nq": a.nq, "cand_mean": float(cnt.float().mean()),
+                      "cand_max": int(cnt.max()), "results": out}))
+
+
 def cmd_scanabl(a):
     """DMA-only vs compute-only vs full scan (D=384), plus a plain torch streaming read."""
     from codename_symbiont_amd.index.shard import HbmIndexShard, _round_up
@@ -547,7 +591,7 @@ def cmd_prefilter(a):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("cmd", choices=["scan", "scanmq", "scanmqabl", "scanabl", "scanstamp", "scanfp8", "gemm", "encoder", "attn", "latency", "gemmfp8", "prefilter"])
+    ap.add_argument("cmd", choices=["scan", "scanmq", "scanmqabl", "scani8abl", "scanabl", "scanstamp", "scanfp8", "gemm", "encoder", "attn", "latency", "gemmfp8", "prefilter"])
     ap.add_argument("--qmode", choices=["random", "near"], default="random", help="prefilter: query kind")
     ap.add_argument("--rows", type=int, default=100_000_000)
     ap.add_argument("--dim", type=int, default=384)
@@ -567,7 +611,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=5)
     a = ap.parse_args()
-    {"scan": cmd_scan, "scanmq": cmd_scanmq, "scanmqabl": cmd_scanmqabl, "scanabl": cmd_scanabl, "scanstamp": cmd_scanstamp, "scanfp8": cmd_scanfp8, "gemm": cmd_gemm, "encoder": cmd_encoder, "attn": cmd_attn, "latency": cmd_latency, "gemmfp8": cmd_gemmfp8, "prefilter": cmd_prefilter}[a.cmd](a)
+    {"scan": cmd_scan, "scanmq": cmd_scanmq, "scanmqabl": cmd_scanmqabl, "scani8abl": cmd_scani8abl, "scanabl": cmd_scanabl, "scanstamp": cmd_scanstamp, "scanfp8": cmd_scanfp8, "gemm": cmd_gemm, "encoder": cmd_encoder, "attn": cmd_attn, "latency": cmd_latency, "gemmfp8": cmd_gemmfp8, "prefilter": cmd_prefilter}[a.cmd](a)
 
 
 if __name__ == "__main__":

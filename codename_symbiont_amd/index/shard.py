@@ -560,6 +560,9 @@ class HbmIndexShard:
         # overflow (some query had more than cap candidates): the exact bf16 scan, seeded with T
         self._scan(n, q_unit, kmax, k, T.contiguous(), n_cus, gate=ovf, out=(out_s, out_i))
         self._mq_last = (cnt, ovf)
+        # (diagnostics / benchmarks/micro.py scani8abl: the scan's inputs and grid)
+        self._pruned_last = dict(q8=q8, thr=thr, rows_per_blk=rows_per_blk, n_rblk=n_rblk, cap=cap,
+                                 cs=cs, ci=ci, cnt=cnt, q=q_unit)
         if self.mq_stats:
             if self._mq_tot is None:
                 self._mq_tot = (torch.zeros(1, dtype=torch.int32, device=dev),

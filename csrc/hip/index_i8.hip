@@ -43,7 +43,10 @@ constexpr int TILE_BYTES = TR * D;          // 24 KiB
 constexpr int LOADS = TILE_BYTES / (1024 * WAVES);  // 3 LDS-DMA pieces per wave per tile
 constexpr int NKS = D / 64;                 // 6 k-steps of v_mfma_i32_16x16x64_i8
 constexpr int PIECE = 1024;
-constexpr int PF = 2;                       // fragment reads in flight
+#ifndef SYMB_I8_PF
+#define SYMB_I8_PF 5
+#endif
+constexpr int PF = SYMB_I8_PF;              // fragment reads in flight (NKS % (PF + 1) == 0)
 constexpr int R = PF + 1;
 constexpr int DMA_EVERY = 2;
 constexpr int SC_BYTES = TR * 4;            // one tile's row scales
@@ -98,6 +101,47 @@ struct I8Chain {
   }
 };
 
+// Fused chain of TWO 16-row sub-tiles (the row-split wave's whole share of a tile): per k-step
+// one fragment per sub-tile and 2 x SETS MFMAs, so a tile is one 48-MFMA chain and one emission
+// block per wave instead of two 24-MFMA chains (half the chain-end pads, waits and tests).
+namespace i8s {
+constexpr int PF2 = 2;                      // k-steps of fragment reads in flight (2 reads each)
+constexpr int R2 = PF2 + 1;
+}  // namespace i8s
+template <int N>
+__device__ __forceinline__ void i8_lgkm2(i32x4& v0, i32x4& v1) {
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(v0), "+v"(v1) : "i"(N));
+}
+template <int KS, int DMA_PIECES>
+struct I8Chain2 {
+  template <class Dma>
+  __device__ __forceinline__ static void run(i32x4 (&acc)[2][i8s::SETS], i32x4 (&a)[i8s::R2][2],
+                                             const i32x4 (&qf)[i8s::SETS][i8s::NKS],
+                                             uint32_t base, const Dma& dma) {
+    using namespace i8s;
+    if constexpr (DMA_PIECES > 0 && KS % DMA_EVERY == 0 && KS / DMA_EVERY < DMA_PIECES)
+      dma(KS / DMA_EVERY);
+    constexpr int steps = (NKS - KS < PF2) ? (NKS - KS) : PF2;   // k-steps in flight, this one too
+    i8_lgkm2<2 * (steps - 1)>(a[KS % R2][0], a[KS % R2][1]);
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int s = 0; s < SETS; ++s) i8_mfma<KS == 0>(acc[c][s], a[KS % R2][c], qf[s][KS]);
+    if constexpr (KS + 1 == NKS) asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+    if constexpr (KS + PF2 < NKS) {
+      i8_read16<(KS + PF2) * PIECE>(a[(KS + PF2) % R2][0], base);
+      i8_read16<(KS + PF2) * PIECE + NKS * PIECE>(a[(KS + PF2) % R2][1], base);
+    }
+    if constexpr (KS + 1 < NKS) I8Chain2<KS + 1, DMA_PIECES>::run(acc, a, qf, base, dma);
+  }
+};
+template <int J>
+__device__ __forceinline__ void i8_prologue2(i32x4 (&a)[i8s::R2][2], uint32_t base) {
+  i8_read16<J * i8s::PIECE>(a[J % i8s::R2][0], base);
+  i8_read16<J * i8s::PIECE + i8s::NKS * i8s::PIECE>(a[J % i8s::R2][1], base);
+  if constexpr (J + 1 < i8s::PF2) i8_prologue2<J + 1>(a, base);
+}
+
 template <int J>
 __device__ __forceinline__ void i8_prologue(i32x4 (&a)[i8s::R], uint32_t base) {
   i8_read16<J * i8s::PIECE>(a[J % i8s::R], base);
@@ -114,7 +158,10 @@ __device__ __forceinline__ const char* i8_uniform(const char* p) {
 // X8: [>= round_up(n_valid, 64), 384] int8 rows; sx: their scales (f32, same padding);
 // Q8: [NQ, 384] int8 queries; thr[NQ]: emit a row iff (q8 . x8) * sx >= thr (already divided by
 // the query's scale).  cand_s/cand_i: [NQ][cap]; cand_n[NQ] zeroed by the host entry.
-template <int RSPLIT>
+// ABL (profiling entry symb_index_scan_i8_ablate only): 1 = no LDS-DMA, 2 = no emission test,
+// 3 = full + s_memtime / s_memrealtime around the tile loop into cand_s[2 * blockIdx.x + {0, 1}],
+// 4 = LDS-DMA ring only.
+template <int RSPLIT, int ABL = 0>
 __global__ __launch_bounds__(512, 1) void index_scan_i8_kernel(
     const int8_t* __restrict__ X8, const float* __restrict__ sx, int n_valid, int rows_per_blk,
     const int8_t* __restrict__ Q8, int NQ, int n_qblk, int xcd, const float* __restrict__ thr_in,
@@ -195,38 +242,49 @@ __global__ __launch_bounds__(512, 1) void index_scan_i8_kernel(
   };
   // one 16-row sub-tile at row0 with this lane's row scales s4
   auto emit = [&](i32x4 (&acc)[SETS], int row0, const f32x4 s4) {
-    const int rl = row0 + 4 * (lane >> 4);
-    float v[SETS][4];
-    float mx[SETS];
+    if constexpr (ABL == 2 || ABL == 4) {
+#pragma unroll
+      for (int s = 0; s < SETS; ++s) asm volatile("" ::"v"(acc[s]), "v"(s4));
+      return;
+    }
+    // hot path, a conservative integer pre-test per set: max_r(acc_r * sx_r) <= max_r acc_r *
+    // (max_r sx_r) for a non-negative max (min_r sx_r for a negative one), so a set whose bound
+    // misses its threshold has no hit; only the rest take the exact per-row test below
+    const float smax = fmaxf(fmaxf(s4[0], s4[1]), fmaxf(s4[2], s4[3]));
+    const float smin = fminf(fminf(s4[0], s4[1]), fminf(s4[2], s4[3]));
+    float ub[SETS];
 #pragma unroll
     for (int s = 0; s < SETS; ++s) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        v[s][r] = (float)acc[s][r] * s4[r];
-        if (rl + r >= row_end) v[s][r] = -INFINITY;
-      }
-      mx[s] = fmaxf(fmaxf(v[s][0], v[s][1]), fmaxf(v[s][2], v[s][3]));
+      int im;
+      asm volatile("v_max3_i32 %0, %1, %2, %3\n\tv_max3_i32 %0, %0, %4, %4"
+                   : "=&v"(im) : "v"(acc[s][0]), "v"(acc[s][1]), "v"(acc[s][2]), "v"(acc[s][3]));
+      ub[s] = (float)im * (im >= 0 ? smax : smin);
     }
     bool hit = false;
 #pragma unroll
-    for (int s = 0; s < SETS; ++s) hit |= mx[s] >= thr[s];
+    for (int s = 0; s < SETS; ++s) hit |= ub[s] >= thr[s];
     if (__builtin_amdgcn_ballot_w64(hit)) {
       int lo = lane;
       asm volatile("" : "+v"(lo));
       const int lrow = row0 + 4 * (lo >> 4), lq = lo & 15;
+      const int rl = row0 + 4 * (lo >> 4);
 #pragma unroll
       for (int s = 0; s < SETS; ++s) {
-        if (!__builtin_amdgcn_ballot_w64(mx[s] >= thr[s])) continue;
+        if (!__builtin_amdgcn_ballot_w64(ub[s] >= thr[s])) continue;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          v[r] = rl + r < row_end ? (float)acc[s][r] * s4[r] : -INFINITY;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const bool p = v[s][r] >= thr[s];
+          const bool p = v[r] >= thr[s];
           const uint64_t m = __builtin_amdgcn_ballot_w64(p);
           if (m) {
             if (nst > STW - 64) flush();
             const int idx = nst + (int)__builtin_amdgcn_mbcnt_hi(
                                       (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
             if (p) {
-              st_s[idx] = v[s][r];
+              st_s[idx] = v[r];
               st_r[idx] = lrow + r;
               st_q[idx] = (uint16_t)(s * 16 + lq);
             }
@@ -239,32 +297,68 @@ __global__ __launch_bounds__(512, 1) void index_scan_i8_kernel(
 
   // wave 0 carries one extra vector-memory op per tile (the scale DMA)
   constexpr int W0X = 1;
-  if (n_tiles > 0) {
+  if (n_tiles > 0 && ABL != 1) {
 #pragma unroll
     for (int p = 0; p < NS - 1; ++p)
 #pragma unroll
       for (int i = 0; i < LOADS; ++i) issue_tile(p, i);
   }
+  uint64_t c0 = 0, r0t = 0;
+  if constexpr (ABL == 3) {
+    c0 = __builtin_amdgcn_s_memtime();
+    r0t = __builtin_amdgcn_s_memrealtime();
+  }
   i32x4 a[R];
   i32x4 acc[SETS];
+  // fused two-sub-tile chain: the row-split form (each wave owns 2 sub-tiles of a tile)
+  constexpr bool FUSE = NSW == 2;
+  i32x4 a2[FUSE ? R2 : 1][2];
+  i32x4 acc2[FUSE ? 2 : 1][SETS];
+  f32x4 s4_prev = {0.f, 0.f, 0.f, 0.f};
   const bool late = wave_u >= WAVES / 2;   // partner waves (w, w + 4) stay half a test apart
   // the late wave tests its last sub-tile after the NEXT barrier, when wave 0 may already be
   // refilling that tile's scale slot: its scales are read into registers before the barrier
   f32x4 s4_last = {0.f, 0.f, 0.f, 0.f};
   for (int t = 0; t < n_tiles; ++t) {
-    if (wave_u == 0)
-      wait_vmcnt<(LOADS + W0X) * (NS - 2)>();
-    else
-      wait_vmcnt<LOADS * (NS - 2)>();
+    if constexpr (ABL != 1) {
+      if (wave_u == 0)
+        wait_vmcnt<(LOADS + W0X) * (NS - 2)>();
+      else
+        wait_vmcnt<LOADS * (NS - 2)>();
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     const int slot = t % NS;
     const uint32_t tbase = lds_smem + (uint32_t)(slot * TILE_BYTES);
     const int row0 = row_begin + t * TR;
     const int tnext = t + NS - 1;
-    auto dma = [&](int i) { issue_tile(tnext, i); };
+    auto dma = [&](int i) {
+      if constexpr (ABL != 1) issue_tile(tnext, i);
+    };
     const uint32_t fw = tbase + foff + j0 * NKS * PIECE;
     const int last = (j0 + NSW - 1) * SUB;
+    if constexpr (ABL == 4) {
+#pragma unroll
+      for (int i = 0; i < LOADS; ++i) dma(i);
+      continue;
+    }
+    if constexpr (FUSE) {
+      i8_prologue2<0>(a2, fw);
+      // a late wave tests the previous tile's two sub-tiles here, under its partner's MFMAs
+      if (late && t > 0) {
+        emit(acc2[0], row0 - TR + j0 * SUB, s4_prev);
+        emit(acc2[1], row0 - TR + last, s4_last);
+      }
+      I8Chain2<0, LOADS>::run(acc2, a2, qf, fw, dma);
+      if (!late) {
+        emit(acc2[0], row0 + j0 * SUB, scales(slot, j0));
+        emit(acc2[1], row0 + last, scales(slot, j0 + 1));
+      } else {
+        s4_prev = scales(slot, j0);
+        s4_last = scales(slot, j0 + 1);
+      }
+      continue;
+    }
     i8_prologue<0>(a, fw);
     if (late && t > 0) emit(acc, row0 - TR + last, s4_last);
     if constexpr (NSW > 1)
@@ -284,18 +378,35 @@ __global__ __launch_bounds__(512, 1) void index_scan_i8_kernel(
     else
       s4_last = scales(slot, j0 + NSW - 1);
   }
-  if (late && n_tiles > 0) emit(acc, row_begin + (n_tiles - 1) * TR + (j0 + NSW - 1) * SUB, s4_last);
+  if (late && n_tiles > 0) {
+    if constexpr (FUSE) {
+      emit(acc2[0], row_begin + (n_tiles - 1) * TR + j0 * SUB, s4_prev);
+      emit(acc2[1], row_begin + (n_tiles - 1) * TR + (j0 + 1) * SUB, s4_last);
+    } else {
+      emit(acc, row_begin + (n_tiles - 1) * TR + (j0 + NSW - 1) * SUB, s4_last);
+    }
+  }
   if (nst) flush();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (ABL == 3) {
+    const uint64_t cyc = __builtin_amdgcn_s_memtime() - c0;
+    const uint64_t rt = __builtin_amdgcn_s_memrealtime() - r0t;
+    if (tid == 0) {
+      cand_s[2 * blockIdx.x] = (float)cyc;
+      cand_s[2 * blockIdx.x + 1] = (float)rt;
+    }
+  }
 }
 
 // Exact re-score of every candidate: cand_s[q][c] = <Q[q], X[cand_i[q][c]]> over the bf16 rows
-// (fp32 accumulation).  One workgroup per query, one wave per candidate, 6 elements per lane.
+// (fp32 accumulation).  SPLIT workgroups per query (blockIdx.y), one wave per candidate with U
+// 768-byte row gathers in flight per wave, 6 elements per lane.
 __global__ __launch_bounds__(256) void rescore_bf16_kernel(
     const __bf16* __restrict__ X, const __bf16* __restrict__ Q, const int* __restrict__ cand_i,
     const int* __restrict__ cand_n, int cap, float* __restrict__ cand_s) {
   constexpr int D = 384, PER = D / 64;
-  const int q = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = blockIdx.x, lane = threadIdx.x & 63;
+  const int wave = blockIdx.y * 4 + (threadIdx.x >> 6), nwaves = gridDim.y * 4;
   const int n = min(cand_n[q], cap);
   float qv[PER];
   {
@@ -309,8 +420,8 @@ __global__ __launch_bounds__(256) void rescore_bf16_kernel(
   }
   const int* ci = cand_i + (size_t)q * cap;
   float* cs = cand_s + (size_t)q * cap;
-  constexpr int U = 4;   // candidates in flight per wave
-  for (int c0 = wave * U; c0 < n; c0 += 4 * U) {
+  constexpr int U = 8;   // candidates in flight per wave
+  for (int c0 = wave * U; c0 < n; c0 += nwaves * U) {
     uint32_t w[U][PER / 2];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -425,11 +536,40 @@ int symb_index_scan_i8(const void* X8, const float* sx, int n_valid, int rows_pe
   return -1;
 }
 
+// Profiling-only entry: the ablations of index_scan_i8_kernel<2> (ABL above), same arguments.
+int symb_index_scan_i8_ablate(const void* X8, const float* sx, int n_valid, int rows_per_blk,
+                              int n_rblk, const void* Q8, int NQ, const float* thr, float* cand_s,
+                              int* cand_i, int* cand_n, int cap, int xcd, hipStream_t st, int abl) {
+  if (NQ <= 0) return 0;
+  if (rows_per_blk % i8s::TR || n_rblk <= 0 || thr == nullptr || cap <= 0 || n_valid <= 0)
+    return -1;
+  if ((long long)n_rblk * rows_per_blk < n_valid) return -1;
+  hipError_t e = hipMemsetAsync(cand_n, 0, sizeof(int) * (size_t)NQ, st);
+  if (e != hipSuccess) return (int)e;
+  const int n_qblk = (NQ + 255) / 256;
+  constexpr int lds = i8s::LDS_BYTES;
+  auto go = [&](auto kern) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipLaunchKernelGGL(kern, dim3(n_rblk * n_qblk), dim3(512), lds, st, (const int8_t*)X8, sx,
+                       n_valid, rows_per_blk, (const int8_t*)Q8, NQ, n_qblk, xcd, thr, cand_s,
+                       cand_i, cand_n, cap);
+    return (int)hipGetLastError();
+  };
+  switch (abl) {
+    case 0: return go(index_scan_i8_kernel<2, 0>);
+    case 1: return go(index_scan_i8_kernel<2, 1>);
+    case 2: return go(index_scan_i8_kernel<2, 2>);
+    case 3: return go(index_scan_i8_kernel<2, 3>);
+    case 4: return go(index_scan_i8_kernel<2, 4>);
+    default: return -1;
+  }
+}
+
 int symb_rescore_bf16(const void* X, const void* Q, int NQ, int dim, const int* cand_i,
                       const int* cand_n, int cap, float* cand_s, hipStream_t st) {
   if (NQ <= 0) return 0;
   if (dim != 384 || cap <= 0) return -1;
-  hipLaunchKernelGGL(rescore_bf16_kernel, dim3(NQ), dim3(256), 0, st, (const __bf16*)X,
+  hipLaunchKernelGGL(rescore_bf16_kernel, dim3(NQ, 8), dim3(256), 0, st, (const __bf16*)X,
                      (const __bf16*)Q, cand_i, cand_n, cap, cand_s);
   return (int)hipGetLastError();
 }
