@@ -74,6 +74,8 @@ def main() -> None:
                          "int8 score cannot reach the query's k-th best (a proven error bound) are "
                          "pruned, the rest re-scored in bf16 (csrc/hip/index_i8.hip); same top-k "
                          "as the full bf16 scan")
+    ap.add_argument("--i8-tile-rows", type=int, choices=[64, 128], default=64,
+                    help="rows per tile of the int8 pruning scan")
     ap.add_argument("--encoder-dtype", choices=["bf16", "fp8"], default="bf16",
                     help="fp8: e4m3 projection GEMMs (BASELINE config #5); the headline stays bf16")
     ap.add_argument("--embed-dp", choices=["replica", "group"], default="replica",
@@ -125,6 +127,10 @@ def main() -> None:
     if args.mode != "embed":
         shard.fill_random(rows_per_rank, seed=100 + info.rank)
     searcher = ShardedSearcher(shard, info)
+    if prune:
+        from codename_symbiont_amd.ops._ext import hip as _hip
+
+        _hip().i8_config(args.i8_tile_rows)
     shard.mq_stats = os.environ.get("SYMB_MQ_STATS", "0") not in ("", "0")
     shard.scan_cus = args.scan_cus
     shard.scan_min_tiles = args.scan_min_tiles

@@ -220,6 +220,7 @@ def cmd_scani8abl(a):
     shard = HbmIndexShard(D, a.rows + 8192, device="cuda", prune="i8")
     shard.fill_random(a.rows, seed=1)
     q = torch.nn.functional.normalize(torch.randn(a.nq, D, device="cuda"), dim=-1).bfloat16()
+    hip().i8_config(a.i8_tr)
     shard.search(q, k)
     torch.cuda.synchronize()
     P = shard._pruned_last
@@ -227,7 +228,8 @@ def cmd_scani8abl(a):
 
     def scan(abl):
         h.index_scan_i8_ablate(shard.rows_i8.data_ptr(), shard.sx_i8.data_ptr(), n,
-                               P["rows_per_blk"], P["n_rblk"], P["q8"].data_ptr(), a.nq,
+                               shard.rows_i8.shape[0], P["rows_per_blk"], P["n_rblk"],
+                               P["q8"].data_ptr(), a.nq,
                                P["thr"].data_ptr(), P["cs"].data_ptr(), P["ci"].data_ptr(),
                                P["cnt"].data_ptr(), P["cap"], 1, st, abl)
 
@@ -248,8 +250,10 @@ def cmd_scani8abl(a):
     nb = P["n_rblk"] * math.ceil(a.nq / 256)
     st_ = P["cs"].view(-1)[: 2 * nb].view(-1, 2).double()
     out["in_kernel_clock_GHz"] = round((st_[:, 0] / st_[:, 1] * 0.1).median().item(), 3)
-    out["cycles_per_tile"] = round((st_[:, 0] / math.ceil(P["rows_per_blk"] / TILE_ROWS)).median().item(), 1)
-    print(json.dumps({"bench": "scani8_ablation", "rows": n, "nq": a.nq, "cand_mean": float(cnt.float().mean()),
+    out["cycles_per_64_rows"] = round((st_[:, 0] / math.ceil(P["rows_per_blk"] / TILE_ROWS)).median().item(), 1)
+    hip().i8_config(64)
+    print(json.dumps({"bench": "scani8_ablation", "rows": n, "nq": a.nq, "tile_rows": a.i8_tr,
+                      "cand_mean": float(cnt.float().mean()),
                       "cand_max": int(cnt.max()), "results": out}))
 
 
@@ -608,6 +612,7 @@ def main():
     ap.add_argument("--sets", type=int, default=4, help="scanmqabl: 16-query sets per wave (2 or 4)")
     ap.add_argument("--rsplit", type=int, default=1, help="scanmqabl: waves per query group (1, 2)")
     ap.add_argument("--prune", action="store_true", help="scanmq: also the exact int8-pruned search")
+    ap.add_argument("--i8-tr", type=int, default=64, help="scani8abl: int8 scan tile rows (64, 128)")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=5)
     a = ap.parse_args()

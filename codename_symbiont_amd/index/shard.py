@@ -166,8 +166,10 @@ class HbmIndexShard:
         # E = max |x - x~| and X = max |x~| over every row ever written (monotone, so conservative)
         self.rows_i8 = self.sx_i8 = self.i8_bounds = None
         if prune:
-            self.rows_i8 = torch.empty(self.rows.shape, dtype=torch.int8, device=self.device)
-            self.sx_i8 = torch.ones(self.rows.shape[0], dtype=torch.float32, device=self.device)
+            # padded to whole 128-row tiles: the int8 scan's DMA reads whole tiles
+            n_alloc = _round_up(self.rows.shape[0], 128)
+            self.rows_i8 = torch.zeros(n_alloc, dim, dtype=torch.int8, device=self.device)
+            self.sx_i8 = torch.ones(n_alloc, dtype=torch.float32, device=self.device)
             self.i8_bounds = torch.zeros(2, dtype=torch.float32, device=self.device)
         self.count = 0      # rows reserved (payload slots exist)
         # rows searches may read: published only after their writes are ENQUEUED on the stream
@@ -539,9 +541,10 @@ class HbmIndexShard:
         # 3. emit every row with (q8 . x8) * sx >= thr, 4. exact bf16 re-score, 5. top-k
         h, dev, cap = hip(), self.device, self.PRUNE_CAP
         rsplit = 2 if NQ < 512 else 1
+        tr = h.i8_tile_rows()
         n_qblk = math.ceil(NQ / h.i8_queries_per_blk(rsplit))
-        n_rblk = max(1, min(math.ceil(n / (TILE_ROWS * 16)), max(1, round(n_cus / n_qblk))))
-        rows_per_blk = _round_up(max(1, math.ceil(n / n_rblk)), TILE_ROWS)
+        n_rblk = max(1, min(math.ceil(n / (tr * 16)), max(1, round(n_cus / n_qblk))))
+        rows_per_blk = _round_up(max(1, math.ceil(n / n_rblk)), tr)
         n_rblk = max(1, math.ceil(n / rows_per_blk))
         cs = torch.empty(NQ, cap, device=dev)
         ci = torch.empty(NQ, cap, dtype=torch.int32, device=dev)
@@ -550,7 +553,8 @@ class HbmIndexShard:
         out_s = torch.empty(NQ, k, device=dev)
         out_i = torch.empty(NQ, k, dtype=torch.int32, device=dev)
         st = stream_handle(dev)
-        h.index_scan_i8(self.rows_i8.data_ptr(), self.sx_i8.data_ptr(), n, rows_per_blk, n_rblk,
+        h.index_scan_i8(self.rows_i8.data_ptr(), self.sx_i8.data_ptr(), n, self.rows_i8.shape[0],
+                        rows_per_blk, n_rblk,
                         q8.data_ptr(), NQ, thr.data_ptr(), cs.data_ptr(), ci.data_ptr(),
                         cnt.data_ptr(), cap, self.scan_xcd, st, rsplit)
         h.rescore_bf16(self.rows.data_ptr(), q_unit.data_ptr(), NQ, self.dim, ci.data_ptr(),

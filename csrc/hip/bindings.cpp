@@ -65,14 +65,18 @@ int symb_topk_merge(const float* cand_s, const int* cand_i, int NQ, int n_cand_p
                     int64_t* out_id64, hipStream_t st, const int* gate = nullptr);
 int symb_mq_queries_per_blk(int sets, int rsplit);
 int symb_i8_queries_per_blk(int rsplit);
-int symb_index_scan_i8(const void* X8, const float* sx, int n_valid, int rows_per_blk, int n_rblk,
-                       const void* Q8, int NQ, const float* thr, float* cand_s, int* cand_i,
-                       int* cand_n, int cap, int xcd, hipStream_t st, int rsplit);
+int symb_index_scan_i8(const void* X8, const float* sx, int n_valid, int alloc_rows,
+                       int rows_per_blk, int n_rblk, const void* Q8, int NQ, const float* thr,
+                       float* cand_s, int* cand_i, int* cand_n, int cap, int xcd, hipStream_t st,
+                       int rsplit);
+int symb_i8_config(int tile_rows);
+int symb_i8_tile_rows();
 int symb_rescore_bf16(const void* X, const void* Q, int NQ, int dim, const int* cand_i,
                       const int* cand_n, int cap, float* cand_s, hipStream_t st);
-int symb_index_scan_i8_ablate(const void* X8, const float* sx, int n_valid, int rows_per_blk,
-                              int n_rblk, const void* Q8, int NQ, const float* thr, float* cand_s,
-                              int* cand_i, int* cand_n, int cap, int xcd, hipStream_t st, int abl);
+int symb_index_scan_i8_ablate(const void* X8, const float* sx, int n_valid, int alloc_rows,
+                              int rows_per_blk, int n_rblk, const void* Q8, int NQ,
+                              const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
+                              int xcd, hipStream_t st, int abl);
 int symb_quant_rows_i8(const void* X, int n, int dim, void* X8, float* sx, float* err, float* xtn,
                        hipStream_t st);
 int symb_gemm_lt_config(int mode);
@@ -338,18 +342,24 @@ PYBIND11_MODULE(_hip, m) {
   // multi-query-block D=384 scan (index_mq.hip): candidates above the seeded thresholds
   m.def("i8_queries_per_blk", [](int rsplit) { return symb_i8_queries_per_blk(rsplit); },
         py::arg("rsplit") = 2);
-  m.def("index_scan_i8", [](uptr X8, uptr sx, int n_valid, int rows_per_blk, int n_rblk, uptr Q8,
-                            int NQ, uptr thr, uptr cand_s, uptr cand_i, uptr cand_n, int cap,
-                            int xcd, uptr st, int rsplit) {
-    check(symb_index_scan_i8(P<void>(X8), P<const float>(sx), n_valid, rows_per_blk, n_rblk,
+  m.def("i8_config", [](int tile_rows) { check(symb_i8_config(tile_rows), "i8_config"); },
+        py::arg("tile_rows"));
+  m.def("i8_tile_rows", []() { return symb_i8_tile_rows(); });
+  m.def("index_scan_i8", [](uptr X8, uptr sx, int n_valid, int alloc_rows, int rows_per_blk,
+                            int n_rblk, uptr Q8, int NQ, uptr thr, uptr cand_s, uptr cand_i,
+                            uptr cand_n, int cap, int xcd, uptr st, int rsplit) {
+    check(symb_index_scan_i8(P<void>(X8), P<const float>(sx), n_valid, alloc_rows, rows_per_blk,
+                             n_rblk,
                              P<void>(Q8), NQ, P<const float>(thr), P<float>(cand_s), P<int>(cand_i),
                              P<int>(cand_n), cap, xcd, S(st), rsplit),
           "index_scan_i8");
   });
-  m.def("index_scan_i8_ablate", [](uptr X8, uptr sx, int n_valid, int rows_per_blk, int n_rblk,
-                                   uptr Q8, int NQ, uptr thr, uptr cand_s, uptr cand_i,
-                                   uptr cand_n, int cap, int xcd, uptr st, int abl) {
-    check(symb_index_scan_i8_ablate(P<void>(X8), P<const float>(sx), n_valid, rows_per_blk, n_rblk,
+  m.def("index_scan_i8_ablate", [](uptr X8, uptr sx, int n_valid, int alloc_rows,
+                                   int rows_per_blk, int n_rblk, uptr Q8, int NQ, uptr thr,
+                                   uptr cand_s, uptr cand_i, uptr cand_n, int cap, int xcd, uptr st,
+                                   int abl) {
+    check(symb_index_scan_i8_ablate(P<void>(X8), P<const float>(sx), n_valid, alloc_rows,
+                                    rows_per_blk, n_rblk,
                                     P<void>(Q8), NQ, P<const float>(thr), P<float>(cand_s),
                                     P<int>(cand_i), P<int>(cand_n), cap, xcd, S(st), abl),
           "index_scan_i8_ablate");

@@ -36,28 +36,39 @@ constexpr int D = 384;                      // int8 bytes per row
 constexpr int WAVES = 8;
 constexpr int SETS = 4;                     // 16-query sets per wave
 constexpr int SUB = 16;
-constexpr int TR = 64;
-constexpr int NSUB = TR / SUB;
-constexpr int NS = 5;                       // LDS ring depth in tiles
-constexpr int TILE_BYTES = TR * D;          // 24 KiB
-constexpr int LOADS = TILE_BYTES / (1024 * WAVES);  // 3 LDS-DMA pieces per wave per tile
 constexpr int NKS = D / 64;                 // 6 k-steps of v_mfma_i32_16x16x64_i8
 constexpr int PIECE = 1024;
+// Tile geometry: TR = 64-row tiles (24 KiB) in a 5-deep ring, or 128-row tiles (48 KiB) in a
+// 3-deep ring -- the same 96 KiB in flight, half the barriers and DMA bursts per row.
+template <int TR_> struct Geo {
+  static constexpr int TR = TR_;
+  static constexpr int NSUB = TR / SUB;
+  static constexpr int NS = TR == 64 ? 5 : 3;
+  static constexpr int TILE_BYTES = TR * D;
+  static constexpr int LOADS = TILE_BYTES / (1024 * WAVES);   // LDS-DMA pieces per wave per tile
+  static constexpr int DMA_EVERY = NKS / LOADS;               // k-steps between pieces
+  static constexpr int SCW = TR / 64;                         // waves carrying a scale DMA
+  static constexpr int SC_BYTES = TR * 4;
+  static constexpr int STW = TR == 64 ? 192 : 128;            // staged candidates per wave
+  static constexpr int STAGE_BYTES = STW * 10;
+  static constexpr int LDS_BYTES = NS * TILE_BYTES + NS * SC_BYTES + WAVES * STAGE_BYTES;
+  static_assert(TILE_BYTES % (1024 * WAVES) == 0, "tile must split evenly over waves");
+  static_assert(NSUB * NKS * PIECE == TILE_BYTES, "a tile is NSUB x NKS pieces");
+  static_assert(LOADS * DMA_EVERY <= NKS && DMA_EVERY >= 1, "DMA pieces must fit the first chain");
+  static_assert(LDS_BYTES <= 160 * 1024, "ring + scales + stages exceed the CU's 160 KiB");
+};
+constexpr int TR = 64;                      // the (unfused) single-sub-tile chain's geometry
+constexpr int NSUB = TR / SUB;
+constexpr int NS = Geo<64>::NS;
+constexpr int TILE_BYTES = Geo<64>::TILE_BYTES;
+constexpr int LOADS = Geo<64>::LOADS;
 #ifndef SYMB_I8_PF
 #define SYMB_I8_PF 5
 #endif
 constexpr int PF = SYMB_I8_PF;              // fragment reads in flight (NKS % (PF + 1) == 0)
 constexpr int R = PF + 1;
-constexpr int DMA_EVERY = 2;
-constexpr int SC_BYTES = TR * 4;            // one tile's row scales
-constexpr int STW = 192;                    // staged candidates per wave
-constexpr int STAGE_BYTES = STW * 10;
-constexpr int LDS_BYTES = NS * TILE_BYTES + NS * SC_BYTES + WAVES * STAGE_BYTES;
-static_assert(TILE_BYTES % (1024 * WAVES) == 0, "tile must split evenly over waves");
-static_assert(NSUB * NKS * PIECE == TILE_BYTES, "a tile is NSUB x NKS pieces");
-static_assert(LOADS * DMA_EVERY <= NKS, "DMA pieces must fit the first chain");
+constexpr int DMA_EVERY = Geo<64>::DMA_EVERY;
 static_assert(NKS % R == 0, "cross-chain prefetch: fragment j of the next chain uses slot j % R");
-static_assert(LDS_BYTES <= 160 * 1024, "ring + scales + stages exceed the CU's 160 KiB");
 }  // namespace i8s
 
 typedef __attribute__((ext_vector_type(4))) int i32x4;
@@ -112,15 +123,14 @@ template <int N>
 __device__ __forceinline__ void i8_lgkm2(i32x4& v0, i32x4& v1) {
   asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(v0), "+v"(v1) : "i"(N));
 }
-template <int KS, int DMA_PIECES>
+template <int KS, int DMA_PIECES, int DE>
 struct I8Chain2 {
   template <class Dma>
   __device__ __forceinline__ static void run(i32x4 (&acc)[2][i8s::SETS], i32x4 (&a)[i8s::R2][2],
                                              const i32x4 (&qf)[i8s::SETS][i8s::NKS],
                                              uint32_t base, const Dma& dma) {
     using namespace i8s;
-    if constexpr (DMA_PIECES > 0 && KS % DMA_EVERY == 0 && KS / DMA_EVERY < DMA_PIECES)
-      dma(KS / DMA_EVERY);
+    if constexpr (DMA_PIECES > 0 && KS % DE == 0 && KS / DE < DMA_PIECES) dma(KS / DE);
     constexpr int steps = (NKS - KS < PF2) ? (NKS - KS) : PF2;   // k-steps in flight, this one too
     i8_lgkm2<2 * (steps - 1)>(a[KS % R2][0], a[KS % R2][1]);
 #pragma unroll
@@ -132,7 +142,7 @@ struct I8Chain2 {
       i8_read16<(KS + PF2) * PIECE>(a[(KS + PF2) % R2][0], base);
       i8_read16<(KS + PF2) * PIECE + NKS * PIECE>(a[(KS + PF2) % R2][1], base);
     }
-    if constexpr (KS + 1 < NKS) I8Chain2<KS + 1, DMA_PIECES>::run(acc, a, qf, base, dma);
+    if constexpr (KS + 1 < NKS) I8Chain2<KS + 1, DMA_PIECES, DE>::run(acc, a, qf, base, dma);
   }
 };
 template <int J>
@@ -161,15 +171,20 @@ __device__ __forceinline__ const char* i8_uniform(const char* p) {
 // ABL (profiling entry symb_index_scan_i8_ablate only): 1 = no LDS-DMA, 2 = no emission test,
 // 3 = full + s_memtime / s_memrealtime around the tile loop into cand_s[2 * blockIdx.x + {0, 1}],
 // 4 = LDS-DMA ring only.
-template <int RSPLIT, int ABL = 0>
+template <int RSPLIT, int ABL = 0, int TRK = 64>
 __global__ __launch_bounds__(512, 1) void index_scan_i8_kernel(
     const int8_t* __restrict__ X8, const float* __restrict__ sx, int n_valid, int rows_per_blk,
     const int8_t* __restrict__ Q8, int NQ, int n_qblk, int xcd, const float* __restrict__ thr_in,
     float* __restrict__ cand_s, int* __restrict__ cand_i, int* __restrict__ cand_n, int cap) {
   using namespace i8s;
+  using G = Geo<TRK>;
+  constexpr int TR = G::TR, NSUB = G::NSUB, NS = G::NS, TILE_BYTES = G::TILE_BYTES;
+  constexpr int LOADS = G::LOADS, SC_BYTES = G::SC_BYTES, STW = G::STW;
+  constexpr int STAGE_BYTES = G::STAGE_BYTES;
   constexpr int QW = SETS * 16, QWAVES = WAVES / RSPLIT, QPB = QWAVES * QW;
   constexpr int NSW = NSUB / RSPLIT;
   static_assert(RSPLIT == 1 || RSPLIT == 2, "row split");
+  static_assert(TRK == 64 || NSW % 2 == 0, "128-row tiles run the fused two-sub-tile chains");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lb = xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
@@ -209,10 +224,11 @@ __global__ __launch_bounds__(512, 1) void index_scan_i8_kernel(
     const int prow = row_begin + tt * TR;
     const char* base = reinterpret_cast<const char*>(X8 + (size_t)(prow + j * SUB) * D + ks * 64);
     glds16_aux<0>(i8_uniform(base) + loff, smem + (t % NS) * TILE_BYTES + p * PIECE);
-    if (wave_u == 0 && i == 0)
+    if (wave_u < G::SCW && i == 0)   // 64 row scales per scale wave
       __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(sx + prow + lane),
-          (__attribute__((address_space(3))) void*)(scl + (t % NS) * SC_BYTES), 4, 0, 0);
+          (const __attribute__((address_space(1))) void*)(sx + prow + 64 * wave_u + lane),
+          (__attribute__((address_space(3))) void*)(scl + (t % NS) * SC_BYTES + 256 * wave_u), 4,
+          0, 0);
   };
   const uint32_t lds_smem = lds_addr(smem);
   const uint32_t foff = (uint32_t)((lane & 15) * 64 + (((lane >> 4) ^ ((lane >> 1) & 2)) * 16));
@@ -295,7 +311,7 @@ __global__ __launch_bounds__(512, 1) void index_scan_i8_kernel(
     }
   };
 
-  // wave 0 carries one extra vector-memory op per tile (the scale DMA)
+  // the scale waves carry one extra vector-memory op per tile
   constexpr int W0X = 1;
   if (n_tiles > 0 && ABL != 1) {
 #pragma unroll
@@ -310,8 +326,9 @@ __global__ __launch_bounds__(512, 1) void index_scan_i8_kernel(
   }
   i32x4 a[R];
   i32x4 acc[SETS];
-  // fused two-sub-tile chain: the row-split form (each wave owns 2 sub-tiles of a tile)
-  constexpr bool FUSE = NSW == 2;
+  // fused two-sub-tile chains: the row-split forms (each wave owns 2 or 4 sub-tiles of a tile)
+  constexpr bool FUSE = NSW % 2 == 0 && (RSPLIT == 2 || TRK == 128);
+  constexpr int NG = FUSE ? NSW / 2 : 1;   // fused chains per wave per tile
   i32x4 a2[FUSE ? R2 : 1][2];
   i32x4 acc2[FUSE ? 2 : 1][SETS];
   f32x4 s4_prev = {0.f, 0.f, 0.f, 0.f};
@@ -321,7 +338,7 @@ __global__ __launch_bounds__(512, 1) void index_scan_i8_kernel(
   f32x4 s4_last = {0.f, 0.f, 0.f, 0.f};
   for (int t = 0; t < n_tiles; ++t) {
     if constexpr (ABL != 1) {
-      if (wave_u == 0)
+      if (wave_u < G::SCW)
         wait_vmcnt<(LOADS + W0X) * (NS - 2)>();
       else
         wait_vmcnt<LOADS * (NS - 2)>();
@@ -343,19 +360,28 @@ __global__ __launch_bounds__(512, 1) void index_scan_i8_kernel(
       continue;
     }
     if constexpr (FUSE) {
-      i8_prologue2<0>(a2, fw);
-      // a late wave tests the previous tile's two sub-tiles here, under its partner's MFMAs
-      if (late && t > 0) {
-        emit(acc2[0], row0 - TR + j0 * SUB, s4_prev);
-        emit(acc2[1], row0 - TR + last, s4_last);
-      }
-      I8Chain2<0, LOADS>::run(acc2, a2, qf, fw, dma);
-      if (!late) {
-        emit(acc2[0], row0 + j0 * SUB, scales(slot, j0));
-        emit(acc2[1], row0 + last, scales(slot, j0 + 1));
-      } else {
-        s4_prev = scales(slot, j0);
-        s4_last = scales(slot, j0 + 1);
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        const uint32_t fg = fw + g * 2 * NKS * PIECE;
+        const int jg = j0 + 2 * g;
+        i8_prologue2<0>(a2, fg);
+        // a late wave tests the previous tile's last two sub-tiles here, under its partner's
+        // MFMAs
+        if (g == 0 && late && t > 0) {
+          emit(acc2[0], row0 - TR + last - SUB, s4_prev);
+          emit(acc2[1], row0 - TR + last, s4_last);
+        }
+        if (g == 0)
+          I8Chain2<0, LOADS, G::DMA_EVERY>::run(acc2, a2, qf, fg, dma);
+        else
+          I8Chain2<0, 0, G::DMA_EVERY>::run(acc2, a2, qf, fg, NoDma());
+        if (g + 1 < NG || !late) {
+          emit(acc2[0], row0 + jg * SUB, scales(slot, jg));
+          emit(acc2[1], row0 + (jg + 1) * SUB, scales(slot, jg + 1));
+        } else {
+          s4_prev = scales(slot, jg);
+          s4_last = scales(slot, jg + 1);
+        }
       }
       continue;
     }
@@ -380,8 +406,8 @@ __global__ __launch_bounds__(512, 1) void index_scan_i8_kernel(
   }
   if (late && n_tiles > 0) {
     if constexpr (FUSE) {
-      emit(acc2[0], row_begin + (n_tiles - 1) * TR + j0 * SUB, s4_prev);
-      emit(acc2[1], row_begin + (n_tiles - 1) * TR + (j0 + 1) * SUB, s4_last);
+      emit(acc2[0], row_begin + (n_tiles - 1) * TR + (j0 + NSW - 2) * SUB, s4_prev);
+      emit(acc2[1], row_begin + (n_tiles - 1) * TR + (j0 + NSW - 1) * SUB, s4_last);
     } else {
       emit(acc, row_begin + (n_tiles - 1) * TR + (j0 + NSW - 1) * SUB, s4_last);
     }
@@ -497,57 +523,70 @@ using namespace symb;
 
 int symb_i8_queries_per_blk(int rsplit) { return i8s::WAVES / rsplit * 16 * i8s::SETS; }
 
-template <int RSPLIT>
+// rows per scan tile (symb_i8_config): 64 or 128
+static int g_i8_tr = 64;
+int symb_i8_config(int tile_rows) {
+  if (tile_rows != 64 && tile_rows != 128) return -1;
+  g_i8_tr = tile_rows;
+  return 0;
+}
+int symb_i8_tile_rows() { return g_i8_tr; }
+
+template <int RSPLIT, int TRK>
 static int launch_i8(const void* X8, const float* sx, int n_valid, int rows_per_blk, int n_rblk,
                      const void* Q8, int NQ, const float* thr, float* cand_s, int* cand_i,
                      int* cand_n, int cap, int xcd, hipStream_t st) {
   constexpr int qpb = i8s::WAVES / RSPLIT * 16 * i8s::SETS;
   const int n_qblk = (NQ + qpb - 1) / qpb;
-  constexpr int lds = i8s::LDS_BYTES;
+  constexpr int lds = i8s::Geo<TRK>::LDS_BYTES;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)index_scan_i8_kernel<RSPLIT>,
+    (void)hipFuncSetAttribute((const void*)index_scan_i8_kernel<RSPLIT, 0, TRK>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
-  hipLaunchKernelGGL((index_scan_i8_kernel<RSPLIT>), dim3(n_rblk * n_qblk), dim3(512), lds, st,
+  hipLaunchKernelGGL((index_scan_i8_kernel<RSPLIT, 0, TRK>), dim3(n_rblk * n_qblk), dim3(512), lds, st,
                      (const int8_t*)X8, sx, n_valid, rows_per_blk, (const int8_t*)Q8, NQ, n_qblk,
                      xcd, thr, cand_s, cand_i, cand_n, cap);
   return (int)hipGetLastError();
 }
 
-// rows_per_blk % 64 == 0, n_rblk * rows_per_blk >= n_valid, X8 / sx padded to a whole last
-// tile (the DMA reads whole tiles).  rsplit 2 = 256 queries per workgroup, 1 = 512.
-int symb_index_scan_i8(const void* X8, const float* sx, int n_valid, int rows_per_blk, int n_rblk,
-                       const void* Q8, int NQ, const float* thr, float* cand_s, int* cand_i,
-                       int* cand_n, int cap, int xcd, hipStream_t st, int rsplit) {
+// rows_per_blk % tile rows == 0, n_rblk * rows_per_blk >= n_valid; X8 / sx hold alloc_rows
+// rows, which must cover n_valid rounded up to a whole tile (the DMA reads whole tiles).
+// rsplit 2 = 256 queries per workgroup, 1 = 512.
+int symb_index_scan_i8(const void* X8, const float* sx, int n_valid, int alloc_rows,
+                       int rows_per_blk, int n_rblk, const void* Q8, int NQ, const float* thr,
+                       float* cand_s, int* cand_i, int* cand_n, int cap, int xcd, hipStream_t st,
+                       int rsplit) {
   if (NQ <= 0) return 0;
-  if (rows_per_blk % i8s::TR || n_rblk <= 0 || thr == nullptr || cap <= 0 || n_valid <= 0)
-    return -1;
+  const int tr = g_i8_tr;
+  if (rows_per_blk % tr || n_rblk <= 0 || thr == nullptr || cap <= 0 || n_valid <= 0) return -1;
   if ((long long)n_rblk * rows_per_blk < n_valid) return -1;
+  if ((long long)(n_valid + tr - 1) / tr * tr > alloc_rows) return -1;   // a tile past the buffer
   hipError_t e = hipMemsetAsync(cand_n, 0, sizeof(int) * (size_t)NQ, st);
   if (e != hipSuccess) return (int)e;
-  if (rsplit == 2)
-    return launch_i8<2>(X8, sx, n_valid, rows_per_blk, n_rblk, Q8, NQ, thr, cand_s, cand_i, cand_n,
-                        cap, xcd, st);
-  if (rsplit == 1)
-    return launch_i8<1>(X8, sx, n_valid, rows_per_blk, n_rblk, Q8, NQ, thr, cand_s, cand_i, cand_n,
-                        cap, xcd, st);
+#define SYMB_I8(RS, T) launch_i8<RS, T>(X8, sx, n_valid, rows_per_blk, n_rblk, Q8, NQ, thr, cand_s, \
+                                        cand_i, cand_n, cap, xcd, st)
+  if (rsplit == 2) return tr == 128 ? SYMB_I8(2, 128) : SYMB_I8(2, 64);
+  if (rsplit == 1) return tr == 128 ? SYMB_I8(1, 128) : SYMB_I8(1, 64);
+#undef SYMB_I8
   return -1;
 }
 
 // Profiling-only entry: the ablations of index_scan_i8_kernel<2> (ABL above), same arguments.
-int symb_index_scan_i8_ablate(const void* X8, const float* sx, int n_valid, int rows_per_blk,
-                              int n_rblk, const void* Q8, int NQ, const float* thr, float* cand_s,
-                              int* cand_i, int* cand_n, int cap, int xcd, hipStream_t st, int abl) {
+int symb_index_scan_i8_ablate(const void* X8, const float* sx, int n_valid, int alloc_rows,
+                              int rows_per_blk, int n_rblk, const void* Q8, int NQ,
+                              const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
+                              int xcd, hipStream_t st, int abl) {
   if (NQ <= 0) return 0;
-  if (rows_per_blk % i8s::TR || n_rblk <= 0 || thr == nullptr || cap <= 0 || n_valid <= 0)
-    return -1;
+  const int tr = g_i8_tr;
+  if (rows_per_blk % tr || n_rblk <= 0 || thr == nullptr || cap <= 0 || n_valid <= 0) return -1;
   if ((long long)n_rblk * rows_per_blk < n_valid) return -1;
+  if ((long long)(n_valid + tr - 1) / tr * tr > alloc_rows) return -1;
   hipError_t e = hipMemsetAsync(cand_n, 0, sizeof(int) * (size_t)NQ, st);
   if (e != hipSuccess) return (int)e;
   const int n_qblk = (NQ + 255) / 256;
-  constexpr int lds = i8s::LDS_BYTES;
+  const int lds = tr == 128 ? i8s::Geo<128>::LDS_BYTES : i8s::Geo<64>::LDS_BYTES;
   auto go = [&](auto kern) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipLaunchKernelGGL(kern, dim3(n_rblk * n_qblk), dim3(512), lds, st, (const int8_t*)X8, sx,
@@ -555,12 +594,17 @@ int symb_index_scan_i8_ablate(const void* X8, const float* sx, int n_valid, int 
                        cand_i, cand_n, cap);
     return (int)hipGetLastError();
   };
-  switch (abl) {
-    case 0: return go(index_scan_i8_kernel<2, 0>);
-    case 1: return go(index_scan_i8_kernel<2, 1>);
-    case 2: return go(index_scan_i8_kernel<2, 2>);
-    case 3: return go(index_scan_i8_kernel<2, 3>);
-    case 4: return go(index_scan_i8_kernel<2, 4>);
+  switch (abl + (tr == 128 ? 8 : 0)) {
+    case 0: return go(index_scan_i8_kernel<2, 0, 64>);
+    case 1: return go(index_scan_i8_kernel<2, 1, 64>);
+    case 2: return go(index_scan_i8_kernel<2, 2, 64>);
+    case 3: return go(index_scan_i8_kernel<2, 3, 64>);
+    case 4: return go(index_scan_i8_kernel<2, 4, 64>);
+    case 8: return go(index_scan_i8_kernel<2, 0, 128>);
+    case 9: return go(index_scan_i8_kernel<2, 1, 128>);
+    case 10: return go(index_scan_i8_kernel<2, 2, 128>);
+    case 11: return go(index_scan_i8_kernel<2, 3, 128>);
+    case 12: return go(index_scan_i8_kernel<2, 4, 128>);
     default: return -1;
   }
 }

@@ -393,9 +393,11 @@ def test_quant_rows_i8_matches_reference():
     _close(xtn, xt.norm(dim=1), atol=1e-5, what="i8 |x~|")
 
 
-@pytest.mark.parametrize("nq,data", [(256, "random"), (300, "random"), (512, "random"),
-                                     (1100, "random"), (256, "clustered"), (512, "near")])
-def test_index_pruned_search_is_exact(nq, data):
+@pytest.mark.parametrize("nq,data,tr", [(256, "random", 64), (300, "random", 64), (512, "random", 64),
+                                        (1100, "random", 64), (256, "clustered", 64), (512, "near", 64),
+                                        (256, "random", 128), (300, "near", 128), (1100, "random", 128),
+                                        (256, "clustered", 128)])
+def test_index_pruned_search_is_exact(nq, data, tr):
     """prune="i8" (int8 bound-pruned scan + exact bf16 re-score) returns the rows and scores of the
     exact bf16 scan: random data, tight clusters (near-ties everywhere: candidate overflow takes
     the gated exact path) and queries that are noisy copies of stored rows."""
@@ -419,8 +421,14 @@ def test_index_pruned_search_is_exact(nq, data):
         q = x[torch.randint(0, n, (nq,), device=DEV, generator=g)].clone()
         q += (0.02 if data == "clustered" else 0.5 / math.sqrt(D)) * torch.randn_like(q)
     q = torch.nn.functional.normalize(q, dim=-1).bfloat16()
+    from codename_symbiont_amd.ops._ext import hip
+
     s0, r0 = ref.search(q, k)
-    s1, r1 = shard.search(q, k)
+    hip().i8_config(tr)    # rows per int8 scan tile
+    try:
+        s1, r1 = shard.search(q, k)
+    finally:
+        hip().i8_config(64)
     cnt, ovf = shard._mq_last
     torch.cuda.synchronize()
     if data != "clustered":
