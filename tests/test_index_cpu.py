@@ -272,3 +272,34 @@ def test_tile_sample_plan_invariants():
         sub_tiles = torch.unique(idx // TILE_ROWS)
         assert idx.numel() == sub_tiles.numel() * TILE_ROWS
         assert bool(torch.isin(sub_tiles, phys).all())        # sub-sample within the sample
+
+
+def test_int8_pruning_bound_holds_and_image_follows_writes():
+    """The exact int8-pruned search (csrc/hip/index_i8.hip) relies on
+    |q.x - q~.x~| <= |q| E + |q - q~| X with E = max |x - x~|, X = max |x~| over the rows written:
+    check it for every (query, row) pair of random and outlier-heavy data, and that the shard's
+    int8 image and its (E, X) follow appends, overwrites and snapshot loads."""
+    from codename_symbiont_amd.index.shard import resolve_prune
+    from codename_symbiont_amd.ops.reference import quant_rows_i8_ref
+
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(3000, 384, generator=g)
+    x[:100, :4] *= 30.0                     # rows dominated by a few large components
+    sh = HbmIndexShard(384, 4000, device="cpu", prune="i8")
+    sh.append_f32(x[:2000])
+    sh.write_f32(5, x[2500:2501])           # an overwrite refreshes that row's image
+    sh.append_f32(x[2000:])
+    xb = sh.rows[:sh.count]
+    x8, sx, err, xtn = quant_rows_i8_ref(xb)
+    assert torch.equal(sh.rows_i8[:sh.count], x8) and torch.allclose(sh.sx_i8[:sh.count], sx)
+    E, X = float(sh.i8_bounds[0]), float(sh.i8_bounds[1])
+    assert E >= float(err.max()) - 1e-7 and X >= float(xtn.max()) - 1e-7
+    q = torch.nn.functional.normalize(torch.randn(64, 384, generator=g), dim=-1).bfloat16()
+    q8, sq, eq, _ = quant_rows_i8_ref(q)
+    s = q.float() @ xb.float().t()
+    s_i8 = (q8.float() @ x8.float().t()) * sq[:, None] * sx[None, :]
+    margin = q.float().norm(dim=1) * E + eq * X
+    assert ((s - s_i8).abs() <= margin[:, None] + 1e-6).all()
+    assert resolve_prune("auto", "bf16", 384) == "i8"
+    assert resolve_prune("auto", "fp8", 1024) is None and resolve_prune("none") is None
+    assert resolve_prune("auto", "bf16", 384, prefilter="fp8") is None
