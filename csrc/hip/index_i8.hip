@@ -123,16 +123,26 @@ template <int N>
 __device__ __forceinline__ void i8_lgkm2(i32x4& v0, i32x4& v1) {
   asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(v0), "+v"(v1) : "i"(N));
 }
+template <int N>
+__device__ __forceinline__ void i8_lgkm2t(i32x4& v0, i32x4& v1, f32x4& t0, f32x4& t1) {
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(v0), "+v"(v1), "+v"(t0), "+v"(t1) : "i"(N));
+}
+// t0 / t1: the two sub-tiles' row scales, read from LDS just before the prologue; the first
+// k-step's wait covers them (older than every fragment read), so the emission after the chain
+// finds them in registers
 template <int KS, int DMA_PIECES, int DE>
 struct I8Chain2 {
   template <class Dma>
   __device__ __forceinline__ static void run(i32x4 (&acc)[2][i8s::SETS], i32x4 (&a)[i8s::R2][2],
                                              const i32x4 (&qf)[i8s::SETS][i8s::NKS],
-                                             uint32_t base, const Dma& dma) {
+                                             uint32_t base, const Dma& dma, f32x4& t0, f32x4& t1) {
     using namespace i8s;
     if constexpr (DMA_PIECES > 0 && KS % DE == 0 && KS / DE < DMA_PIECES) dma(KS / DE);
     constexpr int steps = (NKS - KS < PF2) ? (NKS - KS) : PF2;   // k-steps in flight, this one too
-    i8_lgkm2<2 * (steps - 1)>(a[KS % R2][0], a[KS % R2][1]);
+    if constexpr (KS == 0)
+      i8_lgkm2t<2 * (steps - 1)>(a[KS % R2][0], a[KS % R2][1], t0, t1);
+    else
+      i8_lgkm2<2 * (steps - 1)>(a[KS % R2][0], a[KS % R2][1]);
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll
@@ -142,7 +152,7 @@ struct I8Chain2 {
       i8_read16<(KS + PF2) * PIECE>(a[(KS + PF2) % R2][0], base);
       i8_read16<(KS + PF2) * PIECE + NKS * PIECE>(a[(KS + PF2) % R2][1], base);
     }
-    if constexpr (KS + 1 < NKS) I8Chain2<KS + 1, DMA_PIECES, DE>::run(acc, a, qf, base, dma);
+    if constexpr (KS + 1 < NKS) I8Chain2<KS + 1, DMA_PIECES, DE>::run(acc, a, qf, base, dma, t0, t1);
   }
 };
 template <int J>
@@ -266,19 +276,22 @@ __global__ __launch_bounds__(512, 1) void index_scan_i8_kernel(
     // hot path, a conservative integer pre-test per set: max_r(acc_r * sx_r) <= max_r acc_r *
     // (max_r sx_r) for a non-negative max (min_r sx_r for a negative one), so a set whose bound
     // misses its threshold has no hit; only the rest take the exact per-row test below
-    const float smax = fmaxf(fmaxf(s4[0], s4[1]), fmaxf(s4[2], s4[3]));
-    const float smin = fminf(fminf(s4[0], s4[1]), fminf(s4[2], s4[3]));
-    float ub[SETS];
+    //   max_r acc_r * sx_r >= thr  implies  max_r acc_r >= ceil(thr / max_r sx_r)  (thr > 0),
+    // so with one reciprocal per sub-tile each set's test is two v_max3_i32 and an integer
+    // compare; a set with thr <= 0 always takes the exact test
+    const float rs = __builtin_amdgcn_rcpf(fmaxf(fmaxf(s4[0], s4[1]), fmaxf(s4[2], s4[3])));
+    bool hs[SETS];
+    bool hit = false;
 #pragma unroll
     for (int s = 0; s < SETS; ++s) {
       int im;
       asm volatile("v_max3_i32 %0, %1, %2, %3\n\tv_max3_i32 %0, %0, %4, %4"
                    : "=&v"(im) : "v"(acc[s][0]), "v"(acc[s][1]), "v"(acc[s][2]), "v"(acc[s][3]));
-      ub[s] = (float)im * (im >= 0 ? smax : smin);
+      // (x 0.999: v_rcp_f32 is approximate, so the integer threshold is rounded down, loosely)
+      const int it = thr[s] > 0.f ? (int)fminf(thr[s] * rs * 0.999f, 2.0e9f) : INT_MIN;
+      hs[s] = im >= it;
+      hit |= hs[s];
     }
-    bool hit = false;
-#pragma unroll
-    for (int s = 0; s < SETS; ++s) hit |= ub[s] >= thr[s];
     if (__builtin_amdgcn_ballot_w64(hit)) {
       int lo = lane;
       asm volatile("" : "+v"(lo));
@@ -286,7 +299,7 @@ __global__ __launch_bounds__(512, 1) void index_scan_i8_kernel(
       const int rl = row0 + 4 * (lo >> 4);
 #pragma unroll
       for (int s = 0; s < SETS; ++s) {
-        if (!__builtin_amdgcn_ballot_w64(ub[s] >= thr[s])) continue;
+        if (!__builtin_amdgcn_ballot_w64(hs[s])) continue;
         float v[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -327,6 +340,8 @@ __global__ __launch_bounds__(512, 1) void index_scan_i8_kernel(
   i32x4 a[R];
   i32x4 acc[SETS];
   // fused two-sub-tile chains: the row-split forms (each wave owns 2 or 4 sub-tiles of a tile)
+  // (the 512-query form keeps single-sub-tile chains: its two fused groups per tile have no
+  // cross-chain prefetch and measured slower, 10.55 -> 11.15 ms at 12.5M x 2048)
   constexpr bool FUSE = NSW % 2 == 0 && (RSPLIT == 2 || TRK == 128);
   constexpr int NG = FUSE ? NSW / 2 : 1;   // fused chains per wave per tile
   i32x4 a2[FUSE ? R2 : 1][2];
@@ -364,6 +379,12 @@ __global__ __launch_bounds__(512, 1) void index_scan_i8_kernel(
       for (int g = 0; g < NG; ++g) {
         const uint32_t fg = fw + g * 2 * NKS * PIECE;
         const int jg = j0 + 2 * g;
+        f32x4 sa, sb;   // this lane's row scales of sub-tiles jg, jg + 1
+        {
+          const uint32_t sp = lds_addr(scl) + (uint32_t)(slot * SC_BYTES + (jg * SUB + 4 * (lane >> 4)) * 4);
+          asm volatile("ds_read_b128 %0, %1" : "=v"(sa) : "v"(sp));
+          asm volatile("ds_read_b128 %0, %1 offset:64" : "=v"(sb) : "v"(sp));
+        }
         i8_prologue2<0>(a2, fg);
         // a late wave tests the previous tile's last two sub-tiles here, under its partner's
         // MFMAs
@@ -372,15 +393,15 @@ __global__ __launch_bounds__(512, 1) void index_scan_i8_kernel(
           emit(acc2[1], row0 - TR + last, s4_last);
         }
         if (g == 0)
-          I8Chain2<0, LOADS, G::DMA_EVERY>::run(acc2, a2, qf, fg, dma);
+          I8Chain2<0, LOADS, G::DMA_EVERY>::run(acc2, a2, qf, fg, dma, sa, sb);
         else
-          I8Chain2<0, 0, G::DMA_EVERY>::run(acc2, a2, qf, fg, NoDma());
+          I8Chain2<0, 0, G::DMA_EVERY>::run(acc2, a2, qf, fg, NoDma(), sa, sb);
         if (g + 1 < NG || !late) {
-          emit(acc2[0], row0 + jg * SUB, scales(slot, jg));
-          emit(acc2[1], row0 + (jg + 1) * SUB, scales(slot, jg + 1));
+          emit(acc2[0], row0 + jg * SUB, sa);
+          emit(acc2[1], row0 + (jg + 1) * SUB, sb);
         } else {
-          s4_prev = scales(slot, jg);
-          s4_last = scales(slot, jg + 1);
+          s4_prev = sa;
+          s4_last = sb;
         }
       }
       continue;
