@@ -358,7 +358,8 @@ def main() -> None:
                 "encode_search_overlap": overlap,
                 # per-rank scan kernel: the emitting MFMA scan (csrc/hip/index_mq.hip) for >= 256
                 # seeded queries (512 per workgroup at >= 512), else the 256-query list kernel
-                "index_scan": ("emitting-512q" if B * info.world >= 512 else "emitting-256q")
+                "index_scan": (("int8-pruned-" if prune else "emitting-")
+                               + ("512q" if B * info.world >= 512 else "256q"))
                               if (shard.scan_mq and args.index_dtype == "bf16" and cfg.hidden == 384
                                   and B * info.world >= shard.mq_min_nq and args.k <= 16)
                               else "list-256q",

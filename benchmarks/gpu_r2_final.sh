@@ -1,0 +1,14 @@
+# session-5 final validation: GPU tests, smoke, headline (pruned default + full-bf16 A/B),
+# BASELINE config suite, e2e service, rocprof kernel stats of the headline
+set -o pipefail
+export PYTHONUNBUFFERED=1
+O=gpurun_out/${1:-r2_final}; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/gpu_tests.log 2>&1; rc=$?; tail -1 $O/gpu_tests.log; [ $rc -eq 0 ] &&
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && tail -1 $O/smoke.log &&
+timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err && cat $O/bench.json &&
+timeout -k 10 400 python bench.py --index-prune none > $O/bench_full_bf16.json 2> $O/bench_full_bf16.err && tail -c 300 $O/bench_full_bf16.json &&
+timeout -k 10 900 python benchmarks/suite.py --out $O/suite_1gpu.jsonl > $O/suite.log 2>&1 && cut -c1-200 $O/suite_1gpu.jsonl &&
+timeout -k 10 600 python benchmarks/e2e_service.py > $O/e2e.json 2> $O/e2e.err && tail -c 600 $O/e2e.json &&
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT &&
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- python bench.py --steps 10 --warmup 3 > $O/prof.log 2>&1
+echo done $?
