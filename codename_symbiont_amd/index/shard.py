@@ -249,16 +249,22 @@ class HbmIndexShard:
             dst.copy_((src.float() * FP8_SCALE).to(torch.float8_e4m3fn).view(torch.uint8))
 
     def _quant_i8(self, src, dst8, scale, bounds=None):
-        """Per-row int8 image of bf16 rows (index_i8.hip quant_rows_i8); returns the per-row
-        |x - x~| and |x~|, and folds their maxima into ``bounds`` (E, X) when given."""
+        """Per-row int8 image of bf16 rows (index_i8.hip quant_rows_i8).  With ``bounds`` (the
+        shard's (E, X)) the maxima of |x - x~| and |x~| are folded into it (on the GPU inside the
+        kernel, returning (None, None)); without, the per-row norms are returned (queries)."""
         n = src.shape[0]
         if self.device.type == "cuda":
             from ..ops._ext import hip, stream_handle
 
+            if bounds is not None:   # row writes: the kernel folds the maxima in (one launch)
+                hip().quant_rows_i8(src.data_ptr(), n, self.dim, dst8.data_ptr(), scale.data_ptr(),
+                                    0, 0, stream_handle(self.device), bounds.data_ptr())
+                return None, None
             err = torch.empty(n, dtype=torch.float32, device=self.device)
             xtn = torch.empty(n, dtype=torch.float32, device=self.device)
             hip().quant_rows_i8(src.data_ptr(), n, self.dim, dst8.data_ptr(), scale.data_ptr(),
                                 err.data_ptr(), xtn.data_ptr(), stream_handle(self.device))
+            return err, xtn
         else:
             from ..ops.reference import quant_rows_i8_ref
 
