@@ -120,8 +120,8 @@ def main() -> None:
     from codename_symbiont_amd.index.shard import resolve_prune
 
     # exact either way; i8 applies to 384-wide bf16 shards without a prefilter (else: plain scan)
-    prune = resolve_prune("auto" if args.index_prune == "i8" else "none", args.index_dtype,
-                          cfg.hidden, prefilter)
+    prune = resolve_prune("auto" if args.index_prune == "i8" and args.mode != "embed" else "none",
+                          args.index_dtype, cfg.hidden, prefilter)   # (embed mode never searches)
     shard = HbmIndexShard(cfg.hidden, rows_per_rank + extra, device=dev, dtype=args.index_dtype,
                           prefilter=prefilter, prune=prune)
     if args.mode != "embed":

@@ -78,7 +78,7 @@ int symb_index_scan_i8_ablate(const void* X8, const float* sx, int n_valid, int 
                               const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
                               int xcd, hipStream_t st, int abl);
 int symb_quant_rows_i8(const void* X, int n, int dim, void* X8, float* sx, float* err, float* xtn,
-                       hipStream_t st);
+                       float* bounds, hipStream_t st);
 int symb_gemm_lt_config(int mode);
 int symb_mq_config(int aux);
 int symb_index_scan_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
@@ -370,11 +370,13 @@ PYBIND11_MODULE(_hip, m) {
                             P<const int>(cand_n), cap, P<float>(cand_s), S(st)),
           "rescore_bf16");
   });
-  m.def("quant_rows_i8", [](uptr X, int n, int dim, uptr X8, uptr sx, uptr err, uptr xtn, uptr st) {
+  m.def("quant_rows_i8", [](uptr X, int n, int dim, uptr X8, uptr sx, uptr err, uptr xtn, uptr st,
+                            uptr bounds) {
     check(symb_quant_rows_i8(P<void>(X), n, dim, P<void>(X8), P<float>(sx), P<float>(err),
-                             P<float>(xtn), S(st)),
+                             P<float>(xtn), P<float>(bounds), S(st)),
           "quant_rows_i8");
-  });
+  }, py::arg("X"), py::arg("n"), py::arg("dim"), py::arg("X8"), py::arg("sx"), py::arg("err"),
+     py::arg("xtn"), py::arg("stream"), py::arg("bounds") = 0);
   m.def("gemm_lt_config", [](int mode) { check(symb_gemm_lt_config(mode), "gemm_lt_config"); },
         py::arg("mode"));
   m.def("mq_config", [](int aux) { check(symb_mq_config(aux), "mq_config"); }, py::arg("aux"));

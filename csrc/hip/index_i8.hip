@@ -493,15 +493,25 @@ __global__ __launch_bounds__(256) void rescore_bf16_kernel(
 
 // Per-row int8 quantiser of 384-wide bf16 rows: sx = max|x| / 127, x8 = round(x / sx), and the
 // per-row |x - sx * x8| (err) and |sx * x8| (xtn) the pruning bound needs.  One wave per row.
+// err / xtn (optional) receive the per-row norms; bounds (optional, 2 floats) is raised to
+// (max err, max xtn) by one atomic max per workgroup (non-negative floats order as their bits).
 __global__ __launch_bounds__(256) void quant_rows_i8_kernel(const __bf16* __restrict__ X, int n,
                                                             int8_t* __restrict__ X8,
                                                             float* __restrict__ sx,
                                                             float* __restrict__ err,
-                                                            float* __restrict__ xtn) {
+                                                            float* __restrict__ xtn,
+                                                            float* __restrict__ bounds) {
+  __shared__ float red[2][4];
   constexpr int D = 384, PER = D / 64;
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= n) return;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int row = blockIdx.x * 4 + w;
+  if (row >= n) {   // (block-uniform barrier below: idle waves report zeros)
+    if (bounds) {
+      if (lane == 0) red[0][w] = red[1][w] = 0.f;
+      __syncthreads();
+    }
+    return;
+  }
   float x[PER];
   const uint32_t* xp = reinterpret_cast<const uint32_t*>(X + (size_t)row * D + PER * lane);
 #pragma unroll
@@ -533,8 +543,18 @@ __global__ __launch_bounds__(256) void quant_rows_i8_kernel(const __bf16* __rest
     op[i] = (uint16_t)((qv[2 * i] & 0xff) | ((qv[2 * i + 1] & 0xff) << 8));
   if (lane == 0) {
     sx[row] = s;
-    err[row] = sqrtf(e2);
-    xtn[row] = sqrtf(n2);
+    if (err) err[row] = sqrtf(e2);
+    if (xtn) xtn[row] = sqrtf(n2);
+    red[0][w] = sqrtf(e2);
+    red[1][w] = sqrtf(n2);
+  }
+  if (bounds) {
+    __syncthreads();
+    if (threadIdx.x < 2) {
+      const float m = fmaxf(fmaxf(red[threadIdx.x][0], red[threadIdx.x][1]),
+                            fmaxf(red[threadIdx.x][2], red[threadIdx.x][3]));
+      atomicMax(reinterpret_cast<int*>(bounds) + threadIdx.x, __float_as_int(m));
+    }
   }
 }
 
@@ -640,10 +660,10 @@ int symb_rescore_bf16(const void* X, const void* Q, int NQ, int dim, const int* 
 }
 
 int symb_quant_rows_i8(const void* X, int n, int dim, void* X8, float* sx, float* err, float* xtn,
-                       hipStream_t st) {
+                       float* bounds, hipStream_t st) {
   if (n <= 0) return 0;
   if (dim != 384) return -1;
   hipLaunchKernelGGL(quant_rows_i8_kernel, dim3((n + 3) / 4), dim3(256), 0, st, (const __bf16*)X,
-                     n, (int8_t*)X8, sx, err, xtn);
+                     n, (int8_t*)X8, sx, err, xtn, bounds);
   return (int)hipGetLastError();
 }

@@ -380,10 +380,12 @@ def test_quant_rows_i8_matches_reference():
     sc = torch.empty(5003, device=DEV)
     err = torch.empty(5003, device=DEV)
     xtn = torch.empty(5003, device=DEV)
+    bounds = torch.zeros(2, device=DEV)
     hip().quant_rows_i8(x.data_ptr(), 5003, 384, q8.data_ptr(), sc.data_ptr(), err.data_ptr(),
-                        xtn.data_ptr(), stream_handle())
+                        xtn.data_ptr(), stream_handle(), bounds.data_ptr())
     r8, rs, rerr, rxtn = R.quant_rows_i8_ref(x)
     torch.cuda.synchronize()
+    assert float(bounds[0]) == float(err.max()) and float(bounds[1]) == float(xtn.max())
     _close(sc, rs, atol=0, rtol=1e-6, what="i8 scales")
     assert ((q8.int() - r8.int()).abs() <= 1).all()
     assert (q8 == r8).float().mean().item() > 0.999      # x * (1/s) vs x / s at exact halves
