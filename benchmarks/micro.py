@@ -128,6 +128,17 @@ def cmd_scanmq(a):
         ids_equal = min(ids_equal, float((ref[1] == got4[1]).float().mean()))
         max_score_diff = max(max_score_diff, float((ref[0] - got4[0]).abs().max()))
         variants["pruned_i8"] = lambda: srch(True, True, True)
+        if a.nq >= 512:   # the 256-query fused form for big batches too
+            def rs2():
+                shard.i8_rsplit2 = True
+                try:
+                    return srch(True, True, True)
+                finally:
+                    shard.i8_rsplit2 = False
+            got5 = rs2()
+            torch.cuda.synchronize()
+            ids_equal = min(ids_equal, float((ref[1] == got5[1]).float().mean()))
+            variants["pruned_i8_rs2"] = rs2
     from codename_symbiont_amd.ops._ext import hip
 
     def srch_nt():   # non-temporal row stream

@@ -196,6 +196,9 @@ class HbmIndexShard:
         # (half the LDS fragment reads per tile); False = 2 sets per wave, every wave all rows
         self.mq_rsplit = True
         self.mq_stats = False  # accumulate overflow count / max candidates (diagnostics)
+        # int8 pruned scan at >= 512 queries: False = 512 queries per workgroup (each row tile
+        # streamed once per 512 queries), True = the 256-query fused form (twice the L2 reads)
+        self.i8_rsplit2 = False
         self._mq_tot = None
 
     # ------------------------------------------------------------------ inserts
@@ -546,7 +549,7 @@ class HbmIndexShard:
         thr = ((T - margin) / sq).contiguous()
         # 3. emit every row with (q8 . x8) * sx >= thr, 4. exact bf16 re-score, 5. top-k
         h, dev, cap = hip(), self.device, self.PRUNE_CAP
-        rsplit = 2 if NQ < 512 else 1
+        rsplit = 2 if (NQ < 512 or self.i8_rsplit2) else 1
         tr = h.i8_tile_rows()
         n_qblk = math.ceil(NQ / h.i8_queries_per_blk(rsplit))
         n_rblk = max(1, min(math.ceil(n / (tr * 16)), max(1, round(n_cus / n_qblk))))
