@@ -76,6 +76,8 @@ def main() -> None:
                          "as the full bf16 scan")
     ap.add_argument("--i8-tile-rows", type=int, choices=[64, 128], default=64,
                     help="rows per tile of the int8 pruning scan")
+    ap.add_argument("--i8-waves", type=int, choices=[4, 8], default=8,
+                    help="int8 pruning scan: 8-wave workgroups (one per CU) or 4 (two per CU)")
     ap.add_argument("--encoder-dtype", choices=["bf16", "fp8"], default="bf16",
                     help="fp8: e4m3 projection GEMMs (BASELINE config #5); the headline stays bf16")
     ap.add_argument("--embed-dp", choices=["replica", "group"], default="replica",
@@ -130,7 +132,7 @@ def main() -> None:
     if prune:
         from codename_symbiont_amd.ops._ext import hip as _hip
 
-        _hip().i8_config(args.i8_tile_rows)
+        _hip().i8_config(args.i8_tile_rows, args.i8_waves)
     shard.mq_stats = os.environ.get("SYMB_MQ_STATS", "0") not in ("", "0")
     shard.scan_cus = args.scan_cus
     shard.scan_min_tiles = args.scan_min_tiles

@@ -231,7 +231,7 @@ def cmd_scani8abl(a):
     shard = HbmIndexShard(D, a.rows + 8192, device="cuda", prune="i8")
     shard.fill_random(a.rows, seed=1)
     q = torch.nn.functional.normalize(torch.randn(a.nq, D, device="cuda"), dim=-1).bfloat16()
-    hip().i8_config(a.i8_tr)
+    hip().i8_config(a.i8_tr, a.i8_waves)
     shard.search(q, k)
     torch.cuda.synchronize()
     P = shard._pruned_last
@@ -251,7 +251,7 @@ def cmd_scani8abl(a):
                        cnt0.data_ptr(), P["cap"], cs0.data_ptr(), st)
 
     variants = {"search": lambda: shard.search(q, k), "rescore": rescore}
-    variants.update({f"abl{m}": (lambda m=m: scan(m)) for m in (0, 1, 2, 4)})
+    variants.update({f"abl{m}": (lambda m=m: scan(m)) for m in ((0, 2, 4) if a.i8_waves == 4 else (0, 1, 2, 4))})
     r = ab(variants, rounds=a.rounds, iters=a.iters)
     out = {nm: dict(ms=round(m, 3), TBps=round(n * D / (m / 1e3) / 1e12, 2)) for nm, (m, _) in r.items()}
     cnt = cnt0
@@ -263,7 +263,7 @@ def cmd_scani8abl(a):
     out["in_kernel_clock_GHz"] = round((st_[:, 0] / st_[:, 1] * 0.1).median().item(), 3)
     out["cycles_per_64_rows"] = round((st_[:, 0] / math.ceil(P["rows_per_blk"] / TILE_ROWS)).median().item(), 1)
     hip().i8_config(64)
-    print(json.dumps({"bench": "scani8_ablation", "rows": n, "nq": a.nq, "tile_rows": a.i8_tr,
+    print(json.dumps({"bench": "scani8_ablation", "rows": n, "nq": a.nq, "tile_rows": a.i8_tr, "waves": a.i8_waves,
                       "cand_mean": float(cnt.float().mean()),
                       "cand_max": int(cnt.max()), "results": out}))
 
@@ -624,6 +624,7 @@ def main():
     ap.add_argument("--rsplit", type=int, default=1, help="scanmqabl: waves per query group (1, 2)")
     ap.add_argument("--prune", action="store_true", help="scanmq: also the exact int8-pruned search")
     ap.add_argument("--i8-tr", type=int, default=64, help="scani8abl: int8 scan tile rows (64, 128)")
+    ap.add_argument("--i8-waves", type=int, default=8, help="scani8abl: int8 scan waves per workgroup (8, 4)")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=5)
     a = ap.parse_args()

@@ -552,7 +552,8 @@ class HbmIndexShard:
         rsplit = 2 if (NQ < 512 or self.i8_rsplit2) else 1
         tr = h.i8_tile_rows()
         n_qblk = math.ceil(NQ / h.i8_queries_per_blk(rsplit))
-        n_rblk = max(1, min(math.ceil(n / (tr * 16)), max(1, round(n_cus / n_qblk))))
+        wpc = h.i8_wgs_per_cu()
+        n_rblk = max(1, min(math.ceil(n / (tr * 16)), max(1, round(n_cus * wpc / n_qblk))))
         rows_per_blk = _round_up(max(1, math.ceil(n / n_rblk)), tr)
         n_rblk = max(1, math.ceil(n / rows_per_blk))
         cs = torch.empty(NQ, cap, device=dev)

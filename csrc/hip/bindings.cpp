@@ -69,8 +69,9 @@ int symb_index_scan_i8(const void* X8, const float* sx, int n_valid, int alloc_r
                        int rows_per_blk, int n_rblk, const void* Q8, int NQ, const float* thr,
                        float* cand_s, int* cand_i, int* cand_n, int cap, int xcd, hipStream_t st,
                        int rsplit);
-int symb_i8_config(int tile_rows);
+int symb_i8_config(int tile_rows, int waves);
 int symb_i8_tile_rows();
+int symb_i8_wgs_per_cu();
 int symb_rescore_bf16(const void* X, const void* Q, int NQ, int dim, const int* cand_i,
                       const int* cand_n, int cap, float* cand_s, hipStream_t st);
 int symb_index_scan_i8_ablate(const void* X8, const float* sx, int n_valid, int alloc_rows,
@@ -342,9 +343,10 @@ PYBIND11_MODULE(_hip, m) {
   // multi-query-block D=384 scan (index_mq.hip): candidates above the seeded thresholds
   m.def("i8_queries_per_blk", [](int rsplit) { return symb_i8_queries_per_blk(rsplit); },
         py::arg("rsplit") = 2);
-  m.def("i8_config", [](int tile_rows) { check(symb_i8_config(tile_rows), "i8_config"); },
-        py::arg("tile_rows"));
+  m.def("i8_config", [](int tile_rows, int waves) { check(symb_i8_config(tile_rows, waves), "i8_config"); },
+        py::arg("tile_rows"), py::arg("waves") = 8);
   m.def("i8_tile_rows", []() { return symb_i8_tile_rows(); });
+  m.def("i8_wgs_per_cu", []() { return symb_i8_wgs_per_cu(); });
   m.def("index_scan_i8", [](uptr X8, uptr sx, int n_valid, int alloc_rows, int rows_per_blk,
                             int n_rblk, uptr Q8, int NQ, uptr thr, uptr cand_s, uptr cand_i,
                             uptr cand_n, int cap, int xcd, uptr st, int rsplit) {

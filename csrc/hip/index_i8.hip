@@ -40,19 +40,24 @@ constexpr int NKS = D / 64;                 // 6 k-steps of v_mfma_i32_16x16x64_
 constexpr int PIECE = 1024;
 // Tile geometry: TR = 64-row tiles (24 KiB) in a 5-deep ring, or 128-row tiles (48 KiB) in a
 // 3-deep ring -- the same 96 KiB in flight, half the barriers and DMA bursts per row.
-template <int TR_> struct Geo {
+// WV = 4: 4-wave workgroups (one wave per SIMD), TWO per CU, each with its own 3-deep ring:
+// the two waves sharing a SIMD then belong to different workgroups, so one's barrier, prologue
+// and DMA burst fall under the other's MFMAs instead of in lockstep with them.
+template <int TR_, int WV_ = 8> struct Geo {
   static constexpr int TR = TR_;
+  static constexpr int WV = WV_;
   static constexpr int NSUB = TR / SUB;
-  static constexpr int NS = TR == 64 ? 5 : 3;
+  static constexpr int NS = WV == 4 ? 3 : (TR == 64 ? 5 : 3);
   static constexpr int TILE_BYTES = TR * D;
-  static constexpr int LOADS = TILE_BYTES / (1024 * WAVES);   // LDS-DMA pieces per wave per tile
+  static constexpr int LOADS = TILE_BYTES / (1024 * WV);      // LDS-DMA pieces per wave per tile
   static constexpr int DMA_EVERY = NKS / LOADS;               // k-steps between pieces
   static constexpr int SCW = TR / 64;                         // waves carrying a scale DMA
   static constexpr int SC_BYTES = TR * 4;
-  static constexpr int STW = TR == 64 ? 192 : 128;            // staged candidates per wave
+  static constexpr int STW = WV == 4 ? 160 : (TR == 64 ? 192 : 128);   // staged candidates per wave
   static constexpr int STAGE_BYTES = STW * 10;
-  static constexpr int LDS_BYTES = NS * TILE_BYTES + NS * SC_BYTES + WAVES * STAGE_BYTES;
-  static_assert(TILE_BYTES % (1024 * WAVES) == 0, "tile must split evenly over waves");
+  static constexpr int LDS_BYTES = NS * TILE_BYTES + NS * SC_BYTES + WV * STAGE_BYTES;
+  static_assert(TILE_BYTES % (1024 * WV) == 0, "tile must split evenly over waves");
+  static_assert(WV == 8 || 2 * LDS_BYTES <= 160 * 1024, "two 4-wave workgroups must share a CU");
   static_assert(NSUB * NKS * PIECE == TILE_BYTES, "a tile is NSUB x NKS pieces");
   static_assert(LOADS * DMA_EVERY <= NKS && DMA_EVERY >= 1, "DMA pieces must fit the first chain");
   static_assert(LDS_BYTES <= 160 * 1024, "ring + scales + stages exceed the CU's 160 KiB");
@@ -90,15 +95,15 @@ __device__ __forceinline__ void i8_mfma(i32x4& acc, const i32x4& a, const i32x4&
 }
 
 // k-step KS of one 16-row sub-tile (index_mq.hip MqChain, int8 operands).
-template <int KS, int DMA_PIECES, bool NEXT>
+template <int KS, int DMA_PIECES, bool NEXT, int DE = i8s::DMA_EVERY>
 struct I8Chain {
   template <class Dma>
   __device__ __forceinline__ static void run(i32x4 (&acc)[i8s::SETS], i32x4 (&a)[i8s::R],
                                              const i32x4 (&qf)[i8s::SETS][i8s::NKS],
                                              uint32_t base, uint32_t next, const Dma& dma) {
     using namespace i8s;
-    if constexpr (DMA_PIECES > 0 && KS % DMA_EVERY == 0 && KS / DMA_EVERY < DMA_PIECES)
-      dma(KS / DMA_EVERY);
+    static_assert(DMA_PIECES * DE <= NKS, "every DMA piece must be issued in the chain");
+    if constexpr (DMA_PIECES > 0 && KS % DE == 0 && KS / DE < DMA_PIECES) dma(KS / DE);
     constexpr int outstanding = (NEXT || NKS - KS >= PF) ? PF : (NKS - KS);
     i8_lgkm<outstanding - 1>(a[KS % R]);
 #pragma unroll
@@ -108,7 +113,7 @@ struct I8Chain {
       i8_read16<(KS + PF) * PIECE>(a[(KS + PF) % R], base);
     else if constexpr (NEXT)
       i8_read16<(KS + PF - NKS) * PIECE>(a[(KS + PF) % R], next);
-    if constexpr (KS + 1 < NKS) I8Chain<KS + 1, DMA_PIECES, NEXT>::run(acc, a, qf, base, next, dma);
+    if constexpr (KS + 1 < NKS) I8Chain<KS + 1, DMA_PIECES, NEXT, DE>::run(acc, a, qf, base, next, dma);
   }
 };
 
@@ -181,17 +186,17 @@ __device__ __forceinline__ const char* i8_uniform(const char* p) {
 // ABL (profiling entry symb_index_scan_i8_ablate only): 1 = no LDS-DMA, 2 = no emission test,
 // 3 = full + s_memtime / s_memrealtime around the tile loop into cand_s[2 * blockIdx.x + {0, 1}],
 // 4 = LDS-DMA ring only.
-template <int RSPLIT, int ABL = 0, int TRK = 64>
-__global__ __launch_bounds__(512, 1) void index_scan_i8_kernel(
+template <int RSPLIT, int ABL = 0, int TRK = 64, int WV = 8>
+__global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
     const int8_t* __restrict__ X8, const float* __restrict__ sx, int n_valid, int rows_per_blk,
     const int8_t* __restrict__ Q8, int NQ, int n_qblk, int xcd, const float* __restrict__ thr_in,
     float* __restrict__ cand_s, int* __restrict__ cand_i, int* __restrict__ cand_n, int cap) {
   using namespace i8s;
-  using G = Geo<TRK>;
+  using G = Geo<TRK, WV>;
   constexpr int TR = G::TR, NSUB = G::NSUB, NS = G::NS, TILE_BYTES = G::TILE_BYTES;
   constexpr int LOADS = G::LOADS, SC_BYTES = G::SC_BYTES, STW = G::STW;
   constexpr int STAGE_BYTES = G::STAGE_BYTES;
-  constexpr int QW = SETS * 16, QWAVES = WAVES / RSPLIT, QPB = QWAVES * QW;
+  constexpr int QW = SETS * 16, QWAVES = WV / RSPLIT, QPB = QWAVES * QW;
   constexpr int NSW = NSUB / RSPLIT;
   static_assert(RSPLIT == 1 || RSPLIT == 2, "row split");
   static_assert(TRK == 64 || NSW % 2 == 0, "128-row tiles run the fused two-sub-tile chains");
@@ -230,7 +235,7 @@ __global__ __launch_bounds__(512, 1) void index_scan_i8_kernel(
   char* scl = smem + NS * TILE_BYTES;   // NS x 64 row scales
   auto issue_tile = [&](int t, int i) {  // piece i of tile t (+ the scales: wave 0, piece 0)
     const int tt = min(t, n_tiles - 1);   // past the end: re-load the last tile (vmcnt stays exact)
-    const int p = i * WAVES + wave_u, j = p / NKS, ks = p % NKS;
+    const int p = i * WV + wave_u, j = p / NKS, ks = p % NKS;
     const int prow = row_begin + tt * TR;
     const char* base = reinterpret_cast<const char*>(X8 + (size_t)(prow + j * SUB) * D + ks * 64);
     glds16_aux<0>(i8_uniform(base) + loff, smem + (t % NS) * TILE_BYTES + p * PIECE);
@@ -347,7 +352,8 @@ __global__ __launch_bounds__(512, 1) void index_scan_i8_kernel(
   i32x4 a2[FUSE ? R2 : 1][2];
   i32x4 acc2[FUSE ? 2 : 1][SETS];
   f32x4 s4_prev = {0.f, 0.f, 0.f, 0.f};
-  const bool late = wave_u >= WAVES / 2;   // partner waves (w, w + 4) stay half a test apart
+  // partner waves (w, w + 4) of an 8-wave workgroup stay half a test apart
+  const bool late = WV == 8 && wave_u >= WAVES / 2;
   // the late wave tests its last sub-tile after the NEXT barrier, when wave 0 may already be
   // refilling that tile's scale slot: its scales are read into registers before the barrier
   f32x4 s4_last = {0.f, 0.f, 0.f, 0.f};
@@ -409,9 +415,9 @@ __global__ __launch_bounds__(512, 1) void index_scan_i8_kernel(
     i8_prologue<0>(a, fw);
     if (late && t > 0) emit(acc, row0 - TR + last, s4_last);
     if constexpr (NSW > 1)
-      I8Chain<0, LOADS, true>::run(acc, a, qf, fw, fw + NKS * PIECE, dma);
+      I8Chain<0, LOADS, true, G::DMA_EVERY>::run(acc, a, qf, fw, fw + NKS * PIECE, dma);
     else
-      I8Chain<0, LOADS, false>::run(acc, a, qf, fw, 0, dma);
+      I8Chain<0, LOADS, false, G::DMA_EVERY>::run(acc, a, qf, fw, 0, dma);
 #pragma unroll
     for (int j = 1; j < NSW; ++j) {
       emit(acc, row0 + (j0 + j - 1) * SUB, scales(slot, j0 + j - 1));
@@ -562,31 +568,37 @@ __global__ __launch_bounds__(256) void quant_rows_i8_kernel(const __bf16* __rest
 
 using namespace symb;
 
-int symb_i8_queries_per_blk(int rsplit) { return i8s::WAVES / rsplit * 16 * i8s::SETS; }
-
-// rows per scan tile (symb_i8_config): 64 or 128
+// rows per scan tile and waves per workgroup (symb_i8_config): 64 / 128 rows, 8 waves (one
+// workgroup per CU) or 4 (64-row tiles, two workgroups per CU, 256 queries each)
 static int g_i8_tr = 64;
-int symb_i8_config(int tile_rows) {
+static int g_i8_waves = 8;
+int symb_i8_config(int tile_rows, int waves) {
   if (tile_rows != 64 && tile_rows != 128) return -1;
+  if (waves != 8 && !(waves == 4 && tile_rows == 64)) return -1;
   g_i8_tr = tile_rows;
+  g_i8_waves = waves;
   return 0;
 }
 int symb_i8_tile_rows() { return g_i8_tr; }
+int symb_i8_wgs_per_cu() { return 8 / g_i8_waves; }
+int symb_i8_queries_per_blk(int rsplit) {
+  return g_i8_waves == 4 ? 4 * 16 * i8s::SETS : i8s::WAVES / rsplit * 16 * i8s::SETS;
+}
 
-template <int RSPLIT, int TRK>
+template <int RSPLIT, int TRK, int WV = 8>
 static int launch_i8(const void* X8, const float* sx, int n_valid, int rows_per_blk, int n_rblk,
                      const void* Q8, int NQ, const float* thr, float* cand_s, int* cand_i,
                      int* cand_n, int cap, int xcd, hipStream_t st) {
-  constexpr int qpb = i8s::WAVES / RSPLIT * 16 * i8s::SETS;
+  constexpr int qpb = WV / RSPLIT * 16 * i8s::SETS;
   const int n_qblk = (NQ + qpb - 1) / qpb;
-  constexpr int lds = i8s::Geo<TRK>::LDS_BYTES;
+  constexpr int lds = i8s::Geo<TRK, WV>::LDS_BYTES;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)index_scan_i8_kernel<RSPLIT, 0, TRK>,
+    (void)hipFuncSetAttribute((const void*)index_scan_i8_kernel<RSPLIT, 0, TRK, WV>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
-  hipLaunchKernelGGL((index_scan_i8_kernel<RSPLIT, 0, TRK>), dim3(n_rblk * n_qblk), dim3(512), lds, st,
+  hipLaunchKernelGGL((index_scan_i8_kernel<RSPLIT, 0, TRK, WV>), dim3(n_rblk * n_qblk), dim3(64 * WV), lds, st,
                      (const int8_t*)X8, sx, n_valid, rows_per_blk, (const int8_t*)Q8, NQ, n_qblk,
                      xcd, thr, cand_s, cand_i, cand_n, cap);
   return (int)hipGetLastError();
@@ -608,6 +620,9 @@ int symb_index_scan_i8(const void* X8, const float* sx, int n_valid, int alloc_r
   if (e != hipSuccess) return (int)e;
 #define SYMB_I8(RS, T) launch_i8<RS, T>(X8, sx, n_valid, rows_per_blk, n_rblk, Q8, NQ, thr, cand_s, \
                                         cand_i, cand_n, cap, xcd, st)
+  if (g_i8_waves == 4)
+    return launch_i8<1, 64, 4>(X8, sx, n_valid, rows_per_blk, n_rblk, Q8, NQ, thr, cand_s, cand_i,
+                               cand_n, cap, xcd, st);
   if (rsplit == 2) return tr == 128 ? SYMB_I8(2, 128) : SYMB_I8(2, 64);
   if (rsplit == 1) return tr == 128 ? SYMB_I8(1, 128) : SYMB_I8(1, 64);
 #undef SYMB_I8
@@ -627,14 +642,25 @@ int symb_index_scan_i8_ablate(const void* X8, const float* sx, int n_valid, int 
   hipError_t e = hipMemsetAsync(cand_n, 0, sizeof(int) * (size_t)NQ, st);
   if (e != hipSuccess) return (int)e;
   const int n_qblk = (NQ + 255) / 256;
-  const int lds = tr == 128 ? i8s::Geo<128>::LDS_BYTES : i8s::Geo<64>::LDS_BYTES;
+  const int w4 = g_i8_waves == 4;
+  const int lds = w4 ? i8s::Geo<64, 4>::LDS_BYTES
+                     : (tr == 128 ? i8s::Geo<128>::LDS_BYTES : i8s::Geo<64>::LDS_BYTES);
   auto go = [&](auto kern) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    hipLaunchKernelGGL(kern, dim3(n_rblk * n_qblk), dim3(512), lds, st, (const int8_t*)X8, sx,
+    hipLaunchKernelGGL(kern, dim3(n_rblk * n_qblk), dim3(w4 ? 256 : 512), lds, st, (const int8_t*)X8, sx,
                        n_valid, rows_per_blk, (const int8_t*)Q8, NQ, n_qblk, xcd, thr, cand_s,
                        cand_i, cand_n, cap);
     return (int)hipGetLastError();
   };
+  if (w4) {
+    switch (abl) {
+      case 0: return go(index_scan_i8_kernel<1, 0, 64, 4>);
+      case 2: return go(index_scan_i8_kernel<1, 2, 64, 4>);
+      case 3: return go(index_scan_i8_kernel<1, 3, 64, 4>);
+      case 4: return go(index_scan_i8_kernel<1, 4, 64, 4>);
+      default: return -1;
+    }
+  }
   switch (abl + (tr == 128 ? 8 : 0)) {
     case 0: return go(index_scan_i8_kernel<2, 0, 64>);
     case 1: return go(index_scan_i8_kernel<2, 1, 64>);

@@ -398,7 +398,8 @@ def test_quant_rows_i8_matches_reference():
 @pytest.mark.parametrize("nq,data,tr", [(256, "random", 64), (300, "random", 64), (512, "random", 64),
                                         (1100, "random", 64), (256, "clustered", 64), (512, "near", 64),
                                         (256, "random", 128), (300, "near", 128), (1100, "random", 128),
-                                        (256, "clustered", 128)])
+                                        (256, "clustered", 128), (256, "random", -64),
+                                        (1100, "near", -64), (256, "clustered", -64)])
 def test_index_pruned_search_is_exact(nq, data, tr):
     """prune="i8" (int8 bound-pruned scan + exact bf16 re-score) returns the rows and scores of the
     exact bf16 scan: random data, tight clusters (near-ties everywhere: candidate overflow takes
@@ -426,7 +427,7 @@ def test_index_pruned_search_is_exact(nq, data, tr):
     from codename_symbiont_amd.ops._ext import hip
 
     s0, r0 = ref.search(q, k)
-    hip().i8_config(tr)    # rows per int8 scan tile
+    hip().i8_config(abs(tr), 4 if tr < 0 else 8)   # rows per tile; tr < 0: 4-wave workgroups
     try:
         s1, r1 = shard.search(q, k)
     finally:
