@@ -95,6 +95,9 @@ def main() -> None:
                          "its short latency-bound kernels dispatch ahead of the encoder's")
     ap.add_argument("--scan-min-tiles", type=int, default=16,
                     help="smallest row block (64-row tiles) of the small list scans")
+    ap.add_argument("--prune-sample-shift", type=int, default=0,
+                    help="exact pruned search: threshold sample = 1 tile in 2^shift (0 = the "
+                         "shard default, HbmIndexShard.PRUNE_TILE_SHIFT)")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch the encoder's kernels eagerly every step instead of replaying a "
                          "captured hipGraph of the forward")
@@ -136,6 +139,8 @@ def main() -> None:
     shard.mq_stats = os.environ.get("SYMB_MQ_STATS", "0") not in ("", "0")
     shard.scan_cus = args.scan_cus
     shard.scan_min_tiles = args.scan_min_tiles
+    if args.prune_sample_shift:
+        shard.PRUNE_TILE_SHIFT = args.prune_sample_shift
     torch.cuda.synchronize(dev)
     row_bytes = cfg.hidden * (1 if args.index_dtype == "fp8" else 2)
     log(info, f"[bench] setup {time.time() - t0:.1f}s: {cfg.model_name}, shard {rows_per_rank} "
@@ -368,6 +373,7 @@ def main() -> None:
                 "encoder_hipgraph": use_graph,
                 "search_priority": args.search_priority,
                 "scan_min_tiles": args.scan_min_tiles,
+                "prune_sample_shift": shard.PRUNE_TILE_SHIFT if prune else None,
             },
             "embeds_per_sec": round(total, 2) if args.mode != "search" else 0.0,
             "topk_qps": round(total, 2) if args.mode != "embed" else 0.0,
