@@ -34,14 +34,18 @@ def env_world() -> tuple[int, int, int]:
 
 
 def init(backend: str | None = None, device_type: str | None = None) -> DistInfo:
+    """Rehearsal knobs (one-GPU boxes; never set for real runs): ``SYMB_DIST_BACKEND=gloo`` and
+    ``SYMB_DEVICE_INDEX=0`` put every rank of a multi-rank job on one device over gloo, since RCCL
+    refuses two ranks on one GPU (tests/test_parallel_gpu.py, benchmarks/gpu_bench_rehearsal.sh)."""
     rank, world, local = env_world()
     use_gpu = torch.cuda.is_available() if device_type is None else device_type == "cuda"
     if use_gpu:
-        torch.cuda.set_device(local)
-        device = torch.device("cuda", local)
+        dev_idx = int(os.environ.get("SYMB_DEVICE_INDEX", local))
+        torch.cuda.set_device(dev_idx)
+        device = torch.device("cuda", dev_idx)
     else:
         device = torch.device("cpu")
-    backend = backend or ("nccl" if use_gpu else "gloo")
+    backend = backend or os.environ.get("SYMB_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29512")
@@ -56,7 +60,7 @@ def init(backend: str | None = None, device_type: str | None = None) -> DistInfo
 def barrier(info: DistInfo) -> None:
     if info.world > 1:
         if info.backend == "nccl":
-            dist.barrier(device_ids=[info.local_rank])
+            dist.barrier(device_ids=[info.device.index])
         else:
             dist.barrier()
 
