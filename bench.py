@@ -98,6 +98,9 @@ def main() -> None:
     ap.add_argument("--prune-sample-shift", type=int, default=0,
                     help="exact pruned search: threshold sample = 1 tile in 2^shift (0 = the "
                          "shard default, HbmIndexShard.PRUNE_TILE_SHIFT)")
+    ap.add_argument("--prepass-min-tiles", type=int, default=0,
+                    help="row-block floor of the sampled searches' small pre-pass list scans "
+                         "(0 = the shard default, 1 tile per workgroup)")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch the encoder's kernels eagerly every step instead of replaying a "
                          "captured hipGraph of the forward")
@@ -139,6 +142,8 @@ def main() -> None:
     shard.mq_stats = os.environ.get("SYMB_MQ_STATS", "0") not in ("", "0")
     shard.scan_cus = args.scan_cus
     shard.scan_min_tiles = args.scan_min_tiles
+    if args.prepass_min_tiles:
+        shard.prepass_min_tiles = args.prepass_min_tiles
     if args.prune_sample_shift:
         shard.PRUNE_TILE_SHIFT = args.prune_sample_shift
     torch.cuda.synchronize(dev)
@@ -373,6 +378,7 @@ def main() -> None:
                 "encoder_hipgraph": use_graph,
                 "search_priority": args.search_priority,
                 "scan_min_tiles": args.scan_min_tiles,
+                "prepass_min_tiles": shard.prepass_min_tiles,
                 "prune_sample_shift": shard.PRUNE_TILE_SHIFT if prune else None,
             },
             "embeds_per_sec": round(total, 2) if args.mode != "search" else 0.0,

@@ -181,6 +181,10 @@ class HbmIndexShard:
         # smallest row block (in 64-row tiles) of the 256-query list scan: small scans (threshold
         # seeding, the fresh-row tail) are latency-bound, so fewer tiles per block = more CUs
         self.scan_min_tiles = 16
+        # ... and of the two small list scans on the sampled searches' critical path (seed
+        # sub-sample ~49k rows, fresh-row tail 4096-8191 rows at 100M): one tile per workgroup
+        # spreads them over every CU (106 -> 52 us and 211 -> 57 us; profiles/r2_min_tiles/)
+        self.prepass_min_tiles = 1
         self.scan_aux = -1   # index-stream cache policy (-1 = auto: non-temporal when read once)
         self.seed_threshold = True  # sample pre-pass seeds per-query top-k thresholds
         self.scan_variant = 0        # fp8 scan ring geometry (0 = default)
@@ -389,12 +393,14 @@ class HbmIndexShard:
             # k-th best of the union lower-bounds the final k-th score.
             ts, nv, t0, idx = plan
             sub = torch.index_select(self.rows, 0, idx)       # whole tiles: already tile-padded
-            s0, _ = self._scan(sub.shape[0], q_unit, kmax, k, None, n_cus, sub, dtype)
+            pm = self.prepass_min_tiles
+            s0, _ = self._scan(sub.shape[0], q_unit, kmax, k, None, n_cus, sub, dtype, min_tiles=pm)
             thr0 = s0[:, k - 1].contiguous() - self.MQ_THR_MARGIN
             pre_s, _ = self._scan_mq(nv * TILE_ROWS, q_unit, kmax, k, thr0, n_cus, tshift=ts)
             # (seeded with thr0 too: a tail row below it cannot enter the union's top k, whose
             # k-th best is the sample's, >= thr0; unseeded this small scan took 0.2 ms)
-            tail_s, _ = self._scan(n - t0, q_unit, kmax, k, thr0, n_cus, self.rows[t0:], dtype)
+            tail_s, _ = self._scan(n - t0, q_unit, kmax, k, thr0, n_cus, self.rows[t0:], dtype,
+                                   min_tiles=pm)
             kth = torch.topk(torch.cat([pre_s, tail_s], 1), k, dim=1).values[:, k - 1]
             thr = kth.contiguous() - self.MQ_THR_MARGIN
             return self._scan_mq(n, q_unit, kmax, k, thr, n_cus)
@@ -447,10 +453,16 @@ class HbmIndexShard:
         t0 = nv * group
         if t0 > n:   # (a launch past the rows would fault the GPU)
             raise RuntimeError("tile sample past the visible rows")
-        v = torch.arange(0, nv, self.SEED_DIV, device=self.device, dtype=torch.int64)
-        ph = (v << ts) + (((v * 0x9E3779B1) & 0xFFFFFFFF) >> (32 - ts))
-        idx = (ph[:, None] * TILE_ROWS + torch.arange(TILE_ROWS, device=self.device)).reshape(-1)
-        return ts, nv, t0, idx
+        # idx depends on (nv, ts) only, and nv changes once per 2^ts tiles of appends: cached
+        # (rebuilding it was ~8 small kernels on every search's critical path)
+        key = (nv, ts, self.SEED_DIV)
+        cached = getattr(self, "_plan_idx", None)
+        if cached is None or cached[0] != key:
+            v = torch.arange(0, nv, self.SEED_DIV, device=self.device, dtype=torch.int64)
+            ph = (v << ts) + (((v * 0x9E3779B1) & 0xFFFFFFFF) >> (32 - ts))
+            idx = (ph[:, None] * TILE_ROWS + torch.arange(TILE_ROWS, device=self.device)).reshape(-1)
+            self._plan_idx = cached = (key, idx)
+        return ts, nv, t0, cached[1]
 
     def _mq_ok(self, NQ: int, k: int, rows, dtype: str) -> bool:
         return (self.scan_mq and dtype == "bf16" and self.dim == 384 and rows is self.rows
@@ -535,20 +547,24 @@ class HbmIndexShard:
         #    4096+ rows where fresh inserts sit), as in _search_scan
         ts, nv, t0, idx = plan
         sub = torch.index_select(self.rows, 0, idx)
-        s0, _ = self._scan(sub.shape[0], q_unit, kmax, k, None, n_cus, sub, "bf16")
+        pm = self.prepass_min_tiles
+        s0, _ = self._scan(sub.shape[0], q_unit, kmax, k, None, n_cus, sub, "bf16", min_tiles=pm)
         thr0 = s0[:, k - 1].contiguous() - self.MQ_THR_MARGIN
         pre_s, _ = self._scan_mq(nv * TILE_ROWS, q_unit, kmax, k, thr0, n_cus, tshift=ts)
-        tail_s, _ = self._scan(n - t0, q_unit, kmax, k, thr0, n_cus, self.rows[t0:], "bf16")
-        T = torch.topk(torch.cat([pre_s, tail_s], 1), k, dim=1).values[:, k - 1] - self.MQ_THR_MARGIN
-        # 2. int8 queries and the per-query margin |q| E + |q - q~| X (+ fp32 slack)
-        q8 = torch.empty(NQ, self.dim, dtype=torch.int8, device=self.device)
-        sq = torch.empty(NQ, dtype=torch.float32, device=self.device)
-        eq, _ = self._quant_i8(q_unit, q8, sq)
-        E, X = self.i8_bounds[0], self.i8_bounds[1]
-        margin = q_unit.float().norm(dim=1) * E + eq * X + 1e-5
-        thr = ((T - margin) / sq).contiguous()
-        # 3. emit every row with (q8 . x8) * sx >= thr, 4. exact bf16 re-score, 5. top-k
+        tail_s, _ = self._scan(n - t0, q_unit, kmax, k, thr0, n_cus, self.rows[t0:], "bf16",
+                               min_tiles=pm)
+        # 2. T (k-th best of the union), the int8 queries and the per-query emission threshold
+        #    (T - |q| E - |q - q~| X - fp32 slack) / sq, in one launch (prune_qprep; the torch
+        #    composition it replaces is _prune_thresholds_torch, kept as the test oracle)
         h, dev, cap = hip(), self.device, self.PRUNE_CAP
+        q8 = torch.empty(NQ, self.dim, dtype=torch.int8, device=dev)
+        sq = torch.empty(NQ, dtype=torch.float32, device=dev)
+        T = torch.empty(NQ, dtype=torch.float32, device=dev)
+        thr = torch.empty(NQ, dtype=torch.float32, device=dev)
+        h.prune_qprep(q_unit.data_ptr(), NQ, self.dim, pre_s.data_ptr(), tail_s.data_ptr(), k,
+                      self.MQ_THR_MARGIN, self.i8_bounds.data_ptr(), q8.data_ptr(), sq.data_ptr(),
+                      T.data_ptr(), thr.data_ptr(), stream_handle(dev))
+        # 3. emit every row with (q8 . x8) * sx >= thr, 4. exact bf16 re-score, 5. top-k
         rsplit = 2 if (NQ < 512 or self.i8_rsplit2) else 1
         tr = h.i8_tile_rows()
         n_qblk = math.ceil(NQ / h.i8_queries_per_blk(rsplit))
@@ -585,6 +601,17 @@ class HbmIndexShard:
             torch.maximum(self._mq_tot[1], cnt.max().view(1), out=self._mq_tot[1])
         return out_s, out_i
 
+    def _prune_thresholds_torch(self, q_unit, pre_s, tail_s, k: int):
+        """Torch composition of prune_qprep (test oracle): (T, q8, sq, thr)."""
+        NQ = q_unit.shape[0]
+        T = torch.topk(torch.cat([pre_s, tail_s], 1), k, dim=1).values[:, k - 1] - self.MQ_THR_MARGIN
+        q8 = torch.empty(NQ, self.dim, dtype=torch.int8, device=self.device)
+        sq = torch.empty(NQ, dtype=torch.float32, device=self.device)
+        eq, _ = self._quant_i8(q_unit, q8, sq)
+        E, X = self.i8_bounds[0], self.i8_bounds[1]
+        margin = q_unit.float().norm(dim=1) * E + eq * X + 1e-5
+        return T, q8, sq, ((T - margin) / sq).contiguous()
+
     def _search_prefilter(self, q_unit, k: int, n_cus):
         """fp8 scan for oversample*k candidates, exact bf16 re-score, top-k (see the class doc)."""
         kc = min(32, max(16, self.oversample * k))
@@ -614,9 +641,10 @@ class HbmIndexShard:
         return min(n, self.scan_cus) if self.scan_cus else n
 
     def _scan(self, n: int, q_unit: torch.Tensor, kmax: int, k: int, thr, n_cus, rows=None,
-              dtype=None, gate=None, out=None):
+              dtype=None, gate=None, out=None, min_tiles: int | None = None):
         """Fused 256-query scan + merge.  ``gate`` (int32 device flag): the kernels skip
-        themselves unless it is non-zero; ``out``: (scores, rows) tensors to write."""
+        themselves unless it is non-zero; ``out``: (scores, rows) tensors to write;
+        ``min_tiles``: row-block floor in 64-row tiles (default ``scan_min_tiles``)."""
         from ..ops._ext import hip, stream_handle
 
         rows = self.rows if rows is None else rows
@@ -629,7 +657,8 @@ class HbmIndexShard:
         n_qblk = math.ceil(NQ / qpb)
         if n_cus is None:
             n_cus = self._n_cus()
-        n_rblk = max(1, min(math.ceil(n / (TILE_ROWS * self.scan_min_tiles)),
+        min_tiles = self.scan_min_tiles if min_tiles is None else min_tiles
+        n_rblk = max(1, min(math.ceil(n / (TILE_ROWS * min_tiles)),
                             max(1, round(n_cus / n_qblk))))
         rows_per_blk = _round_up(max(1, math.ceil(n / n_rblk)), TILE_ROWS)
         n_rblk = max(1, math.ceil(n / rows_per_blk))

@@ -80,6 +80,9 @@ int symb_index_scan_i8_ablate(const void* X8, const float* sx, int n_valid, int 
                               int xcd, hipStream_t st, int abl);
 int symb_quant_rows_i8(const void* X, int n, int dim, void* X8, float* sx, float* err, float* xtn,
                        float* bounds, hipStream_t st);
+int symb_prune_qprep(const void* Q, int NQ, int dim, const float* pre_s, const float* tail_s, int k,
+                     float thr_margin, const float* bounds, void* Q8, float* sq, float* T,
+                     float* thr, hipStream_t st);
 int symb_gemm_lt_config(int mode);
 int symb_mq_config(int aux);
 int symb_index_scan_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
@@ -379,6 +382,15 @@ PYBIND11_MODULE(_hip, m) {
           "quant_rows_i8");
   }, py::arg("X"), py::arg("n"), py::arg("dim"), py::arg("X8"), py::arg("sx"), py::arg("err"),
      py::arg("xtn"), py::arg("stream"), py::arg("bounds") = 0);
+  m.def("prune_qprep", [](uptr Q, int NQ, int dim, uptr pre_s, uptr tail_s, int k, float margin,
+                          uptr bounds, uptr Q8, uptr sq, uptr T, uptr thr, uptr st) {
+    check(symb_prune_qprep(P<void>(Q), NQ, dim, P<float>(pre_s), P<float>(tail_s), k, margin,
+                           P<float>(bounds), P<void>(Q8), P<float>(sq), P<float>(T), P<float>(thr),
+                           S(st)),
+          "prune_qprep");
+  }, py::arg("Q"), py::arg("NQ"), py::arg("dim"), py::arg("pre_s"), py::arg("tail_s"),
+     py::arg("k"), py::arg("thr_margin"), py::arg("bounds"), py::arg("Q8"), py::arg("sq"),
+     py::arg("T"), py::arg("thr"), py::arg("stream"));
   m.def("gemm_lt_config", [](int mode) { check(symb_gemm_lt_config(mode), "gemm_lt_config"); },
         py::arg("mode"));
   m.def("mq_config", [](int aux) { check(symb_mq_config(aux), "mq_config"); }, py::arg("aux"));

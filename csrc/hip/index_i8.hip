@@ -564,6 +564,72 @@ __global__ __launch_bounds__(256) void quant_rows_i8_kernel(const __bf16* __rest
   }
 }
 
+// Query preparation of the pruned search in ONE launch (was the quantiser plus ~10 small torch
+// kernels on the search's critical path, ~0.1 ms; profiles/r2_prepass/).  One wave per query:
+//   T    = the k-th best of the union of the exact sample's and the tail's per-query top-k lists
+//          (any order, -inf padded; k <= 32) minus thr_margin -- a lower bound of the final k-th
+//   q8   = the query's int8 image, sq its scale (exactly as quant_rows_i8_kernel)
+//   thr  = (T - (|q| E + |q - q~| X + 1e-5)) / sq, (E, X) = bounds (the shard's tracked maxima),
+// i.e. the threshold index_scan_i8_kernel emits against (see the bound at the top of this file).
+__global__ __launch_bounds__(256) void prune_qprep_kernel(
+    const __bf16* __restrict__ Q, int NQ, const float* __restrict__ pre_s,
+    const float* __restrict__ tail_s, int k, float thr_margin, const float* __restrict__ bounds,
+    int8_t* __restrict__ Q8, float* __restrict__ sq, float* __restrict__ T_out,
+    float* __restrict__ thr) {
+  constexpr int D = 384, PER = D / 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int q = blockIdx.x * 4 + w;
+  if (q >= NQ) return;   // (no barrier in this kernel)
+  // k-th best of 2k values: lane i < 2k holds value i; its rank counts the values above it
+  // (ties: lower index first), so exactly one lane has rank k - 1
+  float v = -INFINITY;
+  if (lane < k) v = pre_s[(size_t)q * k + lane];
+  else if (lane < 2 * k) v = tail_s[(size_t)q * k + lane - k];
+  int rank = 0;
+  for (int j = 0; j < 2 * k; ++j) {
+    const float u = __shfl(v, j);
+    rank += (u > v) || (u == v && j < lane);
+  }
+  const unsigned long long hit = __ballot(lane < 2 * k && rank == k - 1);
+  const float T = __shfl(v, (int)__builtin_ctzll(hit)) - thr_margin;
+
+  float x[PER];
+  const uint32_t* xp = reinterpret_cast<const uint32_t*>(Q + (size_t)q * D + PER * lane);
+#pragma unroll
+  for (int i = 0; i < PER / 2; ++i) {
+    const uint32_t u = xp[i];
+    x[2 * i] = __uint_as_float(u << 16);
+    x[2 * i + 1] = __uint_as_float(u & 0xffff0000u);
+  }
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) amax = fmaxf(amax, fabsf(x[i]));
+  amax = wave_max(amax);
+  const float s = amax > 0.f ? amax / 127.f : 1.f;
+  const float inv = 1.f / s;
+  float e2 = 0.f, x2 = 0.f;
+  int qv[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    qv[i] = max(-127, min(127, (int)rintf(x[i] * inv)));
+    const float xt = (float)qv[i] * s;
+    e2 += (x[i] - xt) * (x[i] - xt);
+    x2 += x[i] * x[i];
+  }
+  e2 = wave_sum(e2);
+  x2 = wave_sum(x2);
+  uint16_t* op = reinterpret_cast<uint16_t*>(Q8 + (size_t)q * D + PER * lane);
+#pragma unroll
+  for (int i = 0; i < PER / 2; ++i)
+    op[i] = (uint16_t)((qv[2 * i] & 0xff) | ((qv[2 * i + 1] & 0xff) << 8));
+  if (lane == 0) {
+    const float margin = sqrtf(x2) * bounds[0] + sqrtf(e2) * bounds[1] + 1e-5f;
+    sq[q] = s;
+    T_out[q] = T;
+    thr[q] = (T - margin) / s;
+  }
+}
+
 }  // namespace symb
 
 using namespace symb;
@@ -691,5 +757,15 @@ int symb_quant_rows_i8(const void* X, int n, int dim, void* X8, float* sx, float
   if (dim != 384) return -1;
   hipLaunchKernelGGL(quant_rows_i8_kernel, dim3((n + 3) / 4), dim3(256), 0, st, (const __bf16*)X,
                      n, (int8_t*)X8, sx, err, xtn, bounds);
+  return (int)hipGetLastError();
+}
+
+int symb_prune_qprep(const void* Q, int NQ, int dim, const float* pre_s, const float* tail_s, int k,
+                     float thr_margin, const float* bounds, void* Q8, float* sq, float* T,
+                     float* thr, hipStream_t st) {
+  if (NQ <= 0) return 0;
+  if (dim != 384 || k < 1 || k > 32) return -1;
+  hipLaunchKernelGGL(prune_qprep_kernel, dim3((NQ + 3) / 4), dim3(256), 0, st, (const __bf16*)Q,
+                     NQ, pre_s, tail_s, k, thr_margin, bounds, (int8_t*)Q8, sq, T, thr);
   return (int)hipGetLastError();
 }

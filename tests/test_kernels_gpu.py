@@ -395,6 +395,36 @@ def test_quant_rows_i8_matches_reference():
     _close(xtn, xt.norm(dim=1), atol=1e-5, what="i8 |x~|")
 
 
+@pytest.mark.parametrize("k", [1, 10, 16])
+def test_prune_qprep_matches_torch_composition(k):
+    """index_i8.hip prune_qprep (T = k-th best of the two lists, int8 query image, emission
+    threshold in one launch) == the torch composition it replaced (_prune_thresholds_torch):
+    unsorted lists, ties and -inf padding included."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+    from codename_symbiont_amd.ops._ext import hip, stream_handle
+
+    nq, n = 301, 20000
+    shard = HbmIndexShard(384, n, prune="i8")
+    shard.append_f32(_f(n, 384, seed=81))
+    q = torch.nn.functional.normalize(_f(nq, 384, seed=82), dim=-1).bfloat16()
+    pre = _f(nq, k, seed=83).round(decimals=1)            # coarse values: ties across the lists
+    tail = _f(nq, k, seed=84).round(decimals=1)
+    pre[::7, k // 2:] = -math.inf                           # short lists (few sampled rows)
+    tail[::5] = -math.inf
+    q8 = torch.empty(nq, 384, dtype=torch.int8, device=DEV)
+    sq, T, thr = (torch.empty(nq, device=DEV) for _ in range(3))
+    hip().prune_qprep(q.data_ptr(), nq, 384, pre.data_ptr(), tail.data_ptr(), k,
+                      shard.MQ_THR_MARGIN, shard.i8_bounds.data_ptr(), q8.data_ptr(),
+                      sq.data_ptr(), T.data_ptr(), thr.data_ptr(), stream_handle())
+    T0, q80, sq0, thr0 = shard._prune_thresholds_torch(q, pre, tail, k)
+    torch.cuda.synchronize()
+    assert torch.equal(T, T0), "T is an exact selection"
+    assert torch.equal(q8, q80) and torch.equal(sq, sq0)
+    fin = torch.isfinite(thr0)
+    assert torch.equal(fin, torch.isfinite(thr))
+    _close(thr[fin], thr0[fin], atol=1e-4, rtol=1e-5, what="emission thresholds (margin sums)")
+
+
 @pytest.mark.parametrize("nq,data,tr", [(256, "random", 64), (300, "random", 64), (512, "random", 64),
                                         (1100, "random", 64), (256, "clustered", 64), (512, "near", 64),
                                         (256, "random", 128), (300, "near", 128), (1100, "random", 128),
