@@ -23,6 +23,8 @@ RANK_SHIFT = 40
 
 def encode_gid(rank: int, rows: torch.Tensor) -> torch.Tensor:
     r = rows.long()
+    if rank == 0:   # (0 << 40) | r == r, and missing slots are already -1: one cast, no kernels more
+        return r
     return torch.where(r >= 0, (rank << RANK_SHIFT) | r, torch.full_like(r, -1))
 
 
