@@ -272,6 +272,15 @@ def test_tile_sample_plan_invariants():
         sub_tiles = torch.unique(idx // TILE_ROWS)
         assert idx.numel() == sub_tiles.numel() * TILE_ROWS
         assert bool(torch.isin(sub_tiles, phys).all())        # sub-sample within the sample
+    # the gather index is cached per (nv, shift): appends inside one tile group reuse it, and a
+    # new group or another shift (the pruned search samples 1 in 2^5) rebuilds it
+    n = 100_000_000
+    a = shard._tile_sample_plan(n)[3]
+    assert shard._tile_sample_plan(n + 1000)[3] is a
+    b = shard._tile_sample_plan(n, shard.PRUNE_TILE_SHIFT)[3]
+    assert b is not a and not torch.equal(b[: a.numel()], a[: b.numel()])
+    c = shard._tile_sample_plan(n + (TILE_ROWS << shard.PRUNE_TILE_SHIFT), shard.PRUNE_TILE_SHIFT)[3]
+    assert c is not b and c.numel() >= b.numel()
 
 
 def test_int8_pruning_bound_holds_and_image_follows_writes():
