@@ -98,6 +98,8 @@ def cmd_scanmq(a):
 
     D, k = 384, 10
     shard = HbmIndexShard(D, a.rows + 8192, device="cuda", prune="i8" if a.prune else None)
+    if a.prune_shift:
+        shard.PRUNE_TILE_SHIFT = a.prune_shift
     shard.fill_random(a.rows, seed=1)
     q = torch.nn.functional.normalize(torch.randn(a.nq, D, device="cuda"), dim=-1).bfloat16()
     if a.qmode == "near":   # bench-like: fresh embeddings appended last, queries near them
@@ -623,6 +625,8 @@ def main():
     ap.add_argument("--sets", type=int, default=4, help="scanmqabl: 16-query sets per wave (2 or 4)")
     ap.add_argument("--rsplit", type=int, default=1, help="scanmqabl: waves per query group (1, 2)")
     ap.add_argument("--prune", action="store_true", help="scanmq: also the exact int8-pruned search")
+    ap.add_argument("--prune-shift", type=int, default=0,
+                    help="scanmq --prune: threshold sample 1 tile in 2^shift (0 = shard default)")
     ap.add_argument("--i8-tr", type=int, default=64, help="scani8abl: int8 scan tile rows (64, 128)")
     ap.add_argument("--i8-waves", type=int, default=8, help="scani8abl: int8 scan waves per workgroup (8, 4)")
     ap.add_argument("--rounds", type=int, default=5)

@@ -527,7 +527,15 @@ class HbmIndexShard:
             torch.maximum(self._mq_tot[1], cnt.max().view(1), out=self._mq_tot[1])
         return out_s, out_i
 
-    PRUNE_TILE_SHIFT = 5      # pruned search: its exact threshold sample is 1 tile in 2^5
+    # pruned search: its exact threshold sample is 1 tile in 2^5.  Sparser samples win the
+    # headline (+2-3 % at 2^7) only because its queries' best matches sit in the exact fresh-row
+    # tail; for queries near random stored rows (the per-rank shapes 12.5M x 2048 and 50M x 512)
+    # 2^6 is 4-9 % slower and 2^7 overflows the candidate slots, 3x slower
+    # (profiles/r2_prune_shift_rank/).  A shard too small for SEED_DIV groups at 2^5 (none at
+    # the default; the override knob may raise the shift) samples more densely, down to
+    # PRUNE_MIN_SHIFT.
+    PRUNE_TILE_SHIFT = 5
+    PRUNE_MIN_SHIFT = 5
     PRUNE_CAP = 8192          # candidate slots per query (expected ~1-2k at 100M x 384)
 
     def _search_pruned(self, q_unit, k: int, n_cus):
@@ -538,7 +546,9 @@ class HbmIndexShard:
         from ..ops._ext import hip, stream_handle
 
         n, NQ, kmax = self.visible, q_unit.shape[0], 16
-        plan = self._tile_sample_plan(n, self.PRUNE_TILE_SHIFT)
+        plan, ts = None, self.PRUNE_TILE_SHIFT
+        while plan is None and ts >= min(self.PRUNE_MIN_SHIFT, self.PRUNE_TILE_SHIFT):
+            plan, ts = self._tile_sample_plan(n, ts), ts - 1
         if plan is None:
             return None
         if n_cus is None:
