@@ -20,7 +20,14 @@ Data: synthetic token ids, random-init weights (real MiniLM-L6 architecture), ra
 index rows -- there is no network for checkpoints or datasets.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-       (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+       N > 1 either under a launcher (python -m torch.distributed.run --nproc-per-node N ...
+       bench.py --gpus N: WORLD_SIZE is set) or plainly: with WORLD_SIZE unset this process
+       launches the N ranks itself as fresh child processes BEFORE touching the GPU (one per GPU,
+       env:// rendezvous on 127.0.0.1) and exits with the first failing rank's status.  A rank
+       whose world differs from --gpus exits non-zero; the JSON carries the backend, the world
+       and a startup collective self-check (all_gather of rank ids + device ids, verified).
+       --device cpu: the same step on the CPU over gloo (fp32 PyTorch encoder, tiny shapes) --
+       the multi-rank contract rehearsal the CPU tests run; never a performance number.
 
 The other BASELINE.json configs run through the same step (benchmarks/suite.py drives them):
   --mode embed                                   all-MiniLM-L6-v2 bf16 embedding, batch 256
@@ -53,7 +60,58 @@ def log(info, *a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def main() -> None:
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(n: int, argv: list[str]) -> int:
+    """Run this script as ``n`` ranks (fresh child processes, one per GPU) and wait for them.
+
+    Called only when WORLD_SIZE is unset, before anything in this process touches the GPU (no
+    HIP call, no torch.cuda query): the children start as new programs, so no GPU state is ever
+    inherited or exec'd over.  Rank 0 prints the JSON line (stdout is inherited).  The first rank
+    to fail ends the job: the others are terminated and its exit status is returned."""
+    import signal
+    import subprocess
+
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), SYMB_BENCH_LAUNCHED="1")
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC (RCCL on this driver)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc, kill_at = 0, None
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                print(f"[bench] rank {procs.index(p)} exited with {code}: stopping the job",
+                      file=sys.stderr, flush=True)
+                for q in live:
+                    q.send_signal(signal.SIGTERM)
+                kill_at = time.time() + 20.0   # a rank stuck in a collective ignores nothing else
+        if kill_at is not None and time.time() > kill_at:
+            for q in live:
+                q.kill()
+            kill_at = None
+        time.sleep(0.05)
+    return rc
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -64,6 +122,25 @@ def main() -> None:
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--model", default="minilm-l6")
     ap.add_argument("--mode", choices=["full", "embed", "search"], default="full")
+    ap.add_argument("--device", choices=["auto", "cuda", "cpu"], default="auto",
+                    help="cpu: contract rehearsal over gloo with the fp32 PyTorch encoder (tiny "
+                         "shapes; tests/test_bench_cpu.py), never a performance number")
+    ap.add_argument("--corpus", choices=["random", "clustered", "anisotropic"], default="random",
+                    help="synthetic index distribution (codename_symbiont_amd/index/synth.py)")
+    ap.add_argument("--clusters", type=int, default=100_000,
+                    help="--corpus clustered: shared cluster centers")
+    ap.add_argument("--cluster-spread", type=float, default=0.6,
+                    help="--corpus clustered: noise norm around a center (cos ~ 1/sqrt(1+s^2))")
+    ap.add_argument("--queries", choices=["self", "heldout"], default=None,
+                    help="full mode: self = the batch is upserted and THEN searched (default), "
+                         "heldout = searched before it is upserted.  search mode: heldout = fresh "
+                         "draws from the corpus distribution, never inserted (default), self = "
+                         "stored rows")
+    ap.add_argument("--verify", action="store_true",
+                    help="after the timed steps, search one batch both ways (this config and the "
+                         "full bf16 scan of every row) and report whether the ids are identical")
+    ap.add_argument("--timeline", default="",
+                    help="write per-step GPU times (+ sampled clock/power) to this JSONL file")
     ap.add_argument("--index-dtype", choices=["bf16", "fp8"], default="bf16")
     ap.add_argument("--index-prefilter", choices=["none", "fp8"], default="none",
                     help="fp8: search the bf16 index through an e4m3 copy for 3k candidates and "
@@ -104,17 +181,207 @@ def main() -> None:
     ap.add_argument("--no-graph", action="store_true",
                     help="launch the encoder's kernels eagerly every step instead of replaying a "
                          "captured hipGraph of the forward")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
+    if args.queries is None:
+        args.queries = "heldout" if args.mode == "search" else "self"
+    return args
 
+
+class ClockSampler:
+    """Background sampler of the GPU's shader clock and power (rocm-smi, ~1 Hz) for --timeline:
+    a sustained run records how the power-bound scan's clock settles, not only its step times."""
+
+    def __init__(self, device_index: int):
+        import threading
+
+        self.samples, self.dev = [], device_index
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True)
+        self._t.start()
+
+    def _run(self):
+        import re
+        import subprocess
+
+        while not self._stop.is_set():
+            try:
+                out = subprocess.run(["rocm-smi", "-d", str(self.dev), "--showclocks",
+                                      "--showpower"], capture_output=True, text=True,
+                                     timeout=5).stdout
+                sclk = re.search(r"sclk.*?\((\d+)Mhz\)", out)
+                pwr = re.search(r"Power \(W\):\s*([\d.]+)", out)
+                self.samples.append((time.time(), int(sclk.group(1)) if sclk else None,
+                                     float(pwr.group(1)) if pwr else None))
+            except Exception:   # noqa: BLE001 -- sampling is best effort
+                pass
+            self._stop.wait(1.0)
+
+    def stop(self):
+        self._stop.set()
+        self._t.join(timeout=6)
+        return self.samples
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # plain `python bench.py --gpus N`: launch the N ranks (nothing has touched the GPU yet)
+        return self_launch(args.gpus, sys.argv[1:] if argv is None else list(argv))
+
+    from codename_symbiont_amd.parallel import dist as D
+
+    info = D.init(device_type=None if args.device == "auto" else args.device)
+    if info.world != args.gpus:
+        print(f"[bench] rank {info.rank}: --gpus {args.gpus} but the job has {info.world} "
+              f"rank(s) (WORLD_SIZE={os.environ.get('WORLD_SIZE')}): refusing to report a "
+              f"{info.world}-rank number as {args.gpus}", file=sys.stderr, flush=True)
+        D.shutdown(info)
+        return 3
+    comm = D.selfcheck(info)
+    if info.device.type == "cpu":
+        rc = run_cpu(args, info, comm)
+    else:
+        rc = run_gpu(args, info, comm)
+    D.shutdown(info)
+    return rc
+
+
+def metric_and_config(args, info, cfg, prune, prefilter, extra_cfg: dict):
+    headline = (args.model in ("minilm-l6", "minilm", "all-MiniLM-L6-v2") and args.mode == "full"
+                and args.index_rows == 100_000_000 and args.index_dtype == "bf16"
+                and args.encoder_dtype == "bf16" and prefilter is None and args.corpus == "random"
+                and args.queries == "self" and info.device.type == "cuda")
+    short = cfg.model_name.split("/")[-1]
+    rows_txt = f"{args.index_rows / 1e6:g}M" if args.index_rows < 10**9 else f"{args.index_rows / 1e9:g}B"
+    dist_txt = "" if args.corpus == "random" else f", {args.corpus} corpus"
+    metric = METRIC if headline else {
+        "full": f"embeds/sec + top-k QPS, {short} / {rows_txt}x{cfg.hidden} {args.index_dtype} index"
+                + (" (fp8 prefilter + exact bf16 rescore)" if prefilter else "") + dist_txt,
+        "embed": f"embeds/sec, {short} ({cfg.key}) {args.encoder_dtype}, batch {args.batch} x seq {args.seq}",
+        "search": f"top-{args.k} QPS, {rows_txt}x{cfg.hidden} {args.index_dtype} index, "
+                  f"{args.batch} {args.queries} queries/rank"
+                  + (" (fp8 prefilter + exact bf16 rescore)" if prefilter else "") + dist_txt,
+    }[args.mode]
+    config = {
+        "model": short, "global_batch": args.batch * info.world, "seq_len": args.seq,
+        "parallelism": (f"dp{info.world}-rccl-group" if extra_cfg.pop("_group_dp", False)
+                        else f"dp{info.world}+index_shard{info.world}"),
+        "index_rows": args.index_rows, "dim": cfg.hidden, "top_k": args.k, "mode": args.mode,
+        "corpus": args.corpus, "queries": args.queries,
+    }
+    if args.corpus == "clustered":
+        config.update(clusters=args.clusters, cluster_spread=args.cluster_spread)
+    config.update(extra_cfg)
+    unit = (f"embeds/s (whole job; every embedded sentence is also answered as a top-{args.k} "
+            f"query over the {rows_txt} x {cfg.hidden} corpus, so this equals top-k QPS)"
+            if args.mode == "full" else ("embeds/s" if args.mode == "embed" else "queries/s"))
+    return metric, config, unit
+
+
+def result_line(args, info, comm, metric, unit, config, total, ms, prune, prefilter, data, extra):
+    res = {
+        "metric": metric,
+        "value": round(total, 2),
+        "unit": unit,
+        "n_gpus": info.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.encoder_dtype,
+        "index_dtype": args.index_dtype,
+        "index_prefilter": prefilter,
+        "index_search": ("exact: int8 bound-pruned scan + bf16 re-score" if prune
+                         else ("fp8 prefilter + bf16 re-score" if prefilter else "exact bf16 scan")),
+        "data": data,
+        "config": config,
+        "backend": comm["backend"],
+        "world": comm["world"],
+        "comm_check": comm,
+        "embeds_per_sec": round(total, 2) if args.mode != "search" else 0.0,
+        "topk_qps": round(total, 2) if args.mode != "embed" else 0.0,
+        "vs_derived_reference_estimate": (round(total / DERIVED_REF_EMBEDS_PER_SEC, 1)
+                                          if args.mode != "search" else None),
+    }
+    res.update(extra)
+    return json.dumps(res)
+
+
+def _data_txt(args) -> str:
+    rows = {"random": "random unit index rows",
+            "clustered": f"clustered unit index rows ({args.clusters} centers, spread "
+                         f"{args.cluster_spread})",
+            "anisotropic": "anisotropic unit index rows (shared mean direction, power-law spread)"}
+    q = ("" if args.mode == "full" else
+         f", {'held-out draws from the corpus distribution' if args.queries == 'heldout' else 'stored rows'} as queries")
+    return f"synthetic token ids, random-init weights, {rows[args.corpus]}{q}"
+
+
+def run_cpu(args, info, comm) -> int:
+    """The step on the CPU (gloo): encode -> upsert -> sharded search, timed the same way.  For the
+    multi-rank contract tests only (fp32 PyTorch encoder, matmul search)."""
     from codename_symbiont_amd.index.shard import HbmIndexShard
+    from codename_symbiont_amd.index.synth import CorpusGen, fill_corpus
+    from codename_symbiont_amd.models import get_config
+    from codename_symbiont_amd.models.encoder import TorchEncoder, synthetic_batch
+    from codename_symbiont_amd.parallel import dist as D
+    from codename_symbiont_amd.parallel.sharded import ShardedSearcher
+
+    torch.manual_seed(1234 + info.rank)
+    cfg = get_config(args.model)
+    B, S, K, W = args.batch, args.seq, args.steps, args.warmup
+    enc = TorchEncoder(cfg, seed=0)
+    rows_per_rank = args.index_rows // info.world
+    shard = HbmIndexShard(cfg.hidden, rows_per_rank + (K + W + 4) * B, device="cpu")
+    gen = CorpusGen(args.corpus, cfg.hidden, "cpu", clusters=args.clusters,
+                    spread=args.cluster_spread)
+    if args.mode != "embed":
+        fill_corpus(shard, gen, rows_per_rank, seed=100 + info.rank)
+    searcher = ShardedSearcher(shard, info)
+    host = [synthetic_batch(cfg, B, S, seed=1000 * info.rank + i) for i in range(4)]
+    qsets = [gen.unit(B, 5000 + 10 * info.rank + i).bfloat16() for i in range(4)]
+
+    def step(i):
+        q = None
+        if args.mode != "search":
+            _, q = enc.forward_packed(host[i % 4])
+            if args.queries == "self":
+                shard.append_unit(q)
+        else:
+            q = qsets[i % 4] if args.queries == "heldout" else shard.rows[(i * B) % max(1, shard.count - B):][:B]
+        if args.mode != "embed":
+            searcher.search(q, args.k)
+        if args.mode != "search" and args.queries == "heldout":
+            shard.append_unit(q)
+
+    for i in range(W):
+        step(i)
+    D.barrier(info)
+    t0 = time.perf_counter()
+    for j in range(K):
+        step(W + j)
+    D.barrier(info)
+    elapsed = D.allreduce_max(info, time.perf_counter() - t0)
+    ms = elapsed * 1000.0 / K
+    total = B * info.world * K / elapsed
+    metric, config, unit = metric_and_config(args, info, cfg, None, None, {"device": "cpu"})
+    if info.rank == 0:
+        print(result_line(args, info, comm, metric, unit, config, total, ms, None, None,
+                          _data_txt(args) + " (CPU rehearsal: not a performance number)", {}),
+              flush=True)
+    return 0
+
+
+def run_gpu(args, info, comm) -> int:
+    from codename_symbiont_amd.index.shard import HbmIndexShard, resolve_prune
+    from codename_symbiont_amd.index.synth import CorpusGen, fill_corpus
     from codename_symbiont_amd.models import get_config
     from codename_symbiont_amd.models.encoder import HipEncoder, synthetic_batch
     from codename_symbiont_amd.parallel import dist as D
     from codename_symbiont_amd.parallel.sharded import ShardedSearcher
 
-    info = D.init()
-    if info.world != args.gpus:
-        log(info, f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={info.world}")
     dev = info.device
     torch.manual_seed(1234 + info.rank)
     cfg = get_config(args.model)
@@ -125,21 +392,22 @@ def main() -> None:
     rows_per_rank = args.index_rows // info.world
     extra = (K + W + 4) * B
     prefilter = None if args.index_prefilter == "none" else args.index_prefilter
-    from codename_symbiont_amd.index.shard import resolve_prune
 
     # exact either way; i8 applies to 384-wide bf16 shards without a prefilter (else: plain scan)
     prune = resolve_prune("auto" if args.index_prune == "i8" and args.mode != "embed" else "none",
-                          args.index_dtype, cfg.hidden, prefilter)   # (embed mode never searches)
+                          args.index_dtype, cfg.hidden, prefilter, device=dev)
     shard = HbmIndexShard(cfg.hidden, rows_per_rank + extra, device=dev, dtype=args.index_dtype,
                           prefilter=prefilter, prune=prune)
+    gen = CorpusGen(args.corpus, cfg.hidden, dev, clusters=args.clusters,
+                    spread=args.cluster_spread)
     if args.mode != "embed":
-        shard.fill_random(rows_per_rank, seed=100 + info.rank)
+        fill_corpus(shard, gen, rows_per_rank, seed=100 + info.rank)
     searcher = ShardedSearcher(shard, info)
     if prune:
         from codename_symbiont_amd.ops._ext import hip as _hip
 
         _hip().i8_config(args.i8_tile_rows, args.i8_waves)
-    shard.mq_stats = os.environ.get("SYMB_MQ_STATS", "0") not in ("", "0")
+    shard.mq_stats = os.environ.get("SYMB_MQ_STATS", "0") not in ("", "0") or args.mode == "search"
     shard.scan_cus = args.scan_cus
     shard.scan_min_tiles = args.scan_min_tiles
     if args.prepass_min_tiles:
@@ -149,7 +417,8 @@ def main() -> None:
     torch.cuda.synchronize(dev)
     row_bytes = cfg.hidden * (1 if args.index_dtype == "fp8" else 2)
     log(info, f"[bench] setup {time.time() - t0:.1f}s: {cfg.model_name}, shard {rows_per_rank} "
-              f"rows x {cfg.hidden} {args.index_dtype} = {rows_per_rank * row_bytes / 1e9:.1f} GB/rank")
+              f"rows x {cfg.hidden} {args.index_dtype} ({args.corpus}) = "
+              f"{rows_per_rank * row_bytes / 1e9:.1f} GB/rank; comm {comm}")
 
     group_dp = args.mode == "embed" and args.embed_dp == "group" and info.world > 1
     if group_dp:
@@ -187,7 +456,13 @@ def main() -> None:
     from codename_symbiont_amd.utils.gpu_debug import BufferRing
 
     in_ring, out_ring = BufferRing(2, "bench.dbuf"), BufferRing(2, "bench.outs")
-    q_fixed = torch.nn.functional.normalize(torch.randn(B, cfg.hidden, device=dev), dim=-1).bfloat16()
+    # search mode: held-out queries are fresh draws from the corpus distribution (never
+    # inserted); self queries are stored rows (each query's best match is itself)
+    if args.queries == "heldout":
+        qsets = [gen.unit(B, 5000 + 10 * info.rank + i).bfloat16() for i in range(NB)]
+    else:
+        stride = max(1, rows_per_rank // (NB * B))
+        qsets = [shard.rows[torch.arange(B, device=dev) * stride + i].clone() for i in range(NB)]
 
     def prefetch(i: int) -> None:
         slot = i % 2
@@ -263,8 +538,11 @@ def main() -> None:
         if ev:
             ev[2].record(compute)
         q = outs[slot][1]
-        shard.append_unit(q)
+        if args.queries == "self":
+            shard.append_unit(q)
         searcher.search(q, args.k)
+        if args.queries == "heldout":
+            shard.append_unit(q)
         out_ring.consume(slot)
         q_free[slot].record(compute)
         if ev:
@@ -290,15 +568,18 @@ def main() -> None:
             run_encoder(slot, out_f32, out_unit)
             consumed[slot].record(compute)
             prefetch(i + 1)
-            shard.append_unit(out_unit)
+            if args.queries == "self":
+                shard.append_unit(out_unit)
             q = out_unit
         else:
-            q = q_fixed
+            q = qsets[i % NB]
         if ev:
             ev[1].record(compute)
             ev[2].record(compute)
         if args.mode != "embed":
             searcher.search(q, args.k)
+        if args.mode == "full" and args.queries == "heldout":
+            shard.append_unit(q)
         if ev:
             ev[3].record(compute)
 
@@ -310,6 +591,10 @@ def main() -> None:
     torch.cuda.synchronize(dev)
     D.barrier(info)
     torch.cuda.synchronize(dev)
+    if shard._mq_tot is not None:   # count overflows of the timed steps only
+        for t in shard._mq_tot:
+            t.zero_()
+    sampler = ClockSampler(dev.index) if (args.timeline and info.is_root) else None
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(K)]
     t_start = time.perf_counter()
     for j in range(K):
@@ -320,78 +605,73 @@ def main() -> None:
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t_start
     elapsed = D.allreduce_max(info, elapsed)
-    e_ms = sum(a.elapsed_time(b) for a, b, _, _ in evs) / K
-    s_ms = sum(c.elapsed_time(d) for _, _, c, d in evs) / K
+    e_each = [a.elapsed_time(b) for a, b, _, _ in evs]
+    s_each = [c.elapsed_time(d) for _, _, c, d in evs]
+    e_ms, s_ms = sum(e_each) / K, sum(s_each) / K
 
     ms = elapsed * 1000.0 / K
     total = B * info.world * K / elapsed
-    headline = (args.model in ("minilm-l6", "minilm", "all-MiniLM-L6-v2") and args.mode == "full"
-                and args.index_rows == 100_000_000 and args.index_dtype == "bf16"
-                and args.encoder_dtype == "bf16" and prefilter is None)
-    short = cfg.model_name.split("/")[-1]
-    rows_txt = f"{args.index_rows / 1e6:g}M" if args.index_rows < 10**9 else f"{args.index_rows / 1e9:g}B"
-    metric = METRIC if headline else {
-        "full": f"embeds/sec + top-k QPS, {short} / {rows_txt}x{cfg.hidden} {args.index_dtype} index"
-                + (" (fp8 prefilter + exact bf16 rescore)" if prefilter else ""),
-        "embed": f"embeds/sec, {short} ({cfg.key}) {args.encoder_dtype}, batch {B} x seq {S}",
-        "search": f"top-{args.k} QPS, {rows_txt}x{cfg.hidden} {args.index_dtype} index, {B} queries/rank"
-                  + (" (fp8 prefilter + exact bf16 rescore)" if prefilter else ""),
-    }[args.mode]
-    if shard._mq_tot is not None:
-        print(f"[bench] rank {info.rank} emitting-scan searches: {int(shard._mq_tot[0].item())} "
-              f"overflowed, max {int(shard._mq_tot[1].item())} candidates per query "
-              f"(cap {shard.MQ_CAP})", file=sys.stderr, flush=True)
+    extra_out = {
+        "embed_ms_per_step_rank0": round(e_ms, 3),
+        "search_ms_per_step_rank0": round(s_ms, 3),
+        "host_enqueue_ms_per_step_rank0": round(host_ms, 3),
+    }
+    if sampler is not None:
+        clocks = sampler.stop()
+        # step boundaries: the search-end events, relative to the first step's start
+        ends = [evs[0][0].elapsed_time(e[3]) for e in evs]
+        with open(args.timeline, "w") as f:
+            for j in range(K):
+                f.write(json.dumps({"step": j, "end_ms": round(ends[j], 3),
+                                    "embed_ms": round(e_each[j], 3),
+                                    "search_ms": round(s_each[j], 3)}) + "\n")
+            for t, sclk, pw in clocks:
+                f.write(json.dumps({"t": round(t - clocks[0][0], 2) if clocks else 0,
+                                    "sclk_mhz": sclk, "power_w": pw}) + "\n")
+        q = max(1, K // 10)
+        extra_out["step_ms_first_decile"] = round((ends[q - 1]) / q, 3)
+        extra_out["step_ms_last_decile"] = round((ends[-1] - ends[-q - 1]) / q, 3) if K > q else None
+        if clocks:
+            extra_out["sclk_mhz_samples"] = [c[1] for c in clocks][:: max(1, len(clocks) // 20)]
+    if shard._mq_tot is not None and args.mode != "embed":
+        ovf = int(shard._mq_tot[0].item())
+        extra_out["search_overflow_batches"] = ovf
+        extra_out["search_max_candidates"] = int(shard._mq_tot[1].item())
+        extra_out["search_dense_route_batches"] = int(shard._mq_tot[2].item()) if len(shard._mq_tot) > 2 else None
+        print(f"[bench] rank {info.rank} searches: {ovf} overflowed, max "
+              f"{int(shard._mq_tot[1].item())} candidates per query", file=sys.stderr, flush=True)
+    if args.verify and args.mode != "embed":
+        q = qsets[0] if args.mode == "search" else outs[0][1] if overlap else out_unit
+        s1, i1 = searcher.search(q, args.k)
+        prune_saved, shard.prune = shard.prune, None
+        mq_saved, shard.scan_mq = shard.scan_mq, False
+        s2, i2 = searcher.search(q, args.k)          # the seeded full bf16 list scan
+        shard.prune, shard.scan_mq = prune_saved, mq_saved
+        torch.cuda.synchronize(dev)
+        same = bool(torch.equal(i1, i2))
+        extra_out["verify_ids_identical"] = D.allreduce_max(info, 0.0 if same else 1.0) == 0.0
+        extra_out["verify_max_score_diff"] = float((s1 - s2).abs().max().item())
+    metric, config, unit = metric_and_config(args, info, cfg, prune, prefilter, {
+        "_group_dp": group_dp,
+        "encode_search_overlap": overlap,
+        # per-rank scan kernel: the emitting MFMA scan (csrc/hip/index_mq.hip) for >= 256
+        # seeded queries (512 per workgroup at >= 512), else the 256-query list kernel
+        "index_scan": (("int8-pruned-" if prune else "emitting-")
+                       + ("512q" if B * info.world >= 512 else "256q"))
+                      if (shard.scan_mq and args.index_dtype == "bf16" and cfg.hidden == 384
+                          and B * info.world >= shard.mq_min_nq and args.k <= 16)
+                      else "list-256q",
+        "encoder_hipgraph": use_graph,
+        "search_priority": args.search_priority,
+        "scan_min_tiles": args.scan_min_tiles,
+        "prepass_min_tiles": shard.prepass_min_tiles,
+        "prune_sample_shift": shard.PRUNE_TILE_SHIFT if prune else None,
+    })
     if info.rank == 0:
-        res = {
-            "metric": metric,
-            "value": round(total, 2),
-            "unit": f"embeds/s (whole job; every embedded sentence is also answered as a top-{args.k} "
-                    f"query over the {rows_txt} x {cfg.hidden} corpus, so this equals top-k QPS)"
-                    if args.mode == "full" else ("embeds/s" if args.mode == "embed" else "queries/s"),
-            "n_gpus": info.world,
-            "steps": K,
-            "warmup": W,
-            "ms_per_step": round(ms, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": args.encoder_dtype,
-            "index_dtype": args.index_dtype,
-            "index_prefilter": prefilter,
-            "index_search": ("exact: int8 bound-pruned scan + bf16 re-score" if prune
-                             else ("fp8 prefilter + bf16 re-score" if prefilter else "exact bf16 scan")),
-            "data": "synthetic token ids, random-init weights, random unit index rows",
-            "config": {
-                "model": short, "global_batch": B * info.world, "seq_len": S,
-                "parallelism": (f"dp{info.world}-rccl-group" if group_dp
-                                else f"dp{info.world}+index_shard{info.world}"),
-                "index_rows": args.index_rows, "dim": cfg.hidden, "top_k": args.k,
-                "mode": args.mode,
-                "encode_search_overlap": overlap,
-                # per-rank scan kernel: the emitting MFMA scan (csrc/hip/index_mq.hip) for >= 256
-                # seeded queries (512 per workgroup at >= 512), else the 256-query list kernel
-                "index_scan": (("int8-pruned-" if prune else "emitting-")
-                               + ("512q" if B * info.world >= 512 else "256q"))
-                              if (shard.scan_mq and args.index_dtype == "bf16" and cfg.hidden == 384
-                                  and B * info.world >= shard.mq_min_nq and args.k <= 16)
-                              else "list-256q",
-                "encoder_hipgraph": use_graph,
-                "search_priority": args.search_priority,
-                "scan_min_tiles": args.scan_min_tiles,
-                "prepass_min_tiles": shard.prepass_min_tiles,
-                "prune_sample_shift": shard.PRUNE_TILE_SHIFT if prune else None,
-            },
-            "embeds_per_sec": round(total, 2) if args.mode != "search" else 0.0,
-            "topk_qps": round(total, 2) if args.mode != "embed" else 0.0,
-            "embed_ms_per_step_rank0": round(e_ms, 3),
-            "search_ms_per_step_rank0": round(s_ms, 3),
-            "host_enqueue_ms_per_step_rank0": round(host_ms, 3),
-            "vs_derived_reference_estimate": (round(total / DERIVED_REF_EMBEDS_PER_SEC, 1)
-                                              if args.mode != "search" else None),
-        }
-        print(json.dumps(res), flush=True)
-    D.shutdown(info)
+        print(result_line(args, info, comm, metric, unit, config, total, ms, prune, prefilter,
+                          _data_txt(args), extra_out), flush=True)
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

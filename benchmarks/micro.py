@@ -234,6 +234,7 @@ def cmd_scani8abl(a):
     shard.fill_random(a.rows, seed=1)
     q = torch.nn.functional.normalize(torch.randn(a.nq, D, device="cuda"), dim=-1).bfloat16()
     hip().i8_config(a.i8_tr, a.i8_waves)
+    shard.mq_stats = True      # keeps _pruned_last (the scan's inputs and grid)
     shard.search(q, k)
     torch.cuda.synchronize()
     P = shard._pruned_last

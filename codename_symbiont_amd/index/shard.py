@@ -107,13 +107,17 @@ FP8_SCALE = 256.0  # == ops.kernels.FP8_SCALE (kept import-free for CPU-only use
 
 
 def resolve_prune(mode: str | None, dtype: str = "bf16", dim: int = 384,
-                  prefilter: str | None = None) -> str | None:
+                  prefilter: str | None = None, device=None) -> str | None:
     """``SYMB_INDEX_PRUNE``: "auto" (default) = the exact int8-pruned search wherever it applies
-    (384-wide bf16 shards without an fp8 prefilter), "i8" = require it, "" / "none" = plain scan."""
+    (384-wide bf16 shards without an fp8 prefilter, on a GPU), "i8" = require it, "" / "none" =
+    plain scan.  ``device``: the shard's device; "auto" on a CPU shard is None (the CPU backend
+    searches by matmul and would only pay for the int8 image on every write)."""
     mode = (mode or "").strip().lower()
     if mode in ("", "none", "0", "off"):
         return None
     if mode == "auto":
+        if device is not None and torch.device(device).type != "cuda":
+            return None
         return "i8" if (dtype == "bf16" and dim == 384 and not prefilter) else None
     return mode
 FP8_DIMS = (256, 384, 512, 768, 1024)   # row widths the fp8 scan kernel takes
@@ -519,13 +523,22 @@ class HbmIndexShard:
         else:
             self._scan(n, q_unit, kmax, k, thr, n_cus, rows, gate=ovf, out=(out_s, out_i))
         self._mq_last = (cnt, ovf)   # candidate counts / overflow flag (tests, diagnostics)
-        if self.mq_stats:            # running totals (two tiny kernels per search; off by default)
-            if self._mq_tot is None:
-                self._mq_tot = (torch.zeros(1, dtype=torch.int32, device=dev),
-                                torch.zeros(1, dtype=torch.int32, device=dev))
-            self._mq_tot[0].add_(ovf)
-            torch.maximum(self._mq_tot[1], cnt.max().view(1), out=self._mq_tot[1])
+        self._stats(ovf, cnt)
         return out_s, out_i
+
+    def _stats(self, ovf, cnt, dense=None) -> None:
+        """``mq_stats``: running totals on the device (a few tiny kernels per search; off by
+        default) -- batches whose candidates overflowed, the most candidates any query emitted,
+        and pruned searches routed to the bf16 scan by their sample."""
+        if not self.mq_stats:
+            return
+        if self._mq_tot is None:
+            self._mq_tot = tuple(torch.zeros(1, dtype=torch.int32, device=self.device)
+                                 for _ in range(3))
+        self._mq_tot[0].add_(ovf)
+        torch.maximum(self._mq_tot[1], cnt.max().view(1), out=self._mq_tot[1])
+        if dense is not None:
+            self._mq_tot[2].add_(dense)
 
     # pruned search: its exact threshold sample is 1 tile in 2^5.  Sparser samples win the
     # headline (+2-3 % at 2^7) only because its queries' best matches sit in the exact fresh-row
@@ -600,15 +613,10 @@ class HbmIndexShard:
         # overflow (some query had more than cap candidates): the exact bf16 scan, seeded with T
         self._scan(n, q_unit, kmax, k, T.contiguous(), n_cus, gate=ovf, out=(out_s, out_i))
         self._mq_last = (cnt, ovf)
-        # (diagnostics / benchmarks/micro.py scani8abl: the scan's inputs and grid)
-        self._pruned_last = dict(q8=q8, thr=thr, rows_per_blk=rows_per_blk, n_rblk=n_rblk, cap=cap,
-                                 cs=cs, ci=ci, cnt=cnt, q=q_unit)
-        if self.mq_stats:
-            if self._mq_tot is None:
-                self._mq_tot = (torch.zeros(1, dtype=torch.int32, device=dev),
-                                torch.zeros(1, dtype=torch.int32, device=dev))
-            self._mq_tot[0].add_(ovf)
-            torch.maximum(self._mq_tot[1], cnt.max().view(1), out=self._mq_tot[1])
+        if self.mq_stats:   # (diagnostics / benchmarks/micro.py scani8abl: inputs and grid)
+            self._pruned_last = dict(q8=q8, thr=thr, rows_per_blk=rows_per_blk, n_rblk=n_rblk,
+                                     cap=cap, cs=cs, ci=ci, cnt=cnt, q=q_unit)
+        self._stats(ovf, cnt)
         return out_s, out_i
 
     def _prune_thresholds_torch(self, q_unit, pre_s, tail_s, k: int):

@@ -73,6 +73,42 @@ def allreduce_max(info: DistInfo, value: float) -> float:
     return float(t.item())
 
 
+def selfcheck(info: DistInfo, group=None) -> dict:
+    """Startup collective self-check: all_gather of (rank, device index) through the job's real
+    backend (RCCL on GPU boxes), verified on every rank, plus a bf16 all_gather_into_tensor (the
+    query wire format of parallel/sharded.py) whose contents are checked too.  Raises on any
+    mismatch; returns what the benchmark JSON reports (backend, world, devices, round-trip)."""
+    import time
+
+    dev_idx = info.device.index if info.device.type == "cuda" else -1
+    out = {"backend": info.backend, "world": info.world, "devices": [dev_idx]}
+    if info.world == 1:
+        out["collective"] = "none (world 1)"
+        return out
+    mine = torch.tensor([info.rank, dev_idx], dtype=torch.int64, device=info.device)
+    allv = torch.empty(info.world * 2, dtype=torch.int64, device=info.device)
+    t0 = time.perf_counter()
+    dist.all_gather_into_tensor(allv, mine, group=group)
+    got = allv.view(info.world, 2).cpu()
+    dt = time.perf_counter() - t0
+    if got[:, 0].tolist() != list(range(info.world)):
+        raise RuntimeError(f"collective self-check failed: ranks {got[:, 0].tolist()}")
+    devs = got[:, 1].tolist()
+    rehearsal = "SYMB_DEVICE_INDEX" in os.environ
+    if info.device.type == "cuda" and not rehearsal and len(set(devs)) != info.world:
+        raise RuntimeError(f"collective self-check: ranks share a GPU: devices {devs}")
+    wire = torch.bfloat16 if info.backend == "nccl" else torch.float32
+    q = torch.full((4, 8), float(info.rank + 1), dtype=wire, device=info.device)
+    qa = torch.empty(info.world * 4, 8, dtype=wire, device=info.device)
+    dist.all_gather_into_tensor(qa, q, group=group)
+    want = torch.arange(1, info.world + 1, dtype=torch.float32).repeat_interleave(4)
+    if not torch.equal(qa.float().cpu()[:, 0], want):
+        raise RuntimeError("collective self-check: query all_gather returned wrong rows")
+    out.update(devices=devs, collective=f"all_gather ok ({wire})".replace("torch.", ""),
+               first_collective_ms=round(dt * 1e3, 2))
+    return out
+
+
 def shutdown(info: DistInfo) -> None:
     if info.world > 1 and dist.is_initialized():
         dist.destroy_process_group()

@@ -43,7 +43,8 @@ class VectorMemoryService(Service):
                                           prefilter=self.cfg.index_prefilter or None,
                                           prune=resolve_prune(self.cfg.index_prune,
                                                               self.cfg.index_dtype, dim,
-                                                              self.cfg.index_prefilter))
+                                                              self.cfg.index_prefilter,
+                                                              device=self._index_device()))
         if self.cfg.index_fill_random and self.store.count == 0:
             self.store.shard.fill_random(self.cfg.index_fill_random, seed=17)
         self.log.info("[INDEX_SETUP] collection '%s': dim %d, capacity %d, device %s, %d points",
@@ -51,6 +52,12 @@ class VectorMemoryService(Service):
                       self.store.count)
         self.searcher = SearchBatcher(self.store.search, metrics=self.metrics)
         self._inflight: asyncio.Semaphore | None = None
+
+    def _index_device(self) -> str:
+        """Where VectorStore(device=None) puts the shard (FORCE_CPU or no GPU: the CPU)."""
+        import torch
+
+        return "cpu" if self.cfg.force_cpu or not torch.cuda.is_available() else "cuda"
 
     async def setup(self) -> None:
         await self.subscribe_loop(subjects.TEXT_WITH_EMBEDDINGS, self.handle_store)
@@ -269,7 +276,7 @@ def main() -> None:
     group = IndexGroup(info, dim, cfg.index_capacity // info.world + 1, dtype=cfg.index_dtype,
                        prefilter=cfg.index_prefilter or None,
                        prune=resolve_prune(cfg.index_prune, cfg.index_dtype, dim,
-                                           cfg.index_prefilter))
+                                           cfg.index_prefilter, device=info.device))
     group.snapshot_root = cfg.snapshot_dir or None
     # liveness: every rank heart-beats on health.index.<rank>; rank 0 refuses ops while a peer is
     # silent (fast error replies instead of a collective blocked until the RCCL timeout)

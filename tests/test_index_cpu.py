@@ -310,5 +310,8 @@ def test_int8_pruning_bound_holds_and_image_follows_writes():
     margin = q.float().norm(dim=1) * E + eq * X
     assert ((s - s_i8).abs() <= margin[:, None] + 1e-6).all()
     assert resolve_prune("auto", "bf16", 384) == "i8"
+    assert resolve_prune("auto", "bf16", 384, device="cuda") == "i8"
+    # a CPU shard never pays for the int8 image under auto
+    assert resolve_prune("auto", "bf16", 384, device="cpu") is None
     assert resolve_prune("auto", "fp8", 1024) is None and resolve_prune("none") is None
     assert resolve_prune("auto", "bf16", 384, prefilter="fp8") is None
