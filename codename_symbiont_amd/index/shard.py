@@ -320,6 +320,34 @@ class HbmIndexShard:
     def write_f32(self, r0: int, vecs: torch.Tensor) -> None:
         self._store(r0, vecs.to(self.device, torch.float32).contiguous(), normalize=True)
 
+    def write_rows_f32(self, rows, vecs: torch.Tensor) -> None:
+        """Overwrite arbitrary existing rows (an upsert of known point ids) in ONE batched pass:
+        the vectors are normalised and encoded into a scratch block by the same kernels as an
+        append (with their int8 / e4m3 images), then scattered by index_copy_ -- a few launches
+        per batch instead of a write per row.  ``rows`` must be distinct."""
+        idx = torch.as_tensor(rows, dtype=torch.int64).flatten()
+        n = idx.numel()
+        if n == 0:
+            return
+        if vecs.shape[0] != n or vecs.shape[1] != self.dim:
+            raise ValueError(f"write_rows_f32: {n} rows but vectors of shape {tuple(vecs.shape)}")
+        if n == 1 or bool((idx[1:] - idx[:-1] == 1).all()):      # one contiguous range
+            self.write_f32(int(idx[0]), vecs)
+            return
+        if int(idx.min()) < 0 or int(idx.max()) >= self.count:
+            raise IndexError("write_rows_f32: row outside the shard")
+        scratch = HbmIndexShard(self.dim, n, self.device, dtype=self.dtype,
+                                prefilter=self.prefilter, prune=self.prune)
+        scratch.append_f32(vecs)
+        di = idx.to(self.device)
+        self.rows.index_copy_(0, di, scratch.rows[:n])
+        if self.rows8 is not None:
+            self.rows8.index_copy_(0, di, scratch.rows8[:n])
+        if self.rows_i8 is not None:
+            self.rows_i8.index_copy_(0, di, scratch.rows_i8[:n])
+            self.sx_i8.index_copy_(0, di, scratch.sx_i8[:n])
+            torch.maximum(self.i8_bounds, scratch.i8_bounds, out=self.i8_bounds)
+
     def upsert(self, point_ids: list[str], vecs: torch.Tensor, payloads: list[Payload]) -> list[int]:
         """Qdrant-style upsert: existing ids are overwritten in place, new ids appended.  An id
         repeated inside one batch is one point and its last occurrence wins (Qdrant semantics);
@@ -333,10 +361,11 @@ class HbmIndexShard:
             r0 = self.append_f32(vecs[new_pos])
             for j, i in enumerate(new_pos):
                 row_of[point_ids[i]] = r0 + j
-        for i in old_pos:
-            r = id_to_row[point_ids[i]]
-            self.write_f32(r, vecs[i:i + 1])
-            row_of[point_ids[i]] = r
+        if old_pos:
+            rows = [id_to_row[point_ids[i]] for i in old_pos]
+            self.write_rows_f32(rows, vecs[old_pos])
+            for i, r in zip(old_pos, rows):
+                row_of[point_ids[i]] = r
         for i in pos:
             self.payloads.set(row_of[point_ids[i]], point_ids[i], payloads[i])
         self.publish()
@@ -486,12 +515,18 @@ class HbmIndexShard:
         return m, buf
 
     def _scan_mq(self, n: int, q_unit: torch.Tensor, kmax: int, k: int, thr, n_cus, rows=None,
-                 tshift: int = 0):
+                 tshift: int = 0, gate=None, out=None, fallback: bool = True, cand: bool = False,
+                 cap: int | None = None):
         """512-query-per-workgroup scan emitting every score above ``thr`` (index_mq.hip), top-k
         of each query's candidates, and the exact 256-query kernel as a fallback that runs on the
         GPU only if some query's candidate buffer overflowed (a device flag gates it).
         ``tshift`` > 0: ``n`` virtual rows of the in-place 1-in-2^tshift tile sample; its
-        fallback scans every row (the exact top-k of all rows is a valid threshold too)."""
+        fallback scans every row (the exact top-k of all rows is a valid threshold too).
+        ``gate`` (int32 device flag): the scan and its select run only if it is non-zero (they
+        then write ``out`` and OR into its overflow flag, ``out[2]``).  ``fallback=False``: no
+        overflow re-scan -- for a threshold sample that is still sound, since the top-k of ANY
+        subset of real rows lower-bounds the k-th best.  ``cand``: also return the candidate
+        buffers (scores, count) for the route estimate of _search_pruned."""
         from ..ops._ext import hip, stream_handle
 
         h = hip()
@@ -505,25 +540,32 @@ class HbmIndexShard:
         rows_per_blk = _round_up(max(1, math.ceil(n / n_rblk)), TILE_ROWS)
         n_rblk = max(1, math.ceil(n / rows_per_blk))
         rows = self.rows if rows is None else rows
-        cap, dev = self.MQ_CAP, self.device
+        cap, dev = cap or self.MQ_CAP, self.device
         cs = torch.empty(NQ, cap, device=dev)
         ci = torch.empty(NQ, cap, dtype=torch.int32, device=dev)
         cnt = torch.empty(NQ, dtype=torch.int32, device=dev)
-        ovf = torch.empty(1, dtype=torch.int32, device=dev)
-        out_s = torch.empty(NQ, k, device=dev)
-        out_i = torch.empty(NQ, k, dtype=torch.int32, device=dev)
+        if out is None:
+            out = (torch.empty(NQ, k, device=dev), torch.empty(NQ, k, dtype=torch.int32, device=dev),
+                   torch.empty(1, dtype=torch.int32, device=dev))
+        out_s, out_i, ovf = out
         st = stream_handle(dev)
+        gp = 0 if gate is None else gate.data_ptr()
         h.index_scan_mq(rows.data_ptr(), n, rows_per_blk, n_rblk, q_unit.data_ptr(), NQ,
                         thr.data_ptr(), cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(), cap,
-                        self.scan_xcd, st, sets, tshift, rsplit)
+                        self.scan_xcd, st, sets, tshift, rsplit, gp)
         h.topk_select_counted(cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(), cap, NQ, kmax, k,
-                              out_s.data_ptr(), out_i.data_ptr(), ovf.data_ptr(), st)
-        if tshift:
-            self._scan(self.visible, q_unit, kmax, k, thr, n_cus, gate=ovf, out=(out_s, out_i))
-        else:
-            self._scan(n, q_unit, kmax, k, thr, n_cus, rows, gate=ovf, out=(out_s, out_i))
+                              out_s.data_ptr(), out_i.data_ptr(), ovf.data_ptr(), st, gate=gp,
+                              reset_ovf=gate is None)
+        if gate is None and fallback:
+            if tshift:
+                self._scan(self.visible, q_unit, kmax, k, thr, n_cus, gate=ovf, out=(out_s, out_i))
+            else:
+                self._scan(n, q_unit, kmax, k, thr, n_cus, rows, gate=ovf, out=(out_s, out_i))
         self._mq_last = (cnt, ovf)   # candidate counts / overflow flag (tests, diagnostics)
-        self._stats(ovf, cnt)
+        if gate is None and fallback:   # (a sample's overflow only steers the route)
+            self._stats(ovf, cnt)
+        if cand:
+            return out_s, out_i, cs, cnt
         return out_s, out_i
 
     def _stats(self, ovf, cnt, dense=None) -> None:
@@ -549,13 +591,29 @@ class HbmIndexShard:
     # PRUNE_MIN_SHIFT.
     PRUNE_TILE_SHIFT = 5
     PRUNE_MIN_SHIFT = 5
-    PRUNE_CAP = 8192          # candidate slots per query (expected ~1-2k at 100M x 384)
+    # candidate slots per query: ~1-2k expected at 100M x 384 on random data, but the busiest of
+    # 256 held-out queries emitted 6k (profiles/r3_real/); slots cost memory only (the re-score
+    # and select walk the emitted count), 256 MiB at 1024 queries
+    PRUNE_CAP = 32768
+    SAMPLE_CAP = 16384        # the pruned search's sample emits down to thr0 - margin
+
+    # route the batch to the bf16 emitting scan when the sample predicts more than this share of
+    # PRUNE_CAP int8 candidates for some query (estimate c << ts has a ~sqrt(c) << ts spread)
+    PRUNE_DENSE_FRAC = 0.6
+    prune_route = True   # False: always take the int8 pass (tests of the overflow fallback)
 
     def _search_pruned(self, q_unit, k: int, n_cus):
         """EXACT top-k through the int8 image (index_i8.hip has the bound): an exact bf16 sample
         gives T <= each query's final k-th score; every row whose int8 score reaches T - margin is
         emitted, re-scored in bf16 and the top-k of those is returned.  A query whose candidates
-        overflow PRUNE_CAP raises the flag that gates the exact bf16 list scan."""
+        overflow PRUNE_CAP raises the flag that gates the exact bf16 list scan.
+
+        Route (decided on the GPU from the same sample, no host sync): the sample is emitted down
+        to thr0 - margin, so counting its rows at or above T - margin estimates each query's int8
+        candidates.  On data whose scores crowd the k-th best (an anisotropic corpus: every pair
+        of rows at cosine ~0.3) that estimate exceeds the buffer, and the batch takes the bf16
+        emitting scan with the exact threshold T instead of an int8 pass that would overflow and
+        then pay the full fallback scan on top (profiles/r3_real/)."""
         from ..ops._ext import hip, stream_handle
 
         n, NQ, kmax = self.visible, q_unit.shape[0], 16
@@ -566,28 +624,40 @@ class HbmIndexShard:
             return None
         if n_cus is None:
             n_cus = self._n_cus()
+        h, dev, cap = hip(), self.device, self.PRUNE_CAP
+        st = stream_handle(dev)
+        # 0. the int8 queries and each query's bound margin |q| E + |q - q~| X (prune_qquant)
+        q8 = torch.empty(NQ, self.dim, dtype=torch.int8, device=dev)
+        sq = torch.empty(NQ, dtype=torch.float32, device=dev)
+        margin = torch.empty(NQ, dtype=torch.float32, device=dev)
+        h.prune_qquant(q_unit.data_ptr(), NQ, self.dim, self.i8_bounds.data_ptr(), q8.data_ptr(),
+                       sq.data_ptr(), margin.data_ptr(), st)
         # 1. T: the k-th best exact score of a sample of real rows (1 tile in 2^ts, plus the last
-        #    4096+ rows where fresh inserts sit), as in _search_scan
+        #    4096+ rows where fresh inserts sit), as in _search_scan; the sample emits down to
+        #    thr0 - margin so that it also counts the rows inside the int8 band
         ts, nv, t0, idx = plan
         sub = torch.index_select(self.rows, 0, idx)
         pm = self.prepass_min_tiles
         s0, _ = self._scan(sub.shape[0], q_unit, kmax, k, None, n_cus, sub, "bf16", min_tiles=pm)
         thr0 = s0[:, k - 1].contiguous() - self.MQ_THR_MARGIN
-        pre_s, _ = self._scan_mq(nv * TILE_ROWS, q_unit, kmax, k, thr0, n_cus, tshift=ts)
+        thr_band = (thr0 - margin).contiguous()
+        pre_s, _, cs_p, cnt_p = self._scan_mq(nv * TILE_ROWS, q_unit, kmax, k, thr_band, n_cus,
+                                              tshift=ts, fallback=False, cand=True,
+                                              cap=self.SAMPLE_CAP)
         tail_s, _ = self._scan(n - t0, q_unit, kmax, k, thr0, n_cus, self.rows[t0:], "bf16",
                                min_tiles=pm)
-        # 2. T (k-th best of the union), the int8 queries and the per-query emission threshold
-        #    (T - |q| E - |q - q~| X - fp32 slack) / sq, in one launch (prune_qprep; the torch
-        #    composition it replaces is _prune_thresholds_torch, kept as the test oracle)
-        h, dev, cap = hip(), self.device, self.PRUNE_CAP
-        q8 = torch.empty(NQ, self.dim, dtype=torch.int8, device=dev)
-        sq = torch.empty(NQ, dtype=torch.float32, device=dev)
+        # 2. T (k-th best of the union), the per-query emission threshold (T - margin) / sq and
+        #    the route flag, in one launch (prune_route)
         T = torch.empty(NQ, dtype=torch.float32, device=dev)
         thr = torch.empty(NQ, dtype=torch.float32, device=dev)
-        h.prune_qprep(q_unit.data_ptr(), NQ, self.dim, pre_s.data_ptr(), tail_s.data_ptr(), k,
-                      self.MQ_THR_MARGIN, self.i8_bounds.data_ptr(), q8.data_ptr(), sq.data_ptr(),
-                      T.data_ptr(), thr.data_ptr(), stream_handle(dev))
-        # 3. emit every row with (q8 . x8) * sx >= thr, 4. exact bf16 re-score, 5. top-k
+        dense = torch.empty(1, dtype=torch.int32, device=dev)
+        limit = int(self.PRUNE_DENSE_FRAC * cap) if self.prune_route else 1 << 62
+        h.prune_route(NQ, pre_s.data_ptr(), tail_s.data_ptr(), k, self.MQ_THR_MARGIN,
+                      sq.data_ptr(), margin.data_ptr(), cs_p.data_ptr(), cnt_p.data_ptr(),
+                      self.SAMPLE_CAP, ts, limit, T.data_ptr(), thr.data_ptr(), dense.data_ptr(),
+                      st)
+        # 3. int8 route: emit every row with (q8 . x8) * sx >= thr, 4. exact bf16 re-score,
+        #    5. top-k (skipped on the device when dense: counts stay 0, the select writes -inf)
         rsplit = 2 if (NQ < 512 or self.i8_rsplit2) else 1
         tr = h.i8_tile_rows()
         n_qblk = math.ceil(NQ / h.i8_queries_per_blk(rsplit))
@@ -601,22 +671,27 @@ class HbmIndexShard:
         ovf = torch.empty(1, dtype=torch.int32, device=dev)
         out_s = torch.empty(NQ, k, device=dev)
         out_i = torch.empty(NQ, k, dtype=torch.int32, device=dev)
-        st = stream_handle(dev)
         h.index_scan_i8(self.rows_i8.data_ptr(), self.sx_i8.data_ptr(), n, self.rows_i8.shape[0],
                         rows_per_blk, n_rblk,
                         q8.data_ptr(), NQ, thr.data_ptr(), cs.data_ptr(), ci.data_ptr(),
-                        cnt.data_ptr(), cap, self.scan_xcd, st, rsplit)
+                        cnt.data_ptr(), cap, self.scan_xcd, st, rsplit, skip=dense.data_ptr())
         h.rescore_bf16(self.rows.data_ptr(), q_unit.data_ptr(), NQ, self.dim, ci.data_ptr(),
                        cnt.data_ptr(), cap, cs.data_ptr(), st)
         h.topk_select_counted(cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(), cap, NQ, kmax, k,
                               out_s.data_ptr(), out_i.data_ptr(), ovf.data_ptr(), st)
+        i8_cnt = cnt
+        # 3'. bf16 route (gated on dense): the emitting scan at the exact threshold T; its select
+        #     ORs into ovf
+        if self.prune_route:
+            self._scan_mq(n, q_unit, kmax, k, T, n_cus, gate=dense, out=(out_s, out_i, ovf))
         # overflow (some query had more than cap candidates): the exact bf16 scan, seeded with T
         self._scan(n, q_unit, kmax, k, T.contiguous(), n_cus, gate=ovf, out=(out_s, out_i))
-        self._mq_last = (cnt, ovf)
+        self._mq_last = (i8_cnt, ovf)
+        self._route_last = dense
         if self.mq_stats:   # (diagnostics / benchmarks/micro.py scani8abl: inputs and grid)
             self._pruned_last = dict(q8=q8, thr=thr, rows_per_blk=rows_per_blk, n_rblk=n_rblk,
                                      cap=cap, cs=cs, ci=ci, cnt=cnt, q=q_unit)
-        self._stats(ovf, cnt)
+        self._stats(ovf, i8_cnt, dense)
         return out_s, out_i
 
     def _prune_thresholds_torch(self, q_unit, pre_s, tail_s, k: int):

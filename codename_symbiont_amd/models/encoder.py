@@ -84,6 +84,21 @@ def synthetic_batch(cfg: EncoderConfig, batch: int, seq_len: int, seed: int = 0,
     return pack_token_ids(toks, cfg)
 
 
+def refill_synthetic(b: PackedBatch, cfg: EncoderConfig, seed: int) -> PackedBatch:
+    """Fresh random token ids IN PLACE (same lengths, positions and framing): a benchmark feeds
+    every step a batch it has never seen, so the sentences it ingests are never exact repeats of
+    earlier ones (a rotating set of a few batches would re-insert identical rows every few steps).
+    ``b`` must live on the host (pinned or not)."""
+    rng = np.random.default_rng(seed)
+    ids = b.ids.numpy()
+    cu = b.cu_seqlens.numpy()
+    ids[:] = rng.integers(1000, cfg.vocab_size, size=ids.shape[0], dtype=np.int32)
+    cls, sep = (101, 102) if cfg.vocab_size > 30000 and cfg.pad_token_id == 0 else (0, 2)
+    ids[cu[:-1]] = cls
+    ids[cu[1:] - 1] = sep
+    return b
+
+
 def quant_weight_fp8(w: torch.Tensor):
     """[N, K] weights -> (e4m3 bytes [N, K], per-output-channel scale f32 [N]); w ~= q * s."""
     wf = w.float()

@@ -33,10 +33,13 @@ def env_world() -> tuple[int, int, int]:
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
-def init(backend: str | None = None, device_type: str | None = None) -> DistInfo:
+def init(backend: str | None = None, device_type: str | None = None,
+         single_rank_group: bool = False) -> DistInfo:
     """Rehearsal knobs (one-GPU boxes; never set for real runs): ``SYMB_DIST_BACKEND=gloo`` and
     ``SYMB_DEVICE_INDEX=0`` put every rank of a multi-rank job on one device over gloo, since RCCL
-    refuses two ranks on one GPU (tests/test_parallel_gpu.py, benchmarks/gpu_bench_rehearsal.sh)."""
+    refuses two ranks on one GPU (tests/test_parallel_gpu.py, benchmarks/gpu_bench_rehearsal.sh).
+    ``single_rank_group``: create the process group even for a world of 1, so a one-GPU box runs
+    the real RCCL calls of the collective paths (tests/test_rccl_gpu.py)."""
     rank, world, local = env_world()
     use_gpu = torch.cuda.is_available() if device_type is None else device_type == "cuda"
     if use_gpu:
@@ -46,7 +49,7 @@ def init(backend: str | None = None, device_type: str | None = None) -> DistInfo
     else:
         device = torch.device("cpu")
     backend = backend or os.environ.get("SYMB_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or single_rank_group) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29512")
         kw = {"device_id": device} if backend == "nccl" else {}
@@ -54,11 +57,12 @@ def init(backend: str | None = None, device_type: str | None = None) -> DistInfo
         # survivors -- the search handler then replies with error_message -- instead of a hang
         timeout = timedelta(seconds=float(os.environ.get("SYMB_COLLECTIVE_TIMEOUT_S", "300")))
         dist.init_process_group(backend=backend, rank=rank, world_size=world, timeout=timeout, **kw)
-    return DistInfo(rank, world, local, device, backend if world > 1 else "none")
+    grouped = world > 1 or single_rank_group
+    return DistInfo(rank, world, local, device, backend if grouped else "none")
 
 
 def barrier(info: DistInfo) -> None:
-    if info.world > 1:
+    if info.world > 1 or (info.backend != "none" and dist.is_initialized()):
         if info.backend == "nccl":
             dist.barrier(device_ids=[info.device.index])
         else:
@@ -82,7 +86,7 @@ def selfcheck(info: DistInfo, group=None) -> dict:
 
     dev_idx = info.device.index if info.device.type == "cuda" else -1
     out = {"backend": info.backend, "world": info.world, "devices": [dev_idx]}
-    if info.world == 1:
+    if info.backend == "none":
         out["collective"] = "none (world 1)"
         return out
     mine = torch.tensor([info.rank, dev_idx], dtype=torch.int64, device=info.device)
@@ -110,5 +114,5 @@ def selfcheck(info: DistInfo, group=None) -> dict:
 
 
 def shutdown(info: DistInfo) -> None:
-    if info.world > 1 and dist.is_initialized():
+    if info.backend != "none" and dist.is_initialized():
         dist.destroy_process_group()

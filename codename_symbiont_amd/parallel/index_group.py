@@ -4,8 +4,12 @@ Process model (one process per GPU): rank 0 hosts vector_memory_service (NATS, p
 ranks 1..N-1 run ``serve()``, a loop that executes the operations rank 0 broadcasts.  Every op is
 a short, fixed sequence of collectives, so all ranks stay in lockstep:
 
-  SEARCH : header -> broadcast queries [nq, D] -> every rank: fused MFMA scan of ITS shard ->
-           all_gather of the per-rank top-k (f32 scores, i64 global ids) -> rank 0 merges.
+  SEARCH : header -> broadcast queries [nq, D] (bf16 over RCCL) -> every rank: fused MFMA scan
+           of ITS shard -> ONE all_gather_into_tensor of the per-rank top-k packed as f64
+           (score, global id) pairs -> rank 0 merges on the GPU.  Three collectives per search
+           (counted in ``comm_stats``); rank 0's op lock covers only their ENQUEUE, so the
+           header / query broadcast / scan of search i+1 queue behind search i's exchange while
+           the caller of search i waits for its result outside the lock.
   UPSERT : header -> broadcast vectors [n, D] f32 + (owner rank, target row) -> owners write rows.
   SNAPSHOT / LOAD : header -> every rank saves / loads its own shard under <dir>/rank<r>/ (raw rows,
            index/persist.py format); rank 0 adds group.json (world, per-rank counts) and the
@@ -62,6 +66,13 @@ class IndexGroup:
         self.shard = HbmIndexShard(dim, capacity_per_rank, dev, dtype=dtype, prefilter=prefilter,
                                    prune=prune)
         self.comm_device = dev if info.backend == "nccl" else torch.device("cpu")
+        # query wire format: bf16 over RCCL (half the bytes), f32 over gloo (no bf16 collectives
+        # on every gloo build)
+        self.wire_dtype = torch.bfloat16 if info.backend == "nccl" else torch.float32
+        # a single-rank process group still runs every collective (RCCL tests on one GPU)
+        self.collective = info.world > 1 or info.backend != "none"
+        # per-op collective accounting: {op: [ops, collectives, bytes this rank sent]}
+        self.comm_stats: dict[str, list[int]] = {}
         # rank-0 bookkeeping; ops may arrive from several executor threads, but the collective
         # sequence of one op must never interleave with another's
         self._op_lock = threading.Lock()
@@ -79,13 +90,23 @@ class IndexGroup:
 
     # ------------------------------------------------------------------ plumbing
     def _bcast(self, t: torch.Tensor) -> torch.Tensor:
-        if self.info.world > 1:
+        if self.collective:
             dist.broadcast(t, src=0, group=self.group)
         return t
 
     def _header(self, op: int, a: int = 0, b: int = 0) -> torch.Tensor:
-        h = torch.tensor([op, a, b, 0], dtype=torch.int64, device=self.comm_device)
+        # pinned + non_blocking: building the header on the GPU must not wait for the stream
+        # (a pageable H2D copy would block the host until the previous search had finished)
+        h = torch.tensor([op, a, b, 0], dtype=torch.int64)
+        if self.comm_device.type == "cuda":
+            h = h.pin_memory().to(self.comm_device, non_blocking=True)
         return self._bcast(h)
+
+    def _count(self, op: str, collectives: int, nbytes: int) -> None:
+        c = self.comm_stats.setdefault(op, [0, 0, 0])
+        c[0] += 1
+        c[1] += collectives
+        c[2] += nbytes
 
     @property
     def count(self) -> int:
@@ -93,31 +114,36 @@ class IndexGroup:
 
     # ------------------------------------------------------------------ ops (collective bodies)
     def _do_search(self, q: torch.Tensor, k: int):
+        """Local scan + the packed exchange; returns the merged top-k on the shard's device
+        (rank 0's result; other ranks discard it)."""
         info = self.info
         s, r = self.shard.search(q.to(self.shard.device, torch.bfloat16), k)
         gid = encode_gid(info.rank, r.to(torch.int64))
-        s = s.to(self.comm_device).contiguous()
-        gid = gid.to(self.comm_device).contiguous()
-        if info.world == 1:
+        if not self.collective:
             return s, gid
-        s_all = [torch.empty_like(s) for _ in range(info.world)]
-        g_all = [torch.empty_like(gid) for _ in range(info.world)]
-        dist.all_gather(s_all, s, group=self.group)
-        dist.all_gather(g_all, gid, group=self.group)
-        return merge_ranked(torch.stack(s_all), torch.stack(g_all), k)
+        # one collective: (score, gid) as f64 pairs -- f32 scores and gids < 2^53 are exact
+        packed = torch.stack([s.double(), gid.double()], dim=-1).to(self.comm_device).contiguous()
+        nq = packed.shape[0]
+        allp = torch.empty((info.world * nq,) + tuple(packed.shape[1:]), dtype=packed.dtype,
+                           device=self.comm_device)
+        dist.all_gather_into_tensor(allp, packed, group=self.group)
+        allp = allp.view(info.world, nq, k, 2).to(self.shard.device, non_blocking=True)
+        return merge_ranked(allp[..., 0].float(), allp[..., 1].long(), k)
 
     def _do_upsert(self, vecs: torch.Tensor, owner: torch.Tensor, target: torch.Tensor) -> None:
+        """This rank's share of an upsert: new rows appended in one call, overwrites written in
+        one batched scatter (HbmIndexShard.write_rows_f32)."""
         mine = (owner == self.info.rank).nonzero().flatten()
         if mine.numel() == 0:
             return
         v = vecs[mine].to(self.shard.device, torch.float32)
-        tg = target[mine].tolist()
-        new = [i for i, t in enumerate(tg) if t < 0]
-        if new:
-            self.shard.append_f32(v[new])
-        for i, t in enumerate(tg):
-            if t >= 0:
-                self.shard.write_f32(int(t), v[i:i + 1])
+        tg = target[mine]
+        new = (tg < 0).nonzero().flatten()
+        old = (tg >= 0).nonzero().flatten()
+        if new.numel():
+            self.shard.append_f32(v[new.to(v.device)])
+        if old.numel():
+            self.shard.write_rows_f32(tg[old].cpu(), v[old.to(v.device)])
 
     def _rank_dir(self, directory: str) -> str:
         return os.path.join(directory, f"rank{self.info.rank}")
@@ -240,10 +266,15 @@ class IndexGroup:
             s, r = self.shard.search(q_unit.to(self.shard.device, torch.bfloat16), k)
             raise PartialSearchError(f"{e}; partial results from index rank 0 only", s,
                                      encode_gid(0, r.to(torch.int64))) from None
-        with self._op_lock:
+        with self._op_lock:   # enqueue only: the caller's D2H of the result waits outside it
             self._header(OP_SEARCH, nq, k)
-            q = self._bcast(q_unit.to(self.comm_device, torch.float32).contiguous())
-            return self._do_search(q, k)
+            q = self._bcast(q_unit.to(self.comm_device, self.wire_dtype).contiguous())
+            out = self._do_search(q, k)
+        W, nc = self.info.world, 3 if self.collective else 0
+        nbytes = 32 + q.numel() * q.element_size() + (W * nq * k * 16 if nc else 0)
+        self._count("search", nc, nbytes)
+        log.debug("[INDEX_GROUP] search nq=%d k=%d: %d collectives, %d bytes", nq, k, nc, nbytes)
+        return out
 
     def upsert(self, point_ids: list[str], vecs: torch.Tensor, payloads: list[Payload]) -> list[int]:
         assert self.info.is_root
@@ -305,7 +336,7 @@ class IndexGroup:
         if op == OP_STOP:
             return False
         if op == OP_SEARCH:
-            q = self._bcast(torch.empty(a, self.dim, dtype=torch.float32, device=self.comm_device))
+            q = self._bcast(torch.empty(a, self.dim, dtype=self.wire_dtype, device=self.comm_device))
             self._do_search(q, b)
         elif op == OP_UPSERT:
             v = self._bcast(torch.empty(a, self.dim, dtype=torch.float32, device=self.comm_device))

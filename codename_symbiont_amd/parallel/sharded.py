@@ -39,12 +39,14 @@ class ShardedSearcher:
         self.group = group
         # gloo has no bf16 collectives on every build: ship queries as f32 there
         self.wire_dtype = torch.bfloat16 if info.backend == "nccl" else torch.float32
+        # a single-rank process group still runs the collective path (RCCL tests on one GPU)
+        self.collective = info.world > 1 or info.backend != "none"
 
     def search(self, q_local: torch.Tensor, k: int):
         """Every rank calls this collectively with its own [nq, D] unit queries (same nq on all
         ranks).  Returns (scores f32 [nq, k], global ids int64 [nq, k]) for the LOCAL queries."""
         info = self.info
-        if info.world == 1:
+        if not self.collective:
             s, r = self.shard.search(q_local, k)
             return s, encode_gid(0, r)
         nq, D = q_local.shape

@@ -163,9 +163,100 @@ def _load_tokenizer_json(path: str):
     raise ValueError(f"unsupported tokenizer model {m['type']!r} in {path}")
 
 
+def build_normalizer(spec):
+    """tokenizer.json ``normalizer`` section -> str -> str (None: no normalizer).
+
+    Sequence / Precompiled (native: csrc/native/spm_norm.cpp) / Replace (string or regex) /
+    Strip / NFC / NFD / NFKC / NFKD / Lowercase / StripAccents / Prepend, applied in file order as
+    the tokenizers crate does (the reference's tokenizer, embedding_generator.rs:25-58).
+    BertNormalizer is the WordPiece front-end's own job (csrc/native/text.cpp) and maps to None
+    here (its lowercase flag is read by ``bert_normalizer_flags``)."""
+    import base64
+    import re
+
+    if spec is None:
+        return None
+    t = spec["type"]
+    if t == "Sequence":
+        steps = [f for f in (build_normalizer(x) for x in spec["normalizers"]) if f is not None]
+        if not steps:
+            return None
+
+        def seq(text: str) -> str:
+            for f in steps:
+                text = f(text)
+            return text
+        return seq
+    if t == "Precompiled":
+        pc = native().Precompiled(base64.b64decode(spec["precompiled_charsmap"] or ""))
+        return pc.normalize
+    if t == "Replace":
+        pat, content = spec["pattern"], spec["content"]
+        if "String" in pat:
+            lit = pat["String"]
+            return lambda text: text.replace(lit, content)
+        rx = re.compile(pat["Regex"])
+        return lambda text: rx.sub(lambda _m: content, text)
+    if t == "Strip":
+        left, right = spec.get("strip_left", False), spec.get("strip_right", True)
+
+        def strip(text: str) -> str:
+            if left:
+                text = text.lstrip()
+            return text.rstrip() if right else text
+        return strip
+    if t in ("NFC", "NFD", "NFKC", "NFKD"):
+        return lambda text: unicodedata.normalize(t, text)
+    if t == "Lowercase":
+        return str.lower
+    if t == "StripAccents":
+        return lambda text: "".join(c for c in unicodedata.normalize("NFD", text)
+                                    if unicodedata.category(c) != "Mn")
+    if t == "Prepend":
+        pre = spec["prepend"]
+        return lambda text: pre + text if text else text
+    if t == "BertNormalizer":
+        return None
+    raise ValueError(f"unsupported tokenizer.json normalizer {t!r}")
+
+
+def metaspace_options(spec):
+    """tokenizer.json ``pre_tokenizer`` -> (replacement, prepend 0/1/2, split) of its Metaspace
+    (inside a Sequence too), or None when it has none."""
+    if spec is None:
+        return None
+    if spec["type"] == "Sequence":
+        for x in spec["pretokenizers"]:
+            o = metaspace_options(x)
+            if o is not None:
+                return o
+        return None
+    if spec["type"] != "Metaspace":
+        return None
+    scheme = spec.get("prepend_scheme")
+    if scheme is None:
+        scheme = "always" if spec.get("add_prefix_space", True) else "never"
+    return (spec.get("replacement", META), {"never": 0, "always": 1, "first": 2}[scheme],
+            bool(spec.get("split", True)))
+
+
+def bert_normalizer_flags(spec):
+    """lowercase flag of a BertNormalizer (inside a Sequence too), or None."""
+    if spec is None:
+        return None
+    if spec["type"] == "Sequence":
+        for x in spec["normalizers"]:
+            o = bert_normalizer_flags(x)
+            if o is not None:
+                return o
+        return None
+    return bool(spec.get("lowercase", True)) if spec["type"] == "BertNormalizer" else None
+
+
 class Tokenizer:
     """Native tokenizer front-end for an encoder family: BERT BasicTokenizer + WordPiece, or (XLM-R
-    family) NFKC + Metaspace + SentencePiece-Unigram Viterbi.  Sources, in order: ``vocab_file``
+    family) the tokenizer.json normalizer (SentencePiece Precompiled charsmap, Replace, ...; NFKC
+    for the synthetic vocabulary) + Metaspace + SentencePiece-Unigram Viterbi.  Sources, in order: ``vocab_file``
     argument / ``SYMB_TOKENIZER`` (a HF tokenizer.json) / ``SYMB_VOCAB`` (a BERT vocab.txt) / the
     model's local HF snapshot (models/hub.py), else the deterministic synthetic vocabulary of the
     family (real special-token layout and size)."""
@@ -183,13 +274,26 @@ class Tokenizer:
                     or tokenizer_file(cfg))
         pieces = scores = None
         unk_id = 3
+        # the tokenizer.json's own normalizer / Metaspace (None: the built-in XLM-R defaults)
+        self._pipeline = None
+        meta = None
+        lower = cfg.lowercase
+        self._from_json = path.endswith(".json")
         if path.endswith(".json"):
+            import json
+
             loaded = _load_tokenizer_json(path)
             self.kind = loaded[0]
             if self.kind == "unigram":
                 _, pieces, scores, unk_id = loaded
             else:
                 pieces = loaded[1]
+            with open(path, encoding="utf-8") as f:
+                full = json.load(f)
+            self._pipeline = build_normalizer(full.get("normalizer"))
+            meta = metaspace_options(full.get("pre_tokenizer"))
+            bl = bert_normalizer_flags(full.get("normalizer"))
+            lower = lower if bl is None else bl
         elif path:
             with open(path, encoding="utf-8") as f:
                 pieces = [line.rstrip("\n") for line in f]
@@ -202,11 +306,14 @@ class Tokenizer:
             if sp["cls"] not in ids or sp["sep"] not in ids:
                 raise ValueError("vocabulary lacks the special tokens of " + cfg.key)
             self._tk = native().Unigram(pieces, scores, unk_id, ids[sp["cls"]], ids[sp["sep"]])
+            if self._from_json:   # the file's normalizer already ran: Metaspace only
+                rep, pre, split = meta or (META, 1, True)
+                self._tk.set_pretokenizer(False, rep, pre, split)
         else:
             if pieces is None:
                 pieces = list(synthetic_vocab(cfg.vocab_size, "bert", cased=not cfg.lowercase))
             self.vocab = pieces
-            self._tk = native().WordPiece(pieces, cfg.lowercase, sp["unk"], sp["cls"], sp["sep"], 100)
+            self._tk = native().WordPiece(pieces, lower, sp["unk"], sp["cls"], sp["sep"], 100)
             if self._tk.unk_id < 0 or self._tk.cls_id < 0 or self._tk.sep_id < 0:
                 raise ValueError("vocabulary lacks the special tokens of " + cfg.key)
 
@@ -214,7 +321,13 @@ class Tokenizer:
         return len(self.vocab)
 
     def _norm(self, text: str) -> str:
-        # XLM-R's precompiled SentencePiece charsmap is an NFKC variant; WordPiece normalises in C++
+        """A tokenizer.json's own normalizer pipeline (Precompiled charsmap in C++, ...), else for
+        the synthetic XLM-R vocabulary NFKC (what nmt_nfkc charsmaps compute, up to their
+        grapheme quirks); WordPiece normalises in C++ (BertNormalizer)."""
+        if self._pipeline is not None:
+            return self._pipeline(text)
+        if self._from_json:
+            return text
         return unicodedata.normalize("NFKC", text) if self.kind == "unigram" else text
 
     def tokenize(self, text: str) -> list[str]:

@@ -68,7 +68,13 @@ int symb_i8_queries_per_blk(int rsplit);
 int symb_index_scan_i8(const void* X8, const float* sx, int n_valid, int alloc_rows,
                        int rows_per_blk, int n_rblk, const void* Q8, int NQ, const float* thr,
                        float* cand_s, int* cand_i, int* cand_n, int cap, int xcd, hipStream_t st,
-                       int rsplit);
+                       int rsplit, const int* skip);
+int symb_prune_qquant(const void* Q, int NQ, int dim, const float* bounds, void* Q8, float* sq,
+                      float* margin, hipStream_t st);
+int symb_prune_route(int NQ, const float* pre_s, const float* tail_s, int k, float thr_margin,
+                     const float* sq, const float* margin, const float* cs_p, const int* cnt_p,
+                     int cap_p, int tshift, long long limit, float* T, float* thr, int* dense,
+                     hipStream_t st);
 int symb_i8_config(int tile_rows, int waves);
 int symb_i8_tile_rows();
 int symb_i8_wgs_per_cu();
@@ -87,14 +93,15 @@ int symb_gemm_lt_config(int mode);
 int symb_mq_config(int aux);
 int symb_index_scan_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                        int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
-                       int xcd, hipStream_t st, int sets, int tshift, int rsplit);
+                       int xcd, hipStream_t st, int sets, int tshift, int rsplit,
+                       const int* gate);
 int symb_index_scan_mq_ablate(const void* X, int n_valid, int rows_per_blk, int n_rblk,
                               const void* Q, int NQ, const float* thr, float* cand_s, int* cand_i,
                               int* cand_n, int cap, int xcd, hipStream_t st, int abl, int sets,
                               int rsplit);
 int symb_topk_select_counted(const float* cand_s, const int* cand_i, const int* cand_n, int cap,
                              int NQ, int kmax, int k, float* out_s, int* out_i, int* ovf,
-                             hipStream_t st);
+                             hipStream_t st, const int* gate, int reset_ovf);
 
 namespace {
 
@@ -352,12 +359,30 @@ PYBIND11_MODULE(_hip, m) {
   m.def("i8_wgs_per_cu", []() { return symb_i8_wgs_per_cu(); });
   m.def("index_scan_i8", [](uptr X8, uptr sx, int n_valid, int alloc_rows, int rows_per_blk,
                             int n_rblk, uptr Q8, int NQ, uptr thr, uptr cand_s, uptr cand_i,
-                            uptr cand_n, int cap, int xcd, uptr st, int rsplit) {
+                            uptr cand_n, int cap, int xcd, uptr st, int rsplit, uptr skip) {
     check(symb_index_scan_i8(P<void>(X8), P<const float>(sx), n_valid, alloc_rows, rows_per_blk,
                              n_rblk,
                              P<void>(Q8), NQ, P<const float>(thr), P<float>(cand_s), P<int>(cand_i),
-                             P<int>(cand_n), cap, xcd, S(st), rsplit),
+                             P<int>(cand_n), cap, xcd, S(st), rsplit, P<const int>(skip)),
           "index_scan_i8");
+  }, py::arg("X8"), py::arg("sx"), py::arg("n_valid"), py::arg("alloc_rows"),
+     py::arg("rows_per_blk"), py::arg("n_rblk"), py::arg("Q8"), py::arg("NQ"), py::arg("thr"),
+     py::arg("cand_s"), py::arg("cand_i"), py::arg("cand_n"), py::arg("cap"), py::arg("xcd"),
+     py::arg("stream"), py::arg("rsplit"), py::arg("skip") = 0);
+  m.def("prune_qquant", [](uptr Q, int NQ, int dim, uptr bounds, uptr Q8, uptr sq, uptr margin,
+                           uptr st) {
+    check(symb_prune_qquant(P<void>(Q), NQ, dim, P<const float>(bounds), P<void>(Q8), P<float>(sq),
+                            P<float>(margin), S(st)),
+          "prune_qquant");
+  });
+  m.def("prune_route", [](int NQ, uptr pre_s, uptr tail_s, int k, float thr_margin, uptr sq,
+                          uptr margin, uptr cs_p, uptr cnt_p, int cap_p, int tshift,
+                          long long limit, uptr T, uptr thr, uptr dense, uptr st) {
+    check(symb_prune_route(NQ, P<const float>(pre_s), P<const float>(tail_s), k, thr_margin,
+                           P<const float>(sq), P<const float>(margin), P<const float>(cs_p),
+                           P<const int>(cnt_p), cap_p, tshift, limit, P<float>(T), P<float>(thr),
+                           P<int>(dense), S(st)),
+          "prune_route");
   });
   m.def("index_scan_i8_ablate", [](uptr X8, uptr sx, int n_valid, int alloc_rows,
                                    int rows_per_blk, int n_rblk, uptr Q8, int NQ, uptr thr,
@@ -398,15 +423,15 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("sets") = 4, py::arg("rsplit") = 1);
   m.def("index_scan_mq", [](uptr X, int n_valid, int rows_per_blk, int n_rblk, uptr Q, int NQ,
                             uptr thr, uptr cand_s, uptr cand_i, uptr cand_n, int cap, int xcd,
-                            uptr st, int sets, int tshift, int rsplit) {
+                            uptr st, int sets, int tshift, int rsplit, uptr gate) {
     check(symb_index_scan_mq(P<void>(X), n_valid, rows_per_blk, n_rblk, P<void>(Q), NQ,
                              P<const float>(thr), P<float>(cand_s), P<int>(cand_i), P<int>(cand_n),
-                             cap, xcd, S(st), sets, tshift, rsplit),
+                             cap, xcd, S(st), sets, tshift, rsplit, P<const int>(gate)),
           "index_scan_mq");
   }, py::arg("X"), py::arg("n_valid"), py::arg("rows_per_blk"), py::arg("n_rblk"), py::arg("Q"),
      py::arg("NQ"), py::arg("thr"), py::arg("cand_s"), py::arg("cand_i"), py::arg("cand_n"),
      py::arg("cap"), py::arg("xcd"), py::arg("stream"), py::arg("sets") = 4,
-     py::arg("tshift") = 0, py::arg("rsplit") = 1);
+     py::arg("tshift") = 0, py::arg("rsplit") = 1, py::arg("gate") = 0);
   m.def("index_scan_mq_ablate", [](uptr X, int n_valid, int rows_per_blk, int n_rblk, uptr Q,
                                    int NQ, uptr thr, uptr cand_s, uptr cand_i, uptr cand_n,
                                    int cap, int xcd, uptr st, int abl, int sets, int rsplit) {
@@ -419,12 +444,16 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("cap"), py::arg("xcd"), py::arg("stream"), py::arg("abl"), py::arg("sets") = 4,
      py::arg("rsplit") = 1);
   m.def("topk_select_counted", [](uptr cand_s, uptr cand_i, uptr cand_n, int cap, int NQ,
-                                  int kmax, int k, uptr out_s, uptr out_i, uptr ovf, uptr st) {
+                                  int kmax, int k, uptr out_s, uptr out_i, uptr ovf, uptr st,
+                                  uptr gate, bool reset_ovf) {
     check(symb_topk_select_counted(P<const float>(cand_s), P<const int>(cand_i),
                                    P<const int>(cand_n), cap, NQ, kmax, k, P<float>(out_s),
-                                   P<int>(out_i), P<int>(ovf), S(st)),
+                                   P<int>(out_i), P<int>(ovf), S(st), P<const int>(gate),
+                                   reset_ovf ? 1 : 0),
           "topk_select_counted");
-  });
+  }, py::arg("cand_s"), py::arg("cand_i"), py::arg("cand_n"), py::arg("cap"), py::arg("NQ"),
+     py::arg("kmax"), py::arg("k"), py::arg("out_s"), py::arg("out_i"), py::arg("ovf"),
+     py::arg("stream"), py::arg("gate") = 0, py::arg("reset_ovf") = true);
   m.def("index_scan_ablate", [](uptr X, int n_valid, int rows_per_blk, int n_rblk, uptr Q, int NQ,
                                 uptr cs, uptr ci, uptr st, int abl, uptr thr) {
     check(symb_index_scan_ablate(P<void>(X), n_valid, rows_per_blk, n_rblk, P<void>(Q), NQ,

@@ -190,7 +190,11 @@ template <int RSPLIT, int ABL = 0, int TRK = 64, int WV = 8>
 __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
     const int8_t* __restrict__ X8, const float* __restrict__ sx, int n_valid, int rows_per_blk,
     const int8_t* __restrict__ Q8, int NQ, int n_qblk, int xcd, const float* __restrict__ thr_in,
-    float* __restrict__ cand_s, int* __restrict__ cand_i, int* __restrict__ cand_n, int cap) {
+    float* __restrict__ cand_s, int* __restrict__ cand_i, int* __restrict__ cand_n, int cap,
+    const int* __restrict__ skip) {
+  // skip (optional): the sampled route decision (prune_route_kernel) sent this batch to the bf16
+  // emitting scan -- every workgroup returns at once (grid-uniform, before any barrier)
+  if (skip != nullptr && *skip != 0) return;
   using namespace i8s;
   using G = Geo<TRK, WV>;
   constexpr int TR = G::TR, NSUB = G::NSUB, NS = G::NS, TILE_BYTES = G::TILE_BYTES;
@@ -630,6 +634,96 @@ __global__ __launch_bounds__(256) void prune_qprep_kernel(
   }
 }
 
+// The pruned search in two query-side launches around its exact sample (index/shard.py
+// _search_pruned), so the sample can decide the route:
+//   prune_qquant: q8 / sq (as prune_qprep) and margin = |q| E + |q - q~| X + 1e-5, known before the
+//                 sample is scanned, so the sample emits every row within the margin band;
+//   prune_route:  T = k-th best of (sample, tail) - thr_margin and thr = (T - margin) / sq (as
+//                 prune_qprep), plus the ROUTE: c = the sample rows (1 tile in 2^tshift) with an
+//                 exact score >= T - margin estimates the int8 scan's candidates as c << tshift.
+//                 If any query's estimate exceeds `limit` (or its sample buffer overflowed) the
+//                 int8 pass would overflow its buffer and pay the exact fallback on top (both full
+//                 scans): *dense = 1 routes the whole batch to the bf16 emitting scan instead.
+//                 Exactness never depends on the route; only the cost does.
+__global__ __launch_bounds__(256) void prune_qquant_kernel(const __bf16* __restrict__ Q, int NQ,
+                                                           const float* __restrict__ bounds,
+                                                           int8_t* __restrict__ Q8,
+                                                           float* __restrict__ sq,
+                                                           float* __restrict__ margin) {
+  constexpr int D = 384, PER = D / 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int q = blockIdx.x * 4 + w;
+  if (q >= NQ) return;   // (no barrier in this kernel)
+  float x[PER];
+  const uint32_t* xp = reinterpret_cast<const uint32_t*>(Q + (size_t)q * D + PER * lane);
+#pragma unroll
+  for (int i = 0; i < PER / 2; ++i) {
+    const uint32_t u = xp[i];
+    x[2 * i] = __uint_as_float(u << 16);
+    x[2 * i + 1] = __uint_as_float(u & 0xffff0000u);
+  }
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) amax = fmaxf(amax, fabsf(x[i]));
+  amax = wave_max(amax);
+  const float s = amax > 0.f ? amax / 127.f : 1.f;
+  const float inv = 1.f / s;
+  float e2 = 0.f, x2 = 0.f;
+  int qv[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    qv[i] = max(-127, min(127, (int)rintf(x[i] * inv)));
+    const float xt = (float)qv[i] * s;
+    e2 += (x[i] - xt) * (x[i] - xt);
+    x2 += x[i] * x[i];
+  }
+  e2 = wave_sum(e2);
+  x2 = wave_sum(x2);
+  uint16_t* op = reinterpret_cast<uint16_t*>(Q8 + (size_t)q * D + PER * lane);
+#pragma unroll
+  for (int i = 0; i < PER / 2; ++i)
+    op[i] = (uint16_t)((qv[2 * i] & 0xff) | ((qv[2 * i + 1] & 0xff) << 8));
+  if (lane == 0) {
+    sq[q] = s;
+    margin[q] = sqrtf(x2) * bounds[0] + sqrtf(e2) * bounds[1] + 1e-5f;
+  }
+}
+
+__global__ __launch_bounds__(256) void prune_route_kernel(
+    int NQ, const float* __restrict__ pre_s, const float* __restrict__ tail_s, int k,
+    float thr_margin, const float* __restrict__ sq, const float* __restrict__ margin,
+    const float* __restrict__ cs_p, const int* __restrict__ cnt_p, int cap_p, int tshift,
+    long long limit, float* __restrict__ T_out, float* __restrict__ thr,
+    int* __restrict__ dense) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int q = blockIdx.x * 4 + w;
+  if (q >= NQ) return;   // (no barrier in this kernel)
+  // k-th best of 2k values (prune_qprep_kernel)
+  float v = -INFINITY;
+  if (lane < k) v = pre_s[(size_t)q * k + lane];
+  else if (lane < 2 * k) v = tail_s[(size_t)q * k + lane - k];
+  int rank = 0;
+  for (int j = 0; j < 2 * k; ++j) {
+    const float u = __shfl(v, j);
+    rank += (u > v) || (u == v && j < lane);
+  }
+  const unsigned long long hit = __ballot(lane < 2 * k && rank == k - 1);
+  const float T = __shfl(v, (int)__builtin_ctzll(hit)) - thr_margin;
+  const float m = margin[q];
+  const int cnt = cnt_p[q];
+  const int n = min(cnt, cap_p);
+  const float band = T - m;
+  const float* cs = cs_p + (size_t)q * cap_p;
+  float c = 0.f;
+  for (int i = lane; i < n; i += 64) c += cs[i] >= band ? 1.f : 0.f;
+  c = wave_sum(c);
+  if (lane == 0) {
+    T_out[q] = T;
+    thr[q] = (T - m) / sq[q];
+    if (cnt > cap_p || ((long long)c << tshift) > limit) atomicOr(dense, 1);
+  }
+}
+
 }  // namespace symb
 
 using namespace symb;
@@ -654,7 +748,7 @@ int symb_i8_queries_per_blk(int rsplit) {
 template <int RSPLIT, int TRK, int WV = 8>
 static int launch_i8(const void* X8, const float* sx, int n_valid, int rows_per_blk, int n_rblk,
                      const void* Q8, int NQ, const float* thr, float* cand_s, int* cand_i,
-                     int* cand_n, int cap, int xcd, hipStream_t st) {
+                     int* cand_n, int cap, int xcd, hipStream_t st, const int* skip) {
   constexpr int qpb = WV / RSPLIT * 16 * i8s::SETS;
   const int n_qblk = (NQ + qpb - 1) / qpb;
   constexpr int lds = i8s::Geo<TRK, WV>::LDS_BYTES;
@@ -666,7 +760,7 @@ static int launch_i8(const void* X8, const float* sx, int n_valid, int rows_per_
   }
   hipLaunchKernelGGL((index_scan_i8_kernel<RSPLIT, 0, TRK, WV>), dim3(n_rblk * n_qblk), dim3(64 * WV), lds, st,
                      (const int8_t*)X8, sx, n_valid, rows_per_blk, (const int8_t*)Q8, NQ, n_qblk,
-                     xcd, thr, cand_s, cand_i, cand_n, cap);
+                     xcd, thr, cand_s, cand_i, cand_n, cap, skip);
   return (int)hipGetLastError();
 }
 
@@ -676,7 +770,7 @@ static int launch_i8(const void* X8, const float* sx, int n_valid, int rows_per_
 int symb_index_scan_i8(const void* X8, const float* sx, int n_valid, int alloc_rows,
                        int rows_per_blk, int n_rblk, const void* Q8, int NQ, const float* thr,
                        float* cand_s, int* cand_i, int* cand_n, int cap, int xcd, hipStream_t st,
-                       int rsplit) {
+                       int rsplit, const int* skip) {
   if (NQ <= 0) return 0;
   const int tr = g_i8_tr;
   if (rows_per_blk % tr || n_rblk <= 0 || thr == nullptr || cap <= 0 || n_valid <= 0) return -1;
@@ -685,10 +779,10 @@ int symb_index_scan_i8(const void* X8, const float* sx, int n_valid, int alloc_r
   hipError_t e = hipMemsetAsync(cand_n, 0, sizeof(int) * (size_t)NQ, st);
   if (e != hipSuccess) return (int)e;
 #define SYMB_I8(RS, T) launch_i8<RS, T>(X8, sx, n_valid, rows_per_blk, n_rblk, Q8, NQ, thr, cand_s, \
-                                        cand_i, cand_n, cap, xcd, st)
+                                        cand_i, cand_n, cap, xcd, st, skip)
   if (g_i8_waves == 4)
     return launch_i8<1, 64, 4>(X8, sx, n_valid, rows_per_blk, n_rblk, Q8, NQ, thr, cand_s, cand_i,
-                               cand_n, cap, xcd, st);
+                               cand_n, cap, xcd, st, skip);
   if (rsplit == 2) return tr == 128 ? SYMB_I8(2, 128) : SYMB_I8(2, 64);
   if (rsplit == 1) return tr == 128 ? SYMB_I8(1, 128) : SYMB_I8(1, 64);
 #undef SYMB_I8
@@ -715,7 +809,7 @@ int symb_index_scan_i8_ablate(const void* X8, const float* sx, int n_valid, int 
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipLaunchKernelGGL(kern, dim3(n_rblk * n_qblk), dim3(w4 ? 256 : 512), lds, st, (const int8_t*)X8, sx,
                        n_valid, rows_per_blk, (const int8_t*)Q8, NQ, n_qblk, xcd, thr, cand_s,
-                       cand_i, cand_n, cap);
+                       cand_i, cand_n, cap, (const int*)nullptr);
     return (int)hipGetLastError();
   };
   if (w4) {
@@ -767,5 +861,28 @@ int symb_prune_qprep(const void* Q, int NQ, int dim, const float* pre_s, const f
   if (dim != 384 || k < 1 || k > 32) return -1;
   hipLaunchKernelGGL(prune_qprep_kernel, dim3((NQ + 3) / 4), dim3(256), 0, st, (const __bf16*)Q,
                      NQ, pre_s, tail_s, k, thr_margin, bounds, (int8_t*)Q8, sq, T, thr);
+  return (int)hipGetLastError();
+}
+
+int symb_prune_qquant(const void* Q, int NQ, int dim, const float* bounds, void* Q8, float* sq,
+                      float* margin, hipStream_t st) {
+  if (NQ <= 0) return 0;
+  if (dim != 384) return -1;
+  hipLaunchKernelGGL(prune_qquant_kernel, dim3((NQ + 3) / 4), dim3(256), 0, st, (const __bf16*)Q,
+                     NQ, bounds, (int8_t*)Q8, sq, margin);
+  return (int)hipGetLastError();
+}
+
+// dense (one int) is zeroed here, then raised by any query routed to the bf16 scan.
+int symb_prune_route(int NQ, const float* pre_s, const float* tail_s, int k, float thr_margin,
+                     const float* sq, const float* margin, const float* cs_p, const int* cnt_p,
+                     int cap_p, int tshift, long long limit, float* T, float* thr, int* dense,
+                     hipStream_t st) {
+  if (NQ <= 0) return 0;
+  if (k < 1 || k > 32 || cap_p <= 0 || tshift < 0 || tshift > 20) return -1;
+  hipError_t e = hipMemsetAsync(dense, 0, sizeof(int), st);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(prune_route_kernel, dim3((NQ + 3) / 4), dim3(256), 0, st, NQ, pre_s, tail_s,
+                     k, thr_margin, sq, margin, cs_p, cnt_p, cap_p, tshift, limit, T, thr, dense);
   return (int)hipGetLastError();
 }

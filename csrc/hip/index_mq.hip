@@ -152,7 +152,10 @@ template <int NSET, int ABL = 0, int RSPLIT = 1, int AUX = 0>
 __global__ __launch_bounds__(512, 1) void index_scan_mq_kernel(
     const __bf16* __restrict__ X, int n_valid, int rows_per_blk, const __bf16* __restrict__ Q,
     int NQ, int n_qblk, int xcd, const float* __restrict__ thr_in, float* __restrict__ cand_s,
-    int* __restrict__ cand_i, int* __restrict__ cand_n, int cap, int tshift) {
+    int* __restrict__ cand_i, int* __restrict__ cand_n, int cap, int tshift,
+    const int* __restrict__ gate) {
+  // gate (optional): run only if *gate != 0 -- the pruned search's bf16 route (index_i8.hip)
+  if (gate != nullptr && *gate == 0) return;
   using namespace mq;
   constexpr int SETS = NSET, QW = SETS * 16, QWAVES = WAVES / RSPLIT, QPB = QWAVES * QW;
   constexpr int NSW = NSUB / RSPLIT;          // 16-row sub-tiles per wave per tile
@@ -379,7 +382,8 @@ template <int KMAX, int NTH>
 __global__ __launch_bounds__(NTH) void topk_select_counted_kernel(
     const float* __restrict__ cand_s, const int* __restrict__ cand_i,
     const int* __restrict__ cand_n, int cap, int k, float* __restrict__ out_s,
-    int* __restrict__ out_i, int* __restrict__ ovf) {
+    int* __restrict__ out_i, int* __restrict__ ovf, const int* __restrict__ gate) {
+  if (gate != nullptr && *gate == 0) return;   // (grid-uniform, before any barrier)
   __shared__ float ls[NTH * KMAX];
   __shared__ int li[NTH * KMAX];
   const int q = blockIdx.x, tid = threadIdx.x;
@@ -457,7 +461,7 @@ int symb_mq_config(int aux) {
 template <int NSET, int RSPLIT, int AUX>
 static int launch_mq_aux(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                      int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
-                     int xcd, hipStream_t st, int tshift) {
+                     int xcd, hipStream_t st, int tshift, const int* gate) {
   constexpr int qpb = mq::WAVES / RSPLIT * 16 * NSET;
   const int n_qblk = (NQ + qpb - 1) / qpb;
   constexpr int lds = mq::LDS_BYTES;
@@ -469,19 +473,19 @@ static int launch_mq_aux(const void* X, int n_valid, int rows_per_blk, int n_rbl
   }
   hipLaunchKernelGGL((index_scan_mq_kernel<NSET, 0, RSPLIT, AUX>), dim3(n_rblk * n_qblk), dim3(512),
                      lds, st, (const __bf16*)X, n_valid, rows_per_blk, (const __bf16*)Q, NQ, n_qblk,
-                     xcd, thr, cand_s, cand_i, cand_n, cap, tshift);
+                     xcd, thr, cand_s, cand_i, cand_n, cap, tshift, gate);
   return (int)hipGetLastError();
 }
 
 template <int NSET, int RSPLIT>
 static int launch_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                      int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
-                     int xcd, hipStream_t st, int tshift) {
+                     int xcd, hipStream_t st, int tshift, const int* gate) {
   return g_mq_aux == 2
              ? launch_mq_aux<NSET, RSPLIT, 2>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, thr, cand_s,
-                                             cand_i, cand_n, cap, xcd, st, tshift)
+                                             cand_i, cand_n, cap, xcd, st, tshift, gate)
              : launch_mq_aux<NSET, RSPLIT, 0>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, thr, cand_s,
-                                             cand_i, cand_n, cap, xcd, st, tshift);
+                                             cand_i, cand_n, cap, xcd, st, tshift, gate);
 }
 
 // tshift: 0 = rows [0, n_valid); k > 0 = virtual rows of a 1-in-2^k tile sample (kernel note).
@@ -489,7 +493,8 @@ static int launch_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk, c
 // row-split form, sets 4 only).  Queries per workgroup: 8 / rsplit * 16 * sets (512 or 256).
 int symb_index_scan_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                        int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
-                       int xcd, hipStream_t st, int sets, int tshift, int rsplit) {
+                       int xcd, hipStream_t st, int sets, int tshift, int rsplit,
+                       const int* gate) {
   if (NQ <= 0) return 0;
   if (rows_per_blk % mq::TR || n_rblk <= 0 || thr == nullptr || cap <= 0) return -1;
   if ((sets != 2 && sets != 4) || tshift < 0 || tshift > 12) return -1;
@@ -498,11 +503,11 @@ int symb_index_scan_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk,
   if (e != hipSuccess) return (int)e;
   if (rsplit == 2)
     return launch_mq<4, 2>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, thr, cand_s, cand_i, cand_n,
-                           cap, xcd, st, tshift);
+                           cap, xcd, st, tshift, gate);
   return sets == 4 ? launch_mq<4, 1>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, thr, cand_s, cand_i,
-                                     cand_n, cap, xcd, st, tshift)
+                                     cand_n, cap, xcd, st, tshift, gate)
                    : launch_mq<2, 1>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, thr, cand_s, cand_i,
-                                     cand_n, cap, xcd, st, tshift);
+                                     cand_n, cap, xcd, st, tshift, gate);
 }
 
 // Profiling-only entry: the ablations of index_scan_mq_kernel (ABL above), same arguments.
@@ -523,7 +528,7 @@ int symb_index_scan_mq_ablate(const void* X, int n_valid, int rows_per_blk, int 
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipLaunchKernelGGL(kern, dim3(n_rblk * n_qblk), dim3(512), lds, st, (const __bf16*)X,
                        n_valid, rows_per_blk, (const __bf16*)Q, NQ, n_qblk, xcd, thr, cand_s,
-                       cand_i, cand_n, cap, 0);
+                       cand_i, cand_n, cap, 0, (const int*)nullptr);
     return (int)hipGetLastError();
   };
   switch (abl + 8 * (sets == 2) + 16 * (rsplit == 2)) {
@@ -546,20 +551,23 @@ int symb_index_scan_mq_ablate(const void* X, int n_valid, int rows_per_blk, int 
   }
 }
 
-// ovf (one int) is zeroed here, then set by any query whose buffer overflowed.
+// ovf (one int) is zeroed here (reset_ovf), then set by any query whose buffer overflowed.
+// gate (optional): the launch is skipped on the device unless *gate != 0.
 int symb_topk_select_counted(const float* cand_s, const int* cand_i, const int* cand_n, int cap,
                              int NQ, int kmax, int k, float* out_s, int* out_i, int* ovf,
-                             hipStream_t st) {
+                             hipStream_t st, const int* gate, int reset_ovf) {
   if (NQ <= 0) return 0;
   if (k > kmax) return -1;
-  hipError_t e = hipMemsetAsync(ovf, 0, sizeof(int), st);
-  if (e != hipSuccess) return (int)e;
+  if (reset_ovf) {
+    hipError_t e = hipMemsetAsync(ovf, 0, sizeof(int), st);
+    if (e != hipSuccess) return (int)e;
+  }
   if (kmax == 16)
     hipLaunchKernelGGL((topk_select_counted_kernel<16, 256>), dim3(NQ), dim3(256), 0, st, cand_s,
-                       cand_i, cand_n, cap, k, out_s, out_i, ovf);
+                       cand_i, cand_n, cap, k, out_s, out_i, ovf, gate);
   else if (kmax == 32)
     hipLaunchKernelGGL((topk_select_counted_kernel<32, 128>), dim3(NQ), dim3(128), 0, st, cand_s,
-                       cand_i, cand_n, cap, k, out_s, out_i, ovf);
+                       cand_i, cand_n, cap, k, out_s, out_i, ovf, gate);
   else
     return -1;
   return (int)hipGetLastError();

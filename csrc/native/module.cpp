@@ -12,6 +12,7 @@ void register_packstream(py::module_& m);
 void register_natsd(py::module_& m);
 void register_gateway(py::module_& m);
 void register_loadgen(py::module_& m);
+void register_spm_norm(py::module_& m);
 }  // namespace symbn
 
 PYBIND11_MODULE(_native, m) {
@@ -24,5 +25,6 @@ PYBIND11_MODULE(_native, m) {
   symbn::register_packstream(m);
   symbn::register_natsd(m);
   symbn::register_gateway(m);
+  symbn::register_spm_norm(m);
   symbn::register_loadgen(m);
 }

@@ -482,21 +482,40 @@ class Unigram {
     unk_score_ = mn - 10.0;
   }
 
+  // Pre-tokeniser of a tokenizer.json: ``builtin_norm`` false = the text arrives normalised by
+  // the file's own normalizer pipeline (text/tokenizer.py), so no Strip / space collapsing here;
+  // Metaspace with its replacement char, prepend scheme (0 never, 1 always, 2 first = always for
+  // a single section) and split flag.
+  void set_pretokenizer(bool builtin_norm, const std::string& replacement, int prepend, bool split) {
+    const std::u32string r = utf8_decode(replacement);
+    if (r.size() != 1) throw std::invalid_argument("Metaspace replacement must be one character");
+    builtin_norm_ = builtin_norm;
+    meta_ = r[0];
+    prepend_ = prepend;
+    split_ = split;
+  }
+
   // Metaspace pre-tokenisation of already-normalised text.
   std::vector<std::u32string> pretokenize(const std::string& text) const {
     std::u32string u = utf8_decode(text), m;
-    while (!u.empty() && is_ws(u.back())) u.pop_back();  // Strip(right)
+    if (builtin_norm_)
+      while (!u.empty() && is_ws(u.back())) u.pop_back();  // Strip(right)
     m.reserve(u.size() + 1);
     for (size_t i = 0; i < u.size(); ++i) {
-      if (u[i] == U' ' && i + 1 < u.size() && u[i + 1] == U' ') continue;  // " {2,}" -> " "
-      m.push_back(u[i] == U' ' ? kMeta : u[i]);
+      if (builtin_norm_ && u[i] == U' ' && i + 1 < u.size() && u[i + 1] == U' ')
+        continue;  // " {2,}" -> " "
+      m.push_back(u[i] == U' ' ? meta_ : u[i]);
     }
     std::vector<std::u32string> words;
     if (m.empty()) return words;
-    if (m[0] != kMeta) m.insert(m.begin(), kMeta);
+    if (prepend_ != 0 && m[0] != meta_) m.insert(m.begin(), meta_);
+    if (!split_) {
+      words.push_back(m);
+      return words;
+    }
     size_t st = 0;
     for (size_t i = 1; i <= m.size(); ++i) {
-      if (i == m.size() || m[i] == kMeta) {
+      if (i == m.size() || m[i] == meta_) {
         words.emplace_back(m.substr(st, i - st));
         st = i;
       }
@@ -598,6 +617,10 @@ class Unigram {
   int unk_, bos_, eos_;
   int max_chars_ = 1;
   double unk_score_ = -10.0;
+  bool builtin_norm_ = true;
+  char32_t meta_ = kMeta;
+  int prepend_ = 1;
+  bool split_ = true;
 };
 
 #ifndef SYMB_NO_PYTHON
@@ -617,6 +640,8 @@ void register_text(py::module_& m) {
       .def(py::init<const std::vector<std::string>&, const std::vector<double>&, int, int, int>(),
            py::arg("pieces"), py::arg("scores"), py::arg("unk_id"), py::arg("bos_id"),
            py::arg("eos_id"))
+      .def("set_pretokenizer", &Unigram::set_pretokenizer, py::arg("builtin_norm"),
+           py::arg("replacement") = "\u2581", py::arg("prepend") = 1, py::arg("split") = true)
       .def("tokenize", &Unigram::tokenize)
       .def("encode", &Unigram::encode, py::arg("text"), py::arg("max_len") = 0,
            py::arg("add_special") = true)

@@ -468,9 +468,86 @@ def test_index_pruned_search_is_exact(nq, data, tr):
         assert int(ovf.item()) == 0, "random / near data must not overflow the candidate buffer"
         assert cnt.float().mean().item() < shard.PRUNE_CAP / 2
     _close(s1, s0, atol=2e-5, what="pruned vs exact scores")
-    assert (r0 == r1).float().mean().item() > 0.999
+    if data != "clustered":   # (tight clusters: near-ties may order differently; scores decide)
+        assert (r0 == r1).float().mean().item() > 0.999
     true = (q.float() @ shard.unit_rows().float().t()).gather(1, r1.long())
     _close(s1, true, atol=2e-3, what="pruned returned rows")
+
+
+def test_prune_qquant_and_route_match_torch():
+    """index_i8.hip prune_qquant (int8 query image + per-query bound margin) and prune_route (T,
+    emission threshold, route estimate from the sample's candidates) == torch compositions."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+    from codename_symbiont_amd.ops._ext import hip, stream_handle
+
+    nq, n, k, cap, ts = 203, 20000, 10, 512, 5
+    shard = HbmIndexShard(384, n, prune="i8")
+    shard.append_f32(_f(n, 384, seed=91))
+    q = torch.nn.functional.normalize(_f(nq, 384, seed=92), dim=-1).bfloat16()
+    q8 = torch.empty(nq, 384, dtype=torch.int8, device=DEV)
+    sq, margin = torch.empty(nq, device=DEV), torch.empty(nq, device=DEV)
+    h, st = hip(), stream_handle()
+    h.prune_qquant(q.data_ptr(), nq, 384, shard.i8_bounds.data_ptr(), q8.data_ptr(), sq.data_ptr(),
+                   margin.data_ptr(), st)
+    pre = _f(nq, k, seed=93) * 0.1 + 0.5
+    tail = _f(nq, k, seed=94) * 0.1 + 0.4
+    T0, q80, sq0, thr_t = shard._prune_thresholds_torch(q, pre, tail, k)
+    m0 = (T0 - thr_t * sq0)                  # the torch margin, recovered
+    torch.cuda.synchronize()
+    assert torch.equal(q8, q80) and torch.equal(sq, sq0)
+    _close(margin, m0, atol=2e-5, what="bound margin")
+    # sample candidates: query j gets j rows inside the band [T - margin, ...), 3 rows below it;
+    # queries >= 200 overflow their buffer
+    cs = torch.full((nq, cap), -1.0, device=DEV)
+    cnt = torch.zeros(nq, dtype=torch.int32, device=DEV)
+    for j in range(nq):
+        c = min(j, cap - 3)
+        cs[j, :c] = T0[j] - 0.5 * margin[j]
+        cs[j, c:c + 3] = T0[j] - 2.0 * margin[j]
+        cnt[j] = c + 3 if j < 200 else cap + 5
+    T, thr = torch.empty(nq, device=DEV), torch.empty(nq, device=DEV)
+    dense = torch.empty(1, dtype=torch.int32, device=DEV)
+
+    def route(rows, limit):
+        h.prune_route(rows, pre.data_ptr(), tail.data_ptr(), k, shard.MQ_THR_MARGIN, sq.data_ptr(),
+                      margin.data_ptr(), cs.data_ptr(), cnt.data_ptr(), cap, ts, limit, T.data_ptr(),
+                      thr.data_ptr(), dense.data_ptr(), st)
+        torch.cuda.synchronize()
+        return int(dense.item())
+
+    assert route(150, 150 << ts) == 0          # at most 149 in-band rows: estimate <= limit
+    assert route(151, 149 << ts) == 1          # query 150 estimates 150 << 5 > limit
+    assert route(nq, 1 << 40) == 1             # overflowed sample buffers always route dense
+    assert torch.equal(T, T0)
+    _close(thr, thr_t, atol=1e-4, rtol=1e-5, what="emission thresholds")
+
+
+@pytest.mark.parametrize("route", [True, False])
+def test_index_pruned_search_routes_dense_data_exactly(route):
+    """An anisotropic corpus (every pair at cosine ~0.3: scores crowd the k-th best) sends the
+    int8 pass past its candidate buffer.  With the sampled route the batch takes the bf16
+    emitting scan instead (no overflow); without it the int8 pass overflows and the gated exact
+    fallback runs.  Either way the answer is the exact bf16 scan's."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+    from codename_symbiont_amd.index.synth import CorpusGen, fill_corpus
+
+    n, k, nq = (1 << 20) + 4321, 10, 256
+    gen = CorpusGen("anisotropic", 384, DEV)
+    ref = HbmIndexShard(384, n)
+    shard = HbmIndexShard(384, n, prune="i8")
+    for sh in (ref, shard):
+        fill_corpus(sh, gen, n, seed=3)
+    shard.prune_route = route
+    q = gen.unit(nq, seed=77).bfloat16()
+    ref.scan_mq = False
+    s0, r0 = ref.search(q, k)
+    s1, r1 = shard.search(q, k)
+    _, ovf = shard._mq_last
+    torch.cuda.synchronize()
+    assert int(shard._route_last.item()) == (1 if route else 0)
+    assert int(ovf.item()) == (0 if route else 1)
+    _close(s1, s0, atol=2e-5, what="routed pruned vs exact scores")
+    assert (r0 == r1).float().mean().item() > 0.999
 
 
 def test_index_scan_mq_overflow_falls_back_exact():

@@ -152,6 +152,61 @@ def test_index_group_upsert_search_overwrite():
     assert out[1] == 100 and out[2] == 100          # least-loaded placement balances the shards
 
 
+def _group4_worker(rank, world, port, out):
+    """4 ranks: batched upserts (new + overwritten ids in one batch) and searches through the lean
+    path (one packed all_gather per search) == one shard holding every point."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard, Payload
+    from codename_symbiont_amd.index.store import VectorStore
+    from codename_symbiont_amd.parallel import dist as D
+    from codename_symbiont_amd.parallel.index_group import IndexGroup
+    info = _init(rank, world, port)
+    grp = IndexGroup(info, dim=48, capacity_per_rank=2000)
+    if rank != 0:
+        grp.serve()
+        out[rank] = grp.shard.count
+    else:
+        store = VectorStore(48, 0, group=grp)
+        ref = HbmIndexShard(48, 8000, device="cpu")
+        rng = np.random.default_rng(11)
+        vecs = rng.standard_normal((3000, 48)).astype(np.float32)
+        ids = [f"p{i}" for i in range(3000)]
+        pls = [Payload(f"d{i}", "u", f"t{i}", i) for i in range(3000)]
+        for s in range(0, 3000, 500):
+            store.upsert(ids[s:s + 500], vecs[s:s + 500], pls[s:s + 500])
+            ref.upsert(ids[s:s + 500], torch.from_numpy(vecs[s:s + 500]), pls[s:s + 500])
+        # one batch mixing 40 overwrites (scattered over every rank) and 10 new points
+        ow = rng.choice(3000, 40, replace=False).tolist()
+        new_v = rng.standard_normal((50, 48)).astype(np.float32)
+        b_ids = [ids[i] for i in ow] + [f"n{i}" for i in range(10)]
+        b_pl = [Payload("x", "u", f"w{i}", i) for i in range(50)]
+        store.upsert(b_ids, new_v, b_pl)
+        ref.upsert(b_ids, torch.from_numpy(new_v), b_pl)
+        q = np.concatenate([rng.standard_normal((20, 48)).astype(np.float32), new_v[:5]])
+        grp.comm_stats.clear()
+        sc, gids = store.search(q, 7)
+        rs, rr = ref.search(torch.nn.functional.normalize(torch.from_numpy(q), dim=-1).bfloat16(), 7)
+        got = [[store.lookup(g)[1].sentence_text for g in row] for row in gids]
+        want = [[ref.payloads.get(int(r))[1].sentence_text for r in row] for row in rr.tolist()]
+        out[0] = (got, want, float(np.abs(sc - rs.numpy()).max()), dict(grp.comm_stats),
+                  store.count)
+        grp.stop()
+    D.shutdown(info)
+
+
+def test_index_group_four_ranks_lean_search_matches_single_shard():
+    world = 4
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.start_processes(_group4_worker, args=(world, _free_port(), out), nprocs=world, join=True,
+                       start_method="spawn")
+    got, want, sdiff, stats, count = out[0]
+    assert got == want and sdiff < 1e-5
+    assert count == 3010 and sum(out[r] for r in range(1, world)) + 0 <= 3010
+    ops, colls, nbytes = stats["search"]
+    assert ops == 1 and colls == 3                 # header, queries, ONE packed all_gather
+    assert nbytes == 32 + 25 * 48 * 4 + world * 25 * 7 * 16   # f32 queries on gloo
+
+
 def _group_snapshot_worker(rank, world, port, snap, phase, out, crash_mid=False):
     """phase 0: ingest, snapshot, ingest more (WAL only), crash.  phase 1: restore + search."""
     from codename_symbiont_amd.index.shard import Payload

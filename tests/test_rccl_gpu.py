@@ -1,0 +1,87 @@
+"""The RCCL-specific code paths on ONE GPU: a single-rank "nccl" process group (RCCL refuses two
+ranks on one device, and the driver's multi-GPU runs are the only N > 1 hardware runs), so every
+collective the sharded search / IndexGroup / bench self-check issue over RCCL actually executes:
+init with device_id, barrier(device_ids=...), bf16 all_gather_into_tensor of queries,
+all_to_all_single of f32 scores and int64 ids, int64 / bf16 broadcasts, the f64 packed result
+all_gather.  Results must equal the collective-free single-shard search."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def rccl():
+    import torch.distributed as dist
+
+    from codename_symbiont_amd.parallel import dist as D
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    saved = {k: os.environ.get(k) for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR",
+                                            "MASTER_PORT")}
+    os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    info = D.init(backend="nccl", single_rank_group=True)
+    assert dist.get_backend() == "nccl" and info.backend == "nccl"
+    yield info
+    D.barrier(info)
+    D.shutdown(info)
+    for k, v in saved.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
+
+
+def test_rccl_selfcheck_and_barrier(rccl):
+    from codename_symbiont_amd.parallel import dist as D
+
+    out = D.selfcheck(rccl)
+    assert out["backend"] == "nccl" and out["collective"] == "all_gather ok (bfloat16)"
+    assert out["devices"] == [rccl.device.index]
+    D.barrier(rccl)
+    assert D.allreduce_max(rccl, 3.5) == 3.5
+
+
+def test_rccl_sharded_search_matches_local(rccl):
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+    from codename_symbiont_amd.parallel.sharded import ShardedSearcher
+
+    shard = HbmIndexShard(384, 300_000, device=rccl.device)
+    shard.fill_random(300_000, seed=5)
+    q = torch.nn.functional.normalize(torch.randn(256, 384, device=rccl.device), dim=-1).bfloat16()
+    ss = ShardedSearcher(shard, rccl)
+    assert ss.collective and ss.wire_dtype == torch.bfloat16
+    s1, g1 = ss.search(q, 10)          # bf16 all_gather_into_tensor + 2 all_to_all_single
+    s0, r0 = shard.search(q, 10)
+    torch.cuda.synchronize()
+    assert torch.equal(g1, r0.long()) and torch.equal(s1, s0)
+
+
+def test_rccl_index_group_store_roundtrip(rccl):
+    from codename_symbiont_amd.index.shard import Payload
+    from codename_symbiont_amd.index.store import VectorStore
+    from codename_symbiont_amd.parallel.index_group import IndexGroup
+
+    grp = IndexGroup(rccl, dim=384, capacity_per_rank=10_000)
+    assert grp.collective and grp.wire_dtype == torch.bfloat16
+    store = VectorStore(384, 0, group=grp)
+    rng = np.random.default_rng(3)
+    v = rng.standard_normal((3000, 384)).astype(np.float32)
+    ids = [f"p{i}" for i in range(3000)]
+    store.upsert(ids, v, [Payload(f"d{i}", "u", f"t{i}", i) for i in range(3000)])
+    store.upsert([ids[7], ids[1500], ids[2999]], -v[[7, 1500, 2999]],     # batched overwrites
+                 [Payload("d", "u", f"neg{i}", i) for i in (7, 1500, 2999)])
+    q = np.concatenate([v[[10, 20]], -v[[7, 1500]]])
+    sc, gids = store.search(q, 3)    # int64 header + bf16 query broadcasts, f64 packed all_gather
+    texts = [store.lookup(int(g[0]))[1].sentence_text for g in gids]
+    assert texts == ["t10", "t20", "neg7", "neg1500"]
+    assert np.allclose(sc[:, 0], 1.0, atol=1e-2)
+    assert grp.comm_stats["search"][1] == 3
