@@ -58,6 +58,10 @@ class PayloadStore:
         self.point_ids: dict[int, str] = {}          # row -> point id
         self.fields: dict[int, tuple] = {}           # row -> payload field tuple (FIELDS order)
         self.id_to_row: dict[str, int] = {}
+        # rows whose point id / payload changed since the last snapshot cut (index/persist.py),
+        # recorded only while a persister tracks this store
+        self.track = False
+        self.dirty: set[int] = set()
 
     def __len__(self):
         return self.n
@@ -78,6 +82,8 @@ class PayloadStore:
             self.fields[row] = tuple(getattr(payload, f) for f in self.FIELDS)
         else:
             self.fields.pop(row, None)
+        if self.track:
+            self.dirty.add(row)
 
     def get(self, row: int) -> tuple[str | None, Payload]:
         t = self.fields.get(row)
@@ -100,6 +106,7 @@ class PayloadStore:
                 del self.id_to_row[pid]
         for r in [r for r in self.fields if r >= n]:
             del self.fields[r]
+        self.dirty = {r for r in self.dirty if r < n}
         self.n = n
 
 
@@ -208,6 +215,11 @@ class HbmIndexShard:
         # streamed once per 512 queries), True = the 256-query fused form (twice the L2 reads)
         self.i8_rsplit2 = False
         self._mq_tot = None
+        # snapshot change record (index/persist.py ShardPersister): rows covered by the last cut
+        # and the covered rows overwritten since; kept only while ``payloads.track`` is on
+        self._persisted = 0
+        self._dirty: set[int] = set()
+        self._persist_key = None
 
     # ------------------------------------------------------------------ inserts
     def _reserve(self, n: int) -> int:
@@ -225,6 +237,13 @@ class HbmIndexShard:
         self.payloads.truncate(n)
         self.count = n
         self.visible = min(self.visible, n)
+        self._persisted = min(self._persisted, n)
+        self._dirty = {r for r in self._dirty if r < n}
+
+    def _mark_written(self, rows) -> None:
+        """Rows overwritten in place: remember the ones the last snapshot already covers."""
+        if self.payloads.track and self._persisted:
+            self._dirty.update(int(r) for r in rows if r < self._persisted)
 
     def publish(self) -> None:
         """Make every reserved row searchable (call after its write is enqueued)."""
@@ -318,6 +337,8 @@ class HbmIndexShard:
         return r0
 
     def write_f32(self, r0: int, vecs: torch.Tensor) -> None:
+        if r0 < self._persisted:
+            self._mark_written(range(r0, min(r0 + vecs.shape[0], self._persisted)))
         self._store(r0, vecs.to(self.device, torch.float32).contiguous(), normalize=True)
 
     def write_rows_f32(self, rows, vecs: torch.Tensor) -> None:
@@ -336,6 +357,7 @@ class HbmIndexShard:
             return
         if int(idx.min()) < 0 or int(idx.max()) >= self.count:
             raise IndexError("write_rows_f32: row outside the shard")
+        self._mark_written(idx.tolist())
         scratch = HbmIndexShard(self.dim, n, self.device, dtype=self.dtype,
                                 prefilter=self.prefilter, prune=self.prune)
         scratch.append_f32(vecs)

@@ -16,7 +16,7 @@ import threading
 import numpy as np
 import torch
 
-from .persist import Wal, load_snapshot, save_snapshot
+from .persist import ShardPersister, Wal, committed_gen, load_snapshot, wal_files
 from .shard import HbmIndexShard, Payload
 
 log = logging.getLogger("symbiont.index")
@@ -46,16 +46,30 @@ class VectorStore:
         self._lock = threading.Lock()
         self._frag: dict[int, tuple[bytes, bytes]] = {}
         self.wal = None
+        self._bg: threading.Thread | None = None   # background snapshot writer
+        self.snapshot_error: BaseException | None = None
+        self.last_snapshot: dict = {}
         if snapshot_dir:
+            import time
+
             os.makedirs(snapshot_dir, exist_ok=True)
+            t0 = time.perf_counter()
             # a group restores every rank's shard collectively, then re-applies the WAL over it
             n = load_snapshot(self.shard, snapshot_dir) if group is None else group.load(snapshot_dir)
+            self.shard.payloads.track = True
+            t1 = time.perf_counter()
             m = 0
-            Wal.repair(os.path.join(snapshot_dir, "wal.log"))
-            for ids, pls, vecs in Wal.replay(os.path.join(snapshot_dir, "wal.log"), dim):
-                self._upsert_nolog(ids, vecs, pls)
-                m += len(ids)
-            log.info("[INDEX_RESTORE] snapshot rows=%d, WAL replayed=%d", n, m)
+            # every WAL file the committed snapshot does not cover, in order (a crash between a
+            # cut and its commit leaves the rotated file of that cut)
+            for path in wal_files(snapshot_dir, committed_gen(snapshot_dir) if group is None else 0):
+                Wal.repair(path)
+                for ids, pls, vecs in Wal.replay(path, dim):
+                    self._upsert_nolog(ids, vecs, pls)
+                    m += len(ids)
+            self.boot_s = {"snapshot_load_s": round(t1 - t0, 3),
+                           "wal_replay_s": round(time.perf_counter() - t1, 3)}
+            log.info("[INDEX_RESTORE] snapshot rows=%d (%.2fs), WAL replayed=%d (%.2fs)", n,
+                     t1 - t0, m, self.boot_s["wal_replay_s"])
             self.wal = Wal(os.path.join(snapshot_dir, "wal.log"), dim)
 
     @property
@@ -86,19 +100,68 @@ class VectorStore:
             if self.shard.device.type == "cuda":
                 torch.cuda.synchronize(self.shard.device)  # wait=true: searchable on return
             self._since_snapshot += len(point_ids)
-            if self.wal is not None and self._since_snapshot >= self.snapshot_every:
-                self.snapshot()
+            if (self.wal is not None and self._since_snapshot >= self.snapshot_every
+                    and not self.snapshot_running()):
+                # cut under the lock (O(rows since the last snapshot)), write in the background
+                self._start(self._cut_locked(), background=True)
 
-    def snapshot(self) -> None:
-        if not self.dir:
-            return
+    def snapshot_running(self) -> bool:
+        return self._bg is not None and self._bg.is_alive()
+
+    def flush(self) -> None:
+        """Wait for a background snapshot to commit."""
+        if self._bg is not None:
+            self._bg.join()
+            self._bg = None
+
+    def _cut_locked(self):
+        """The snapshot cut (caller holds ``_lock``): a group checkpoints collectively and
+        synchronously (every rank incremental), then the WAL restarts; a single shard captures its
+        changes and rotates the WAL, and returns the job that writes them."""
+        self._since_snapshot = 0
         if self.group is not None:
             self.group.snapshot(self.dir)
+            if self.wal is not None:
+                self.wal.truncate()
+            return None
+        return ShardPersister(self.dir).cut(
+            self.shard, rotate_wal=self.wal.rotate if self.wal is not None else None)
+
+    def _start(self, job, background: bool) -> None:
+        if job is None:
+            return
+
+        def run():
+            import time
+
+            t0 = time.perf_counter()
+            try:
+                job.write()
+                self.last_snapshot = {"gen": job.gen, "bytes": job.bytes_written,
+                                      "write_s": round(time.perf_counter() - t0, 3),
+                                      "rows": job.manifest["count"]}
+            except BaseException as e:  # noqa: BLE001 -- reported; the next snapshot is full
+                self.snapshot_error = e
+                self.shard._persist_key = None
+                log.error("[INDEX_SNAPSHOT] generation %d failed: %s", job.gen, e)
+        if background:
+            self._bg = threading.Thread(target=run, name="index-snapshot", daemon=True)
+            self._bg.start()
         else:
-            save_snapshot(self.shard, self.dir)
-        if self.wal is not None:
-            self.wal.truncate()
-        self._since_snapshot = 0
+            run()
+            if self.snapshot_error is not None:
+                e, self.snapshot_error = self.snapshot_error, None
+                raise e
+
+    def snapshot(self, wait: bool = True) -> None:
+        """Checkpoint now: incremental (rows, overwrites and payloads changed since the previous
+        snapshot); ``wait=False`` writes in the background."""
+        if not self.dir:
+            return
+        self.flush()
+        with self._lock:
+            job = self._cut_locked()
+        self._start(job, background=not wait)
 
     def search(self, queries: np.ndarray, k: int):
         """queries f32 [nq, D] (any norm) -> (scores f32 [nq, k'], rows int64 [nq, k']); -1 = empty."""
@@ -155,5 +218,6 @@ class VectorStore:
 
     def close(self) -> None:
         if self.wal is not None:
+            self.flush()
             self.snapshot()
             self.wal.close()

@@ -11,9 +11,11 @@ a short, fixed sequence of collectives, so all ranks stay in lockstep:
            header / query broadcast / scan of search i+1 queue behind search i's exchange while
            the caller of search i waits for its result outside the lock.
   UPSERT : header -> broadcast vectors [n, D] f32 + (owner rank, target row) -> owners write rows.
-  SNAPSHOT / LOAD : header -> every rank saves / loads its own shard under <dir>/rank<r>/ (raw rows,
-           index/persist.py format); rank 0 adds group.json (world, per-rank counts) and the
-           gid -> (point id, payload) table.  A load requires the same world size.
+  SNAPSHOT / LOAD : header -> every rank saves / loads its own shard under <dir>/rank<r>/
+           (index/persist.py: incremental segments of the rows written since the previous
+           snapshot); rank 0 adds group.json (world, per-rank counts) and a DELTA of the
+           gid -> (point id, payload) table (the gids upserted since, merged geometrically with
+           earlier deltas).  A load requires the same world size.
   STOP   : header only.
 Owner assignment is least-loaded-first, so shards stay balanced (the reference's Qdrant has a
 single shard: vector_memory_service/src/main.rs:50).  Global id = rank << 40 | row.
@@ -30,7 +32,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from ..index.shard import HbmIndexShard, Payload, dedupe_last
+from ..index.shard import HbmIndexShard, Payload, PayloadStore, dedupe_last
 from .dist import DistInfo
 from .sharded import RANK_SHIFT, encode_gid, merge_ranked
 
@@ -79,6 +81,10 @@ class IndexGroup:
         self.counts = [0] * info.world
         self.payload_by_gid: dict[int, tuple[str, Payload]] = {}
         self.gid_by_pid: dict[str, int] = {}
+        # gids upserted since the last group snapshot, and the (directory, generation) that
+        # record is relative to (another directory / generation: the next snapshot is full)
+        self._dirty_gids: set[int] = set()
+        self._group_key = None
         self.snapshot_root: str | None = None   # shared snapshot directory (all ranks)
         # rank 0: parallel/heartbeat.HeartbeatMonitor -- refuse ops while a peer is down
         self.liveness = None
@@ -189,30 +195,52 @@ class IndexGroup:
             self._commit_group(directory)
 
     def _commit_group(self, directory: str, _crash_before_commit: bool = False) -> None:
-        """The payload table goes to a NEW versioned file (fsync'd) that group.json names; the
-        atomic group.json replace is the one commit point for counts + payloads together, so a
-        crash can never pair a new payload table with old per-rank counts."""
-        from ..index.persist import fsync_dir, write_atomic
+        """The payload table's DELTA (gids upserted since the previous group snapshot; every gid
+        when that record does not belong to this directory's committed generation) goes to a NEW
+        versioned file, folded geometrically with the previous deltas (a delta absorbs its
+        predecessor while it holds at least half as many entries, read back from disk).  The
+        atomic group.json replace is the one commit point for counts + payload files together,
+        so a crash can never pair new payloads with old per-rank counts."""
+        from ..index.persist import fsync_dir, merge_payload_files, write_atomic, write_payloads
 
         prev = self._group_meta(directory)
         gen = (prev or {}).get("gen", 0) + 1
-        name = f"group_payloads.{gen}.jsonl"
-        path = os.path.join(directory, name)
-        with open(path, "w", encoding="utf-8") as f:
-            for g, (pid, p) in self.payload_by_gid.items():
-                f.write(json.dumps([g, pid, p.original_document_id, p.source_url, p.sentence_text,
-                                    p.sentence_order, p.model_name, p.processed_at_ms],
-                                   ensure_ascii=False) + "\n")
-            f.flush()
-            os.fsync(f.fileno())
+        incremental = (prev is not None and prev.get("format") == 3
+                       and self._group_key == (os.path.abspath(directory), prev["gen"]))
+        files = [dict(f) for f in prev["payload_files"]] if incremental else []
+        gids = sorted(self._dirty_gids) if incremental else sorted(self.payload_by_gid)
+        entries = []
+        for g in gids:
+            pid, p = self.payload_by_gid.get(g, (None, None))
+            entries.append((pid, None if p is None else tuple(getattr(p, f)
+                                                                for f in PayloadStore.FIELDS)))
+        m, merge = len(gids), []
+        while files and 2 * m >= files[-1]["m"]:
+            last = files.pop()
+            merge.insert(0, last["gen"])
+            m += last["m"]
+        if gids or merge:
+            tmp = os.path.join(directory, f"group_pay.{gen}.delta")
+            write_payloads(tmp, np.asarray(gids, dtype=np.int64), entries)
+            out = os.path.join(directory, f"group_pay.{gen}.bin")
+            if merge:
+                m = merge_payload_files([os.path.join(directory, f"group_pay.{x}.bin")
+                                         for x in merge] + [tmp], out)
+                os.remove(tmp)
+            else:
+                os.replace(tmp, out)
+            files.append({"gen": gen, "m": m})
         fsync_dir(directory)
         if _crash_before_commit:
             return
-        meta = {"world": self.info.world, "counts": self.counts, "dim": self.dim, "format": 2,
-                "gen": gen, "payloads": name}
+        meta = {"world": self.info.world, "counts": self.counts, "dim": self.dim, "format": 3,
+                "gen": gen, "payload_files": files}
         write_atomic(os.path.join(directory, "group.json"), json.dumps(meta).encode())
-        for fn in os.listdir(directory):   # committed: older tables are garbage
-            if fn.startswith("group_payloads") and fn != name:
+        self._dirty_gids = set()
+        self._group_key = (os.path.abspath(directory), gen)
+        keep = {f"group_pay.{f['gen']}.bin" for f in files}
+        for fn in os.listdir(directory):   # committed: unreferenced tables are garbage
+            if (fn.startswith("group_pay") or fn.startswith("group_payloads")) and fn not in keep:
                 os.remove(os.path.join(directory, fn))
 
     @staticmethod
@@ -239,18 +267,36 @@ class IndexGroup:
         self.counts = list(meta["counts"])
         self.payload_by_gid.clear()
         self.gid_by_pid.clear()
-        # format 1 (one unversioned table) is still read; either way entries past a rank's
-        # committed row count are dropped, so a table newer than the counts cannot leave gids
-        # pointing beyond a shard
-        name = meta.get("payloads", "group_payloads.jsonl")
-        with open(os.path.join(directory, name), encoding="utf-8") as f:
-            for line in f:
-                a = json.loads(line)
-                g = a[0]
-                if (g & ((1 << RANK_SHIFT) - 1)) >= self.counts[g >> RANK_SHIFT]:
-                    continue
-                self.payload_by_gid[g] = (a[1], Payload(*a[2:]))
-                self.gid_by_pid[a[1]] = g
+
+        def put(g, pid, p):
+            # entries past a rank's committed row count are dropped, so a table newer than the
+            # counts cannot leave gids pointing beyond a shard
+            if (g & ((1 << RANK_SHIFT) - 1)) >= self.counts[g >> RANK_SHIFT]:
+                return
+            old = self.payload_by_gid.get(g)
+            if old is not None and self.gid_by_pid.get(old[0]) == g:
+                del self.gid_by_pid[old[0]]
+            if pid is None:
+                self.payload_by_gid.pop(g, None)
+                return
+            self.payload_by_gid[g] = (pid, p)
+            self.gid_by_pid[pid] = g
+
+        if meta.get("format") == 3:   # binary deltas, applied in generation order
+            from ..index.persist import read_payloads
+
+            for fdesc in meta["payload_files"]:
+                keys, ents = read_payloads(os.path.join(directory, f"group_pay.{fdesc['gen']}.bin"))
+                for g, (pid, f) in zip(keys.tolist(), ents):
+                    put(g, pid, Payload(*f) if f is not None else Payload())
+            self._group_key = (os.path.abspath(directory), meta["gen"])
+        else:   # formats 1 / 2: one JSON-lines table
+            name = meta.get("payloads", "group_payloads.jsonl")
+            with open(os.path.join(directory, name), encoding="utf-8") as f:
+                for line in f:
+                    a = json.loads(line)
+                    put(a[0], a[1], Payload(*a[2:]))
+        self._dirty_gids = set()
         return sum(self.counts)
 
     def snapshot_dir_exists(self, directory: str) -> bool:
@@ -313,6 +359,8 @@ class IndexGroup:
         for pid, g, p in zip(point_ids, gids, payloads):
             self.payload_by_gid[g] = (pid, p)
             self.gid_by_pid[pid] = g
+        if self.snapshot_root is not None or self._group_key is not None:
+            self._dirty_gids.update(gids)
         return gids
 
     def payload(self, gid: int) -> tuple[str | None, Payload]:

@@ -40,17 +40,25 @@ def test_upsert_overwrites_existing_ids():
         st.upsert(["x"], _vecs(1, 5), [Payload()])
 
 
+def _files(d, prefix=("manifest", "seg", "patch", "pay", "wal", "snapshot")):
+    return sorted(n for n in os.listdir(d) if n.split(".")[0] in prefix)
+
+
 def test_snapshot_wal_resume_and_torn_tail(tmp_path):
     d = str(tmp_path / "idx")
     st = VectorStore(8, 1000, device="cpu", snapshot_dir=d, snapshot_every=10)
     v = _vecs(25, 8, 1)
-    for i in range(0, 25, 5):   # 25 points: snapshot at 10 and 20, 5 rows left in the WAL
+    for i in range(0, 25, 5):   # 25 points: snapshots at 10 and 20, 5 rows left in the WAL
         st.upsert([f"p{j}" for j in range(i, i + 5)], v[i:i + 5],
                   [Payload(f"doc{j}", "u", f"s{j}", j, "m", 100 + j) for j in range(i, i + 5)])
-    from codename_symbiont_amd.index.persist import committed_snapshot
+        st.flush()                                    # background snapshots, one at a time
+    from codename_symbiont_amd.index.persist import committed_manifest
 
-    assert os.path.exists(os.path.join(committed_snapshot(d), "vectors.npy"))
-    assert sorted(n for n in os.listdir(d) if n.startswith("snapshot")) == ["snapshot.2"]
+    man = committed_manifest(d)
+    assert man["gen"] == 2 and man["count"] == 20
+    # generation 2 absorbed generation 1 (10 new rows >= half of 10): one segment, one delta,
+    # the rotated WALs both generations covered are gone
+    assert _files(d) == ["manifest.2.json", "pay.2.bin", "seg.2.npy", "wal.log"]
     st.wal.close()  # crash: no close() snapshot
     with open(os.path.join(d, "wal.log"), "ab") as f:   # torn record at the tail
         f.write(b"SYMB\x05\x00\x00\x00garbage")
@@ -78,43 +86,155 @@ def _store_with(d, n, seed=1, snapshot_every=1 << 30):
 def test_snapshot_crash_before_commit_keeps_previous_generation(tmp_path):
     """A crash after the new generation is written but before CURRENT moves: the boot loads the
     previous committed generation and replays the (untruncated) WAL -- nothing is lost, and the
-    next snapshot still succeeds over the leftover directory."""
+    next snapshot still succeeds over the leftover files (and removes them)."""
     from codename_symbiont_amd.index import persist
 
     d = str(tmp_path / "idx")
     st, v = _store_with(d, 10)
-    st.snapshot()                                     # gen 1 committed, WAL empty
+    st.snapshot()                                     # gen 1 committed, its WAL deleted
     more = _vecs(5, 8, 9)
     st.upsert([f"q{j}" for j in range(5)], more, [Payload("dq")] * 5)   # in the WAL only
     persist.save_snapshot(st.shard, d, _crash_before_commit=True)       # gen 2 uncommitted
-    st.wal.close()                                    # crash: WAL not truncated
-    assert open(os.path.join(d, "CURRENT")).read().strip() == "snapshot.1"
+    st.wal.close()                                    # crash
+    assert open(os.path.join(d, "CURRENT")).read().strip() == "manifest.1.json"
     st2 = VectorStore(8, 1000, device="cpu", snapshot_dir=d)
     assert st2.count == 15
     s, r = st2.search(more[3], 1)
     assert st2.lookup(r[0, 0])[0] == "q3"
-    st2.snapshot()                                    # gen 3 commits; 1 and 2 are removed
-    assert sorted(n for n in os.listdir(d) if n.startswith("snapshot")) == ["snapshot.3"]
+    st2.snapshot()                                    # gen 3 commits; gens 1 and 2 are removed
+    assert _files(d) == ["manifest.3.json", "pay.3.bin", "seg.3.npy", "wal.log"]
     st2.wal.close()
     assert VectorStore(8, 1000, device="cpu", snapshot_dir=d).count == 15
 
 
+def _write_legacy(sh, d, name="snapshot.1"):
+    """The round-2 full-rewrite format (meta.json + vectors.npy + payloads.jsonl)."""
+    import json
+
+    p = os.path.join(d, name)
+    os.makedirs(p)
+    with open(os.path.join(p, "meta.json"), "w") as f:
+        json.dump({"dim": sh.dim, "count": sh.count, "format": 1, "dtype": "bf16"}, f)
+    np.save(os.path.join(p, "vectors.npy"),
+            sh.rows[:sh.count].view(torch.int16).numpy().view(np.uint16))
+    with open(os.path.join(p, "payloads.jsonl"), "w") as f:
+        for r in range(sh.count):
+            pid, pl = sh.payloads.get(r)
+            f.write(json.dumps([pid, pl.original_document_id, pl.source_url, pl.sentence_text,
+                                pl.sentence_order, pl.model_name, pl.processed_at_ms]) + "\n")
+
+
 def test_snapshot_legacy_layout_and_interrupted_swap(tmp_path):
-    """Directories written by the old two-rename swap still load: ``snapshot/``, or only
-    ``snapshot.old`` when a crash hit between the two renames."""
+    """Directories written by the previous formats still load: ``snapshot.<gen>`` named by
+    CURRENT, or (pre-pointer) ``snapshot.old`` when a crash hit the old two-rename swap; the
+    next snapshot writes the incremental format and removes the legacy directories."""
     from codename_symbiont_amd.index import persist
 
     d = str(tmp_path / "idx")
+    os.makedirs(d)
     sh = HbmIndexShard(8, 100, device="cpu")
-    sh.append_f32(torch.from_numpy(_vecs(7, 8)))
-    persist.save_snapshot(sh, d)
+    sh.upsert([f"a{i}" for i in range(7)], torch.from_numpy(_vecs(7, 8)),
+              [Payload(f"d{i}") for i in range(7)])
+    _write_legacy(sh, d)
+    with open(os.path.join(d, "CURRENT"), "w") as f:
+        f.write("snapshot.1\n")
+    sh1 = HbmIndexShard(8, 100, device="cpu")
+    assert persist.load_snapshot(sh1, d) == 7 and sh1.payloads.get(3)[0] == "a3"
     os.remove(os.path.join(d, "CURRENT"))
     os.rename(os.path.join(d, "snapshot.1"), os.path.join(d, "snapshot.old"))
     sh2 = HbmIndexShard(8, 100, device="cpu")
     assert persist.load_snapshot(sh2, d) == 7
+    assert torch.equal(sh2.rows[:7], sh.rows[:7])
     persist.save_snapshot(sh2, d)                     # stale .old no longer blocks a snapshot
     assert not os.path.exists(os.path.join(d, "snapshot.old"))
-    assert persist.load_snapshot(HbmIndexShard(8, 100, device="cpu"), d) == 7
+    sh3 = HbmIndexShard(8, 100, device="cpu")
+    assert persist.load_snapshot(sh3, d) == 7 and sh3.payloads.get(6)[1].original_document_id == "d6"
+
+
+def test_incremental_snapshot_cost_follows_new_rows(tmp_path):
+    """5M-row shard: the first snapshot writes every row; the next one, after 10k new points and
+    50 overwrites of old rows, writes only those (one segment, one patch, one payload delta) --
+    its bytes and time follow the rows written since, not the shard.  Boot applies segment,
+    patch and delta in generation order and reproduces the shard exactly."""
+    import time
+
+    from codename_symbiont_amd.index import persist
+
+    D, N, NEW = 64, 5_000_000, 10_000
+    d = str(tmp_path / "big")
+    sh = HbmIndexShard(D, N + NEW, device="cpu")
+    sh.fill_random(N, seed=3)
+    t0 = time.perf_counter()
+    j1 = persist.save_snapshot(sh, d)
+    full_s = time.perf_counter() - t0
+    assert j1.bytes_written >= N * D * 2
+    rng = np.random.default_rng(0)
+    v = rng.standard_normal((NEW, D)).astype(np.float32)
+    sh.upsert([f"n{i}" for i in range(NEW)], torch.from_numpy(v),
+              [Payload(f"doc{i}", "u", f"t{i}", i) for i in range(NEW)])
+    old = rng.choice(N, 50, replace=False)
+    sh.write_rows_f32(np.sort(old), torch.from_numpy(rng.standard_normal((50, D)).astype(np.float32)))
+    t0 = time.perf_counter()
+    j2 = persist.save_snapshot(sh, d)
+    inc_s = time.perf_counter() - t0
+    man = persist.committed_manifest(d)
+    assert [s["n"] for s in man["segments"]] == [N, NEW] and man["patches"][0]["m"] == 50
+    assert j2.bytes_written < (NEW + 50) * D * 2 * 2 + 4 * 1024 * 1024   # rows + payload delta
+    assert inc_s < full_s / 5, (inc_s, full_s)
+    t0 = time.perf_counter()
+    sh2 = HbmIndexShard(D, N + NEW, device="cpu")
+    assert persist.load_snapshot(sh2, d) == N + NEW
+    boot_s = time.perf_counter() - t0
+    assert torch.equal(sh2.rows[:N + NEW], sh.rows[:N + NEW])
+    assert sh2.payloads.get(N + 77)[1].sentence_text == "t77" and sh2.payloads.get(5)[0] is None
+    print(f"full {full_s:.2f}s, incremental {inc_s:.3f}s, boot {boot_s:.2f}s")
+
+
+def test_geometric_merges_bound_the_file_count(tmp_path):
+    from codename_symbiont_amd.index import persist
+
+    d = str(tmp_path / "m")
+    sh = HbmIndexShard(8, 5000, device="cpu")
+    v = _vecs(3000, 8, 4)
+    for i in range(0, 3000, 100):
+        sh.upsert([f"p{j}" for j in range(i, i + 100)], torch.from_numpy(v[i:i + 100]),
+                  [Payload(f"d{j}") for j in range(i, i + 100)])
+        persist.save_snapshot(sh, d)
+        man = persist.committed_manifest(d)
+        assert len(man["segments"]) <= 8 and len(man["payloads"]) <= 8
+        assert sum(s["n"] for s in man["segments"]) == sh.count
+    sh2 = HbmIndexShard(8, 5000, device="cpu")
+    assert persist.load_snapshot(sh2, d) == 3000
+    assert torch.equal(sh2.rows[:3000], sh.rows[:3000])
+    assert all(sh2.payloads.get(r)[0] == f"p{r}" for r in range(0, 3000, 37))
+
+
+def test_background_snapshot_does_not_block_upserts(tmp_path, monkeypatch):
+    import threading
+    import time
+
+    from codename_symbiont_amd.index import persist
+
+    d = str(tmp_path / "bg")
+    st, v = _store_with(d, 50)
+    release = threading.Event()
+    real = persist.SnapshotJob.write
+
+    def slow(self, **kw):
+        release.wait(10)
+        return real(self, **kw)
+    monkeypatch.setattr(persist.SnapshotJob, "write", slow)
+    st.snapshot(wait=False)                           # cut taken; the write is held back
+    assert st.snapshot_running()
+    t0 = time.perf_counter()
+    st.upsert(["late"], _vecs(1, 8, 8), [Payload("dl")])   # not blocked by the snapshot
+    assert time.perf_counter() - t0 < 1.0 and st.snapshot_running()
+    release.set()
+    st.flush()
+    assert persist.committed_manifest(d)["count"] == 50   # the cut, not the later upsert
+    st.wal.close()
+    st2 = VectorStore(8, 1000, device="cpu", snapshot_dir=d)
+    assert st2.count == 51 and st2.lookup(50)[0] == "late"
 
 
 def test_upsert_duplicate_ids_in_one_batch_last_wins():

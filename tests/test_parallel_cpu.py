@@ -252,7 +252,7 @@ def _group_snapshot_worker(rank, world, port, snap, phase, out, crash_mid=False)
 
 @pytest.mark.parametrize("crash_mid", [False, True], ids=["clean", "crash_mid_snapshot"])
 def test_index_group_snapshot_restore(tmp_path, crash_mid):
-    from codename_symbiont_amd.index.persist import committed_snapshot
+    from codename_symbiont_amd.index.persist import committed_manifest
 
     world = 2
     snap = str(tmp_path / "snap")
@@ -263,8 +263,14 @@ def test_index_group_snapshot_restore(tmp_path, crash_mid):
                            args=(world, _free_port(), snap, phase, out, crash_mid),
                            nprocs=world, join=True, start_method="spawn")
     assert os.path.exists(os.path.join(snap, "group.json"))
-    assert os.path.exists(os.path.join(committed_snapshot(os.path.join(snap, "rank1")),
-                                       "vectors.npy"))
+    man = committed_manifest(os.path.join(snap, "rank1"))
+    assert man is not None and all(os.path.exists(os.path.join(snap, "rank1", f"seg.{s['gen']}.npy"))
+                                   for s in man["segments"])
+    import json
+
+    meta = json.load(open(os.path.join(snap, "group.json")))
+    assert meta["format"] == 3 and all(os.path.exists(os.path.join(snap, f"group_pay.{f['gen']}.bin"))
+                                       for f in meta["payload_files"])
     assert out[(0, 0)] == 200 and out[(1, 0)] == 200      # 150 from the snapshot + 50 from the WAL
     assert out[(1, 1)] == 100                             # rank 1's shard restored, then WAL rows
     assert out["texts"] == ["t10", "t170", "t3-new"]
