@@ -414,9 +414,15 @@ class HbmIndexShard:
         if NQ == 0 or k <= 0:
             return (torch.empty(NQ, max(k, 0), device=self.device),
                     torch.empty(NQ, max(k, 0), dtype=torch.int32, device=self.device))
-        if self.device.type != "cuda" or k > 32:
+        if self.device.type != "cuda" or k > self.K_MAX_HIP:
             return self._search_matmul(q_unit, k)
         q_unit = q_unit.to(torch.bfloat16).contiguous()
+        if k > 16 and not self.prefilter:
+            out = self._search_large_k(q_unit, k, n_cus)
+            if out is not None:
+                return out
+            if k > 32:
+                return self._search_matmul(q_unit, k)
         if self.prefilter and k < 32:
             return self._search_prefilter(q_unit, k, n_cus)
         if self.prune and k <= 16 and NQ >= self.mq_min_nq and self._seed_rows(self.visible, k):
@@ -617,7 +623,7 @@ class HbmIndexShard:
     # 256 held-out queries emitted 6k (profiles/r3_real/); slots cost memory only (the re-score
     # and select walk the emitted count), 256 MiB at 1024 queries
     PRUNE_CAP = 32768
-    SAMPLE_CAP = 16384        # the pruned search's sample emits down to thr0 - margin
+    SAMPLE_CAP = 16384        # candidate slots per query of the sampled searches' sample scan
 
     # route the batch to the bf16 emitting scan when the sample predicts more than this share of
     # PRUNE_CAP int8 candidates for some query (estimate c << ts has a ~sqrt(c) << ts spread)
@@ -630,9 +636,9 @@ class HbmIndexShard:
         emitted, re-scored in bf16 and the top-k of those is returned.  A query whose candidates
         overflow PRUNE_CAP raises the flag that gates the exact bf16 list scan.
 
-        Route (decided on the GPU from the same sample, no host sync): the sample is emitted down
-        to thr0 - margin, so counting its rows at or above T - margin estimates each query's int8
-        candidates.  On data whose scores crowd the k-th best (an anisotropic corpus: every pair
+        Route (decided on the GPU from the same sample, no host sync): counting the sample's
+        emitted rows at or above T - margin (extrapolated when that band reaches below the
+        sample's seed threshold) estimates each query's int8 candidates.  On data whose scores crowd the k-th best (an anisotropic corpus: every pair
         of rows at cosine ~0.3) that estimate exceeds the buffer, and the batch takes the bf16
         emitting scan with the exact threshold T instead of an int8 pass that would overflow and
         then pay the full fallback scan on top (profiles/r3_real/)."""
@@ -655,15 +661,14 @@ class HbmIndexShard:
         h.prune_qquant(q_unit.data_ptr(), NQ, self.dim, self.i8_bounds.data_ptr(), q8.data_ptr(),
                        sq.data_ptr(), margin.data_ptr(), st)
         # 1. T: the k-th best exact score of a sample of real rows (1 tile in 2^ts, plus the last
-        #    4096+ rows where fresh inserts sit), as in _search_scan; the sample emits down to
-        #    thr0 - margin so that it also counts the rows inside the int8 band
+        #    4096+ rows where fresh inserts sit), as in _search_scan; its emitted candidates also
+        #    estimate the int8 band's population (prune_route)
         ts, nv, t0, idx = plan
         sub = torch.index_select(self.rows, 0, idx)
         pm = self.prepass_min_tiles
         s0, _ = self._scan(sub.shape[0], q_unit, kmax, k, None, n_cus, sub, "bf16", min_tiles=pm)
         thr0 = s0[:, k - 1].contiguous() - self.MQ_THR_MARGIN
-        thr_band = (thr0 - margin).contiguous()
-        pre_s, _, cs_p, cnt_p = self._scan_mq(nv * TILE_ROWS, q_unit, kmax, k, thr_band, n_cus,
+        pre_s, _, cs_p, cnt_p = self._scan_mq(nv * TILE_ROWS, q_unit, kmax, k, thr0, n_cus,
                                               tshift=ts, fallback=False, cand=True,
                                               cap=self.SAMPLE_CAP)
         tail_s, _ = self._scan(n - t0, q_unit, kmax, k, thr0, n_cus, self.rows[t0:], "bf16",
@@ -675,7 +680,8 @@ class HbmIndexShard:
         dense = torch.empty(1, dtype=torch.int32, device=dev)
         limit = int(self.PRUNE_DENSE_FRAC * cap) if self.prune_route else 1 << 62
         h.prune_route(NQ, pre_s.data_ptr(), tail_s.data_ptr(), k, self.MQ_THR_MARGIN,
-                      sq.data_ptr(), margin.data_ptr(), cs_p.data_ptr(), cnt_p.data_ptr(),
+                      sq.data_ptr(), margin.data_ptr(), thr0.data_ptr(), cs_p.data_ptr(),
+                      cnt_p.data_ptr(),
                       self.SAMPLE_CAP, ts, limit, T.data_ptr(), thr.data_ptr(), dense.data_ptr(),
                       st)
         # 3. int8 route: emit every row with (q8 . x8) * sx >= thr, 4. exact bf16 re-score,
@@ -726,6 +732,48 @@ class HbmIndexShard:
         E, X = self.i8_bounds[0], self.i8_bounds[1]
         margin = q_unit.float().norm(dim=1) * E + eq * X + 1e-5
         return T, q8, sq, ((T - margin) / sq).contiguous()
+
+    K_MAX_HIP = 128          # top_k up to this runs on the HIP scans (radix select); above: matmul
+    LARGE_K_CAP = 16384      # candidate slots per query of the large-k emitting scan
+
+    def _search_large_k(self, q_unit, k: int, n_cus):
+        """EXACT top-k for 16 < k <= 128 on a 384-wide bf16 shard: T = the k-th best exact score
+        of a 1-in-32 tile sample of real rows (seeded from a 1-in-2048 sub-sample scored by an
+        fp32 GEMM) plus the fresh-row tail, then the bf16 emitting scan keeps every row scoring
+        >= T (a lower bound on each query's final k-th score), and the radix select
+        (topk_select_radix_kernel) takes each query's top k.  A query whose candidates overflow
+        LARGE_K_CAP sends the batch to the exact chunked GEMM (host check; rare).  None when the
+        shard is too small or not 384-wide bf16 (the caller takes the list scan / GEMM)."""
+        n, NQ = self.visible, q_unit.shape[0]
+        if self.dtype != "bf16" or self.dim != 384 or not self.scan_mq or k > self.K_MAX_HIP:
+            return None
+        if n < self.SEED_MIN_ROWS:
+            return None
+        plan = self._tile_sample_plan(n, self.PRUNE_TILE_SHIFT)
+        if plan is None:
+            return None
+        ts, nv, t0, idx = plan
+        if idx.numel() < k or n - t0 < 1:
+            return None
+        if n_cus is None:
+            n_cus = self._n_cus()
+        qf = q_unit.float()
+        sub = torch.index_select(self.rows, 0, idx)
+        s0 = torch.topk(qf @ sub.float().t(), k, dim=1).values
+        thr0 = (s0[:, k - 1] - self.MQ_THR_MARGIN).contiguous()
+        pre_s, _ = self._scan_mq(nv * TILE_ROWS, q_unit, 128, k, thr0, n_cus, tshift=ts,
+                                 fallback=False, cap=self.SAMPLE_CAP)
+        ts_ = qf @ self.rows[t0:n].float().t()
+        kk = min(k, n - t0)
+        tail_s = torch.topk(ts_, kk, dim=1).values
+        T = torch.topk(torch.cat([pre_s, tail_s], 1), k, dim=1).values[:, k - 1]
+        T = (T - self.MQ_THR_MARGIN).contiguous()
+        out_s, out_i = self._scan_mq(n, q_unit, 128, k, T, n_cus, fallback=False,
+                                     cap=self.LARGE_K_CAP)
+        _, ovf = self._mq_last
+        if int(ovf.item()):
+            return self._search_matmul(q_unit, k)
+        return out_s, out_i
 
     def _search_prefilter(self, q_unit, k: int, n_cus):
         """fp8 scan for oversample*k candidates, exact bf16 re-score, top-k (see the class doc)."""

@@ -17,10 +17,12 @@ with <cache> = $HF_HUB_CACHE | $HUGGINGFACE_HUB_CACHE | $HF_HOME/hub | ~/.cache/
 real config, weights and tokenizer; otherwise the built-in families fall back to their
 deterministic synthetic vocabulary and seeded random weights (models/config.py).
 
-sentence-transformers metadata is honoured when present: ``modules.json`` (a Normalize module ->
-L2-normalised output), ``1_Pooling/config.json`` (CLS vs mean pooling) and
-``sentence_bert_config.json`` (max_seq_length).  Without it the reference's behaviour applies:
-masked mean pooling, no normalisation (embedding_generator.rs:201-207).
+Pooling follows the reference by default: masked mean pooling, no normalisation, whatever the
+snapshot's sentence-transformers files say (embedding_generator.rs:201-207 always mean-pools and
+never normalises), so published vectors match the reference contract for every model.
+``SYMB_ST_POOLING=1`` opts in to the sentence-transformers metadata instead: ``modules.json`` (a
+Normalize module -> L2-normalised output) and ``1_Pooling/config.json`` (CLS vs mean pooling).
+``sentence_bert_config.json`` (max_seq_length) is always honoured.
 """
 from __future__ import annotations
 
@@ -126,6 +128,9 @@ def config_from_dir(d: Path, model_name: str, key: str = "") -> EncoderConfig:
         raise ValueError(f"{model_name}: hidden_act {act!r} unsupported (erf GELU only)")
     pad = int(c.get("pad_token_id", 0 if family == "bert" else 1) or 0)
     meta = _sentence_transformers_meta(d)
+    if os.environ.get("SYMB_ST_POOLING", "0") in ("", "0", "false", "False"):
+        meta.pop("pooling", None)       # the reference's mean pooling, no normalisation
+        meta.pop("normalize", None)
     H = int(c["hidden_size"])
     max_pos = int(c.get("max_position_embeddings", 512))
     offset = pad + 1 if family == "xlmr" else 0

@@ -72,9 +72,9 @@ int symb_index_scan_i8(const void* X8, const float* sx, int n_valid, int alloc_r
 int symb_prune_qquant(const void* Q, int NQ, int dim, const float* bounds, void* Q8, float* sq,
                       float* margin, hipStream_t st);
 int symb_prune_route(int NQ, const float* pre_s, const float* tail_s, int k, float thr_margin,
-                     const float* sq, const float* margin, const float* cs_p, const int* cnt_p,
-                     int cap_p, int tshift, long long limit, float* T, float* thr, int* dense,
-                     hipStream_t st);
+                     const float* sq, const float* margin, const float* thr0, const float* cs_p,
+                     const int* cnt_p, int cap_p, int tshift, long long limit, float* T,
+                     float* thr, int* dense, hipStream_t st);
 int symb_i8_config(int tile_rows, int waves);
 int symb_i8_tile_rows();
 int symb_i8_wgs_per_cu();
@@ -90,6 +90,7 @@ int symb_prune_qprep(const void* Q, int NQ, int dim, const float* pre_s, const f
                      float thr_margin, const float* bounds, void* Q8, float* sq, float* T,
                      float* thr, hipStream_t st);
 int symb_gemm_lt_config(int mode);
+int symb_gemm_lt_plans();
 int symb_mq_config(int aux);
 int symb_index_scan_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                        int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
@@ -376,12 +377,12 @@ PYBIND11_MODULE(_hip, m) {
           "prune_qquant");
   });
   m.def("prune_route", [](int NQ, uptr pre_s, uptr tail_s, int k, float thr_margin, uptr sq,
-                          uptr margin, uptr cs_p, uptr cnt_p, int cap_p, int tshift,
+                          uptr margin, uptr thr0, uptr cs_p, uptr cnt_p, int cap_p, int tshift,
                           long long limit, uptr T, uptr thr, uptr dense, uptr st) {
     check(symb_prune_route(NQ, P<const float>(pre_s), P<const float>(tail_s), k, thr_margin,
-                           P<const float>(sq), P<const float>(margin), P<const float>(cs_p),
-                           P<const int>(cnt_p), cap_p, tshift, limit, P<float>(T), P<float>(thr),
-                           P<int>(dense), S(st)),
+                           P<const float>(sq), P<const float>(margin), P<const float>(thr0),
+                           P<const float>(cs_p), P<const int>(cnt_p), cap_p, tshift, limit,
+                           P<float>(T), P<float>(thr), P<int>(dense), S(st)),
           "prune_route");
   });
   m.def("index_scan_i8_ablate", [](uptr X8, uptr sx, int n_valid, int alloc_rows,
@@ -418,6 +419,7 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("T"), py::arg("thr"), py::arg("stream"));
   m.def("gemm_lt_config", [](int mode) { check(symb_gemm_lt_config(mode), "gemm_lt_config"); },
         py::arg("mode"));
+  m.def("gemm_lt_plans", []() { return symb_gemm_lt_plans(); });
   m.def("mq_config", [](int aux) { check(symb_mq_config(aux), "mq_config"); }, py::arg("aux"));
   m.def("mq_queries_per_blk", [](int sets, int rsplit) { return symb_mq_queries_per_blk(sets, rsplit); },
         py::arg("sets") = 4, py::arg("rsplit") = 1);

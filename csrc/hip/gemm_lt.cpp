@@ -12,12 +12,16 @@
 // Layout: hipBLASLt is column-major, so the row-major product is computed as its transpose,
 // D^T[N,M] = op(W^T) . A^T with W^T read as a K x N column-major matrix (ld = ldw, transposed)
 // and A^T as K x M (ld = lda); bias is then a per-row vector of D^T (length N, fp32), and the
-// residual R enters as C with beta = 1.  One plan (descriptors + heuristic algorithm) per shape,
-// cached; one 64 MiB workspace per device.
+// residual R enters as C with beta = 1.  One plan (descriptors + heuristic algorithm) per shape;
+// the service's packed batches give a new M almost every call, so the cache is an LRU of
+// kMaxPlans plans per device whose evicted descriptors are destroyed (a plan miss costs one
+// heuristic query, ~tens of us, taken outside any stream capture); one 64 MiB workspace per
+// device.
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt.h>
 
 #include <cstdint>
+#include <list>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -25,18 +29,32 @@
 namespace {
 
 constexpr size_t kWorkspace = 64u << 20;
+constexpr size_t kMaxPlans = 64;
+
+using Key = std::tuple<int, int, int, int, int, int, int, int>;
 
 struct Plan {
   hipblasLtMatmulDesc_t desc = nullptr;
   hipblasLtMatrixLayout_t a = nullptr, b = nullptr, c = nullptr, d = nullptr;
   hipblasLtMatmulAlgo_t algo{};
   bool ok = false;
+  std::list<Key>::iterator lru;
 };
+
+void destroy_plan(Plan& p) {
+  if (p.a) hipblasLtMatrixLayoutDestroy(p.a);
+  if (p.b) hipblasLtMatrixLayoutDestroy(p.b);
+  if (p.c) hipblasLtMatrixLayoutDestroy(p.c);
+  if (p.d) hipblasLtMatrixLayoutDestroy(p.d);
+  if (p.desc) hipblasLtMatmulDescDestroy(p.desc);
+  p = Plan{};
+}
 
 struct DeviceState {
   hipblasLtHandle_t handle = nullptr;
   void* ws = nullptr;
-  std::map<std::tuple<int, int, int, int, int, int, int, int>, Plan> plans;
+  std::map<Key, Plan> plans;
+  std::list<Key> order;   // most recently used first
 };
 
 std::mutex g_mu;
@@ -113,10 +131,22 @@ int symb_gemm_lt(int epi, const void* A, int lda, const void* W, int ldw, const 
     LT_TRY(hipblasLtCreate(&ds.handle));
   }
   if (it == ds.plans.end()) {
+    while (ds.plans.size() >= kMaxPlans) {   // evict the least recently used plan
+      auto victim = ds.plans.find(ds.order.back());
+      ds.order.pop_back();
+      if (victim != ds.plans.end()) {
+        destroy_plan(victim->second);
+        ds.plans.erase(victim);
+      }
+    }
     Plan p;
     const int rc = make_plan(ds, p, res, M, N, K, lda, ldw, ldr, ldc);
+    ds.order.push_front(key);
+    p.lru = ds.order.begin();
     it = ds.plans.emplace(key, p).first;
     if (rc != 0) return rc;
+  } else {
+    ds.order.splice(ds.order.begin(), ds.order, it->second.lru);
   }
   Plan& p = it->second;
   if (!p.ok) return -1;
@@ -126,4 +156,13 @@ int symb_gemm_lt(int epi, const void* A, int lda, const void* W, int ldw, const 
   LT_TRY(hipblasLtMatmul(ds.handle, p.desc, &alpha, W, p.a, A, p.b, &beta, res ? R : C, p.c, C, p.d,
                          &p.algo, ds.ws, kWorkspace, st));
   return 0;
+}
+
+// Plans cached on the current device (tests: the cache stays bounded).
+int symb_gemm_lt_plans() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -1;
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = g_dev.find(dev);
+  return it == g_dev.end() ? 0 : (int)it->second.plans.size();
 }

@@ -641,9 +641,13 @@ __global__ __launch_bounds__(256) void prune_qprep_kernel(
 //   prune_route:  T = k-th best of (sample, tail) - thr_margin and thr = (T - margin) / sq (as
 //                 prune_qprep), plus the ROUTE: c = the sample rows (1 tile in 2^tshift) with an
 //                 exact score >= T - margin estimates the int8 scan's candidates as c << tshift.
-//                 If any query's estimate exceeds `limit` (or its sample buffer overflowed) the
-//                 int8 pass would overflow its buffer and pay the exact fallback on top (both full
-//                 scans): *dense = 1 routes the whole batch to the bf16 emitting scan instead.
+//                 The sample emitted every row >= thr0 (its seed threshold), so c is exact when
+//                 T - margin >= thr0; below thr0 the band holds at least the cnt rows >= thr0,
+//                 and, scores thinning out upwards, at least the density of [thr0, T] times the
+//                 band width: c = max(cnt, (cnt - k) * margin / (T - thr0)).  If any query's
+//                 estimate exceeds `limit` (or its sample buffer overflowed) the int8 pass would
+//                 overflow its buffer and pay the exact fallback on top (both full scans):
+//                 *dense = 1 routes the whole batch to the bf16 emitting scan instead.
 //                 Exactness never depends on the route; only the cost does.
 __global__ __launch_bounds__(256) void prune_qquant_kernel(const __bf16* __restrict__ Q, int NQ,
                                                            const float* __restrict__ bounds,
@@ -692,8 +696,8 @@ __global__ __launch_bounds__(256) void prune_qquant_kernel(const __bf16* __restr
 __global__ __launch_bounds__(256) void prune_route_kernel(
     int NQ, const float* __restrict__ pre_s, const float* __restrict__ tail_s, int k,
     float thr_margin, const float* __restrict__ sq, const float* __restrict__ margin,
-    const float* __restrict__ cs_p, const int* __restrict__ cnt_p, int cap_p, int tshift,
-    long long limit, float* __restrict__ T_out, float* __restrict__ thr,
+    const float* __restrict__ thr0, const float* __restrict__ cs_p, const int* __restrict__ cnt_p,
+    int cap_p, int tshift, long long limit, float* __restrict__ T_out, float* __restrict__ thr,
     int* __restrict__ dense) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int q = blockIdx.x * 4 + w;
@@ -713,14 +717,17 @@ __global__ __launch_bounds__(256) void prune_route_kernel(
   const int cnt = cnt_p[q];
   const int n = min(cnt, cap_p);
   const float band = T - m;
+  const float t0 = thr0[q];
   const float* cs = cs_p + (size_t)q * cap_p;
   float c = 0.f;
   for (int i = lane; i < n; i += 64) c += cs[i] >= band ? 1.f : 0.f;
   c = wave_sum(c);
+  if (band < t0)   // the band reaches below what the sample emitted: extrapolate (see above)
+    c = fmaxf((float)cnt, fmaxf(0.f, (float)(cnt - k)) * m / fmaxf(T - t0, 1e-6f));
   if (lane == 0) {
     T_out[q] = T;
     thr[q] = (T - m) / sq[q];
-    if (cnt > cap_p || ((long long)c << tshift) > limit) atomicOr(dense, 1);
+    if (cnt > cap_p || (double)c * (double)(1ll << tshift) > (double)limit) atomicOr(dense, 1);
   }
 }
 
@@ -875,14 +882,15 @@ int symb_prune_qquant(const void* Q, int NQ, int dim, const float* bounds, void*
 
 // dense (one int) is zeroed here, then raised by any query routed to the bf16 scan.
 int symb_prune_route(int NQ, const float* pre_s, const float* tail_s, int k, float thr_margin,
-                     const float* sq, const float* margin, const float* cs_p, const int* cnt_p,
-                     int cap_p, int tshift, long long limit, float* T, float* thr, int* dense,
-                     hipStream_t st) {
+                     const float* sq, const float* margin, const float* thr0, const float* cs_p,
+                     const int* cnt_p, int cap_p, int tshift, long long limit, float* T,
+                     float* thr, int* dense, hipStream_t st) {
   if (NQ <= 0) return 0;
   if (k < 1 || k > 32 || cap_p <= 0 || tshift < 0 || tshift > 20) return -1;
   hipError_t e = hipMemsetAsync(dense, 0, sizeof(int), st);
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(prune_route_kernel, dim3((NQ + 3) / 4), dim3(256), 0, st, NQ, pre_s, tail_s,
-                     k, thr_margin, sq, margin, cs_p, cnt_p, cap_p, tshift, limit, T, thr, dense);
+                     k, thr_margin, sq, margin, thr0, cs_p, cnt_p, cap_p, tshift, limit, T, thr,
+                     dense);
   return (int)hipGetLastError();
 }

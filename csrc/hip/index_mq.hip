@@ -443,6 +443,141 @@ __global__ __launch_bounds__(NTH) void topk_select_counted_kernel(
   }
 }
 
+// Top-k of each query's emitted candidates for ANY k <= SEL_MAX (the reference passes top_k
+// straight to Qdrant: vector_memory_service/src/main.rs:261-284).  One 256-thread workgroup per
+// query: an exact radix select of the k-th largest score over its candidates (3 passes of 11, 11
+// and 10 bits over an order-preserving uint32 image of the floats, LDS histograms, block-wide
+// suffix sums), then every score above it and as many equal ones as k needs are gathered into LDS
+// and bitonic-sorted descending.  Cost: 4 reads of the candidate list, independent of k.
+namespace sel {
+constexpr int NTH = 256;
+constexpr int SEL_MAX = 128;
+}  // namespace sel
+
+__device__ __forceinline__ uint32_t ord_key(float f) {
+  const uint32_t b = __float_as_uint(f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+
+__global__ __launch_bounds__(sel::NTH) void topk_select_radix_kernel(
+    const float* __restrict__ cand_s, const int* __restrict__ cand_i,
+    const int* __restrict__ cand_n, int cap, int k, float* __restrict__ out_s,
+    int* __restrict__ out_i, int* __restrict__ ovf, const int* __restrict__ gate) {
+  using namespace sel;
+  if (gate != nullptr && *gate == 0) return;   // (grid-uniform, before any barrier)
+  __shared__ uint32_t hist[2048];
+  __shared__ uint32_t part[NTH];
+  __shared__ uint32_t s_bin, s_above;
+  __shared__ float ss[SEL_MAX];
+  __shared__ int si[SEL_MAX];
+  __shared__ int n_gt, n_eq;
+  const int q = blockIdx.x, tid = threadIdx.x;
+  const int cnt = cand_n[q];
+  const int n = min(cnt, cap);
+  if (tid == 0 && cnt > cap) *ovf = 1;
+  const float* cs = cand_s + (size_t)q * cap;
+  const int* ci = cand_i + (size_t)q * cap;
+  uint32_t prefix = 0, mask = 0;
+  int remaining = k;     // rank of the wanted value among those matching the prefix so far
+  if (n > k) {
+    constexpr int SHIFT[3] = {21, 10, 0};
+    constexpr int BITS[3] = {11, 11, 10};
+#pragma unroll
+    for (int pass = 0; pass < 3; ++pass) {
+      const int nb = 1 << BITS[pass], sh = SHIFT[pass];
+      for (int b = tid; b < nb; b += NTH) hist[b] = 0;
+      __syncthreads();
+      for (int c = tid; c < n; c += NTH) {
+        const uint32_t key = ord_key(cs[c]);
+        if ((key & mask) == prefix) atomicAdd(&hist[(key >> sh) & (nb - 1)], 1u);
+      }
+      __syncthreads();
+      // suffix sums from the TOP bin down: thread t owns bins [t * per, (t + 1) * per)
+      const int per = nb / NTH;
+      uint32_t local = 0;
+      for (int j = 0; j < per; ++j) local += hist[tid * per + j];
+      part[tid] = local;
+      __syncthreads();
+      if (tid == 0) {
+        uint32_t above = 0;            // candidates in bins above the current thread's range
+        for (int t = NTH - 1; t >= 0; --t) {
+          if (above + part[t] >= (uint32_t)remaining) {
+            for (int j = per - 1; j >= 0; --j) {
+              const uint32_t h = hist[t * per + j];
+              if (above + h >= (uint32_t)remaining) {
+                s_bin = (uint32_t)(t * per + j);
+                s_above = above;
+                break;
+              }
+              above += h;
+            }
+            break;
+          }
+          above += part[t];
+        }
+      }
+      __syncthreads();
+      prefix |= s_bin << sh;
+      mask |= (uint32_t)(nb - 1) << sh;
+      remaining -= (int)s_above;
+      __syncthreads();
+    }
+  }
+  // gather: every value above the k-th, then `remaining` values equal to it (n <= k: all)
+  if (tid == 0) {
+    n_gt = 0;
+    n_eq = 0;
+  }
+  for (int j = tid; j < SEL_MAX; j += NTH) {
+    ss[j] = -INFINITY;
+    si[j] = -1;
+  }
+  __syncthreads();
+  const int take_gt = n > k ? k - remaining : n;
+  for (int c = tid; c < n; c += NTH) {
+    const float v = cs[c];
+    const uint32_t key = ord_key(v);
+    if (n <= k || key > prefix) {
+      const int pos = atomicAdd(&n_gt, 1);
+      if (pos < SEL_MAX) {
+        ss[pos] = v;
+        si[pos] = ci[c];
+      }
+    } else if (key == prefix) {
+      const int e = atomicAdd(&n_eq, 1);
+      if (e < remaining) {
+        ss[take_gt + e] = v;
+        si[take_gt + e] = ci[c];
+      }
+    }
+  }
+  __syncthreads();
+  // bitonic sort of SEL_MAX entries, descending (ties: lower row first)
+  for (int size = 2; size <= SEL_MAX; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = tid; t < SEL_MAX / 2; t += NTH) {
+        const int lo = 2 * t - (t & (stride - 1));
+        const int hi = lo + stride;
+        const bool desc = (lo & size) == 0;
+        const float a = ss[lo], b = ss[hi];
+        const int ia = si[lo], ib = si[hi];
+        const bool a_first = a > b || (a == b && (unsigned)ia <= (unsigned)ib);
+        if (a_first != desc) {
+          ss[lo] = b;
+          ss[hi] = a;
+          si[lo] = ib;
+          si[hi] = ia;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int j = tid; j < k; j += NTH) {
+    out_s[(size_t)q * k + j] = ss[j];
+    out_i[(size_t)q * k + j] = si[j];
+  }
+}
+
 }  // namespace symb
 
 using namespace symb;
@@ -562,7 +697,10 @@ int symb_topk_select_counted(const float* cand_s, const int* cand_i, const int* 
     hipError_t e = hipMemsetAsync(ovf, 0, sizeof(int), st);
     if (e != hipSuccess) return (int)e;
   }
-  if (kmax == 16)
+  if (kmax == sel::SEL_MAX)   // any k <= 128: radix select + bitonic sort
+    hipLaunchKernelGGL(topk_select_radix_kernel, dim3(NQ), dim3(sel::NTH), 0, st, cand_s, cand_i,
+                       cand_n, cap, k, out_s, out_i, ovf, gate);
+  else if (kmax == 16)
     hipLaunchKernelGGL((topk_select_counted_kernel<16, 256>), dim3(NQ), dim3(256), 0, st, cand_s,
                        cand_i, cand_n, cap, k, out_s, out_i, ovf, gate);
   else if (kmax == 32)

@@ -117,7 +117,7 @@ def hub(tmp_path, monkeypatch):
     return tmp_path / "hub"
 
 
-def test_snapshot_config_weights_tokenizer_match_hf(hub):
+def test_snapshot_config_weights_tokenizer_match_hf(hub, monkeypatch):
     from codename_symbiont_amd.text.tokenizer import Tokenizer
 
     _, n_vocab = _wordpiece_tokenizer_json(hub.parent / "probe.json")
@@ -126,17 +126,25 @@ def test_snapshot_config_weights_tokenizer_match_hf(hub):
     cfg = get_config("acme/tiny-bert")
     assert cfg.source_dir == str(snap) and cfg.model_name == "acme/tiny-bert"
     assert (cfg.hidden, cfg.layers, cfg.heads, cfg.ffn) == (64, 2, 2, 128)
-    assert cfg.pooling == "mean" and cfg.normalize and cfg.max_seq_len == 32 and cfg.lowercase
+    # the reference's contract by default: mean pooling, no normalisation, even though the
+    # snapshot's modules.json lists a Normalize module (embedding_generator.rs:201-207)
+    assert cfg.pooling == "mean" and not cfg.normalize and cfg.max_seq_len == 32 and cfg.lowercase
     texts = ["The quick brown fox jumps over the lazy dog!", "semantic search", "vectors, indexing?"]
     tok = Tokenizer(cfg)
     ids = [tok.encode(t) for t in texts]
     assert ids == [hf_tok.encode(t).ids for t in texts]
     enc = TorchEncoder(cfg)                       # weights come from the snapshot
     got = enc.forward_packed(pack_token_ids([np.array(i, np.int32) for i in ids], cfg))[0]
+    torch.testing.assert_close(got, _hf_pooled(m, ids, 0, "mean", False), atol=2e-4, rtol=2e-4)
+    monkeypatch.setenv("SYMB_ST_POOLING", "1")    # opt in to the sentence-transformers metadata
+    cfg = get_config("acme/tiny-bert")
+    assert cfg.normalize
+    got = TorchEncoder(cfg).forward_packed(pack_token_ids([np.array(i, np.int32) for i in ids], cfg))[0]
     torch.testing.assert_close(got, _hf_pooled(m, ids, 0), atol=2e-4, rtol=2e-4)
 
 
 def test_revisions_shards_and_local_dir(hub, monkeypatch):
+    monkeypatch.setenv("SYMB_ST_POOLING", "1")
     m = _bert(200)
     snap, _ = _write_snapshot(hub, "acme/sharded", m, tokenizer=False, normalize=False,
                               pooling="cls", shards=3, refs=("main", "v1"))

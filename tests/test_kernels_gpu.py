@@ -133,6 +133,28 @@ def test_gemm_hipblaslt_route(M, N, K, epi):
     _close(out, ref, atol=4e-2, rtol=2e-2, what=f"hipblaslt gemm epi={epi}")
 
 
+def test_gemm_hipblaslt_plan_cache_is_bounded():
+    """Packed service batches give a new M almost every call: the hipBLASLt plan cache stays an
+    LRU of 64 plans (evicted descriptors destroyed) and results stay right."""
+    from codename_symbiont_amd.ops._ext import hip
+    from codename_symbiont_amd.ops.kernels import gemm
+
+    N, K = 768, 768
+    w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=2)
+    bias = _f(N, scale=0.5, seed=3)
+    hip().gemm_lt_config(2)
+    try:
+        for M in range(4096, 4096 + 100 * 37, 37):
+            a = _bf(M, K, seed=M)
+            out = gemm(a, w, bias, 0)
+            assert hip().gemm_lt_plans() <= 64
+        ref = R.gemm_ref(a, w, bias, 0, None, None, None, 1e-12)
+    finally:
+        hip().gemm_lt_config(1)
+    _close(out, ref, atol=4e-2, rtol=2e-2, what="hipblaslt gemm after evictions")
+    assert hip().gemm_lt_plans() == 64
+
+
 @pytest.mark.parametrize("D,nh", [(32, 12), (64, 12), (64, 16)])
 @pytest.mark.parametrize("lens", [[1, 7, 64, 65, 128, 200, 3, 511],   # 64-key tiles
                                   [1, 7, 64, 65, 100, 128, 3],        # <=128: one 128-key tile
@@ -507,11 +529,12 @@ def test_prune_qquant_and_route_match_torch():
         cnt[j] = c + 3 if j < 200 else cap + 5
     T, thr = torch.empty(nq, device=DEV), torch.empty(nq, device=DEV)
     dense = torch.empty(1, dtype=torch.int32, device=DEV)
+    thr0 = (T0 - 3.0 * margin).contiguous()    # the sample emitted below the band: exact counts
 
-    def route(rows, limit):
+    def route(rows, limit, t0=thr0):
         h.prune_route(rows, pre.data_ptr(), tail.data_ptr(), k, shard.MQ_THR_MARGIN, sq.data_ptr(),
-                      margin.data_ptr(), cs.data_ptr(), cnt.data_ptr(), cap, ts, limit, T.data_ptr(),
-                      thr.data_ptr(), dense.data_ptr(), st)
+                      margin.data_ptr(), t0.data_ptr(), cs.data_ptr(), cnt.data_ptr(), cap, ts,
+                      limit, T.data_ptr(), thr.data_ptr(), dense.data_ptr(), st)
         torch.cuda.synchronize()
         return int(dense.item())
 
@@ -520,6 +543,10 @@ def test_prune_qquant_and_route_match_torch():
     assert route(nq, 1 << 40) == 1             # overflowed sample buffers always route dense
     assert torch.equal(T, T0)
     _close(thr, thr_t, atol=1e-4, rtol=1e-5, what="emission thresholds")
+    # seed threshold above the band: extrapolated from the density of [thr0, T]
+    # (query 60: cnt 63, (63 - 10) * m / (0.1 m) = 530 rows -> 530 << 5 = 16960)
+    high = (T0 - 0.1 * margin).contiguous()
+    assert route(61, 16000, high) == 1 and route(61, 17500, high) == 0
 
 
 @pytest.mark.parametrize("route", [True, False])
@@ -551,6 +578,68 @@ def test_index_pruned_search_routes_dense_data_exactly(route):
     assert int(ovf.item()) == (0 if route else 1)
     _close(s1, s0, atol=2e-5, what="routed pruned vs exact scores")
     assert (r0 == r1).float().mean().item() > 0.999
+
+
+@pytest.mark.parametrize("k", [1, 10, 17, 64, 100, 128])
+def test_topk_select_radix_matches_torch(k):
+    """topk_select_radix_kernel (any k <= 128): exact top-k of each query's candidate list vs
+    torch.topk -- coarse values (many ties), lists shorter than k (-inf padding), an overflowed
+    list (flag raised, first cap entries used), a gated-off launch."""
+    from codename_symbiont_amd.ops._ext import hip, stream_handle
+
+    nq, cap = 37, 3000
+    cs = _f(nq, cap, seed=101).round(decimals=2)
+    ci = torch.arange(nq * cap, dtype=torch.int32, device=DEV).view(nq, cap)
+    cnt = torch.randint(0, cap, (nq,), dtype=torch.int32, device=DEV)
+    cnt[0], cnt[1], cnt[2] = 0, min(k, 5), cap + 7       # empty, short, overflowed
+    out_s = torch.empty(nq, k, device=DEV)
+    out_i = torch.empty(nq, k, dtype=torch.int32, device=DEV)
+    ovf = torch.zeros(1, dtype=torch.int32, device=DEV)
+    hip().topk_select_counted(cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(), cap, nq, 128, k,
+                              out_s.data_ptr(), out_i.data_ptr(), ovf.data_ptr(), stream_handle())
+    torch.cuda.synchronize()
+    assert int(ovf.item()) == 1
+    for q in range(nq):
+        n = min(int(cnt[q]), cap)
+        ref = torch.full((k,), -math.inf, device=DEV)
+        if n:
+            v = torch.topk(cs[q, :n], min(k, n)).values
+            ref[:v.numel()] = v
+        assert torch.equal(out_s[q], ref), q
+        ok = out_i[q][torch.isfinite(ref)].long()
+        assert torch.equal(cs.view(-1)[ok], ref[torch.isfinite(ref)]), q   # ids point at them
+        assert ok.unique().numel() == ok.numel()
+        assert (out_i[q][~torch.isfinite(ref)] == -1).all()
+    gate = torch.zeros(1, dtype=torch.int32, device=DEV)
+    out_s.fill_(7.0)
+    hip().topk_select_counted(cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(), cap, nq, 128, k,
+                              out_s.data_ptr(), out_i.data_ptr(), ovf.data_ptr(), stream_handle(),
+                              gate=gate.data_ptr())
+    torch.cuda.synchronize()
+    assert (out_s == 7.0).all()
+
+
+@pytest.mark.parametrize("k", [17, 32, 64, 100, 128])
+@pytest.mark.parametrize("data", ["random", "clustered"])
+def test_index_large_k_search_is_exact(k, data):
+    """16 < k <= 128 on the HIP path (sampled threshold + bf16 emitting scan + radix select) ==
+    torch.topk over every row."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+    from codename_symbiont_amd.index.synth import CorpusGen, fill_corpus
+
+    n, nq = (1 << 20) + 999, 300
+    gen = CorpusGen(data, 384, DEV, clusters=2000, spread=0.6)
+    shard = HbmIndexShard(384, n, prune="i8")
+    fill_corpus(shard, gen, n, seed=12)
+    q = gen.unit(nq, seed=13).bfloat16()
+    s1, r1 = shard.search(q, k)
+    assert shard._mq_last is not None and r1.dtype == torch.int32
+    full = q.float() @ shard.unit_rows().float().t()
+    s0, r0 = torch.topk(full, k, dim=1)
+    torch.cuda.synchronize()
+    _close(s1, s0, atol=2e-5, what=f"top-{k} scores")
+    _close(full.gather(1, r1.long()), s0, atol=2e-5, what=f"top-{k} returned rows")
+    assert (r0.int() == r1).float().mean().item() > 0.99
 
 
 def test_index_scan_mq_overflow_falls_back_exact():
