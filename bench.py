@@ -178,6 +178,10 @@ def parse_args(argv=None):
     ap.add_argument("--prepass-min-tiles", type=int, default=0,
                     help="row-block floor of the sampled searches' small pre-pass list scans "
                          "(0 = the shard default, 1 tile per workgroup)")
+    ap.add_argument("--no-search-pipeline", action="store_true",
+                    help="--mode full: run each batch's query-side search work (int8 queries, "
+                         "exact sample, thresholds) right before its scan instead of on a third "
+                         "stream under the previous batch's scan")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch the encoder's kernels eagerly every step instead of replaying a "
                          "captured hipGraph of the forward")
@@ -538,8 +542,41 @@ def run_gpu(args, info, comm) -> int:
             enc_done[slot].record(enc_stream)
         prefetch(i + 1)
 
+    # --mode full, self queries: the search is pipelined too.  Batch i+1's query-side search
+    # work (upsert, int8 queries, the exact threshold sample, route) runs on pre_stream as soon
+    # as it is encoded, under batch i's full-shard scan; the compute stream only runs the scans
+    # back to back (ShardedSearcher.begin / end, HbmIndexShard.search_begin / search_end).
+    pipeline = overlap and args.queries == "self" and not args.no_search_pipeline
+    pre_stream = torch.cuda.Stream(dev)
+    pre_done = [torch.cuda.Event(), torch.cuda.Event()]
+    handles: dict = {}
+
+    def begin_search(i: int) -> None:
+        slot = i % 2
+        with torch.cuda.stream(pre_stream):
+            pre_stream.wait_event(enc_done[slot])
+            q = outs[slot][1]
+            shard.append_unit(q)
+            handles[i] = searcher.begin(q, args.k)
+            pre_done[slot].record(pre_stream)
+
+    def step_pipelined(i: int, ev=None) -> None:
+        slot = i % 2
+        encode_async(i + 1, ev)
+        begin_search(i + 1)
+        compute.wait_event(pre_done[slot])
+        if ev:
+            ev[2].record(compute)
+        searcher.end(handles.pop(i))
+        out_ring.consume(slot)
+        q_free[slot].record(compute)
+        if ev:
+            ev[3].record(compute)
+
     def step_overlap(i: int, ev=None) -> None:
         """Search batch i (encoded by the previous step) while batch i+1 encodes."""
+        if pipeline:
+            return step_pipelined(i, ev)
         slot = i % 2
         encode_async(i + 1, ev)
         compute.wait_event(enc_done[slot])
@@ -594,6 +631,8 @@ def run_gpu(args, info, comm) -> int:
     prefetch(0)
     if overlap:
         encode_async(0)
+        if pipeline:
+            begin_search(0)
     for i in range(W):
         step(i)
     torch.cuda.synchronize(dev)
@@ -678,6 +717,7 @@ def run_gpu(args, info, comm) -> int:
     metric, config, unit = metric_and_config(args, info, cfg, prune, prefilter, {
         "_group_dp": group_dp,
         "encode_search_overlap": overlap,
+        "search_pipeline": pipeline,
         # per-rank scan kernel: the emitting MFMA scan (csrc/hip/index_mq.hip) for >= 256
         # seeded queries (512 per workgroup at >= 512), else the 256-query list kernel
         "index_scan": (("int8-pruned-" if prune else "emitting-")

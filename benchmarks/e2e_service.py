@@ -288,6 +288,11 @@ def main():
                                  f"{a.api_impl} gateway x {a.api_workers} workers"},
         "endpoint": a.endpoint,
         "gateway_hops_ms": m.get("api_service", {}).get("latency_ms", {}),
+        # per-service stage timers (utils/trace.py) and counters: where each hop's time goes
+        "service_stages_ms": {svc: v.get("latency_ms", {})
+                              for svc, v in m.get("services", {}).items()},
+        "service_counters": {svc: v.get("counters", {})
+                             for svc, v in m.get("services", {}).items()},
         "data": "synthetic sentences over the synthetic vocabulary, random-init weights",
     }))
 

@@ -207,6 +207,10 @@ class HbmIndexShard:
         self.scan_cus = 0      # 0 = every CU (see _n_cus)
         self.scan_mq = True
         self.mq_min_nq = 256   # smallest batch for the emitting kernel (< 512: a 256-query form)
+        # smallest batch for the int8-pruned search: its scan costs about the same for 1..256
+        # queries (one 256-query block per row block), and a service's bursts under load are
+        # often smaller than 256 -- they would otherwise take the full bf16 list scan
+        self.prune_min_nq = 16
         # 256-query form: True = 4 query sets per wave, waves w / w + 4 splitting each tile's rows
         # (half the LDS fragment reads per tile); False = 2 sets per wave, every wave all rows
         self.mq_rsplit = True
@@ -425,7 +429,7 @@ class HbmIndexShard:
                 return self._search_matmul(q_unit, k)
         if self.prefilter and k < 32:
             return self._search_prefilter(q_unit, k, n_cus)
-        if self.prune and k <= 16 and NQ >= self.mq_min_nq and self._seed_rows(self.visible, k):
+        if self.prune and k <= 16 and NQ >= self.prune_min_nq and self._seed_rows(self.visible, k):
             out = self._search_pruned(q_unit, k, n_cus)
             if out is not None:
                 return out
@@ -433,6 +437,26 @@ class HbmIndexShard:
         if self.dtype == "fp8":
             out_s.mul_(1.0 / (FP8_SCALE * FP8_SCALE))
         return out_s, out_i
+
+    def search_begin(self, q_unit: torch.Tensor, k: int, n_cus: int | None = None) -> dict:
+        """First half of ``search`` for a pipelined caller: on the pruned path, the query-side
+        work (int8 queries, exact sample, thresholds, route) runs now on the current stream and
+        ``search_end`` runs the full-shard scan later, possibly on another stream -- the bench
+        overlaps batch i + 1's begin with batch i's scan.  Any other path runs whole here."""
+        q = q_unit.to(torch.bfloat16).contiguous()
+        k = int(k)
+        if (self.device.type == "cuda" and self.prune and not self.prefilter and 0 < k <= 16
+                and q.shape[0] >= self.prune_min_nq and self._seed_rows(self.visible, k)):
+            ctx = self._pruned_begin(q, k, n_cus)
+            if ctx is not None:
+                return ctx
+        return {"full": self.search(q, k, n_cus)}
+
+    def search_end(self, ctx: dict):
+        """-> (scores f32 [NQ, k], rows int32 [NQ, k]) of a ``search_begin`` context."""
+        if "full" in ctx:
+            return ctx["full"]
+        return self._pruned_end(ctx)
 
     def _search_scan(self, q_unit, k: int, rows, dtype: str, n_cus):
         """Seeded fused scan + merge over ``rows`` (bf16 slab, or e4m3 bytes for dtype fp8)."""
@@ -638,10 +662,18 @@ class HbmIndexShard:
 
         Route (decided on the GPU from the same sample, no host sync): counting the sample's
         emitted rows at or above T - margin (extrapolated when that band reaches below the
-        sample's seed threshold) estimates each query's int8 candidates.  On data whose scores crowd the k-th best (an anisotropic corpus: every pair
-        of rows at cosine ~0.3) that estimate exceeds the buffer, and the batch takes the bf16
+        sample's seed threshold) estimates each query's int8 candidates.  On data whose scores
+        crowd the k-th best (an anisotropic corpus: every pair of rows at cosine ~0.3) that
+        estimate exceeds the buffer, and the batch takes the bf16
         emitting scan with the exact threshold T instead of an int8 pass that would overflow and
         then pay the full fallback scan on top (profiles/r3_real/)."""
+        ctx = self._pruned_begin(q_unit, k, n_cus)
+        return None if ctx is None else self._pruned_end(ctx)
+
+    def _pruned_begin(self, q_unit, k: int, n_cus):
+        """Query-side half of the pruned search: int8 queries, the exact sample, T, thresholds and
+        the route flag -- everything before the full-shard scan, on the current stream, for the
+        rows visible NOW (a pipelined caller runs it for batch i + 1 under batch i's scan)."""
         from ..ops._ext import hip, stream_handle
 
         n, NQ, kmax = self.visible, q_unit.shape[0], 16
@@ -684,6 +716,22 @@ class HbmIndexShard:
                       cnt_p.data_ptr(),
                       self.SAMPLE_CAP, ts, limit, T.data_ptr(), thr.data_ptr(), dense.data_ptr(),
                       st)
+        return dict(q=q_unit, k=k, n=n, n_cus=n_cus, q8=q8, sq=sq, thr=thr, T=T, dense=dense)
+
+    def _pruned_end(self, ctx):
+        """The full-shard half of the pruned search over the rows ``_pruned_begin`` saw, on the
+        current stream (which may differ from the one the begin ran on: its tensors are marked
+        as used here, so the allocator cannot recycle them under this stream's kernels)."""
+        from ..ops._ext import hip, stream_handle
+
+        h, dev, cap, kmax = hip(), self.device, self.PRUNE_CAP, 16
+        cur = torch.cuda.current_stream(dev)
+        for t in ("q", "q8", "sq", "thr", "T", "dense"):
+            ctx[t].record_stream(cur)
+        q_unit, k, n, n_cus = ctx["q"], ctx["k"], ctx["n"], ctx["n_cus"]
+        q8, thr, T, dense = ctx["q8"], ctx["thr"], ctx["T"], ctx["dense"]
+        NQ = q_unit.shape[0]
+        st = stream_handle(dev)
         # 3. int8 route: emit every row with (q8 . x8) * sx >= thr, 4. exact bf16 re-score,
         #    5. top-k (skipped on the device when dense: counts stay 0, the select writes -inf)
         rsplit = 2 if (NQ < 512 or self.i8_rsplit2) else 1

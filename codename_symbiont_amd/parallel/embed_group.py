@@ -50,10 +50,12 @@ class EmbedGroup:
         self.H = encoder.cfg.hidden
         self.comm_device = info.device if info.backend == "nccl" else torch.device("cpu")
         self._lock = threading.Lock()
+        # a single-rank process group still runs every collective (RCCL tests on one GPU)
+        self.collective = info.world > 1 or info.backend != "none"
 
     # ------------------------------------------------------------------ plumbing
     def _bcast(self, t: torch.Tensor) -> torch.Tensor:
-        if self.info.world > 1:
+        if self.collective:
             dist.broadcast(t, src=0, group=self.group)
         return t
 
@@ -75,7 +77,7 @@ class EmbedGroup:
                                 (cu[s:e + 1] - t0).to(dev, torch.int32), int(lens.max()))
             pooled, _ = self.enc.forward_packed(local)
             out[:e - s].copy_(pooled.float())
-        if info.world == 1:
+        if not self.collective:
             return out[:e - s]
         gathered = torch.empty(info.world * maxb, self.H, dtype=torch.float32, device=self.comm_device)
         dist.all_gather_into_tensor(gathered, out, group=self.group)

@@ -62,6 +62,33 @@ class ShardedSearcher:
         return merge_ranked(s_recv.view(info.world, nq, k), g_recv.view(info.world, nq, k), k)
 
 
+    def begin(self, q_local: torch.Tensor, k: int) -> dict:
+        """First half of ``search`` for a pipelined caller (bench.py): the query all_gather and
+        the shard's query-side pre-pass run now, on the current stream; ``end`` runs the
+        full-shard scan, the exchange and the merge (HbmIndexShard.search_begin)."""
+        info = self.info
+        if not self.collective:
+            return {"ctx": self.shard.search_begin(q_local, k), "k": k}
+        nq, D = q_local.shape
+        q_send = q_local.to(self.wire_dtype).contiguous()
+        q_all = torch.empty(info.world * nq, D, dtype=self.wire_dtype, device=q_send.device)
+        dist.all_gather_into_tensor(q_all, q_send, group=self.group)
+        return {"ctx": self.shard.search_begin(q_all.to(torch.bfloat16), k), "k": k, "nq": nq}
+
+    def end(self, h: dict):
+        info, k = self.info, h["k"]
+        s, r = self.shard.search_end(h["ctx"])
+        if not self.collective:
+            return s, encode_gid(0, r)
+        nq = h["nq"]
+        gid = encode_gid(info.rank, r)
+        s_recv = torch.empty_like(s)
+        g_recv = torch.empty_like(gid)
+        dist.all_to_all_single(s_recv, s.contiguous(), group=self.group)
+        dist.all_to_all_single(g_recv, gid.contiguous(), group=self.group)
+        return merge_ranked(s_recv.view(info.world, nq, k), g_recv.view(info.world, nq, k), k)
+
+
 def merge_ranked(scores: torch.Tensor, gids: torch.Tensor, k: int):
     """[world, nq, k] per-rank sorted lists -> [nq, k] global top-k (ties: lower rank first)."""
     W, nq, kk = scores.shape

@@ -13,6 +13,7 @@
 from __future__ import annotations
 
 import asyncio
+import time
 import uuid
 
 import numpy as np
@@ -47,6 +48,8 @@ class VectorMemoryService(Service):
                                                               device=self._index_device()))
         if self.cfg.index_fill_random and self.store.count == 0:
             self.store.shard.fill_random(self.cfg.index_fill_random, seed=17)
+        self.store.shard.scan_cus = self.cfg.scan_cus
+        self.SEARCH_MAX_BATCH = max(1, self.cfg.search_max_batch)
         self.log.info("[INDEX_SETUP] collection '%s': dim %d, capacity %d, device %s, %d points",
                       self.cfg.collection, dim, self.store.shard.capacity, self.store.shard.device,
                       self.store.count)
@@ -123,7 +126,9 @@ class VectorMemoryService(Service):
         dimension, extra keys) take ``handle_search``, which produces the reference's error
         replies.  The scan runs in an executor thread while this loop goes back for the next
         burst (at most SEARCH_MAX_INFLIGHT scans in flight)."""
-        ok, ids, topk, q = native().search_tasks_batch([bytes(m.data) for m in msgs], self.store.dim)
+        with stage("search_decode", self.metrics, n=len(msgs)):
+            ok, ids, topk, q = native().search_tasks_batch([bytes(m.data) for m in msgs],
+                                                           self.store.dim)
         good = np.flatnonzero(ok)
         if len(good) < len(msgs):
             for i in np.flatnonzero(~ok):
@@ -166,6 +171,7 @@ class VectorMemoryService(Service):
             self._inflight.release()
         self.metrics.inc("search.batched_queries", len(msgs))
         self.metrics.inc("search.launches")
+        t_enc = time.perf_counter()
         out, skipped, sent = [], 0, 0
         frag = self.store.result_fragments
         encode = native().search_result_json
@@ -190,6 +196,7 @@ class VectorMemoryService(Service):
         if skipped:
             self.log.warning("[SEARCH_HANDLER] Found %d point(s) with missing or unexpected ID format. "
                              "Skipping.", skipped)
+        self.metrics.observe("search_encode", (time.perf_counter() - t_enc) * 1e3)
         await self.nc.publish_many(out)
         self.log.info("[SEARCH_HANDLER] Sent search results for %d request(s) (one scan, request_ids "
                       "%s..%s)", sent, rids[0], rids[-1])

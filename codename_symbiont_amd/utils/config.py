@@ -73,6 +73,11 @@ class Config:
     # pruned, the rest re-scored in bf16 (csrc/hip/index_i8.hip); "none": scan every row in bf16
     index_prune: str = field(default_factory=lambda: os.environ.get("SYMB_INDEX_PRUNE", "auto"))
     snapshot_dir: str = field(default_factory=lambda: _env("SYMB_SNAPSHOT_DIR", ""))
+    # queries per fused scan launch of the search service (a 100M-row scan costs about the same
+    # for 16 or 256 queries, so bigger bursts buy throughput at the price of latency)
+    search_max_batch: int = field(default_factory=lambda: _int("SYMB_SEARCH_MAX_BATCH", 256))
+    # CUs the index scans may occupy (0 = all): leave some to an encoder sharing the GPU
+    scan_cus: int = field(default_factory=lambda: _int("SYMB_SCAN_CUS", 0))
     collection: str = "symbiont_document_embeddings"
     embed_timeout_s: float = field(default_factory=lambda: _float("SYMB_EMBED_TIMEOUT_S", 15.0))
     search_timeout_s: float = field(default_factory=lambda: _float("SYMB_SEARCH_TIMEOUT_S", 20.0))

@@ -40,6 +40,8 @@ struct Conn {
   size_t out_off = 0;       // bytes of it written
   std::string in;           // response bytes so far
   double t0 = 0.0;
+  bool want_out = false;    // EPOLLOUT armed (only while a request is partly written)
+  bool dead = false;
 };
 
 // Content-Length of a complete header block (`hdr` ends at the blank line), -1 if absent.
@@ -89,11 +91,30 @@ Result run(const std::string& host, int port, const std::vector<std::string>& re
     setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
     fcntl(fd, F_SETFL, fcntl(fd, F_GETFL) | O_NONBLOCK);
     cs[(size_t)i].fd = fd;
+    // level-triggered EPOLLIN only: EPOLLOUT is armed just while a send is blocked, so idle or
+    // fully written connections never wake the loop (the client must not spin a core beside
+    // the service it measures)
     epoll_event ev{};
-    ev.events = EPOLLIN | EPOLLOUT;
+    ev.events = EPOLLIN;
     ev.data.u32 = (uint32_t)i;
     epoll_ctl(ep, EPOLL_CTL_ADD, fd, &ev);
   }
+  int alive = conns;
+  auto arm_out = [&](Conn& c, uint32_t idx, bool on) {
+    if (c.want_out == on) return;
+    epoll_event ev{};
+    ev.events = EPOLLIN | (on ? EPOLLOUT : 0u);
+    ev.data.u32 = idx;
+    epoll_ctl(ep, EPOLL_CTL_MOD, c.fd, &ev);
+    c.want_out = on;
+  };
+  auto kill = [&](Conn& c) {   // broken connection: count its request, stop polling it
+    if (c.dead) return;
+    epoll_ctl(ep, EPOLL_CTL_DEL, c.fd, nullptr);
+    close(c.fd);
+    c.dead = true;
+    --alive;
+  };
   const long total = (long)reqs.size();
   long next = 0, done = 0;
   res.latency_s.reserve(reqs.size());
@@ -120,29 +141,35 @@ Result run(const std::string& host, int port, const std::vector<std::string>& re
     }
     return true;
   };
-  for (auto& c : cs) {
-    start_req(c);
-    if (c.req >= 0 && !flush(c)) {
+  // start (or continue) writing a connection's request; false: the connection broke
+  auto send_req = [&](Conn& c, uint32_t idx) -> bool {
+    if (!flush(c)) {
       ++res.errors;
       ++done;
       c.req = -1;
+      kill(c);
+      return false;
     }
+    arm_out(c, idx, c.out_off < reqs[(size_t)c.req].size());
+    return true;
+  };
+  for (int i = 0; i < conns; ++i) {
+    start_req(cs[(size_t)i]);
+    if (cs[(size_t)i].req >= 0) send_req(cs[(size_t)i], (uint32_t)i);
   }
   std::vector<epoll_event> evs(256);
   char buf[65536];
-  while (done < total && now_s() < deadline) {
+  while (done < total && alive > 0 && now_s() < deadline) {
     const int n = epoll_wait(ep, evs.data(), (int)evs.size(), 100);
     for (int e = 0; e < n; ++e) {
-      Conn& c = cs[evs[(size_t)e].data.u32];
-      if (c.req < 0) continue;
-      if (evs[(size_t)e].events & EPOLLOUT) {
-        if (!flush(c)) {
-          ++res.errors;
-          ++done;
-          c.req = -1;
-          continue;
-        }
+      const uint32_t idx = evs[(size_t)e].data.u32;
+      Conn& c = cs[idx];
+      if (c.dead) continue;
+      if (c.req < 0) {   // idle: only a hang-up can arrive
+        if (evs[(size_t)e].events & (EPOLLHUP | EPOLLERR)) kill(c);
+        continue;
       }
+      if ((evs[(size_t)e].events & EPOLLOUT) && !send_req(c, idx)) continue;
       if (!(evs[(size_t)e].events & (EPOLLIN | EPOLLHUP | EPOLLERR))) continue;
       for (;;) {
         const ssize_t r = recv(c.fd, buf, sizeof(buf), 0);
@@ -155,6 +182,7 @@ Result run(const std::string& host, int port, const std::vector<std::string>& re
         ++res.errors;
         ++done;
         c.req = -1;
+        kill(c);
         break;
       }
       if (c.req < 0) continue;
@@ -174,16 +202,13 @@ Result run(const std::string& host, int port, const std::vector<std::string>& re
       ++done;
       c.req = -1;
       start_req(c);
-      if (c.req >= 0 && !flush(c)) {
-        ++res.errors;
-        ++done;
-        c.req = -1;
-      }
+      if (c.req >= 0) send_req(c, idx);
     }
   }
   res.t_end = now_s();
-  res.errors += total - done;   // unanswered at the deadline
-  for (auto& c : cs) close(c.fd);
+  res.errors += total - done;   // unanswered at the deadline / never sent (no live connection)
+  for (auto& c : cs)
+    if (!c.dead) close(c.fd);
   close(ep);
   return res;
 }

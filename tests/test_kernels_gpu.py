@@ -580,6 +580,31 @@ def test_index_pruned_search_routes_dense_data_exactly(route):
     assert (r0 == r1).float().mean().item() > 0.999
 
 
+def test_pruned_search_split_across_streams_matches_search():
+    """search_begin on one stream (the bench runs it under the previous batch's scan), rows
+    appended after it, search_end on another stream == search() over the rows begin saw."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+
+    n, k, nq = (1 << 20) + 4000, 10, 256
+    shard = HbmIndexShard(384, n + 1024, prune="i8")
+    shard.fill_random(n, seed=21)
+    q = torch.nn.functional.normalize(_f(nq, 384, seed=22), dim=-1).bfloat16()
+    s0, r0 = shard.search(q, k)
+    a, b = torch.cuda.Stream(), torch.cuda.Stream()
+    a.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(a):
+        ctx = shard.search_begin(q, k)
+        done = torch.cuda.Event()
+        done.record(a)
+        assert "full" not in ctx and ctx["n"] == n
+        shard.append_unit(q)          # invisible to this search: its n is fixed at begin
+    b.wait_event(done)
+    with torch.cuda.stream(b):
+        s1, r1 = shard.search_end(ctx)
+    torch.cuda.synchronize()
+    assert torch.equal(r0, r1) and torch.equal(s0, s1)
+
+
 @pytest.mark.parametrize("k", [1, 10, 17, 64, 100, 128])
 def test_topk_select_radix_matches_torch(k):
     """topk_select_radix_kernel (any k <= 128): exact top-k of each query's candidate list vs

@@ -190,3 +190,43 @@ def test_http_load_generator_frames_keepalive_responses():
     assert r["errors"] == 0 and r["non200"] == 5
     assert len(r["latency_s"]) == 300 and min(r["latency_s"]) > 0
     assert r["t_end"] >= r["t_start"]
+
+
+def test_http_load_generator_stops_when_every_connection_breaks():
+    """Connections the server closes are dropped and their requests counted as errors; once no
+    connection is left the client returns at once instead of spinning until its timeout."""
+    import asyncio
+    import threading
+    import time
+
+    from codename_symbiont_amd.ops._ext import native
+
+    ready = threading.Event()
+    box = {}
+
+    async def handle(reader, writer):
+        for _ in range(2):   # two answers, then hang up
+            try:
+                await reader.readuntil(b"\r\n\r\n")
+            except (asyncio.IncompleteReadError, ConnectionError):
+                break
+            writer.write(b"HTTP/1.1 200 OK\r\nContent-Length: 2\r\n\r\n{}")
+            await writer.drain()
+        writer.close()
+
+    def serve():
+        loop = asyncio.new_event_loop()
+        srv = loop.run_until_complete(asyncio.start_server(handle, "127.0.0.1", 0))
+        box["port"] = srv.sockets[0].getsockname()[1]
+        box["loop"] = loop
+        ready.set()
+        loop.run_forever()
+
+    threading.Thread(target=serve, daemon=True).start()
+    assert ready.wait(10)
+    reqs = [b"GET /ok HTTP/1.1\r\nHost: t\r\n\r\n"] * 100
+    t0 = time.time()
+    r = native().http_load("127.0.0.1", box["port"], reqs, 4, 30.0)
+    box["loop"].call_soon_threadsafe(box["loop"].stop)
+    assert time.time() - t0 < 10.0
+    assert len(r["latency_s"]) == 8 and r["errors"] == 92

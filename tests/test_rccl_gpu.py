@@ -85,3 +85,21 @@ def test_rccl_index_group_store_roundtrip(rccl):
     assert texts == ["t10", "t20", "neg7", "neg1500"]
     assert np.allclose(sc[:, 0], 1.0, atol=1e-2)
     assert grp.comm_stats["search"][1] == 3
+
+
+def test_rccl_embed_group_matches_encoder(rccl):
+    """DP embedding (EmbedGroup: int64 header + int32 batch broadcasts, f32 all_gather of the
+    pooled rows over RCCL) == the encoder run directly."""
+    from codename_symbiont_amd.models import get_config
+    from codename_symbiont_amd.models.encoder import HipEncoder, synthetic_batch
+    from codename_symbiont_amd.parallel.embed_group import EmbedGroup
+
+    cfg = get_config("minilm-l6")
+    enc = HipEncoder(cfg, seed=0, device=rccl.device)
+    grp = EmbedGroup(rccl, enc)
+    assert grp.collective
+    b = synthetic_batch(cfg, 37, 48, seed=5, varlen=True).to(rccl.device)
+    got = grp.embed(b)
+    want, _ = enc.forward_packed(b)
+    torch.cuda.synchronize()
+    assert got.shape == want.shape and torch.equal(got, want)
