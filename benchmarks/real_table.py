@@ -38,7 +38,7 @@ def main(d: str) -> None:
                       .replace("clustered ", "clustered, ", 1))
         print(f"| {rows / 1e6:g}M x {nq} | {corpus_txt} | {i8['ms_per_step']:.2f} | "
               f"{bf['ms_per_step']:.2f} | {ratio:.2f} | {i8.get('search_dense_route_batches')} / "
-              f"{i8['steps'] + i8['warmup'] + 2} | {i8.get('search_overflow_batches')} | "
+              f"{i8['steps']} | {i8.get('search_overflow_batches')} | "
               f"{i8.get('search_max_candidates')} | {i8.get('verify_exact')} / "
               f"{bf.get('verify_exact')} |")
 

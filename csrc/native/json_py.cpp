@@ -259,6 +259,80 @@ py::bytes search_result_json(const std::string& request_id,
 }
 
 
+// A whole scan's replies in ONE call (vector_memory's per-burst loop): for query j, the first
+// ks[j] (score, row) pairs with row >= 0 whose cached result fragments exist become
+// SemanticSearchNatsResult JSON -- the same bytes search_result_json builds per request.  The
+// fragments come from `cache` (dict row -> (prefix, suffix) bytes, read without Python bytecode);
+// a miss calls `miss(row)` (the store's payload lookup, which fills the cache) and a None from it
+// skips the row (a point without an id, as the reference skips undecodable ids).  errs: None or
+// a list of per-query error_message values (str or None).  Returns (list of bytes, skipped).
+static py::tuple search_results_batch(py::list rids,
+                                      py::array_t<float, py::array::c_style | py::array::forcecast> scores,
+                                      py::array_t<int64_t, py::array::c_style | py::array::forcecast> rows,
+                                      py::array_t<int64_t, py::array::c_style | py::array::forcecast> ks,
+                                      py::dict cache, py::object miss, py::object errs) {
+  const size_t n = (size_t)py::len(rids);
+  if (scores.ndim() != 2 || rows.ndim() != 2 || scores.shape(0) != rows.shape(0) ||
+      scores.shape(1) != rows.shape(1) || (size_t)scores.shape(0) < n || (size_t)ks.size() < n)
+    throw std::runtime_error("search_results_batch: shape mismatch");
+  const size_t kmax = (size_t)scores.shape(1);
+  const float* sc = scores.data();
+  const int64_t* rw = rows.data();
+  const int64_t* kp = ks.data();
+  const bool have_errs = !errs.is_none();
+  py::list out(n);
+  long skipped = 0;
+  std::string buf;
+  for (size_t j = 0; j < n; ++j) {
+    buf.clear();
+    buf += "{\"request_id\":";
+    const std::string rid = rids[j].cast<std::string>();
+    append_json_string(buf, rid.data(), rid.size());
+    buf += ",\"results\":[";
+    const size_t k = std::min(kmax, (size_t)std::max<int64_t>(0, kp[j]));
+    bool first = true;
+    for (size_t c = 0; c < k; ++c) {
+      const int64_t r = rw[j * kmax + c];
+      if (r < 0) continue;
+      py::object key = py::int_(r);
+      PyObject* f = PyDict_GetItem(cache.ptr(), key.ptr());   // borrowed
+      py::object hold;
+      if (f == nullptr) {
+        hold = miss(key);
+        if (hold.is_none()) {
+          ++skipped;
+          continue;
+        }
+        f = hold.ptr();
+      }
+      PyObject* a = PyTuple_GetItem(f, 0);
+      PyObject* b = PyTuple_GetItem(f, 1);
+      char* pa;
+      char* pb;
+      Py_ssize_t na, nb;
+      if (a == nullptr || b == nullptr || PyBytes_AsStringAndSize(a, &pa, &na) ||
+          PyBytes_AsStringAndSize(b, &pb, &nb))
+        throw py::error_already_set();
+      if (!first) buf.push_back(',');
+      first = false;
+      buf.append(pa, (size_t)na);
+      append_f32(buf, sc[j * kmax + c]);
+      buf.append(pb, (size_t)nb);
+    }
+    buf += "],\"error_message\":";
+    py::object e = have_errs ? errs.cast<py::list>()[j] : py::object(py::none());
+    if (e.is_none()) {
+      buf += "null";
+    } else {
+      const std::string es = e.cast<std::string>();
+      append_json_string(buf, es.data(), es.size());
+    }
+    buf += "}";
+    out[j] = py::bytes(buf);
+  }
+  return py::make_tuple(out, skipped);
+}
+
 // A batch of SemanticSearchNatsTask messages -> (ok[n], request_ids[n], top_k[n], queries[n, dim]).
 // Only the regular shape {"request_id": str, "query_embedding": [dim numbers], "top_k": int}
 // (keys in any order, each once) is decoded here; anything else -- malformed JSON, other keys,
@@ -353,6 +427,9 @@ void register_json(py::module_& m) {
         py::arg("frags"), py::arg("error_message") = py::none());
   py::register_exception<JsonError>(m, "JsonError", PyExc_ValueError);
   m.def("search_tasks_batch", &search_tasks_batch, py::arg("msgs"), py::arg("dim"));
+  m.def("search_results_batch", &search_results_batch, py::arg("request_ids"), py::arg("scores"),
+        py::arg("rows"), py::arg("ks"), py::arg("cache"), py::arg("miss"),
+        py::arg("errors") = py::none());
   m.def("json_dumps", &dumps, "serde_json-compatible compact encoding (floats as f32)");
   m.def("json_dumps_f32_array", &dumps_f32_array);
   m.def("json_loads", &loads, py::arg("data"), py::arg("f32_arrays") = false);

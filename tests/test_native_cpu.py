@@ -230,3 +230,46 @@ def test_http_load_generator_stops_when_every_connection_breaks():
     box["loop"].call_soon_threadsafe(box["loop"].stop)
     assert time.time() - t0 < 10.0
     assert len(r["latency_s"]) == 8 and r["errors"] == 92
+
+
+def test_search_results_batch_matches_per_request_encoding():
+    """vector_memory's one-call burst encoder == search_result_json per request (cached
+    fragments, misses through the callback, skipped rows, -1 slots, per-query k, errors)."""
+    import numpy as np
+
+    from codename_symbiont_amd.ops._ext import native
+
+    frag = {r: (b'{"qdrant_point_id":"p%d","score":' % r, b',"payload":{"x":%d}}' % r)
+            for r in range(0, 40, 2)}
+    cache = dict(list(frag.items())[:5])
+    calls = []
+
+    def miss(r):
+        calls.append(r)
+        f = frag.get(r)
+        if f is not None:
+            cache[r] = f
+        return f
+
+    rng = np.random.default_rng(0)
+    n, kmax = 6, 5
+    scores = rng.standard_normal((n, kmax)).astype(np.float32)
+    rows = rng.integers(-1, 40, (n, kmax)).astype(np.int64)
+    ks = np.array([5, 3, 0, 5, 1, 4])
+    rids = [f"req-{j}" for j in range(n)]
+    errs = [None, "boom", None, None, None, "x\"y"]
+    bodies, skipped = native().search_results_batch(rids, scores, rows, ks, cache, miss, errs)
+    want_skip = 0
+    for j in range(n):
+        keep, fr = [], []
+        for s, r in zip(scores[j, :ks[j]], rows[j, :ks[j]]):
+            if r < 0:
+                continue
+            if int(r) not in frag:
+                want_skip += 1
+                continue
+            keep.append(s)
+            fr.append(frag[int(r)])
+        want = native().search_result_json(rids[j], np.asarray(keep, np.float32), fr, errs[j])
+        assert bodies[j] == want, j
+    assert skipped == want_skip and calls
