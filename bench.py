@@ -175,6 +175,11 @@ def parse_args(argv=None):
     ap.add_argument("--prune-sample-shift", type=int, default=0,
                     help="exact pruned search: threshold sample = 1 tile in 2^shift (0 = the "
                          "shard default, HbmIndexShard.PRUNE_TILE_SHIFT)")
+    ap.add_argument("--prune-block-frac", type=float, default=0.0,
+                    help="exact pruned search: a row block goes to the bf16 scan when some query "
+                         "would emit more than this share of the candidate slots from it (0 = "
+                         "the shard default, HbmIndexShard.PRUNE_BLOCK_FRAC; >= 1 turns the "
+                         "per-block route off)")
     ap.add_argument("--prepass-min-tiles", type=int, default=0,
                     help="row-block floor of the sampled searches' small pre-pass list scans "
                          "(0 = the shard default, 1 tile per workgroup)")
@@ -418,6 +423,8 @@ def run_gpu(args, info, comm) -> int:
         shard.prepass_min_tiles = args.prepass_min_tiles
     if args.prune_sample_shift:
         shard.PRUNE_TILE_SHIFT = args.prune_sample_shift
+    if args.prune_block_frac:
+        shard.PRUNE_BLOCK_FRAC = args.prune_block_frac
     torch.cuda.synchronize(dev)
     row_bytes = cfg.hidden * (1 if args.index_dtype == "fp8" else 2)
     log(info, f"[bench] setup {time.time() - t0:.1f}s: {cfg.model_name}, shard {rows_per_rank} "
@@ -685,6 +692,9 @@ def run_gpu(args, info, comm) -> int:
         extra_out["search_overflow_batches"] = ovf
         extra_out["search_max_candidates"] = int(shard._mq_tot[1].item())
         extra_out["search_dense_route_batches"] = int(shard._mq_tot[2].item()) if len(shard._mq_tot) > 2 else None
+        if len(shard._mq_tot) > 4:   # searches that sent only some row blocks to the bf16 scan
+            extra_out["search_block_route_batches"] = int(shard._mq_tot[3].item())
+            extra_out["search_block_routed_blocks"] = int(shard._mq_tot[4].item())
         print(f"[bench] rank {info.rank} searches: {ovf} overflowed, max "
               f"{int(shard._mq_tot[1].item())} candidates per query", file=sys.stderr, flush=True)
     if args.verify and args.mode != "embed":
@@ -730,6 +740,7 @@ def run_gpu(args, info, comm) -> int:
         "scan_min_tiles": args.scan_min_tiles,
         "prepass_min_tiles": shard.prepass_min_tiles,
         "prune_sample_shift": shard.PRUNE_TILE_SHIFT if prune else None,
+        "prune_block_frac": shard.PRUNE_BLOCK_FRAC if prune else None,
     })
     if info.rank == 0:
         print(result_line(args, info, comm, metric, unit, config, total, ms, prune, prefilter,

@@ -578,7 +578,7 @@ class HbmIndexShard:
         then write ``out`` and OR into its overflow flag, ``out[2]``).  ``fallback=False``: no
         overflow re-scan -- for a threshold sample that is still sound, since the top-k of ANY
         subset of real rows lower-bounds the k-th best.  ``cand``: also return the candidate
-        buffers (scores, count) for the route estimate of _search_pruned."""
+        buffers (scores, rows, count) for the route estimate of _search_pruned."""
         from ..ops._ext import hip, stream_handle
 
         h = hip()
@@ -617,22 +617,27 @@ class HbmIndexShard:
         if gate is None and fallback:   # (a sample's overflow only steers the route)
             self._stats(ovf, cnt)
         if cand:
-            return out_s, out_i, cs, cnt
+            return out_s, out_i, cs, ci, cnt
         return out_s, out_i
 
-    def _stats(self, ovf, cnt, dense=None) -> None:
+    def _stats(self, ovf, cnt, dense=None, blk=None) -> None:
         """``mq_stats``: running totals on the device (a few tiny kernels per search; off by
         default) -- batches whose candidates overflowed, the most candidates any query emitted,
-        and pruned searches routed to the bf16 scan by their sample."""
+        pruned searches routed whole to the bf16 scan by their sample, pruned searches that
+        routed only some row blocks there, and the row blocks so routed."""
         if not self.mq_stats:
             return
         if self._mq_tot is None:
             self._mq_tot = tuple(torch.zeros(1, dtype=torch.int32, device=self.device)
-                                 for _ in range(3))
+                                 for _ in range(5))
         self._mq_tot[0].add_(ovf)
         torch.maximum(self._mq_tot[1], cnt.max().view(1), out=self._mq_tot[1])
         if dense is not None:
             self._mq_tot[2].add_(dense)
+        if blk is not None and dense is not None:
+            part = (blk[:1] > 0).int() * (1 - dense)
+            self._mq_tot[3].add_(part)
+            self._mq_tot[4].add_(blk[:1] * part)
 
     # pruned search: its exact threshold sample is 1 tile in 2^5.  Sparser samples win the
     # headline (+2-3 % at 2^7) only because its queries' best matches sit in the exact fresh-row
@@ -649,9 +654,14 @@ class HbmIndexShard:
     PRUNE_CAP = 32768
     SAMPLE_CAP = 16384        # candidate slots per query of the sampled searches' sample scan
 
-    # route the batch to the bf16 emitting scan when the sample predicts more than this share of
-    # PRUNE_CAP int8 candidates for some query (estimate c << ts has a ~sqrt(c) << ts spread)
+    # route a row block to the bf16 emitting scan when the sample predicts more than this share
+    # of PRUNE_CAP int8 candidates from it for some query, and EVERY block when some query's
+    # estimate over the blocks left to the int8 scan still exceeds PRUNE_DENSE_FRAC of it
+    # (estimates c << ts have a ~sqrt(c) << ts spread).  A block in the bf16 scan costs ~1.7x its
+    # int8 scan but spreads over the whole chip; 1024 int8 candidates from one block per query
+    # cost about as much to emit and re-score.
     PRUNE_DENSE_FRAC = 0.6
+    PRUNE_BLOCK_FRAC = 1 / 32
     prune_route = True   # False: always take the int8 pass (tests of the overflow fallback)
 
     def _search_pruned(self, q_unit, k: int, n_cus):
@@ -660,13 +670,17 @@ class HbmIndexShard:
         emitted, re-scored in bf16 and the top-k of those is returned.  A query whose candidates
         overflow PRUNE_CAP raises the flag that gates the exact bf16 list scan.
 
-        Route (decided on the GPU from the same sample, no host sync): counting the sample's
-        emitted rows at or above T - margin (extrapolated when that band reaches below the
-        sample's seed threshold) estimates each query's int8 candidates.  On data whose scores
-        crowd the k-th best (an anisotropic corpus: every pair of rows at cosine ~0.3) that
-        estimate exceeds the buffer, and the batch takes the bf16
-        emitting scan with the exact threshold T instead of an int8 pass that would overflow and
-        then pay the full fallback scan on top (profiles/r3_real/)."""
+        Route (decided on the GPU from the same sample, no host sync, per row block of the int8
+        scan): counting the sample's emitted rows at or above T - margin (extrapolated when that
+        band reaches below the sample's seed threshold), binned by block, estimates each query's
+        int8 candidates per block.  A block that some query would flood -- a crowd of
+        near-duplicates the int8 bound cannot separate, such as the freshly ingested rows of a
+        corpus whose embeddings all sit together -- goes to the bf16 emitting scan at the exact
+        threshold T, spread over the whole chip, and the int8 scan skips it; both emit into the
+        same candidate buffers.  On data whose scores crowd the k-th best everywhere (an
+        anisotropic corpus: every pair of rows at cosine ~0.3) every block goes to the bf16
+        scan, instead of an int8 pass that would overflow and then pay the full fallback scan on
+        top (profiles/r3_real/, profiles/r3_sustain/)."""
         ctx = self._pruned_begin(q_unit, k, n_cus)
         return None if ctx is None else self._pruned_end(ctx)
 
@@ -700,23 +714,57 @@ class HbmIndexShard:
         pm = self.prepass_min_tiles
         s0, _ = self._scan(sub.shape[0], q_unit, kmax, k, None, n_cus, sub, "bf16", min_tiles=pm)
         thr0 = s0[:, k - 1].contiguous() - self.MQ_THR_MARGIN
-        pre_s, _, cs_p, cnt_p = self._scan_mq(nv * TILE_ROWS, q_unit, kmax, k, thr0, n_cus,
-                                              tshift=ts, fallback=False, cand=True,
-                                              cap=self.SAMPLE_CAP)
+        pre_s, _, cs_p, ci_p, cnt_p = self._scan_mq(nv * TILE_ROWS, q_unit, kmax, k, thr0, n_cus,
+                                                    tshift=ts, fallback=False, cand=True,
+                                                    cap=self.SAMPLE_CAP)
         tail_s, _ = self._scan(n - t0, q_unit, kmax, k, thr0, n_cus, self.rows[t0:], "bf16",
                                min_tiles=pm)
         # 2. T (k-th best of the union), the per-query emission threshold (T - margin) / sq and
-        #    the route flag, in one launch (prune_route)
+        #    the per-row-block route (prune_route): the blocks some query would flood with int8
+        #    candidates go to the bf16 emitting scan at T, the rest to the int8 scan
+        geo = self._i8_geometry(n, NQ, n_cus)
+        n_rblk = geo[2]
         T = torch.empty(NQ, dtype=torch.float32, device=dev)
         thr = torch.empty(NQ, dtype=torch.float32, device=dev)
         dense = torch.empty(1, dtype=torch.int32, device=dev)
-        limit = int(self.PRUNE_DENSE_FRAC * cap) if self.prune_route else 1 << 62
+        est = torch.empty(NQ, n_rblk, dtype=torch.float32, device=dev)
+        blkmax = torch.empty(n_rblk, dtype=torch.int32, device=dev)
+        blk = torch.empty(2 + 2 * n_rblk, dtype=torch.int32, device=dev)
+        inf = float("inf")
+        limit = self.PRUNE_DENSE_FRAC * cap if self.prune_route else inf
+        blk_limit = self.PRUNE_BLOCK_FRAC * cap if self.prune_route else inf
         h.prune_route(NQ, pre_s.data_ptr(), tail_s.data_ptr(), k, self.MQ_THR_MARGIN,
                       sq.data_ptr(), margin.data_ptr(), thr0.data_ptr(), cs_p.data_ptr(),
-                      cnt_p.data_ptr(),
-                      self.SAMPLE_CAP, ts, limit, T.data_ptr(), thr.data_ptr(), dense.data_ptr(),
-                      st)
-        return dict(q=q_unit, k=k, n=n, n_cus=n_cus, q8=q8, sq=sq, thr=thr, T=T, dense=dense)
+                      ci_p.data_ptr(), cnt_p.data_ptr(), self.SAMPLE_CAP, ts, geo[1], n_rblk,
+                      blk_limit, limit, self._mq_slots(NQ, n_cus)[3], T.data_ptr(),
+                      thr.data_ptr(), dense.data_ptr(), est.data_ptr(), blkmax.data_ptr(),
+                      blk.data_ptr(), st)
+        return dict(q=q_unit, k=k, n=n, n_cus=n_cus, q8=q8, sq=sq, thr=thr, T=T, dense=dense,
+                    blk=blk, geo=geo)
+
+    def _i8_geometry(self, n: int, NQ: int, n_cus: int):
+        """(rsplit, rows_per_blk, n_rblk) of the int8 scan over n rows: ~one workgroup per CU
+        slot, whole tiles per block."""
+        from ..ops._ext import hip
+
+        h = hip()
+        rsplit = 2 if (NQ < 512 or self.i8_rsplit2) else 1
+        tr = h.i8_tile_rows()
+        n_qblk = math.ceil(NQ / h.i8_queries_per_blk(rsplit))
+        wpc = h.i8_wgs_per_cu()
+        n_rblk = max(1, min(math.ceil(n / (tr * 16)), max(1, round(n_cus * wpc / n_qblk))))
+        rows_per_blk = _round_up(max(1, math.ceil(n / n_rblk)), tr)
+        n_rblk = max(1, math.ceil(n / rows_per_blk))
+        return rsplit, rows_per_blk, n_rblk
+
+    def _mq_slots(self, NQ: int, n_cus: int):
+        """(sets, rsplit, n_qblk, row slots) of a full-chip emitting-scan launch for NQ queries
+        (as _scan_mq)."""
+        from ..ops._ext import hip
+
+        sets, rsplit = (4, 1) if NQ >= 512 else ((4, 2) if self.mq_rsplit else (2, 1))
+        n_qblk = math.ceil(NQ / hip().mq_queries_per_blk(sets, rsplit))
+        return sets, rsplit, n_qblk, max(1, round(n_cus / n_qblk))
 
     def _pruned_end(self, ctx):
         """The full-shard half of the pruned search over the rows ``_pruned_begin`` saw, on the
@@ -726,48 +774,47 @@ class HbmIndexShard:
 
         h, dev, cap, kmax = hip(), self.device, self.PRUNE_CAP, 16
         cur = torch.cuda.current_stream(dev)
-        for t in ("q", "q8", "sq", "thr", "T", "dense"):
+        for t in ("q", "q8", "sq", "thr", "T", "dense", "blk"):
             ctx[t].record_stream(cur)
         q_unit, k, n, n_cus = ctx["q"], ctx["k"], ctx["n"], ctx["n_cus"]
-        q8, thr, T, dense = ctx["q8"], ctx["thr"], ctx["T"], ctx["dense"]
+        q8, thr, T, dense, blk = ctx["q8"], ctx["thr"], ctx["T"], ctx["dense"], ctx["blk"]
+        rsplit, rows_per_blk, n_rblk = ctx["geo"]
         NQ = q_unit.shape[0]
         st = stream_handle(dev)
-        # 3. int8 route: emit every row with (q8 . x8) * sx >= thr, 4. exact bf16 re-score,
-        #    5. top-k (skipped on the device when dense: counts stay 0, the select writes -inf)
-        rsplit = 2 if (NQ < 512 or self.i8_rsplit2) else 1
-        tr = h.i8_tile_rows()
-        n_qblk = math.ceil(NQ / h.i8_queries_per_blk(rsplit))
-        wpc = h.i8_wgs_per_cu()
-        n_rblk = max(1, min(math.ceil(n / (tr * 16)), max(1, round(n_cus * wpc / n_qblk))))
-        rows_per_blk = _round_up(max(1, math.ceil(n / n_rblk)), tr)
-        n_rblk = max(1, math.ceil(n / rows_per_blk))
+        # 3. int8 scan of the blocks the route kept: emit every row with (q8 . x8) * sx >= thr
         cs = torch.empty(NQ, cap, device=dev)
         ci = torch.empty(NQ, cap, dtype=torch.int32, device=dev)
         cnt = torch.empty(NQ, dtype=torch.int32, device=dev)
         ovf = torch.empty(1, dtype=torch.int32, device=dev)
         out_s = torch.empty(NQ, k, device=dev)
         out_i = torch.empty(NQ, k, dtype=torch.int32, device=dev)
+        skip = blk[2 + n_rblk:].data_ptr() if self.prune_route else 0
         h.index_scan_i8(self.rows_i8.data_ptr(), self.sx_i8.data_ptr(), n, self.rows_i8.shape[0],
                         rows_per_blk, n_rblk,
                         q8.data_ptr(), NQ, thr.data_ptr(), cs.data_ptr(), ci.data_ptr(),
-                        cnt.data_ptr(), cap, self.scan_xcd, st, rsplit, skip=dense.data_ptr())
+                        cnt.data_ptr(), cap, self.scan_xcd, st, rsplit, skip=skip)
+        # 3'. the bf16 emitting scan of the blocks the route listed, at the exact threshold T,
+        #     into the same candidate buffers (no launch work when none is listed)
+        if self.prune_route:
+            sets, mrs, _, slots = self._mq_slots(NQ, n_cus)
+            h.index_scan_mq(self.rows.data_ptr(), n, TILE_ROWS, slots, q_unit.data_ptr(), NQ,
+                            T.data_ptr(), cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(), cap,
+                            self.scan_xcd, st, sets, 0, mrs, blist=blk.data_ptr(),
+                            list_tiles=rows_per_blk // TILE_ROWS, zero_cnt=False)
+        # 4. exact bf16 re-score of every candidate, 5. top-k
         h.rescore_bf16(self.rows.data_ptr(), q_unit.data_ptr(), NQ, self.dim, ci.data_ptr(),
                        cnt.data_ptr(), cap, cs.data_ptr(), st)
         h.topk_select_counted(cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(), cap, NQ, kmax, k,
                               out_s.data_ptr(), out_i.data_ptr(), ovf.data_ptr(), st)
-        i8_cnt = cnt
-        # 3'. bf16 route (gated on dense): the emitting scan at the exact threshold T; its select
-        #     ORs into ovf
-        if self.prune_route:
-            self._scan_mq(n, q_unit, kmax, k, T, n_cus, gate=dense, out=(out_s, out_i, ovf))
         # overflow (some query had more than cap candidates): the exact bf16 scan, seeded with T
         self._scan(n, q_unit, kmax, k, T.contiguous(), n_cus, gate=ovf, out=(out_s, out_i))
-        self._mq_last = (i8_cnt, ovf)
+        self._mq_last = (cnt, ovf)
         self._route_last = dense
+        self._route_blk_last = blk
         if self.mq_stats:   # (diagnostics / benchmarks/micro.py scani8abl: inputs and grid)
             self._pruned_last = dict(q8=q8, thr=thr, rows_per_blk=rows_per_blk, n_rblk=n_rblk,
                                      cap=cap, cs=cs, ci=ci, cnt=cnt, q=q_unit)
-        self._stats(ovf, i8_cnt, dense)
+        self._stats(ovf, cnt, dense, blk)
         return out_s, out_i
 
     def _prune_thresholds_torch(self, q_unit, pre_s, tail_s, k: int):

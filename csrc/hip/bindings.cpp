@@ -73,8 +73,9 @@ int symb_prune_qquant(const void* Q, int NQ, int dim, const float* bounds, void*
                       float* margin, hipStream_t st);
 int symb_prune_route(int NQ, const float* pre_s, const float* tail_s, int k, float thr_margin,
                      const float* sq, const float* margin, const float* thr0, const float* cs_p,
-                     const int* cnt_p, int cap_p, int tshift, long long limit, float* T,
-                     float* thr, int* dense, hipStream_t st);
+                     const int* ci_p, const int* cnt_p, int cap_p, int tshift, int rows_per_blk,
+                     int n_rblk, float blk_limit, float limit, int max_list, float* T, float* thr,
+                     int* dense, float* est, int* blkmax, int* blk, hipStream_t st);
 int symb_i8_config(int tile_rows, int waves);
 int symb_i8_tile_rows();
 int symb_i8_wgs_per_cu();
@@ -95,7 +96,7 @@ int symb_mq_config(int aux);
 int symb_index_scan_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                        int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
                        int xcd, hipStream_t st, int sets, int tshift, int rsplit,
-                       const int* gate);
+                       const int* gate, const int* blist, int list_tiles, int zero_cnt);
 int symb_index_scan_mq_ablate(const void* X, int n_valid, int rows_per_blk, int n_rblk,
                               const void* Q, int NQ, const float* thr, float* cand_s, int* cand_i,
                               int* cand_n, int cap, int xcd, hipStream_t st, int abl, int sets,
@@ -377,12 +378,16 @@ PYBIND11_MODULE(_hip, m) {
           "prune_qquant");
   });
   m.def("prune_route", [](int NQ, uptr pre_s, uptr tail_s, int k, float thr_margin, uptr sq,
-                          uptr margin, uptr thr0, uptr cs_p, uptr cnt_p, int cap_p, int tshift,
-                          long long limit, uptr T, uptr thr, uptr dense, uptr st) {
+                          uptr margin, uptr thr0, uptr cs_p, uptr ci_p, uptr cnt_p, int cap_p,
+                          int tshift, int rows_per_blk, int n_rblk, float blk_limit, float limit,
+                          int max_list, uptr T, uptr thr, uptr dense, uptr est, uptr blkmax,
+                          uptr blk, uptr st) {
     check(symb_prune_route(NQ, P<const float>(pre_s), P<const float>(tail_s), k, thr_margin,
                            P<const float>(sq), P<const float>(margin), P<const float>(thr0),
-                           P<const float>(cs_p), P<const int>(cnt_p), cap_p, tshift, limit,
-                           P<float>(T), P<float>(thr), P<int>(dense), S(st)),
+                           P<const float>(cs_p), P<const int>(ci_p), P<const int>(cnt_p), cap_p,
+                           tshift, rows_per_blk, n_rblk, blk_limit, limit, max_list, P<float>(T),
+                           P<float>(thr), P<int>(dense), P<float>(est), P<int>(blkmax),
+                           P<int>(blk), S(st)),
           "prune_route");
   });
   m.def("index_scan_i8_ablate", [](uptr X8, uptr sx, int n_valid, int alloc_rows,
@@ -425,15 +430,18 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("sets") = 4, py::arg("rsplit") = 1);
   m.def("index_scan_mq", [](uptr X, int n_valid, int rows_per_blk, int n_rblk, uptr Q, int NQ,
                             uptr thr, uptr cand_s, uptr cand_i, uptr cand_n, int cap, int xcd,
-                            uptr st, int sets, int tshift, int rsplit, uptr gate) {
+                            uptr st, int sets, int tshift, int rsplit, uptr gate, uptr blist,
+                            int list_tiles, bool zero_cnt) {
     check(symb_index_scan_mq(P<void>(X), n_valid, rows_per_blk, n_rblk, P<void>(Q), NQ,
                              P<const float>(thr), P<float>(cand_s), P<int>(cand_i), P<int>(cand_n),
-                             cap, xcd, S(st), sets, tshift, rsplit, P<const int>(gate)),
+                             cap, xcd, S(st), sets, tshift, rsplit, P<const int>(gate),
+                             P<const int>(blist), list_tiles, zero_cnt ? 1 : 0),
           "index_scan_mq");
   }, py::arg("X"), py::arg("n_valid"), py::arg("rows_per_blk"), py::arg("n_rblk"), py::arg("Q"),
      py::arg("NQ"), py::arg("thr"), py::arg("cand_s"), py::arg("cand_i"), py::arg("cand_n"),
      py::arg("cap"), py::arg("xcd"), py::arg("stream"), py::arg("sets") = 4,
-     py::arg("tshift") = 0, py::arg("rsplit") = 1, py::arg("gate") = 0);
+     py::arg("tshift") = 0, py::arg("rsplit") = 1, py::arg("gate") = 0, py::arg("blist") = 0,
+     py::arg("list_tiles") = 0, py::arg("zero_cnt") = true);
   m.def("index_scan_mq_ablate", [](uptr X, int n_valid, int rows_per_blk, int n_rblk, uptr Q,
                                    int NQ, uptr thr, uptr cand_s, uptr cand_i, uptr cand_n,
                                    int cap, int xcd, uptr st, int abl, int sets, int rsplit) {

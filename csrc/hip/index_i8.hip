@@ -192,9 +192,6 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
     const int8_t* __restrict__ Q8, int NQ, int n_qblk, int xcd, const float* __restrict__ thr_in,
     float* __restrict__ cand_s, int* __restrict__ cand_i, int* __restrict__ cand_n, int cap,
     const int* __restrict__ skip) {
-  // skip (optional): the sampled route decision (prune_route_kernel) sent this batch to the bf16
-  // emitting scan -- every workgroup returns at once (grid-uniform, before any barrier)
-  if (skip != nullptr && *skip != 0) return;
   using namespace i8s;
   using G = Geo<TRK, WV>;
   constexpr int TR = G::TR, NSUB = G::NSUB, NS = G::NS, TILE_BYTES = G::TILE_BYTES;
@@ -208,6 +205,10 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lb = xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
   const int qb = lb % n_qblk, rb = lb / n_qblk;
+  // skip (optional, one flag per row block): the sampled route (prune_route_kernel) sent this
+  // block to the bf16 emitting scan -- the workgroup returns at once (workgroup-uniform, before
+  // any barrier)
+  if (skip != nullptr && skip[rb] != 0) return;
   const int row_begin = rb * rows_per_blk;
   const int row_end = min(row_begin + rows_per_blk, n_valid);
   const int n_tiles = row_end > row_begin ? (row_end - row_begin + TR - 1) / TR : 0;
@@ -644,11 +645,19 @@ __global__ __launch_bounds__(256) void prune_qprep_kernel(
 //                 The sample emitted every row >= thr0 (its seed threshold), so c is exact when
 //                 T - margin >= thr0; below thr0 the band holds at least the cnt rows >= thr0,
 //                 and, scores thinning out upwards, at least the density of [thr0, T] times the
-//                 band width: c = max(cnt, (cnt - k) * margin / (T - thr0)).  If any query's
-//                 estimate exceeds `limit` (or its sample buffer overflowed) the int8 pass would
-//                 overflow its buffer and pay the exact fallback on top (both full scans):
-//                 *dense = 1 routes the whole batch to the bf16 emitting scan instead.
-//                 Exactness never depends on the route; only the cost does.
+//                 band width: c = max(cnt, (cnt - k) * margin / (T - thr0)).
+//                 The route is decided PER ROW BLOCK of the int8 scan: each query's sample rows
+//                 in the band are binned by block, est[q][b] = (rows of block b) * c / (rows
+//                 binned) << tshift.  prune_route_final then sends to the bf16 emitting scan
+//                 every block some query would flood (max_q est[q][b] > blk_limit: a crowd of
+//                 near-duplicates the int8 bound cannot separate, such as freshly ingested rows
+//                 of one document), and EVERY block when a query's estimate over the remaining
+//                 blocks still exceeds `limit`, when a sample buffer overflowed (the bins are
+//                 then truncated), or when more blocks are listed than the bf16 scan has row
+//                 slots (index_mq.hip MqList).  The int8 scan skips the listed blocks
+//                 (skip[b]), the bf16 scan at the exact threshold T scans only them, and both
+//                 emit into the same candidate buffers: every row is covered by exactly one
+//                 exact-bound scan.  Exactness never depends on the route; only the cost does.
 __global__ __launch_bounds__(256) void prune_qquant_kernel(const __bf16* __restrict__ Q, int NQ,
                                                            const float* __restrict__ bounds,
                                                            int8_t* __restrict__ Q8,
@@ -693,15 +702,19 @@ __global__ __launch_bounds__(256) void prune_qquant_kernel(const __bf16* __restr
   }
 }
 
+constexpr int ROUTE_MAX_BLOCKS = 1024;   // int8 row blocks the per-block route can bin
+
 __global__ __launch_bounds__(256) void prune_route_kernel(
     int NQ, const float* __restrict__ pre_s, const float* __restrict__ tail_s, int k,
     float thr_margin, const float* __restrict__ sq, const float* __restrict__ margin,
-    const float* __restrict__ thr0, const float* __restrict__ cs_p, const int* __restrict__ cnt_p,
-    int cap_p, int tshift, long long limit, float* __restrict__ T_out, float* __restrict__ thr,
-    int* __restrict__ dense) {
+    const float* __restrict__ thr0, const float* __restrict__ cs_p, const int* __restrict__ ci_p,
+    const int* __restrict__ cnt_p, int cap_p, int tshift, int rows_per_blk, int n_rblk,
+    float* __restrict__ T_out, float* __restrict__ thr, int* __restrict__ dense,
+    float* __restrict__ est, int* __restrict__ blkmax) {
+  __shared__ int hist[4][ROUTE_MAX_BLOCKS];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int q = blockIdx.x * 4 + w;
-  if (q >= NQ) return;   // (no barrier in this kernel)
+  if (q >= NQ) return;   // (no barrier in this kernel: each wave bins its own query)
   // k-th best of 2k values (prune_qprep_kernel)
   float v = -INFINITY;
   if (lane < k) v = pre_s[(size_t)q * k + lane];
@@ -719,15 +732,78 @@ __global__ __launch_bounds__(256) void prune_route_kernel(
   const float band = T - m;
   const float t0 = thr0[q];
   const float* cs = cs_p + (size_t)q * cap_p;
+  const int* ci = ci_p + (size_t)q * cap_p;
+  int* h = hist[w];
+  for (int b = lane; b < n_rblk; b += 64) h[b] = 0;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   float c = 0.f;
-  for (int i = lane; i < n; i += 64) c += cs[i] >= band ? 1.f : 0.f;
+  for (int i = lane; i < n; i += 64) {
+    if (cs[i] >= band) {
+      c += 1.f;
+      atomicAdd(&h[min(ci[i] / rows_per_blk, n_rblk - 1)], 1);
+    }
+  }
   c = wave_sum(c);
+  const float binned = c;
   if (band < t0)   // the band reaches below what the sample emitted: extrapolate (see above)
     c = fmaxf((float)cnt, fmaxf(0.f, (float)(cnt - k)) * m / fmaxf(T - t0, 1e-6f));
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const float scale = (binned > 0.f ? c / binned : 0.f) * (float)(1 << tshift);
+  for (int b = lane; b < n_rblk; b += 64) {
+    const float e = (float)h[b] * scale;
+    est[(size_t)q * n_rblk + b] = e;
+    if (e > 0.f) atomicMax(blkmax + b, __float_as_int(e));   // (non-negative floats order as ints)
+  }
   if (lane == 0) {
     T_out[q] = T;
     thr[q] = (T - m) / sq[q];
-    if (cnt > cap_p || (double)c * (double)(1ll << tshift) > (double)limit) atomicOr(dense, 1);
+    if (cnt > cap_p) atomicOr(dense, 1);
+  }
+}
+
+// One workgroup: the per-block decision of prune_route_kernel.  blk: [0] = listed blocks, [1] =
+// n_rblk, [2 .. 2 + n_rblk) = the listed blocks in order, [2 + n_rblk .. 2 + 2 n_rblk) = skip
+// flags of the int8 scan.  *dense ends as 1 iff every block went to the bf16 scan.
+__global__ __launch_bounds__(1024) void prune_route_final_kernel(
+    int NQ, int n_rblk, const float* __restrict__ est, const int* __restrict__ blkmax,
+    float blk_limit, float limit, int max_list, int* __restrict__ dense, int* __restrict__ blk) {
+  __shared__ int flag[ROUTE_MAX_BLOCKS];
+  __shared__ int wtot[16];
+  __shared__ int all;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (tid == 0) all = *dense;
+  for (int b = tid; b < n_rblk; b += 1024) flag[b] = __int_as_float(blkmax[b]) > blk_limit;
+  __syncthreads();
+  for (int q = tid; q < NQ; q += 1024) {   // what each query would still emit in the int8 scan
+    const float* e = est + (size_t)q * n_rblk;
+    float s = 0.f;
+    for (int b = 0; b < n_rblk; ++b) s += flag[b] ? 0.f : e[b];
+    if (s > limit) atomicOr(&all, 1);
+  }
+  __syncthreads();
+  // listed blocks in order: one bin per thread (n_rblk <= 1024), ballot prefix per wave
+  const int f = tid < n_rblk && (all || flag[tid]);
+  const unsigned long long bal = __ballot(f);
+  if (lane == 0) wtot[w] = __popcll(bal);
+  __syncthreads();
+  int off = 0, nl = 0;
+  for (int i = 0; i < 16; ++i) {
+    off += i < w ? wtot[i] : 0;
+    nl += wtot[i];
+  }
+  const bool every = all || nl > max_list;
+  if (every) nl = n_rblk;
+  if (tid < n_rblk) {
+    const int pos = every ? tid
+                          : off + (int)__builtin_amdgcn_mbcnt_hi(
+                                      (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+    if (every || f) blk[2 + pos] = tid;
+    blk[2 + n_rblk + tid] = every || f;
+  }
+  if (tid == 0) {
+    blk[0] = nl;
+    blk[1] = n_rblk;
+    *dense = every ? 1 : 0;
   }
 }
 
@@ -791,7 +867,12 @@ int symb_index_scan_i8(const void* X8, const float* sx, int n_valid, int alloc_r
     return launch_i8<1, 64, 4>(X8, sx, n_valid, rows_per_blk, n_rblk, Q8, NQ, thr, cand_s, cand_i,
                                cand_n, cap, xcd, st, skip);
   if (rsplit == 2) return tr == 128 ? SYMB_I8(2, 128) : SYMB_I8(2, 64);
-  if (rsplit == 1) return tr == 128 ? SYMB_I8(1, 128) : SYMB_I8(1, 64);
+  // 512 queries per workgroup always run 64-row tiles: the 128-row form (four fused two-sub-tile
+  // chains per wave per tile) emitted a few rows per million with wrong scores, differently from
+  // run to run (benchmarks/diag/i8_determinism.py: 1100 queries, candidate totals 1317690 ..
+  // 1317766 against a constant 1317699 for every other form, profiles/r3_blockroute/), so it is
+  // not dispatched until that race is found
+  if (rsplit == 1) return SYMB_I8(1, 64);
 #undef SYMB_I8
   return -1;
 }
@@ -880,17 +961,25 @@ int symb_prune_qquant(const void* Q, int NQ, int dim, const float* bounds, void*
   return (int)hipGetLastError();
 }
 
-// dense (one int) is zeroed here, then raised by any query routed to the bf16 scan.
+// The per-block route (prune_route_kernel + prune_route_final_kernel).  dense (one int) ends 1
+// iff every block went to the bf16 scan; blk holds 2 + 2 n_rblk ints (layout at the final
+// kernel); est: NQ x n_rblk floats and blkmax: n_rblk ints of scratch.  ci_p: the sample's
+// candidate rows (physical), rows_per_blk / n_rblk: the int8 scan's row blocks (n_rblk <= 1024).
 int symb_prune_route(int NQ, const float* pre_s, const float* tail_s, int k, float thr_margin,
                      const float* sq, const float* margin, const float* thr0, const float* cs_p,
-                     const int* cnt_p, int cap_p, int tshift, long long limit, float* T,
-                     float* thr, int* dense, hipStream_t st) {
+                     const int* ci_p, const int* cnt_p, int cap_p, int tshift, int rows_per_blk,
+                     int n_rblk, float blk_limit, float limit, int max_list, float* T, float* thr,
+                     int* dense, float* est, int* blkmax, int* blk, hipStream_t st) {
   if (NQ <= 0) return 0;
   if (k < 1 || k > 32 || cap_p <= 0 || tshift < 0 || tshift > 20) return -1;
+  if (n_rblk < 1 || n_rblk > ROUTE_MAX_BLOCKS || rows_per_blk < 1 || max_list < 1) return -1;
   hipError_t e = hipMemsetAsync(dense, 0, sizeof(int), st);
+  if (e == hipSuccess) e = hipMemsetAsync(blkmax, 0, sizeof(int) * (size_t)n_rblk, st);
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(prune_route_kernel, dim3((NQ + 3) / 4), dim3(256), 0, st, NQ, pre_s, tail_s,
-                     k, thr_margin, sq, margin, thr0, cs_p, cnt_p, cap_p, tshift, limit, T, thr,
-                     dense);
+                     k, thr_margin, sq, margin, thr0, cs_p, ci_p, cnt_p, cap_p, tshift,
+                     rows_per_blk, n_rblk, T, thr, dense, est, blkmax);
+  hipLaunchKernelGGL(prune_route_final_kernel, dim3(1), dim3(1024), 0, st, NQ, n_rblk, est, blkmax,
+                     blk_limit, limit, max_list, dense, blk);
   return (int)hipGetLastError();
 }

@@ -148,12 +148,26 @@ __device__ __forceinline__ void mq_prologue(bf16x8 (&a)[mq::R], uint32_t base) {
 // same MFMA cycles per SIMD: at 256 queries the scan is bound by the chip's power limit (HBM
 // streaming + MFMAs hold the in-kernel clock near 1.5 GHz), so bytes moved per FLOP count.
 // AUX: cache policy bits of the row stream's LDS-DMA (0 = default, 2 = non-temporal).
+// MqList (block-list mode, blist != nullptr): scan only the row blocks that the pruned search's
+// route sent to the bf16 path (prune_route_kernel, index_i8.hip) instead of rows [0, n_valid).
+// blist[0] = nl listed blocks, blist[1] = the int8 scan's block count, blist[2 + i] = the i-th
+// listed block; a block is list_tiles 64-row tiles, rows >= n_valid are never scanned.  The
+// launch's n_rblk row slots share the listed blocks: block i gets slots [ceil(i n_rblk / nl),
+// ceil((i + 1) n_rblk / nl)) and splits its rows evenly over them (the route never lists more
+// blocks than slots), so each workgroup still scans one contiguous physical row range and a
+// single crowded block spreads over the whole chip.  Every block listed: rows [0, n_valid) split
+// evenly, as without a list.
+struct MqList {
+  const int* blist;
+  int list_tiles;
+};
+
 template <int NSET, int ABL = 0, int RSPLIT = 1, int AUX = 0>
 __global__ __launch_bounds__(512, 1) void index_scan_mq_kernel(
     const __bf16* __restrict__ X, int n_valid, int rows_per_blk, const __bf16* __restrict__ Q,
     int NQ, int n_qblk, int xcd, const float* __restrict__ thr_in, float* __restrict__ cand_s,
     int* __restrict__ cand_i, int* __restrict__ cand_n, int cap, int tshift,
-    const int* __restrict__ gate) {
+    const int* __restrict__ gate, MqList lst) {
   // gate (optional): run only if *gate != 0 -- the pruned search's bf16 route (index_i8.hip)
   if (gate != nullptr && *gate == 0) return;
   using namespace mq;
@@ -164,8 +178,29 @@ __global__ __launch_bounds__(512, 1) void index_scan_mq_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lb = xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
   const int qb = lb % n_qblk, rb = lb / n_qblk;
-  const int row_begin = rb * rows_per_blk;
-  const int row_end = min(row_begin + rows_per_blk, n_valid);
+  int row_begin = rb * rows_per_blk;
+  int row_end = min(row_begin + rows_per_blk, n_valid);
+  if (lst.blist != nullptr) {   // (grid-uniform, before any barrier)
+    const int nl = lst.blist[0], n_rblk = gridDim.x / n_qblk;
+    if (nl <= 0) return;
+    // every block (the route escalates a list longer than the slots to every block; the second
+    // test only keeps a corrupt list from dividing by zero below)
+    if (nl >= lst.blist[1] || nl > n_rblk) {
+      const int per = (n_valid + n_rblk * TR - 1) / (n_rblk * TR) * TR;
+      row_begin = min(rb * per, n_valid);
+      row_end = min(row_begin + per, n_valid);
+    } else {
+      const int i = (int)((long long)rb * nl / n_rblk);
+      const int s0 = (int)(((long long)i * n_rblk + nl - 1) / nl);
+      const int s1 = (int)(((long long)(i + 1) * n_rblk + nl - 1) / nl);
+      const int per = (lst.list_tiles + (s1 - s0) - 1) / (s1 - s0);
+      const int base = lst.blist[2 + i] * lst.list_tiles;
+      const int t0 = base + min((rb - s0) * per, lst.list_tiles);
+      const int t1 = base + min((rb - s0 + 1) * per, lst.list_tiles);
+      row_begin = min(t0 * TR, n_valid);
+      row_end = min(t1 * TR, n_valid);
+    }
+  }
   const int n_tiles = row_end > row_begin ? (row_end - row_begin + TR - 1) / TR : 0;
   // Row numbers above are VIRTUAL.  tshift = 0: virtual = physical.  tshift > 0 (a row sample for
   // threshold seeding, scanned in place): virtual 64-row tile v is physical tile
@@ -596,7 +631,7 @@ int symb_mq_config(int aux) {
 template <int NSET, int RSPLIT, int AUX>
 static int launch_mq_aux(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                      int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
-                     int xcd, hipStream_t st, int tshift, const int* gate) {
+                     int xcd, hipStream_t st, int tshift, const int* gate, MqList lst) {
   constexpr int qpb = mq::WAVES / RSPLIT * 16 * NSET;
   const int n_qblk = (NQ + qpb - 1) / qpb;
   constexpr int lds = mq::LDS_BYTES;
@@ -608,41 +643,49 @@ static int launch_mq_aux(const void* X, int n_valid, int rows_per_blk, int n_rbl
   }
   hipLaunchKernelGGL((index_scan_mq_kernel<NSET, 0, RSPLIT, AUX>), dim3(n_rblk * n_qblk), dim3(512),
                      lds, st, (const __bf16*)X, n_valid, rows_per_blk, (const __bf16*)Q, NQ, n_qblk,
-                     xcd, thr, cand_s, cand_i, cand_n, cap, tshift, gate);
+                     xcd, thr, cand_s, cand_i, cand_n, cap, tshift, gate, lst);
   return (int)hipGetLastError();
 }
 
 template <int NSET, int RSPLIT>
 static int launch_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                      int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
-                     int xcd, hipStream_t st, int tshift, const int* gate) {
+                     int xcd, hipStream_t st, int tshift, const int* gate, MqList lst) {
   return g_mq_aux == 2
              ? launch_mq_aux<NSET, RSPLIT, 2>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, thr, cand_s,
-                                             cand_i, cand_n, cap, xcd, st, tshift, gate)
+                                             cand_i, cand_n, cap, xcd, st, tshift, gate, lst)
              : launch_mq_aux<NSET, RSPLIT, 0>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, thr, cand_s,
-                                             cand_i, cand_n, cap, xcd, st, tshift, gate);
+                                             cand_i, cand_n, cap, xcd, st, tshift, gate, lst);
 }
 
 // tshift: 0 = rows [0, n_valid); k > 0 = virtual rows of a 1-in-2^k tile sample (kernel note).
 // sets: 16-query sets per wave, 4 or 2; rsplit: waves sharing each query group (1, or 2 = the
 // row-split form, sets 4 only).  Queries per workgroup: 8 / rsplit * 16 * sets (512 or 256).
+// blist (optional, list mode): scan the row blocks listed there (MqList; list_tiles 64-row tiles
+// each, rows >= n_valid never scanned) instead of rows [0, n_valid); rows_per_blk is then unused
+// and the n_rblk row slots of the grid share the listed rows.  zero_cnt = 0 appends to cand_n (another
+// scan's candidates already there) instead of zeroing it.
 int symb_index_scan_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                        int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
                        int xcd, hipStream_t st, int sets, int tshift, int rsplit,
-                       const int* gate) {
+                       const int* gate, const int* blist, int list_tiles, int zero_cnt) {
   if (NQ <= 0) return 0;
   if (rows_per_blk % mq::TR || n_rblk <= 0 || thr == nullptr || cap <= 0) return -1;
   if ((sets != 2 && sets != 4) || tshift < 0 || tshift > 12) return -1;
   if (rsplit != 1 && !(rsplit == 2 && sets == 4)) return -1;
-  hipError_t e = hipMemsetAsync(cand_n, 0, sizeof(int) * (size_t)NQ, st);
-  if (e != hipSuccess) return (int)e;
+  if (blist != nullptr && (tshift != 0 || list_tiles <= 0 || n_valid <= 0)) return -1;
+  MqList lst{blist, list_tiles};
+  if (zero_cnt) {
+    hipError_t e = hipMemsetAsync(cand_n, 0, sizeof(int) * (size_t)NQ, st);
+    if (e != hipSuccess) return (int)e;
+  }
   if (rsplit == 2)
     return launch_mq<4, 2>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, thr, cand_s, cand_i, cand_n,
-                           cap, xcd, st, tshift, gate);
+                           cap, xcd, st, tshift, gate, lst);
   return sets == 4 ? launch_mq<4, 1>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, thr, cand_s, cand_i,
-                                     cand_n, cap, xcd, st, tshift, gate)
+                                     cand_n, cap, xcd, st, tshift, gate, lst)
                    : launch_mq<2, 1>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, thr, cand_s, cand_i,
-                                     cand_n, cap, xcd, st, tshift, gate);
+                                     cand_n, cap, xcd, st, tshift, gate, lst);
 }
 
 // Profiling-only entry: the ablations of index_scan_mq_kernel (ABL above), same arguments.
@@ -663,7 +706,7 @@ int symb_index_scan_mq_ablate(const void* X, int n_valid, int rows_per_blk, int 
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipLaunchKernelGGL(kern, dim3(n_rblk * n_qblk), dim3(512), lds, st, (const __bf16*)X,
                        n_valid, rows_per_blk, (const __bf16*)Q, NQ, n_qblk, xcd, thr, cand_s,
-                       cand_i, cand_n, cap, 0, (const int*)nullptr);
+                       cand_i, cand_n, cap, 0, (const int*)nullptr, MqList{nullptr, 0});
     return (int)hipGetLastError();
   };
   switch (abl + 8 * (sets == 2) + 16 * (rsplit == 2)) {

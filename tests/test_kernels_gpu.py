@@ -527,19 +527,37 @@ def test_prune_qquant_and_route_match_torch():
         cs[j, :c] = T0[j] - 0.5 * margin[j]
         cs[j, c:c + 3] = T0[j] - 2.0 * margin[j]
         cnt[j] = c + 3 if j < 200 else cap + 5
+    # their rows: block 2 (of 4 blocks of 5000 rows) for queries >= 120, else block j % 2
+    rpb, nblk = 5000, 4
+    blk_of = torch.tensor([2 if j >= 120 else j % 2 for j in range(nq)], dtype=torch.int32,
+                          device=DEV)
+    ci = (blk_of[:, None] * rpb + torch.arange(cap, dtype=torch.int32, device=DEV)[None] % rpb)
+    ci = ci.to(torch.int32).contiguous()
     T, thr = torch.empty(nq, device=DEV), torch.empty(nq, device=DEV)
     dense = torch.empty(1, dtype=torch.int32, device=DEV)
+    est = torch.empty(nq, nblk, device=DEV)
+    blkmax = torch.empty(nblk, dtype=torch.int32, device=DEV)
+    blk = torch.empty(2 + 2 * nblk, dtype=torch.int32, device=DEV)
     thr0 = (T0 - 3.0 * margin).contiguous()    # the sample emitted below the band: exact counts
+    inf = float("inf")
 
-    def route(rows, limit, t0=thr0):
+    def route(rows, limit, t0=thr0, blk_limit=inf, max_list=nblk):
         h.prune_route(rows, pre.data_ptr(), tail.data_ptr(), k, shard.MQ_THR_MARGIN, sq.data_ptr(),
-                      margin.data_ptr(), t0.data_ptr(), cs.data_ptr(), cnt.data_ptr(), cap, ts,
-                      limit, T.data_ptr(), thr.data_ptr(), dense.data_ptr(), st)
+                      margin.data_ptr(), t0.data_ptr(), cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(),
+                      cap, ts, rpb, nblk, blk_limit, limit, max_list, T.data_ptr(), thr.data_ptr(),
+                      dense.data_ptr(), est.data_ptr(), blkmax.data_ptr(), blk.data_ptr(), st)
         torch.cuda.synchronize()
         return int(dense.item())
 
     assert route(150, 150 << ts) == 0          # at most 149 in-band rows: estimate <= limit
+    assert blk[0].item() == 0 and blk[2 + nblk:].sum().item() == 0
+    # per-block estimates: query j's j in-band rows, all in its block
+    want = torch.zeros(150, nblk, device=DEV)
+    want[torch.arange(150), blk_of[:150].long()] = torch.arange(150, device=DEV).float() * (1 << ts)
+    _close(est[:150], want, atol=0, what="per-block estimates")
     assert route(151, 149 << ts) == 1          # query 150 estimates 150 << 5 > limit
+    assert blk[0].item() == nblk and blk[2 + nblk:].tolist() == [1] * nblk
+    assert blk[2:2 + nblk].tolist() == list(range(nblk))
     assert route(nq, 1 << 40) == 1             # overflowed sample buffers always route dense
     assert torch.equal(T, T0)
     _close(thr, thr_t, atol=1e-4, rtol=1e-5, what="emission thresholds")
@@ -547,6 +565,18 @@ def test_prune_qquant_and_route_match_torch():
     # (query 60: cnt 63, (63 - 10) * m / (0.1 m) = 530 rows -> 530 << 5 = 16960)
     high = (T0 - 0.1 * margin).contiguous()
     assert route(61, 16000, high) == 1 and route(61, 17500, high) == 0
+    # per-block route: only block 2 holds a query estimating > 120 << 5 rows (queries 120-149;
+    # blocks 0 / 1 peak at queries 118 / 119) -> it alone goes to the bf16 scan
+    assert route(150, 1 << 40, blk_limit=120 << ts) == 0
+    assert blk[:3].tolist() == [1, nblk, 2] and blk[2 + nblk:].tolist() == [0, 0, 1, 0]
+    # ... and what is left to the int8 scan decides: query 119 keeps 119 << 5 rows there
+    assert route(150, 118 << ts, blk_limit=120 << ts) == 1
+    assert route(150, 119 << ts, blk_limit=120 << ts) == 0
+    # more flooded blocks (0, 1, 2) than the bf16 scan's row slots (2): every block
+    assert route(150, 1 << 40, blk_limit=50 << ts, max_list=2) == 1
+    assert blk[0].item() == nblk and blk[2 + nblk:].tolist() == [1] * nblk
+    assert route(150, 1 << 40, blk_limit=50 << ts, max_list=3) == 0
+    assert blk[:5].tolist() == [3, nblk, 0, 1, 2] and blk[2 + nblk:].tolist() == [1, 1, 1, 0]
 
 
 @pytest.mark.parametrize("route", [True, False])
@@ -568,6 +598,8 @@ def test_index_pruned_search_routes_dense_data_exactly(route):
     # 1M rows crowd the int8 band ~100x less than the 100M-row benchmark shard: scale the
     # candidate buffer down with them (the busiest query emits ~2k candidates here)
     shard.PRUNE_CAP = 1024
+    # (and no single block holds a flood at this scale: the whole-batch rule decides here)
+    shard.PRUNE_BLOCK_FRAC = 1.0
     q = gen.unit(nq, seed=77).bfloat16()
     ref.scan_mq = False
     s0, r0 = ref.search(q, k)
@@ -578,6 +610,55 @@ def test_index_pruned_search_routes_dense_data_exactly(route):
     assert int(ovf.item()) == (0 if route else 1)
     _close(s1, s0, atol=2e-5, what="routed pruned vs exact scores")
     assert (r0 == r1).float().mean().item() > 0.999
+
+
+@pytest.mark.parametrize("where", ["middle", "tail"])
+def test_index_pruned_search_routes_crowded_blocks_exactly(where):
+    """A crowd of near-duplicates (cosine ~0.99, like freshly ingested random-init embeddings)
+    in one row range: the int8 bound cannot separate it, so its blocks alone go to the bf16
+    emitting scan (index_mq.hip list mode) while the int8 scan skips them, both filling the same
+    candidate buffers.  Same rows and scores as the exact bf16 scan, no overflow, and only a few
+    blocks routed (the old whole-batch route would have scanned every row in bf16)."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+
+    n, crowd, k, nq = (1 << 20) + 3000, 60_000, 10, 256
+    g = torch.Generator(device=DEV).manual_seed(5)
+    center = torch.nn.functional.normalize(torch.randn(1, 384, device=DEV, generator=g), dim=-1)
+
+    def near(m):
+        return torch.nn.functional.normalize(
+            center + 0.0051 * torch.randn(m, 384, device=DEV, generator=g), dim=-1)
+
+    rows = torch.nn.functional.normalize(torch.randn(n, 384, device=DEV, generator=g), dim=-1)
+    c0 = 400_000 if where == "middle" else n - crowd
+    rows[c0:c0 + crowd] = near(crowd)
+    ref = HbmIndexShard(384, n)
+    shard = HbmIndexShard(384, n, prune="i8")
+    for sh in (ref, shard):
+        sh.append_f32(rows)
+    q = near(nq).bfloat16()
+    ref.scan_mq = False
+    s0, r0 = ref.search(q, k)
+    s1, r1 = shard.search(q, k)
+    cnt, ovf = shard._mq_last
+    blk = shard._route_blk_last
+    torch.cuda.synchronize()
+    n_rblk = int(blk[1].item())
+    listed = int(blk[0].item())
+    assert int(shard._route_last.item()) == 0 and int(ovf.item()) == 0
+    assert 1 <= listed <= n_rblk // 4, (listed, n_rblk)
+    flags = blk[2 + n_rblk:2 + 2 * n_rblk].bool()
+    rpb = shard._i8_geometry(n, nq, shard._n_cus())[1]
+    lo, hi = c0 // rpb, (c0 + crowd - 1) // rpb
+    # every block inside the crowd goes to the bf16 scan (the edge blocks hold a partial crowd,
+    # and the last ~4-8k rows are the exact tail, never sampled: either route is exact there)
+    assert flags[lo + 1:hi].all(), "the crowd's blocks go to the bf16 scan"
+    _close(s1, s0, atol=2e-5, what="block-routed pruned vs exact scores")
+    true = (q.float() @ shard.unit_rows().float().t()).gather(1, r1.long())
+    _close(s1, true, atol=2e-3, what="block-routed returned rows")
+    srt = r1.sort(dim=1).values
+    assert (srt[:, 1:] != srt[:, :-1]).all(), "a row emitted by both scans would repeat"
+    assert ((r1 >= c0) & (r1 < c0 + crowd)).all(), "the crowd holds every query's top-k"
 
 
 def test_pruned_search_split_across_streams_matches_search():
