@@ -1,6 +1,6 @@
 # Round 3 batch I: the driver's scaling-run shapes rehearsed on one GPU (gloo ranks, both launch
-# forms: torch.distributed.run and bench.py's own self-launch), the held-out search sustained for
-# 1000 searches with a clock/power timeline, then the full GPU test suite and smoke.
+# forms: torch.distributed.run and bench.py's own self-launch), then the full GPU test suite and
+# smoke.
 set -o pipefail
 export PYTHONUNBUFFERED=1
 O=gpurun_out/${1:-r3_i}; mkdir -p $O
@@ -13,9 +13,6 @@ done
 SYMB_DIST_BACKEND=gloo SYMB_DEVICE_INDEX=0 timeout -k 10 400 python bench.py --gpus 2 --steps 5 --warmup 2 \
     > $O/self_n2.json 2> $O/self_n2.err || { tail -30 $O/self_n2.err; exit 1; }
 tail -c 600 $O/self_n2.json; echo
-timeout -k 10 400 python bench.py --mode search --steps 1000 --warmup 5 --timeline $O/timeline_search.jsonl \
-    > $O/search_1000.json 2> $O/search_1000.err || { tail -30 $O/search_1000.err; exit 1; }
-python -c "import json;r=json.loads(open('$O/search_1000.json').read().strip().splitlines()[-1]);print('search1000',r['ms_per_step'],r['value'],r.get('step_ms_first_decile'),r.get('step_ms_last_decile'),r.get('search_dense_route_batches'),r.get('search_overflow_batches'))"
 timeout -k 10 1500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
 tail -3 $O/gpu_tests.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -30 $O/smoke.log; exit 1; }
