@@ -568,7 +568,7 @@ class HbmIndexShard:
 
     def _scan_mq(self, n: int, q_unit: torch.Tensor, kmax: int, k: int, thr, n_cus, rows=None,
                  tshift: int = 0, gate=None, out=None, fallback: bool = True, cand: bool = False,
-                 cap: int | None = None):
+                 cap: int | None = None, min_tiles: int = 16):
         """512-query-per-workgroup scan emitting every score above ``thr`` (index_mq.hip), top-k
         of each query's candidates, and the exact 256-query kernel as a fallback that runs on the
         GPU only if some query's candidate buffer overflowed (a device flag gates it).
@@ -578,7 +578,8 @@ class HbmIndexShard:
         then write ``out`` and OR into its overflow flag, ``out[2]``).  ``fallback=False``: no
         overflow re-scan -- for a threshold sample that is still sound, since the top-k of ANY
         subset of real rows lower-bounds the k-th best.  ``cand``: also return the candidate
-        buffers (scores, rows, count) for the route estimate of _search_pruned."""
+        buffers (scores, rows, count) for the route estimate of _search_pruned.  ``min_tiles``:
+        row-block floor in 64-row tiles (1 spreads a small scan over every CU)."""
         from ..ops._ext import hip, stream_handle
 
         h = hip()
@@ -588,7 +589,7 @@ class HbmIndexShard:
         n_qblk = math.ceil(NQ / h.mq_queries_per_blk(sets, rsplit))
         if n_cus is None:
             n_cus = self._n_cus()
-        n_rblk = max(1, min(math.ceil(n / (TILE_ROWS * 16)), max(1, round(n_cus / n_qblk))))
+        n_rblk = max(1, min(math.ceil(n / (TILE_ROWS * min_tiles)), max(1, round(n_cus / n_qblk))))
         rows_per_blk = _round_up(max(1, math.ceil(n / n_rblk)), TILE_ROWS)
         n_rblk = max(1, math.ceil(n / rows_per_blk))
         rows = self.rows if rows is None else rows
@@ -717,8 +718,13 @@ class HbmIndexShard:
         pre_s, _, cs_p, ci_p, cnt_p = self._scan_mq(nv * TILE_ROWS, q_unit, kmax, k, thr0, n_cus,
                                                     tshift=ts, fallback=False, cand=True,
                                                     cap=self.SAMPLE_CAP)
-        tail_s, _ = self._scan(n - t0, q_unit, kmax, k, thr0, n_cus, self.rows[t0:], "bf16",
-                               min_tiles=pm)
+        # the fresh-row tail [t0, n) (never sampled) is scanned exactly and emits every row >= thr0
+        # too (one slot per tail row: no overflow), so the route counts its band rows one by one
+        # -- a crowd of fresh near-duplicates sits there first
+        tcap = n - t0
+        tail_s, _, tcs, tci, tcnt = self._scan_mq(tcap, q_unit, kmax, k, thr0, n_cus,
+                                                  rows=self.rows[t0:], fallback=False, cand=True,
+                                                  cap=tcap, min_tiles=pm)
         # 2. T (k-th best of the union), the per-query emission threshold (T - margin) / sq and
         #    the per-row-block route (prune_route): the blocks some query would flood with int8
         #    candidates go to the bf16 emitting scan at T, the rest to the int8 scan
@@ -738,7 +744,8 @@ class HbmIndexShard:
                       ci_p.data_ptr(), cnt_p.data_ptr(), self.SAMPLE_CAP, ts, geo[1], n_rblk,
                       blk_limit, limit, self._mq_slots(NQ, n_cus)[3], T.data_ptr(),
                       thr.data_ptr(), dense.data_ptr(), est.data_ptr(), blkmax.data_ptr(),
-                      blk.data_ptr(), st)
+                      blk.data_ptr(), st, tail_cs=tcs.data_ptr(), tail_ci=tci.data_ptr(),
+                      tail_cnt=tcnt.data_ptr(), tail_cap=tcap, tail_off=t0)
         return dict(q=q_unit, k=k, n=n, n_cus=n_cus, q8=q8, sq=sq, thr=thr, T=T, dense=dense,
                     blk=blk, geo=geo)
 

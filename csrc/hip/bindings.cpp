@@ -75,7 +75,9 @@ int symb_prune_route(int NQ, const float* pre_s, const float* tail_s, int k, flo
                      const float* sq, const float* margin, const float* thr0, const float* cs_p,
                      const int* ci_p, const int* cnt_p, int cap_p, int tshift, int rows_per_blk,
                      int n_rblk, float blk_limit, float limit, int max_list, float* T, float* thr,
-                     int* dense, float* est, int* blkmax, int* blk, hipStream_t st);
+                     int* dense, float* est, int* blkmax, int* blk, hipStream_t st,
+                     const float* tail_cs, const int* tail_ci, const int* tail_cnt, int tail_cap,
+                     int tail_off);
 int symb_i8_config(int tile_rows, int waves);
 int symb_i8_tile_rows();
 int symb_i8_wgs_per_cu();
@@ -381,15 +383,23 @@ PYBIND11_MODULE(_hip, m) {
                           uptr margin, uptr thr0, uptr cs_p, uptr ci_p, uptr cnt_p, int cap_p,
                           int tshift, int rows_per_blk, int n_rblk, float blk_limit, float limit,
                           int max_list, uptr T, uptr thr, uptr dense, uptr est, uptr blkmax,
-                          uptr blk, uptr st) {
+                          uptr blk, uptr st, uptr tail_cs, uptr tail_ci, uptr tail_cnt,
+                          int tail_cap, int tail_off) {
     check(symb_prune_route(NQ, P<const float>(pre_s), P<const float>(tail_s), k, thr_margin,
                            P<const float>(sq), P<const float>(margin), P<const float>(thr0),
                            P<const float>(cs_p), P<const int>(ci_p), P<const int>(cnt_p), cap_p,
                            tshift, rows_per_blk, n_rblk, blk_limit, limit, max_list, P<float>(T),
                            P<float>(thr), P<int>(dense), P<float>(est), P<int>(blkmax),
-                           P<int>(blk), S(st)),
+                           P<int>(blk), S(st), P<const float>(tail_cs), P<const int>(tail_ci),
+                           P<const int>(tail_cnt), tail_cap, tail_off),
           "prune_route");
-  });
+  }, py::arg("NQ"), py::arg("pre_s"), py::arg("tail_s"), py::arg("k"), py::arg("thr_margin"),
+     py::arg("sq"), py::arg("margin"), py::arg("thr0"), py::arg("cs_p"), py::arg("ci_p"),
+     py::arg("cnt_p"), py::arg("cap_p"), py::arg("tshift"), py::arg("rows_per_blk"),
+     py::arg("n_rblk"), py::arg("blk_limit"), py::arg("limit"), py::arg("max_list"), py::arg("T"),
+     py::arg("thr"), py::arg("dense"), py::arg("est"), py::arg("blkmax"), py::arg("blk"),
+     py::arg("stream"), py::arg("tail_cs") = 0, py::arg("tail_ci") = 0, py::arg("tail_cnt") = 0,
+     py::arg("tail_cap") = 0, py::arg("tail_off") = 0);
   m.def("index_scan_i8_ablate", [](uptr X8, uptr sx, int n_valid, int alloc_rows,
                                    int rows_per_blk, int n_rblk, uptr Q8, int NQ, uptr thr,
                                    uptr cand_s, uptr cand_i, uptr cand_n, int cap, int xcd, uptr st,

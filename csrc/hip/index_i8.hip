@@ -704,14 +704,25 @@ __global__ __launch_bounds__(256) void prune_qquant_kernel(const __bf16* __restr
 
 constexpr int ROUTE_MAX_BLOCKS = 1024;   // int8 row blocks the per-block route can bin
 
+// The exact tail scan's candidates (rows >= thr0 of the fresh rows [off, n), ids relative to
+// off, one slot per tail row so none is dropped): binned one by one, no sampling scale.
+struct RouteTail {
+  const float* cs;
+  const int* ci;
+  const int* cnt;
+  int cap;
+  int off;
+};
+
 __global__ __launch_bounds__(256) void prune_route_kernel(
     int NQ, const float* __restrict__ pre_s, const float* __restrict__ tail_s, int k,
     float thr_margin, const float* __restrict__ sq, const float* __restrict__ margin,
     const float* __restrict__ thr0, const float* __restrict__ cs_p, const int* __restrict__ ci_p,
     const int* __restrict__ cnt_p, int cap_p, int tshift, int rows_per_blk, int n_rblk,
     float* __restrict__ T_out, float* __restrict__ thr, int* __restrict__ dense,
-    float* __restrict__ est, int* __restrict__ blkmax) {
+    float* __restrict__ est, int* __restrict__ blkmax, RouteTail tail) {
   __shared__ int hist[4][ROUTE_MAX_BLOCKS];
+  __shared__ int thist[4][ROUTE_MAX_BLOCKS];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int q = blockIdx.x * 4 + w;
   if (q >= NQ) return;   // (no barrier in this kernel: each wave bins its own query)
@@ -734,7 +745,11 @@ __global__ __launch_bounds__(256) void prune_route_kernel(
   const float* cs = cs_p + (size_t)q * cap_p;
   const int* ci = ci_p + (size_t)q * cap_p;
   int* h = hist[w];
-  for (int b = lane; b < n_rblk; b += 64) h[b] = 0;
+  int* th = thist[w];
+  for (int b = lane; b < n_rblk; b += 64) {
+    h[b] = 0;
+    th[b] = 0;
+  }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   float c = 0.f;
   for (int i = lane; i < n; i += 64) {
@@ -743,14 +758,24 @@ __global__ __launch_bounds__(256) void prune_route_kernel(
       atomicAdd(&h[min(ci[i] / rows_per_blk, n_rblk - 1)], 1);
     }
   }
+  if (tail.cs != nullptr) {   // the exact tail: every row >= thr0 of it, counted one by one
+    const int tn = min(tail.cnt[q], tail.cap);
+    const float* tcs = tail.cs + (size_t)q * tail.cap;
+    const int* tci = tail.ci + (size_t)q * tail.cap;
+    for (int i = lane; i < tn; i += 64)
+      if (tcs[i] >= band) atomicAdd(&th[min((tci[i] + tail.off) / rows_per_blk, n_rblk - 1)], 1);
+  }
   c = wave_sum(c);
   const float binned = c;
-  if (band < t0)   // the band reaches below what the sample emitted: extrapolate (see above)
+  float tscale = 1.f;
+  if (band < t0) {   // the band reaches below what the sample emitted: extrapolate (see above)
     c = fmaxf((float)cnt, fmaxf(0.f, (float)(cnt - k)) * m / fmaxf(T - t0, 1e-6f));
+    tscale = binned > 0.f ? fmaxf(1.f, c / binned) : 1.f;   // (the tail emitted >= thr0 too)
+  }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   const float scale = (binned > 0.f ? c / binned : 0.f) * (float)(1 << tshift);
   for (int b = lane; b < n_rblk; b += 64) {
-    const float e = (float)h[b] * scale;
+    const float e = (float)h[b] * scale + (float)th[b] * tscale;
     est[(size_t)q * n_rblk + b] = e;
     if (e > 0.f) atomicMax(blkmax + b, __float_as_int(e));   // (non-negative floats order as ints)
   }
@@ -965,20 +990,26 @@ int symb_prune_qquant(const void* Q, int NQ, int dim, const float* bounds, void*
 // iff every block went to the bf16 scan; blk holds 2 + 2 n_rblk ints (layout at the final
 // kernel); est: NQ x n_rblk floats and blkmax: n_rblk ints of scratch.  ci_p: the sample's
 // candidate rows (physical), rows_per_blk / n_rblk: the int8 scan's row blocks (n_rblk <= 1024).
+// tail_* (optional): the exact tail scan's candidates (RouteTail).
 int symb_prune_route(int NQ, const float* pre_s, const float* tail_s, int k, float thr_margin,
                      const float* sq, const float* margin, const float* thr0, const float* cs_p,
                      const int* ci_p, const int* cnt_p, int cap_p, int tshift, int rows_per_blk,
                      int n_rblk, float blk_limit, float limit, int max_list, float* T, float* thr,
-                     int* dense, float* est, int* blkmax, int* blk, hipStream_t st) {
+                     int* dense, float* est, int* blkmax, int* blk, hipStream_t st,
+                     const float* tail_cs, const int* tail_ci, const int* tail_cnt, int tail_cap,
+                     int tail_off) {
   if (NQ <= 0) return 0;
   if (k < 1 || k > 32 || cap_p <= 0 || tshift < 0 || tshift > 20) return -1;
   if (n_rblk < 1 || n_rblk > ROUTE_MAX_BLOCKS || rows_per_blk < 1 || max_list < 1) return -1;
+  if (tail_cs != nullptr && (tail_ci == nullptr || tail_cnt == nullptr || tail_cap < 1 || tail_off < 0))
+    return -1;
   hipError_t e = hipMemsetAsync(dense, 0, sizeof(int), st);
   if (e == hipSuccess) e = hipMemsetAsync(blkmax, 0, sizeof(int) * (size_t)n_rblk, st);
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(prune_route_kernel, dim3((NQ + 3) / 4), dim3(256), 0, st, NQ, pre_s, tail_s,
                      k, thr_margin, sq, margin, thr0, cs_p, ci_p, cnt_p, cap_p, tshift,
-                     rows_per_blk, n_rblk, T, thr, dense, est, blkmax);
+                     rows_per_blk, n_rblk, T, thr, dense, est, blkmax,
+                     RouteTail{tail_cs, tail_ci, tail_cnt, tail_cap, tail_off});
   hipLaunchKernelGGL(prune_route_final_kernel, dim3(1), dim3(1024), 0, st, NQ, n_rblk, est, blkmax,
                      blk_limit, limit, max_list, dense, blk);
   return (int)hipGetLastError();

@@ -577,6 +577,25 @@ def test_prune_qquant_and_route_match_torch():
     assert blk[0].item() == nblk and blk[2 + nblk:].tolist() == [1] * nblk
     assert route(150, 1 << 40, blk_limit=50 << ts, max_list=3) == 0
     assert blk[:5].tolist() == [3, nblk, 0, 1, 2] and blk[2 + nblk:].tolist() == [1, 1, 1, 0]
+    # the exact tail's candidates count one by one (no sampling scale): query j gets j % 7 band
+    # rows and 2 rows below the band in a tail starting at row 3 * rpb + 10 (block 3)
+    tcap = 16
+    tcs = torch.full((nq, tcap), -1.0, device=DEV)
+    tcnt = torch.zeros(nq, dtype=torch.int32, device=DEV)
+    for j in range(nq):
+        tcs[j, :j % 7] = T0[j] - 0.5 * margin[j]
+        tcs[j, j % 7:j % 7 + 2] = T0[j] - 2.0 * margin[j]
+        tcnt[j] = j % 7 + 2
+    tci = torch.arange(tcap, dtype=torch.int32, device=DEV).repeat(nq, 1).contiguous()
+    h.prune_route(150, pre.data_ptr(), tail.data_ptr(), k, shard.MQ_THR_MARGIN, sq.data_ptr(),
+                  margin.data_ptr(), thr0.data_ptr(), cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(),
+                  cap, ts, rpb, nblk, inf, inf, nblk, T.data_ptr(), thr.data_ptr(),
+                  dense.data_ptr(), est.data_ptr(), blkmax.data_ptr(), blk.data_ptr(), st,
+                  tail_cs=tcs.data_ptr(), tail_ci=tci.data_ptr(), tail_cnt=tcnt.data_ptr(),
+                  tail_cap=tcap, tail_off=3 * rpb + 10)
+    torch.cuda.synchronize()
+    want[:, 3] += torch.arange(150, device=DEV).float() % 7
+    _close(est[:150], want, atol=0, what="per-block estimates with the exact tail")
 
 
 @pytest.mark.parametrize("route", [True, False])
@@ -653,6 +672,8 @@ def test_index_pruned_search_routes_crowded_blocks_exactly(where):
     # every block inside the crowd goes to the bf16 scan (the edge blocks hold a partial crowd,
     # and the last ~4-8k rows are the exact tail, never sampled: either route is exact there)
     assert flags[lo + 1:hi].all(), "the crowd's blocks go to the bf16 scan"
+    if where == "tail":   # the exact tail scan counts its crowd rows: the last block goes too
+        assert flags[n_rblk - 1], "the tail's block goes to the bf16 scan"
     _close(s1, s0, atol=2e-5, what="block-routed pruned vs exact scores")
     true = (q.float() @ shard.unit_rows().float().t()).gather(1, r1.long())
     _close(s1, true, atol=2e-3, what="block-routed returned rows")
