@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--tile", type=int, default=9)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--torch", action="store_true")
+    ap.add_argument("--w4", type=int, default=-1,
+                    help="gemm4w.hip (persistent 4-wave kernel) with this many rows per tile (0 = auto)")
     ap.add_argument("--abl", type=int, default=0, help="gemm256 ablation (1: no stores, 2: no epilogue)")
     ap.add_argument("--lt", type=int, default=0,
                     help="hipBLASLt route for plain projections (gemm_lt_config: 0 off, 1 auto)")
@@ -44,6 +46,8 @@ def main():
     hip().gemm_config(128, a.tile, 8)
     hip().gemm256_ablate(a.abl)
     hip().gemm_lt_config(a.lt)
+    if a.w4 >= 0:
+        hip().gemm4w_config(3, a.w4)
     f = (lambda: torch.matmul(x, w.t(), out=y)) if a.torch else (lambda: K.gemm(x, w, b, a.epi, r, out=y))
     for _ in range(3):
         f()
@@ -55,7 +59,7 @@ def main():
     e.record()
     torch.cuda.synchronize()
     ms = s.elapsed_time(e) / a.iters
-    print(json.dumps({"abl": a.abl, "lt": a.lt, "m": a.m, "n": a.n, "k": a.k, "epi": a.epi, "tile": a.tile, "torch": a.torch,
+    print(json.dumps({"w4": a.w4, "abl": a.abl, "lt": a.lt, "m": a.m, "n": a.n, "k": a.k, "epi": a.epi, "tile": a.tile, "torch": a.torch,
                       "ms": round(ms, 4), "TFLOPs": round(2 * a.m * a.n * a.k / ms / 1e9)}))
 
 

@@ -1,0 +1,92 @@
+#!/usr/bin/env python3
+"""Encoder GEMM shapes, every route in ONE process with interleaved rounds (A/B discipline).
+
+    python benchmarks/gemm_sweep.py [--models bge-base,e5-large] [--variants t3,t9,lt,torch]
+
+Variants: tN = gemm.hip with symb_gemm_config tile mode N and the hipBLASLt route off;
+lt = the default tiles with the hipBLASLt route on; torch = torch.matmul (hipBLASLt, no epilogue).
+Operands are random (the clock the chip holds depends on the data).  One JSON line per
+(shape, variant): median / min us over the rounds and TFLOP/s at the median.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+# (name, N, K, epi) per model at M = batch x seq tokens; epi 0 bias, 1 GELU, 2 bias + residual
+SHAPES = {
+    "minilm-l6": [("qkv", 1152, 384, 0), ("ffn1", 1536, 384, 1)],
+    "bge-base": [("qkv", 2304, 768, 0), ("out", 768, 768, 2), ("ffn1", 3072, 768, 1), ("ffn2", 768, 3072, 2)],
+    "e5-large": [("qkv", 3072, 1024, 0), ("out", 1024, 1024, 2), ("ffn1", 4096, 1024, 1), ("ffn2", 1024, 4096, 2)],
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--models", default="bge-base,e5-large")
+    ap.add_argument("--variants", default="t3,t9,lt,torch")
+    ap.add_argument("--m", type=int, default=32768)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    from codename_symbiont_amd.ops import kernels as K
+    from codename_symbiont_amd.ops._ext import hip
+
+    g = torch.Generator(device="cuda").manual_seed(0)
+    for model in a.models.split(","):
+        for name, n, k, epi in SHAPES[model]:
+            x = torch.randn(a.m, k, device="cuda", generator=g).bfloat16()
+            w = (torch.randn(n, k, device="cuda", generator=g) / math.sqrt(k)).bfloat16()
+            b = torch.randn(n, device="cuda", generator=g)
+            r = torch.randn(a.m, n, device="cuda", generator=g).bfloat16() if epi >= 2 else None
+            y = torch.empty(a.m, n, device="cuda", dtype=torch.bfloat16)
+
+            def mk(v):
+                if v == "torch":
+                    return lambda: torch.matmul(x, w.t(), out=y)
+                if v == "lt":
+                    return lambda: (hip().gemm_config(128, 3, 8), hip().gemm_lt_config(1),
+                                    K.gemm(x, w, b, epi, r, out=y))
+                if v.startswith("w4"):   # gemm4w.hip (w4 = auto rows per tile, w4_192 / w4_256)
+                    bm = int(v[3:]) if "_" in v else 0
+                    return lambda: (hip().gemm4w_config(3, bm), hip().gemm_lt_config(0),
+                                    K.gemm(x, w, b, epi, r, out=y), hip().gemm4w_config(0, 0))
+                t = int(v[1:])
+                return lambda: (hip().gemm_config(128, t, 8), hip().gemm_lt_config(0),
+                                K.gemm(x, w, b, epi, r, out=y))
+
+            fns = {v: mk(v) for v in a.variants.split(",")}
+            times = {v: [] for v in fns}
+            for f in fns.values():
+                for _ in range(3):
+                    f()
+            torch.cuda.synchronize()
+            for _ in range(a.rounds):
+                for v, f in fns.items():
+                    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    f()
+                    s.record()
+                    for _ in range(a.iters):
+                        f()
+                    e.record()
+                    torch.cuda.synchronize()
+                    times[v].append(s.elapsed_time(e) / a.iters * 1e3)
+            for v, ts in times.items():
+                med = statistics.median(ts)
+                print(json.dumps({"model": model, "gemm": name, "m": a.m, "n": n, "k": k, "epi": epi,
+                                  "variant": v, "us_med": round(med, 1), "us_min": round(min(ts), 1),
+                                  "TFLOPs": round(2 * a.m * n * k / med / 1e6)}), flush=True)
+    hip().gemm_config(128, 3, 8)
+    hip().gemm_lt_config(1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,5 +1,5 @@
 # round-2 validation: pytest -m gpu, smoke, headline bench, rocprof kernel stats of the headline
-# usage: bash benchmarks/gpu_r2.sh <tag>
+# usage: bash benchmarks/gpu/archive/gpu_r2.sh <tag>
 set -o pipefail
 export PYTHONUNBUFFERED=1
 O=gpurun_out/${1:-r2}; mkdir -p $O

@@ -9,4 +9,4 @@ for v in i8 none; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_aniso_$v -o s -- python bench.py --mode search --corpus anisotropic --steps 10 --warmup 2 --index-prune $v > $O/aniso_$v.json 2> $O/aniso_$v.err || exit 1
   tail -c 400 $O/aniso_$v.json; echo
 done
-bash benchmarks/gpu_r3_sustain.sh r3_c/sustain 1000
+bash benchmarks/gpu/archive/gpu_r3_sustain.sh r3_c/sustain 1000

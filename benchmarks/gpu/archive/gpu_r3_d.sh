@@ -10,4 +10,4 @@ for a in "aniso_i8:--corpus anisotropic" "aniso_none:--corpus anisotropic --inde
   timeout -k 10 300 python bench.py $S $args > $O/$name.json 2> $O/$name.err || { echo FAIL $name; tail -20 $O/$name.err; exit 1; }
   python -c "import json;r=json.load(open('$O/$name.json'));print('$name',r['ms_per_step'],r['value'],r.get('search_dense_route_batches'),r.get('verify_exact'),r.get('verify_ids_identical'))"
 done
-bash benchmarks/gpu_r3_sustain.sh r3_d/sustain 1000
+bash benchmarks/gpu/archive/gpu_r3_sustain.sh r3_d/sustain 1000

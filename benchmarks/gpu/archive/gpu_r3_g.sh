@@ -10,4 +10,4 @@ for r in 0 248 240 0 248 240; do
 done
 SYMB_SEARCH_MAX_BATCH=512 SYMB_SCAN_CUS=224 timeout -k 10 600 python benchmarks/e2e_service.py --index-rows 100000000 --requests 40000 --warmup-requests 8000 --concurrency 256 > $O/e2e.json 2> $O/e2e.err || { tail -30 $O/e2e.err; exit 1; }
 tail -1 $O/e2e.json | python -c "import json,sys;r=json.loads(sys.stdin.read());print(r['value'],r['search_latency_ms']);print(json.dumps(r['service_stages_ms']));print(json.dumps(r['service_counters']))"
-bash benchmarks/gpu_r3_real.sh r3_g/real
+bash benchmarks/gpu/archive/gpu_r3_real.sh r3_g/real

@@ -11,4 +11,4 @@ for c in 256 512; do
   SYMB_SEARCH_MAX_BATCH=512 SYMB_SCAN_CUS=224 timeout -k 10 600 python benchmarks/e2e_service.py --index-rows 100000000 --requests 40000 --warmup-requests 8000 --concurrency $c > $O/e2e_c$c.json 2> $O/e2e_c$c.err || { tail -30 $O/e2e_c$c.err; exit 1; }
   tail -1 $O/e2e_c$c.json | python -c "import json,sys;r=json.loads(sys.stdin.read());print('e2e c$c',r['value'],r['search_latency_ms'],r['gateway_hops_ms']);print(json.dumps(r['service_stages_ms']['vector_memory_service']))"
 done
-bash benchmarks/gpu_r3_sustain.sh r3_h/sustain 1000
+bash benchmarks/gpu/archive/gpu_r3_sustain.sh r3_h/sustain 1000

@@ -2,7 +2,7 @@
 # held-out queries) for the exact int8-pruned search (with its sampled route) vs the plain bf16
 # emitting scan, ids verified against the full bf16 list scan, at the 1-GPU headline shape and the
 # per-rank shapes of the N = 2 / 4 / 8 sharded search (rows / N per rank, 256 N gathered queries).
-# usage: bash benchmarks/gpu_r3_real.sh <out-subdir> ["rows:batch ..."]
+# usage: bash benchmarks/gpu/archive/gpu_r3_real.sh <out-subdir> ["rows:batch ..."]
 set -o pipefail
 export PYTHONUNBUFFERED=1
 O=gpurun_out/${1:-r3_real}; mkdir -p $O

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Markdown table of a benchmarks/gpu_r3_real.sh output directory: per shape and corpus, the
+"""Markdown table of a benchmarks/gpu/archive/gpu_r3_real.sh output directory: per shape and corpus, the
 exact int8-pruned search (with its sampled route) against the plain bf16 emitting scan.
 
     python benchmarks/real_table.py gpurun_out/<dir> > profiles/<dir>/table.md

@@ -103,15 +103,24 @@ class Subscription:
             raise StopAsyncIteration
         return m
 
-    async def next_batch(self, max_n: int = 256) -> list[Msg] | None:
+    async def next_batch(self, max_n: int = 256, align: int = 0) -> list[Msg] | None:
         """Wait for one message, then take whatever else is already queued (up to ``max_n``);
-        None once the subscription has ended."""
+        None once the subscription has ended.
+
+        ``align`` > 0: when more than ``align`` messages are ready, take a whole multiple of it
+        and leave the rest queued for the next call -- a consumer whose unit of work is a block
+        of ``align`` items (the index scan's 256-query block) then never pays a whole extra
+        block for a few stragglers; a burst of ``align`` or fewer is taken whole (latency)."""
         if self._closed and self._q.empty():
             return None
         m = await self._q.get()
         if m is None:
             return None
         batch = [m]
+        if align > 0:
+            ready = 1 + self._q.qsize()   # (may count an end marker: at worst one short batch)
+            if ready > align:
+                max_n = min(max_n, ready) // align * align or max_n
         while len(batch) < max_n:
             try:
                 x = self._q.get_nowait()

@@ -881,6 +881,25 @@ class HbmIndexShard:
         """fp8 scan for oversample*k candidates, exact bf16 re-score, top-k (see the class doc)."""
         kc = min(32, max(16, self.oversample * k))
         _, cand = self._search_scan(q_unit, kc, self.rows8, "fp8", n_cus)    # [NQ, kc] rows
+        if self.dim == 384:
+            # the pruned search's kernels: exact bf16 re-score of the candidate rows (8 waves per
+            # query gather them) and the counted select; the scan's list is score-sorted, so the
+            # valid candidates are a prefix of each row
+            from ..ops._ext import hip, stream_handle
+
+            NQ, st, h = q_unit.shape[0], stream_handle(self.device), hip()
+            cand = cand.contiguous()
+            cnt = (cand >= 0).sum(1, dtype=torch.int32)
+            cs = torch.empty(NQ, kc, device=self.device)
+            h.rescore_bf16(self.rows.data_ptr(), q_unit.data_ptr(), NQ, self.dim, cand.data_ptr(),
+                           cnt.data_ptr(), kc, cs.data_ptr(), st)
+            out_s = torch.empty(NQ, k, device=self.device)
+            out_i = torch.empty(NQ, k, dtype=torch.int32, device=self.device)
+            ovf = torch.empty(1, dtype=torch.int32, device=self.device)
+            h.topk_select_counted(cs.data_ptr(), cand.data_ptr(), cnt.data_ptr(), kc, NQ,
+                                  16 if kc <= 16 else 32, k, out_s.data_ptr(), out_i.data_ptr(),
+                                  ovf.data_ptr(), st)
+            return out_s, out_i
         valid = cand >= 0
         rows = self.rows[cand.clamp_min(0).long()]                           # [NQ, kc, D] bf16
         exact = torch.bmm(rows.float(), q_unit.float().unsqueeze(-1)).squeeze(-1)

@@ -37,7 +37,7 @@ def init(backend: str | None = None, device_type: str | None = None,
          single_rank_group: bool = False) -> DistInfo:
     """Rehearsal knobs (one-GPU boxes; never set for real runs): ``SYMB_DIST_BACKEND=gloo`` and
     ``SYMB_DEVICE_INDEX=0`` put every rank of a multi-rank job on one device over gloo, since RCCL
-    refuses two ranks on one GPU (tests/test_parallel_gpu.py, benchmarks/gpu_bench_rehearsal.sh).
+    refuses two ranks on one GPU (tests/test_parallel_gpu.py, benchmarks/gpu/archive/gpu_bench_rehearsal.sh).
     ``single_rank_group``: create the process group even for a world of 1, so a one-GPU box runs
     the real RCCL calls of the collective paths (tests/test_rccl_gpu.py)."""
     rank, world, local = env_world()

@@ -66,7 +66,7 @@ class VectorMemoryService(Service):
         await self.subscribe_loop(subjects.TEXT_WITH_EMBEDDINGS, self.handle_store)
         # searches: whole drained bursts -> one native decode + one index scan + one socket write
         await self.subscribe_batches(subjects.SEARCH_SEMANTIC_REQUEST, self.handle_search_batch,
-                                     max_batch=self.SEARCH_MAX_BATCH)
+                                     max_batch=self.SEARCH_MAX_BATCH, align=self.cfg.search_align)
 
     # ------------------------------------------------------------------ storage
     async def handle_store(self, nmsg) -> None:

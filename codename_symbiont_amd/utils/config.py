@@ -76,6 +76,9 @@ class Config:
     # queries per fused scan launch of the search service (a 100M-row scan costs about the same
     # for 16 or 256 queries, so bigger bursts buy throughput at the price of latency)
     search_max_batch: int = field(default_factory=lambda: _int("SYMB_SEARCH_MAX_BATCH", 256))
+    # bursts larger than this take a whole multiple of it (the int8 scan's 256-query block: a
+    # 369-query burst would cost two full scans of the shard; 0 = take whatever is queued)
+    search_align: int = field(default_factory=lambda: _int("SYMB_SEARCH_ALIGN", 256))
     # CUs the index scans may occupy (0 = all): leave some to an encoder sharing the GPU
     scan_cus: int = field(default_factory=lambda: _int("SYMB_SCAN_CUS", 0))
     collection: str = "symbiont_document_embeddings"

@@ -46,6 +46,7 @@ int symb_index_scan_ablate(const void* X, int n_valid, int rows_per_blk, int n_r
                            const float* thr);
 int symb_gemm_config(int resln_bm, int tile, int group_m);
 int symb_gemm256_ablate(int abl);
+int symb_gemm4w_config(int mode, int bm);
 int symb_gemm_fp8_config(int waves, int big);
 int symb_gemm_resln_config(int waves);
 int symb_gemm_gelu_config(int poly);
@@ -486,6 +487,8 @@ PYBIND11_MODULE(_hip, m) {
     check(symb_attention_config(waves, kvt, xcd), "attention_config");
   }, py::arg("waves") = 8, py::arg("kvt") = 64, py::arg("xcd") = 2);
   m.def("gemm256_ablate", [](int abl) { check(symb_gemm256_ablate(abl), "gemm256_ablate"); });
+  m.def("gemm4w_config", [](int mode, int bm) { check(symb_gemm4w_config(mode, bm), "gemm4w_config"); },
+        py::arg("mode"), py::arg("bm") = 0);
   m.def("gemm_config", [](int resln_bm, int tile, int group_m) {
     check(symb_gemm_config(resln_bm, tile, group_m), "gemm_config");
   }, py::arg("resln_bm") = 128, py::arg("tile") = 3, py::arg("group_m") = 8);

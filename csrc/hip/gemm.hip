@@ -485,6 +485,30 @@ int symb_gemm_fp8_config(int waves, int big) {
   return 0;
 }
 
+// 4-wave persistent 256x256 kernel (gemm4w.hip): 0 = never, 1 = the plain bias / residual
+// projections of the wide shapes (K >= 768, N >= 768, M >= 4096 -- the ones the hipBLASLt route
+// below would take; this kernel then goes first), 2 = those plus the GELU FFN1 of the same
+// shapes, 3 = every shape it supports (N % 256, K % 64).  g_gemm4w_bm: rows per tile, 256 / 192
+// (0 = auto: the one whose last partial wave of tiles costs least).
+bool symb_gemm4w_supported(int M, int N, int K);
+int symb_gemm4w(int epi, int bm, const void* A, int lda, const void* W, int ldw, const float* bias,
+                const void* R, int ldr, void* C, int ldc, int M, int N, int K, int group_m,
+                int gelu_poly, hipStream_t st);
+static int g_gemm4w = 0, g_gemm4w_bm = 0;
+int symb_gemm4w_config(int mode, int bm) {
+  if (mode < 0 || mode > 3 || (bm != 0 && bm != 256 && bm != 192)) return -1;
+  g_gemm4w = mode;
+  g_gemm4w_bm = bm;
+  return 0;
+}
+static int gemm4w_bm(int M, int N) {
+  if (g_gemm4w_bm) return g_gemm4w_bm;
+  // time ~ (waves of tiles over 256 CUs) x (rows per tile)
+  const long w256 = ((((M + 255) / 256) * (N / 256)) + 255) / 256;
+  const long w192 = ((((M + 191) / 192) * (N / 256)) + 255) / 256;
+  return w192 * 192 < w256 * 256 ? 192 : 256;
+}
+
 // hipBLASLt for the plain bias / bias + residual projections (gemm_lt.cpp): 0 = never, 1 = auto
 // (K >= 768 and N >= 768 and M >= 4096: the bge-base / e5-large shapes, where the library's
 // kernels are faster; MiniLM's K = 384 projections stay here), 2 = every bias / residual GEMM.
@@ -521,6 +545,14 @@ int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const flo
     return -1;  // wider rows: EPI_RES + symb_add_ln
   }
   if (N % 128 != 0) return -1;
+  if (g_gemm4w && symb_gemm4w_supported(M, N, K)) {
+    const bool wide = K >= 768 && N >= 768 && M >= 4096;
+    const bool take = g_gemm4w == 3 || (wide && (epi == EPI_BIAS || epi == EPI_RES)) ||
+                      (wide && g_gemm4w == 2 && epi == EPI_GELU);
+    if (take)
+      return symb_gemm4w(epi, gemm4w_bm(M, N), A, lda, W, ldw, bias, R, ldr, C, ldc, M, N, K,
+                         g_group_m, g_gelu_poly, st);
+  }
   if ((epi == EPI_BIAS || epi == EPI_RES) &&
       (g_gemm_lt == 2 || (g_gemm_lt == 1 && K >= 768 && N >= 768 && M >= 4096))) {
     const int rc = symb_gemm_lt(epi, A, lda, W, ldw, bias, R, ldr, C, ldc, M, N, K, st);

@@ -300,3 +300,27 @@ def test_native_broker_http_monitoring():
         await a.close()
         await b.stop()
     run(main())
+
+
+def test_next_batch_align():
+    """next_batch(align=A): with more than A messages ready it takes a whole multiple of A (the
+    rest stays queued, in order); A or fewer ready are taken whole."""
+    from codename_symbiont_amd.bus.client import Msg, Subscription
+
+    async def with_timeout():
+        sub = Subscription(None, "1", "s", None)
+        for i in range(700):
+            sub._deliver(Msg("s", None, b"%d" % i))
+        a = await sub.next_batch(1024, align=256)
+        b = await sub.next_batch(1024, align=256)
+        assert (len(a), len(b)) == (512, 188)
+        assert [int(m.data) for m in a + b] == list(range(700))
+        for _ in range(300):
+            sub._deliver(Msg("s", None, b"x"))
+        assert len(await sub.next_batch(1024, align=0)) == 300
+        for _ in range(300):
+            sub._deliver(Msg("s", None, b"x"))
+        assert len(await sub.next_batch(200, align=256)) == 200   # max_n < align: plain cap
+        assert len(await sub.next_batch(200, align=256)) == 100
+
+    asyncio.run(with_timeout())

@@ -112,6 +112,33 @@ def test_gemm(M, N, K, epi, tile):
     _close(out, ref, atol=4e-2, rtol=2e-2, what=f"gemm epi={epi}")
 
 
+@pytest.mark.parametrize("bm", [256, 192])
+@pytest.mark.parametrize("M,N,K", [(32768, 768, 768), (4100, 2304, 768), (999, 768, 3072),
+                                   (77, 1024, 1024), (256, 256, 64), (70000, 512, 128),
+                                   (1000, 3072, 192)])
+@pytest.mark.parametrize("epi", [0, 1, 2])
+def test_gemm4w(M, N, K, epi, bm):
+    """The persistent 4-wave 256x256 / 192x256 kernel (gemm4w.hip): ragged M (partial last row
+    tile), single k-tile, several tiles per workgroup (persistence + next-tile prefetch), every
+    epilogue, against the fp32 oracle."""
+    from codename_symbiont_amd.ops._ext import hip
+    from codename_symbiont_amd.ops.kernels import gemm
+
+    a = _bf(M, K, seed=1)
+    w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=2)
+    bias = _f(N, scale=0.5, seed=3)
+    res = _bf(M, N, seed=4) if epi == 2 else None
+    hip().gemm4w_config(3, bm)
+    try:
+        out = gemm(a, w, bias, epi, res)
+        out2 = gemm(a, w, bias, epi, res)
+    finally:
+        hip().gemm4w_config(0, 0)
+    ref = R.gemm_ref(a, w, bias, epi, res, None, None, 1e-12)
+    _close(out, ref, atol=4e-2, rtol=2e-2, what=f"gemm4w epi={epi} bm={bm}")
+    assert torch.equal(out, out2), "gemm4w is not deterministic"
+
+
 @pytest.mark.parametrize("M,N,K,epi", [(300, 1152, 384, 0), (4100, 768, 3072, 2), (999, 2304, 768, 0),
                                       (77, 1024, 4096, 2)])
 def test_gemm_hipblaslt_route(M, N, K, epi):
