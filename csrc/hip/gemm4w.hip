@@ -29,12 +29,23 @@
 //    stores drain under the next tile's first k-tile (counted vmcnt).
 #include "common.h"
 
+#ifndef SYMB_G4_NULL_DMA
+#define SYMB_G4_NULL_DMA 0   // 1: a dropped DMA batch on even half-steps (uniform vmcnt; slower)
+#endif
+
 namespace symb {
 
 enum { G4_BIAS = 0, G4_GELU = 1, G4_RES = 2 };
 
 namespace g4 {
 constexpr int BN = 256, NT = 256;
+// lane id from v_mbcnt; volatile so that each use recomputes it instead of keeping one copy
+// (and everything derived from it) live across the k-loop
+__device__ __forceinline__ int lane_id() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
 __device__ __forceinline__ void tile_origin(int id, int n_all, int n_tiles, int group_m, int bm,
                                             int& m0, int& n0) {
   const int tile = xcd_remap(id, n_all);
@@ -64,6 +75,8 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(
   constexpr int A_LD = BM * 8 / NT, B_LD = BN * 8 / NT;   // 16-byte DMA pieces per thread
   constexpr int LD = A_LD + B_LD;
   constexpr int SCRATCH = 2 * STAGE;      // 4 KiB: the dropped pieces' LDS destination
+  constexpr int ZERO = SCRATCH + 4096;    // 16 KiB of zeros (see the k-loop)
+  constexpr int ZERO_BYTES = 16384;
   constexpr int ST = RM * 4;              // 16-byte output stores per lane per tile
   static_assert(BM % 32 == 0 && RM >= 1, "tile rows");
   static_assert(LD + ST <= 63, "vmcnt range");
@@ -91,8 +104,10 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(
   int arow = 0;          // this thread's first A row of the current tile
   uint32_t vb = 0;
   auto set_tile = [&](int m0, int n0) {
-    arow = m0 + (tid >> 3);
-    vb = (uint32_t)((n0 + gcol) * ldw * 2 + chunk16);
+    const int t2 = wave * 64 + lane_id();
+    const int ch = ((t2 & 7) ^ ((t2 >> 4) & 7)) * 16, cr = (t2 >> 3) & 15;
+    arow = m0 + (t2 >> 3);
+    vb = (uint32_t)((n0 + 8 * (cr >> 2) + 4 * (t2 >> 7) + (cr & 3)) * ldw * 2 + ch);
   };
   auto stage = [&](int kt, int buf) {
     char* sA = smem + buf * STAGE;
@@ -150,15 +165,24 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(
   // loop-carried values keep their registers (a second, ping-ponged set made hipcc rotate the
   // 256 accumulators through copies).
   bf16x8 a[RM], b[RN];
-  auto rd_b = [&](int buf, int kk, int j0) {
-    const char* base = smem + buf * STAGE + ob[kk];
+  // fragment base offsets; zero = the last half-step's "next" reads, which come from an
+  // all-zero LDS region (uniform address) so that the trailing MFMA pass adds exact zeros
+  auto off_b = [&](int buf, int kk, bool zero) { return zero ? (uint32_t)ZERO : buf * STAGE + ob[kk]; };
+  auto off_a = [&](int buf, int kk, bool zero) { return zero ? (uint32_t)ZERO : buf * STAGE + oa[kk]; };
+  auto rd_b = [&](uint32_t off, int j0) {
 #pragma unroll
-    for (int j = j0; j < j0 + 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(base + j * 2048);
+    for (int j = j0; j < j0 + 4; ++j)
+      b[j] = *reinterpret_cast<const bf16x8*>(smem + off + j * 2048);
   };
-  auto rd_a = [&](int buf, int kk, int i) {
-    a[i] = *reinterpret_cast<const bf16x8*>(smem + buf * STAGE + oa[kk] + i * 2048);
+  auto rd_a = [&](uint32_t off, int i) {
+    a[i] = *reinterpret_cast<const bf16x8*>(smem + off + i * 2048);
   };
   f32x4 acc[RM][RN];
+
+  // zero the region the last half-step's reads come from (never a DMA destination)
+#pragma unroll
+  for (int c = 0; c < ZERO_BYTES / (NT * 16); ++c)
+    *reinterpret_cast<f32x4*>(smem + ZERO + (c * NT + tid) * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
 
   int id = blockIdx.x;
   int m0, n0;
@@ -185,9 +209,9 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(
 #pragma unroll
       for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < RM; ++i) rd_a(0, 0, i);
-    rd_b(0, 0, 0);
-    rd_b(0, 0, 4);
+    for (int i = 0; i < RM; ++i) rd_a(off_a(0, 0, false), i);
+    rd_b(off_b(0, 0, false), 0);
+    rd_b(off_b(0, 0, false), 4);
 
     // The loop body is rotated so that its one barrier comes first: iteration h = barrier h,
     // DMA batch, reads of half-step h + 1 (interleaved with pass 2 of h), pass 1 of h + 1.  A
@@ -200,32 +224,47 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
     };
-    auto pass2 = [&](bool reads, int nbuf, int nkk) {
+    auto pass2 = [&](uint32_t aoff) {
 #pragma unroll
       for (int i = 0; i < RM; ++i) {
 #pragma unroll
         for (int j = 4; j < 8; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
-        if (reads) rd_a(nbuf, nkk, i);
+        rd_a(aoff, i);
       }
     };
     pass1();
+    // 2 KT identical iterations (no peeled tail: hipcc started moving the accumulators out of
+    // the AGPRs before a peeled last pass and spilled); the last one's pass 1 runs on the zero
+    // fragments
 #pragma unroll 1
-    for (int h = 0; h + 1 < 2 * KT; ++h) {
+    for (int h = 0; h < 2 * KT; ++h) {
       const int t = h >> 1;
       // the next half-step: (t, 1) in the same buffer, or (t + 1, 0) in the other one
       const int nbuf = (t + (h & 1)) & 1, nkk = (h & 1) ^ 1;
+      const bool last = h + 1 == 2 * KT;
       // every batch but the latest landed (on an odd half-step that is k-tile t + 1), and every
       // wave's reads issued before this barrier retired: on odd half-steps buffer t (whose
       // fragments are all in registers by now) takes k-tile t + 2
+#if SYMB_G4_NULL_DMA
       asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(LD) : "memory");
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       stage_sel((h & 1) && t + 2 < KT, t + 2, t & 1);
       __builtin_amdgcn_sched_barrier(0);
-      rd_b(nbuf, nkk, 0);
-      pass2(true, nbuf, nkk);     // columns 4-7 of h; row i's A fragment refilled after (i, 7)
-      rd_b(nbuf, nkk, 4);
+#else
+      if (h & 1)
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      else
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if ((h & 1) && t + 2 < KT) stage(t + 2, t & 1);
+      __builtin_amdgcn_sched_barrier(0);
+#endif
+      rd_b(off_b(nbuf, nkk, last), 0);
+      pass2(off_a(nbuf, nkk, last));   // columns 4-7 of h; row i's A fragment refilled after (i, 7)
+      rd_b(off_b(nbuf, nkk, last), 4);
       pass1();                    // columns 0-3 of h + 1 (b[4..7] are first needed in pass 2)
       __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
 #pragma unroll
@@ -236,13 +275,6 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(
       __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, 4 * RM, 0);
     }
-    pass2(false, 0, 0);
-    // pin the accumulators in AGPRs up to here (else hipcc starts moving them to VGPRs for the
-    // epilogue before the last MFMAs and spills the overflow)
-#pragma unroll
-    for (int i = 0; i < RM; ++i)
-#pragma unroll
-      for (int j = 0; j < RN; ++j) asm volatile("" ::"a"(acc[i][j]));
     pend = false;
 
     // ---- epilogue (registers only): bias / GELU / residual, 16-byte stores ----
@@ -253,23 +285,35 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     // lane columns: group p covers cn0 + wn * 128 + 32 p + 8 fq + (0..7)
-    const int col0 = cn0 + wn * 128 + 8 * fq;
+    // lane-derived addresses recomputed here from a fresh lane id (a volatile asm is never
+    // CSE'd with the loop's copies): kept live across the k-loop they were spilled, and the
+    // reloads' waits drained the next tile's DMA
+    const int elane = lane_id();
+    const int col0 = cn0 + wn * 128 + 8 * (elane >> 4);
     f32x4 bv[4][2];
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       bv[p][0] = *reinterpret_cast<const f32x4*>(bias + col0 + 32 * p);
       bv[p][1] = *reinterpret_cast<const f32x4*>(bias + col0 + 32 * p + 4);
     }
-    const int row0 = cm0 + wm * WTM + fr;   // + 16 i
+    const int row0 = cm0 + wm * WTM + (elane & 15);   // + 16 i
+    // residual rows: the first half of the row blocks is loaded before the next tile's DMA, the
+    // second half after the first half's stores (all of them up front spilled)
+    constexpr int RH = (RM + 1) / 2;
     bf16x8 res[RM][4];
-    if constexpr (EPI == G4_RES) {
+    auto load_res = [&](int i0, int i1) {
 #pragma unroll
-      for (int i = 0; i < RM; ++i)
+      for (int i = i0; i < i1; ++i)
 #pragma unroll
         for (int p = 0; p < 4; ++p)
           res[i][p] = *reinterpret_cast<const bf16x8*>(
               R + (size_t)min(row0 + 16 * i, M - 1) * ldr + col0 + 32 * p);
-    }
+    };
+    if constexpr (EPI == G4_RES) load_res(0, RH);
+    // bias (and residual) loads land BEFORE the next tile's DMA is issued: a load waited for
+    // after it would wait for the DMA too (vmcnt retires in issue order).  A real S_WAITCNT
+    // (vmcnt(0)), so hipcc's own bookkeeping knows those registers are ready.
+    __builtin_amdgcn_s_waitcnt(0x0F70);
     // the next tile's first two k-tiles stream in under this epilogue
     if (id + (int)gridDim.x < n_all) {
       tile_origin(id + gridDim.x, n_all, n_tiles, group_m, BM, m0, n0);
@@ -279,6 +323,9 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(
     }
 #pragma unroll
     for (int i = 0; i < RM; ++i) {
+      if constexpr (EPI == G4_RES) {
+        if (i == RH) load_res(RH, RM);
+      }
       const int row = row0 + 16 * i;
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
@@ -358,7 +405,7 @@ int symb_gemm4w(int epi, int bm, const void* A, int lda, const void* W, int ldw,
                        K, group_m, gelu_poly ? 1.f : 0.f);
     return (int)hipGetLastError();
   };
-  constexpr int L256 = 2 * (256 + 256) * 128 + 4096, L192 = 2 * (192 + 256) * 128 + 4096;
+  constexpr int L256 = 2 * (256 + 256) * 128 + 20480, L192 = 2 * (192 + 256) * 128 + 20480;
   if (bm == 256) {
     switch (epi) {
       case G4_BIAS: return go(gemm4w_kernel<256, G4_BIAS>, L256);
