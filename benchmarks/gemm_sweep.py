@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--m", type=int, default=32768)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only", default="", help="comma list of GEMM names to keep (e.g. ffn1)")
     a = ap.parse_args()
     from codename_symbiont_amd.ops import kernels as K
     from codename_symbiont_amd.ops._ext import hip
@@ -43,6 +44,8 @@ def main():
     g = torch.Generator(device="cuda").manual_seed(0)
     for model in a.models.split(","):
         for name, n, k, epi in SHAPES[model]:
+            if a.only and name not in a.only.split(","):
+                continue
             x = torch.randn(a.m, k, device="cuda", generator=g).bfloat16()
             w = (torch.randn(n, k, device="cuda", generator=g) / math.sqrt(k)).bfloat16()
             b = torch.randn(n, device="cuda", generator=g)
