@@ -45,6 +45,14 @@ class VectorStore:
         self._since_snapshot = 0
         self._lock = threading.Lock()
         self._frag: dict[int, tuple[bytes, bytes]] = {}
+        # SYMB_SEARCH_PIPELINE (default on, single GPU shard): a search's query-side pre-pass
+        # (HbmIndexShard.search_begin) runs on one stream and its full-shard scan (search_end) on
+        # another, so with the service's two scans in flight the next burst's pre-pass runs
+        # under the current burst's scan (the bench's pipelined step, profiles/r3_pipeline/)
+        self._streams = None
+        if (group is None and self.shard.device.type == "cuda"
+                and os.environ.get("SYMB_SEARCH_PIPELINE", "1") not in ("", "0")):
+            self._streams = (torch.cuda.Stream(self.shard.device), torch.cuda.Stream(self.shard.device))
         self.wal = None
         self._bg: threading.Thread | None = None   # background snapshot writer
         self.snapshot_error: BaseException | None = None
@@ -78,6 +86,9 @@ class VectorStore:
 
     def _upsert_nolog(self, point_ids, vecs, payloads):
         t = torch.as_tensor(np.ascontiguousarray(vecs, dtype=np.float32))
+        if self._streams is not None:
+            # in-place overwrites must not land under a pipelined search's scan of those rows
+            torch.cuda.current_stream(self.shard.device).wait_stream(self._streams[1])
         if self.group is not None:
             out = self.group.upsert(point_ids, t, payloads)
         else:
@@ -174,6 +185,8 @@ class VectorStore:
         k = int(k)
         if k <= 0 or self.count == 0:
             return np.zeros((q.shape[0], 0), np.float32), np.zeros((q.shape[0], 0), np.int64)
+        if self._streams is not None:
+            return self._search_pipelined(q, k)
         qt = torch.nn.functional.normalize(torch.from_numpy(q).to(self.shard.device), dim=-1)
         qt = qt.to(torch.bfloat16)
         if self.group is not None:
@@ -186,6 +199,25 @@ class VectorStore:
         else:
             s, r = self.shard.search(qt, k)
         return s.float().cpu().numpy(), r.long().cpu().numpy()
+
+    def _search_pipelined(self, q: np.ndarray, k: int):
+        """search() of a single GPU shard on two streams: pre-pass (begin) on the first, scan
+        (end) on the second.  Both order after every write already enqueued on the default
+        stream (upserts), and each stream runs its calls in the order they were made, so two
+        concurrent callers overlap one's pre-pass with the other's scan."""
+        pre, scan = self._streams
+        dev = self.shard.device
+        pre.wait_stream(torch.cuda.default_stream(dev))
+        with torch.cuda.stream(pre):
+            qt = torch.nn.functional.normalize(torch.from_numpy(q).to(dev, non_blocking=False),
+                                               dim=-1).to(torch.bfloat16)
+            ctx = self.shard.search_begin(qt, k)
+            done = torch.cuda.Event()
+            done.record(pre)
+        scan.wait_event(done)
+        with torch.cuda.stream(scan):
+            s, r = self.shard.search_end(ctx)
+            return s.float().cpu().numpy(), r.long().cpu().numpy()
 
     def lookup(self, gid: int):
         if self.group is not None:

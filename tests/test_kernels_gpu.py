@@ -280,6 +280,54 @@ def test_index_scan_small_and_partial():
     assert sorted(r[0, :3].tolist()) == [0, 1, 2]
 
 
+def test_store_pipelined_search_concurrent_and_ordered_after_upserts():
+    """VectorStore on one GPU shard runs each search as pre-pass (stream 1) + scan (stream 2).
+    Four threads searching at once (the pruned path: >= 1M rows, 384-wide bf16) get exactly
+    the single-stream results, and a search issued after an upsert that OVERWRITES rows sees
+    the new vectors (the overwrite also waits for scans already in flight)."""
+    import threading
+
+    import numpy as np
+
+    from codename_symbiont_amd.index.shard import Payload
+    from codename_symbiont_amd.index.store import VectorStore
+
+    D, n, nq, k = 384, (1 << 20) + 4321, 48, 10
+    st = VectorStore(D, n + 1000, device="cuda")
+    assert st._streams is not None
+    st.shard.fill_random(n, seed=5)
+    ids = [f"p{i}" for i in range(64)]
+    g = torch.Generator().manual_seed(9)
+    vec = torch.randn(64, D, generator=g).numpy()
+    st.upsert(ids, vec, [Payload("d", "u", f"s{i}", i, "m", 0) for i in range(64)])
+    qs = [torch.nn.functional.normalize(torch.randn(nq, D, generator=g), dim=-1).numpy()
+          for _ in range(4)]
+    qs[0][:8] = vec[:8] / np.linalg.norm(vec[:8], axis=1, keepdims=True)   # self matches
+    streams, st._streams = st._streams, None
+    seq = [st.search(q, k) for q in qs]                  # the plain single-stream path
+    st._streams = streams
+    assert (seq[0][1][:8, 0] == np.arange(n, n + 8)).all()
+    got = [None] * 4
+    start = threading.Barrier(4)
+
+    def run(t):
+        start.wait()
+        got[t] = [st.search(qs[t], k) for _ in range(6)]
+
+    th = [threading.Thread(target=run, args=(t,)) for t in range(4)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(180)
+    for t in range(4):
+        for s_, r_ in got[t]:
+            assert (r_ == seq[t][1]).all() and np.allclose(s_, seq[t][0], atol=1e-6), t
+    # overwrite the 8 self-matched points with the negated vectors: now nothing matches them
+    st.upsert(ids[:8], -vec[:8], [Payload("d", "u", f"s{i}", i, "m", 0) for i in range(8)])
+    s2, r2 = st.search(qs[0][:8], k)
+    assert not np.isin(np.arange(n, n + 8), r2).any()
+
+
 @pytest.mark.parametrize("dtype", ["bf16", "fp8"])
 def test_concurrent_searches_match_sequential(dtype):
     """The service runs searches from several executor threads on one shard and one stream:
