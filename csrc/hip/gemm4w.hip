@@ -29,10 +29,6 @@
 //    stores drain under the next tile's first k-tile (counted vmcnt).
 #include "common.h"
 
-#ifndef SYMB_G4_NULL_DMA
-#define SYMB_G4_NULL_DMA 0   // 1: a dropped DMA batch on even half-steps (uniform vmcnt; slower)
-#endif
-
 namespace symb {
 
 enum { G4_BIAS = 0, G4_GELU = 1, G4_RES = 2 };
@@ -74,8 +70,7 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(
   constexpr int STAGE = (BM + BN) * 128;
   constexpr int A_LD = BM * 8 / NT, B_LD = BN * 8 / NT;   // 16-byte DMA pieces per thread
   constexpr int LD = A_LD + B_LD;
-  constexpr int SCRATCH = 2 * STAGE;      // 4 KiB: the dropped pieces' LDS destination
-  constexpr int ZERO = SCRATCH + 4096;    // 16 KiB of zeros (see the k-loop)
+  constexpr int ZERO = 2 * STAGE;         // 16 KiB of zeros (see the k-loop)
   constexpr int ZERO_BYTES = 16384;
   constexpr int ST = RM * 4;              // 16-byte output stores per lane per tile
   static_assert(BM % 32 == 0 && RM >= 1, "tile rows");
@@ -123,32 +118,6 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(
           rsW, (__attribute__((address_space(3))) void*)(sB + (i * NT + wave * 64) * 16), 16, vb,
           i * 32 * ldw * 2 + kt * 128, 0, 0);
   };
-  // The k-loop issues a batch of LD pieces at EVERY half-step so that one counted wait,
-  // vmcnt(LD), means "the batch before the previous one has landed" at every barrier: a real
-  // k-tile on odd half-steps, on even ones (and past the last k-tile) a batch through a
-  // zero-size descriptor -- the range check drops every piece, no memory is touched -- aimed at
-  // a scratch KiB per wave beyond the stages.  Selecting descriptor and destination with scalar
-  // selects keeps the loop body one basic block (a branch there made hipcc split the live
-  // ranges of the 256 accumulators and copy them around).
-  const auto rsNull = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, 0, 0x00020000);
-  auto stage_sel = [&](bool real, int kt, int buf) {
-    const auto ra = real ? rsA : rsNull;
-    const auto rw = real ? rsW : rsNull;
-    char* sA = real ? smem + buf * STAGE : smem + SCRATCH;
-    char* sB = real ? sA + A_BYTES : smem + SCRATCH;
-    const int pstep = real ? NT * 16 : 0;   // LDS bytes between pieces
-#pragma unroll
-    for (int i = 0; i < A_LD; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          ra, (__attribute__((address_space(3))) void*)(sA + i * pstep + wave * 1024), 16,
-          (uint32_t)(min(arow + 32 * i, M - 1) * lda * 2 + chunk16), kt * 128, 0, 0);
-#pragma unroll
-    for (int i = 0; i < B_LD; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rw, (__attribute__((address_space(3))) void*)(sB + i * pstep + wave * 1024), 16, vb,
-          i * 32 * ldw * 2 + kt * 128, 0, 0);
-  };
-
   // ---- fragments: lane row fr, 8 k at chunk kk * 4 + fq; the XOR term is (fr >> 1) & 7 ----
   const int x = (fr >> 1) & 7;
   uint32_t oa[2], ob[2];
@@ -243,16 +212,9 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(
       // the next half-step: (t, 1) in the same buffer, or (t + 1, 0) in the other one
       const int nbuf = (t + (h & 1)) & 1, nkk = (h & 1) ^ 1;
       const bool last = h + 1 == 2 * KT;
-      // every batch but the latest landed (on an odd half-step that is k-tile t + 1), and every
-      // wave's reads issued before this barrier retired: on odd half-steps buffer t (whose
-      // fragments are all in registers by now) takes k-tile t + 2
-#if SYMB_G4_NULL_DMA
-      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(LD) : "memory");
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      stage_sel((h & 1) && t + 2 < KT, t + 2, t & 1);
-      __builtin_amdgcn_sched_barrier(0);
-#else
+      // odd half-steps: k-tile t + 1 landed everywhere, and every wave's reads issued before
+      // this barrier retired, so buffer t (whose fragments are all in registers by now) takes
+      // k-tile t + 2; even half-steps only order the LDS reads
       if (h & 1)
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       else
@@ -261,7 +223,6 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(
       __builtin_amdgcn_sched_barrier(0);
       if ((h & 1) && t + 2 < KT) stage(t + 2, t & 1);
       __builtin_amdgcn_sched_barrier(0);
-#endif
       rd_b(off_b(nbuf, nkk, last), 0);
       pass2(off_a(nbuf, nkk, last));   // columns 4-7 of h; row i's A fragment refilled after (i, 7)
       rd_b(off_b(nbuf, nkk, last), 4);
@@ -405,7 +366,7 @@ int symb_gemm4w(int epi, int bm, const void* A, int lda, const void* W, int ldw,
                        K, group_m, gelu_poly ? 1.f : 0.f);
     return (int)hipGetLastError();
   };
-  constexpr int L256 = 2 * (256 + 256) * 128 + 20480, L192 = 2 * (192 + 256) * 128 + 20480;
+  constexpr int L256 = 2 * (256 + 256) * 128 + 16384, L192 = 2 * (192 + 256) * 128 + 16384;
   if (bm == 256) {
     switch (epi) {
       case G4_BIAS: return go(gemm4w_kernel<256, G4_BIAS>, L256);
