@@ -117,7 +117,7 @@ class VectorMemoryService(Service):
             self.log.warning("[SEARCH_HANDLER] No reply subject provided for search task_id %s. "
                              "Results not sent.", res.request_id)
 
-    SEARCH_MAX_BATCH = 256      # queries per fused scan launch
+    SEARCH_MAX_BATCH = 512      # queries per fused scan launch (cfg.search_max_batch)
     SEARCH_MAX_INFLIGHT = 2     # scans in flight: batch i+1 decodes/scans while i's replies encode
 
     async def handle_search_batch(self, msgs) -> None:

@@ -74,8 +74,10 @@ class Config:
     index_prune: str = field(default_factory=lambda: os.environ.get("SYMB_INDEX_PRUNE", "auto"))
     snapshot_dir: str = field(default_factory=lambda: _env("SYMB_SNAPSHOT_DIR", ""))
     # queries per fused scan launch of the search service (a 100M-row scan costs about the same
-    # for 16 or 256 queries, so bigger bursts buy throughput at the price of latency)
-    search_max_batch: int = field(default_factory=lambda: _int("SYMB_SEARCH_MAX_BATCH", 256))
+    # for 16 or 256 queries, so bigger bursts buy throughput at the price of latency); 512 = two
+    # of the int8 scan's 256-query blocks, taken whole under load (search_align below;
+    # profiles/r3_e2e/: 16.1k req/s at 2048 in flight)
+    search_max_batch: int = field(default_factory=lambda: _int("SYMB_SEARCH_MAX_BATCH", 512))
     # bursts larger than this take a whole multiple of it (the int8 scan's 256-query block: a
     # 369-query burst would cost two full scans of the shard; 0 = take whatever is queued)
     search_align: int = field(default_factory=lambda: _int("SYMB_SEARCH_ALIGN", 256))
