@@ -14,6 +14,7 @@ live host-side in a sparse ``PayloadStore`` keyed by row (rows without a point c
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -662,6 +663,9 @@ class HbmIndexShard:
     # int8 scan but spreads over the whole chip; 1024 int8 candidates from one block per query
     # cost about as much to emit and re-score.
     PRUNE_DENSE_FRAC = 0.6
+    # batches up to this many queries score the exact tail densely (see _pruned_begin);
+    # SYMB_TAIL_DENSE_MAX_NQ=0 keeps the emitting tail scan (A/B)
+    tail_dense_max_nq = int(os.environ.get("SYMB_TAIL_DENSE_MAX_NQ", "512"))
     PRUNE_BLOCK_FRAC = 1 / 32
     prune_route = True   # False: always take the int8 pass (tests of the overflow fallback)
 
@@ -722,9 +726,23 @@ class HbmIndexShard:
         # too (one slot per tail row: no overflow), so the route counts its band rows one by one
         # -- a crowd of fresh near-duplicates sits there first
         tcap = n - t0
-        tail_s, _, tcs, tci, tcnt = self._scan_mq(tcap, q_unit, kmax, k, thr0, n_cus,
-                                                  rows=self.rows[t0:], fallback=False, cand=True,
-                                                  cap=tcap, min_tiles=pm)
+        if NQ <= self.tail_dense_max_nq:
+            # dense exact scores of the tail (one small fp32 GEMM: 4-8k rows) and their top-k;
+            # the route counts every tail row >= the band.  The emitting scan it replaces
+            # reserved one slot per emitted row with a global atomic on the query's counter:
+            # with a fresh near-duplicate crowd in the tail every (query, row) pair emitted and
+            # the counters serialized (0.6 ms per headline step, profiles/r3_step_trace/)
+            tcs = torch.mm(q_unit.float(), self.rows[t0:n].float().t())
+            tail_s = torch.empty(NQ, k, device=dev)
+            tail_i = torch.empty(NQ, k, dtype=torch.int32, device=dev)
+            tovf = torch.empty(1, dtype=torch.int32, device=dev)
+            h.topk_select_counted(tcs.data_ptr(), 0, 0, tcap, NQ, kmax, k, tail_s.data_ptr(),
+                                  tail_i.data_ptr(), tovf.data_ptr(), st)   # (dense rows)
+            tci = tcnt = None
+        else:
+            tail_s, _, tcs, tci, tcnt = self._scan_mq(tcap, q_unit, kmax, k, thr0, n_cus,
+                                                      rows=self.rows[t0:], fallback=False,
+                                                      cand=True, cap=tcap, min_tiles=pm)
         # 2. T (k-th best of the union), the per-query emission threshold (T - margin) / sq and
         #    the per-row-block route (prune_route): the blocks some query would flood with int8
         #    candidates go to the bf16 emitting scan at T, the rest to the int8 scan
@@ -744,8 +762,9 @@ class HbmIndexShard:
                       ci_p.data_ptr(), cnt_p.data_ptr(), self.SAMPLE_CAP, ts, geo[1], n_rblk,
                       blk_limit, limit, self._mq_slots(NQ, n_cus)[3], T.data_ptr(),
                       thr.data_ptr(), dense.data_ptr(), est.data_ptr(), blkmax.data_ptr(),
-                      blk.data_ptr(), st, tail_cs=tcs.data_ptr(), tail_ci=tci.data_ptr(),
-                      tail_cnt=tcnt.data_ptr(), tail_cap=tcap, tail_off=t0)
+                      blk.data_ptr(), st, tail_cs=tcs.data_ptr(),
+                      tail_ci=0 if tci is None else tci.data_ptr(),
+                      tail_cnt=0 if tcnt is None else tcnt.data_ptr(), tail_cap=tcap, tail_off=t0)
         return dict(q=q_unit, k=k, n=n, n_cus=n_cus, q8=q8, sq=sq, thr=thr, T=T, dense=dense,
                     blk=blk, geo=geo)
 

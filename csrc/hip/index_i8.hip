@@ -758,7 +758,22 @@ __global__ __launch_bounds__(256) void prune_route_kernel(
       atomicAdd(&h[min(ci[i] / rows_per_blk, n_rblk - 1)], 1);
     }
   }
-  if (tail.cs != nullptr) {   // the exact tail: every row >= thr0 of it, counted one by one
+  const bool tail_dense = tail.cs != nullptr && tail.ci == nullptr;
+  if (tail_dense) {   // the exact tail as dense scores [NQ][cap] (row i = tail.off + i)
+    const float* tcs = tail.cs + (size_t)q * tail.cap;
+    for (int i0 = 0; i0 < tail.cap; i0 += 64) {
+      const int i = i0 + lane;
+      const bool hit = i < tail.cap && tcs[i] >= band;
+      const int b = min((min(i, tail.cap - 1) + tail.off) / rows_per_blk, n_rblk - 1);
+      const int b0 = __shfl(b, 0), b63 = __shfl(b, 63);
+      if (b0 == b63) {   // (64 consecutive rows: almost always one block) one add per chunk
+        const int nh = __popcll(__ballot(hit));
+        if (lane == 0 && nh) atomicAdd(&th[b0], nh);
+      } else if (hit) {
+        atomicAdd(&th[b], 1);
+      }
+    }
+  } else if (tail.cs != nullptr) {   // the exact tail: every row >= thr0 of it, one by one
     const int tn = min(tail.cnt[q], tail.cap);
     const float* tcs = tail.cs + (size_t)q * tail.cap;
     const int* tci = tail.ci + (size_t)q * tail.cap;
@@ -770,7 +785,8 @@ __global__ __launch_bounds__(256) void prune_route_kernel(
   float tscale = 1.f;
   if (band < t0) {   // the band reaches below what the sample emitted: extrapolate (see above)
     c = fmaxf((float)cnt, fmaxf(0.f, (float)(cnt - k)) * m / fmaxf(T - t0, 1e-6f));
-    tscale = binned > 0.f ? fmaxf(1.f, c / binned) : 1.f;   // (the tail emitted >= thr0 too)
+    // (an emitting tail scan kept only rows >= thr0 too; a dense tail counted every row)
+    tscale = tail_dense ? 1.f : binned > 0.f ? fmaxf(1.f, c / binned) : 1.f;
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   const float scale = (binned > 0.f ? c / binned : 0.f) * (float)(1 << tshift);
@@ -1001,7 +1017,8 @@ int symb_prune_route(int NQ, const float* pre_s, const float* tail_s, int k, flo
   if (NQ <= 0) return 0;
   if (k < 1 || k > 32 || cap_p <= 0 || tshift < 0 || tshift > 20) return -1;
   if (n_rblk < 1 || n_rblk > ROUTE_MAX_BLOCKS || rows_per_blk < 1 || max_list < 1) return -1;
-  if (tail_cs != nullptr && (tail_ci == nullptr || tail_cnt == nullptr || tail_cap < 1 || tail_off < 0))
+  // tail_ci == nullptr: tail_cs holds DENSE scores [NQ][tail_cap] of rows tail_off + i
+  if (tail_cs != nullptr && ((tail_ci != nullptr) != (tail_cnt != nullptr) || tail_cap < 1 || tail_off < 0))
     return -1;
   hipError_t e = hipMemsetAsync(dense, 0, sizeof(int), st);
   if (e == hipSuccess) e = hipMemsetAsync(blkmax, 0, sizeof(int) * (size_t)n_rblk, st);

@@ -422,11 +422,13 @@ __global__ __launch_bounds__(NTH) void topk_select_counted_kernel(
   __shared__ float ls[NTH * KMAX];
   __shared__ int li[NTH * KMAX];
   const int q = blockIdx.x, tid = threadIdx.x;
-  const int cnt = cand_n[q];
+  // cand_n == nullptr: every row holds cap candidates; cand_i == nullptr: a candidate's id is
+  // its position (dense score rows, e.g. the pruned search's exact tail)
+  const int cnt = cand_n != nullptr ? cand_n[q] : cap;
   const int n = min(cnt, cap);
   if (tid == 0 && cnt > cap) *ovf = 1;
   const float* cs = cand_s + (size_t)q * cap;
-  const int* ci = cand_i + (size_t)q * cap;
+  const int* ci = cand_i != nullptr ? cand_i + (size_t)q * cap : nullptr;
   float tv[KMAX];
   int ti[KMAX];
 #pragma unroll
@@ -436,7 +438,7 @@ __global__ __launch_bounds__(NTH) void topk_select_counted_kernel(
   }
   for (int c = tid; c < n; c += NTH) {
     const float s = cs[c];
-    if (s > tv[KMAX - 1]) topk_insert<KMAX>(tv, ti, s, ci[c]);
+    if (s > tv[KMAX - 1]) topk_insert<KMAX>(tv, ti, s, ci != nullptr ? ci[c] : c);
   }
 #pragma unroll
   for (int i = 0; i < KMAX; ++i) {
@@ -736,6 +738,7 @@ int symb_topk_select_counted(const float* cand_s, const int* cand_i, const int* 
                              hipStream_t st, const int* gate, int reset_ovf) {
   if (NQ <= 0) return 0;
   if (k > kmax) return -1;
+  if (kmax == sel::SEL_MAX && (cand_i == nullptr || cand_n == nullptr)) return -1;   // (dense rows: KMAX 16 / 32 forms)
   if (reset_ovf) {
     hipError_t e = hipMemsetAsync(ovf, 0, sizeof(int), st);
     if (e != hipSuccess) return (int)e;
