@@ -183,6 +183,10 @@ def parse_args(argv=None):
     ap.add_argument("--prepass-min-tiles", type=int, default=0,
                     help="row-block floor of the sampled searches' small pre-pass list scans "
                          "(0 = the shard default, 1 tile per workgroup)")
+    ap.add_argument("--encode-ahead", type=int, choices=[1, 2], default=2,
+                    help="pipelined step: batch i + AHEAD is encoded during step i (2: the "
+                         "encoder runs beside batch i + 1's pre-pass, before batch i + 1's scan; "
+                         "1: it queues behind batch i's scan)")
     ap.add_argument("--no-search-pipeline", action="store_true",
                     help="--mode full: run each batch's query-side search work (int8 queries, "
                          "exact sample, thresholds) right before its scan instead of on a third "
@@ -460,14 +464,18 @@ def run_gpu(args, info, comm) -> int:
     # still encodes one batch and searches one batch.
     overlap = args.mode == "full" and not group_dp and not args.no_overlap
     enc_stream = torch.cuda.Stream(dev)
+    # output slots: batch i's embeddings live in outs[i % NO] from its encode to its search's end
+    pipeline = overlap and args.queries == "self" and not args.no_search_pipeline
+    AHEAD = args.encode_ahead if pipeline else 1
+    NO = AHEAD + 1
     outs = [(torch.empty(B, cfg.hidden, device=dev),
-             torch.empty(B, cfg.hidden, dtype=torch.bfloat16, device=dev)) for _ in range(2)]
-    enc_done = [torch.cuda.Event(), torch.cuda.Event()]
-    q_free = [torch.cuda.Event(), torch.cuda.Event()]
+             torch.empty(B, cfg.hidden, dtype=torch.bfloat16, device=dev)) for _ in range(NO)]
+    enc_done = [torch.cuda.Event() for _ in range(NO)]
+    q_free = [torch.cuda.Event() for _ in range(NO)]
     # SYMB_GPU_DEBUG=1: assert the host enqueue order the events above rely on
     from codename_symbiont_amd.utils.gpu_debug import BufferRing
 
-    in_ring, out_ring = BufferRing(2, "bench.dbuf"), BufferRing(2, "bench.outs")
+    in_ring, out_ring = BufferRing(2, "bench.dbuf"), BufferRing(NO, "bench.outs")
     # search mode: held-out queries are fresh draws from the corpus distribution (never
     # inserted); self queries are stored rows (each query's best match is itself)
     if args.queries == "heldout":
@@ -532,34 +540,33 @@ def run_gpu(args, info, comm) -> int:
             capture_encoder(slot, *(outs[slot] if overlap else (out_f32, out_unit)))
 
     def encode_async(i: int, ev=None) -> None:
-        """Encode batch i on enc_stream into outs[i % 2] (overlap mode)."""
-        slot = i % 2
+        """Encode batch i (input slot i % 2) on enc_stream into outs[i % NO] (overlap mode)."""
+        slot, o = i % 2, i % NO
         with torch.cuda.stream(enc_stream):
             enc_stream.wait_event(copy_done[slot])
-            if i >= 2:
-                enc_stream.wait_event(q_free[slot])   # batch i-2's queries are searched
+            if i >= NO:
+                enc_stream.wait_event(q_free[o])   # batch i - NO's queries are searched
             if ev:
                 ev[0].record(enc_stream)
             in_ring.consume(slot)
-            out_ring.fill(slot)
-            run_encoder(slot, *outs[slot])
+            out_ring.fill(o)
+            run_encoder(slot, *outs[o])
             if ev:
                 ev[1].record(enc_stream)
             consumed[slot].record(enc_stream)
-            enc_done[slot].record(enc_stream)
+            enc_done[o].record(enc_stream)
         prefetch(i + 1)
 
     # --mode full, self queries: the search is pipelined too.  Batch i+1's query-side search
     # work (upsert, int8 queries, the exact threshold sample, route) runs on pre_stream as soon
     # as it is encoded, under batch i's full-shard scan; the compute stream only runs the scans
     # back to back (ShardedSearcher.begin / end, HbmIndexShard.search_begin / search_end).
-    pipeline = overlap and args.queries == "self" and not args.no_search_pipeline
     pre_stream = torch.cuda.Stream(dev)
-    pre_done = [torch.cuda.Event(), torch.cuda.Event()]
+    pre_done = [torch.cuda.Event() for _ in range(NO)]
     handles: dict = {}
 
     def begin_search(i: int) -> None:
-        slot = i % 2
+        slot = i % NO
         with torch.cuda.stream(pre_stream):
             pre_stream.wait_event(enc_done[slot])
             q = outs[slot][1]
@@ -568,8 +575,10 @@ def run_gpu(args, info, comm) -> int:
             pre_done[slot].record(pre_stream)
 
     def step_pipelined(i: int, ev=None) -> None:
-        slot = i % 2
-        encode_async(i + 1, ev)
+        slot = i % NO
+        # with AHEAD = 2, batch i + 2's encoder is enqueued now: it runs once batch i's scan
+        # releases the CUs, beside batch i + 1's pre-pass, instead of between them
+        encode_async(i + AHEAD, ev)
         begin_search(i + 1)
         compute.wait_event(pre_done[slot])
         if ev:
@@ -584,7 +593,7 @@ def run_gpu(args, info, comm) -> int:
         """Search batch i (encoded by the previous step) while batch i+1 encodes."""
         if pipeline:
             return step_pipelined(i, ev)
-        slot = i % 2
+        slot = i % NO
         encode_async(i + 1, ev)
         compute.wait_event(enc_done[slot])
         if ev:
@@ -637,7 +646,8 @@ def run_gpu(args, info, comm) -> int:
 
     prefetch(0)
     if overlap:
-        encode_async(0)
+        for j in range(AHEAD):
+            encode_async(j)
         if pipeline:
             begin_search(0)
     for i in range(W):
@@ -728,6 +738,7 @@ def run_gpu(args, info, comm) -> int:
         "_group_dp": group_dp,
         "encode_search_overlap": overlap,
         "search_pipeline": pipeline,
+        "encode_ahead": AHEAD,
         # per-rank scan kernel: the emitting MFMA scan (csrc/hip/index_mq.hip) for >= 256
         # seeded queries (512 per workgroup at >= 512), else the 256-query list kernel
         "index_scan": (("int8-pruned-" if prune else "emitting-")
