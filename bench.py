@@ -187,6 +187,10 @@ def parse_args(argv=None):
                     help="pipelined step: batch i + AHEAD is encoded during step i (2: the "
                          "encoder runs beside batch i + 1's pre-pass, before batch i + 1's scan; "
                          "1: it queues behind batch i's scan)")
+    ap.add_argument("--scan-waits-encoder", type=int, choices=[0, 1], default=0,
+                    help="encode-ahead 2: batch i's scan also waits for batch i + 1's encoder, so "
+                         "that encoder runs beside batch i's pre-pass instead of being starved by "
+                         "the scan (which holds every CU) and finishing after it")
     ap.add_argument("--no-search-pipeline", action="store_true",
                     help="--mode full: run each batch's query-side search work (int8 queries, "
                          "exact sample, thresholds) right before its scan instead of on a third "
@@ -581,6 +585,8 @@ def run_gpu(args, info, comm) -> int:
         encode_async(i + AHEAD, ev)
         begin_search(i + 1)
         compute.wait_event(pre_done[slot])
+        if AHEAD == 2 and args.scan_waits_encoder:
+            compute.wait_event(enc_done[(i + 1) % NO])
         if ev:
             ev[2].record(compute)
         searcher.end(handles.pop(i))
@@ -739,6 +745,7 @@ def run_gpu(args, info, comm) -> int:
         "encode_search_overlap": overlap,
         "search_pipeline": pipeline,
         "encode_ahead": AHEAD,
+        "scan_waits_encoder": bool(AHEAD == 2 and args.scan_waits_encoder),
         # per-rank scan kernel: the emitting MFMA scan (csrc/hip/index_mq.hip) for >= 256
         # seeded queries (512 per workgroup at >= 512), else the 256-query list kernel
         "index_scan": (("int8-pruned-" if prune else "emitting-")
