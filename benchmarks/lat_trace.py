@@ -1,0 +1,49 @@
+"""Small-batch encoder forwards in a loop, for a rocprofv3 kernel trace of the query path.
+
+    rocprofv3 --kernel-trace --stats -d gpurun_out/lat -- python benchmarks/lat_trace.py --b 1 --s 16
+
+Prints the host-timed eager latency (us per forward, synchronised) as one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="minilm-l6")
+    ap.add_argument("--b", type=int, default=1)
+    ap.add_argument("--s", type=int, default=16)
+    ap.add_argument("--iters", type=int, default=200)
+    a = ap.parse_args()
+    from codename_symbiont_amd.models import get_config
+    from codename_symbiont_amd.models.encoder import HipEncoder, synthetic_batch
+
+    cfg = get_config(a.model)
+    enc = HipEncoder(cfg, seed=0)
+    b = synthetic_batch(cfg, a.b, a.s, seed=1).to("cuda")
+    for _ in range(20):
+        enc.forward_packed(b)
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(a.iters):
+        t0 = time.perf_counter()
+        enc.forward_packed(b)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    print(json.dumps({"bench": "encoder_latency_us", "model": a.model, "B": a.b, "S": a.s,
+                      "p50_us": round(ts[len(ts) // 2] * 1e6, 1),
+                      "p10_us": round(ts[len(ts) // 10] * 1e6, 1)}))
+
+
+if __name__ == "__main__":
+    main()

@@ -521,11 +521,23 @@ int symb_gemm_lt_config(int mode) {
   return 0;
 }
 
+// Small-M split-K path (gemm_skinny.hip): M <= symb_gemm_skinny_max_m() (default 64, the
+// query-path batches) goes there first.
+int symb_gemm_skinny_max_m();
+bool symb_gemm_skinny_supported(int epi, int M, int N, int K);
+int symb_gemm_skinny(int epi, const void* A, int lda, const void* W, int ldw, const float* bias,
+                     const void* R, int ldr, const float* gamma, const float* beta, float eps,
+                     int gelu_poly, void* C, int ldc, int M, int N, int K, hipStream_t st);
+
 // Returns 0 on success, a HIP error code, or -1 for an unsupported shape.
 int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const float* bias,
               const void* R, int ldr, const float* gamma, const float* beta, float eps, void* C,
               int ldc, int M, int N, int K, hipStream_t st) {
   if (M <= 0) return 0;
+  if (M <= symb_gemm_skinny_max_m() && symb_gemm_skinny_supported(epi, M, N, K) &&
+      (epi != EPI_RES_LN || N == 384))   // wider rows: EPI_RES + symb_add_ln, as below
+    return symb_gemm_skinny(epi, A, lda, W, ldw, bias, R, ldr, gamma, beta, eps, g_gelu_poly, C,
+                            ldc, M, N, K, st);
   if (epi == EPI_GELU) eps = g_gelu_poly ? 1.f : 0.f;
   if (K % GEMM_BK != 0) return -1;
   auto a = (const __bf16*)A;

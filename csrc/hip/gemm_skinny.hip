@@ -1,0 +1,287 @@
+// Small-M ("skinny") split-K GEMM for the query path: C[M,N] = epi(A[M,K] . W[N,K]^T + bias), M <= 64.
+//
+// A query-embedding forward (B = 1..32 sentences, tens to a few hundred tokens) is bound by the
+// serial k-loop of the big-tile GEMM: a 128-row tile holding a handful of real rows still walks
+// every k-tile of W one after another, and the row-complete RES_LN tile of MiniLM's FFN2 runs
+// 24 k-tiles in ONE workgroup (profiles/r1_gemm/latency.log: 386 us for a 1 x 16 MiniLM-L6
+// forward).  Replaces, for that regime, the same reference op as gemm.hip (the K5 / K12-K17
+// linears of candle's BertModel, /root/reference/services/preprocessing_service/src/
+// embedding_generator.rs:198).
+//
+// CDNA4 design:
+//  * Split K as far as it goes: one WAVE per (64-column block, 128-k granule).  A workgroup is
+//    4 waves = 4 consecutive granules of one column block; grid = (N/64, ceil(K/128 / 4)).
+//    Every wave issues all of its loads at once (one round trip to HBM/L2) and then 4 x RM x 4
+//    v_mfma_f32_16x16x32_bf16 -- no LDS staging, no k-loop.
+//  * Each lane loads 64 contiguous bytes of a row (4 x 16-byte loads): the 4 lane groups of a row
+//    cover 256 contiguous bytes.  The MFMA's k order is a permutation of memory order (step t,
+//    lane group g, element e <-> k = 32g + 8t + e), applied identically to A and W, so the dot
+//    products are unchanged.
+//  * The 4 waves' accumulators are summed through LDS; the workgroup writes one fp32 partial
+//    slice P[split][M][64 cols].  A second kernel (one wave per row) sums the splits in a fixed
+//    order (deterministic), adds bias, and applies GELU / residual / residual + LayerNorm, with
+//    16-byte bf16 stores.  LayerNorm needs whole rows, which only exist after the split sum.
+#include <mutex>
+#include <unordered_map>
+
+#include "common.h"
+
+namespace symb {
+
+namespace {
+
+enum { SK_BIAS = 0, SK_GELU = 1, SK_RES = 2, SK_RES_LN = 3 };   // == gemm.hip's EPI_* values
+
+template <int RM>
+__global__ __launch_bounds__(256) void skinny_partial_kernel(
+    const __bf16* __restrict__ A, int lda, const __bf16* __restrict__ W, int ldw,
+    float* __restrict__ P, int M, int N, int KG) {
+  constexpr int MP = RM * 16;
+  __shared__ float red[3][MP][64 + 4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n0 = blockIdx.x * 64;
+  const int g = blockIdx.y * 4 + wave;            // this wave's 128-k granule
+  const int r = lane & 15, grp = lane >> 4;
+
+  f32x4 acc[RM][4];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (g < KG) {
+    const size_t k0 = (size_t)g * 128 + grp * 32;
+    bf16x8 a[RM][4], b[4][4];
+#pragma unroll
+    for (int i = 0; i < RM; ++i) {
+      const __bf16* pa = A + (size_t)min(i * 16 + r, M - 1) * lda + k0;   // rows >= M: ignored
+#pragma unroll
+      for (int t = 0; t < 4; ++t) a[i][t] = *reinterpret_cast<const bf16x8*>(pa + 8 * t);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const __bf16* pb = W + (size_t)(n0 + j * 16 + r) * ldw + k0;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) b[j][t] = *reinterpret_cast<const bf16x8*>(pb + 8 * t);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][t], b[j][t], acc[i][j], 0, 0, 0);
+  }
+
+  // accumulator (i, j)[e] sits at row i*16 + grp*4 + e, column j*16 + r of the 64-column block
+  if (wave > 0) {
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) red[wave - 1][i * 16 + grp * 4 + e][j * 16 + r] = acc[i][j][e];
+  }
+  __syncthreads();
+  if (wave == 0) {
+    float* Pb = P + (size_t)blockIdx.y * M * N + n0;
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = i * 16 + grp * 4 + e;
+        if (row >= M) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int col = j * 16 + r;
+          Pb[(size_t)row * N + col] =
+              acc[i][j][e] + red[0][row][col] + red[1][row][col] + red[2][row][col];
+        }
+      }
+  }
+}
+
+// One wave per output row; lane owns 8 consecutive columns per PER-chunk (N <= PER * 512).
+template <int EPI, int PER>
+__global__ __launch_bounds__(256) void skinny_epi_kernel(
+    const float* __restrict__ P, int S, const float* __restrict__ bias,
+    const __bf16* __restrict__ R, int ldr, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, int gelu_poly, __bf16* __restrict__ C, int ldc,
+    int M, int N) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int NV = N / 8;
+  float x[PER][8];
+  float s = 0.f;
+#pragma unroll
+  for (int p = 0; p < PER; ++p) {
+    const int v = lane + 64 * p;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[p][e] = 0.f;
+    if (v >= NV) continue;
+    const f32x4 b0 = *reinterpret_cast<const f32x4*>(bias + v * 8);
+    const f32x4 b1 = *reinterpret_cast<const f32x4*>(bias + v * 8 + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      x[p][e] = b0[e];
+      x[p][e + 4] = b1[e];
+    }
+    for (int sp = 0; sp < S; ++sp) {   // fixed order: deterministic
+      const float* q = P + ((size_t)sp * M + row) * N + v * 8;
+      const f32x4 q0 = *reinterpret_cast<const f32x4*>(q);
+      const f32x4 q1 = *reinterpret_cast<const f32x4*>(q + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        x[p][e] += q0[e];
+        x[p][e + 4] += q1[e];
+      }
+    }
+    if constexpr (EPI == SK_GELU) {
+      if (gelu_poly) {
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+          const f32x2 y = gelu2_poly(f32x2{x[p][e], x[p][e + 1]});
+          x[p][e] = y.x;
+          x[p][e + 1] = y.y;
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[p][e] = gelu_erf(x[p][e]);
+      }
+    }
+    if constexpr (EPI == SK_RES || EPI == SK_RES_LN) {
+      float rr[8];
+      load8(R + (size_t)row * ldr + v * 8, rr);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[p][e] += rr[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += x[p][e];
+  }
+  if constexpr (EPI == SK_RES_LN) {
+    const float mean = wave_sum(s) / (float)N;
+    float ss = 0.f;
+#pragma unroll
+    for (int p = 0; p < PER; ++p)
+      if (lane + 64 * p < NV)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = x[p][e] - mean;
+          ss += d * d;
+        }
+    const float rstd = rsqrtf(wave_sum(ss) / (float)N + eps);
+#pragma unroll
+    for (int p = 0; p < PER; ++p) {
+      const int v = lane + 64 * p;
+      if (v >= NV) continue;
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        x[p][e] = (x[p][e] - mean) * rstd * gamma[v * 8 + e] + beta[v * 8 + e];
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < PER; ++p) {
+    const int v = lane + 64 * p;
+    if (v < NV) store8(C + (size_t)row * ldc + v * 8, x[p]);
+  }
+}
+
+// fp32 split partials, one buffer per stream (encoders on different streams must not share it);
+// grown on demand -- the first call of a shape happens before any graph capture of it.
+struct Scratch {
+  float* p = nullptr;
+  size_t bytes = 0;
+};
+std::mutex g_scratch_mu;
+std::unordered_map<hipStream_t, Scratch> g_scratch;
+
+float* scratch_for(hipStream_t st, size_t bytes) {
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  Scratch& s = g_scratch[st];
+  if (s.bytes < bytes) {
+    if (s.p) {
+      (void)hipStreamSynchronize(st);   // in-flight kernels of this stream may still read it
+      (void)hipFree(s.p);
+      s.p = nullptr;
+      s.bytes = 0;
+    }
+    const size_t want = bytes < ((size_t)1 << 20) ? ((size_t)1 << 20) : bytes;
+    if (hipMalloc(&s.p, want) != hipSuccess) return nullptr;
+    s.bytes = want;
+  }
+  return s.p;
+}
+
+template <int EPI>
+int launch_epi(int per, const float* P, int S, const float* bias, const __bf16* R, int ldr,
+               const float* g, const float* b, float eps, int gelu_poly, __bf16* C, int ldc, int M,
+               int N, hipStream_t st) {
+  const dim3 grid((M + 3) / 4), block(256);
+#define SK_E(PER_) hipLaunchKernelGGL((skinny_epi_kernel<EPI, PER_>), grid, block, 0, st, P, S, \
+                                      bias, R, ldr, g, b, eps, gelu_poly, C, ldc, M, N)
+  switch (per) {
+    case 1: SK_E(1); break;
+    case 2: SK_E(2); break;
+    case 4: SK_E(4); break;
+    case 8: SK_E(8); break;
+    default: return -1;
+  }
+#undef SK_E
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// Largest M the skinny path takes (0 = off); symb_gemm consults it first.
+static int g_skinny_max_m = 64;
+int symb_gemm_skinny_config(int max_m) {
+  if (max_m < 0 || max_m > 64) return -1;
+  g_skinny_max_m = max_m;
+  return 0;
+}
+int symb_gemm_skinny_max_m() { return g_skinny_max_m; }
+
+bool symb_gemm_skinny_supported(int epi, int M, int N, int K) {
+  return M >= 1 && M <= 64 && epi >= SK_BIAS && epi <= SK_RES_LN && K % 128 == 0 && N % 64 == 0 &&
+         N <= 4096;
+}
+
+// Returns 0, a HIP error code, or -1 (shape not supported: the caller takes its other paths).
+int symb_gemm_skinny(int epi, const void* A, int lda, const void* W, int ldw, const float* bias,
+                     const void* R, int ldr, const float* gamma, const float* beta, float eps,
+                     int gelu_poly, void* C, int ldc, int M, int N, int K, hipStream_t st) {
+  if (!symb_gemm_skinny_supported(epi, M, N, K)) return -1;
+  const int KG = K / 128, S = (KG + 3) / 4;
+  float* P = scratch_for(st, (size_t)S * M * N * sizeof(float));
+  if (!P) return (int)hipErrorOutOfMemory;
+  const dim3 grid(N / 64, S), block(256);
+  auto a = (const __bf16*)A;
+  auto w = (const __bf16*)W;
+  const int rm = (M + 15) / 16;
+  if (rm == 1)
+    hipLaunchKernelGGL(skinny_partial_kernel<1>, grid, block, 0, st, a, lda, w, ldw, P, M, N, KG);
+  else if (rm == 2)
+    hipLaunchKernelGGL(skinny_partial_kernel<2>, grid, block, 0, st, a, lda, w, ldw, P, M, N, KG);
+  else
+    hipLaunchKernelGGL(skinny_partial_kernel<4>, grid, block, 0, st, a, lda, w, ldw, P, M, N, KG);
+  int rc = (int)hipGetLastError();
+  if (rc) return rc;
+  const int nv = N / 8;
+  const int per = nv <= 64 ? 1 : nv <= 128 ? 2 : nv <= 256 ? 4 : 8;
+  auto r = (const __bf16*)R;
+  auto c = (__bf16*)C;
+  switch (epi) {
+    case SK_BIAS:
+      return launch_epi<SK_BIAS>(per, P, S, bias, r, ldr, gamma, beta, eps, gelu_poly, c, ldc, M, N, st);
+    case SK_GELU:
+      return launch_epi<SK_GELU>(per, P, S, bias, r, ldr, gamma, beta, eps, gelu_poly, c, ldc, M, N, st);
+    case SK_RES:
+      return launch_epi<SK_RES>(per, P, S, bias, r, ldr, gamma, beta, eps, gelu_poly, c, ldc, M, N, st);
+    case SK_RES_LN:
+      return launch_epi<SK_RES_LN>(per, P, S, bias, r, ldr, gamma, beta, eps, gelu_poly, c, ldc, M, N, st);
+  }
+  return -1;
+}
+
+}  // namespace symb
