@@ -23,7 +23,12 @@ def main() -> None:
     ap.add_argument("--b", type=int, default=1)
     ap.add_argument("--s", type=int, default=16)
     ap.add_argument("--iters", type=int, default=200)
+    ap.add_argument("--skinny-max-m", type=int, default=64,
+                    help="largest M of the small-M split-K GEMM path (0: tiled GEMMs only)")
     a = ap.parse_args()
+    from codename_symbiont_amd.ops._ext import hip
+
+    hip().gemm_skinny_config(a.skinny_max_m)
     from codename_symbiont_amd.models import get_config
     from codename_symbiont_amd.models.encoder import HipEncoder, synthetic_batch
 
@@ -41,6 +46,7 @@ def main() -> None:
         ts.append(time.perf_counter() - t0)
     ts.sort()
     print(json.dumps({"bench": "encoder_latency_us", "model": a.model, "B": a.b, "S": a.s,
+                      "tokens": int(b.num_tokens), "skinny_max_m": a.skinny_max_m,
                       "p50_us": round(ts[len(ts) // 2] * 1e6, 1),
                       "p10_us": round(ts[len(ts) // 10] * 1e6, 1)}))
 
