@@ -95,7 +95,7 @@ int symb_prune_qprep(const void* Q, int NQ, int dim, const float* pre_s, const f
                      float* thr, hipStream_t st);
 int symb_gemm_lt_config(int mode);
 int symb_gemm_lt_plans();
-int symb_gemm_skinny_config(int max_m);
+int symb_gemm_skinny_config(int max_m, int fuse);
 int symb_gemm_skinny_max_m();
 int symb_mq_config(int aux);
 int symb_index_scan_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
@@ -494,9 +494,9 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gemm_config", [](int resln_bm, int tile, int group_m) {
     check(symb_gemm_config(resln_bm, tile, group_m), "gemm_config");
   }, py::arg("resln_bm") = 128, py::arg("tile") = 3, py::arg("group_m") = 8);
-  m.def("gemm_skinny_config", [](int max_m) {
-    check(symb_gemm_skinny_config(max_m), "gemm_skinny_config");
-  }, py::arg("max_m") = 64);
+  m.def("gemm_skinny_config", [](int max_m, int fuse) {
+    check(symb_gemm_skinny_config(max_m, fuse), "gemm_skinny_config");
+  }, py::arg("max_m") = 64, py::arg("fuse") = 1);
   m.def("gemm_skinny_max_m", []() { return symb_gemm_skinny_max_m(); });
   m.def("gemm_resln_config", [](int waves) { check(symb_gemm_resln_config(waves), "gemm_resln_config"); },
         py::arg("waves") = 16);

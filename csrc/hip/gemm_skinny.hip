@@ -21,6 +21,8 @@
 //    slice P[split][M][64 cols].  A second kernel (one wave per row) sums the splits in a fixed
 //    order (deterministic), adds bias, and applies GELU / residual / residual + LayerNorm, with
 //    16-byte bf16 stores.  LayerNorm needs whole rows, which only exist after the split sum.
+//    With a single split (K <= 512: MiniLM's QKV and FFN1) and a row-local epilogue, the split
+//    kernel applies bias / GELU / residual itself and there is no second launch.
 #include <mutex>
 #include <unordered_map>
 
@@ -32,10 +34,15 @@ namespace {
 
 enum { SK_BIAS = 0, SK_GELU = 1, SK_RES = 2, SK_RES_LN = 3 };   // == gemm.hip's EPI_* values
 
-template <int RM>
+// EPI = SK_PARTIAL: write the fp32 split partial; else (one split, K <= 512) apply bias / GELU /
+// residual here and store bf16 -- no second launch.
+constexpr int SK_PARTIAL = -1;
+
+template <int RM, int EPI>
 __global__ __launch_bounds__(256) void skinny_partial_kernel(
     const __bf16* __restrict__ A, int lda, const __bf16* __restrict__ W, int ldw,
-    float* __restrict__ P, int M, int N, int KG) {
+    float* __restrict__ P, int M, int N, int KG, const float* __restrict__ bias,
+    const __bf16* __restrict__ R, int ldr, int gelu_poly, __bf16* __restrict__ C, int ldc) {
   constexpr int MP = RM * 16;
   __shared__ float red[3][MP][64 + 4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -94,8 +101,21 @@ __global__ __launch_bounds__(256) void skinny_partial_kernel(
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int col = j * 16 + r;
-          Pb[(size_t)row * N + col] =
-              acc[i][j][e] + red[0][row][col] + red[1][row][col] + red[2][row][col];
+          float v = acc[i][j][e] + red[0][row][col] + red[1][row][col] + red[2][row][col];
+          if constexpr (EPI == SK_PARTIAL) {
+            Pb[(size_t)row * N + col] = v;
+          } else {
+            v += bias[n0 + col];
+            if constexpr (EPI == SK_GELU) {
+              if (gelu_poly) {
+                v = gelu2_poly(f32x2{v, v}).x;
+              } else {
+                v = gelu_erf(v);
+              }
+            }
+            if constexpr (EPI == SK_RES) v += (float)R[(size_t)row * ldr + n0 + col];
+            C[(size_t)row * ldc + n0 + col] = (__bf16)v;
+          }
         }
       }
   }
@@ -235,9 +255,12 @@ int launch_epi(int per, const float* P, int S, const float* bias, const __bf16* 
 
 // Largest M the skinny path takes (0 = off); symb_gemm consults it first.
 static int g_skinny_max_m = 64;
-int symb_gemm_skinny_config(int max_m) {
-  if (max_m < 0 || max_m > 64) return -1;
+// 1: a single-split bias / GELU / residual GEMM applies its epilogue in the split kernel
+static int g_skinny_fuse = 1;
+int symb_gemm_skinny_config(int max_m, int fuse) {
+  if (max_m < 0 || max_m > 64 || fuse < 0 || fuse > 1) return -1;
   g_skinny_max_m = max_m;
+  g_skinny_fuse = fuse;
   return 0;
 }
 int symb_gemm_skinny_max_m() { return g_skinny_max_m; }
@@ -258,19 +281,33 @@ int symb_gemm_skinny(int epi, const void* A, int lda, const void* W, int ldw, co
   const dim3 grid(N / 64, S), block(256);
   auto a = (const __bf16*)A;
   auto w = (const __bf16*)W;
-  const int rm = (M + 15) / 16;
-  if (rm == 1)
-    hipLaunchKernelGGL(skinny_partial_kernel<1>, grid, block, 0, st, a, lda, w, ldw, P, M, N, KG);
-  else if (rm == 2)
-    hipLaunchKernelGGL(skinny_partial_kernel<2>, grid, block, 0, st, a, lda, w, ldw, P, M, N, KG);
-  else
-    hipLaunchKernelGGL(skinny_partial_kernel<4>, grid, block, 0, st, a, lda, w, ldw, P, M, N, KG);
-  int rc = (int)hipGetLastError();
-  if (rc) return rc;
-  const int nv = N / 8;
-  const int per = nv <= 64 ? 1 : nv <= 128 ? 2 : nv <= 256 ? 4 : 8;
   auto r = (const __bf16*)R;
   auto c = (__bf16*)C;
+  const int rm = (M + 15) / 16;
+  // one split and a row-local epilogue: finished in the one kernel
+  const int fused = (S == 1 && epi != SK_RES_LN && g_skinny_fuse) ? epi : SK_PARTIAL;
+#define SK_P(RM_, E_) hipLaunchKernelGGL((skinny_partial_kernel<RM_, E_>), grid, block, 0, st, a, \
+                                         lda, w, ldw, P, M, N, KG, bias, r, ldr, gelu_poly, c, ldc)
+#define SK_PE(RM_)                         \
+  switch (fused) {                         \
+    case SK_BIAS: SK_P(RM_, SK_BIAS); break; \
+    case SK_GELU: SK_P(RM_, SK_GELU); break; \
+    case SK_RES: SK_P(RM_, SK_RES); break;   \
+    default: SK_P(RM_, SK_PARTIAL); break;   \
+  }
+  if (rm == 1) {
+    SK_PE(1)
+  } else if (rm == 2) {
+    SK_PE(2)
+  } else {
+    SK_PE(4)
+  }
+#undef SK_PE
+#undef SK_P
+  int rc = (int)hipGetLastError();
+  if (rc || fused != SK_PARTIAL) return rc;
+  const int nv = N / 8;
+  const int per = nv <= 64 ? 1 : nv <= 128 ? 2 : nv <= 256 ? 4 : 8;
   switch (epi) {
     case SK_BIAS:
       return launch_epi<SK_BIAS>(per, P, S, bias, r, ldr, gamma, beta, eps, gelu_poly, c, ldc, M, N, st);

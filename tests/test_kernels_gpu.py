@@ -205,6 +205,12 @@ def test_gemm_skinny(M, N, K, epi):
     ref = R.gemm_ref(a, w, bias, epi, res, g, b, 1e-12)
     _close(out, ref, atol=4e-2, rtol=2e-2, what=f"skinny gemm epi={epi}")
     assert torch.equal(out, out2), "skinny gemm is not deterministic"
+    hip().gemm_skinny_config(64, 0)   # the single-split epilogue in the second kernel instead
+    try:
+        unfused = gemm(a, w, bias, epi, res, g, b, 1e-12)
+    finally:
+        hip().gemm_skinny_config(64, 1)
+    assert torch.equal(out, unfused), "fused and two-kernel skinny epilogues differ"
     hip().gemm_skinny_config(0)
     try:
         big = gemm(a, w, bias, epi, res, g, b, 1e-12)
