@@ -25,6 +25,8 @@ def main() -> None:
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--skinny-max-m", type=int, default=64,
                     help="largest M of the small-M split-K GEMM path (0: tiled GEMMs only)")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the bucketed hipGraph (HipEncoder.forward_graphed) instead of eager")
     a = ap.parse_args()
     from codename_symbiont_amd.ops._ext import hip
 
@@ -35,18 +37,20 @@ def main() -> None:
     cfg = get_config(a.model)
     enc = HipEncoder(cfg, seed=0)
     b = synthetic_batch(cfg, a.b, a.s, seed=1).to("cuda")
+    fwd = enc.forward_graphed if a.graph else enc.forward_packed
     for _ in range(20):
-        enc.forward_packed(b)
+        fwd(b)
     torch.cuda.synchronize()
     ts = []
     for _ in range(a.iters):
         t0 = time.perf_counter()
-        enc.forward_packed(b)
+        fwd(b)
         torch.cuda.synchronize()
         ts.append(time.perf_counter() - t0)
     ts.sort()
     print(json.dumps({"bench": "encoder_latency_us", "model": a.model, "B": a.b, "S": a.s,
                       "tokens": int(b.num_tokens), "skinny_max_m": a.skinny_max_m,
+                      "graph": a.graph,
                       "p50_us": round(ts[len(ts) // 2] * 1e6, 1),
                       "p10_us": round(ts[len(ts) // 10] * 1e6, 1)}))
 

@@ -253,6 +253,10 @@ int launch_epi(int per, const float* P, int S, const float* bias, const __bf16* 
 
 }  // namespace
 
+}  // namespace symb
+
+using namespace symb;
+
 // Largest M the skinny path takes (0 = off); symb_gemm consults it first.
 static int g_skinny_max_m = 64;
 // 1: a single-split bias / GELU / residual GEMM applies its epilogue in the split kernel
@@ -320,5 +324,3 @@ int symb_gemm_skinny(int epi, const void* A, int lda, const void* W, int ldw, co
   }
   return -1;
 }
-
-}  // namespace symb
