@@ -171,8 +171,15 @@ class HipEncoder:
             if self.precision == "fp8":   # e4m3 activations + per-token scales
                 self._ws += [torch.empty(cap, max(H, F), dtype=torch.uint8, device=self.device),
                              torch.empty(cap, dtype=torch.float32, device=self.device)]
+            self._ws += self._skinny_ws()
             self._ws_tokens = cap
         return [t.data_ptr() for t in self._ws]
+
+    def _skinny_ws(self) -> list[torch.Tensor]:
+        """The small-M GEMMs' split-partial buffer (gemm_skinny.hip), last in the workspace: a
+        captured graph owns its own, so replay never shares it with an eager forward."""
+        n = self.rt.skinny_ws_bytes()
+        return [torch.empty(max(n, 4) // 4, dtype=torch.float32, device=self.device)]
 
     def last_hidden(self) -> torch.Tensor:
         return self._ws[0]
@@ -266,6 +273,7 @@ class HipEncoder:
         if self.precision == "fp8":
             ws += [torch.empty(Tb, max(H, cfg.ffn), dtype=torch.uint8, device=dev),
                    torch.empty(Tb, dtype=torch.float32, device=dev)]
+        ws += self._skinny_ws()
         f32 = torch.empty(Bb + 1, H, dtype=torch.float32, device=dev)
         unit = torch.empty(Bb + 1, H, dtype=torch.bfloat16, device=dev)
         max_len = min(Tb, cfg.max_position - cfg.position_offset)

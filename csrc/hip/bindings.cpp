@@ -13,6 +13,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -97,6 +98,8 @@ int symb_gemm_lt_config(int mode);
 int symb_gemm_lt_plans();
 int symb_gemm_skinny_config(int max_m, int fuse);
 int symb_gemm_skinny_max_m();
+size_t symb_gemm_skinny_scratch_bytes(int epi, int M, int N, int K);
+void symb_gemm_skinny_set_scratch(void* p, size_t bytes);
 int symb_mq_config(int aux);
 int symb_index_scan_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                        int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
@@ -172,13 +175,33 @@ class EncoderRuntime {
   }
   int num_layers() const { return (int)layers_.size(); }
 
+  // Split-partial buffer the bf16 layers' small-M (query-path) GEMMs need: skinny_ws_bytes().
+  size_t skinny_ws_bytes() const {
+    const int H = H_, M = 64;
+    size_t b = 0;
+    auto mx = [&](int epi, int N, int K) { b = std::max(b, symb_gemm_skinny_scratch_bytes(epi, M, N, K)); };
+    mx(EPI_BIAS, 3 * H, H);
+    mx(H == 384 ? EPI_RES_LN : EPI_RES, H, H);
+    mx(EPI_GELU, FF_, H);
+    mx(H == 384 ? EPI_RES_LN : EPI_RES, H, FF_);
+    return b;
+  }
+
   // ws: {h, h2, qkv, ctx, ff, tmp} device buffers sized for T tokens; fp8 layers add
-  // {a8 (T x max(H, FF) bytes), sa (T floats)}.
+  // {a8 (T x max(H, FF) bytes), sa (T floats)}.  Optionally one more, last: the small-M GEMMs'
+  // split-partial buffer of skinny_ws_bytes() bytes (a captured graph then owns its own).
   void forward(uptr ids, uptr pos, uptr tt, uptr cu, int T, int B, int max_len,
-               const std::vector<uptr>& ws, int pool_mode, int normalize_f32, uptr out_f32,
+               const std::vector<uptr>& ws_in, int pool_mode, int normalize_f32, uptr out_f32,
                uptr out_norm, uptr stream) {
-    if (ws.size() != (any_fp8_ ? 8u : 6u))
-      throw std::invalid_argument(any_fp8_ ? "fp8 workspace needs 8 buffers" : "workspace needs 6 buffers");
+    const size_t base = any_fp8_ ? 8u : 6u;
+    if (ws_in.size() != base && ws_in.size() != base + 1)
+      throw std::invalid_argument(any_fp8_ ? "fp8 workspace needs 8 buffers (+ skinny scratch)"
+                                           : "workspace needs 6 buffers (+ skinny scratch)");
+    std::vector<uptr> ws(ws_in.begin(), ws_in.begin() + base);
+    struct ScratchGuard {
+      ScratchGuard(uptr p, size_t n) { symb_gemm_skinny_set_scratch(P<void>(p), n); }
+      ~ScratchGuard() { symb_gemm_skinny_set_scratch(nullptr, 0); }
+    } guard(ws_in.size() > base ? ws_in.back() : 0, skinny_ws_bytes());
     hipStream_t st = S(stream);
     const int H = H_;
     uptr h = ws[0], h2 = ws[1], qkv = ws[2], ctx = ws[3], ff = ws[4], tmp = ws[5];
@@ -552,5 +575,6 @@ PYBIND11_MODULE(_hip, m) {
       .def("add_layer", &EncoderRuntime::add_layer)
       .def("add_layer_fp8", &EncoderRuntime::add_layer_fp8)
       .def("num_layers", &EncoderRuntime::num_layers)
+      .def("skinny_ws_bytes", &EncoderRuntime::skinny_ws_bytes)
       .def("forward", &EncoderRuntime::forward);
 }

@@ -207,30 +207,30 @@ __global__ __launch_bounds__(256) void skinny_epi_kernel(
   }
 }
 
-// fp32 split partials, one buffer per stream (encoders on different streams must not share it);
-// grown on demand -- the first call of a shape happens before any graph capture of it.
-struct Scratch {
-  float* p = nullptr;
-  size_t bytes = 0;
-};
+// fp32 split partials.  An encoder forward hands in its own buffer (part of its workspace, so a
+// captured hipGraph bakes a pointer that lives as long as the graph): symb_gemm_skinny_set_scratch,
+// thread-local, set for the duration of the forward.  Other callers get one fixed-size buffer
+// per stream (concurrent streams must not share one), allocated on first use and never moved;
+// a stream under capture that has none takes the tiled path instead (no allocation in a capture).
+constexpr size_t kStreamScratchBytes = (size_t)64 * 4096 * 8 * sizeof(float);  // M, N, splits max
+thread_local float* t_scratch = nullptr;
+thread_local size_t t_scratch_bytes = 0;
 std::mutex g_scratch_mu;
-std::unordered_map<hipStream_t, Scratch> g_scratch;
+std::unordered_map<hipStream_t, float*> g_scratch;
 
 float* scratch_for(hipStream_t st, size_t bytes) {
+  if (t_scratch && t_scratch_bytes >= bytes) return t_scratch;
+  if (bytes > kStreamScratchBytes) return nullptr;
   std::lock_guard<std::mutex> lk(g_scratch_mu);
-  Scratch& s = g_scratch[st];
-  if (s.bytes < bytes) {
-    if (s.p) {
-      (void)hipStreamSynchronize(st);   // in-flight kernels of this stream may still read it
-      (void)hipFree(s.p);
-      s.p = nullptr;
-      s.bytes = 0;
-    }
-    const size_t want = bytes < ((size_t)1 << 20) ? ((size_t)1 << 20) : bytes;
-    if (hipMalloc(&s.p, want) != hipSuccess) return nullptr;
-    s.bytes = want;
-  }
-  return s.p;
+  auto it = g_scratch.find(st);
+  if (it != g_scratch.end()) return it->second;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
+    return nullptr;
+  float* p = nullptr;
+  if (hipMalloc(&p, kStreamScratchBytes) != hipSuccess) return nullptr;
+  g_scratch[st] = p;
+  return p;
 }
 
 template <int EPI>
@@ -269,27 +269,42 @@ int symb_gemm_skinny_config(int max_m, int fuse) {
 }
 int symb_gemm_skinny_max_m() { return g_skinny_max_m; }
 
-bool symb_gemm_skinny_supported(int epi, int M, int N, int K) {
-  return M >= 1 && M <= 64 && epi >= SK_BIAS && epi <= SK_RES_LN && K % 128 == 0 && N % 64 == 0 &&
-         N <= 4096;
+void symb_gemm_skinny_set_scratch(void* p, size_t bytes) {
+  t_scratch = (float*)p;
+  t_scratch_bytes = p ? bytes : 0;
 }
 
+bool symb_gemm_skinny_supported(int epi, int M, int N, int K) {
+  return M >= 1 && M <= 64 && epi >= SK_BIAS && epi <= SK_RES_LN && K % 128 == 0 && K <= 4096 &&
+         N % 64 == 0 && N <= 4096;
+}
+
+// Split-partial bytes an M x N x K skinny GEMM may need (an upper bound: independent of the
+// fused single-split epilogue, which needs none; 0 for shapes the path does not take).
+size_t symb_gemm_skinny_scratch_bytes(int epi, int M, int N, int K) {
+  if (!symb_gemm_skinny_supported(epi, M, N, K)) return 0;
+  const int S = (K / 128 + 3) / 4;
+  return (size_t)S * M * N * sizeof(float);
+}
 // Returns 0, a HIP error code, or -1 (shape not supported: the caller takes its other paths).
 int symb_gemm_skinny(int epi, const void* A, int lda, const void* W, int ldw, const float* bias,
                      const void* R, int ldr, const float* gamma, const float* beta, float eps,
                      int gelu_poly, void* C, int ldc, int M, int N, int K, hipStream_t st) {
   if (!symb_gemm_skinny_supported(epi, M, N, K)) return -1;
   const int KG = K / 128, S = (KG + 3) / 4;
-  float* P = scratch_for(st, (size_t)S * M * N * sizeof(float));
-  if (!P) return (int)hipErrorOutOfMemory;
+  // one split and a row-local epilogue: finished in the one kernel
+  const int fused = (S == 1 && epi != SK_RES_LN && g_skinny_fuse) ? epi : SK_PARTIAL;
+  float* P = nullptr;
+  if (fused == SK_PARTIAL) {
+    P = scratch_for(st, (size_t)S * M * N * sizeof(float));
+    if (!P) return -1;   // no buffer for this stream (capturing, or out of memory): tiled path
+  }
   const dim3 grid(N / 64, S), block(256);
   auto a = (const __bf16*)A;
   auto w = (const __bf16*)W;
   auto r = (const __bf16*)R;
   auto c = (__bf16*)C;
   const int rm = (M + 15) / 16;
-  // one split and a row-local epilogue: finished in the one kernel
-  const int fused = (S == 1 && epi != SK_RES_LN && g_skinny_fuse) ? epi : SK_PARTIAL;
 #define SK_P(RM_, E_) hipLaunchKernelGGL((skinny_partial_kernel<RM_, E_>), grid, block, 0, st, a, \
                                          lda, w, ldw, P, M, N, KG, bias, r, ldr, gelu_poly, c, ldc)
 #define SK_PE(RM_)                         \

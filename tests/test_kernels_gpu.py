@@ -995,6 +995,34 @@ def test_index_scan_fp8_seeded_matches_unseeded():
 
 
 @pytest.mark.gpu
+def test_encoder_graph_replay_skinny():
+    """Query-path batches whose token bucket stays <= 64 run the small-M GEMMs inside the
+    captured graph too (the graph owns its split-partial buffer): replay == eager, also after
+    eager forwards of other shapes in between."""
+    from codename_symbiont_amd.models import get_config
+    from codename_symbiont_amd.models.encoder import HipEncoder, synthetic_batch
+    from codename_symbiont_amd.ops._ext import hip
+
+    assert hip().gemm_skinny_max_m() == 64
+    for model in ("minilm-l6", "bge-base"):
+        cfg = get_config(model)
+        enc = HipEncoder(cfg, seed=4)
+        batches = [synthetic_batch(cfg, B, S, seed=seed, varlen=True).to(DEV)
+                   for B, S, seed in [(1, 9, 0), (3, 17, 4), (2, 30, 7)]]
+        for rnd in range(2):
+            for b in batches:
+                assert b.num_tokens + 1 <= 64
+                e32, eu = enc.forward_packed(b)
+                e32, eu = e32.clone(), eu.clone()
+                other = synthetic_batch(cfg, 1, 40, seed=99 + rnd).to(DEV)
+                g32, gu = enc.forward_graphed(b)
+                enc.forward_packed(other)          # eager work between replay and the check
+                torch.cuda.synchronize()
+                _close(g32, e32, atol=1e-5, what=f"{model} graph f32 T={b.num_tokens}")
+                assert torch.equal(gu, eu)
+
+
+@pytest.mark.gpu
 def test_encoder_graph_replay_matches_eager():
     """hipGraph path (bucketed, dummy-padded) == eager forward, across buckets and re-use."""
     from codename_symbiont_amd.models import get_config
