@@ -178,8 +178,8 @@ class HipEncoder:
     def _skinny_ws(self) -> list[torch.Tensor]:
         """The small-M GEMMs' split-partial buffer (gemm_skinny.hip), last in the workspace: a
         captured graph owns its own, so replay never shares it with an eager forward."""
-        n = self.rt.skinny_ws_bytes()
-        return [torch.empty(max(n, 4) // 4, dtype=torch.float32, device=self.device)]
+        n = self.rt.skinny_ws_bytes()   # header (zeroed last-workgroup counter) + partials
+        return [torch.zeros(max(n, 4) // 4, dtype=torch.float32, device=self.device)]
 
     def last_hidden(self) -> torch.Tensor:
         return self._ws[0]

@@ -17,12 +17,15 @@
 //    cover 256 contiguous bytes.  The MFMA's k order is a permutation of memory order (step t,
 //    lane group g, element e <-> k = 32g + 8t + e), applied identically to A and W, so the dot
 //    products are unchanged.
-//  * The 4 waves' accumulators are summed through LDS; the workgroup writes one fp32 partial
-//    slice P[split][M][64 cols].  A second kernel (one wave per row) sums the splits in a fixed
+//  * The 4 waves' accumulators are summed through LDS (every thread then owns 8 consecutive
+//    columns of a row: 16-byte reads and stores); the workgroup writes one fp32 partial slice
+//    P[split][M][64 cols].  A second kernel (one wave per row) sums the splits in a fixed
 //    order (deterministic), adds bias, and applies GELU / residual / residual + LayerNorm, with
 //    16-byte bf16 stores.  LayerNorm needs whole rows, which only exist after the split sum.
 //    With a single split (K <= 512: MiniLM's QKV and FFN1) and a row-local epilogue, the split
-//    kernel applies bias / GELU / residual itself and there is no second launch.
+//    kernel applies bias / GELU / residual itself; for small outputs (M x N <= 16384, N <= 1024:
+//    MiniLM's out-proj + LN and FFN2 + LN at M <= 42, bge's out-proj / FFN2 at M <= 21) the last
+//    workgroup to finish does the split sum and epilogue -- either way, no second launch.
 #include <mutex>
 #include <unordered_map>
 
@@ -34,103 +37,14 @@ namespace {
 
 enum { SK_BIAS = 0, SK_GELU = 1, SK_RES = 2, SK_RES_LN = 3 };   // == gemm.hip's EPI_* values
 
-// EPI = SK_PARTIAL: write the fp32 split partial; else (one split, K <= 512) apply bias / GELU /
-// residual here and store bf16 -- no second launch.
-constexpr int SK_PARTIAL = -1;
-
-template <int RM, int EPI>
-__global__ __launch_bounds__(256) void skinny_partial_kernel(
-    const __bf16* __restrict__ A, int lda, const __bf16* __restrict__ W, int ldw,
-    float* __restrict__ P, int M, int N, int KG, const float* __restrict__ bias,
-    const __bf16* __restrict__ R, int ldr, int gelu_poly, __bf16* __restrict__ C, int ldc) {
-  constexpr int MP = RM * 16;
-  __shared__ float red[3][MP][64 + 4];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int n0 = blockIdx.x * 64;
-  const int g = blockIdx.y * 4 + wave;            // this wave's 128-k granule
-  const int r = lane & 15, grp = lane >> 4;
-
-  f32x4 acc[RM][4];
-#pragma unroll
-  for (int i = 0; i < RM; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  if (g < KG) {
-    const size_t k0 = (size_t)g * 128 + grp * 32;
-    bf16x8 a[RM][4], b[4][4];
-#pragma unroll
-    for (int i = 0; i < RM; ++i) {
-      const __bf16* pa = A + (size_t)min(i * 16 + r, M - 1) * lda + k0;   // rows >= M: ignored
-#pragma unroll
-      for (int t = 0; t < 4; ++t) a[i][t] = *reinterpret_cast<const bf16x8*>(pa + 8 * t);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const __bf16* pb = W + (size_t)(n0 + j * 16 + r) * ldw + k0;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) b[j][t] = *reinterpret_cast<const bf16x8*>(pb + 8 * t);
-    }
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int i = 0; i < RM; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][t], b[j][t], acc[i][j], 0, 0, 0);
-  }
-
-  // accumulator (i, j)[e] sits at row i*16 + grp*4 + e, column j*16 + r of the 64-column block
-  if (wave > 0) {
-#pragma unroll
-    for (int i = 0; i < RM; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) red[wave - 1][i * 16 + grp * 4 + e][j * 16 + r] = acc[i][j][e];
-  }
-  __syncthreads();
-  if (wave == 0) {
-    float* Pb = P + (size_t)blockIdx.y * M * N + n0;
-#pragma unroll
-    for (int i = 0; i < RM; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = i * 16 + grp * 4 + e;
-        if (row >= M) continue;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int col = j * 16 + r;
-          float v = acc[i][j][e] + red[0][row][col] + red[1][row][col] + red[2][row][col];
-          if constexpr (EPI == SK_PARTIAL) {
-            Pb[(size_t)row * N + col] = v;
-          } else {
-            v += bias[n0 + col];
-            if constexpr (EPI == SK_GELU) {
-              if (gelu_poly) {
-                v = gelu2_poly(f32x2{v, v}).x;
-              } else {
-                v = gelu_erf(v);
-              }
-            }
-            if constexpr (EPI == SK_RES) v += (float)R[(size_t)row * ldr + n0 + col];
-            C[(size_t)row * ldc + n0 + col] = (__bf16)v;
-          }
-        }
-      }
-  }
-}
-
-// One wave per output row; lane owns 8 consecutive columns per PER-chunk (N <= PER * 512).
+// Sum the S split partials of one output row (fixed order: deterministic), add bias and apply the
+// epilogue; one wave per row, lane owns 8 consecutive columns per PER-chunk (N <= PER * 512).
 template <int EPI, int PER>
-__global__ __launch_bounds__(256) void skinny_epi_kernel(
+__device__ __forceinline__ void finish_row(
     const float* __restrict__ P, int S, const float* __restrict__ bias,
     const __bf16* __restrict__ R, int ldr, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, int gelu_poly, __bf16* __restrict__ C, int ldc,
-    int M, int N) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= M) return;
+    int M, int N, int row, int lane) {
   const int NV = N / 8;
   float x[PER][8];
   float s = 0.f;
@@ -207,12 +121,157 @@ __global__ __launch_bounds__(256) void skinny_epi_kernel(
   }
 }
 
+template <int EPI, int PER>
+__global__ __launch_bounds__(256) void skinny_epi_kernel(
+    const float* __restrict__ P, int S, const float* __restrict__ bias,
+    const __bf16* __restrict__ R, int ldr, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, int gelu_poly, __bf16* __restrict__ C, int ldc,
+    int M, int N) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  finish_row<EPI, PER>(P, S, bias, R, ldr, gamma, beta, eps, gelu_poly, C, ldc, M, N, row,
+                       threadIdx.x & 63);
+}
+
+// EPI = SK_PARTIAL: write the fp32 split partial; else (one split, K <= 512) apply bias / GELU /
+// residual here and store bf16 -- no second launch.
+constexpr int SK_PARTIAL = -1;
+
+// FIN != SK_PARTIAL (with EPI == SK_PARTIAL; small outputs, N <= 1024): the LAST workgroup to
+// finish (agent-scope release / acquire around one counter) sums every split and applies the FIN
+// epilogue itself -- no second launch; it re-arms the counter for the next GEMM on the stream.
+template <int RM, int EPI, int FIN>
+__global__ __launch_bounds__(256) void skinny_partial_kernel(
+    const __bf16* __restrict__ A, int lda, const __bf16* __restrict__ W, int ldw,
+    float* __restrict__ P, int M, int N, int KG, const float* __restrict__ bias,
+    const __bf16* __restrict__ R, int ldr, int gelu_poly, __bf16* __restrict__ C, int ldc,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+    int* __restrict__ counter) {
+  static_assert(FIN == SK_PARTIAL || EPI == SK_PARTIAL, "the finish needs split partials");
+  constexpr int MP = RM * 16, LS = 64 + 4;   // LDS row stride: 272 bytes (16-byte aligned)
+  extern __shared__ __attribute__((aligned(16))) float red[];   // [4 waves][MP rows][LS]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n0 = blockIdx.x * 64;
+  const int g = blockIdx.y * 4 + wave;            // this wave's 128-k granule
+  const int r = lane & 15, grp = lane >> 4;
+
+  f32x4 acc[RM][4];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (g < KG) {
+    const size_t k0 = (size_t)g * 128 + grp * 32;
+    bf16x8 a[RM][4], b[4][4];
+#pragma unroll
+    for (int i = 0; i < RM; ++i) {
+      const __bf16* pa = A + (size_t)min(i * 16 + r, M - 1) * lda + k0;   // rows >= M: ignored
+#pragma unroll
+      for (int t = 0; t < 4; ++t) a[i][t] = *reinterpret_cast<const bf16x8*>(pa + 8 * t);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const __bf16* pb = W + (size_t)(n0 + j * 16 + r) * ldw + k0;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) b[j][t] = *reinterpret_cast<const bf16x8*>(pb + 8 * t);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][t], b[j][t], acc[i][j], 0, 0, 0);
+  }
+
+  // accumulator (i, j)[e] sits at row i*16 + grp*4 + e, column j*16 + r of the 64-column block;
+  // all 4 waves park theirs in LDS, then every thread finishes 8 consecutive columns of a row
+  // (fixed wave order: deterministic) with 16-byte loads and stores
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[(wave * MP + i * 16 + grp * 4 + e) * LS + j * 16 + r] = acc[i][j][e];
+  __syncthreads();
+  for (int q = threadIdx.x; q < MP * 8; q += 256) {
+    const int row = q >> 3, c8 = (q & 7) * 8;
+    if (row >= M) break;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float* src = red + (w * MP + row) * LS + c8;
+      const f32x4 x0 = *reinterpret_cast<const f32x4*>(src);
+      const f32x4 x1 = *reinterpret_cast<const f32x4*>(src + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] += x0[e];
+        v[e + 4] += x1[e];
+      }
+    }
+    if constexpr (EPI == SK_PARTIAL) {
+      float* dst = P + ((size_t)blockIdx.y * M + row) * N + n0 + c8;
+      *reinterpret_cast<f32x4*>(dst) = f32x4{v[0], v[1], v[2], v[3]};
+      *reinterpret_cast<f32x4*>(dst + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    } else {
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(bias + n0 + c8);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(bias + n0 + c8 + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] += b0[e];
+        v[e + 4] += b1[e];
+      }
+      if constexpr (EPI == SK_GELU) {
+        if (gelu_poly) {
+#pragma unroll
+          for (int e = 0; e < 8; e += 2) {
+            const f32x2 y = gelu2_poly(f32x2{v[e], v[e + 1]});
+            v[e] = y.x;
+            v[e + 1] = y.y;
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
+        }
+      }
+      if constexpr (EPI == SK_RES) {
+        float rr[8];
+        load8(R + (size_t)row * ldr + n0 + c8, rr);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += rr[e];
+      }
+      store8(C + (size_t)row * ldc + n0 + c8, v);
+    }
+  }
+  if constexpr (FIN != SK_PARTIAL) {
+    __shared__ int s_last;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // this thread's partials, device-wide
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int prev = __hip_atomic_fetch_add(counter, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = prev == (int)(gridDim.x * gridDim.y) - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // every workgroup's partials
+    const int S = gridDim.y;
+    for (int row = wave; row < M; row += 4)
+      finish_row<FIN, 2>(P, S, bias, R, ldr, gamma, beta, eps, gelu_poly, C, ldc, M, N, row, lane);
+    if (threadIdx.x == 0) __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // fp32 split partials.  An encoder forward hands in its own buffer (part of its workspace, so a
 // captured hipGraph bakes a pointer that lives as long as the graph): symb_gemm_skinny_set_scratch,
 // thread-local, set for the duration of the forward.  Other callers get one fixed-size buffer
 // per stream (concurrent streams must not share one), allocated on first use and never moved;
 // a stream under capture that has none takes the tiled path instead (no allocation in a capture).
-constexpr size_t kStreamScratchBytes = (size_t)64 * 4096 * 8 * sizeof(float);  // M, N, splits max
+// Layout: a 256-byte header (the last-workgroup counter, zero between launches) + the partials.
+constexpr size_t kScratchHeader = 256;
+constexpr size_t kStreamScratchBytes = kScratchHeader + (size_t)64 * 4096 * 8 * sizeof(float);
 thread_local float* t_scratch = nullptr;
 thread_local size_t t_scratch_bytes = 0;
 std::mutex g_scratch_mu;
@@ -229,8 +288,28 @@ float* scratch_for(hipStream_t st, size_t bytes) {
     return nullptr;
   float* p = nullptr;
   if (hipMalloc(&p, kStreamScratchBytes) != hipSuccess) return nullptr;
+  if (hipMemset(p, 0, kScratchHeader) != hipSuccess) {
+    (void)hipFree(p);
+    return nullptr;
+  }
   g_scratch[st] = p;
   return p;
+}
+
+template <int RM, int EPI, int FIN>
+void launch_partial(dim3 grid, hipStream_t st, const __bf16* a, int lda, const __bf16* w, int ldw,
+                    float* P, int M, int N, int KG, const float* bias, const __bf16* r, int ldr,
+                    int gelu_poly, __bf16* c, int ldc, const float* g, const float* b, float eps,
+                    int* counter) {
+  constexpr int lds = 4 * RM * 16 * (64 + 4) * (int)sizeof(float);   // <= 68 KiB
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)skinny_partial_kernel<RM, EPI, FIN>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL((skinny_partial_kernel<RM, EPI, FIN>), grid, dim3(256), lds, st, a, lda, w,
+                     ldw, P, M, N, KG, bias, r, ldr, gelu_poly, c, ldc, g, b, eps, counter);
 }
 
 template <int EPI>
@@ -259,10 +338,11 @@ using namespace symb;
 
 // Largest M the skinny path takes (0 = off); symb_gemm consults it first.
 static int g_skinny_max_m = 64;
-// 1: a single-split bias / GELU / residual GEMM applies its epilogue in the split kernel
-static int g_skinny_fuse = 1;
+// bit 0: a single-split bias / GELU / residual GEMM applies its epilogue in the split kernel;
+// bit 1: a small multi-split / LayerNorm GEMM is finished by its last workgroup (no epi kernel)
+static int g_skinny_fuse = 3;
 int symb_gemm_skinny_config(int max_m, int fuse) {
-  if (max_m < 0 || max_m > 64 || fuse < 0 || fuse > 1) return -1;
+  if (max_m < 0 || max_m > 64 || fuse < 0 || fuse > 3) return -1;
   g_skinny_max_m = max_m;
   g_skinny_fuse = fuse;
   return 0;
@@ -284,7 +364,7 @@ bool symb_gemm_skinny_supported(int epi, int M, int N, int K) {
 size_t symb_gemm_skinny_scratch_bytes(int epi, int M, int N, int K) {
   if (!symb_gemm_skinny_supported(epi, M, N, K)) return 0;
   const int S = (K / 128 + 3) / 4;
-  return (size_t)S * M * N * sizeof(float);
+  return kScratchHeader + (size_t)S * M * N * sizeof(float);
 }
 // Returns 0, a HIP error code, or -1 (shape not supported: the caller takes its other paths).
 int symb_gemm_skinny(int epi, const void* A, int lda, const void* W, int ldw, const float* bias,
@@ -293,11 +373,17 @@ int symb_gemm_skinny(int epi, const void* A, int lda, const void* W, int ldw, co
   if (!symb_gemm_skinny_supported(epi, M, N, K)) return -1;
   const int KG = K / 128, S = (KG + 3) / 4;
   // one split and a row-local epilogue: finished in the one kernel
-  const int fused = (S == 1 && epi != SK_RES_LN && g_skinny_fuse) ? epi : SK_PARTIAL;
+  const int fused = (S == 1 && epi != SK_RES_LN && (g_skinny_fuse & 1)) ? epi : SK_PARTIAL;
+  // small outputs: the last workgroup sums the splits (one CU reads S x M x N floats)
+  const int fin = (fused == SK_PARTIAL && (g_skinny_fuse & 2) && N <= 1024 && M * N <= 16384)
+                      ? epi : SK_PARTIAL;
   float* P = nullptr;
+  int* counter = nullptr;
   if (fused == SK_PARTIAL) {
-    P = scratch_for(st, (size_t)S * M * N * sizeof(float));
-    if (!P) return -1;   // no buffer for this stream (capturing, or out of memory): tiled path
+    char* base = (char*)scratch_for(st, kScratchHeader + (size_t)S * M * N * sizeof(float));
+    if (!base) return -1;   // no buffer for this stream (capturing, or out of memory): tiled path
+    counter = (int*)base;
+    P = (float*)(base + kScratchHeader);
   }
   const dim3 grid(N / 64, S), block(256);
   auto a = (const __bf16*)A;
@@ -305,14 +391,22 @@ int symb_gemm_skinny(int epi, const void* A, int lda, const void* W, int ldw, co
   auto r = (const __bf16*)R;
   auto c = (__bf16*)C;
   const int rm = (M + 15) / 16;
-#define SK_P(RM_, E_) hipLaunchKernelGGL((skinny_partial_kernel<RM_, E_>), grid, block, 0, st, a, \
-                                         lda, w, ldw, P, M, N, KG, bias, r, ldr, gelu_poly, c, ldc)
-#define SK_PE(RM_)                         \
-  switch (fused) {                         \
-    case SK_BIAS: SK_P(RM_, SK_BIAS); break; \
-    case SK_GELU: SK_P(RM_, SK_GELU); break; \
-    case SK_RES: SK_P(RM_, SK_RES); break;   \
-    default: SK_P(RM_, SK_PARTIAL); break;   \
+#define SK_P(RM_, E_, F_)                                                                   \
+  launch_partial<RM_, E_, F_>(grid, st, a, lda, w, ldw, P, M, N, KG, bias, r, ldr, gelu_poly, c, \
+                              ldc, gamma, beta, eps, counter)
+#define SK_PE(RM_)                                                    \
+  switch (fused) {                                                    \
+    case SK_BIAS: SK_P(RM_, SK_BIAS, SK_PARTIAL); break;              \
+    case SK_GELU: SK_P(RM_, SK_GELU, SK_PARTIAL); break;              \
+    case SK_RES: SK_P(RM_, SK_RES, SK_PARTIAL); break;                \
+    default:                                                          \
+      switch (fin) {                                                  \
+        case SK_BIAS: SK_P(RM_, SK_PARTIAL, SK_BIAS); break;          \
+        case SK_GELU: SK_P(RM_, SK_PARTIAL, SK_GELU); break;          \
+        case SK_RES: SK_P(RM_, SK_PARTIAL, SK_RES); break;            \
+        case SK_RES_LN: SK_P(RM_, SK_PARTIAL, SK_RES_LN); break;      \
+        default: SK_P(RM_, SK_PARTIAL, SK_PARTIAL); break;            \
+      }                                                               \
   }
   if (rm == 1) {
     SK_PE(1)
@@ -324,7 +418,7 @@ int symb_gemm_skinny(int epi, const void* A, int lda, const void* W, int ldw, co
 #undef SK_PE
 #undef SK_P
   int rc = (int)hipGetLastError();
-  if (rc || fused != SK_PARTIAL) return rc;
+  if (rc || fused != SK_PARTIAL || fin != SK_PARTIAL) return rc;
   const int nv = N / 8;
   const int per = nv <= 64 ? 1 : nv <= 128 ? 2 : nv <= 256 ? 4 : 8;
   switch (epi) {
