@@ -519,7 +519,7 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("resln_bm") = 128, py::arg("tile") = 3, py::arg("group_m") = 8);
   m.def("gemm_skinny_config", [](int max_m, int fuse) {
     check(symb_gemm_skinny_config(max_m, fuse), "gemm_skinny_config");
-  }, py::arg("max_m") = 64, py::arg("fuse") = 3);
+  }, py::arg("max_m") = 64, py::arg("fuse") = 1);
   m.def("gemm_skinny_max_m", []() { return symb_gemm_skinny_max_m(); });
   m.def("gemm_resln_config", [](int waves) { check(symb_gemm_resln_config(waves), "gemm_resln_config"); },
         py::arg("waves") = 16);

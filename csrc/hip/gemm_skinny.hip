@@ -23,9 +23,9 @@
 //    order (deterministic), adds bias, and applies GELU / residual / residual + LayerNorm, with
 //    16-byte bf16 stores.  LayerNorm needs whole rows, which only exist after the split sum.
 //    With a single split (K <= 512: MiniLM's QKV and FFN1) and a row-local epilogue, the split
-//    kernel applies bias / GELU / residual itself; for small outputs (M x N <= 16384, N <= 1024:
-//    MiniLM's out-proj + LN and FFN2 + LN at M <= 42, bge's out-proj / FFN2 at M <= 21) the last
-//    workgroup to finish does the split sum and epilogue -- either way, no second launch.
+//    kernel applies bias / GELU / residual itself (no second launch).  An opt-in form lets the
+//    last workgroup to finish a small multi-split GEMM do the split sum and epilogue (measured
+//    slower; see g_skinny_fuse).
 #include <mutex>
 #include <unordered_map>
 
@@ -339,8 +339,11 @@ using namespace symb;
 // Largest M the skinny path takes (0 = off); symb_gemm consults it first.
 static int g_skinny_max_m = 64;
 // bit 0: a single-split bias / GELU / residual GEMM applies its epilogue in the split kernel;
-// bit 1: a small multi-split / LayerNorm GEMM is finished by its last workgroup (no epi kernel)
-static int g_skinny_fuse = 3;
+// bit 1 (opt-in): a small multi-split / LayerNorm GEMM is finished by its last workgroup instead
+// of the epilogue kernel.  Measured slower (profiles/r3_skinny: MiniLM out-proj/FFN2 + LN 12.7 us
+// vs 5.7 + 3.8 us for split + epilogue kernel): one workgroup walks the rows 4 at a time, each
+// row a dependent chain of partial loads, while the epilogue kernel spreads them over M waves.
+static int g_skinny_fuse = 1;
 int symb_gemm_skinny_config(int max_m, int fuse) {
   if (max_m < 0 || max_m > 64 || fuse < 0 || fuse > 3) return -1;
   g_skinny_max_m = max_m;

@@ -194,7 +194,7 @@ def test_gemm_skinny(M, N, K, epi):
     from codename_symbiont_amd.ops.kernels import gemm
 
     assert hip().gemm_skinny_max_m() == 64
-    a = _bf(M, K, seed=1)   # (M x N <= 16384, N <= 1024: the last-workgroup finish; else 2 kernels)
+    a = _bf(M, K, seed=1)   # (opt-in last-workgroup finish where M x N <= 16384, N <= 1024)
     w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=2)
     bias = _f(N, scale=0.5, seed=3)
     res = _bf(M, N, seed=4) if epi in (2, 3) else None
@@ -205,13 +205,13 @@ def test_gemm_skinny(M, N, K, epi):
     ref = R.gemm_ref(a, w, bias, epi, res, g, b, 1e-12)
     _close(out, ref, atol=4e-2, rtol=2e-2, what=f"skinny gemm epi={epi}")
     assert torch.equal(out, out2), "skinny gemm is not deterministic"
-    for fuse in (0, 1, 2):   # epilogues in the second kernel / the split kernel / the last workgroup
+    for fuse in (0, 2, 3):   # epilogues in the second kernel / the last workgroup (opt-in) / both
         hip().gemm_skinny_config(64, fuse)
         try:
             other = gemm(a, w, bias, epi, res, g, b, 1e-12)
             other2 = gemm(a, w, bias, epi, res, g, b, 1e-12)   # the last-workgroup counter re-armed
         finally:
-            hip().gemm_skinny_config(64, 3)
+            hip().gemm_skinny_config(64, 1)
         assert torch.equal(out, other) and torch.equal(out, other2), f"skinny epilogue form {fuse} differs"
     hip().gemm_skinny_config(0)
     try:
