@@ -224,7 +224,9 @@ class HipEncoder:
     # Measured (profiles/r1_gemm/latency.log, MiniLM-L6): eager 386 / 458 / 575 / 593 us vs graph
     # 475 / 577 / 656 / 766 us at B x S = 1x16, 1x64, 8x32, 32x48 -- these forwards are bound by
     # the small-M GEMMs' k-loop latency on the GPU, not by launches, and the bucket padding adds
-    # work, so replay is opt-in (set use_graphs = True) until a small-M GEMM path exists.
+    # work, so replay is opt-in (set use_graphs = True).  With the small-M split-K GEMMs
+    # (gemm_skinny.hip) eager forwards got faster and replay is still slower (MiniLM 1 x 16:
+    # 269 us replayed vs 252 us eager, profiles/r3_skinny/v2/lat.jsonl).
     GRAPH_MAX_TOKENS = 2048
     GRAPH_MAX_SEQS = 32
     use_graphs = False

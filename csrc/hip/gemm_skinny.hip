@@ -44,7 +44,7 @@ __device__ __forceinline__ void finish_row(
     const float* __restrict__ P, int S, const float* __restrict__ bias,
     const __bf16* __restrict__ R, int ldr, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, int gelu_poly, __bf16* __restrict__ C, int ldc,
-    int M, int N, int row, int lane) {
+    int M, int N, int ldp, int row, int lane) {
   const int NV = N / 8;
   float x[PER][8];
   float s = 0.f;
@@ -62,7 +62,7 @@ __device__ __forceinline__ void finish_row(
       x[p][e + 4] = b1[e];
     }
     for (int sp = 0; sp < S; ++sp) {   // fixed order: deterministic
-      const float* q = P + ((size_t)sp * M + row) * N + v * 8;
+      const float* q = P + ((size_t)sp * M + row) * ldp + v * 8;
       const f32x4 q0 = *reinterpret_cast<const f32x4*>(q);
       const f32x4 q1 = *reinterpret_cast<const f32x4*>(q + 4);
 #pragma unroll
@@ -129,7 +129,10 @@ __global__ __launch_bounds__(256) void skinny_epi_kernel(
     int M, int N) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
-  finish_row<EPI, PER>(P, S, bias, R, ldr, gamma, beta, eps, gelu_poly, C, ldc, M, N, row,
+  // row-local epilogues: blockIdx.y picks a PER * 512-column slice (more waves for wide N)
+  const int col0 = blockIdx.y * PER * 512;
+  finish_row<EPI, PER>(P + col0, S, bias + col0, R ? R + col0 : R, ldr, gamma, beta, eps,
+                       gelu_poly, C + col0, ldc, M, min(PER * 512, N - col0), N, row,
                        threadIdx.x & 63);
 }
 
@@ -259,7 +262,7 @@ __global__ __launch_bounds__(256) void skinny_partial_kernel(
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // every workgroup's partials
     const int S = gridDim.y;
     for (int row = wave; row < M; row += 4)
-      finish_row<FIN, 2>(P, S, bias, R, ldr, gamma, beta, eps, gelu_poly, C, ldc, M, N, row, lane);
+      finish_row<FIN, 2>(P, S, bias, R, ldr, gamma, beta, eps, gelu_poly, C, ldc, M, N, N, row, lane);
     if (threadIdx.x == 0) __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -316,7 +319,9 @@ template <int EPI>
 int launch_epi(int per, const float* P, int S, const float* bias, const __bf16* R, int ldr,
                const float* g, const float* b, float eps, int gelu_poly, __bf16* C, int ldc, int M,
                int N, hipStream_t st) {
-  const dim3 grid((M + 3) / 4), block(256);
+  // LayerNorm needs whole rows (PER * 512 >= N); the others take 512-column slices, one wave each
+  if (EPI != SK_RES_LN) per = 1;
+  const dim3 grid((M + 3) / 4, EPI == SK_RES_LN ? 1 : (N + 511) / 512), block(256);
 #define SK_E(PER_) hipLaunchKernelGGL((skinny_epi_kernel<EPI, PER_>), grid, block, 0, st, P, S, \
                                       bias, R, ldr, g, b, eps, gelu_poly, C, ldc, M, N)
   switch (per) {
