@@ -26,8 +26,9 @@
 //    kernel applies bias / GELU / residual itself (no second launch).  An opt-in form lets the
 //    last workgroup to finish a small multi-split GEMM do the split sum and epilogue (measured
 //    slower; see g_skinny_fuse).
+#include <map>
 #include <mutex>
-#include <unordered_map>
+#include <utility>
 
 #include "common.h"
 
@@ -278,13 +279,16 @@ constexpr size_t kStreamScratchBytes = kScratchHeader + (size_t)64 * 4096 * 8 * 
 thread_local float* t_scratch = nullptr;
 thread_local size_t t_scratch_bytes = 0;
 std::mutex g_scratch_mu;
-std::unordered_map<hipStream_t, float*> g_scratch;
+std::map<std::pair<int, hipStream_t>, float*> g_scratch;   // (device, stream): the null stream is per device
 
 float* scratch_for(hipStream_t st, size_t bytes) {
   if (t_scratch && t_scratch_bytes >= bytes) return t_scratch;
   if (bytes > kStreamScratchBytes) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  const auto key = std::make_pair(dev, st);
   std::lock_guard<std::mutex> lk(g_scratch_mu);
-  auto it = g_scratch.find(st);
+  auto it = g_scratch.find(key);
   if (it != g_scratch.end()) return it->second;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
@@ -295,7 +299,7 @@ float* scratch_for(hipStream_t st, size_t bytes) {
     (void)hipFree(p);
     return nullptr;
   }
-  g_scratch[st] = p;
+  g_scratch[key] = p;
   return p;
 }
 
