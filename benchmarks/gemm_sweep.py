@@ -3,8 +3,11 @@
 
     python benchmarks/gemm_sweep.py [--models bge-base,e5-large] [--variants t3,t9,lt,torch]
 
-Variants: tN = gemm.hip with symb_gemm_config tile mode N and the hipBLASLt route off;
-lt = the default tiles with the hipBLASLt route on; torch = torch.matmul (hipBLASLt, no epilogue).
+Variants: tN = symb_gemm with tile mode N (3 = auto: the deep-ring kernel for the wide shapes,
+10 = the round-3 auto rule without it, 2 = gemm.hip's 2-stage 256x256), hipBLASLt route off;
+dN = auto with the deep kernel's ring depth N (4 / 5); dNnosk = the same without last-wave
+split-K; lt = the hipBLASLt route for the plain projections (round-3 default);
+torch = torch.matmul (hipBLASLt, no epilogue).
 Operands are random (the clock the chip holds depends on the data).  One JSON line per
 (shape, variant): median / min us over the rounds and TFLOP/s at the median.
 """
@@ -32,7 +35,7 @@ SHAPES = {
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--models", default="bge-base,e5-large")
-    ap.add_argument("--variants", default="t3,t9,lt,torch")
+    ap.add_argument("--variants", default="d5,d4,d5nosk,t10,lt,torch")
     ap.add_argument("--m", type=int, default=32768)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
@@ -56,12 +59,12 @@ def main():
                 if v == "torch":
                     return lambda: torch.matmul(x, w.t(), out=y)
                 if v == "lt":
-                    return lambda: (hip().gemm_config(128, 3, 8), hip().gemm_lt_config(1),
-                                    K.gemm(x, w, b, epi, r, out=y))
-                if v.startswith("w4"):   # gemm4w.hip (w4 = auto rows per tile, w4_192 / w4_256)
-                    bm = int(v[3:]) if "_" in v else 0
-                    return lambda: (hip().gemm4w_config(3, bm), hip().gemm_lt_config(0),
-                                    K.gemm(x, w, b, epi, r, out=y), hip().gemm4w_config(0, 0))
+                    return lambda: (hip().gemm_config(128, 10, 8), hip().gemm_lt_config(1),
+                                    K.gemm(x, w, b, epi, r, out=y), hip().gemm_lt_config(0))
+                if v.startswith("d"):
+                    ns, sk = int(v[1]), 0 if v.endswith("nosk") else 1
+                    return lambda: (hip().gemm_config(128, 3, 8), hip().gemm_deep_config(ns, sk),
+                                    K.gemm(x, w, b, epi, r, out=y), hip().gemm_deep_config(5, 1))
                 t = int(v[1:])
                 return lambda: (hip().gemm_config(128, t, 8), hip().gemm_lt_config(0),
                                 K.gemm(x, w, b, epi, r, out=y))
@@ -88,7 +91,7 @@ def main():
                                   "variant": v, "us_med": round(med, 1), "us_min": round(min(ts), 1),
                                   "TFLOPs": round(2 * a.m * n * k / med / 1e6)}), flush=True)
     hip().gemm_config(128, 3, 8)
-    hip().gemm_lt_config(1)
+    hip().gemm_lt_config(0)
 
 
 if __name__ == "__main__":

@@ -451,16 +451,16 @@ def cmd_encoder(a):
                 name = p + ("" if len(tiles) == 1 else f"_tile{t}") + ("" if len(fw) == 1 else f"_w{w}")
                 # w = 256 / 257: 8-wave fp8 tiles plus the 256x256 fp8 tile wherever the bf16
                 # rule takes it / where the fp8 auto rule does (the default); else no 256x256
-                # t = 12: the default tiles with hipBLASLt for the plain K, N >= 768 projections
-                # (the default); other t: gemm.hip's tiles everywhere
-                var[name] = (lambda e=e, t=t, w=w: (_hip().gemm_config(128, 3 if t == 12 else t, 8),
+                # t = 12: the round-3 default (tile rule 10 + hipBLASLt for the plain K, N >= 768
+                # projections); other t: symb_gemm_config tile modes (3 = auto, the default)
+                var[name] = (lambda e=e, t=t, w=w: (_hip().gemm_config(128, 10 if t == 12 else t, 8),
                                                     _hip().gemm_lt_config(1 if t == 12 else 0),
                                                     _hip().gemm_fp8_config(8 if w >= 256 else w,
                                                                            {256: 1, 257: 2}.get(w, 0)),
                                                     e.forward_packed(b, o1, o2)))
     res = ab(var, rounds=a.rounds, iters=a.iters)
     _hip().gemm_config(128, 3, 8)
-    _hip().gemm_lt_config(1)
+    _hip().gemm_lt_config(0)
     _hip().gemm_fp8_config(8)
     toks = a.batch * a.seq
     fl = cfg.flops_per_token(a.seq) * toks
@@ -620,8 +620,8 @@ def main():
     ap.add_argument("--model", default="minilm-l6")
     ap.add_argument("--seed", type=int, default=1, help="scanabl: seed per-query thresholds")
     ap.add_argument("--precision", default="bf16", help="encoder: comma list of bf16,fp8")
-    ap.add_argument("--tiles", default="12", help="encoder: comma list of gemm_config tile modes "
-                    "(12 = the default: auto tiles + the hipBLASLt route; 3 = auto tiles only)")
+    ap.add_argument("--tiles", default="3", help="encoder: comma list of gemm_config tile modes "
+                    "(3 = the default auto tiles, 10 = round-3 auto, 12 = round-3 default with hipBLASLt)")
     ap.add_argument("--fp8-waves", default="8", help="encoder: comma list of fp8 GEMM wave counts")
     ap.add_argument("--sets", type=int, default=4, help="scanmqabl: 16-query sets per wave (2 or 4)")
     ap.add_argument("--rsplit", type=int, default=1, help="scanmqabl: waves per query group (1, 2)")

@@ -22,9 +22,15 @@ so a shard of N rows is O(log N) files and every row is rewritten O(log N) times
 many patched rows trigger one full rewrite.  Boot applies the files in generation order (a later
 segment, patch or delta wins), so a merged segment supersedes the patches written before it.
 
-The cut (``ShardPersister.cut``) runs under the caller's lock: it copies the new / merged rows
-(D2H) and the payload delta to host memory and notes the WAL rotation; ``SnapshotJob.write``
-then writes, fsyncs and commits from a background thread while upserts continue.  A crash at any
+The cut (``ShardPersister.cut``) runs under the caller's lock and captures only what is not on
+disk yet: the rows appended since the last cut, the older rows overwritten since (D2H) and the
+payload delta, plus the WAL rotation.  ``SnapshotJob.write`` then writes, fsyncs and commits from
+a background thread while upserts continue; a merged segment is STREAMED there from the older
+segment files (memory-mapped), their patches, the captured overwrites and the captured new rows
+into an ``open_memmap`` output, a chunk at a time -- host memory never holds a whole segment.  A
+snapshot with no committed base (the first one, or a shard from elsewhere) streams the shard D2H
+in chunks straight into its segment file under the lock when it is larger than FULL_CAPTURE_MAX
+bytes, else captures it in host memory and writes in the background.  A crash at any
 point leaves the previous committed manifest and every WAL file it does not cover, so boot =
 committed manifest -> HBM, then replay of the uncovered WAL files in order.
 
@@ -332,8 +338,78 @@ def _save_npy(path: str, a: np.ndarray) -> None:
         os.fsync(f.fileno())
 
 
+def _rows_to_file(shard: HbmIndexShard, r0: int, r1: int, path: str, chunk: int = 1 << 20) -> int:
+    """Rows [r0, r1) straight into the .npy ``path`` (chunked D2H, fsync'd); returns its bytes."""
+    fp8 = shard.dtype == "fp8"
+    out = np.lib.format.open_memmap(path, mode="w+", dtype=np.uint8 if fp8 else np.uint16,
+                                    shape=(r1 - r0, shard.dim))
+    for s in range(r0, r1, chunk):
+        e = min(r1, s + chunk)
+        t = shard.rows[s:e]
+        t = t if fp8 else t.view(torch.int16)
+        out[s - r0:e - r0] = t.cpu().numpy().view(out.dtype)
+    out.flush()
+    nbytes = out.nbytes
+    del out
+    fsync_file(path)
+    return nbytes
+
+
+class SegMerge:
+    """A merged segment [row0, n) to stream at write time: the older segments ``sources`` (gen,
+    row0, n) covering [row0, p0) read from their files, every older patch (gen, file) applied in
+    generation order to the rows of segments older than it, then the overwrites captured at the
+    cut (``dirty`` rows / vecs inside [row0, p0)), then the captured new rows [p0, n)."""
+
+    def __init__(self, directory: str, dim: int, dtype, row0: int, p0: int, n: int, sources,
+                 patches, dirty, new_rows):
+        self.directory, self.dim, self.dtype = directory, dim, dtype
+        self.row0, self.p0, self.n = row0, p0, n
+        self.sources, self.patches, self.dirty, self.new_rows = sources, patches, dirty, new_rows
+
+    def write(self, path: str, chunk: int = 1 << 20) -> int:
+        d, row0 = self.directory, self.row0
+        out = np.lib.format.open_memmap(path, mode="w+", dtype=self.dtype,
+                                        shape=(self.n - row0, self.dim))
+        seg_gen = []   # (start, end, gen) of every source segment
+        for gen, s0, m in self.sources:
+            src = np.load(os.path.join(d, f"seg.{gen}.npy"), mmap_mode="r")
+            for a in range(0, m, chunk):
+                b = min(m, a + chunk)
+                out[s0 - row0 + a:s0 - row0 + b] = src[a:b]
+            del src
+            seg_gen.append((s0, s0 + m, gen))
+        starts = np.asarray([x[0] for x in seg_gen], np.int64)
+        gens = np.asarray([x[2] for x in seg_gen], np.int64)
+        for pg in sorted(self.patches):
+            rows = np.load(os.path.join(d, f"patch.{pg}.rows.npy"), mmap_mode="r")
+            vecs = np.load(os.path.join(d, f"patch.{pg}.vecs.npy"), mmap_mode="r")
+            for a in range(0, rows.shape[0], chunk):
+                r = np.asarray(rows[a:a + chunk])
+                keep = (r >= row0) & (r < self.p0)
+                if not keep.any():
+                    continue
+                # a patch overrides only segments older than itself
+                owner = gens[np.searchsorted(starts, r[keep], side="right") - 1]
+                sel = np.flatnonzero(keep)[owner < pg]
+                if sel.size:
+                    out[r[sel] - row0] = np.asarray(vecs[a:a + chunk])[sel]
+            del rows, vecs
+        if self.dirty is not None:
+            rows, vecs = self.dirty
+            out[rows - row0] = vecs
+        if self.new_rows is not None:
+            out[self.p0 - row0:] = self.new_rows
+        out.flush()
+        nbytes = out.nbytes
+        del out
+        fsync_file(path)
+        return nbytes
+
+
 class SnapshotJob:
-    """Everything one generation writes, captured in host memory at the cut."""
+    """Everything one generation writes: captured in host memory at the cut, a ``SegMerge`` to
+    stream from the older files, or a segment file the cut already wrote (``seg_file``)."""
 
     def __init__(self, directory: str, gen: int, manifest: dict, seg, patch, pay, pay_merge,
                  cleanup_wal_upto: int | None):
@@ -346,8 +422,14 @@ class SnapshotJob:
         d, g = self.directory, self.gen
         if self.seg is not None:
             p = os.path.join(d, f"seg.{g}.npy")
-            _save_npy(p, self.seg)
-            self.bytes_written += self.seg.nbytes
+            if isinstance(self.seg, SegMerge):
+                self.bytes_written += self.seg.write(p)
+            elif isinstance(self.seg, str):      # written (and fsync'd) by the cut
+                os.replace(self.seg, p)
+                self.bytes_written += os.path.getsize(p)
+            else:
+                _save_npy(p, self.seg)
+                self.bytes_written += self.seg.nbytes
         if self.patch is not None:
             rows, vecs = self.patch
             _save_npy(os.path.join(d, f"patch.{g}.rows.npy"), rows)
@@ -443,6 +525,9 @@ class ShardPersister:
 
     MAX_PATCH_FRAC = 0.25     # patched rows above this share of the shard: full rewrite
     MAX_PATCH_FILES = 32
+    # a base snapshot (no committed generation to build on) larger than this streams the rows
+    # into its segment file under the lock instead of capturing them in host memory
+    FULL_CAPTURE_MAX = 1 << 30
 
     def __init__(self, directory: str):
         self.directory = directory
@@ -471,26 +556,51 @@ class ShardPersister:
         pays = [dict(p) for p in man["payloads"]] if incremental else []
         p0 = shard._persisted if incremental else 0
         dirty = sorted(r for r in shard._dirty if r < p0) if incremental else []
-        if incremental and (len(dirty) + sum(p["m"] for p in patches) > self.MAX_PATCH_FRAC * max(n, 1)
-                            or len(patches) >= self.MAX_PATCH_FILES):
-            return self.cut(shard, rotate_wal, full=True)
-        # new segment = rows [p0, n), merged geometrically with its predecessors
+        # too many patched rows or patch files: one segment rewritten from disk (row0 = 0)
+        rewrite = incremental and (
+            len(dirty) + sum(p["m"] for p in patches) > self.MAX_PATCH_FRAC * max(n, 1)
+            or len(patches) >= self.MAX_PATCH_FILES)
+        # new segment = rows [p0, n), merged geometrically with its predecessors; a rewrite for
+        # too many patches merges every segment (row0 = 0) the same way, from disk
         row0 = p0
-        while segs and n - row0 > 0 and 2 * (n - row0) >= segs[-1]["n"]:
-            row0 = segs.pop()["row0"]
-        seg = _rows_to_host(shard, row0, n) if n > row0 else None
-        if seg is not None:
+        popped = []
+        while segs and n - row0 > 0 and (rewrite or 2 * (n - row0) >= segs[-1]["n"]):
+            popped.insert(0, segs.pop())
+            row0 = popped[0]["row0"]
+        fp8 = shard.dtype == "fp8"
+        host_dt = np.uint8 if fp8 else np.uint16
+
+        def capture(rows_list):
+            rows = np.asarray(rows_list, np.int64)
+            v = shard.rows.index_select(0, torch.from_numpy(rows).to(shard.device))
+            v = v if fp8 else v.view(torch.int16)
+            return rows, v.cpu().numpy().view(host_dt)
+
+        seg = None
+        if n > row0:
+            if incremental:
+                # only what is not on disk: the new rows and the overwrites inside the merged range
+                in_seg = [r for r in dirty if r >= row0]
+                seg = SegMerge(d, shard.dim, host_dt, row0, p0, n,
+                               [(x["gen"], x["row0"], x["n"]) for x in popped],
+                               [x["gen"] for x in patches] if popped else [],
+                               capture(in_seg) if in_seg else None,
+                               _rows_to_host(shard, p0, n) if n > p0 else None)
+            elif (n - row0) * shard.dim * (1 if fp8 else 2) > self.FULL_CAPTURE_MAX:
+                # no committed base: stream the shard into the segment file now (under the lock)
+                tmp = os.path.join(d, f"seg.{gen}.npy.tmp")
+                _rows_to_file(shard, row0, n, tmp)
+                seg = tmp
+            else:
+                seg = _rows_to_host(shard, row0, n)
             segs.append({"gen": gen, "row0": row0, "n": n - row0})
             # patches wholly inside the rewritten range are superseded by it
             patches = [p for p in patches if p["min_row"] < row0]
         patch = None
         dirty = [r for r in dirty if r < row0]
         if dirty:
-            rows = np.asarray(dirty, np.int64)
-            idx = torch.from_numpy(rows).to(shard.device)
-            v = shard.rows.index_select(0, idx)
-            v = v if shard.dtype == "fp8" else v.view(torch.int16)
-            patch = (rows, v.cpu().numpy().view(np.uint8 if shard.dtype == "fp8" else np.uint16))
+            rows, vecs = capture(dirty)
+            patch = (rows, vecs)
             patches.append({"gen": gen, "m": len(dirty), "min_row": int(rows.min())})
         # payload delta: every row whose point / payload changed since the last cut (all rows
         # on a full snapshot), merged geometrically with the previous deltas

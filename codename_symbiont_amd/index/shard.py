@@ -422,14 +422,16 @@ class HbmIndexShard:
         if self.device.type != "cuda" or k > self.K_MAX_HIP:
             return self._search_matmul(q_unit, k)
         q_unit = q_unit.to(torch.bfloat16).contiguous()
-        if k > 16 and not self.prefilter:
+        if self.prefilter and k < 32:
+            return self._search_prefilter(q_unit, k, n_cus)
+        if k > 16:
+            # exact over the bf16 rows (a prefilter shard keeps them too): the large-k emitting
+            # scan, else the list scan up to its kmax = 32, else the chunked GEMM
             out = self._search_large_k(q_unit, k, n_cus)
             if out is not None:
                 return out
             if k > 32:
                 return self._search_matmul(q_unit, k)
-        if self.prefilter and k < 32:
-            return self._search_prefilter(q_unit, k, n_cus)
         if self.prune and k <= 16 and NQ >= self.prune_min_nq and self._seed_rows(self.visible, k):
             out = self._search_pruned(q_unit, k, n_cus)
             if out is not None:
@@ -889,9 +891,12 @@ class HbmIndexShard:
         tail_s = torch.topk(ts_, kk, dim=1).values
         T = torch.topk(torch.cat([pre_s, tail_s], 1), k, dim=1).values[:, k - 1]
         T = (T - self.MQ_THR_MARGIN).contiguous()
-        out_s, out_i = self._scan_mq(n, q_unit, 128, k, T, n_cus, fallback=False,
-                                     cap=self.LARGE_K_CAP)
-        _, ovf = self._mq_last
+        # this search's own overflow flag (self._mq_last is shared by concurrent searches)
+        ovf = torch.empty(1, dtype=torch.int32, device=self.device)
+        out_s = torch.empty(NQ, k, device=self.device)
+        out_i = torch.empty(NQ, k, dtype=torch.int32, device=self.device)
+        self._scan_mq(n, q_unit, 128, k, T, n_cus, fallback=False, cap=self.LARGE_K_CAP,
+                      out=(out_s, out_i, ovf))
         if int(ovf.item()):
             return self._search_matmul(q_unit, k)
         return out_s, out_i

@@ -28,6 +28,39 @@ class DimensionError(ValueError):
 
 from ..ops._ext import native as _native  # noqa: E402
 
+class _RWLock:
+    """Many readers (searches enqueuing their two halves) or one writer (an upsert enqueuing its
+    row writes).  Held only while kernels are ENQUEUED, never across a device sync."""
+
+    def __init__(self):
+        self._cv = threading.Condition()
+        self._readers = 0
+        self._writer = False
+
+    def acquire_read(self):
+        with self._cv:
+            while self._writer:
+                self._cv.wait()
+            self._readers += 1
+
+    def release_read(self):
+        with self._cv:
+            self._readers -= 1
+            if self._readers == 0:
+                self._cv.notify_all()
+
+    def acquire_write(self):
+        with self._cv:
+            while self._writer or self._readers:
+                self._cv.wait()
+            self._writer = True
+
+    def release_write(self):
+        with self._cv:
+            self._writer = False
+            self._cv.notify_all()
+
+
 class VectorStore:
     def __init__(self, dim: int, capacity: int, device=None, snapshot_dir: str = "",
                  snapshot_every: int = 100_000, group=None, dtype: str = "bf16",
@@ -53,6 +86,11 @@ class VectorStore:
         if (group is None and self.shard.device.type == "cuda"
                 and os.environ.get("SYMB_SEARCH_PIPELINE", "1") not in ("", "0")):
             self._streams = (torch.cuda.Stream(self.shard.device), torch.cuda.Stream(self.shard.device))
+        # a pipelined search enqueues its pre-pass (begin) and its scan (end) under the read
+        # side, an upsert its row writes under the write side: no write can land between one
+        # search's begin and end (the scan would see rows, int8 images and bounds the pre-pass's
+        # thresholds never saw), and every write is ordered after both halves (wait_stream)
+        self._rw = _RWLock()
         self.wal = None
         self._bg: threading.Thread | None = None   # background snapshot writer
         self.snapshot_error: BaseException | None = None
@@ -87,9 +125,17 @@ class VectorStore:
     def _upsert_nolog(self, point_ids, vecs, payloads):
         t = torch.as_tensor(np.ascontiguousarray(vecs, dtype=np.float32))
         if self._streams is not None:
-            # in-place overwrites must not land under a pipelined search's scan of those rows
-            torch.cuda.current_stream(self.shard.device).wait_stream(self._streams[1])
-        if self.group is not None:
+            self._rw.acquire_write()
+            try:
+                # in-place overwrites (rows, int8 image, bounds) must not land under a pipelined
+                # search's pre-pass or scan of those rows: order them after both streams' work
+                cur = torch.cuda.current_stream(self.shard.device)
+                cur.wait_stream(self._streams[0])
+                cur.wait_stream(self._streams[1])
+                out = self.shard.upsert(point_ids, t, payloads)
+            finally:
+                self._rw.release_write()
+        elif self.group is not None:
             out = self.group.upsert(point_ids, t, payloads)
         else:
             out = self.shard.upsert(point_ids, t, payloads)
@@ -207,17 +253,24 @@ class VectorStore:
         concurrent callers overlap one's pre-pass with the other's scan."""
         pre, scan = self._streams
         dev = self.shard.device
-        pre.wait_stream(torch.cuda.default_stream(dev))
-        with torch.cuda.stream(pre):
-            qt = torch.nn.functional.normalize(torch.from_numpy(q).to(dev, non_blocking=False),
-                                               dim=-1).to(torch.bfloat16)
-            ctx = self.shard.search_begin(qt, k)
-            done = torch.cuda.Event()
-            done.record(pre)
-        scan.wait_event(done)
-        with torch.cuda.stream(scan):
-            s, r = self.shard.search_end(ctx)
-            return s.float().cpu().numpy(), r.long().cpu().numpy()
+        qh = torch.from_numpy(q).to(dev, non_blocking=False)   # (before the lock: a host copy)
+        self._rw.acquire_read()
+        try:
+            pre.wait_stream(torch.cuda.default_stream(dev))
+            with torch.cuda.stream(pre):
+                qt = torch.nn.functional.normalize(qh, dim=-1).to(torch.bfloat16)
+                ctx = self.shard.search_begin(qt, k)
+                done = torch.cuda.Event()
+                done.record(pre)
+            scan.wait_event(done)
+            with torch.cuda.stream(scan):
+                s, r = self.shard.search_end(ctx)
+                ev = torch.cuda.Event()
+                ev.record(scan)
+        finally:
+            self._rw.release_read()
+        ev.synchronize()
+        return s.float().cpu().numpy(), r.long().cpu().numpy()
 
     def lookup(self, gid: int):
         if self.group is not None:

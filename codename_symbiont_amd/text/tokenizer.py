@@ -210,8 +210,9 @@ def build_normalizer(spec):
     if t == "Lowercase":
         return str.lower
     if t == "StripAccents":
-        return lambda text: "".join(c for c in unicodedata.normalize("NFD", text)
-                                    if unicodedata.category(c) != "Mn")
+        # the crate only FILTERS marks (general category Mn / Mc / Me) and leaves decomposition
+        # to an explicit NFD step before it: a precomposed "é" or a Hangul syllable passes as is
+        return lambda text: "".join(c for c in text if unicodedata.category(c)[0] != "M")
     if t == "Prepend":
         pre = spec["prepend"]
         return lambda text: pre + text if text else text

@@ -409,11 +409,7 @@ static int launch_cfg(const void* A, int lda, const void* W, int ldw, const floa
   constexpr int full_epi = BM * (BN + 4) * 4;
   constexpr int epi_bytes = full_epi > 160 * 1024 ? (BM / WM) * (BN + 4) * 4 : full_epi;
   constexpr int lds = main_bytes > epi_bytes ? main_bytes : epi_bytes;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    attr_set = true;
-  }
+  set_max_lds<gemm_bf16_kernel<BM, BN, WM, WN, EPI, NSTAGE, F8, AMX>>(lds);
   const int nwg = ((M + BM - 1) / BM) * (N / BN);
   hipLaunchKernelGGL(kern, dim3(nwg), dim3(64 * WM * WN), lds, st, A, lda, W, ldw, bias, R, ldr,
                      g, b, eps, C, ldc, M, N, K, sa, sw, g_group_m, ascale, cscale);
@@ -424,40 +420,38 @@ static int launch_cfg(const void* A, int lda, const void* W, int ldw, const floa
 
 using namespace symb;
 
-// 256x256 8-phase kernel (gemm256.hip)
-bool symb_gemm256_supported(int M, int N, int K);
-int symb_gemm256(int epi, const void* A, int lda, const void* W, int ldw, const float* bias,
-                 const void* R, int ldr, void* C, int ldc, int M, int N, int K, int group_m,
-                 hipStream_t st);
+// Deep-ring 256x256 kernel with last-wave split-K (gemm_deep.hip): the wide projections.
+bool symb_gemm_deep_supported(int M, int N, int K);
+int symb_gemm_deep(int epi, const void* A, int lda, const void* W, int ldw, const float* bias,
+                   const void* R, int ldr, void* C, int ldc, int M, int N, int K, int group_m,
+                   int gelu_poly, hipStream_t st);
 
 // Tile height of the row-complete RES_LN GEMM (64 or 128); a tuning knob, see symb_gemm_config.
 static int g_resln_bm = 128;
-// Tile of the bias / GELU / residual GEMMs: 0 = 128x128 (4 waves, 2-stage ring),
-// 1 = 256x128 (8 waves, 3-stage ring with a tile in flight across each barrier),
-// 2 = 256x256 (8 waves of 128x64, 2-stage ring, one workgroup per CU) whenever N % 256 == 0,
-// 3 = auto: 256x256 when N % 256 == 0, K >= 768 and the grid fills whole waves of the 256 CUs
-//     (or is long enough that a partial last wave costs little), else 128x128 with 8 waves of 64x32
-//     (4 waves per SIMD at 2 workgroups per CU: +3-8 % over 4 waves of 64x64,
-//     profiles/r1_s4/gemm_8wave.json); grids smaller than the 256 CUs take a 4-deep ring;
-// 4 / 5 = 128x128 with a 3- / 4-deep ring at one workgroup per CU (A/B knobs);
-// 6 / 7 = 128x128 with 8 waves of 32x64 / 64x32; 8 = 128x128 with 16 waves of 32x32;
-// 9 = the 256x256 8-phase kernel (gemm256.hip) wherever it applies (N % 256, K % 128): faster
-//     in isolation (+3-8 % at K >= 768 with >= 3 tiles per CU) but not inside the encoders
-//     (bge-base 7.93 vs 7.73 ms, e5-large 23.09 vs 22.86 ms; profiles/r2_gemm), so opt-in;
-// 10 = same as 3 (kept for the A/B scripts).
+// Tile of the bias / GELU / residual GEMMs (one path per shape class under the default 3):
+// 3 = auto: gemm_deep.hip's 256x256 deep-ring tile (last-wave split-K) when N % 256 == 0,
+//     K >= 512 and the grid holds at least half a wave of 256 tiles; else 128x128 with 8 waves of
+//     64x32 (4 waves per SIMD at 2 workgroups per CU), a 4-deep ring when the grid is smaller than
+//     the 256 CUs (small M: each tile's serial k-loop is the latency);
+// 0 = 128x128 with 4 waves, 2-stage ring (A/B baseline);
+// 2 = this file's 2-stage 256x256 tile wherever N % 256 == 0 (the round-3 big tile, A/B);
+// 10 = auto without the deep kernel (the round-3 auto rule, A/B).
 static int g_tile = 3;
+static bool use_deep(int M, int N, int K) {
+  if (!symb_gemm_deep_supported(M, N, K) || K < 512) return false;
+  return ((M + 255) / 256) * (N / 256) >= 128;
+}
 static bool use_big_tile(int tile, int M, int N, int K) {
-  if (N % 256 != 0 || (tile != 2 && tile != 3)) return false;
+  if (N % 256 != 0 || (tile != 2 && tile != 10)) return false;
   if (tile == 2) return true;
   // short K (MiniLM's 384): the 256x256 tile's fill and epilogue outweigh its operand reuse
-  // (FFN1 32768x1536x384: 546 vs 585 TFLOP/s for the 8-wave 128x128 tile)
   if (K < 768) return false;
   const int tiles = ((M + 255) / 256) * (N / 256);
   return tiles % 256 == 0 || tiles >= 4 * 256;
 }
 int symb_gemm_config(int resln_bm, int tile, int group_m) {
   if (resln_bm != 64 && resln_bm != 128) return -1;
-  if (tile < 0 || tile > 10) return -1;
+  if (tile != 0 && tile != 2 && tile != 3 && tile != 10) return -1;
   if (group_m < 0 || group_m > 64) return -1;
   g_resln_bm = resln_bm;
   g_tile = tile;
@@ -485,36 +479,12 @@ int symb_gemm_fp8_config(int waves, int big) {
   return 0;
 }
 
-// 4-wave persistent 256x256 kernel (gemm4w.hip): 0 = never, 1 = the plain bias / residual
-// projections of the wide shapes (K >= 768, N >= 768, M >= 4096 -- the ones the hipBLASLt route
-// below would take; this kernel then goes first), 2 = those plus the GELU FFN1 of the same
-// shapes, 3 = every shape it supports (N % 256, K % 64).  g_gemm4w_bm: rows per tile, 256 / 192
-// (0 = auto: the one whose last partial wave of tiles costs least).
-bool symb_gemm4w_supported(int M, int N, int K);
-int symb_gemm4w(int epi, int bm, const void* A, int lda, const void* W, int ldw, const float* bias,
-                const void* R, int ldr, void* C, int ldc, int M, int N, int K, int group_m,
-                int gelu_poly, hipStream_t st);
-static int g_gemm4w = 0, g_gemm4w_bm = 0;
-int symb_gemm4w_config(int mode, int bm) {
-  if (mode < 0 || mode > 3 || (bm != 0 && bm != 256 && bm != 192)) return -1;
-  g_gemm4w = mode;
-  g_gemm4w_bm = bm;
-  return 0;
-}
-static int gemm4w_bm(int M, int N) {
-  if (g_gemm4w_bm) return g_gemm4w_bm;
-  // time ~ (waves of tiles over 256 CUs) x (rows per tile)
-  const long w256 = ((((M + 255) / 256) * (N / 256)) + 255) / 256;
-  const long w192 = ((((M + 191) / 192) * (N / 256)) + 255) / 256;
-  return w192 * 192 < w256 * 256 ? 192 : 256;
-}
-
-// hipBLASLt for the plain bias / bias + residual projections (gemm_lt.cpp): 0 = never, 1 = auto
-// (K >= 768 and N >= 768 and M >= 4096: the bge-base / e5-large shapes, where the library's
-// kernels are faster; MiniLM's K = 384 projections stay here), 2 = every bias / residual GEMM.
+// hipBLASLt for the plain bias / bias + residual projections (gemm_lt.cpp), kept as the vendor
+// baseline for A/B runs: 0 = never (default: every projection on this repo's kernels), 1 = the
+// wide shapes (K >= 768, N >= 768, M >= 4096), 2 = every bias / residual GEMM.
 int symb_gemm_lt(int epi, const void* A, int lda, const void* W, int ldw, const float* bias,
                  const void* R, int ldr, void* C, int ldc, int M, int N, int K, hipStream_t st);
-static int g_gemm_lt = 1;
+static int g_gemm_lt = 0;
 int symb_gemm_lt_config(int mode) {
   if (mode < 0 || mode > 2) return -1;
   g_gemm_lt = mode;
@@ -557,23 +527,17 @@ int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const flo
     return -1;  // wider rows: EPI_RES + symb_add_ln
   }
   if (N % 128 != 0) return -1;
-  if (g_gemm4w && symb_gemm4w_supported(M, N, K)) {
-    const bool wide = K >= 768 && N >= 768 && M >= 4096;
-    const bool take = g_gemm4w == 3 || (wide && (epi == EPI_BIAS || epi == EPI_RES)) ||
-                      (wide && g_gemm4w == 2 && epi == EPI_GELU);
-    if (take)
-      return symb_gemm4w(epi, gemm4w_bm(M, N), A, lda, W, ldw, bias, R, ldr, C, ldc, M, N, K,
-                         g_group_m, g_gelu_poly, st);
-  }
   if ((epi == EPI_BIAS || epi == EPI_RES) &&
       (g_gemm_lt == 2 || (g_gemm_lt == 1 && K >= 768 && N >= 768 && M >= 4096))) {
     const int rc = symb_gemm_lt(epi, A, lda, W, ldw, bias, R, ldr, C, ldc, M, N, K, st);
     if (rc != -1 && rc != -2) return rc;   // 0, or a HIP error; else this file's kernels
   }
-  if (g_tile == 9 && symb_gemm256_supported(M, N, K))
-    return symb_gemm256(epi, A, lda, W, ldw, bias, R, ldr, C, ldc, M, N, K, g_group_m, st);
-  const int tile_mode = g_tile == 10 ? 3 : g_tile;   // 10: auto without the 8-phase kernel (A/B)
-  if (use_big_tile(tile_mode, M, N, K)) {
+  if (g_tile == 3 && use_deep(M, N, K)) {
+    const int rc = symb_gemm_deep(epi == EPI_GELU ? 1 : epi == EPI_RES ? 2 : 0, A, lda, W, ldw,
+                                  bias, R, ldr, C, ldc, M, N, K, g_group_m, g_gelu_poly, st);
+    if (rc != -1) return rc;
+  }
+  if (use_big_tile(g_tile, M, N, K)) {
 #define SYMB_G(E) launch_cfg<256, 256, 2, 4, E>(a, lda, w, ldw, bias, r, ldr, gamma, beta, eps, c, \
                                                ldc, M, N, K, st)
     switch (epi) {
@@ -584,19 +548,7 @@ int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const flo
 #undef SYMB_G
     return -1;
   }
-  if (tile_mode == 8) {
-    // 128x128 with 16 waves of 32x32 (A/B knob)
-#define SYMB_G(E) launch_cfg<128, 128, 4, 4, E>(a, lda, w, ldw, bias, r, ldr, gamma, beta, eps, c, \
-                                               ldc, M, N, K, st)
-    switch (epi) {
-      case EPI_BIAS: return SYMB_G(EPI_BIAS);
-      case EPI_GELU: return SYMB_G(EPI_GELU);
-      case EPI_RES: return SYMB_G(EPI_RES);
-    }
-#undef SYMB_G
-    return -1;
-  }
-  if (tile_mode == 3 && ((M + 127) / 128) * (N / 128) < 256) {
+  if ((g_tile == 3 || g_tile == 10) && ((M + 127) / 128) * (N / 128) < 256) {
     // small M (query-path batches): fewer tiles than CUs, so occupancy is moot and each tile's
     // serial k-loop is the latency -- a 4-deep ring keeps 3 k-tiles' loads in flight
 #define SYMB_G(E) launch_cfg<128, 128, 2, 4, E, 4>(a, lda, w, ldw, bias, r, ldr, gamma, beta, eps, \
@@ -609,36 +561,10 @@ int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const flo
 #undef SYMB_G
     return -1;
   }
-  if (tile_mode == 3 || tile_mode == 6 || tile_mode == 7) {
-    // 128x128 with 8 waves (32x64 or 64x32 wave tiles): 4 waves per SIMD at 2 workgroups per CU
-#define SYMB_G(E, WM_, WN_) launch_cfg<128, 128, WM_, WN_, E>(a, lda, w, ldw, bias, r, ldr, gamma, \
-                                                             beta, eps, c, ldc, M, N, K, st)
-    const bool tall = tile_mode == 6;  // auto (3) takes the 64x32 wave tiles
-    switch (epi) {
-      case EPI_BIAS: return tall ? SYMB_G(EPI_BIAS, 4, 2) : SYMB_G(EPI_BIAS, 2, 4);
-      case EPI_GELU: return tall ? SYMB_G(EPI_GELU, 4, 2) : SYMB_G(EPI_GELU, 2, 4);
-      case EPI_RES: return tall ? SYMB_G(EPI_RES, 4, 2) : SYMB_G(EPI_RES, 2, 4);
-    }
-#undef SYMB_G
-    return -1;
-  }
-  if (tile_mode == 4 || tile_mode == 5) {
-    // 128x128, one workgroup per CU with a 3- or 4-deep ring (1-2 tiles in flight across each
-    // barrier) instead of two workgroups with 2-deep rings; A/B knob
-#define SYMB_G(E, NS) launch_cfg<128, 128, 2, 2, E, NS>(a, lda, w, ldw, bias, r, ldr, gamma, beta, \
-                                                       eps, c, ldc, M, N, K, st)
-    const bool four = tile_mode == 5;
-    switch (epi) {
-      case EPI_BIAS: return four ? SYMB_G(EPI_BIAS, 4) : SYMB_G(EPI_BIAS, 3);
-      case EPI_GELU: return four ? SYMB_G(EPI_GELU, 4) : SYMB_G(EPI_GELU, 3);
-      case EPI_RES: return four ? SYMB_G(EPI_RES, 4) : SYMB_G(EPI_RES, 3);
-    }
-#undef SYMB_G
-    return -1;
-  }
-  if (tile_mode == 1) {
-#define SYMB_G(E) launch_cfg<256, 128, 4, 2, E, 3>(a, lda, w, ldw, bias, r, ldr, gamma, beta, eps, \
-                                                 c, ldc, M, N, K, st)
+  if (g_tile == 3 || g_tile == 10) {
+    // 128x128 with 8 waves of 64x32: 4 waves per SIMD at 2 workgroups per CU
+#define SYMB_G(E) launch_cfg<128, 128, 2, 4, E>(a, lda, w, ldw, bias, r, ldr, gamma, beta, eps, c, \
+                                               ldc, M, N, K, st)
     switch (epi) {
       case EPI_BIAS: return SYMB_G(EPI_BIAS);
       case EPI_GELU: return SYMB_G(EPI_GELU);

@@ -309,12 +309,7 @@ void launch_partial(dim3 grid, hipStream_t st, const __bf16* a, int lda, const _
                     int gelu_poly, __bf16* c, int ldc, const float* g, const float* b, float eps,
                     int* counter) {
   constexpr int lds = 4 * RM * 16 * (64 + 4) * (int)sizeof(float);   // <= 68 KiB
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)skinny_partial_kernel<RM, EPI, FIN>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    attr = true;
-  }
+  set_max_lds<skinny_partial_kernel<RM, EPI, FIN>>(lds);
   hipLaunchKernelGGL((skinny_partial_kernel<RM, EPI, FIN>), grid, dim3(256), lds, st, a, lda, w,
                      ldw, P, M, N, KG, bias, r, ldr, gelu_poly, c, ldc, g, b, eps, counter);
 }

@@ -297,11 +297,7 @@ static int launch_fp8(const void* X, int n_valid, int rows_per_blk, int n_rblk, 
                       hipStream_t st) {
   auto kern = index_scan_fp8_kernel<D, KMAX, NS, SUBS, AUX>;
   constexpr int lds = NS * 32 * SUBS * D;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    attr = true;
-  }
+  set_max_lds<index_scan_fp8_kernel<D, KMAX, NS, SUBS, AUX>>(lds);
   hipLaunchKernelGGL(kern, dim3(n_rblk * n_qblk), dim3(256), lds, st, (const uint8_t*)X, n_valid,
                      rows_per_blk, (const uint8_t*)Q, NQ, n_qblk, xcd, thr, cs, ci);
   return (int)hipGetLastError();

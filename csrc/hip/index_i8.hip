@@ -876,12 +876,7 @@ static int launch_i8(const void* X8, const float* sx, int n_valid, int rows_per_
   constexpr int qpb = WV / RSPLIT * 16 * i8s::SETS;
   const int n_qblk = (NQ + qpb - 1) / qpb;
   constexpr int lds = i8s::Geo<TRK, WV>::LDS_BYTES;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)index_scan_i8_kernel<RSPLIT, 0, TRK, WV>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    attr = true;
-  }
+  set_max_lds<index_scan_i8_kernel<RSPLIT, 0, TRK, WV>>(lds);
   hipLaunchKernelGGL((index_scan_i8_kernel<RSPLIT, 0, TRK, WV>), dim3(n_rblk * n_qblk), dim3(64 * WV), lds, st,
                      (const int8_t*)X8, sx, n_valid, rows_per_blk, (const int8_t*)Q8, NQ, n_qblk,
                      xcd, thr, cand_s, cand_i, cand_n, cap, skip);

@@ -637,12 +637,7 @@ static int launch_mq_aux(const void* X, int n_valid, int rows_per_blk, int n_rbl
   constexpr int qpb = mq::WAVES / RSPLIT * 16 * NSET;
   const int n_qblk = (NQ + qpb - 1) / qpb;
   constexpr int lds = mq::LDS_BYTES;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)index_scan_mq_kernel<NSET, 0, RSPLIT, AUX>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    attr = true;
-  }
+  set_max_lds<index_scan_mq_kernel<NSET, 0, RSPLIT, AUX>>(lds);
   hipLaunchKernelGGL((index_scan_mq_kernel<NSET, 0, RSPLIT, AUX>), dim3(n_rblk * n_qblk), dim3(512),
                      lds, st, (const __bf16*)X, n_valid, rows_per_blk, (const __bf16*)Q, NQ, n_qblk,
                      xcd, thr, cand_s, cand_i, cand_n, cap, tshift, gate, lst);

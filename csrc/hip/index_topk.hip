@@ -587,11 +587,7 @@ static int launch_scan(const void* X, int n_valid, int rows_per_blk, int n_rblk,
                        hipStream_t st, const int* gate) {
   auto kern = index_scan_topk_kernel<D, M32, KMAX, NS, AUX>;
   constexpr int lds = NS * (M32 ? 64 : 32) * D * 2;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    attr = true;
-  }
+  set_max_lds<index_scan_topk_kernel<D, M32, KMAX, NS, AUX>>(lds);
   hipLaunchKernelGGL(kern, dim3(n_rblk * n_qblk), dim3(512), lds, st, (const __bf16*)X, n_valid,
                      rows_per_blk, (const __bf16*)Q, NQ, n_qblk, xcd, thr, cs, ci, gate);
   return (int)hipGetLastError();

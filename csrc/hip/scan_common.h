@@ -23,11 +23,6 @@ struct NoDma {
   __device__ __forceinline__ void operator()(int) const {}
 };
 
-// LDS byte address of a __shared__ pointer (for hand-issued ds_read offsets)
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
-}
-
 template <int KMAX>
 __device__ __forceinline__ void topk_insert(float (&tv)[KMAX], int (&ti)[KMAX], float s, int id) {
 #pragma unroll

@@ -191,6 +191,56 @@ def test_incremental_snapshot_cost_follows_new_rows(tmp_path):
     print(f"full {full_s:.2f}s, incremental {inc_s:.3f}s, boot {boot_s:.2f}s")
 
 
+def test_snapshot_merges_stream_from_disk_with_bounded_host_memory(tmp_path):
+    """A cut that merges the big segment (here: too many patched rows, so every segment is
+    rewritten) holds only the new rows and the overwrites in host memory: the merged segment is
+    streamed from the older files at write time.  A base snapshot above
+    FULL_CAPTURE_MAX streams the shard into its file under the lock instead of capturing it.
+    Both reload exactly, patches of older generations included."""
+    import tracemalloc
+
+    from codename_symbiont_amd.index import persist
+
+    D, N = 64, 400_000
+    shard_bytes = N * D * 2
+    d = str(tmp_path / "s")
+    sh = HbmIndexShard(D, N + 5000, device="cpu")
+    sh.fill_random(N, seed=11)
+    old_cap = persist.ShardPersister.FULL_CAPTURE_MAX
+    persist.ShardPersister.FULL_CAPTURE_MAX = shard_bytes // 8
+    try:
+        tracemalloc.start()
+        j1 = persist.ShardPersister(d).cut(sh)      # base snapshot: streamed to its file
+        peak1 = tracemalloc.get_traced_memory()[1]
+        j1.write()
+        tracemalloc.stop()
+    finally:
+        persist.ShardPersister.FULL_CAPTURE_MAX = old_cap
+    assert isinstance(j1.seg, str) and peak1 < shard_bytes / 4, peak1
+    rng = np.random.default_rng(5)
+    # gen 2: a small patch on old rows; gen 3: > MAX_PATCH_FRAC patched rows -> full merge
+    a = np.sort(rng.choice(N, 500, replace=False))
+    sh.write_rows_f32(a, torch.from_numpy(rng.standard_normal((500, D)).astype(np.float32)))
+    persist.save_snapshot(sh, d)
+    assert len(persist.committed_manifest(d)["patches"]) == 1
+    b = np.sort(rng.choice(N, int(N * 0.3), replace=False))
+    sh.write_rows_f32(b, torch.from_numpy(rng.standard_normal((b.size, D)).astype(np.float32)))
+    sh.append_f32(torch.from_numpy(rng.standard_normal((3000, D)).astype(np.float32)))
+    tracemalloc.start()
+    j3 = persist.ShardPersister(d).cut(sh)
+    peak3 = tracemalloc.get_traced_memory()[1]
+    tracemalloc.stop()
+    assert isinstance(j3.seg, persist.SegMerge) and j3.seg.row0 == 0
+    # the overwrites (30 % of the rows) and new rows, not the shard: < 0.45 x its bytes
+    assert peak3 < 0.45 * shard_bytes, (peak3, shard_bytes)
+    j3.write()
+    man = persist.committed_manifest(d)
+    assert man["patches"] == [] and [x["n"] for x in man["segments"]] == [N + 3000]
+    sh2 = HbmIndexShard(D, N + 5000, device="cpu")
+    assert persist.load_snapshot(sh2, d) == N + 3000
+    assert torch.equal(sh2.rows[:N + 3000], sh.rows[:N + 3000])
+
+
 def test_geometric_merges_bound_the_file_count(tmp_path):
     from codename_symbiont_amd.index import persist
 

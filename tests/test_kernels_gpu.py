@@ -67,76 +67,99 @@ def test_add_ln(H):
     _close(add_ln(x, None, g, b, 1e-5), R.add_ln_ref(x, None, g, b, 1e-5), 3e-2, 1e-2, "ln")
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 4, 5, 6, 7, 8, 9, 16])
+@pytest.mark.parametrize("tile", [0, 2, 3, 10, 16])
 @pytest.mark.parametrize("M,N,K,epi", [
     (300, 1152, 384, 0), (129, 1536, 384, 1), (517, 384, 384, 2), (517, 384, 384, 3),
     (300, 384, 1536, 3), (64, 768, 768, 2), (1000, 2304, 768, 0), (77, 1024, 4096, 2),
     (4099, 1536, 384, 1), (700, 384, 1536, 3),
     # > 256 tiles: more tiles than CUs
     (16384, 1152, 384, 0), (12800, 1536, 384, 1), (9000, 768, 3072, 2),
-    # tile=2 (256x256, banded epilogue) on every epilogue, ragged last row tile
-    (2000, 3072, 768, 1), (4353, 768, 3072, 2), (999, 2304, 768, 0),
-    # tile=9 (8-phase 256x256): one and two loop iterations, a single 256-wide column tile
+    # 256x256 tiles (tile 2, and the deep kernel under auto) on every epilogue, ragged last row
+    (2000, 3072, 768, 1), (4353, 768, 3072, 2), (999, 2304, 768, 0), (33000, 768, 768, 2),
     (300, 512, 128, 0), (513, 256, 256, 2),
 ])
 def test_gemm(M, N, K, epi, tile):
     from codename_symbiont_amd.ops._ext import hip
     from codename_symbiont_amd.ops.kernels import gemm
 
-    # tile=1: 256x128 3-stage / 64-row RES_LN, and a grouped tile order whose last band is short
-    # (group_m=3 rarely divides the row-tile count); tile=0: the default 8-row bands;
-    # tile=2: 256x256 wherever N % 256 == 0 (others fall back to 128x128), row-major order;
-    # the default (3, auto) is covered by the encoder tests
-    # tile=4/5: 128x128 with 3-/4-deep rings at one workgroup per CU
-    # tile=16: default tiles with the 8-wave (64x96 wave tiles) row-complete RES_LN tile
-    # (others: the default 16-wave one); tile=8: 16 waves of 32x32; tile=9: the 8-phase
-    # 256x256 kernel (gemm256.hip) where N % 256 == 0 and K % 128 == 0
-    hip().gemm_config(64 if tile == 1 else 128, 3 if tile == 16 else tile,
-                      {0: 8, 1: 3, 2: 0, 4: 8, 5: 5, 6: 8, 7: 2, 8: 8, 9: 8, 16: 8}[tile])
+    # tile=0: 128x128 4-wave tiles, 8-row grouped order; tile=2: gemm.hip's 256x256 wherever
+    # N % 256 == 0 (others fall back to 128x128), row-major order; tile=3: auto (the deep-ring
+    # kernel for the wide shapes), grouped order whose last band is short (group_m=3);
+    # tile=10: auto without the deep kernel; tile=16: auto with the 8-wave (64x96 wave tiles)
+    # row-complete RES_LN tile and the 64-row RES_LN tile (others: 16-wave, 128 rows)
+    hip().gemm_config(64 if tile == 16 else 128, 3 if tile == 16 else tile,
+                      {0: 8, 2: 0, 3: 3, 10: 8, 16: 8}[tile])
     hip().gemm_resln_config(8 if tile == 16 else 16)
-    hip().gemm_lt_config(0)   # gemm.hip's own tiles (the hipBLASLt route has its own test)
-
-    a = _bf(M, K, seed=1)
-    w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=2)
-    bias = _f(N, scale=0.5, seed=3)
-    res = _bf(M, N, seed=4) if epi in (2, 3) else None
-    g = _f(N, scale=0.1, offset=1.0, seed=5) if epi == 3 else None
-    b = _f(N, scale=0.1, seed=6) if epi == 3 else None
     try:
-        out = gemm(a, w, bias, epi, res, g, b, 1e-12)
+        out = gemm(a := _bf(M, K, seed=1), w := _bf(N, K, scale=1.0 / math.sqrt(K), seed=2),
+                   bias := _f(N, scale=0.5, seed=3), epi,
+                   res := (_bf(M, N, seed=4) if epi in (2, 3) else None),
+                   g := (_f(N, scale=0.1, offset=1.0, seed=5) if epi == 3 else None),
+                   b := (_f(N, scale=0.1, seed=6) if epi == 3 else None), 1e-12)
     finally:
         hip().gemm_config(128, 3, 8)
         hip().gemm_resln_config(16)
-        hip().gemm_lt_config(1)
     ref = R.gemm_ref(a, w, bias, epi, res, g, b, 1e-12)
     _close(out, ref, atol=4e-2, rtol=2e-2, what=f"gemm epi={epi}")
 
 
-@pytest.mark.parametrize("bm", [256, 192])
-@pytest.mark.parametrize("M,N,K", [(32768, 768, 768), (4100, 2304, 768), (999, 768, 3072),
-                                   (77, 1024, 1024), (256, 256, 64), (70000, 512, 128),
-                                   (1000, 3072, 192)])
+@pytest.mark.parametrize("ns,sk", [(5, 1), (4, 1), (5, 0)])
+@pytest.mark.parametrize("M,N,K", [
+    (32768, 768, 768),    # 384 tiles: 256 whole + 128 split 2 ways (the bge out-projection)
+    (32768, 768, 3072),   # the bge FFN2 shape, long K
+    (9000, 768, 3072),    # ragged last row tile, 108 tiles: split 2 ways
+    (4100, 2304, 768),    # 153 tiles (> P/2): no split
+    (999, 1024, 1024),    # 16 tiles: split 4 ways (K/32 = 32 k-steps, 8 per slice)
+    (300, 512, 128),      # 4 k-steps: one slice (the >= 4 k-steps per slice rule)
+    (777, 256, 2048),     # one column tile, split 4 ways
+    (65536, 1024, 1024),  # 1024 tiles: whole waves, no split
+])
 @pytest.mark.parametrize("epi", [0, 1, 2])
-def test_gemm4w(M, N, K, epi, bm):
-    """The persistent 4-wave 256x256 / 192x256 kernel (gemm4w.hip): ragged M (partial last row
-    tile), single k-tile, several tiles per workgroup (persistence + next-tile prefetch), every
-    epilogue, against the fp32 oracle."""
-    from codename_symbiont_amd.ops._ext import hip
-    from codename_symbiont_amd.ops.kernels import gemm
+def test_gemm_deep(M, N, K, epi, ns, sk):
+    """The deep-ring 256x256 kernel (gemm_deep.hip) through its own entry: ragged M, whole and
+    split last waves (2 and 4 slices, fp32 partials combined by the last arriving slice), both
+    ring depths, every epilogue, against the fp32 oracle -- and two launches are bit-identical
+    (slices are summed in slice order whichever arrives last)."""
+    from codename_symbiont_amd.ops._ext import hip, stream_handle
 
     a = _bf(M, K, seed=1)
     w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=2)
     bias = _f(N, scale=0.5, seed=3)
     res = _bf(M, N, seed=4) if epi == 2 else None
-    hip().gemm4w_config(3, bm)
+    outs = []
+    hip().gemm_deep_config(ns, sk)
     try:
-        out = gemm(a, w, bias, epi, res)
-        out2 = gemm(a, w, bias, epi, res)
+        for _ in range(2):
+            out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+            hip().gemm_deep(epi, a.data_ptr(), K, w.data_ptr(), K, bias.data_ptr(),
+                            res.data_ptr() if res is not None else 0, N, out.data_ptr(), N, M, N, K,
+                            8, 1, stream_handle(a.device))
+            outs.append(out)
+        torch.cuda.synchronize()
     finally:
-        hip().gemm4w_config(0, 0)
+        hip().gemm_deep_config(5, 1)
     ref = R.gemm_ref(a, w, bias, epi, res, None, None, 1e-12)
-    _close(out, ref, atol=4e-2, rtol=2e-2, what=f"gemm4w epi={epi} bm={bm}")
-    assert torch.equal(out, out2), "gemm4w is not deterministic"
+    _close(outs[0], ref, atol=4e-2, rtol=2e-2, what=f"gemm_deep epi={epi} ns={ns} sk={sk}")
+    assert torch.equal(outs[0], outs[1]), "gemm_deep is not deterministic"
+
+
+def test_gemm_deep_split_counters_survive_many_launches():
+    """The split tiles' arrival / done counters are reset by each last arriver: 50 back-to-back
+    launches of a split shape (and a graph-free mix with an unsplit one) stay exact."""
+    from codename_symbiont_amd.ops.kernels import gemm
+
+    M, N, K = 4353, 768, 1536
+    a = _bf(M, K, seed=7)
+    w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=8)
+    bias = _f(N, scale=0.5, seed=9)
+    a2 = _bf(65536, 768, seed=10)
+    first = gemm(a, w, bias, 0)
+    for i in range(50):
+        out = gemm(a, w, bias, 0)
+        if i % 10 == 0:
+            gemm(a2, w[:, :768].contiguous(), bias, 0)
+        assert torch.equal(out, first), i
+    _close(first, R.gemm_ref(a, w, bias, 0, None, None, None, 1e-12), atol=4e-2, rtol=2e-2)
 
 
 @pytest.mark.parametrize("M,N,K,epi", [(300, 1152, 384, 0), (4100, 768, 3072, 2), (999, 2304, 768, 0),
@@ -155,7 +178,7 @@ def test_gemm_hipblaslt_route(M, N, K, epi):
     try:
         out = gemm(a, w, bias, epi, res)
     finally:
-        hip().gemm_lt_config(1)
+        hip().gemm_lt_config(0)
     ref = R.gemm_ref(a, w, bias, epi, res, None, None, 1e-12)
     _close(out, ref, atol=4e-2, rtol=2e-2, what=f"hipblaslt gemm epi={epi}")
 
@@ -177,7 +200,7 @@ def test_gemm_hipblaslt_plan_cache_is_bounded():
             assert hip().gemm_lt_plans() <= 64
         ref = R.gemm_ref(a, w, bias, 0, None, None, None, 1e-12)
     finally:
-        hip().gemm_lt_config(1)
+        hip().gemm_lt_config(0)
     _close(out, ref, atol=4e-2, rtol=2e-2, what="hipblaslt gemm after evictions")
     assert hip().gemm_lt_plans() == 64
 
@@ -397,6 +420,72 @@ def test_store_pipelined_search_concurrent_and_ordered_after_upserts():
     assert not np.isin(np.arange(n, n + 8), r2).any()
 
 
+def test_store_upserts_racing_pipelined_searches_stay_exact():
+    """Overwrites that race pipelined searches (pre-pass on one stream, scan on another): a
+    writer flips 64 points between the first 64 queries' own directions (state A: each query's
+    best match, score 1) and their negations (state B) while 3 threads search.  An upsert can only
+    land between two searches, never between one search's pre-pass and its scan, so every batch
+    equals the exact single-stream answer of A or of B -- a torn search (thresholds from one
+    state, rows from the other) would drop true neighbours."""
+    import threading
+
+    import numpy as np
+
+    from codename_symbiont_amd.index.shard import Payload
+    from codename_symbiont_amd.index.store import VectorStore
+
+    D, n, nq, k = 384, (1 << 20) + 777, 96, 10
+    st = VectorStore(D, n + 1000, device="cuda")
+    st.shard.fill_random(n, seed=6)
+    g = torch.Generator().manual_seed(11)
+    q = torch.nn.functional.normalize(torch.randn(nq, D, generator=g), dim=-1).numpy()
+    ids = [f"w{i}" for i in range(64)]
+    pls = [Payload("d", "u", f"s{i}", i, "m", 0) for i in range(64)]
+    states = (q[:64].copy(), -q[:64])
+    want = []
+    streams, st._streams = st._streams, None
+    for v in states + states:          # twice: the int8 bounds have seen both states
+        st.upsert(ids, v, pls)
+        want.append(st.search(q, k))
+    st._streams = streams
+    want = want[2:]
+    assert (want[0][1][:64, 0] == np.arange(n, n + 64)).all()
+    stop = threading.Event()
+    got, errors = [], []
+
+    def writer():
+        i = 0
+        while not stop.is_set():
+            st.upsert(ids, states[i % 2], pls)
+            i += 1
+
+    def reader():
+        try:
+            for _ in range(12):
+                got.append(st.search(q, k))
+        except BaseException as e:   # noqa: BLE001
+            errors.append(e)
+
+    w = threading.Thread(target=writer)
+    rs = [threading.Thread(target=reader) for _ in range(3)]
+    w.start()
+    for r in rs:
+        r.start()
+    for r in rs:
+        r.join(240)
+    stop.set()
+    w.join(60)
+    assert not errors, errors
+    assert len(got) == 36
+    seen = set()
+    for s_, r_ in got:
+        match = [j for j, (ws, wr) in enumerate(want)
+                 if (r_ == wr).all() and np.allclose(s_, ws, atol=1e-6)]
+        assert match, "a search matched neither state"
+        seen.add(match[0])
+    assert seen, seen
+
+
 @pytest.mark.parametrize("dtype", ["bf16", "fp8"])
 def test_concurrent_searches_match_sequential(dtype):
     """The service runs searches from several executor threads on one shard and one stream:
@@ -458,6 +547,24 @@ def test_prefilter_fp8_rescored_search(D, nq):
     _close(ps, true, atol=1e-4, what="rescored scores")
     hits = sum(len(set(pi[i].tolist()) & set(ei[i].tolist())) for i in range(nq))
     assert hits / (nq * k) >= 0.998, hits / (nq * k)
+
+
+@pytest.mark.parametrize("k", [32, 64, 128])
+def test_prefilter_shard_large_k_is_exact(k):
+    """A prefilter shard keeps its bf16 rows, so top_k >= 32 is answered exactly over them (the
+    large-k emitting scan or the GEMM), never by the kmax-32 list kernels with k > kmax."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+
+    n, nq = (1 << 20) + 91, 40
+    sh = HbmIndexShard(384, n, prefilter="fp8")
+    sh.fill_random(n, seed=3)
+    q = torch.nn.functional.normalize(_f(nq, 384, seed=4), dim=-1).bfloat16()
+    s, r = sh.search(q, k)
+    ref = q.float() @ sh.rows[:n].float().t()
+    rs, ri = torch.topk(ref, k, dim=1)
+    assert s.shape == (nq, k) and (r >= 0).all()
+    _close(s, rs, atol=2e-5, what="scores")
+    _close(ref.gather(1, r.long()), rs, atol=2e-5, what="returned rows' scores")
 
 
 @pytest.mark.gpu

@@ -119,3 +119,19 @@ def test_normalizer_pipeline_steps():
         == ("_", 2, False)
     with pytest.raises(ValueError):
         build_normalizer({"type": "Nmt"})
+
+
+@pytest.mark.parametrize("seq", [["StripAccents"], ["NFD", "StripAccents"],
+                                 ["NFKD", "StripAccents", "Lowercase"], ["NFC", "StripAccents"]])
+def test_strip_accents_matches_hf(seq):
+    """StripAccents only filters marks (Mn / Mc / Me); decomposition is an explicit NFD step.
+    Hangul syllables, precomposed Latin and Devanagari spacing marks pin the difference."""
+    from tokenizers import normalizers
+
+    from codename_symbiont_amd.text.tokenizer import build_normalizer
+
+    spec = {"type": "Sequence", "normalizers": [{"type": t} for t in seq]}
+    ours = build_normalizer(spec)
+    hf = normalizers.Sequence([getattr(normalizers, t)() for t in seq])
+    for s in CASES + ["café 한국어 नमस्ते ñ x́ ⃝ qः ा", "Ångström Ελληνικά ῷ", "각 ㄱ ᄀ"]:
+        assert ours(s) == hf.normalize_str(s), (seq, s)
