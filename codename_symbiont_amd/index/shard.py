@@ -117,7 +117,7 @@ FP8_SCALE = 256.0  # == ops.kernels.FP8_SCALE (kept import-free for CPU-only use
 def resolve_prune(mode: str | None, dtype: str = "bf16", dim: int = 384,
                   prefilter: str | None = None, device=None) -> str | None:
     """``SYMB_INDEX_PRUNE``: "auto" (default) = the exact int8-pruned search wherever it applies
-    (384-wide bf16 shards without an fp8 prefilter, on a GPU), "i8" = require it, "" / "none" =
+    (384- or 768-wide bf16 shards without an fp8 prefilter, on a GPU), "i8" = require it, "" / "none" =
     plain scan.  ``device``: the shard's device; "auto" on a CPU shard is None (the CPU backend
     searches by matmul and would only pay for the int8 image on every write)."""
     mode = (mode or "").strip().lower()
@@ -126,9 +126,13 @@ def resolve_prune(mode: str | None, dtype: str = "bf16", dim: int = 384,
     if mode == "auto":
         if device is not None and torch.device(device).type != "cuda":
             return None
-        return "i8" if (dtype == "bf16" and dim == 384 and not prefilter) else None
+        return "i8" if (dtype == "bf16" and dim in PRUNE_DIMS and not prefilter) else None
     return mode
+
+
 FP8_DIMS = (256, 384, 512, 768, 1024)   # row widths the fp8 scan kernel takes
+MQ_DIMS = (384, 768, 1024)              # ... the emitting bf16 scan (index_mq.hip)
+PRUNE_DIMS = (384, 768)                 # ... the int8-pruned scan (index_i8.hip)
 
 
 class HbmIndexShard:
@@ -158,8 +162,8 @@ class HbmIndexShard:
         prune = prune or None
         if prune not in (None, "i8"):
             raise ValueError(f"index prune must be i8 or None, got {prune!r}")
-        if prune and (dtype != "bf16" or dim != 384):
-            raise ValueError("the int8 pruned search needs a 384-wide bf16 shard")
+        if prune and (dtype != "bf16" or dim not in PRUNE_DIMS):
+            raise ValueError(f"the int8 pruned search needs a bf16 shard of width {PRUNE_DIMS}")
         self.prune = prune
         self.dim = dim
         self.dtype = dtype
@@ -553,8 +557,16 @@ class HbmIndexShard:
         return ts, nv, t0, cached[1]
 
     def _mq_ok(self, NQ: int, k: int, rows, dtype: str) -> bool:
-        return (self.scan_mq and dtype == "bf16" and self.dim == 384 and rows is self.rows
+        return (self.scan_mq and dtype == "bf16" and self.dim in MQ_DIMS and rows is self.rows
                 and NQ >= self.mq_min_nq and k <= 16)
+
+    def _mq_form(self, NQ: int):
+        """(sets, rsplit) of the emitting scan: 16-query sets per wave and waves sharing a query
+        group.  D = 384: 4 sets (512 queries per workgroup, or 256 with the row split); wider rows
+        hold fewer resident query sets (768: 2, 1024: 1)."""
+        if self.dim != 384:
+            return (2 if self.dim == 768 else 1), 1
+        return (4, 1) if NQ >= 512 else ((4, 2) if self.mq_rsplit else (2, 1))
 
     def _block_sample(self, n: int):
         """Row sample for threshold seeding: row 64 i + h(i) of every full 64-row block i (h a
@@ -587,8 +599,7 @@ class HbmIndexShard:
 
         h = hip()
         NQ = q_unit.shape[0]
-        # 512 queries per workgroup, or 256 (row-split 4-set or 2-set form)
-        sets, rsplit = (4, 1) if NQ >= 512 else ((4, 2) if self.mq_rsplit else (2, 1))
+        sets, rsplit = self._mq_form(NQ)
         n_qblk = math.ceil(NQ / h.mq_queries_per_blk(sets, rsplit))
         if n_cus is None:
             n_cus = self._n_cus()
@@ -608,7 +619,7 @@ class HbmIndexShard:
         gp = 0 if gate is None else gate.data_ptr()
         h.index_scan_mq(rows.data_ptr(), n, rows_per_blk, n_rblk, q_unit.data_ptr(), NQ,
                         thr.data_ptr(), cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(), cap,
-                        self.scan_xcd, st, sets, tshift, rsplit, gp)
+                        self.scan_xcd, st, sets, tshift, rsplit, gp, dim=self.dim)
         h.topk_select_counted(cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(), cap, NQ, kmax, k,
                               out_s.data_ptr(), out_i.data_ptr(), ovf.data_ptr(), st, gate=gp,
                               reset_ovf=gate is None)
@@ -777,7 +788,7 @@ class HbmIndexShard:
 
         h = hip()
         rsplit = 2 if (NQ < 512 or self.i8_rsplit2) else 1
-        tr = h.i8_tile_rows()
+        tr = h.i8_tile_rows(self.dim)
         n_qblk = math.ceil(NQ / h.i8_queries_per_blk(rsplit))
         wpc = h.i8_wgs_per_cu()
         n_rblk = max(1, min(math.ceil(n / (tr * 16)), max(1, round(n_cus * wpc / n_qblk))))
@@ -790,7 +801,7 @@ class HbmIndexShard:
         (as _scan_mq)."""
         from ..ops._ext import hip
 
-        sets, rsplit = (4, 1) if NQ >= 512 else ((4, 2) if self.mq_rsplit else (2, 1))
+        sets, rsplit = self._mq_form(NQ)
         n_qblk = math.ceil(NQ / hip().mq_queries_per_blk(sets, rsplit))
         return sets, rsplit, n_qblk, max(1, round(n_cus / n_qblk))
 
@@ -820,7 +831,7 @@ class HbmIndexShard:
         h.index_scan_i8(self.rows_i8.data_ptr(), self.sx_i8.data_ptr(), n, self.rows_i8.shape[0],
                         rows_per_blk, n_rblk,
                         q8.data_ptr(), NQ, thr.data_ptr(), cs.data_ptr(), ci.data_ptr(),
-                        cnt.data_ptr(), cap, self.scan_xcd, st, rsplit, skip=skip)
+                        cnt.data_ptr(), cap, self.scan_xcd, st, rsplit, skip=skip, dim=self.dim)
         # 3'. the bf16 emitting scan of the blocks the route listed, at the exact threshold T,
         #     into the same candidate buffers (no launch work when none is listed)
         if self.prune_route:
@@ -828,7 +839,7 @@ class HbmIndexShard:
             h.index_scan_mq(self.rows.data_ptr(), n, TILE_ROWS, slots, q_unit.data_ptr(), NQ,
                             T.data_ptr(), cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(), cap,
                             self.scan_xcd, st, sets, 0, mrs, blist=blk.data_ptr(),
-                            list_tiles=rows_per_blk // TILE_ROWS, zero_cnt=False)
+                            list_tiles=rows_per_blk // TILE_ROWS, zero_cnt=False, dim=self.dim)
         # 4. exact bf16 re-score of every candidate, 5. top-k
         h.rescore_bf16(self.rows.data_ptr(), q_unit.data_ptr(), NQ, self.dim, ci.data_ptr(),
                        cnt.data_ptr(), cap, cs.data_ptr(), st)
@@ -860,15 +871,17 @@ class HbmIndexShard:
     LARGE_K_CAP = 16384      # candidate slots per query of the large-k emitting scan
 
     def _search_large_k(self, q_unit, k: int, n_cus):
-        """EXACT top-k for 16 < k <= 128 on a 384-wide bf16 shard: T = the k-th best exact score
+        """EXACT top-k for 16 < k <= 128 on a bf16 shard (D = 384 / 768 / 1024): T = the k-th best exact score
         of a 1-in-32 tile sample of real rows (seeded from a 1-in-2048 sub-sample scored by an
         fp32 GEMM) plus the fresh-row tail, then the bf16 emitting scan keeps every row scoring
         >= T (a lower bound on each query's final k-th score), and the radix select
         (topk_select_radix_kernel) takes each query's top k.  A query whose candidates overflow
         LARGE_K_CAP sends the batch to the exact chunked GEMM (host check; rare).  None when the
-        shard is too small or not 384-wide bf16 (the caller takes the list scan / GEMM)."""
+        shard is too small or not a bf16 shard of an emitting-scan width (the caller takes the
+        list scan / GEMM)."""
         n, NQ = self.visible, q_unit.shape[0]
-        if self.dtype != "bf16" or self.dim != 384 or not self.scan_mq or k > self.K_MAX_HIP:
+        if (self.dtype != "bf16" or self.dim not in MQ_DIMS or not self.scan_mq
+                or k > self.K_MAX_HIP):
             return None
         if n < self.SEED_MIN_ROWS:
             return None
@@ -905,7 +918,7 @@ class HbmIndexShard:
         """fp8 scan for oversample*k candidates, exact bf16 re-score, top-k (see the class doc)."""
         kc = min(32, max(16, self.oversample * k))
         _, cand = self._search_scan(q_unit, kc, self.rows8, "fp8", n_cus)    # [NQ, kc] rows
-        if self.dim == 384:
+        if self.dim in MQ_DIMS:
             # the pruned search's kernels: exact bf16 re-score of the candidate rows (8 waves per
             # query gather them) and the counted select; the scan's list is score-sorted, so the
             # valid candidates are a prefix of each row

@@ -72,7 +72,8 @@ int symb_i8_queries_per_blk(int rsplit);
 int symb_index_scan_i8(const void* X8, const float* sx, int n_valid, int alloc_rows,
                        int rows_per_blk, int n_rblk, const void* Q8, int NQ, const float* thr,
                        float* cand_s, int* cand_i, int* cand_n, int cap, int xcd, hipStream_t st,
-                       int rsplit, const int* skip);
+                       int rsplit, const int* skip, int dim);
+int symb_i8_tile_rows_for(int dim);
 int symb_prune_qquant(const void* Q, int NQ, int dim, const float* bounds, void* Q8, float* sq,
                       float* margin, hipStream_t st);
 int symb_prune_route(int NQ, const float* pre_s, const float* tail_s, int k, float thr_margin,
@@ -106,7 +107,8 @@ int symb_mq_config(int aux);
 int symb_index_scan_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                        int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
                        int xcd, hipStream_t st, int sets, int tshift, int rsplit,
-                       const int* gate, const int* blist, int list_tiles, int zero_cnt);
+                       const int* gate, const int* blist, int list_tiles, int zero_cnt, int dim);
+int symb_mq_max_sets(int dim);
 int symb_index_scan_mq_ablate(const void* X, int n_valid, int rows_per_blk, int n_rblk,
                               const void* Q, int NQ, const float* thr, float* cand_s, int* cand_i,
                               int* cand_n, int cap, int xcd, hipStream_t st, int abl, int sets,
@@ -387,20 +389,20 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("rsplit") = 2);
   m.def("i8_config", [](int tile_rows, int waves) { check(symb_i8_config(tile_rows, waves), "i8_config"); },
         py::arg("tile_rows"), py::arg("waves") = 8);
-  m.def("i8_tile_rows", []() { return symb_i8_tile_rows(); });
+  m.def("i8_tile_rows", [](int dim) { return symb_i8_tile_rows_for(dim); }, py::arg("dim") = 384);
   m.def("i8_wgs_per_cu", []() { return symb_i8_wgs_per_cu(); });
   m.def("index_scan_i8", [](uptr X8, uptr sx, int n_valid, int alloc_rows, int rows_per_blk,
                             int n_rblk, uptr Q8, int NQ, uptr thr, uptr cand_s, uptr cand_i,
-                            uptr cand_n, int cap, int xcd, uptr st, int rsplit, uptr skip) {
+                            uptr cand_n, int cap, int xcd, uptr st, int rsplit, uptr skip, int dim) {
     check(symb_index_scan_i8(P<void>(X8), P<const float>(sx), n_valid, alloc_rows, rows_per_blk,
                              n_rblk,
                              P<void>(Q8), NQ, P<const float>(thr), P<float>(cand_s), P<int>(cand_i),
-                             P<int>(cand_n), cap, xcd, S(st), rsplit, P<const int>(skip)),
+                             P<int>(cand_n), cap, xcd, S(st), rsplit, P<const int>(skip), dim),
           "index_scan_i8");
   }, py::arg("X8"), py::arg("sx"), py::arg("n_valid"), py::arg("alloc_rows"),
      py::arg("rows_per_blk"), py::arg("n_rblk"), py::arg("Q8"), py::arg("NQ"), py::arg("thr"),
      py::arg("cand_s"), py::arg("cand_i"), py::arg("cand_n"), py::arg("cap"), py::arg("xcd"),
-     py::arg("stream"), py::arg("rsplit"), py::arg("skip") = 0);
+     py::arg("stream"), py::arg("rsplit"), py::arg("skip") = 0, py::arg("dim") = 384);
   m.def("prune_qquant", [](uptr Q, int NQ, int dim, uptr bounds, uptr Q8, uptr sq, uptr margin,
                            uptr st) {
     check(symb_prune_qquant(P<void>(Q), NQ, dim, P<const float>(bounds), P<void>(Q8), P<float>(sq),
@@ -469,17 +471,18 @@ PYBIND11_MODULE(_hip, m) {
   m.def("index_scan_mq", [](uptr X, int n_valid, int rows_per_blk, int n_rblk, uptr Q, int NQ,
                             uptr thr, uptr cand_s, uptr cand_i, uptr cand_n, int cap, int xcd,
                             uptr st, int sets, int tshift, int rsplit, uptr gate, uptr blist,
-                            int list_tiles, bool zero_cnt) {
+                            int list_tiles, bool zero_cnt, int dim) {
     check(symb_index_scan_mq(P<void>(X), n_valid, rows_per_blk, n_rblk, P<void>(Q), NQ,
                              P<const float>(thr), P<float>(cand_s), P<int>(cand_i), P<int>(cand_n),
                              cap, xcd, S(st), sets, tshift, rsplit, P<const int>(gate),
-                             P<const int>(blist), list_tiles, zero_cnt ? 1 : 0),
+                             P<const int>(blist), list_tiles, zero_cnt ? 1 : 0, dim),
           "index_scan_mq");
   }, py::arg("X"), py::arg("n_valid"), py::arg("rows_per_blk"), py::arg("n_rblk"), py::arg("Q"),
      py::arg("NQ"), py::arg("thr"), py::arg("cand_s"), py::arg("cand_i"), py::arg("cand_n"),
      py::arg("cap"), py::arg("xcd"), py::arg("stream"), py::arg("sets") = 4,
      py::arg("tshift") = 0, py::arg("rsplit") = 1, py::arg("gate") = 0, py::arg("blist") = 0,
-     py::arg("list_tiles") = 0, py::arg("zero_cnt") = true);
+     py::arg("list_tiles") = 0, py::arg("zero_cnt") = true, py::arg("dim") = 384);
+  m.def("mq_max_sets", [](int dim) { return symb_mq_max_sets(dim); }, py::arg("dim"));
   m.def("index_scan_mq_ablate", [](uptr X, int n_valid, int rows_per_blk, int n_rblk, uptr Q,
                                    int NQ, uptr thr, uptr cand_s, uptr cand_i, uptr cand_n,
                                    int cap, int xcd, uptr st, int abl, int sets, int rsplit) {

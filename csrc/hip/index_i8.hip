@@ -32,23 +32,40 @@
 namespace symb {
 
 namespace i8s {
-constexpr int D = 384;                      // int8 bytes per row
 constexpr int WAVES = 8;
 constexpr int SETS = 4;                     // 16-query sets per wave
 constexpr int SUB = 16;
-constexpr int NKS = D / 64;                 // 6 k-steps of v_mfma_i32_16x16x64_i8
 constexpr int PIECE = 1024;
-// Tile geometry: TR = 64-row tiles (24 KiB) in a 5-deep ring, or 128-row tiles (48 KiB) in a
-// 3-deep ring -- the same 96 KiB in flight, half the barriers and DMA bursts per row.
-// WV = 4: 4-wave workgroups (one wave per SIMD), TWO per CU, each with its own 3-deep ring:
-// the two waves sharing a SIMD then belong to different workgroups, so one's barrier, prologue
-// and DMA burst fall under the other's MFMAs instead of in lockstep with them.
-template <int TR_, int WV_ = 8> struct Geo {
+#ifndef SYMB_I8_PF
+#define SYMB_I8_PF 5
+#endif
+}  // namespace i8s
+
+// Row width: D = 384 (the headline shard) or 768 (the reference's collection,
+// vector_memory_service/src/main.rs:22).  v_mfma_i32_16x16x64_i8 k-steps: 6 / 12; the queries'
+// B fragments take SETS x NKS x 4 = 96 / 192 VGPRs.
+// Fragment reads in flight: PF (NKS % (PF + 1) == 0); 3 at D = 768, whose 192 query registers
+// leave no room for a 6-slot fragment ring.
+template <int D> struct I8Dim {
+  static constexpr int NKS = D / 64;
+  static constexpr int PF = D == 384 ? SYMB_I8_PF : 3;
+  static constexpr int R = PF + 1;
+  static_assert(D == 384 || D == 768, "int8 scan row width");
+  static_assert(NKS % R == 0, "cross-chain prefetch: fragment j of the next chain uses slot j % R");
+};
+
+// Tile geometry: TR = 64-row tiles in a 5-deep ring (24 KiB tiles, D = 384) or a 3-deep ring
+// (48 KiB: D = 768, or 128-row tiles at D = 384) -- ~96-144 KiB in flight.
+// WV = 4 (D = 384): 4-wave workgroups (one wave per SIMD), TWO per CU, each with its own 3-deep
+// ring: the two waves sharing a SIMD then belong to different workgroups, so one's barrier,
+// prologue and DMA burst fall under the other's MFMAs instead of in lockstep with them.
+template <int D, int TR_, int WV_ = 8> struct Geo {
   static constexpr int TR = TR_;
   static constexpr int WV = WV_;
-  static constexpr int NSUB = TR / SUB;
-  static constexpr int NS = WV == 4 ? 3 : (TR == 64 ? 5 : 3);
+  static constexpr int NKS = I8Dim<D>::NKS;
+  static constexpr int NSUB = TR / i8s::SUB;
   static constexpr int TILE_BYTES = TR * D;
+  static constexpr int NS = WV == 4 ? 3 : (TILE_BYTES <= 24 * 1024 ? 5 : 3);
   static constexpr int LOADS = TILE_BYTES / (1024 * WV);      // LDS-DMA pieces per wave per tile
   static constexpr int DMA_EVERY = NKS / LOADS;               // k-steps between pieces
   static constexpr int SCW = TR / 64;                         // waves carrying a scale DMA
@@ -58,23 +75,10 @@ template <int TR_, int WV_ = 8> struct Geo {
   static constexpr int LDS_BYTES = NS * TILE_BYTES + NS * SC_BYTES + WV * STAGE_BYTES;
   static_assert(TILE_BYTES % (1024 * WV) == 0, "tile must split evenly over waves");
   static_assert(WV == 8 || 2 * LDS_BYTES <= 160 * 1024, "two 4-wave workgroups must share a CU");
-  static_assert(NSUB * NKS * PIECE == TILE_BYTES, "a tile is NSUB x NKS pieces");
+  static_assert(NSUB * NKS * i8s::PIECE == TILE_BYTES, "a tile is NSUB x NKS pieces");
   static_assert(LOADS * DMA_EVERY <= NKS && DMA_EVERY >= 1, "DMA pieces must fit the first chain");
   static_assert(LDS_BYTES <= 160 * 1024, "ring + scales + stages exceed the CU's 160 KiB");
 };
-constexpr int TR = 64;                      // the (unfused) single-sub-tile chain's geometry
-constexpr int NSUB = TR / SUB;
-constexpr int NS = Geo<64>::NS;
-constexpr int TILE_BYTES = Geo<64>::TILE_BYTES;
-constexpr int LOADS = Geo<64>::LOADS;
-#ifndef SYMB_I8_PF
-#define SYMB_I8_PF 5
-#endif
-constexpr int PF = SYMB_I8_PF;              // fragment reads in flight (NKS % (PF + 1) == 0)
-constexpr int R = PF + 1;
-constexpr int DMA_EVERY = Geo<64>::DMA_EVERY;
-static_assert(NKS % R == 0, "cross-chain prefetch: fragment j of the next chain uses slot j % R");
-}  // namespace i8s
 
 typedef __attribute__((ext_vector_type(4))) int i32x4;
 
@@ -95,11 +99,12 @@ __device__ __forceinline__ void i8_mfma(i32x4& acc, const i32x4& a, const i32x4&
 }
 
 // k-step KS of one 16-row sub-tile (index_mq.hip MqChain, int8 operands).
-template <int KS, int DMA_PIECES, bool NEXT, int DE = i8s::DMA_EVERY>
+template <int D, int KS, int DMA_PIECES, bool NEXT, int DE>
 struct I8Chain {
+  static constexpr int NKS = I8Dim<D>::NKS, PF = I8Dim<D>::PF, R = I8Dim<D>::R;
   template <class Dma>
-  __device__ __forceinline__ static void run(i32x4 (&acc)[i8s::SETS], i32x4 (&a)[i8s::R],
-                                             const i32x4 (&qf)[i8s::SETS][i8s::NKS],
+  __device__ __forceinline__ static void run(i32x4 (&acc)[i8s::SETS], i32x4 (&a)[R],
+                                             const i32x4 (&qf)[i8s::SETS][NKS],
                                              uint32_t base, uint32_t next, const Dma& dma) {
     using namespace i8s;
     static_assert(DMA_PIECES * DE <= NKS, "every DMA piece must be issued in the chain");
@@ -113,7 +118,7 @@ struct I8Chain {
       i8_read16<(KS + PF) * PIECE>(a[(KS + PF) % R], base);
     else if constexpr (NEXT)
       i8_read16<(KS + PF - NKS) * PIECE>(a[(KS + PF) % R], next);
-    if constexpr (KS + 1 < NKS) I8Chain<KS + 1, DMA_PIECES, NEXT, DE>::run(acc, a, qf, base, next, dma);
+    if constexpr (KS + 1 < NKS) I8Chain<D, KS + 1, DMA_PIECES, NEXT, DE>::run(acc, a, qf, base, next, dma);
   }
 };
 
@@ -135,11 +140,12 @@ __device__ __forceinline__ void i8_lgkm2t(i32x4& v0, i32x4& v1, f32x4& t0, f32x4
 // t0 / t1: the two sub-tiles' row scales, read from LDS just before the prologue; the first
 // k-step's wait covers them (older than every fragment read), so the emission after the chain
 // finds them in registers
-template <int KS, int DMA_PIECES, int DE>
+template <int D, int KS, int DMA_PIECES, int DE>
 struct I8Chain2 {
+  static constexpr int NKS = I8Dim<D>::NKS;
   template <class Dma>
   __device__ __forceinline__ static void run(i32x4 (&acc)[2][i8s::SETS], i32x4 (&a)[i8s::R2][2],
-                                             const i32x4 (&qf)[i8s::SETS][i8s::NKS],
+                                             const i32x4 (&qf)[i8s::SETS][NKS],
                                              uint32_t base, const Dma& dma, f32x4& t0, f32x4& t1) {
     using namespace i8s;
     if constexpr (DMA_PIECES > 0 && KS % DE == 0 && KS / DE < DMA_PIECES) dma(KS / DE);
@@ -157,20 +163,20 @@ struct I8Chain2 {
       i8_read16<(KS + PF2) * PIECE>(a[(KS + PF2) % R2][0], base);
       i8_read16<(KS + PF2) * PIECE + NKS * PIECE>(a[(KS + PF2) % R2][1], base);
     }
-    if constexpr (KS + 1 < NKS) I8Chain2<KS + 1, DMA_PIECES, DE>::run(acc, a, qf, base, dma, t0, t1);
+    if constexpr (KS + 1 < NKS) I8Chain2<D, KS + 1, DMA_PIECES, DE>::run(acc, a, qf, base, dma, t0, t1);
   }
 };
-template <int J>
+template <int D, int J>
 __device__ __forceinline__ void i8_prologue2(i32x4 (&a)[i8s::R2][2], uint32_t base) {
   i8_read16<J * i8s::PIECE>(a[J % i8s::R2][0], base);
-  i8_read16<J * i8s::PIECE + i8s::NKS * i8s::PIECE>(a[J % i8s::R2][1], base);
-  if constexpr (J + 1 < i8s::PF2) i8_prologue2<J + 1>(a, base);
+  i8_read16<J * i8s::PIECE + I8Dim<D>::NKS * i8s::PIECE>(a[J % i8s::R2][1], base);
+  if constexpr (J + 1 < i8s::PF2) i8_prologue2<D, J + 1>(a, base);
 }
 
-template <int J>
-__device__ __forceinline__ void i8_prologue(i32x4 (&a)[i8s::R], uint32_t base) {
-  i8_read16<J * i8s::PIECE>(a[J % i8s::R], base);
-  if constexpr (J + 1 < i8s::PF) i8_prologue<J + 1>(a, base);
+template <int D, int J>
+__device__ __forceinline__ void i8_prologue(i32x4 (&a)[I8Dim<D>::R], uint32_t base) {
+  i8_read16<J * i8s::PIECE>(a[J % I8Dim<D>::R], base);
+  if constexpr (J + 1 < I8Dim<D>::PF) i8_prologue<D, J + 1>(a, base);
 }
 
 __device__ __forceinline__ const char* i8_uniform(const char* p) {
@@ -186,14 +192,15 @@ __device__ __forceinline__ const char* i8_uniform(const char* p) {
 // ABL (profiling entry symb_index_scan_i8_ablate only): 1 = no LDS-DMA, 2 = no emission test,
 // 3 = full + s_memtime / s_memrealtime around the tile loop into cand_s[2 * blockIdx.x + {0, 1}],
 // 4 = LDS-DMA ring only.
-template <int RSPLIT, int ABL = 0, int TRK = 64, int WV = 8>
+template <int D, int RSPLIT, int ABL = 0, int TRK = 64, int WV = 8>
 __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
     const int8_t* __restrict__ X8, const float* __restrict__ sx, int n_valid, int rows_per_blk,
     const int8_t* __restrict__ Q8, int NQ, int n_qblk, int xcd, const float* __restrict__ thr_in,
     float* __restrict__ cand_s, int* __restrict__ cand_i, int* __restrict__ cand_n, int cap,
     const int* __restrict__ skip) {
   using namespace i8s;
-  using G = Geo<TRK, WV>;
+  using G = Geo<D, TRK, WV>;
+  constexpr int NKS = G::NKS;
   constexpr int TR = G::TR, NSUB = G::NSUB, NS = G::NS, TILE_BYTES = G::TILE_BYTES;
   constexpr int LOADS = G::LOADS, SC_BYTES = G::SC_BYTES, STW = G::STW;
   constexpr int STAGE_BYTES = G::STAGE_BYTES;
@@ -347,12 +354,14 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
     c0 = __builtin_amdgcn_s_memtime();
     r0t = __builtin_amdgcn_s_memrealtime();
   }
-  i32x4 a[R];
+  i32x4 a[I8Dim<D>::R];
   i32x4 acc[SETS];
   // fused two-sub-tile chains: the row-split forms (each wave owns 2 or 4 sub-tiles of a tile)
   // (the 512-query form keeps single-sub-tile chains: its two fused groups per tile have no
   // cross-chain prefetch and measured slower, 10.55 -> 11.15 ms at 12.5M x 2048)
-  constexpr bool FUSE = NSW % 2 == 0 && (RSPLIT == 2 || TRK == 128);
+  // (D = 768: single-sub-tile chains -- the fused pair's extra fragment and accumulator
+  // registers do not fit beside 192 query registers)
+  constexpr bool FUSE = D == 384 && NSW % 2 == 0 && (RSPLIT == 2 || TRK == 128);
   constexpr int NG = FUSE ? NSW / 2 : 1;   // fused chains per wave per tile
   i32x4 a2[FUSE ? R2 : 1][2];
   i32x4 acc2[FUSE ? 2 : 1][SETS];
@@ -396,7 +405,7 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
           asm volatile("ds_read_b128 %0, %1" : "=v"(sa) : "v"(sp));
           asm volatile("ds_read_b128 %0, %1 offset:64" : "=v"(sb) : "v"(sp));
         }
-        i8_prologue2<0>(a2, fg);
+        i8_prologue2<D, 0>(a2, fg);
         // a late wave tests the previous tile's last two sub-tiles here, under its partner's
         // MFMAs
         if (g == 0 && late && t > 0) {
@@ -404,9 +413,9 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
           emit(acc2[1], row0 - TR + last, s4_last);
         }
         if (g == 0)
-          I8Chain2<0, LOADS, G::DMA_EVERY>::run(acc2, a2, qf, fg, dma, sa, sb);
+          I8Chain2<D, 0, LOADS, G::DMA_EVERY>::run(acc2, a2, qf, fg, dma, sa, sb);
         else
-          I8Chain2<0, 0, G::DMA_EVERY>::run(acc2, a2, qf, fg, NoDma(), sa, sb);
+          I8Chain2<D, 0, 0, G::DMA_EVERY>::run(acc2, a2, qf, fg, NoDma(), sa, sb);
         if (g + 1 < NG || !late) {
           emit(acc2[0], row0 + jg * SUB, sa);
           emit(acc2[1], row0 + (jg + 1) * SUB, sb);
@@ -417,19 +426,20 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
       }
       continue;
     }
-    i8_prologue<0>(a, fw);
+    i8_prologue<D, 0>(a, fw);
     if (late && t > 0) emit(acc, row0 - TR + last, s4_last);
     if constexpr (NSW > 1)
-      I8Chain<0, LOADS, true, G::DMA_EVERY>::run(acc, a, qf, fw, fw + NKS * PIECE, dma);
+      I8Chain<D, 0, LOADS, true, G::DMA_EVERY>::run(acc, a, qf, fw, fw + NKS * PIECE, dma);
     else
-      I8Chain<0, LOADS, false, G::DMA_EVERY>::run(acc, a, qf, fw, 0, dma);
+      I8Chain<D, 0, LOADS, false, G::DMA_EVERY>::run(acc, a, qf, fw, 0, dma);
 #pragma unroll
     for (int j = 1; j < NSW; ++j) {
       emit(acc, row0 + (j0 + j - 1) * SUB, scales(slot, j0 + j - 1));
       if (j + 1 < NSW)
-        I8Chain<0, 0, true>::run(acc, a, qf, fw + j * NKS * PIECE, fw + (j + 1) * NKS * PIECE, NoDma());
+        I8Chain<D, 0, 0, true, G::DMA_EVERY>::run(acc, a, qf, fw + j * NKS * PIECE,
+                                                 fw + (j + 1) * NKS * PIECE, NoDma());
       else
-        I8Chain<0, 0, false>::run(acc, a, qf, fw + j * NKS * PIECE, 0, NoDma());
+        I8Chain<D, 0, 0, false, G::DMA_EVERY>::run(acc, a, qf, fw + j * NKS * PIECE, 0, NoDma());
     }
     if (!late)
       emit(acc, row0 + last, scales(slot, j0 + NSW - 1));
@@ -459,10 +469,11 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
 // Exact re-score of every candidate: cand_s[q][c] = <Q[q], X[cand_i[q][c]]> over the bf16 rows
 // (fp32 accumulation).  SPLIT workgroups per query (blockIdx.y), one wave per candidate with U
 // 768-byte row gathers in flight per wave, 6 elements per lane.
+template <int D>
 __global__ __launch_bounds__(256) void rescore_bf16_kernel(
     const __bf16* __restrict__ X, const __bf16* __restrict__ Q, const int* __restrict__ cand_i,
     const int* __restrict__ cand_n, int cap, float* __restrict__ cand_s) {
-  constexpr int D = 384, PER = D / 64;
+  constexpr int PER = D / 64;
   const int q = blockIdx.x, lane = threadIdx.x & 63;
   const int wave = blockIdx.y * 4 + (threadIdx.x >> 6), nwaves = gridDim.y * 4;
   const int n = min(cand_n[q], cap);
@@ -502,10 +513,11 @@ __global__ __launch_bounds__(256) void rescore_bf16_kernel(
   }
 }
 
-// Per-row int8 quantiser of 384-wide bf16 rows: sx = max|x| / 127, x8 = round(x / sx), and the
+// Per-row int8 quantiser of D-wide bf16 rows (D = 384 / 768 / 1024): sx = max|x| / 127, x8 = round(x / sx), and the
 // per-row |x - sx * x8| (err) and |sx * x8| (xtn) the pruning bound needs.  One wave per row.
 // err / xtn (optional) receive the per-row norms; bounds (optional, 2 floats) is raised to
 // (max err, max xtn) by one atomic max per workgroup (non-negative floats order as their bits).
+template <int D>
 __global__ __launch_bounds__(256) void quant_rows_i8_kernel(const __bf16* __restrict__ X, int n,
                                                             int8_t* __restrict__ X8,
                                                             float* __restrict__ sx,
@@ -513,7 +525,7 @@ __global__ __launch_bounds__(256) void quant_rows_i8_kernel(const __bf16* __rest
                                                             float* __restrict__ xtn,
                                                             float* __restrict__ bounds) {
   __shared__ float red[2][4];
-  constexpr int D = 384, PER = D / 64;
+  constexpr int PER = D / 64;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int row = blockIdx.x * 4 + w;
   if (row >= n) {   // (block-uniform barrier below: idle waves report zeros)
@@ -576,12 +588,13 @@ __global__ __launch_bounds__(256) void quant_rows_i8_kernel(const __bf16* __rest
 //   q8   = the query's int8 image, sq its scale (exactly as quant_rows_i8_kernel)
 //   thr  = (T - (|q| E + |q - q~| X + 1e-5)) / sq, (E, X) = bounds (the shard's tracked maxima),
 // i.e. the threshold index_scan_i8_kernel emits against (see the bound at the top of this file).
+template <int D>
 __global__ __launch_bounds__(256) void prune_qprep_kernel(
     const __bf16* __restrict__ Q, int NQ, const float* __restrict__ pre_s,
     const float* __restrict__ tail_s, int k, float thr_margin, const float* __restrict__ bounds,
     int8_t* __restrict__ Q8, float* __restrict__ sq, float* __restrict__ T_out,
     float* __restrict__ thr) {
-  constexpr int D = 384, PER = D / 64;
+  constexpr int PER = D / 64;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int q = blockIdx.x * 4 + w;
   if (q >= NQ) return;   // (no barrier in this kernel)
@@ -658,12 +671,13 @@ __global__ __launch_bounds__(256) void prune_qprep_kernel(
 //                 (skip[b]), the bf16 scan at the exact threshold T scans only them, and both
 //                 emit into the same candidate buffers: every row is covered by exactly one
 //                 exact-bound scan.  Exactness never depends on the route; only the cost does.
+template <int D>
 __global__ __launch_bounds__(256) void prune_qquant_kernel(const __bf16* __restrict__ Q, int NQ,
                                                            const float* __restrict__ bounds,
                                                            int8_t* __restrict__ Q8,
                                                            float* __restrict__ sq,
                                                            float* __restrict__ margin) {
-  constexpr int D = 384, PER = D / 64;
+  constexpr int PER = D / 64;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int q = blockIdx.x * 4 + w;
   if (q >= NQ) return;   // (no barrier in this kernel)
@@ -869,51 +883,56 @@ int symb_i8_queries_per_blk(int rsplit) {
   return g_i8_waves == 4 ? 4 * 16 * i8s::SETS : i8s::WAVES / rsplit * 16 * i8s::SETS;
 }
 
-template <int RSPLIT, int TRK, int WV = 8>
+template <int D, int RSPLIT, int TRK, int WV = 8>
 static int launch_i8(const void* X8, const float* sx, int n_valid, int rows_per_blk, int n_rblk,
                      const void* Q8, int NQ, const float* thr, float* cand_s, int* cand_i,
                      int* cand_n, int cap, int xcd, hipStream_t st, const int* skip) {
   constexpr int qpb = WV / RSPLIT * 16 * i8s::SETS;
   const int n_qblk = (NQ + qpb - 1) / qpb;
-  constexpr int lds = i8s::Geo<TRK, WV>::LDS_BYTES;
-  set_max_lds<index_scan_i8_kernel<RSPLIT, 0, TRK, WV>>(lds);
-  hipLaunchKernelGGL((index_scan_i8_kernel<RSPLIT, 0, TRK, WV>), dim3(n_rblk * n_qblk), dim3(64 * WV), lds, st,
-                     (const int8_t*)X8, sx, n_valid, rows_per_blk, (const int8_t*)Q8, NQ, n_qblk,
-                     xcd, thr, cand_s, cand_i, cand_n, cap, skip);
+  constexpr int lds = Geo<D, TRK, WV>::LDS_BYTES;
+  set_max_lds<index_scan_i8_kernel<D, RSPLIT, 0, TRK, WV>>(lds);
+  hipLaunchKernelGGL((index_scan_i8_kernel<D, RSPLIT, 0, TRK, WV>), dim3(n_rblk * n_qblk),
+                     dim3(64 * WV), lds, st, (const int8_t*)X8, sx, n_valid, rows_per_blk,
+                     (const int8_t*)Q8, NQ, n_qblk, xcd, thr, cand_s, cand_i, cand_n, cap, skip);
   return (int)hipGetLastError();
 }
 
+// Tile rows the D-wide scan runs with (the 128-row and 4-wave forms are D = 384 knobs).
+int symb_i8_tile_rows_for(int dim) { return dim == 384 ? g_i8_tr : 64; }
+
 // rows_per_blk % tile rows == 0, n_rblk * rows_per_blk >= n_valid; X8 / sx hold alloc_rows
 // rows, which must cover n_valid rounded up to a whole tile (the DMA reads whole tiles).
-// rsplit 2 = 256 queries per workgroup, 1 = 512.
+// rsplit 2 = 256 queries per workgroup, 1 = 512.  dim: 384 or 768.
 int symb_index_scan_i8(const void* X8, const float* sx, int n_valid, int alloc_rows,
                        int rows_per_blk, int n_rblk, const void* Q8, int NQ, const float* thr,
                        float* cand_s, int* cand_i, int* cand_n, int cap, int xcd, hipStream_t st,
-                       int rsplit, const int* skip) {
+                       int rsplit, const int* skip, int dim) {
   if (NQ <= 0) return 0;
-  const int tr = g_i8_tr;
+  if (dim != 384 && dim != 768) return -1;
+  const int tr = symb_i8_tile_rows_for(dim);
   if (rows_per_blk % tr || n_rblk <= 0 || thr == nullptr || cap <= 0 || n_valid <= 0) return -1;
   if ((long long)n_rblk * rows_per_blk < n_valid) return -1;
   if ((long long)(n_valid + tr - 1) / tr * tr > alloc_rows) return -1;   // a tile past the buffer
   hipError_t e = hipMemsetAsync(cand_n, 0, sizeof(int) * (size_t)NQ, st);
   if (e != hipSuccess) return (int)e;
-#define SYMB_I8(RS, T) launch_i8<RS, T>(X8, sx, n_valid, rows_per_blk, n_rblk, Q8, NQ, thr, cand_s, \
-                                        cand_i, cand_n, cap, xcd, st, skip)
+#define SYMB_I8(D_, RS, T) launch_i8<D_, RS, T>(X8, sx, n_valid, rows_per_blk, n_rblk, Q8, NQ, thr, \
+                                                cand_s, cand_i, cand_n, cap, xcd, st, skip)
+  if (dim == 768) return rsplit == 2 ? SYMB_I8(768, 2, 64) : SYMB_I8(768, 1, 64);
   if (g_i8_waves == 4)
-    return launch_i8<1, 64, 4>(X8, sx, n_valid, rows_per_blk, n_rblk, Q8, NQ, thr, cand_s, cand_i,
-                               cand_n, cap, xcd, st, skip);
-  if (rsplit == 2) return tr == 128 ? SYMB_I8(2, 128) : SYMB_I8(2, 64);
+    return launch_i8<384, 1, 64, 4>(X8, sx, n_valid, rows_per_blk, n_rblk, Q8, NQ, thr, cand_s,
+                                    cand_i, cand_n, cap, xcd, st, skip);
+  if (rsplit == 2) return tr == 128 ? SYMB_I8(384, 2, 128) : SYMB_I8(384, 2, 64);
   // 512 queries per workgroup always run 64-row tiles: the 128-row form (four fused two-sub-tile
   // chains per wave per tile) emitted a few rows per million with wrong scores, differently from
   // run to run (benchmarks/diag/i8_determinism.py: 1100 queries, candidate totals 1317690 ..
   // 1317766 against a constant 1317699 for every other form, profiles/r3_blockroute/), so it is
   // not dispatched until that race is found
-  if (rsplit == 1) return SYMB_I8(1, 64);
+  if (rsplit == 1) return SYMB_I8(384, 1, 64);
 #undef SYMB_I8
   return -1;
 }
 
-// Profiling-only entry: the ablations of index_scan_i8_kernel<2> (ABL above), same arguments.
+// Profiling-only entry: the ablations of index_scan_i8_kernel<384, 2> (ABL above), same arguments.
 int symb_index_scan_i8_ablate(const void* X8, const float* sx, int n_valid, int alloc_rows,
                               int rows_per_blk, int n_rblk, const void* Q8, int NQ,
                               const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
@@ -927,8 +946,8 @@ int symb_index_scan_i8_ablate(const void* X8, const float* sx, int n_valid, int 
   if (e != hipSuccess) return (int)e;
   const int n_qblk = (NQ + 255) / 256;
   const int w4 = g_i8_waves == 4;
-  const int lds = w4 ? i8s::Geo<64, 4>::LDS_BYTES
-                     : (tr == 128 ? i8s::Geo<128>::LDS_BYTES : i8s::Geo<64>::LDS_BYTES);
+  const int lds = w4 ? Geo<384, 64, 4>::LDS_BYTES
+                     : (tr == 128 ? Geo<384, 128>::LDS_BYTES : Geo<384, 64>::LDS_BYTES);
   auto go = [&](auto kern) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipLaunchKernelGGL(kern, dim3(n_rblk * n_qblk), dim3(w4 ? 256 : 512), lds, st, (const int8_t*)X8, sx,
@@ -938,43 +957,60 @@ int symb_index_scan_i8_ablate(const void* X8, const float* sx, int n_valid, int 
   };
   if (w4) {
     switch (abl) {
-      case 0: return go(index_scan_i8_kernel<1, 0, 64, 4>);
-      case 2: return go(index_scan_i8_kernel<1, 2, 64, 4>);
-      case 3: return go(index_scan_i8_kernel<1, 3, 64, 4>);
-      case 4: return go(index_scan_i8_kernel<1, 4, 64, 4>);
+      case 0: return go(index_scan_i8_kernel<384, 1, 0, 64, 4>);
+      case 2: return go(index_scan_i8_kernel<384, 1, 2, 64, 4>);
+      case 3: return go(index_scan_i8_kernel<384, 1, 3, 64, 4>);
+      case 4: return go(index_scan_i8_kernel<384, 1, 4, 64, 4>);
       default: return -1;
     }
   }
   switch (abl + (tr == 128 ? 8 : 0)) {
-    case 0: return go(index_scan_i8_kernel<2, 0, 64>);
-    case 1: return go(index_scan_i8_kernel<2, 1, 64>);
-    case 2: return go(index_scan_i8_kernel<2, 2, 64>);
-    case 3: return go(index_scan_i8_kernel<2, 3, 64>);
-    case 4: return go(index_scan_i8_kernel<2, 4, 64>);
-    case 8: return go(index_scan_i8_kernel<2, 0, 128>);
-    case 9: return go(index_scan_i8_kernel<2, 1, 128>);
-    case 10: return go(index_scan_i8_kernel<2, 2, 128>);
-    case 11: return go(index_scan_i8_kernel<2, 3, 128>);
-    case 12: return go(index_scan_i8_kernel<2, 4, 128>);
+    case 0: return go(index_scan_i8_kernel<384, 2, 0, 64>);
+    case 1: return go(index_scan_i8_kernel<384, 2, 1, 64>);
+    case 2: return go(index_scan_i8_kernel<384, 2, 2, 64>);
+    case 3: return go(index_scan_i8_kernel<384, 2, 3, 64>);
+    case 4: return go(index_scan_i8_kernel<384, 2, 4, 64>);
+    case 8: return go(index_scan_i8_kernel<384, 2, 0, 128>);
+    case 9: return go(index_scan_i8_kernel<384, 2, 1, 128>);
+    case 10: return go(index_scan_i8_kernel<384, 2, 2, 128>);
+    case 11: return go(index_scan_i8_kernel<384, 2, 3, 128>);
+    case 12: return go(index_scan_i8_kernel<384, 2, 4, 128>);
     default: return -1;
   }
 }
 
+// launch F(D) for the shard's row width (D = 384 / 768 / 1024); -1 for any other
+#define SYMB_BY_DIM(dim, F)      \
+  do {                           \
+    if ((dim) == 384) {          \
+      F(384);                    \
+    } else if ((dim) == 768) {   \
+      F(768);                    \
+    } else if ((dim) == 1024) {  \
+      F(1024);                   \
+    } else {                     \
+      return -1;                 \
+    }                            \
+  } while (0)
+
 int symb_rescore_bf16(const void* X, const void* Q, int NQ, int dim, const int* cand_i,
                       const int* cand_n, int cap, float* cand_s, hipStream_t st) {
   if (NQ <= 0) return 0;
-  if (dim != 384 || cap <= 0) return -1;
-  hipLaunchKernelGGL(rescore_bf16_kernel, dim3(NQ, 8), dim3(256), 0, st, (const __bf16*)X,
-                     (const __bf16*)Q, cand_i, cand_n, cap, cand_s);
+  if (cap <= 0) return -1;
+#define L(D_) hipLaunchKernelGGL(rescore_bf16_kernel<D_>, dim3(NQ, 8), dim3(256), 0, st, \
+                                 (const __bf16*)X, (const __bf16*)Q, cand_i, cand_n, cap, cand_s)
+  SYMB_BY_DIM(dim, L);
+#undef L
   return (int)hipGetLastError();
 }
 
 int symb_quant_rows_i8(const void* X, int n, int dim, void* X8, float* sx, float* err, float* xtn,
                        float* bounds, hipStream_t st) {
   if (n <= 0) return 0;
-  if (dim != 384) return -1;
-  hipLaunchKernelGGL(quant_rows_i8_kernel, dim3((n + 3) / 4), dim3(256), 0, st, (const __bf16*)X,
-                     n, (int8_t*)X8, sx, err, xtn, bounds);
+#define L(D_) hipLaunchKernelGGL(quant_rows_i8_kernel<D_>, dim3((n + 3) / 4), dim3(256), 0, st, \
+                                 (const __bf16*)X, n, (int8_t*)X8, sx, err, xtn, bounds)
+  SYMB_BY_DIM(dim, L);
+#undef L
   return (int)hipGetLastError();
 }
 
@@ -982,20 +1018,25 @@ int symb_prune_qprep(const void* Q, int NQ, int dim, const float* pre_s, const f
                      float thr_margin, const float* bounds, void* Q8, float* sq, float* T,
                      float* thr, hipStream_t st) {
   if (NQ <= 0) return 0;
-  if (dim != 384 || k < 1 || k > 32) return -1;
-  hipLaunchKernelGGL(prune_qprep_kernel, dim3((NQ + 3) / 4), dim3(256), 0, st, (const __bf16*)Q,
-                     NQ, pre_s, tail_s, k, thr_margin, bounds, (int8_t*)Q8, sq, T, thr);
+  if (k < 1 || k > 32) return -1;
+#define L(D_) hipLaunchKernelGGL(prune_qprep_kernel<D_>, dim3((NQ + 3) / 4), dim3(256), 0, st, \
+                                 (const __bf16*)Q, NQ, pre_s, tail_s, k, thr_margin, bounds,     \
+                                 (int8_t*)Q8, sq, T, thr)
+  SYMB_BY_DIM(dim, L);
+#undef L
   return (int)hipGetLastError();
 }
 
 int symb_prune_qquant(const void* Q, int NQ, int dim, const float* bounds, void* Q8, float* sq,
                       float* margin, hipStream_t st) {
   if (NQ <= 0) return 0;
-  if (dim != 384) return -1;
-  hipLaunchKernelGGL(prune_qquant_kernel, dim3((NQ + 3) / 4), dim3(256), 0, st, (const __bf16*)Q,
-                     NQ, bounds, (int8_t*)Q8, sq, margin);
+#define L(D_) hipLaunchKernelGGL(prune_qquant_kernel<D_>, dim3((NQ + 3) / 4), dim3(256), 0, st, \
+                                 (const __bf16*)Q, NQ, bounds, (int8_t*)Q8, sq, margin)
+  SYMB_BY_DIM(dim, L);
+#undef L
   return (int)hipGetLastError();
 }
+#undef SYMB_BY_DIM
 
 // The per-block route (prune_route_kernel + prune_route_final_kernel).  dense (one int) ends 1
 // iff every block went to the bf16 scan; blk holds 2 + 2 n_rblk ints (layout at the final

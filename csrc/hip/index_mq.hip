@@ -1,5 +1,5 @@
-// Multi-query-block fused scan for D = 384 bf16 shards: the per-rank shape of the sharded search
-// at N >= 2 GPUs (every rank scores the 256*N all-gathered queries against its 100M/N rows;
+// Multi-query-block fused scan for bf16 shards of D = 384 / 768 / 1024: the per-rank shape of the
+// sharded search at N >= 2 GPUs (every rank scores the 256*N all-gathered queries against its 100M/N rows;
 // SURVEY.md §2.5 X2, §2.6 index sharding).  Complements index_topk.hip, whose kernel holds 256
 // queries per workgroup and keeps per-lane top-k lists in registers.
 //
@@ -38,34 +38,39 @@
 namespace symb {
 
 namespace mq {
-constexpr int D = 384;
 constexpr int WAVES = 8;
-// query sets (16 queries each) per wave: a kernel template parameter NSET, 4 (512 queries per
-// workgroup: 192 registers of queries) or 2 (256 per workgroup, for 256-query batches)
 constexpr int SUB = 16;                     // rows per MFMA chain
-constexpr int TR = 64;                      // rows per barrier interval (tile)
-constexpr int NSUB = TR / SUB;
-constexpr int NS = 3;                       // LDS ring depth in tiles
-constexpr int CPR = D / 8;                  // 16-byte chunks per row
-constexpr int TILE_BYTES = TR * D * 2;      // 48 KiB
-constexpr int SUB_BYTES = SUB * D * 2;
-constexpr int LOADS = TILE_BYTES / (1024 * WAVES);  // LDS-DMA pieces per wave per tile (6)
-constexpr int NKS = D / 32;                 // 16x16x32 k-steps over D (12)
 constexpr int PIECE = 1024;                 // LDS bytes per (sub-tile, k-step) piece
 constexpr int PF = 3;                       // fragment reads in flight
 constexpr int R = PF + 1;                   // fragment ring slots
-constexpr int DMA_EVERY = 2;                // k-steps between DMA pieces in sub-tile 0
-static_assert(TILE_BYTES % (1024 * WAVES) == 0, "tile must split evenly over waves");
-static_assert(NSUB * NKS * PIECE == TILE_BYTES, "a tile is NSUB x NKS pieces");
-static_assert(LOADS * DMA_EVERY <= NKS, "DMA pieces must fit the first chain");
-static_assert(NS * TILE_BYTES <= 160 * 1024, "LDS ring exceeds the CU's 160 KiB");
 // per-wave candidate stage in LDS after the ring: score f32, row i32, query-in-wave u16
 constexpr int STW = 192;                    // staged candidates per wave (flushed past STW - 64)
 constexpr int STAGE_BYTES = STW * 10;
-constexpr int LDS_BYTES = NS * TILE_BYTES + WAVES * STAGE_BYTES;
-static_assert(LDS_BYTES <= 160 * 1024, "ring + stages exceed the CU's 160 KiB");
-static_assert(NKS % R == 0, "cross-chain prefetch: fragment j of the next chain must use slot j % R");
 }  // namespace mq
+
+// Geometry per row width.  Queries stay resident as B fragments: SETS x D/32 k-steps x 4 VGPRs,
+// at most 192 of a wave's 256 registers, so the query sets per wave shrink as D grows --
+//   D = 384 : 64-row tiles (48 KiB), 3-deep ring, up to 4 sets (512 queries per workgroup);
+//   D = 768 : 32-row tiles (48 KiB), 3-deep ring, 2 sets (256 queries: the reference's 768-d
+//             collection, vector_memory_service/src/main.rs:22);
+//   D = 1024: 16-row tiles (32 KiB), 4-deep ring, 1 set (128 queries).
+template <int D> struct MqGeo {
+  static constexpr int NKS = D / 32;                    // 16x16x32 k-steps over D
+  static constexpr int TR = D == 384 ? 64 : D == 768 ? 32 : 16;   // rows per barrier interval
+  static constexpr int NSUB = TR / mq::SUB;
+  static constexpr int NS = D == 1024 ? 4 : 3;          // LDS ring depth in tiles
+  static constexpr int TILE_BYTES = TR * D * 2;
+  static constexpr int LOADS = TILE_BYTES / (1024 * mq::WAVES);  // LDS-DMA pieces per wave per tile
+  static constexpr int DMA_EVERY = NKS / LOADS;         // k-steps between DMA pieces in sub-tile 0
+  static constexpr int MAX_SETS = D == 384 ? 4 : D == 768 ? 2 : 1;
+  static constexpr int LDS_BYTES = NS * TILE_BYTES + mq::WAVES * mq::STAGE_BYTES;
+  static_assert(D == 384 || D == 768 || D == 1024, "row width");
+  static_assert(TILE_BYTES % (1024 * mq::WAVES) == 0, "tile must split evenly over waves");
+  static_assert(NSUB * NKS * mq::PIECE == TILE_BYTES, "a tile is NSUB x NKS pieces");
+  static_assert(LOADS * DMA_EVERY <= NKS && DMA_EVERY >= 1, "DMA pieces must fit the first chain");
+  static_assert(LDS_BYTES <= 160 * 1024, "ring + stages exceed the CU's 160 KiB");
+  static_assert(NKS % mq::R == 0, "cross-chain prefetch: fragment j of the next chain must use slot j % R");
+};
 
 template <int OFF>
 __device__ __forceinline__ void mq_read16(bf16x8& dst, uint32_t addr) {
@@ -91,11 +96,12 @@ __device__ __forceinline__ void mq_mfma(f32x4& acc, const bf16x8& a, const bf16x
 // refill the ring slot PF steps ahead -- in the last PF steps with the first fragments of the
 // NEXT sub-tile (at ``next``, when NEXT), so its chain starts without an LDS round trip.
 // DMA(i) issues LDS-DMA piece i of a later tile.
-template <int KS, int DMA_PIECES, bool NEXT, int SETS>
+template <int D, int KS, int DMA_PIECES, bool NEXT, int SETS>
 struct MqChain {
+  static constexpr int NKS = MqGeo<D>::NKS, DMA_EVERY = MqGeo<D>::DMA_EVERY;
   template <class Dma>
   __device__ __forceinline__ static void run(f32x4 (&acc)[SETS], bf16x8 (&a)[mq::R],
-                                             const bf16x8 (&qf)[SETS][mq::NKS],
+                                             const bf16x8 (&qf)[SETS][NKS],
                                              uint32_t base, uint32_t next, const Dma& dma) {
     using namespace mq;
     if constexpr (DMA_PIECES > 0 && KS % DMA_EVERY == 0 && KS / DMA_EVERY < DMA_PIECES)
@@ -113,7 +119,7 @@ struct MqChain {
     else if constexpr (NEXT)  // fragment KS + PF - NKS of the next sub-tile, same ring slot order
       mq_read16<(KS + PF - NKS) * PIECE>(a[(KS + PF) % R], next);
     if constexpr (KS + 1 < NKS)
-      MqChain<KS + 1, DMA_PIECES, NEXT, SETS>::run(acc, a, qf, base, next, dma);
+      MqChain<D, KS + 1, DMA_PIECES, NEXT, SETS>::run(acc, a, qf, base, next, dma);
   }
 };
 
@@ -162,7 +168,7 @@ struct MqList {
   int list_tiles;
 };
 
-template <int NSET, int ABL = 0, int RSPLIT = 1, int AUX = 0>
+template <int D, int NSET, int ABL = 0, int RSPLIT = 1, int AUX = 0>
 __global__ __launch_bounds__(512, 1) void index_scan_mq_kernel(
     const __bf16* __restrict__ X, int n_valid, int rows_per_blk, const __bf16* __restrict__ Q,
     int NQ, int n_qblk, int xcd, const float* __restrict__ thr_in, float* __restrict__ cand_s,
@@ -171,9 +177,13 @@ __global__ __launch_bounds__(512, 1) void index_scan_mq_kernel(
   // gate (optional): run only if *gate != 0 -- the pruned search's bf16 route (index_i8.hip)
   if (gate != nullptr && *gate == 0) return;
   using namespace mq;
+  using G = MqGeo<D>;
+  constexpr int NKS = G::NKS, TR = G::TR, NSUB = G::NSUB, NS = G::NS;
+  constexpr int TILE_BYTES = G::TILE_BYTES, LOADS = G::LOADS;
   constexpr int SETS = NSET, QW = SETS * 16, QWAVES = WAVES / RSPLIT, QPB = QWAVES * QW;
   constexpr int NSW = NSUB / RSPLIT;          // 16-row sub-tiles per wave per tile
-  static_assert(RSPLIT == 1 || RSPLIT == 2, "row split");
+  static_assert(RSPLIT == 1 || (RSPLIT == 2 && NSUB % 2 == 0), "row split");
+  static_assert(SETS >= 1 && SETS <= G::MAX_SETS, "query registers");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lb = xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
@@ -378,19 +388,19 @@ __global__ __launch_bounds__(512, 1) void index_scan_mq_kernel(
     prow_last = prow0;
     const uint32_t fw = fb + j0 * NKS * PIECE;
     if constexpr (NSW > 1)
-      MqChain<0, LOADS, true, SETS>::run(acc, a, qf, fw, fw + NKS * PIECE, dma);
+      MqChain<D, 0, LOADS, true, SETS>::run(acc, a, qf, fw, fw + NKS * PIECE, dma);
     else
-      MqChain<0, LOADS, false, SETS>::run(acc, a, qf, fw, 0, dma);
+      MqChain<D, 0, LOADS, false, SETS>::run(acc, a, qf, fw, 0, dma);
 #pragma unroll
     for (int j = 1; j < NSW; ++j) {
       // sub-tile j's first fragments were read by the previous chain's tail and fly while this
       // wave tests the previous sub-tile's scores
       emit(acc, row0 + (j0 + j - 1) * SUB, prow0 + (j0 + j - 1) * SUB);
       if (j + 1 < NSW)
-        MqChain<0, 0, true, SETS>::run(acc, a, qf, fw + j * NKS * PIECE, fw + (j + 1) * NKS * PIECE,
-                                 NoDma());
+        MqChain<D, 0, 0, true, SETS>::run(acc, a, qf, fw + j * NKS * PIECE,
+                                          fw + (j + 1) * NKS * PIECE, NoDma());
       else
-        MqChain<0, 0, false, SETS>::run(acc, a, qf, fw + j * NKS * PIECE, 0, NoDma());
+        MqChain<D, 0, 0, false, SETS>::run(acc, a, qf, fw + j * NKS * PIECE, 0, NoDma());
     }
     if (!late) emit(acc, row0 + last, prow0 + last);
   }
@@ -620,6 +630,11 @@ __global__ __launch_bounds__(sel::NTH) void topk_select_radix_kernel(
 using namespace symb;
 
 int symb_mq_queries_per_blk(int sets, int rsplit) { return mq::WAVES / rsplit * 16 * sets; }
+// Query sets per wave the D-wide form holds (its 16-query sets x D/32 k-steps stay in registers)
+int symb_mq_max_sets(int dim) {
+  return dim == 384 ? MqGeo<384>::MAX_SETS : dim == 768 ? MqGeo<768>::MAX_SETS
+                                                        : dim == 1024 ? MqGeo<1024>::MAX_SETS : 0;
+}
 
 // rows_per_blk must be a multiple of 64; n_rblk * rows_per_blk >= n_valid.  cand_n is zeroed here.
 // cache policy of the row stream (symb_mq_config): 0 default, 2 non-temporal
@@ -630,75 +645,81 @@ int symb_mq_config(int aux) {
   return 0;
 }
 
-template <int NSET, int RSPLIT, int AUX>
+template <int D, int NSET, int RSPLIT, int AUX>
 static int launch_mq_aux(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                      int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
                      int xcd, hipStream_t st, int tshift, const int* gate, MqList lst) {
   constexpr int qpb = mq::WAVES / RSPLIT * 16 * NSET;
   const int n_qblk = (NQ + qpb - 1) / qpb;
-  constexpr int lds = mq::LDS_BYTES;
-  set_max_lds<index_scan_mq_kernel<NSET, 0, RSPLIT, AUX>>(lds);
-  hipLaunchKernelGGL((index_scan_mq_kernel<NSET, 0, RSPLIT, AUX>), dim3(n_rblk * n_qblk), dim3(512),
-                     lds, st, (const __bf16*)X, n_valid, rows_per_blk, (const __bf16*)Q, NQ, n_qblk,
-                     xcd, thr, cand_s, cand_i, cand_n, cap, tshift, gate, lst);
+  constexpr int lds = MqGeo<D>::LDS_BYTES;
+  set_max_lds<index_scan_mq_kernel<D, NSET, 0, RSPLIT, AUX>>(lds);
+  hipLaunchKernelGGL((index_scan_mq_kernel<D, NSET, 0, RSPLIT, AUX>), dim3(n_rblk * n_qblk),
+                     dim3(512), lds, st, (const __bf16*)X, n_valid, rows_per_blk, (const __bf16*)Q,
+                     NQ, n_qblk, xcd, thr, cand_s, cand_i, cand_n, cap, tshift, gate, lst);
   return (int)hipGetLastError();
 }
 
-template <int NSET, int RSPLIT>
+template <int D, int NSET, int RSPLIT>
 static int launch_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                      int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
                      int xcd, hipStream_t st, int tshift, const int* gate, MqList lst) {
   return g_mq_aux == 2
-             ? launch_mq_aux<NSET, RSPLIT, 2>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, thr, cand_s,
-                                             cand_i, cand_n, cap, xcd, st, tshift, gate, lst)
-             : launch_mq_aux<NSET, RSPLIT, 0>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, thr, cand_s,
-                                             cand_i, cand_n, cap, xcd, st, tshift, gate, lst);
+             ? launch_mq_aux<D, NSET, RSPLIT, 2>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, thr,
+                                                 cand_s, cand_i, cand_n, cap, xcd, st, tshift,
+                                                 gate, lst)
+             : launch_mq_aux<D, NSET, RSPLIT, 0>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, thr,
+                                                 cand_s, cand_i, cand_n, cap, xcd, st, tshift,
+                                                 gate, lst);
 }
 
+// dim: 384 (sets 4 or 2; rsplit 2 with sets 4), 768 (sets 2), 1024 (sets 1); rsplit 1 otherwise.
 // tshift: 0 = rows [0, n_valid); k > 0 = virtual rows of a 1-in-2^k tile sample (kernel note).
-// sets: 16-query sets per wave, 4 or 2; rsplit: waves sharing each query group (1, or 2 = the
-// row-split form, sets 4 only).  Queries per workgroup: 8 / rsplit * 16 * sets (512 or 256).
+// Queries per workgroup: 8 / rsplit * 16 * sets.
 // blist (optional, list mode): scan the row blocks listed there (MqList; list_tiles 64-row tiles
 // each, rows >= n_valid never scanned) instead of rows [0, n_valid); rows_per_blk is then unused
-// and the n_rblk row slots of the grid share the listed rows.  zero_cnt = 0 appends to cand_n (another
-// scan's candidates already there) instead of zeroing it.
+// and the n_rblk row slots of the grid share the listed rows.  zero_cnt = 0 appends to cand_n
+// (another scan's candidates already there) instead of zeroing it.
 int symb_index_scan_mq(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                        int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
                        int xcd, hipStream_t st, int sets, int tshift, int rsplit,
-                       const int* gate, const int* blist, int list_tiles, int zero_cnt) {
+                       const int* gate, const int* blist, int list_tiles, int zero_cnt, int dim) {
   if (NQ <= 0) return 0;
-  if (rows_per_blk % mq::TR || n_rblk <= 0 || thr == nullptr || cap <= 0) return -1;
-  if ((sets != 2 && sets != 4) || tshift < 0 || tshift > 12) return -1;
-  if (rsplit != 1 && !(rsplit == 2 && sets == 4)) return -1;
+  if (rows_per_blk % 64 || n_rblk <= 0 || thr == nullptr || cap <= 0) return -1;
+  if (tshift < 0 || tshift > 12) return -1;
+  if (dim == 384 && ((sets != 2 && sets != 4) || (rsplit != 1 && !(rsplit == 2 && sets == 4))))
+    return -1;
+  if (dim == 768 && (sets != 2 || rsplit != 1)) return -1;
+  if (dim == 1024 && (sets != 1 || rsplit != 1)) return -1;
+  if (dim != 384 && dim != 768 && dim != 1024) return -1;
   if (blist != nullptr && (tshift != 0 || list_tiles <= 0 || n_valid <= 0)) return -1;
   MqList lst{blist, list_tiles};
   if (zero_cnt) {
     hipError_t e = hipMemsetAsync(cand_n, 0, sizeof(int) * (size_t)NQ, st);
     if (e != hipSuccess) return (int)e;
   }
-  if (rsplit == 2)
-    return launch_mq<4, 2>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, thr, cand_s, cand_i, cand_n,
-                           cap, xcd, st, tshift, gate, lst);
-  return sets == 4 ? launch_mq<4, 1>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, thr, cand_s, cand_i,
-                                     cand_n, cap, xcd, st, tshift, gate, lst)
-                   : launch_mq<2, 1>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, thr, cand_s, cand_i,
-                                     cand_n, cap, xcd, st, tshift, gate, lst);
+#define SYMB_MQ(D_, S_, R_) launch_mq<D_, S_, R_>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, thr, \
+                                                 cand_s, cand_i, cand_n, cap, xcd, st, tshift, gate, lst)
+  if (dim == 768) return SYMB_MQ(768, 2, 1);
+  if (dim == 1024) return SYMB_MQ(1024, 1, 1);
+  if (rsplit == 2) return SYMB_MQ(384, 4, 2);
+  return sets == 4 ? SYMB_MQ(384, 4, 1) : SYMB_MQ(384, 2, 1);
+#undef SYMB_MQ
 }
 
-// Profiling-only entry: the ablations of index_scan_mq_kernel (ABL above), same arguments.
+// Profiling-only entry: the ablations of index_scan_mq_kernel (ABL above), D = 384, same arguments.
 int symb_index_scan_mq_ablate(const void* X, int n_valid, int rows_per_blk, int n_rblk,
                               const void* Q, int NQ, const float* thr, float* cand_s, int* cand_i,
                               int* cand_n, int cap, int xcd, hipStream_t st, int abl, int sets,
                               int rsplit) {
   if (NQ <= 0) return 0;
-  if (rows_per_blk % mq::TR || n_rblk <= 0 || thr == nullptr || cap <= 0) return -1;
+  if (rows_per_blk % 64 || n_rblk <= 0 || thr == nullptr || cap <= 0) return -1;
   if (sets != 2 && sets != 4) return -1;
   if (rsplit != 1 && !(rsplit == 2 && sets == 4)) return -1;
   hipError_t e = hipMemsetAsync(cand_n, 0, sizeof(int) * (size_t)NQ, st);
   if (e != hipSuccess) return (int)e;
   const int qpb = mq::WAVES / rsplit * 16 * sets;
   const int n_qblk = (NQ + qpb - 1) / qpb;
-  constexpr int lds = mq::LDS_BYTES;
+  constexpr int lds = MqGeo<384>::LDS_BYTES;
   auto go = [&](auto kern) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipLaunchKernelGGL(kern, dim3(n_rblk * n_qblk), dim3(512), lds, st, (const __bf16*)X,
@@ -707,21 +728,21 @@ int symb_index_scan_mq_ablate(const void* X, int n_valid, int rows_per_blk, int 
     return (int)hipGetLastError();
   };
   switch (abl + 8 * (sets == 2) + 16 * (rsplit == 2)) {
-    case 0: return go(index_scan_mq_kernel<4, 0>);
-    case 1: return go(index_scan_mq_kernel<4, 1>);
-    case 2: return go(index_scan_mq_kernel<4, 2>);
-    case 3: return go(index_scan_mq_kernel<4, 3>);
-    case 4: return go(index_scan_mq_kernel<4, 4>);
-    case 8: return go(index_scan_mq_kernel<2, 0>);
-    case 9: return go(index_scan_mq_kernel<2, 1>);
-    case 10: return go(index_scan_mq_kernel<2, 2>);
-    case 11: return go(index_scan_mq_kernel<2, 3>);
-    case 12: return go(index_scan_mq_kernel<2, 4>);
-    case 16: return go(index_scan_mq_kernel<4, 0, 2>);
-    case 17: return go(index_scan_mq_kernel<4, 1, 2>);
-    case 18: return go(index_scan_mq_kernel<4, 2, 2>);
-    case 19: return go(index_scan_mq_kernel<4, 3, 2>);
-    case 20: return go(index_scan_mq_kernel<4, 4, 2>);
+    case 0: return go(index_scan_mq_kernel<384, 4, 0>);
+    case 1: return go(index_scan_mq_kernel<384, 4, 1>);
+    case 2: return go(index_scan_mq_kernel<384, 4, 2>);
+    case 3: return go(index_scan_mq_kernel<384, 4, 3>);
+    case 4: return go(index_scan_mq_kernel<384, 4, 4>);
+    case 8: return go(index_scan_mq_kernel<384, 2, 0>);
+    case 9: return go(index_scan_mq_kernel<384, 2, 1>);
+    case 10: return go(index_scan_mq_kernel<384, 2, 2>);
+    case 11: return go(index_scan_mq_kernel<384, 2, 3>);
+    case 12: return go(index_scan_mq_kernel<384, 2, 4>);
+    case 16: return go(index_scan_mq_kernel<384, 4, 0, 2>);
+    case 17: return go(index_scan_mq_kernel<384, 4, 1, 2>);
+    case 18: return go(index_scan_mq_kernel<384, 4, 2, 2>);
+    case 19: return go(index_scan_mq_kernel<384, 4, 3, 2>);
+    case 20: return go(index_scan_mq_kernel<384, 4, 4, 2>);
     default: return -1;
   }
 }

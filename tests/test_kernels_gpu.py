@@ -643,18 +643,19 @@ def test_index_scan_mq_exact(nq, rsplit):
     _close(s1, true, atol=2e-3, what="mq returned rows")
 
 
-def test_quant_rows_i8_matches_reference():
+@pytest.mark.parametrize("D", [384, 768, 1024])
+def test_quant_rows_i8_matches_reference(D):
     """index_i8.hip's per-row int8 quantiser == the torch reference (scale, codes, error norms)."""
     from codename_symbiont_amd.ops._ext import hip, stream_handle
 
-    x = torch.nn.functional.normalize(_f(5003, 384, seed=61), dim=-1).bfloat16()
+    x = torch.nn.functional.normalize(_f(5003, D, seed=61), dim=-1).bfloat16()
     x[7] = 0   # a zero row keeps scale 1 and codes 0
-    q8 = torch.empty(5003, 384, dtype=torch.int8, device=DEV)
+    q8 = torch.empty(5003, D, dtype=torch.int8, device=DEV)
     sc = torch.empty(5003, device=DEV)
     err = torch.empty(5003, device=DEV)
     xtn = torch.empty(5003, device=DEV)
     bounds = torch.zeros(2, device=DEV)
-    hip().quant_rows_i8(x.data_ptr(), 5003, 384, q8.data_ptr(), sc.data_ptr(), err.data_ptr(),
+    hip().quant_rows_i8(x.data_ptr(), 5003, D, q8.data_ptr(), sc.data_ptr(), err.data_ptr(),
                         xtn.data_ptr(), stream_handle(), bounds.data_ptr())
     r8, rs, rerr, rxtn = R.quant_rows_i8_ref(x)
     torch.cuda.synchronize()
@@ -668,8 +669,9 @@ def test_quant_rows_i8_matches_reference():
     _close(xtn, xt.norm(dim=1), atol=1e-5, what="i8 |x~|")
 
 
+@pytest.mark.parametrize("D", [384, 768])
 @pytest.mark.parametrize("k", [1, 10, 16])
-def test_prune_qprep_matches_torch_composition(k):
+def test_prune_qprep_matches_torch_composition(k, D):
     """index_i8.hip prune_qprep (T = k-th best of the two lists, int8 query image, emission
     threshold in one launch) == the torch composition it replaced (_prune_thresholds_torch):
     unsorted lists, ties and -inf padding included."""
@@ -677,16 +679,16 @@ def test_prune_qprep_matches_torch_composition(k):
     from codename_symbiont_amd.ops._ext import hip, stream_handle
 
     nq, n = 301, 20000
-    shard = HbmIndexShard(384, n, prune="i8")
-    shard.append_f32(_f(n, 384, seed=81))
-    q = torch.nn.functional.normalize(_f(nq, 384, seed=82), dim=-1).bfloat16()
+    shard = HbmIndexShard(D, n, prune="i8")
+    shard.append_f32(_f(n, D, seed=81))
+    q = torch.nn.functional.normalize(_f(nq, D, seed=82), dim=-1).bfloat16()
     pre = _f(nq, k, seed=83).round(decimals=1)            # coarse values: ties across the lists
     tail = _f(nq, k, seed=84).round(decimals=1)
     pre[::7, k // 2:] = -math.inf                           # short lists (few sampled rows)
     tail[::5] = -math.inf
-    q8 = torch.empty(nq, 384, dtype=torch.int8, device=DEV)
+    q8 = torch.empty(nq, D, dtype=torch.int8, device=DEV)
     sq, T, thr = (torch.empty(nq, device=DEV) for _ in range(3))
-    hip().prune_qprep(q.data_ptr(), nq, 384, pre.data_ptr(), tail.data_ptr(), k,
+    hip().prune_qprep(q.data_ptr(), nq, D, pre.data_ptr(), tail.data_ptr(), k,
                       shard.MQ_THR_MARGIN, shard.i8_bounds.data_ptr(), q8.data_ptr(),
                       sq.data_ptr(), T.data_ptr(), thr.data_ptr(), stream_handle())
     T0, q80, sq0, thr0 = shard._prune_thresholds_torch(q, pre, tail, k)
@@ -745,6 +747,96 @@ def test_index_pruned_search_is_exact(nq, data, tr):
         assert (r0 == r1).float().mean().item() > 0.999
     true = (q.float() @ shard.unit_rows().float().t()).gather(1, r1.long())
     _close(s1, true, atol=2e-3, what="pruned returned rows")
+
+
+@pytest.mark.parametrize("D", [768, 1024])
+def test_index_scan_mq_wide_rows_exact(D):
+    """The emitting scan at the reference's 768-d (2 resident query sets, 32-row tiles) and at
+    1024-d (1 set, 16-row tiles, 4-deep ring): rows and scores of the list kernel / fp32 oracle,
+    no overflow on random data, ragged row count and query count."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+
+    n, k = (1 << 20) + 555, 10
+    shard = HbmIndexShard(D, n + 4096)
+    shard.fill_random(n, seed=33)
+    q = torch.nn.functional.normalize(_f(300, D, seed=34), dim=-1).bfloat16()
+    assert shard._seed_rows(n, k) and shard._mq_ok(300, k, shard.rows, "bf16")
+    shard.scan_mq = False
+    s0, r0 = shard.search(q, k)
+    shard.scan_mq = True
+    s1, r1 = shard.search(q, k)
+    cnt, ovf = shard._mq_last
+    torch.cuda.synchronize()
+    assert int(ovf.item()) == 0 and cnt.float().mean().item() > 0
+    _close(s1, s0, atol=1e-5, what=f"mq{D} vs list scores")
+    assert (r0 == r1).float().mean().item() > 0.999
+    true = (q.float() @ shard.unit_rows().float().t()).gather(1, r1.long())
+    _close(s1, true, atol=2e-3, what=f"mq{D} returned rows")
+
+
+@pytest.mark.parametrize("D", [768, 1024])
+@pytest.mark.parametrize("k", [10, 32, 100])
+def test_wide_index_topk_exact_vs_torch_topk(D, k):
+    """top-k at 768 / 1024-d for k = 10 (pruned at 768, emitting scan at 1024), 32 and 100 (the
+    large-k emitting scan + radix select, no GEMM fallback) == torch.topk over the fp32 scores,
+    with fresh near-duplicate rows in the tail (a query's own direction appended)."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard, resolve_prune
+
+    n = (1 << 20) + 321
+    shard = HbmIndexShard(D, n + 4096, prune=resolve_prune("auto", "bf16", D, device="cuda"))
+    shard.fill_random(n, seed=35)
+    q = torch.nn.functional.normalize(_f(256, D, seed=36), dim=-1).bfloat16()
+    shard.append_unit(q[:8])
+    calls = []
+    orig = shard._search_matmul
+    shard._search_matmul = lambda *a, **kw: calls.append(1) or orig(*a, **kw)
+    s, r = shard.search(q, k)
+    torch.cuda.synchronize()
+    assert not calls, "a k <= 128 search at this size must stay on the HIP scans"
+    sc = q.float() @ shard.unit_rows().float().t()
+    ts, ti = torch.topk(sc, k, dim=1)
+    _close(s, ts, atol=2e-5, what=f"D={D} k={k} scores")
+    _close(sc.gather(1, r.long()), ts, atol=2e-5, what=f"D={D} k={k} returned rows")
+    assert r[:8, 0].tolist() == list(range(n, n + 8))
+
+
+@pytest.mark.parametrize("nq,data", [(256, "random"), (300, "near"), (512, "random"),
+                                     (256, "clustered")])
+def test_index_pruned_search_768_is_exact(nq, data):
+    """The int8-pruned search at the reference's 768-d collection (12 i8 k-steps, 192 query
+    registers, single-sub-tile chains): the rows and scores of the exact bf16 scan."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+
+    n, k, D = (1 << 20) + 777, 10, 768
+    g = torch.Generator(device=DEV).manual_seed(72)
+    if data == "clustered":
+        centers = torch.randn(64, D, device=DEV, generator=g)
+        x = centers[torch.randint(0, 64, (n,), device=DEV, generator=g)]
+        x = x + 0.05 * torch.randn(n, D, device=DEV, generator=g)
+    else:
+        x = torch.randn(n, D, device=DEV, generator=g)
+    ref = HbmIndexShard(D, n + 4096)
+    shard = HbmIndexShard(D, n + 4096, prune="i8")
+    for sh in (ref, shard):
+        sh.append_f32(x)
+    del x
+    if data == "random":
+        q = torch.randn(nq, D, device=DEV, generator=g)
+    else:
+        q = ref.unit_rows()[torch.randint(0, n, (nq,), device=DEV, generator=g)].float()
+        q += (0.02 if data == "clustered" else 0.5 / math.sqrt(D)) * torch.randn_like(q)
+    q = torch.nn.functional.normalize(q, dim=-1).bfloat16()
+    s0, r0 = ref.search(q, k)
+    s1, r1 = shard.search(q, k)
+    cnt, ovf = shard._mq_last
+    torch.cuda.synchronize()
+    if data != "clustered":
+        assert int(ovf.item()) == 0
+    _close(s1, s0, atol=2e-5, what="pruned768 vs exact scores")
+    if data != "clustered":
+        assert (r0 == r1).float().mean().item() > 0.999
+    true = (q.float() @ shard.unit_rows().float().t()).gather(1, r1.long())
+    _close(s1, true, atol=2e-3, what="pruned768 returned rows")
 
 
 def test_prune_qquant_and_route_match_torch():
