@@ -195,10 +195,20 @@ def parse_args(argv=None):
                     help="--mode full: run each batch's query-side search work (int8 queries, "
                          "exact sample, thresholds) right before its scan instead of on a third "
                          "stream under the previous batch's scan")
+    ap.add_argument("--simulate-world", type=int, default=0,
+                    help="PROJECTION on one GPU: run the per-rank work of the N-GPU step (a 100M/N "
+                         "shard, 256*N gathered queries of which 256*(N-1) are foreign embeddings, "
+                         "the result-sized all_to_all through a single-rank RCCL group, the merge). "
+                         "The JSON says 'SIMULATED' and n_gpus stays 1; not a scaling measurement")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch the encoder's kernels eagerly every step instead of replaying a "
                          "captured hipGraph of the forward")
     args = ap.parse_args(argv)
+    if args.simulate_world == 1:
+        args.simulate_world = 0
+    if args.simulate_world and (args.gpus != 1 or args.mode == "embed"):
+        ap.error("--simulate-world projects the N-GPU search step on ONE GPU: --gpus 1, "
+                 "--mode full or search")
     if args.queries is None:
         args.queries = "heldout" if args.mode == "search" else "self"
     return args
@@ -247,7 +257,8 @@ def main(argv=None) -> int:
 
     from codename_symbiont_amd.parallel import dist as D
 
-    info = D.init(device_type=None if args.device == "auto" else args.device)
+    info = D.init(device_type=None if args.device == "auto" else args.device,
+                  single_rank_group=bool(args.simulate_world))
     if info.world != args.gpus:
         print(f"[bench] rank {info.rank}: --gpus {args.gpus} but the job has {info.world} "
               f"rank(s) (WORLD_SIZE={os.environ.get('WORLD_SIZE')}): refusing to report a "
@@ -264,7 +275,9 @@ def main(argv=None) -> int:
 
 
 def metric_and_config(args, info, cfg, prune, prefilter, extra_cfg: dict):
-    headline = (args.model in ("minilm-l6", "minilm", "all-MiniLM-L6-v2") and args.mode == "full"
+    vw = args.simulate_world or 0
+    headline = (not vw and args.model in ("minilm-l6", "minilm", "all-MiniLM-L6-v2")
+                and args.mode == "full"
                 and args.index_rows == 100_000_000 and args.index_dtype == "bf16"
                 and args.encoder_dtype == "bf16" and prefilter is None and args.corpus == "random"
                 and args.queries == "self" and info.device.type == "cuda")
@@ -279,6 +292,9 @@ def metric_and_config(args, info, cfg, prune, prefilter, extra_cfg: dict):
                   f"{args.batch} {args.queries} queries/rank"
                   + (" (fp8 prefilter + exact bf16 rescore)" if prefilter else "") + dist_txt,
     }[args.mode]
+    if vw:
+        metric = (f"SIMULATED {vw}-GPU per-rank step on 1 GPU (projection, not a measurement): "
+                  + metric)
     config = {
         "model": short, "global_batch": args.batch * info.world, "seq_len": args.seq,
         "parallelism": (f"dp{info.world}-rccl-group" if extra_cfg.pop("_group_dp", False)
@@ -289,6 +305,9 @@ def metric_and_config(args, info, cfg, prune, prefilter, extra_cfg: dict):
     if args.corpus == "clustered":
         config.update(clusters=args.clusters, cluster_spread=args.cluster_spread)
     config.update(extra_cfg)
+    if vw:
+        config.update(simulated_world=vw, parallelism=f"simulated dp{vw}+index_shard{vw} on 1 GPU",
+                      global_batch=args.batch * vw, index_rows_per_rank=args.index_rows // vw)
     unit = (f"embeds/s (whole job; every embedded sentence is also answered as a top-{args.k} "
             f"query over the {rows_txt} x {cfg.hidden} corpus, so this equals top-k QPS)"
             if args.mode == "full" else ("embeds/s" if args.mode == "embed" else "queries/s"))
@@ -323,6 +342,17 @@ def result_line(args, info, comm, metric, unit, config, total, ms, prune, prefil
                                           if args.mode != "search" else None),
     }
     res.update(extra)
+    vw = args.simulate_world or 0
+    if vw:
+        # value = the projected whole-job rate of the N-GPU job (N ranks each running this step);
+        # n_gpus stays the GPUs actually used
+        res.update(simulated=True, simulated_world=vw, value=round(total * vw, 2),
+                   projected_per_rank_ms=round(ms, 3),
+                   projected_job_rate=round(total * vw, 2),
+                   note="projection: per-rank step of the N-GPU job measured on one GPU; "
+                        "excludes xGMI transfer time and waiting for the slowest peer")
+        res["embeds_per_sec"] = round(total * vw, 2) if args.mode != "search" else 0.0
+        res["topk_qps"] = round(total * vw, 2) if args.mode != "embed" else 0.0
     return json.dumps(res)
 
 
@@ -336,6 +366,19 @@ def _data_txt(args) -> str:
     return f"synthetic token ids, random-init weights, {rows[args.corpus]}{q}"
 
 
+def _make_searcher(args, shard, info, embed):
+    """The step's sharded searcher; --simulate-world N: the per-rank work of the N-GPU search
+    on this one rank, the other ranks' queries stood in for by (N - 1) * batch foreign embeddings
+    (``embed(n, seed)``: n fresh sentences through this encoder, never inserted here)."""
+    from codename_symbiont_amd.parallel.sharded import ShardedSearcher, SimulatedShardedSearcher
+
+    vw = args.simulate_world or 0
+    if not vw:
+        return ShardedSearcher(shard, info)
+    foreign = [embed((vw - 1) * args.batch, 777_000 + j).bfloat16() for j in range(2)]
+    return SimulatedShardedSearcher(shard, info, vw, foreign)
+
+
 def run_cpu(args, info, comm) -> int:
     """The step on the CPU (gloo): encode -> upsert -> sharded search, timed the same way.  For the
     multi-rank contract tests only (fp32 PyTorch encoder, matmul search)."""
@@ -344,19 +387,20 @@ def run_cpu(args, info, comm) -> int:
     from codename_symbiont_amd.models import get_config
     from codename_symbiont_amd.models.encoder import TorchEncoder, synthetic_batch
     from codename_symbiont_amd.parallel import dist as D
-    from codename_symbiont_amd.parallel.sharded import ShardedSearcher
 
     torch.manual_seed(1234 + info.rank)
     cfg = get_config(args.model)
     B, S, K, W = args.batch, args.seq, args.steps, args.warmup
     enc = TorchEncoder(cfg, seed=0)
-    rows_per_rank = args.index_rows // info.world
+    vw = args.simulate_world or 0
+    rows_per_rank = args.index_rows // (vw or info.world)
     shard = HbmIndexShard(cfg.hidden, rows_per_rank + (K + W + 4) * B, device="cpu")
     gen = CorpusGen(args.corpus, cfg.hidden, "cpu", clusters=args.clusters,
                     spread=args.cluster_spread)
     if args.mode != "embed":
         fill_corpus(shard, gen, rows_per_rank, seed=100 + info.rank)
-    searcher = ShardedSearcher(shard, info)
+    searcher = _make_searcher(args, shard, info, lambda n, seed: enc.forward_packed(
+        synthetic_batch(cfg, n, S, seed=seed))[1])
     host = [synthetic_batch(cfg, B, S, seed=1000 * info.rank + i) for i in range(4)]
     qsets = [gen.unit(B, 5000 + 10 * info.rank + i).bfloat16() for i in range(4)]
 
@@ -397,7 +441,6 @@ def run_gpu(args, info, comm) -> int:
     from codename_symbiont_amd.models import get_config
     from codename_symbiont_amd.models.encoder import HipEncoder, refill_synthetic, synthetic_batch
     from codename_symbiont_amd.parallel import dist as D
-    from codename_symbiont_amd.parallel.sharded import ShardedSearcher
 
     dev = info.device
     torch.manual_seed(1234 + info.rank)
@@ -406,7 +449,8 @@ def run_gpu(args, info, comm) -> int:
 
     t0 = time.time()
     enc = HipEncoder(cfg, seed=0, device=dev, precision=args.encoder_dtype)
-    rows_per_rank = args.index_rows // info.world
+    vw = args.simulate_world or 0
+    rows_per_rank = args.index_rows // (vw or info.world)
     extra = (K + W + 4) * B
     prefilter = None if args.index_prefilter == "none" else args.index_prefilter
 
@@ -419,7 +463,8 @@ def run_gpu(args, info, comm) -> int:
                     spread=args.cluster_spread)
     if args.mode != "embed":
         fill_corpus(shard, gen, rows_per_rank, seed=100 + info.rank)
-    searcher = ShardedSearcher(shard, info)
+    searcher = _make_searcher(args, shard, info, lambda n, seed: enc.forward_packed(
+        synthetic_batch(cfg, n, S, seed=seed).to(dev))[1].clone())
     if prune:
         from codename_symbiont_amd.ops._ext import hip as _hip
 
@@ -749,9 +794,9 @@ def run_gpu(args, info, comm) -> int:
         # per-rank scan kernel: the emitting MFMA scan (csrc/hip/index_mq.hip) for >= 256
         # seeded queries (512 per workgroup at >= 512), else the 256-query list kernel
         "index_scan": (("int8-pruned-" if prune else "emitting-")
-                       + ("512q" if B * info.world >= 512 else "256q"))
+                       + ("512q" if B * (vw or info.world) >= 512 else "256q"))
                       if (shard.scan_mq and args.index_dtype == "bf16" and cfg.hidden == 384
-                          and B * info.world >= shard.mq_min_nq and args.k <= 16)
+                          and B * (vw or info.world) >= shard.mq_min_nq and args.k <= 16)
                       else "list-256q",
         "encoder_hipgraph": use_graph,
         "search_priority": args.search_priority,

@@ -89,6 +89,65 @@ class ShardedSearcher:
         return merge_ranked(s_recv.view(info.world, nq, k), g_recv.view(info.world, nq, k), k)
 
 
+class SimulatedShardedSearcher(ShardedSearcher):
+    """The per-rank work of a ``vworld``-GPU sharded search, on ONE GPU (bench.py
+    --simulate-world N): a PROJECTION, never a multi-GPU measurement.
+
+    The real collectives run through a single-rank RCCL group, so their kernels are launched and
+    contend for CUs with the scans exactly as on each rank of the real job, and each moves the
+    payload ONE rank sends (its [nq, D] queries; its [vworld * nq, k] score + id lists).  What
+    the other ranks would contribute is stood in for locally: the all_gathered batch is this
+    rank's queries followed by (vworld - 1) * nq foreign queries from ``foreign`` (embeddings that
+    are NOT in this shard, as the other ranks' are not), so the shard scan, the pre-pass and the
+    merge see the per-rank shapes of the N-GPU step.  Not modelled: xGMI transfer time and the
+    wait for the slowest peer."""
+
+    def __init__(self, shard: HbmIndexShard, info: DistInfo, vworld: int, foreign: list,
+                 group=None):
+        super().__init__(shard, info, group)
+        if info.world != 1:
+            raise ValueError("a simulated world runs on exactly one rank")
+        self.vworld = int(vworld)
+        self.foreign = foreign      # list of [(vworld - 1) * nq, D] bf16 query blocks
+        self._fi = 0
+
+    def _gather(self, q_local: torch.Tensor) -> torch.Tensor:
+        nq, D = q_local.shape
+        q_send = q_local.to(self.wire_dtype).contiguous()
+        q_own = torch.empty(nq, D, dtype=self.wire_dtype, device=q_send.device)
+        if self.collective:
+            dist.all_gather_into_tensor(q_own, q_send, group=self.group)
+        else:
+            q_own.copy_(q_send)
+        f = self.foreign[self._fi % len(self.foreign)]
+        self._fi += 1
+        return torch.cat([q_own.to(torch.bfloat16), f[:(self.vworld - 1) * nq]])
+
+    def _exchange(self, s: torch.Tensor, gid: torch.Tensor, nq: int, k: int):
+        s_recv = torch.empty_like(s)
+        g_recv = torch.empty_like(gid)
+        if self.collective:
+            dist.all_to_all_single(s_recv, s.contiguous(), group=self.group)
+            dist.all_to_all_single(g_recv, gid.contiguous(), group=self.group)
+        else:
+            s_recv.copy_(s)
+            g_recv.copy_(gid)
+        return merge_ranked(s_recv.view(self.vworld, nq, k), g_recv.view(self.vworld, nq, k), k)
+
+    def search(self, q_local: torch.Tensor, k: int):
+        nq = q_local.shape[0]
+        s, r = self.shard.search(self._gather(q_local), k)
+        return self._exchange(s, encode_gid(0, r), nq, k)
+
+    def begin(self, q_local: torch.Tensor, k: int) -> dict:
+        return {"ctx": self.shard.search_begin(self._gather(q_local), k), "k": k,
+                "nq": q_local.shape[0]}
+
+    def end(self, h: dict):
+        s, r = self.shard.search_end(h["ctx"])
+        return self._exchange(s, encode_gid(0, r), h["nq"], h["k"])
+
+
 def merge_ranked(scores: torch.Tensor, gids: torch.Tensor, k: int):
     """[world, nq, k] per-rank sorted lists -> [nq, k] global top-k (ties: lower rank first)."""
     W, nq, kk = scores.shape

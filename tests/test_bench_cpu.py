@@ -43,6 +43,25 @@ def test_bench_world_mismatch_fails():
     assert "refusing" in p.stderr
 
 
+def test_bench_simulated_world_is_labelled_a_projection():
+    """--simulate-world N runs the per-rank work of the N-GPU step on ONE rank (a 1/N shard,
+    N x batch gathered queries, the result exchange through a single-rank group): its JSON can
+    never pass for an N-GPU measurement -- the metric says SIMULATED, n_gpus and world stay 1,
+    and the N-GPU numbers sit in the simulated_* / projected_* fields only."""
+    p, out = _run(["--simulate-world", "4"] + TINY)
+    assert p.returncode == 0, p.stderr[-2000:]
+    r = out[0]
+    assert r["metric"].startswith("SIMULATED 4-GPU") and "projection" in r["metric"]
+    assert r["n_gpus"] == 1 and r["world"] == 1 and r["simulated"] is True
+    assert r["simulated_world"] == 4 and r["config"]["simulated_world"] == 4
+    assert r["config"]["index_rows_per_rank"] == 1500 and r["config"]["global_batch"] == 16
+    assert "simulated" in r["config"]["parallelism"]
+    assert r["value"] == r["projected_job_rate"] > 0
+    # and it refuses to pose as a multi-rank run
+    p2, out2 = _run(["--simulate-world", "4", "--gpus", "2"] + TINY)
+    assert p2.returncode != 0 and not out2
+
+
 def test_bench_search_clustered_heldout_two_ranks():
     p, out = _run(["--gpus", "2", "--mode", "search", "--corpus", "clustered", "--clusters", "50",
                    "--queries", "heldout"] + TINY)
