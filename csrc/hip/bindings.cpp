@@ -181,7 +181,7 @@ class EncoderRuntime {
 
   // Split-partial buffer the bf16 layers' small-M (query-path) GEMMs need: skinny_ws_bytes().
   size_t skinny_ws_bytes() const {
-    const int H = H_, M = 64;
+    const int H = H_, M = 256;   // the largest M the small-M path may be configured to take
     size_t b = 0;
     auto mx = [&](int epi, int N, int K) { b = std::max(b, symb_gemm_skinny_scratch_bytes(epi, M, N, K)); };
     mx(EPI_BIAS, 3 * H, H);

@@ -26,6 +26,7 @@
 //    kernel applies bias / GELU / residual itself (no second launch).  An opt-in form lets the
 //    last workgroup to finish a small multi-split GEMM do the split sum and epilogue (measured
 //    slower; see g_skinny_fuse).
+#include <algorithm>
 #include <map>
 #include <mutex>
 #include <utility>
@@ -156,6 +157,7 @@ __global__ __launch_bounds__(256) void skinny_partial_kernel(
   extern __shared__ __attribute__((aligned(16))) float red[];   // [4 waves][MP rows][LS]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n0 = blockIdx.x * 64;
+  const int m0 = blockIdx.z * 64;                  // 64-row block (M > 64: several, in z)
   const int g = blockIdx.y * 4 + wave;            // this wave's 128-k granule
   const int r = lane & 15, grp = lane >> 4;
 
@@ -170,7 +172,7 @@ __global__ __launch_bounds__(256) void skinny_partial_kernel(
     bf16x8 a[RM][4], b[4][4];
 #pragma unroll
     for (int i = 0; i < RM; ++i) {
-      const __bf16* pa = A + (size_t)min(i * 16 + r, M - 1) * lda + k0;   // rows >= M: ignored
+      const __bf16* pa = A + (size_t)min(m0 + i * 16 + r, M - 1) * lda + k0;   // rows >= M: ignored
 #pragma unroll
       for (int t = 0; t < 4; ++t) a[i][t] = *reinterpret_cast<const bf16x8*>(pa + 8 * t);
     }
@@ -200,14 +202,14 @@ __global__ __launch_bounds__(256) void skinny_partial_kernel(
       for (int e = 0; e < 4; ++e) red[(wave * MP + i * 16 + grp * 4 + e) * LS + j * 16 + r] = acc[i][j][e];
   __syncthreads();
   for (int q = threadIdx.x; q < MP * 8; q += 256) {
-    const int row = q >> 3, c8 = (q & 7) * 8;
+    const int lrow = q >> 3, c8 = (q & 7) * 8, row = m0 + lrow;
     if (row >= M) break;
     float v[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = 0.f;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
-      const float* src = red + (w * MP + row) * LS + c8;
+      const float* src = red + (w * MP + lrow) * LS + c8;
       const f32x4 x0 = *reinterpret_cast<const f32x4*>(src);
       const f32x4 x1 = *reinterpret_cast<const f32x4*>(src + 4);
 #pragma unroll
@@ -256,7 +258,7 @@ __global__ __launch_bounds__(256) void skinny_partial_kernel(
     __syncthreads();
     if (threadIdx.x == 0) {
       const int prev = __hip_atomic_fetch_add(counter, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      s_last = prev == (int)(gridDim.x * gridDim.y) - 1;
+      s_last = prev == (int)(gridDim.x * gridDim.y * gridDim.z) - 1;
     }
     __syncthreads();
     if (!s_last) return;
@@ -275,7 +277,7 @@ __global__ __launch_bounds__(256) void skinny_partial_kernel(
 // a stream under capture that has none takes the tiled path instead (no allocation in a capture).
 // Layout: a 256-byte header (the last-workgroup counter, zero between launches) + the partials.
 constexpr size_t kScratchHeader = 256;
-constexpr size_t kStreamScratchBytes = kScratchHeader + (size_t)64 * 4096 * 8 * sizeof(float);
+constexpr size_t kStreamScratchBytes = kScratchHeader + (size_t)256 * 4096 * 8 * sizeof(float);
 thread_local float* t_scratch = nullptr;
 thread_local size_t t_scratch_bytes = 0;
 std::mutex g_scratch_mu;
@@ -349,7 +351,7 @@ static int g_skinny_max_m = 64;
 // row a dependent chain of partial loads, while the epilogue kernel spreads them over M waves.
 static int g_skinny_fuse = 1;
 int symb_gemm_skinny_config(int max_m, int fuse) {
-  if (max_m < 0 || max_m > 64 || fuse < 0 || fuse > 3) return -1;
+  if (max_m < 0 || max_m > 256 || fuse < 0 || fuse > 3) return -1;
   g_skinny_max_m = max_m;
   g_skinny_fuse = fuse;
   return 0;
@@ -362,7 +364,7 @@ void symb_gemm_skinny_set_scratch(void* p, size_t bytes) {
 }
 
 bool symb_gemm_skinny_supported(int epi, int M, int N, int K) {
-  return M >= 1 && M <= 64 && epi >= SK_BIAS && epi <= SK_RES_LN && K % 128 == 0 && K <= 4096 &&
+  return M >= 1 && M <= 256 && epi >= SK_BIAS && epi <= SK_RES_LN && K % 128 == 0 && K <= 4096 &&
          N % 64 == 0 && N <= 4096;
 }
 
@@ -392,12 +394,12 @@ int symb_gemm_skinny(int epi, const void* A, int lda, const void* W, int ldw, co
     counter = (int*)base;
     P = (float*)(base + kScratchHeader);
   }
-  const dim3 grid(N / 64, S), block(256);
+  const dim3 grid(N / 64, S, (M + 63) / 64), block(256);
   auto a = (const __bf16*)A;
   auto w = (const __bf16*)W;
   auto r = (const __bf16*)R;
   auto c = (__bf16*)C;
-  const int rm = (M + 15) / 16;
+  const int rm = (std::min(M, 64) + 15) / 16;   // fragments per 64-row block
 #define SK_P(RM_, E_, F_)                                                                   \
   launch_partial<RM_, E_, F_>(grid, st, a, lda, w, ldw, P, M, N, KG, bias, r, ldr, gelu_poly, c, \
                               ldc, gamma, beta, eps, counter)

@@ -244,6 +244,34 @@ def test_gemm_skinny(M, N, K, epi):
     _close(out, big, atol=2e-2, rtol=1e-2, what="skinny vs tiled")
 
 
+@pytest.mark.parametrize("M", [65, 100, 128, 200, 256])
+@pytest.mark.parametrize("N,K,epi", [(1152, 384, 0), (1536, 384, 1), (384, 1536, 3), (768, 3072, 2),
+                                     (3072, 768, 1)])
+def test_gemm_skinny_row_blocks(M, N, K, epi):
+    """gemm_skinny_config(max_m=256): M > 64 runs as several 64-row blocks (grid z) of the same
+    split kernel; against the fp32 oracle, the tiled path, and bit-exact on repeat."""
+    from codename_symbiont_amd.ops._ext import hip
+    from codename_symbiont_amd.ops.kernels import gemm
+
+    a = _bf(M, K, seed=1)
+    w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=2)
+    bias = _f(N, scale=0.5, seed=3)
+    res = _bf(M, N, seed=4) if epi in (2, 3) else None
+    g = _f(N, scale=0.1, offset=1.0, seed=5) if epi == 3 else None
+    b = _f(N, scale=0.1, seed=6) if epi == 3 else None
+    big = gemm(a, w, bias, epi, res, g, b, 1e-12)          # default max_m 64: tiled
+    hip().gemm_skinny_config(256)
+    try:
+        out = gemm(a, w, bias, epi, res, g, b, 1e-12)
+        out2 = gemm(a, w, bias, epi, res, g, b, 1e-12)
+    finally:
+        hip().gemm_skinny_config(64)
+    ref = R.gemm_ref(a, w, bias, epi, res, g, b, 1e-12)
+    _close(out, ref, atol=4e-2, rtol=2e-2, what=f"skinny row blocks epi={epi}")
+    assert torch.equal(out, out2)
+    _close(out, big, atol=2e-2, rtol=1e-2, what="skinny row blocks vs tiled")
+
+
 @pytest.mark.parametrize("model", ["minilm-l6", "bge-base"])
 def test_encoder_small_batch_skinny(model):
     """Query-path forwards (T <= 64 tokens: every GEMM on the skinny path) match the fp32 oracle
