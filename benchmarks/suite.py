@@ -10,6 +10,12 @@ Configs (BASELINE.md "Measured" table):
   4 bge-dp          bge-base-en-v1.5 DP embedding over RCCL         bench.py --model bge-base --mode embed --embed-dp group
   5 e5-fp8          e5-large-v2 + fp8 index (1B rows at N >= 4)     bench.py --model e5-large --index-dtype fp8
   + headline        MiniLM embed + top-10 over 100M x 384           bench.py
+  + mpnet-embed     the reference's own model (paraphrase-multilingual-mpnet-base-v2, 768-d)
+                    bf16 embedding, batch 256                       bench.py --model mpnet-multi --mode embed
+  + mpnet-full      the reference's default deployment: mpnet embed + top-10 over a
+                    100M x 768 collection (vector_memory_service/src/main.rs:22)
+                                                                    bench.py --model mpnet-multi
+  + e5-embed        e5-large-v2 bf16 embedding (every projection on our kernels)
 Each config runs as a CHILD process (torch.distributed.run for N > 1) under its own timeout.
 """
 from __future__ import annotations
@@ -66,6 +72,9 @@ def main():
         ("e5-fp8", launch + common + ["--model", "e5-large", "--index-dtype", "fp8",
                                       "--encoder-dtype", "fp8", "--index-rows", str(fp8_rows)], 1200),
         ("headline", launch + common, 900),
+        ("mpnet-embed", launch + common + ["--model", "mpnet-multi", "--mode", "embed"], 600),
+        ("mpnet-full", launch + common + ["--model", "mpnet-multi"], 1200),
+        ("e5-embed", launch + common + ["--model", "e5-large", "--mode", "embed"], 600),
     ]
     only = set(filter(None, a.only.split(",")))
     results = []

@@ -22,8 +22,8 @@
 //    the same way: each 16-lane ds_read_b128 group then covers 16 distinct 16-byte bank slots.
 //  * Last-wave split-K (a stream-K form without a persistent loop): of T output tiles, the
 //    T mod P that would form a partial last wave over the P CUs are cut into S = P / (T mod P)
-//    k-slices (S in 2..4) that run after the full tiles.  Each slice takes an arrival
-//    ticket; the non-last ones publish fp32 partials (plain stores, release fence, done counter),
+//    k-slices (S = 2) that run after the full tiles.  Each slice takes an arrival
+//    ticket; the non-last ones publish fp32 partials (write-through sc1 stores, done counter),
 //    the LAST arriver waits only for slices that already hold a ticket (so they are resident and
 //    finishing: no deadlock whatever the dispatch order), adds their partials and runs the
 //    epilogue.  The last arriver resets both counters, so graph replays need no memset.
@@ -49,13 +49,26 @@ constexpr int CS = BN + 4;                   // fp32 epilogue row stride (floats
 constexpr int PROWS = WTM;                   // epilogue rows per pass (one wave-row band)
 constexpr int EPI_BYTES = PROWS * CS * 4;    // 130 KiB
 constexpr int PART_FLOATS = BM * BN;         // one split partial (256 KiB)
-constexpr int MAX_SPLITS = 4;
+constexpr int MAX_SPLITS = 2;              // (the combine prefetches ONE other slice's band)
 static_assert(LA * NT == BM * 4 && LB * NT == BN * 4, "slot rows must cover the threads");
 }  // namespace gd
 
 enum { GD_BIAS = 0, GD_GELU = 1, GD_RES = 2 };
 
 __device__ __forceinline__ int gd_swz(int row) { return (4 - ((row >> 2) & 3)) & 3; }
+
+// The split partial hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, first row of the
+// sc1 table): every partial byte is stored write-through (sc1, 16 B), each storing wave drains
+// its vmcnt, ONE lane adds to the tile's done counter behind a workgroup barrier; the consumer
+// polls that counter with sc1 loads and reads EVERY partial byte with sc1 loads after a barrier.
+// No L2 write-back fence (it would also flush every other dirty line of the producer's XCD L2:
+// the tiles' output stores) and no acquire.
+__device__ __forceinline__ void gd_store_wt(float* p, const f32x4& v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void gd_load_wt(f32x4& v, const float* p) {   // (no wait)
+  asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
+}
 
 __device__ __forceinline__ bf16x8 gd_lds16(const char* p) {
   return *reinterpret_cast<const bf16x8*>(p);
@@ -79,33 +92,28 @@ __device__ __forceinline__ void gd_barrier() {
 
 // One k-step: the 32 MFMAs (row-major over the 8 x 4 wave tile) with the NEXT k-step's 12
 // fragment reads between them.  A fragment i is last read by MFMA (i, 3), so its refill follows
-// that MFMA (same registers); the B fragments are read by every row, so the next k-step's B is
-// loaded into a second set during the first two rows.  8 A + 2 x 4 B = 64 fragment VGPRs next to
+// that MFMA (same registers); the B fragments are read by every row, so the next k-step's B goes
+// to the other B set (bn) during the first two rows.  8 A + 2 x 4 B = 64 fragment VGPRs next to
 // 128 accumulators.  The order is pinned by sched_group_barrier: (2 MFMA, 1 read) x 12, 8 MFMA.
-template <bool NEXT = true>
 __device__ __forceinline__ void gd_kstep(f32x4 (&acc)[gd::RM][gd::RN], bf16x8 (&a)[gd::RM],
-                                         bf16x8 (&b)[gd::RN], const char* na, const char* nb) {
+                                         const bf16x8 (&b)[gd::RN], bf16x8 (&bn)[gd::RN],
+                                         const char* na, const char* nb) {
   using namespace gd;
-  bf16x8 bn[RN];
 #pragma unroll
   for (int i = 0; i < RM; ++i) {
 #pragma unroll
     for (int j = 0; j < RN; ++j) {
       acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-      if (NEXT && i < 2 && (j == 0 || j == 2)) bn[i * 2 + j / 2] = gd_lds16(nb + (i * 2 + j / 2) * 16 * ROWB);
+      if (i < 2 && (j == 0 || j == 2)) bn[i * 2 + j / 2] = gd_lds16(nb + (i * 2 + j / 2) * 16 * ROWB);
     }
-    if (NEXT) a[i] = gd_lds16(na + i * 16 * ROWB);
+    a[i] = gd_lds16(na + i * 16 * ROWB);
   }
-  if (NEXT) {
 #pragma unroll
-    for (int j = 0; j < RN; ++j) b[j] = bn[j];
-#pragma unroll
-    for (int r = 0; r < RM + RN; ++r) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // 2 MFMAs
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // 1 DS read
-    }
-    __builtin_amdgcn_sched_group_barrier(0x008, RM * RN - 2 * (RM + RN), 0);
+  for (int r = 0; r < RM + RN; ++r) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // 2 MFMAs
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // 1 DS read
   }
+  __builtin_amdgcn_sched_group_barrier(0x008, RM * RN - 2 * (RM + RN), 0);
 }
 
 template <int EPI, int NS>
@@ -158,16 +166,27 @@ __global__ __launch_bounds__(gd::NT, 1) void gemm_deep_kernel(
     const int s = i * NT + tid, row = s >> 2, c = (s & 3) ^ gd_swz(row);
     boff[i] = (uint32_t)(n0 + row) * (uint32_t)ldw * 2u + (uint32_t)(c * 16);
   }
-  const char* Ab = reinterpret_cast<const char*>(A);
-  const char* Wb = reinterpret_cast<const char*>(W);
+  // buffer descriptors: one SGPR base per operand, the per-lane row offsets above in VGPRs and
+  // the k-step's byte offset in an SGPR -- one instruction per 1-KiB piece, no address VALU
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)A, (short)0, (int)((uint32_t)M * (uint32_t)lda * 2u), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)W, (short)0, (int)((uint32_t)N * (uint32_t)ldw * 2u), 0x00020000);
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   auto stage = [&](int kt, int slot) {
     char* sA = smem + slot * SLOT;
     char* sB = sA + A_BYTES;
-    const uint32_t k0 = (uint32_t)kt * ROWB;
+    const int k0 = kt * ROWB;
 #pragma unroll
-    for (int i = 0; i < LA; ++i) glds16(Ab + aoff[i] + k0, sA + (i * NT + wave * 64) * 16);
+    for (int i = 0; i < LA; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          ra, (__attribute__((address_space(3))) void*)(sA + (i * NT + wave_u * 64) * 16), 16,
+          (int)aoff[i], k0, 0, 0);
 #pragma unroll
-    for (int i = 0; i < LB; ++i) glds16(Wb + boff[i] + k0, sB + (i * NT + wave * 64) * 16);
+    for (int i = 0; i < LB; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rw, (__attribute__((address_space(3))) void*)(sB + (i * NT + wave_u * 64) * 16), 16,
+          (int)boff[i], k0, 0, 0);
   };
 
   // ---- per-lane fragment addresses: A row wm*128 + i*16 + (lane&15), B row wn*64 + j*16 + ... --
@@ -181,7 +200,7 @@ __global__ __launch_bounds__(gd::NT, 1) void gemm_deep_kernel(
 #pragma unroll
     for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  bf16x8 af[RM], bf[RN];
+  bf16x8 af[RM], bf0[RN], bf1[RN];
   // prologue: slots 0 .. NS-2 in flight, slot 0 landed and visible, its fragments in registers
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p)
@@ -191,21 +210,29 @@ __global__ __launch_bounds__(gd::NT, 1) void gemm_deep_kernel(
 #pragma unroll
   for (int i = 0; i < RM; ++i) af[i] = gd_lds16(smem + fa + i * 16 * ROWB);
 #pragma unroll
-  for (int j = 0; j < RN; ++j) bf[j] = gd_lds16(smem + fb + j * 16 * ROWB);
+  for (int j = 0; j < RN; ++j) bf0[j] = gd_lds16(smem + fb + j * 16 * ROWB);
 
-  // k-step `it`, reading k-step it + 1's fragments.  Slot it + 1 landed for this wave once only
-  // the younger slots' pieces remain; the barrier makes every wave's pieces visible and retires
-  // every wave's reads of slot it - 1, which stage(it + NS - 1) refills.
-  for (int it = 0; it < nk; ++it) {
-    const bool more = it + 1 < nk;
-    if (more) gd_wait_slots(min(NS - 3, nk - 2 - it));
-    gd_barrier();
-    if (it + NS - 1 < nk) stage(kb + it + NS - 1, (it + NS - 1) % NS);
-    // (the last k-step reads a stale slot it never uses: one code path keeps the register
-    // allocation of the MFMA loop at 192 VGPRs; two spilled)
-    const char* nbase = smem + ((it + 1) % NS) * SLOT;
-    gd_kstep<true>(acc, af, bf, nbase + fa, nbase + fb);
+  // k-step `it` on B set CB, reading k-step it + 1's fragments (B into NB).  Slot it + 1 landed
+  // for this wave once only the younger slots' pieces remain; the barrier makes every wave's
+  // pieces visible and retires every wave's reads of slot it - 1, which stage(it + NS - 1)
+  // refills.  The last k-step reads a stale slot it never uses: one code shape for every step
+  // keeps the MFMA loop's registers allocated once (two shapes spilled).
+#define GD_ITER(CB, NB)                                                         \
+  {                                                                             \
+    if (it + 1 < nk) gd_wait_slots(min(NS - 3, nk - 2 - it));                   \
+    gd_barrier();                                                               \
+    if (it + NS - 1 < nk) stage(kb + it + NS - 1, (it + NS - 1) % NS);          \
+    const char* nbase = smem + ((it + 1) % NS) * SLOT;                          \
+    gd_kstep(acc, af, CB, NB, nbase + fa, nbase + fb);                          \
   }
+  int it = 0;
+  for (; it + 1 < nk; ++it) {
+    GD_ITER(bf0, bf1)
+    ++it;
+    GD_ITER(bf1, bf0)
+  }
+  if (it < nk) GD_ITER(bf0, bf1)
+#undef GD_ITER
 
   // ---- last-wave split-K: take a ticket; the last arriver combines, the others publish ----
   // Partials are row-major fp32 256 x 256 tiles, one per split slot, written and read in the
@@ -226,8 +253,6 @@ __global__ __launch_bounds__(gd::NT, 1) void gemm_deep_kernel(
       // every other slice holds a ticket, i.e. is resident and publishing: a bounded wait
       while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < splits - 1)
         __builtin_amdgcn_s_sleep(2);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       // reset for the next launch (ordered by the kernel boundary; graph replays need no memset)
       __hip_atomic_store(arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -252,43 +277,47 @@ __global__ __launch_bounds__(gd::NT, 1) void gemm_deep_kernel(
     __syncthreads();
     const int band0 = m0 + pass * PROWS;
     constexpr int VPR = BN / 8;
-    for (int v = tid; v < PROWS * VPR; v += NT) {
-      const int row = v / VPR, c8 = (v % VPR) * 8;
+    constexpr int PER = PROWS * VPR / NT;    // 16-byte column groups per thread per pass
+    static_assert(PER * NT == PROWS * VPR && PER == 8, "epilogue work split (pp ties 4 x 2)");
+    // combine: the other slice's band, half a pass in flight at a time (sc1 loads, one wait)
+    constexpr int PH = PER / 2;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+    f32x4 pp[PH][2];
+    if (combine) {
+      const float* pb = part + (size_t)(st * splits + (1 - slice)) * PART_FLOATS +
+                        (size_t)(pass * PROWS) * BN;
+#pragma unroll
+      for (int jj = 0; jj < PH; ++jj) {
+        const int v = tid + (h * PH + jj) * NT, row = v / VPR, c8 = (v % VPR) * 8;
+        gd_load_wt(pp[jj][0], pb + row * BN + c8);
+        gd_load_wt(pp[jj][1], pb + row * BN + c8 + 4);
+      }
+      asm volatile("s_waitcnt vmcnt(0)"
+                   : "+v"(pp[0][0]), "+v"(pp[0][1]), "+v"(pp[1][0]), "+v"(pp[1][1]),
+                     "+v"(pp[2][0]), "+v"(pp[2][1]), "+v"(pp[3][0]), "+v"(pp[3][1])
+                   :: "memory");
+    }
+#pragma unroll
+    for (int jj = 0; jj < PH; ++jj) {
+      const int j = jj;
+      const int v = tid + (h * PH + jj) * NT, row = v / VPR, c8 = (v % VPR) * 8;
       const int grow = band0 + row;
       const f32x4 x0 = *reinterpret_cast<const f32x4*>(Cs + row * CS + c8);
       const f32x4 x1 = *reinterpret_cast<const f32x4*>(Cs + row * CS + c8 + 4);
-      const size_t poff = (size_t)(pass * PROWS + row) * BN + c8;
       if (publish) {
-        float* p = part + (size_t)sk * PART_FLOATS + poff;
-        *reinterpret_cast<f32x4*>(p) = x0;
-        *reinterpret_cast<f32x4*>(p + 4) = x1;
+        float* p = part + (size_t)sk * PART_FLOATS + (size_t)(pass * PROWS + row) * BN + c8;
+        gd_store_wt(p, x0);
+        gd_store_wt(p + 4, x1);
         continue;
       }
       if (grow >= M) continue;
       float y[8];
+      // two slices summed in slice order whichever arrived last: bit-identical launches
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        y[e] = x0[e];
-        y[e + 4] = x1[e];
-      }
-      if (combine) {
-        // slices summed in slice order whichever arrived last: bit-identical launches
-        float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        for (int s2 = 0; s2 < splits; ++s2) {
-          f32x4 p0 = x0, p1 = x1;
-          if (s2 != slice) {
-            const float* p = part + (size_t)(st * splits + s2) * PART_FLOATS + poff;
-            p0 = *reinterpret_cast<const f32x4*>(p);
-            p1 = *reinterpret_cast<const f32x4*>(p + 4);
-          }
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            z[e] += p0[e];
-            z[e + 4] += p1[e];
-          }
-        }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) y[e] = z[e];
+        y[e] = combine ? (slice == 0 ? x0[e] + pp[j][0][e] : pp[j][0][e] + x0[e]) : x0[e];
+        y[e + 4] = combine ? (slice == 0 ? x1[e] + pp[j][1][e] : pp[j][1][e] + x1[e]) : x1[e];
       }
       const f32x4 b0 = *reinterpret_cast<const f32x4*>(bias + n0 + c8);
       const f32x4 b1 = *reinterpret_cast<const f32x4*>(bias + n0 + c8 + 4);
@@ -318,18 +347,15 @@ __global__ __launch_bounds__(gd::NT, 1) void gemm_deep_kernel(
       }
       store8(C + (size_t)grow * ldc + n0 + c8, y);
     }
+    }
     if (pass + 1 < WM) __syncthreads();
   }
   if (publish) {
-    // every storing wave drained, then one release and the done count
+    // every storing wave drained its write-through stores, then one done count per workgroup
     int* done = ctr + (T - dp_tiles) + st;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (tid == 0) __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 

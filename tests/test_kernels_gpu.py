@@ -109,15 +109,15 @@ def test_gemm(M, N, K, epi, tile):
     (32768, 768, 3072),   # the bge FFN2 shape, long K
     (9000, 768, 3072),    # ragged last row tile, 108 tiles: split 2 ways
     (4100, 2304, 768),    # 153 tiles (> P/2): no split
-    (999, 1024, 1024),    # 16 tiles: split 4 ways (K/32 = 32 k-steps, 8 per slice)
+    (999, 1024, 1024),    # 16 tiles: split 2 ways (K/32 = 32 k-steps)
     (300, 512, 128),      # 4 k-steps: one slice (the >= 4 k-steps per slice rule)
-    (777, 256, 2048),     # one column tile, split 4 ways
+    (777, 256, 2048),     # one column tile, split 2 ways
     (65536, 1024, 1024),  # 1024 tiles: whole waves, no split
 ])
 @pytest.mark.parametrize("epi", [0, 1, 2])
 def test_gemm_deep(M, N, K, epi, ns, sk):
     """The deep-ring 256x256 kernel (gemm_deep.hip) through its own entry: ragged M, whole and
-    split last waves (2 and 4 slices, fp32 partials combined by the last arriving slice), both
+    split last waves (2 slices, fp32 partials combined by the last arriving slice), both
     ring depths, every epilogue, against the fp32 oracle -- and two launches are bit-identical
     (slices are summed in slice order whichever arrives last)."""
     from codename_symbiont_amd.ops._ext import hip, stream_handle
