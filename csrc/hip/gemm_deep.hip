@@ -62,12 +62,15 @@ __device__ __forceinline__ int gd_swz(int row) { return (4 - ((row >> 2) & 3)) &
 // its vmcnt, ONE lane adds to the tile's done counter behind a workgroup barrier; the consumer
 // polls that counter with sc1 loads and reads EVERY partial byte with sc1 loads after a barrier.
 // No L2 write-back fence (it would also flush every other dirty line of the producer's XCD L2:
-// the tiles' output stores) and no acquire.
-__device__ __forceinline__ void gd_store_wt(float* p, const f32x4& v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+// the tiles' output stores) and no acquire.  Buffer loads / stores with the sc1 cache-policy bit
+// (aux 16): the compiler tracks their data registers (inline asm stores read registers whose
+// LDS loads it did not wait for).
+constexpr int GD_SC1 = 16;
+__device__ __forceinline__ void gd_store_wt(__amdgpu_buffer_rsrc_t r, int off, const f32x4& v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, GD_SC1);
 }
-__device__ __forceinline__ void gd_load_wt(f32x4& v, const float* p) {   // (no wait)
-  asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
+__device__ __forceinline__ f32x4 gd_load_wt(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, GD_SC1));
 }
 
 __device__ __forceinline__ bf16x8 gd_lds16(const char* p) {
@@ -121,7 +124,7 @@ __global__ __launch_bounds__(gd::NT, 1) void gemm_deep_kernel(
     const __bf16* __restrict__ A, int lda, const __bf16* __restrict__ W, int ldw,
     const float* __restrict__ bias, const __bf16* __restrict__ R, int ldr, int gelu_poly,
     __bf16* __restrict__ C, int ldc, int M, int N, int K, int group_m, int dp_tiles, int splits,
-    float* __restrict__ part, int* __restrict__ ctr) {
+    float* __restrict__ part, int* __restrict__ ctr, int dma_mode) {
   using namespace gd;
   static_assert(NS >= 3 && NS * SLOT <= 160 * 1024, "LDS ring depth");
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -173,10 +176,19 @@ __global__ __launch_bounds__(gd::NT, 1) void gemm_deep_kernel(
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
       (void*)W, (short)0, (int)((uint32_t)N * (uint32_t)ldw * 2u), 0x00020000);
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const char* Ab = reinterpret_cast<const char*>(A);
+  const char* Wb = reinterpret_cast<const char*>(W);
   auto stage = [&](int kt, int slot) {
     char* sA = smem + slot * SLOT;
     char* sB = sA + A_BYTES;
     const int k0 = kt * ROWB;
+    if (dma_mode == 1) {   // (A/B: per-lane 64-bit addresses, global_load_lds)
+#pragma unroll
+      for (int i = 0; i < LA; ++i) glds16(Ab + aoff[i] + k0, sA + (i * NT + wave_u * 64) * 16);
+#pragma unroll
+      for (int i = 0; i < LB; ++i) glds16(Wb + boff[i] + k0, sB + (i * NT + wave_u * 64) * 16);
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < LA; ++i)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
@@ -260,6 +272,9 @@ __global__ __launch_bounds__(gd::NT, 1) void gemm_deep_kernel(
     __syncthreads();   // (also orders the ticket read before the epilogue's LDS writes)
   }
   const bool combine = sk >= 0 && splits > 1 && !publish;
+  // the split partials as one buffer (byte offsets fit 32 bits: <= P x 256 KiB)
+  const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)part, (short)0, part ? (int)((T - dp_tiles) * splits * PART_FLOATS * 4) : 0, 0x00020000);
 
   // ---- epilogue: fp32 tile -> LDS (one 128-row band per pass) -> 16-byte row stores ----
   float* Cs = reinterpret_cast<float*>(smem);
@@ -285,18 +300,13 @@ __global__ __launch_bounds__(gd::NT, 1) void gemm_deep_kernel(
     for (int h = 0; h < 2; ++h) {
     f32x4 pp[PH][2];
     if (combine) {
-      const float* pb = part + (size_t)(st * splits + (1 - slice)) * PART_FLOATS +
-                        (size_t)(pass * PROWS) * BN;
+      const int pb = ((st * splits + (1 - slice)) * PART_FLOATS + pass * PROWS * BN) * 4;
 #pragma unroll
       for (int jj = 0; jj < PH; ++jj) {
         const int v = tid + (h * PH + jj) * NT, row = v / VPR, c8 = (v % VPR) * 8;
-        gd_load_wt(pp[jj][0], pb + row * BN + c8);
-        gd_load_wt(pp[jj][1], pb + row * BN + c8 + 4);
+        pp[jj][0] = gd_load_wt(rp, pb + (row * BN + c8) * 4);
+        pp[jj][1] = gd_load_wt(rp, pb + (row * BN + c8 + 4) * 4);
       }
-      asm volatile("s_waitcnt vmcnt(0)"
-                   : "+v"(pp[0][0]), "+v"(pp[0][1]), "+v"(pp[1][0]), "+v"(pp[1][1]),
-                     "+v"(pp[2][0]), "+v"(pp[2][1]), "+v"(pp[3][0]), "+v"(pp[3][1])
-                   :: "memory");
     }
 #pragma unroll
     for (int jj = 0; jj < PH; ++jj) {
@@ -306,9 +316,9 @@ __global__ __launch_bounds__(gd::NT, 1) void gemm_deep_kernel(
       const f32x4 x0 = *reinterpret_cast<const f32x4*>(Cs + row * CS + c8);
       const f32x4 x1 = *reinterpret_cast<const f32x4*>(Cs + row * CS + c8 + 4);
       if (publish) {
-        float* p = part + (size_t)sk * PART_FLOATS + (size_t)(pass * PROWS + row) * BN + c8;
-        gd_store_wt(p, x0);
-        gd_store_wt(p + 4, x1);
+        const int off = (sk * PART_FLOATS + (pass * PROWS + row) * BN + c8) * 4;
+        gd_store_wt(rp, off, x0);
+        gd_store_wt(rp, off + 16, x1);
         continue;
       }
       if (grow >= M) continue;
@@ -358,6 +368,8 @@ __global__ __launch_bounds__(gd::NT, 1) void gemm_deep_kernel(
     if (tid == 0) __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
+
+static int g_deep_dma = 0;   // 0: buffer-descriptor LDS-DMA, 1: global_load_lds (A/B)
 
 namespace {
 
@@ -411,7 +423,7 @@ int launch_deep(const void* A, int lda, const void* W, int ldw, const float* bia
   set_max_lds<gemm_deep_kernel<EPI, NS>>(lds);
   hipLaunchKernelGGL(kern, dim3(nwg), dim3(gd::NT), lds, st, (const __bf16*)A, lda,
                      (const __bf16*)W, ldw, bias, (const __bf16*)R, ldr, gelu_poly, (__bf16*)C, ldc,
-                     M, N, K, group_m, dp_tiles, splits, part, ctr);
+                     M, N, K, group_m, dp_tiles, splits, part, ctr, g_deep_dma);
   return (int)hipGetLastError();
 }
 
@@ -425,10 +437,11 @@ using namespace symb;
 // partial wave (0 off, 1 on); symb_gemm_deep_config.
 static int g_deep_ns = 5;
 static int g_deep_sk = 1;
-int symb_gemm_deep_config(int ns, int sk) {
-  if ((ns != 4 && ns != 5) || sk < 0 || sk > 1) return -1;
+int symb_gemm_deep_config(int ns, int sk, int dma) {
+  if ((ns != 4 && ns != 5) || sk < 0 || sk > 1 || dma < 0 || dma > 1) return -1;
   g_deep_ns = ns;
   g_deep_sk = sk;
+  g_deep_dma = dma;
   return 0;
 }
 
