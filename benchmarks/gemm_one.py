@@ -2,8 +2,8 @@
 """Run ONE encoder GEMM configuration repeatedly (for rocprofv3 --pmc / kernel-trace passes).
 
     python benchmarks/gemm_one.py --m 32768 --n 3072 --k 768 --epi 1 --tile 3 --iters 50
-    tile: symb_gemm_config tile mode (3 = auto: deep-ring kernel for wide shapes, 10 = round-3
-    auto, 2 = gemm.hip 256x256 2-stage); --ns / --sk: the deep kernel's ring depth / split-K;
+    tile: symb_gemm_config tile mode (3 = auto with the 256x192 tile, 10 = round-3 auto,
+    2 = 256x256 wherever N % 256 == 0);
     --torch runs torch.matmul (hipBLASLt) on the same operands instead.
 Prints one JSON line: ms per call and TFLOP/s.
 """
@@ -29,8 +29,6 @@ def main():
     ap.add_argument("--tile", type=int, default=3)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--torch", action="store_true")
-    ap.add_argument("--ns", type=int, default=5)
-    ap.add_argument("--sk", type=int, default=1)
     ap.add_argument("--lt", type=int, default=0,
                     help="hipBLASLt route for plain projections (gemm_lt_config: 0 off, 1 auto)")
     a = ap.parse_args()
@@ -45,7 +43,6 @@ def main():
     y = torch.empty(a.m, a.n, device="cuda", dtype=torch.bfloat16)
     hip().gemm_config(128, a.tile, 8)
     hip().gemm_lt_config(a.lt)
-    hip().gemm_deep_config(a.ns, a.sk)
     f = (lambda: torch.matmul(x, w.t(), out=y)) if a.torch else (lambda: K.gemm(x, w, b, a.epi, r, out=y))
     for _ in range(3):
         f()
@@ -57,7 +54,7 @@ def main():
     e.record()
     torch.cuda.synchronize()
     ms = s.elapsed_time(e) / a.iters
-    print(json.dumps({"ns": a.ns, "sk": a.sk, "lt": a.lt, "m": a.m, "n": a.n, "k": a.k, "epi": a.epi, "tile": a.tile, "torch": a.torch,
+    print(json.dumps({"lt": a.lt, "m": a.m, "n": a.n, "k": a.k, "epi": a.epi, "tile": a.tile, "torch": a.torch,
                       "ms": round(ms, 4), "TFLOPs": round(2 * a.m * a.n * a.k / ms / 1e9)}))
 
 

@@ -3,10 +3,9 @@
 
     python benchmarks/gemm_sweep.py [--models bge-base,e5-large] [--variants t3,t9,lt,torch]
 
-Variants: tN = symb_gemm with tile mode N (3 = auto: the deep-ring kernel for the wide shapes,
-10 = the round-3 auto rule without it, 2 = gemm.hip's 2-stage 256x256), hipBLASLt route off;
-dN = auto with the deep kernel's ring depth N (4 / 5); dNnosk = the same without last-wave
-split-K; lt = the hipBLASLt route for the plain projections (round-3 default);
+Variants: tN = symb_gemm with tile mode N (3 = auto with the 256x192 tile, 10 = the round-3
+auto rule, 2 = the 256x256 tile wherever N % 256 == 0), hipBLASLt route off; lt = the hipBLASLt
+route for the plain projections (round-3 default);
 torch = torch.matmul (hipBLASLt, no epilogue).
 Operands are random (the clock the chip holds depends on the data).  One JSON line per
 (shape, variant): median / min us over the rounds and TFLOP/s at the median.
@@ -35,7 +34,7 @@ SHAPES = {
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--models", default="bge-base,e5-large")
-    ap.add_argument("--variants", default="d5,d4,d5nosk,t10,lt,torch")
+    ap.add_argument("--variants", default="t3,t10,lt,torch")
     ap.add_argument("--m", type=int, default=32768)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
@@ -61,10 +60,6 @@ def main():
                 if v == "lt":
                     return lambda: (hip().gemm_config(128, 10, 8), hip().gemm_lt_config(1),
                                     K.gemm(x, w, b, epi, r, out=y), hip().gemm_lt_config(0))
-                if v.startswith("d"):
-                    ns, sk = int(v[1]), 0 if v.endswith("nosk") else 1
-                    return lambda: (hip().gemm_config(128, 3, 8), hip().gemm_deep_config(ns, sk),
-                                    K.gemm(x, w, b, epi, r, out=y), hip().gemm_deep_config(5, 1))
                 t = int(v[1:])
                 return lambda: (hip().gemm_config(128, t, 8), hip().gemm_lt_config(0),
                                 K.gemm(x, w, b, epi, r, out=y))

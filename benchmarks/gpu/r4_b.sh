@@ -6,6 +6,7 @@ cd "$(dirname "$0")/../.."
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 O=gpurun_out/r4_b
 mkdir -p $O
+timeout -k 10 200 python -u benchmarks/diag/deep_debug.py > $O/diag.txt 2>&1; cat $O/diag.txt
 timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread \
   -k "gemm_deep" > $O/tests_gemm.log 2>&1 || { tail -40 $O/tests_gemm.log; exit 1; }
 tail -2 $O/tests_gemm.log

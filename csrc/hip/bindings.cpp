@@ -46,10 +46,6 @@ int symb_index_scan_ablate(const void* X, int n_valid, int rows_per_blk, int n_r
                            const void* Q, int NQ, float* cs, int* ci, hipStream_t st, int abl,
                            const float* thr);
 int symb_gemm_config(int resln_bm, int tile, int group_m);
-int symb_gemm_deep_config(int ns, int sk, int dma);
-int symb_gemm_deep(int epi, const void* A, int lda, const void* W, int ldw, const float* bias,
-                   const void* R, int ldr, void* C, int ldc, int M, int N, int K, int group_m,
-                   int gelu_poly, hipStream_t st);
 int symb_gemm_fp8_config(int waves, int big);
 int symb_gemm_resln_config(int waves);
 int symb_gemm_gelu_config(int poly);
@@ -516,17 +512,6 @@ PYBIND11_MODULE(_hip, m) {
   m.def("attention_config", [](int waves, int kvt, int xcd) {
     check(symb_attention_config(waves, kvt, xcd), "attention_config");
   }, py::arg("waves") = 8, py::arg("kvt") = 64, py::arg("xcd") = 2);
-  m.def("gemm_deep_config", [](int ns, int sk, int dma) {
-    check(symb_gemm_deep_config(ns, sk, dma), "gemm_deep_config");
-  }, py::arg("ns") = 5, py::arg("sk") = 1, py::arg("dma") = 0);
-  // direct entry of the deep-ring kernel (tests / benchmarks): epi 0 bias, 1 GELU, 2 + residual
-  m.def("gemm_deep", [](int epi, uptr A, int lda, uptr W, int ldw, uptr bias, uptr R, int ldr,
-                        uptr C, int ldc, int M, int N, int K, int group_m, int gelu_poly, uptr st) {
-    check(symb_gemm_deep(epi, P<void>(A), lda, P<void>(W), ldw, P<float>(bias), P<void>(R), ldr,
-                         P<void>(C), ldc, M, N, K, group_m, gelu_poly, S(st)), "gemm_deep");
-  }, py::arg("epi"), py::arg("A"), py::arg("lda"), py::arg("W"), py::arg("ldw"), py::arg("bias"),
-     py::arg("R"), py::arg("ldr"), py::arg("C"), py::arg("ldc"), py::arg("M"), py::arg("N"),
-     py::arg("K"), py::arg("group_m"), py::arg("gelu_poly"), py::arg("stream"));
   m.def("gemm_config", [](int resln_bm, int tile, int group_m) {
     check(symb_gemm_config(resln_bm, tile, group_m), "gemm_config");
   }, py::arg("resln_bm") = 128, py::arg("tile") = 3, py::arg("group_m") = 8);

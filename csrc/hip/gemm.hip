@@ -420,38 +420,45 @@ static int launch_cfg(const void* A, int lda, const void* W, int ldw, const floa
 
 using namespace symb;
 
-// Deep-ring 256x256 kernel with last-wave split-K (gemm_deep.hip): the wide projections.
-bool symb_gemm_deep_supported(int M, int N, int K);
-int symb_gemm_deep(int epi, const void* A, int lda, const void* W, int ldw, const float* bias,
-                   const void* R, int ldr, void* C, int ldc, int M, int N, int K, int group_m,
-                   int gelu_poly, hipStream_t st);
-
 // Tile height of the row-complete RES_LN GEMM (64 or 128); a tuning knob, see symb_gemm_config.
 static int g_resln_bm = 128;
 // Tile of the bias / GELU / residual GEMMs (one path per shape class under the default 3):
-// 3 = auto: gemm_deep.hip's 256x256 deep-ring tile (last-wave split-K) when N % 256 == 0,
-//     K >= 512 and the grid holds at least half a wave of 256 tiles; else 128x128 with 8 waves of
-//     64x32 (4 waves per SIMD at 2 workgroups per CU), a 4-deep ring when the grid is smaller than
-//     the 256 CUs (small M: each tile's serial k-loop is the latency);
+// 3 = auto: a 256-row big tile (8 waves, 2-stage ring, one workgroup per CU) when K >= 768 and a
+//     256 x 256 or 256 x 192 grid fills whole waves of the 256 CUs (or is long enough that a
+//     partial last wave costs little) -- of the two, the one with the least
+//     (waves of tiles) x (tile area), ties to 256; else 128x128 with 8 waves of 64x32 (4 waves per
+//     SIMD at 2 workgroups per CU), a 4-deep ring when the grid is smaller than the 256 CUs (small
+//     M: each tile's serial k-loop is the latency);
 // 0 = 128x128 with 4 waves, 2-stage ring (A/B baseline);
-// 2 = this file's 2-stage 256x256 tile wherever N % 256 == 0 (the round-3 big tile, A/B);
-// 10 = auto without the deep kernel (the round-3 auto rule, A/B).
+// 2 = the 256 x 256 tile wherever N % 256 == 0 (A/B);
+// 10 = auto without the 256 x 192 tile (the round-3 rule, A/B).
+// Why 192: N = 768 at M = 32768 is 384 tiles of 256 x 256 = 1.5 waves on 256 CUs; as 256 x 192
+// it is 512 tiles = 2 whole waves of 3/4-size tiles, the last-wave fill a stream-K split gives,
+// without partials or a fix-up (a deep-ring kernel with last-wave split-K was built and measured
+// slower on every shape: profiles/r4_gemm/).
 static int g_tile = 3;
-static bool use_deep(int M, int N, int K) {
-  if (!symb_gemm_deep_supported(M, N, K) || K < 512) return false;
-  return ((M + 255) / 256) * (N / 256) >= 128;
-}
-static bool use_big_tile(int tile, int M, int N, int K) {
-  if (N % 256 != 0 || (tile != 2 && tile != 10)) return false;
-  if (tile == 2) return true;
-  // short K (MiniLM's 384): the 256x256 tile's fill and epilogue outweigh its operand reuse
-  if (K < 768) return false;
-  const int tiles = ((M + 255) / 256) * (N / 256);
-  return tiles % 256 == 0 || tiles >= 4 * 256;
+static int big_tile_bn(int tile, int M, int N, int K) {
+  if (tile == 2) return N % 256 == 0 ? 256 : 0;
+  if (tile != 3 && tile != 10) return 0;
+  // short K (MiniLM's 384): the big tile's fill and epilogue outweigh its operand reuse
+  if (K < 768) return 0;
+  int best = 0;
+  long best_cost = 0;
+  for (int bn : {256, 192}) {
+    if (N % bn != 0 || (bn == 192 && tile == 10)) continue;
+    const long tiles = (long)((M + 255) / 256) * (N / bn);
+    if (!(tiles % 256 == 0 || tiles >= 4 * 256)) continue;
+    const long cost = (tiles + 255) / 256 * bn;
+    if (!best || cost < best_cost) {
+      best = bn;
+      best_cost = cost;
+    }
+  }
+  return best;
 }
 int symb_gemm_config(int resln_bm, int tile, int group_m) {
   if (resln_bm != 64 && resln_bm != 128) return -1;
-  if (tile != 0 && tile != 2 && tile != 3 && tile != 10) return -1;
+  if (tile != 0 && tile != 2 && tile != 3 && tile != 10) return -1;   // (see g_tile)
   if (group_m < 0 || group_m > 64) return -1;
   g_resln_bm = resln_bm;
   g_tile = tile;
@@ -532,18 +539,13 @@ int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const flo
     const int rc = symb_gemm_lt(epi, A, lda, W, ldw, bias, R, ldr, C, ldc, M, N, K, st);
     if (rc != -1 && rc != -2) return rc;   // 0, or a HIP error; else this file's kernels
   }
-  if (g_tile == 3 && use_deep(M, N, K)) {
-    const int rc = symb_gemm_deep(epi == EPI_GELU ? 1 : epi == EPI_RES ? 2 : 0, A, lda, W, ldw,
-                                  bias, R, ldr, C, ldc, M, N, K, g_group_m, g_gelu_poly, st);
-    if (rc != -1) return rc;
-  }
-  if (use_big_tile(g_tile, M, N, K)) {
-#define SYMB_G(E) launch_cfg<256, 256, 2, 4, E>(a, lda, w, ldw, bias, r, ldr, gamma, beta, eps, c, \
-                                               ldc, M, N, K, st)
+  if (const int bn = big_tile_bn(g_tile, M, N, K)) {
+#define SYMB_G(E, BN_) launch_cfg<256, BN_, 2, 4, E>(a, lda, w, ldw, bias, r, ldr, gamma, beta, eps, \
+                                                    c, ldc, M, N, K, st)
     switch (epi) {
-      case EPI_BIAS: return SYMB_G(EPI_BIAS);
-      case EPI_GELU: return SYMB_G(EPI_GELU);
-      case EPI_RES: return SYMB_G(EPI_RES);
+      case EPI_BIAS: return bn == 256 ? SYMB_G(EPI_BIAS, 256) : SYMB_G(EPI_BIAS, 192);
+      case EPI_GELU: return bn == 256 ? SYMB_G(EPI_GELU, 256) : SYMB_G(EPI_GELU, 192);
+      case EPI_RES: return bn == 256 ? SYMB_G(EPI_RES, 256) : SYMB_G(EPI_RES, 192);
     }
 #undef SYMB_G
     return -1;
@@ -605,7 +607,7 @@ int symb_gemm_fp8(int epi, const void* A8, int lda, const void* W8, int ldw, con
   // measured faster -- long-K or wide-N projections (e5 QKV 1337 -> 1458, FFN2 MX-in 1687 -> 1867
   // TFLOP/s), not the square out-projection or the MX-emitting FFN1 (both slower),
   // profiles/r1_s4/fp8_waves/gemmfp8_256.json
-  const bool big = g_fp8_big != 0 && use_big_tile(3, M, N, K) &&
+  const bool big = g_fp8_big != 0 && big_tile_bn(10, M, N, K) == 256 &&
                    (g_fp8_big == 1 || (K >= 1024 && N != K && epi != EPI_GELU_MX8));
 #define SYMB_G8W(E, X, BMN, WM_, WN_) launch_cfg<BMN, BMN, WM_, WN_, E, 2, true, X>(              \
     A8, lda, W8, ldw, bias, r, ldr, nullptr, nullptr, g_gelu_poly ? 1.f : 0.f, c, ldc, M, N, K, \

@@ -74,17 +74,18 @@ def test_add_ln(H):
     (4099, 1536, 384, 1), (700, 384, 1536, 3),
     # > 256 tiles: more tiles than CUs
     (16384, 1152, 384, 0), (12800, 1536, 384, 1), (9000, 768, 3072, 2),
-    # 256x256 tiles (tile 2, and the deep kernel under auto) on every epilogue, ragged last row
-    (2000, 3072, 768, 1), (4353, 768, 3072, 2), (999, 2304, 768, 0), (33000, 768, 768, 2),
-    (300, 512, 128, 0), (513, 256, 256, 2),
+    # 256x256 tiles (tile 2) on every epilogue, ragged last row; 256x192 under auto (3): whole
+    # waves of N = 768 / 2304 grids, ragged last row tile
+    (2000, 3072, 768, 1), (4353, 768, 3072, 2), (999, 2304, 768, 0), (32700, 768, 768, 1),
+    (16384, 768, 3072, 2), (32768, 2304, 768, 0), (300, 512, 128, 0), (513, 256, 256, 2),
 ])
 def test_gemm(M, N, K, epi, tile):
     from codename_symbiont_amd.ops._ext import hip
     from codename_symbiont_amd.ops.kernels import gemm
 
     # tile=0: 128x128 4-wave tiles, 8-row grouped order; tile=2: gemm.hip's 256x256 wherever
-    # N % 256 == 0 (others fall back to 128x128), row-major order; tile=3: auto (the deep-ring
-    # kernel for the wide shapes), grouped order whose last band is short (group_m=3);
+    # N % 256 == 0 (others fall back to 128x128), row-major order; tile=3: auto (256x256 or
+    # 256x192 for the wide shapes), grouped order whose last band is short (group_m=3);
     # tile=10: auto without the deep kernel; tile=16: auto with the 8-wave (64x96 wave tiles)
     # row-complete RES_LN tile and the 64-row RES_LN tile (others: 16-wave, 128 rows)
     hip().gemm_config(64 if tile == 16 else 128, 3 if tile == 16 else tile,
@@ -101,65 +102,6 @@ def test_gemm(M, N, K, epi, tile):
         hip().gemm_resln_config(16)
     ref = R.gemm_ref(a, w, bias, epi, res, g, b, 1e-12)
     _close(out, ref, atol=4e-2, rtol=2e-2, what=f"gemm epi={epi}")
-
-
-@pytest.mark.parametrize("ns,sk", [(5, 1), (4, 1), (5, 0)])
-@pytest.mark.parametrize("M,N,K", [
-    (32768, 768, 768),    # 384 tiles: 256 whole + 128 split 2 ways (the bge out-projection)
-    (32768, 768, 3072),   # the bge FFN2 shape, long K
-    (9000, 768, 3072),    # ragged last row tile, 108 tiles: split 2 ways
-    (4100, 2304, 768),    # 153 tiles (> P/2): no split
-    (999, 1024, 1024),    # 16 tiles: split 2 ways (K/32 = 32 k-steps)
-    (300, 512, 128),      # 4 k-steps: one slice (the >= 4 k-steps per slice rule)
-    (777, 256, 2048),     # one column tile, split 2 ways
-    (65536, 1024, 1024),  # 1024 tiles: whole waves, no split
-])
-@pytest.mark.parametrize("epi", [0, 1, 2])
-def test_gemm_deep(M, N, K, epi, ns, sk):
-    """The deep-ring 256x256 kernel (gemm_deep.hip) through its own entry: ragged M, whole and
-    split last waves (2 slices, fp32 partials combined by the last arriving slice), both
-    ring depths, every epilogue, against the fp32 oracle -- and two launches are bit-identical
-    (slices are summed in slice order whichever arrives last)."""
-    from codename_symbiont_amd.ops._ext import hip, stream_handle
-
-    a = _bf(M, K, seed=1)
-    w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=2)
-    bias = _f(N, scale=0.5, seed=3)
-    res = _bf(M, N, seed=4) if epi == 2 else None
-    outs = []
-    hip().gemm_deep_config(ns, sk)
-    try:
-        for _ in range(2):
-            out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
-            hip().gemm_deep(epi, a.data_ptr(), K, w.data_ptr(), K, bias.data_ptr(),
-                            res.data_ptr() if res is not None else 0, N, out.data_ptr(), N, M, N, K,
-                            8, 1, stream_handle(a.device))
-            outs.append(out)
-        torch.cuda.synchronize()
-    finally:
-        hip().gemm_deep_config(5, 1)
-    ref = R.gemm_ref(a, w, bias, epi, res, None, None, 1e-12)
-    _close(outs[0], ref, atol=4e-2, rtol=2e-2, what=f"gemm_deep epi={epi} ns={ns} sk={sk}")
-    assert torch.equal(outs[0], outs[1]), "gemm_deep is not deterministic"
-
-
-def test_gemm_deep_split_counters_survive_many_launches():
-    """The split tiles' arrival / done counters are reset by each last arriver: 50 back-to-back
-    launches of a split shape (and a graph-free mix with an unsplit one) stay exact."""
-    from codename_symbiont_amd.ops.kernels import gemm
-
-    M, N, K = 4353, 768, 1536
-    a = _bf(M, K, seed=7)
-    w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=8)
-    bias = _f(N, scale=0.5, seed=9)
-    a2 = _bf(65536, 768, seed=10)
-    first = gemm(a, w, bias, 0)
-    for i in range(50):
-        out = gemm(a, w, bias, 0)
-        if i % 10 == 0:
-            gemm(a2, w[:, :768].contiguous(), bias, 0)
-        assert torch.equal(out, first), i
-    _close(first, R.gemm_ref(a, w, bias, 0, None, None, None, 1e-12), atol=4e-2, rtol=2e-2)
 
 
 @pytest.mark.parametrize("M,N,K,epi", [(300, 1152, 384, 0), (4100, 768, 3072, 2), (999, 2304, 768, 0),
