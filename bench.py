@@ -756,6 +756,10 @@ def run_gpu(args, info, comm) -> int:
         if len(shard._mq_tot) > 4:   # searches that sent only some row blocks to the bf16 scan
             extra_out["search_block_route_batches"] = int(shard._mq_tot[3].item())
             extra_out["search_block_routed_blocks"] = int(shard._mq_tot[4].item())
+        if shard.rows_i8 is not None:   # the pruning image's form (HbmIndexShard.calibrate_prune)
+            extra_out["i8_image"] = "split" if shard._i8_heavy else "plain"
+            extra_out["i8_calib_share"] = (None if shard.calib_share is None
+                                           else round(shard.calib_share, 3))
         print(f"[bench] rank {info.rank} searches: {ovf} overflowed, max "
               f"{int(shard._mq_tot[1].item())} candidates per query", file=sys.stderr, flush=True)
     if args.verify and args.mode != "embed":

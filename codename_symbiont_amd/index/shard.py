@@ -133,6 +133,8 @@ def resolve_prune(mode: str | None, dtype: str = "bf16", dim: int = 384,
 FP8_DIMS = (256, 384, 512, 768, 1024)   # row widths the fp8 scan kernel takes
 MQ_DIMS = (384, 768, 1024)              # ... the emitting bf16 scan (index_mq.hip)
 PRUNE_DIMS = (384, 768)                 # ... the int8-pruned scan (index_i8.hip)
+SPLIT_DIMS = (384,)                     # ... its split image (calibrate_prune)
+SPLIT_HEAVY = 64                        # leading components the split image keeps as fp16
 
 
 class HbmIndexShard:
@@ -181,12 +183,24 @@ class HbmIndexShard:
         # search (csrc/hip/index_i8.hip), plus the two global maxima its error bound needs:
         # E = max |x - x~| and X = max |x~| over every row ever written (monotone, so conservative)
         self.rows_i8 = self.sx_i8 = self.i8_bounds = None
+        # the image's form (calibrate_prune): 0 = plain int8 rows; SPLIT_HEAVY = the split image
+        # of PCA-rotated rows (leading components fp16, the rest int8) for anisotropic corpora
+        self.i8_split = os.environ.get("SYMB_I8_SPLIT", "auto").strip().lower()
+        self._i8_heavy = 0
+        self._i8_rot = None          # fp64 [D, D] orthogonal basis (rows: components) or None
+        self._calib_gen = 0
+        self._calib_next = self.CALIB_MIN_ROWS
+        self.calib_share = None      # variance share of the leading components at calibration
         if prune:
-            # padded to whole 128-row tiles: the int8 scan's DMA reads whole tiles
+            # padded to whole 128-row tiles: the int8 scan's DMA reads whole tiles; one flat byte
+            # store sized for the split form's wider rows where it applies (viewed per form)
             n_alloc = _round_up(self.rows.shape[0], 128)
-            self.rows_i8 = torch.zeros(n_alloc, dim, dtype=torch.int8, device=self.device)
+            rb = dim + SPLIT_HEAVY if dim in SPLIT_DIMS else dim
+            self._i8_store = torch.zeros(n_alloc * rb, dtype=torch.int8, device=self.device)
+            self.rows_i8 = self._i8_store[:n_alloc * dim].view(n_alloc, dim)
             self.sx_i8 = torch.ones(n_alloc, dtype=torch.float32, device=self.device)
-            self.i8_bounds = torch.zeros(2, dtype=torch.float32, device=self.device)
+            # (E, X) of the plain form; (E_l, X_l, E_h, X_h) of the split form
+            self.i8_bounds = torch.zeros(4, dtype=torch.float32, device=self.device)
         self.count = 0      # rows reserved (payload slots exist)
         # rows searches may read: published only after their writes are ENQUEUED on the stream
         # the scans share, so a search racing an upsert in another thread never scans a reserved
@@ -275,8 +289,12 @@ class HbmIndexShard:
         pruning image (no-ops without them).  Callers that write ``rows`` directly (snapshot loads)
         must call this too."""
         if self.rows_i8 is not None and n > 0:
-            self._quant_i8(self.rows[r0:r0 + n], self.rows_i8[r0:r0 + n], self.sx_i8[r0:r0 + n],
-                           self.i8_bounds)
+            due = r0 + n >= self._calib_next or (self.i8_split == "on" and not self._i8_heavy)
+            if due and self.i8_split != "off" and self.dim in SPLIT_DIMS:
+                self.calibrate_prune(r0 + n)   # (re-images every row below r0 + n)
+            else:
+                self._i8_image(self.rows[r0:r0 + n], self.rows_i8[r0:r0 + n],
+                               self.sx_i8[r0:r0 + n], self.i8_bounds)
         if self.rows8 is None or n <= 0:
             return
         src, dst = self.rows[r0:r0 + n], self.rows8[r0:r0 + n]
@@ -286,6 +304,135 @@ class HbmIndexShard:
             K.quant_fp8(src, dst, FP8_SCALE, False)
         else:
             dst.copy_((src.float() * FP8_SCALE).to(torch.float8_e4m3fn).view(torch.uint8))
+
+    # ------------------------------------------------------------------ int8 image form
+    CALIB_MIN_ROWS = 1 << 16   # first calibration once this many rows are written ...
+    CALIB_GROWTH = 16          # ... and again each time the shard grows this many times over
+    CALIB_SAMPLE = 1 << 16     # rows the second-moment matrix is estimated from
+    # the split form pays (+17 % image bytes and MFMA work) once the leading SPLIT_HEAVY principal
+    # components hold this share of the rows' energy: 64 / 384 = 0.17 for isotropic rows; the
+    # anisotropic corpus (index/synth.py) holds ~0.8, sentence-embedding spaces typically 0.4+
+    SPLIT_MIN_SHARE = 0.3
+
+    def calibrate_prune(self, hi: int | None = None) -> None:
+        """Choose the pruning image's form from the rows [0, hi) and re-image them all.
+
+        The int8 bound |q| E + |q - q~| X is a Cauchy-Schwarz bound with the scale set by each
+        row's largest component.  Where a few directions carry most of the energy (an anisotropic
+        corpus: a shared mean direction plus a power-law spread, as in sentence-embedding spaces)
+        those components set every row's int8 step, the bound covers a wide band of the crowded
+        scores and the route sends every block to the bf16 scan (profiles/r3_real: pruned = 1.00x
+        plain).  The split form rotates rows and queries into the principal basis of the rows'
+        second-moment matrix (fp64, orthogonal: q . x = (R q) . (R x)), keeps the leading
+        SPLIT_HEAVY components as fp16 (~11 bits, their rounding in the bound) and quantises only
+        the trailing ones to int8 with their own, much finer, per-row step.  On the anisotropic
+        corpus the candidates per query drop ~30x (tests/test_index_cpu.py); exactness never
+        depends on R, only the cost does, so R is fixed between calibrations (first at
+        CALIB_MIN_ROWS rows, then at every CALIB_GROWTH-fold growth)."""
+        if self.rows_i8 is None:
+            return
+        hi = self.count if hi is None else int(hi)
+        if hi <= 0:
+            return
+        heavy, rot, share = 0, None, None
+        if self.dim in SPLIT_DIMS and self.i8_split != "off":
+            stride = max(1, hi // self.CALIB_SAMPLE)
+            smp = self.rows[0:hi:stride][:self.CALIB_SAMPLE].double()
+            m2 = smp.t() @ smp / smp.shape[0]
+            ev, vec = torch.linalg.eigh(m2)                 # ascending
+            ev, vec = ev.flip(0), vec.flip(1)
+            share = float(ev[:SPLIT_HEAVY].sum() / ev.sum().clamp_min(1e-30))
+            if self.i8_split == "on" or share >= self.SPLIT_MIN_SHARE:
+                heavy, rot = SPLIT_HEAVY, vec.t().contiguous()
+        self._i8_heavy, self._i8_rot, self.calib_share = heavy, rot, share
+        rb = self.dim + heavy
+        n_alloc = self.sx_i8.shape[0]
+        self.rows_i8 = self._i8_store[:n_alloc * rb].view(n_alloc, rb)
+        self.i8_bounds.zero_()
+        chunk = 1 << 18
+        for s in range(0, hi, chunk):
+            e = min(hi, s + chunk)
+            self._i8_image(self.rows[s:e], self.rows_i8[s:e], self.sx_i8[s:e], self.i8_bounds)
+        self._calib_gen += 1
+        self._calib_next = max(hi * self.CALIB_GROWTH, self.CALIB_MIN_ROWS)
+
+    def prune_query_image(self, q_unit: torch.Tensor):
+        """(image, scale, margin) of unit queries in the shard's current form: the int8 image and
+        |q| E + |q - q~| X + 1e-5 (prune_qquant), or the split image in the shard's basis and
+        |q_l| E_l + |q_l - q~_l| X_l + |q_h| E_h + |q_h - q^_h| X_h + 1e-5 (quant_rows_split)."""
+        NQ, dev, heavy = q_unit.shape[0], self.device, self._i8_heavy
+        q8 = torch.empty(NQ, self.dim + heavy, dtype=torch.int8, device=dev)
+        sq = torch.empty(NQ, dtype=torch.float32, device=dev)
+        margin = torch.empty(NQ, dtype=torch.float32, device=dev)
+        if dev.type != "cuda":
+            from ..ops import reference as R
+
+            b = self.i8_bounds
+            if heavy:
+                img, sc, nr = R.quant_rows_split_ref(self._rotate(q_unit), heavy)
+                m = nr[:, 2] * b[0] + nr[:, 0] * b[1] + nr[:, 5] * b[2] + nr[:, 3] * b[3]
+            else:
+                img, sc, err, _ = R.quant_rows_i8_ref(q_unit)
+                m = q_unit.float().norm(dim=1) * b[0] + err * b[1]
+            q8.copy_(img)
+            sq.copy_(sc)
+            margin.copy_(m + 1e-5)
+            return q8, sq, margin
+        from ..ops._ext import hip, stream_handle
+
+        st = stream_handle(dev)
+        if heavy:
+            qr = self._rotate(q_unit)
+            hip().quant_rows_split(qr.data_ptr(), NQ, self.dim, q8.data_ptr(), sq.data_ptr(),
+                                   self.i8_bounds.data_ptr(), margin.data_ptr(), st)
+        else:
+            hip().prune_qquant(q_unit.data_ptr(), NQ, self.dim, self.i8_bounds.data_ptr(),
+                               q8.data_ptr(), sq.data_ptr(), margin.data_ptr(), st)
+        return q8, sq, margin
+
+    def prune_estimate(self, q8: torch.Tensor, sq: torch.Tensor, r0: int = 0,
+                       r1: int | None = None) -> torch.Tensor:
+        """The int8 scan's estimate of every (query, row) score over rows [r0, r1) (torch; the
+        bound oracle of the tests): sq sx (q8 . x8), or the split form's q^_h . x^_h + sq sx
+        (q8_l . x8_l)."""
+        from ..ops import reference as R
+
+        r1 = self.count if r1 is None else r1
+        x8, sx = self.rows_i8[r0:r1], self.sx_i8[r0:r1]
+        if self._i8_heavy:
+            return R.split_estimate_ref(q8, sq, x8, sx, self._i8_heavy)
+        return (q8.float() @ x8.float().t()) * sq[:, None] * sx[None, :]
+
+    def _rotate(self, x: torch.Tensor) -> torch.Tensor:
+        """Rows / queries in the split form's basis: fp64 product, rounded once to fp32."""
+        return (x.double() @ self._i8_rot.t()).float().contiguous()
+
+    def _i8_image(self, src, dst8, scale, bounds) -> None:
+        """The pruning image of bf16 rows ``src`` in the shard's current form (bounds raised)."""
+        n = src.shape[0]
+        if n == 0:
+            return
+        if not self._i8_heavy:
+            self._quant_i8(src, dst8, scale, bounds)
+            return
+        chunk = 1 << 18      # bounds the fp64 / fp32 rotation temporaries (~1.2 GB at 384)
+        for s in range(0, n, chunk):
+            e = min(n, s + chunk)
+            xr = self._rotate(src[s:e])
+            if self.device.type == "cuda":
+                from ..ops._ext import hip, stream_handle
+
+                hip().quant_rows_split(xr.data_ptr(), e - s, self.dim, dst8[s:e].data_ptr(),
+                                       scale[s:e].data_ptr(), bounds.data_ptr(), 0,
+                                       stream_handle(self.device))
+            else:
+                from ..ops.reference import quant_rows_split_ref
+
+                img, sc, nrm = quant_rows_split_ref(xr, self._i8_heavy)
+                dst8[s:e].copy_(img)
+                scale[s:e].copy_(sc)
+                m = nrm.amax(0)
+                torch.maximum(bounds, torch.stack([m[0], m[1], m[3], m[4]]), out=bounds)
 
     def _quant_i8(self, src, dst8, scale, bounds=None):
         """Per-row int8 image of bf16 rows (index_i8.hip quant_rows_i8).  With ``bounds`` (the
@@ -311,7 +458,7 @@ class HbmIndexShard:
             dst8.copy_(q8)
             scale.copy_(sc)
         if bounds is not None:
-            torch.maximum(bounds, torch.stack([err.max(), xtn.max()]), out=bounds)
+            torch.maximum(bounds[:2], torch.stack([err.max(), xtn.max()]), out=bounds[:2])
         return err, xtn
 
     def _store(self, r0: int, x: torch.Tensor, normalize: bool) -> None:
@@ -368,16 +515,18 @@ class HbmIndexShard:
             raise IndexError("write_rows_f32: row outside the shard")
         self._mark_written(idx.tolist())
         scratch = HbmIndexShard(self.dim, n, self.device, dtype=self.dtype,
-                                prefilter=self.prefilter, prune=self.prune)
+                                prefilter=self.prefilter)
         scratch.append_f32(vecs)
         di = idx.to(self.device)
         self.rows.index_copy_(0, di, scratch.rows[:n])
         if self.rows8 is not None:
             self.rows8.index_copy_(0, di, scratch.rows8[:n])
-        if self.rows_i8 is not None:
-            self.rows_i8.index_copy_(0, di, scratch.rows_i8[:n])
-            self.sx_i8.index_copy_(0, di, scratch.sx_i8[:n])
-            torch.maximum(self.i8_bounds, scratch.i8_bounds, out=self.i8_bounds)
+        if self.rows_i8 is not None:   # the image in THIS shard's form (its basis, its bounds)
+            img = torch.empty(n, self.rows_i8.shape[1], dtype=torch.int8, device=self.device)
+            sc = torch.empty(n, dtype=torch.float32, device=self.device)
+            self._i8_image(scratch.rows[:n], img, sc, self.i8_bounds)
+            self.rows_i8.index_copy_(0, di, img)
+            self.sx_i8.index_copy_(0, di, sc)
 
     def upsert(self, point_ids: list[str], vecs: torch.Tensor, payloads: list[Payload]) -> list[int]:
         """Qdrant-style upsert: existing ids are overwritten in place, new ids appended.  An id
@@ -718,12 +867,10 @@ class HbmIndexShard:
             n_cus = self._n_cus()
         h, dev, cap = hip(), self.device, self.PRUNE_CAP
         st = stream_handle(dev)
-        # 0. the int8 queries and each query's bound margin |q| E + |q - q~| X (prune_qquant)
-        q8 = torch.empty(NQ, self.dim, dtype=torch.int8, device=dev)
-        sq = torch.empty(NQ, dtype=torch.float32, device=dev)
-        margin = torch.empty(NQ, dtype=torch.float32, device=dev)
-        h.prune_qquant(q_unit.data_ptr(), NQ, self.dim, self.i8_bounds.data_ptr(), q8.data_ptr(),
-                       sq.data_ptr(), margin.data_ptr(), st)
+        # 0. the int8 queries and each query's bound margin |q| E + |q - q~| X (prune_qquant), or
+        #    their split image in the shard's basis and its margin (quant_rows_split)
+        heavy = self._i8_heavy
+        q8, sq, margin = self.prune_query_image(q_unit)
         # 1. T: the k-th best exact score of a sample of real rows (1 tile in 2^ts, plus the last
         #    4096+ rows where fresh inserts sit), as in _search_scan; its emitted candidates also
         #    estimate the int8 band's population (prune_route)
@@ -779,7 +926,7 @@ class HbmIndexShard:
                       tail_ci=0 if tci is None else tci.data_ptr(),
                       tail_cnt=0 if tcnt is None else tcnt.data_ptr(), tail_cap=tcap, tail_off=t0)
         return dict(q=q_unit, k=k, n=n, n_cus=n_cus, q8=q8, sq=sq, thr=thr, T=T, dense=dense,
-                    blk=blk, geo=geo)
+                    blk=blk, geo=geo, heavy=heavy, gen=self._calib_gen)
 
     def _i8_geometry(self, n: int, NQ: int, n_cus: int):
         """(rsplit, rows_per_blk, n_rblk) of the int8 scan over n rows: ~one workgroup per CU
@@ -787,10 +934,13 @@ class HbmIndexShard:
         from ..ops._ext import hip
 
         h = hip()
+        heavy = self._i8_heavy
         rsplit = 2 if (NQ < 512 or self.i8_rsplit2) else 1
-        tr = h.i8_tile_rows(self.dim)
-        n_qblk = math.ceil(NQ / h.i8_queries_per_blk(rsplit))
-        wpc = h.i8_wgs_per_cu()
+        tr = h.i8_tile_rows(self.dim, heavy)
+        if heavy:   # (the split image always runs 8-wave workgroups, one per CU)
+            n_qblk, wpc = math.ceil(NQ / h.i8_split_queries_per_blk(rsplit)), 1
+        else:
+            n_qblk, wpc = math.ceil(NQ / h.i8_queries_per_blk(rsplit)), h.i8_wgs_per_cu()
         n_rblk = max(1, min(math.ceil(n / (tr * 16)), max(1, round(n_cus * wpc / n_qblk))))
         rows_per_blk = _round_up(max(1, math.ceil(n / n_rblk)), tr)
         n_rblk = max(1, math.ceil(n / rows_per_blk))
@@ -820,6 +970,12 @@ class HbmIndexShard:
         rsplit, rows_per_blk, n_rblk = ctx["geo"]
         NQ = q_unit.shape[0]
         st = stream_handle(dev)
+        if ctx["gen"] != self._calib_gen:
+            # the image was re-calibrated between the halves (a new basis / bounds): its query
+            # image no longer matches -- the exact bf16 list scan, seeded with the exact T
+            out = (torch.empty(NQ, k, device=dev), torch.empty(NQ, k, dtype=torch.int32, device=dev))
+            self._scan(n, q_unit, kmax, k, T.contiguous(), n_cus, out=out)
+            return out
         # 3. int8 scan of the blocks the route kept: emit every row with (q8 . x8) * sx >= thr
         cs = torch.empty(NQ, cap, device=dev)
         ci = torch.empty(NQ, cap, dtype=torch.int32, device=dev)
@@ -831,7 +987,8 @@ class HbmIndexShard:
         h.index_scan_i8(self.rows_i8.data_ptr(), self.sx_i8.data_ptr(), n, self.rows_i8.shape[0],
                         rows_per_blk, n_rblk,
                         q8.data_ptr(), NQ, thr.data_ptr(), cs.data_ptr(), ci.data_ptr(),
-                        cnt.data_ptr(), cap, self.scan_xcd, st, rsplit, skip=skip, dim=self.dim)
+                        cnt.data_ptr(), cap, self.scan_xcd, st, rsplit, skip=skip, dim=self.dim,
+                        heavy=ctx["heavy"], sq=ctx["sq"].data_ptr())
         # 3'. the bf16 emitting scan of the blocks the route listed, at the exact threshold T,
         #     into the same candidate buffers (no launch work when none is listed)
         if self.prune_route:

@@ -106,3 +106,37 @@ def quant_rows_i8_ref(x: torch.Tensor):
     q = torch.round(xf / sc[:, None]).clamp_(-127, 127)
     xt = q * sc[:, None]
     return q.to(torch.int8), sc, (xf - xt).norm(dim=1), xt.norm(dim=1)
+
+
+SPLIT_HEAVY = 64   # leading (rotated) dims the split int8 image keeps as fp16
+
+
+def quant_rows_split_ref(xr: torch.Tensor, heavy: int = SPLIT_HEAVY):
+    """Split image of ROTATED fp32 rows (index_i8.hip quant_rows_split): the leading ``heavy``
+    dims as fp16 (bytes 0 .. 2 heavy of each image row), the rest as int8 with scale
+    max |x_l| / 127.  Returns (img int8 [n, D + heavy], scale, norms) with norms = the 6 per-row
+    norms (|x_l - x~_l|, |x~_l|, |x_l|, |x_h - x^_h|, |x^_h|, |x_h|) the bound is built from."""
+    xf = xr.float()
+    xh, xl = xf[:, :heavy], xf[:, heavy:]
+    amax = xl.abs().amax(dim=1)
+    sc = torch.where(amax > 0, amax / 127.0, torch.ones_like(amax))
+    q = torch.round(xl * (1.0 / sc)[:, None]).clamp_(-127, 127)
+    xt = q * sc[:, None]
+    hh = xh.half()
+    img = torch.cat([hh.view(torch.int8).reshape(xf.shape[0], 2 * heavy), q.to(torch.int8)], 1)
+    hf = hh.float()
+    norms = torch.stack([(xl - xt).norm(dim=1), xt.norm(dim=1), xl.norm(dim=1),
+                         (xh - hf).norm(dim=1), hf.norm(dim=1), xh.norm(dim=1)], 1)
+    return img, sc, norms
+
+
+def split_estimate_ref(q_img: torch.Tensor, sq: torch.Tensor, x_img: torch.Tensor,
+                       sx: torch.Tensor, heavy: int = SPLIT_HEAVY) -> torch.Tensor:
+    """The split scan's estimate of every (query, row) score, q^_h . x^_h + sq sx (q8_l . x8_l)
+    (index_scan_i8_kernel HK = 2, as acc_f + acc_i * sq * sx)."""
+    def parts(img):
+        h = img[:, :2 * heavy].contiguous().view(torch.float16).float()
+        return h, img[:, 2 * heavy:].float()
+    qh, ql = parts(q_img)
+    xh, xl = parts(x_img)
+    return qh @ xh.t() + (ql @ xl.t()) * sq[:, None] * sx[None, :]

@@ -68,8 +68,11 @@ int symb_i8_queries_per_blk(int rsplit);
 int symb_index_scan_i8(const void* X8, const float* sx, int n_valid, int alloc_rows,
                        int rows_per_blk, int n_rblk, const void* Q8, int NQ, const float* thr,
                        float* cand_s, int* cand_i, int* cand_n, int cap, int xcd, hipStream_t st,
-                       int rsplit, const int* skip, int dim);
-int symb_i8_tile_rows_for(int dim);
+                       int rsplit, const int* skip, int dim, int heavy, const float* sq);
+int symb_i8_tile_rows_for(int dim, int heavy);
+int symb_i8_split_queries_per_blk(int rsplit);
+int symb_quant_rows_split(const float* X, int n, int dim, void* X8, float* sx, float* bounds,
+                          float* margin, hipStream_t st);
 int symb_prune_qquant(const void* Q, int NQ, int dim, const float* bounds, void* Q8, float* sq,
                       float* margin, hipStream_t st);
 int symb_prune_route(int NQ, const float* pre_s, const float* tail_s, int k, float thr_margin,
@@ -385,20 +388,33 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("rsplit") = 2);
   m.def("i8_config", [](int tile_rows, int waves) { check(symb_i8_config(tile_rows, waves), "i8_config"); },
         py::arg("tile_rows"), py::arg("waves") = 8);
-  m.def("i8_tile_rows", [](int dim) { return symb_i8_tile_rows_for(dim); }, py::arg("dim") = 384);
+  m.def("i8_tile_rows", [](int dim, int heavy) { return symb_i8_tile_rows_for(dim, heavy); },
+        py::arg("dim") = 384, py::arg("heavy") = 0);
+  m.def("i8_split_queries_per_blk", [](int rsplit) { return symb_i8_split_queries_per_blk(rsplit); },
+        py::arg("rsplit") = 2);
+  m.def("quant_rows_split", [](uptr X, int n, int dim, uptr X8, uptr sx, uptr bounds, uptr margin,
+                               uptr st) {
+    check(symb_quant_rows_split(P<const float>(X), n, dim, P<void>(X8), P<float>(sx),
+                                P<float>(bounds), P<float>(margin), S(st)),
+          "quant_rows_split");
+  }, py::arg("X"), py::arg("n"), py::arg("dim"), py::arg("X8"), py::arg("sx"), py::arg("bounds"),
+     py::arg("margin"), py::arg("stream"));
   m.def("i8_wgs_per_cu", []() { return symb_i8_wgs_per_cu(); });
   m.def("index_scan_i8", [](uptr X8, uptr sx, int n_valid, int alloc_rows, int rows_per_blk,
                             int n_rblk, uptr Q8, int NQ, uptr thr, uptr cand_s, uptr cand_i,
-                            uptr cand_n, int cap, int xcd, uptr st, int rsplit, uptr skip, int dim) {
+                            uptr cand_n, int cap, int xcd, uptr st, int rsplit, uptr skip, int dim,
+                            int heavy, uptr sq) {
     check(symb_index_scan_i8(P<void>(X8), P<const float>(sx), n_valid, alloc_rows, rows_per_blk,
                              n_rblk,
                              P<void>(Q8), NQ, P<const float>(thr), P<float>(cand_s), P<int>(cand_i),
-                             P<int>(cand_n), cap, xcd, S(st), rsplit, P<const int>(skip), dim),
+                             P<int>(cand_n), cap, xcd, S(st), rsplit, P<const int>(skip), dim,
+                             heavy, P<const float>(sq)),
           "index_scan_i8");
   }, py::arg("X8"), py::arg("sx"), py::arg("n_valid"), py::arg("alloc_rows"),
      py::arg("rows_per_blk"), py::arg("n_rblk"), py::arg("Q8"), py::arg("NQ"), py::arg("thr"),
      py::arg("cand_s"), py::arg("cand_i"), py::arg("cand_n"), py::arg("cap"), py::arg("xcd"),
-     py::arg("stream"), py::arg("rsplit"), py::arg("skip") = 0, py::arg("dim") = 384);
+     py::arg("stream"), py::arg("rsplit"), py::arg("skip") = 0, py::arg("dim") = 384,
+     py::arg("heavy") = 0, py::arg("sq") = 0);
   m.def("prune_qquant", [](uptr Q, int NQ, int dim, uptr bounds, uptr Q8, uptr sq, uptr margin,
                            uptr st) {
     check(symb_prune_qquant(P<void>(Q), NQ, dim, P<const float>(bounds), P<void>(Q8), P<float>(sq),

@@ -248,6 +248,8 @@ __global__ __launch_bounds__(256, 1) void index_scan_fp8_kernel(
       }
       if (sub + 1 < SUBS)  // next sub-tile's first fragments fly during this top-k
         fp8_prologue<0, PF, R, G>(lo, hi, voff, base + SUB_BYTES);
+      // (reads of the asm MFMA results stay below the chain-end s_nops: index_i8.hip emit)
+      asm volatile("" : "+v"(acc0), "+v"(acc1));
       update(acc0, tv0, ti0, thr0, row0 + sub * SUB);
       update(acc1, tv1, ti1, thr1, row0 + sub * SUB);
     }

@@ -46,11 +46,16 @@ constexpr int PIECE = 1024;
 // B fragments take SETS x NKS x 4 = 96 / 192 VGPRs.
 // Fragment reads in flight: PF (NKS % (PF + 1) == 0); 3 at D = 768, whose 192 query registers
 // leave no room for a 6-slot fragment ring.
-template <int D> struct I8Dim {
-  static constexpr int NKS = D / 64;
-  static constexpr int PF = D == 384 ? SYMB_I8_PF : 3;
+// HK > 0: the SPLIT image (see "split image" below): the first 32 * HK dims of each (rotated) row
+// as fp16, HK v_mfma_f32_16x16x32_f16 k-steps of 64 bytes, then the other D - 32 * HK dims as
+// int8 -- RB = 448 bytes per 384-wide row.  Only the fused two-sub-tile chains run it.
+template <int D, int HK = 0> struct I8Dim {
+  static constexpr int NKS = (D + 32 * HK) / 64;
+  static constexpr int RB = NKS * 64;            // image bytes per row
+  static constexpr int PF = HK ? NKS - 1 : (D == 384 ? SYMB_I8_PF : 3);
   static constexpr int R = PF + 1;
   static_assert(D == 384 || D == 768, "int8 scan row width");
+  static_assert(HK == 0 || (D == 384 && HK == 2), "split image: 64 fp16 + 320 int8 dims");
   static_assert(NKS % R == 0, "cross-chain prefetch: fragment j of the next chain uses slot j % R");
 };
 
@@ -59,21 +64,30 @@ template <int D> struct I8Dim {
 // WV = 4 (D = 384): 4-wave workgroups (one wave per SIMD), TWO per CU, each with its own 3-deep
 // ring: the two waves sharing a SIMD then belong to different workgroups, so one's barrier,
 // prologue and DMA burst fall under the other's MFMAs instead of in lockstep with them.
-template <int D, int TR_, int WV_ = 8> struct Geo {
+// Split image (HK = 2): 28 KiB tiles = 28 pieces over 8 waves, so waves 0-3 carry 4 pieces and
+// waves 4-7 three (FULLW); a 5-deep ring still fits (156 KiB with the stages).
+template <int D, int TR_, int WV_ = 8, int HK = 0> struct Geo {
   static constexpr int TR = TR_;
   static constexpr int WV = WV_;
-  static constexpr int NKS = I8Dim<D>::NKS;
+  static constexpr int NKS = I8Dim<D, HK>::NKS;
+  static constexpr int RB = I8Dim<D, HK>::RB;
   static constexpr int NSUB = TR / i8s::SUB;
-  static constexpr int TILE_BYTES = TR * D;
-  static constexpr int NS = WV == 4 ? 3 : (TILE_BYTES <= 24 * 1024 ? 5 : 3);
-  static constexpr int LOADS = TILE_BYTES / (1024 * WV);      // LDS-DMA pieces per wave per tile
+  static constexpr int TILE_BYTES = TR * RB;
+  static constexpr int PIECES = TILE_BYTES / 1024;
+  static constexpr int LOADS = (PIECES + WV - 1) / WV;        // LDS-DMA pieces per wave per tile
+  static constexpr int FULLW = PIECES % WV ? PIECES % WV : WV;   // waves carrying LOADS (rest: - 1)
   static constexpr int DMA_EVERY = NKS / LOADS;               // k-steps between pieces
   static constexpr int SCW = TR / 64;                         // waves carrying a scale DMA
   static constexpr int SC_BYTES = TR * 4;
   static constexpr int STW = WV == 4 ? 160 : (TR == 64 ? 192 : 128);   // staged candidates per wave
   static constexpr int STAGE_BYTES = STW * 10;
+  static constexpr int NS = WV == 4 ? 3
+                            : (TILE_BYTES <= 24 * 1024 ||
+                               (HK && 5 * (TILE_BYTES + SC_BYTES) + WV * STAGE_BYTES <= 160 * 1024))
+                                ? 5 : 3;
   static constexpr int LDS_BYTES = NS * TILE_BYTES + NS * SC_BYTES + WV * STAGE_BYTES;
-  static_assert(TILE_BYTES % (1024 * WV) == 0, "tile must split evenly over waves");
+  static_assert(TILE_BYTES % 1024 == 0 && (HK || PIECES % WV == 0), "tile must split over waves");
+  static_assert(SCW <= FULLW, "the scale waves carry a full share of pieces");
   static_assert(WV == 8 || 2 * LDS_BYTES <= 160 * 1024, "two 4-wave workgroups must share a CU");
   static_assert(NSUB * NKS * i8s::PIECE == TILE_BYTES, "a tile is NSUB x NKS pieces");
   static_assert(LOADS * DMA_EVERY <= NKS && DMA_EVERY >= 1, "DMA pieces must fit the first chain");
@@ -96,6 +110,15 @@ __device__ __forceinline__ void i8_mfma(i32x4& acc, const i32x4& a, const i32x4&
     asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, 0" : "=&v"(acc) : "v"(a), "v"(q));
   else
     asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(q));
+}
+// the split image's fp16 k-steps: the same 16-byte-per-lane operand layout (row / query lane & 15,
+// k-bytes 16 * (lane >> 4)), so fragments come from the same LDS offsets as the int8 ones
+template <bool FIRST>
+__device__ __forceinline__ void h16_mfma(f32x4& acc, const i32x4& a, const i32x4& q) {
+  if constexpr (FIRST)
+    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "=&v"(acc) : "v"(a), "v"(q));
+  else
+    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(q));
 }
 
 // k-step KS of one 16-row sub-tile (index_mq.hip MqChain, int8 operands).
@@ -140,11 +163,13 @@ __device__ __forceinline__ void i8_lgkm2t(i32x4& v0, i32x4& v1, f32x4& t0, f32x4
 // t0 / t1: the two sub-tiles' row scales, read from LDS just before the prologue; the first
 // k-step's wait covers them (older than every fragment read), so the emission after the chain
 // finds them in registers
-template <int D, int KS, int DMA_PIECES, int DE>
+template <int D, int KS, int DMA_PIECES, int DE, int HK = 0>
 struct I8Chain2 {
-  static constexpr int NKS = I8Dim<D>::NKS;
+  static constexpr int NKS = I8Dim<D, HK>::NKS;
   template <class Dma>
-  __device__ __forceinline__ static void run(i32x4 (&acc)[2][i8s::SETS], i32x4 (&a)[i8s::R2][2],
+  __device__ __forceinline__ static void run(i32x4 (&acc)[2][i8s::SETS],
+                                             f32x4 (&accf)[HK ? 2 : 1][i8s::SETS],
+                                             i32x4 (&a)[i8s::R2][2],
                                              const i32x4 (&qf)[i8s::SETS][NKS],
                                              uint32_t base, const Dma& dma, f32x4& t0, f32x4& t1) {
     using namespace i8s;
@@ -157,20 +182,26 @@ struct I8Chain2 {
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll
-      for (int s = 0; s < SETS; ++s) i8_mfma<KS == 0>(acc[c][s], a[KS % R2][c], qf[s][KS]);
+      for (int s = 0; s < SETS; ++s) {
+        if constexpr (KS < HK)
+          h16_mfma<KS == 0>(accf[c][s], a[KS % R2][c], qf[s][KS]);
+        else
+          i8_mfma<KS == HK>(acc[c][s], a[KS % R2][c], qf[s][KS]);
+      }
     if constexpr (KS + 1 == NKS) asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
     if constexpr (KS + PF2 < NKS) {
       i8_read16<(KS + PF2) * PIECE>(a[(KS + PF2) % R2][0], base);
       i8_read16<(KS + PF2) * PIECE + NKS * PIECE>(a[(KS + PF2) % R2][1], base);
     }
-    if constexpr (KS + 1 < NKS) I8Chain2<D, KS + 1, DMA_PIECES, DE>::run(acc, a, qf, base, dma, t0, t1);
+    if constexpr (KS + 1 < NKS)
+      I8Chain2<D, KS + 1, DMA_PIECES, DE, HK>::run(acc, accf, a, qf, base, dma, t0, t1);
   }
 };
-template <int D, int J>
+template <int D, int J, int HK = 0>
 __device__ __forceinline__ void i8_prologue2(i32x4 (&a)[i8s::R2][2], uint32_t base) {
   i8_read16<J * i8s::PIECE>(a[J % i8s::R2][0], base);
-  i8_read16<J * i8s::PIECE + I8Dim<D>::NKS * i8s::PIECE>(a[J % i8s::R2][1], base);
-  if constexpr (J + 1 < i8s::PF2) i8_prologue2<D, J + 1>(a, base);
+  i8_read16<J * i8s::PIECE + I8Dim<D, HK>::NKS * i8s::PIECE>(a[J % i8s::R2][1], base);
+  if constexpr (J + 1 < i8s::PF2) i8_prologue2<D, J + 1, HK>(a, base);
 }
 
 template <int D, int J>
@@ -192,15 +223,21 @@ __device__ __forceinline__ const char* i8_uniform(const char* p) {
 // ABL (profiling entry symb_index_scan_i8_ablate only): 1 = no LDS-DMA, 2 = no emission test,
 // 3 = full + s_memtime / s_memrealtime around the tile loop into cand_s[2 * blockIdx.x + {0, 1}],
 // 4 = LDS-DMA ring only.
-template <int D, int RSPLIT, int ABL = 0, int TRK = 64, int WV = 8>
+//
+// HK = 2 (the split image, index/shard.py calibrate_prune): rows and queries are rotated by the
+// shard's orthogonal PCA basis, the 64 leading components are kept as fp16 (an fp32 MFMA dot, ~11
+// bits each) and only the 320 trailing ones quantised to int8 with their own per-row scale.
+// Emit iff acc_f / sq + acc_i * sx >= thr (sq_in: the queries' int8 scales); the bound (prune_
+// qquant_h) is the int8 one on the trailing dims plus the fp16 rounding of the leading ones.
+template <int D, int RSPLIT, int ABL = 0, int TRK = 64, int WV = 8, int HK = 0>
 __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
     const int8_t* __restrict__ X8, const float* __restrict__ sx, int n_valid, int rows_per_blk,
     const int8_t* __restrict__ Q8, int NQ, int n_qblk, int xcd, const float* __restrict__ thr_in,
     float* __restrict__ cand_s, int* __restrict__ cand_i, int* __restrict__ cand_n, int cap,
-    const int* __restrict__ skip) {
+    const int* __restrict__ skip, const float* __restrict__ sq_in) {
   using namespace i8s;
-  using G = Geo<D, TRK, WV>;
-  constexpr int NKS = G::NKS;
+  using G = Geo<D, TRK, WV, HK>;
+  constexpr int NKS = G::NKS, RB = G::RB;
   constexpr int TR = G::TR, NSUB = G::NSUB, NS = G::NS, TILE_BYTES = G::TILE_BYTES;
   constexpr int LOADS = G::LOADS, SC_BYTES = G::SC_BYTES, STW = G::STW;
   constexpr int STAGE_BYTES = G::STAGE_BYTES;
@@ -226,31 +263,36 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
   const int qbase = qb * QPB + qwave * QW + (lane & 15);
   i32x4 qf[SETS][NKS];
   float thr[SETS];
+  float rsq[SETS];   // (split image) 1 / the query's int8 scale: acc_f is in score units
 #pragma unroll
   for (int s = 0; s < SETS; ++s) {
     const int q = qbase + s * 16;
-    const int8_t* qp = Q8 + (size_t)min(q, NQ - 1) * D + (lane >> 4) * 16;
+    const int8_t* qp = Q8 + (size_t)min(q, NQ - 1) * RB + (lane >> 4) * 16;
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) qf[s][ks] = *reinterpret_cast<const i32x4*>(qp + ks * 64);
     thr[s] = q < NQ ? thr_in[q] : INFINITY;
+    if constexpr (HK > 0) rsq[s] = 1.f / sq_in[min(q, NQ - 1)];
   }
 #pragma unroll
   for (int s = 0; s < SETS; ++s) {
     asm volatile("" ::"v"(thr[s]));
+    if constexpr (HK > 0) asm volatile("" ::"v"(rsq[s]));
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) asm volatile("" ::"v"(qf[s][ks]));
   }
 
   // ---- LDS-DMA (index_mq.hip layout): lane l fetches row l>>2 of a piece, chunk (l&3)^f ------
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
-  const uint32_t loff = (uint32_t)((lane >> 2) * D + (((lane & 3) ^ ((lane >> 3) & 2)) * 16));
+  const uint32_t loff = (uint32_t)((lane >> 2) * RB + (((lane & 3) ^ ((lane >> 3) & 2)) * 16));
   char* scl = smem + NS * TILE_BYTES;   // NS x 64 row scales
   auto issue_tile = [&](int t, int i) {  // piece i of tile t (+ the scales: wave 0, piece 0)
     const int tt = min(t, n_tiles - 1);   // past the end: re-load the last tile (vmcnt stays exact)
     const int p = i * WV + wave_u, j = p / NKS, ks = p % NKS;
     const int prow = row_begin + tt * TR;
-    const char* base = reinterpret_cast<const char*>(X8 + (size_t)(prow + j * SUB) * D + ks * 64);
-    glds16_aux<0>(i8_uniform(base) + loff, smem + (t % NS) * TILE_BYTES + p * PIECE);
+    const char* base = reinterpret_cast<const char*>(X8 + (size_t)(prow + j * SUB) * RB + ks * 64);
+    // (split image: the last round of pieces covers waves < FULLW only; wave-uniform)
+    if (G::FULLW == WV || p < G::PIECES)
+      glds16_aux<0>(i8_uniform(base) + loff, smem + (t % NS) * TILE_BYTES + p * PIECE);
     if (wave_u < G::SCW && i == 0)   // 64 row scales per scale wave
       __builtin_amdgcn_global_load_lds(
           (const __attribute__((address_space(1))) void*)(sx + prow + 64 * wave_u + lane),
@@ -283,11 +325,55 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
   auto scales = [&](int slot, int jj) {
     return *reinterpret_cast<const f32x4*>(scl + slot * SC_BYTES + (jj * SUB + 4 * (lane >> 4)) * 4);
   };
-  // one 16-row sub-tile at row0 with this lane's row scales s4
-  auto emit = [&](i32x4 (&acc)[SETS], int row0, const f32x4 s4) {
+  // one 16-row sub-tile at row0 with this lane's row scales s4 (af: the split image's fp16-part
+  // accumulators, unused without it)
+  auto emit = [&](i32x4 (&acc)[SETS], auto& af, int row0, const f32x4 s4) {
+    // the chains' MFMAs are inline asm, invisible to the compiler's MFMA -> VALU hazard
+    // recognizer: their results are only safe to read after the chain-end s_nops.  An empty
+    // volatile asm "rewriting" the accumulators keeps every read below it (volatile asm stays in
+    // program order); without it a plain C++ read was scheduled above the s_nops and saw a
+    // stale first accumulator register (the split image's 512-query form lost rows 0 mod 4 of
+    // sub-tile 0, set 0: benchmarks/diag/split_emit.py)
+#pragma unroll
+    for (int s = 0; s < SETS; ++s) {
+      asm volatile("" : "+v"(acc[s]));
+      if constexpr (HK > 0) asm volatile("" : "+v"(af[s]));
+    }
     if constexpr (ABL == 2 || ABL == 4) {
 #pragma unroll
       for (int s = 0; s < SETS; ++s) asm volatile("" ::"v"(acc[s]), "v"(s4));
+      return;
+    }
+    if constexpr (HK > 0) {
+      // split image: the exact per-row test (the integer pre-test has no fp16 part)
+      const int rl = row0 + 4 * (lane >> 4), lq = lane & 15;
+#pragma unroll
+      for (int s = 0; s < SETS; ++s) {
+        float v[4];
+        bool any = false;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = rl + r < row_end ? fmaf((float)acc[s][r], s4[r], af[s][r] * rsq[s]) : -INFINITY;
+          any |= v[r] >= thr[s];
+        }
+        if (!__builtin_amdgcn_ballot_w64(any)) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool p = v[r] >= thr[s];
+          const uint64_t m = __builtin_amdgcn_ballot_w64(p);
+          if (m) {
+            if (nst > STW - 64) flush();
+            const int idx = nst + (int)__builtin_amdgcn_mbcnt_hi(
+                                      (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+            if (p) {
+              st_s[idx] = v[r];
+              st_r[idx] = rl + r;
+              st_q[idx] = (uint16_t)(s * 16 + lq);
+            }
+            nst += __builtin_popcountll(m);
+          }
+        }
+      }
       return;
     }
     // hot path, a conservative integer pre-test per set: max_r(acc_r * sx_r) <= max_r acc_r *
@@ -361,10 +447,13 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
   // cross-chain prefetch and measured slower, 10.55 -> 11.15 ms at 12.5M x 2048)
   // (D = 768: single-sub-tile chains -- the fused pair's extra fragment and accumulator
   // registers do not fit beside 192 query registers)
-  constexpr bool FUSE = D == 384 && NSW % 2 == 0 && (RSPLIT == 2 || TRK == 128);
+  // (the split image always runs fused chains)
+  constexpr bool FUSE = D == 384 && NSW % 2 == 0 && (RSPLIT == 2 || TRK == 128 || HK > 0);
+  static_assert(HK == 0 || FUSE, "split image: fused chains only");
   constexpr int NG = FUSE ? NSW / 2 : 1;   // fused chains per wave per tile
   i32x4 a2[FUSE ? R2 : 1][2];
   i32x4 acc2[FUSE ? 2 : 1][SETS];
+  f32x4 accf2[HK ? 2 : 1][SETS];
   f32x4 s4_prev = {0.f, 0.f, 0.f, 0.f};
   // partner waves (w, w + 4) of an 8-wave workgroup stay half a test apart
   const bool late = WV == 8 && wave_u >= WAVES / 2;
@@ -375,8 +464,10 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
     if constexpr (ABL != 1) {
       if (wave_u < G::SCW)
         wait_vmcnt<(LOADS + W0X) * (NS - 2)>();
-      else
+      else if (G::FULLW == WV || wave_u < G::FULLW)
         wait_vmcnt<LOADS * (NS - 2)>();
+      else   // (split image: the waves carrying one piece fewer per tile)
+        wait_vmcnt<(LOADS - 1) * (NS - 2)>();
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -405,36 +496,36 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
           asm volatile("ds_read_b128 %0, %1" : "=v"(sa) : "v"(sp));
           asm volatile("ds_read_b128 %0, %1 offset:64" : "=v"(sb) : "v"(sp));
         }
-        i8_prologue2<D, 0>(a2, fg);
+        i8_prologue2<D, 0, HK>(a2, fg);
         // a late wave tests the previous tile's last two sub-tiles here, under its partner's
         // MFMAs
         if (g == 0 && late && t > 0) {
-          emit(acc2[0], row0 - TR + last - SUB, s4_prev);
-          emit(acc2[1], row0 - TR + last, s4_last);
+          emit(acc2[0], accf2[0], row0 - TR + last - SUB, s4_prev);
+          emit(acc2[1], accf2[HK ? 1 : 0], row0 - TR + last, s4_last);
         }
         if (g == 0)
-          I8Chain2<D, 0, LOADS, G::DMA_EVERY>::run(acc2, a2, qf, fg, dma, sa, sb);
+          I8Chain2<D, 0, LOADS, G::DMA_EVERY, HK>::run(acc2, accf2, a2, qf, fg, dma, sa, sb);
         else
-          I8Chain2<D, 0, 0, G::DMA_EVERY>::run(acc2, a2, qf, fg, NoDma(), sa, sb);
+          I8Chain2<D, 0, 0, G::DMA_EVERY, HK>::run(acc2, accf2, a2, qf, fg, NoDma(), sa, sb);
         if (g + 1 < NG || !late) {
-          emit(acc2[0], row0 + jg * SUB, sa);
-          emit(acc2[1], row0 + (jg + 1) * SUB, sb);
+          emit(acc2[0], accf2[0], row0 + jg * SUB, sa);
+          emit(acc2[1], accf2[HK ? 1 : 0], row0 + (jg + 1) * SUB, sb);
         } else {
           s4_prev = sa;
           s4_last = sb;
         }
       }
       continue;
-    }
+    } else {
     i8_prologue<D, 0>(a, fw);
-    if (late && t > 0) emit(acc, row0 - TR + last, s4_last);
+    if (late && t > 0) emit(acc, acc, row0 - TR + last, s4_last);
     if constexpr (NSW > 1)
       I8Chain<D, 0, LOADS, true, G::DMA_EVERY>::run(acc, a, qf, fw, fw + NKS * PIECE, dma);
     else
       I8Chain<D, 0, LOADS, false, G::DMA_EVERY>::run(acc, a, qf, fw, 0, dma);
 #pragma unroll
     for (int j = 1; j < NSW; ++j) {
-      emit(acc, row0 + (j0 + j - 1) * SUB, scales(slot, j0 + j - 1));
+      emit(acc, acc, row0 + (j0 + j - 1) * SUB, scales(slot, j0 + j - 1));
       if (j + 1 < NSW)
         I8Chain<D, 0, 0, true, G::DMA_EVERY>::run(acc, a, qf, fw + j * NKS * PIECE,
                                                  fw + (j + 1) * NKS * PIECE, NoDma());
@@ -442,16 +533,17 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
         I8Chain<D, 0, 0, false, G::DMA_EVERY>::run(acc, a, qf, fw + j * NKS * PIECE, 0, NoDma());
     }
     if (!late)
-      emit(acc, row0 + last, scales(slot, j0 + NSW - 1));
+      emit(acc, acc, row0 + last, scales(slot, j0 + NSW - 1));
     else
       s4_last = scales(slot, j0 + NSW - 1);
+    }
   }
   if (late && n_tiles > 0) {
     if constexpr (FUSE) {
-      emit(acc2[0], row_begin + (n_tiles - 1) * TR + (j0 + NSW - 2) * SUB, s4_prev);
-      emit(acc2[1], row_begin + (n_tiles - 1) * TR + (j0 + NSW - 1) * SUB, s4_last);
+      emit(acc2[0], accf2[0], row_begin + (n_tiles - 1) * TR + (j0 + NSW - 2) * SUB, s4_prev);
+      emit(acc2[1], accf2[HK ? 1 : 0], row_begin + (n_tiles - 1) * TR + (j0 + NSW - 1) * SUB, s4_last);
     } else {
-      emit(acc, row_begin + (n_tiles - 1) * TR + (j0 + NSW - 1) * SUB, s4_last);
+      emit(acc, acc, row_begin + (n_tiles - 1) * TR + (j0 + NSW - 1) * SUB, s4_last);
     }
   }
   if (nst) flush();
@@ -716,6 +808,87 @@ __global__ __launch_bounds__(256) void prune_qquant_kernel(const __bf16* __restr
   }
 }
 
+// Split image of rotated rows (index_scan_i8_kernel HK = 2): X = [n, D] fp32 rows already in the
+// shard's PCA basis (index/shard.py calibrate_prune).  Dims 0 .. H-1 -> fp16 (image bytes 0 .. 2H),
+// dims H .. D-1 -> int8 with sx = max |x_l| / 127 (bytes 2H .. 2H + D - H).  One wave per row: lane
+// l holds leading dim l and trailing dims H + L l .. + L - 1.
+//   rows    (margin == nullptr): bounds[0..3] raised to (max |x_l - x~_l|, max |x~_l|,
+//            max |x_h - x^_h|, max |x^_h|) -- E_l, X_l, E_h, X_h;
+//   queries (margin != nullptr): sq = sx and the bound of |q . x - est| (est = q~_l . x~_l +
+//            q^_h . x^_h, the scan's acc_i * sq * sx + acc_f):
+//            margin = |q_l| E_l + |q_l - q~_l| X_l + |q_h| E_h + |q_h - q^_h| X_h + 1e-5.
+template <int D, int H>
+__global__ __launch_bounds__(256) void quant_rows_split_kernel(const float* __restrict__ X, int n,
+                                                               int8_t* __restrict__ X8,
+                                                               float* __restrict__ sx,
+                                                               float* __restrict__ bounds,
+                                                               float* __restrict__ margin) {
+  static_assert(H == 64 && (D - H) % 64 == 0, "64 leading dims, whole int8 k-steps");
+  constexpr int L = (D - H) / 64;
+  constexpr int RB = 2 * H + (D - H);
+  __shared__ float red[4][4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int row = blockIdx.x * 4 + w;
+  const bool rows = margin == nullptr;
+  if (row >= n) {   // (block-uniform barrier below: idle waves report zeros)
+    if (rows && bounds) {
+      if (lane < 4) red[lane][w] = 0.f;
+      __syncthreads();
+    }
+    return;
+  }
+  const float* xp = X + (size_t)row * D;
+  const float xh = xp[lane];
+  float xl[L];
+#pragma unroll
+  for (int i = 0; i < L; ++i) xl[i] = xp[H + L * lane + i];
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < L; ++i) amax = fmaxf(amax, fabsf(xl[i]));
+  amax = wave_max(amax);
+  const float s = amax > 0.f ? amax / 127.f : 1.f;
+  const float inv = 1.f / s;
+  float el2 = 0.f, nl2 = 0.f, ql2 = 0.f;
+  int8_t* op = X8 + (size_t)row * RB;
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    const int qv = max(-127, min(127, (int)rintf(xl[i] * inv)));
+    const float xt = (float)qv * s;
+    el2 += (xl[i] - xt) * (xl[i] - xt);
+    nl2 += xt * xt;
+    ql2 += xl[i] * xl[i];
+    op[2 * H + L * lane + i] = (int8_t)qv;
+  }
+  const _Float16 hh = (_Float16)xh;
+  const float xhh = (float)hh;
+  reinterpret_cast<uint16_t*>(op)[lane] = __builtin_bit_cast(uint16_t, hh);
+  const float el = sqrtf(wave_sum(el2)), nl = sqrtf(wave_sum(nl2)), ql = sqrtf(wave_sum(ql2));
+  const float eh = sqrtf(wave_sum((xh - xhh) * (xh - xhh)));
+  const float nh = sqrtf(wave_sum(xhh * xhh)), qh = sqrtf(wave_sum(xh * xh));
+  if (!rows) {
+    if (lane == 0) {
+      sx[row] = s;
+      margin[row] = ql * bounds[0] + el * bounds[1] + qh * bounds[2] + eh * bounds[3] + 1e-5f;
+    }
+    return;
+  }
+  if (lane == 0) {
+    sx[row] = s;
+    red[0][w] = el;
+    red[1][w] = nl;
+    red[2][w] = eh;
+    red[3][w] = nh;
+  }
+  if (bounds) {
+    __syncthreads();
+    if (threadIdx.x < 4) {
+      const float m = fmaxf(fmaxf(red[threadIdx.x][0], red[threadIdx.x][1]),
+                            fmaxf(red[threadIdx.x][2], red[threadIdx.x][3]));
+      atomicMax(reinterpret_cast<int*>(bounds) + threadIdx.x, __float_as_int(m));
+    }
+  }
+}
+
 constexpr int ROUTE_MAX_BLOCKS = 1024;   // int8 row blocks the per-block route can bin
 
 // The exact tail scan's candidates (rows >= thr0 of the fresh rows [off, n), ids relative to
@@ -883,33 +1056,38 @@ int symb_i8_queries_per_blk(int rsplit) {
   return g_i8_waves == 4 ? 4 * 16 * i8s::SETS : i8s::WAVES / rsplit * 16 * i8s::SETS;
 }
 
-template <int D, int RSPLIT, int TRK, int WV = 8>
+template <int D, int RSPLIT, int TRK, int WV = 8, int HK = 0>
 static int launch_i8(const void* X8, const float* sx, int n_valid, int rows_per_blk, int n_rblk,
                      const void* Q8, int NQ, const float* thr, float* cand_s, int* cand_i,
-                     int* cand_n, int cap, int xcd, hipStream_t st, const int* skip) {
+                     int* cand_n, int cap, int xcd, hipStream_t st, const int* skip,
+                     const float* sq = nullptr) {
   constexpr int qpb = WV / RSPLIT * 16 * i8s::SETS;
   const int n_qblk = (NQ + qpb - 1) / qpb;
-  constexpr int lds = Geo<D, TRK, WV>::LDS_BYTES;
-  set_max_lds<index_scan_i8_kernel<D, RSPLIT, 0, TRK, WV>>(lds);
-  hipLaunchKernelGGL((index_scan_i8_kernel<D, RSPLIT, 0, TRK, WV>), dim3(n_rblk * n_qblk),
+  constexpr int lds = Geo<D, TRK, WV, HK>::LDS_BYTES;
+  set_max_lds<index_scan_i8_kernel<D, RSPLIT, 0, TRK, WV, HK>>(lds);
+  hipLaunchKernelGGL((index_scan_i8_kernel<D, RSPLIT, 0, TRK, WV, HK>), dim3(n_rblk * n_qblk),
                      dim3(64 * WV), lds, st, (const int8_t*)X8, sx, n_valid, rows_per_blk,
-                     (const int8_t*)Q8, NQ, n_qblk, xcd, thr, cand_s, cand_i, cand_n, cap, skip);
+                     (const int8_t*)Q8, NQ, n_qblk, xcd, thr, cand_s, cand_i, cand_n, cap, skip, sq);
   return (int)hipGetLastError();
 }
 
-// Tile rows the D-wide scan runs with (the 128-row and 4-wave forms are D = 384 knobs).
-int symb_i8_tile_rows_for(int dim) { return dim == 384 ? g_i8_tr : 64; }
+// Tile rows the D-wide scan runs with (the 128-row and 4-wave forms are D = 384 knobs; the split
+// image runs 64-row tiles, 8 waves).
+int symb_i8_tile_rows_for(int dim, int heavy) { return dim == 384 && !heavy ? g_i8_tr : 64; }
+int symb_i8_split_queries_per_blk(int rsplit) { return i8s::WAVES / rsplit * 16 * i8s::SETS; }
 
 // rows_per_blk % tile rows == 0, n_rblk * rows_per_blk >= n_valid; X8 / sx hold alloc_rows
 // rows, which must cover n_valid rounded up to a whole tile (the DMA reads whole tiles).
-// rsplit 2 = 256 queries per workgroup, 1 = 512.  dim: 384 or 768.
+// rsplit 2 = 256 queries per workgroup, 1 = 512.  dim: 384 or 768.  heavy = 64: the split image
+// (448-byte rows and queries, quant_rows_split), sq = the queries' int8 scales; 0: plain int8.
 int symb_index_scan_i8(const void* X8, const float* sx, int n_valid, int alloc_rows,
                        int rows_per_blk, int n_rblk, const void* Q8, int NQ, const float* thr,
                        float* cand_s, int* cand_i, int* cand_n, int cap, int xcd, hipStream_t st,
-                       int rsplit, const int* skip, int dim) {
+                       int rsplit, const int* skip, int dim, int heavy, const float* sq) {
   if (NQ <= 0) return 0;
   if (dim != 384 && dim != 768) return -1;
-  const int tr = symb_i8_tile_rows_for(dim);
+  if (heavy != 0 && (heavy != 64 || dim != 384 || sq == nullptr)) return -1;
+  const int tr = symb_i8_tile_rows_for(dim, heavy);
   if (rows_per_blk % tr || n_rblk <= 0 || thr == nullptr || cap <= 0 || n_valid <= 0) return -1;
   if ((long long)n_rblk * rows_per_blk < n_valid) return -1;
   if ((long long)(n_valid + tr - 1) / tr * tr > alloc_rows) return -1;   // a tile past the buffer
@@ -917,6 +1095,13 @@ int symb_index_scan_i8(const void* X8, const float* sx, int n_valid, int alloc_r
   if (e != hipSuccess) return (int)e;
 #define SYMB_I8(D_, RS, T) launch_i8<D_, RS, T>(X8, sx, n_valid, rows_per_blk, n_rblk, Q8, NQ, thr, \
                                                 cand_s, cand_i, cand_n, cap, xcd, st, skip)
+  if (heavy)
+    return rsplit == 2 ? launch_i8<384, 2, 64, 8, 2>(X8, sx, n_valid, rows_per_blk, n_rblk, Q8, NQ,
+                                                     thr, cand_s, cand_i, cand_n, cap, xcd, st,
+                                                     skip, sq)
+                       : launch_i8<384, 1, 64, 8, 2>(X8, sx, n_valid, rows_per_blk, n_rblk, Q8, NQ,
+                                                     thr, cand_s, cand_i, cand_n, cap, xcd, st,
+                                                     skip, sq);
   if (dim == 768) return rsplit == 2 ? SYMB_I8(768, 2, 64) : SYMB_I8(768, 1, 64);
   if (g_i8_waves == 4)
     return launch_i8<384, 1, 64, 4>(X8, sx, n_valid, rows_per_blk, n_rblk, Q8, NQ, thr, cand_s,
@@ -952,7 +1137,7 @@ int symb_index_scan_i8_ablate(const void* X8, const float* sx, int n_valid, int 
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipLaunchKernelGGL(kern, dim3(n_rblk * n_qblk), dim3(w4 ? 256 : 512), lds, st, (const int8_t*)X8, sx,
                        n_valid, rows_per_blk, (const int8_t*)Q8, NQ, n_qblk, xcd, thr, cand_s,
-                       cand_i, cand_n, cap, (const int*)nullptr);
+                       cand_i, cand_n, cap, (const int*)nullptr, (const float*)nullptr);
     return (int)hipGetLastError();
   };
   if (w4) {
@@ -1011,6 +1196,18 @@ int symb_quant_rows_i8(const void* X, int n, int dim, void* X8, float* sx, float
                                  (const __bf16*)X, n, (int8_t*)X8, sx, err, xtn, bounds)
   SYMB_BY_DIM(dim, L);
 #undef L
+  return (int)hipGetLastError();
+}
+
+// The split image of D-wide fp32 rows already rotated into the shard's basis
+// (quant_rows_split_kernel): rows (margin == nullptr, bounds raised) or queries (margin and sq =
+// sx written, bounds read).  X8: [n, D + 64] bytes.
+int symb_quant_rows_split(const float* X, int n, int dim, void* X8, float* sx, float* bounds,
+                          float* margin, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (dim != 384 || bounds == nullptr) return -1;
+  hipLaunchKernelGGL((quant_rows_split_kernel<384, 64>), dim3((n + 3) / 4), dim3(256), 0, st, X, n,
+                     (int8_t*)X8, sx, bounds, margin);
   return (int)hipGetLastError();
 }
 

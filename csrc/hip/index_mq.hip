@@ -292,6 +292,10 @@ __global__ __launch_bounds__(512, 1) void index_scan_mq_kernel(
   // one 16-row sub-tile at virtual row row0 / physical row prow0: lane holds rows
   // 4*(lane>>4) + r of it for the 16 queries of each set (column lane & 15)
   auto emit = [&](f32x4 (&acc)[SETS], int row0, int prow0) {
+    // keep every read of the inline-asm MFMA results below the chain-end s_nops (the compiler's
+    // hazard recognizer does not see asm MFMAs; index_i8.hip emit has the story)
+#pragma unroll
+    for (int s = 0; s < SETS; ++s) asm volatile("" : "+v"(acc[s]));
     if constexpr (ABL == 2 || ABL == 4) {
 #pragma unroll
       for (int s = 0; s < SETS; ++s) asm volatile("" ::"v"(acc[s]));

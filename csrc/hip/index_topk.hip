@@ -464,9 +464,12 @@ __global__ __launch_bounds__(256, 1) void index_scan_wide_kernel(
     frag_prologue<0, PF, M, R>(a, voff, base0);
     FragChain2<0, NKS, PF, M, 2, LOADS>::run(acc0, acc1, a, q0, q1, voff, base0, dma);
     frag_prologue<0, PF, M, R>(a, voff, base1);
+    // (reads of the asm MFMA results stay below the chain-end s_nops: index_i8.hip emit)
+    asm volatile("" : "+v"(acc0), "+v"(acc1));
     update(acc0, tv0, ti0, thr0, row0);
     update(acc1, tv1, ti1, thr1, row0);
     FragChain2<0, NKS, PF, M, 0, 0>::run(acc0, acc1, a, q0, q1, voff, base1, NoDma());
+    asm volatile("" : "+v"(acc0), "+v"(acc1));
     update(acc0, tv0, ti0, thr0, row0 + SUB);
     update(acc1, tv1, ti1, thr1, row0 + SUB);
   }

@@ -486,3 +486,51 @@ def test_int8_pruning_bound_holds_and_image_follows_writes():
     assert resolve_prune("auto", "bf16", 384, device="cpu") is None
     assert resolve_prune("auto", "fp8", 1024) is None and resolve_prune("none") is None
     assert resolve_prune("auto", "bf16", 384, prefilter="fp8") is None
+
+
+def test_split_image_bound_holds_and_prunes_anisotropic_rows():
+    """calibrate_prune: on the anisotropic corpus (a shared mean direction, power-law spread) the
+    shard switches to the split image -- rows and queries rotated into the principal basis, 64
+    leading components fp16, the rest int8 -- whose bound must hold for every (query, row) pair
+    and must leave far fewer candidates above the true k-th score than the plain int8 bound; on
+    isotropic rows the plain image stays.  Overwrites and appends after the calibration are imaged
+    in the same basis."""
+    from codename_symbiont_amd.index.synth import CorpusGen
+
+    n, k = 20000, 10
+    g = CorpusGen("anisotropic", 384, "cpu")
+    sh = HbmIndexShard(384, n + 100, device="cpu", prune="i8")
+    sh.append_f32(g.rows(n, seed=1))
+    assert sh._i8_heavy == 0                       # below CALIB_MIN_ROWS: not calibrated yet
+    q = g.unit(48, seed=99).bfloat16()
+    xb = sh.rows[:n].float()
+    s = q.float() @ xb.t()
+    T = s.topk(k, dim=1).values[:, -1:]
+    q8, sq, m_plain = sh.prune_query_image(q)
+    est = sh.prune_estimate(q8, sq)
+    assert ((s - est).abs() <= m_plain[:, None]).all()
+    c_plain = (est + m_plain[:, None] >= T).sum(1).float()
+
+    sh.calibrate_prune()
+    assert sh._i8_heavy == 64 and sh.calib_share > 0.6 and sh.rows_i8.shape[1] == 448
+    rot = sh._i8_rot
+    assert torch.allclose(rot @ rot.t(), torch.eye(384, dtype=torch.float64), atol=1e-10)
+    sh.write_f32(7, g.rows(1, seed=3))              # an overwrite, imaged in the new basis
+    sh.append_f32(g.rows(50, seed=4))
+    xb = sh.rows[:sh.count].float()
+    s = q.float() @ xb.t()
+    q8, sq, m = sh.prune_query_image(q)
+    assert q8.shape == (48, 448)
+    est = sh.prune_estimate(q8, sq)
+    assert ((s - est).abs() <= m[:, None]).all(), float(((s - est).abs() - m[:, None]).max())
+    T = s.topk(k, dim=1).values[:, -1:]
+    c_split = (est + m[:, None] >= T).sum(1).float()
+    assert (c_split >= k).all()                    # (the true top-k always survive)
+    assert float(c_split.mean()) * 8 < float(c_plain.mean()), (c_split.mean(), c_plain.mean())
+    assert float(m.mean()) * 3 < float(m_plain.mean())
+
+    # isotropic rows keep the plain image (the split one would only cost bytes there)
+    r = HbmIndexShard(384, 5000, device="cpu", prune="i8")
+    r.append_f32(torch.randn(5000, 384, generator=torch.Generator().manual_seed(2)))
+    r.calibrate_prune()
+    assert r._i8_heavy == 0 and r.calib_share < 0.3 and r.rows_i8.shape[1] == 384

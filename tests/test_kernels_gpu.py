@@ -809,6 +809,119 @@ def test_index_pruned_search_768_is_exact(nq, data):
     _close(s1, true, atol=2e-3, what="pruned768 returned rows")
 
 
+def test_quant_rows_split_matches_reference():
+    """index_i8.hip quant_rows_split (the split image: 64 fp16 + 320 int8 per rotated row) == the
+    torch reference, rows raising (E_l, X_l, E_h, X_h) and queries getting sq and the margin."""
+    from codename_symbiont_amd.ops._ext import hip, stream_handle
+
+    n = 5003
+    x = torch.nn.functional.normalize(_f(n, 384, seed=81) * torch.linspace(3, 0.1, 384,
+                                                                            device=DEV), dim=-1)
+    img = torch.empty(n, 448, dtype=torch.int8, device=DEV)
+    sx = torch.empty(n, device=DEV)
+    b = torch.zeros(4, device=DEV)
+    st = stream_handle(torch.device(DEV))
+    hip().quant_rows_split(x.data_ptr(), n, 384, img.data_ptr(), sx.data_ptr(), b.data_ptr(), 0, st)
+    rimg, rsx, nr = R.quant_rows_split_ref(x)
+    torch.cuda.synchronize()
+    _close(sx, rsx, atol=0, rtol=1e-6, what="split scales")
+    assert torch.equal(img[:, :128], rimg[:, :128])               # fp16 part: bit-exact
+    assert (img[:, 128:].int() - rimg[:, 128:].int()).abs().max() <= 1   # (x * 1/s rounding ties)
+    m = nr.amax(0)
+    _close(b, torch.stack([m[0], m[1], m[3], m[4]]), atol=1e-6, rtol=1e-4, what="split bounds")
+    q = torch.nn.functional.normalize(_f(300, 384, seed=82), dim=-1)
+    qi = torch.empty(300, 448, dtype=torch.int8, device=DEV)
+    sq = torch.empty(300, device=DEV)
+    mg = torch.empty(300, device=DEV)
+    hip().quant_rows_split(q.data_ptr(), 300, 384, qi.data_ptr(), sq.data_ptr(), b.data_ptr(),
+                           mg.data_ptr(), st)
+    _, rsq, qn = R.quant_rows_split_ref(q)
+    want = qn[:, 2] * b[0] + qn[:, 0] * b[1] + qn[:, 5] * b[2] + qn[:, 3] * b[3] + 1e-5
+    torch.cuda.synchronize()
+    _close(sq, rsq, atol=0, rtol=1e-6, what="split query scales")
+    _close(mg, want, atol=1e-6, rtol=1e-4, what="split query margins")
+
+
+def _aniso_shard(n, seed=1):
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+    from codename_symbiont_amd.index.synth import CorpusGen, fill_corpus
+
+    gen = CorpusGen("anisotropic", 384, DEV)
+    shard = HbmIndexShard(384, n + 4096, prune="i8")
+    fill_corpus(shard, gen, n, seed=seed)
+    return shard, gen
+
+
+def test_index_scan_i8_split_emits_the_bound_set():
+    """index_scan_i8_kernel HK = 2 (fp16 MFMA k-steps + int8 k-steps, 28-piece tiles over 8
+    waves): every row whose split estimate reaches the threshold is emitted, and no other, for
+    both row-split forms -- against the torch estimate (rows within fp32 noise of the threshold
+    excepted)."""
+    from codename_symbiont_amd.ops._ext import hip, stream_handle
+
+    n = 300_000 + 77
+    shard, gen = _aniso_shard(n)
+    assert shard._i8_heavy == 64, shard.calib_share
+    h, st = hip(), stream_handle(shard.device)
+    for nq in (256, 600):
+        q = gen.unit(nq, seed=5).bfloat16()
+        q8, sq, margin = shard.prune_query_image(q)
+        est = shard.prune_estimate(q8, sq, 0, n)
+        # a threshold near the 40th best estimate: a few dozen rows per query
+        t = est.topk(40, dim=1).values[:, -1]
+        thr = (t / sq).contiguous()
+        rsplit, rows_per_blk, n_rblk = shard._i8_geometry(n, nq, shard._n_cus())
+        cap = 4096
+        cs = torch.empty(nq, cap, device=DEV)
+        ci = torch.empty(nq, cap, dtype=torch.int32, device=DEV)
+        cnt = torch.empty(nq, dtype=torch.int32, device=DEV)
+        h.index_scan_i8(shard.rows_i8.data_ptr(), shard.sx_i8.data_ptr(), n, shard.rows_i8.shape[0],
+                        rows_per_blk, n_rblk, q8.data_ptr(), nq, thr.data_ptr(), cs.data_ptr(),
+                        ci.data_ptr(), cnt.data_ptr(), cap, 1, st, rsplit, heavy=64,
+                        sq=sq.data_ptr())
+        torch.cuda.synchronize()
+        want = est >= t[:, None]
+        near = (est - t[:, None]).abs() <= 1e-5 * est.abs().clamp_min(1.0)
+        assert int(cnt.max()) <= cap
+        got = torch.zeros_like(want)
+        for i in range(nq):
+            got[i, ci[i, :int(cnt[i])].long()] = True
+        bad = (got != want) & ~near
+        assert not bad.any(), f"nq={nq}: {int(bad.sum())} rows differ"
+        assert (cnt >= 40 - near.sum(1)).all()
+
+
+def test_index_pruned_search_split_is_exact():
+    """The pruned search on the anisotropic corpus through the split image: the exact bf16
+    results (scores and rows), no batch routed whole to the bf16 scan, no overflow, and far
+    fewer candidates than the plain int8 form emits."""
+    n, k = (1 << 21) + 333, 10
+    shard, gen = _aniso_shard(n, seed=3)
+    assert shard._i8_heavy == 64
+    shard.mq_stats = True
+    q = gen.unit(256, seed=17).bfloat16()
+    s1, r1 = shard.search(q, k)
+    cnt, ovf = shard._mq_last
+    dense = shard._route_last
+    sc = q.float() @ shard.unit_rows().float().t()
+    ts, ti = torch.topk(sc, k, dim=1)
+    torch.cuda.synchronize()
+    assert int(ovf.item()) == 0 and int(dense.item()) == 0
+    _close(s1, ts, atol=2e-5, what="split pruned vs exact scores")
+    _close(sc.gather(1, r1.long()), ts, atol=2e-5, what="split pruned returned rows")
+    split_max = int(cnt.max())
+    # the plain int8 image of the same rows (same sample, same thresholds) emits far more
+    shard.i8_split = "off"
+    shard.calibrate_prune()
+    assert shard._i8_heavy == 0
+    shard.prune_route = False
+    s2, r2 = shard.search(q, k)
+    cnt2, _ = shard._mq_last
+    torch.cuda.synchronize()
+    _close(s2, ts, atol=2e-5, what="plain pruned vs exact scores")
+    assert split_max * 5 < int(cnt2.max()), (split_max, int(cnt2.max()))
+
+
 def test_prune_qquant_and_route_match_torch():
     """index_i8.hip prune_qquant (int8 query image + per-query bound margin) and prune_route (T,
     emission threshold, route estimate from the sample's candidates) == torch compositions."""
@@ -924,6 +1037,9 @@ def test_index_pruned_search_routes_dense_data_exactly(route):
     gen = CorpusGen("anisotropic", 384, DEV)
     ref = HbmIndexShard(384, n)
     shard = HbmIndexShard(384, n, prune="i8")
+    # the PLAIN int8 image (the split one, calibrate_prune, prunes this corpus without a flood:
+    # test_index_pruned_search_split_is_exact)
+    shard.i8_split = "off"
     for sh in (ref, shard):
         fill_corpus(sh, gen, n, seed=3)
     shard.prune_route = route
