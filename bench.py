@@ -475,7 +475,7 @@ def run_gpu(args, info, comm) -> int:
     if args.prepass_min_tiles:
         shard.prepass_min_tiles = args.prepass_min_tiles
     if args.prune_sample_shift:
-        shard.PRUNE_TILE_SHIFT = args.prune_sample_shift
+        shard.PRUNE_TILE_SHIFT = shard.PRUNE_TILE_SHIFT_SPLIT = args.prune_sample_shift
     if args.prune_block_frac:
         shard.PRUNE_BLOCK_FRAC = args.prune_block_frac
     torch.cuda.synchronize(dev)
@@ -806,7 +806,8 @@ def run_gpu(args, info, comm) -> int:
         "search_priority": args.search_priority,
         "scan_min_tiles": args.scan_min_tiles,
         "prepass_min_tiles": shard.prepass_min_tiles,
-        "prune_sample_shift": shard.PRUNE_TILE_SHIFT if prune else None,
+        "prune_sample_shift": ((shard.PRUNE_TILE_SHIFT_SPLIT if shard._i8_heavy
+                                else shard.PRUNE_TILE_SHIFT) if prune else None),
         "prune_block_frac": shard.PRUNE_BLOCK_FRAC if prune else None,
     })
     if info.rank == 0:

@@ -86,7 +86,7 @@ def main():
                                   "variant": v, "us_med": round(med, 1), "us_min": round(min(ts), 1),
                                   "TFLOPs": round(2 * a.m * n * k / med / 1e6)}), flush=True)
     hip().gemm_config(128, 3, 8)
-    hip().gemm_lt_config(0)
+    hip().gemm_lt_config(1)
 
 
 if __name__ == "__main__":

@@ -451,8 +451,8 @@ def cmd_encoder(a):
                 name = p + ("" if len(tiles) == 1 else f"_tile{t}") + ("" if len(fw) == 1 else f"_w{w}")
                 # w = 256 / 257: 8-wave fp8 tiles plus the 256x256 fp8 tile wherever the bf16
                 # rule takes it / where the fp8 auto rule does (the default); else no 256x256
-                # t = 12: the round-3 default (tile rule 10 + hipBLASLt for the plain K, N >= 768
-                # projections); other t: symb_gemm_config tile modes (3 = auto, the default)
+                # t = 12: tile rule 10 + hipBLASLt for the plain K, N >= 768 projections (the
+                # default route); other t: symb_gemm_config tile modes, every projection ours
                 var[name] = (lambda e=e, t=t, w=w: (_hip().gemm_config(128, 10 if t == 12 else t, 8),
                                                     _hip().gemm_lt_config(1 if t == 12 else 0),
                                                     _hip().gemm_fp8_config(8 if w >= 256 else w,
@@ -460,7 +460,7 @@ def cmd_encoder(a):
                                                     e.forward_packed(b, o1, o2)))
     res = ab(var, rounds=a.rounds, iters=a.iters)
     _hip().gemm_config(128, 3, 8)
-    _hip().gemm_lt_config(0)
+    _hip().gemm_lt_config(1)
     _hip().gemm_fp8_config(8)
     toks = a.batch * a.seq
     fl = cfg.flops_per_token(a.seq) * toks

@@ -812,6 +812,9 @@ class HbmIndexShard:
     # PRUNE_MIN_SHIFT.
     PRUNE_TILE_SHIFT = 5
     PRUNE_MIN_SHIFT = 5
+    # the split image's band is ~10x narrower (calibrate_prune): half the sample, a lower T, and
+    # still far from PRUNE_CAP (max 2.3k candidates per query at 2^5 on the anisotropic corpus)
+    PRUNE_TILE_SHIFT_SPLIT = 6
     # candidate slots per query: ~1-2k expected at 100M x 384 on random data, but the busiest of
     # 256 held-out queries emitted 6k (profiles/r3_real/); slots cost memory only (the re-score
     # and select walk the emitted count), 256 MiB at 1024 queries
@@ -858,8 +861,9 @@ class HbmIndexShard:
         from ..ops._ext import hip, stream_handle
 
         n, NQ, kmax = self.visible, q_unit.shape[0], 16
-        plan, ts = None, self.PRUNE_TILE_SHIFT
-        while plan is None and ts >= min(self.PRUNE_MIN_SHIFT, self.PRUNE_TILE_SHIFT):
+        shift = self.PRUNE_TILE_SHIFT_SPLIT if self._i8_heavy else self.PRUNE_TILE_SHIFT
+        plan, ts = None, shift
+        while plan is None and ts >= min(self.PRUNE_MIN_SHIFT, shift):
             plan, ts = self._tile_sample_plan(n, ts), ts - 1
         if plan is None:
             return None

@@ -486,12 +486,16 @@ int symb_gemm_fp8_config(int waves, int big) {
   return 0;
 }
 
-// hipBLASLt for the plain bias / bias + residual projections (gemm_lt.cpp), kept as the vendor
-// baseline for A/B runs: 0 = never (default: every projection on this repo's kernels), 1 = the
-// wide shapes (K >= 768, N >= 768, M >= 4096), 2 = every bias / residual GEMM.
+// hipBLASLt for the plain bias / bias + residual projections (gemm_lt.cpp): 0 = never (every
+// projection on this repo's kernels), 1 = the wide shapes (K >= 768, N >= 768, M >= 4096;
+// default), 2 = every bias / residual GEMM.  Round 4 measured this repo's best tiles (256 x 256 /
+// 256 x 192, and a deep-ring split-K kernel since removed) against it at M = 32768: the QKV
+// (N = 2304 / 3072) and FFN2 (K = 3072 / 4096) shapes stay 13-25 % faster in hipBLASLt, so the
+// bge / mpnet / e5 encoders run 6.73 / 6.74 / 19.95 ms with it against 7.52 / 7.55 / 22.50 ms
+// without (profiles/r4_gemm/README.md); the GELU / LayerNorm-fused and H = 384 GEMMs are ours.
 int symb_gemm_lt(int epi, const void* A, int lda, const void* W, int ldw, const float* bias,
                  const void* R, int ldr, void* C, int ldc, int M, int N, int K, hipStream_t st);
-static int g_gemm_lt = 0;
+static int g_gemm_lt = 1;
 int symb_gemm_lt_config(int mode) {
   if (mode < 0 || mode > 2) return -1;
   g_gemm_lt = mode;

@@ -345,18 +345,37 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
       return;
     }
     if constexpr (HK > 0) {
-      // split image: the exact per-row test (the integer pre-test has no fp16 part)
+      // split image, a conservative pre-test per set as for the plain image:
+      //   max_r (acc_f,r / sq + acc_i,r sx_r) <= max_r acc_f,r / sq + max_r acc_i,r * (max_r sx_r
+      //   for a non-negative integer max, min_r sx_r for a negative one)
+      // -- two v_max3_i32, two v_max3_f32, a convert and an FMA per set; only the sets whose
+      // bound reaches the threshold take the exact per-row test
+      const float smx = fmaxf(fmaxf(s4[0], s4[1]), fmaxf(s4[2], s4[3]));
+      const float smn = fminf(fminf(s4[0], s4[1]), fminf(s4[2], s4[3]));
+      bool hs[SETS];
+      bool hit = false;
+#pragma unroll
+      for (int s = 0; s < SETS; ++s) {
+        int im;
+        float fm;
+        asm volatile("v_max3_i32 %0, %1, %2, %3\n\tv_max3_i32 %0, %0, %4, %4"
+                     : "=&v"(im) : "v"(acc[s][0]), "v"(acc[s][1]), "v"(acc[s][2]), "v"(acc[s][3]));
+        asm volatile("v_max3_f32 %0, %1, %2, %3\n\tv_max3_f32 %0, %0, %4, %4"
+                     : "=&v"(fm) : "v"(af[s][0]), "v"(af[s][1]), "v"(af[s][2]), "v"(af[s][3]));
+        // (+ |ub| 1e-4 + 1e-6: covers the rounding of this bound's own products)
+        const float ub = fmaf((float)im, im >= 0 ? smx : smn, fm * rsq[s]);
+        hs[s] = ub + fabsf(ub) * 1e-4f + 1e-6f >= thr[s];
+        hit |= hs[s];
+      }
+      if (!__builtin_amdgcn_ballot_w64(hit)) return;
       const int rl = row0 + 4 * (lane >> 4), lq = lane & 15;
 #pragma unroll
       for (int s = 0; s < SETS; ++s) {
+        if (!__builtin_amdgcn_ballot_w64(hs[s])) continue;
         float v[4];
-        bool any = false;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
+        for (int r = 0; r < 4; ++r)
           v[r] = rl + r < row_end ? fmaf((float)acc[s][r], s4[r], af[s][r] * rsq[s]) : -INFINITY;
-          any |= v[r] >= thr[s];
-        }
-        if (!__builtin_amdgcn_ballot_w64(any)) continue;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const bool p = v[r] >= thr[s];

@@ -91,7 +91,8 @@ def test_gemm(M, N, K, epi, tile):
     hip().gemm_config(64 if tile == 16 else 128, 3 if tile == 16 else tile,
                       {0: 8, 2: 0, 3: 3, 10: 8, 16: 8}[tile])
     hip().gemm_resln_config(8 if tile == 16 else 16)
-    try:
+    hip().gemm_lt_config(0)   # this repo's tiles for every shape (the default sends the wide
+    try:                      # plain projections to hipBLASLt: test_gemm_hipblaslt_route)
         out = gemm(a := _bf(M, K, seed=1), w := _bf(N, K, scale=1.0 / math.sqrt(K), seed=2),
                    bias := _f(N, scale=0.5, seed=3), epi,
                    res := (_bf(M, N, seed=4) if epi in (2, 3) else None),
@@ -100,6 +101,7 @@ def test_gemm(M, N, K, epi, tile):
     finally:
         hip().gemm_config(128, 3, 8)
         hip().gemm_resln_config(16)
+        hip().gemm_lt_config(1)
     ref = R.gemm_ref(a, w, bias, epi, res, g, b, 1e-12)
     _close(out, ref, atol=4e-2, rtol=2e-2, what=f"gemm epi={epi}")
 
@@ -120,7 +122,7 @@ def test_gemm_hipblaslt_route(M, N, K, epi):
     try:
         out = gemm(a, w, bias, epi, res)
     finally:
-        hip().gemm_lt_config(0)
+        hip().gemm_lt_config(1)   # (the default route)
     ref = R.gemm_ref(a, w, bias, epi, res, None, None, 1e-12)
     _close(out, ref, atol=4e-2, rtol=2e-2, what=f"hipblaslt gemm epi={epi}")
 
@@ -142,7 +144,7 @@ def test_gemm_hipblaslt_plan_cache_is_bounded():
             assert hip().gemm_lt_plans() <= 64
         ref = R.gemm_ref(a, w, bias, 0, None, None, None, 1e-12)
     finally:
-        hip().gemm_lt_config(0)
+        hip().gemm_lt_config(1)   # (the default route)
     _close(out, ref, atol=4e-2, rtol=2e-2, what="hipblaslt gemm after evictions")
     assert hip().gemm_lt_plans() == 64
 
