@@ -436,7 +436,7 @@ def run_cpu(args, info, comm) -> int:
 
 
 def run_gpu(args, info, comm) -> int:
-    from codename_symbiont_amd.index.shard import HbmIndexShard, resolve_prune
+    from codename_symbiont_amd.index.shard import MQ_DIMS, HbmIndexShard, resolve_prune
     from codename_symbiont_amd.index.synth import CorpusGen, fill_corpus
     from codename_symbiont_amd.models import get_config
     from codename_symbiont_amd.models.encoder import HipEncoder, refill_synthetic, synthetic_batch
@@ -533,14 +533,23 @@ def run_gpu(args, info, comm) -> int:
         stride = max(1, rows_per_rank // (NB * B))
         qsets = [shard.rows[torch.arange(B, device=dev) * stride + i].clone() for i in range(NB)]
 
+    # host time per phase of the timed steps (reported as host_phase_ms_per_step): waits on the
+    # copy ring, synthetic token generation, and the enqueue of the encoder / search halves
+    hph = {"wait_copy_slot": 0.0, "synth_tokens": 0.0, "enc_enqueue": 0.0,
+           "search_begin_enqueue": 0.0, "search_end_enqueue": 0.0}
+
     def prefetch(i: int) -> None:
         """H2D of batch i on the copy stream.  Every step gets NEVER-SEEN token ids: host slot
         i % NB is refilled in place once its previous copy has finished (the host runs at most
         NB batches ahead of the copy stream)."""
         slot, hs = i % 2, i % NB
+        t0 = time.perf_counter()
         if i >= NB:
             host_free[hs].synchronize()
+        t1 = time.perf_counter()
         refill_synthetic(host[hs], cfg, seed=(info.rank << 32) + i)
+        hph["wait_copy_slot"] += t1 - t0
+        hph["synth_tokens"] += time.perf_counter() - t1
         with torch.cuda.stream(copy_stream):
             if i >= 2:
                 copy_stream.wait_event(consumed[slot])
@@ -627,14 +636,20 @@ def run_gpu(args, info, comm) -> int:
         slot = i % NO
         # with AHEAD = 2, batch i + 2's encoder is enqueued now: it runs once batch i's scan
         # releases the CUs, beside batch i + 1's pre-pass, instead of between them
+        t0 = time.perf_counter()
         encode_async(i + AHEAD, ev)
+        t1 = time.perf_counter()
         begin_search(i + 1)
+        t2 = time.perf_counter()
         compute.wait_event(pre_done[slot])
         if AHEAD == 2 and args.scan_waits_encoder:
             compute.wait_event(enc_done[(i + 1) % NO])
         if ev:
             ev[2].record(compute)
         searcher.end(handles.pop(i))
+        hph["enc_enqueue"] += t1 - t0      # (includes prefetch: its waits / tokens counted too)
+        hph["search_begin_enqueue"] += t2 - t1
+        hph["search_end_enqueue"] += time.perf_counter() - t2
         out_ring.consume(slot)
         q_free[slot].record(compute)
         if ev:
@@ -709,6 +724,8 @@ def run_gpu(args, info, comm) -> int:
     if shard._mq_tot is not None:   # count overflows of the timed steps only
         for t in shard._mq_tot:
             t.zero_()
+    for kph in hph:
+        hph[kph] = 0.0
     sampler = ClockSampler(dev.index) if (args.timeline and info.is_root) else None
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(K)]
     t_start = time.perf_counter()
@@ -730,6 +747,7 @@ def run_gpu(args, info, comm) -> int:
         "embed_ms_per_step_rank0": round(e_ms, 3),
         "search_ms_per_step_rank0": round(s_ms, 3),
         "host_enqueue_ms_per_step_rank0": round(host_ms, 3),
+        "host_phase_ms_per_step_rank0": {kph: round(v * 1000.0 / K, 3) for kph, v in hph.items()},
     }
     if sampler is not None:
         clocks = sampler.stop()
@@ -799,9 +817,10 @@ def run_gpu(args, info, comm) -> int:
         # seeded queries (512 per workgroup at >= 512), else the 256-query list kernel
         "index_scan": (("int8-pruned-" if prune else "emitting-")
                        + ("512q" if B * (vw or info.world) >= 512 else "256q"))
-                      if (shard.scan_mq and args.index_dtype == "bf16" and cfg.hidden == 384
+                      if (shard.scan_mq and args.index_dtype == "bf16" and cfg.hidden in MQ_DIMS
                           and B * (vw or info.world) >= shard.mq_min_nq and args.k <= 16)
-                      else "list-256q",
+                      else ("emitting-large-k" if (args.index_dtype == "bf16" and 16 < args.k <= 128
+                                                   and cfg.hidden in MQ_DIMS) else "list-256q"),
         "encoder_hipgraph": use_graph,
         "search_priority": args.search_priority,
         "scan_min_tiles": args.scan_min_tiles,

@@ -812,9 +812,9 @@ class HbmIndexShard:
     # PRUNE_MIN_SHIFT.
     PRUNE_TILE_SHIFT = 5
     PRUNE_MIN_SHIFT = 5
-    # the split image's band is ~10x narrower (calibrate_prune): half the sample, a lower T, and
-    # still far from PRUNE_CAP (max 2.3k candidates per query at 2^5 on the anisotropic corpus)
-    PRUNE_TILE_SHIFT_SPLIT = 6
+    # the split image's own sample density: 2^6 (half the sample, max 3.7k candidates per query)
+    # measured the same as 2^5 (13.07 vs 13.05 ms at 100M x 256 anisotropic, profiles/r4_split/)
+    PRUNE_TILE_SHIFT_SPLIT = 5
     # candidate slots per query: ~1-2k expected at 100M x 384 on random data, but the busiest of
     # 256 held-out queries emitted 6k (profiles/r3_real/); slots cost memory only (the re-score
     # and select walk the emitted count), 256 MiB at 1024 queries

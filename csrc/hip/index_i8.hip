@@ -325,82 +325,70 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
   auto scales = [&](int slot, int jj) {
     return *reinterpret_cast<const f32x4*>(scl + slot * SC_BYTES + (jj * SUB + 4 * (lane >> 4)) * 4);
   };
-  // one 16-row sub-tile at row0 with this lane's row scales s4 (af: the split image's fp16-part
-  // accumulators, unused without it)
-  auto emit = [&](i32x4 (&acc)[SETS], auto& af, int row0, const f32x4 s4) {
-    // the chains' MFMAs are inline asm, invisible to the compiler's MFMA -> VALU hazard
-    // recognizer: their results are only safe to read after the chain-end s_nops.  An empty
-    // volatile asm "rewriting" the accumulators keeps every read below it (volatile asm stays in
-    // program order); without it a plain C++ read was scheduled above the s_nops and saw a
-    // stale first accumulator register (the split image's 512-query form lost rows 0 mod 4 of
-    // sub-tile 0, set 0: benchmarks/diag/split_emit.py)
+  // ---- emission.  The chains' MFMAs are inline asm, invisible to the compiler's MFMA -> VALU
+  // hazard recognizer: their results are only safe to read after the chain-end s_nops.  An empty
+  // volatile asm "rewriting" the accumulators keeps every read below it (volatile asm stays in
+  // program order); without it a plain C++ read was scheduled above the s_nops and saw a stale
+  // first accumulator register (the split image's 512-query form lost rows 0 mod 4 of sub-tile 0,
+  // set 0: benchmarks/diag/split_emit.py).
+  auto fence_acc = [&](i32x4 (&acc)[SETS], auto& af) {
 #pragma unroll
     for (int s = 0; s < SETS; ++s) {
       asm volatile("" : "+v"(acc[s]));
       if constexpr (HK > 0) asm volatile("" : "+v"(af[s]));
     }
+  };
+  // the exact per-row test of one 16-row sub-tile at row0 (this lane's row scales s4; af: the
+  // split image's fp16-part accumulators, unused without it) for the sets the pre-test kept
+  auto exact = [&](i32x4 (&acc)[SETS], auto& af, int row0, const f32x4 s4, const bool (&hs)[SETS]) {
+    // (per-lane values from an opaque copy made here, so nothing derived from them can be
+    // hoisted out of the tile loop into the full register budget)
+    int lo = lane;
+    asm volatile("" : "+v"(lo));
+    const int rl = row0 + 4 * (lo >> 4), lq = lo & 15;
+#pragma unroll
+    for (int s = 0; s < SETS; ++s) {
+      if (!__builtin_amdgcn_ballot_w64(hs[s])) continue;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if constexpr (HK > 0)
+          v[r] = rl + r < row_end ? fmaf((float)acc[s][r], s4[r], af[s][r] * rsq[s]) : -INFINITY;
+        else
+          v[r] = rl + r < row_end ? (float)acc[s][r] * s4[r] : -INFINITY;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool p = v[r] >= thr[s];
+        const uint64_t m = __builtin_amdgcn_ballot_w64(p);
+        if (m) {
+          if (nst > STW - 64) flush();
+          const int idx = nst + (int)__builtin_amdgcn_mbcnt_hi(
+                                    (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+          if (p) {
+            st_s[idx] = v[r];
+            st_r[idx] = rl + r;
+            st_q[idx] = (uint16_t)(s * 16 + lq);
+          }
+          nst += __builtin_popcountll(m);
+        }
+      }
+    }
+  };
+  // one 16-row sub-tile (the single-sub-tile chains; plain image only).  Hot path, a conservative
+  // integer pre-test per set: max_r(acc_r * sx_r) <= max_r acc_r * (max_r sx_r) for a
+  // non-negative max, so a set whose bound misses its threshold has no hit; only the rest take
+  // the exact per-row test
+  //   max_r acc_r * sx_r >= thr  implies  max_r acc_r >= ceil(thr / max_r sx_r)  (thr > 0),
+  // so with one reciprocal per sub-tile each set's test is two v_max3_i32 and an integer
+  // compare; a set with thr <= 0 always takes the exact test
+  auto emit = [&](i32x4 (&acc)[SETS], int row0, const f32x4 s4) {
+    fence_acc(acc, acc);
     if constexpr (ABL == 2 || ABL == 4) {
 #pragma unroll
       for (int s = 0; s < SETS; ++s) asm volatile("" ::"v"(acc[s]), "v"(s4));
       return;
     }
-    if constexpr (HK > 0) {
-      // split image, a conservative pre-test per set as for the plain image:
-      //   max_r (acc_f,r / sq + acc_i,r sx_r) <= max_r acc_f,r / sq + max_r acc_i,r * (max_r sx_r
-      //   for a non-negative integer max, min_r sx_r for a negative one)
-      // -- two v_max3_i32, two v_max3_f32, a convert and an FMA per set; only the sets whose
-      // bound reaches the threshold take the exact per-row test
-      const float smx = fmaxf(fmaxf(s4[0], s4[1]), fmaxf(s4[2], s4[3]));
-      const float smn = fminf(fminf(s4[0], s4[1]), fminf(s4[2], s4[3]));
-      bool hs[SETS];
-      bool hit = false;
-#pragma unroll
-      for (int s = 0; s < SETS; ++s) {
-        int im;
-        float fm;
-        asm volatile("v_max3_i32 %0, %1, %2, %3\n\tv_max3_i32 %0, %0, %4, %4"
-                     : "=&v"(im) : "v"(acc[s][0]), "v"(acc[s][1]), "v"(acc[s][2]), "v"(acc[s][3]));
-        asm volatile("v_max3_f32 %0, %1, %2, %3\n\tv_max3_f32 %0, %0, %4, %4"
-                     : "=&v"(fm) : "v"(af[s][0]), "v"(af[s][1]), "v"(af[s][2]), "v"(af[s][3]));
-        // (+ |ub| 1e-4 + 1e-6: covers the rounding of this bound's own products)
-        const float ub = fmaf((float)im, im >= 0 ? smx : smn, fm * rsq[s]);
-        hs[s] = ub + fabsf(ub) * 1e-4f + 1e-6f >= thr[s];
-        hit |= hs[s];
-      }
-      if (!__builtin_amdgcn_ballot_w64(hit)) return;
-      const int rl = row0 + 4 * (lane >> 4), lq = lane & 15;
-#pragma unroll
-      for (int s = 0; s < SETS; ++s) {
-        if (!__builtin_amdgcn_ballot_w64(hs[s])) continue;
-        float v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          v[r] = rl + r < row_end ? fmaf((float)acc[s][r], s4[r], af[s][r] * rsq[s]) : -INFINITY;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bool p = v[r] >= thr[s];
-          const uint64_t m = __builtin_amdgcn_ballot_w64(p);
-          if (m) {
-            if (nst > STW - 64) flush();
-            const int idx = nst + (int)__builtin_amdgcn_mbcnt_hi(
-                                      (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-            if (p) {
-              st_s[idx] = v[r];
-              st_r[idx] = rl + r;
-              st_q[idx] = (uint16_t)(s * 16 + lq);
-            }
-            nst += __builtin_popcountll(m);
-          }
-        }
-      }
-      return;
-    }
-    // hot path, a conservative integer pre-test per set: max_r(acc_r * sx_r) <= max_r acc_r *
-    // (max_r sx_r) for a non-negative max (min_r sx_r for a negative one), so a set whose bound
-    // misses its threshold has no hit; only the rest take the exact per-row test below
-    //   max_r acc_r * sx_r >= thr  implies  max_r acc_r >= ceil(thr / max_r sx_r)  (thr > 0),
-    // so with one reciprocal per sub-tile each set's test is two v_max3_i32 and an integer
-    // compare; a set with thr <= 0 always takes the exact test
     const float rs = __builtin_amdgcn_rcpf(fmaxf(fmaxf(s4[0], s4[1]), fmaxf(s4[2], s4[3])));
     bool hs[SETS];
     bool hit = false;
@@ -414,36 +402,60 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
       hs[s] = im >= it;
       hit |= hs[s];
     }
-    if (__builtin_amdgcn_ballot_w64(hit)) {
-      int lo = lane;
-      asm volatile("" : "+v"(lo));
-      const int lrow = row0 + 4 * (lo >> 4), lq = lo & 15;
-      const int rl = row0 + 4 * (lo >> 4);
+    if (__builtin_amdgcn_ballot_w64(hit)) exact(acc, acc, row0, s4, hs);
+  };
+  // the fused chain's TWO sub-tiles (rows row0 .. row0 + 31, this lane's scales sa / sb) under
+  // ONE pre-test per set over all 8 of the lane's rows: max_r of the 8 estimates is bounded by
+  //   plain: max_r acc_r * max_r sx_r (thr > 0: a negative integer max cannot reach it; a set
+  //          with thr <= 0 always takes the exact test)
+  //   split: max_r acc_f,r / sq + max_r acc_i,r * (max_r sx_r, or min_r sx_r for a negative
+  //          integer max)
+  // -- half the pre-test instructions of two per-sub-tile tests (4 v_max3 per set for 8 values
+  // against 2 x 2, one convert / multiply / compare instead of two), the exact test as before
+  auto emit2 = [&](i32x4 (&acc)[2][SETS], auto& af, int row0, const f32x4 sa, const f32x4 sb) {
+    fence_acc(acc[0], af[0]);
+    fence_acc(acc[1], af[HK ? 1 : 0]);
+    if constexpr (ABL == 2 || ABL == 4) {
 #pragma unroll
-      for (int s = 0; s < SETS; ++s) {
-        if (!__builtin_amdgcn_ballot_w64(hs[s])) continue;
-        float v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          v[r] = rl + r < row_end ? (float)acc[s][r] * s4[r] : -INFINITY;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bool p = v[r] >= thr[s];
-          const uint64_t m = __builtin_amdgcn_ballot_w64(p);
-          if (m) {
-            if (nst > STW - 64) flush();
-            const int idx = nst + (int)__builtin_amdgcn_mbcnt_hi(
-                                      (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-            if (p) {
-              st_s[idx] = v[r];
-              st_r[idx] = lrow + r;
-              st_q[idx] = (uint16_t)(s * 16 + lq);
-            }
-            nst += __builtin_popcountll(m);
-          }
-        }
-      }
+      for (int s = 0; s < SETS; ++s) asm volatile("" ::"v"(acc[0][s]), "v"(acc[1][s]), "v"(sa), "v"(sb));
+      return;
     }
+    float smx;
+    asm volatile("v_max3_f32 %0, %1, %2, %3\n\tv_max3_f32 %0, %0, %4, %5\n\tv_max3_f32 %0, %0, %6, %7\n\tv_max3_f32 %0, %0, %8, %8"
+                 : "=&v"(smx) : "v"(sa[0]), "v"(sa[1]), "v"(sa[2]), "v"(sa[3]), "v"(sb[0]),
+                   "v"(sb[1]), "v"(sb[2]), "v"(sb[3]));
+    float smn = 0.f;
+    if constexpr (HK > 0)
+      smn = fminf(fminf(fminf(sa[0], sa[1]), fminf(sa[2], sa[3])),
+                  fminf(fminf(sb[0], sb[1]), fminf(sb[2], sb[3])));
+    bool hs[SETS];
+    bool hit = false;
+#pragma unroll
+    for (int s = 0; s < SETS; ++s) {
+      int im;
+      asm volatile("v_max3_i32 %0, %1, %2, %3\n\tv_max3_i32 %0, %0, %4, %5\n\tv_max3_i32 %0, %0, %6, %7\n\tv_max3_i32 %0, %0, %8, %8"
+                   : "=&v"(im) : "v"(acc[0][s][0]), "v"(acc[0][s][1]), "v"(acc[0][s][2]),
+                     "v"(acc[0][s][3]), "v"(acc[1][s][0]), "v"(acc[1][s][1]), "v"(acc[1][s][2]),
+                     "v"(acc[1][s][3]));
+      if constexpr (HK > 0) {
+        float fm;
+        asm volatile("v_max3_f32 %0, %1, %2, %3\n\tv_max3_f32 %0, %0, %4, %5\n\tv_max3_f32 %0, %0, %6, %7\n\tv_max3_f32 %0, %0, %8, %8"
+                     : "=&v"(fm) : "v"(af[0][s][0]), "v"(af[0][s][1]), "v"(af[0][s][2]),
+                       "v"(af[0][s][3]), "v"(af[1][s][0]), "v"(af[1][s][1]), "v"(af[1][s][2]),
+                       "v"(af[1][s][3]));
+        // (+ |ub| 1e-4 + 1e-6: covers the rounding of this bound's own products)
+        const float ub = fmaf((float)im, im >= 0 ? smx : smn, fm * rsq[s]);
+        hs[s] = ub + fabsf(ub) * 1e-4f + 1e-6f >= thr[s];
+      } else {
+        // (cvt and multiply are monotone: (float)im * smx >= every (float)acc_r * sx_r of a
+        // non-negative max, exactly as the exact test computes them)
+        hs[s] = thr[s] <= 0.f || (float)im * smx >= thr[s];
+      }
+      hit |= hs[s];
+    }
+    if (!__builtin_amdgcn_ballot_w64(hit)) return;
+    exact(acc[0], af[0], row0, sa, hs);
+    exact(acc[1], af[HK ? 1 : 0], row0 + SUB, sb, hs);
   };
 
   // the scale waves carry one extra vector-memory op per tile
@@ -519,16 +531,14 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
         // a late wave tests the previous tile's last two sub-tiles here, under its partner's
         // MFMAs
         if (g == 0 && late && t > 0) {
-          emit(acc2[0], accf2[0], row0 - TR + last - SUB, s4_prev);
-          emit(acc2[1], accf2[HK ? 1 : 0], row0 - TR + last, s4_last);
+          emit2(acc2, accf2, row0 - TR + last - SUB, s4_prev, s4_last);
         }
         if (g == 0)
           I8Chain2<D, 0, LOADS, G::DMA_EVERY, HK>::run(acc2, accf2, a2, qf, fg, dma, sa, sb);
         else
           I8Chain2<D, 0, 0, G::DMA_EVERY, HK>::run(acc2, accf2, a2, qf, fg, NoDma(), sa, sb);
         if (g + 1 < NG || !late) {
-          emit(acc2[0], accf2[0], row0 + jg * SUB, sa);
-          emit(acc2[1], accf2[HK ? 1 : 0], row0 + (jg + 1) * SUB, sb);
+          emit2(acc2, accf2, row0 + jg * SUB, sa, sb);
         } else {
           s4_prev = sa;
           s4_last = sb;
@@ -537,14 +547,14 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
       continue;
     } else {
     i8_prologue<D, 0>(a, fw);
-    if (late && t > 0) emit(acc, acc, row0 - TR + last, s4_last);
+    if (late && t > 0) emit(acc, row0 - TR + last, s4_last);
     if constexpr (NSW > 1)
       I8Chain<D, 0, LOADS, true, G::DMA_EVERY>::run(acc, a, qf, fw, fw + NKS * PIECE, dma);
     else
       I8Chain<D, 0, LOADS, false, G::DMA_EVERY>::run(acc, a, qf, fw, 0, dma);
 #pragma unroll
     for (int j = 1; j < NSW; ++j) {
-      emit(acc, acc, row0 + (j0 + j - 1) * SUB, scales(slot, j0 + j - 1));
+      emit(acc, row0 + (j0 + j - 1) * SUB, scales(slot, j0 + j - 1));
       if (j + 1 < NSW)
         I8Chain<D, 0, 0, true, G::DMA_EVERY>::run(acc, a, qf, fw + j * NKS * PIECE,
                                                  fw + (j + 1) * NKS * PIECE, NoDma());
@@ -552,17 +562,16 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
         I8Chain<D, 0, 0, false, G::DMA_EVERY>::run(acc, a, qf, fw + j * NKS * PIECE, 0, NoDma());
     }
     if (!late)
-      emit(acc, acc, row0 + last, scales(slot, j0 + NSW - 1));
+      emit(acc, row0 + last, scales(slot, j0 + NSW - 1));
     else
       s4_last = scales(slot, j0 + NSW - 1);
     }
   }
   if (late && n_tiles > 0) {
     if constexpr (FUSE) {
-      emit(acc2[0], accf2[0], row_begin + (n_tiles - 1) * TR + (j0 + NSW - 2) * SUB, s4_prev);
-      emit(acc2[1], accf2[HK ? 1 : 0], row_begin + (n_tiles - 1) * TR + (j0 + NSW - 1) * SUB, s4_last);
+      emit2(acc2, accf2, row_begin + (n_tiles - 1) * TR + (j0 + NSW - 2) * SUB, s4_prev, s4_last);
     } else {
-      emit(acc, acc, row_begin + (n_tiles - 1) * TR + (j0 + NSW - 1) * SUB, s4_last);
+      emit(acc, row_begin + (n_tiles - 1) * TR + (j0 + NSW - 1) * SUB, s4_last);
     }
   }
   if (nst) flush();
