@@ -167,6 +167,12 @@ def parse_args(argv=None):
     ap.add_argument("--scan-cus", type=int, default=0,
                     help="spread the index scans over this many CUs (0 = all), leaving the rest to "
                          "the encoder running beside them on the second stream")
+    ap.add_argument("--scan-cu-reserve", type=int, default=0,
+                    help="--mode full: CU-partitioned streams (parallel/cu_partition.py): the scans "
+                         "run on a stream masked to all CUs but this many per XCD, the encoder and "
+                         "the query-side pre-pass on streams that always have those CUs")
+    ap.add_argument("--side-cus", choices=["all", "reserve"], default="all",
+                    help="--scan-cu-reserve: the side streams' CUs (the reserve only, or every CU)")
     ap.add_argument("--search-priority", action="store_true",
                     help="run the search (and the step's bookkeeping) on a high-priority stream so "
                          "its short latency-bound kernels dispatch ahead of the encoder's")
@@ -502,6 +508,17 @@ def run_gpu(args, info, comm) -> int:
         torch.cuda.synchronize(dev)
         compute = torch.cuda.Stream(dev, priority=-1)
         torch.cuda.set_stream(compute)
+    cu_part = None
+    if args.scan_cu_reserve and args.mode == "full":
+        from codename_symbiont_amd.parallel.cu_partition import CuPartition
+
+        torch.cuda.synchronize(dev)
+        cu_part = CuPartition(dev, args.scan_cu_reserve, side_all=args.side_cus == "all", n_side=2)
+        compute = cu_part.main
+        torch.cuda.set_stream(compute)
+        shard.scan_cus = cu_part.main_cus
+        log(info, f"[bench] CU partition: scans on {cu_part.main_cus} CUs, reserve "
+                  f"{len(cu_part.reserve)} CUs ({args.side_cus} for the encoder / pre-pass)")
     copy_done = [torch.cuda.Event(), torch.cuda.Event()]
     consumed = [torch.cuda.Event(), torch.cuda.Event()]
     host_free = [torch.cuda.Event() for _ in range(NB)]   # host slot's H2D copy has finished
@@ -512,7 +529,7 @@ def run_gpu(args, info, comm) -> int:
     # power-bound; the encoder's small kernels fill its tail and launch gaps).  Every timed step
     # still encodes one batch and searches one batch.
     overlap = args.mode == "full" and not group_dp and not args.no_overlap
-    enc_stream = torch.cuda.Stream(dev)
+    enc_stream = torch.cuda.Stream(dev) if cu_part is None else cu_part.sides[0]
     # output slots: batch i's embeddings live in outs[i % NO] from its encode to its search's end
     pipeline = overlap and args.queries == "self" and not args.no_search_pipeline
     AHEAD = args.encode_ahead if pipeline else 1
@@ -619,7 +636,7 @@ def run_gpu(args, info, comm) -> int:
     # work (upsert, int8 queries, the exact threshold sample, route) runs on pre_stream as soon
     # as it is encoded, under batch i's full-shard scan; the compute stream only runs the scans
     # back to back (ShardedSearcher.begin / end, HbmIndexShard.search_begin / search_end).
-    pre_stream = torch.cuda.Stream(dev)
+    pre_stream = torch.cuda.Stream(dev) if cu_part is None else cu_part.sides[1]
     pre_done = [torch.cuda.Event() for _ in range(NO)]
     handles: dict = {}
 
@@ -823,6 +840,7 @@ def run_gpu(args, info, comm) -> int:
                                                    and cfg.hidden in MQ_DIMS) else "list-256q"),
         "encoder_hipgraph": use_graph,
         "search_priority": args.search_priority,
+        "scan_cu_reserve_per_xcd": args.scan_cu_reserve,
         "scan_min_tiles": args.scan_min_tiles,
         "prepass_min_tiles": shard.prepass_min_tiles,
         "prune_sample_shift": ((shard.PRUNE_TILE_SHIFT_SPLIT if shard._i8_heavy

@@ -328,6 +328,30 @@ class EncoderRuntime {
 PYBIND11_MODULE(_hip, m) {
   m.doc() = "CDNA4 (gfx950) HIP kernels of codename_symbiont_amd";
   m.def("arch", []() { return std::string("gfx950"); });
+  // CU-partitioned streams (hipExtStreamCreateWithCUMask): a stream whose kernels the hardware
+  // dispatches only to the CUs set in `mask` (bit i of word i / 32 = CU i as the runtime numbers
+  // them).  Returned as a raw handle for torch.cuda.ExternalStream; streams live until
+  // stream_destroy.  cu_mask_of reads a stream's mask back (tests).
+  m.def("stream_with_cu_mask", [](int device, std::vector<uint32_t> mask) {
+    check((int)hipSetDevice(device), "hipSetDevice");
+    hipStream_t st = nullptr;
+    check((int)hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()),
+          "hipExtStreamCreateWithCUMask");
+    return (uptr)st;
+  }, py::arg("device"), py::arg("mask"));
+  m.def("cu_mask_of", [](uptr st, int words) {
+    std::vector<uint32_t> mask((size_t)words, 0u);
+    check((int)hipExtStreamGetCUMask(S(st), (uint32_t)words, mask.data()), "hipExtStreamGetCUMask");
+    return mask;
+  }, py::arg("stream"), py::arg("words"));
+  m.def("stream_destroy", [](uptr st) { check((int)hipStreamDestroy(S(st)), "hipStreamDestroy"); },
+        py::arg("stream"));
+  m.def("cu_count", [](int device) {
+    int n = 0;
+    check((int)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device),
+          "hipDeviceGetAttribute");
+    return n;
+  }, py::arg("device"));
   m.def("set_debug", [](bool on) { g_debug = on; }, py::arg("on"));
   m.def("debug", []() { return g_debug; });
   m.def("embed_ln", [](uptr ids, uptr pos, uptr tt, uptr wemb, uptr pemb, uptr temb, uptr g,
