@@ -16,3 +16,4 @@ for v in "0 all" "1 all" "2 all" "4 all" "2 reserve" "0 all"; do set -- $v
 done
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o h -- python bench.py --steps 30 --warmup 5 > $O/prof.json 2> $O/prof.err || { tail -20 $O/prof.err; exit 1; }
 python benchmarks/step_trace.py $O/prof/h_kernel_trace.csv
+find $O/prof -name "*kernel_trace.csv" -size +8M -delete

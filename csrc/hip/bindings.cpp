@@ -71,6 +71,7 @@ int symb_index_scan_i8(const void* X8, const float* sx, int n_valid, int alloc_r
                        int rsplit, const int* skip, int dim, int heavy, const float* sq);
 int symb_i8_tile_rows_for(int dim, int heavy);
 int symb_i8_split_queries_per_blk(int rsplit);
+int symb_i8_pair_config(int pair);
 int symb_quant_rows_split(const float* X, int n, int dim, void* X8, float* sx, float* bounds,
                           float* margin, hipStream_t st);
 int symb_prune_qquant(const void* Q, int NQ, int dim, const float* bounds, void* Q8, float* sq,
@@ -414,6 +415,8 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("tile_rows"), py::arg("waves") = 8);
   m.def("i8_tile_rows", [](int dim, int heavy) { return symb_i8_tile_rows_for(dim, heavy); },
         py::arg("dim") = 384, py::arg("heavy") = 0);
+  m.def("i8_pair_config", [](int pair) { check(symb_i8_pair_config(pair), "i8_pair_config"); },
+        py::arg("pair"));
   m.def("i8_split_queries_per_blk", [](int rsplit) { return symb_i8_split_queries_per_blk(rsplit); },
         py::arg("rsplit") = 2);
   m.def("quant_rows_split", [](uptr X, int n, int dim, uptr X8, uptr sx, uptr bounds, uptr margin,

@@ -229,7 +229,12 @@ __device__ __forceinline__ const char* i8_uniform(const char* p) {
 // bits each) and only the 320 trailing ones quantised to int8 with their own per-row scale.
 // Emit iff acc_f / sq + acc_i * sx >= thr (sq_in: the queries' int8 scales); the bound (prune_
 // qquant_h) is the int8 one on the trailing dims plus the fp16 rounding of the leading ones.
-template <int D, int RSPLIT, int ABL = 0, int TRK = 64, int WV = 8, int HK = 0>
+// PAIR (fused chains): one pre-test over both sub-tiles of a chain first (emit2), then the
+// per-sub-tile ones; false (default) = the per-sub-tile pre-tests alone.  Same-box A/B
+// (profiles/r4_split/pair/): headline 11.10-11.19 vs 11.20 ms, anisotropic 13.19-13.20 vs
+// 13.21-13.25, random held-out 11.86 vs 11.03-11.05 (its busy band pays both tests): the
+// emission pre-test is not what bounds the scan, so the pair test stays an A/B knob.
+template <int D, int RSPLIT, int ABL = 0, int TRK = 64, int WV = 8, int HK = 0, bool PAIR = true>
 __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
     const int8_t* __restrict__ X8, const float* __restrict__ sx, int n_valid, int rows_per_blk,
     const int8_t* __restrict__ Q8, int NQ, int n_qblk, int xcd, const float* __restrict__ thr_in,
@@ -420,6 +425,11 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
       for (int s = 0; s < SETS; ++s) asm volatile("" ::"v"(acc[0][s]), "v"(acc[1][s]), "v"(sa), "v"(sb));
       return;
     }
+    bool hs[SETS];
+    if constexpr (!PAIR) {   // (A/B: the per-sub-tile pre-tests alone)
+#pragma unroll
+      for (int s = 0; s < SETS; ++s) hs[s] = true;
+    } else {
     float smx;
     asm volatile("v_max3_f32 %0, %1, %2, %3\n\tv_max3_f32 %0, %0, %4, %5\n\tv_max3_f32 %0, %0, %6, %7\n\tv_max3_f32 %0, %0, %8, %8"
                  : "=&v"(smx) : "v"(sa[0]), "v"(sa[1]), "v"(sa[2]), "v"(sa[3]), "v"(sb[0]),
@@ -428,7 +438,6 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
     if constexpr (HK > 0)
       smn = fminf(fminf(fminf(sa[0], sa[1]), fminf(sa[2], sa[3])),
                   fminf(fminf(sb[0], sb[1]), fminf(sb[2], sb[3])));
-    bool hs[SETS];
     bool hit = false;
 #pragma unroll
     for (int s = 0; s < SETS; ++s) {
@@ -454,8 +463,36 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
       hit |= hs[s];
     }
     if (!__builtin_amdgcn_ballot_w64(hit)) return;
-    exact(acc[0], af[0], row0, sa, hs);
-    exact(acc[1], af[HK ? 1 : 0], row0 + SUB, sb, hs);
+    }
+    // a pair that reaches a threshold: the per-sub-tile pre-test (as `emit`) before the exact
+    // test, so a busy band (held-out queries over random rows: thousands of candidates per query)
+    // costs what it did with per-sub-tile tests, while the common miss costs half
+    auto sub = [&](i32x4 (&ac)[SETS], auto& afc, int r0, const f32x4 s4) {
+      const float sm = fmaxf(fmaxf(s4[0], s4[1]), fmaxf(s4[2], s4[3]));
+      float sn = 0.f;
+      if constexpr (HK > 0) sn = fminf(fminf(s4[0], s4[1]), fminf(s4[2], s4[3]));
+      bool hc[SETS];
+      bool any = false;
+#pragma unroll
+      for (int s = 0; s < SETS; ++s) {
+        int im;
+        asm volatile("v_max3_i32 %0, %1, %2, %3\n\tv_max3_i32 %0, %0, %4, %4"
+                     : "=&v"(im) : "v"(ac[s][0]), "v"(ac[s][1]), "v"(ac[s][2]), "v"(ac[s][3]));
+        if constexpr (HK > 0) {
+          float fm;
+          asm volatile("v_max3_f32 %0, %1, %2, %3\n\tv_max3_f32 %0, %0, %4, %4"
+                       : "=&v"(fm) : "v"(afc[s][0]), "v"(afc[s][1]), "v"(afc[s][2]), "v"(afc[s][3]));
+          const float ub = fmaf((float)im, im >= 0 ? sm : sn, fm * rsq[s]);
+          hc[s] = hs[s] && ub + fabsf(ub) * 1e-4f + 1e-6f >= thr[s];
+        } else {
+          hc[s] = hs[s] && (thr[s] <= 0.f || (float)im * sm >= thr[s]);
+        }
+        any |= hc[s];
+      }
+      if (__builtin_amdgcn_ballot_w64(any)) exact(ac, afc, r0, s4, hc);
+    };
+    sub(acc[0], af[0], row0, sa);
+    sub(acc[1], af[HK ? 1 : 0], row0 + SUB, sb);
   };
 
   // the scale waves carry one extra vector-memory op per tile
@@ -1084,6 +1121,13 @@ int symb_i8_queries_per_blk(int rsplit) {
   return g_i8_waves == 4 ? 4 * 16 * i8s::SETS : i8s::WAVES / rsplit * 16 * i8s::SETS;
 }
 
+static int g_i8_pair = 0;
+int symb_i8_pair_config(int pair) {
+  if (pair != 0 && pair != 1) return -1;
+  g_i8_pair = pair;
+  return 0;
+}
+
 template <int D, int RSPLIT, int TRK, int WV = 8, int HK = 0>
 static int launch_i8(const void* X8, const float* sx, int n_valid, int rows_per_blk, int n_rblk,
                      const void* Q8, int NQ, const float* thr, float* cand_s, int* cand_i,
@@ -1092,11 +1136,18 @@ static int launch_i8(const void* X8, const float* sx, int n_valid, int rows_per_
   constexpr int qpb = WV / RSPLIT * 16 * i8s::SETS;
   const int n_qblk = (NQ + qpb - 1) / qpb;
   constexpr int lds = Geo<D, TRK, WV, HK>::LDS_BYTES;
-  set_max_lds<index_scan_i8_kernel<D, RSPLIT, 0, TRK, WV, HK>>(lds);
-  hipLaunchKernelGGL((index_scan_i8_kernel<D, RSPLIT, 0, TRK, WV, HK>), dim3(n_rblk * n_qblk),
-                     dim3(64 * WV), lds, st, (const int8_t*)X8, sx, n_valid, rows_per_blk,
-                     (const int8_t*)Q8, NQ, n_qblk, xcd, thr, cand_s, cand_i, cand_n, cap, skip, sq);
-  return (int)hipGetLastError();
+  auto go = [&](auto kern) {
+    set_max_lds<decltype(kern)::value>(lds);
+    hipLaunchKernelGGL(decltype(kern)::value, dim3(n_rblk * n_qblk), dim3(64 * WV), lds, st,
+                       (const int8_t*)X8, sx, n_valid, rows_per_blk, (const int8_t*)Q8, NQ, n_qblk,
+                       xcd, thr, cand_s, cand_i, cand_n, cap, skip, sq);
+    return (int)hipGetLastError();
+  };
+  if (g_i8_pair)
+    return go(std::integral_constant<decltype(&index_scan_i8_kernel<D, RSPLIT, 0, TRK, WV, HK, true>),
+                                     &index_scan_i8_kernel<D, RSPLIT, 0, TRK, WV, HK, true>>());
+  return go(std::integral_constant<decltype(&index_scan_i8_kernel<D, RSPLIT, 0, TRK, WV, HK, false>),
+                                   &index_scan_i8_kernel<D, RSPLIT, 0, TRK, WV, HK, false>>());
 }
 
 // Tile rows the D-wide scan runs with (the 128-row and 4-wave forms are D = 384 knobs; the split
