@@ -1012,8 +1012,8 @@ class HbmIndexShard:
         self._route_last = dense
         self._route_blk_last = blk
         if self.mq_stats:   # (diagnostics / benchmarks/micro.py scani8abl: inputs and grid)
-            self._pruned_last = dict(q8=q8, thr=thr, rows_per_blk=rows_per_blk, n_rblk=n_rblk,
-                                     cap=cap, cs=cs, ci=ci, cnt=cnt, q=q_unit)
+            self._pruned_last = dict(q8=q8, thr=thr, sq=ctx["sq"], rows_per_blk=rows_per_blk,
+                                     n_rblk=n_rblk, cap=cap, cs=cs, ci=ci, cnt=cnt, q=q_unit)
         self._stats(ovf, cnt, dense, blk)
         return out_s, out_i
 

@@ -7,10 +7,13 @@ A CU mask makes the partition a property of the STREAM: the scan stream's kernel
 only to its CUs, and the reserve stays free for the other streams whatever the grid sizes are
 (unlike a grid-size cap, which the dispatcher may still place anywhere).
 
-Which CUs to reserve: MI355X has 256 CUs in 8 XCDs.  The runtime numbers CUs 0..255; whether CU
-i sits on XCD i // 32 or on XCD i % 8 is not documented here, so the reserve takes CUs
-32 x + ((x + 8 j) mod 32) for XCD slot x and j < per_xcd -- exactly ``per_xcd`` CUs of every XCD
-under either numbering, so each XCD's L2 keeps serving the same share of the scan.
+Which CUs to reserve: MI355X has 256 CUs in 8 XCDs, and how the runtime's mask bits map onto
+(XCD, shader engine, CU) is not documented here.  ``probe_cu_map`` measures it (one tiny launch per
+mask bit reads the hardware ids of the CU it ran on) and the reserve takes ``per_xcd`` CUs of
+every XCD, dealt over its shader engines, so every XCD keeps the same share of the scan's
+workgroups (which are dealt round-robin over the XCDs).  A first version guessed two numberings
+(``balanced_reserve``); at 1-2 CUs per XCD it left some XCD with fewer free CUs than scan
+workgroups and the step went from 11.0 to 16.1-16.7 ms (profiles/r4_cu_partition/).
 """
 from __future__ import annotations
 
@@ -43,6 +46,63 @@ def mask_words(n_cus: int, cus) -> list[int]:
     return words
 
 
+_MAPS: dict = {}
+
+
+def probe_cu_map(device) -> list[tuple[int, int, int]]:
+    """(xcc, se, cu) of every CU-mask bit of ``device``, measured: for each bit, 16 workgroups on a
+    stream masked to that CU alone record HW_ID / XCC_ID (csrc/hip/cu_probe.hip).  Cached."""
+    from ..ops._ext import hip, stream_handle
+
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    if idx in _MAPS:
+        return _MAPS[idx]
+    h = hip()
+    n = h.cu_count(idx)
+    out = torch.zeros(n, 16, 2, dtype=torch.int32, device=torch.device("cuda", idx))
+    streams = []
+    torch.cuda.synchronize(idx)
+    for c in range(n):
+        st = h.stream_with_cu_mask(idx, mask_words(n, [c]))
+        streams.append(st)
+        h.cu_probe(out[c].data_ptr(), 16, st)
+    torch.cuda.synchronize(idx)
+    for st in streams:
+        h.stream_destroy(st)
+    ids = out.cpu().to(torch.int64) & 0xFFFFFFFF
+    res = []
+    for c in range(n):
+        hw, xcc = ids[c, :, 0], ids[c, :, 1] & 0xF
+        cu, se = (hw >> 8) & 0xF, (hw >> 13) & 0x7
+        key = {(int(a), int(b), int(d)) for a, b, d in zip(xcc, se, cu)}
+        if len(key) != 1:
+            raise RuntimeError(f"CU mask bit {c} ran on {sorted(key)}: not one CU")
+        res.append(key.pop())
+    _MAPS[idx] = res
+    return res
+
+
+def reserve_from_map(cu_map, per_xcd: int) -> list[int]:
+    """``per_xcd`` mask bits of every XCC, dealt round-robin over its shader engines."""
+    by_xcc: dict = {}
+    for bit, (xcc, se, cu) in enumerate(cu_map):
+        by_xcc.setdefault(xcc, {}).setdefault(se, []).append((cu, bit))
+    out = []
+    for xcc, ses in sorted(by_xcc.items()):
+        lists = [sorted(v) for _, v in sorted(ses.items())]
+        picked, j = [], 0
+        while len(picked) < per_xcd:
+            lst = lists[j % len(lists)]
+            k = j // len(lists)
+            if k >= len(lst):
+                raise ValueError(f"XCC {xcc} has too few CUs for {per_xcd}")
+            picked.append(lst[k][1])
+            j += 1
+        out += picked
+    return sorted(out)
+
+
 class CuPartition:
     """CU-masked streams on ``device``: ``main`` on every CU but the reserve (the scans) and
     ``n_side`` side streams (``sides``; ``side`` = the first) on the reserve only
@@ -50,14 +110,18 @@ class CuPartition:
     idle).  ``main_cus`` is the number of CUs the main stream owns (the scans size their grids to
     it)."""
 
-    def __init__(self, device, per_xcd: int, side_all: bool = True, n_side: int = 1):
+    def __init__(self, device, per_xcd: int, side_all: bool = True, n_side: int = 1,
+                 probe: bool = True):
         from ..ops._ext import hip
 
         self.device = torch.device(device)
         idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
         h = hip()
         self.n_cus = h.cu_count(idx)
-        self.reserve = balanced_reserve(self.n_cus, per_xcd)
+        # the measured bit -> (XCC, SE, CU) map (probe_cu_map), else the numbering-agnostic guess
+        self.cu_map = probe_cu_map(self.device) if probe else None
+        self.reserve = (reserve_from_map(self.cu_map, per_xcd) if probe
+                        else balanced_reserve(self.n_cus, per_xcd))
         rest = [c for c in range(self.n_cus) if c not in set(self.reserve)]
         self.main_cus = len(rest)
         side_mask = mask_words(self.n_cus, range(self.n_cus) if side_all else self.reserve)

@@ -72,6 +72,7 @@ int symb_index_scan_i8(const void* X8, const float* sx, int n_valid, int alloc_r
 int symb_i8_tile_rows_for(int dim, int heavy);
 int symb_i8_split_queries_per_blk(int rsplit);
 int symb_i8_pair_config(int pair);
+int symb_cu_probe(uint32_t* out, int n_blocks, hipStream_t st);
 int symb_quant_rows_split(const float* X, int n, int dim, void* X8, float* sx, float* bounds,
                           float* margin, hipStream_t st);
 int symb_prune_qquant(const void* Q, int NQ, int dim, const float* bounds, void* Q8, float* sq,
@@ -345,6 +346,9 @@ PYBIND11_MODULE(_hip, m) {
     check((int)hipExtStreamGetCUMask(S(st), (uint32_t)words, mask.data()), "hipExtStreamGetCUMask");
     return mask;
   }, py::arg("stream"), py::arg("words"));
+  m.def("cu_probe", [](uptr out, int n_blocks, uptr st) {
+    check(symb_cu_probe(P<uint32_t>(out), n_blocks, S(st)), "cu_probe");
+  }, py::arg("out"), py::arg("n_blocks"), py::arg("stream"));
   m.def("stream_destroy", [](uptr st) { check((int)hipStreamDestroy(S(st)), "hipStreamDestroy"); },
         py::arg("stream"));
   m.def("cu_count", [](int device) {

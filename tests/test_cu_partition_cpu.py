@@ -24,3 +24,16 @@ def test_mask_words_and_limits():
         balanced_reserve(256, 5)
     with pytest.raises(ValueError):
         mask_words(64, [64])
+
+
+def test_reserve_from_a_measured_map_spreads_over_xcc_and_se():
+    from codename_symbiont_amd.parallel.cu_partition import reserve_from_map
+
+    # a made-up numbering: bit b -> XCC (b // 4) % 8, SE (b // 32) % 4, CU b % 4 + 4 * (b // 128)
+    m = [((b // 4) % 8, (b // 32) % 4, b % 4 + 4 * (b // 128)) for b in range(256)]
+    assert len(set(m)) == 256
+    r = reserve_from_map(m, 4)
+    assert len(r) == 32
+    for x in range(8):
+        mine = [m[b] for b in r if m[b][0] == x]
+        assert len(mine) == 4 and len({se for _, se, _ in mine}) == 4   # one per shader engine
