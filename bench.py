@@ -746,6 +746,8 @@ def run_gpu(args, info, comm) -> int:
     if shard._mq_tot is not None:   # count overflows of the timed steps only
         for t in shard._mq_tot:
             t.zero_()
+    if shard._mx4_tot is not None:
+        shard._mx4_tot.zero_()
     for kph in hph:
         hph[kph] = 0.0
     sampler = ClockSampler(dev.index) if (args.timeline and info.is_root) else None
@@ -796,6 +798,8 @@ def run_gpu(args, info, comm) -> int:
         if len(shard._mq_tot) > 4:   # searches that sent only some row blocks to the bf16 scan
             extra_out["search_block_route_batches"] = int(shard._mq_tot[3].item())
             extra_out["search_block_routed_blocks"] = int(shard._mq_tot[4].item())
+        if shard._mx4_tot is not None:   # batches whose first tier was the MX-fp4 scan
+            extra_out["search_mx4_tier_batches"] = int(shard._mx4_tot.item())
         if shard.rows_i8 is not None:   # the pruning image's form (HbmIndexShard.calibrate_prune)
             extra_out["i8_image"] = "split" if shard._i8_heavy else "plain"
             extra_out["i8_calib_share"] = (None if shard.calib_share is None

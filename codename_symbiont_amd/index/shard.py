@@ -135,6 +135,7 @@ MQ_DIMS = (384, 768, 1024)              # ... the emitting bf16 scan (index_mq.h
 PRUNE_DIMS = (384, 768)                 # ... the int8-pruned scan (index_i8.hip)
 SPLIT_DIMS = (384,)                     # ... its split image (calibrate_prune)
 SPLIT_HEAVY = 64                        # leading components the split image keeps as fp16
+MX4_DIMS = (384,)                       # ... the MX-fp4 first tier (index_i8.hip HK = MX4)
 
 
 class HbmIndexShard:
@@ -201,6 +202,14 @@ class HbmIndexShard:
             self.sx_i8 = torch.ones(n_alloc, dtype=torch.float32, device=self.device)
             # (E, X) of the plain form; (E_l, X_l, E_h, X_h) of the split form
             self.i8_bounds = torch.zeros(4, dtype=torch.float32, device=self.device)
+        # the MX-fp4 image (a first tier below the int8 one, _pruned_end): 192 bytes of e2m1
+        # nibbles + 16 bytes of block scales per 384-wide row, and its (E4, X4) maxima
+        self.rows_mx4 = self.sc_mx4 = self.mx4_bounds = None
+        if prune and dim in MX4_DIMS and os.environ.get("SYMB_PRUNE_MX4", "1") not in ("", "0"):
+            n_alloc = _round_up(self.rows.shape[0], 128)
+            self.rows_mx4 = torch.zeros(n_alloc, dim // 2, dtype=torch.uint8, device=self.device)
+            self.sc_mx4 = torch.zeros(n_alloc, 16, dtype=torch.uint8, device=self.device)
+            self.mx4_bounds = torch.zeros(2, dtype=torch.float32, device=self.device)
         self.count = 0      # rows reserved (payload slots exist)
         # rows searches may read: published only after their writes are ENQUEUED on the stream
         # the scans share, so a search racing an upsert in another thread never scans a reserved
@@ -238,6 +247,8 @@ class HbmIndexShard:
         # streamed once per 512 queries), True = the 256-query fused form (twice the L2 reads)
         self.i8_rsplit2 = False
         self._mq_tot = None
+        self._mx4_tot = None     # searches whose first tier was the MX-fp4 scan (mq_stats)
+        self._mx4_last = None
         # snapshot change record (index/persist.py ShardPersister): rows covered by the last cut
         # and the covered rows overwritten since; kept only while ``payloads.track`` is on
         self._persisted = 0
@@ -295,6 +306,9 @@ class HbmIndexShard:
             else:
                 self._i8_image(self.rows[r0:r0 + n], self.rows_i8[r0:r0 + n],
                                self.sx_i8[r0:r0 + n], self.i8_bounds)
+        if self.rows_mx4 is not None and n > 0:
+            self._mx4_image(self.rows[r0:r0 + n], self.rows_mx4[r0:r0 + n],
+                            self.sc_mx4[r0:r0 + n], self.mx4_bounds)
         if self.rows8 is None or n <= 0:
             return
         src, dst = self.rows[r0:r0 + n], self.rows8[r0:r0 + n]
@@ -355,6 +369,29 @@ class HbmIndexShard:
             self._i8_image(self.rows[s:e], self.rows_i8[s:e], self.sx_i8[s:e], self.i8_bounds)
         self._calib_gen += 1
         self._calib_next = max(hi * self.CALIB_GROWTH, self.CALIB_MIN_ROWS)
+
+    def _mx4_image(self, src, dst, sc, bounds, margin=None) -> None:
+        """MX-fp4 image of bf16 rows (bounds raised) or, with ``margin``, of queries (margin
+        = |q| E4 + |q - q~| X4 + 1e-5 from bounds): index_i8.hip quant_rows_mx4."""
+        n = src.shape[0]
+        if n == 0:
+            return
+        if self.device.type == "cuda":
+            from ..ops._ext import hip, stream_handle
+
+            hip().quant_rows_mx4(src.data_ptr(), n, self.dim, dst.data_ptr(), sc.data_ptr(),
+                                 bounds.data_ptr(), 0 if margin is None else margin.data_ptr(),
+                                 stream_handle(self.device))
+            return
+        from ..ops.reference import quant_rows_mx4_ref
+
+        img, scr, _, nr = quant_rows_mx4_ref(src)
+        dst.copy_(img)
+        sc.copy_(scr)
+        if margin is None:
+            torch.maximum(bounds, nr[:, :2].amax(0), out=bounds)
+        else:
+            margin.copy_(nr[:, 2] * bounds[0] + nr[:, 0] * bounds[1] + 1e-5)
 
     def prune_query_image(self, q_unit: torch.Tensor):
         """(image, scale, margin) of unit queries in the shard's current form: the int8 image and
@@ -527,6 +564,12 @@ class HbmIndexShard:
             self._i8_image(scratch.rows[:n], img, sc, self.i8_bounds)
             self.rows_i8.index_copy_(0, di, img)
             self.sx_i8.index_copy_(0, di, sc)
+        if self.rows_mx4 is not None:
+            img4 = torch.empty(n, self.dim // 2, dtype=torch.uint8, device=self.device)
+            sc4 = torch.empty(n, 16, dtype=torch.uint8, device=self.device)
+            self._mx4_image(scratch.rows[:n], img4, sc4, self.mx4_bounds)
+            self.rows_mx4.index_copy_(0, di, img4)
+            self.sc_mx4.index_copy_(0, di, sc4)
 
     def upsert(self, point_ids: list[str], vecs: torch.Tensor, payloads: list[Payload]) -> list[int]:
         """Qdrant-style upsert: existing ids are overwritten in place, new ids appended.  An id
@@ -832,6 +875,9 @@ class HbmIndexShard:
     # SYMB_TAIL_DENSE_MAX_NQ=0 keeps the emitting tail scan (A/B)
     tail_dense_max_nq = int(os.environ.get("SYMB_TAIL_DENSE_MAX_NQ", "512"))
     PRUNE_BLOCK_FRAC = 1 / 32
+    # the MX-fp4 first tier runs when every query's estimated fp4 band holds at most this share
+    # of PRUNE_CAP (its candidates are re-scored exactly like the int8 ones)
+    MX4_LIMIT_FRAC = 0.25
     prune_route = True   # False: always take the int8 pass (tests of the overflow fallback)
 
     def _search_pruned(self, q_unit, k: int, n_cus):
@@ -929,8 +975,28 @@ class HbmIndexShard:
                       blk.data_ptr(), st, tail_cs=tcs.data_ptr(),
                       tail_ci=0 if tci is None else tci.data_ptr(),
                       tail_cnt=0 if tcnt is None else tcnt.data_ptr(), tail_cap=tcap, tail_off=t0)
-        return dict(q=q_unit, k=k, n=n, n_cus=n_cus, q8=q8, sq=sq, thr=thr, T=T, dense=dense,
-                    blk=blk, geo=geo, heavy=heavy, gen=self._calib_gen)
+        ctx = dict(q=q_unit, k=k, n=n, n_cus=n_cus, q8=q8, sq=sq, thr=thr, T=T, dense=dense,
+                   blk=blk, geo=geo, heavy=heavy, gen=self._calib_gen, mx4=None)
+        # 3. the MX-fp4 first tier (mx4_select): when every query's k-th score sits so far above
+        #    the corpus bulk that even the coarse fp4 bound (|q| E4 + |q - q~| X4, ~0.25 on unit
+        #    rows) leaves few rows in its band -- self / near-duplicate queries, such as the
+        #    headline's freshly inserted random-init embeddings -- the scan streams the 208-byte
+        #    fp4 image at twice the int8 MFMA rate instead of the 384-byte int8 one.  Decided on the
+        #    GPU from the same exact sample (the band must lie above the sample's seed threshold,
+        #    so the sample counted it): the int8 / split scan and the fp4 scan are both enqueued,
+        #    each gated on the flag, and exactly one runs.
+        if self.rows_mx4 is not None and self.prune_route and tci is None:
+            q4 = torch.empty(NQ, self.dim // 2, dtype=torch.uint8, device=dev)
+            qs4 = torch.empty(NQ, 16, dtype=torch.uint8, device=dev)
+            m4 = torch.empty(NQ, dtype=torch.float32, device=dev)
+            self._mx4_image(q_unit, q4, qs4, self.mx4_bounds, margin=m4)
+            thr4 = torch.empty(NQ, dtype=torch.float32, device=dev)
+            nv = torch.empty(1, dtype=torch.int32, device=dev)
+            h.mx4_select(NQ, T.data_ptr(), m4.data_ptr(), thr0.data_ptr(), cs_p.data_ptr(),
+                         cnt_p.data_ptr(), self.SAMPLE_CAP, ts, tcs.data_ptr(), tcap,
+                         self.MX4_LIMIT_FRAC * cap, thr4.data_ptr(), nv.data_ptr(), st)
+            ctx["mx4"] = dict(q4=q4, qs4=qs4, thr4=thr4, nv=nv)
+        return ctx
 
     def _i8_geometry(self, n: int, NQ: int, n_cus: int):
         """(rsplit, rows_per_blk, n_rblk) of the int8 scan over n rows: ~one workgroup per CU
@@ -988,11 +1054,24 @@ class HbmIndexShard:
         out_s = torch.empty(NQ, k, device=dev)
         out_i = torch.empty(NQ, k, dtype=torch.int32, device=dev)
         skip = blk[2 + n_rblk:].data_ptr() if self.prune_route else 0
+        m4 = ctx.get("mx4")
+        if m4 is not None:   # both tiers enqueued, gated on the flag: exactly one runs
+            for t in ("q4", "qs4", "thr4", "nv"):
+                m4[t].record_stream(cur)
+            cnt.zero_()
+        gate, want = (m4["nv"].data_ptr(), 1) if m4 is not None else (0, 0)
         h.index_scan_i8(self.rows_i8.data_ptr(), self.sx_i8.data_ptr(), n, self.rows_i8.shape[0],
                         rows_per_blk, n_rblk,
                         q8.data_ptr(), NQ, thr.data_ptr(), cs.data_ptr(), ci.data_ptr(),
                         cnt.data_ptr(), cap, self.scan_xcd, st, rsplit, skip=skip, dim=self.dim,
-                        heavy=ctx["heavy"], sq=ctx["sq"].data_ptr())
+                        heavy=ctx["heavy"], sq=ctx["sq"].data_ptr(), gate=gate, gate_want=want)
+        if m4 is not None:
+            h.index_scan_i8(self.rows_mx4.data_ptr(), self.sc_mx4.data_ptr(), n,
+                            self.rows_mx4.shape[0], rows_per_blk, n_rblk, m4["q4"].data_ptr(), NQ,
+                            m4["thr4"].data_ptr(), cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(),
+                            cap, self.scan_xcd, st, rsplit, skip=skip, dim=self.dim,
+                            sq=m4["qs4"].data_ptr(), form=1, gate=m4["nv"].data_ptr(),
+                            gate_want=0)
         # 3'. the bf16 emitting scan of the blocks the route listed, at the exact threshold T,
         #     into the same candidate buffers (no launch work when none is listed)
         if self.prune_route:
@@ -1010,6 +1089,11 @@ class HbmIndexShard:
         self._scan(n, q_unit, kmax, k, T.contiguous(), n_cus, gate=ovf, out=(out_s, out_i))
         self._mq_last = (cnt, ovf)
         self._route_last = dense
+        self._mx4_last = None if m4 is None else m4["nv"]   # 0: the MX-fp4 tier ran
+        if self.mq_stats and m4 is not None:
+            if self._mx4_tot is None:
+                self._mx4_tot = torch.zeros(1, dtype=torch.int32, device=dev)
+            self._mx4_tot.add_(1 - m4["nv"])
         self._route_blk_last = blk
         if self.mq_stats:   # (diagnostics / benchmarks/micro.py scani8abl: inputs and grid)
             self._pruned_last = dict(q8=q8, thr=thr, sq=ctx["sq"], rows_per_blk=rows_per_blk,

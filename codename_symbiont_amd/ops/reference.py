@@ -140,3 +140,51 @@ def split_estimate_ref(q_img: torch.Tensor, sq: torch.Tensor, x_img: torch.Tenso
     qh, ql = parts(q_img)
     xh, xl = parts(x_img)
     return qh @ xh.t() + (ql @ xl.t()) * sq[:, None] * sx[None, :]
+
+
+E2M1 = (0.0, 0.5, 1.0, 1.5, 2.0, 3.0, 4.0, 6.0)
+
+
+def quant_rows_mx4_ref(x: torch.Tensor):
+    """MX-fp4 image of 384-wide rows (index_i8.hip quant_rows_mx4): per 32-dim block the scale
+    2^ceil(log2(max|x| / 6)) (e8m0 byte e + 127), each element the nearest e2m1 value of x / s,
+    element 2j in the low nibble of byte j; block-scale bytes in a 16-byte record per row, dword g
+    = blocks g, 4 + g, 8 + g.  Returns (img uint8 [n, 192], scales uint8 [n, 16], decoded x~ f32
+    [n, 384], norms [n, 3] = (|x - x~|, |x~|, |x|))."""
+    xf = x.float()
+    n, d = xf.shape
+    assert d == 384
+    blk = xf.view(n, 12, 32)
+    amax = blk.abs().amax(-1)
+    _, k = torch.frexp(amax / 6.0)
+    e = k.clone()
+    e = torch.where(amax <= 6.0 * torch.ldexp(torch.ones_like(amax), k - 1), k - 1, e)
+    e = torch.where(amax > 6.0 * torch.ldexp(torch.ones_like(amax), e), e + 1, e)
+    e = torch.where(amax > 0, e, torch.full_like(e, -127)).clamp_(min=-127)
+    a = blk.abs() * torch.ldexp(torch.ones_like(amax), -e)[..., None]
+    q = torch.where(a < 2.0, torch.round(a * 2.0) * 0.5,
+                    torch.where(a < 4.0, torch.round(a), torch.where(a < 5.0, 4.0, 6.0)))
+    grid = torch.tensor(E2M1, dtype=torch.float32, device=xf.device)
+    code = (q[..., None] == grid).float().argmax(-1)
+    code = code | torch.where((blk < 0) & (code != 0), 8, 0)
+    xt = torch.where(blk < 0, -q, q) * torch.ldexp(torch.ones_like(amax), e)[..., None]
+    codes = code.view(n, d).to(torch.int32)
+    img = (codes[:, 0::2] | (codes[:, 1::2] << 4)).to(torch.uint8)
+    sc = torch.zeros(n, 16, dtype=torch.uint8, device=xf.device)
+    for b in range(12):
+        sc[:, 4 * (b & 3) + (b >> 2)] = (e[:, b] + 127).to(torch.uint8)
+    xt = xt.view(n, d)
+    norms = torch.stack([(xf - xt).norm(dim=1), xt.norm(dim=1), xf.norm(dim=1)], 1)
+    return img, sc, xt, norms
+
+
+def mx4_decode_ref(img: torch.Tensor, sc: torch.Tensor) -> torch.Tensor:
+    """Decoded f32 rows of an MX-fp4 image (quant_rows_mx4_ref's layout)."""
+    n = img.shape[0]
+    b = img.to(torch.int32)
+    codes = torch.stack([b & 15, b >> 4], -1).view(n, 384)
+    grid = torch.tensor(E2M1, dtype=torch.float32, device=img.device)
+    v = grid[codes & 7] * torch.where(codes & 8 != 0, -1.0, 1.0)
+    e = torch.stack([sc[:, 4 * (blk & 3) + (blk >> 2)].to(torch.int32) - 127
+                     for blk in range(12)], 1)
+    return (v.view(n, 12, 32) * torch.ldexp(torch.ones(n, 12, device=img.device), e)[..., None]).view(n, 384)

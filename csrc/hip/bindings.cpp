@@ -68,7 +68,14 @@ int symb_i8_queries_per_blk(int rsplit);
 int symb_index_scan_i8(const void* X8, const float* sx, int n_valid, int alloc_rows,
                        int rows_per_blk, int n_rblk, const void* Q8, int NQ, const float* thr,
                        float* cand_s, int* cand_i, int* cand_n, int cap, int xcd, hipStream_t st,
-                       int rsplit, const int* skip, int dim, int heavy, const float* sq);
+                       int rsplit, const int* skip, int dim, int heavy, const float* sq, int form,
+                       const int* gate, int gate_want);
+int symb_quant_rows_mx4(const void* X, int n, int dim, void* X4, void* SC, float* bounds,
+                        float* margin, hipStream_t st);
+int symb_mx4_select(int NQ, const float* T, const float* margin4, const float* thr0,
+                    const float* cs_p, const int* cnt_p, int cap_p, int tshift,
+                    const float* tail_cs, int tail_cap, float limit, float* thr4, int* nv,
+                    hipStream_t st);
 int symb_i8_tile_rows_for(int dim, int heavy);
 int symb_i8_split_queries_per_blk(int rsplit);
 int symb_i8_pair_config(int pair);
@@ -434,18 +441,35 @@ PYBIND11_MODULE(_hip, m) {
   m.def("index_scan_i8", [](uptr X8, uptr sx, int n_valid, int alloc_rows, int rows_per_blk,
                             int n_rblk, uptr Q8, int NQ, uptr thr, uptr cand_s, uptr cand_i,
                             uptr cand_n, int cap, int xcd, uptr st, int rsplit, uptr skip, int dim,
-                            int heavy, uptr sq) {
+                            int heavy, uptr sq, int form, uptr gate, int gate_want) {
     check(symb_index_scan_i8(P<void>(X8), P<const float>(sx), n_valid, alloc_rows, rows_per_blk,
                              n_rblk,
                              P<void>(Q8), NQ, P<const float>(thr), P<float>(cand_s), P<int>(cand_i),
                              P<int>(cand_n), cap, xcd, S(st), rsplit, P<const int>(skip), dim,
-                             heavy, P<const float>(sq)),
+                             heavy, P<const float>(sq), form, P<const int>(gate), gate_want),
           "index_scan_i8");
   }, py::arg("X8"), py::arg("sx"), py::arg("n_valid"), py::arg("alloc_rows"),
      py::arg("rows_per_blk"), py::arg("n_rblk"), py::arg("Q8"), py::arg("NQ"), py::arg("thr"),
      py::arg("cand_s"), py::arg("cand_i"), py::arg("cand_n"), py::arg("cap"), py::arg("xcd"),
      py::arg("stream"), py::arg("rsplit"), py::arg("skip") = 0, py::arg("dim") = 384,
-     py::arg("heavy") = 0, py::arg("sq") = 0);
+     py::arg("heavy") = 0, py::arg("sq") = 0, py::arg("form") = 0, py::arg("gate") = 0,
+     py::arg("gate_want") = 0);
+  m.def("quant_rows_mx4", [](uptr X, int n, int dim, uptr X4, uptr SC, uptr bounds, uptr margin,
+                             uptr st) {
+    check(symb_quant_rows_mx4(P<void>(X), n, dim, P<void>(X4), P<void>(SC), P<float>(bounds),
+                              P<float>(margin), S(st)),
+          "quant_rows_mx4");
+  }, py::arg("X"), py::arg("n"), py::arg("dim"), py::arg("X4"), py::arg("SC"), py::arg("bounds"),
+     py::arg("margin"), py::arg("stream"));
+  m.def("mx4_select", [](int NQ, uptr T, uptr margin4, uptr thr0, uptr cs_p, uptr cnt_p, int cap_p,
+                         int tshift, uptr tail_cs, int tail_cap, float limit, uptr thr4, uptr nv,
+                         uptr st) {
+    check(symb_mx4_select(NQ, P<const float>(T), P<const float>(margin4), P<const float>(thr0),
+                          P<const float>(cs_p), P<const int>(cnt_p), cap_p, tshift,
+                          P<const float>(tail_cs), tail_cap, limit, P<float>(thr4), P<int>(nv),
+                          S(st)),
+          "mx4_select");
+  });
   m.def("prune_qquant", [](uptr Q, int NQ, int dim, uptr bounds, uptr Q8, uptr sq, uptr margin,
                            uptr st) {
     check(symb_prune_qquant(P<void>(Q), NQ, dim, P<const float>(bounds), P<void>(Q8), P<float>(sq),

@@ -49,13 +49,18 @@ constexpr int PIECE = 1024;
 // HK > 0: the SPLIT image (see "split image" below): the first 32 * HK dims of each (rotated) row
 // as fp16, HK v_mfma_f32_16x16x32_f16 k-steps of 64 bytes, then the other D - 32 * HK dims as
 // int8 -- RB = 448 bytes per 384-wide row.  Only the fused two-sub-tile chains run it.
+// HK = MX4 (4): the MX-fp4 image (see "MX-fp4 image" below): every 32-dim block of a row as OCP
+// e2m1 nibbles with a power-of-two block scale, 3 v_mfma_scale_f32_16x16x128_f8f6f4 k-steps of 64
+// bytes -- RB = 192 bytes per 384-wide row, plus 16 bytes of block scales in a side array.
+constexpr int MX4 = 4;
 template <int D, int HK = 0> struct I8Dim {
-  static constexpr int NKS = (D + 32 * HK) / 64;
+  static constexpr int NKS = HK == MX4 ? D / 128 : (D + 32 * HK) / 64;
   static constexpr int RB = NKS * 64;            // image bytes per row
   static constexpr int PF = HK ? NKS - 1 : (D == 384 ? SYMB_I8_PF : 3);
   static constexpr int R = PF + 1;
   static_assert(D == 384 || D == 768, "int8 scan row width");
-  static_assert(HK == 0 || (D == 384 && HK == 2), "split image: 64 fp16 + 320 int8 dims");
+  static_assert(HK == 0 || (D == 384 && (HK == 2 || HK == MX4)),
+                "split image: 64 fp16 + 320 int8 dims; MX-fp4 image: 384 dims");
   static_assert(NKS % R == 0, "cross-chain prefetch: fragment j of the next chain uses slot j % R");
 };
 
@@ -78,10 +83,12 @@ template <int D, int TR_, int WV_ = 8, int HK = 0> struct Geo {
   static constexpr int FULLW = PIECES % WV ? PIECES % WV : WV;   // waves carrying LOADS (rest: - 1)
   static constexpr int DMA_EVERY = NKS / LOADS;               // k-steps between pieces
   static constexpr int SCW = TR / 64;                         // waves carrying a scale DMA
-  static constexpr int SC_BYTES = TR * 4;
+  static constexpr int SC_BYTES = TR * (HK == MX4 ? 16 : 4);   // row scales (MX4: block scales)
   static constexpr int STW = WV == 4 ? 160 : (TR == 64 ? 192 : 128);   // staged candidates per wave
   static constexpr int STAGE_BYTES = STW * 10;
+  // (MX4: 12 KiB tiles, an 8-deep ring keeps ~84 KiB in flight like the int8 5-deep ring)
   static constexpr int NS = WV == 4 ? 3
+                            : HK == MX4 ? 8
                             : (TILE_BYTES <= 24 * 1024 ||
                                (HK && 5 * (TILE_BYTES + SC_BYTES) + WV * STAGE_BYTES <= 160 * 1024))
                                 ? 5 : 3;
@@ -119,6 +126,29 @@ __device__ __forceinline__ void h16_mfma(f32x4& acc, const i32x4& a, const i32x4
     asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "=&v"(acc) : "v"(a), "v"(q));
   else
     asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(q));
+}
+
+// the MX-fp4 image's k-steps: 16x16x128 with e2m1 A and B (cbsz / blgp 4: 16 bytes per lane, the
+// int8 layout), each lane's 32 elements one scale block; the e8m0 block scales of k-step KS are
+// byte KS of the lane's row-scale (rs) and query-scale (qs) dwords (op_sel / op_sel_hi pick it)
+template <int KS, bool FIRST>
+__device__ __forceinline__ void mx4_mfma(f32x4& acc, const i32x4& a, const i32x4& q, float rs,
+                                         float qs) {
+  if constexpr (FIRST) {
+    static_assert(KS == 0, "the first k-step zero-initialises");
+    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, 0, %3, %4 op_sel_hi:[0,0,0] cbsz:4 blgp:4"
+                 : "=&v"(acc) : "v"(a), "v"(q), "v"(rs), "v"(qs));
+  } else if constexpr (KS == 0) {
+    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel_hi:[0,0,0] cbsz:4 blgp:4"
+                 : "+v"(acc) : "v"(a), "v"(q), "v"(rs), "v"(qs));
+  } else if constexpr (KS == 1) {
+    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel:[1,1,0] op_sel_hi:[0,0,0] cbsz:4 blgp:4"
+                 : "+v"(acc) : "v"(a), "v"(q), "v"(rs), "v"(qs));
+  } else {
+    static_assert(KS == 2, "three k-steps per 384-wide row");
+    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel:[0,0,0] op_sel_hi:[1,1,0] cbsz:4 blgp:4"
+                 : "+v"(acc) : "v"(a), "v"(q), "v"(rs), "v"(qs));
+  }
 }
 
 // k-step KS of one 16-row sub-tile (index_mq.hip MqChain, int8 operands).
@@ -171,7 +201,8 @@ struct I8Chain2 {
                                              f32x4 (&accf)[HK ? 2 : 1][i8s::SETS],
                                              i32x4 (&a)[i8s::R2][2],
                                              const i32x4 (&qf)[i8s::SETS][NKS],
-                                             uint32_t base, const Dma& dma, f32x4& t0, f32x4& t1) {
+                                             uint32_t base, const Dma& dma, f32x4& t0, f32x4& t1,
+                                             const float (&qsc)[i8s::SETS]) {
     using namespace i8s;
     if constexpr (DMA_PIECES > 0 && KS % DE == 0 && KS / DE < DMA_PIECES) dma(KS / DE);
     constexpr int steps = (NKS - KS < PF2) ? (NKS - KS) : PF2;   // k-steps in flight, this one too
@@ -183,7 +214,9 @@ struct I8Chain2 {
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int s = 0; s < SETS; ++s) {
-        if constexpr (KS < HK)
+        if constexpr (HK == MX4)   // (t0 / t1 .x: the two sub-tiles' row block-scale dwords)
+          mx4_mfma<KS, KS == 0>(accf[c][s], a[KS % R2][c], qf[s][KS], c ? t1[0] : t0[0], qsc[s]);
+        else if constexpr (KS < HK)
           h16_mfma<KS == 0>(accf[c][s], a[KS % R2][c], qf[s][KS]);
         else
           i8_mfma<KS == HK>(acc[c][s], a[KS % R2][c], qf[s][KS]);
@@ -194,7 +227,7 @@ struct I8Chain2 {
       i8_read16<(KS + PF2) * PIECE + NKS * PIECE>(a[(KS + PF2) % R2][1], base);
     }
     if constexpr (KS + 1 < NKS)
-      I8Chain2<D, KS + 1, DMA_PIECES, DE, HK>::run(acc, accf, a, qf, base, dma, t0, t1);
+      I8Chain2<D, KS + 1, DMA_PIECES, DE, HK>::run(acc, accf, a, qf, base, dma, t0, t1, qsc);
   }
 };
 template <int D, int J, int HK = 0>
@@ -234,12 +267,20 @@ __device__ __forceinline__ const char* i8_uniform(const char* p) {
 // (profiles/r4_split/pair/): headline 11.10-11.19 vs 11.20 ms, anisotropic 13.19-13.20 vs
 // 13.21-13.25, random held-out 11.86 vs 11.03-11.05 (its busy band pays both tests): the
 // emission pre-test is not what bounds the scan, so the pair test stays an A/B knob.
+//
+// HK = MX4 (the MX-fp4 image, index/shard.py, the first tier of a batch whose k-th scores sit far
+// above the corpus bulk): X8 = [rows][192] e2m1 nibbles, sx = [rows][16] bytes of e8m0 block
+// scales (dword g = the scales of blocks g, 4 + g, 8 + g), Q8 / sq_in likewise for the queries.
+// The MFMA applies the scales, so acc_f is the approximate score itself: emit iff acc_f >= thr
+// (thr = T - margin in score units, the bound of quant_rows_mx4).
+// gate (optional): the kernel runs only if *gate == gate_want (the device-side tier choice).
 template <int D, int RSPLIT, int ABL = 0, int TRK = 64, int WV = 8, int HK = 0, bool PAIR = true>
 __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
     const int8_t* __restrict__ X8, const float* __restrict__ sx, int n_valid, int rows_per_blk,
     const int8_t* __restrict__ Q8, int NQ, int n_qblk, int xcd, const float* __restrict__ thr_in,
     float* __restrict__ cand_s, int* __restrict__ cand_i, int* __restrict__ cand_n, int cap,
-    const int* __restrict__ skip, const float* __restrict__ sq_in) {
+    const int* __restrict__ skip, const float* __restrict__ sq_in, const int* __restrict__ gate,
+    int gate_want) {
   using namespace i8s;
   using G = Geo<D, TRK, WV, HK>;
   constexpr int NKS = G::NKS, RB = G::RB;
@@ -258,6 +299,7 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
   // block to the bf16 emitting scan -- the workgroup returns at once (workgroup-uniform, before
   // any barrier)
   if (skip != nullptr && skip[rb] != 0) return;
+  if (gate != nullptr && *gate != gate_want) return;
   const int row_begin = rb * rows_per_blk;
   const int row_end = min(row_begin + rows_per_blk, n_valid);
   const int n_tiles = row_end > row_begin ? (row_end - row_begin + TR - 1) / TR : 0;
@@ -268,7 +310,8 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
   const int qbase = qb * QPB + qwave * QW + (lane & 15);
   i32x4 qf[SETS][NKS];
   float thr[SETS];
-  float rsq[SETS];   // (split image) 1 / the query's int8 scale: acc_f is in score units
+  float rsq[SETS];   // split image: 1 / the query's int8 scale (acc_f is in score units);
+                     // MX4: the lane's query block-scale dword (its bits, as a float register)
 #pragma unroll
   for (int s = 0; s < SETS; ++s) {
     const int q = qbase + s * 16;
@@ -276,7 +319,10 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) qf[s][ks] = *reinterpret_cast<const i32x4*>(qp + ks * 64);
     thr[s] = q < NQ ? thr_in[q] : INFINITY;
-    if constexpr (HK > 0) rsq[s] = 1.f / sq_in[min(q, NQ - 1)];
+    if constexpr (HK == MX4)
+      rsq[s] = sq_in[(size_t)min(q, NQ - 1) * 4 + (lane >> 4)];
+    else if constexpr (HK > 0)
+      rsq[s] = 1.f / sq_in[min(q, NQ - 1)];
   }
 #pragma unroll
   for (int s = 0; s < SETS; ++s) {
@@ -298,11 +344,18 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
     // (split image: the last round of pieces covers waves < FULLW only; wave-uniform)
     if (G::FULLW == WV || p < G::PIECES)
       glds16_aux<0>(i8_uniform(base) + loff, smem + (t % NS) * TILE_BYTES + p * PIECE);
-    if (wave_u < G::SCW && i == 0)   // 64 row scales per scale wave
+    if constexpr (HK == MX4) {   // 64 rows x 16 bytes of block scales per scale wave
+      if (wave_u < G::SCW && i == 0)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(sx + (size_t)(prow + 64 * wave_u + lane) * 4),
+            (__attribute__((address_space(3))) void*)(scl + (t % NS) * SC_BYTES + 1024 * wave_u),
+            16, 0, 0);
+    } else if (wave_u < G::SCW && i == 0) {   // 64 row scales per scale wave
       __builtin_amdgcn_global_load_lds(
           (const __attribute__((address_space(1))) void*)(sx + prow + 64 * wave_u + lane),
           (__attribute__((address_space(3))) void*)(scl + (t % NS) * SC_BYTES + 256 * wave_u), 4,
           0, 0);
+    }
   };
   const uint32_t lds_smem = lds_addr(smem);
   const uint32_t foff = (uint32_t)((lane & 15) * 64 + (((lane >> 4) ^ ((lane >> 1) & 2)) * 16));
@@ -339,7 +392,7 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
   auto fence_acc = [&](i32x4 (&acc)[SETS], auto& af) {
 #pragma unroll
     for (int s = 0; s < SETS; ++s) {
-      asm volatile("" : "+v"(acc[s]));
+      if constexpr (HK != MX4) asm volatile("" : "+v"(acc[s]));   // (MX4: no int accumulators)
       if constexpr (HK > 0) asm volatile("" : "+v"(af[s]));
     }
   };
@@ -357,7 +410,9 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
       float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        if constexpr (HK > 0)
+        if constexpr (HK == MX4)
+          v[r] = rl + r < row_end ? af[s][r] : -INFINITY;
+        else if constexpr (HK > 0)
           v[r] = rl + r < row_end ? fmaf((float)acc[s][r], s4[r], af[s][r] * rsq[s]) : -INFINITY;
         else
           v[r] = rl + r < row_end ? (float)acc[s][r] * s4[r] : -INFINITY;
@@ -426,7 +481,7 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
       return;
     }
     bool hs[SETS];
-    if constexpr (!PAIR) {   // (A/B: the per-sub-tile pre-tests alone)
+    if constexpr (!PAIR || HK == MX4) {   // (A/B: the per-sub-tile pre-tests alone)
 #pragma unroll
       for (int s = 0; s < SETS; ++s) hs[s] = true;
     } else {
@@ -475,6 +530,14 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
       bool any = false;
 #pragma unroll
       for (int s = 0; s < SETS; ++s) {
+        if constexpr (HK == MX4) {   // the accumulator is the estimate: its max against thr
+          float fm;
+          asm volatile("v_max3_f32 %0, %1, %2, %3\n\tv_max3_f32 %0, %0, %4, %4"
+                       : "=&v"(fm) : "v"(afc[s][0]), "v"(afc[s][1]), "v"(afc[s][2]), "v"(afc[s][3]));
+          hc[s] = hs[s] && fm >= thr[s];
+          any |= hc[s];
+          continue;
+        }
         int im;
         asm volatile("v_max3_i32 %0, %1, %2, %3\n\tv_max3_i32 %0, %0, %4, %4"
                      : "=&v"(im) : "v"(ac[s][0]), "v"(ac[s][1]), "v"(ac[s][2]), "v"(ac[s][3]));
@@ -559,7 +622,17 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
         const uint32_t fg = fw + g * 2 * NKS * PIECE;
         const int jg = j0 + 2 * g;
         f32x4 sa, sb;   // this lane's row scales of sub-tiles jg, jg + 1
-        {
+        if constexpr (HK == MX4) {
+          // the block-scale dword of the lane's A row (lane & 15) and k-group (lane >> 4), both
+          // sub-tiles (.x; the rest unused)
+          float a0, b0;
+          const uint32_t sp = lds_addr(scl) +
+                              (uint32_t)(slot * SC_BYTES + (jg * SUB + (lane & 15)) * 16 + 4 * (lane >> 4));
+          asm volatile("ds_read_b32 %0, %1" : "=v"(a0) : "v"(sp));
+          asm volatile("ds_read_b32 %0, %1 offset:256" : "=v"(b0) : "v"(sp));
+          sa = f32x4{a0, 0.f, 0.f, 0.f};
+          sb = f32x4{b0, 0.f, 0.f, 0.f};
+        } else {
           const uint32_t sp = lds_addr(scl) + (uint32_t)(slot * SC_BYTES + (jg * SUB + 4 * (lane >> 4)) * 4);
           asm volatile("ds_read_b128 %0, %1" : "=v"(sa) : "v"(sp));
           asm volatile("ds_read_b128 %0, %1 offset:64" : "=v"(sb) : "v"(sp));
@@ -571,9 +644,9 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
           emit2(acc2, accf2, row0 - TR + last - SUB, s4_prev, s4_last);
         }
         if (g == 0)
-          I8Chain2<D, 0, LOADS, G::DMA_EVERY, HK>::run(acc2, accf2, a2, qf, fg, dma, sa, sb);
+          I8Chain2<D, 0, LOADS, G::DMA_EVERY, HK>::run(acc2, accf2, a2, qf, fg, dma, sa, sb, rsq);
         else
-          I8Chain2<D, 0, 0, G::DMA_EVERY, HK>::run(acc2, accf2, a2, qf, fg, NoDma(), sa, sb);
+          I8Chain2<D, 0, 0, G::DMA_EVERY, HK>::run(acc2, accf2, a2, qf, fg, NoDma(), sa, sb, rsq);
         if (g + 1 < NG || !late) {
           emit2(acc2, accf2, row0 + jg * SUB, sa, sb);
         } else {
@@ -954,6 +1027,138 @@ __global__ __launch_bounds__(256) void quant_rows_split_kernel(const float* __re
   }
 }
 
+// MX-fp4 image of bf16 rows (index_scan_i8_kernel HK = MX4): every 32-dim block b gets the
+// power-of-two scale s_b = 2^ceil(log2(max |x_b| / 6)) (so |x| / s_b <= 6: no clamping) as an e8m0
+// byte, and each element the nearest OCP e2m1 value of x / s_b (0, .5, 1, 1.5, 2, 3, 4, 6; sign in
+// bit 3), two per byte, element 2j in the low nibble of byte j.  Block-scale bytes go to a
+// 16-byte side record per row, dword g = blocks g, 4 + g, 8 + g (the scan's per-lane operand).
+// One wave per row: lane l holds dims l + 64 m (m < 6), so dims of block 2 m + (l >> 5) sit in
+// one half-wave.
+//   rows    (margin == nullptr): bounds[0..1] raised to (max |x - x~|, max |x~|) -- E4, X4;
+//   queries (margin != nullptr): margin = |q| E4 + |q - q~| X4 + 1e-5 from bounds.
+__device__ __forceinline__ float half_max(float v) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ int e2m1_code(float a, float& q) {   // a = |x| / s <= 6
+  int c;
+  if (a < 2.f) {
+    q = rintf(a * 2.f) * 0.5f;
+    c = (int)(q * 2.f);          // 0 .. 4 -> 0, .5, 1, 1.5, 2
+  } else if (a < 4.f) {
+    q = rintf(a);                // 2, 3, 4
+    c = q == 2.f ? 4 : q == 3.f ? 5 : 6;
+  } else {
+    q = a < 5.f ? 4.f : 6.f;
+    c = q == 4.f ? 6 : 7;
+  }
+  return c;
+}
+template <int D>
+__global__ __launch_bounds__(256) void quant_rows_mx4_kernel(const __bf16* __restrict__ X, int n,
+                                                             uint8_t* __restrict__ X4,
+                                                             uint8_t* __restrict__ SC,
+                                                             float* __restrict__ bounds,
+                                                             float* __restrict__ margin) {
+  static_assert(D == 384, "12 blocks of 32 dims");
+  constexpr int M = D / 64;
+  __shared__ float red[2][4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int row = blockIdx.x * 4 + w;
+  const bool rows = margin == nullptr;
+  if (row >= n) {   // (block-uniform barrier below: idle waves report zeros)
+    if (rows && bounds) {
+      if (lane < 2) red[lane][w] = 0.f;
+      __syncthreads();
+    }
+    return;
+  }
+  const uint16_t* xp = reinterpret_cast<const uint16_t*>(X + (size_t)row * D);
+  uint8_t* op = X4 + (size_t)row * (D / 2);
+  uint8_t* sp = SC + (size_t)row * 16;
+  float e2 = 0.f, n2 = 0.f, x2 = 0.f;
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const float x = __uint_as_float((uint32_t)xp[lane + 64 * m] << 16);
+    const float amax = half_max(fabsf(x));
+    int e = -127;
+    if (amax > 0.f) {
+      int k;
+      frexpf(amax / 6.f, &k);              // amax / 6 in [2^(k-1), 2^k)
+      e = k;
+      if (amax <= 6.f * ldexpf(1.f, k - 1)) e = k - 1;
+      if (amax > 6.f * ldexpf(1.f, e)) ++e;   // (guard the division's rounding)
+      e = max(e, -127);
+    }
+    const float sc = ldexpf(1.f, e);
+    float q;
+    const int c = amax > 0.f ? e2m1_code(fabsf(x) * ldexpf(1.f, -e), q) : (q = 0.f, 0);
+    const int code = c | (x < 0.f && c ? 8 : 0);
+    const float xt = (x < 0.f ? -q : q) * sc;
+    e2 += (x - xt) * (x - xt);
+    n2 += xt * xt;
+    x2 += x * x;
+    const int hi = __shfl_down(code, 1);
+    if ((lane & 1) == 0) op[(lane >> 1) + 32 * m] = (uint8_t)(code | (hi << 4));
+    if ((lane & 31) == 0) {
+      const int b = 2 * m + (lane >> 5);
+      sp[4 * (b & 3) + (b >> 2)] = (uint8_t)(e + 127);
+    }
+  }
+  if (lane < 4) sp[4 * lane + 3] = 0;
+  const float en = sqrtf(wave_sum(e2)), nn = sqrtf(wave_sum(n2)), xn = sqrtf(wave_sum(x2));
+  if (!rows) {
+    if (lane == 0) margin[row] = xn * bounds[0] + en * bounds[1] + 1e-5f;
+    return;
+  }
+  if (lane == 0) {
+    red[0][w] = en;
+    red[1][w] = nn;
+  }
+  if (bounds) {
+    __syncthreads();
+    if (threadIdx.x < 2) {
+      const float mx = fmaxf(fmaxf(red[threadIdx.x][0], red[threadIdx.x][1]),
+                             fmaxf(red[threadIdx.x][2], red[threadIdx.x][3]));
+      atomicMax(reinterpret_cast<int*>(bounds) + threadIdx.x, __float_as_int(mx));
+    }
+  }
+}
+
+// The first tier's choice (after prune_route, from the same exact sample): the MX-fp4 scan is
+// viable for the batch iff for EVERY query the band T - margin4 lies at or above the sample's
+// seed threshold thr0 (so the sample emitted every row of it) and the band's estimated
+// population, (sample rows >= band) << tshift + dense tail rows >= band, is at most `limit`.
+// *nv ends 1 (not viable: the int8 tier runs) or stays 0 (the MX-fp4 tier runs, at thr4 = band).
+__global__ __launch_bounds__(256) void mx4_select_kernel(
+    int NQ, const float* __restrict__ T, const float* __restrict__ margin4,
+    const float* __restrict__ thr0, const float* __restrict__ cs_p, const int* __restrict__ cnt_p,
+    int cap_p, int tshift, const float* __restrict__ tail_cs, int tail_cap, float limit,
+    float* __restrict__ thr4, int* __restrict__ nv) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int q = blockIdx.x * 4 + w;
+  if (q >= NQ) return;
+  const float band = T[q] - margin4[q];
+  const int cnt = cnt_p[q];
+  float c = 0.f;
+  const float* cs = cs_p + (size_t)q * cap_p;
+  for (int i = lane; i < min(cnt, cap_p); i += 64) c += cs[i] >= band ? 1.f : 0.f;
+  float tc = 0.f;
+  if (tail_cs != nullptr) {
+    const float* tcs = tail_cs + (size_t)q * tail_cap;
+    for (int i = lane; i < tail_cap; i += 64) tc += tcs[i] >= band ? 1.f : 0.f;
+  }
+  c = wave_sum(c);
+  tc = wave_sum(tc);
+  if (lane == 0) {
+    thr4[q] = band;
+    const bool ok = band >= thr0[q] && cnt <= cap_p && tail_cs != nullptr &&
+                    c * (float)(1 << tshift) + tc <= limit;
+    if (!ok) atomicOr(nv, 1);
+  }
+}
+
 constexpr int ROUTE_MAX_BLOCKS = 1024;   // int8 row blocks the per-block route can bin
 
 // The exact tail scan's candidates (rows >= thr0 of the fresh rows [off, n), ids relative to
@@ -1132,7 +1337,7 @@ template <int D, int RSPLIT, int TRK, int WV = 8, int HK = 0>
 static int launch_i8(const void* X8, const float* sx, int n_valid, int rows_per_blk, int n_rblk,
                      const void* Q8, int NQ, const float* thr, float* cand_s, int* cand_i,
                      int* cand_n, int cap, int xcd, hipStream_t st, const int* skip,
-                     const float* sq = nullptr) {
+                     const float* sq = nullptr, const int* gate = nullptr, int gate_want = 0) {
   constexpr int qpb = WV / RSPLIT * 16 * i8s::SETS;
   const int n_qblk = (NQ + qpb - 1) / qpb;
   constexpr int lds = Geo<D, TRK, WV, HK>::LDS_BYTES;
@@ -1140,7 +1345,7 @@ static int launch_i8(const void* X8, const float* sx, int n_valid, int rows_per_
     set_max_lds<decltype(kern)::value>(lds);
     hipLaunchKernelGGL(decltype(kern)::value, dim3(n_rblk * n_qblk), dim3(64 * WV), lds, st,
                        (const int8_t*)X8, sx, n_valid, rows_per_blk, (const int8_t*)Q8, NQ, n_qblk,
-                       xcd, thr, cand_s, cand_i, cand_n, cap, skip, sq);
+                       xcd, thr, cand_s, cand_i, cand_n, cap, skip, sq, gate, gate_want);
     return (int)hipGetLastError();
   };
   if (g_i8_pair)
@@ -1159,32 +1364,47 @@ int symb_i8_split_queries_per_blk(int rsplit) { return i8s::WAVES / rsplit * 16 
 // rows, which must cover n_valid rounded up to a whole tile (the DMA reads whole tiles).
 // rsplit 2 = 256 queries per workgroup, 1 = 512.  dim: 384 or 768.  heavy = 64: the split image
 // (448-byte rows and queries, quant_rows_split), sq = the queries' int8 scales; 0: plain int8.
+// form: 0 = plain int8 (heavy 0) or split (heavy 64); 1 = the MX-fp4 image (sx = the rows'
+// block scales, sq = the queries'; quant_rows_mx4).  gate / gate_want: the launch runs only if
+// *gate == gate_want (nullptr: always); cand_n is zeroed only by an ungated launch.
 int symb_index_scan_i8(const void* X8, const float* sx, int n_valid, int alloc_rows,
                        int rows_per_blk, int n_rblk, const void* Q8, int NQ, const float* thr,
                        float* cand_s, int* cand_i, int* cand_n, int cap, int xcd, hipStream_t st,
-                       int rsplit, const int* skip, int dim, int heavy, const float* sq) {
+                       int rsplit, const int* skip, int dim, int heavy, const float* sq, int form,
+                       const int* gate, int gate_want) {
   if (NQ <= 0) return 0;
   if (dim != 384 && dim != 768) return -1;
   if (heavy != 0 && (heavy != 64 || dim != 384 || sq == nullptr)) return -1;
-  const int tr = symb_i8_tile_rows_for(dim, heavy);
+  if (form != 0 && (form != 1 || heavy != 0 || dim != 384 || sq == nullptr)) return -1;
+  const int tr = form ? 64 : symb_i8_tile_rows_for(dim, heavy);
   if (rows_per_blk % tr || n_rblk <= 0 || thr == nullptr || cap <= 0 || n_valid <= 0) return -1;
   if ((long long)n_rblk * rows_per_blk < n_valid) return -1;
   if ((long long)(n_valid + tr - 1) / tr * tr > alloc_rows) return -1;   // a tile past the buffer
-  hipError_t e = hipMemsetAsync(cand_n, 0, sizeof(int) * (size_t)NQ, st);
-  if (e != hipSuccess) return (int)e;
+  if (gate == nullptr) {
+    hipError_t e = hipMemsetAsync(cand_n, 0, sizeof(int) * (size_t)NQ, st);
+    if (e != hipSuccess) return (int)e;
+  }
 #define SYMB_I8(D_, RS, T) launch_i8<D_, RS, T>(X8, sx, n_valid, rows_per_blk, n_rblk, Q8, NQ, thr, \
-                                                cand_s, cand_i, cand_n, cap, xcd, st, skip)
+                                                cand_s, cand_i, cand_n, cap, xcd, st, skip,       \
+                                                nullptr, gate, gate_want)
+  if (form)
+    return rsplit == 2 ? launch_i8<384, 2, 64, 8, MX4>(X8, sx, n_valid, rows_per_blk, n_rblk, Q8,
+                                                       NQ, thr, cand_s, cand_i, cand_n, cap, xcd,
+                                                       st, skip, sq, gate, gate_want)
+                       : launch_i8<384, 1, 64, 8, MX4>(X8, sx, n_valid, rows_per_blk, n_rblk, Q8,
+                                                       NQ, thr, cand_s, cand_i, cand_n, cap, xcd,
+                                                       st, skip, sq, gate, gate_want);
   if (heavy)
     return rsplit == 2 ? launch_i8<384, 2, 64, 8, 2>(X8, sx, n_valid, rows_per_blk, n_rblk, Q8, NQ,
                                                      thr, cand_s, cand_i, cand_n, cap, xcd, st,
-                                                     skip, sq)
+                                                     skip, sq, gate, gate_want)
                        : launch_i8<384, 1, 64, 8, 2>(X8, sx, n_valid, rows_per_blk, n_rblk, Q8, NQ,
                                                      thr, cand_s, cand_i, cand_n, cap, xcd, st,
-                                                     skip, sq);
+                                                     skip, sq, gate, gate_want);
   if (dim == 768) return rsplit == 2 ? SYMB_I8(768, 2, 64) : SYMB_I8(768, 1, 64);
   if (g_i8_waves == 4)
     return launch_i8<384, 1, 64, 4>(X8, sx, n_valid, rows_per_blk, n_rblk, Q8, NQ, thr, cand_s,
-                                    cand_i, cand_n, cap, xcd, st, skip);
+                                    cand_i, cand_n, cap, xcd, st, skip, nullptr, gate, gate_want);
   if (rsplit == 2) return tr == 128 ? SYMB_I8(384, 2, 128) : SYMB_I8(384, 2, 64);
   // 512 queries per workgroup always run 64-row tiles: the 128-row form (four fused two-sub-tile
   // chains per wave per tile) emitted a few rows per million with wrong scores, differently from
@@ -1216,7 +1436,8 @@ int symb_index_scan_i8_ablate(const void* X8, const float* sx, int n_valid, int 
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipLaunchKernelGGL(kern, dim3(n_rblk * n_qblk), dim3(w4 ? 256 : 512), lds, st, (const int8_t*)X8, sx,
                        n_valid, rows_per_blk, (const int8_t*)Q8, NQ, n_qblk, xcd, thr, cand_s,
-                       cand_i, cand_n, cap, (const int*)nullptr, (const float*)nullptr);
+                       cand_i, cand_n, cap, (const int*)nullptr, (const float*)nullptr,
+                       (const int*)nullptr, 0);
     return (int)hipGetLastError();
   };
   if (w4) {
@@ -1287,6 +1508,30 @@ int symb_quant_rows_split(const float* X, int n, int dim, void* X8, float* sx, f
   if (dim != 384 || bounds == nullptr) return -1;
   hipLaunchKernelGGL((quant_rows_split_kernel<384, 64>), dim3((n + 3) / 4), dim3(256), 0, st, X, n,
                      (int8_t*)X8, sx, bounds, margin);
+  return (int)hipGetLastError();
+}
+
+// MX-fp4 image of bf16 rows / queries (quant_rows_mx4_kernel): X4 = [n][D / 2], SC = [n][16].
+int symb_quant_rows_mx4(const void* X, int n, int dim, void* X4, void* SC, float* bounds,
+                        float* margin, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (dim != 384 || bounds == nullptr) return -1;
+  hipLaunchKernelGGL(quant_rows_mx4_kernel<384>, dim3((n + 3) / 4), dim3(256), 0, st,
+                     (const __bf16*)X, n, (uint8_t*)X4, (uint8_t*)SC, bounds, margin);
+  return (int)hipGetLastError();
+}
+
+// The MX-fp4 tier choice (mx4_select_kernel); nv (one int) is zeroed here.
+int symb_mx4_select(int NQ, const float* T, const float* margin4, const float* thr0,
+                    const float* cs_p, const int* cnt_p, int cap_p, int tshift,
+                    const float* tail_cs, int tail_cap, float limit, float* thr4, int* nv,
+                    hipStream_t st) {
+  if (NQ <= 0) return 0;
+  if (cap_p <= 0 || tshift < 0 || tshift > 20) return -1;
+  hipError_t e = hipMemsetAsync(nv, 0, sizeof(int), st);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(mx4_select_kernel, dim3((NQ + 3) / 4), dim3(256), 0, st, NQ, T, margin4, thr0,
+                     cs_p, cnt_p, cap_p, tshift, tail_cs, tail_cap, limit, thr4, nv);
   return (int)hipGetLastError();
 }
 

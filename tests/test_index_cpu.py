@@ -534,3 +534,30 @@ def test_split_image_bound_holds_and_prunes_anisotropic_rows():
     r.append_f32(torch.randn(5000, 384, generator=torch.Generator().manual_seed(2)))
     r.calibrate_prune()
     assert r._i8_heavy == 0 and r.calib_share < 0.3 and r.rows_i8.shape[1] == 384
+
+
+def test_mx4_image_follows_writes_and_bounds_every_pair():
+    """The MX-fp4 first-tier image (e2m1 nibbles + e8m0 block scales) follows appends and
+    scattered overwrites, its (E4, X4) cover every row written, and |q.x - q~.x~| stays within
+    |q| E4 + |q - q~| X4 for every (query, row) pair."""
+    from codename_symbiont_amd.ops.reference import mx4_decode_ref, quant_rows_mx4_ref
+
+    g = torch.Generator().manual_seed(9)
+    sh = HbmIndexShard(384, 3000, device="cpu", prune="i8")
+    sh.append_f32(torch.randn(2000, 384, generator=g))
+    sh.upsert(["a", "b"], torch.randn(2, 384, generator=g), [Payload("da"), Payload("db")])
+    sh.write_rows_f32([3, 100, 1999], torch.randn(3, 384, generator=g))
+    n = sh.count
+    img, sc, xt, nr = quant_rows_mx4_ref(sh.rows[:n])
+    assert torch.equal(sh.rows_mx4[:n], img) and torch.equal(sh.sc_mx4[:n], sc)
+    assert torch.equal(mx4_decode_ref(img, sc), xt)
+    E4, X4 = sh.mx4_bounds.tolist()
+    assert E4 >= float(nr[:, 0].max()) - 1e-7 and X4 >= float(nr[:, 1].max()) - 1e-7
+    q = torch.nn.functional.normalize(torch.randn(32, 384, generator=g), dim=-1).bfloat16()
+    q4 = torch.empty(32, 192, dtype=torch.uint8)
+    qs4 = torch.empty(32, 16, dtype=torch.uint8)
+    m4 = torch.empty(32)
+    sh._mx4_image(q, q4, qs4, sh.mx4_bounds, margin=m4)
+    est = mx4_decode_ref(q4, qs4) @ xt.t()
+    s = q.float() @ sh.rows[:n].float().t()
+    assert ((s - est).abs() <= m4[:, None]).all()

@@ -924,6 +924,113 @@ def test_index_pruned_search_split_is_exact():
     assert split_max * 5 < int(cnt2.max()), (split_max, int(cnt2.max()))
 
 
+def test_quant_rows_mx4_matches_reference():
+    """index_i8.hip quant_rows_mx4 (e2m1 nibbles + e8m0 block scales) == the torch reference,
+    rows raising (E4, X4), queries getting the margin."""
+    from codename_symbiont_amd.ops._ext import hip, stream_handle
+
+    n = 4099
+    x = torch.nn.functional.normalize(_f(n, 384, seed=91), dim=-1).bfloat16()
+    x[7, :40] = 0                                        # zero blocks: scale byte 0, zero nibbles
+    img = torch.empty(n, 192, dtype=torch.uint8, device=DEV)
+    sc = torch.empty(n, 16, dtype=torch.uint8, device=DEV)
+    b = torch.zeros(2, device=DEV)
+    st = stream_handle(torch.device(DEV))
+    hip().quant_rows_mx4(x.data_ptr(), n, 384, img.data_ptr(), sc.data_ptr(), b.data_ptr(), 0, st)
+    rimg, rsc, xt, nr = R.quant_rows_mx4_ref(x)
+    torch.cuda.synchronize()
+    assert torch.equal(sc, rsc)
+    assert torch.equal(img, rimg)
+    _close(b, nr[:, :2].amax(0), atol=1e-6, rtol=1e-4, what="mx4 bounds")
+    q = torch.nn.functional.normalize(_f(300, 384, seed=92), dim=-1).bfloat16()
+    qi = torch.empty(300, 192, dtype=torch.uint8, device=DEV)
+    qs = torch.empty(300, 16, dtype=torch.uint8, device=DEV)
+    mg = torch.empty(300, device=DEV)
+    hip().quant_rows_mx4(q.data_ptr(), 300, 384, qi.data_ptr(), qs.data_ptr(), b.data_ptr(),
+                         mg.data_ptr(), st)
+    _, _, qt, qn = R.quant_rows_mx4_ref(q)
+    torch.cuda.synchronize()
+    _close(mg, qn[:, 2] * b[0] + qn[:, 0] * b[1] + 1e-5, atol=1e-6, rtol=1e-4, what="mx4 margin")
+    s = q.float() @ x.float().t()
+    assert ((s - qt @ xt.t()).abs() <= mg[:, None]).all()
+
+
+def test_index_scan_mx4_emits_the_bound_set():
+    """index_scan_i8_kernel HK = MX4 (v_mfma_scale_f32_16x16x128_f8f6f4 on e2m1 nibbles with
+    e8m0 block scales, 12-piece tiles over 8 waves, 8-deep ring): exactly the rows whose decoded
+    fp4 estimate reaches the threshold, both row-split forms -- pins the nibble order, the scale
+    bytes' lane / k-step mapping and the fragment layout."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+    from codename_symbiont_amd.ops._ext import hip, stream_handle
+
+    n = 300_000 + 77
+    shard = HbmIndexShard(384, n + 4096, prune="i8")
+    shard.fill_random(n, seed=5)
+    assert shard.rows_mx4 is not None
+    xt = R.mx4_decode_ref(shard.rows_mx4[:n], shard.sc_mx4[:n])
+    h, st = hip(), stream_handle(shard.device)
+    for nq in (256, 600):
+        q = torch.nn.functional.normalize(_f(nq, 384, seed=nq), dim=-1).bfloat16()
+        q4 = torch.empty(nq, 192, dtype=torch.uint8, device=DEV)
+        qs4 = torch.empty(nq, 16, dtype=torch.uint8, device=DEV)
+        m4 = torch.empty(nq, device=DEV)
+        shard._mx4_image(q, q4, qs4, shard.mx4_bounds, margin=m4)
+        est = R.mx4_decode_ref(q4, qs4) @ xt.t()
+        t = est.topk(40, dim=1).values[:, -1].contiguous()
+        rsplit, rows_per_blk, n_rblk = shard._i8_geometry(n, nq, shard._n_cus())
+        cap = 4096
+        cs = torch.empty(nq, cap, device=DEV)
+        ci = torch.empty(nq, cap, dtype=torch.int32, device=DEV)
+        cnt = torch.empty(nq, dtype=torch.int32, device=DEV)
+        h.index_scan_i8(shard.rows_mx4.data_ptr(), shard.sc_mx4.data_ptr(), n,
+                        shard.rows_mx4.shape[0], rows_per_blk, n_rblk, q4.data_ptr(), nq,
+                        t.data_ptr(), cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(), cap, 1, st,
+                        rsplit, dim=384, sq=qs4.data_ptr(), form=1)
+        torch.cuda.synchronize()
+        want = est >= t[:, None]
+        near = (est - t[:, None]).abs() <= 1e-5 * est.abs().clamp_min(1.0)
+        assert int(cnt.max()) <= cap
+        got = torch.zeros_like(want)
+        for i in range(nq):
+            got[i, ci[i, :int(cnt[i])].long()] = True
+        bad = (got != want) & ~near
+        assert not bad.any(), f"nq={nq}: {int(bad.sum())} rows differ"
+        # the emitted scores are the estimates
+        c0 = int(cnt[0])
+        _close(cs[0, :c0], est[0, ci[0, :c0].long()], atol=1e-4, what="mx4 emitted scores")
+
+
+@pytest.mark.parametrize("nq", [256, 600])
+def test_index_pruned_search_mx4_tier_is_exact(nq):
+    """The pruned search with the MX-fp4 first tier: near-duplicate queries (their k-th score far
+    above the random bulk) take the fp4 tier, random held-out queries the int8 one; both give
+    the exact bf16 results."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+
+    n, k = (1 << 20) + 555, 10
+    g = torch.Generator(device=DEV).manual_seed(12)
+    shard = HbmIndexShard(384, n + 8192, prune="i8")
+    shard.fill_random(n, seed=6)
+    c = torch.nn.functional.normalize(torch.randn(384, device=DEV, generator=g), dim=0)
+    crowd = c + 0.1 * torch.randn(5000, 384, device=DEV, generator=g) / math.sqrt(384)
+    shard.append_f32(crowd)          # a near-duplicate crowd (cos ~0.99), the fresh-row tail
+    rows = shard.unit_rows().float()
+    for kind in ("near", "random"):
+        if kind == "near":
+            q = c + 0.1 * torch.randn(nq, 384, device=DEV, generator=g) / math.sqrt(384)
+        else:
+            q = torch.randn(nq, 384, device=DEV, generator=g)
+        q = torch.nn.functional.normalize(q, dim=-1).bfloat16()
+        s1, r1 = shard.search(q, k)
+        nv = shard._mx4_last
+        sc = q.float() @ rows.t()
+        ts, _ = torch.topk(sc, k, dim=1)
+        torch.cuda.synchronize()
+        assert nv is not None and int(nv.item()) == (0 if kind == "near" else 1), kind
+        _close(s1, ts, atol=2e-5, what=f"mx4 tier {kind} scores")
+        _close(sc.gather(1, r1.long()), ts, atol=2e-5, what=f"mx4 tier {kind} rows")
+
+
 def test_prune_qquant_and_route_match_torch():
     """index_i8.hip prune_qquant (int8 query image + per-query bound margin) and prune_route (T,
     emission threshold, route estimate from the sample's candidates) == torch compositions."""
