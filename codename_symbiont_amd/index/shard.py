@@ -990,10 +990,13 @@ class HbmIndexShard:
             qs4 = torch.empty(NQ, 16, dtype=torch.uint8, device=dev)
             m4 = torch.empty(NQ, dtype=torch.float32, device=dev)
             self._mx4_image(q_unit, q4, qs4, self.mx4_bounds, margin=m4)
+            # the probe: every 4th seed tile, scored exactly (one small fp32 GEMM)
+            probe = sub.view(-1, TILE_ROWS, self.dim)[::4].reshape(-1, self.dim)
+            ps = torch.mm(q_unit.float(), probe.float().t())
             thr4 = torch.empty(NQ, dtype=torch.float32, device=dev)
             nv = torch.empty(1, dtype=torch.int32, device=dev)
-            h.mx4_select(NQ, T.data_ptr(), m4.data_ptr(), thr0.data_ptr(), cs_p.data_ptr(),
-                         cnt_p.data_ptr(), self.SAMPLE_CAP, ts, tcs.data_ptr(), tcap,
+            h.mx4_select(NQ, T.data_ptr(), m4.data_ptr(), margin.data_ptr(), ps.data_ptr(),
+                         probe.shape[0], float(t0) / probe.shape[0], tcs.data_ptr(), tcap,
                          self.MX4_LIMIT_FRAC * cap, thr4.data_ptr(), nv.data_ptr(), st)
             ctx["mx4"] = dict(q4=q4, qs4=qs4, thr4=thr4, nv=nv)
         return ctx

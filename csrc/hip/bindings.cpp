@@ -72,10 +72,9 @@ int symb_index_scan_i8(const void* X8, const float* sx, int n_valid, int alloc_r
                        const int* gate, int gate_want);
 int symb_quant_rows_mx4(const void* X, int n, int dim, void* X4, void* SC, float* bounds,
                         float* margin, hipStream_t st);
-int symb_mx4_select(int NQ, const float* T, const float* margin4, const float* thr0,
-                    const float* cs_p, const int* cnt_p, int cap_p, int tshift,
-                    const float* tail_cs, int tail_cap, float limit, float* thr4, int* nv,
-                    hipStream_t st);
+int symb_mx4_select(int NQ, const float* T, const float* margin4, const float* margin8,
+                    const float* probe_s, int n_probe, float rate, const float* tail_cs,
+                    int tail_cap, float limit, float* thr4, int* nv, hipStream_t st);
 int symb_i8_tile_rows_for(int dim, int heavy);
 int symb_i8_split_queries_per_blk(int rsplit);
 int symb_i8_pair_config(int pair);
@@ -461,13 +460,12 @@ PYBIND11_MODULE(_hip, m) {
           "quant_rows_mx4");
   }, py::arg("X"), py::arg("n"), py::arg("dim"), py::arg("X4"), py::arg("SC"), py::arg("bounds"),
      py::arg("margin"), py::arg("stream"));
-  m.def("mx4_select", [](int NQ, uptr T, uptr margin4, uptr thr0, uptr cs_p, uptr cnt_p, int cap_p,
-                         int tshift, uptr tail_cs, int tail_cap, float limit, uptr thr4, uptr nv,
+  m.def("mx4_select", [](int NQ, uptr T, uptr margin4, uptr margin8, uptr probe_s, int n_probe,
+                         float rate, uptr tail_cs, int tail_cap, float limit, uptr thr4, uptr nv,
                          uptr st) {
-    check(symb_mx4_select(NQ, P<const float>(T), P<const float>(margin4), P<const float>(thr0),
-                          P<const float>(cs_p), P<const int>(cnt_p), cap_p, tshift,
-                          P<const float>(tail_cs), tail_cap, limit, P<float>(thr4), P<int>(nv),
-                          S(st)),
+    check(symb_mx4_select(NQ, P<const float>(T), P<const float>(margin4), P<const float>(margin8),
+                          P<const float>(probe_s), n_probe, rate, P<const float>(tail_cs),
+                          tail_cap, limit, P<float>(thr4), P<int>(nv), S(st)),
           "mx4_select");
   });
   m.def("prune_qquant", [](uptr Q, int NQ, int dim, uptr bounds, uptr Q8, uptr sq, uptr margin,

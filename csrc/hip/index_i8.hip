@@ -1126,36 +1126,36 @@ __global__ __launch_bounds__(256) void quant_rows_mx4_kernel(const __bf16* __res
   }
 }
 
-// The first tier's choice (after prune_route, from the same exact sample): the MX-fp4 scan is
-// viable for the batch iff for EVERY query the band T - margin4 lies at or above the sample's
-// seed threshold thr0 (so the sample emitted every row of it) and the band's estimated
-// population, (sample rows >= band) << tshift + dense tail rows >= band, is at most `limit`.
-// *nv ends 1 (not viable: the int8 tier runs) or stays 0 (the MX-fp4 tier runs, at thr4 = band).
+// The first tier's choice (after prune_route): the MX-fp4 scan emits, beyond the int8 scan's
+// candidates, the rows whose fp4 estimate reaches T - margin4 although their exact score is
+// below the int8 band T - margin8 -- rows scoring at least T - 2 margin4.  Their population per
+// query is estimated from exact dense scores of a row probe (every 4th seed tile of the sample,
+// `rate` corpus rows per probe row) plus the exact dense tail: the MX-fp4 tier is viable iff for
+// EVERY query probe rows in [T - 2 margin4, T - margin8) x rate + such tail rows <= `limit`.  A
+// crowd scoring above the int8 band (fresh near-duplicates) is left to the per-block route, as
+// in the int8 tier.  *nv ends 1 (not viable: the int8 tier runs) or stays 0 (the MX-fp4 tier
+// runs at thr4 = T - margin4).  Exactness never depends on the choice.
 __global__ __launch_bounds__(256) void mx4_select_kernel(
     int NQ, const float* __restrict__ T, const float* __restrict__ margin4,
-    const float* __restrict__ thr0, const float* __restrict__ cs_p, const int* __restrict__ cnt_p,
-    int cap_p, int tshift, const float* __restrict__ tail_cs, int tail_cap, float limit,
-    float* __restrict__ thr4, int* __restrict__ nv) {
+    const float* __restrict__ margin8, const float* __restrict__ probe_s, int n_probe, float rate,
+    const float* __restrict__ tail_cs, int tail_cap, float limit, float* __restrict__ thr4,
+    int* __restrict__ nv) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int q = blockIdx.x * 4 + w;
   if (q >= NQ) return;
-  const float band = T[q] - margin4[q];
-  const int cnt = cnt_p[q];
+  const float t = T[q];
+  const float lo = t - 2.f * margin4[q], hi = t - margin8[q];
   float c = 0.f;
-  const float* cs = cs_p + (size_t)q * cap_p;
-  for (int i = lane; i < min(cnt, cap_p); i += 64) c += cs[i] >= band ? 1.f : 0.f;
+  const float* ps = probe_s + (size_t)q * n_probe;
+  for (int i = lane; i < n_probe; i += 64) c += (ps[i] >= lo && ps[i] < hi) ? 1.f : 0.f;
   float tc = 0.f;
-  if (tail_cs != nullptr) {
-    const float* tcs = tail_cs + (size_t)q * tail_cap;
-    for (int i = lane; i < tail_cap; i += 64) tc += tcs[i] >= band ? 1.f : 0.f;
-  }
+  const float* tcs = tail_cs + (size_t)q * tail_cap;
+  for (int i = lane; i < tail_cap; i += 64) tc += (tcs[i] >= lo && tcs[i] < hi) ? 1.f : 0.f;
   c = wave_sum(c);
   tc = wave_sum(tc);
   if (lane == 0) {
-    thr4[q] = band;
-    const bool ok = band >= thr0[q] && cnt <= cap_p && tail_cs != nullptr &&
-                    c * (float)(1 << tshift) + tc <= limit;
-    if (!ok) atomicOr(nv, 1);
+    thr4[q] = t - margin4[q];
+    if (!(c * rate + tc <= limit)) atomicOr(nv, 1);
   }
 }
 
@@ -1521,17 +1521,18 @@ int symb_quant_rows_mx4(const void* X, int n, int dim, void* X4, void* SC, float
   return (int)hipGetLastError();
 }
 
-// The MX-fp4 tier choice (mx4_select_kernel); nv (one int) is zeroed here.
-int symb_mx4_select(int NQ, const float* T, const float* margin4, const float* thr0,
-                    const float* cs_p, const int* cnt_p, int cap_p, int tshift,
-                    const float* tail_cs, int tail_cap, float limit, float* thr4, int* nv,
-                    hipStream_t st) {
+// The MX-fp4 tier choice (mx4_select_kernel); nv (one int) is zeroed here.  probe_s: [NQ][n_probe]
+// exact scores of the probe rows, tail_cs: [NQ][tail_cap] exact scores of the tail rows.
+int symb_mx4_select(int NQ, const float* T, const float* margin4, const float* margin8,
+                    const float* probe_s, int n_probe, float rate, const float* tail_cs,
+                    int tail_cap, float limit, float* thr4, int* nv, hipStream_t st) {
   if (NQ <= 0) return 0;
-  if (cap_p <= 0 || tshift < 0 || tshift > 20) return -1;
+  if (n_probe <= 0 || tail_cap < 0 || probe_s == nullptr || (tail_cap > 0 && tail_cs == nullptr))
+    return -1;
   hipError_t e = hipMemsetAsync(nv, 0, sizeof(int), st);
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(mx4_select_kernel, dim3((NQ + 3) / 4), dim3(256), 0, st, NQ, T, margin4, thr0,
-                     cs_p, cnt_p, cap_p, tshift, tail_cs, tail_cap, limit, thr4, nv);
+  hipLaunchKernelGGL(mx4_select_kernel, dim3((NQ + 3) / 4), dim3(256), 0, st, NQ, T, margin4,
+                     margin8, probe_s, n_probe, rate, tail_cs, tail_cap, limit, thr4, nv);
   return (int)hipGetLastError();
 }
 
