@@ -190,6 +190,13 @@ template <int N>
 __device__ __forceinline__ void i8_lgkm2t(i32x4& v0, i32x4& v1, f32x4& t0, f32x4& t1) {
   asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(v0), "+v"(v1), "+v"(t0), "+v"(t1) : "i"(N));
 }
+// (MX4: the two sub-tiles' block-scale dwords are single registers, read by ds_read_b32 straight
+// into the registers the MFMAs use -- a copy into a vector before this wait would read them
+// before they arrive)
+template <int N>
+__device__ __forceinline__ void i8_lgkm2s(i32x4& v0, i32x4& v1, float& t0, float& t1) {
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(v0), "+v"(v1), "+v"(t0), "+v"(t1) : "i"(N));
+}
 // t0 / t1: the two sub-tiles' row scales, read from LDS just before the prologue; the first
 // k-step's wait covers them (older than every fragment read), so the emission after the chain
 // finds them in registers
@@ -202,11 +209,13 @@ struct I8Chain2 {
                                              i32x4 (&a)[i8s::R2][2],
                                              const i32x4 (&qf)[i8s::SETS][NKS],
                                              uint32_t base, const Dma& dma, f32x4& t0, f32x4& t1,
-                                             const float (&qsc)[i8s::SETS]) {
+                                             const float (&qsc)[i8s::SETS], float& r0, float& r1) {
     using namespace i8s;
     if constexpr (DMA_PIECES > 0 && KS % DE == 0 && KS / DE < DMA_PIECES) dma(KS / DE);
     constexpr int steps = (NKS - KS < PF2) ? (NKS - KS) : PF2;   // k-steps in flight, this one too
-    if constexpr (KS == 0)
+    if constexpr (KS == 0 && HK == MX4)
+      i8_lgkm2s<2 * (steps - 1)>(a[KS % R2][0], a[KS % R2][1], r0, r1);
+    else if constexpr (KS == 0)
       i8_lgkm2t<2 * (steps - 1)>(a[KS % R2][0], a[KS % R2][1], t0, t1);
     else
       i8_lgkm2<2 * (steps - 1)>(a[KS % R2][0], a[KS % R2][1]);
@@ -214,8 +223,8 @@ struct I8Chain2 {
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int s = 0; s < SETS; ++s) {
-        if constexpr (HK == MX4)   // (t0 / t1 .x: the two sub-tiles' row block-scale dwords)
-          mx4_mfma<KS, KS == 0>(accf[c][s], a[KS % R2][c], qf[s][KS], c ? t1[0] : t0[0], qsc[s]);
+        if constexpr (HK == MX4)   // (r0 / r1: the two sub-tiles' row block-scale dwords)
+          mx4_mfma<KS, KS == 0>(accf[c][s], a[KS % R2][c], qf[s][KS], c ? r1 : r0, qsc[s]);
         else if constexpr (KS < HK)
           h16_mfma<KS == 0>(accf[c][s], a[KS % R2][c], qf[s][KS]);
         else
@@ -227,7 +236,8 @@ struct I8Chain2 {
       i8_read16<(KS + PF2) * PIECE + NKS * PIECE>(a[(KS + PF2) % R2][1], base);
     }
     if constexpr (KS + 1 < NKS)
-      I8Chain2<D, KS + 1, DMA_PIECES, DE, HK>::run(acc, accf, a, qf, base, dma, t0, t1, qsc);
+      I8Chain2<D, KS + 1, DMA_PIECES, DE, HK>::run(acc, accf, a, qf, base, dma, t0, t1, qsc, r0,
+                                                   r1);
   }
 };
 template <int D, int J, int HK = 0>
@@ -622,16 +632,14 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
         const uint32_t fg = fw + g * 2 * NKS * PIECE;
         const int jg = j0 + 2 * g;
         f32x4 sa, sb;   // this lane's row scales of sub-tiles jg, jg + 1
+        float ra = 0.f, rb = 0.f;   // (MX4) the block-scale dwords of the lane's A row (lane & 15)
+                                    // and k-group (lane >> 4), both sub-tiles
         if constexpr (HK == MX4) {
-          // the block-scale dword of the lane's A row (lane & 15) and k-group (lane >> 4), both
-          // sub-tiles (.x; the rest unused)
-          float a0, b0;
+          sa = sb = f32x4{0.f, 0.f, 0.f, 0.f};
           const uint32_t sp = lds_addr(scl) +
                               (uint32_t)(slot * SC_BYTES + (jg * SUB + (lane & 15)) * 16 + 4 * (lane >> 4));
-          asm volatile("ds_read_b32 %0, %1" : "=v"(a0) : "v"(sp));
-          asm volatile("ds_read_b32 %0, %1 offset:256" : "=v"(b0) : "v"(sp));
-          sa = f32x4{a0, 0.f, 0.f, 0.f};
-          sb = f32x4{b0, 0.f, 0.f, 0.f};
+          asm volatile("ds_read_b32 %0, %1" : "=v"(ra) : "v"(sp));
+          asm volatile("ds_read_b32 %0, %1 offset:256" : "=v"(rb) : "v"(sp));
         } else {
           const uint32_t sp = lds_addr(scl) + (uint32_t)(slot * SC_BYTES + (jg * SUB + 4 * (lane >> 4)) * 4);
           asm volatile("ds_read_b128 %0, %1" : "=v"(sa) : "v"(sp));
@@ -644,9 +652,11 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
           emit2(acc2, accf2, row0 - TR + last - SUB, s4_prev, s4_last);
         }
         if (g == 0)
-          I8Chain2<D, 0, LOADS, G::DMA_EVERY, HK>::run(acc2, accf2, a2, qf, fg, dma, sa, sb, rsq);
+          I8Chain2<D, 0, LOADS, G::DMA_EVERY, HK>::run(acc2, accf2, a2, qf, fg, dma, sa, sb, rsq, ra,
+                                                      rb);
         else
-          I8Chain2<D, 0, 0, G::DMA_EVERY, HK>::run(acc2, accf2, a2, qf, fg, NoDma(), sa, sb, rsq);
+          I8Chain2<D, 0, 0, G::DMA_EVERY, HK>::run(acc2, accf2, a2, qf, fg, NoDma(), sa, sb, rsq, ra,
+                                                  rb);
         if (g + 1 < NG || !late) {
           emit2(acc2, accf2, row0 + jg * SUB, sa, sb);
         } else {
