@@ -13,6 +13,8 @@ for n in 2 4 8; do
   timeout -k 10 400 python -u bench.py --simulate-world $n --steps 30 --warmup 5 > $O/proj_n$n.json 2> $O/proj_n$n.err || { tail -20 $O/proj_n$n.err; exit 1; }
   cat $O/proj_n$n.json
 done
+timeout -k 10 600 python -u bench.py --steps 1000 --warmup 10 --verify > $O/sustained_1000.json 2> $O/sustained_1000.err || { tail -20 $O/sustained_1000.err; exit 1; }
+cat $O/sustained_1000.json
 timeout -k 10 400 python -u bench.py --corpus anisotropic --queries heldout --verify > $O/full_aniso.json 2> $O/full_aniso.err || { tail -20 $O/full_aniso.err; exit 1; }
 cat $O/full_aniso.json
 timeout -k 10 900 python -u benchmarks/suite.py --out $O/suite_1gpu.jsonl > $O/suite.log 2>&1 || { tail -30 $O/suite.log; exit 1; }
