@@ -25,7 +25,8 @@ def main():
     ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]), r["Queue_Id"])
           for r in rows]
     ks.sort()
-    scans = [k for k in ks if k[2] == "index_scan_i8_kernel"]
+    # the full-shard scans (a gated launch that returned at once is not one)
+    scans = [k for k in ks if k[2] == "index_scan_i8_kernel" and k[1] - k[0] > 200_000]
     gaps = list(zip(scans[:-1], scans[1:]))[-a.steps:]
     agg = collections.defaultdict(float)
     tot_gap = tot_idle = 0.0

@@ -5,7 +5,7 @@ import csv, sys, statistics
 def analyze(path):
     rows=list(csv.DictReader(open(path)))
     rows.sort(key=lambda r:int(r['Start_Timestamp']))
-    idx=[i for i,r in enumerate(rows) if 'index_scan_i8' in r['Kernel_Name']]
+    idx=[i for i,r in enumerate(rows) if 'index_scan_i8' in r['Kernel_Name'] and int(r['End_Timestamp'])-int(r['Start_Timestamp'])>200000]  # (gated no-op launches excluded)
     pre=[]; topk=[]; steps=[]
     for a,b in zip(idx[3:-1], idx[4:]):
         t_end=int(rows[a]['End_Timestamp']); t_next=int(rows[b]['Start_Timestamp'])
