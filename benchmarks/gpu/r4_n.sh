@@ -15,7 +15,7 @@ m = probe_cu_map('cuda')
 print(json.dumps({'bit_to_xcc_se_cu': m, 'reserve_2': reserve_from_map(m, 2), 'reserve_4': reserve_from_map(m, 4)}))
 " > $O/cu_map.json 2>&1 || { cat $O/cu_map.json; exit 1; }
 cut -c1-300 $O/cu_map.json
-for r in 1 2; do for v in 0 1 2 3 4; do
+for r in 1 2; do for v in 0 2 4 6 8; do
   timeout -k 10 400 python -u bench.py --steps 40 --warmup 5 --scan-cu-reserve $v > $O/cu_${v}_r$r.json 2> $O/cu_${v}_r$r.err || { tail -20 $O/cu_${v}_r$r.err; exit 1; }
   grep -o '"ms_per_step": [0-9.]*' $O/cu_${v}_r$r.json | sed "s/^/reserve $v r$r /"
 done; done

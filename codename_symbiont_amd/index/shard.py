@@ -871,9 +871,10 @@ class HbmIndexShard:
     # int8 scan but spreads over the whole chip; 1024 int8 candidates from one block per query
     # cost about as much to emit and re-score.
     PRUNE_DENSE_FRAC = 0.6
-    # batches up to this many queries score the exact tail densely (see _pruned_begin);
-    # SYMB_TAIL_DENSE_MAX_NQ=0 keeps the emitting tail scan (A/B)
-    tail_dense_max_nq = int(os.environ.get("SYMB_TAIL_DENSE_MAX_NQ", "512"))
+    # batches up to this many queries score the exact tail densely (see _pruned_begin; the
+    # MX-fp4 tier's choice needs those dense scores, so 2048 covers the gathered batches of the
+    # 8-GPU step); SYMB_TAIL_DENSE_MAX_NQ=0 keeps the emitting tail scan (A/B)
+    tail_dense_max_nq = int(os.environ.get("SYMB_TAIL_DENSE_MAX_NQ", "2048"))
     PRUNE_BLOCK_FRAC = 1 / 32
     # the MX-fp4 first tier runs when every query's estimated fp4 band holds at most this share
     # of PRUNE_CAP (its candidates are re-scored exactly like the int8 ones)

@@ -1000,11 +1000,11 @@ def test_index_scan_mx4_emits_the_bound_set():
         _close(cs[0, :c0], est[0, ci[0, :c0].long()], atol=1e-4, what="mx4 emitted scores")
 
 
-@pytest.mark.parametrize("nq", [256, 512])
+@pytest.mark.parametrize("nq", [256, 512, 2048])
 def test_index_pruned_search_mx4_tier_is_exact(nq):
     """The pruned search with the MX-fp4 first tier: near-duplicate queries (their k-th score far
     above the random bulk) take the fp4 tier, random held-out queries the int8 one; both give
-    the exact bf16 results.  (Batches above tail_dense_max_nq = 512 queries have no dense tail
+    the exact bf16 results.  (Batches above tail_dense_max_nq = 2048 queries have no dense tail
     scores to probe and always take the int8 tier.)"""
     from codename_symbiont_amd.index.shard import HbmIndexShard
 
