@@ -61,14 +61,13 @@ def probe_cu_map(device) -> list[tuple[int, int, int]]:
     h = hip()
     n = h.cu_count(idx)
     out = torch.zeros(n, 16, 2, dtype=torch.int32, device=torch.device("cuda", idx))
-    streams = []
     torch.cuda.synchronize(idx)
+    # one masked stream at a time: a CU mask is a property of a hardware queue, and 256 live
+    # masked streams crashed the runtime (profiles/r4_cu_partition/README.md)
     for c in range(n):
         st = h.stream_with_cu_mask(idx, mask_words(n, [c]))
-        streams.append(st)
         h.cu_probe(out[c].data_ptr(), 16, st)
-    torch.cuda.synchronize(idx)
-    for st in streams:
+        torch.cuda.synchronize(idx)
         h.stream_destroy(st)
     ids = out.cpu().to(torch.int64) & 0xFFFFFFFF
     res = []
