@@ -153,6 +153,8 @@ def parse_args(argv=None):
                          "as the full bf16 scan")
     ap.add_argument("--i8-tile-rows", type=int, choices=[64, 128], default=64,
                     help="rows per tile of the int8 pruning scan")
+    ap.add_argument("--mx4-tile-rows", type=int, choices=[64, 128], default=64,
+                    help="MX-fp4 first-tier scan: rows per tile at 256 queries per workgroup")
     ap.add_argument("--i8-pair", type=int, choices=[0, 1], default=0,
                     help="int8 scan: one emission pre-test over both sub-tiles of a fused chain "
                          "before the per-sub-tile ones (1) or the per-sub-tile tests alone (0, "
@@ -480,6 +482,7 @@ def run_gpu(args, info, comm) -> int:
 
         _hip().i8_config(args.i8_tile_rows, args.i8_waves)
         _hip().i8_pair_config(args.i8_pair)
+        _hip().mx4_config(args.mx4_tile_rows)
     shard.mq_stats = os.environ.get("SYMB_MQ_STATS", "0") not in ("", "0") or args.mode == "search"
     shard.scan_cus = args.scan_cus
     shard.scan_min_tiles = args.scan_min_tiles
@@ -851,6 +854,7 @@ def run_gpu(args, info, comm) -> int:
         "search_priority": args.search_priority,
         "scan_cu_reserve_per_xcd": args.scan_cu_reserve,
         "i8_pair_pretest": args.i8_pair if prune else None,
+        "mx4_tile_rows": args.mx4_tile_rows if prune else None,
         "scan_min_tiles": args.scan_min_tiles,
         "prepass_min_tiles": shard.prepass_min_tiles,
         "prune_sample_shift": ((shard.PRUNE_TILE_SHIFT_SPLIT if shard._i8_heavy

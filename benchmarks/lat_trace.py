@@ -23,7 +23,7 @@ def main() -> None:
     ap.add_argument("--b", type=int, default=1)
     ap.add_argument("--s", type=int, default=16)
     ap.add_argument("--iters", type=int, default=200)
-    ap.add_argument("--skinny-max-m", type=int, default=64,
+    ap.add_argument("--skinny-max-m", type=int, default=256,
                     help="largest M of the small-M split-K GEMM path (0: tiled GEMMs only)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the bucketed hipGraph (HipEncoder.forward_graphed) instead of eager")

@@ -1011,6 +1011,8 @@ class HbmIndexShard:
         heavy = self._i8_heavy
         rsplit = 2 if (NQ < 512 or self.i8_rsplit2) else 1
         tr = h.i8_tile_rows(self.dim, heavy)
+        if self.rows_mx4 is not None and rsplit == 2:   # (one block grid for both tiers)
+            tr = max(tr, h.mx4_tile_rows())
         if heavy:   # (the split image always runs 8-wave workgroups, one per CU)
             n_qblk, wpc = math.ceil(NQ / h.i8_split_queries_per_blk(rsplit)), 1
         else:

@@ -250,13 +250,17 @@ class HipEncoder:
         """Graph token bucket: n rounded up to 64 tokens (one skinny / tiled GEMM row block) up to
         512, to 128 up to 1024, then to 256 -- 16 buckets to GRAPH_MAX_TOKENS.  Power-of-two
         buckets (round 1-3) padded an 8 x 32 batch (256 tokens + the dummy) to 512, twice the
-        work of the eager forward: that, not launch cost, made replay slower than eager."""
+        work of the eager forward: that, not launch cost, made replay slower than eager (the
+        replay's kernel gaps are 1.5 us against 3.6 us eager, profiles/r4_small_m/)."""
         g = 64 if n <= 512 else 128 if n <= 1024 else 256
         return (n + g - 1) // g * g
 
     def forward_graphed(self, b: PackedBatch):
         T, B = b.num_tokens, b.num_seqs
-        Tb = self._token_bucket(T + 1)      # +1: the dummy sequence always owns >= 1 token
+        # (no +1: a batch already on a bucket boundary gets an EMPTY dummy sequence -- zero-
+        # length sequences are legal, the filler slots use them -- so 256 tokens stay 256 and
+        # keep the small-M GEMM path instead of crossing into the tiled one at 320)
+        Tb = self._token_bucket(max(T, 1))
         Bb = self._bucket(B, 1)
         g = self._graph(Tb, Bb)
         # real tokens first; rows [T, Tb) keep whatever valid ids/positions they last held and

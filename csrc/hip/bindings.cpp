@@ -78,6 +78,8 @@ int symb_mx4_select(int NQ, const float* T, const float* margin4, const float* m
 int symb_i8_tile_rows_for(int dim, int heavy);
 int symb_i8_split_queries_per_blk(int rsplit);
 int symb_i8_pair_config(int pair);
+int symb_mx4_config(int tile_rows);
+int symb_mx4_tile_rows();
 int symb_cu_probe(uint32_t* out, int n_blocks, hipStream_t st);
 int symb_quant_rows_split(const float* X, int n, int dim, void* X8, float* sx, float* bounds,
                           float* margin, hipStream_t st);
@@ -425,6 +427,9 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("tile_rows"), py::arg("waves") = 8);
   m.def("i8_tile_rows", [](int dim, int heavy) { return symb_i8_tile_rows_for(dim, heavy); },
         py::arg("dim") = 384, py::arg("heavy") = 0);
+  m.def("mx4_config", [](int tile_rows) { check(symb_mx4_config(tile_rows), "mx4_config"); },
+        py::arg("tile_rows"));
+  m.def("mx4_tile_rows", []() { return symb_mx4_tile_rows(); });
   m.def("i8_pair_config", [](int pair) { check(symb_i8_pair_config(pair), "i8_pair_config"); },
         py::arg("pair"));
   m.def("i8_split_queries_per_blk", [](int rsplit) { return symb_i8_split_queries_per_blk(rsplit); },

@@ -502,7 +502,7 @@ int symb_gemm_lt_config(int mode) {
   return 0;
 }
 
-// Small-M split-K path (gemm_skinny.hip): M <= symb_gemm_skinny_max_m() (default 64, the
+// Small-M split-K path (gemm_skinny.hip): M <= symb_gemm_skinny_max_m() (default 256, the
 // query-path batches) goes there first.
 int symb_gemm_skinny_max_m();
 bool symb_gemm_skinny_supported(int epi, int M, int N, int K);

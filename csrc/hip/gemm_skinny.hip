@@ -342,8 +342,11 @@ int launch_epi(int per, const float* P, int S, const float* bias, const __bf16* 
 
 using namespace symb;
 
-// Largest M the skinny path takes (0 = off); symb_gemm consults it first.
-static int g_skinny_max_m = 64;
+// Largest M the skinny path takes (0 = off); symb_gemm consults it first.  256 (the z-blocked
+// form: several 64-row blocks in grid z): MiniLM 8 x 32 / 16 x 16 / 4 x 32 / 1 x 128-token
+// forwards 280 / 283 / 279 / 286 us against 511 / 512 / 502 / 524 with the tiled GEMMs above 64,
+// bge 8 x 32 850 vs 891 us (profiles/r4_small_m/lat.jsonl).
+static int g_skinny_max_m = 256;
 // bit 0: a single-split bias / GELU / residual GEMM applies its epilogue in the split kernel;
 // bit 1 (opt-in): a small multi-split / LayerNorm GEMM is finished by its last workgroup instead
 // of the epilogue kernel.  Measured slower (profiles/r3_skinny: MiniLM out-proj/FFN2 + LN 12.7 us

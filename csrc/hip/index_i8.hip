@@ -88,7 +88,7 @@ template <int D, int TR_, int WV_ = 8, int HK = 0> struct Geo {
   static constexpr int STAGE_BYTES = STW * 10;
   // (MX4: 12 KiB tiles, an 8-deep ring keeps ~84 KiB in flight like the int8 5-deep ring)
   static constexpr int NS = WV == 4 ? 3
-                            : HK == MX4 ? 8
+                            : HK == MX4 ? (TILE_BYTES <= 12 * 1024 ? 8 : 5)
                             : (TILE_BYTES <= 24 * 1024 ||
                                (HK && 5 * (TILE_BYTES + SC_BYTES) + WV * STAGE_BYTES <= 160 * 1024))
                                 ? 5 : 3;
@@ -1345,6 +1345,15 @@ int symb_i8_queries_per_blk(int rsplit) {
 }
 
 static int g_i8_pair = 0;
+// MX-fp4 scan tile rows at 256 queries per workgroup: 64 (12 KiB tiles, 8-deep ring) or 128
+// (24 KiB tiles, 5-deep ring: half the barriers per row); symb_mx4_config
+static int g_mx4_tr = 64;
+int symb_mx4_config(int tile_rows) {
+  if (tile_rows != 64 && tile_rows != 128) return -1;
+  g_mx4_tr = tile_rows;
+  return 0;
+}
+int symb_mx4_tile_rows() { return g_mx4_tr; }
 int symb_i8_pair_config(int pair) {
   if (pair != 0 && pair != 1) return -1;
   g_i8_pair = pair;
@@ -1394,7 +1403,7 @@ int symb_index_scan_i8(const void* X8, const float* sx, int n_valid, int alloc_r
   if (dim != 384 && dim != 768) return -1;
   if (heavy != 0 && (heavy != 64 || dim != 384 || sq == nullptr)) return -1;
   if (form != 0 && (form != 1 || heavy != 0 || dim != 384 || sq == nullptr)) return -1;
-  const int tr = form ? 64 : symb_i8_tile_rows_for(dim, heavy);
+  const int tr = form ? (rsplit == 2 ? g_mx4_tr : 64) : symb_i8_tile_rows_for(dim, heavy);
   if (rows_per_blk % tr || n_rblk <= 0 || thr == nullptr || cap <= 0 || n_valid <= 0) return -1;
   if ((long long)n_rblk * rows_per_blk < n_valid) return -1;
   if ((long long)(n_valid + tr - 1) / tr * tr > alloc_rows) return -1;   // a tile past the buffer
@@ -1405,6 +1414,10 @@ int symb_index_scan_i8(const void* X8, const float* sx, int n_valid, int alloc_r
 #define SYMB_I8(D_, RS, T) launch_i8<D_, RS, T>(X8, sx, n_valid, rows_per_blk, n_rblk, Q8, NQ, thr, \
                                                 cand_s, cand_i, cand_n, cap, xcd, st, skip,       \
                                                 nullptr, gate, gate_want)
+  if (form && rsplit == 2 && g_mx4_tr == 128)   // (rows_per_blk: a multiple of 128, the host's)
+    return launch_i8<384, 2, 128, 8, MX4>(X8, sx, n_valid, rows_per_blk, n_rblk, Q8, NQ, thr,
+                                          cand_s, cand_i, cand_n, cap, xcd, st, skip, sq, gate,
+                                          gate_want);
   if (form)
     return rsplit == 2 ? launch_i8<384, 2, 64, 8, MX4>(X8, sx, n_valid, rows_per_blk, n_rblk, Q8,
                                                        NQ, thr, cand_s, cand_i, cand_n, cap, xcd,

@@ -160,7 +160,7 @@ def test_gemm_skinny(M, N, K, epi):
     from codename_symbiont_amd.ops._ext import hip
     from codename_symbiont_amd.ops.kernels import gemm
 
-    assert hip().gemm_skinny_max_m() == 64
+    assert hip().gemm_skinny_max_m() == 256
     a = _bf(M, K, seed=1)   # (opt-in last-workgroup finish where M x N <= 16384, N <= 1024)
     w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=2)
     bias = _f(N, scale=0.5, seed=3)
@@ -178,13 +178,13 @@ def test_gemm_skinny(M, N, K, epi):
             other = gemm(a, w, bias, epi, res, g, b, 1e-12)
             other2 = gemm(a, w, bias, epi, res, g, b, 1e-12)   # the last-workgroup counter re-armed
         finally:
-            hip().gemm_skinny_config(64, 1)
+            hip().gemm_skinny_config(256, 1)
         assert torch.equal(out, other) and torch.equal(out, other2), f"skinny epilogue form {fuse} differs"
     hip().gemm_skinny_config(0)
     try:
         big = gemm(a, w, bias, epi, res, g, b, 1e-12)
     finally:
-        hip().gemm_skinny_config(64)
+        hip().gemm_skinny_config(256)
     _close(out, big, atol=2e-2, rtol=1e-2, what="skinny vs tiled")
 
 
@@ -203,13 +203,13 @@ def test_gemm_skinny_row_blocks(M, N, K, epi):
     res = _bf(M, N, seed=4) if epi in (2, 3) else None
     g = _f(N, scale=0.1, offset=1.0, seed=5) if epi == 3 else None
     b = _f(N, scale=0.1, seed=6) if epi == 3 else None
-    big = gemm(a, w, bias, epi, res, g, b, 1e-12)          # default max_m 64: tiled
-    hip().gemm_skinny_config(256)
+    hip().gemm_skinny_config(64)
     try:
-        out = gemm(a, w, bias, epi, res, g, b, 1e-12)
-        out2 = gemm(a, w, bias, epi, res, g, b, 1e-12)
+        big = gemm(a, w, bias, epi, res, g, b, 1e-12)      # max_m 64: the tiled path
     finally:
-        hip().gemm_skinny_config(64)
+        hip().gemm_skinny_config(256)
+    out = gemm(a, w, bias, epi, res, g, b, 1e-12)          # the default (max_m 256): row blocks
+    out2 = gemm(a, w, bias, epi, res, g, b, 1e-12)
     ref = R.gemm_ref(a, w, bias, epi, res, g, b, 1e-12)
     _close(out, ref, atol=4e-2, rtol=2e-2, what=f"skinny row blocks epi={epi}")
     assert torch.equal(out, out2)
@@ -238,7 +238,7 @@ def test_encoder_small_batch_skinny(model):
         try:
             tiled, _ = hip_enc.forward_packed(b.to(DEV))
         finally:
-            hip().gemm_skinny_config(64)
+            hip().gemm_skinny_config(256)
         ref, _ = ref_enc.forward_packed(b)
         cos = torch.nn.functional.cosine_similarity(out.float().cpu(), ref.float(), dim=-1)
         assert cos.min().item() > 0.999, (B, S, cos)
@@ -1400,7 +1400,7 @@ def test_encoder_graph_replay_skinny():
     from codename_symbiont_amd.models.encoder import HipEncoder, synthetic_batch
     from codename_symbiont_amd.ops._ext import hip
 
-    assert hip().gemm_skinny_max_m() == 64
+    assert hip().gemm_skinny_max_m() == 256
     for model in ("minilm-l6", "bge-base"):
         cfg = get_config(model)
         enc = HipEncoder(cfg, seed=4)
@@ -1443,7 +1443,7 @@ def test_encoder_graph_replay_matches_eager():
             _close(g32, e32, atol=1e-5, what=f"graph f32 B={B} S={S}")
             assert torch.equal(gu, eu)
     finally:
-        hip().gemm_skinny_config(64)
+        hip().gemm_skinny_config(256)
     assert len(enc._graphs) >= 4
 
 
