@@ -153,7 +153,7 @@ def parse_args(argv=None):
                          "as the full bf16 scan")
     ap.add_argument("--i8-tile-rows", type=int, choices=[64, 128], default=64,
                     help="rows per tile of the int8 pruning scan")
-    ap.add_argument("--mx4-tile-rows", type=int, choices=[64, 128], default=64,
+    ap.add_argument("--mx4-tile-rows", type=int, choices=[64, 128], default=128,
                     help="MX-fp4 first-tier scan: rows per tile at 256 queries per workgroup")
     ap.add_argument("--i8-pair", type=int, choices=[0, 1], default=0,
                     help="int8 scan: one emission pre-test over both sub-tiles of a fused chain "

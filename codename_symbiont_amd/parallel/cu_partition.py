@@ -11,9 +11,10 @@ Which CUs to reserve: MI355X has 256 CUs in 8 XCDs, and how the runtime's mask b
 (XCD, shader engine, CU) is not documented here.  ``probe_cu_map`` measures it (one tiny launch per
 mask bit reads the hardware ids of the CU it ran on) and the reserve takes ``per_xcd`` CUs of
 every XCD, dealt over its shader engines, so every XCD keeps the same share of the scan's
-workgroups (which are dealt round-robin over the XCDs).  A first version guessed two numberings
-(``balanced_reserve``); at 1-2 CUs per XCD it left some XCD with fewer free CUs than scan
-workgroups and the step went from 11.0 to 16.1-16.7 ms (profiles/r4_cu_partition/).
+workgroups (which are dealt round-robin over the XCDs).  Measured: it cannot -- a single-bit mask
+let a launch run on 15 CUs across all 8 XCDs -- so the partition uses ``balanced_reserve`` (two
+guessed numberings) and is an A/B knob, off by default: with 1-2 reserved CUs per XCD the
+headline went from 11.0 to 16.1-16.7 ms, with 4 per XCD 10.84 ms (profiles/r4_cu_partition/).
 """
 from __future__ import annotations
 
@@ -49,41 +50,45 @@ def mask_words(n_cus: int, cus) -> list[int]:
 _MAPS: dict = {}
 
 
-def probe_cu_map(device) -> list[tuple[int, int, int]]:
-    """(xcc, se, cu) of every CU-mask bit of ``device``, measured: for each bit, 16 workgroups on a
-    stream masked to that CU alone record HW_ID / XCC_ID (csrc/hip/cu_probe.hip).  Cached."""
+def probe_cu_map(device, bits=None) -> list[list[tuple[int, int, int]]]:
+    """The (xcc, se, cu) hardware ids the workgroups of a launch on a stream masked to ONE
+    mask bit actually ran on, per bit (csrc/hip/cu_probe.hip: 16 workgroups each record HW_ID /
+    XCC_ID).  Measured on MI355X / ROCm 7: a single-bit mask does NOT confine a launch to one CU
+    -- bit 0's workgroups ran on 15 CUs across all 8 XCDs (profiles/r4_cu_partition/) -- so the
+    result is a list of id sets, not a bijection.  Cached per device (all bits only)."""
     from ..ops._ext import hip, stream_handle
 
     dev = torch.device(device)
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
-    if idx in _MAPS:
+    if bits is None and idx in _MAPS:
         return _MAPS[idx]
     h = hip()
     n = h.cu_count(idx)
-    out = torch.zeros(n, 16, 2, dtype=torch.int32, device=torch.device("cuda", idx))
+    bits = list(range(n)) if bits is None else list(bits)
+    out = torch.zeros(len(bits), 16, 2, dtype=torch.int32, device=torch.device("cuda", idx))
     torch.cuda.synchronize(idx)
     # one masked stream at a time: a CU mask is a property of a hardware queue, and 256 live
     # masked streams crashed the runtime (profiles/r4_cu_partition/README.md)
-    for c in range(n):
+    for i, c in enumerate(bits):
         st = h.stream_with_cu_mask(idx, mask_words(n, [c]))
-        h.cu_probe(out[c].data_ptr(), 16, st)
+        h.cu_probe(out[i].data_ptr(), 16, st)
         torch.cuda.synchronize(idx)
         h.stream_destroy(st)
     ids = out.cpu().to(torch.int64) & 0xFFFFFFFF
     res = []
-    for c in range(n):
-        hw, xcc = ids[c, :, 0], ids[c, :, 1] & 0xF
+    for i in range(len(bits)):
+        hw, xcc = ids[i, :, 0], ids[i, :, 1] & 0xF
         cu, se = (hw >> 8) & 0xF, (hw >> 13) & 0x7
-        key = {(int(a), int(b), int(d)) for a, b, d in zip(xcc, se, cu)}
-        if len(key) != 1:
-            raise RuntimeError(f"CU mask bit {c} ran on {sorted(key)}: not one CU")
-        res.append(key.pop())
-    _MAPS[idx] = res
+        res.append(sorted({(int(a), int(b), int(d)) for a, b, d in zip(xcc, se, cu)}))
+    if len(bits) == n:
+        _MAPS[idx] = res
     return res
 
 
 def reserve_from_map(cu_map, per_xcd: int) -> list[int]:
-    """``per_xcd`` mask bits of every XCC, dealt round-robin over its shader engines."""
+    """``per_xcd`` mask bits of every XCC, dealt round-robin over its shader engines, for a map
+    in which every bit confines work to one CU (a list of (xcc, se, cu)); probe_cu_map shows
+    that MI355X / ROCm 7 masks do not, so CuPartition uses balanced_reserve."""
     by_xcc: dict = {}
     for bit, (xcc, se, cu) in enumerate(cu_map):
         by_xcc.setdefault(xcc, {}).setdefault(se, []).append((cu, bit))
@@ -110,15 +115,15 @@ class CuPartition:
     it)."""
 
     def __init__(self, device, per_xcd: int, side_all: bool = True, n_side: int = 1,
-                 probe: bool = True):
+                 probe: bool = False):
         from ..ops._ext import hip
 
         self.device = torch.device(device)
         idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
         h = hip()
         self.n_cus = h.cu_count(idx)
-        # the measured bit -> (XCC, SE, CU) map (probe_cu_map), else the numbering-agnostic guess
-        self.cu_map = probe_cu_map(self.device) if probe else None
+        # (probe=True only with a driver whose masks confine work to single CUs, see probe_cu_map)
+        self.cu_map = [m[0] for m in probe_cu_map(self.device)] if probe else None
         self.reserve = (reserve_from_map(self.cu_map, per_xcd) if probe
                         else balanced_reserve(self.n_cus, per_xcd))
         rest = [c for c in range(self.n_cus) if c not in set(self.reserve)]

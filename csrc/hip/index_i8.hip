@@ -1346,8 +1346,9 @@ int symb_i8_queries_per_blk(int rsplit) {
 
 static int g_i8_pair = 0;
 // MX-fp4 scan tile rows at 256 queries per workgroup: 64 (12 KiB tiles, 8-deep ring) or 128
-// (24 KiB tiles, 5-deep ring: half the barriers per row); symb_mx4_config
-static int g_mx4_tr = 64;
+// (24 KiB tiles, 5-deep ring: half the barriers per row; default -- headline 7.35 vs 7.72 ms
+// per step, same box, profiles/r4_mx4/tile/); symb_mx4_config
+static int g_mx4_tr = 128;
 int symb_mx4_config(int tile_rows) {
   if (tile_rows != 64 && tile_rows != 128) return -1;
   g_mx4_tr = tile_rows;
