@@ -1260,8 +1260,11 @@ class HbmIndexShard:
         return out_s, out_i
 
     def _search_matmul(self, q_unit: torch.Tensor, k: int, chunk: int = 1 << 22):
-        """Chunked exact fallback (CPU backend, or k > 32 on GPU)."""
+        """Chunked exact fallback (CPU backend, or k > 32 on GPU).  Each chunk's fp32 score block
+        stays <= 512 MiB: one GEMM output past 2 GiB came back with its tail unwritten on the
+        GPU stack (benchmarks/diag/gemm_2g.py)."""
         NQ = q_unit.shape[0]
+        chunk = max(4096, min(chunk, (1 << 27) // max(1, NQ)))
         best_s = torch.full((NQ, k), -math.inf, device=self.device)
         best_i = torch.full((NQ, k), -1, dtype=torch.int64, device=self.device)
         q = q_unit.to(self.device).float()

@@ -91,10 +91,29 @@ def encoder_ref(params: dict, cfg, ids, pos, type_ids, cu_seqlens):
 
 
 def topk_ref(index_rows: torch.Tensor, queries: torch.Tensor, k: int):
-    """Exact cosine top-k of unit rows (fp32 math on the same bf16 data)."""
-    s = queries.float() @ index_rows.float().t()
-    k = min(k, index_rows.shape[0])
-    return torch.topk(s, k, dim=1)
+    """Exact cosine top-k of unit rows (fp32 math on the same bf16 data), over row chunks so
+    no fp32 score block reaches 256 MiB (a single [NQ, n] GEMM output past 2 GiB came back with
+    its tail unwritten on the GPU stack: benchmarks/diag/gemm_2g.py)."""
+    qf = queries.float()
+    n = index_rows.shape[0]
+    k = min(k, n)
+    chunk = max(4096, (1 << 26) // max(1, qf.shape[0]))
+    if n <= chunk:
+        return torch.topk(qf @ index_rows.float().t(), k, dim=1)
+    vs, ix = [], []
+    for s in range(0, n, chunk):
+        v, i = torch.topk(qf @ index_rows[s:s + chunk].float().t(), min(k, n - s), dim=1)
+        vs.append(v)
+        ix.append(i + s)
+    v, j = torch.topk(torch.cat(vs, 1), k, dim=1)
+    return v, torch.gather(torch.cat(ix, 1), 1, j)
+
+
+def row_scores_ref(index_rows: torch.Tensor, queries: torch.Tensor, r: torch.Tensor):
+    """Exact fp32 scores of the rows r [NQ, k] a search returned (no full score matrix)."""
+    if r.numel() and int(r.min()) < 0:
+        raise ValueError("row_scores_ref: negative row id")
+    return (index_rows[r.long()].float() * queries.float()[:, None, :]).sum(-1)
 
 
 def quant_rows_i8_ref(x: torch.Tensor):

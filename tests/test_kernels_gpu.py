@@ -329,7 +329,7 @@ def test_index_scan_topk_exact(D, k, n, nq):
         hits += len(set(r[i].tolist()) & set(ref_i[i].tolist()))
     assert hits / (nq * k) > 0.995
     # every returned row's true score equals the returned score
-    true = (q.float() @ shard.unit_rows().float().t()).gather(1, r.long())
+    true = R.row_scores_ref(shard.unit_rows(), q, r)
     _close(s, true, atol=2e-3, what="returned rows")
 
 
@@ -515,7 +515,7 @@ def test_prefilter_fp8_rescored_search(D, nq):
     torch.cuda.synchronize()
     assert torch.equal(pre.rows[:pre.count], exact.rows[:exact.count])
     assert pi[:5, 0].tolist() == list(range(n, n + 5))
-    true = (q.float() @ pre.unit_rows().float().t()).gather(1, pi.long())
+    true = R.row_scores_ref(pre.unit_rows(), q, pi)
     _close(ps, true, atol=1e-4, what="rescored scores")
     hits = sum(len(set(pi[i].tolist()) & set(ei[i].tolist())) for i in range(nq))
     assert hits / (nq * k) >= 0.998, hits / (nq * k)
@@ -532,11 +532,10 @@ def test_prefilter_shard_large_k_is_exact(k):
     sh.fill_random(n, seed=3)
     q = torch.nn.functional.normalize(_f(nq, 384, seed=4), dim=-1).bfloat16()
     s, r = sh.search(q, k)
-    ref = q.float() @ sh.rows[:n].float().t()
-    rs, ri = torch.topk(ref, k, dim=1)
+    rs, ri = R.topk_ref(sh.rows[:n], q, k)
     assert s.shape == (nq, k) and (r >= 0).all()
     _close(s, rs, atol=2e-5, what="scores")
-    _close(ref.gather(1, r.long()), rs, atol=2e-5, what="returned rows' scores")
+    _close(R.row_scores_ref(sh.rows[:n], q, r), rs, atol=2e-5, what="returned rows' scores")
 
 
 @pytest.mark.gpu
@@ -611,7 +610,7 @@ def test_index_scan_mq_exact(nq, rsplit):
     assert (r0 == r1).float().mean().item() > 0.999
     ref_s, _ = R.topk_ref(shard.unit_rows(), q, k)
     _close(s1, ref_s, atol=2e-3, what="mq topk scores")
-    true = (q.float() @ shard.unit_rows().float().t()).gather(1, r1.long())
+    true = R.row_scores_ref(shard.unit_rows(), q, r1)
     _close(s1, true, atol=2e-3, what="mq returned rows")
 
 
@@ -717,7 +716,7 @@ def test_index_pruned_search_is_exact(nq, data, tr):
     _close(s1, s0, atol=2e-5, what="pruned vs exact scores")
     if data != "clustered":   # (tight clusters: near-ties may order differently; scores decide)
         assert (r0 == r1).float().mean().item() > 0.999
-    true = (q.float() @ shard.unit_rows().float().t()).gather(1, r1.long())
+    true = R.row_scores_ref(shard.unit_rows(), q, r1)
     _close(s1, true, atol=2e-3, what="pruned returned rows")
 
 
@@ -742,7 +741,7 @@ def test_index_scan_mq_wide_rows_exact(D):
     assert int(ovf.item()) == 0 and cnt.float().mean().item() > 0
     _close(s1, s0, atol=1e-5, what=f"mq{D} vs list scores")
     assert (r0 == r1).float().mean().item() > 0.999
-    true = (q.float() @ shard.unit_rows().float().t()).gather(1, r1.long())
+    true = R.row_scores_ref(shard.unit_rows(), q, r1)
     _close(s1, true, atol=2e-3, what=f"mq{D} returned rows")
 
 
@@ -765,10 +764,10 @@ def test_wide_index_topk_exact_vs_torch_topk(D, k):
     s, r = shard.search(q, k)
     torch.cuda.synchronize()
     assert not calls, "a k <= 128 search at this size must stay on the HIP scans"
-    sc = q.float() @ shard.unit_rows().float().t()
-    ts, ti = torch.topk(sc, k, dim=1)
+    ts, ti = R.topk_ref(shard.unit_rows(), q, k)
     _close(s, ts, atol=2e-5, what=f"D={D} k={k} scores")
-    _close(sc.gather(1, r.long()), ts, atol=2e-5, what=f"D={D} k={k} returned rows")
+    _close(R.row_scores_ref(shard.unit_rows(), q, r), ts, atol=2e-5,
+           what=f"D={D} k={k} returned rows")
     assert r[:8, 0].tolist() == list(range(n, n + 8))
 
 
@@ -807,7 +806,7 @@ def test_index_pruned_search_768_is_exact(nq, data):
     _close(s1, s0, atol=2e-5, what="pruned768 vs exact scores")
     if data != "clustered":
         assert (r0 == r1).float().mean().item() > 0.999
-    true = (q.float() @ shard.unit_rows().float().t()).gather(1, r1.long())
+    true = R.row_scores_ref(shard.unit_rows(), q, r1)
     _close(s1, true, atol=2e-3, what="pruned768 returned rows")
 
 
@@ -905,12 +904,12 @@ def test_index_pruned_search_split_is_exact():
     s1, r1 = shard.search(q, k)
     cnt, ovf = shard._mq_last
     dense = shard._route_last
-    sc = q.float() @ shard.unit_rows().float().t()
-    ts, ti = torch.topk(sc, k, dim=1)
+    ts, ti = R.topk_ref(shard.unit_rows(), q, k)
     torch.cuda.synchronize()
     assert int(ovf.item()) == 0 and int(dense.item()) == 0
     _close(s1, ts, atol=2e-5, what="split pruned vs exact scores")
-    _close(sc.gather(1, r1.long()), ts, atol=2e-5, what="split pruned returned rows")
+    _close(R.row_scores_ref(shard.unit_rows(), q, r1), ts, atol=2e-5,
+           what="split pruned returned rows")
     split_max = int(cnt.max())
     # the plain int8 image of the same rows (same sample, same thresholds) emits far more
     shard.i8_split = "off"
@@ -1024,12 +1023,11 @@ def test_index_pruned_search_mx4_tier_is_exact(nq):
         q = torch.nn.functional.normalize(q, dim=-1).bfloat16()
         s1, r1 = shard.search(q, k)
         nv = shard._mx4_last
-        sc = q.float() @ rows.t()
-        ts, _ = torch.topk(sc, k, dim=1)
+        ts, _ = R.topk_ref(rows, q, k)
         torch.cuda.synchronize()
         assert nv is not None and int(nv.item()) == (0 if kind == "near" else 1), kind
         _close(s1, ts, atol=2e-5, what=f"mx4 tier {kind} scores")
-        _close(sc.gather(1, r1.long()), ts, atol=2e-5, what=f"mx4 tier {kind} rows")
+        _close(R.row_scores_ref(rows, q, r1), ts, atol=2e-5, what=f"mx4 tier {kind} rows")
 
 
 def test_prune_qquant_and_route_match_torch():
@@ -1214,7 +1212,7 @@ def test_index_pruned_search_routes_crowded_blocks_exactly(where):
     if where == "tail":   # the exact tail scan counts its crowd rows: the last block goes too
         assert flags[n_rblk - 1], "the tail's block goes to the bf16 scan"
     _close(s1, s0, atol=2e-5, what="block-routed pruned vs exact scores")
-    true = (q.float() @ shard.unit_rows().float().t()).gather(1, r1.long())
+    true = R.row_scores_ref(shard.unit_rows(), q, r1)
     _close(s1, true, atol=2e-3, what="block-routed returned rows")
     srt = r1.sort(dim=1).values
     assert (srt[:, 1:] != srt[:, :-1]).all(), "a row emitted by both scans would repeat"
@@ -1300,11 +1298,11 @@ def test_index_large_k_search_is_exact(k, data):
     q = gen.unit(nq, seed=13).bfloat16()
     s1, r1 = shard.search(q, k)
     assert shard._mq_last is not None and r1.dtype == torch.int32
-    full = q.float() @ shard.unit_rows().float().t()
-    s0, r0 = torch.topk(full, k, dim=1)
+    s0, r0 = R.topk_ref(shard.unit_rows(), q, k)
     torch.cuda.synchronize()
     _close(s1, s0, atol=2e-5, what=f"top-{k} scores")
-    _close(full.gather(1, r1.long()), s0, atol=2e-5, what=f"top-{k} returned rows")
+    _close(R.row_scores_ref(shard.unit_rows(), q, r1), s0, atol=2e-5,
+           what=f"top-{k} returned rows")
     assert (r0.int() == r1).float().mean().item() > 0.99
 
 
@@ -1368,7 +1366,7 @@ def test_index_scan_fp8_exact_on_decoded_rows(D, k, n, nq):
     _close(s, ref_s.float(), atol=2e-3, what="fp8 topk scores")
     hits = sum(len(set(r[i].tolist()) & set(ref_i[i].tolist())) for i in range(nq))
     assert hits / (nq * min(k, n)) > 0.99
-    true = (qd @ shard.unit_rows().float().t()).gather(1, r.long())
+    true = R.row_scores_ref(shard.unit_rows(), qd, r)
     _close(s, true, atol=2e-3, what="fp8 returned rows")
 
 

@@ -229,7 +229,9 @@ def test_http_load_generator_stops_when_every_connection_breaks():
     r = native().http_load("127.0.0.1", box["port"], reqs, 4, 30.0)
     box["loop"].call_soon_threadsafe(box["loop"].stop)
     assert time.time() - t0 < 10.0
-    assert len(r["latency_s"]) == 8 and r["errors"] == 92
+    # 2 answers per connection; under load a hang-up can overtake the 2nd answer (a request the
+    # client already sent to the closing socket draws a reset that drops unread bytes)
+    assert 4 <= len(r["latency_s"]) <= 8 and len(r["latency_s"]) + r["errors"] == 100, r
 
 
 def test_search_results_batch_matches_per_request_encoding():
