@@ -25,12 +25,17 @@ def main() -> None:
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--skinny-max-m", type=int, default=256,
                     help="largest M of the small-M split-K GEMM path (0: tiled GEMMs only)")
+    ap.add_argument("--nw8-max-kg", type=int, default=8,
+                    help="8-wave small-M workgroups for 4 < K/128 <= this (gemm_skinny_nw8)")
+    ap.add_argument("--nw8-min-wgs", type=int, default=128,
+                    help="... and above that K for M > 64 while the grid keeps this many workgroups")
     ap.add_argument("--graph", action="store_true",
                     help="replay the bucketed hipGraph (HipEncoder.forward_graphed) instead of eager")
     a = ap.parse_args()
     from codename_symbiont_amd.ops._ext import hip
 
     hip().gemm_skinny_config(a.skinny_max_m)
+    hip().gemm_skinny_nw8(a.nw8_max_kg, a.nw8_min_wgs)
     from codename_symbiont_amd.models import get_config
     from codename_symbiont_amd.models.encoder import HipEncoder, synthetic_batch
 
@@ -49,7 +54,7 @@ def main() -> None:
         ts.append(time.perf_counter() - t0)
     ts.sort()
     print(json.dumps({"bench": "encoder_latency_us", "model": a.model, "B": a.b, "S": a.s,
-                      "tokens": int(b.num_tokens), "skinny_max_m": a.skinny_max_m,
+                      "tokens": int(b.num_tokens), "skinny_max_m": a.skinny_max_m, "nw8_max_kg": a.nw8_max_kg, "nw8_min_wgs": a.nw8_min_wgs,
                       "graph": a.graph,
                       "p50_us": round(ts[len(ts) // 2] * 1e6, 1),
                       "p10_us": round(ts[len(ts) // 10] * 1e6, 1)}))

@@ -77,8 +77,10 @@ def gemm(a, w, bias, epi=EPI_BIAS, residual=None, gamma=None, beta=None, eps=1e-
     if K % 64:
         raise ValueError("K must be a multiple of 64")
     if epi == EPI_RES_LN:
-        if N != 384:
-            raise ValueError("fused LayerNorm epilogue needs N == 384 (use EPI_RES + add_ln)")
+        # 384-wide row-complete tiles, or any width <= 4096 on the small-M path's split-sum kernel
+        if N != 384 and not (M <= hip().gemm_skinny_max_m() and N % 64 == 0 and N <= 4096):
+            raise ValueError("fused LayerNorm epilogue needs N == 384 or M <= the small-M "
+                             "limit (else EPI_RES + add_ln)")
     elif N % 128:
         raise ValueError("N must be a multiple of 128")
     if epi in (EPI_RES, EPI_RES_LN):

@@ -110,6 +110,7 @@ int symb_gemm_lt_config(int mode);
 int symb_gemm_lt_plans();
 int symb_gemm_skinny_config(int max_m, int fuse);
 int symb_gemm_skinny_max_m();
+int symb_gemm_skinny_nw8(int max_kg, int min_wgs);
 size_t symb_gemm_skinny_scratch_bytes(int epi, int M, int N, int K);
 void symb_gemm_skinny_set_scratch(void* p, size_t bytes);
 int symb_mq_config(int aux);
@@ -222,7 +223,12 @@ class EncoderRuntime {
                         P<void>(pemb_), P<void>(temb_), P<float>(eln_g_), P<float>(eln_b_), eps_,
                         P<void>(h), T, H, st),
           "embed_ln");
-    const bool fuse_ln = (H == 384);
+    // residual + LayerNorm inside the out-proj / FFN2 GEMM: the 384-wide row-complete tiles, or,
+    // at any width, the small-M path's split-sum kernel (query-path batches, scratch provided)
+    const bool fuse_ln = (H == 384) ||
+                         (ws_in.size() > base && T <= symb_gemm_skinny_max_m() &&
+                          symb_gemm_skinny_scratch_bytes(EPI_RES_LN, T, H, H) > 0 &&
+                          symb_gemm_skinny_scratch_bytes(EPI_RES_LN, T, H, FF_) > 0);
     bool h_quantized = false;  // a8/sa hold the per-token e4m3 image of h (fp8 layers)
     for (size_t li = 0; li < layers_.size(); ++li) {
       const auto& L = layers_[li];
@@ -593,6 +599,9 @@ PYBIND11_MODULE(_hip, m) {
     check(symb_gemm_skinny_config(max_m, fuse), "gemm_skinny_config");
   }, py::arg("max_m") = 64, py::arg("fuse") = 1);
   m.def("gemm_skinny_max_m", []() { return symb_gemm_skinny_max_m(); });
+  m.def("gemm_skinny_nw8", [](int max_kg, int min_wgs) {
+    check(symb_gemm_skinny_nw8(max_kg, min_wgs), "gemm_skinny_nw8");
+  }, py::arg("max_kg"), py::arg("min_wgs") = 128);
   m.def("gemm_resln_config", [](int waves) { check(symb_gemm_resln_config(waves), "gemm_resln_config"); },
         py::arg("waves") = 16);
   m.def("gemm_gelu_config", [](int poly) { check(symb_gemm_gelu_config(poly), "gemm_gelu_config"); },

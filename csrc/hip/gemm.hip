@@ -515,8 +515,8 @@ int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const flo
               const void* R, int ldr, const float* gamma, const float* beta, float eps, void* C,
               int ldc, int M, int N, int K, hipStream_t st) {
   if (M <= 0) return 0;
-  if (M <= symb_gemm_skinny_max_m() && symb_gemm_skinny_supported(epi, M, N, K) &&
-      (epi != EPI_RES_LN || N == 384))   // wider rows: EPI_RES + symb_add_ln, as below
+  // (the skinny path's split-sum kernel does residual + LayerNorm for any row width <= 4096)
+  if (M <= symb_gemm_skinny_max_m() && symb_gemm_skinny_supported(epi, M, N, K))
     return symb_gemm_skinny(epi, A, lda, W, ldw, bias, R, ldr, gamma, beta, eps, g_gelu_poly, C,
                             ldc, M, N, K, st);
   if (epi == EPI_GELU) eps = g_gelu_poly ? 1.f : 0.f;

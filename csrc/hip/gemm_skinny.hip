@@ -10,7 +10,9 @@
 //
 // CDNA4 design:
 //  * Split K as far as it goes: one WAVE per (64-column block, 128-k granule).  A workgroup is
-//    4 waves = 4 consecutive granules of one column block; grid = (N/64, ceil(K/128 / 4)).
+//    NW waves = NW consecutive granules of one column block; grid = (N/64, ceil(K/128 / NW)).
+//    NW = 8 when that makes ONE split of a K of 640..1024 (bge / mpnet / e5 QKV, out-proj and
+//    FFN1): the epilogue then runs in this kernel and the second launch goes away; else NW = 4.
 //    Every wave issues all of its loads at once (one round trip to HBM/L2) and then 4 x RM x 4
 //    v_mfma_f32_16x16x32_bf16 -- no LDS staging, no k-loop.
 //  * Each lane loads 64 contiguous bytes of a row (4 x 16-byte loads): the 4 lane groups of a row
@@ -145,8 +147,8 @@ constexpr int SK_PARTIAL = -1;
 // FIN != SK_PARTIAL (with EPI == SK_PARTIAL; small outputs, N <= 1024): the LAST workgroup to
 // finish (agent-scope release / acquire around one counter) sums every split and applies the FIN
 // epilogue itself -- no second launch; it re-arms the counter for the next GEMM on the stream.
-template <int RM, int EPI, int FIN>
-__global__ __launch_bounds__(256) void skinny_partial_kernel(
+template <int RM, int EPI, int FIN, int NW>
+__global__ __launch_bounds__(NW * 64) void skinny_partial_kernel(
     const __bf16* __restrict__ A, int lda, const __bf16* __restrict__ W, int ldw,
     float* __restrict__ P, int M, int N, int KG, const float* __restrict__ bias,
     const __bf16* __restrict__ R, int ldr, int gelu_poly, __bf16* __restrict__ C, int ldc,
@@ -154,11 +156,11 @@ __global__ __launch_bounds__(256) void skinny_partial_kernel(
     int* __restrict__ counter) {
   static_assert(FIN == SK_PARTIAL || EPI == SK_PARTIAL, "the finish needs split partials");
   constexpr int MP = RM * 16, LS = 64 + 4;   // LDS row stride: 272 bytes (16-byte aligned)
-  extern __shared__ __attribute__((aligned(16))) float red[];   // [4 waves][MP rows][LS]
+  extern __shared__ __attribute__((aligned(16))) float red[];   // [NW waves][MP rows][LS]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n0 = blockIdx.x * 64;
   const int m0 = blockIdx.z * 64;                  // 64-row block (M > 64: several, in z)
-  const int g = blockIdx.y * 4 + wave;            // this wave's 128-k granule
+  const int g = blockIdx.y * NW + wave;           // this wave's 128-k granule
   const int r = lane & 15, grp = lane >> 4;
 
   f32x4 acc[RM][4];
@@ -192,7 +194,7 @@ __global__ __launch_bounds__(256) void skinny_partial_kernel(
   }
 
   // accumulator (i, j)[e] sits at row i*16 + grp*4 + e, column j*16 + r of the 64-column block;
-  // all 4 waves park theirs in LDS, then every thread finishes 8 consecutive columns of a row
+  // all NW waves park theirs in LDS, then every thread finishes 8 consecutive columns of a row
   // (fixed wave order: deterministic) with 16-byte loads and stores
 #pragma unroll
   for (int i = 0; i < RM; ++i)
@@ -201,14 +203,14 @@ __global__ __launch_bounds__(256) void skinny_partial_kernel(
 #pragma unroll
       for (int e = 0; e < 4; ++e) red[(wave * MP + i * 16 + grp * 4 + e) * LS + j * 16 + r] = acc[i][j][e];
   __syncthreads();
-  for (int q = threadIdx.x; q < MP * 8; q += 256) {
+  for (int q = threadIdx.x; q < MP * 8; q += NW * 64) {
     const int lrow = q >> 3, c8 = (q & 7) * 8, row = m0 + lrow;
     if (row >= M) break;
     float v[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = 0.f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < NW; ++w) {
       const float* src = red + (w * MP + lrow) * LS + c8;
       const f32x4 x0 = *reinterpret_cast<const f32x4*>(src);
       const f32x4 x1 = *reinterpret_cast<const f32x4*>(src + 4);
@@ -264,7 +266,7 @@ __global__ __launch_bounds__(256) void skinny_partial_kernel(
     if (!s_last) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // every workgroup's partials
     const int S = gridDim.y;
-    for (int row = wave; row < M; row += 4)
+    for (int row = wave; row < M; row += NW)
       finish_row<FIN, 2>(P, S, bias, R, ldr, gamma, beta, eps, gelu_poly, C, ldc, M, N, N, row, lane);
     if (threadIdx.x == 0) __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -305,15 +307,16 @@ float* scratch_for(hipStream_t st, size_t bytes) {
   return p;
 }
 
-template <int RM, int EPI, int FIN>
+template <int RM, int EPI, int FIN, int NW>
 void launch_partial(dim3 grid, hipStream_t st, const __bf16* a, int lda, const __bf16* w, int ldw,
                     float* P, int M, int N, int KG, const float* bias, const __bf16* r, int ldr,
                     int gelu_poly, __bf16* c, int ldc, const float* g, const float* b, float eps,
                     int* counter) {
-  constexpr int lds = 4 * RM * 16 * (64 + 4) * (int)sizeof(float);   // <= 68 KiB
-  set_max_lds<skinny_partial_kernel<RM, EPI, FIN>>(lds);
-  hipLaunchKernelGGL((skinny_partial_kernel<RM, EPI, FIN>), grid, dim3(256), lds, st, a, lda, w,
-                     ldw, P, M, N, KG, bias, r, ldr, gelu_poly, c, ldc, g, b, eps, counter);
+  constexpr int lds = NW * RM * 16 * (64 + 4) * (int)sizeof(float);   // <= 136 KiB
+  static_assert(lds <= 160 * 1024, "LDS");
+  set_max_lds<skinny_partial_kernel<RM, EPI, FIN, NW>>(lds);
+  hipLaunchKernelGGL((skinny_partial_kernel<RM, EPI, FIN, NW>), grid, dim3(NW * 64), lds, st, a,
+                     lda, w, ldw, P, M, N, KG, bias, r, ldr, gelu_poly, c, ldc, g, b, eps, counter);
 }
 
 template <int EPI>
@@ -360,6 +363,18 @@ int symb_gemm_skinny_config(int max_m, int fuse) {
   return 0;
 }
 int symb_gemm_skinny_max_m() { return g_skinny_max_m; }
+// 8-wave workgroups (8 granules per split) for 4 < K / 128 <= max_kg, and above it for M > 64
+// when the grid keeps >= min_wgs workgroups (0: never); else 4-wave ones.  With fewer, larger
+// splits a small-M forward (MiniLM 8 x 32: 2 splits of 48 workgroups; M <= 64) got slower
+// (profiles/r4_small_m/nw8.jsonl).
+static int g_skinny_nw8_max_kg = 8;
+static int g_skinny_nw8_min_wgs = 128;
+int symb_gemm_skinny_nw8(int max_kg, int min_wgs) {
+  if (max_kg < 0 || max_kg > 32 || min_wgs < 0) return -1;
+  g_skinny_nw8_max_kg = max_kg;
+  g_skinny_nw8_min_wgs = min_wgs;
+  return 0;
+}
 
 void symb_gemm_skinny_set_scratch(void* p, size_t bytes) {
   t_scratch = (float*)p;
@@ -383,7 +398,14 @@ int symb_gemm_skinny(int epi, const void* A, int lda, const void* W, int ldw, co
                      const void* R, int ldr, const float* gamma, const float* beta, float eps,
                      int gelu_poly, void* C, int ldc, int M, int N, int K, hipStream_t st) {
   if (!symb_gemm_skinny_supported(epi, M, N, K)) return -1;
-  const int KG = K / 128, S = (KG + 3) / 4;
+  const int KG = K / 128;
+  // 8 waves: K = 640..1024 in one split; above, when the 8-wave grid still spans >= min_wgs
+  // workgroups (bge / e5 FFN2 at M = 256: 642 / 1552 us per 8 x 32 forward vs 684 / 1643)
+  const int wgs8 = (N / 64) * ((KG + 7) / 8) * ((M + 63) / 64);
+  const int NW = (KG > 4 && (KG <= g_skinny_nw8_max_kg ||
+                             (g_skinny_nw8_min_wgs > 0 && M > 64 && wgs8 >= g_skinny_nw8_min_wgs)))
+                     ? 8 : 4;
+  const int S = (KG + NW - 1) / NW;
   // one split and a row-local epilogue: finished in the one kernel
   const int fused = (S == 1 && epi != SK_RES_LN && (g_skinny_fuse & 1)) ? epi : SK_PARTIAL;
   // small outputs: the last workgroup sums the splits (one CU reads S x M x N floats)
@@ -403,9 +425,11 @@ int symb_gemm_skinny(int epi, const void* A, int lda, const void* W, int ldw, co
   auto r = (const __bf16*)R;
   auto c = (__bf16*)C;
   const int rm = (std::min(M, 64) + 15) / 16;   // fragments per 64-row block
-#define SK_P(RM_, E_, F_)                                                                   \
-  launch_partial<RM_, E_, F_>(grid, st, a, lda, w, ldw, P, M, N, KG, bias, r, ldr, gelu_poly, c, \
-                              ldc, gamma, beta, eps, counter)
+#define SK_P(RM_, E_, F_)                                                                      \
+  (NW == 8 ? launch_partial<RM_, E_, F_, 8>(grid, st, a, lda, w, ldw, P, M, N, KG, bias, r, ldr,  \
+                                            gelu_poly, c, ldc, gamma, beta, eps, counter)         \
+           : launch_partial<RM_, E_, F_, 4>(grid, st, a, lda, w, ldw, P, M, N, KG, bias, r, ldr,  \
+                                            gelu_poly, c, ldc, gamma, beta, eps, counter))
 #define SK_PE(RM_)                                                    \
   switch (fused) {                                                    \
     case SK_BIAS: SK_P(RM_, SK_BIAS, SK_PARTIAL); break;              \

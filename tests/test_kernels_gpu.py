@@ -152,11 +152,13 @@ def test_gemm_hipblaslt_plan_cache_is_bounded():
 @pytest.mark.parametrize("M", [1, 5, 16, 17, 33, 64])
 @pytest.mark.parametrize("N,K,epi", [(1152, 384, 0), (1536, 384, 1), (384, 384, 3), (384, 1536, 3),
                                      (768, 768, 2), (3072, 768, 1), (768, 3072, 2),
-                                     (1024, 4096, 2), (4096, 1024, 0), (256, 128, 0)])
+                                     (1024, 4096, 2), (4096, 1024, 0), (256, 128, 0),
+                                     (768, 768, 3), (1024, 4096, 3), (256, 640, 2)])
 def test_gemm_skinny(M, N, K, epi):
     """Small-M split-K path (gemm_skinny.hip; the query-path batches, M <= 64): every epilogue,
-    1..32 k-granules (1..8 splits), ragged 16-row fragments, against the fp32 oracle and bit-exact
-    on repeat; symb_gemm routes these shapes there by default."""
+    1..32 k-granules (1..8 splits; the 8-wave single split for K = 640..1024), ragged 16-row
+    fragments, residual + LayerNorm at 384 / 768 / 1024 wide rows, against the fp32 oracle and
+    bit-exact on repeat; symb_gemm routes these shapes there by default."""
     from codename_symbiont_amd.ops._ext import hip
     from codename_symbiont_amd.ops.kernels import gemm
 
@@ -180,6 +182,8 @@ def test_gemm_skinny(M, N, K, epi):
         finally:
             hip().gemm_skinny_config(256, 1)
         assert torch.equal(out, other) and torch.equal(out, other2), f"skinny epilogue form {fuse} differs"
+    if epi == 3 and N != 384:
+        return   # (no tiled residual + LayerNorm GEMM for wider rows: EPI_RES + add_ln there)
     hip().gemm_skinny_config(0)
     try:
         big = gemm(a, w, bias, epi, res, g, b, 1e-12)
@@ -190,7 +194,8 @@ def test_gemm_skinny(M, N, K, epi):
 
 @pytest.mark.parametrize("M", [65, 100, 128, 200, 256])
 @pytest.mark.parametrize("N,K,epi", [(1152, 384, 0), (1536, 384, 1), (384, 1536, 3), (768, 3072, 2),
-                                     (3072, 768, 1)])
+                                     (3072, 768, 1), (2304, 768, 0), (768, 768, 3), (768, 3072, 3),
+                                     (1024, 1024, 3)])
 def test_gemm_skinny_row_blocks(M, N, K, epi):
     """gemm_skinny_config(max_m=256): M > 64 runs as several 64-row blocks (grid z) of the same
     split kernel; against the fp32 oracle, the tiled path, and bit-exact on repeat."""
@@ -203,23 +208,52 @@ def test_gemm_skinny_row_blocks(M, N, K, epi):
     res = _bf(M, N, seed=4) if epi in (2, 3) else None
     g = _f(N, scale=0.1, offset=1.0, seed=5) if epi == 3 else None
     b = _f(N, scale=0.1, seed=6) if epi == 3 else None
-    hip().gemm_skinny_config(64)
-    try:
-        big = gemm(a, w, bias, epi, res, g, b, 1e-12)      # max_m 64: the tiled path
-    finally:
-        hip().gemm_skinny_config(256)
+    tiled = not (epi == 3 and N != 384)   # (wider rows: no tiled residual + LayerNorm GEMM)
+    if tiled:
+        hip().gemm_skinny_config(64)
+        try:
+            big = gemm(a, w, bias, epi, res, g, b, 1e-12)      # max_m 64: the tiled path
+        finally:
+            hip().gemm_skinny_config(256)
     out = gemm(a, w, bias, epi, res, g, b, 1e-12)          # the default (max_m 256): row blocks
     out2 = gemm(a, w, bias, epi, res, g, b, 1e-12)
     ref = R.gemm_ref(a, w, bias, epi, res, g, b, 1e-12)
     _close(out, ref, atol=4e-2, rtol=2e-2, what=f"skinny row blocks epi={epi}")
     assert torch.equal(out, out2)
-    _close(out, big, atol=2e-2, rtol=1e-2, what="skinny row blocks vs tiled")
+    if tiled:
+        _close(out, big, atol=2e-2, rtol=1e-2, what="skinny row blocks vs tiled")
+
+
+@pytest.mark.parametrize("M", [16, 200])
+@pytest.mark.parametrize("N,K,epi", [(384, 1536, 3), (768, 3072, 3), (1024, 4096, 2), (3072, 2048, 1)])
+def test_gemm_skinny_nw8_multi_split(M, N, K, epi):
+    """gemm_skinny_nw8(32, 0): 8-wave workgroups also for several splits (K / 128 = 12..32) --
+    against the fp32 oracle and the 4-wave form (gemm_skinny_nw8(8, 0))."""
+    from codename_symbiont_amd.ops._ext import hip
+    from codename_symbiont_amd.ops.kernels import gemm
+
+    a = _bf(M, K, seed=11)
+    w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=12)
+    bias = _f(N, scale=0.5, seed=13)
+    res = _bf(M, N, seed=14) if epi in (2, 3) else None
+    g = _f(N, scale=0.1, offset=1.0, seed=15) if epi == 3 else None
+    b = _f(N, scale=0.1, seed=16) if epi == 3 else None
+    hip().gemm_skinny_nw8(8, 0)
+    try:
+        four = gemm(a, w, bias, epi, res, g, b, 1e-12)
+        hip().gemm_skinny_nw8(32, 0)
+        eight = gemm(a, w, bias, epi, res, g, b, 1e-12)
+    finally:
+        hip().gemm_skinny_nw8(8, 128)
+    ref = R.gemm_ref(a, w, bias, epi, res, g, b, 1e-12)
+    _close(eight, ref, atol=4e-2, rtol=2e-2, what=f"8-wave skinny epi={epi}")
+    _close(eight, four, atol=2e-2, rtol=1e-2, what="8-wave vs 4-wave skinny")
 
 
 @pytest.mark.parametrize("model", ["minilm-l6", "bge-base"])
 def test_encoder_small_batch_skinny(model):
-    """Query-path forwards (T <= 64 tokens: every GEMM on the skinny path) match the fp32 oracle
-    and the tiled path."""
+    """Query-path forwards (T <= 256 tokens: every GEMM on the skinny path; bge's residual +
+    LayerNorm fused into its split-sum kernel) match the fp32 oracle and the tiled path."""
     from codename_symbiont_amd.models import get_config
     from codename_symbiont_amd.models.encoder import HipEncoder, TorchEncoder, synthetic_batch
     from codename_symbiont_amd.models.weights import random_params
@@ -229,9 +263,9 @@ def test_encoder_small_batch_skinny(model):
     params = random_params(cfg, seed=3)
     hip_enc = HipEncoder(cfg, params=params)
     ref_enc = TorchEncoder(cfg, params=params)
-    for B, S in [(1, 16), (1, 64), (4, 12), (3, 20)]:
+    for B, S in [(1, 16), (1, 64), (4, 12), (3, 20), (8, 32)]:
         b = synthetic_batch(cfg, B, S, seed=B * 100 + S, varlen=True)
-        assert b.num_tokens <= 64
+        assert b.num_tokens <= 256
         out, _ = hip_enc.forward_packed(b.to(DEV))
         out = out.clone()
         hip().gemm_skinny_config(0)
