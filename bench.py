@@ -155,6 +155,9 @@ def parse_args(argv=None):
                     help="rows per tile of the int8 pruning scan")
     ap.add_argument("--mx4-tile-rows", type=int, choices=[64, 128], default=128,
                     help="MX-fp4 first-tier scan: rows per tile at 256 queries per workgroup")
+    ap.add_argument("--mlp-fused", type=int, choices=[0, 1], default=0,
+                    help="384-wide encoders: the whole FFN block in one kernel (mlp_fused.hip, 1; "
+                         "opt-in, profiles/r4_mlp/) or as two GEMMs (0, default)")
     ap.add_argument("--i8-pair", type=int, choices=[0, 1], default=0,
                     help="int8 scan: one emission pre-test over both sub-tiles of a fused chain "
                          "before the per-sub-tile ones (1) or the per-sub-tile tests alone (0, "
@@ -461,6 +464,9 @@ def run_gpu(args, info, comm) -> int:
 
     t0 = time.time()
     enc = HipEncoder(cfg, seed=0, device=dev, precision=args.encoder_dtype)
+    from codename_symbiont_amd.ops._ext import hip as _hip_ext
+
+    _hip_ext().mlp_fused_config(args.mlp_fused)
     vw = args.simulate_world or 0
     rows_per_rank = args.index_rows // (vw or info.world)
     extra = (K + W + 4) * B
@@ -854,6 +860,7 @@ def run_gpu(args, info, comm) -> int:
         "search_priority": args.search_priority,
         "scan_cu_reserve_per_xcd": args.scan_cu_reserve,
         "i8_pair_pretest": args.i8_pair if prune else None,
+        "mlp_fused": args.mlp_fused,
         "mx4_tile_rows": args.mx4_tile_rows if prune else None,
         "scan_min_tiles": args.scan_min_tiles,
         "prepass_min_tiles": shard.prepass_min_tiles,

@@ -445,15 +445,18 @@ def cmd_encoder(a):
     tiles = [int(t) for t in a.tiles.split(",")]
     fw = [int(t) for t in a.fp8_waves.split(",")]
     var = {}
+    mlps = [int(m) for m in a.mlp.split(",")]
     for p, e in encs.items():
         for t in tiles:
-            for w in (fw if p == "fp8" else fw[:1]):
-                name = p + ("" if len(tiles) == 1 else f"_tile{t}") + ("" if len(fw) == 1 else f"_w{w}")
+            for w, m in [(w, m) for w in (fw if p == "fp8" else fw[:1]) for m in mlps]:
+                name = p + ("" if len(tiles) == 1 else f"_tile{t}") + ("" if len(fw) == 1 else f"_w{w}") \
+                    + ("" if len(mlps) == 1 else f"_mlp{m}")
                 # w = 256 / 257: 8-wave fp8 tiles plus the 256x256 fp8 tile wherever the bf16
                 # rule takes it / where the fp8 auto rule does (the default); else no 256x256
                 # t = 12: tile rule 10 + hipBLASLt for the plain K, N >= 768 projections (the
                 # default route); other t: symb_gemm_config tile modes, every projection ours
-                var[name] = (lambda e=e, t=t, w=w: (_hip().gemm_config(128, 10 if t == 12 else t, 8),
+                var[name] = (lambda e=e, t=t, w=w, m=m: (_hip().gemm_config(128, 10 if t == 12 else t, 8),
+                                                    _hip().mlp_fused_config(m),
                                                     _hip().gemm_lt_config(1 if t == 12 else 0),
                                                     _hip().gemm_fp8_config(8 if w >= 256 else w,
                                                                            {256: 1, 257: 2}.get(w, 0)),
@@ -462,6 +465,7 @@ def cmd_encoder(a):
     _hip().gemm_config(128, 3, 8)
     _hip().gemm_lt_config(1)
     _hip().gemm_fp8_config(8)
+    _hip().mlp_fused_config(0)
     toks = a.batch * a.seq
     fl = cfg.flops_per_token(a.seq) * toks
     out = {p: dict(ms=round(m, 3), embeds_per_s=round(a.batch / (m / 1e3)),
@@ -620,6 +624,8 @@ def main():
     ap.add_argument("--model", default="minilm-l6")
     ap.add_argument("--seed", type=int, default=1, help="scanabl: seed per-query thresholds")
     ap.add_argument("--precision", default="bf16", help="encoder: comma list of bf16,fp8")
+    ap.add_argument("--mlp", default="0", help="encoder: comma list of mlp_fused_config values "
+                    "(1: the fused 384-wide FFN block, 0: two GEMMs)")
     ap.add_argument("--tiles", default="3", help="encoder: comma list of gemm_config tile modes "
                     "(3 = the default auto tiles, 10 = round-3 auto, 12 = round-3 default with hipBLASLt)")
     ap.add_argument("--fp8-waves", default="8", help="encoder: comma list of fp8 GEMM wave counts")

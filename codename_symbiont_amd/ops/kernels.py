@@ -93,6 +93,30 @@ def gemm(a, w, bias, epi=EPI_BIAS, residual=None, gamma=None, beta=None, eps=1e-
     return out
 
 
+def mlp_fused(x, w1, b1, w2, b2, gamma, beta, eps=1e-12, out=None):
+    """out = LayerNorm(GELU(x @ w1.T + b1) @ w2.T + b2 + x) in one launch (mlp_fused.hip;
+    x: [M, 384] bf16, w1: [1536, 384], w2: [384, 1536] bf16; the intermediate is rounded to bf16
+    as the two-GEMM path stores it)."""
+    _chk(x, torch.bfloat16, "x", 2)
+    _chk(w1, torch.bfloat16, "w1", 2)
+    _chk(w2, torch.bfloat16, "w2", 2)
+    M, H = x.shape
+    FF = w1.shape[0]
+    if (H, FF) != (384, 1536) or w1.shape != (FF, H) or w2.shape != (H, FF):
+        raise ValueError("mlp_fused takes H = 384, FF = 1536")
+    for t, n in ((b1, FF), (b2, H), (gamma, H), (beta, H)):
+        _chk(t, torch.float32, "vector", 1)
+        if t.shape[0] != n:
+            raise ValueError("mlp_fused: vector length")
+    if out is None:
+        out = torch.empty(M, H, dtype=torch.bfloat16, device=x.device)
+    if out.shape != (M, H) or not out.is_contiguous() or out.data_ptr() == x.data_ptr():
+        raise ValueError("mlp_fused: bad output")
+    hip().mlp_fused(_ptr(x), _ptr(w1), _ptr(b1), _ptr(w2), _ptr(b2), _ptr(gamma), _ptr(beta),
+                    float(eps), _ptr(out), M, H, FF, stream_handle())
+    return out
+
+
 def attention(qkv, cu_seqlens, max_len, n_heads, head_dim, out=None):
     """Varlen attention over packed [T, 3H] QKV rows -> [T, H]."""
     _chk(qkv, torch.bfloat16, "qkv", 2)

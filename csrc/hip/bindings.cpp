@@ -49,6 +49,16 @@ int symb_gemm_config(int resln_bm, int tile, int group_m);
 int symb_gemm_fp8_config(int waves, int big);
 int symb_gemm_resln_config(int waves);
 int symb_gemm_gelu_config(int poly);
+int symb_gemm_gelu_poly();
+int symb_mlp_fused(const void* X, const void* W1, const float* b1, const void* W2, const float* b2,
+                   const float* gamma, const float* beta, float eps, int gelu_poly, void* C, int M,
+                   int H, int FF, hipStream_t st);
+// The fused FFN block (mlp_fused.hip) for bf16 384 x 1536 layers above the small-M limit (1,
+// opt-in); 0: the two-GEMM path (FFN1 GELU GEMM + FFN2 residual/LayerNorm GEMM).  Measured
+// (profiles/r4_mlp): the bare MiniLM forward 1.414-1.427 vs 1.443-1.444 ms, but the headline step
+// 7.47-7.49 vs 7.38-7.39 ms -- its one 128 KiB-LDS workgroup per CU for 128 us shares the chip
+// worse with the concurrent scans than the two GEMMs' shorter tiles.
+static int g_mlp_fused = 0;
 int symb_gemm_fp8(int epi, const void* A8, int lda, const void* W8, int ldw, const float* sa,
                   const float* sw, const float* bias, const void* R, int ldr, void* C, int ldc,
                   int M, int N, int K, hipStream_t st, const void* ascale = nullptr,
@@ -257,6 +267,14 @@ class EncoderRuntime {
         check(symb_add_ln(P<void>(tmp), nullptr, P<float>(L.ln1_g), P<float>(L.ln1_b), eps_,
                           P<void>(h2), T, H, st),
               "ln1");
+      }
+      if (g_mlp_fused && H == 384 && FF_ == 1536 && T > symb_gemm_skinny_max_m()) {
+        // the whole FFN block in one launch: the 1536-wide activation never leaves the CU
+        check(symb_mlp_fused(P<void>(h2), P<void>(L.wi), P<float>(L.bi), P<void>(L.wo2),
+                             P<float>(L.bo2), P<float>(L.ln2_g), P<float>(L.ln2_b), eps_,
+                             symb_gemm_gelu_poly(), P<void>(h), T, H, FF_, st),
+              "fused ffn");
+        continue;
       }
       check(symb_gemm(EPI_GELU, P<void>(h2), H, P<void>(L.wi), H, P<float>(L.bi), nullptr, 0,
                       nullptr, nullptr, 0.f, P<void>(ff), FF_, T, FF_, H, st),
@@ -604,6 +622,14 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("max_kg"), py::arg("min_wgs") = 128);
   m.def("gemm_resln_config", [](int waves) { check(symb_gemm_resln_config(waves), "gemm_resln_config"); },
         py::arg("waves") = 16);
+  m.def("mlp_fused", [](uptr X, uptr W1, uptr b1, uptr W2, uptr b2, uptr g, uptr b, float eps,
+                        uptr C, int M, int H, int FF, uptr st) {
+    check(symb_mlp_fused(P<void>(X), P<void>(W1), P<float>(b1), P<void>(W2), P<float>(b2),
+                         P<float>(g), P<float>(b), eps, symb_gemm_gelu_poly(), P<void>(C), M, H, FF,
+                         S(st)),
+          "mlp_fused");
+  });
+  m.def("mlp_fused_config", [](int on) { g_mlp_fused = on ? 1 : 0; });
   m.def("gemm_gelu_config", [](int poly) { check(symb_gemm_gelu_config(poly), "gemm_gelu_config"); },
         py::arg("poly"));
   m.def("gemm_fp8_config", [](int waves, int big) {

@@ -689,3 +689,4 @@ int symb_gemm_gelu_config(int poly) {
   g_gelu_poly = poly;
   return 0;
 }
+int symb_gemm_gelu_poly() { return g_gelu_poly; }

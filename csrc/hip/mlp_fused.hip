@@ -1,0 +1,259 @@
+// Fused BERT feed-forward block for 384-wide encoders (all-MiniLM-L6-v2, the headline model):
+//
+//   out[M, 384] = LayerNorm( GELU(X W1^T + b1) W2^T + b2 + X )      W1: [1536, 384], W2: [384, 1536]
+//
+// Replaces the reference's intermediate + output linears of each BERT layer (candle BertModel's
+// BertIntermediate / BertOutput: /root/reference/services/preprocessing_service/src/
+// embedding_generator.rs:198), which this repo otherwise runs as two GEMMs (gemm.hip EPI_GELU,
+// then EPI_RES_LN) with a 4H-wide activation round trip through HBM: at 32768 tokens that is a
+// 100 MB write plus a 100 MB read per layer, and the FFN1 GEMM's short K (384) leaves its 128x128
+// tiles mostly prologue and epilogue (profiles/r4_mlp: 66 + 63 us per layer).
+//
+// Measured: 128 us per layer, on par with the two GEMMs (profiles/r4_mlp/README.md): each of
+// the 96 ring steps waits a full L2 round trip for a 32-48 KiB stage that its MFMAs consume in a
+// fraction of that, so the kernel is latency-bound at 2 stages; opt-in (mlp_fused_config).
+//
+// CDNA4 design (one 128-row block of tokens per workgroup, 8 waves as 4 x 2):
+//  * The 1536-wide intermediate is produced and consumed in 12 chunks of 128 columns that never
+//    leave the CU: phase A computes the chunk H_c = GELU(X W1_c^T + b1_c) (128 x 128, K = 384)
+//    into fp32 accumulators, rounds it to bf16 (the same rounding the two-GEMM path stores) into
+//    LDS; phase B accumulates out += H_c W2_c^T (128 x 384, K = 128) into registers that live
+//    across all 12 chunks (24 accumulators per wave).
+//  * Operands stream through ONE 2-slot LDS ring of 48 KiB slots: phase A's k-tiles (X 128 x 64
+//    + W1_c 128 x 64 = 32 KiB) and phase B's (W2_c 384 x 64 = 48 KiB) form one sequence of
+//    8 steps per chunk; step s+1's global_load_lds DMA is issued right after step s's barrier, so
+//    every load overlaps the previous step's MFMAs, across phase and chunk boundaries alike.
+//  * X (re-read per chunk) and W1 / W2 (re-read per row block) come from L2: X's 96 KiB row
+//    panel is private to the workgroup, the 2.4 MB of weights are shared by all of them.
+//  * v_mfma_f32_16x16x32_bf16; 128-byte LDS rows with the XOR chunk swizzle of gemm.hip on both
+//    the DMA source address and the ds_read address; H_c is written in the same swizzled layout,
+//    so phase B reads it exactly like a DMA'd tile.
+//  * Epilogue: + b2 + X (the residual is the block's own input), LayerNorm over the 384 columns,
+//    bf16 16-byte stores; the fp32 tile is staged through LDS in two 64-row passes.
+#include "common.h"
+
+namespace symb {
+
+namespace {
+
+constexpr int MF_H = 384, MF_FF = 1536, MF_BM = 128, MF_FC = 128;
+constexpr int MF_WM = 4, MF_WN = 2, MF_NW = MF_WM * MF_WN, MF_NT = 64 * MF_NW;
+constexpr int MF_SLOT = 48 * 1024;                   // one ring slot (phase B's W2 k-tile)
+constexpr int MF_HC = 2 * MF_SLOT;                   // H_c: 2 k-tiles of 128 rows x 128 B
+constexpr int MF_LDS = MF_HC + 2 * MF_BM * 128;      // 128 KiB
+constexpr int MF_CS = MF_H + 4;                      // epilogue fp32 row stride
+static_assert(64 * MF_CS * 4 <= MF_LDS, "epilogue pass fits the LDS");
+
+__device__ __forceinline__ int mf_swz(int row, int chunk) {
+  return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
+}
+
+__global__ __launch_bounds__(MF_NT) void mlp_fused_kernel(
+    const __bf16* __restrict__ X, const __bf16* __restrict__ W1, const float* __restrict__ b1,
+    const __bf16* __restrict__ W2, const float* __restrict__ b2, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, int gelu_poly, __bf16* __restrict__ C, int M) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / MF_WN, wn = wave % MF_WN;
+  const int m0 = xcd_remap(blockIdx.x, gridDim.x) * MF_BM;
+  constexpr int KT_A = MF_H / 64;                    // 6 k-tiles of X . W1_c^T
+  constexpr int KT_B = MF_FC / 64;                   // 2 k-tiles of H_c . W2_c^T
+  constexpr int STEPS = KT_A + KT_B;                 // per chunk
+  constexpr int NCHUNK = MF_FF / MF_FC;
+  char* hc = smem + MF_HC;
+
+  // step q of the whole sequence -> (chunk, phase step); DMA into slot q & 1
+  auto stage = [&](int q) {
+    const int c = q / STEPS, s = q % STEPS;
+    char* base = smem + (q & 1) * MF_SLOT;
+    if (s < KT_A) {
+      const size_t k0 = (size_t)s * 128;             // byte offset of the k-tile
+#pragma unroll
+      for (int i = 0; i < (MF_BM * 8) / MF_NT; ++i) {
+        const int v = i * MF_NT + tid;
+        const int row = v >> 3, pc = v & 7, ch = pc ^ ((row >> 1) & 7);
+        const int grow = min(m0 + row, M - 1);
+        glds16(reinterpret_cast<const char*>(X + (size_t)grow * MF_H) + k0 + ch * 16,
+               base + (i * MF_NT + wave * 64) * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < (MF_FC * 8) / MF_NT; ++i) {
+        const int v = i * MF_NT + tid;
+        const int row = v >> 3, pc = v & 7, ch = pc ^ ((row >> 1) & 7);
+        glds16(reinterpret_cast<const char*>(W1 + (size_t)(c * MF_FC + row) * MF_H) + k0 + ch * 16,
+               base + MF_BM * 128 + (i * MF_NT + wave * 64) * 16);
+      }
+    } else {
+      const size_t k0 = (size_t)(c * MF_FC + (s - KT_A) * 64) * 2;
+#pragma unroll
+      for (int i = 0; i < (MF_H * 8) / MF_NT; ++i) {
+        const int v = i * MF_NT + tid;
+        const int row = v >> 3, pc = v & 7, ch = pc ^ ((row >> 1) & 7);
+        glds16(reinterpret_cast<const char*>(W2 + (size_t)row * MF_FF) + k0 + ch * 16,
+               base + (i * MF_NT + wave * 64) * 16);
+      }
+    }
+  };
+
+  f32x4 acc[2][12];                                  // out rows wm*32 + 16i, cols wn*192 + 16j
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 12; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int r16 = lane & 15, g4 = lane >> 4;
+  // step q landed; every wave is done with slot (q+1)&1 and with H_c's writes / reads
+  auto step_begin = [&](int q) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (q + 1 < NCHUNK * STEPS) stage(q + 1);
+  };
+  stage(0);
+  int q = 0;
+#pragma unroll 1
+  for (int c = 0; c < NCHUNK; ++c) {
+    // phase A: H_c (rows wm*32 + 16i, cols wn*64 + 16j); its registers are dead in phase B
+    f32x4 ha[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ha[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KT_A; ++s, ++q) {
+      step_begin(q);
+      const char* sA = smem + (q & 1) * MF_SLOT;
+      const char* sB = sA + MF_BM * 128;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int chunk = kk * 4 + g4;
+        bf16x8 a[2], b[4];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          a[i] = *reinterpret_cast<const bf16x8*>(sA + mf_swz(wm * 32 + i * 16 + r16, chunk));
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          b[j] = *reinterpret_cast<const bf16x8*>(sB + mf_swz(wn * 64 + j * 16 + r16, chunk));
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            ha[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], ha[i][j], 0, 0, 0);
+      }
+    }
+    // H_c = GELU(. + b1) -> bf16 into the swizzled 2-k-tile image; element (row, col): k-tile
+    // col / 64, 16-byte chunk (col % 64) / 8, position col % 8.  (Every wave's phase-B reads of
+    // the previous chunk's H_c finished before this chunk's first barrier.)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = wn * 64 + j * 16 + r16;
+      const float bb = b1[c * MF_FC + col];
+      char* kt = hc + (col >> 6) * (MF_BM * 128);
+      const int off = (col & 63) >> 3, pos = (col & 7) * 2;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {
+          const int row = wm * 32 + i * 16 + g4 * 4 + e;
+          f32x2 y{ha[i][j][e] + bb, ha[i][j][e + 1] + bb};
+          if (gelu_poly) {
+            y = gelu2_poly(y);
+          } else {
+            y.x = gelu_erf(y.x);
+            y.y = gelu_erf(y.y);
+          }
+          *reinterpret_cast<__bf16*>(kt + mf_swz(row, off) + pos) = (__bf16)y.x;
+          *reinterpret_cast<__bf16*>(kt + mf_swz(row + 1, off) + pos) = (__bf16)y.y;
+        }
+    }
+    // phase B: out += H_c W2_c^T
+#pragma unroll
+    for (int t = 0; t < KT_B; ++t, ++q) {
+      step_begin(q);
+      const char* sA = hc + t * (MF_BM * 128);
+      const char* sB = smem + (q & 1) * MF_SLOT;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int chunk = kk * 4 + g4;
+        bf16x8 a[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          a[i] = *reinterpret_cast<const bf16x8*>(sA + mf_swz(wm * 32 + i * 16 + r16, chunk));
+#pragma unroll
+        for (int j = 0; j < 12; ++j) {
+          const bf16x8 b = *reinterpret_cast<const bf16x8*>(sB + mf_swz(wn * 192 + j * 16 + r16, chunk));
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b, acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  // ---- epilogue: + b2 + X, LayerNorm, bf16; two 64-row passes through LDS ----
+  float* Cs = reinterpret_cast<float*>(smem);
+#pragma unroll 1
+  for (int p = 0; p < 2; ++p) {
+    __syncthreads();   // (pass 0: every wave's last MFMA reads of the ring are done)
+    if ((wm >> 1) == p) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 12; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = (wm & 1) * 32 + i * 16 + g4 * 4 + r;
+            Cs[row * MF_CS + wn * 192 + j * 16 + r16] = acc[i][j][r];
+          }
+    }
+    __syncthreads();
+    constexpr int NV = MF_H / 8;                     // 48 eight-column groups: lanes 0..47
+    for (int row = wave; row < 64; row += MF_NW) {
+      const int grow = m0 + p * 64 + row;
+      if (grow >= M) break;
+      float x[8];
+      float sum = 0.f;
+      if (lane < NV) {
+        float rr[8];
+        load8(X + (size_t)grow * MF_H + lane * 8, rr);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          x[e] = Cs[row * MF_CS + lane * 8 + e] + b2[lane * 8 + e] + rr[e];
+          sum += x[e];
+        }
+      }
+      const float mean = wave_sum(sum) * (1.0f / MF_H);
+      float ss = 0.f;
+      if (lane < NV)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ss += (x[e] - mean) * (x[e] - mean);
+      const float rstd = rsqrtf(wave_sum(ss) * (1.0f / MF_H) + eps);
+      if (lane < NV) {
+        float y[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          y[e] = (x[e] - mean) * rstd * gamma[lane * 8 + e] + beta[lane * 8 + e];
+        store8(C + (size_t)grow * MF_H + lane * 8, y);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+}  // namespace symb
+
+using namespace symb;
+
+// The whole FFN block of a 384-wide layer in one launch (X, C: [M, 384] bf16, row stride 384;
+// C must not alias X).  Returns 0, a HIP error, or -1 (shape not supported).
+int symb_mlp_fused(const void* X, const void* W1, const float* b1, const void* W2, const float* b2,
+                   const float* gamma, const float* beta, float eps, int gelu_poly, void* C, int M,
+                   int H, int FF, hipStream_t st) {
+  if (M <= 0) return 0;
+  if (H != MF_H || FF != MF_FF || X == C) return -1;
+  set_max_lds<mlp_fused_kernel>(MF_LDS);
+  hipLaunchKernelGGL(mlp_fused_kernel, dim3((M + MF_BM - 1) / MF_BM), dim3(MF_NT), MF_LDS, st,
+                     (const __bf16*)X, (const __bf16*)W1, b1, (const __bf16*)W2, b2, gamma, beta,
+                     eps, gelu_poly, (__bf16*)C, M);
+  return (int)hipGetLastError();
+}

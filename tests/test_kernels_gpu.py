@@ -250,6 +250,31 @@ def test_gemm_skinny_nw8_multi_split(M, N, K, epi):
     _close(eight, four, atol=2e-2, rtol=1e-2, what="8-wave vs 4-wave skinny")
 
 
+@pytest.mark.parametrize("M", [128, 1000, 4173])
+def test_mlp_fused(M):
+    """mlp_fused.hip (the whole 384-wide FFN block in one launch: 12 chunks of 128 intermediate
+    columns through LDS, ragged last row block) == the fp32 oracle with the intermediate rounded
+    to bf16, and == the two-GEMM path it replaces, bit-exact on repeat."""
+    from codename_symbiont_amd.ops.kernels import EPI_GELU, EPI_RES_LN, gemm, mlp_fused
+
+    x = torch.nn.functional.layer_norm(_f(M, 384, seed=21), (384,)).bfloat16()
+    w1 = _bf(1536, 384, scale=1.0 / math.sqrt(384), seed=22)
+    w2 = _bf(384, 1536, scale=1.0 / math.sqrt(1536), seed=23)
+    b1 = _f(1536, scale=0.5, seed=24)
+    b2 = _f(384, scale=0.5, seed=25)
+    g = _f(384, scale=0.1, offset=1.0, seed=26)
+    b = _f(384, scale=0.1, seed=27)
+    out = mlp_fused(x, w1, b1, w2, b2, g, b, 1e-12)
+    out2 = mlp_fused(x, w1, b1, w2, b2, g, b, 1e-12)
+    h = torch.nn.functional.gelu(x.float() @ w1.float().t() + b1).bfloat16().float()
+    ref = torch.nn.functional.layer_norm(h @ w2.float().t() + b2 + x.float(), (384,), g, b, 1e-12)
+    two = gemm(gemm(x, w1, b1, EPI_GELU), w2, b2, EPI_RES_LN, x, g, b, 1e-12)
+    torch.cuda.synchronize()
+    _close(out, ref, atol=6e-2, rtol=2e-2, what="fused mlp vs fp32 oracle")
+    _close(out, two, atol=3e-2, rtol=1e-2, what="fused mlp vs two GEMMs")
+    assert torch.equal(out, out2)
+
+
 @pytest.mark.parametrize("model", ["minilm-l6", "bge-base"])
 def test_encoder_small_batch_skinny(model):
     """Query-path forwards (T <= 256 tokens: every GEMM on the skinny path; bge's residual +
