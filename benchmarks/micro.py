@@ -465,7 +465,7 @@ def cmd_encoder(a):
     _hip().gemm_config(128, 3, 8)
     _hip().gemm_lt_config(1)
     _hip().gemm_fp8_config(8)
-    _hip().mlp_fused_config(0)
+    _hip().mlp_fused_config(1)
     toks = a.batch * a.seq
     fl = cfg.flops_per_token(a.seq) * toks
     out = {p: dict(ms=round(m, 3), embeds_per_s=round(a.batch / (m / 1e3)),
@@ -624,7 +624,7 @@ def main():
     ap.add_argument("--model", default="minilm-l6")
     ap.add_argument("--seed", type=int, default=1, help="scanabl: seed per-query thresholds")
     ap.add_argument("--precision", default="bf16", help="encoder: comma list of bf16,fp8")
-    ap.add_argument("--mlp", default="0", help="encoder: comma list of mlp_fused_config values "
+    ap.add_argument("--mlp", default="1", help="encoder: comma list of mlp_fused_config values "
                     "(1: the fused 384-wide FFN block, 0: two GEMMs)")
     ap.add_argument("--tiles", default="3", help="encoder: comma list of gemm_config tile modes "
                     "(3 = the default auto tiles, 10 = round-3 auto, 12 = round-3 default with hipBLASLt)")

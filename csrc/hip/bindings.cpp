@@ -54,11 +54,10 @@ int symb_mlp_fused(const void* X, const void* W1, const float* b1, const void* W
                    const float* gamma, const float* beta, float eps, int gelu_poly, void* C, int M,
                    int H, int FF, hipStream_t st);
 // The fused FFN block (mlp_fused.hip) for bf16 384 x 1536 layers above the small-M limit (1,
-// opt-in); 0: the two-GEMM path (FFN1 GELU GEMM + FFN2 residual/LayerNorm GEMM).  Measured
-// (profiles/r4_mlp): the bare MiniLM forward 1.414-1.427 vs 1.443-1.444 ms, but the headline step
-// 7.47-7.49 vs 7.38-7.39 ms -- its one 128 KiB-LDS workgroup per CU for 128 us shares the chip
-// worse with the concurrent scans than the two GEMMs' shorter tiles.
-static int g_mlp_fused = 0;
+// default); 0: the two-GEMM path (FFN1 GELU GEMM + FFN2 residual/LayerNorm GEMM).  Measured
+// (profiles/r4_mlp): 112 vs 129 us per layer, the bare MiniLM forward 1.285 vs 1.367 ms, the
+// headline step 7.27 / 7.32 vs 7.30 / 7.33 ms.
+static int g_mlp_fused = 1;
 int symb_gemm_fp8(int epi, const void* A8, int lda, const void* W8, int ldw, const float* sa,
                   const float* sw, const float* bias, const void* R, int ldr, void* C, int ldc,
                   int M, int N, int K, hipStream_t st, const void* ascale = nullptr,

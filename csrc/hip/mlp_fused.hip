@@ -9,9 +9,9 @@
 // 100 MB write plus a 100 MB read per layer, and the FFN1 GEMM's short K (384) leaves its 128x128
 // tiles mostly prologue and epilogue (profiles/r4_mlp: 66 + 63 us per layer).
 //
-// Measured: 128 us per layer, on par with the two GEMMs (profiles/r4_mlp/README.md): each of
-// the 96 ring steps waits a full L2 round trip for a 32-48 KiB stage that its MFMAs consume in a
-// fraction of that, so the kernel is latency-bound at 2 stages; opt-in (mlp_fused_config).
+// Measured (profiles/r4_mlp/README.md): 112 us per layer against 129 us for the two GEMMs
+// (128 us with one k-tile per phase-A stage); still ~3.6x its MFMA floor -- 60 ring steps, each a
+// barrier plus a full L2 / Infinity-Cache round trip for a 48-64 KiB stage.
 //
 // CDNA4 design (one 128-row block of tokens per workgroup, 8 waves as 4 x 2):
 //  * The 1536-wide intermediate is produced and consumed in 12 chunks of 128 columns that never
@@ -19,10 +19,11 @@
 //    into fp32 accumulators, rounds it to bf16 (the same rounding the two-GEMM path stores) into
 //    LDS; phase B accumulates out += H_c W2_c^T (128 x 384, K = 128) into registers that live
 //    across all 12 chunks (24 accumulators per wave).
-//  * Operands stream through ONE 2-slot LDS ring of 48 KiB slots: phase A's k-tiles (X 128 x 64
-//    + W1_c 128 x 64 = 32 KiB) and phase B's (W2_c 384 x 64 = 48 KiB) form one sequence of
-//    8 steps per chunk; step s+1's global_load_lds DMA is issued right after step s's barrier, so
-//    every load overlaps the previous step's MFMAs, across phase and chunk boundaries alike.
+//  * Operands stream through ONE 2-slot LDS ring of 64 KiB slots: phase A's stages (two k-tiles
+//    each of X 128 x 64 and W1_c 128 x 64 = 64 KiB) and phase B's (W2_c 384 x 64 = 48 KiB) form
+//    one sequence of 5 steps per chunk; step s+1's global_load_lds DMA is issued right after
+//    step s's barrier, so every load overlaps the previous step's MFMAs, across phase and chunk
+//    boundaries alike.
 //  * X (re-read per chunk) and W1 / W2 (re-read per row block) come from L2: X's 96 KiB row
 //    panel is private to the workgroup, the 2.4 MB of weights are shared by all of them.
 //  * v_mfma_f32_16x16x32_bf16; 128-byte LDS rows with the XOR chunk swizzle of gemm.hip on both
@@ -38,9 +39,10 @@ namespace {
 
 constexpr int MF_H = 384, MF_FF = 1536, MF_BM = 128, MF_FC = 128;
 constexpr int MF_WM = 4, MF_WN = 2, MF_NW = MF_WM * MF_WN, MF_NT = 64 * MF_NW;
-constexpr int MF_SLOT = 48 * 1024;                   // one ring slot (phase B's W2 k-tile)
+constexpr int MF_KA = 2;                             // k-tiles of X and W1_c per phase-A stage
+constexpr int MF_SLOT = 64 * 1024;                   // one ring slot (a phase-A stage)
 constexpr int MF_HC = 2 * MF_SLOT;                   // H_c: 2 k-tiles of 128 rows x 128 B
-constexpr int MF_LDS = MF_HC + 2 * MF_BM * 128;      // 128 KiB
+constexpr int MF_LDS = MF_HC + 2 * MF_BM * 128;      // 160 KiB: all of it
 constexpr int MF_CS = MF_H + 4;                      // epilogue fp32 row stride
 static_assert(64 * MF_CS * 4 <= MF_LDS, "epilogue pass fits the LDS");
 
@@ -56,7 +58,7 @@ __global__ __launch_bounds__(MF_NT) void mlp_fused_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / MF_WN, wn = wave % MF_WN;
   const int m0 = xcd_remap(blockIdx.x, gridDim.x) * MF_BM;
-  constexpr int KT_A = MF_H / 64;                    // 6 k-tiles of X . W1_c^T
+  constexpr int KT_A = MF_H / 64 / MF_KA;            // 3 stages of 2 k-tiles of X . W1_c^T
   constexpr int KT_B = MF_FC / 64;                   // 2 k-tiles of H_c . W2_c^T
   constexpr int STEPS = KT_A + KT_B;                 // per chunk
   constexpr int NCHUNK = MF_FF / MF_FC;
@@ -67,21 +69,25 @@ __global__ __launch_bounds__(MF_NT) void mlp_fused_kernel(
     const int c = q / STEPS, s = q % STEPS;
     char* base = smem + (q & 1) * MF_SLOT;
     if (s < KT_A) {
-      const size_t k0 = (size_t)s * 128;             // byte offset of the k-tile
+      // slot: X k-tiles 2s, 2s+1 (16 KiB each), then W1_c k-tiles 2s, 2s+1
 #pragma unroll
-      for (int i = 0; i < (MF_BM * 8) / MF_NT; ++i) {
-        const int v = i * MF_NT + tid;
-        const int row = v >> 3, pc = v & 7, ch = pc ^ ((row >> 1) & 7);
-        const int grow = min(m0 + row, M - 1);
-        glds16(reinterpret_cast<const char*>(X + (size_t)grow * MF_H) + k0 + ch * 16,
-               base + (i * MF_NT + wave * 64) * 16);
-      }
+      for (int t = 0; t < MF_KA; ++t) {
+        const size_t k0 = (size_t)(s * MF_KA + t) * 128;   // byte offset of the k-tile
 #pragma unroll
-      for (int i = 0; i < (MF_FC * 8) / MF_NT; ++i) {
-        const int v = i * MF_NT + tid;
-        const int row = v >> 3, pc = v & 7, ch = pc ^ ((row >> 1) & 7);
-        glds16(reinterpret_cast<const char*>(W1 + (size_t)(c * MF_FC + row) * MF_H) + k0 + ch * 16,
-               base + MF_BM * 128 + (i * MF_NT + wave * 64) * 16);
+        for (int i = 0; i < (MF_BM * 8) / MF_NT; ++i) {
+          const int v = i * MF_NT + tid;
+          const int row = v >> 3, pc = v & 7, ch = pc ^ ((row >> 1) & 7);
+          const int grow = min(m0 + row, M - 1);
+          glds16(reinterpret_cast<const char*>(X + (size_t)grow * MF_H) + k0 + ch * 16,
+                 base + t * (MF_BM * 128) + (i * MF_NT + wave * 64) * 16);
+        }
+#pragma unroll
+        for (int i = 0; i < (MF_FC * 8) / MF_NT; ++i) {
+          const int v = i * MF_NT + tid;
+          const int row = v >> 3, pc = v & 7, ch = pc ^ ((row >> 1) & 7);
+          glds16(reinterpret_cast<const char*>(W1 + (size_t)(c * MF_FC + row) * MF_H) + k0 + ch * 16,
+                 base + (MF_KA + t) * (MF_BM * 128) + (i * MF_NT + wave * 64) * 16);
+        }
       }
     } else {
       const size_t k0 = (size_t)(c * MF_FC + (s - KT_A) * 64) * 2;
@@ -121,10 +127,11 @@ __global__ __launch_bounds__(MF_NT) void mlp_fused_kernel(
 #pragma unroll
     for (int s = 0; s < KT_A; ++s, ++q) {
       step_begin(q);
-      const char* sA = smem + (q & 1) * MF_SLOT;
-      const char* sB = sA + MF_BM * 128;
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
+      for (int kq = 0; kq < 2 * MF_KA; ++kq) {
+        const int kt = kq >> 1, kk = kq & 1;
+        const char* sA = smem + (q & 1) * MF_SLOT + kt * (MF_BM * 128);
+        const char* sB = smem + (q & 1) * MF_SLOT + (MF_KA + kt) * (MF_BM * 128);
         const int chunk = kk * 4 + g4;
         bf16x8 a[2], b[4];
 #pragma unroll

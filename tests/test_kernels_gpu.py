@@ -364,9 +364,20 @@ def test_encoder_matches_fp32_oracle(model):
     ref_enc = TorchEncoder(cfg, params=params)
     b = synthetic_batch(cfg, 24, 96, seed=1, varlen=True)
     out, unit = hip_enc.forward_packed(b.to(DEV))
+    out = out.clone()
     ref, _ = ref_enc.forward_packed(b)
     cos = torch.nn.functional.cosine_similarity(out.float().cpu(), ref.float(), dim=-1)
     assert cos.min().item() > 0.999, cos
+    if cfg.hidden == 384:   # the fused FFN block (default) vs the two-GEMM path
+        from codename_symbiont_amd.ops._ext import hip
+
+        hip().mlp_fused_config(0)
+        try:
+            two, _ = hip_enc.forward_packed(b.to(DEV))
+        finally:
+            hip().mlp_fused_config(1)
+        cos2 = torch.nn.functional.cosine_similarity(out.float(), two.float(), dim=-1)
+        assert cos2.min().item() > 0.9999, cos2
 
 
 @pytest.mark.parametrize("D,k,n,nq", [(384, 10, 10_007, 300), (384, 20, 5000, 17),
