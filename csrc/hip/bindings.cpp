@@ -55,8 +55,8 @@ int symb_mlp_fused(const void* X, const void* W1, const float* b1, const void* W
                    int H, int FF, hipStream_t st);
 // The fused FFN block (mlp_fused.hip) for bf16 384 x 1536 layers above the small-M limit (1,
 // default); 0: the two-GEMM path (FFN1 GELU GEMM + FFN2 residual/LayerNorm GEMM).  Measured
-// (profiles/r4_mlp): 112 vs 129 us per layer, the bare MiniLM forward 1.285 vs 1.367 ms, the
-// headline step 7.27 / 7.32 vs 7.30 / 7.33 ms.
+// (profiles/r4_mlp): 110 vs 129 us per layer, the bare MiniLM forward 1.297 vs 1.437 ms, the
+// headline step 7.33 / 7.30 vs 7.33 / 7.36 ms (same box, interleaved).
 static int g_mlp_fused = 1;
 int symb_gemm_fp8(int epi, const void* A8, int lda, const void* W8, int ldw, const float* sa,
                   const float* sw, const float* bias, const void* R, int ldr, void* C, int ldc,

@@ -9,9 +9,10 @@
 // 100 MB write plus a 100 MB read per layer, and the FFN1 GEMM's short K (384) leaves its 128x128
 // tiles mostly prologue and epilogue (profiles/r4_mlp: 66 + 63 us per layer).
 //
-// Measured (profiles/r4_mlp/README.md): 112 us per layer against 129 us for the two GEMMs
-// (128 us with one k-tile per phase-A stage); still ~3.6x its MFMA floor -- 60 ring steps, each a
-// barrier plus a full L2 / Infinity-Cache round trip for a 48-64 KiB stage.
+// Measured (profiles/r4_mlp/README.md): 110 us per layer against 129 us for the two GEMMs
+// (128 us with one k-tile per phase-A stage); still ~3.5x its MFMA floor -- 60 ring steps, each a
+// barrier plus an L2 round trip for a 48-64 KiB stage (deeper rings and an LDS-resident X
+// measured slower: v3 / v4 there).
 //
 // CDNA4 design (one 128-row block of tokens per workgroup, 8 waves as 4 x 2):
 //  * The 1536-wide intermediate is produced and consumed in 12 chunks of 128 columns that never
@@ -144,33 +145,43 @@ __global__ __launch_bounds__(MF_NT) void mlp_fused_kernel(
         for (int i = 0; i < 2; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            ha[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], ha[i][j], 0, 0, 0);
+            ha[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], ha[i][j], 0, 0, 0);
       }
     }
-    // H_c = GELU(. + b1) -> bf16 into the swizzled 2-k-tile image; element (row, col): k-tile
-    // col / 64, 16-byte chunk (col % 64) / 8, position col % 8.  (Every wave's phase-B reads of
-    // the previous chunk's H_c finished before this chunk's first barrier.)
+    // H_c = GELU(. + b1) -> bf16 into the swizzled 2-k-tile image.  The MFMA operands are
+    // swapped (W1_c rows first), so accumulator (i, j) holds H_c^T: lane element e is token row
+    // wm*32 + 16i + (lane & 15), column wn*64 + 16j + 4 (lane >> 4) + e -- 4 consecutive columns
+    // of one row, one 8-byte ds_write (a 2-byte scatter of 4 rows per lane bank-conflicted).
+    // Element (row, col): k-tile col / 64, 16-byte chunk (col % 64) / 8, position col % 8.
+    // (Every wave's phase-B reads of the previous chunk's H_c finished before this chunk's first
+    // barrier.)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int col = wn * 64 + j * 16 + r16;
-      const float bb = b1[c * MF_FC + col];
+      const int col = wn * 64 + j * 16 + g4 * 4;
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(b1 + c * MF_FC + col);
       char* kt = hc + (col >> 6) * (MF_BM * 128);
       const int off = (col & 63) >> 3, pos = (col & 7) * 2;
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; e += 2) {
-          const int row = wm * 32 + i * 16 + g4 * 4 + e;
-          f32x2 y{ha[i][j][e] + bb, ha[i][j][e + 1] + bb};
-          if (gelu_poly) {
-            y = gelu2_poly(y);
-          } else {
-            y.x = gelu_erf(y.x);
-            y.y = gelu_erf(y.y);
-          }
-          *reinterpret_cast<__bf16*>(kt + mf_swz(row, off) + pos) = (__bf16)y.x;
-          *reinterpret_cast<__bf16*>(kt + mf_swz(row + 1, off) + pos) = (__bf16)y.y;
+      for (int i = 0; i < 2; ++i) {
+        const int row = wm * 32 + i * 16 + r16;
+        f32x2 y0{ha[i][j][0] + bb[0], ha[i][j][1] + bb[1]};
+        f32x2 y1{ha[i][j][2] + bb[2], ha[i][j][3] + bb[3]};
+        if (gelu_poly) {
+          y0 = gelu2_poly(y0);
+          y1 = gelu2_poly(y1);
+        } else {
+          y0.x = gelu_erf(y0.x);
+          y0.y = gelu_erf(y0.y);
+          y1.x = gelu_erf(y1.x);
+          y1.y = gelu_erf(y1.y);
         }
+        bf16x4 w;
+        w[0] = (__bf16)y0.x;
+        w[1] = (__bf16)y0.y;
+        w[2] = (__bf16)y1.x;
+        w[3] = (__bf16)y1.y;
+        *reinterpret_cast<bf16x4*>(kt + mf_swz(row, off) + pos) = w;
+      }
     }
     // phase B: out += H_c W2_c^T
 #pragma unroll
