@@ -155,9 +155,10 @@ def parse_args(argv=None):
                     help="rows per tile of the int8 pruning scan")
     ap.add_argument("--mx4-tile-rows", type=int, choices=[64, 128], default=128,
                     help="MX-fp4 first-tier scan: rows per tile at 256 queries per workgroup")
-    ap.add_argument("--mlp-fused", type=int, choices=[0, 1], default=1,
+    ap.add_argument("--mlp-fused", type=int, choices=[0, 1, 2], default=1,
                     help="384-wide encoders: the whole FFN block in one kernel (mlp_fused.hip, 1, "
-                         "default; profiles/r4_mlp/) or as two GEMMs (0)")
+                         "default; profiles/r4_mlp/), with the out-projection too (2), or as two "
+                         "GEMMs (0)")
     ap.add_argument("--i8-pair", type=int, choices=[0, 1], default=0,
                     help="int8 scan: one emission pre-test over both sub-tiles of a fused chain "
                          "before the per-sub-tile ones (1) or the per-sub-tile tests alone (0, "

@@ -625,7 +625,7 @@ def main():
     ap.add_argument("--seed", type=int, default=1, help="scanabl: seed per-query thresholds")
     ap.add_argument("--precision", default="bf16", help="encoder: comma list of bf16,fp8")
     ap.add_argument("--mlp", default="1", help="encoder: comma list of mlp_fused_config values "
-                    "(1: the fused 384-wide FFN block, 0: two GEMMs)")
+                    "(1: the fused 384-wide FFN block, 2: + the out-projection, 0: two GEMMs)")
     ap.add_argument("--tiles", default="3", help="encoder: comma list of gemm_config tile modes "
                     "(3 = the default auto tiles, 10 = round-3 auto, 12 = round-3 default with hipBLASLt)")
     ap.add_argument("--fp8-waves", default="8", help="encoder: comma list of fp8 GEMM wave counts")

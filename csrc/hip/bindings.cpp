@@ -52,7 +52,8 @@ int symb_gemm_gelu_config(int poly);
 int symb_gemm_gelu_poly();
 int symb_mlp_fused(const void* X, const void* W1, const float* b1, const void* W2, const float* b2,
                    const float* gamma, const float* beta, float eps, int gelu_poly, void* C, int M,
-                   int H, int FF, hipStream_t st);
+                   int H, int FF, hipStream_t st, const void* Cx, const void* Wo, const float* bo,
+                   const void* Hres, const float* g1, const float* be1);
 // The fused FFN block (mlp_fused.hip) for bf16 384 x 1536 layers above the small-M limit (1,
 // default); 0: the two-GEMM path (FFN1 GELU GEMM + FFN2 residual/LayerNorm GEMM).  Measured
 // (profiles/r4_mlp): 110 vs 129 us per layer, the bare MiniLM forward 1.297 vs 1.437 ms, the
@@ -254,6 +255,18 @@ class EncoderRuntime {
       check(symb_attention(P<void>(qkv), 3 * H, P<int32_t>(cu), B, max_len, nh_, hd_,
                            P<void>(ctx), H, st),
             "attention");
+      // the fused FFN block (mlp_fused.hip) for 384 x 1536 layers above the small-M limit;
+      // mode 2 also takes the out-projection + LN1 into the same launch
+      const bool fused_ffn = g_mlp_fused && H == 384 && FF_ == 1536 && T > symb_gemm_skinny_max_m();
+      if (fused_ffn && g_mlp_fused == 2) {
+        check(symb_mlp_fused(P<void>(h2), P<void>(L.wi), P<float>(L.bi), P<void>(L.wo2),
+                             P<float>(L.bo2), P<float>(L.ln2_g), P<float>(L.ln2_b), eps_,
+                             symb_gemm_gelu_poly(), P<void>(h), T, H, FF_, st, P<void>(ctx),
+                             P<void>(L.wo), P<float>(L.bo), P<void>(h), P<float>(L.ln1_g),
+                             P<float>(L.ln1_b)),
+              "fused out-proj + ffn");
+        continue;
+      }
       if (fuse_ln) {
         check(symb_gemm(EPI_RES_LN, P<void>(ctx), H, P<void>(L.wo), H, P<float>(L.bo),
                         P<void>(h), H, P<float>(L.ln1_g), P<float>(L.ln1_b), eps_, P<void>(h2),
@@ -267,11 +280,12 @@ class EncoderRuntime {
                           P<void>(h2), T, H, st),
               "ln1");
       }
-      if (g_mlp_fused && H == 384 && FF_ == 1536 && T > symb_gemm_skinny_max_m()) {
+      if (fused_ffn) {
         // the whole FFN block in one launch: the 1536-wide activation never leaves the CU
         check(symb_mlp_fused(P<void>(h2), P<void>(L.wi), P<float>(L.bi), P<void>(L.wo2),
                              P<float>(L.bo2), P<float>(L.ln2_g), P<float>(L.ln2_b), eps_,
-                             symb_gemm_gelu_poly(), P<void>(h), T, H, FF_, st),
+                             symb_gemm_gelu_poly(), P<void>(h), T, H, FF_, st, nullptr, nullptr,
+                             nullptr, nullptr, nullptr, nullptr),
               "fused ffn");
         continue;
       }
@@ -625,10 +639,23 @@ PYBIND11_MODULE(_hip, m) {
                         uptr C, int M, int H, int FF, uptr st) {
     check(symb_mlp_fused(P<void>(X), P<void>(W1), P<float>(b1), P<void>(W2), P<float>(b2),
                          P<float>(g), P<float>(b), eps, symb_gemm_gelu_poly(), P<void>(C), M, H, FF,
-                         S(st)),
+                         S(st), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr),
           "mlp_fused");
   });
-  m.def("mlp_fused_config", [](int on) { g_mlp_fused = on ? 1 : 0; });
+  // out-projection + LN1 + the FFN block in one launch: X receives LN1(Cx Wo^T + bo + Hres)
+  m.def("mlp_fused_op", [](uptr Cx, uptr Wo, uptr bo, uptr Hres, uptr g1, uptr be1, uptr X, uptr W1,
+                           uptr b1, uptr W2, uptr b2, uptr g, uptr b, float eps, uptr C, int M,
+                           int H, int FF, uptr st) {
+    check(symb_mlp_fused(P<void>(X), P<void>(W1), P<float>(b1), P<void>(W2), P<float>(b2),
+                         P<float>(g), P<float>(b), eps, symb_gemm_gelu_poly(), P<void>(C), M, H, FF,
+                         S(st), P<void>(Cx), P<void>(Wo), P<float>(bo), P<void>(Hres), P<float>(g1),
+                         P<float>(be1)),
+          "mlp_fused_op");
+  });
+  m.def("mlp_fused_config", [](int mode) {   // 0: two GEMMs, 1: fused FFN, 2: + out-projection
+    if (mode < 0 || mode > 2) throw std::invalid_argument("mlp_fused_config: mode 0, 1 or 2");
+    g_mlp_fused = mode;
+  });
   m.def("gemm_gelu_config", [](int poly) { check(symb_gemm_gelu_config(poly), "gemm_gelu_config"); },
         py::arg("poly"));
   m.def("gemm_fp8_config", [](int waves, int big) {

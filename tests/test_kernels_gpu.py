@@ -275,6 +275,39 @@ def test_mlp_fused(M):
     assert torch.equal(out, out2)
 
 
+@pytest.mark.parametrize("M", [128, 1000, 4173])
+def test_mlp_fused_out_projection(M):
+    """mlp_fused.hip with the out-projection prologue (mode 2): h2 == the residual + LayerNorm
+    GEMM's, the FFN half bit-exact with mlp_fused on that h2, and the output may alias the
+    residual input h (as the encoder calls it)."""
+    from codename_symbiont_amd.ops.kernels import EPI_RES_LN, gemm, mlp_fused, mlp_fused_op
+
+    ctx = _bf(M, 384, seed=31)
+    h = torch.nn.functional.layer_norm(_f(M, 384, seed=32), (384,)).bfloat16()
+    wo = _bf(384, 384, scale=1.0 / math.sqrt(384), seed=33)
+    bo = _f(384, scale=0.5, seed=34)
+    g1 = _f(384, scale=0.1, offset=1.0, seed=35)
+    be1 = _f(384, scale=0.1, seed=36)
+    w1 = _bf(1536, 384, scale=1.0 / math.sqrt(384), seed=22)
+    w2 = _bf(384, 1536, scale=1.0 / math.sqrt(1536), seed=23)
+    b1 = _f(1536, scale=0.5, seed=24)
+    b2 = _f(384, scale=0.5, seed=25)
+    g2 = _f(384, scale=0.1, offset=1.0, seed=26)
+    be2 = _f(384, scale=0.1, seed=27)
+    h2, out = mlp_fused_op(ctx, wo, bo, h, g1, be1, w1, b1, w2, b2, g2, be2, 1e-12)
+    h2_ref = gemm(ctx, wo, bo, EPI_RES_LN, h, g1, be1, 1e-12)
+    ffn = mlp_fused(h2, w1, b1, w2, b2, g2, be2, 1e-12)
+    hh = h.clone()
+    _, alias = mlp_fused_op(ctx, wo, bo, hh, g1, be1, w1, b1, w2, b2, g2, be2, 1e-12, out=hh)
+    ref = torch.nn.functional.layer_norm(ctx.float() @ wo.float().t() + bo + h.float(), (384,),
+                                         g1, be1, 1e-12)
+    torch.cuda.synchronize()
+    _close(h2, ref, atol=3e-2, rtol=1e-2, what="fused out-projection vs fp32 oracle")
+    _close(h2, h2_ref, atol=2e-2, rtol=1e-2, what="fused out-projection vs RES_LN GEMM")
+    assert torch.equal(out, ffn), "FFN half differs from mlp_fused on the same h2"
+    assert torch.equal(alias, out), "output aliasing the residual input changed the result"
+
+
 @pytest.mark.parametrize("model", ["minilm-l6", "bge-base"])
 def test_encoder_small_batch_skinny(model):
     """Query-path forwards (T <= 256 tokens: every GEMM on the skinny path; bge's residual +
@@ -368,16 +401,19 @@ def test_encoder_matches_fp32_oracle(model):
     ref, _ = ref_enc.forward_packed(b)
     cos = torch.nn.functional.cosine_similarity(out.float().cpu(), ref.float(), dim=-1)
     assert cos.min().item() > 0.999, cos
-    if cfg.hidden == 384:   # the fused FFN block (default) vs the two-GEMM path
+    if cfg.hidden == 384:   # the fused FFN block (default) vs the two-GEMM path / + out-proj
         from codename_symbiont_amd.ops._ext import hip
 
-        hip().mlp_fused_config(0)
+        others = {}
         try:
-            two, _ = hip_enc.forward_packed(b.to(DEV))
+            for mode in (0, 2):
+                hip().mlp_fused_config(mode)
+                others[mode] = hip_enc.forward_packed(b.to(DEV))[0].clone()
         finally:
             hip().mlp_fused_config(1)
-        cos2 = torch.nn.functional.cosine_similarity(out.float(), two.float(), dim=-1)
-        assert cos2.min().item() > 0.9999, cos2
+        for mode, o in others.items():
+            cos2 = torch.nn.functional.cosine_similarity(out.float(), o.float(), dim=-1)
+            assert cos2.min().item() > 0.9999, (mode, cos2)
 
 
 @pytest.mark.parametrize("D,k,n,nq", [(384, 10, 10_007, 300), (384, 20, 5000, 17),
