@@ -497,6 +497,7 @@ def run_gpu(args, info, comm) -> int:
         shard.prepass_min_tiles = args.prepass_min_tiles
     if args.prune_sample_shift:
         shard.PRUNE_TILE_SHIFT = shard.PRUNE_TILE_SHIFT_SPLIT = args.prune_sample_shift
+        shard.PRUNE_TILE_SHIFT_MX4 = args.prune_sample_shift
     if args.prune_block_frac:
         shard.PRUNE_BLOCK_FRAC = args.prune_block_frac
     torch.cuda.synchronize(dev)
@@ -868,6 +869,7 @@ def run_gpu(args, info, comm) -> int:
         "prune_sample_shift": ((shard.PRUNE_TILE_SHIFT_SPLIT if shard._i8_heavy
                                 else shard.PRUNE_TILE_SHIFT) if prune else None),
         "prune_block_frac": shard.PRUNE_BLOCK_FRAC if prune else None,
+        "prune_sample_shift_mx4_tier": shard.PRUNE_TILE_SHIFT_MX4 if prune else None,
     })
     if info.rank == 0:
         print(result_line(args, info, comm, metric, unit, config, total, ms, prune, prefilter,

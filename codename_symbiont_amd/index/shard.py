@@ -13,6 +13,7 @@ live host-side in a sparse ``PayloadStore`` keyed by row (rows without a point c
 """
 from __future__ import annotations
 
+import collections
 import math
 import os
 from dataclasses import dataclass
@@ -249,6 +250,10 @@ class HbmIndexShard:
         self._mq_tot = None
         self._mx4_tot = None     # searches whose first tier was the MX-fp4 scan (mq_stats)
         self._mx4_last = None
+        # the tier recent searches took, read back without a sync: (pinned int, event) of each
+        # search's MX-fp4 flag, and the last one known to have landed (True: the fp4 tier ran)
+        self._tier_pending = collections.deque()
+        self._tier_mx4 = False
         # snapshot change record (index/persist.py ShardPersister): rows covered by the last cut
         # and the covered rows overwritten since; kept only while ``payloads.track`` is on
         self._persisted = 0
@@ -858,6 +863,13 @@ class HbmIndexShard:
     # the split image's own sample density: 2^6 (half the sample, max 3.7k candidates per query)
     # measured the same as 2^5 (13.07 vs 13.05 ms at 100M x 256 anisotropic, profiles/r4_split/)
     PRUNE_TILE_SHIFT_SPLIT = 5
+    # ... and 2^7 while recent searches took the MX-fp4 tier (self / near-duplicate queries: each
+    # query's k-th score sits far above the bulk, so a quarter of the sample finds the same T):
+    # headline 7.19-7.25 -> 6.88-6.97 ms per step, while held-out random queries, whose T a
+    # sparser sample loosens, keep 2^5 (11.36 vs 12.36 ms at 2^7; profiles/r4_final/shift/).
+    # Decided from the last search whose tier flag has reached the host (no sync); exactness
+    # never depends on it
+    PRUNE_TILE_SHIFT_MX4 = 7
     # candidate slots per query: ~1-2k expected at 100M x 384 on random data, but the busiest of
     # 256 held-out queries emitted 6k (profiles/r3_real/); slots cost memory only (the re-score
     # and select walk the emitted count), 256 MiB at 1024 queries
@@ -909,6 +921,10 @@ class HbmIndexShard:
 
         n, NQ, kmax = self.visible, q_unit.shape[0], 16
         shift = self.PRUNE_TILE_SHIFT_SPLIT if self._i8_heavy else self.PRUNE_TILE_SHIFT
+        while self._tier_pending and self._tier_pending[0][1].query():
+            self._tier_mx4 = int(self._tier_pending.popleft()[0].item()) == 0
+        if self._tier_mx4 and self.rows_mx4 is not None:
+            shift = max(shift, self.PRUNE_TILE_SHIFT_MX4)
         plan, ts = None, shift
         while plan is None and ts >= min(self.PRUNE_MIN_SHIFT, shift):
             plan, ts = self._tile_sample_plan(n, ts), ts - 1
@@ -1096,6 +1112,14 @@ class HbmIndexShard:
         self._mq_last = (cnt, ovf)
         self._route_last = dense
         self._mx4_last = None if m4 is None else m4["nv"]   # 0: the MX-fp4 tier ran
+        if m4 is not None and dev.type == "cuda":
+            flag = torch.empty(1, dtype=torch.int32, pin_memory=True)
+            flag.copy_(m4["nv"], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            self._tier_pending.append((flag, ev))
+            while len(self._tier_pending) > 8:    # (a caller that never begins another search)
+                self._tier_pending.popleft()
         if self.mq_stats and m4 is not None:
             if self._mx4_tot is None:
                 self._mx4_tot = torch.zeros(1, dtype=torch.int32, device=dev)
