@@ -565,7 +565,7 @@ def cmd_attn(a):
         hip().attention_config(w, kv, x)
         return K.attention(qkv, cu, a.seq, nh, hd, out=out)
     res = ab({f"waves{w}_kvt{kv}_xcd{x}": (lambda w=w, kv=kv, x=x: run(w, kv, x))
-              for w in (4, 8) for kv in (64, 128) for x in (0, 1)}, a.rounds, a.iters)
+              for w in (4, 8) for kv in (64, 128) for x in (0, 1, 2)}, a.rounds, a.iters)
     hip().attention_config(8, 64, 2)
     fl = 4 * a.batch * nh * a.seq * a.seq * hd
     print(json.dumps({"bench": "attn", "head_dim": hd, "seq": a.seq, "results": {
