@@ -925,6 +925,7 @@ class HbmIndexShard:
             self._tier_mx4 = int(self._tier_pending.popleft()[0].item()) == 0
         if self._tier_mx4 and self.rows_mx4 is not None:
             shift = max(shift, self.PRUNE_TILE_SHIFT_MX4)
+        self._sample_shift_last = shift   # (diagnostics / tests)
         plan, ts = None, shift
         while plan is None and ts >= min(self.PRUNE_MIN_SHIFT, shift):
             plan, ts = self._tile_sample_plan(n, ts), ts - 1

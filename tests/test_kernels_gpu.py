@@ -1134,6 +1134,13 @@ def test_index_pruned_search_mx4_tier_is_exact(nq):
         assert nv is not None and int(nv.item()) == (0 if kind == "near" else 1), kind
         _close(s1, ts, atol=2e-5, what=f"mx4 tier {kind} scores")
         _close(R.row_scores_ref(rows, q, r1), ts, atol=2e-5, what=f"mx4 tier {kind} rows")
+        # the next search samples 1 tile in 2^7 after an fp4-tier search (its flag has landed by
+        # now), the int8 / split density after an int8-tier one -- exact either way
+        s2, r2 = shard.search(q, k)
+        torch.cuda.synchronize()
+        want = shard.PRUNE_TILE_SHIFT_MX4 if kind == "near" else shard.PRUNE_TILE_SHIFT
+        assert shard._sample_shift_last == want, (kind, shard._sample_shift_last)
+        _close(s2, ts, atol=2e-5, what=f"mx4 tier {kind} scores, second search")
 
 
 def test_prune_qquant_and_route_match_torch():
