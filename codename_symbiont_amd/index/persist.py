@@ -564,7 +564,9 @@ class ShardPersister:
         # too many patches merges every segment (row0 = 0) the same way, from disk
         row0 = p0
         popped = []
-        while segs and n - row0 > 0 and (rewrite or 2 * (n - row0) >= segs[-1]["n"]):
+        # (a rewrite merges every segment even when no row was appended since the last cut: a
+        # shard that only gets overwrites must still fold its patches back in)
+        while segs and (rewrite or (n - row0 > 0 and 2 * (n - row0) >= segs[-1]["n"])):
             popped.insert(0, segs.pop())
             row0 = popped[0]["row0"]
         fp8 = shard.dtype == "fp8"

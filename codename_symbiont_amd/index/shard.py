@@ -16,6 +16,7 @@ from __future__ import annotations
 import collections
 import math
 import os
+import threading
 from dataclasses import dataclass
 
 import torch
@@ -253,6 +254,7 @@ class HbmIndexShard:
         # the tier recent searches took, read back without a sync: (pinned int, event) of each
         # search's MX-fp4 flag, and the last one known to have landed (True: the fp4 tier ran)
         self._tier_pending = collections.deque()
+        self._tier_lock = threading.Lock()   # concurrent searches drain / append it
         self._tier_mx4 = False
         # snapshot change record (index/persist.py ShardPersister): rows covered by the last cut
         # and the covered rows overwritten since; kept only while ``payloads.track`` is on
@@ -307,7 +309,8 @@ class HbmIndexShard:
         if self.rows_i8 is not None and n > 0:
             due = r0 + n >= self._calib_next or (self.i8_split == "on" and not self._i8_heavy)
             if due and self.i8_split != "off" and self.dim in SPLIT_DIMS:
-                self.calibrate_prune(r0 + n)   # (re-images every row below r0 + n)
+                # (re-images every row below r0 + n when the image's form changes)
+                self.calibrate_prune(r0 + n, lo=r0)
             else:
                 self._i8_image(self.rows[r0:r0 + n], self.rows_i8[r0:r0 + n],
                                self.sx_i8[r0:r0 + n], self.i8_bounds)
@@ -333,7 +336,7 @@ class HbmIndexShard:
     # anisotropic corpus (index/synth.py) holds ~0.8, sentence-embedding spaces typically 0.4+
     SPLIT_MIN_SHARE = 0.3
 
-    def calibrate_prune(self, hi: int | None = None) -> None:
+    def calibrate_prune(self, hi: int | None = None, lo: int | None = None) -> None:
         """Choose the pruning image's form from the rows [0, hi) and re-image them all.
 
         The int8 bound |q| E + |q - q~| X is a Cauchy-Schwarz bound with the scale set by each
@@ -347,7 +350,11 @@ class HbmIndexShard:
         the trailing ones to int8 with their own, much finer, per-row step.  On the anisotropic
         corpus the candidates per query drop ~30x (tests/test_index_cpu.py); exactness never
         depends on R, only the cost does, so R is fixed between calibrations (first at
-        CALIB_MIN_ROWS rows, then at every CALIB_GROWTH-fold growth)."""
+        CALIB_MIN_ROWS rows, then at every CALIB_GROWTH-fold growth).
+
+        ``lo``: rows [0, lo) already carry the current image.  When the chosen form stays the
+        plain int8 one (no basis), only [lo, hi) is imaged and the generation is kept: a
+        re-image of every row would change nothing."""
         if self.rows_i8 is None:
             return
         hi = self.count if hi is None else int(hi)
@@ -363,6 +370,12 @@ class HbmIndexShard:
             share = float(ev[:SPLIT_HEAVY].sum() / ev.sum().clamp_min(1e-30))
             if self.i8_split == "on" or share >= self.SPLIT_MIN_SHARE:
                 heavy, rot = SPLIT_HEAVY, vec.t().contiguous()
+        if heavy == 0 and self._i8_heavy == 0 and lo is not None:
+            self.calib_share = share
+            self._i8_image(self.rows[lo:hi], self.rows_i8[lo:hi], self.sx_i8[lo:hi],
+                           self.i8_bounds)
+            self._calib_next = max(hi * self.CALIB_GROWTH, self.CALIB_MIN_ROWS)
+            return
         self._i8_heavy, self._i8_rot, self.calib_share = heavy, rot, share
         rb = self.dim + heavy
         n_alloc = self.sx_i8.shape[0]
@@ -921,8 +934,9 @@ class HbmIndexShard:
 
         n, NQ, kmax = self.visible, q_unit.shape[0], 16
         shift = self.PRUNE_TILE_SHIFT_SPLIT if self._i8_heavy else self.PRUNE_TILE_SHIFT
-        while self._tier_pending and self._tier_pending[0][1].query():
-            self._tier_mx4 = int(self._tier_pending.popleft()[0].item()) == 0
+        with self._tier_lock:
+            while self._tier_pending and self._tier_pending[0][1].query():
+                self._tier_mx4 = int(self._tier_pending.popleft()[0].item()) == 0
         if self._tier_mx4 and self.rows_mx4 is not None:
             shift = max(shift, self.PRUNE_TILE_SHIFT_MX4)
         self._sample_shift_last = shift   # (diagnostics / tests)
@@ -1118,9 +1132,10 @@ class HbmIndexShard:
             flag.copy_(m4["nv"], non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(cur)
-            self._tier_pending.append((flag, ev))
-            while len(self._tier_pending) > 8:    # (a caller that never begins another search)
-                self._tier_pending.popleft()
+            with self._tier_lock:
+                self._tier_pending.append((flag, ev))
+                while len(self._tier_pending) > 8:    # (a caller that never begins another search)
+                    self._tier_pending.popleft()
         if self.mq_stats and m4 is not None:
             if self._mx4_tot is None:
                 self._mx4_tot = torch.zeros(1, dtype=torch.int32, device=dev)

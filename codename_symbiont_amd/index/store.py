@@ -30,16 +30,19 @@ from ..ops._ext import native as _native  # noqa: E402
 
 class _RWLock:
     """Many readers (searches enqueuing their two halves) or one writer (an upsert enqueuing its
-    row writes).  Held only while kernels are ENQUEUED, never across a device sync."""
+    row writes), writer-preferring: once a writer waits, new readers queue behind it, so a steady
+    stream of searches cannot starve upserts.  Held while kernels are ENQUEUED; the only device
+    sync under the read side is the large-k search's overflow check (k > 16, one ``item()``)."""
 
     def __init__(self):
         self._cv = threading.Condition()
         self._readers = 0
         self._writer = False
+        self._writers_waiting = 0
 
     def acquire_read(self):
         with self._cv:
-            while self._writer:
+            while self._writer or self._writers_waiting:
                 self._cv.wait()
             self._readers += 1
 
@@ -51,8 +54,12 @@ class _RWLock:
 
     def acquire_write(self):
         with self._cv:
-            while self._writer or self._readers:
-                self._cv.wait()
+            self._writers_waiting += 1
+            try:
+                while self._writer or self._readers:
+                    self._cv.wait()
+            finally:
+                self._writers_waiting -= 1
             self._writer = True
 
     def release_write(self):

@@ -241,6 +241,32 @@ def test_snapshot_merges_stream_from_disk_with_bounded_host_memory(tmp_path):
     assert torch.equal(sh2.rows[:N + 3000], sh.rows[:N + 3000])
 
 
+def test_overwrite_only_shard_keeps_patch_files_bounded(tmp_path):
+    """A shard that only gets overwrites (no appends between cuts) still folds its patches back
+    into one segment once MAX_PATCH_FILES is reached (the rewrite used to need new
+    rows), and every generation reloads exactly."""
+    from codename_symbiont_amd.index import persist
+
+    D, N = 8, 2000
+    d = str(tmp_path / "o")
+    sh = HbmIndexShard(D, N, device="cpu")
+    sh.fill_random(N, seed=2)
+    persist.save_snapshot(sh, d)
+    rng = np.random.default_rng(1)
+    for _ in range(3 * persist.ShardPersister.MAX_PATCH_FILES):
+        rows = np.sort(rng.choice(N, 5, replace=False))
+        sh.write_rows_f32(rows, torch.from_numpy(rng.standard_normal((5, D)).astype(np.float32)))
+        persist.save_snapshot(sh, d)
+        man = persist.committed_manifest(d)
+        assert len(man["patches"]) <= persist.ShardPersister.MAX_PATCH_FILES
+        assert sum(s["n"] for s in man["segments"]) == N
+        n_patch_files = sum(1 for f in os.listdir(d) if f.startswith("patch.") and f.endswith(".rows.npy"))
+        assert n_patch_files <= persist.ShardPersister.MAX_PATCH_FILES
+    sh2 = HbmIndexShard(D, N, device="cpu")
+    assert persist.load_snapshot(sh2, d) == N
+    assert torch.equal(sh2.rows[:N], sh.rows[:N])
+
+
 def test_geometric_merges_bound_the_file_count(tmp_path):
     from codename_symbiont_amd.index import persist
 
@@ -561,3 +587,38 @@ def test_mx4_image_follows_writes_and_bounds_every_pair():
     est = mx4_decode_ref(q4, qs4) @ xt.t()
     s = q.float() @ sh.rows[:n].float().t()
     assert ((s - est).abs() <= m4[:, None]).all()
+
+
+def test_rwlock_prefers_a_waiting_writer():
+    """Once a writer waits, new readers queue behind it (a stream of searches could
+    starve upserts)."""
+    import threading
+    import time
+
+    from codename_symbiont_amd.index.store import _RWLock
+
+    lk = _RWLock()
+    lk.acquire_read()                       # a search in flight
+    order = []
+
+    def writer():
+        lk.acquire_write()
+        order.append("w")
+        lk.release_write()
+
+    def reader():
+        lk.acquire_read()
+        order.append("r")
+        lk.release_read()
+
+    tw = threading.Thread(target=writer)
+    tw.start()
+    time.sleep(0.05)                        # the writer is now waiting on the first reader
+    tr = threading.Thread(target=reader)
+    tr.start()
+    time.sleep(0.05)
+    assert order == []                      # the new reader did not overtake the writer
+    lk.release_read()
+    tw.join(5)
+    tr.join(5)
+    assert order == ["w", "r"]

@@ -92,7 +92,11 @@ def test_gemm(M, N, K, epi, tile):
                       {0: 8, 2: 0, 3: 3, 10: 8, 16: 8}[tile])
     hip().gemm_resln_config(8 if tile == 16 else 16)
     hip().gemm_lt_config(0)   # this repo's tiles for every shape (the default sends the wide
-    try:                      # plain projections to hipBLASLt: test_gemm_hipblaslt_route)
+    # plain projections to hipBLASLt: test_gemm_hipblaslt_route); the skinny split-K path off, so
+    # the M <= 256 shapes exercise the tiled kernels' ragged small-M handling (test_gemm_skinny
+    # covers the skinny path)
+    hip().gemm_skinny_config(0)
+    try:
         out = gemm(a := _bf(M, K, seed=1), w := _bf(N, K, scale=1.0 / math.sqrt(K), seed=2),
                    bias := _f(N, scale=0.5, seed=3), epi,
                    res := (_bf(M, N, seed=4) if epi in (2, 3) else None),
@@ -102,6 +106,7 @@ def test_gemm(M, N, K, epi, tile):
         hip().gemm_config(128, 3, 8)
         hip().gemm_resln_config(16)
         hip().gemm_lt_config(1)
+        hip().gemm_skinny_config(256)
     ref = R.gemm_ref(a, w, bias, epi, res, g, b, 1e-12)
     _close(out, ref, atol=4e-2, rtol=2e-2, what=f"gemm epi={epi}")
 
