@@ -7,32 +7,35 @@ One STEP = the system's ingest+search cycle on every rank (one process per GPU):
   3. upsert the 256 unit embeddings into this rank's HBM index shard
   4. semantic search: the 256 new embeddings are the queries; all_gather the queries of all
      ranks, EXACT top-10 over the rank's shard of the 100M x 384 bf16 corpus, all_to_all the
-     partial top-k back to each query's owner and merge.  The exact top-10 is found by an int8
-     MFMA scan of an int8 image of the rows that prunes only rows whose score provably cannot
-     reach the query's k-th best (Cauchy-Schwarz bound on the quantisation error, tracked at
-     every write), and the survivors are re-scored in bf16 (csrc/hip/index_i8.hip): the same
-     rows and scores as scanning every row in bf16 (GPU tests compare them); --index-prune none
-     runs that full bf16 scan.
+     partial top-k back to each query's owner and merge.  The exact top-10 is found by a
+     streaming MFMA scan of an int8 or MX-fp4 image of the rows (csrc/hip/index_stream.hip) that
+     prunes only rows whose score provably cannot reach the query's k-th best (Cauchy-Schwarz
+     bound on the quantisation error, tracked at every write); the survivors are re-scored in
+     bf16: the same rows and scores as scanning every row in bf16 (GPU tests compare them;
+     --opt index_prune=none runs that full bf16 scan).
 So every step embeds 256*N sentences AND answers 256*N top-10 queries over the full 100M-row
 corpus: value = embeds/s = top-k QPS (whole job).  Per-rank work is constant in N ("weak").
+After the timed steps the same line also reports the held-out search rate (heldout_topk_qps:
+fresh queries drawn from the corpus distribution, never inserted, on the same shard).
 
 Data: synthetic token ids, random-init weights (real MiniLM-L6 architecture), random unit
 index rows -- there is no network for checkpoints or datasets.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--opt KEY=VALUE ...]
        N > 1 either under a launcher (python -m torch.distributed.run --nproc-per-node N ...
        bench.py --gpus N: WORLD_SIZE is set) or plainly: with WORLD_SIZE unset this process
        launches the N ranks itself as fresh child processes BEFORE touching the GPU (one per GPU,
        env:// rendezvous on 127.0.0.1) and exits with the first failing rank's status.  A rank
        whose world differs from --gpus exits non-zero; the JSON carries the backend, the world
        and a startup collective self-check (all_gather of rank ids + device ids, verified).
-       --device cpu: the same step on the CPU over gloo (fp32 PyTorch encoder, tiny shapes) --
-       the multi-rank contract rehearsal the CPU tests run; never a performance number.
+       --opt device=cpu: the same step on the CPU over gloo (fp32 PyTorch encoder, tiny shapes)
+       -- the multi-rank contract rehearsal the CPU tests run; never a performance number.
 
 The other BASELINE.json configs run through the same step (benchmarks/suite.py drives them):
   --mode embed                                   all-MiniLM-L6-v2 bf16 embedding, batch 256
   --mode search                                  100M x 384 sharded cosine top-k
-  --model bge-base --mode embed                  bge-base-en-v1.5 DP embedding
+  --model bge-base --mode embed --opt embed_dp=group
+                                                 bge-base-en-v1.5 DP embedding over RCCL
   --model e5-large --index-dtype fp8 --index-rows 1000000000
                                                  e5-large-v2 + 1B-vector fp8 index (1B/N rows
                                                  per rank: needs N >= 4 for 1 TB; smaller N
@@ -111,8 +114,50 @@ def self_launch(n: int, argv: list[str]) -> int:
     return rc
 
 
+# Secondary knobs: --opt KEY=VALUE (repeatable).  The defaults are the headline configuration;
+# the JSON line's config lists every knob set away from its default.
+OPTS = {
+    "device": ("auto", str, "auto | cuda | cpu (cpu: the multi-rank contract rehearsal over gloo "
+                            "with the fp32 PyTorch encoder and tiny shapes; never a performance "
+                            "number)"),
+    "clusters": (100_000, int, "--corpus clustered: shared cluster centers"),
+    "cluster_spread": (0.6, float, "--corpus clustered: noise norm around a center "
+                                   "(cos ~ 1/sqrt(1+s^2))"),
+    "embed_dp": ("replica", str, "--mode embed, N > 1: replica (independent ranks) | group (ONE "
+                                 "global batch of batch*N sentences split over the ranks and "
+                                 "gathered to rank 0 over RCCL, parallel/embed_group.py)"),
+    "simulate_world": (0, int, "PROJECTION on one GPU: the per-rank work of the N-GPU step (a "
+                               "100M/N shard, 256*N gathered queries); the JSON says SIMULATED"),
+    "timeline": ("", str, "write per-step GPU times (+ sampled clock/power) to this JSONL file"),
+    "heldout_searches": (20, int, "--mode full: after the timed steps, time this many searches of "
+                                  "fresh held-out queries (drawn from the corpus distribution, "
+                                  "never inserted) on the same shard: heldout_topk_qps"),
+    "index_prefilter": ("none", str, "none | fp8 (e4m3 copy for 3k candidates + exact bf16 "
+                                     "rescore; Qdrant quantization + rescore)"),
+    "index_prune": ("i8", str, "i8 (EXACT pruned search: int8 / MX-fp4 stream scan of a "
+                               "bound-checked image + bf16 re-score) | none (full bf16 scan)"),
+    "overlap": (1, int, "--mode full: encode batch i+1 on a second stream while batch i is "
+                        "searched (0: back to back on one stream)"),
+    "search_pipeline": (1, int, "--mode full: run batch i+1's query-side search work under "
+                                "batch i's scan on a third stream"),
+    "encode_ahead": (2, int, "pipelined step: batch i + AHEAD is encoded during step i (1 | 2)"),
+    "graph": (1, int, "--mode embed: replay a captured hipGraph of the encoder forward"),
+    "prune_sample_shift": (0, int, "exact pruned search: threshold sample = 1 tile in 2^shift "
+                                   "(0 = the shard default)"),
+    "prune_block_frac": (0.0, float, "exact pruned search: route a row block to the bf16 scan "
+                                     "above this share of the candidate slots (0 = default)"),
+}
+
+
+def _opts_help() -> str:
+    return "secondary knobs, KEY=VALUE (repeatable): " + "; ".join(
+        f"{k} (default {d!r}): {h}" for k, (d, _, h) in OPTS.items())
+
+
 def parse_args(argv=None):
-    ap = argparse.ArgumentParser()
+    ap = argparse.ArgumentParser(
+        description="Headline benchmark: MiniLM-L6 embeds/s = exact top-10 QPS over 100M x 384",
+        epilog="--opt keys: " + ", ".join(OPTS))
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
@@ -122,15 +167,8 @@ def parse_args(argv=None):
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--model", default="minilm-l6")
     ap.add_argument("--mode", choices=["full", "embed", "search"], default="full")
-    ap.add_argument("--device", choices=["auto", "cuda", "cpu"], default="auto",
-                    help="cpu: contract rehearsal over gloo with the fp32 PyTorch encoder (tiny "
-                         "shapes; tests/test_bench_cpu.py), never a performance number")
     ap.add_argument("--corpus", choices=["random", "clustered", "anisotropic"], default="random",
                     help="synthetic index distribution (codename_symbiont_amd/index/synth.py)")
-    ap.add_argument("--clusters", type=int, default=100_000,
-                    help="--corpus clustered: shared cluster centers")
-    ap.add_argument("--cluster-spread", type=float, default=0.6,
-                    help="--corpus clustered: noise norm around a center (cos ~ 1/sqrt(1+s^2))")
     ap.add_argument("--queries", choices=["self", "heldout"], default=None,
                     help="full mode: self = the batch is upserted and THEN searched (default), "
                          "heldout = searched before it is upserted.  search mode: heldout = fresh "
@@ -139,91 +177,39 @@ def parse_args(argv=None):
     ap.add_argument("--verify", action="store_true",
                     help="after the timed steps, search one batch both ways (this config and the "
                          "full bf16 scan of every row) and report whether the ids are identical")
-    ap.add_argument("--timeline", default="",
-                    help="write per-step GPU times (+ sampled clock/power) to this JSONL file")
     ap.add_argument("--index-dtype", choices=["bf16", "fp8"], default="bf16")
-    ap.add_argument("--index-prefilter", choices=["none", "fp8"], default="none",
-                    help="fp8: search the bf16 index through an e4m3 copy for 3k candidates and "
-                         "re-score them exactly in bf16 (Qdrant quantization + rescore); the "
-                         "headline default is the exact bf16 scan")
-    ap.add_argument("--index-prune", choices=["none", "i8"], default="i8",
-                    help="i8: EXACT search through an int8 image of the bf16 rows -- rows whose "
-                         "int8 score cannot reach the query's k-th best (a proven error bound) are "
-                         "pruned, the rest re-scored in bf16 (csrc/hip/index_i8.hip); same top-k "
-                         "as the full bf16 scan")
-    ap.add_argument("--i8-tile-rows", type=int, choices=[64, 128], default=64,
-                    help="rows per tile of the int8 pruning scan")
-    ap.add_argument("--mx4-tile-rows", type=int, choices=[64, 128], default=128,
-                    help="MX-fp4 first-tier scan: rows per tile at 256 queries per workgroup")
-    ap.add_argument("--mlp-fused", type=int, choices=[0, 1, 2], default=1,
-                    help="384-wide encoders: the whole FFN block in one kernel (mlp_fused.hip, 1, "
-                         "default; profiles/r4_mlp/), with the out-projection too (2), or as two "
-                         "GEMMs (0)")
-    ap.add_argument("--i8-pair", type=int, choices=[0, 1], default=0,
-                    help="int8 scan: one emission pre-test over both sub-tiles of a fused chain "
-                         "before the per-sub-tile ones (1) or the per-sub-tile tests alone (0, "
-                         "default; profiles/r4_split/pair/)")
-    ap.add_argument("--i8-waves", type=int, choices=[4, 8], default=8,
-                    help="int8 pruning scan: 8-wave workgroups (one per CU) or 4 (two per CU)")
     ap.add_argument("--encoder-dtype", choices=["bf16", "fp8"], default="bf16",
                     help="fp8: e4m3 projection GEMMs (BASELINE config #5); the headline stays bf16")
-    ap.add_argument("--embed-dp", choices=["replica", "group"], default="replica",
-                    help="--mode embed, N > 1: independent replicas, or ONE global batch of "
-                         "batch*N sentences per step split over the ranks and gathered back to "
-                         "rank 0 over RCCL (parallel/embed_group.py; BASELINE config #4 over xGMI)")
-    ap.add_argument("--no-overlap", action="store_true",
-                    help="--mode full: run encode and search back to back on one stream instead of "
-                         "encoding batch i+1 on a second stream while batch i is searched")
-    ap.add_argument("--scan-cus", type=int, default=0,
-                    help="spread the index scans over this many CUs (0 = all), leaving the rest to "
-                         "the encoder running beside them on the second stream")
-    ap.add_argument("--scan-cu-reserve", type=int, default=0,
-                    help="--mode full: CU-partitioned streams (parallel/cu_partition.py): the scans "
-                         "run on a stream masked to all CUs but this many per XCD, the encoder and "
-                         "the query-side pre-pass on streams that always have those CUs")
-    ap.add_argument("--side-cus", choices=["all", "reserve"], default="all",
-                    help="--scan-cu-reserve: the side streams' CUs (the reserve only, or every CU)")
-    ap.add_argument("--search-priority", action="store_true",
-                    help="run the search (and the step's bookkeeping) on a high-priority stream so "
-                         "its short latency-bound kernels dispatch ahead of the encoder's")
-    ap.add_argument("--scan-min-tiles", type=int, default=16,
-                    help="smallest row block (64-row tiles) of the small list scans")
-    ap.add_argument("--prune-sample-shift", type=int, default=0,
-                    help="exact pruned search: threshold sample = 1 tile in 2^shift (0 = the "
-                         "shard default, HbmIndexShard.PRUNE_TILE_SHIFT)")
-    ap.add_argument("--prune-block-frac", type=float, default=0.0,
-                    help="exact pruned search: a row block goes to the bf16 scan when some query "
-                         "would emit more than this share of the candidate slots from it (0 = "
-                         "the shard default, HbmIndexShard.PRUNE_BLOCK_FRAC; >= 1 turns the "
-                         "per-block route off)")
-    ap.add_argument("--prepass-min-tiles", type=int, default=0,
-                    help="row-block floor of the sampled searches' small pre-pass list scans "
-                         "(0 = the shard default, 1 tile per workgroup)")
-    ap.add_argument("--encode-ahead", type=int, choices=[1, 2], default=2,
-                    help="pipelined step: batch i + AHEAD is encoded during step i (2: the "
-                         "encoder runs beside batch i + 1's pre-pass, before batch i + 1's scan; "
-                         "1: it queues behind batch i's scan)")
-    ap.add_argument("--scan-waits-encoder", type=int, choices=[0, 1], default=0,
-                    help="encode-ahead 2: batch i's scan also waits for batch i + 1's encoder, so "
-                         "that encoder runs beside batch i's pre-pass instead of being starved by "
-                         "the scan (which holds every CU) and finishing after it")
-    ap.add_argument("--no-search-pipeline", action="store_true",
-                    help="--mode full: run each batch's query-side search work (int8 queries, "
-                         "exact sample, thresholds) right before its scan instead of on a third "
-                         "stream under the previous batch's scan")
-    ap.add_argument("--simulate-world", type=int, default=0,
-                    help="PROJECTION on one GPU: run the per-rank work of the N-GPU step (a 100M/N "
-                         "shard, 256*N gathered queries of which 256*(N-1) are foreign embeddings, "
-                         "the result-sized all_to_all through a single-rank RCCL group, the merge). "
-                         "The JSON says 'SIMULATED' and n_gpus stays 1; not a scaling measurement")
-    ap.add_argument("--no-graph", action="store_true",
-                    help="launch the encoder's kernels eagerly every step instead of replaying a "
-                         "captured hipGraph of the forward")
+    ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE", help=_opts_help())
     args = ap.parse_args(argv)
+    opts = {k: d for k, (d, _, _) in OPTS.items()}
+    for kv in args.opt:
+        key, sep, val = kv.partition("=")
+        key = key.strip().replace("-", "_")
+        if not sep or key not in OPTS:
+            ap.error(f"--opt {kv!r}: expected KEY=VALUE with KEY in {sorted(OPTS)}")
+        try:
+            opts[key] = OPTS[key][1](val)
+        except ValueError:
+            ap.error(f"--opt {kv!r}: bad value")
+    if opts["device"] not in ("auto", "cuda", "cpu"):
+        ap.error("--opt device: auto | cuda | cpu")
+    if opts["embed_dp"] not in ("replica", "group"):
+        ap.error("--opt embed_dp: replica | group")
+    if opts["index_prefilter"] not in ("none", "fp8") or opts["index_prune"] not in ("none", "i8"):
+        ap.error("--opt index_prefilter: none | fp8; index_prune: i8 | none")
+    if opts["encode_ahead"] not in (1, 2):
+        ap.error("--opt encode_ahead: 1 | 2")
+    args.opts_changed = {k: v for k, v in opts.items() if v != OPTS[k][0]}
+    for k, v in opts.items():
+        setattr(args, k, v)
+    args.no_overlap = not opts["overlap"]
+    args.no_search_pipeline = not opts["search_pipeline"]
+    args.no_graph = not opts["graph"]
     if args.simulate_world == 1:
         args.simulate_world = 0
     if args.simulate_world and (args.gpus != 1 or args.mode == "embed"):
-        ap.error("--simulate-world projects the N-GPU search step on ONE GPU: --gpus 1, "
+        ap.error("--opt simulate_world projects the N-GPU search step on ONE GPU: --gpus 1, "
                  "--mode full or search")
     if args.queries is None:
         args.queries = "heldout" if args.mode == "search" else "self"
@@ -330,6 +316,30 @@ def metric_and_config(args, info, cfg, prune, prefilter, extra_cfg: dict):
     return metric, config, unit
 
 
+def scan_label(args, shard, prune, prefilter, dim: int, nq: int) -> str:
+    """What the per-rank search actually runs (the JSON's index_scan): the evidence trail, so it
+    names the kernel, the image and the exactness."""
+    from codename_symbiont_amd.index.shard import MQ_DIMS
+
+    if args.index_dtype == "fp8":
+        return ("fp8 index: the list scan (index_fp8.hip) of the e4m3 rows, exact top-k of the "
+                "stored fp8 rows")
+    if prefilter:
+        return "fp8 prefilter scan + exact bf16 re-score of 3k candidates"
+    if args.k > 16:
+        return ("bf16 emitting scan + radix select (exact, large k)" if dim in MQ_DIMS
+                else "bf16 list scan (exact)")
+    if prune:
+        if shard.stream and not shard._i8_heavy:
+            return ("exact pruned: int8 / MX-fp4 stream scan (index_stream.hip) of bound-checked "
+                    "images + bf16 re-score")
+        return ("exact pruned: " + ("split" if shard._i8_heavy else "int8") +
+                " LDS-ring scan (index_i8.hip) + bf16 re-score")
+    if shard.scan_mq and dim in MQ_DIMS and nq >= shard.mq_min_nq:
+        return f"bf16 emitting scan (index_mq.hip, {'512' if nq >= 512 else '256'} queries/WG)"
+    return "bf16 list scan (index_topk.hip, 256 queries/WG)"
+
+
 def result_line(args, info, comm, metric, unit, config, total, ms, prune, prefilter, data, extra):
     res = {
         "metric": metric,
@@ -345,8 +355,10 @@ def result_line(args, info, comm, metric, unit, config, total, ms, prune, prefil
         "dtype": args.encoder_dtype,
         "index_dtype": args.index_dtype,
         "index_prefilter": prefilter,
-        "index_search": ("exact: int8 bound-pruned scan + bf16 re-score" if prune
-                         else ("fp8 prefilter + bf16 re-score" if prefilter else "exact bf16 scan")),
+        "index_search": ("exact: bound-pruned scan + bf16 re-score" if prune
+                         else ("fp8 prefilter + bf16 re-score" if prefilter
+                               else ("exact scan of the e4m3 rows" if args.index_dtype == "fp8"
+                                     else "exact bf16 scan"))),
         "data": data,
         "config": config,
         "backend": comm["backend"],
@@ -383,7 +395,7 @@ def _data_txt(args) -> str:
 
 
 def _make_searcher(args, shard, info, embed):
-    """The step's sharded searcher; --simulate-world N: the per-rank work of the N-GPU search
+    """The step's sharded searcher; --opt simulate_world=N: the per-rank work of the N-GPU search
     on this one rank, the other ranks' queries stood in for by (N - 1) * batch foreign embeddings
     (``embed(n, seed)``: n fresh sentences through this encoder, never inserted here)."""
     from codename_symbiont_amd.parallel.sharded import ShardedSearcher, SimulatedShardedSearcher
@@ -443,10 +455,22 @@ def run_cpu(args, info, comm) -> int:
     elapsed = D.allreduce_max(info, time.perf_counter() - t0)
     ms = elapsed * 1000.0 / K
     total = B * info.world * K / elapsed
+    extra = {}
+    if args.mode == "full" and args.heldout_searches > 0:   # (the GPU run's held-out phase)
+        H = args.heldout_searches
+        hq = [gen.unit(B, 9000 + 10 * info.rank + i).bfloat16() for i in range(2)]
+        D.barrier(info)
+        t_h = time.perf_counter()
+        for i in range(H):
+            searcher.search(hq[i % 2], args.k)
+        D.barrier(info)
+        el_h = D.allreduce_max(info, time.perf_counter() - t_h)
+        extra = {"heldout_topk_qps": round(B * info.world * H / el_h, 2),
+                 "heldout_ms_per_search": round(el_h * 1000.0 / H, 3), "heldout_searches": H}
     metric, config, unit = metric_and_config(args, info, cfg, None, None, {"device": "cpu"})
     if info.rank == 0:
         print(result_line(args, info, comm, metric, unit, config, total, ms, None, None,
-                          _data_txt(args) + " (CPU rehearsal: not a performance number)", {}),
+                          _data_txt(args) + " (CPU rehearsal: not a performance number)", extra),
               flush=True)
     return 0
 
@@ -465,9 +489,6 @@ def run_gpu(args, info, comm) -> int:
 
     t0 = time.time()
     enc = HipEncoder(cfg, seed=0, device=dev, precision=args.encoder_dtype)
-    from codename_symbiont_amd.ops._ext import hip as _hip_ext
-
-    _hip_ext().mlp_fused_config(args.mlp_fused)
     vw = args.simulate_world or 0
     rows_per_rank = args.index_rows // (vw or info.world)
     extra = (K + W + 4) * B
@@ -484,17 +505,7 @@ def run_gpu(args, info, comm) -> int:
         fill_corpus(shard, gen, rows_per_rank, seed=100 + info.rank)
     searcher = _make_searcher(args, shard, info, lambda n, seed: enc.forward_packed(
         synthetic_batch(cfg, n, S, seed=seed).to(dev))[1].clone())
-    if prune:
-        from codename_symbiont_amd.ops._ext import hip as _hip
-
-        _hip().i8_config(args.i8_tile_rows, args.i8_waves)
-        _hip().i8_pair_config(args.i8_pair)
-        _hip().mx4_config(args.mx4_tile_rows)
     shard.mq_stats = os.environ.get("SYMB_MQ_STATS", "0") not in ("", "0") or args.mode == "search"
-    shard.scan_cus = args.scan_cus
-    shard.scan_min_tiles = args.scan_min_tiles
-    if args.prepass_min_tiles:
-        shard.prepass_min_tiles = args.prepass_min_tiles
     if args.prune_sample_shift:
         shard.PRUNE_TILE_SHIFT = shard.PRUNE_TILE_SHIFT_SPLIT = args.prune_sample_shift
         shard.PRUNE_TILE_SHIFT_MX4 = args.prune_sample_shift
@@ -520,21 +531,6 @@ def run_gpu(args, info, comm) -> int:
     dbuf = [host[0].to(dev), host[1].to(dev)]
     copy_stream = torch.cuda.Stream(dev)
     compute = torch.cuda.current_stream(dev)
-    if args.search_priority:
-        torch.cuda.synchronize(dev)
-        compute = torch.cuda.Stream(dev, priority=-1)
-        torch.cuda.set_stream(compute)
-    cu_part = None
-    if args.scan_cu_reserve and args.mode == "full":
-        from codename_symbiont_amd.parallel.cu_partition import CuPartition
-
-        torch.cuda.synchronize(dev)
-        cu_part = CuPartition(dev, args.scan_cu_reserve, side_all=args.side_cus == "all", n_side=2)
-        compute = cu_part.main
-        torch.cuda.set_stream(compute)
-        shard.scan_cus = cu_part.main_cus
-        log(info, f"[bench] CU partition: scans on {cu_part.main_cus} CUs, reserve "
-                  f"{len(cu_part.reserve)} CUs ({args.side_cus} for the encoder / pre-pass)")
     copy_done = [torch.cuda.Event(), torch.cuda.Event()]
     consumed = [torch.cuda.Event(), torch.cuda.Event()]
     host_free = [torch.cuda.Event() for _ in range(NB)]   # host slot's H2D copy has finished
@@ -545,7 +541,7 @@ def run_gpu(args, info, comm) -> int:
     # power-bound; the encoder's small kernels fill its tail and launch gaps).  Every timed step
     # still encodes one batch and searches one batch.
     overlap = args.mode == "full" and not group_dp and not args.no_overlap
-    enc_stream = torch.cuda.Stream(dev) if cu_part is None else cu_part.sides[0]
+    enc_stream = torch.cuda.Stream(dev)
     # output slots: batch i's embeddings live in outs[i % NO] from its encode to its search's end
     pipeline = overlap and args.queries == "self" and not args.no_search_pipeline
     AHEAD = args.encode_ahead if pipeline else 1
@@ -652,7 +648,7 @@ def run_gpu(args, info, comm) -> int:
     # work (upsert, int8 queries, the exact threshold sample, route) runs on pre_stream as soon
     # as it is encoded, under batch i's full-shard scan; the compute stream only runs the scans
     # back to back (ShardedSearcher.begin / end, HbmIndexShard.search_begin / search_end).
-    pre_stream = torch.cuda.Stream(dev) if cu_part is None else cu_part.sides[1]
+    pre_stream = torch.cuda.Stream(dev)
     pre_done = [torch.cuda.Event() for _ in range(NO)]
     handles: dict = {}
 
@@ -675,8 +671,6 @@ def run_gpu(args, info, comm) -> int:
         begin_search(i + 1)
         t2 = time.perf_counter()
         compute.wait_event(pre_done[slot])
-        if AHEAD == 2 and args.scan_waits_encoder:
-            compute.wait_event(enc_done[(i + 1) % NO])
         if ev:
             ev[2].record(compute)
         searcher.end(handles.pop(i))
@@ -801,6 +795,8 @@ def run_gpu(args, info, comm) -> int:
         extra_out["step_ms_last_decile"] = round((ends[-1] - ends[-q - 1]) / q, 3) if K > q else None
         if clocks:
             extra_out["sclk_mhz_samples"] = [c[1] for c in clocks][:: max(1, len(clocks) // 20)]
+    if shard._mx4_tot is not None and args.mode != "embed":   # batches the MX-fp4 tier served
+        extra_out["search_mx4_tier_batches"] = int(shard._mx4_tot.item())
     if shard._mq_tot is not None and args.mode != "embed":
         ovf = int(shard._mq_tot[0].item())
         extra_out["search_overflow_batches"] = ovf
@@ -809,14 +805,36 @@ def run_gpu(args, info, comm) -> int:
         if len(shard._mq_tot) > 4:   # searches that sent only some row blocks to the bf16 scan
             extra_out["search_block_route_batches"] = int(shard._mq_tot[3].item())
             extra_out["search_block_routed_blocks"] = int(shard._mq_tot[4].item())
-        if shard._mx4_tot is not None:   # batches whose first tier was the MX-fp4 scan
-            extra_out["search_mx4_tier_batches"] = int(shard._mx4_tot.item())
-        if shard.rows_i8 is not None:   # the pruning image's form (HbmIndexShard.calibrate_prune)
+        if shard.prune_on:   # the pruning image's form (HbmIndexShard.calibrate_prune)
             extra_out["i8_image"] = "split" if shard._i8_heavy else "plain"
             extra_out["i8_calib_share"] = (None if shard.calib_share is None
                                            else round(shard.calib_share, 3))
         print(f"[bench] rank {info.rank} searches: {ovf} overflowed, max "
               f"{int(shard._mq_tot[1].item())} candidates per query", file=sys.stderr, flush=True)
+    if args.mode == "full" and args.heldout_searches > 0:
+        # the realistic search rate beside the headline: fresh held-out queries (drawn from the
+        # corpus distribution, never inserted -- the reference serves arbitrary user text,
+        # api_service/src/main.rs:272-512) searched on the same shard after the timed steps
+        H = args.heldout_searches
+        hq = [gen.unit(B, 9000 + 10 * info.rank + i).bfloat16() for i in range(4)]
+        for i in range(2):   # (the sample density adapts to the tier the last searches took)
+            searcher.search(hq[i % 4], args.k)
+        torch.cuda.synchronize(dev)
+        D.barrier(info)
+        torch.cuda.synchronize(dev)
+        mx_before = int(shard._mx4_tot.item()) if shard._mx4_tot is not None else None
+        t_h = time.perf_counter()
+        for i in range(H):
+            searcher.search(hq[i % 4], args.k)
+        torch.cuda.synchronize(dev)
+        D.barrier(info)
+        torch.cuda.synchronize(dev)
+        el_h = D.allreduce_max(info, time.perf_counter() - t_h)
+        extra_out["heldout_topk_qps"] = round(B * info.world * H / el_h, 2)
+        extra_out["heldout_ms_per_search"] = round(el_h * 1000.0 / H, 3)
+        extra_out["heldout_searches"] = H
+        if mx_before is not None:
+            extra_out["heldout_mx4_tier_batches"] = int(shard._mx4_tot.item()) - mx_before
     if args.verify and args.mode != "embed":
         q = qsets[0] if args.mode == "search" else outs[0][1] if overlap else out_unit
         s1, i1 = searcher.search(q, args.k)
@@ -844,33 +862,15 @@ def run_gpu(args, info, comm) -> int:
         extra_out["verify_ids_identical"] = n_mism == 0
         extra_out["verify_id_mismatches_all_ties"] = ties_only
         extra_out["verify_max_score_diff"] = d_s
-    metric, config, unit = metric_and_config(args, info, cfg, prune, prefilter, {
-        "_group_dp": group_dp,
-        "encode_search_overlap": overlap,
-        "search_pipeline": pipeline,
-        "encode_ahead": AHEAD,
-        "scan_waits_encoder": bool(AHEAD == 2 and args.scan_waits_encoder),
-        # per-rank scan kernel: the emitting MFMA scan (csrc/hip/index_mq.hip) for >= 256
-        # seeded queries (512 per workgroup at >= 512), else the 256-query list kernel
-        "index_scan": (("int8-pruned-" if prune else "emitting-")
-                       + ("512q" if B * (vw or info.world) >= 512 else "256q"))
-                      if (shard.scan_mq and args.index_dtype == "bf16" and cfg.hidden in MQ_DIMS
-                          and B * (vw or info.world) >= shard.mq_min_nq and args.k <= 16)
-                      else ("emitting-large-k" if (args.index_dtype == "bf16" and 16 < args.k <= 128
-                                                   and cfg.hidden in MQ_DIMS) else "list-256q"),
-        "encoder_hipgraph": use_graph,
-        "search_priority": args.search_priority,
-        "scan_cu_reserve_per_xcd": args.scan_cu_reserve,
-        "i8_pair_pretest": args.i8_pair if prune else None,
-        "mlp_fused": args.mlp_fused,
-        "mx4_tile_rows": args.mx4_tile_rows if prune else None,
-        "scan_min_tiles": args.scan_min_tiles,
-        "prepass_min_tiles": shard.prepass_min_tiles,
-        "prune_sample_shift": ((shard.PRUNE_TILE_SHIFT_SPLIT if shard._i8_heavy
-                                else shard.PRUNE_TILE_SHIFT) if prune else None),
-        "prune_block_frac": shard.PRUNE_BLOCK_FRAC if prune else None,
-        "prune_sample_shift_mx4_tier": shard.PRUNE_TILE_SHIFT_MX4 if prune else None,
-    })
+    cfg_extra = dict(args.opts_changed)
+    cfg_extra.pop("timeline", None)
+    if args.mode != "embed":
+        cfg_extra["index_scan"] = scan_label(args, shard, prune, prefilter, cfg.hidden,
+                                             B * (vw or info.world))
+    if use_graph:
+        cfg_extra["encoder_hipgraph"] = True
+    metric, config, unit = metric_and_config(args, info, cfg, prune, prefilter,
+                                             dict(cfg_extra, _group_dp=group_dp))
     if info.rank == 0:
         print(result_line(args, info, comm, metric, unit, config, total, ms, prune, prefilter,
                           _data_txt(args), extra_out), flush=True)

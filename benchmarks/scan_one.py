@@ -1,9 +1,14 @@
 #!/usr/bin/env python3
-"""Repeat the int8-pruned search's full-shard scan kernel (index_scan_i8_kernel) on the inputs one
-real search prepared -- the target of rocprofv3 --pmc passes (benchmarks/pmc_kernel.py
---match index_scan_i8).
+"""Repeat the pruned search's full-shard first-pass scan on the inputs one real search prepared --
+the target of timing A/Bs and rocprofv3 --pmc passes (benchmarks/pmc_kernel.py --match scan).
 
     python benchmarks/scan_one.py [--rows 25000000] [--nq 256] [--corpus random] [--iters 10]
+                                  [--tier i8|mx4] [--queries heldout|self]
+
+The shard's scan is the stream scan (index_stream.hip) unless SYMB_PRUNE_STREAM=0 (the round-4
+LDS-ring scan, index_i8.hip).  --tier mx4 times the MX-fp4 first tier on the same block grid with
+the thresholds the tier choice computed (--queries self: stored rows as queries, whose k-th
+scores sit far above the bulk, as in the headline).
 """
 from __future__ import annotations
 
@@ -22,31 +27,77 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=25_000_000)
     ap.add_argument("--nq", type=int, default=256)
+    ap.add_argument("--dim", type=int, default=384)
     ap.add_argument("--corpus", default="random")
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--tier", choices=["i8", "mx4"], default="i8")
+    ap.add_argument("--queries", choices=["heldout", "self"], default="heldout")
+    ap.add_argument("--variant", type=int, default=-1, help="stream MX-fp4 form (stream_config)")
     a = ap.parse_args()
-    from codename_symbiont_amd.index.shard import HbmIndexShard
+    from codename_symbiont_amd.index.shard import STREAM_SUB, HbmIndexShard
     from codename_symbiont_amd.index.synth import CorpusGen, fill_corpus
     from codename_symbiont_amd.ops._ext import hip, stream_handle
 
-    gen = CorpusGen(a.corpus, 384, "cuda")
-    shard = HbmIndexShard(384, a.rows + 8192, device="cuda", prune="i8")
+    h, st = hip(), stream_handle()
+    if a.variant >= 0:
+        h.stream_config(a.variant)
+    gen = CorpusGen(a.corpus, a.dim, "cuda")
+    shard = HbmIndexShard(a.dim, a.rows + 8192, device="cuda", prune="i8")
+    t0 = time.perf_counter()
     fill_corpus(shard, gen, a.rows, seed=1)
-    q = gen.unit(a.nq, seed=7).bfloat16()
+    torch.cuda.synchronize()
+    fill_s = time.perf_counter() - t0
+    if a.queries == "self":
+        idx = torch.randint(0, a.rows, (a.nq,), device="cuda")
+        q = shard.rows[idx].clone()
+    else:
+        q = gen.unit(a.nq, seed=7).bfloat16()
     shard.mq_stats = True
     shard.search(q, 10)
     torch.cuda.synchronize()
     P, n = shard._pruned_last, shard.visible
-    h, st = hip(), stream_handle()
     rsplit = 2 if a.nq < 512 else 1
-    heavy = shard._i8_heavy
+    heavy = P["heavy"]
+    m4 = P["m4"]
+    if a.tier == "mx4" and m4 is None:
+        raise SystemExit("no MX-fp4 tier on this shard")
+    nbytes = 0
 
     def scan():
-        h.index_scan_i8(shard.rows_i8.data_ptr(), shard.sx_i8.data_ptr(), n, shard.rows_i8.shape[0],
-                        P["rows_per_blk"], P["n_rblk"], P["q8"].data_ptr(), a.nq, P["thr"].data_ptr(),
-                        P["cs"].data_ptr(), P["ci"].data_ptr(), P["cnt"].data_ptr(), P["cap"], 1, st,
-                        rsplit, heavy=heavy, sq=P["sq"].data_ptr() if heavy else 0)
+        if a.tier == "mx4":
+            P["cnt"].zero_()
+            if shard.img_mx4 is not None:
+                h.index_scan_stream(shard.img_mx4.data_ptr(), n, shard.img_mx4.shape[0] * STREAM_SUB,
+                                    P["rows_per_blk"], P["n_rblk"], m4["q4"].data_ptr(),
+                                    m4["qs4"].data_ptr(), a.nq, m4["thr4"].data_ptr(),
+                                    P["cs"].data_ptr(), P["ci"].data_ptr(), P["cnt"].data_ptr(),
+                                    P["cap"], 1, st, dim=a.dim, form=1)
+            else:
+                h.index_scan_i8(shard.rows_mx4.data_ptr(), shard.sc_mx4.data_ptr(), n,
+                                shard.rows_mx4.shape[0], P["rows_per_blk"], P["n_rblk"],
+                                m4["q4"].data_ptr(), a.nq, m4["thr4"].data_ptr(), P["cs"].data_ptr(),
+                                P["ci"].data_ptr(), P["cnt"].data_ptr(), P["cap"], 1, st, rsplit,
+                                dim=a.dim, sq=m4["qs4"].data_ptr(), form=1)
+        elif shard.img_i8 is not None and not heavy:
+            h.index_scan_stream(shard.img_i8.data_ptr(), n, shard.img_i8.shape[0] * STREAM_SUB,
+                                P["rows_per_blk"], P["n_rblk"], P["q8"].data_ptr(), 0, a.nq,
+                                P["thr"].data_ptr(), P["cs"].data_ptr(), P["ci"].data_ptr(),
+                                P["cnt"].data_ptr(), P["cap"], 1, st, dim=a.dim, form=0)
+        else:
+            h.index_scan_i8(shard.rows_i8.data_ptr(), shard.sx_i8.data_ptr(), n,
+                            shard.rows_i8.shape[0], P["rows_per_blk"], P["n_rblk"],
+                            P["q8"].data_ptr(), a.nq, P["thr"].data_ptr(), P["cs"].data_ptr(),
+                            P["ci"].data_ptr(), P["cnt"].data_ptr(), P["cap"], 1, st, rsplit,
+                            dim=a.dim, heavy=heavy, sq=P["sq"].data_ptr() if heavy else 0)
 
+    if a.tier == "mx4":
+        nbytes = (shard.img_mx4.shape[1] / STREAM_SUB if shard.img_mx4 is not None
+                  else a.dim // 2 + 16)
+        kernel = "stream-mx4" if shard.img_mx4 is not None else "ldsring-mx4"
+    elif shard.img_i8 is not None and not heavy:
+        nbytes, kernel = shard.img_i8.shape[1] / STREAM_SUB, "stream-i8"
+    else:
+        nbytes, kernel = shard.rows_i8.shape[1] + 4, "ldsring-" + ("split" if heavy else "i8")
     scan()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -54,10 +105,12 @@ def main() -> None:
         scan()
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / a.iters
-    print(json.dumps({"bench": "scan_one", "rows": n, "nq": a.nq, "corpus": a.corpus,
-                      "image": "split" if heavy else "plain", "ms": round(ms, 3),
-                      "row_bytes_TBps": round(n * shard.rows_i8.shape[1] / ms / 1e9, 2),
-                      "cand_max": int(P["cnt"].max())}))
+    print(json.dumps({"bench": "scan_one", "kernel": kernel, "rows": n, "nq": a.nq, "dim": a.dim,
+                      "corpus": a.corpus, "queries": a.queries, "image": "split" if heavy else "plain",
+                      "ms": round(ms, 3), "TBps": round(n * nbytes / ms / 1e9, 2),
+                      "n_rblk": P["n_rblk"], "rows_per_blk": P["rows_per_blk"],
+                      "cand_mean": round(float(P["cnt"].float().mean()), 1),
+                      "cand_max": int(P["cnt"].max()), "fill_s": round(fill_s, 1)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -7,7 +7,7 @@ Configs (BASELINE.md "Measured" table):
   1 markov          Markov text generation over NATS (CPU)         benchmarks/markov_nats.py
   2 minilm-embed    all-MiniLM-L6-v2 bf16 embedding, batch 256      bench.py --mode embed
   3 index-100m      100M x 384 sharded cosine top-10                bench.py --mode search
-  4 bge-dp          bge-base-en-v1.5 DP embedding over RCCL         bench.py --model bge-base --mode embed --embed-dp group
+  4 bge-dp          bge-base-en-v1.5 DP embedding over RCCL         bench.py --model bge-base --mode embed --opt embed_dp=group
   5 e5-fp8          e5-large-v2 + fp8 index (1B rows at N >= 4)     bench.py --model e5-large --index-dtype fp8
   + headline        MiniLM embed + top-10 over 100M x 384           bench.py
   + mpnet-embed     the reference's own model (paraphrase-multilingual-mpnet-base-v2, 768-d)
@@ -68,7 +68,7 @@ def main():
         ("index-100m", launch + common + ["--mode", "search"], 900),
         # N > 1: one global batch per step split over the GPUs and gathered back over RCCL
         ("bge-dp", launch + common + ["--model", "bge-base", "--mode", "embed",
-                                      "--embed-dp", "group"], 600),
+                                      "--opt", "embed_dp=group"], 600),
         ("e5-fp8", launch + common + ["--model", "e5-large", "--index-dtype", "fp8",
                                       "--encoder-dtype", "fp8", "--index-rows", str(fp8_rows)], 1200),
         ("headline", launch + common, 900),

@@ -137,7 +137,11 @@ MQ_DIMS = (384, 768, 1024)              # ... the emitting bf16 scan (index_mq.h
 PRUNE_DIMS = (384, 768)                 # ... the int8-pruned scan (index_i8.hip)
 SPLIT_DIMS = (384,)                     # ... its split image (calibrate_prune)
 SPLIT_HEAVY = 64                        # leading components the split image keeps as fp16
-MX4_DIMS = (384,)                       # ... the MX-fp4 first tier (index_i8.hip HK = MX4)
+MX4_DIMS = (384, 768)                   # ... the MX-fp4 first tier (384-only on the LDS-ring scan)
+# widths of the streaming pruning scan (index_stream.hip): fragment-major int8 / MX-fp4 images,
+# one wave per SIMD, no LDS ring (SYMB_PRUNE_STREAM=0: the round-4 LDS-ring scan, index_i8.hip)
+STREAM_DIMS = (384, 768)
+STREAM_SUB = 32                         # rows per sub-tile record of the stream images
 
 
 class HbmIndexShard:
@@ -194,23 +198,36 @@ class HbmIndexShard:
         self._calib_gen = 0
         self._calib_next = self.CALIB_MIN_ROWS
         self.calib_share = None      # variance share of the leading components at calibration
+        # the stream images (index_stream.hip) for the plain int8 form and the MX-fp4 tier:
+        # [n_sub, REC] bytes, 32-row sub-tiles in fragment-major order (img_i8 / img_mx4)
+        self.stream = bool(prune) and dim in STREAM_DIMS and os.environ.get(
+            "SYMB_PRUNE_STREAM", "1") not in ("", "0")
+        self.img_i8 = self.img_mx4 = None
         if prune:
             # padded to whole 128-row tiles: the int8 scan's DMA reads whole tiles; one flat byte
-            # store sized for the split form's wider rows where it applies (viewed per form)
+            # store sized for the widest form that applies (viewed per form)
             n_alloc = _round_up(self.rows.shape[0], 128)
             rb = dim + SPLIT_HEAVY if dim in SPLIT_DIMS else dim
-            self._i8_store = torch.zeros(n_alloc * rb, dtype=torch.int8, device=self.device)
-            self.rows_i8 = self._i8_store[:n_alloc * dim].view(n_alloc, dim)
+            nbytes = n_alloc * rb
+            if self.stream:
+                nbytes = max(nbytes, n_alloc // STREAM_SUB * self._stream_rec(0))
+            self._i8_store = torch.zeros(nbytes, dtype=torch.int8, device=self.device)
             self.sx_i8 = torch.ones(n_alloc, dtype=torch.float32, device=self.device)
+            self._set_i8_view(0)
             # (E, X) of the plain form; (E_l, X_l, E_h, X_h) of the split form
             self.i8_bounds = torch.zeros(4, dtype=torch.float32, device=self.device)
         # the MX-fp4 image (a first tier below the int8 one, _pruned_end): 192 bytes of e2m1
         # nibbles + 16 bytes of block scales per 384-wide row, and its (E4, X4) maxima
         self.rows_mx4 = self.sc_mx4 = self.mx4_bounds = None
-        if prune and dim in MX4_DIMS and os.environ.get("SYMB_PRUNE_MX4", "1") not in ("", "0"):
+        if (prune and dim in (MX4_DIMS if self.stream else (384,))
+                and os.environ.get("SYMB_PRUNE_MX4", "1") not in ("", "0")):
             n_alloc = _round_up(self.rows.shape[0], 128)
-            self.rows_mx4 = torch.zeros(n_alloc, dim // 2, dtype=torch.uint8, device=self.device)
-            self.sc_mx4 = torch.zeros(n_alloc, 16, dtype=torch.uint8, device=self.device)
+            if self.stream:
+                self.img_mx4 = torch.zeros(n_alloc // STREAM_SUB, self._stream_rec(1),
+                                           dtype=torch.uint8, device=self.device)
+            else:
+                self.rows_mx4 = torch.zeros(n_alloc, dim // 2, dtype=torch.uint8, device=self.device)
+                self.sc_mx4 = torch.zeros(n_alloc, 16, dtype=torch.uint8, device=self.device)
             self.mx4_bounds = torch.zeros(2, dtype=torch.float32, device=self.device)
         self.count = 0      # rows reserved (payload slots exist)
         # rows searches may read: published only after their writes are ENQUEUED on the stream
@@ -250,6 +267,7 @@ class HbmIndexShard:
         self.i8_rsplit2 = False
         self._mq_tot = None
         self._mx4_tot = None     # searches whose first tier was the MX-fp4 scan (mq_stats)
+        self.tier_stats = True   # ... counted even without mq_stats (one tiny add per search)
         self._mx4_last = None
         # the tier recent searches took, read back without a sync: (pinned int, event) of each
         # search's MX-fp4 flag, and the last one known to have landed (True: the fp4 tier ran)
@@ -261,6 +279,140 @@ class HbmIndexShard:
         self._persisted = 0
         self._dirty: set[int] = set()
         self._persist_key = None
+
+    # ------------------------------------------------------------------ pruning images
+    def _stream_rec(self, form: int) -> int:
+        """Bytes per 32-row sub-tile of the stream image (form 0 = int8, 1 = MX-fp4); the same
+        numbers as index_stream.hip SDim (checked against the extension on a GPU)."""
+        nks = self.dim // (64 if form else 32)
+        return nks * 1024 + ((nks + 3) // 4 * 256 if form else 128)
+
+    def _set_i8_view(self, heavy: int) -> None:
+        """Views of the flat int8 store for the form: the stream image (plain form on a stream
+        shard) or the row-major image [n_alloc, D + heavy] (split form, or stream off)."""
+        n_alloc = self.sx_i8.shape[0]
+        if self.stream and not heavy:
+            rec = self._stream_rec(0)
+            self.img_i8 = self._i8_store[:n_alloc // STREAM_SUB * rec].view(torch.uint8).view(
+                n_alloc // STREAM_SUB, rec)
+            self.rows_i8 = None
+        else:
+            rb = self.dim + heavy
+            self.img_i8 = None
+            self.rows_i8 = self._i8_store[:n_alloc * rb].view(n_alloc, rb)
+
+    @property
+    def prune_on(self) -> bool:
+        """The shard keeps a pruning image (prune="i8")."""
+        return self.i8_bounds is not None
+
+    @property
+    def mx4_on(self) -> bool:
+        """The shard keeps the MX-fp4 first-tier image."""
+        return self.mx4_bounds is not None
+
+    def _stream_subtiles_cpu(self, img, form: int, r0: int, r1: int) -> None:
+        """CPU backend: recompute the stream records of the sub-tiles covering rows [r0, r1) from
+        the bf16 rows (per-row images: the other rows' bytes come out unchanged)."""
+        from ..ops import reference as R
+
+        g0, g1 = r0 // STREAM_SUB, (r1 + STREAM_SUB - 1) // STREAM_SUB
+        hi = min(g1 * STREAM_SUB, self.count)
+        src = self.rows[g0 * STREAM_SUB:hi]
+        if form:
+            rec, nr = R.stream_mx4_ref(src)
+            w = nr[r0 - g0 * STREAM_SUB:r1 - g0 * STREAM_SUB]
+            torch.maximum(self.mx4_bounds, w[:, :2].amax(0), out=self.mx4_bounds)
+        else:
+            rec, err, xtn = R.stream_i8_ref(src)
+            a, b = r0 - g0 * STREAM_SUB, r1 - g0 * STREAM_SUB
+            torch.maximum(self.i8_bounds[:2], torch.stack([err[a:b].max(), xtn[a:b].max()]),
+                          out=self.i8_bounds[:2])
+        img[g0:g0 + rec.shape[0]] = rec
+
+    def _image_rows(self, r0: int = 0, n: int = 0, rows=None) -> None:
+        """(Re)write the pruning images (int8 / split form and MX-fp4) of bf16 rows [r0, r0 + n)
+        or of the listed rows (a distinct int tensor), bounds raised."""
+        if rows is not None:
+            rows = torch.as_tensor(rows).to(self.device, torch.int32).contiguous()
+            n = rows.numel()
+        if n <= 0:
+            return
+        gpu = self.device.type == "cuda"
+        if gpu:
+            from ..ops._ext import hip, stream_handle
+
+            h, st = hip(), stream_handle(self.device)
+            rp = 0 if rows is None else rows.data_ptr()
+        if self.prune_on:
+            if self.img_i8 is not None:
+                if gpu:
+                    h.quant_stream_i8(self.rows.data_ptr(), r0, rp, n, self.dim,
+                                      self.img_i8.data_ptr(), self.i8_bounds.data_ptr(), st)
+                elif rows is None:
+                    self._stream_subtiles_cpu(self.img_i8, 0, r0, r0 + n)
+                else:
+                    for r in rows.tolist():
+                        self._stream_subtiles_cpu(self.img_i8, 0, r, r + 1)
+            elif rows is None:
+                self._i8_image(self.rows[r0:r0 + n], self.rows_i8[r0:r0 + n],
+                               self.sx_i8[r0:r0 + n], self.i8_bounds)
+            else:
+                ri = rows.long()
+                img = torch.empty(n, self.rows_i8.shape[1], dtype=torch.int8, device=self.device)
+                sc = torch.empty(n, dtype=torch.float32, device=self.device)
+                self._i8_image(self.rows[ri], img, sc, self.i8_bounds)
+                self.rows_i8.index_copy_(0, ri, img)
+                self.sx_i8.index_copy_(0, ri, sc)
+        if self.mx4_on:
+            if self.img_mx4 is not None:
+                if gpu:
+                    h.quant_stream_mx4(self.rows.data_ptr(), r0, rp, n, self.dim,
+                                       self.img_mx4.data_ptr(), 0, 0, self.mx4_bounds.data_ptr(),
+                                       0, st)
+                elif rows is None:
+                    self._stream_subtiles_cpu(self.img_mx4, 1, r0, r0 + n)
+                else:
+                    for r in rows.tolist():
+                        self._stream_subtiles_cpu(self.img_mx4, 1, r, r + 1)
+            elif rows is None:
+                self._mx4_image(self.rows[r0:r0 + n], self.rows_mx4[r0:r0 + n],
+                                self.sc_mx4[r0:r0 + n], self.mx4_bounds)
+            else:
+                ri = rows.long()
+                img4 = torch.empty(n, self.dim // 2, dtype=torch.uint8, device=self.device)
+                sc4 = torch.empty(n, 16, dtype=torch.uint8, device=self.device)
+                self._mx4_image(self.rows[ri], img4, sc4, self.mx4_bounds)
+                self.rows_mx4.index_copy_(0, ri, img4)
+                self.sc_mx4.index_copy_(0, ri, sc4)
+
+    def mx4_query_image(self, q_unit: torch.Tensor):
+        """(nibbles, scale record, margin) of unit queries for the MX-fp4 tier: the stream form
+        (quant_stream_mx4: [NQ][D / 2], [NQ][2 NSC] dwords) or the LDS-ring form (quant_rows_mx4:
+        [NQ][192], [NQ][16] bytes); margin = |q| E4 + |q - q~| X4 + 1e-5."""
+        NQ, dev = q_unit.shape[0], self.device
+        q4 = torch.empty(NQ, self.dim // 2, dtype=torch.uint8, device=dev)
+        m4 = torch.empty(NQ, dtype=torch.float32, device=dev)
+        if self.img_mx4 is None:
+            qs4 = torch.empty(NQ, 16, dtype=torch.uint8, device=dev)
+            self._mx4_image(q_unit, q4, qs4, self.mx4_bounds, margin=m4)
+            return q4, qs4, m4
+        nsc = (self.dim // 64 + 3) // 4
+        qs4 = torch.empty(NQ, 2 * nsc, dtype=torch.int32, device=dev)
+        if dev.type == "cuda":
+            from ..ops._ext import hip, stream_handle
+
+            hip().quant_stream_mx4(q_unit.data_ptr(), 0, 0, NQ, self.dim, 0, q4.data_ptr(),
+                                   qs4.data_ptr(), self.mx4_bounds.data_ptr(), m4.data_ptr(),
+                                   stream_handle(dev))
+            return q4, qs4, m4
+        from ..ops.reference import stream_mx4_query_ref
+
+        img, qs, _, nr = stream_mx4_query_ref(q_unit)
+        q4.copy_(img)
+        qs4.copy_(qs)
+        m4.copy_(nr[:, 2] * self.mx4_bounds[0] + nr[:, 0] * self.mx4_bounds[1] + 1e-5)
+        return q4, qs4, m4
 
     # ------------------------------------------------------------------ inserts
     def _reserve(self, n: int) -> int:
@@ -306,17 +458,22 @@ class HbmIndexShard:
         """bf16 rows [r0, r0+n) changed: refresh their e4m3 prefilter image and their int8
         pruning image (no-ops without them).  Callers that write ``rows`` directly (snapshot loads)
         must call this too."""
-        if self.rows_i8 is not None and n > 0:
+        if self.prune_on and n > 0:
             due = r0 + n >= self._calib_next or (self.i8_split == "on" and not self._i8_heavy)
             if due and self.i8_split != "off" and self.dim in SPLIT_DIMS:
-                # (re-images every row below r0 + n when the image's form changes)
+                # (re-images every row below r0 + n when the image's form changes; the new
+                # rows' MX-fp4 image below)
                 self.calibrate_prune(r0 + n, lo=r0)
+                if self.mx4_on:
+                    saved, self.i8_bounds = self.i8_bounds, None
+                    try:
+                        self._image_rows(r0, n)
+                    finally:
+                        self.i8_bounds = saved
             else:
-                self._i8_image(self.rows[r0:r0 + n], self.rows_i8[r0:r0 + n],
-                               self.sx_i8[r0:r0 + n], self.i8_bounds)
-        if self.rows_mx4 is not None and n > 0:
-            self._mx4_image(self.rows[r0:r0 + n], self.rows_mx4[r0:r0 + n],
-                            self.sc_mx4[r0:r0 + n], self.mx4_bounds)
+                self._image_rows(r0, n)
+        elif self.mx4_on and n > 0:
+            self._image_rows(r0, n)
         if self.rows8 is None or n <= 0:
             return
         src, dst = self.rows[r0:r0 + n], self.rows8[r0:r0 + n]
@@ -355,7 +512,7 @@ class HbmIndexShard:
         ``lo``: rows [0, lo) already carry the current image.  When the chosen form stays the
         plain int8 one (no basis), only [lo, hi) is imaged and the generation is kept: a
         re-image of every row would change nothing."""
-        if self.rows_i8 is None:
+        if not self.prune_on:
             return
         hi = self.count if hi is None else int(hi)
         if hi <= 0:
@@ -370,21 +527,21 @@ class HbmIndexShard:
             share = float(ev[:SPLIT_HEAVY].sum() / ev.sum().clamp_min(1e-30))
             if self.i8_split == "on" or share >= self.SPLIT_MIN_SHARE:
                 heavy, rot = SPLIT_HEAVY, vec.t().contiguous()
-        if heavy == 0 and self._i8_heavy == 0 and lo is not None:
-            self.calib_share = share
-            self._i8_image(self.rows[lo:hi], self.rows_i8[lo:hi], self.sx_i8[lo:hi],
-                           self.i8_bounds)
-            self._calib_next = max(hi * self.CALIB_GROWTH, self.CALIB_MIN_ROWS)
-            return
-        self._i8_heavy, self._i8_rot, self.calib_share = heavy, rot, share
-        rb = self.dim + heavy
-        n_alloc = self.sx_i8.shape[0]
-        self.rows_i8 = self._i8_store[:n_alloc * rb].view(n_alloc, rb)
-        self.i8_bounds.zero_()
-        chunk = 1 << 18
-        for s in range(0, hi, chunk):
-            e = min(hi, s + chunk)
-            self._i8_image(self.rows[s:e], self.rows_i8[s:e], self.sx_i8[s:e], self.i8_bounds)
+        mx4_saved, self.mx4_bounds = self.mx4_bounds, None   # (the int8 / split image only)
+        try:
+            if heavy == 0 and self._i8_heavy == 0 and lo is not None:
+                self.calib_share = share
+                self._image_rows(lo, hi - lo)
+                self._calib_next = max(hi * self.CALIB_GROWTH, self.CALIB_MIN_ROWS)
+                return
+            self._i8_heavy, self._i8_rot, self.calib_share = heavy, rot, share
+            self._set_i8_view(heavy)
+            self.i8_bounds.zero_()
+            chunk = 1 << 18
+            for s in range(0, hi, chunk):
+                self._image_rows(s, min(hi, s + chunk) - s)
+        finally:
+            self.mx4_bounds = mx4_saved
         self._calib_gen += 1
         self._calib_next = max(hi * self.CALIB_GROWTH, self.CALIB_MIN_ROWS)
 
@@ -453,7 +610,12 @@ class HbmIndexShard:
         from ..ops import reference as R
 
         r1 = self.count if r1 is None else r1
-        x8, sx = self.rows_i8[r0:r1], self.sx_i8[r0:r1]
+        if self.img_i8 is not None:
+            g0, g1 = r0 // STREAM_SUB, (r1 + STREAM_SUB - 1) // STREAM_SUB
+            x8, sx = R.stream_i8_decode(self.img_i8[g0:g1], (g1 - g0) * STREAM_SUB, self.dim)
+            x8, sx = x8[r0 - g0 * STREAM_SUB:r1 - g0 * STREAM_SUB], sx[r0 - g0 * STREAM_SUB:r1 - g0 * STREAM_SUB]
+        else:
+            x8, sx = self.rows_i8[r0:r1], self.sx_i8[r0:r1]
         if self._i8_heavy:
             return R.split_estimate_ref(q8, sq, x8, sx, self._i8_heavy)
         return (q8.float() @ x8.float().t()) * sq[:, None] * sx[None, :]
@@ -576,18 +738,8 @@ class HbmIndexShard:
         self.rows.index_copy_(0, di, scratch.rows[:n])
         if self.rows8 is not None:
             self.rows8.index_copy_(0, di, scratch.rows8[:n])
-        if self.rows_i8 is not None:   # the image in THIS shard's form (its basis, its bounds)
-            img = torch.empty(n, self.rows_i8.shape[1], dtype=torch.int8, device=self.device)
-            sc = torch.empty(n, dtype=torch.float32, device=self.device)
-            self._i8_image(scratch.rows[:n], img, sc, self.i8_bounds)
-            self.rows_i8.index_copy_(0, di, img)
-            self.sx_i8.index_copy_(0, di, sc)
-        if self.rows_mx4 is not None:
-            img4 = torch.empty(n, self.dim // 2, dtype=torch.uint8, device=self.device)
-            sc4 = torch.empty(n, 16, dtype=torch.uint8, device=self.device)
-            self._mx4_image(scratch.rows[:n], img4, sc4, self.mx4_bounds)
-            self.rows_mx4.index_copy_(0, di, img4)
-            self.sc_mx4.index_copy_(0, di, sc4)
+        # the pruning images in THIS shard's form (its basis, its bounds), from the new rows
+        self._image_rows(rows=di)
 
     def upsert(self, point_ids: list[str], vecs: torch.Tensor, payloads: list[Payload]) -> list[int]:
         """Qdrant-style upsert: existing ids are overwritten in place, new ids appended.  An id
@@ -937,7 +1089,7 @@ class HbmIndexShard:
         with self._tier_lock:
             while self._tier_pending and self._tier_pending[0][1].query():
                 self._tier_mx4 = int(self._tier_pending.popleft()[0].item()) == 0
-        if self._tier_mx4 and self.rows_mx4 is not None:
+        if self._tier_mx4 and self.mx4_on:
             shift = max(shift, self.PRUNE_TILE_SHIFT_MX4)
         self._sample_shift_last = shift   # (diagnostics / tests)
         plan, ts = None, shift
@@ -1017,11 +1169,8 @@ class HbmIndexShard:
         #    GPU from the same exact sample (the band must lie above the sample's seed threshold,
         #    so the sample counted it): the int8 / split scan and the fp4 scan are both enqueued,
         #    each gated on the flag, and exactly one runs.
-        if self.rows_mx4 is not None and self.prune_route and tci is None:
-            q4 = torch.empty(NQ, self.dim // 2, dtype=torch.uint8, device=dev)
-            qs4 = torch.empty(NQ, 16, dtype=torch.uint8, device=dev)
-            m4 = torch.empty(NQ, dtype=torch.float32, device=dev)
-            self._mx4_image(q_unit, q4, qs4, self.mx4_bounds, margin=m4)
+        if self.mx4_on and self.prune_route and tci is None:
+            q4, qs4, m4 = self.mx4_query_image(q_unit)
             # the probe: every 4th seed tile, scored exactly (one small fp32 GEMM)
             probe = sub.view(-1, TILE_ROWS, self.dim)[::4].reshape(-1, self.dim)
             ps = torch.mm(q_unit.float(), probe.float().t())
@@ -1041,8 +1190,25 @@ class HbmIndexShard:
         h = hip()
         heavy = self._i8_heavy
         rsplit = 2 if (NQ < 512 or self.i8_rsplit2) else 1
+        if self.stream:
+            # the stream scans (one wave per SIMD): one block grid for both tiers, sized for the
+            # tier with more workgroups per CU; rows_per_blk a multiple of 128 (the bf16 list
+            # scan of routed blocks reads 64-row tiles).  A split-form shard runs its int8 tier
+            # on the LDS-ring kernel: 64-row tiles there too.
+            if heavy:
+                n_qblk, wpc = math.ceil(NQ / h.i8_split_queries_per_blk(rsplit)), 1
+            else:
+                qpb, wpc = h.stream_geometry(self.dim, 0)
+                n_qblk = math.ceil(NQ / qpb)
+            if self.mx4_on:
+                qpb4, wpc4 = h.stream_geometry(self.dim, 1)
+                n_qblk, wpc = max(n_qblk, math.ceil(NQ / qpb4)), max(wpc, wpc4)
+            n_rblk = max(1, min(math.ceil(n / (128 * 4)), 1024, max(1, round(n_cus * wpc / n_qblk))))
+            rows_per_blk = _round_up(max(1, math.ceil(n / n_rblk)), 128)
+            n_rblk = max(1, math.ceil(n / rows_per_blk))
+            return rsplit, rows_per_blk, n_rblk
         tr = h.i8_tile_rows(self.dim, heavy)
-        if self.rows_mx4 is not None and rsplit == 2:   # (one block grid for both tiers)
+        if self.mx4_on and rsplit == 2:   # (one block grid for both tiers)
             tr = max(tr, h.mx4_tile_rows())
         if heavy:   # (the split image always runs 8-wave workgroups, one per CU)
             n_qblk, wpc = math.ceil(NQ / h.i8_split_queries_per_blk(rsplit)), 1
@@ -1097,12 +1263,25 @@ class HbmIndexShard:
                 m4[t].record_stream(cur)
             cnt.zero_()
         gate, want = (m4["nv"].data_ptr(), 1) if m4 is not None else (0, 0)
-        h.index_scan_i8(self.rows_i8.data_ptr(), self.sx_i8.data_ptr(), n, self.rows_i8.shape[0],
-                        rows_per_blk, n_rblk,
-                        q8.data_ptr(), NQ, thr.data_ptr(), cs.data_ptr(), ci.data_ptr(),
-                        cnt.data_ptr(), cap, self.scan_xcd, st, rsplit, skip=skip, dim=self.dim,
-                        heavy=ctx["heavy"], sq=ctx["sq"].data_ptr(), gate=gate, gate_want=want)
-        if m4 is not None:
+        if self.img_i8 is not None and not ctx["heavy"]:   # the stream scan (index_stream.hip)
+            h.index_scan_stream(self.img_i8.data_ptr(), n, self.img_i8.shape[0] * STREAM_SUB,
+                                rows_per_blk, n_rblk, q8.data_ptr(), 0, NQ, thr.data_ptr(),
+                                cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(), cap, self.scan_xcd,
+                                st, skip=skip, dim=self.dim, form=0, gate=gate, gate_want=want)
+        else:
+            h.index_scan_i8(self.rows_i8.data_ptr(), self.sx_i8.data_ptr(), n,
+                            self.rows_i8.shape[0], rows_per_blk, n_rblk,
+                            q8.data_ptr(), NQ, thr.data_ptr(), cs.data_ptr(), ci.data_ptr(),
+                            cnt.data_ptr(), cap, self.scan_xcd, st, rsplit, skip=skip,
+                            dim=self.dim, heavy=ctx["heavy"], sq=ctx["sq"].data_ptr(), gate=gate,
+                            gate_want=want)
+        if m4 is not None and self.img_mx4 is not None:
+            h.index_scan_stream(self.img_mx4.data_ptr(), n, self.img_mx4.shape[0] * STREAM_SUB,
+                                rows_per_blk, n_rblk, m4["q4"].data_ptr(), m4["qs4"].data_ptr(),
+                                NQ, m4["thr4"].data_ptr(), cs.data_ptr(), ci.data_ptr(),
+                                cnt.data_ptr(), cap, self.scan_xcd, st, skip=skip, dim=self.dim,
+                                form=1, gate=m4["nv"].data_ptr(), gate_want=0)
+        elif m4 is not None:
             h.index_scan_i8(self.rows_mx4.data_ptr(), self.sc_mx4.data_ptr(), n,
                             self.rows_mx4.shape[0], rows_per_blk, n_rblk, m4["q4"].data_ptr(), NQ,
                             m4["thr4"].data_ptr(), cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(),
@@ -1136,14 +1315,15 @@ class HbmIndexShard:
                 self._tier_pending.append((flag, ev))
                 while len(self._tier_pending) > 8:    # (a caller that never begins another search)
                     self._tier_pending.popleft()
-        if self.mq_stats and m4 is not None:
+        if (self.mq_stats or self.tier_stats) and m4 is not None:
             if self._mx4_tot is None:
                 self._mx4_tot = torch.zeros(1, dtype=torch.int32, device=dev)
             self._mx4_tot.add_(1 - m4["nv"])
         self._route_blk_last = blk
         if self.mq_stats:   # (diagnostics / benchmarks/micro.py scani8abl: inputs and grid)
             self._pruned_last = dict(q8=q8, thr=thr, sq=ctx["sq"], rows_per_blk=rows_per_blk,
-                                     n_rblk=n_rblk, cap=cap, cs=cs, ci=ci, cnt=cnt, q=q_unit)
+                                     n_rblk=n_rblk, cap=cap, cs=cs, ci=ci, cnt=cnt, q=q_unit,
+                                     m4=m4, heavy=ctx["heavy"])
         self._stats(ovf, cnt, dense, blk)
         return out_s, out_i
 

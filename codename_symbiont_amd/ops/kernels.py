@@ -117,42 +117,6 @@ def mlp_fused(x, w1, b1, w2, b2, gamma, beta, eps=1e-12, out=None):
     return out
 
 
-def mlp_fused_op(ctx, wo, bo, h, g1, be1, w1, b1, w2, b2, g2, be2, eps=1e-12, h2=None, out=None):
-    """One launch of a 384-wide layer's attention out-projection + LN1 + FFN block:
-    h2 = LayerNorm(ctx @ wo.T + bo + h) (written to ``h2``), out = mlp_fused(h2, ...).  ``out``
-    may be ``h`` itself (each row block reads its residual rows before it writes them)."""
-    _chk(ctx, torch.bfloat16, "ctx", 2)
-    _chk(wo, torch.bfloat16, "wo", 2)
-    _chk(h, torch.bfloat16, "h", 2)
-    M, H = ctx.shape
-    if wo.shape != (H, H) or h.shape != (M, H):
-        raise ValueError("mlp_fused_op: shapes")
-    for t in (bo, g1, be1):
-        _chk(t, torch.float32, "vector", 1)
-        if t.shape[0] != H:
-            raise ValueError("mlp_fused_op: vector length")
-    if h2 is None:
-        h2 = torch.empty(M, H, dtype=torch.bfloat16, device=ctx.device)
-    if out is None:
-        out = torch.empty(M, H, dtype=torch.bfloat16, device=ctx.device)
-    if h2.shape != (M, H) or not h2.is_contiguous() or h2.data_ptr() in (out.data_ptr(), h.data_ptr(), ctx.data_ptr()):
-        raise ValueError("mlp_fused_op: bad h2")
-    # (mlp_fused's own checks, on the FFN half)
-    FF = w1.shape[0]
-    if (H, FF) != (384, 1536) or w1.shape != (FF, H) or w2.shape != (H, FF):
-        raise ValueError("mlp_fused takes H = 384, FF = 1536")
-    for t, n in ((b1, FF), (b2, H), (g2, H), (be2, H)):
-        _chk(t, torch.float32, "vector", 1)
-        if t.shape[0] != n:
-            raise ValueError("mlp_fused: vector length")
-    if out.shape != (M, H) or not out.is_contiguous():
-        raise ValueError("mlp_fused_op: bad output")
-    hip().mlp_fused_op(_ptr(ctx), _ptr(wo), _ptr(bo), _ptr(h), _ptr(g1), _ptr(be1), _ptr(h2),
-                       _ptr(w1), _ptr(b1), _ptr(w2), _ptr(b2), _ptr(g2), _ptr(be2), float(eps),
-                       _ptr(out), M, H, FF, stream_handle())
-    return h2, out
-
-
 def attention(qkv, cu_seqlens, max_len, n_heads, head_dim, out=None):
     """Varlen attention over packed [T, 3H] QKV rows -> [T, H]."""
     _chk(qkv, torch.bfloat16, "qkv", 2)

@@ -164,6 +164,146 @@ def split_estimate_ref(q_img: torch.Tensor, sq: torch.Tensor, x_img: torch.Tenso
 E2M1 = (0.0, 0.5, 1.0, 1.5, 2.0, 3.0, 4.0, 6.0)
 
 
+def mx4_codes_ref(x: torch.Tensor):
+    """MX-fp4 quantisation of rows (D a multiple of 32): per 32-dim block the scale
+    2^ceil(log2(max|x| / 6)) (exponent e, e8m0 byte e + 127), each element the nearest e2m1 value of
+    x / s.  Returns (nibble bytes uint8 [n, D / 2] (element 2j in the low nibble of byte j),
+    exponents int [n, D / 32], decoded x~ f32 [n, D], norms [n, 3] = (|x - x~|, |x~|, |x|))."""
+    xf = x.float()
+    n, d = xf.shape
+    nb = d // 32
+    blk = xf.view(n, nb, 32)
+    amax = blk.abs().amax(-1)
+    _, k = torch.frexp(amax / 6.0)
+    e = k.clone()
+    e = torch.where(amax <= 6.0 * torch.ldexp(torch.ones_like(amax), k - 1), k - 1, e)
+    e = torch.where(amax > 6.0 * torch.ldexp(torch.ones_like(amax), e), e + 1, e)
+    e = torch.where(amax > 0, e, torch.full_like(e, -127)).clamp_(min=-127)
+    a = blk.abs() * torch.ldexp(torch.ones_like(amax), -e)[..., None]
+    q = torch.where(a < 2.0, torch.round(a * 2.0) * 0.5,
+                    torch.where(a < 4.0, torch.round(a), torch.where(a < 5.0, 4.0, 6.0)))
+    grid = torch.tensor(E2M1, dtype=torch.float32, device=xf.device)
+    code = (q[..., None] == grid).float().argmax(-1)
+    code = code | torch.where((blk < 0) & (code != 0), 8, 0)
+    xt = torch.where(blk < 0, -q, q) * torch.ldexp(torch.ones_like(amax), e)[..., None]
+    codes = code.view(n, d).to(torch.int32)
+    img = (codes[:, 0::2] | (codes[:, 1::2] << 4)).to(torch.uint8)
+    xt = xt.view(n, d)
+    norms = torch.stack([(xf - xt).norm(dim=1), xt.norm(dim=1), xf.norm(dim=1)], 1)
+    return img, e, xt, norms
+
+
+# ---- the stream images (index_stream.hip): 32-row sub-tiles, fragment-major ----------------
+def _stream_frags(rowbytes: torch.Tensor) -> torch.Tensor:
+    """Row-major image bytes [n, RB] (RB = 32 NKS) -> fragment-major [n_sub, NKS * 1024]: k-step
+    ks, lane l = 32 hh + rr holds row rr's bytes 32 ks + 16 hh .. + 16 at 1024 ks + 16 l."""
+    n, rb = rowbytes.shape
+    n_sub = (n + 31) // 32
+    pad = torch.zeros(n_sub * 32, rb, dtype=torch.uint8, device=rowbytes.device)
+    pad[:n] = rowbytes.view(torch.uint8)
+    nks = rb // 32
+    return pad.view(n_sub, 32, nks, 2, 16).permute(0, 2, 3, 1, 4).reshape(n_sub, nks * 1024)
+
+
+def _stream_rows(frags: torch.Tensor, n: int, rb: int) -> torch.Tensor:
+    """Inverse of _stream_frags: row-major bytes [n, rb]."""
+    n_sub = frags.shape[0]
+    nks = rb // 32
+    return frags.reshape(n_sub, nks, 2, 32, 16).permute(0, 3, 1, 2, 4).reshape(n_sub * 32, rb)[:n]
+
+
+STREAM_HDR_POS = [16 * ((r >> 2) & 1) + (r & 3) + 4 * (r >> 3) for r in range(32)]
+
+
+def stream_i8_ref(x: torch.Tensor):
+    """int8 stream image of bf16 rows (quant_stream_i8): records uint8 [n_sub, 128 + D * 32]
+    (the 32 row scales as f32 at STREAM_HDR_POS, then the fragments), plus (|x - x~|, |x~|)."""
+    q8, sc, err, xtn = quant_rows_i8_ref(x)
+    n, d = q8.shape
+    frags = _stream_frags(q8.view(torch.uint8))
+    n_sub = frags.shape[0]
+    hdr = torch.zeros(n_sub * 32, dtype=torch.float32, device=x.device)
+    hdr[:n] = sc
+    h2 = torch.zeros(n_sub, 32, dtype=torch.float32, device=x.device)
+    h2[:, STREAM_HDR_POS] = hdr.view(n_sub, 32)
+    return torch.cat([h2.view(torch.uint8), frags], 1), err, xtn
+
+
+def stream_i8_decode(rec: torch.Tensor, n: int, d: int):
+    """(x8 int8 [n, d], sx f32 [n]) of an int8 stream image."""
+    hdr = rec[:, :128].contiguous().view(torch.float32)[:, STREAM_HDR_POS].reshape(-1)[:n]
+    x8 = _stream_rows(rec[:, 128:], n, d).contiguous().view(torch.int8)
+    return x8, hdr
+
+
+def stream_mx4_ref(x: torch.Tensor):
+    """MX-fp4 stream image of bf16 rows (quant_stream_mx4, rows): records uint8 [n_sub, D * 16 +
+    NSC * 256] (fragments, then dword j of lane l = 32 hh + rr: the e8m0 bytes of k-steps 4j ..
+    4j + 3 of row rr, block 2 ks + hh), plus norms [n, 3]."""
+    img, e, _, norms = mx4_codes_ref(x)
+    n, d = x.shape
+    nks = d // 64
+    nsc = (nks + 3) // 4
+    frags = _stream_frags(img)
+    n_sub = frags.shape[0]
+    sc = torch.zeros(n_sub * 32, nsc, 2, 4, dtype=torch.uint8, device=x.device)  # [row][j][hh][b]
+    for b in range(d // 32):
+        ks, hh = b // 2, b % 2
+        sc[:n, ks // 4, hh, ks % 4] = (e[:, b] + 127).to(torch.uint8)
+    # -> [n_sub][j][lane = 32 hh + rr][byte]
+    sc = sc.view(n_sub, 32, nsc, 2, 4).permute(0, 2, 3, 1, 4).reshape(n_sub, nsc * 256)
+    return torch.cat([frags, sc], 1), norms
+
+
+def stream_mx4_query_ref(x: torch.Tensor):
+    """The MX-fp4 query image (quant_stream_mx4, queries): nibbles [n, D / 2] row-major and the
+    scale record int32 [n, 2 NSC] (dword hh NSC + j, byte b = block 2 (4 j + b) + hh), plus the
+    decoded x~ and norms."""
+    img, e, xt, norms = mx4_codes_ref(x)
+    n, d = x.shape
+    nks = d // 64
+    nsc = (nks + 3) // 4
+    qs = torch.zeros(n, 2, nsc, 4, dtype=torch.uint8, device=x.device)
+    for b in range(d // 32):
+        ks, hh = b // 2, b % 2
+        qs[:, hh, ks // 4, ks % 4] = (e[:, b] + 127).to(torch.uint8)
+    return img, qs.view(n, 2 * nsc * 4).view(torch.int32), xt, norms
+
+
+def mx4_decode_codes(img: torch.Tensor, e: torch.Tensor) -> torch.Tensor:
+    """Decoded f32 rows from nibble bytes [n, D / 2] and exponents [n, D / 32]."""
+    n = img.shape[0]
+    d = img.shape[1] * 2
+    b = img.to(torch.int32)
+    codes = torch.stack([b & 15, b >> 4], -1).view(n, d)
+    grid = torch.tensor(E2M1, dtype=torch.float32, device=img.device)
+    v = grid[codes & 7] * torch.where(codes & 8 != 0, -1.0, 1.0)
+    return (v.view(n, d // 32, 32) * torch.ldexp(torch.ones_like(e, dtype=torch.float32),
+                                                  e.to(torch.int32))[..., None]).view(n, d)
+
+
+def stream_mx4_query_decode(q4: torch.Tensor, qs: torch.Tensor) -> torch.Tensor:
+    """Decoded f32 queries of a stream MX-fp4 query image (stream_mx4_query_ref's layout)."""
+    n, d = q4.shape[0], q4.shape[1] * 2
+    nsc = (d // 64 + 3) // 4
+    b = qs.contiguous().view(torch.uint8).view(n, 2, nsc, 4)
+    e = torch.stack([b[:, blk % 2, (blk // 2) // 4, (blk // 2) % 4].to(torch.int32) - 127
+                     for blk in range(d // 32)], 1)
+    return mx4_decode_codes(q4, e)
+
+
+def stream_mx4_decode(rec: torch.Tensor, n: int, d: int) -> torch.Tensor:
+    """Decoded f32 rows [n, d] of an MX-fp4 stream image."""
+    nks = d // 64
+    nsc = (nks + 3) // 4
+    n_sub = rec.shape[0]
+    img = _stream_rows(rec[:, :nks * 1024], n, d // 2)
+    sc = rec[:, nks * 1024:].reshape(n_sub, nsc, 2, 32, 4).permute(0, 3, 1, 2, 4).reshape(n_sub * 32, nsc, 2, 4)[:n]
+    e = torch.stack([sc[:, (b // 2) // 4, b % 2, (b // 2) % 4].to(torch.int32) - 127
+                     for b in range(d // 32)], 1)
+    return mx4_decode_codes(img, e)
+
+
 def quant_rows_mx4_ref(x: torch.Tensor):
     """MX-fp4 image of 384-wide rows (index_i8.hip quant_rows_mx4): per 32-dim block the scale
     2^ceil(log2(max|x| / 6)) (e8m0 byte e + 127), each element the nearest e2m1 value of x / s,

@@ -52,8 +52,7 @@ int symb_gemm_gelu_config(int poly);
 int symb_gemm_gelu_poly();
 int symb_mlp_fused(const void* X, const void* W1, const float* b1, const void* W2, const float* b2,
                    const float* gamma, const float* beta, float eps, int gelu_poly, void* C, int M,
-                   int H, int FF, hipStream_t st, const void* Cx, const void* Wo, const float* bo,
-                   const void* Hres, const float* g1, const float* be1);
+                   int H, int FF, hipStream_t st);
 // The fused FFN block (mlp_fused.hip) for bf16 384 x 1536 layers above the small-M limit (1,
 // default); 0: the two-GEMM path (FFN1 GELU GEMM + FFN2 residual/LayerNorm GEMM).  Measured
 // (profiles/r4_mlp): 110 vs 129 us per layer, the bare MiniLM forward 1.297 vs 1.437 ms, the
@@ -86,11 +85,22 @@ int symb_mx4_select(int NQ, const float* T, const float* margin4, const float* m
                     const float* probe_s, int n_probe, float rate, const float* tail_cs,
                     int tail_cap, float limit, float* thr4, int* nv, hipStream_t st);
 int symb_i8_tile_rows_for(int dim, int heavy);
+// the streaming pruning scan (index_stream.hip)
+int symb_stream_rec_bytes(int dim, int form);
+int symb_stream_config(int mx4_variant);
+int symb_stream_geometry(int dim, int form, int* qpb, int* wgs_per_cu);
+int symb_index_scan_stream(const void* img, int n_valid, int alloc_rows, int rows_per_blk,
+                           int n_rblk, const void* Q, const void* qsc, int NQ, const float* thr,
+                           float* cand_s, int* cand_i, int* cand_n, int cap, int xcd,
+                           hipStream_t st, const int* skip, int dim, int form, const int* gate,
+                           int gate_want);
+int symb_quant_stream_i8(const void* X, int r0, const int* rows, int n, int dim, void* img,
+                         float* bounds, hipStream_t st);
+int symb_quant_stream_mx4(const void* X, int r0, const int* rows, int n, int dim, void* img,
+                          void* Xq, void* QS, float* bounds, float* margin, hipStream_t st);
 int symb_i8_split_queries_per_blk(int rsplit);
-int symb_i8_pair_config(int pair);
 int symb_mx4_config(int tile_rows);
 int symb_mx4_tile_rows();
-int symb_cu_probe(uint32_t* out, int n_blocks, hipStream_t st);
 int symb_quant_rows_split(const float* X, int n, int dim, void* X8, float* sx, float* bounds,
                           float* margin, hipStream_t st);
 int symb_prune_qquant(const void* Q, int NQ, int dim, const float* bounds, void* Q8, float* sq,
@@ -255,18 +265,8 @@ class EncoderRuntime {
       check(symb_attention(P<void>(qkv), 3 * H, P<int32_t>(cu), B, max_len, nh_, hd_,
                            P<void>(ctx), H, st),
             "attention");
-      // the fused FFN block (mlp_fused.hip) for 384 x 1536 layers above the small-M limit;
-      // mode 2 also takes the out-projection + LN1 into the same launch
+      // the fused FFN block (mlp_fused.hip) for 384 x 1536 layers above the small-M limit
       const bool fused_ffn = g_mlp_fused && H == 384 && FF_ == 1536 && T > symb_gemm_skinny_max_m();
-      if (fused_ffn && g_mlp_fused == 2) {
-        check(symb_mlp_fused(P<void>(h2), P<void>(L.wi), P<float>(L.bi), P<void>(L.wo2),
-                             P<float>(L.bo2), P<float>(L.ln2_g), P<float>(L.ln2_b), eps_,
-                             symb_gemm_gelu_poly(), P<void>(h), T, H, FF_, st, P<void>(ctx),
-                             P<void>(L.wo), P<float>(L.bo), P<void>(h), P<float>(L.ln1_g),
-                             P<float>(L.ln1_b)),
-              "fused out-proj + ffn");
-        continue;
-      }
       if (fuse_ln) {
         check(symb_gemm(EPI_RES_LN, P<void>(ctx), H, P<void>(L.wo), H, P<float>(L.bo),
                         P<void>(h), H, P<float>(L.ln1_g), P<float>(L.ln1_b), eps_, P<void>(h2),
@@ -284,8 +284,7 @@ class EncoderRuntime {
         // the whole FFN block in one launch: the 1536-wide activation never leaves the CU
         check(symb_mlp_fused(P<void>(h2), P<void>(L.wi), P<float>(L.bi), P<void>(L.wo2),
                              P<float>(L.bo2), P<float>(L.ln2_g), P<float>(L.ln2_b), eps_,
-                             symb_gemm_gelu_poly(), P<void>(h), T, H, FF_, st, nullptr, nullptr,
-                             nullptr, nullptr, nullptr, nullptr),
+                             symb_gemm_gelu_poly(), P<void>(h), T, H, FF_, st),
               "fused ffn");
         continue;
       }
@@ -375,25 +374,6 @@ class EncoderRuntime {
 PYBIND11_MODULE(_hip, m) {
   m.doc() = "CDNA4 (gfx950) HIP kernels of codename_symbiont_amd";
   m.def("arch", []() { return std::string("gfx950"); });
-  // CU-partitioned streams (hipExtStreamCreateWithCUMask): a stream whose kernels the hardware
-  // dispatches only to the CUs set in `mask` (bit i of word i / 32 = CU i as the runtime numbers
-  // them).  Returned as a raw handle for torch.cuda.ExternalStream; streams live until
-  // stream_destroy.  cu_mask_of reads a stream's mask back (tests).
-  m.def("stream_with_cu_mask", [](int device, std::vector<uint32_t> mask) {
-    check((int)hipSetDevice(device), "hipSetDevice");
-    hipStream_t st = nullptr;
-    check((int)hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()),
-          "hipExtStreamCreateWithCUMask");
-    return (uptr)st;
-  }, py::arg("device"), py::arg("mask"));
-  m.def("cu_mask_of", [](uptr st, int words) {
-    std::vector<uint32_t> mask((size_t)words, 0u);
-    check((int)hipExtStreamGetCUMask(S(st), (uint32_t)words, mask.data()), "hipExtStreamGetCUMask");
-    return mask;
-  }, py::arg("stream"), py::arg("words"));
-  m.def("cu_probe", [](uptr out, int n_blocks, uptr st) {
-    check(symb_cu_probe(P<uint32_t>(out), n_blocks, S(st)), "cu_probe");
-  }, py::arg("out"), py::arg("n_blocks"), py::arg("stream"));
   m.def("stream_destroy", [](uptr st) { check((int)hipStreamDestroy(S(st)), "hipStreamDestroy"); },
         py::arg("stream"));
   m.def("cu_count", [](int device) {
@@ -467,8 +447,6 @@ PYBIND11_MODULE(_hip, m) {
   m.def("mx4_config", [](int tile_rows) { check(symb_mx4_config(tile_rows), "mx4_config"); },
         py::arg("tile_rows"));
   m.def("mx4_tile_rows", []() { return symb_mx4_tile_rows(); });
-  m.def("i8_pair_config", [](int pair) { check(symb_i8_pair_config(pair), "i8_pair_config"); },
-        py::arg("pair"));
   m.def("i8_split_queries_per_blk", [](int rsplit) { return symb_i8_split_queries_per_blk(rsplit); },
         py::arg("rsplit") = 2);
   m.def("quant_rows_split", [](uptr X, int n, int dim, uptr X8, uptr sx, uptr bounds, uptr margin,
@@ -495,6 +473,45 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("stream"), py::arg("rsplit"), py::arg("skip") = 0, py::arg("dim") = 384,
      py::arg("heavy") = 0, py::arg("sq") = 0, py::arg("form") = 0, py::arg("gate") = 0,
      py::arg("gate_want") = 0);
+  m.def("stream_rec_bytes", [](int dim, int form) { return symb_stream_rec_bytes(dim, form); },
+        py::arg("dim"), py::arg("form"));
+  m.def("stream_config", [](int mx4_variant) {
+    check(symb_stream_config(mx4_variant), "stream_config");
+  }, py::arg("mx4_variant"));
+  m.def("stream_geometry", [](int dim, int form) {
+    int qpb = 0, wpc = 0;
+    check(symb_stream_geometry(dim, form, &qpb, &wpc), "stream_geometry");
+    return py::make_tuple(qpb, wpc);
+  }, py::arg("dim"), py::arg("form"));
+  m.def("index_scan_stream", [](uptr img, int n_valid, int alloc_rows, int rows_per_blk, int n_rblk,
+                                uptr Q, uptr qsc, int NQ, uptr thr, uptr cand_s, uptr cand_i,
+                                uptr cand_n, int cap, int xcd, uptr st, uptr skip, int dim,
+                                int form, uptr gate, int gate_want) {
+    check(symb_index_scan_stream(P<void>(img), n_valid, alloc_rows, rows_per_blk, n_rblk,
+                                 P<void>(Q), P<void>(qsc), NQ, P<const float>(thr),
+                                 P<float>(cand_s), P<int>(cand_i), P<int>(cand_n), cap, xcd, S(st),
+                                 P<const int>(skip), dim, form, P<const int>(gate), gate_want),
+          "index_scan_stream");
+  }, py::arg("img"), py::arg("n_valid"), py::arg("alloc_rows"), py::arg("rows_per_blk"),
+     py::arg("n_rblk"), py::arg("Q"), py::arg("qsc"), py::arg("NQ"), py::arg("thr"),
+     py::arg("cand_s"), py::arg("cand_i"), py::arg("cand_n"), py::arg("cap"), py::arg("xcd"),
+     py::arg("stream"), py::arg("skip") = 0, py::arg("dim") = 384, py::arg("form") = 0,
+     py::arg("gate") = 0, py::arg("gate_want") = 0);
+  m.def("quant_stream_i8", [](uptr X, int r0, uptr rows, int n, int dim, uptr img, uptr bounds,
+                              uptr st) {
+    check(symb_quant_stream_i8(P<void>(X), r0, P<const int>(rows), n, dim, P<void>(img),
+                               P<float>(bounds), S(st)),
+          "quant_stream_i8");
+  }, py::arg("X"), py::arg("r0"), py::arg("rows"), py::arg("n"), py::arg("dim"), py::arg("img"),
+     py::arg("bounds"), py::arg("stream"));
+  m.def("quant_stream_mx4", [](uptr X, int r0, uptr rows, int n, int dim, uptr img, uptr Xq,
+                               uptr QS, uptr bounds, uptr margin, uptr st) {
+    check(symb_quant_stream_mx4(P<void>(X), r0, P<const int>(rows), n, dim, P<void>(img),
+                                P<void>(Xq), P<void>(QS), P<float>(bounds), P<float>(margin),
+                                S(st)),
+          "quant_stream_mx4");
+  }, py::arg("X"), py::arg("r0"), py::arg("rows"), py::arg("n"), py::arg("dim"), py::arg("img"),
+     py::arg("Xq"), py::arg("QS"), py::arg("bounds"), py::arg("margin"), py::arg("stream"));
   m.def("quant_rows_mx4", [](uptr X, int n, int dim, uptr X4, uptr SC, uptr bounds, uptr margin,
                              uptr st) {
     check(symb_quant_rows_mx4(P<void>(X), n, dim, P<void>(X4), P<void>(SC), P<float>(bounds),
@@ -639,21 +656,11 @@ PYBIND11_MODULE(_hip, m) {
                         uptr C, int M, int H, int FF, uptr st) {
     check(symb_mlp_fused(P<void>(X), P<void>(W1), P<float>(b1), P<void>(W2), P<float>(b2),
                          P<float>(g), P<float>(b), eps, symb_gemm_gelu_poly(), P<void>(C), M, H, FF,
-                         S(st), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr),
+                         S(st)),
           "mlp_fused");
   });
-  // out-projection + LN1 + the FFN block in one launch: X receives LN1(Cx Wo^T + bo + Hres)
-  m.def("mlp_fused_op", [](uptr Cx, uptr Wo, uptr bo, uptr Hres, uptr g1, uptr be1, uptr X, uptr W1,
-                           uptr b1, uptr W2, uptr b2, uptr g, uptr b, float eps, uptr C, int M,
-                           int H, int FF, uptr st) {
-    check(symb_mlp_fused(P<void>(X), P<void>(W1), P<float>(b1), P<void>(W2), P<float>(b2),
-                         P<float>(g), P<float>(b), eps, symb_gemm_gelu_poly(), P<void>(C), M, H, FF,
-                         S(st), P<void>(Cx), P<void>(Wo), P<float>(bo), P<void>(Hres), P<float>(g1),
-                         P<float>(be1)),
-          "mlp_fused_op");
-  });
-  m.def("mlp_fused_config", [](int mode) {   // 0: two GEMMs, 1: fused FFN, 2: + out-projection
-    if (mode < 0 || mode > 2) throw std::invalid_argument("mlp_fused_config: mode 0, 1 or 2");
+  m.def("mlp_fused_config", [](int mode) {   // 0: two GEMMs, 1: the fused FFN block (default)
+    if (mode < 0 || mode > 1) throw std::invalid_argument("mlp_fused_config: mode 0 or 1");
     g_mlp_fused = mode;
   });
   m.def("gemm_gelu_config", [](int poly) { check(symb_gemm_gelu_config(poly), "gemm_gelu_config"); },

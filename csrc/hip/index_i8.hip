@@ -272,11 +272,8 @@ __device__ __forceinline__ const char* i8_uniform(const char* p) {
 // bits each) and only the 320 trailing ones quantised to int8 with their own per-row scale.
 // Emit iff acc_f / sq + acc_i * sx >= thr (sq_in: the queries' int8 scales); the bound (prune_
 // qquant_h) is the int8 one on the trailing dims plus the fp16 rounding of the leading ones.
-// PAIR (fused chains): one pre-test over both sub-tiles of a chain first (emit2), then the
-// per-sub-tile ones; false (default) = the per-sub-tile pre-tests alone.  Same-box A/B
-// (profiles/r4_split/pair/): headline 11.10-11.19 vs 11.20 ms, anisotropic 13.19-13.20 vs
-// 13.21-13.25, random held-out 11.86 vs 11.03-11.05 (its busy band pays both tests): the
-// emission pre-test is not what bounds the scan, so the pair test stays an A/B knob.
+// (Round 4's pair pre-test over both sub-tiles of a fused chain measured parity-to-slower,
+// profiles/r4_split/pair/, and was removed in round 5: the per-sub-tile pre-tests alone.)
 //
 // HK = MX4 (the MX-fp4 image, index/shard.py, the first tier of a batch whose k-th scores sit far
 // above the corpus bulk): X8 = [rows][192] e2m1 nibbles, sx = [rows][16] bytes of e8m0 block
@@ -284,7 +281,7 @@ __device__ __forceinline__ const char* i8_uniform(const char* p) {
 // The MFMA applies the scales, so acc_f is the approximate score itself: emit iff acc_f >= thr
 // (thr = T - margin in score units, the bound of quant_rows_mx4).
 // gate (optional): the kernel runs only if *gate == gate_want (the device-side tier choice).
-template <int D, int RSPLIT, int ABL = 0, int TRK = 64, int WV = 8, int HK = 0, bool PAIR = true>
+template <int D, int RSPLIT, int ABL = 0, int TRK = 64, int WV = 8, int HK = 0>
 __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
     const int8_t* __restrict__ X8, const float* __restrict__ sx, int n_valid, int rows_per_blk,
     const int8_t* __restrict__ Q8, int NQ, int n_qblk, int xcd, const float* __restrict__ thr_in,
@@ -491,44 +488,8 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void index_scan_i8_kernel(
       return;
     }
     bool hs[SETS];
-    if constexpr (!PAIR || HK == MX4) {   // (A/B: the per-sub-tile pre-tests alone)
 #pragma unroll
-      for (int s = 0; s < SETS; ++s) hs[s] = true;
-    } else {
-    float smx;
-    asm volatile("v_max3_f32 %0, %1, %2, %3\n\tv_max3_f32 %0, %0, %4, %5\n\tv_max3_f32 %0, %0, %6, %7\n\tv_max3_f32 %0, %0, %8, %8"
-                 : "=&v"(smx) : "v"(sa[0]), "v"(sa[1]), "v"(sa[2]), "v"(sa[3]), "v"(sb[0]),
-                   "v"(sb[1]), "v"(sb[2]), "v"(sb[3]));
-    float smn = 0.f;
-    if constexpr (HK > 0)
-      smn = fminf(fminf(fminf(sa[0], sa[1]), fminf(sa[2], sa[3])),
-                  fminf(fminf(sb[0], sb[1]), fminf(sb[2], sb[3])));
-    bool hit = false;
-#pragma unroll
-    for (int s = 0; s < SETS; ++s) {
-      int im;
-      asm volatile("v_max3_i32 %0, %1, %2, %3\n\tv_max3_i32 %0, %0, %4, %5\n\tv_max3_i32 %0, %0, %6, %7\n\tv_max3_i32 %0, %0, %8, %8"
-                   : "=&v"(im) : "v"(acc[0][s][0]), "v"(acc[0][s][1]), "v"(acc[0][s][2]),
-                     "v"(acc[0][s][3]), "v"(acc[1][s][0]), "v"(acc[1][s][1]), "v"(acc[1][s][2]),
-                     "v"(acc[1][s][3]));
-      if constexpr (HK > 0) {
-        float fm;
-        asm volatile("v_max3_f32 %0, %1, %2, %3\n\tv_max3_f32 %0, %0, %4, %5\n\tv_max3_f32 %0, %0, %6, %7\n\tv_max3_f32 %0, %0, %8, %8"
-                     : "=&v"(fm) : "v"(af[0][s][0]), "v"(af[0][s][1]), "v"(af[0][s][2]),
-                       "v"(af[0][s][3]), "v"(af[1][s][0]), "v"(af[1][s][1]), "v"(af[1][s][2]),
-                       "v"(af[1][s][3]));
-        // (+ |ub| 1e-4 + 1e-6: covers the rounding of this bound's own products)
-        const float ub = fmaf((float)im, im >= 0 ? smx : smn, fm * rsq[s]);
-        hs[s] = ub + fabsf(ub) * 1e-4f + 1e-6f >= thr[s];
-      } else {
-        // (cvt and multiply are monotone: (float)im * smx >= every (float)acc_r * sx_r of a
-        // non-negative max, exactly as the exact test computes them)
-        hs[s] = thr[s] <= 0.f || (float)im * smx >= thr[s];
-      }
-      hit |= hs[s];
-    }
-    if (!__builtin_amdgcn_ballot_w64(hit)) return;
-    }
+    for (int s = 0; s < SETS; ++s) hs[s] = true;
     // a pair that reaches a threshold: the per-sub-tile pre-test (as `emit`) before the exact
     // test, so a busy band (held-out queries over random rows: thousands of candidates per query)
     // costs what it did with per-sub-tile tests, while the common miss costs half
@@ -1344,7 +1305,6 @@ int symb_i8_queries_per_blk(int rsplit) {
   return g_i8_waves == 4 ? 4 * 16 * i8s::SETS : i8s::WAVES / rsplit * 16 * i8s::SETS;
 }
 
-static int g_i8_pair = 0;
 // MX-fp4 scan tile rows at 256 queries per workgroup: 64 (12 KiB tiles, 8-deep ring) or 128
 // (24 KiB tiles, 5-deep ring: half the barriers per row; default -- headline 7.35 vs 7.72 ms
 // per step, same box, profiles/r4_mx4/tile/); symb_mx4_config
@@ -1355,11 +1315,6 @@ int symb_mx4_config(int tile_rows) {
   return 0;
 }
 int symb_mx4_tile_rows() { return g_mx4_tr; }
-int symb_i8_pair_config(int pair) {
-  if (pair != 0 && pair != 1) return -1;
-  g_i8_pair = pair;
-  return 0;
-}
 
 template <int D, int RSPLIT, int TRK, int WV = 8, int HK = 0>
 static int launch_i8(const void* X8, const float* sx, int n_valid, int rows_per_blk, int n_rblk,
@@ -1376,11 +1331,8 @@ static int launch_i8(const void* X8, const float* sx, int n_valid, int rows_per_
                        xcd, thr, cand_s, cand_i, cand_n, cap, skip, sq, gate, gate_want);
     return (int)hipGetLastError();
   };
-  if (g_i8_pair)
-    return go(std::integral_constant<decltype(&index_scan_i8_kernel<D, RSPLIT, 0, TRK, WV, HK, true>),
-                                     &index_scan_i8_kernel<D, RSPLIT, 0, TRK, WV, HK, true>>());
-  return go(std::integral_constant<decltype(&index_scan_i8_kernel<D, RSPLIT, 0, TRK, WV, HK, false>),
-                                   &index_scan_i8_kernel<D, RSPLIT, 0, TRK, WV, HK, false>>());
+  return go(std::integral_constant<decltype(&index_scan_i8_kernel<D, RSPLIT, 0, TRK, WV, HK>),
+                                   &index_scan_i8_kernel<D, RSPLIT, 0, TRK, WV, HK>>());
 }
 
 // Tile rows the D-wide scan runs with (the 128-row and 4-wave forms are D = 384 knobs; the split

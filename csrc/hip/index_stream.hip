@@ -1,0 +1,566 @@
+// Streaming pruning scan (the first pass of the EXACT pruned search): the
+// index's int8 or MX-fp4 image streamed from HBM straight into VGPRs, one wave per SIMD, no LDS
+// ring and no barriers.  Round 5's replacement of index_scan_i8_kernel (index_i8.hip) for the
+// plain int8 image and the MX-fp4 tier.
+//
+// Why (profiles/r4_scan_pmc/): the LDS-ring scan shares each row tile among 8 waves through LDS,
+// so every 64-row tile costs a barrier, a fragment-read prologue and an emission block in which
+// the two waves of a SIMD meet in lockstep; it ran 3,419 cycles per tile against an MFMA floor of
+// 1,536 with waves parked 44 % of their cycles, and its MX-fp4 form moved 4.0 TB/s.  Here a wave
+// holds its queries as resident B operands (256 MX-fp4 queries or 128 int8 queries = 192 VGPRs)
+// and pulls 32-row sub-tiles of a FRAGMENT-MAJOR image: every 16-byte lane fragment of one
+// MFMA k-step is contiguous, so one global_load_dwordx4 per k-step moves a whole 1 KiB piece and
+// DEPTH sub-tiles stay in flight per wave (~50-80 KiB per CU).  Waves never wait on each other;
+// the two waves of an int8 workgroup read the same rows (their second read hits L1/L2).
+//
+// MFMA shapes: v_mfma_i32_32x32x32_i8 and v_mfma_scale_f32_32x32x64_f8f6f4 (e2m1 x e2m1, block
+// scales per lane): half the instructions of the 16x16 forms and 24 of every 32 issue cycles
+// free for the emission test (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost').  The
+// accumulator holds 16 rows of one query per lane (col = lane & 31, row = (r & 3) + 8 (r >> 2) +
+// 4 (lane >> 5)), so the test per 32 x 32 block is 8 v_max3 + 1 compare (MX-fp4: the MFMA applies
+// the block scales, the accumulator IS the estimate) or 16 cvt + 16 mul first (int8: each row's
+// own scale, carried in the sub-tile record).  Only a block with a hit branches to the per-row
+// emission, which stages (score, row, query) in a per-wave LDS buffer and reserves slots with one
+// atomic per staged candidate, 64 at a time.
+//
+// Images (quant_stream_*_kernel below), per 32-row sub-tile g:
+//   int8  : [128 B: the 32 row scales, lane-half h = (r >> 2) & 1 major, index (r & 3) + 4 (r >> 3)]
+//           [NKS x 1 KiB: k-step ks, lane l: row l & 31, bytes 32 ks + 16 (l >> 5) .. + 16]
+//   MX-fp4: [NKS x 1 KiB, the same byte map over the 192 nibble bytes of a 384-wide row]
+//           [NSC x 256 B: dword j of lane l = the e8m0 scales of k-steps 4 j .. 4 j + 3 (byte
+//            ks % 4) of row l & 31, block 2 ks + (l >> 5)]
+// Each row's bytes depend only on that row (per-row scales), so appending rows into a partly
+// filled sub-tile never rewrites bytes a concurrent scan may be reading.
+#include "scan_common.h"
+
+namespace symb {
+
+enum : int { SF_I8 = 0, SF_MX4 = 1 };
+
+typedef __attribute__((ext_vector_type(4))) int i32x4s;
+typedef __attribute__((ext_vector_type(8))) int i32x8s;
+typedef __attribute__((ext_vector_type(16))) int i32x16s;
+typedef __attribute__((ext_vector_type(16))) float f32x16s;
+
+template <int FMT, int D>
+struct SDim {
+  static constexpr int KE = FMT == SF_MX4 ? 64 : 32;            // k elements per 32-byte k-step
+  static constexpr int NKS = D / KE;                             // k-steps per row
+  static constexpr int RB = NKS * 32;                            // image bytes per row
+  static constexpr int NSC = FMT == SF_MX4 ? (NKS + 3) / 4 : 0;  // block-scale dwords per lane
+  static constexpr int HDR = FMT == SF_I8 ? 128 : 0;             // row scales (int8)
+  static constexpr int FRAG = NKS * 1024;
+  static constexpr int REC = HDR + FRAG + NSC * 256;             // bytes per 32-row sub-tile
+  static_assert(D % KE == 0 && (D == 384 || D == 768), "stream image row width");
+};
+
+// Scan geometry: SETS 32-query sets per wave (resident B operands: SETS x NKS x 4 VGPRs), NW
+// waves per workgroup on the same rows, DEPTH sub-tiles in flight per wave.  V selects among the
+// measured forms (symb_stream_config): V = 0 the default of each (format, width).
+template <int FMT, int D, int V = 0>
+struct SGeo {
+  static constexpr int NKS = SDim<FMT, D>::NKS;
+  // MX-fp4 384: 256 queries per wave (V 0) or 128 per wave, two waves per workgroup (V 1)
+  static constexpr int SETS = FMT == SF_MX4 ? (D == 384 && V == 0 ? 8 : 4) : (D == 384 ? 4 : 2);
+  static constexpr int NW = 256 / (SETS * 32) > 0 ? 256 / (SETS * 32) : 1;
+  static constexpr int DEPTH = FMT == SF_MX4 ? 3 : 2;
+  static constexpr int QPB = SETS * 32 * NW;                      // queries per workgroup
+  static constexpr int STW = 512;                                 // staged candidates per wave
+  static constexpr int STAGE = STW * 10;
+  static_assert(SETS * NKS * 4 <= 192, "resident query operands");
+  static_assert(NW >= 1 && NW <= 4, "waves per workgroup");
+};
+
+// compile-time loop: f(integral_constant<int, i>) for i = I .. N - 1
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>());
+    static_for<I + 1, N>(f);
+  }
+}
+
+__device__ __forceinline__ float max16(const float (&v)[16]) {
+  float a = __builtin_fmaxf(__builtin_fmaxf(v[0], v[1]), v[2]);   // v_max3_f32 chains
+  float b = __builtin_fmaxf(__builtin_fmaxf(v[3], v[4]), v[5]);
+  float c = __builtin_fmaxf(__builtin_fmaxf(v[6], v[7]), v[8]);
+  float d = __builtin_fmaxf(__builtin_fmaxf(v[9], v[10]), v[11]);
+  float e = __builtin_fmaxf(__builtin_fmaxf(v[12], v[13]), v[14]);
+  a = __builtin_fmaxf(__builtin_fmaxf(a, b), c);
+  d = __builtin_fmaxf(__builtin_fmaxf(d, e), v[15]);
+  return __builtin_fmaxf(a, d);
+}
+
+// img: the stream image (SDim::REC bytes per 32-row sub-tile); Q: the queries' row-major image
+// (int8 [NQ][D] from prune_qquant, or MX-fp4 nibbles [NQ][D / 2] from quant_stream_mx4 with
+// qsc = its scale record [NQ][2 NSC] dwords); thr[q]: emit a row iff its estimate >= thr (int8:
+// (q8 . x8) * sx >= thr, thr already divided by the query's scale; MX-fp4: the scaled dot).
+// Workgroup lb = (row block rb, query block qb); cand_n must be zeroed by the caller.
+template <int FMT, int D, int V>
+__global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_kernel(
+    const uint8_t* __restrict__ img, int n_valid, int rows_per_blk, const uint8_t* __restrict__ Q,
+    const uint32_t* __restrict__ qsc, int NQ, int n_qblk, int xcd, const float* __restrict__ thr_in,
+    float* __restrict__ cand_s, int* __restrict__ cand_i, int* __restrict__ cand_n, int cap,
+    const int* __restrict__ skip, const int* __restrict__ gate, int gate_want) {
+  using S = SDim<FMT, D>;
+  using G = SGeo<FMT, D, V>;
+  constexpr int NKS = S::NKS, NSC = S::NSC ? S::NSC : 1, REC = S::REC;
+  constexpr int SETS = G::SETS, DEPTH = G::DEPTH, STW = G::STW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
+  const int lb = xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int qb = lb % n_qblk, rb = lb / n_qblk;
+  if (skip != nullptr && skip[rb] != 0) return;   // (routed to the bf16 scan; no barrier here)
+  if (gate != nullptr && *gate != gate_want) return;
+  const int row_begin = rb * rows_per_blk;
+  const int row_end = min(row_begin + rows_per_blk, n_valid);
+  if (row_end <= row_begin) return;
+  const int g0 = row_begin >> 5, ns = (row_end - row_begin + 31) >> 5;
+  const int qw = (qb * G::NW + wave) * SETS * 32;   // the wave's first query
+
+  // ---- resident queries: B operand of set s, k-step ks = query qw + 32 s + (lane & 31), bytes
+  //      32 ks + 16 h .. + 16 of its row-major image ----
+  i32x4s qf[SETS][NKS];
+  uint32_t qs[SETS][NSC];
+  float thr[SETS];
+#pragma unroll
+  for (int s = 0; s < SETS; ++s) {
+    const int q = qw + 32 * s + (lane & 31);
+    const int qq = min(q, NQ - 1);
+    const uint8_t* qp = Q + (size_t)qq * S::RB + 16 * h;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) qf[s][ks] = *reinterpret_cast<const i32x4s*>(qp + 32 * ks);
+#pragma unroll
+    for (int j = 0; j < NSC; ++j) {
+      if constexpr (FMT == SF_MX4)
+        qs[s][j] = qsc[(size_t)qq * 2 * NSC + h * NSC + j];
+      else
+        qs[s][j] = 0u;
+    }
+    thr[s] = q < NQ ? thr_in[q] : INFINITY;
+  }
+
+  // ---- per-wave candidate stage (LDS) ----
+  char* stage = smem + wave * G::STAGE;
+  float* st_s = reinterpret_cast<float*>(stage);
+  int* st_r = reinterpret_cast<int*>(stage + STW * 4);
+  uint16_t* st_q = reinterpret_cast<uint16_t*>(stage + STW * 8);
+  int nst = 0;
+  auto flush = [&]() {
+    for (int e = lane; e < nst; e += 64) {
+      const int q = qw + st_q[e];
+      const int slot = atomicAdd(cand_n + q, 1);
+      if (slot < cap) {
+        cand_s[(size_t)q * cap + slot] = st_s[e];
+        cand_i[(size_t)q * cap + slot] = st_r[e];
+      }
+    }
+    nst = 0;
+  };
+
+  // ---- the sub-tile ring: fragments (+ row scales / block scales) of DEPTH sub-tiles ----
+  const uint8_t* rec0 = img + (size_t)g0 * REC;
+  i32x4s fk[DEPTH][NKS];
+  uint32_t fsc[DEPTH][NSC];
+  f32x4 frs[DEPTH][FMT == SF_I8 ? 4 : 1];
+  auto load = [&](auto dc, int i) {
+    constexpr int d = decltype(dc)::value;
+    const uint8_t* r = rec0 + (size_t)min(i, ns - 1) * REC;   // (past the end: the last again)
+    if constexpr (FMT == SF_I8) {
+      const f32x4* sp = reinterpret_cast<const f32x4*>(r + 64 * h);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) frs[d][c] = sp[c];
+    }
+    const uint8_t* f = r + S::HDR + 16 * lane;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) fk[d][ks] = *reinterpret_cast<const i32x4s*>(f + 1024 * ks);
+    if constexpr (FMT == SF_MX4) {
+#pragma unroll
+      for (int j = 0; j < NSC; ++j)
+        fsc[d][j] = *reinterpret_cast<const uint32_t*>(r + S::FRAG + 256 * j + 4 * lane);
+    }
+  };
+
+  // the 32 x 32 block of set s over sub-tile slot d, as estimates (16 rows of one query)
+  auto block = [&](auto dc, auto sc, float (&v)[16]) {
+    constexpr int d = decltype(dc)::value, s = decltype(sc)::value;
+    if constexpr (FMT == SF_MX4) {
+      f32x16s acc = {};
+      static_for<0, NKS>([&](auto kc) {
+        constexpr int ks = decltype(kc)::value;
+        const i32x8s a = __builtin_shufflevector(fk[d][ks], (i32x4s){0, 0, 0, 0}, 0, 1, 2, 3, 4, 5, 6, 7);
+        const i32x8s b = __builtin_shufflevector(qf[s][ks], (i32x4s){0, 0, 0, 0}, 0, 1, 2, 3, 4, 5, 6, 7);
+        acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, acc, 4, 4, ks & 3,
+                                                              (int)fsc[d][ks >> 2], ks & 3,
+                                                              (int)qs[s][ks >> 2]);
+      });
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = acc[r];
+    } else {
+      i32x16s acc = {};
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks)
+        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(fk[d][ks], qf[s][ks], acc, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = (float)acc[r] * frs[d][r >> 2][r & 3];
+    }
+  };
+
+  auto process = [&](auto dc, int i) {
+    const int row0 = (g0 + i) * 32 + 4 * h;   // + (r & 3) + 8 (r >> 2)
+    uint32_t hm = 0;                          // sets with a hit in this lane
+    static_for<0, SETS>([&](auto sc) {
+      constexpr int s = decltype(sc)::value;
+      float v[16];
+      block(dc, sc, v);
+      hm |= (max16(v) >= thr[s] ? 1u : 0u) << s;
+    });
+    if (__builtin_amdgcn_ballot_w64(hm != 0)) {   // rare: recompute the hit sets, emit per row
+      static_for<0, SETS>([&](auto sc) {
+        constexpr int s = decltype(sc)::value;
+        if (!__builtin_amdgcn_ballot_w64((hm >> s) & 1)) return;
+        float v[16];
+        block(dc, sc, v);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = row0 + (r & 3) + 8 * (r >> 2);
+          const bool p = v[r] >= thr[s] && row < row_end;
+          const uint64_t m = __builtin_amdgcn_ballot_w64(p);
+          if (m) {
+            if (nst > STW - 64) flush();
+            const int idx = nst + (int)__builtin_amdgcn_mbcnt_hi(
+                                      (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+            if (p) {
+              st_s[idx] = v[r];
+              st_r[idx] = row;
+              st_q[idx] = (uint16_t)(32 * s + (lane & 31));
+            }
+            nst += __builtin_popcountll(m);
+          }
+        }
+      });
+    }
+  };
+
+  // prologue: DEPTH sub-tiles in flight, then use one / refill its slot
+  static_for<0, DEPTH>([&](auto dc) { load(dc, decltype(dc)::value); });
+  // (the last round may run past ns: those slots re-read the last sub-tile and emit nothing, as
+  // every row they name is >= row_end -- a branch-free body keeps the loads' waits counted)
+  for (int i0 = 0; i0 < ns; i0 += DEPTH) {
+    static_for<0, DEPTH>([&](auto dc) {
+      constexpr int d = decltype(dc)::value;
+      process(dc, i0 + d);
+      load(dc, i0 + d + DEPTH);
+    });
+  }
+  if (nst) flush();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Image writers.  Row r of sub-tile g = r >> 5, rr = r & 31; row byte b (k-step ks = b >> 5,
+// half hh = (b >> 4) & 1, byte bi = b & 15) sits at REC g + HDR + 1024 ks + 16 (32 hh + rr) + bi.
+
+__device__ __forceinline__ size_t stream_frag_off(int rec, int hdr, int r, int b) {
+  const int rr = r & 31;
+  return (size_t)(r >> 5) * rec + hdr + 1024 * (b >> 5) + 16 * (32 * ((b >> 4) & 1) + rr) + (b & 15);
+}
+
+// int8 image of bf16 rows [r0, r0 + n) (or of the rows listed in `rows`, n of them): per-row scale
+// sx = max|x| / 127, x8 = round(x / sx) -- quant_rows_i8_kernel's numbers in the stream layout.
+// bounds (2 floats) raised to (max |x - x~|, max |x~|).  One wave per row.
+template <int D>
+__global__ __launch_bounds__(256) void quant_stream_i8_kernel(const __bf16* __restrict__ X, int r0,
+                                                              const int* __restrict__ rows, int n,
+                                                              uint8_t* __restrict__ img,
+                                                              float* __restrict__ bounds) {
+  using S = SDim<SF_I8, D>;
+  __shared__ float red[2][4];
+  constexpr int PER = D / 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int j = blockIdx.x * 4 + w;
+  if (j >= n) {   // (block-uniform barrier below)
+    if (lane == 0) red[0][w] = red[1][w] = 0.f;
+    __syncthreads();
+    goto reduce;
+  }
+  {
+    const int row = rows ? rows[j] : r0 + j;
+    float x[PER];
+    const uint32_t* xp = reinterpret_cast<const uint32_t*>(X + (size_t)row * D + PER * lane);
+#pragma unroll
+    for (int i = 0; i < PER / 2; ++i) {
+      const uint32_t u = xp[i];
+      x[2 * i] = __uint_as_float(u << 16);
+      x[2 * i + 1] = __uint_as_float(u & 0xffff0000u);
+    }
+    float amax = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) amax = fmaxf(amax, fabsf(x[i]));
+    amax = wave_max(amax);
+    const float s = amax > 0.f ? amax / 127.f : 1.f;
+    const float inv = 1.f / s;
+    float e2 = 0.f, n2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int qv = max(-127, min(127, (int)rintf(x[i] * inv)));
+      const float xt = (float)qv * s;
+      e2 += (x[i] - xt) * (x[i] - xt);
+      n2 += xt * xt;
+      img[stream_frag_off(S::REC, S::HDR, row, PER * lane + i)] = (uint8_t)(qv & 0xff);
+    }
+    e2 = wave_sum(e2);
+    n2 = wave_sum(n2);
+    if (lane == 0) {
+      const int rr = row & 31;
+      float* hdr = reinterpret_cast<float*>(img + (size_t)(row >> 5) * S::REC);
+      hdr[16 * ((rr >> 2) & 1) + (rr & 3) + 4 * (rr >> 3)] = s;
+      red[0][w] = sqrtf(e2);
+      red[1][w] = sqrtf(n2);
+    }
+    __syncthreads();
+  }
+reduce:
+  if (threadIdx.x < 2) {
+    const float m = fmaxf(fmaxf(red[threadIdx.x][0], red[threadIdx.x][1]),
+                          fmaxf(red[threadIdx.x][2], red[threadIdx.x][3]));
+    atomicMax(reinterpret_cast<int*>(bounds) + threadIdx.x, __float_as_int(m));
+  }
+}
+
+__device__ __forceinline__ float half_max32(float v) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ int e2m1_code_s(float a, float& q) {   // a = |x| / s <= 6
+  int c;
+  if (a < 2.f) {
+    q = rintf(a * 2.f) * 0.5f;
+    c = (int)(q * 2.f);          // 0 .. 4 -> 0, .5, 1, 1.5, 2
+  } else if (a < 4.f) {
+    q = rintf(a);                // 2, 3, 4
+    c = q == 2.f ? 4 : q == 3.f ? 5 : 6;
+  } else {
+    q = a < 5.f ? 4.f : 6.f;
+    c = q == 4.f ? 6 : 7;
+  }
+  return c;
+}
+
+// MX-fp4 image: every 32-dim block b gets s_b = 2^ceil(log2(max |x_b| / 6)) (an e8m0 byte) and each
+// element the nearest OCP e2m1 value of x / s_b, two per byte (element 2 j in the low nibble of
+// byte j) -- quant_rows_mx4_kernel's numbers.  One wave per row, lane l holds dims l + 64 m.
+//   rows    (margin == nullptr): written in the stream layout at rows [r0, r0 + n) or `rows`;
+//            bounds[0..1] raised to (max |x - x~|, max |x~|) -- E4, X4;
+//   queries (margin != nullptr): row-major nibbles Xq [n][D / 2] and the scale record
+//            QS [n][2 NSC] dwords (dword h NSC + j, byte b = block 2 (4 j + b) + h: the scan's
+//            per-lane B scales); margin = |q| E4 + |q - q~| X4 + 1e-5 from bounds.
+template <int D>
+__global__ __launch_bounds__(256) void quant_stream_mx4_kernel(
+    const __bf16* __restrict__ X, int r0, const int* __restrict__ rows, int n,
+    uint8_t* __restrict__ img, uint8_t* __restrict__ Xq, uint32_t* __restrict__ QS,
+    float* __restrict__ bounds, float* __restrict__ margin) {
+  using S = SDim<SF_MX4, D>;
+  constexpr int M = D / 64, NSC = S::NSC;
+  __shared__ float red[2][4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int j = blockIdx.x * 4 + w;
+  const bool query = margin != nullptr;
+  if (j >= n) {   // (block-uniform barrier below: idle waves report zeros)
+    if (!query) {
+      if (lane == 0) red[0][w] = red[1][w] = 0.f;
+      __syncthreads();
+      if (threadIdx.x < 2) {
+        const float mx = fmaxf(fmaxf(red[threadIdx.x][0], red[threadIdx.x][1]),
+                               fmaxf(red[threadIdx.x][2], red[threadIdx.x][3]));
+        atomicMax(reinterpret_cast<int*>(bounds) + threadIdx.x, __float_as_int(mx));
+      }
+    }
+    return;
+  }
+  const int row = query ? j : (rows ? rows[j] : r0 + j);
+  const uint16_t* xp = reinterpret_cast<const uint16_t*>(X + (size_t)row * D);
+  // this row's scale record (queries): half 0's words built in lanes 0-31, half 1's in 32-63
+  uint32_t scw[NSC];
+#pragma unroll
+  for (int i = 0; i < NSC; ++i) scw[i] = 0u;
+  float e2 = 0.f, n2 = 0.f, x2 = 0.f;
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const float x = __uint_as_float((uint32_t)xp[lane + 64 * m] << 16);
+    const float amax = half_max32(fabsf(x));
+    int e = -127;
+    if (amax > 0.f) {
+      int k;
+      frexpf(amax / 6.f, &k);              // amax / 6 in [2^(k-1), 2^k)
+      e = k;
+      if (amax <= 6.f * ldexpf(1.f, k - 1)) e = k - 1;
+      if (amax > 6.f * ldexpf(1.f, e)) ++e;   // (guard the division's rounding)
+      e = max(e, -127);
+    }
+    const float sc = ldexpf(1.f, e);
+    float qv;
+    const int c = amax > 0.f ? e2m1_code_s(fabsf(x) * ldexpf(1.f, -e), qv) : (qv = 0.f, 0);
+    const int code = c | (x < 0.f && c ? 8 : 0);
+    const float xt = (x < 0.f ? -qv : qv) * sc;
+    e2 += (x - xt) * (x - xt);
+    n2 += xt * xt;
+    x2 += x * x;
+    const int hi = __shfl_down(code, 1);
+    const int hh = lane >> 5;                // this half-wave's block 2 m + hh: k-step m
+    const uint8_t byte = (uint8_t)(code | (hi << 4));
+    const int bj = (lane >> 1) + 32 * m;     // row byte of the even lane's pair
+    if (query) {
+      if ((lane & 1) == 0) Xq[(size_t)row * (D / 2) + bj] = byte;
+      scw[m >> 2] |= (uint32_t)(e + 127) << (8 * (m & 3));
+    } else {
+      if ((lane & 1) == 0) img[stream_frag_off(S::REC, 0, row, bj)] = byte;
+      if ((lane & 31) == 0)
+        img[(size_t)(row >> 5) * S::REC + S::FRAG + 256 * (m >> 2) + 4 * (32 * hh + (row & 31)) +
+            (m & 3)] = (uint8_t)(e + 127);
+    }
+  }
+  const float en = sqrtf(wave_sum(e2)), nn = sqrtf(wave_sum(n2)), xn = sqrtf(wave_sum(x2));
+  if (query) {
+    // lanes 0 and 32 built the two halves' scale words (identical within a half-wave)
+#pragma unroll
+    for (int i = 0; i < NSC; ++i) {
+      const uint32_t lo = (uint32_t)__shfl((int)scw[i], 0), hi = (uint32_t)__shfl((int)scw[i], 32);
+      if (lane == 0) {
+        QS[(size_t)row * 2 * NSC + i] = lo;
+        QS[(size_t)row * 2 * NSC + NSC + i] = hi;
+      }
+    }
+    if (lane == 0) margin[row] = xn * bounds[0] + en * bounds[1] + 1e-5f;
+    return;
+  }
+  if (lane == 0) {
+    red[0][w] = en;
+    red[1][w] = nn;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    const float mx = fmaxf(fmaxf(red[threadIdx.x][0], red[threadIdx.x][1]),
+                           fmaxf(red[threadIdx.x][2], red[threadIdx.x][3]));
+    atomicMax(reinterpret_cast<int*>(bounds) + threadIdx.x, __float_as_int(mx));
+  }
+}
+
+}  // namespace symb
+
+using namespace symb;
+
+// bytes per 32-row sub-tile of the stream image (form 0 = int8, 1 = MX-fp4); 0 = unsupported
+int symb_stream_rec_bytes(int dim, int form) {
+  if (dim == 384) return form ? SDim<SF_MX4, 384>::REC : SDim<SF_I8, 384>::REC;
+  if (dim == 768) return form ? SDim<SF_MX4, 768>::REC : SDim<SF_I8, 768>::REC;
+  return 0;
+}
+
+// the MX-fp4 384 form (symb_stream_config): 0 = 256 queries per wave, 1 = 128 per wave x 2
+static int g_stream_mx4_v = 0;
+int symb_stream_config(int mx4_variant) {
+  if (mx4_variant != 0 && mx4_variant != 1) return -1;
+  g_stream_mx4_v = mx4_variant;
+  return 0;
+}
+
+// queries per workgroup and workgroups per CU (one wave per SIMD) of the stream scan
+int symb_stream_geometry(int dim, int form, int* qpb, int* wgs_per_cu) {
+#define G_(F, D_, V_)                                \
+  do {                                               \
+    *qpb = SGeo<F, D_, V_>::QPB;                     \
+    *wgs_per_cu = 4 / SGeo<F, D_, V_>::NW;           \
+    return 0;                                        \
+  } while (0)
+  if (dim == 384) {
+    if (form && g_stream_mx4_v) G_(SF_MX4, 384, 1);
+    if (form) G_(SF_MX4, 384, 0);
+    G_(SF_I8, 384, 0);
+  }
+  if (dim == 768) {
+    if (form) G_(SF_MX4, 768, 0);
+    G_(SF_I8, 768, 0);
+  }
+#undef G_
+  return -1;
+}
+
+template <int F, int D, int V>
+static int launch_stream(const void* img, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
+                         const void* qsc, int NQ, const float* thr, float* cand_s, int* cand_i,
+                         int* cand_n, int cap, int xcd, hipStream_t st, const int* skip,
+                         const int* gate, int gate_want) {
+  using G = SGeo<F, D, V>;
+  const int n_qblk = (NQ + G::QPB - 1) / G::QPB;
+  constexpr int lds = G::STAGE * G::NW;
+  hipLaunchKernelGGL((scan_stream_kernel<F, D, V>), dim3(n_rblk * n_qblk), dim3(64 * G::NW), lds,
+                     st, (const uint8_t*)img, n_valid, rows_per_blk, (const uint8_t*)Q,
+                     (const uint32_t*)qsc, NQ, n_qblk, xcd, thr, cand_s, cand_i, cand_n, cap, skip,
+                     gate, gate_want);
+  return (int)hipGetLastError();
+}
+
+// The stream scan over rows [0, n_valid) of a stream image covering alloc_rows rows (a multiple of
+// 32 that covers n_valid).  rows_per_blk: a multiple of 32; n_rblk * rows_per_blk >= n_valid.
+// form 0: int8 (Q = [NQ][dim] int8, qsc unused); 1: MX-fp4 (Q = [NQ][dim / 2] nibbles, qsc =
+// [NQ][2 NSC] scale dwords).  cand_n is zeroed here unless the launch is gated (gate != nullptr:
+// it runs only if *gate == gate_want; the caller zeroes).
+int symb_index_scan_stream(const void* img, int n_valid, int alloc_rows, int rows_per_blk,
+                           int n_rblk, const void* Q, const void* qsc, int NQ, const float* thr,
+                           float* cand_s, int* cand_i, int* cand_n, int cap, int xcd,
+                           hipStream_t st, const int* skip, int dim, int form, const int* gate,
+                           int gate_want) {
+  if (NQ <= 0) return 0;
+  if ((dim != 384 && dim != 768) || (form != 0 && form != 1)) return -1;
+  if (form == 1 && qsc == nullptr) return -1;
+  if (rows_per_blk % 32 || n_rblk <= 0 || thr == nullptr || cap <= 0 || n_valid <= 0) return -1;
+  if ((long long)n_rblk * rows_per_blk < n_valid) return -1;
+  if (alloc_rows % 32 || (long long)(n_valid + 31) / 32 * 32 > alloc_rows) return -1;
+  if (gate == nullptr) {
+    hipError_t e = hipMemsetAsync(cand_n, 0, sizeof(int) * (size_t)NQ, st);
+    if (e != hipSuccess) return (int)e;
+  }
+#define L(F, D_, V_) launch_stream<F, D_, V_>(img, n_valid, rows_per_blk, n_rblk, Q, qsc, NQ, thr, \
+                                              cand_s, cand_i, cand_n, cap, xcd, st, skip, gate,   \
+                                              gate_want)
+  if (dim == 384) {
+    if (form && g_stream_mx4_v) return L(SF_MX4, 384, 1);
+    return form ? L(SF_MX4, 384, 0) : L(SF_I8, 384, 0);
+  }
+  return form ? L(SF_MX4, 768, 0) : L(SF_I8, 768, 0);
+#undef L
+}
+
+// int8 stream image of bf16 rows X: rows [r0, r0 + n) (rows == nullptr) or the n listed rows.
+int symb_quant_stream_i8(const void* X, int r0, const int* rows, int n, int dim, void* img,
+                         float* bounds, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (bounds == nullptr || (rows == nullptr && r0 < 0)) return -1;
+#define L(D_) hipLaunchKernelGGL(quant_stream_i8_kernel<D_>, dim3((n + 3) / 4), dim3(256), 0, st, \
+                                 (const __bf16*)X, r0, rows, n, (uint8_t*)img, bounds)
+  if (dim == 384) L(384);
+  else if (dim == 768) L(768);
+  else return -1;
+#undef L
+  return (int)hipGetLastError();
+}
+
+// MX-fp4 stream image of bf16 rows (margin == nullptr: rows [r0, r0 + n) or the listed rows into
+// img, bounds raised) or the query image (margin != nullptr: Xq / QS / margin for rows 0 .. n-1).
+int symb_quant_stream_mx4(const void* X, int r0, const int* rows, int n, int dim, void* img,
+                          void* Xq, void* QS, float* bounds, float* margin, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (bounds == nullptr) return -1;
+  if (margin == nullptr ? (img == nullptr || (rows == nullptr && r0 < 0))
+                        : (Xq == nullptr || QS == nullptr))
+    return -1;
+#define L(D_) hipLaunchKernelGGL(quant_stream_mx4_kernel<D_>, dim3((n + 3) / 4), dim3(256), 0, st, \
+                                 (const __bf16*)X, r0, rows, n, (uint8_t*)img, (uint8_t*)Xq,       \
+                                 (uint32_t*)QS, bounds, margin)
+  if (dim == 384) L(384);
+  else if (dim == 768) L(768);
+  else return -1;
+#undef L
+  return (int)hipGetLastError();
+}

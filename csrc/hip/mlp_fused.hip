@@ -51,17 +51,12 @@ __device__ __forceinline__ int mf_swz(int row, int chunk) {
   return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
 }
 
-// OP: the layer's attention out-projection + residual + LayerNorm runs first, in the same
-// workgroup: X = LN1(Cx Wo^T + bo + Hres) is written (it is the FFN's input and residual) and
-// read back through the same DMA ring; the FFN's output C may alias Hres (each workgroup reads
-// its own rows of Hres before it writes them).
-template <bool OP>
+// (Round 4 also built a form that ran the attention out-projection + LayerNorm first in the same
+// workgroup; it measured parity-to-slower and was removed in round 5.)
 __global__ __launch_bounds__(MF_NT) void mlp_fused_kernel(
     const __bf16* X, const __bf16* __restrict__ W1, const float* __restrict__ b1,
     const __bf16* __restrict__ W2, const float* __restrict__ b2, const float* __restrict__ gamma,
-    const float* __restrict__ beta, float eps, int gelu_poly, __bf16* C, int M,
-    const __bf16* __restrict__ Cx, const __bf16* __restrict__ Wo, const float* __restrict__ bo,
-    const __bf16* Hres, const float* __restrict__ g1, const float* __restrict__ be1) {
+    const float* __restrict__ beta, float eps, int gelu_poly, __bf16* C, int M) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / MF_WN, wn = wave % MF_WN;
@@ -88,12 +83,7 @@ __global__ __launch_bounds__(MF_NT) void mlp_fused_kernel(
           const int grow = min(m0 + row, M - 1);
           const void* src = reinterpret_cast<const char*>(X + (size_t)grow * MF_H) + k0 + ch * 16;
           void* dst = base + t * (MF_BM * 128) + (i * MF_NT + wave * 64) * 16;
-          if constexpr (OP)
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                             (__attribute__((address_space(3))) void*)dst, 16, 0,
-                                             16 /* sc1 */);
-          else
-            glds16(src, dst);
+          glds16(src, dst);
         }
 #pragma unroll
         for (int i = 0; i < (MF_FC * 8) / MF_NT; ++i) {
@@ -180,61 +170,6 @@ __global__ __launch_bounds__(MF_NT) void mlp_fused_kernel(
   }
   };
 
-  if constexpr (OP) {
-    // prologue: acc = Cx Wo^T over 6 k-tiles (slot: Cx k-tile 16 KiB, then Wo k-tile 48 KiB)
-    auto stage_op = [&](int p) {
-      char* base = smem + (p & 1) * MF_SLOT;
-#pragma unroll
-      for (int i = 0; i < (MF_BM * 8) / MF_NT; ++i) {
-        const int v = i * MF_NT + tid;
-        const int row = v >> 3, pc = v & 7, ch = pc ^ ((row >> 1) & 7);
-        const int grow = min(m0 + row, M - 1);
-        glds16(reinterpret_cast<const char*>(Cx + (size_t)grow * MF_H) + p * 128 + ch * 16,
-               base + (i * MF_NT + wave * 64) * 16);
-      }
-#pragma unroll
-      for (int i = 0; i < (MF_H * 8) / MF_NT; ++i) {
-        const int v = i * MF_NT + tid;
-        const int row = v >> 3, pc = v & 7, ch = pc ^ ((row >> 1) & 7);
-        glds16(reinterpret_cast<const char*>(Wo + (size_t)row * MF_H) + p * 128 + ch * 16,
-               base + MF_BM * 128 + (i * MF_NT + wave * 64) * 16);
-      }
-    };
-    stage_op(0);
-#pragma unroll 1
-    for (int p = 0; p < MF_H / 64; ++p) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (p + 1 < MF_H / 64) stage_op(p + 1);
-      const char* sA = smem + (p & 1) * MF_SLOT;
-      const char* sB = sA + MF_BM * 128;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int chunk = kk * 4 + g4;
-        bf16x8 a[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-          a[i] = *reinterpret_cast<const bf16x8*>(sA + mf_swz(wm * 32 + i * 16 + r16, chunk));
-#pragma unroll
-        for (int j = 0; j < 12; ++j) {
-          const bf16x8 b = *reinterpret_cast<const bf16x8*>(sB + mf_swz(wn * 192 + j * 16 + r16, chunk));
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b, acc[i][j], 0, 0, 0);
-        }
-      }
-    }
-    ln_store(bo, Hres, g1, be1, const_cast<__bf16*>(X));
-    // X's rows, written by this workgroup's waves (write-through to L2), are read back by its
-    // DMA with device-scope loads (sc1: they miss the vector L1, which may still hold a previous
-    // layer's X); the stores only have to have completed -- no agent-scope L2 write-back
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 12; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
   stage(0);
   int q = 0;
 #pragma unroll 1
@@ -338,28 +273,16 @@ __global__ __launch_bounds__(MF_NT) void mlp_fused_kernel(
 using namespace symb;
 
 // The whole FFN block of a 384-wide layer in one launch (X, C: [M, 384] bf16, row stride 384;
-// C must not alias X).  With Cx != nullptr the layer's attention out-projection runs first in
-// the same launch: X (then an output) = LayerNorm(Cx Wo^T + bo + Hres) with g1 / be1, and C may
-// alias Hres.  Returns 0, a HIP error, or -1 (shape not supported).
+// C must not alias X).  Returns 0, a HIP error, or -1 (shape not supported).
 int symb_mlp_fused(const void* X, const void* W1, const float* b1, const void* W2, const float* b2,
                    const float* gamma, const float* beta, float eps, int gelu_poly, void* C, int M,
-                   int H, int FF, hipStream_t st, const void* Cx, const void* Wo, const float* bo,
-                   const void* Hres, const float* g1, const float* be1) {
+                   int H, int FF, hipStream_t st) {
   if (M <= 0) return 0;
   if (H != MF_H || FF != MF_FF || X == C) return -1;
   const dim3 grid((M + MF_BM - 1) / MF_BM), block(MF_NT);
-  if (Cx) {
-    if (!Wo || !bo || !Hres || !g1 || !be1 || X == Hres || X == Cx) return -1;
-    set_max_lds<mlp_fused_kernel<true>>(MF_LDS);
-    hipLaunchKernelGGL(mlp_fused_kernel<true>, grid, block, MF_LDS, st, (const __bf16*)X,
-                       (const __bf16*)W1, b1, (const __bf16*)W2, b2, gamma, beta, eps, gelu_poly,
-                       (__bf16*)C, M, (const __bf16*)Cx, (const __bf16*)Wo, bo,
-                       (const __bf16*)Hres, g1, be1);
-  } else {
-    set_max_lds<mlp_fused_kernel<false>>(MF_LDS);
-    hipLaunchKernelGGL(mlp_fused_kernel<false>, grid, block, MF_LDS, st, (const __bf16*)X,
-                       (const __bf16*)W1, b1, (const __bf16*)W2, b2, gamma, beta, eps, gelu_poly,
-                       (__bf16*)C, M, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
-  }
+  set_max_lds<mlp_fused_kernel>(MF_LDS);
+  hipLaunchKernelGGL(mlp_fused_kernel, grid, block, MF_LDS, st, (const __bf16*)X,
+                     (const __bf16*)W1, b1, (const __bf16*)W2, b2, gamma, beta, eps, gelu_poly,
+                     (__bf16*)C, M);
   return (int)hipGetLastError();
 }

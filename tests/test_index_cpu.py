@@ -480,24 +480,34 @@ def test_tile_sample_plan_invariants():
     assert c is not b and c.numel() >= b.numel()
 
 
-def test_int8_pruning_bound_holds_and_image_follows_writes():
-    """The exact int8-pruned search (csrc/hip/index_i8.hip) relies on
+@pytest.mark.parametrize("stream", ["1", "0"])
+def test_int8_pruning_bound_holds_and_image_follows_writes(stream, monkeypatch):
+    """The exact int8-pruned search (csrc/hip/index_stream.hip, index_i8.hip) relies on
     |q.x - q~.x~| <= |q| E + |q - q~| X with E = max |x - x~|, X = max |x~| over the rows written:
     check it for every (query, row) pair of random and outlier-heavy data, and that the shard's
-    int8 image and its (E, X) follow appends, overwrites and snapshot loads."""
+    int8 image (the stream image, or the row-major one with SYMB_PRUNE_STREAM=0) and its (E, X)
+    follow appends, scattered overwrites and snapshot loads."""
     from codename_symbiont_amd.index.shard import resolve_prune
-    from codename_symbiont_amd.ops.reference import quant_rows_i8_ref
+    from codename_symbiont_amd.ops.reference import quant_rows_i8_ref, stream_i8_decode
 
+    monkeypatch.setenv("SYMB_PRUNE_STREAM", stream)
     g = torch.Generator().manual_seed(5)
     x = torch.randn(3000, 384, generator=g)
     x[:100, :4] *= 30.0                     # rows dominated by a few large components
     sh = HbmIndexShard(384, 4000, device="cpu", prune="i8")
+    assert sh.stream == (stream == "1")
     sh.append_f32(x[:2000])
     sh.write_f32(5, x[2500:2501])           # an overwrite refreshes that row's image
+    sh.write_rows_f32([40, 7, 1999], x[2600:2603])   # scattered overwrites too
     sh.append_f32(x[2000:])
     xb = sh.rows[:sh.count]
     x8, sx, err, xtn = quant_rows_i8_ref(xb)
-    assert torch.equal(sh.rows_i8[:sh.count], x8) and torch.allclose(sh.sx_i8[:sh.count], sx)
+    if sh.stream:
+        y8, ysx = stream_i8_decode(sh.img_i8[:(sh.count + 31) // 32], sh.count, 384)
+        assert torch.equal(y8, x8) and torch.allclose(ysx, sx)
+        assert sh.rows_i8 is None
+    else:
+        assert torch.equal(sh.rows_i8[:sh.count], x8) and torch.allclose(sh.sx_i8[:sh.count], sx)
     E, X = float(sh.i8_bounds[0]), float(sh.i8_bounds[1])
     assert E >= float(err.max()) - 1e-7 and X >= float(xtn.max()) - 1e-7
     q = torch.nn.functional.normalize(torch.randn(64, 384, generator=g), dim=-1).bfloat16()
@@ -559,32 +569,40 @@ def test_split_image_bound_holds_and_prunes_anisotropic_rows():
     r = HbmIndexShard(384, 5000, device="cpu", prune="i8")
     r.append_f32(torch.randn(5000, 384, generator=torch.Generator().manual_seed(2)))
     r.calibrate_prune()
-    assert r._i8_heavy == 0 and r.calib_share < 0.3 and r.rows_i8.shape[1] == 384
+    assert r._i8_heavy == 0 and r.calib_share < 0.3
+    assert (r.img_i8 is not None) if r.stream else r.rows_i8.shape[1] == 384
 
 
-def test_mx4_image_follows_writes_and_bounds_every_pair():
-    """The MX-fp4 first-tier image (e2m1 nibbles + e8m0 block scales) follows appends and
-    scattered overwrites, its (E4, X4) cover every row written, and |q.x - q~.x~| stays within
-    |q| E4 + |q - q~| X4 for every (query, row) pair."""
-    from codename_symbiont_amd.ops.reference import mx4_decode_ref, quant_rows_mx4_ref
+@pytest.mark.parametrize("stream,D", [("1", 384), ("1", 768), ("0", 384)])
+def test_mx4_image_follows_writes_and_bounds_every_pair(stream, D, monkeypatch):
+    """The MX-fp4 first-tier image (e2m1 nibbles + e8m0 block scales; the stream image at 384 and
+    768, the row-major one with SYMB_PRUNE_STREAM=0) follows appends and scattered overwrites, its
+    (E4, X4) cover every row written, and |q.x - q~.x~| stays within |q| E4 + |q - q~| X4 for every
+    (query, row) pair."""
+    from codename_symbiont_amd.ops import reference as R
 
+    monkeypatch.setenv("SYMB_PRUNE_STREAM", stream)
     g = torch.Generator().manual_seed(9)
-    sh = HbmIndexShard(384, 3000, device="cpu", prune="i8")
-    sh.append_f32(torch.randn(2000, 384, generator=g))
-    sh.upsert(["a", "b"], torch.randn(2, 384, generator=g), [Payload("da"), Payload("db")])
-    sh.write_rows_f32([3, 100, 1999], torch.randn(3, 384, generator=g))
+    sh = HbmIndexShard(D, 3000, device="cpu", prune="i8")
+    assert sh.mx4_on
+    sh.append_f32(torch.randn(2000, D, generator=g))
+    sh.upsert(["a", "b"], torch.randn(2, D, generator=g), [Payload("da"), Payload("db")])
+    sh.write_rows_f32([3, 100, 1999], torch.randn(3, D, generator=g))
     n = sh.count
-    img, sc, xt, nr = quant_rows_mx4_ref(sh.rows[:n])
-    assert torch.equal(sh.rows_mx4[:n], img) and torch.equal(sh.sc_mx4[:n], sc)
-    assert torch.equal(mx4_decode_ref(img, sc), xt)
+    _, _, xt, nr = R.mx4_codes_ref(sh.rows[:n])
+    if sh.stream:
+        assert torch.equal(R.stream_mx4_decode(sh.img_mx4[:(n + 31) // 32], n, D), xt)
+    else:
+        img, sc, xt0, _ = R.quant_rows_mx4_ref(sh.rows[:n])
+        assert torch.equal(sh.rows_mx4[:n], img) and torch.equal(sh.sc_mx4[:n], sc)
+        assert torch.equal(R.mx4_decode_ref(img, sc), xt) and torch.equal(xt0, xt)
     E4, X4 = sh.mx4_bounds.tolist()
     assert E4 >= float(nr[:, 0].max()) - 1e-7 and X4 >= float(nr[:, 1].max()) - 1e-7
-    q = torch.nn.functional.normalize(torch.randn(32, 384, generator=g), dim=-1).bfloat16()
-    q4 = torch.empty(32, 192, dtype=torch.uint8)
-    qs4 = torch.empty(32, 16, dtype=torch.uint8)
-    m4 = torch.empty(32)
-    sh._mx4_image(q, q4, qs4, sh.mx4_bounds, margin=m4)
-    est = mx4_decode_ref(q4, qs4) @ xt.t()
+    q = torch.nn.functional.normalize(torch.randn(32, D, generator=g), dim=-1).bfloat16()
+    q4, qs4, m4 = sh.mx4_query_image(q)
+    qt = (R.stream_mx4_query_decode(q4, qs4) if sh.stream else R.mx4_decode_ref(q4, qs4))
+    assert torch.equal(qt, R.mx4_codes_ref(q)[2])
+    est = qt @ xt.t()
     s = q.float() @ sh.rows[:n].float().t()
     assert ((s - est).abs() <= m4[:, None]).all()
 

@@ -280,39 +280,6 @@ def test_mlp_fused(M):
     assert torch.equal(out, out2)
 
 
-@pytest.mark.parametrize("M", [128, 1000, 4173])
-def test_mlp_fused_out_projection(M):
-    """mlp_fused.hip with the out-projection prologue (mode 2): h2 == the residual + LayerNorm
-    GEMM's, the FFN half bit-exact with mlp_fused on that h2, and the output may alias the
-    residual input h (as the encoder calls it)."""
-    from codename_symbiont_amd.ops.kernels import EPI_RES_LN, gemm, mlp_fused, mlp_fused_op
-
-    ctx = _bf(M, 384, seed=31)
-    h = torch.nn.functional.layer_norm(_f(M, 384, seed=32), (384,)).bfloat16()
-    wo = _bf(384, 384, scale=1.0 / math.sqrt(384), seed=33)
-    bo = _f(384, scale=0.5, seed=34)
-    g1 = _f(384, scale=0.1, offset=1.0, seed=35)
-    be1 = _f(384, scale=0.1, seed=36)
-    w1 = _bf(1536, 384, scale=1.0 / math.sqrt(384), seed=22)
-    w2 = _bf(384, 1536, scale=1.0 / math.sqrt(1536), seed=23)
-    b1 = _f(1536, scale=0.5, seed=24)
-    b2 = _f(384, scale=0.5, seed=25)
-    g2 = _f(384, scale=0.1, offset=1.0, seed=26)
-    be2 = _f(384, scale=0.1, seed=27)
-    h2, out = mlp_fused_op(ctx, wo, bo, h, g1, be1, w1, b1, w2, b2, g2, be2, 1e-12)
-    h2_ref = gemm(ctx, wo, bo, EPI_RES_LN, h, g1, be1, 1e-12)
-    ffn = mlp_fused(h2, w1, b1, w2, b2, g2, be2, 1e-12)
-    hh = h.clone()
-    _, alias = mlp_fused_op(ctx, wo, bo, hh, g1, be1, w1, b1, w2, b2, g2, be2, 1e-12, out=hh)
-    ref = torch.nn.functional.layer_norm(ctx.float() @ wo.float().t() + bo + h.float(), (384,),
-                                         g1, be1, 1e-12)
-    torch.cuda.synchronize()
-    _close(h2, ref, atol=3e-2, rtol=1e-2, what="fused out-projection vs fp32 oracle")
-    _close(h2, h2_ref, atol=2e-2, rtol=1e-2, what="fused out-projection vs RES_LN GEMM")
-    assert torch.equal(out, ffn), "FFN half differs from mlp_fused on the same h2"
-    assert torch.equal(alias, out), "output aliasing the residual input changed the result"
-
-
 @pytest.mark.parametrize("model", ["minilm-l6", "bge-base"])
 def test_encoder_small_batch_skinny(model):
     """Query-path forwards (T <= 256 tokens: every GEMM on the skinny path; bge's residual +
@@ -406,12 +373,12 @@ def test_encoder_matches_fp32_oracle(model):
     ref, _ = ref_enc.forward_packed(b)
     cos = torch.nn.functional.cosine_similarity(out.float().cpu(), ref.float(), dim=-1)
     assert cos.min().item() > 0.999, cos
-    if cfg.hidden == 384:   # the fused FFN block (default) vs the two-GEMM path / + out-proj
+    if cfg.hidden == 384:   # the fused FFN block (default) vs the two-GEMM path
         from codename_symbiont_amd.ops._ext import hip
 
         others = {}
         try:
-            for mode in (0, 2):
+            for mode in (0,):
                 hip().mlp_fused_config(mode)
                 others[mode] = hip_enc.forward_packed(b.to(DEV))[0].clone()
         finally:
@@ -752,6 +719,126 @@ def test_quant_rows_i8_matches_reference(D):
 
 
 @pytest.mark.parametrize("D", [384, 768])
+def test_quant_stream_images_match_reference(D):
+    """index_stream.hip's image writers == the torch references: the int8 stream image (per-row
+    scale header + fragment-major codes) and the MX-fp4 one (fragment-major nibbles + per-lane
+    block-scale dwords), written for a contiguous range and for scattered rows, with (E, X) /
+    (E4, X4) raised; the MX-fp4 query image (row-major nibbles + scale record) and its margin."""
+    from codename_symbiont_amd.ops._ext import hip, stream_handle
+
+    h, st = hip(), stream_handle()
+    n = 4099
+    x = torch.nn.functional.normalize(_f(n, D, seed=63), dim=-1).bfloat16()
+    x[7] = 0                                   # a zero row: scale 1 (int8), scale byte 0 (MX-fp4)
+    x[9, :40] = 0                              # zero MX blocks
+    n_sub = (n + 31) // 32
+    for form in (0, 1):
+        rec = h.stream_rec_bytes(D, form)
+        img = torch.zeros(n_sub, rec, dtype=torch.uint8, device=DEV)
+        b = torch.zeros(2, device=DEV)
+        # rows [0, 1000) as a range, the rest as a scattered list (reversed order)
+        rows = torch.arange(n - 1, 999, -1, dtype=torch.int32, device=DEV)
+        if form == 0:
+            h.quant_stream_i8(x.data_ptr(), 0, 0, 1000, D, img.data_ptr(), b.data_ptr(), st)
+            h.quant_stream_i8(x.data_ptr(), 0, rows.data_ptr(), rows.numel(), D, img.data_ptr(),
+                              b.data_ptr(), st)
+            ref, err, xtn = R.stream_i8_ref(x)
+            torch.cuda.synchronize()
+            y8, ysx = R.stream_i8_decode(img, n, D)
+            r8, rsx = R.stream_i8_decode(ref, n, D)
+            _close(ysx, rsx, atol=0, rtol=1e-6, what="stream i8 scales")
+            assert ((y8.int() - r8.int()).abs() <= 1).all()
+            assert (y8 == r8).float().mean().item() > 0.999   # x * (1/s) vs x / s at exact halves
+            assert float(b[0]) >= float(err.max()) * (1 - 1e-6) and float(b[1]) >= float(xtn.max()) * (1 - 1e-6)
+        else:
+            h.quant_stream_mx4(x.data_ptr(), 0, 0, 1000, D, img.data_ptr(), 0, 0, b.data_ptr(), 0, st)
+            h.quant_stream_mx4(x.data_ptr(), 0, rows.data_ptr(), rows.numel(), D, img.data_ptr(),
+                               0, 0, b.data_ptr(), 0, st)
+            ref, nr = R.stream_mx4_ref(x)
+            torch.cuda.synchronize()
+            assert torch.equal(img[:, :D * 16], ref[:, :D * 16]), "MX-fp4 stream nibbles"
+            nks = D // 64
+            nsc = (nks + 3) // 4
+            # scale dwords: only bytes ks % 4 < the k-steps in that dword are defined
+            used = torch.zeros(nsc, 64, 4, dtype=torch.bool, device=DEV)
+            for ks in range(nks):
+                used[ks // 4, :, ks % 4] = True
+            got = img[:, D * 16:].reshape(n_sub, nsc, 64, 4)
+            want = ref[:, D * 16:].reshape(n_sub, nsc, 64, 4)
+            assert torch.equal(got[:, used], want[:, used]), "MX-fp4 stream block scales"
+            _close(b, nr[:, :2].amax(0), atol=1e-6, rtol=1e-4, what="stream mx4 bounds")
+            q = torch.nn.functional.normalize(_f(300, D, seed=64), dim=-1).bfloat16()
+            q4 = torch.empty(300, D // 2, dtype=torch.uint8, device=DEV)
+            qs = torch.empty(300, 2 * nsc, dtype=torch.int32, device=DEV)
+            mg = torch.empty(300, device=DEV)
+            h.quant_stream_mx4(q.data_ptr(), 0, 0, 300, D, 0, q4.data_ptr(), qs.data_ptr(),
+                               b.data_ptr(), mg.data_ptr(), st)
+            rq4, rqs, qt, qn = R.stream_mx4_query_ref(q)
+            torch.cuda.synchronize()
+            assert torch.equal(q4, rq4)
+            assert torch.equal(R.stream_mx4_query_decode(q4, qs), qt)
+            _close(mg, qn[:, 2] * b[0] + qn[:, 0] * b[1] + 1e-5, atol=1e-6, rtol=1e-4,
+                   what="stream mx4 margin")
+
+
+@pytest.mark.parametrize("form,D", [(0, 384), (1, 384), (0, 768), (1, 768)])
+def test_index_scan_stream_emits_the_bound_set(form, D):
+    """index_stream.hip scan_stream_kernel (v_mfma_i32_32x32x32_i8 / v_mfma_scale_f32_32x32x64
+    on fragment-major images, one wave per SIMD): exactly the rows whose estimate (int8: (q8 .
+    x8) sx, MX-fp4: the decoded dot) reaches the threshold, for 1, 2 and 3 query blocks, a ragged
+    row count and skipped row blocks -- pins the fragment layout, the accumulator row map, the
+    row-scale header and the block-scale bytes' lane / k-step mapping."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+    from codename_symbiont_amd.ops._ext import hip, stream_handle
+
+    n = 200_000 + 77
+    shard = HbmIndexShard(D, n + 4096, prune="i8")
+    shard.fill_random(n, seed=5)
+    assert shard.stream and (shard.img_i8 is not None) and (shard.img_mx4 is not None)
+    h, st = hip(), stream_handle(shard.device)
+    if form == 0:
+        x8, sx = R.stream_i8_decode(shard.img_i8[:(n + 31) // 32], n, D)
+        img = shard.img_i8
+    else:
+        xt = R.stream_mx4_decode(shard.img_mx4[:(n + 31) // 32], n, D)
+        img = shard.img_mx4
+    for nq in (200, 256, 600):
+        q = torch.nn.functional.normalize(_f(nq, D, seed=nq + D), dim=-1).bfloat16()
+        if form == 0:
+            q8, sq, _ = shard.prune_query_image(q)
+            est = (q8.float() @ x8.float().t()) * sx[None, :]        # (acc * sx: thr / sq units)
+            qa, qs = q8, None
+        else:
+            qa, qs, _ = shard.mx4_query_image(q)
+            est = R.stream_mx4_query_decode(qa, qs) @ xt.t()
+        t = est.topk(40, dim=1).values[:, -1].contiguous()
+        _, rows_per_blk, n_rblk = shard._i8_geometry(n, nq, shard._n_cus())
+        skip = torch.zeros(n_rblk, dtype=torch.int32, device=DEV)
+        skip[1::3] = 1                                            # every third block skipped
+        cap = 4096
+        cs = torch.empty(nq, cap, device=DEV)
+        ci = torch.empty(nq, cap, dtype=torch.int32, device=DEV)
+        cnt = torch.empty(nq, dtype=torch.int32, device=DEV)
+        h.index_scan_stream(img.data_ptr(), n, img.shape[0] * 32, rows_per_blk, n_rblk,
+                            qa.data_ptr(), 0 if qs is None else qs.data_ptr(), nq, t.data_ptr(),
+                            cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(), cap, 1, st,
+                            skip=skip.data_ptr(), dim=D, form=form)
+        torch.cuda.synchronize()
+        live = ~skip.bool().repeat_interleave(rows_per_blk)[:n]
+        want = (est >= t[:, None]) & live[None, :]
+        near = (est - t[:, None]).abs() <= 1e-5 * est.abs().clamp_min(1.0)
+        assert int(cnt.max()) <= cap
+        got = torch.zeros_like(want)
+        for i in range(nq):
+            got[i, ci[i, :int(cnt[i])].long()] = True
+        bad = (got != want) & ~near
+        assert not bad.any(), f"form={form} D={D} nq={nq}: {int(bad.sum())} rows differ"
+        c0 = int(cnt[0])
+        _close(cs[0, :c0], est[0, ci[0, :c0].long()], atol=1e-4, rtol=1e-5,
+               what="stream emitted scores")
+
+
+@pytest.mark.parametrize("D", [384, 768])
 @pytest.mark.parametrize("k", [1, 10, 16])
 def test_prune_qprep_matches_torch_composition(k, D):
     """index_i8.hip prune_qprep (T = k-th best of the two lists, int8 query image, emission
@@ -782,16 +869,23 @@ def test_prune_qprep_matches_torch_composition(k, D):
     _close(thr[fin], thr0[fin], atol=1e-4, rtol=1e-5, what="emission thresholds (margin sums)")
 
 
-@pytest.mark.parametrize("nq,data,tr", [(256, "random", 64), (300, "random", 64), (512, "random", 64),
-                                        (1100, "random", 64), (256, "clustered", 64), (512, "near", 64),
+@pytest.mark.parametrize("nq,data,tr", [(256, "random", 0), (300, "random", 0), (512, "random", 0),
+                                        (1100, "random", 0), (256, "clustered", 0), (512, "near", 0),
+                                        (300, "near", 0), (2048, "random", 0),
+                                        (256, "random", 64), (1100, "random", 64),
+                                        (256, "clustered", 64), (512, "near", 64),
                                         (256, "random", 128), (300, "near", 128), (1100, "random", 128),
                                         (256, "clustered", 128), (256, "random", -64),
                                         (1100, "near", -64), (256, "clustered", -64)])
-def test_index_pruned_search_is_exact(nq, data, tr):
+def test_index_pruned_search_is_exact(nq, data, tr, monkeypatch):
     """prune="i8" (int8 bound-pruned scan + exact bf16 re-score) returns the rows and scores of the
     exact bf16 scan: random data, tight clusters (near-ties everywhere: candidate overflow takes
-    the gated exact path) and queries that are noisy copies of stored rows."""
+    the gated exact path) and queries that are noisy copies of stored rows.  tr = 0: the stream
+    scan (index_stream.hip, default); tr != 0: the LDS-ring scan (SYMB_PRUNE_STREAM=0) with that
+    tile geometry."""
     from codename_symbiont_amd.index.shard import HbmIndexShard
+
+    monkeypatch.setenv("SYMB_PRUNE_STREAM", "1" if tr == 0 else "0")
 
     n, k, D = (1 << 20) + 777, 10, 384
     g = torch.Generator(device=DEV).manual_seed(71)
@@ -814,7 +908,8 @@ def test_index_pruned_search_is_exact(nq, data, tr):
     from codename_symbiont_amd.ops._ext import hip
 
     s0, r0 = ref.search(q, k)
-    hip().i8_config(abs(tr), 4 if tr < 0 else 8)   # rows per tile; tr < 0: 4-wave workgroups
+    assert shard.stream == (tr == 0)
+    hip().i8_config(abs(tr) or 64, 4 if tr < 0 else 8)   # rows per tile; tr < 0: 4-wave workgroups
     try:
         s1, r1 = shard.search(q, k)
     finally:
@@ -1065,13 +1160,16 @@ def test_quant_rows_mx4_matches_reference():
     assert ((s - qt @ xt.t()).abs() <= mg[:, None]).all()
 
 
-def test_index_scan_mx4_emits_the_bound_set():
-    """index_scan_i8_kernel HK = MX4 (v_mfma_scale_f32_16x16x128_f8f6f4 on e2m1 nibbles with
-    e8m0 block scales, 12-piece tiles over 8 waves, 8-deep ring): exactly the rows whose decoded
-    fp4 estimate reaches the threshold, both row-split forms -- pins the nibble order, the scale
-    bytes' lane / k-step mapping and the fragment layout."""
+def test_index_scan_mx4_emits_the_bound_set(monkeypatch):
+    """index_scan_i8_kernel HK = MX4 (the LDS-ring scan: v_mfma_scale_f32_16x16x128_f8f6f4 on
+    e2m1 nibbles with e8m0 block scales, 12-piece tiles over 8 waves, 8-deep ring; the shard runs
+    it with SYMB_PRUNE_STREAM=0): exactly the rows whose decoded fp4 estimate reaches the
+    threshold, both row-split forms -- pins the nibble order, the scale bytes' lane / k-step
+    mapping and the fragment layout."""
     from codename_symbiont_amd.index.shard import HbmIndexShard
     from codename_symbiont_amd.ops._ext import hip, stream_handle
+
+    monkeypatch.setenv("SYMB_PRUNE_STREAM", "0")
 
     n = 300_000 + 77
     shard = HbmIndexShard(384, n + 4096, prune="i8")
@@ -1110,27 +1208,30 @@ def test_index_scan_mx4_emits_the_bound_set():
         _close(cs[0, :c0], est[0, ci[0, :c0].long()], atol=1e-4, what="mx4 emitted scores")
 
 
-@pytest.mark.parametrize("nq", [256, 512, 2048])
-def test_index_pruned_search_mx4_tier_is_exact(nq):
+@pytest.mark.parametrize("nq,stream,D", [(256, "1", 384), (512, "1", 384), (2048, "1", 384),
+                                         (256, "0", 384), (2048, "0", 384), (256, "1", 768),
+                                         (512, "1", 768)])
+def test_index_pruned_search_mx4_tier_is_exact(nq, stream, D, monkeypatch):
     """The pruned search with the MX-fp4 first tier: near-duplicate queries (their k-th score far
     above the random bulk) take the fp4 tier, random held-out queries the int8 one; both give
     the exact bf16 results.  (Batches above tail_dense_max_nq = 2048 queries have no dense tail
     scores to probe and always take the int8 tier.)"""
     from codename_symbiont_amd.index.shard import HbmIndexShard
 
+    monkeypatch.setenv("SYMB_PRUNE_STREAM", stream)
     n, k = (1 << 20) + 555, 10
     g = torch.Generator(device=DEV).manual_seed(12)
-    shard = HbmIndexShard(384, n + 8192, prune="i8")
+    shard = HbmIndexShard(D, n + 8192, prune="i8")
     shard.fill_random(n, seed=6)
-    c = torch.nn.functional.normalize(torch.randn(384, device=DEV, generator=g), dim=0)
-    crowd = c + 0.1 * torch.randn(5000, 384, device=DEV, generator=g) / math.sqrt(384)
+    c = torch.nn.functional.normalize(torch.randn(D, device=DEV, generator=g), dim=0)
+    crowd = c + 0.1 * torch.randn(5000, D, device=DEV, generator=g) / math.sqrt(D)
     shard.append_f32(crowd)          # a near-duplicate crowd (cos ~0.99), the fresh-row tail
     rows = shard.unit_rows().float()
     for kind in ("near", "random"):
         if kind == "near":
-            q = c + 0.1 * torch.randn(nq, 384, device=DEV, generator=g) / math.sqrt(384)
+            q = c + 0.1 * torch.randn(nq, D, device=DEV, generator=g) / math.sqrt(D)
         else:
-            q = torch.randn(nq, 384, device=DEV, generator=g)
+            q = torch.randn(nq, D, device=DEV, generator=g)
         q = torch.nn.functional.normalize(q, dim=-1).bfloat16()
         s1, r1 = shard.search(q, k)
         nv = shard._mx4_last

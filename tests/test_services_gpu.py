@@ -76,9 +76,9 @@ def test_ingest_and_search_on_gpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("extra,debug", [([], False), (["--no-overlap"], False), ([], True),
+@pytest.mark.parametrize("extra,debug", [([], False), (["--opt", "overlap=0"], False), ([], True),
                                          (["--mode", "embed"], False),
-                                         (["--mode", "embed", "--no-graph"], False)])
+                                         (["--mode", "embed", "--opt", "graph=0"], False)])
 def test_bench_contract_small_index(extra, debug):
     """bench.py's driver contract (one JSON line, whole-job value, step timing) on a small index,
     with and without the encode/search stream overlap."""
@@ -99,10 +99,13 @@ def test_bench_contract_small_index(extra, debug):
     assert r["n_gpus"] == 1 and r["steps"] == 3 and r["warmup"] == 2
     assert r["value"] > 0 and r["higher_is_better"] is True and r["dtype"] == "bf16"
     assert abs(r["value"] - 256 * 1000.0 / r["ms_per_step"]) / r["value"] < 0.01
-    assert r["config"]["encode_search_overlap"] is ("--no-overlap" not in extra
-                                                    and "--mode" not in extra)
-    assert r["config"]["encoder_hipgraph"] is ("--mode" in extra and "--no-graph" not in extra
-                                               and not debug)
+    # the config lists the knobs set away from their defaults (VERDICT r4 housekeeping)
+    assert ("overlap" in r["config"]) is ("overlap=0" in extra)
+    assert r["config"].get("encoder_hipgraph", False) is ("--mode" in extra
+                                                          and "graph=0" not in extra and not debug)
+    if "--mode" not in extra:   # the held-out search rate rides in the headline's line
+        assert r["heldout_searches"] == 20 and r["heldout_topk_qps"] > 0
+        assert "stream scan" in r["config"]["index_scan"]
 
 
 @pytest.mark.gpu
