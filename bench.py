@@ -711,7 +711,7 @@ def run_gpu(args, info, comm) -> int:
         if group_dp:
             if info.is_root:
                 compute.wait_event(copy_done[slot])
-                egroup.embed(dbuf[slot])
+                egroup.embed(dbuf[slot], cu_host=host[i % NB].cu_seqlens)
                 consumed[slot].record(compute)
                 prefetch(i + 1)
             else:

@@ -4,17 +4,21 @@ The reference embeds on ONE GPU in padded batches of 8 (services/preprocessing_s
 embedding_generator.rs:146, :75-91).  Here the preprocessing endpoint (rank 0) hands each packed
 token batch to the group and every GPU of the node encodes a share of it:
 
-  EMBED : header (op, B, T) -> broadcast cu_seqlens [B+1] and the ids/positions [2, T] (int32) ->
-          every rank takes a token-balanced contiguous slice of the sentences (a pure function of
-          cu_seqlens, so only the batch itself travels), encodes it with its own HIP encoder, pads
-          the pooled f32 rows to the largest slice and all_gather_into_tensor's them over xGMI ->
-          rank 0 reassembles [B, H] in input order.
+  EMBED : header (op, B, T, wire, the per-rank split) -> broadcast cu_seqlens [B+1] and the
+          ids/positions [2, T] (int32) -> every rank encodes its token-balanced contiguous slice of
+          the sentences (rank 0 computes the split from the host copy of cu_seqlens and sends it
+          in the header, with each slice's longest sentence, so no rank reads cu_seqlens back
+          from the device) -> the pooled rows, padded to the largest slice, are all_gathered over
+          xGMI as bf16 (f32 on gloo) -> rank 0 reassembles [B, H] in input order as f32.
   STOP  : header only.
 
-Messages are tiny next to the work (a 256 x 128-token batch is 256 KB of ids in, 256 x H x 4 B of
+Messages are tiny next to the work (a 256 x 128-token batch is 256 KB of ids in, 256 x H x 2 B of
 embeddings out), so one broadcast + one all_gather per batch keeps every link's share small.  The
 slice each rank encodes runs on its own compute stream; rank 0's H2D of the next batch overlaps
-through the embed batcher's copy stream (services/batcher.py).  Ranks 1..N-1 run ``serve()``.
+through the embed batcher's copy stream (services/batcher.py).  Ranks 1..N-1 run ``serve()``; the
+header is the only host read a batch costs them (they must learn its shapes to receive it).
+The bf16 wire rounds each pooled value once (relative 2^-9; cosine to the f32 rows >= 0.99999,
+tests/test_parallel_cpu.py); ``wire_dtype`` = torch.float32 keeps the f32 values exactly.
 """
 from __future__ import annotations
 
@@ -42,8 +46,12 @@ def split_by_tokens(cu: np.ndarray, world: int) -> list[tuple[int, int]]:
     return [(bounds[r], bounds[r + 1]) for r in range(world)]
 
 
+HDR_FIXED = 5    # op, B, T, wire (0 = f32, 1 = bf16), maxb
+HDR_RANK = 5     # then per rank: sentences [s, e), tokens [t0, t1), the slice's longest sentence
+
+
 class EmbedGroup:
-    def __init__(self, info: DistInfo, encoder, group=None):
+    def __init__(self, info: DistInfo, encoder, group=None, wire_dtype=None):
         self.info = info
         self.enc = encoder
         self.group = group
@@ -52,6 +60,12 @@ class EmbedGroup:
         self._lock = threading.Lock()
         # a single-rank process group still runs every collective (RCCL tests on one GPU)
         self.collective = info.world > 1 or info.backend != "none"
+        # the embeddings' wire format: bf16 over RCCL (half the bytes), f32 on gloo (no bf16
+        # collectives on every build)
+        if wire_dtype is None:
+            wire_dtype = torch.bfloat16 if info.backend == "nccl" else torch.float32
+        self.wire_dtype = wire_dtype
+        self.hdr_len = HDR_FIXED + HDR_RANK * info.world
 
     # ------------------------------------------------------------------ plumbing
     def _bcast(self, t: torch.Tensor) -> torch.Tensor:
@@ -59,70 +73,95 @@ class EmbedGroup:
             dist.broadcast(t, src=0, group=self.group)
         return t
 
-    def _header(self, op: int, a: int = 0, b: int = 0) -> torch.Tensor:
-        return self._bcast(torch.tensor([op, a, b, 0], dtype=torch.int64, device=self.comm_device))
+    def _header(self, vals=None) -> list[int]:
+        """Broadcast the op header from rank 0 (vals) / receive it (vals None); host ints."""
+        t = torch.zeros(self.hdr_len, dtype=torch.int64, device=self.comm_device)
+        if vals is not None:
+            t.copy_(torch.tensor(vals + [0] * (self.hdr_len - len(vals)), dtype=torch.int64))
+            self._bcast(t)
+            return vals
+        return self._bcast(t).tolist()
 
-    def _do_embed(self, cu: torch.Tensor, toks: torch.Tensor) -> torch.Tensor | None:
+    def _plan(self, cu_host: np.ndarray) -> list[int]:
+        """Rank 0: the EMBED header for a batch with these (host) cu_seqlens."""
+        B, T = len(cu_host) - 1, int(cu_host[-1])
+        ranges = split_by_tokens(cu_host, self.info.world)
+        maxb = max(1, max(e - s for s, e in ranges))
+        per = []
+        for s, e in ranges:
+            ml = int(np.diff(cu_host[s:e + 1]).max()) if e > s else 0
+            per += [s, e, int(cu_host[s]), int(cu_host[e]), ml]
+        wire = 1 if self.wire_dtype == torch.bfloat16 else 0
+        return [OP_EMBED, B, T, wire, maxb] + per
+
+    def _do_embed(self, hdr: list[int], cu: torch.Tensor, toks: torch.Tensor) -> torch.Tensor | None:
         info = self.info
-        cu_np = cu.cpu().numpy()
-        ranges = split_by_tokens(cu_np, info.world)
-        s, e = ranges[info.rank]
-        maxb = max(1, max(b - a for a, b in ranges))
-        out = torch.zeros(maxb, self.H, dtype=torch.float32, device=self.comm_device)
+        maxb = hdr[4]
+        wdt = torch.bfloat16 if hdr[3] else torch.float32
+        def part(r):
+            return hdr[HDR_FIXED + HDR_RANK * r:HDR_FIXED + HDR_RANK * (r + 1)]
+        ranges = [tuple(part(r)[:2]) for r in range(info.world)]
+        s, e, t0, t1, max_len = part(info.rank)
+        out = torch.zeros(maxb, self.H, dtype=wdt, device=self.comm_device)
         if e > s:
-            t0, t1 = int(cu_np[s]), int(cu_np[e])
             dev = getattr(self.enc, "device", torch.device("cpu"))
-            lens = np.diff(cu_np[s:e + 1])
+            # the slice's sentences and tokens by the header's host offsets: no device read
             local = PackedBatch(toks[0, t0:t1].to(dev), toks[1, t0:t1].to(dev), None,
-                                (cu[s:e + 1] - t0).to(dev, torch.int32), int(lens.max()))
+                                (cu[s:e + 1] - t0).to(dev, torch.int32), max_len)
             pooled, _ = self.enc.forward_packed(local)
-            out[:e - s].copy_(pooled.float())
+            out[:e - s].copy_(pooled)
         if not self.collective:
-            return out[:e - s]
-        gathered = torch.empty(info.world * maxb, self.H, dtype=torch.float32, device=self.comm_device)
+            return out[:e - s].float()
+        gathered = torch.empty(info.world * maxb, self.H, dtype=wdt, device=self.comm_device)
         dist.all_gather_into_tensor(gathered, out, group=self.group)
         if not info.is_root:
             return None
-        return torch.cat([gathered[r * maxb: r * maxb + (b - a)] for r, (a, b) in enumerate(ranges)])
+        return torch.cat([gathered[r * maxb: r * maxb + (b - a)] for r, (a, b) in
+                          enumerate(ranges)]).float()
 
     # ------------------------------------------------------------------ collective entry points
-    def embed(self, b: PackedBatch | None) -> torch.Tensor | None:
-        """Collective: rank 0 passes the batch (any device), the others pass None (or run
-        ``serve``).  Returns the pooled f32 embeddings [B, H] on rank 0, None elsewhere."""
+    def embed(self, b: PackedBatch | None, cu_host=None) -> torch.Tensor | None:
+        """Collective: rank 0 passes the batch (any device) and, when it has one, a host copy of
+        its cu_seqlens (``cu_host``: else rank 0 reads them back once); the others pass None (or
+        run ``serve``).  Returns the pooled f32 embeddings [B, H] on rank 0, None elsewhere."""
         info = self.info
         with self._lock:
             if info.is_root:
-                B, T = b.num_seqs, b.num_tokens
-                self._header(OP_EMBED, B, T)
+                if cu_host is None:
+                    cu_host = b.cu_seqlens.cpu()
+                cu_np = np.asarray(cu_host, dtype=np.int64)
+                hdr = self._header(self._plan(cu_np))
                 cu = self._bcast(b.cu_seqlens.to(self.comm_device, torch.int32).contiguous())
                 toks = self._bcast(torch.stack([b.ids.to(self.comm_device, torch.int32),
                                                 b.pos.to(self.comm_device, torch.int32)]).contiguous())
             else:
-                h = self._header(OP_STOP).tolist()
-                if h[0] != OP_EMBED:
-                    raise RuntimeError(f"embed group: expected EMBED, got op {h[0]}")
-                B, T = h[1], h[2]
-                cu = self._bcast(torch.empty(B + 1, dtype=torch.int32, device=self.comm_device))
-                toks = self._bcast(torch.empty(2, T, dtype=torch.int32, device=self.comm_device))
-            return self._do_embed(cu, toks)
+                hdr = self._header()
+                if hdr[0] != OP_EMBED:
+                    raise RuntimeError(f"embed group: expected EMBED, got op {hdr[0]}")
+                cu, toks = self._recv_batch(hdr)
+            return self._do_embed(hdr, cu, toks)
+
+    def _recv_batch(self, hdr):
+        cu = self._bcast(torch.empty(hdr[1] + 1, dtype=torch.int32, device=self.comm_device))
+        toks = self._bcast(torch.empty(2, hdr[2], dtype=torch.int32, device=self.comm_device))
+        return cu, toks
 
     def stop(self) -> None:
         if self.info.is_root and self.info.world > 1:
             with self._lock:
-                self._header(OP_STOP)
+                self._header([OP_STOP])
 
     def serve(self) -> None:
         """Ranks 1..N-1: execute rank 0's ops until STOP."""
         assert not self.info.is_root
         while True:
-            h = self._header(OP_STOP).tolist()
-            if h[0] == OP_STOP:
+            hdr = self._header()
+            if hdr[0] == OP_STOP:
                 return
-            if h[0] != OP_EMBED:
-                raise RuntimeError(f"unknown embed op {h[0]}")
-            cu = self._bcast(torch.empty(h[1] + 1, dtype=torch.int32, device=self.comm_device))
-            toks = self._bcast(torch.empty(2, h[2], dtype=torch.int32, device=self.comm_device))
-            self._do_embed(cu, toks)
+            if hdr[0] != OP_EMBED:
+                raise RuntimeError(f"unknown embed op {hdr[0]}")
+            cu, toks = self._recv_batch(hdr)
+            self._do_embed(hdr, cu, toks)
 
 
 class GroupEncoder:

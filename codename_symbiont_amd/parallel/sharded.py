@@ -8,7 +8,20 @@ Replaces Qdrant's single-node HNSW (services/vector_memory_service/src/main.rs:2
 
 Message sizes are tiny (nq x D bf16 queries, nq x k x (f32+i64) results) and xGMI is a full mesh
 of point-to-point links, so all_gather / all_to_all (direct, α-dominated) are used and
-all_reduce is avoided entirely.  Global point ids are ``rank << 40 | row``.
+all_reduce is avoided entirely: exactly TWO collectives per search, the query all_gather and ONE
+all_to_all of the packed (score, id) lists (12 bytes per entry as int32 triples).  Global point
+ids are ``rank << 40 | row``.
+
+Stream order of the pipelined step (bench.py: ``begin`` of batch i+1 on a pre-pass stream, then
+``end`` of batch i on the compute stream).  Every rank issues the collectives in the same host
+order -- all_gather(i+1), all_to_all(i), all_gather(i+2), ... -- which is what RCCL requires of
+one communicator; torch's ProcessGroupNCCL runs them on the group's internal stream in that order,
+each after the issuing stream's prior work (an event wait).  all_gather(i+1) depends only on
+batch i+1's encoder, all_to_all(i) on batch i's scan, and neither stream waits on the other's
+collective, so no rank can block on a peer that is itself blocked: the order is deadlock-free for
+any world size (tests/test_parallel_cpu.py rehearses it on gloo up to 8 ranks).  Its cost: the
+all_to_all of batch i queues behind the all_gather of batch i+1, which is issued under batch i's
+scan; an RCCL kernel that waits for a late peer there occupies a few CUs of the scan.
 """
 from __future__ import annotations
 
@@ -54,12 +67,21 @@ class ShardedSearcher:
         q_all = torch.empty(info.world * nq, D, dtype=self.wire_dtype, device=q_send.device)
         dist.all_gather_into_tensor(q_all, q_send, group=self.group)
         s, r = self.shard.search(q_all.to(torch.bfloat16), k)
-        gid = encode_gid(info.rank, r)
-        s_recv = torch.empty_like(s)
-        g_recv = torch.empty_like(gid)
-        dist.all_to_all_single(s_recv, s.contiguous(), group=self.group)
-        dist.all_to_all_single(g_recv, gid.contiguous(), group=self.group)
-        return merge_ranked(s_recv.view(info.world, nq, k), g_recv.view(info.world, nq, k), k)
+        self.collectives += 1
+        return self._exchange(s, encode_gid(info.rank, r), nq, k)
+
+    collectives = 0   # collectives issued (tests: 2 per search)
+
+    def _exchange(self, s: torch.Tensor, gid: torch.Tensor, nq: int, k: int):
+        """ONE all_to_all of the per-rank (score, id) lists packed as int32 triples [W*nq, k, 3]
+        (score bits, id low, id high), then the k-way merge of what came back."""
+        W = self.info.world
+        packed = pack_results(s, gid)
+        recv = torch.empty_like(packed)
+        dist.all_to_all_single(recv, packed, group=self.group)
+        self.collectives += 1
+        s_recv, g_recv = unpack_results(recv)
+        return merge_ranked(s_recv.view(W, nq, k), g_recv.view(W, nq, k), k)
 
 
     def begin(self, q_local: torch.Tensor, k: int) -> dict:
@@ -73,6 +95,7 @@ class ShardedSearcher:
         q_send = q_local.to(self.wire_dtype).contiguous()
         q_all = torch.empty(info.world * nq, D, dtype=self.wire_dtype, device=q_send.device)
         dist.all_gather_into_tensor(q_all, q_send, group=self.group)
+        self.collectives += 1
         return {"ctx": self.shard.search_begin(q_all.to(torch.bfloat16), k), "k": k, "nq": nq}
 
     def end(self, h: dict):
@@ -80,13 +103,7 @@ class ShardedSearcher:
         s, r = self.shard.search_end(h["ctx"])
         if not self.collective:
             return s, encode_gid(0, r)
-        nq = h["nq"]
-        gid = encode_gid(info.rank, r)
-        s_recv = torch.empty_like(s)
-        g_recv = torch.empty_like(gid)
-        dist.all_to_all_single(s_recv, s.contiguous(), group=self.group)
-        dist.all_to_all_single(g_recv, gid.contiguous(), group=self.group)
-        return merge_ranked(s_recv.view(info.world, nq, k), g_recv.view(info.world, nq, k), k)
+        return self._exchange(s, encode_gid(info.rank, r), h["nq"], k)
 
 
 class SimulatedShardedSearcher(ShardedSearcher):
@@ -124,14 +141,13 @@ class SimulatedShardedSearcher(ShardedSearcher):
         return torch.cat([q_own.to(torch.bfloat16), f[:(self.vworld - 1) * nq]])
 
     def _exchange(self, s: torch.Tensor, gid: torch.Tensor, nq: int, k: int):
-        s_recv = torch.empty_like(s)
-        g_recv = torch.empty_like(gid)
+        packed = pack_results(s, gid)
+        recv = torch.empty_like(packed)
         if self.collective:
-            dist.all_to_all_single(s_recv, s.contiguous(), group=self.group)
-            dist.all_to_all_single(g_recv, gid.contiguous(), group=self.group)
+            dist.all_to_all_single(recv, packed, group=self.group)
         else:
-            s_recv.copy_(s)
-            g_recv.copy_(gid)
+            recv.copy_(packed)
+        s_recv, g_recv = unpack_results(recv)
         return merge_ranked(s_recv.view(self.vworld, nq, k), g_recv.view(self.vworld, nq, k), k)
 
     def search(self, q_local: torch.Tensor, k: int):
@@ -146,6 +162,21 @@ class SimulatedShardedSearcher(ShardedSearcher):
     def end(self, h: dict):
         s, r = self.shard.search_end(h["ctx"])
         return self._exchange(s, encode_gid(0, r), h["nq"], h["k"])
+
+
+def pack_results(s: torch.Tensor, gid: torch.Tensor) -> torch.Tensor:
+    """[n, k] f32 scores + [n, k] int64 ids -> [n, k, 3] int32 (score bits, id lo, id hi): one
+    buffer, one collective."""
+    n, k = s.shape
+    return torch.cat([s.contiguous().view(torch.int32).view(n, k, 1),
+                      gid.contiguous().view(torch.int32).view(n, k, 2)], 2)
+
+
+def unpack_results(p: torch.Tensor):
+    """Inverse of pack_results: ([n, k] f32, [n, k] int64)."""
+    n, k, _ = p.shape
+    return (p[:, :, 0].contiguous().view(torch.float32),
+            p[:, :, 1:].contiguous().view(torch.int64).view(n, k))
 
 
 def merge_ranked(scores: torch.Tensor, gids: torch.Tensor, k: int):

@@ -25,6 +25,49 @@ def _init(rank, world, port):
     return D.init(backend="gloo", device_type="cpu")
 
 
+def _pipelined_worker(rank, world, port, out):
+    """The bench's pipelined order on every rank: begin(i + 1) (query all_gather + pre-pass) is
+    issued BEFORE end(i) (the packed all_to_all + merge); results equal plain search(), and each
+    search costs exactly two collectives."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+    from codename_symbiont_amd.parallel import dist as D
+    from codename_symbiont_amd.parallel.sharded import ShardedSearcher
+    info = _init(rank, world, port)
+    D_, n, nq, k, steps = 32, 300, 5, 4, 4
+    g = torch.Generator().manual_seed(1)
+    all_rows = torch.nn.functional.normalize(torch.randn(world * n, D_, generator=g), dim=-1)
+    qs = [torch.nn.functional.normalize(torch.randn(world * nq, D_, generator=g), dim=-1)
+          for _ in range(steps)]
+    shard = HbmIndexShard(D_, n, device="cpu")
+    shard.append_unit(all_rows[rank * n:(rank + 1) * n].bfloat16())
+    sr = ShardedSearcher(shard, info)
+    mine = [q[rank * nq:(rank + 1) * nq].bfloat16() for q in qs]
+    plain = [sr.search(q, k) for q in mine]
+    c0 = sr.collectives
+    h = {0: sr.begin(mine[0], k)}
+    piped = []
+    for i in range(steps):
+        if i + 1 < steps:
+            h[i + 1] = sr.begin(mine[i + 1], k)   # batch i+1's all_gather before batch i's end
+        piped.append(sr.end(h.pop(i)))
+    out[rank] = (all(torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+                     for a, b in zip(plain, piped)), c0, sr.collectives - c0)
+    D.barrier(info)
+    D.shutdown(info)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_sharded_pipelined_order_matches_search(world):
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.start_processes(_pipelined_worker, args=(world, _free_port(), out), nprocs=world, join=True,
+                       start_method="spawn")
+    for r in range(world):
+        same, c_plain, c_piped = out[r]
+        assert same, f"rank {r}: pipelined results differ"
+        assert c_plain == 2 * 4 and c_piped == 2 * 4   # all_gather + ONE packed all_to_all each
+
+
 def _sharded_worker(rank, world, port, out):
     from codename_symbiont_amd.index.shard import HbmIndexShard
     from codename_symbiont_amd.parallel import dist as D
@@ -71,14 +114,15 @@ def _embed_batches(cfg):
             for lens in _EMBED_LENS]
 
 
-def _embed_worker(rank, world, port, out):
+def _embed_worker(rank, world, port, out, wire=None):
     from codename_symbiont_amd.models import get_config
     from codename_symbiont_amd.models.encoder import TorchEncoder
     from codename_symbiont_amd.parallel import dist as D
     from codename_symbiont_amd.parallel.embed_group import EmbedGroup, GroupEncoder
     info = _init(rank, world, port)
     cfg = get_config("minilm-l6")
-    group = EmbedGroup(info, TorchEncoder(cfg, seed=0))
+    group = EmbedGroup(info, TorchEncoder(cfg, seed=0),
+                       wire_dtype=None if wire is None else getattr(torch, wire))
     if info.is_root:
         enc = GroupEncoder(group)
         out[0] = [enc.forward_packed(b)[0].numpy() for b in _embed_batches(cfg)]
@@ -89,10 +133,12 @@ def _embed_worker(rank, world, port, out):
     D.shutdown(info)
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])   # 8: the driver's N=8 rank count, on gloo
 def test_embed_group_matches_single_process(world):
-    """DP embedding over the group (token-balanced slices, all_gather back to rank 0) returns the
-    same pooled embeddings, in input order, as one process encoding the whole batch."""
+    """DP embedding over the group (token-balanced slices planned by rank 0 and sent in the
+    header, all_gather back to rank 0) returns the same pooled embeddings, in input order, as one
+    process encoding the whole batch -- also when ranks get no sentence at all (world 8, a
+    2-sentence batch)."""
     from codename_symbiont_amd.models import get_config
     from codename_symbiont_amd.models.encoder import TorchEncoder
     from codename_symbiont_amd.parallel.embed_group import split_by_tokens
@@ -109,6 +155,28 @@ def test_embed_group_matches_single_process(world):
     ref = TorchEncoder(cfg, seed=0)
     for got, b in zip(out[0], _embed_batches(cfg)):
         np.testing.assert_allclose(got, ref.forward_packed(b)[0].numpy(), rtol=1e-4, atol=1e-4)
+
+
+def test_embed_group_bf16_wire():
+    """The RCCL default wire (bf16 pooled rows) rounds each value once: every row keeps cosine
+    >= 0.99999 to the f32 embedding (run here over gloo when its build has bf16 collectives)."""
+    from codename_symbiont_amd.models import get_config
+    from codename_symbiont_amd.models.encoder import TorchEncoder
+
+    mgr = mp.Manager()
+    out = mgr.dict()
+    try:
+        mp.start_processes(_embed_worker, args=(2, _free_port(), out, "bfloat16"), nprocs=2,
+                           join=True, start_method="spawn")
+    except Exception as e:   # noqa: BLE001 -- a gloo build without bf16 all_gather
+        pytest.skip(f"gloo bf16 collectives unavailable: {e}")
+    cfg = get_config("minilm-l6")
+    ref = TorchEncoder(cfg, seed=0)
+    for got, b in zip(out[0], _embed_batches(cfg)):
+        want = ref.forward_packed(b)[0]
+        cos = torch.nn.functional.cosine_similarity(torch.from_numpy(got), want, dim=-1)
+        assert cos.min().item() >= 0.99999, cos
+        np.testing.assert_allclose(got, want.numpy(), rtol=2 ** -8, atol=1e-6)
 
 
 def _group_worker(rank, world, port, out):
@@ -193,8 +261,8 @@ def _group4_worker(rank, world, port, out):
     D.shutdown(info)
 
 
-def test_index_group_four_ranks_lean_search_matches_single_shard():
-    world = 4
+@pytest.mark.parametrize("world", [4, 8])   # 8: the driver's N=8 rank count, on gloo
+def test_index_group_four_ranks_lean_search_matches_single_shard(world):
     mgr = mp.Manager()
     out = mgr.dict()
     mp.start_processes(_group4_worker, args=(world, _free_port(), out), nprocs=world, join=True,
