@@ -82,8 +82,9 @@ int symb_index_scan_i8(const void* X8, const float* sx, int n_valid, int alloc_r
 int symb_quant_rows_mx4(const void* X, int n, int dim, void* X4, void* SC, float* bounds,
                         float* margin, hipStream_t st);
 int symb_mx4_select(int NQ, const float* T, const float* margin4, const float* margin8,
-                    const float* probe_s, int n_probe, float rate, const float* tail_cs,
-                    int tail_cap, float limit, float* thr4, int* nv, hipStream_t st);
+                    const float* probe_s, int n_cols, int ld, int tile_stride, float rate,
+                    const float* tail_cs, int tail_cap, int tail_ld, float limit, float* thr4,
+                    int* nv, hipStream_t st, int nv_zeroed);
 int symb_i8_tile_rows_for(int dim, int heavy);
 // the streaming pruning scan (index_stream.hip)
 int symb_stream_rec_bytes(int dim, int form);
@@ -93,7 +94,11 @@ int symb_index_scan_stream(const void* img, int n_valid, int alloc_rows, int row
                            int n_rblk, const void* Q, const void* qsc, int NQ, const float* thr,
                            float* cand_s, int* cand_i, int* cand_n, int cap, int xcd,
                            hipStream_t st, const int* skip, int dim, int form, const int* gate,
-                           int gate_want);
+                           int gate_want, int zero_cnt, int* runs);
+int symb_append_rows(const void* src, int n, int dim, void* rows, int r0, void* img8, float* b8,
+                     void* img4, float* b4, hipStream_t st);
+int symb_dense_scores(const void* X, int dim, const int* rows, int n_list, int r_lo, int n_range,
+                      const void* Q, int NQ, float* out, int ld, hipStream_t st);
 int symb_quant_stream_i8(const void* X, int r0, const int* rows, int n, int dim, void* img,
                          float* bounds, hipStream_t st);
 int symb_quant_stream_mx4(const void* X, int r0, const int* rows, int n, int dim, void* img,
@@ -104,14 +109,14 @@ int symb_mx4_tile_rows();
 int symb_quant_rows_split(const float* X, int n, int dim, void* X8, float* sx, float* bounds,
                           float* margin, hipStream_t st);
 int symb_prune_qquant(const void* Q, int NQ, int dim, const float* bounds, void* Q8, float* sq,
-                      float* margin, hipStream_t st);
+                      float* margin, hipStream_t st, int* zero, int zero_n);
 int symb_prune_route(int NQ, const float* pre_s, const float* tail_s, int k, float thr_margin,
                      const float* sq, const float* margin, const float* thr0, const float* cs_p,
                      const int* ci_p, const int* cnt_p, int cap_p, int tshift, int rows_per_blk,
                      int n_rblk, float blk_limit, float limit, int max_list, float* T, float* thr,
                      int* dense, float* est, int* blkmax, int* blk, hipStream_t st,
                      const float* tail_cs, const int* tail_ci, const int* tail_cnt, int tail_cap,
-                     int tail_off);
+                     int tail_off, int tail_ld, int zeroed);
 int symb_i8_config(int tile_rows, int waves);
 int symb_i8_tile_rows();
 int symb_i8_wgs_per_cu();
@@ -145,7 +150,8 @@ int symb_index_scan_mq_ablate(const void* X, int n_valid, int rows_per_blk, int 
                               int rsplit);
 int symb_topk_select_counted(const float* cand_s, const int* cand_i, const int* cand_n, int cap,
                              int NQ, int kmax, int k, float* out_s, int* out_i, int* ovf,
-                             hipStream_t st, const int* gate, int reset_ovf);
+                             hipStream_t st, const int* gate, int reset_ovf, int ld = 0,
+                             float* kth_out = nullptr, float kth_margin = 0.f);
 
 namespace {
 
@@ -486,17 +492,33 @@ PYBIND11_MODULE(_hip, m) {
   m.def("index_scan_stream", [](uptr img, int n_valid, int alloc_rows, int rows_per_blk, int n_rblk,
                                 uptr Q, uptr qsc, int NQ, uptr thr, uptr cand_s, uptr cand_i,
                                 uptr cand_n, int cap, int xcd, uptr st, uptr skip, int dim,
-                                int form, uptr gate, int gate_want) {
+                                int form, uptr gate, int gate_want, int zero_cnt, uptr runs) {
     check(symb_index_scan_stream(P<void>(img), n_valid, alloc_rows, rows_per_blk, n_rblk,
                                  P<void>(Q), P<void>(qsc), NQ, P<const float>(thr),
                                  P<float>(cand_s), P<int>(cand_i), P<int>(cand_n), cap, xcd, S(st),
-                                 P<const int>(skip), dim, form, P<const int>(gate), gate_want),
+                                 P<const int>(skip), dim, form, P<const int>(gate), gate_want,
+                                 zero_cnt, P<int>(runs)),
           "index_scan_stream");
   }, py::arg("img"), py::arg("n_valid"), py::arg("alloc_rows"), py::arg("rows_per_blk"),
      py::arg("n_rblk"), py::arg("Q"), py::arg("qsc"), py::arg("NQ"), py::arg("thr"),
      py::arg("cand_s"), py::arg("cand_i"), py::arg("cand_n"), py::arg("cap"), py::arg("xcd"),
      py::arg("stream"), py::arg("skip") = 0, py::arg("dim") = 384, py::arg("form") = 0,
-     py::arg("gate") = 0, py::arg("gate_want") = 0);
+     py::arg("gate") = 0, py::arg("gate_want") = 0, py::arg("zero_cnt") = 1, py::arg("runs") = 0);
+  m.def("append_rows", [](uptr src, int n, int dim, uptr rows, int r0, uptr img8, uptr b8,
+                          uptr img4, uptr b4, uptr st) {
+    check(symb_append_rows(P<void>(src), n, dim, P<void>(rows), r0, P<void>(img8), P<float>(b8),
+                           P<void>(img4), P<float>(b4), S(st)),
+          "append_rows");
+  }, py::arg("src"), py::arg("n"), py::arg("dim"), py::arg("rows"), py::arg("r0"),
+     py::arg("img8"), py::arg("b8"), py::arg("img4"), py::arg("b4"), py::arg("stream"));
+  m.def("dense_scores", [](uptr X, int dim, uptr rows, int n_list, int r_lo, int n_range, uptr Q,
+                           int NQ, uptr out, int ld, uptr st) {
+    check(symb_dense_scores(P<void>(X), dim, P<const int>(rows), n_list, r_lo, n_range,
+                            P<void>(Q), NQ, P<float>(out), ld, S(st)),
+          "dense_scores");
+  }, py::arg("X"), py::arg("dim"), py::arg("rows"), py::arg("n_list"), py::arg("r_lo"),
+     py::arg("n_range"), py::arg("Q"), py::arg("NQ"), py::arg("out"), py::arg("ld"),
+     py::arg("stream"));
   m.def("quant_stream_i8", [](uptr X, int r0, uptr rows, int n, int dim, uptr img, uptr bounds,
                               uptr st) {
     check(symb_quant_stream_i8(P<void>(X), r0, P<const int>(rows), n, dim, P<void>(img),
@@ -519,33 +541,38 @@ PYBIND11_MODULE(_hip, m) {
           "quant_rows_mx4");
   }, py::arg("X"), py::arg("n"), py::arg("dim"), py::arg("X4"), py::arg("SC"), py::arg("bounds"),
      py::arg("margin"), py::arg("stream"));
-  m.def("mx4_select", [](int NQ, uptr T, uptr margin4, uptr margin8, uptr probe_s, int n_probe,
+  m.def("mx4_select", [](int NQ, uptr T, uptr margin4, uptr margin8, uptr probe_s, int n_cols,
                          float rate, uptr tail_cs, int tail_cap, float limit, uptr thr4, uptr nv,
-                         uptr st) {
+                         uptr st, int ld, int tile_stride, int tail_ld, bool nv_zeroed) {
     check(symb_mx4_select(NQ, P<const float>(T), P<const float>(margin4), P<const float>(margin8),
-                          P<const float>(probe_s), n_probe, rate, P<const float>(tail_cs),
-                          tail_cap, limit, P<float>(thr4), P<int>(nv), S(st)),
+                          P<const float>(probe_s), n_cols, ld, tile_stride, rate,
+                          P<const float>(tail_cs), tail_cap, tail_ld, limit, P<float>(thr4),
+                          P<int>(nv), S(st), nv_zeroed ? 1 : 0),
           "mx4_select");
-  });
+  }, py::arg("NQ"), py::arg("T"), py::arg("margin4"), py::arg("margin8"), py::arg("probe_s"),
+     py::arg("n_cols"), py::arg("rate"), py::arg("tail_cs"), py::arg("tail_cap"), py::arg("limit"),
+     py::arg("thr4"), py::arg("nv"), py::arg("stream"), py::arg("ld") = 0,
+     py::arg("tile_stride") = 1, py::arg("tail_ld") = 0, py::arg("nv_zeroed") = false);
   m.def("prune_qquant", [](uptr Q, int NQ, int dim, uptr bounds, uptr Q8, uptr sq, uptr margin,
-                           uptr st) {
+                           uptr st, uptr zero, int zero_n) {
     check(symb_prune_qquant(P<void>(Q), NQ, dim, P<const float>(bounds), P<void>(Q8), P<float>(sq),
-                            P<float>(margin), S(st)),
+                            P<float>(margin), S(st), P<int>(zero), zero_n),
           "prune_qquant");
-  });
+  }, py::arg("Q"), py::arg("NQ"), py::arg("dim"), py::arg("bounds"), py::arg("Q8"), py::arg("sq"),
+     py::arg("margin"), py::arg("stream"), py::arg("zero") = 0, py::arg("zero_n") = 0);
   m.def("prune_route", [](int NQ, uptr pre_s, uptr tail_s, int k, float thr_margin, uptr sq,
                           uptr margin, uptr thr0, uptr cs_p, uptr ci_p, uptr cnt_p, int cap_p,
                           int tshift, int rows_per_blk, int n_rblk, float blk_limit, float limit,
                           int max_list, uptr T, uptr thr, uptr dense, uptr est, uptr blkmax,
                           uptr blk, uptr st, uptr tail_cs, uptr tail_ci, uptr tail_cnt,
-                          int tail_cap, int tail_off) {
+                          int tail_cap, int tail_off, int tail_ld, bool zeroed) {
     check(symb_prune_route(NQ, P<const float>(pre_s), P<const float>(tail_s), k, thr_margin,
                            P<const float>(sq), P<const float>(margin), P<const float>(thr0),
                            P<const float>(cs_p), P<const int>(ci_p), P<const int>(cnt_p), cap_p,
                            tshift, rows_per_blk, n_rblk, blk_limit, limit, max_list, P<float>(T),
                            P<float>(thr), P<int>(dense), P<float>(est), P<int>(blkmax),
                            P<int>(blk), S(st), P<const float>(tail_cs), P<const int>(tail_ci),
-                           P<const int>(tail_cnt), tail_cap, tail_off),
+                           P<const int>(tail_cnt), tail_cap, tail_off, tail_ld, zeroed ? 1 : 0),
           "prune_route");
   }, py::arg("NQ"), py::arg("pre_s"), py::arg("tail_s"), py::arg("k"), py::arg("thr_margin"),
      py::arg("sq"), py::arg("margin"), py::arg("thr0"), py::arg("cs_p"), py::arg("ci_p"),
@@ -553,7 +580,8 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("n_rblk"), py::arg("blk_limit"), py::arg("limit"), py::arg("max_list"), py::arg("T"),
      py::arg("thr"), py::arg("dense"), py::arg("est"), py::arg("blkmax"), py::arg("blk"),
      py::arg("stream"), py::arg("tail_cs") = 0, py::arg("tail_ci") = 0, py::arg("tail_cnt") = 0,
-     py::arg("tail_cap") = 0, py::arg("tail_off") = 0);
+     py::arg("tail_cap") = 0, py::arg("tail_off") = 0, py::arg("tail_ld") = 0,
+     py::arg("zeroed") = false);
   m.def("index_scan_i8_ablate", [](uptr X8, uptr sx, int n_valid, int alloc_rows,
                                    int rows_per_blk, int n_rblk, uptr Q8, int NQ, uptr thr,
                                    uptr cand_s, uptr cand_i, uptr cand_n, int cap, int xcd, uptr st,
@@ -620,15 +648,17 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("rsplit") = 1);
   m.def("topk_select_counted", [](uptr cand_s, uptr cand_i, uptr cand_n, int cap, int NQ,
                                   int kmax, int k, uptr out_s, uptr out_i, uptr ovf, uptr st,
-                                  uptr gate, bool reset_ovf) {
+                                  uptr gate, bool reset_ovf, int ld, uptr kth_out,
+                                  float kth_margin) {
     check(symb_topk_select_counted(P<const float>(cand_s), P<const int>(cand_i),
                                    P<const int>(cand_n), cap, NQ, kmax, k, P<float>(out_s),
                                    P<int>(out_i), P<int>(ovf), S(st), P<const int>(gate),
-                                   reset_ovf ? 1 : 0),
+                                   reset_ovf ? 1 : 0, ld, P<float>(kth_out), kth_margin),
           "topk_select_counted");
   }, py::arg("cand_s"), py::arg("cand_i"), py::arg("cand_n"), py::arg("cap"), py::arg("NQ"),
      py::arg("kmax"), py::arg("k"), py::arg("out_s"), py::arg("out_i"), py::arg("ovf"),
-     py::arg("stream"), py::arg("gate") = 0, py::arg("reset_ovf") = true);
+     py::arg("stream"), py::arg("gate") = 0, py::arg("reset_ovf") = true, py::arg("ld") = 0,
+     py::arg("kth_out") = 0, py::arg("kth_margin") = 0.f);
   m.def("index_scan_ablate", [](uptr X, int n_valid, int rows_per_blk, int n_rblk, uptr Q, int NQ,
                                 uptr cs, uptr ci, uptr st, int abl, uptr thr) {
     check(symb_index_scan_ablate(P<void>(X), n_valid, rows_per_blk, n_rblk, P<void>(Q), NQ,

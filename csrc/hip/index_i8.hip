@@ -872,14 +872,19 @@ __global__ __launch_bounds__(256) void prune_qprep_kernel(
 //                 (skip[b]), the bf16 scan at the exact threshold T scans only them, and both
 //                 emit into the same candidate buffers: every row is covered by exactly one
 //                 exact-bound scan.  Exactness never depends on the route; only the cost does.
+// zero (optional): the search's counter workspace (zero_n ints), cleared here so the search's
+// later kernels start from zeroed candidate counts and flags without memset launches.
 template <int D>
 __global__ __launch_bounds__(256) void prune_qquant_kernel(const __bf16* __restrict__ Q, int NQ,
                                                            const float* __restrict__ bounds,
                                                            int8_t* __restrict__ Q8,
                                                            float* __restrict__ sq,
-                                                           float* __restrict__ margin) {
+                                                           float* __restrict__ margin,
+                                                           int* __restrict__ zero, int zero_n) {
   constexpr int PER = D / 64;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (zero != nullptr)
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < zero_n; i += gridDim.x * 256) zero[i] = 0;
   const int q = blockIdx.x * 4 + w;
   if (q >= NQ) return;   // (no barrier in this kernel)
   float x[PER];
@@ -1106,11 +1111,13 @@ __global__ __launch_bounds__(256) void quant_rows_mx4_kernel(const __bf16* __res
 // crowd scoring above the int8 band (fresh near-duplicates) is left to the per-block route, as
 // in the int8 tier.  *nv ends 1 (not viable: the int8 tier runs) or stays 0 (the MX-fp4 tier
 // runs at thr4 = T - margin4).  Exactness never depends on the choice.
+// probe_s: [NQ][ld] exact scores; the probe is columns c < n_cols whose 64-row tile c / 64 is a
+// multiple of tile_stride (1: every column), scaled by `rate`; tail_cs: [NQ][tail_ld].
 __global__ __launch_bounds__(256) void mx4_select_kernel(
     int NQ, const float* __restrict__ T, const float* __restrict__ margin4,
-    const float* __restrict__ margin8, const float* __restrict__ probe_s, int n_probe, float rate,
-    const float* __restrict__ tail_cs, int tail_cap, float limit, float* __restrict__ thr4,
-    int* __restrict__ nv) {
+    const float* __restrict__ margin8, const float* __restrict__ probe_s, int n_cols, int ld,
+    int tile_stride, float rate, const float* __restrict__ tail_cs, int tail_cap, int tail_ld,
+    float limit, float* __restrict__ thr4, int* __restrict__ nv) {
   // one 256-thread workgroup per query (a wave per query took 146 us for 256 queries)
   __shared__ float red[2][4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1118,10 +1125,11 @@ __global__ __launch_bounds__(256) void mx4_select_kernel(
   const float t = T[q];
   const float lo = t - 2.f * margin4[q], hi = t - margin8[q];
   float c = 0.f;
-  const float* ps = probe_s + (size_t)q * n_probe;
-  for (int i = threadIdx.x; i < n_probe; i += 256) c += (ps[i] >= lo && ps[i] < hi) ? 1.f : 0.f;
+  const float* ps = probe_s + (size_t)q * ld;
+  for (int i = threadIdx.x; i < n_cols; i += 256)
+    if (((i >> 6) % tile_stride) == 0) c += (ps[i] >= lo && ps[i] < hi) ? 1.f : 0.f;
   float tc = 0.f;
-  const float* tcs = tail_cs + (size_t)q * tail_cap;
+  const float* tcs = tail_cs + (size_t)q * tail_ld;
   for (int i = threadIdx.x; i < tail_cap; i += 256) tc += (tcs[i] >= lo && tcs[i] < hi) ? 1.f : 0.f;
   c = wave_sum(c);
   tc = wave_sum(tc);
@@ -1148,6 +1156,7 @@ struct RouteTail {
   const int* cnt;
   int cap;
   int off;
+  int ld;    // row stride of cs (dense form; = cap unless the tail shares a wider score matrix)
 };
 
 __global__ __launch_bounds__(256) void prune_route_kernel(
@@ -1196,7 +1205,7 @@ __global__ __launch_bounds__(256) void prune_route_kernel(
   }
   const bool tail_dense = tail.cs != nullptr && tail.ci == nullptr;
   if (tail_dense) {   // the exact tail as dense scores [NQ][cap] (row i = tail.off + i)
-    const float* tcs = tail.cs + (size_t)q * tail.cap;
+    const float* tcs = tail.cs + (size_t)q * tail.ld;
     for (int i0 = 0; i0 < tail.cap; i0 += 64) {
       const int i = i0 + lane;
       const bool hit = i < tail.cap && tcs[i] >= band;
@@ -1508,15 +1517,22 @@ int symb_quant_rows_mx4(const void* X, int n, int dim, void* X4, void* SC, float
 // The MX-fp4 tier choice (mx4_select_kernel); nv (one int) is zeroed here.  probe_s: [NQ][n_probe]
 // exact scores of the probe rows, tail_cs: [NQ][tail_cap] exact scores of the tail rows.
 int symb_mx4_select(int NQ, const float* T, const float* margin4, const float* margin8,
-                    const float* probe_s, int n_probe, float rate, const float* tail_cs,
-                    int tail_cap, float limit, float* thr4, int* nv, hipStream_t st) {
+                    const float* probe_s, int n_cols, int ld, int tile_stride, float rate,
+                    const float* tail_cs, int tail_cap, int tail_ld, float limit, float* thr4,
+                    int* nv, hipStream_t st, int nv_zeroed) {
   if (NQ <= 0) return 0;
-  if (n_probe <= 0 || tail_cap < 0 || probe_s == nullptr || (tail_cap > 0 && tail_cs == nullptr))
+  if (ld <= 0) ld = n_cols;
+  if (tail_ld <= 0) tail_ld = tail_cap;
+  if (n_cols <= 0 || ld < n_cols || tile_stride < 1 || tail_cap < 0 || tail_ld < tail_cap ||
+      probe_s == nullptr || (tail_cap > 0 && tail_cs == nullptr))
     return -1;
-  hipError_t e = hipMemsetAsync(nv, 0, sizeof(int), st);
-  if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(mx4_select_kernel, dim3(NQ), dim3(256), 0, st, NQ, T, margin4,
-                     margin8, probe_s, n_probe, rate, tail_cs, tail_cap, limit, thr4, nv);
+  if (!nv_zeroed) {
+    hipError_t e = hipMemsetAsync(nv, 0, sizeof(int), st);
+    if (e != hipSuccess) return (int)e;
+  }
+  hipLaunchKernelGGL(mx4_select_kernel, dim3(NQ), dim3(256), 0, st, NQ, T, margin4, margin8,
+                     probe_s, n_cols, ld, tile_stride, rate, tail_cs, tail_cap, tail_ld, limit,
+                     thr4, nv);
   return (int)hipGetLastError();
 }
 
@@ -1534,10 +1550,12 @@ int symb_prune_qprep(const void* Q, int NQ, int dim, const float* pre_s, const f
 }
 
 int symb_prune_qquant(const void* Q, int NQ, int dim, const float* bounds, void* Q8, float* sq,
-                      float* margin, hipStream_t st) {
+                      float* margin, hipStream_t st, int* zero, int zero_n) {
   if (NQ <= 0) return 0;
+  if (zero_n < 0 || (zero_n > 0 && zero == nullptr)) return -1;
 #define L(D_) hipLaunchKernelGGL(prune_qquant_kernel<D_>, dim3((NQ + 3) / 4), dim3(256), 0, st, \
-                                 (const __bf16*)Q, NQ, bounds, (int8_t*)Q8, sq, margin)
+                                 (const __bf16*)Q, NQ, bounds, (int8_t*)Q8, sq, margin, zero,    \
+                                 zero_n)
   SYMB_BY_DIM(dim, L);
 #undef L
   return (int)hipGetLastError();
@@ -1555,20 +1573,24 @@ int symb_prune_route(int NQ, const float* pre_s, const float* tail_s, int k, flo
                      int n_rblk, float blk_limit, float limit, int max_list, float* T, float* thr,
                      int* dense, float* est, int* blkmax, int* blk, hipStream_t st,
                      const float* tail_cs, const int* tail_ci, const int* tail_cnt, int tail_cap,
-                     int tail_off) {
+                     int tail_off, int tail_ld, int zeroed) {
   if (NQ <= 0) return 0;
   if (k < 1 || k > 32 || cap_p <= 0 || tshift < 0 || tshift > 20) return -1;
   if (n_rblk < 1 || n_rblk > ROUTE_MAX_BLOCKS || rows_per_blk < 1 || max_list < 1) return -1;
   // tail_ci == nullptr: tail_cs holds DENSE scores [NQ][tail_cap] of rows tail_off + i
   if (tail_cs != nullptr && ((tail_ci != nullptr) != (tail_cnt != nullptr) || tail_cap < 1 || tail_off < 0))
     return -1;
-  hipError_t e = hipMemsetAsync(dense, 0, sizeof(int), st);
-  if (e == hipSuccess) e = hipMemsetAsync(blkmax, 0, sizeof(int) * (size_t)n_rblk, st);
-  if (e != hipSuccess) return (int)e;
+  if (tail_ld <= 0) tail_ld = tail_cap;
+  if (tail_cs != nullptr && tail_ld < tail_cap) return -1;
+  if (!zeroed) {   // (zeroed: the caller's workspace, cleared by prune_qquant)
+    hipError_t e = hipMemsetAsync(dense, 0, sizeof(int), st);
+    if (e == hipSuccess) e = hipMemsetAsync(blkmax, 0, sizeof(int) * (size_t)n_rblk, st);
+    if (e != hipSuccess) return (int)e;
+  }
   hipLaunchKernelGGL(prune_route_kernel, dim3((NQ + 3) / 4), dim3(256), 0, st, NQ, pre_s, tail_s,
                      k, thr_margin, sq, margin, thr0, cs_p, ci_p, cnt_p, cap_p, tshift,
                      rows_per_blk, n_rblk, T, thr, dense, est, blkmax,
-                     RouteTail{tail_cs, tail_ci, tail_cnt, tail_cap, tail_off});
+                     RouteTail{tail_cs, tail_ci, tail_cnt, tail_cap, tail_off, tail_ld});
   hipLaunchKernelGGL(prune_route_final_kernel, dim3(1), dim3(1024), 0, st, NQ, n_rblk, est, blkmax,
                      blk_limit, limit, max_list, dense, blk);
   return (int)hipGetLastError();

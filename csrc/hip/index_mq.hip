@@ -431,7 +431,8 @@ template <int KMAX, int NTH>
 __global__ __launch_bounds__(NTH) void topk_select_counted_kernel(
     const float* __restrict__ cand_s, const int* __restrict__ cand_i,
     const int* __restrict__ cand_n, int cap, int k, float* __restrict__ out_s,
-    int* __restrict__ out_i, int* __restrict__ ovf, const int* __restrict__ gate) {
+    int* __restrict__ out_i, int* __restrict__ ovf, const int* __restrict__ gate, int ld,
+    float* __restrict__ kth_out, float kth_margin) {
   if (gate != nullptr && *gate == 0) return;   // (grid-uniform, before any barrier)
   __shared__ float ls[NTH * KMAX];
   __shared__ int li[NTH * KMAX];
@@ -441,8 +442,8 @@ __global__ __launch_bounds__(NTH) void topk_select_counted_kernel(
   const int cnt = cand_n != nullptr ? cand_n[q] : cap;
   const int n = min(cnt, cap);
   if (tid == 0 && cnt > cap) *ovf = 1;
-  const float* cs = cand_s + (size_t)q * cap;
-  const int* ci = cand_i != nullptr ? cand_i + (size_t)q * cap : nullptr;
+  const float* cs = cand_s + (size_t)q * ld;
+  const int* ci = cand_i != nullptr ? cand_i + (size_t)q * ld : nullptr;
   float tv[KMAX];
   int ti[KMAX];
 #pragma unroll
@@ -492,6 +493,8 @@ __global__ __launch_bounds__(NTH) void topk_select_counted_kernel(
     out_s[(size_t)q * k + tid] = tid < KMAX ? ls[tid] : -INFINITY;
     out_i[(size_t)q * k + tid] = tid < KMAX ? li[tid] : -1;
   }
+  // (optional) the k-th best minus a margin: a seed threshold for the next scan, no torch op
+  if (kth_out != nullptr && tid == 0) kth_out[q] = (k <= KMAX ? ls[k - 1] : -INFINITY) - kth_margin;
 }
 
 // Top-k of each query's emitted candidates for ANY k <= SEL_MAX (the reference passes top_k
@@ -755,10 +758,14 @@ int symb_index_scan_mq_ablate(const void* X, int n_valid, int rows_per_blk, int 
 // gate (optional): the launch is skipped on the device unless *gate != 0.
 int symb_topk_select_counted(const float* cand_s, const int* cand_i, const int* cand_n, int cap,
                              int NQ, int kmax, int k, float* out_s, int* out_i, int* ovf,
-                             hipStream_t st, const int* gate, int reset_ovf) {
+                             hipStream_t st, const int* gate, int reset_ovf, int ld,
+                             float* kth_out, float kth_margin) {
   if (NQ <= 0) return 0;
   if (k > kmax) return -1;
+  if (ld <= 0) ld = cap;
+  if (ld < cap) return -1;
   if (kmax == sel::SEL_MAX && (cand_i == nullptr || cand_n == nullptr)) return -1;   // (dense rows: KMAX 16 / 32 forms)
+  if (kmax == sel::SEL_MAX && (ld != cap || kth_out != nullptr)) return -1;
   if (reset_ovf) {
     hipError_t e = hipMemsetAsync(ovf, 0, sizeof(int), st);
     if (e != hipSuccess) return (int)e;
@@ -768,10 +775,10 @@ int symb_topk_select_counted(const float* cand_s, const int* cand_i, const int* 
                        cand_n, cap, k, out_s, out_i, ovf, gate);
   else if (kmax == 16)
     hipLaunchKernelGGL((topk_select_counted_kernel<16, 256>), dim3(NQ), dim3(256), 0, st, cand_s,
-                       cand_i, cand_n, cap, k, out_s, out_i, ovf, gate);
+                       cand_i, cand_n, cap, k, out_s, out_i, ovf, gate, ld, kth_out, kth_margin);
   else if (kmax == 32)
     hipLaunchKernelGGL((topk_select_counted_kernel<32, 128>), dim3(NQ), dim3(128), 0, st, cand_s,
-                       cand_i, cand_n, cap, k, out_s, out_i, ovf, gate);
+                       cand_i, cand_n, cap, k, out_s, out_i, ovf, gate, ld, kth_out, kth_margin);
   else
     return -1;
   return (int)hipGetLastError();

@@ -101,7 +101,8 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
     const uint8_t* __restrict__ img, int n_valid, int rows_per_blk, const uint8_t* __restrict__ Q,
     const uint32_t* __restrict__ qsc, int NQ, int n_qblk, int xcd, const float* __restrict__ thr_in,
     float* __restrict__ cand_s, int* __restrict__ cand_i, int* __restrict__ cand_n, int cap,
-    const int* __restrict__ skip, const int* __restrict__ gate, int gate_want) {
+    const int* __restrict__ skip, const int* __restrict__ gate, int gate_want,
+    int* __restrict__ runs) {
   using S = SDim<FMT, D>;
   using G = SGeo<FMT, D, V>;
   constexpr int NKS = S::NKS, NSC = S::NSC ? S::NSC : 1, REC = S::REC;
@@ -110,8 +111,10 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
   const int lb = xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
   const int qb = lb % n_qblk, rb = lb / n_qblk;
-  if (skip != nullptr && skip[rb] != 0) return;   // (routed to the bf16 scan; no barrier here)
-  if (gate != nullptr && *gate != gate_want) return;
+  if (gate != nullptr && *gate != gate_want) return;   // (no barrier in this kernel)
+  // runs (optional): counts the launches that passed the gate (the MX-fp4 tier's batches)
+  if (runs != nullptr && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(runs, 1);
+  if (skip != nullptr && skip[rb] != 0) return;   // (routed to the bf16 scan)
   const int row_begin = rb * rows_per_blk;
   const int row_end = min(row_begin + rows_per_blk, n_valid);
   if (row_end <= row_begin) return;
@@ -265,65 +268,44 @@ __device__ __forceinline__ size_t stream_frag_off(int rec, int hdr, int r, int b
   return (size_t)(r >> 5) * rec + hdr + 1024 * (b >> 5) + 16 * (32 * ((b >> 4) & 1) + rr) + (b & 15);
 }
 
-// int8 image of bf16 rows [r0, r0 + n) (or of the rows listed in `rows`, n of them): per-row scale
-// sx = max|x| / 127, x8 = round(x / sx) -- quant_rows_i8_kernel's numbers in the stream layout.
-// bounds (2 floats) raised to (max |x - x~|, max |x~|).  One wave per row.
+// One row's int8 stream image (quant_rows_i8_kernel's numbers: sx = max|x| / 127, x8 =
+// round(x / sx)): codes at row `row` of img, its scale in the sub-tile header; en / nn =
+// |x - x~| / |x~| in every lane.  One wave; lane l holds elements PER l .. PER l + PER - 1.
 template <int D>
-__global__ __launch_bounds__(256) void quant_stream_i8_kernel(const __bf16* __restrict__ X, int r0,
-                                                              const int* __restrict__ rows, int n,
-                                                              uint8_t* __restrict__ img,
-                                                              float* __restrict__ bounds) {
+__device__ __forceinline__ void i8_stream_row(const __bf16* __restrict__ xrow, int row,
+                                              uint8_t* __restrict__ img, float& en, float& nn) {
   using S = SDim<SF_I8, D>;
-  __shared__ float red[2][4];
   constexpr int PER = D / 64;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int j = blockIdx.x * 4 + w;
-  if (j >= n) {   // (block-uniform barrier below)
-    if (lane == 0) red[0][w] = red[1][w] = 0.f;
-    __syncthreads();
-    goto reduce;
+  const int lane = threadIdx.x & 63;
+  float x[PER];
+  const uint32_t* xp = reinterpret_cast<const uint32_t*>(xrow + PER * lane);
+#pragma unroll
+  for (int i = 0; i < PER / 2; ++i) {
+    const uint32_t u = xp[i];
+    x[2 * i] = __uint_as_float(u << 16);
+    x[2 * i + 1] = __uint_as_float(u & 0xffff0000u);
   }
-  {
-    const int row = rows ? rows[j] : r0 + j;
-    float x[PER];
-    const uint32_t* xp = reinterpret_cast<const uint32_t*>(X + (size_t)row * D + PER * lane);
+  float amax = 0.f;
 #pragma unroll
-    for (int i = 0; i < PER / 2; ++i) {
-      const uint32_t u = xp[i];
-      x[2 * i] = __uint_as_float(u << 16);
-      x[2 * i + 1] = __uint_as_float(u & 0xffff0000u);
-    }
-    float amax = 0.f;
+  for (int i = 0; i < PER; ++i) amax = fmaxf(amax, fabsf(x[i]));
+  amax = wave_max(amax);
+  const float s = amax > 0.f ? amax / 127.f : 1.f;
+  const float inv = 1.f / s;
+  float e2 = 0.f, n2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < PER; ++i) amax = fmaxf(amax, fabsf(x[i]));
-    amax = wave_max(amax);
-    const float s = amax > 0.f ? amax / 127.f : 1.f;
-    const float inv = 1.f / s;
-    float e2 = 0.f, n2 = 0.f;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int qv = max(-127, min(127, (int)rintf(x[i] * inv)));
-      const float xt = (float)qv * s;
-      e2 += (x[i] - xt) * (x[i] - xt);
-      n2 += xt * xt;
-      img[stream_frag_off(S::REC, S::HDR, row, PER * lane + i)] = (uint8_t)(qv & 0xff);
-    }
-    e2 = wave_sum(e2);
-    n2 = wave_sum(n2);
-    if (lane == 0) {
-      const int rr = row & 31;
-      float* hdr = reinterpret_cast<float*>(img + (size_t)(row >> 5) * S::REC);
-      hdr[16 * ((rr >> 2) & 1) + (rr & 3) + 4 * (rr >> 3)] = s;
-      red[0][w] = sqrtf(e2);
-      red[1][w] = sqrtf(n2);
-    }
-    __syncthreads();
+  for (int i = 0; i < PER; ++i) {
+    const int qv = max(-127, min(127, (int)rintf(x[i] * inv)));
+    const float xt = (float)qv * s;
+    e2 += (x[i] - xt) * (x[i] - xt);
+    n2 += xt * xt;
+    img[stream_frag_off(S::REC, S::HDR, row, PER * lane + i)] = (uint8_t)(qv & 0xff);
   }
-reduce:
-  if (threadIdx.x < 2) {
-    const float m = fmaxf(fmaxf(red[threadIdx.x][0], red[threadIdx.x][1]),
-                          fmaxf(red[threadIdx.x][2], red[threadIdx.x][3]));
-    atomicMax(reinterpret_cast<int*>(bounds) + threadIdx.x, __float_as_int(m));
+  en = sqrtf(wave_sum(e2));
+  nn = sqrtf(wave_sum(n2));
+  if (lane == 0) {
+    const int rr = row & 31;
+    float* hdr = reinterpret_cast<float*>(img + (size_t)(row >> 5) * S::REC);
+    hdr[16 * ((rr >> 2) & 1) + (rr & 3) + 4 * (rr >> 3)] = s;
   }
 }
 
@@ -347,39 +329,22 @@ __device__ __forceinline__ int e2m1_code_s(float a, float& q) {   // a = |x| / s
   return c;
 }
 
-// MX-fp4 image: every 32-dim block b gets s_b = 2^ceil(log2(max |x_b| / 6)) (an e8m0 byte) and each
-// element the nearest OCP e2m1 value of x / s_b, two per byte (element 2 j in the low nibble of
-// byte j) -- quant_rows_mx4_kernel's numbers.  One wave per row, lane l holds dims l + 64 m.
-//   rows    (margin == nullptr): written in the stream layout at rows [r0, r0 + n) or `rows`;
-//            bounds[0..1] raised to (max |x - x~|, max |x~|) -- E4, X4;
-//   queries (margin != nullptr): row-major nibbles Xq [n][D / 2] and the scale record
-//            QS [n][2 NSC] dwords (dword h NSC + j, byte b = block 2 (4 j + b) + h: the scan's
-//            per-lane B scales); margin = |q| E4 + |q - q~| X4 + 1e-5 from bounds.
+// One row's MX-fp4 image: every 32-dim block b gets s_b = 2^ceil(log2(max |x_b| / 6)) (an e8m0
+// byte) and each element the nearest OCP e2m1 value of x / s_b, two per byte (element 2 j in the
+// low nibble of byte j) -- quant_rows_mx4_kernel's numbers.  One wave, lane l holds dims l + 64 m.
+// Xq == nullptr: into the stream image img at row `row`; else the query layout: row-major nibbles
+// Xq [.][D / 2] and the scale record QS [.][2 NSC] dwords (dword h NSC + j, byte b = block
+// 2 (4 j + b) + h: the scan's per-lane B scales).  en / nn / xn = |x - x~| / |x~| / |x|.
 template <int D>
-__global__ __launch_bounds__(256) void quant_stream_mx4_kernel(
-    const __bf16* __restrict__ X, int r0, const int* __restrict__ rows, int n,
-    uint8_t* __restrict__ img, uint8_t* __restrict__ Xq, uint32_t* __restrict__ QS,
-    float* __restrict__ bounds, float* __restrict__ margin) {
+__device__ __forceinline__ void mx4_stream_row(const __bf16* __restrict__ xrow, int row,
+                                               uint8_t* __restrict__ img, uint8_t* __restrict__ Xq,
+                                               uint32_t* __restrict__ QS, float& en, float& nn,
+                                               float& xn) {
   using S = SDim<SF_MX4, D>;
   constexpr int M = D / 64, NSC = S::NSC;
-  __shared__ float red[2][4];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int j = blockIdx.x * 4 + w;
-  const bool query = margin != nullptr;
-  if (j >= n) {   // (block-uniform barrier below: idle waves report zeros)
-    if (!query) {
-      if (lane == 0) red[0][w] = red[1][w] = 0.f;
-      __syncthreads();
-      if (threadIdx.x < 2) {
-        const float mx = fmaxf(fmaxf(red[threadIdx.x][0], red[threadIdx.x][1]),
-                               fmaxf(red[threadIdx.x][2], red[threadIdx.x][3]));
-        atomicMax(reinterpret_cast<int*>(bounds) + threadIdx.x, __float_as_int(mx));
-      }
-    }
-    return;
-  }
-  const int row = query ? j : (rows ? rows[j] : r0 + j);
-  const uint16_t* xp = reinterpret_cast<const uint16_t*>(X + (size_t)row * D);
+  const int lane = threadIdx.x & 63;
+  const bool query = Xq != nullptr;
+  const uint16_t* xp = reinterpret_cast<const uint16_t*>(xrow);
   // this row's scale record (queries): half 0's words built in lanes 0-31, half 1's in 32-63
   uint32_t scw[NSC];
 #pragma unroll
@@ -420,7 +385,9 @@ __global__ __launch_bounds__(256) void quant_stream_mx4_kernel(
             (m & 3)] = (uint8_t)(e + 127);
     }
   }
-  const float en = sqrtf(wave_sum(e2)), nn = sqrtf(wave_sum(n2)), xn = sqrtf(wave_sum(x2));
+  en = sqrtf(wave_sum(e2));
+  nn = sqrtf(wave_sum(n2));
+  xn = sqrtf(wave_sum(x2));
   if (query) {
     // lanes 0 and 32 built the two halves' scale words (identical within a half-wave)
 #pragma unroll
@@ -431,19 +398,90 @@ __global__ __launch_bounds__(256) void quant_stream_mx4_kernel(
         QS[(size_t)row * 2 * NSC + NSC + i] = hi;
       }
     }
-    if (lane == 0) margin[row] = xn * bounds[0] + en * bounds[1] + 1e-5f;
-    return;
   }
+}
+
+// raise bounds[0..1] to the maxima of (a, b) over the workgroup's 4 waves (idle waves pass 0)
+__device__ __forceinline__ void raise_bounds2(float* bounds, float a, float b) {
+  __shared__ float red[2][4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (lane == 0) {
-    red[0][w] = en;
-    red[1][w] = nn;
+    red[0][w] = a;
+    red[1][w] = b;
   }
   __syncthreads();
   if (threadIdx.x < 2) {
-    const float mx = fmaxf(fmaxf(red[threadIdx.x][0], red[threadIdx.x][1]),
-                           fmaxf(red[threadIdx.x][2], red[threadIdx.x][3]));
-    atomicMax(reinterpret_cast<int*>(bounds) + threadIdx.x, __float_as_int(mx));
+    const float m = fmaxf(fmaxf(red[threadIdx.x][0], red[threadIdx.x][1]),
+                          fmaxf(red[threadIdx.x][2], red[threadIdx.x][3]));
+    atomicMax(reinterpret_cast<int*>(bounds) + threadIdx.x, __float_as_int(m));
   }
+}
+
+// int8 stream image of bf16 rows [r0, r0 + n) (or of the rows listed in `rows`, n of them);
+// bounds (2 floats) raised to (max |x - x~|, max |x~|).  One wave per row.
+template <int D>
+__global__ __launch_bounds__(256) void quant_stream_i8_kernel(const __bf16* __restrict__ X, int r0,
+                                                              const int* __restrict__ rows, int n,
+                                                              uint8_t* __restrict__ img,
+                                                              float* __restrict__ bounds) {
+  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  float en = 0.f, nn = 0.f;
+  if (j < n) {   // (block-uniform barrier in raise_bounds2: idle waves report zeros)
+    const int row = rows ? rows[j] : r0 + j;
+    i8_stream_row<D>(X + (size_t)row * D, row, img, en, nn);
+  }
+  raise_bounds2(bounds, en, nn);
+}
+
+// MX-fp4 stream image of bf16 rows (margin == nullptr: rows [r0, r0 + n) or the listed rows into
+// img, bounds[0..1] raised to (E4, X4)) or the query image (margin != nullptr: Xq / QS for rows
+// 0 .. n - 1 and margin = |q| E4 + |q - q~| X4 + 1e-5 from bounds).  One wave per row.
+template <int D>
+__global__ __launch_bounds__(256) void quant_stream_mx4_kernel(
+    const __bf16* __restrict__ X, int r0, const int* __restrict__ rows, int n,
+    uint8_t* __restrict__ img, uint8_t* __restrict__ Xq, uint32_t* __restrict__ QS,
+    float* __restrict__ bounds, float* __restrict__ margin) {
+  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const bool query = margin != nullptr;
+  float en = 0.f, nn = 0.f, xn = 0.f;
+  if (query) {
+    if (j >= n) return;   // (no barrier on the query path)
+    mx4_stream_row<D>(X + (size_t)j * D, j, nullptr, Xq, QS, en, nn, xn);
+    if ((threadIdx.x & 63) == 0) margin[j] = xn * bounds[0] + en * bounds[1] + 1e-5f;
+    return;
+  }
+  if (j < n) {
+    const int row = rows ? rows[j] : r0 + j;
+    mx4_stream_row<D>(X + (size_t)row * D, row, img, nullptr, nullptr, en, nn, xn);
+  }
+  raise_bounds2(bounds, en, nn);
+}
+
+// An append of n unit bf16 rows at row r0 in one launch: the rows themselves (src -> rows), their
+// int8 stream image (img8, bounds b8[0..1]) and their MX-fp4 stream image (img4, bounds b4[0..1])
+// -- either image may be absent (nullptr).  One wave per row.
+template <int D>
+__global__ __launch_bounds__(256) void append_rows_kernel(const __bf16* __restrict__ src, int n,
+                                                          __bf16* __restrict__ rows, int r0,
+                                                          uint8_t* __restrict__ img8,
+                                                          float* __restrict__ b8,
+                                                          uint8_t* __restrict__ img4,
+                                                          float* __restrict__ b4) {
+  const int j = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  float e8 = 0.f, n8 = 0.f, e4 = 0.f, n4 = 0.f, x4 = 0.f;
+  if (j < n) {
+    const __bf16* xr = src + (size_t)j * D;
+    // the bf16 row: D * 2 bytes as 4-byte words, D / 128 per lane
+    const uint32_t* sp = reinterpret_cast<const uint32_t*>(xr);
+    uint32_t* dp = reinterpret_cast<uint32_t*>(rows + (size_t)(r0 + j) * D);
+#pragma unroll
+    for (int i = 0; i < D / 128; ++i) dp[lane + 64 * i] = sp[lane + 64 * i];
+    if (img8) i8_stream_row<D>(xr, r0 + j, img8, e8, n8);
+    if (img4) mx4_stream_row<D>(xr, r0 + j, img4, nullptr, nullptr, e4, n4, x4);
+  }
+  if (b8) raise_bounds2(b8, e8, n8);
+  __syncthreads();   // (raise_bounds2's LDS reused)
+  if (b4) raise_bounds2(b4, e4, n4);
 }
 
 }  // namespace symb
@@ -490,46 +528,63 @@ template <int F, int D, int V>
 static int launch_stream(const void* img, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                          const void* qsc, int NQ, const float* thr, float* cand_s, int* cand_i,
                          int* cand_n, int cap, int xcd, hipStream_t st, const int* skip,
-                         const int* gate, int gate_want) {
+                         const int* gate, int gate_want, int* runs) {
   using G = SGeo<F, D, V>;
   const int n_qblk = (NQ + G::QPB - 1) / G::QPB;
   constexpr int lds = G::STAGE * G::NW;
   hipLaunchKernelGGL((scan_stream_kernel<F, D, V>), dim3(n_rblk * n_qblk), dim3(64 * G::NW), lds,
                      st, (const uint8_t*)img, n_valid, rows_per_blk, (const uint8_t*)Q,
                      (const uint32_t*)qsc, NQ, n_qblk, xcd, thr, cand_s, cand_i, cand_n, cap, skip,
-                     gate, gate_want);
+                     gate, gate_want, runs);
   return (int)hipGetLastError();
 }
 
 // The stream scan over rows [0, n_valid) of a stream image covering alloc_rows rows (a multiple of
 // 32 that covers n_valid).  rows_per_blk: a multiple of 32; n_rblk * rows_per_blk >= n_valid.
 // form 0: int8 (Q = [NQ][dim] int8, qsc unused); 1: MX-fp4 (Q = [NQ][dim / 2] nibbles, qsc =
-// [NQ][2 NSC] scale dwords).  cand_n is zeroed here unless the launch is gated (gate != nullptr:
-// it runs only if *gate == gate_want; the caller zeroes).
+// [NQ][2 NSC] scale dwords).  cand_n is zeroed here iff zero_cnt (else the caller's zeroed
+// workspace); gate != nullptr: the launch runs only if *gate == gate_want; runs (optional) is
+// incremented once by a launch that ran.
 int symb_index_scan_stream(const void* img, int n_valid, int alloc_rows, int rows_per_blk,
                            int n_rblk, const void* Q, const void* qsc, int NQ, const float* thr,
                            float* cand_s, int* cand_i, int* cand_n, int cap, int xcd,
                            hipStream_t st, const int* skip, int dim, int form, const int* gate,
-                           int gate_want) {
+                           int gate_want, int zero_cnt, int* runs) {
   if (NQ <= 0) return 0;
   if ((dim != 384 && dim != 768) || (form != 0 && form != 1)) return -1;
   if (form == 1 && qsc == nullptr) return -1;
   if (rows_per_blk % 32 || n_rblk <= 0 || thr == nullptr || cap <= 0 || n_valid <= 0) return -1;
   if ((long long)n_rblk * rows_per_blk < n_valid) return -1;
   if (alloc_rows % 32 || (long long)(n_valid + 31) / 32 * 32 > alloc_rows) return -1;
-  if (gate == nullptr) {
+  if (zero_cnt) {
     hipError_t e = hipMemsetAsync(cand_n, 0, sizeof(int) * (size_t)NQ, st);
     if (e != hipSuccess) return (int)e;
   }
 #define L(F, D_, V_) launch_stream<F, D_, V_>(img, n_valid, rows_per_blk, n_rblk, Q, qsc, NQ, thr, \
                                               cand_s, cand_i, cand_n, cap, xcd, st, skip, gate,   \
-                                              gate_want)
+                                              gate_want, runs)
   if (dim == 384) {
     if (form && g_stream_mx4_v) return L(SF_MX4, 384, 1);
     return form ? L(SF_MX4, 384, 0) : L(SF_I8, 384, 0);
   }
   return form ? L(SF_MX4, 768, 0) : L(SF_I8, 768, 0);
 #undef L
+}
+
+// Append n unit bf16 rows (src) at row r0 of the shard: rows, int8 stream image (img8 / b8) and
+// MX-fp4 stream image (img4 / b4); an image pointer may be nullptr (then its bounds too).
+int symb_append_rows(const void* src, int n, int dim, void* rows, int r0, void* img8, float* b8,
+                     void* img4, float* b4, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (r0 < 0 || rows == nullptr || src == nullptr || (img8 && !b8) || (img4 && !b4)) return -1;
+#define L(D_) hipLaunchKernelGGL(append_rows_kernel<D_>, dim3((n + 3) / 4), dim3(256), 0, st,      \
+                                 (const __bf16*)src, n, (__bf16*)rows, r0, (uint8_t*)img8, b8,    \
+                                 (uint8_t*)img4, b4)
+  if (dim == 384) L(384);
+  else if (dim == 768) L(768);
+  else return -1;
+#undef L
+  return (int)hipGetLastError();
 }
 
 // int8 stream image of bf16 rows X: rows [r0, r0 + n) (rows == nullptr) or the n listed rows.
