@@ -448,11 +448,35 @@ class HbmIndexShard:
         r0 = self._reserve(n)
         if self.dtype == "fp8":
             self._store(r0, unit_bf16.to(self.device), normalize=False)
-        else:
+        elif not self._append_fused(unit_bf16, r0, n):
             self.rows[r0:r0 + n].copy_(unit_bf16, non_blocking=True)
             self.rows_written(r0, n)
         self.publish()
         return r0
+
+    def _append_fused(self, src: torch.Tensor, r0: int, n: int) -> bool:
+        """One-launch append (prepass.hip append_rows_kernel: the bf16 rows, their int8 and
+        MX-fp4 stream images and both bound pairs) when the shard keeps plain stream images, no
+        fp8 prefilter image and no re-calibration is due; False: the caller takes the general
+        path (copy + rows_written)."""
+        if (self.device.type != "cuda" or n <= 0 or self.rows8 is not None
+                or self.img_i8 is None or self._i8_heavy or not self.prune_on
+                or self.dim not in STREAM_DIMS or self.mx4_on != (self.img_mx4 is not None)):
+            return False
+        due = r0 + n >= self._calib_next or (self.i8_split == "on" and not self._i8_heavy)
+        if due and self.i8_split != "off" and self.dim in SPLIT_DIMS:
+            return False
+        if (src.device != self.device or src.dtype != torch.bfloat16 or not src.is_contiguous()
+                or src.shape[-1] != self.dim):
+            return False
+        from ..ops._ext import hip, stream_handle
+
+        m4 = self.img_mx4 is not None
+        hip().append_rows(src.data_ptr(), n, self.dim, self.rows.data_ptr(), r0,
+                          self.img_i8.data_ptr(), self.i8_bounds.data_ptr(),
+                          self.img_mx4.data_ptr() if m4 else 0,
+                          self.mx4_bounds.data_ptr() if m4 else 0, stream_handle(self.device))
+        return True
 
     def rows_written(self, r0: int, n: int) -> None:
         """bf16 rows [r0, r0+n) changed: refresh their e4m3 prefilter image and their int8
@@ -568,10 +592,12 @@ class HbmIndexShard:
         else:
             margin.copy_(nr[:, 2] * bounds[0] + nr[:, 0] * bounds[1] + 1e-5)
 
-    def prune_query_image(self, q_unit: torch.Tensor):
+    def prune_query_image(self, q_unit: torch.Tensor, zero: torch.Tensor | None = None):
         """(image, scale, margin) of unit queries in the shard's current form: the int8 image and
         |q| E + |q - q~| X + 1e-5 (prune_qquant), or the split image in the shard's basis and
-        |q_l| E_l + |q_l - q~_l| X_l + |q_h| E_h + |q_h - q^_h| X_h + 1e-5 (quant_rows_split)."""
+        |q_l| E_l + |q_l - q~_l| X_l + |q_h| E_h + |q_h - q^_h| X_h + 1e-5 (quant_rows_split).
+        ``zero`` (int32, optional): a workspace cleared on the way (by the quantiser itself on the
+        plain form: no memset launch)."""
         NQ, dev, heavy = q_unit.shape[0], self.device, self._i8_heavy
         q8 = torch.empty(NQ, self.dim + heavy, dtype=torch.int8, device=dev)
         sq = torch.empty(NQ, dtype=torch.float32, device=dev)
@@ -589,6 +615,8 @@ class HbmIndexShard:
             q8.copy_(img)
             sq.copy_(sc)
             margin.copy_(m + 1e-5)
+            if zero is not None:
+                zero.zero_()
             return q8, sq, margin
         from ..ops._ext import hip, stream_handle
 
@@ -597,9 +625,13 @@ class HbmIndexShard:
             qr = self._rotate(q_unit)
             hip().quant_rows_split(qr.data_ptr(), NQ, self.dim, q8.data_ptr(), sq.data_ptr(),
                                    self.i8_bounds.data_ptr(), margin.data_ptr(), st)
+            if zero is not None:
+                zero.zero_()
         else:
             hip().prune_qquant(q_unit.data_ptr(), NQ, self.dim, self.i8_bounds.data_ptr(),
-                               q8.data_ptr(), sq.data_ptr(), margin.data_ptr(), st)
+                               q8.data_ptr(), sq.data_ptr(), margin.data_ptr(), st,
+                               zero=0 if zero is None else zero.data_ptr(),
+                               zero_n=0 if zero is None else zero.numel())
         return q8, sq, margin
 
     def prune_estimate(self, q8: torch.Tensor, sq: torch.Tensor, r0: int = 0,
@@ -891,14 +923,15 @@ class HbmIndexShard:
     MQ_TILE_SHIFT = 6         # threshold sample: one 64-row tile in 2^6
     MQ_TAIL_ROWS = 4096       # ... plus at least the last 4096 rows
 
-    def _tile_sample_plan(self, n: int, ts: int | None = None):
+    def _tile_sample_plan(self, n: int, ts: int | None = None, want_idx: bool = True):
         """In-place threshold sample over n visible rows, or None when n is too small.
 
         Returns (ts, nv, t0, idx): the emitting kernel's virtual tile v < nv reads physical tile
         (v << ts) + h(v) (h = top ts bits of v * 0x9E3779B1, as in index_mq.hip), i.e. one tile
         of each group of 2^ts; rows [t0, n) (4096..8191 of them) are the exact tail; idx are the
         rows of every SEED_DIV-th sampled tile (the sub-sample that seeds the sample scan, a
-        subset of the sample).  Every sampled row lies below t0 <= n - MQ_TAIL_ROWS."""
+        subset of the sample; None unless ``want_idx`` -- dense_scores computes the same rows
+        in-kernel).  Every sampled row lies below t0 <= n - MQ_TAIL_ROWS."""
         ts = self.MQ_TILE_SHIFT if ts is None else ts
         group = TILE_ROWS << ts                                # rows per tile group
         nv = (n - self.MQ_TAIL_ROWS) // group if n > self.MQ_TAIL_ROWS else 0
@@ -907,6 +940,8 @@ class HbmIndexShard:
         t0 = nv * group
         if t0 > n:   # (a launch past the rows would fault the GPU)
             raise RuntimeError("tile sample past the visible rows")
+        if not want_idx:
+            return ts, nv, t0, None
         # idx depends on (nv, ts) only, and nv changes once per 2^ts tiles of appends: cached
         # (rebuilding it was ~8 small kernels on every search's critical path)
         key = (nv, ts, self.SEED_DIV)
@@ -945,7 +980,7 @@ class HbmIndexShard:
 
     def _scan_mq(self, n: int, q_unit: torch.Tensor, kmax: int, k: int, thr, n_cus, rows=None,
                  tshift: int = 0, gate=None, out=None, fallback: bool = True, cand: bool = False,
-                 cap: int | None = None, min_tiles: int = 16):
+                 cap: int | None = None, min_tiles: int = 16, cnt=None):
         """512-query-per-workgroup scan emitting every score above ``thr`` (index_mq.hip), top-k
         of each query's candidates, and the exact 256-query kernel as a fallback that runs on the
         GPU only if some query's candidate buffer overflowed (a device flag gates it).
@@ -956,7 +991,9 @@ class HbmIndexShard:
         overflow re-scan -- for a threshold sample that is still sound, since the top-k of ANY
         subset of real rows lower-bounds the k-th best.  ``cand``: also return the candidate
         buffers (scores, rows, count) for the route estimate of _search_pruned.  ``min_tiles``:
-        row-block floor in 64-row tiles (1 spreads a small scan over every CU)."""
+        row-block floor in 64-row tiles (1 spreads a small scan over every CU).  ``cnt``: the
+        caller's candidate counters, already zeroed together with ``out``'s overflow flag (no
+        memset launches)."""
         from ..ops._ext import hip, stream_handle
 
         h = hip()
@@ -972,7 +1009,9 @@ class HbmIndexShard:
         cap, dev = cap or self.MQ_CAP, self.device
         cs = torch.empty(NQ, cap, device=dev)
         ci = torch.empty(NQ, cap, dtype=torch.int32, device=dev)
-        cnt = torch.empty(NQ, dtype=torch.int32, device=dev)
+        zeroed = cnt is not None
+        if cnt is None:
+            cnt = torch.empty(NQ, dtype=torch.int32, device=dev)
         if out is None:
             out = (torch.empty(NQ, k, device=dev), torch.empty(NQ, k, dtype=torch.int32, device=dev),
                    torch.empty(1, dtype=torch.int32, device=dev))
@@ -981,10 +1020,11 @@ class HbmIndexShard:
         gp = 0 if gate is None else gate.data_ptr()
         h.index_scan_mq(rows.data_ptr(), n, rows_per_blk, n_rblk, q_unit.data_ptr(), NQ,
                         thr.data_ptr(), cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(), cap,
-                        self.scan_xcd, st, sets, tshift, rsplit, gp, dim=self.dim)
+                        self.scan_xcd, st, sets, tshift, rsplit, gp, zero_cnt=not zeroed,
+                        dim=self.dim)
         h.topk_select_counted(cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(), cap, NQ, kmax, k,
                               out_s.data_ptr(), out_i.data_ptr(), ovf.data_ptr(), st, gate=gp,
-                              reset_ovf=gate is None)
+                              reset_ovf=gate is None and not zeroed)
         if gate is None and fallback:
             if tshift:
                 self._scan(self.visible, q_unit, kmax, k, thr, n_cus, gate=ovf, out=(out_s, out_i))
@@ -1094,59 +1134,81 @@ class HbmIndexShard:
         self._sample_shift_last = shift   # (diagnostics / tests)
         plan, ts = None, shift
         while plan is None and ts >= min(self.PRUNE_MIN_SHIFT, shift):
-            plan, ts = self._tile_sample_plan(n, ts), ts - 1
+            plan, ts = self._tile_sample_plan(n, ts, want_idx=False), ts - 1
         if plan is None:
             return None
         if n_cus is None:
             n_cus = self._n_cus()
         h, dev, cap = hip(), self.device, self.PRUNE_CAP
         st = stream_handle(dev)
+        ts, nv, t0, _ = plan
+        tcap = n - t0
+        dense_tail = NQ <= self.tail_dense_max_nq
+        geo = self._i8_geometry(n, NQ, n_cus)
+        n_rblk = geo[2]
+        # one int32 workspace for every counter and flag of the search, cleared by the query
+        # quantiser on its way (no memset launches): the sample's and the final scan's candidate
+        # counters, flags (WS_* below) and the route's per-block maxima
+        ws = torch.empty(2 * NQ + self.WS_FLAGS + n_rblk, dtype=torch.int32, device=dev)
+        cnt_p, cnt_f = ws[:NQ], ws[NQ:2 * NQ]
+        flags = ws[2 * NQ:2 * NQ + self.WS_FLAGS]
+        blkmax = ws[2 * NQ + self.WS_FLAGS:]
         # 0. the int8 queries and each query's bound margin |q| E + |q - q~| X (prune_qquant), or
         #    their split image in the shard's basis and its margin (quant_rows_split)
         heavy = self._i8_heavy
-        q8, sq, margin = self.prune_query_image(q_unit)
+        q8, sq, margin = self.prune_query_image(q_unit, zero=ws)
         # 1. T: the k-th best exact score of a sample of real rows (1 tile in 2^ts, plus the last
         #    4096+ rows where fresh inserts sit), as in _search_scan; its emitted candidates also
-        #    estimate the int8 band's population (prune_route)
-        ts, nv, t0, idx = plan
-        sub = torch.index_select(self.rows, 0, idx)
+        #    estimate the int8 band's population (prune_route).  The sample scan is seeded by the
+        #    exact scores of every SEED_DIV-th sampled tile, and a batch of up to
+        #    tail_dense_max_nq queries scores the tail [t0, n) densely in the same launch
+        #    (dense_scores: the seed tiles' rows are computed in-kernel, no gather); the selects
+        #    read their columns in place and write the seed threshold directly
+        m_seed = -(-nv // self.SEED_DIV) * TILE_ROWS
+        ld = _round_up(m_seed + (tcap if dense_tail else 0), 4)
+        S = torch.empty(NQ, ld, device=dev)
+        h.dense_scores(self.rows.data_ptr(), self.dim, 0, m_seed, t0, tcap if dense_tail else 0,
+                       q_unit.data_ptr(), NQ, S.data_ptr(), ld, st, ts=ts, div=self.SEED_DIV)
+        thr0 = torch.empty(NQ, dtype=torch.float32, device=dev)
+        seed_s = torch.empty(NQ, k, device=dev)
+        seed_i = torch.empty(NQ, k, dtype=torch.int32, device=dev)
+        h.topk_select_counted(S.data_ptr(), 0, 0, m_seed, NQ, kmax, k, seed_s.data_ptr(),
+                              seed_i.data_ptr(), flags[self.WS_SCRATCH].data_ptr(), st,
+                              reset_ovf=False, ld=ld, kth_out=thr0.data_ptr(),
+                              kth_margin=self.MQ_THR_MARGIN)
         pm = self.prepass_min_tiles
-        s0, _ = self._scan(sub.shape[0], q_unit, kmax, k, None, n_cus, sub, "bf16", min_tiles=pm)
-        thr0 = s0[:, k - 1].contiguous() - self.MQ_THR_MARGIN
-        pre_s, _, cs_p, ci_p, cnt_p = self._scan_mq(nv * TILE_ROWS, q_unit, kmax, k, thr0, n_cus,
-                                                    tshift=ts, fallback=False, cand=True,
-                                                    cap=self.SAMPLE_CAP)
-        # the fresh-row tail [t0, n) (never sampled) is scanned exactly and emits every row >= thr0
-        # too (one slot per tail row: no overflow), so the route counts its band rows one by one
-        # -- a crowd of fresh near-duplicates sits there first
-        tcap = n - t0
-        if NQ <= self.tail_dense_max_nq:
-            # dense exact scores of the tail (one small fp32 GEMM: 4-8k rows) and their top-k;
-            # the route counts every tail row >= the band.  The emitting scan it replaces
-            # reserved one slot per emitted row with a global atomic on the query's counter:
-            # with a fresh near-duplicate crowd in the tail every (query, row) pair emitted and
-            # the counters serialized (0.6 ms per headline step, profiles/r3_step_trace/)
-            tcs = torch.mm(q_unit.float(), self.rows[t0:n].float().t())
-            tail_s = torch.empty(NQ, k, device=dev)
+        pre_s, _, cs_p, ci_p, cnt_p = self._scan_mq(
+            nv * TILE_ROWS, q_unit, kmax, k, thr0, n_cus, tshift=ts, fallback=False, cand=True,
+            cap=self.SAMPLE_CAP, cnt=cnt_p,
+            out=(torch.empty(NQ, k, device=dev), torch.empty(NQ, k, dtype=torch.int32, device=dev),
+                 flags[self.WS_SAMPLE_OVF:self.WS_SAMPLE_OVF + 1]))
+        # the fresh-row tail [t0, n) (never sampled) is scored exactly and the route counts every
+        # tail row >= the band one by one -- a crowd of fresh near-duplicates sits there first.
+        # The emitting tail scan (larger batches) reserved one slot per emitted row with a global
+        # atomic on the query's counter: with a fresh near-duplicate crowd in the tail every
+        # (query, row) pair emitted and the counters serialized (0.6 ms per headline step,
+        # profiles/r3_step_trace/)
+        tail_s = torch.empty(NQ, k, device=dev)
+        if dense_tail:
             tail_i = torch.empty(NQ, k, dtype=torch.int32, device=dev)
-            tovf = torch.empty(1, dtype=torch.int32, device=dev)
-            h.topk_select_counted(tcs.data_ptr(), 0, 0, tcap, NQ, kmax, k, tail_s.data_ptr(),
-                                  tail_i.data_ptr(), tovf.data_ptr(), st)   # (dense rows)
+            tcs_p = S.data_ptr() + 4 * m_seed
+            h.topk_select_counted(tcs_p, 0, 0, tcap, NQ, kmax, k, tail_s.data_ptr(),
+                                  tail_i.data_ptr(), flags[self.WS_SCRATCH].data_ptr(), st,
+                                  reset_ovf=False, ld=ld)
             tci = tcnt = None
+            tail_ld = ld
         else:
             tail_s, _, tcs, tci, tcnt = self._scan_mq(tcap, q_unit, kmax, k, thr0, n_cus,
                                                       rows=self.rows[t0:], fallback=False,
                                                       cand=True, cap=tcap, min_tiles=pm)
+            tcs_p, tail_ld = tcs.data_ptr(), tcap
         # 2. T (k-th best of the union), the per-query emission threshold (T - margin) / sq and
         #    the per-row-block route (prune_route): the blocks some query would flood with int8
         #    candidates go to the bf16 emitting scan at T, the rest to the int8 scan
-        geo = self._i8_geometry(n, NQ, n_cus)
-        n_rblk = geo[2]
         T = torch.empty(NQ, dtype=torch.float32, device=dev)
         thr = torch.empty(NQ, dtype=torch.float32, device=dev)
-        dense = torch.empty(1, dtype=torch.int32, device=dev)
+        dense = flags[self.WS_DENSE:self.WS_DENSE + 1]
         est = torch.empty(NQ, n_rblk, dtype=torch.float32, device=dev)
-        blkmax = torch.empty(n_rblk, dtype=torch.int32, device=dev)
         blk = torch.empty(2 + 2 * n_rblk, dtype=torch.int32, device=dev)
         inf = float("inf")
         limit = self.PRUNE_DENSE_FRAC * cap if self.prune_route else inf
@@ -1156,31 +1218,36 @@ class HbmIndexShard:
                       ci_p.data_ptr(), cnt_p.data_ptr(), self.SAMPLE_CAP, ts, geo[1], n_rblk,
                       blk_limit, limit, self._mq_slots(NQ, n_cus)[3], T.data_ptr(),
                       thr.data_ptr(), dense.data_ptr(), est.data_ptr(), blkmax.data_ptr(),
-                      blk.data_ptr(), st, tail_cs=tcs.data_ptr(),
+                      blk.data_ptr(), st, tail_cs=tcs_p,
                       tail_ci=0 if tci is None else tci.data_ptr(),
-                      tail_cnt=0 if tcnt is None else tcnt.data_ptr(), tail_cap=tcap, tail_off=t0)
+                      tail_cnt=0 if tcnt is None else tcnt.data_ptr(), tail_cap=tcap, tail_off=t0,
+                      tail_ld=tail_ld, zeroed=True)
         ctx = dict(q=q_unit, k=k, n=n, n_cus=n_cus, q8=q8, sq=sq, thr=thr, T=T, dense=dense,
-                   blk=blk, geo=geo, heavy=heavy, gen=self._calib_gen, mx4=None)
+                   blk=blk, geo=geo, heavy=heavy, gen=self._calib_gen, mx4=None, ws=ws)
         # 3. the MX-fp4 first tier (mx4_select): when every query's k-th score sits so far above
         #    the corpus bulk that even the coarse fp4 bound (|q| E4 + |q - q~| X4, ~0.25 on unit
         #    rows) leaves few rows in its band -- self / near-duplicate queries, such as the
-        #    headline's freshly inserted random-init embeddings -- the scan streams the 208-byte
-        #    fp4 image at twice the int8 MFMA rate instead of the 384-byte int8 one.  Decided on the
-        #    GPU from the same exact sample (the band must lie above the sample's seed threshold,
-        #    so the sample counted it): the int8 / split scan and the fp4 scan are both enqueued,
-        #    each gated on the flag, and exactly one runs.
-        if self.mx4_on and self.prune_route and tci is None:
+        #    headline's freshly inserted random-init embeddings -- the scan streams the fp4 image
+        #    at twice the int8 MFMA rate instead of the int8 one.  Decided on the GPU from the same
+        #    exact scores (the probe: every 4th seed tile, read in place; the band must lie above
+        #    the sample's seed threshold, so the sample counted it): the int8 / split scan and
+        #    the fp4 scan are both enqueued, each gated on the flag, and exactly one runs.
+        if self.mx4_on and self.prune_route and dense_tail:
             q4, qs4, m4 = self.mx4_query_image(q_unit)
-            # the probe: every 4th seed tile, scored exactly (one small fp32 GEMM)
-            probe = sub.view(-1, TILE_ROWS, self.dim)[::4].reshape(-1, self.dim)
-            ps = torch.mm(q_unit.float(), probe.float().t())
             thr4 = torch.empty(NQ, dtype=torch.float32, device=dev)
-            nv = torch.empty(1, dtype=torch.int32, device=dev)
-            h.mx4_select(NQ, T.data_ptr(), m4.data_ptr(), margin.data_ptr(), ps.data_ptr(),
-                         probe.shape[0], float(t0) / probe.shape[0], tcs.data_ptr(), tcap,
-                         self.MX4_LIMIT_FRAC * cap, thr4.data_ptr(), nv.data_ptr(), st)
-            ctx["mx4"] = dict(q4=q4, qs4=qs4, thr4=thr4, nv=nv)
+            nvf = flags[self.WS_NV:self.WS_NV + 1]
+            n_probe = TILE_ROWS * -(-(m_seed // TILE_ROWS) // 4)
+            h.mx4_select(NQ, T.data_ptr(), m4.data_ptr(), margin.data_ptr(), S.data_ptr(), m_seed,
+                         float(t0) / n_probe, tcs_p, tcap, self.MX4_LIMIT_FRAC * cap,
+                         thr4.data_ptr(), nvf.data_ptr(), st, ld=ld, tile_stride=4, tail_ld=ld,
+                         nv_zeroed=True)
+            ctx["mx4"] = dict(q4=q4, qs4=qs4, thr4=thr4, nv=nvf)
         return ctx
+
+    # the search workspace's flag slots (_pruned_begin): route "every block dense", the MX-fp4
+    # tier's "not viable" flag, the sample's and the final select's overflow flags, and a slot
+    # the dense selects may write (they never overflow)
+    WS_DENSE, WS_NV, WS_SAMPLE_OVF, WS_OVF, WS_SCRATCH, WS_FLAGS = 0, 1, 2, 3, 4, 8
 
     def _i8_geometry(self, n: int, NQ: int, n_cus: int):
         """(rsplit, rows_per_blk, n_rblk) of the int8 scan over n rows: ~one workgroup per CU
@@ -1236,7 +1303,7 @@ class HbmIndexShard:
 
         h, dev, cap, kmax = hip(), self.device, self.PRUNE_CAP, 16
         cur = torch.cuda.current_stream(dev)
-        for t in ("q", "q8", "sq", "thr", "T", "dense", "blk"):
+        for t in ("q", "q8", "sq", "thr", "T", "dense", "blk", "ws"):
             ctx[t].record_stream(cur)
         q_unit, k, n, n_cus = ctx["q"], ctx["k"], ctx["n"], ctx["n_cus"]
         q8, thr, T, dense, blk = ctx["q8"], ctx["thr"], ctx["T"], ctx["dense"], ctx["blk"]
@@ -1250,24 +1317,26 @@ class HbmIndexShard:
             self._scan(n, q_unit, kmax, k, T.contiguous(), n_cus, out=out)
             return out
         # 3. int8 scan of the blocks the route kept: emit every row with (q8 . x8) * sx >= thr
+        #    (candidate counters and overflow flag: the workspace _pruned_begin cleared)
+        ws = ctx["ws"]
         cs = torch.empty(NQ, cap, device=dev)
         ci = torch.empty(NQ, cap, dtype=torch.int32, device=dev)
-        cnt = torch.empty(NQ, dtype=torch.int32, device=dev)
-        ovf = torch.empty(1, dtype=torch.int32, device=dev)
+        cnt = ws[NQ:2 * NQ]
+        ovf = ws[2 * NQ + self.WS_OVF:2 * NQ + self.WS_OVF + 1]
         out_s = torch.empty(NQ, k, device=dev)
         out_i = torch.empty(NQ, k, dtype=torch.int32, device=dev)
         skip = blk[2 + n_rblk:].data_ptr() if self.prune_route else 0
         m4 = ctx.get("mx4")
         if m4 is not None:   # both tiers enqueued, gated on the flag: exactly one runs
-            for t in ("q4", "qs4", "thr4", "nv"):
+            for t in ("q4", "qs4", "thr4"):
                 m4[t].record_stream(cur)
-            cnt.zero_()
         gate, want = (m4["nv"].data_ptr(), 1) if m4 is not None else (0, 0)
         if self.img_i8 is not None and not ctx["heavy"]:   # the stream scan (index_stream.hip)
             h.index_scan_stream(self.img_i8.data_ptr(), n, self.img_i8.shape[0] * STREAM_SUB,
                                 rows_per_blk, n_rblk, q8.data_ptr(), 0, NQ, thr.data_ptr(),
                                 cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(), cap, self.scan_xcd,
-                                st, skip=skip, dim=self.dim, form=0, gate=gate, gate_want=want)
+                                st, skip=skip, dim=self.dim, form=0, gate=gate, gate_want=want,
+                                zero_cnt=0)
         else:
             h.index_scan_i8(self.rows_i8.data_ptr(), self.sx_i8.data_ptr(), n,
                             self.rows_i8.shape[0], rows_per_blk, n_rblk,
@@ -1276,11 +1345,18 @@ class HbmIndexShard:
                             dim=self.dim, heavy=ctx["heavy"], sq=ctx["sq"].data_ptr(), gate=gate,
                             gate_want=want)
         if m4 is not None and self.img_mx4 is not None:
+            # (runs: the device counter of searches whose first tier was this scan)
+            runs = 0
+            if self.mq_stats or self.tier_stats:
+                if self._mx4_tot is None:
+                    self._mx4_tot = torch.zeros(1, dtype=torch.int32, device=dev)
+                runs = self._mx4_tot.data_ptr()
             h.index_scan_stream(self.img_mx4.data_ptr(), n, self.img_mx4.shape[0] * STREAM_SUB,
                                 rows_per_blk, n_rblk, m4["q4"].data_ptr(), m4["qs4"].data_ptr(),
                                 NQ, m4["thr4"].data_ptr(), cs.data_ptr(), ci.data_ptr(),
                                 cnt.data_ptr(), cap, self.scan_xcd, st, skip=skip, dim=self.dim,
-                                form=1, gate=m4["nv"].data_ptr(), gate_want=0)
+                                form=1, gate=m4["nv"].data_ptr(), gate_want=0, zero_cnt=0,
+                                runs=runs)
         elif m4 is not None:
             h.index_scan_i8(self.rows_mx4.data_ptr(), self.sc_mx4.data_ptr(), n,
                             self.rows_mx4.shape[0], rows_per_blk, n_rblk, m4["q4"].data_ptr(), NQ,
@@ -1300,7 +1376,8 @@ class HbmIndexShard:
         h.rescore_bf16(self.rows.data_ptr(), q_unit.data_ptr(), NQ, self.dim, ci.data_ptr(),
                        cnt.data_ptr(), cap, cs.data_ptr(), st)
         h.topk_select_counted(cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(), cap, NQ, kmax, k,
-                              out_s.data_ptr(), out_i.data_ptr(), ovf.data_ptr(), st)
+                              out_s.data_ptr(), out_i.data_ptr(), ovf.data_ptr(), st,
+                              reset_ovf=False)
         # overflow (some query had more than cap candidates): the exact bf16 scan, seeded with T
         self._scan(n, q_unit, kmax, k, T.contiguous(), n_cus, gate=ovf, out=(out_s, out_i))
         self._mq_last = (cnt, ovf)
@@ -1315,10 +1392,10 @@ class HbmIndexShard:
                 self._tier_pending.append((flag, ev))
                 while len(self._tier_pending) > 8:    # (a caller that never begins another search)
                     self._tier_pending.popleft()
-        if (self.mq_stats or self.tier_stats) and m4 is not None:
+        if (self.mq_stats or self.tier_stats) and m4 is not None and self.img_mx4 is None:
             if self._mx4_tot is None:
                 self._mx4_tot = torch.zeros(1, dtype=torch.int32, device=dev)
-            self._mx4_tot.add_(1 - m4["nv"])
+            self._mx4_tot.add_(1 - m4["nv"])   # (the LDS-ring fp4 scan counts no runs itself)
         self._route_blk_last = blk
         if self.mq_stats:   # (diagnostics / benchmarks/micro.py scani8abl: inputs and grid)
             self._pruned_last = dict(q8=q8, thr=thr, sq=ctx["sq"], rows_per_blk=rows_per_blk,

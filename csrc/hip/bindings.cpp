@@ -97,8 +97,9 @@ int symb_index_scan_stream(const void* img, int n_valid, int alloc_rows, int row
                            int gate_want, int zero_cnt, int* runs);
 int symb_append_rows(const void* src, int n, int dim, void* rows, int r0, void* img8, float* b8,
                      void* img4, float* b4, hipStream_t st);
-int symb_dense_scores(const void* X, int dim, const int* rows, int n_list, int r_lo, int n_range,
-                      const void* Q, int NQ, float* out, int ld, hipStream_t st);
+int symb_dense_scores(const void* X, int dim, const int* rows, int n_list, int ts, int div,
+                      int r_lo, int n_range, const void* Q, int NQ, float* out, int ld,
+                      hipStream_t st);
 int symb_quant_stream_i8(const void* X, int r0, const int* rows, int n, int dim, void* img,
                          float* bounds, hipStream_t st);
 int symb_quant_stream_mx4(const void* X, int r0, const int* rows, int n, int dim, void* img,
@@ -512,13 +513,13 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("src"), py::arg("n"), py::arg("dim"), py::arg("rows"), py::arg("r0"),
      py::arg("img8"), py::arg("b8"), py::arg("img4"), py::arg("b4"), py::arg("stream"));
   m.def("dense_scores", [](uptr X, int dim, uptr rows, int n_list, int r_lo, int n_range, uptr Q,
-                           int NQ, uptr out, int ld, uptr st) {
-    check(symb_dense_scores(P<void>(X), dim, P<const int>(rows), n_list, r_lo, n_range,
+                           int NQ, uptr out, int ld, uptr st, int ts, int div) {
+    check(symb_dense_scores(P<void>(X), dim, P<const int>(rows), n_list, ts, div, r_lo, n_range,
                             P<void>(Q), NQ, P<float>(out), ld, S(st)),
           "dense_scores");
   }, py::arg("X"), py::arg("dim"), py::arg("rows"), py::arg("n_list"), py::arg("r_lo"),
      py::arg("n_range"), py::arg("Q"), py::arg("NQ"), py::arg("out"), py::arg("ld"),
-     py::arg("stream"));
+     py::arg("stream"), py::arg("ts") = 0, py::arg("div") = 1);
   m.def("quant_stream_i8", [](uptr X, int r0, uptr rows, int n, int dim, uptr img, uptr bounds,
                               uptr st) {
     check(symb_quant_stream_i8(P<void>(X), r0, P<const int>(rows), n, dim, P<void>(img),

@@ -15,14 +15,16 @@
 
 namespace symb {
 
-// out[q * ld + j] = <Q[q], X[row(j)]>, row(j) = rows[j] for j < n_list, r_lo + j - n_list for
-// n_list <= j < n_list + n_range.  One wave per 32 rows x 64 queries (two 32 x 32 blocks that
+// out[q * ld + j] = <Q[q], X[row(j)]>, row(j) = rows[j] for j < n_list (rows == nullptr: the
+// threshold sample's seed tiles, computed here -- tile v = (j / 64) div is physical tile
+// (v << ts) + (v * 0x9E3779B1 mod 2^32) >> (32 - ts), as index/shard.py _tile_sample_plan and
+// index_mq.hip's sample), r_lo + j - n_list for n_list <= j < n_list + n_range.  One wave per 32 rows x 64 queries (two 32 x 32 blocks that
 // share the row fragments), 4 waves per workgroup side by side over the queries: 32 rows x 256
 // queries per workgroup, grid (row tiles, query blocks).
 template <int D>
 __global__ __launch_bounds__(256) void dense_scores_kernel(const __bf16* __restrict__ X,
                                                            const int* __restrict__ rows, int n_list,
-                                                           int r_lo, int n_range,
+                                                           int ts, int div, int r_lo, int n_range,
                                                            const __bf16* __restrict__ Q, int NQ,
                                                            float* __restrict__ out, int ld) {
   constexpr int KS = D / 16;
@@ -33,7 +35,15 @@ __global__ __launch_bounds__(256) void dense_scores_kernel(const __bf16* __restr
   if (q0 >= NQ) return;   // (no barrier in this kernel)
   // this lane's A row (row l & 31 of the tile) and its two queries (l & 31 of each set)
   const int j = min(j0 + (lane & 31), m - 1);
-  const int row = j < n_list ? rows[j] : r_lo + (j - n_list);
+  int row;
+  if (j >= n_list) {
+    row = r_lo + (j - n_list);
+  } else if (rows != nullptr) {
+    row = rows[j];
+  } else {
+    const uint32_t v = (uint32_t)(j >> 6) * (uint32_t)div;
+    row = (int)(((v << ts) + ((v * 0x9E3779B1u) >> (32 - ts))) * 64u) + (j & 63);
+  }
   const __bf16* xp = X + (size_t)row * D + 8 * h;
   const __bf16* qa = Q + (size_t)min(q0 + (lane & 31), NQ - 1) * D + 8 * h;
   const __bf16* qb = Q + (size_t)min(q0 + 32 + (lane & 31), NQ - 1) * D + 8 * h;
@@ -74,15 +84,17 @@ using namespace symb;
 
 // Exact fp32 scores (dense_scores_kernel): out [NQ][ld] f32, columns 0 .. n_list - 1 for the
 // listed rows, n_list .. n_list + n_range - 1 for rows r_lo ..; ld >= n_list + n_range.
-int symb_dense_scores(const void* X, int dim, const int* rows, int n_list, int r_lo, int n_range,
-                      const void* Q, int NQ, float* out, int ld, hipStream_t st) {
+// rows == nullptr with n_list > 0: the hashed seed-tile list of (ts, div) (n_list a multiple of 64).
+int symb_dense_scores(const void* X, int dim, const int* rows, int n_list, int ts, int div,
+                      int r_lo, int n_range, const void* Q, int NQ, float* out, int ld,
+                      hipStream_t st) {
   const int m = n_list + n_range;
   if (NQ <= 0 || m <= 0) return 0;
-  if (n_list < 0 || n_range < 0 || ld < m || (n_list > 0 && rows == nullptr) || r_lo < 0)
-    return -1;
+  if (n_list < 0 || n_range < 0 || ld < m || r_lo < 0) return -1;
+  if (n_list > 0 && rows == nullptr && (ts < 1 || ts > 24 || div < 1 || n_list % 64)) return -1;
   const dim3 grid((m + 31) / 32, (NQ + 255) / 256);
 #define L(D_) hipLaunchKernelGGL(dense_scores_kernel<D_>, grid, dim3(256), 0, st, (const __bf16*)X, \
-                                 rows, n_list, r_lo, n_range, (const __bf16*)Q, NQ, out, ld)
+                                 rows, n_list, ts, div, r_lo, n_range, (const __bf16*)Q, NQ, out, ld)
   if (dim == 384) L(384);
   else if (dim == 768) L(768);
   else if (dim == 1024) L(1024);

@@ -781,6 +781,86 @@ def test_quant_stream_images_match_reference(D):
                    what="stream mx4 margin")
 
 
+@pytest.mark.parametrize("D", [384, 768, 1024])
+def test_dense_scores_list_range_and_seed_tiles(D):
+    """prepass.hip dense_scores == fp32 torch scores: a row list plus a row range in one launch
+    (ragged counts, a row stride ld > columns), and the hashed seed-tile list computed in-kernel
+    == _tile_sample_plan's idx rows; then the dense counted select reads its columns in place
+    (ld) and writes the k-th best minus the margin (kth_out)."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+    from codename_symbiont_amd.ops._ext import hip, stream_handle
+
+    h, st = hip(), stream_handle()
+    n = 300_000
+    x = torch.nn.functional.normalize(_f(n, D, seed=71), dim=-1).bfloat16()
+    q = torch.nn.functional.normalize(_f(301, D, seed=72), dim=-1).bfloat16()
+    rows = torch.randint(0, n, (1000,), device=DEV, dtype=torch.int32)
+    ld = 1000 + 777 + 3
+    out = torch.full((301, ld), 7.0, device=DEV)
+    h.dense_scores(x.data_ptr(), D, rows.data_ptr(), 1000, 5000, 777, q.data_ptr(), 301,
+                   out.data_ptr(), ld, st)
+    want = q.float() @ torch.cat([x[rows.long()], x[5000:5777]]).float().t()
+    torch.cuda.synchronize()
+    _close(out[:, :1777], want, atol=1e-5, rtol=1e-5, what="dense scores")
+    assert (out[:, 1777:] == 7.0).all(), "dense_scores wrote past its columns"
+    shard = HbmIndexShard(D, n)
+    shard.rows[:n].copy_(x)
+    shard.count = shard.visible = n
+    ts, nv, t0, idx = shard._tile_sample_plan(n, 5)
+    m = idx.numel()
+    assert m == -(-nv // shard.SEED_DIV) * 64
+    S = torch.empty(301, m + 4, device=DEV)
+    h.dense_scores(x.data_ptr(), D, 0, m, 0, 0, q.data_ptr(), 301, S.data_ptr(), m + 4, st,
+                   ts=ts, div=shard.SEED_DIV)
+    want = q.float() @ x[idx].float().t()
+    torch.cuda.synchronize()
+    _close(S[:, :m], want, atol=1e-5, rtol=1e-5, what="seed-tile scores")
+    k = 10
+    ts_, ti_ = (torch.empty(301, k, device=DEV), torch.empty(301, k, dtype=torch.int32, device=DEV))
+    kth = torch.empty(301, device=DEV)
+    flag = torch.zeros(1, dtype=torch.int32, device=DEV)
+    h.topk_select_counted(S.data_ptr(), 0, 0, m, 301, 16, k, ts_.data_ptr(), ti_.data_ptr(),
+                          flag.data_ptr(), st, reset_ovf=False, ld=m + 4, kth_out=kth.data_ptr(),
+                          kth_margin=2.0 ** -12)
+    ref = torch.topk(S[:, :m], k, dim=1)
+    torch.cuda.synchronize()
+    _close(ts_, ref.values, atol=0, rtol=0, what="dense select")
+    _close(kth, ref.values[:, k - 1] - 2.0 ** -12, atol=0, rtol=0, what="kth_out")
+    assert int(flag) == 0
+
+
+@pytest.mark.parametrize("D", [384, 768])
+def test_append_rows_writes_rows_and_both_images(D):
+    """prepass.hip's append_rows_kernel (one launch per upsert) == the bf16 copy plus the two
+    stream quantisers: the rows, the int8 and MX-fp4 stream images and both bound pairs."""
+    from codename_symbiont_amd.ops._ext import hip, stream_handle
+
+    h, st = hip(), stream_handle()
+    n, r0, cap = 333, 1000 + 17, 2048
+    x = torch.nn.functional.normalize(_f(n, D, seed=73), dim=-1).bfloat16()
+    n_sub = cap // 32
+    imgs, bs = [], []
+    for form in (0, 1):
+        imgs.append(torch.zeros(2, n_sub, h.stream_rec_bytes(D, form), dtype=torch.uint8, device=DEV))
+        bs.append(torch.zeros(2, 2, device=DEV))
+    rows = torch.zeros(2, cap, D, dtype=torch.bfloat16, device=DEV)
+    h.append_rows(x.data_ptr(), n, D, rows[0].data_ptr(), r0, imgs[0][0].data_ptr(),
+                  bs[0][0].data_ptr(), imgs[1][0].data_ptr(), bs[1][0].data_ptr(), st)
+    rows[1, r0:r0 + n].copy_(x)
+    h.quant_stream_i8(rows[1].data_ptr(), r0, 0, n, D, imgs[0][1].data_ptr(), bs[0][1].data_ptr(), st)
+    h.quant_stream_mx4(rows[1].data_ptr(), r0, 0, n, D, imgs[1][1].data_ptr(), 0, 0,
+                       bs[1][1].data_ptr(), 0, st)
+    torch.cuda.synchronize()
+    assert torch.equal(rows[0], rows[1])
+    y8, ysx = R.stream_i8_decode(imgs[0][0], cap, D)
+    r8, rsx = R.stream_i8_decode(imgs[0][1], cap, D)
+    assert torch.equal(ysx, rsx) and torch.equal(y8, r8), "int8 stream image"
+    assert torch.equal(imgs[1][0][:, :D * 16], imgs[1][1][:, :D * 16]), "MX-fp4 nibbles"
+    assert torch.equal(R.stream_mx4_decode(imgs[1][0], cap, D), R.stream_mx4_decode(imgs[1][1], cap, D))
+    for b in bs:
+        _close(b[0], b[1], atol=0, rtol=1e-6, what="append bounds")
+
+
 @pytest.mark.parametrize("form,D", [(0, 384), (1, 384), (0, 768), (1, 768)])
 def test_index_scan_stream_emits_the_bound_set(form, D):
     """index_stream.hip scan_stream_kernel (v_mfma_i32_32x32x32_i8 / v_mfma_scale_f32_32x32x64
@@ -1271,6 +1351,12 @@ def test_prune_qquant_and_route_match_torch():
     torch.cuda.synchronize()
     assert torch.equal(q8, q80) and torch.equal(sq, sq0)
     _close(margin, m0, atol=2e-5, what="bound margin")
+    # the search workspace (counters, flags, route maxima) is cleared by the same launch
+    ws = torch.full((2 * nq + 8 + 1000,), 7, dtype=torch.int32, device=DEV)
+    h.prune_qquant(q.data_ptr(), nq, 384, shard.i8_bounds.data_ptr(), q8.data_ptr(), sq.data_ptr(),
+                   margin.data_ptr(), st, zero=ws.data_ptr(), zero_n=ws.numel() - 1)
+    torch.cuda.synchronize()
+    assert (ws[:-1] == 0).all() and int(ws[-1]) == 7 and torch.equal(q8, q80)
     # sample candidates: query j gets j rows inside the band [T - margin, ...), 3 rows below it;
     # queries >= 200 overflow their buffer
     cs = torch.full((nq, cap), -1.0, device=DEV)
