@@ -3,7 +3,8 @@
 
     python benchmarks/gemm_sweep.py [--models bge-base,e5-large] [--variants t3,t9,lt,torch]
 
-Variants: tN = symb_gemm with tile mode N (3 = auto with the 256x192 tile, 10 = the round-3
+Variants: pp / pp256 / pp128 = the ping-pong kernel (gemm_pp.hip; auto / forced tile rows);
+tN = symb_gemm with tile mode N (3 = auto with the 256x192 tile, 10 = the round-3
 auto rule, 2 = the 256x256 tile wherever N % 256 == 0), hipBLASLt route off; lt = the hipBLASLt
 route for the plain projections (round-3 default);
 torch = torch.matmul (hipBLASLt, no epilogue).
@@ -58,11 +59,16 @@ def main():
                 if v == "torch":
                     return lambda: torch.matmul(x, w.t(), out=y)
                 if v == "lt":
-                    return lambda: (hip().gemm_config(128, 10, 8), hip().gemm_lt_config(1),
-                                    K.gemm(x, w, b, epi, r, out=y), hip().gemm_lt_config(0))
+                    return lambda: (hip().gemm_config(128, 10, 8), hip().gemm_pp_config(0),
+                                    hip().gemm_lt_config(1), K.gemm(x, w, b, epi, r, out=y),
+                                    hip().gemm_lt_config(0))
+                if v.startswith("pp"):
+                    bm = int(v[2:] or 0)
+                    return lambda: (hip().gemm_config(128, 3, 8), hip().gemm_lt_config(0),
+                                    hip().gemm_pp_config(2, bm), K.gemm(x, w, b, epi, r, out=y))
                 t = int(v[1:])
                 return lambda: (hip().gemm_config(128, t, 8), hip().gemm_lt_config(0),
-                                K.gemm(x, w, b, epi, r, out=y))
+                                hip().gemm_pp_config(0), K.gemm(x, w, b, epi, r, out=y))
 
             fns = {v: mk(v) for v in a.variants.split(",")}
             times = {v: [] for v in fns}
@@ -87,6 +93,7 @@ def main():
                                   "TFLOPs": round(2 * a.m * n * k / med / 1e6)}), flush=True)
     hip().gemm_config(128, 3, 8)
     hip().gemm_lt_config(1)
+    hip().gemm_pp_config(0)
 
 
 if __name__ == "__main__":

@@ -128,19 +128,21 @@ def resolve_prune(mode: str | None, dtype: str = "bf16", dim: int = 384,
     if mode == "auto":
         if device is not None and torch.device(device).type != "cuda":
             return None
-        return "i8" if (dtype == "bf16" and dim in PRUNE_DIMS and not prefilter) else None
+        return "i8" if (dtype == "bf16" and dim in AUTO_PRUNE_DIMS and not prefilter) else None
     return mode
 
 
 FP8_DIMS = (256, 384, 512, 768, 1024)   # row widths the fp8 scan kernel takes
 MQ_DIMS = (384, 768, 1024)              # ... the emitting bf16 scan (index_mq.hip)
-PRUNE_DIMS = (384, 768)                 # ... the int8-pruned scan (index_i8.hip)
+PRUNE_DIMS = (384, 768, 1024)           # ... the int8-pruned scan (1024: stream scan only)
+AUTO_PRUNE_DIMS = (384, 768)            # ... where SYMB_INDEX_PRUNE=auto takes it
 SPLIT_DIMS = (384,)                     # ... its split image (calibrate_prune)
 SPLIT_HEAVY = 64                        # leading components the split image keeps as fp16
-MX4_DIMS = (384, 768)                   # ... the MX-fp4 first tier (384-only on the LDS-ring scan)
+MX4_DIMS = (384, 768, 1024)             # ... the MX-fp4 first tier (384-only on the LDS-ring scan)
 # widths of the streaming pruning scan (index_stream.hip): fragment-major int8 / MX-fp4 images,
-# one wave per SIMD, no LDS ring (SYMB_PRUNE_STREAM=0: the round-4 LDS-ring scan, index_i8.hip)
-STREAM_DIMS = (384, 768)
+# one wave per SIMD, no LDS ring (SYMB_PRUNE_STREAM=0: the round-4 LDS-ring scan, index_i8.hip,
+# 384 / 768 only)
+STREAM_DIMS = (384, 768, 1024)
 STREAM_SUB = 32                         # rows per sub-tile record of the stream images
 
 
@@ -173,6 +175,9 @@ class HbmIndexShard:
             raise ValueError(f"index prune must be i8 or None, got {prune!r}")
         if prune and (dtype != "bf16" or dim not in PRUNE_DIMS):
             raise ValueError(f"the int8 pruned search needs a bf16 shard of width {PRUNE_DIMS}")
+        if (prune and dim not in (384, 768)
+                and os.environ.get("SYMB_PRUNE_STREAM", "1") in ("", "0")):
+            raise ValueError(f"the {dim}-wide pruned search runs on the stream scan only")
         self.prune = prune
         self.dim = dim
         self.dtype = dtype

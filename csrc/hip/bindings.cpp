@@ -133,6 +133,7 @@ int symb_prune_qprep(const void* Q, int NQ, int dim, const float* pre_s, const f
                      float thr_margin, const float* bounds, void* Q8, float* sq, float* T,
                      float* thr, hipStream_t st);
 int symb_gemm_lt_config(int mode);
+int symb_gemm_pp_mode(int mode, int bm);
 int symb_gemm_lt_plans();
 int symb_gemm_skinny_config(int max_m, int fuse);
 int symb_gemm_skinny_max_m();
@@ -615,6 +616,8 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("Q"), py::arg("NQ"), py::arg("dim"), py::arg("pre_s"), py::arg("tail_s"),
      py::arg("k"), py::arg("thr_margin"), py::arg("bounds"), py::arg("Q8"), py::arg("sq"),
      py::arg("T"), py::arg("thr"), py::arg("stream"));
+  m.def("gemm_pp_config", [](int mode, int bm) { check(symb_gemm_pp_mode(mode, bm), "gemm_pp_config"); },
+        py::arg("mode"), py::arg("bm") = 0);
   m.def("gemm_lt_config", [](int mode) { check(symb_gemm_lt_config(mode), "gemm_lt_config"); },
         py::arg("mode"));
   m.def("gemm_lt_plans", []() { return symb_gemm_lt_plans(); });

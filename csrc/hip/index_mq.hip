@@ -207,8 +207,10 @@ __global__ __launch_bounds__(512, 1) void index_scan_mq_kernel(
       const int base = lst.blist[2 + i] * lst.list_tiles;
       const int t0 = base + min((rb - s0) * per, lst.list_tiles);
       const int t1 = base + min((rb - s0 + 1) * per, lst.list_tiles);
-      row_begin = min(t0 * TR, n_valid);
-      row_end = min(t1 * TR, n_valid);
+      // (list tiles are the caller's 64-row tiles, whatever this width's TR: 768 / 1024 scan
+      // 32- / 16-row tiles, and reading t0 * TR there scanned the wrong rows)
+      row_begin = min(t0 * 64, n_valid);
+      row_end = min(t1 * 64, n_valid);
     }
   }
   const int n_tiles = row_end > row_begin ? (row_end - row_begin + TR - 1) / TR : 0;

@@ -51,7 +51,7 @@ struct SDim {
   static constexpr int HDR = FMT == SF_I8 ? 128 : 0;             // row scales (int8)
   static constexpr int FRAG = NKS * 1024;
   static constexpr int REC = HDR + FRAG + NSC * 256;             // bytes per 32-row sub-tile
-  static_assert(D % KE == 0 && (D == 384 || D == 768), "stream image row width");
+  static_assert(D % KE == 0 && (D == 384 || D == 768 || D == 1024), "stream image row width");
 };
 
 // Scan geometry: SETS 32-query sets per wave (resident B operands: SETS x NKS x 4 VGPRs), NW
@@ -60,9 +60,12 @@ struct SDim {
 template <int FMT, int D, int V = 0>
 struct SGeo {
   static constexpr int NKS = SDim<FMT, D>::NKS;
-  // MX-fp4 384: 256 queries per wave (V 0) or 128 per wave, two waves per workgroup (V 1)
-  static constexpr int SETS = FMT == SF_MX4 ? (D == 384 && V == 0 ? 8 : 4) : (D == 384 ? 4 : 2);
-  static constexpr int NW = 256 / (SETS * 32) > 0 ? 256 / (SETS * 32) : 1;
+  // MX-fp4 384: 256 queries per wave (V 0) or 128 per wave, two waves per workgroup (V 1); the
+  // wider rows hold fewer resident sets (1024: int8 one set, 4 waves = 128 queries per workgroup)
+  static constexpr int SETS = FMT == SF_MX4 ? (D == 384 && V == 0 ? 8 : D == 1024 ? 2 : 4)
+                                            : (D == 384 ? 4 : D == 768 ? 2 : 1);
+  static constexpr int NW0 = 256 / (SETS * 32) > 0 ? 256 / (SETS * 32) : 1;
+  static constexpr int NW = NW0 > 4 ? 4 : NW0;
   static constexpr int DEPTH = FMT == SF_MX4 ? 3 : 2;
   static constexpr int QPB = SETS * 32 * NW;                      // queries per workgroup
   static constexpr int STW = 512;                                 // staged candidates per wave
@@ -78,6 +81,13 @@ __device__ __forceinline__ void static_for(F&& f) {
     f(std::integral_constant<int, I>());
     static_for<I + 1, N>(f);
   }
+}
+
+__device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b), c); }
+__device__ __forceinline__ int max16i(const i32x16s& v) {   // v_max3_i32 chains
+  const int a = max3i(v[0], v[1], v[2]), b = max3i(v[3], v[4], v[5]), c = max3i(v[6], v[7], v[8]);
+  const int d = max3i(v[9], v[10], v[11]), e = max3i(v[12], v[13], v[14]);
+  return max3i(max3i(a, b, c), max3i(d, e, v[15]), v[15]);
 }
 
 __device__ __forceinline__ float max16(const float (&v)[16]) {
@@ -209,15 +219,42 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
     }
   };
 
+  // int8 pre-test: max_r acc[r] sx[r] <= imax * (imax >= 0 ? max sx : min sx) over this lane's 16
+  // rows -- 8 integer max3 + 4 ops per set instead of 16 cvt + 16 mul + 8 max3 (the VALU that
+  // competed with the MFMA issue); a block that passes it is re-tested exactly row by row below
+  auto block_raw = [&](auto dc, auto sc) {
+    constexpr int d = decltype(dc)::value, s = decltype(sc)::value;
+    i32x16s acc = {};
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+      acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(fk[d][ks], qf[s][ks], acc, 0, 0, 0);
+    return acc;
+  };
+
   auto process = [&](auto dc, int i) {
+    constexpr int d = decltype(dc)::value;
     const int row0 = (g0 + i) * 32 + 4 * h;   // + (r & 3) + 8 (r >> 2)
     uint32_t hm = 0;                          // sets with a hit in this lane
-    static_for<0, SETS>([&](auto sc) {
-      constexpr int s = decltype(sc)::value;
-      float v[16];
-      block(dc, sc, v);
-      hm |= (max16(v) >= thr[s] ? 1u : 0u) << s;
-    });
+    if constexpr (FMT == SF_I8) {
+      float smax = frs[d][0][0], smin = smax;
+#pragma unroll
+      for (int r = 1; r < 16; ++r) {
+        smax = fmaxf(smax, frs[d][r >> 2][r & 3]);
+        smin = fminf(smin, frs[d][r >> 2][r & 3]);
+      }
+      static_for<0, SETS>([&](auto sc) {
+        constexpr int s = decltype(sc)::value;
+        const int im = max16i(block_raw(dc, sc));
+        hm |= ((float)im * (im >= 0 ? smax : smin) >= thr[s] ? 1u : 0u) << s;
+      });
+    } else {
+      static_for<0, SETS>([&](auto sc) {
+        constexpr int s = decltype(sc)::value;
+        float v[16];
+        block(dc, sc, v);
+        hm |= (max16(v) >= thr[s] ? 1u : 0u) << s;
+      });
+    }
     if (__builtin_amdgcn_ballot_w64(hm != 0)) {   // rare: recompute the hit sets, emit per row
       static_for<0, SETS>([&](auto sc) {
         constexpr int s = decltype(sc)::value;
@@ -492,6 +529,7 @@ using namespace symb;
 int symb_stream_rec_bytes(int dim, int form) {
   if (dim == 384) return form ? SDim<SF_MX4, 384>::REC : SDim<SF_I8, 384>::REC;
   if (dim == 768) return form ? SDim<SF_MX4, 768>::REC : SDim<SF_I8, 768>::REC;
+  if (dim == 1024) return form ? SDim<SF_MX4, 1024>::REC : SDim<SF_I8, 1024>::REC;
   return 0;
 }
 
@@ -519,6 +557,10 @@ int symb_stream_geometry(int dim, int form, int* qpb, int* wgs_per_cu) {
   if (dim == 768) {
     if (form) G_(SF_MX4, 768, 0);
     G_(SF_I8, 768, 0);
+  }
+  if (dim == 1024) {
+    if (form) G_(SF_MX4, 1024, 0);
+    G_(SF_I8, 1024, 0);
   }
 #undef G_
   return -1;
@@ -551,7 +593,7 @@ int symb_index_scan_stream(const void* img, int n_valid, int alloc_rows, int row
                            hipStream_t st, const int* skip, int dim, int form, const int* gate,
                            int gate_want, int zero_cnt, int* runs) {
   if (NQ <= 0) return 0;
-  if ((dim != 384 && dim != 768) || (form != 0 && form != 1)) return -1;
+  if ((dim != 384 && dim != 768 && dim != 1024) || (form != 0 && form != 1)) return -1;
   if (form == 1 && qsc == nullptr) return -1;
   if (rows_per_blk % 32 || n_rblk <= 0 || thr == nullptr || cap <= 0 || n_valid <= 0) return -1;
   if ((long long)n_rblk * rows_per_blk < n_valid) return -1;
@@ -567,7 +609,8 @@ int symb_index_scan_stream(const void* img, int n_valid, int alloc_rows, int row
     if (form && g_stream_mx4_v) return L(SF_MX4, 384, 1);
     return form ? L(SF_MX4, 384, 0) : L(SF_I8, 384, 0);
   }
-  return form ? L(SF_MX4, 768, 0) : L(SF_I8, 768, 0);
+  if (dim == 768) return form ? L(SF_MX4, 768, 0) : L(SF_I8, 768, 0);
+  return form ? L(SF_MX4, 1024, 0) : L(SF_I8, 1024, 0);
 #undef L
 }
 
@@ -582,6 +625,7 @@ int symb_append_rows(const void* src, int n, int dim, void* rows, int r0, void* 
                                  (uint8_t*)img4, b4)
   if (dim == 384) L(384);
   else if (dim == 768) L(768);
+  else if (dim == 1024) L(1024);
   else return -1;
 #undef L
   return (int)hipGetLastError();
@@ -596,6 +640,7 @@ int symb_quant_stream_i8(const void* X, int r0, const int* rows, int n, int dim,
                                  (const __bf16*)X, r0, rows, n, (uint8_t*)img, bounds)
   if (dim == 384) L(384);
   else if (dim == 768) L(768);
+  else if (dim == 1024) L(1024);
   else return -1;
 #undef L
   return (int)hipGetLastError();
@@ -615,6 +660,7 @@ int symb_quant_stream_mx4(const void* X, int r0, const int* rows, int n, int dim
                                  (uint32_t*)QS, bounds, margin)
   if (dim == 384) L(384);
   else if (dim == 768) L(768);
+  else if (dim == 1024) L(1024);
   else return -1;
 #undef L
   return (int)hipGetLastError();

@@ -480,21 +480,21 @@ def test_tile_sample_plan_invariants():
     assert c is not b and c.numel() >= b.numel()
 
 
-@pytest.mark.parametrize("stream", ["1", "0"])
-def test_int8_pruning_bound_holds_and_image_follows_writes(stream, monkeypatch):
+@pytest.mark.parametrize("stream,D", [("1", 384), ("0", 384), ("1", 1024)])
+def test_int8_pruning_bound_holds_and_image_follows_writes(stream, D, monkeypatch):
     """The exact int8-pruned search (csrc/hip/index_stream.hip, index_i8.hip) relies on
     |q.x - q~.x~| <= |q| E + |q - q~| X with E = max |x - x~|, X = max |x~| over the rows written:
     check it for every (query, row) pair of random and outlier-heavy data, and that the shard's
     int8 image (the stream image, or the row-major one with SYMB_PRUNE_STREAM=0) and its (E, X)
-    follow appends, scattered overwrites and snapshot loads."""
+    follow appends, scattered overwrites and snapshot loads (1024: stream scan only)."""
     from codename_symbiont_amd.index.shard import resolve_prune
     from codename_symbiont_amd.ops.reference import quant_rows_i8_ref, stream_i8_decode
 
     monkeypatch.setenv("SYMB_PRUNE_STREAM", stream)
     g = torch.Generator().manual_seed(5)
-    x = torch.randn(3000, 384, generator=g)
+    x = torch.randn(3000, D, generator=g)
     x[:100, :4] *= 30.0                     # rows dominated by a few large components
-    sh = HbmIndexShard(384, 4000, device="cpu", prune="i8")
+    sh = HbmIndexShard(D, 4000, device="cpu", prune="i8")
     assert sh.stream == (stream == "1")
     sh.append_f32(x[:2000])
     sh.write_f32(5, x[2500:2501])           # an overwrite refreshes that row's image
@@ -503,14 +503,14 @@ def test_int8_pruning_bound_holds_and_image_follows_writes(stream, monkeypatch):
     xb = sh.rows[:sh.count]
     x8, sx, err, xtn = quant_rows_i8_ref(xb)
     if sh.stream:
-        y8, ysx = stream_i8_decode(sh.img_i8[:(sh.count + 31) // 32], sh.count, 384)
+        y8, ysx = stream_i8_decode(sh.img_i8[:(sh.count + 31) // 32], sh.count, D)
         assert torch.equal(y8, x8) and torch.allclose(ysx, sx)
         assert sh.rows_i8 is None
     else:
         assert torch.equal(sh.rows_i8[:sh.count], x8) and torch.allclose(sh.sx_i8[:sh.count], sx)
     E, X = float(sh.i8_bounds[0]), float(sh.i8_bounds[1])
     assert E >= float(err.max()) - 1e-7 and X >= float(xtn.max()) - 1e-7
-    q = torch.nn.functional.normalize(torch.randn(64, 384, generator=g), dim=-1).bfloat16()
+    q = torch.nn.functional.normalize(torch.randn(64, D, generator=g), dim=-1).bfloat16()
     q8, sq, eq, _ = quant_rows_i8_ref(q)
     s = q.float() @ xb.float().t()
     s_i8 = (q8.float() @ x8.float().t()) * sq[:, None] * sx[None, :]
@@ -573,7 +573,7 @@ def test_split_image_bound_holds_and_prunes_anisotropic_rows():
     assert (r.img_i8 is not None) if r.stream else r.rows_i8.shape[1] == 384
 
 
-@pytest.mark.parametrize("stream,D", [("1", 384), ("1", 768), ("0", 384)])
+@pytest.mark.parametrize("stream,D", [("1", 384), ("1", 768), ("1", 1024), ("0", 384)])
 def test_mx4_image_follows_writes_and_bounds_every_pair(stream, D, monkeypatch):
     """The MX-fp4 first-tier image (e2m1 nibbles + e8m0 block scales; the stream image at 384 and
     768, the row-major one with SYMB_PRUNE_STREAM=0) follows appends and scattered overwrites, its

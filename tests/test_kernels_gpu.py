@@ -96,6 +96,7 @@ def test_gemm(M, N, K, epi, tile):
     # the M <= 256 shapes exercise the tiled kernels' ragged small-M handling (test_gemm_skinny
     # covers the skinny path)
     hip().gemm_skinny_config(0)
+    hip().gemm_pp_config(0)   # (the ping-pong kernel: test_gemm_pingpong)
     try:
         out = gemm(a := _bf(M, K, seed=1), w := _bf(N, K, scale=1.0 / math.sqrt(K), seed=2),
                    bias := _f(N, scale=0.5, seed=3), epi,
@@ -107,8 +108,35 @@ def test_gemm(M, N, K, epi, tile):
         hip().gemm_resln_config(16)
         hip().gemm_lt_config(1)
         hip().gemm_skinny_config(256)
+        hip().gemm_pp_config(0)
     ref = R.gemm_ref(a, w, bias, epi, res, g, b, 1e-12)
     _close(out, ref, atol=4e-2, rtol=2e-2, what=f"gemm epi={epi}")
+
+
+@pytest.mark.parametrize("bm", [256, 128])
+@pytest.mark.parametrize("M,N,K,epi", [
+    (300, 256, 128, 0), (1000, 768, 768, 2), (2049, 2304, 768, 0), (4353, 768, 3072, 2),
+    (777, 3072, 768, 1), (5000, 1024, 4096, 2), (257, 512, 320, 1), (32768, 768, 768, 0),
+    (130, 4096, 1024, 1),
+])
+def test_gemm_pingpong(M, N, K, epi, bm):
+    """gemm_pp.hip (the wide projections' kernel: two wave rows half a phase apart, LDS-DMA
+    half-tiles) == the fp32 oracle on every epilogue, both tile heights, ragged M, an odd number of
+    64-deep k-tiles (K = 320) and single-tile K (128)."""
+    from codename_symbiont_amd.ops._ext import hip
+    from codename_symbiont_amd.ops.kernels import gemm
+
+    hip().gemm_pp_config(2, bm)
+    hip().gemm_skinny_config(0)
+    try:
+        out = gemm(a := _bf(M, K, seed=1), w := _bf(N, K, scale=1.0 / math.sqrt(K), seed=2),
+                   bias := _f(N, scale=0.5, seed=3), epi,
+                   res := (_bf(M, N, seed=4) if epi == 2 else None))
+    finally:
+        hip().gemm_pp_config(0)
+        hip().gemm_skinny_config(256)
+    ref = R.gemm_ref(a, w, bias, epi, res, None, None, 1e-12)
+    _close(out, ref, atol=4e-2, rtol=2e-2, what=f"pingpong gemm bm={bm} epi={epi}")
 
 
 @pytest.mark.parametrize("M,N,K,epi", [(300, 1152, 384, 0), (4100, 768, 3072, 2), (999, 2304, 768, 0),
@@ -718,7 +746,7 @@ def test_quant_rows_i8_matches_reference(D):
     _close(xtn, xt.norm(dim=1), atol=1e-5, what="i8 |x~|")
 
 
-@pytest.mark.parametrize("D", [384, 768])
+@pytest.mark.parametrize("D", [384, 768, 1024])
 def test_quant_stream_images_match_reference(D):
     """index_stream.hip's image writers == the torch references: the int8 stream image (per-row
     scale header + fragment-major codes) and the MX-fp4 one (fragment-major nibbles + per-lane
@@ -829,7 +857,7 @@ def test_dense_scores_list_range_and_seed_tiles(D):
     assert int(flag) == 0
 
 
-@pytest.mark.parametrize("D", [384, 768])
+@pytest.mark.parametrize("D", [384, 768, 1024])
 def test_append_rows_writes_rows_and_both_images(D):
     """prepass.hip's append_rows_kernel (one launch per upsert) == the bf16 copy plus the two
     stream quantisers: the rows, the int8 and MX-fp4 stream images and both bound pairs."""
@@ -861,7 +889,7 @@ def test_append_rows_writes_rows_and_both_images(D):
         _close(b[0], b[1], atol=0, rtol=1e-6, what="append bounds")
 
 
-@pytest.mark.parametrize("form,D", [(0, 384), (1, 384), (0, 768), (1, 768)])
+@pytest.mark.parametrize("form,D", [(0, 384), (1, 384), (0, 768), (1, 768), (0, 1024), (1, 1024)])
 def test_index_scan_stream_emits_the_bound_set(form, D):
     """index_stream.hip scan_stream_kernel (v_mfma_i32_32x32x32_i8 / v_mfma_scale_f32_32x32x64
     on fragment-major images, one wave per SIMD): exactly the rows whose estimate (int8: (q8 .
@@ -1057,14 +1085,16 @@ def test_wide_index_topk_exact_vs_torch_topk(D, k):
     assert r[:8, 0].tolist() == list(range(n, n + 8))
 
 
-@pytest.mark.parametrize("nq,data", [(256, "random"), (300, "near"), (512, "random"),
-                                     (256, "clustered")])
-def test_index_pruned_search_768_is_exact(nq, data):
+@pytest.mark.parametrize("nq,data,D", [(256, "random", 768), (300, "near", 768),
+                                       (512, "random", 768), (256, "clustered", 768),
+                                       (256, "random", 1024), (300, "near", 1024)])
+def test_index_pruned_search_768_is_exact(nq, data, D):
     """The int8-pruned search at the reference's 768-d collection (12 i8 k-steps, 192 query
-    registers, single-sub-tile chains): the rows and scores of the exact bf16 scan."""
+    registers) and at 1024 (the stream scan's one-set form): the rows and scores of the exact
+    bf16 scan."""
     from codename_symbiont_amd.index.shard import HbmIndexShard
 
-    n, k, D = (1 << 20) + 777, 10, 768
+    n, k = (1 << 20) + 777, 10
     g = torch.Generator(device=DEV).manual_seed(72)
     if data == "clustered":
         centers = torch.randn(64, D, device=DEV, generator=g)
@@ -1290,7 +1320,7 @@ def test_index_scan_mx4_emits_the_bound_set(monkeypatch):
 
 @pytest.mark.parametrize("nq,stream,D", [(256, "1", 384), (512, "1", 384), (2048, "1", 384),
                                          (256, "0", 384), (2048, "0", 384), (256, "1", 768),
-                                         (512, "1", 768)])
+                                         (512, "1", 768), (256, "1", 1024)])
 def test_index_pruned_search_mx4_tier_is_exact(nq, stream, D, monkeypatch):
     """The pruned search with the MX-fp4 first tier: near-duplicate queries (their k-th score far
     above the random bulk) take the fp4 tier, random held-out queries the int8 one; both give
@@ -1473,28 +1503,29 @@ def test_index_pruned_search_routes_dense_data_exactly(route):
     assert (r0 == r1).float().mean().item() > 0.999
 
 
-@pytest.mark.parametrize("where", ["middle", "tail"])
-def test_index_pruned_search_routes_crowded_blocks_exactly(where):
+@pytest.mark.parametrize("where,D", [("middle", 384), ("tail", 384), ("middle", 768), ("tail", 1024)])
+def test_index_pruned_search_routes_crowded_blocks_exactly(where, D):
     """A crowd of near-duplicates (cosine ~0.99, like freshly ingested random-init embeddings)
     in one row range: the int8 bound cannot separate it, so its blocks alone go to the bf16
     emitting scan (index_mq.hip list mode) while the int8 scan skips them, both filling the same
     candidate buffers.  Same rows and scores as the exact bf16 scan, no overflow, and only a few
-    blocks routed (the old whole-batch route would have scanned every row in bf16)."""
+    blocks routed (the old whole-batch route would have scanned every row in bf16).  At 768 / 1024
+    the bf16 scan runs 32- / 16-row tiles while the route lists 64-row tiles."""
     from codename_symbiont_amd.index.shard import HbmIndexShard
 
     n, crowd, k, nq = (1 << 20) + 3000, 60_000, 10, 256
     g = torch.Generator(device=DEV).manual_seed(5)
-    center = torch.nn.functional.normalize(torch.randn(1, 384, device=DEV, generator=g), dim=-1)
+    center = torch.nn.functional.normalize(torch.randn(1, D, device=DEV, generator=g), dim=-1)
 
     def near(m):
         return torch.nn.functional.normalize(
-            center + 0.0051 * torch.randn(m, 384, device=DEV, generator=g), dim=-1)
+            center + 0.0051 * torch.randn(m, D, device=DEV, generator=g), dim=-1)
 
-    rows = torch.nn.functional.normalize(torch.randn(n, 384, device=DEV, generator=g), dim=-1)
+    rows = torch.nn.functional.normalize(torch.randn(n, D, device=DEV, generator=g), dim=-1)
     c0 = 400_000 if where == "middle" else n - crowd
     rows[c0:c0 + crowd] = near(crowd)
-    ref = HbmIndexShard(384, n)
-    shard = HbmIndexShard(384, n, prune="i8")
+    ref = HbmIndexShard(D, n)
+    shard = HbmIndexShard(D, n, prune="i8")
     for sh in (ref, shard):
         sh.append_f32(rows)
     q = near(nq).bfloat16()
