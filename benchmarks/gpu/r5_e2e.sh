@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round 5: the end-to-end service on the round-5 tree: the reference's own
+# deployment shape -- native NATS broker, preprocessing (HIP encoder), vector_memory (100M-row
+# HBM index) and the native gateway as separate processes sharing the card -- driven by the
+# native load generator; search requests carry held-out query text (never ingested).
+#   1. MiniLM-L6 / 100M x 384 (the round-3 setup: 2048 in flight, bursts aligned to 256)
+#   2. paraphrase-multilingual-mpnet / 100M x 768 (the reference's 768-d collection)
+set -o pipefail
+cd "$(dirname "$0")/../.."
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+O=gpurun_out/r5_e2e
+mkdir -p $O
+SYMB_SEARCH_ALIGN=256 SYMB_SEARCH_MAX_BATCH=512 timeout -k 10 540 python -u benchmarks/e2e_service.py \
+  --model minilm-l6 --index-rows 100000000 --requests 40000 --warmup-requests 8000 --concurrency 512 \
+  > $O/minilm_100m_c512.json 2> $O/minilm_100m_c512.err || { tail -30 $O/minilm_100m_c512.err; exit 1; }
+cat $O/minilm_100m_c512.json
+SYMB_SEARCH_ALIGN=256 SYMB_SEARCH_MAX_BATCH=512 timeout -k 10 540 python -u benchmarks/e2e_service.py \
+  --model mpnet-multi --index-rows 100000000 --requests 20000 --warmup-requests 4000 --concurrency 512 \
+  > $O/mpnet_100m_c512.json 2> $O/mpnet_100m_c512.err || { tail -30 $O/mpnet_100m_c512.err; exit 1; }
+cat $O/mpnet_100m_c512.json

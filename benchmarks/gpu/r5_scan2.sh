@@ -21,7 +21,7 @@ cat $O/scan_i8_768.json
 P="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"
 for t in i8 mx4; do
   q=heldout; [ $t = mx4 ] && q=self
-  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $P -d $O/pmc_$t -o run -- python3 benchmarks/scan_one.py --rows 25000000 --iters 3 --tier $t --queries $q > $O/pmc_$t.log 2>&1 || { tail -20 $O/pmc_$t.log; exit 1; }
+  timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv --pmc $P -d $O/pmc_$t -o run -- python3 benchmarks/scan_one.py --rows 25000000 --iters 3 --tier $t --queries $q > $O/pmc_$t.log 2>&1 || { tail -20 $O/pmc_$t.log; exit 1; }
   python3 benchmarks/pmc_kernel.py $(find $O/pmc_$t -name "*counter_collection.csv") --match scan_stream > $O/pmc_$t.txt
   cat $O/pmc_$t.txt
 done

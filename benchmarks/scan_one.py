@@ -32,6 +32,10 @@ def main() -> None:
     ap.add_argument("--tier", choices=["i8", "mx4"], default="i8")
     ap.add_argument("--queries", choices=["heldout", "self"], default="heldout")
     ap.add_argument("--variant", type=int, default=-1, help="stream MX-fp4 form (stream_config)")
+    ap.add_argument("--ab", default="",
+                    help="stream forms timed in one process, interleaved: comma list of "
+                         "mx4variant:i8variant:ablation[:land] (e.g. 0:0:0:1,0:0:0:0,0:0:1)")
+    ap.add_argument("--rounds", type=int, default=3)
     a = ap.parse_args()
     from codename_symbiont_amd.index.shard import STREAM_SUB, HbmIndexShard
     from codename_symbiont_amd.index.synth import CorpusGen, fill_corpus
@@ -103,19 +107,30 @@ def main() -> None:
         nbytes, kernel = shard.img_i8.shape[1] / STREAM_SUB, "stream-i8"
     else:
         nbytes, kernel = shard.rows_i8.shape[1] + 4, "ldsring-" + ("split" if heavy else "i8")
-    scan()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.iters):
-        scan()
-    torch.cuda.synchronize()
-    ms = (time.perf_counter() - t0) * 1e3 / a.iters
-    print(json.dumps({"bench": "scan_one", "kernel": kernel, "rows": n, "nq": a.nq, "dim": a.dim,
-                      "corpus": a.corpus, "queries": a.queries, "image": "split" if heavy else "plain",
-                      "ms": round(ms, 3), "TBps": round(n * nbytes / ms / 1e9, 2),
-                      "n_rblk": P["n_rblk"], "rows_per_blk": P["rows_per_blk"],
-                      "cand_mean": round(float(P["cnt"].float().mean()), 1),
-                      "cand_max": int(P["cnt"].max()), "fill_s": round(fill_s, 1)}), flush=True)
+    forms = [tuple(int(x) for x in f.split(":")) for f in a.ab.split(",")] if a.ab else [None]
+    times = {f: [] for f in forms}
+    for _ in range(a.rounds if a.ab else 1):
+        for f in forms:
+            if f is not None:
+                h.stream_config(*f)
+            scan()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.iters):
+                scan()
+            torch.cuda.synchronize()
+            times[f].append((time.perf_counter() - t0) * 1e3 / a.iters)
+    if a.ab:
+        h.stream_config(0, 0, 0, 1)
+    for f, ts in times.items():
+        ms = sorted(ts)[len(ts) // 2]
+        print(json.dumps({"bench": "scan_one", "kernel": kernel, "form": f, "rows": n, "nq": a.nq,
+                          "dim": a.dim, "corpus": a.corpus, "queries": a.queries,
+                          "image": "split" if heavy else "plain",
+                          "ms": round(ms, 3), "TBps": round(n * nbytes / ms / 1e9, 2),
+                          "n_rblk": P["n_rblk"], "rows_per_blk": P["rows_per_blk"],
+                          "cand_mean": round(float(P["cnt"].float().mean()), 1),
+                          "cand_max": int(P["cnt"].max()), "fill_s": round(fill_s, 1)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -1275,7 +1275,10 @@ class HbmIndexShard:
             if self.mx4_on:
                 qpb4, wpc4 = h.stream_geometry(self.dim, 1)
                 n_qblk, wpc = max(n_qblk, math.ceil(NQ / qpb4)), max(wpc, wpc4)
-            n_rblk = max(1, min(math.ceil(n / (128 * 4)), 1024, max(1, round(n_cus * wpc / n_qblk))))
+            # (>= 8192 rows per block: the route estimates each block from the exact sample's
+            # 1-in-2^5 tiles, so a block needs a few sampled tiles -- ~1k-row blocks saw 0 or 1
+            # and left crowded blocks to the int8 scan)
+            n_rblk = max(1, min(math.ceil(n / 8192), 1024, max(1, round(n_cus * wpc / n_qblk))))
             rows_per_blk = _round_up(max(1, math.ceil(n / n_rblk)), 128)
             n_rblk = max(1, math.ceil(n / rows_per_blk))
             return rsplit, rows_per_blk, n_rblk

@@ -88,7 +88,7 @@ int symb_mx4_select(int NQ, const float* T, const float* margin4, const float* m
 int symb_i8_tile_rows_for(int dim, int heavy);
 // the streaming pruning scan (index_stream.hip)
 int symb_stream_rec_bytes(int dim, int form);
-int symb_stream_config(int mx4_variant);
+int symb_stream_config(int mx4_variant, int i8_variant, int abl, int land);
 int symb_stream_geometry(int dim, int form, int* qpb, int* wgs_per_cu);
 int symb_index_scan_stream(const void* img, int n_valid, int alloc_rows, int rows_per_blk,
                            int n_rblk, const void* Q, const void* qsc, int NQ, const float* thr,
@@ -134,6 +134,9 @@ int symb_prune_qprep(const void* Q, int NQ, int dim, const float* pre_s, const f
                      float* thr, hipStream_t st);
 int symb_gemm_lt_config(int mode);
 int symb_gemm_pp_mode(int mode, int bm);
+int symb_gemm_pp_ring(int ring);
+int symb_mfma_f8f6f4_probe(const int* a, const int* b, const int* sa, const int* sb, float* out,
+                           int fmt, hipStream_t st);
 int symb_gemm_lt_plans();
 int symb_gemm_skinny_config(int max_m, int fuse);
 int symb_gemm_skinny_max_m();
@@ -483,9 +486,9 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("gate_want") = 0);
   m.def("stream_rec_bytes", [](int dim, int form) { return symb_stream_rec_bytes(dim, form); },
         py::arg("dim"), py::arg("form"));
-  m.def("stream_config", [](int mx4_variant) {
-    check(symb_stream_config(mx4_variant), "stream_config");
-  }, py::arg("mx4_variant"));
+  m.def("stream_config", [](int mx4_variant, int i8_variant, int abl, int land) {
+    check(symb_stream_config(mx4_variant, i8_variant, abl, land), "stream_config");
+  }, py::arg("mx4_variant"), py::arg("i8_variant") = 0, py::arg("abl") = 0, py::arg("land") = 1);
   m.def("stream_geometry", [](int dim, int form) {
     int qpb = 0, wpc = 0;
     check(symb_stream_geometry(dim, form, &qpb, &wpc), "stream_geometry");
@@ -618,6 +621,12 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("T"), py::arg("thr"), py::arg("stream"));
   m.def("gemm_pp_config", [](int mode, int bm) { check(symb_gemm_pp_mode(mode, bm), "gemm_pp_config"); },
         py::arg("mode"), py::arg("bm") = 0);
+  m.def("gemm_pp_ring", [](int ring) { check(symb_gemm_pp_ring(ring), "gemm_pp_ring"); });
+  m.def("mfma_f8f6f4_probe", [](uptr a, uptr b, uptr sa, uptr sb, uptr out, int fmt, uptr st) {
+    check(symb_mfma_f8f6f4_probe(P<const int>(a), P<const int>(b), P<const int>(sa),
+                                 P<const int>(sb), P<float>(out), fmt, S(st)),
+          "mfma_f8f6f4_probe");
+  });
   m.def("gemm_lt_config", [](int mode) { check(symb_gemm_lt_config(mode), "gemm_lt_config"); },
         py::arg("mode"));
   m.def("gemm_lt_plans", []() { return symb_gemm_lt_plans(); });

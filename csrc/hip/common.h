@@ -114,6 +114,25 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
 }
 
+// LDS-DMA issued as inline asm (16 / 4 / 2 bytes per lane; lane l lands at lds + size * l, lds a
+// wave-uniform LDS byte address).  hipcc neither counts these loads nor inserts its conservative
+// "any pending LDS-DMA may alias this ds_read" vmcnt(0): the caller retires them with its own
+// counted s_waitcnt vmcnt before reading the data (same wave; other waves also need a barrier).
+// M0 is written and restored inside the statement (the compiler reserves it).
+#define SYMB_DMA_ASM(NAME, INSN)                                                                 \
+  __device__ __forceinline__ void NAME(const void* gsrc, uint32_t lds) {                        \
+    unsigned keep;                                                                               \
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t" INSN " %1, off\n\t"        \
+                 "s_mov_b32 m0, %0"                                                              \
+                 : "=&s"(keep)                                                                   \
+                 : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds))                          \
+                 : "memory");                                                                    \
+  }
+SYMB_DMA_ASM(dma16_asm, "global_load_lds_dwordx4")
+SYMB_DMA_ASM(dma4_asm, "global_load_lds_dword")
+SYMB_DMA_ASM(dma2_asm, "global_load_lds_ushort")
+#undef SYMB_DMA_ASM
+
 // Raise a kernel's dynamic-LDS limit (hipFuncAttributeMaxDynamicSharedMemorySize) before its
 // first launch ON EACH DEVICE: the attribute is per device, so a process driving several GPUs
 // must set it once per device, not once per process.  One bit per device id per kernel.

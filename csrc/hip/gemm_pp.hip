@@ -68,7 +68,10 @@ __device__ __forceinline__ void pp_barrier() {
 }  // namespace ggp
 
 // BM: tile rows (256: 128 x 64 per wave, 4 x 2 blocks of 32 x 32; 128: 64 x 64 per wave).
-template <int BM, int EPI>
+// ABL (timing ablations, wrong results): 1 = no vmcnt wait in the k-loop, 2 = no DMA in the k-loop
+// either (MFMA + LDS reads + barriers only).  RING (BM = 256): the half-tile ring below instead of
+// two k-tile buffers.
+template <int BM, int EPI, int ABL = 0, int RING = 0>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
     const __bf16* __restrict__ A, int lda, const __bf16* __restrict__ W, int ldw,
     const float* __restrict__ bias, const __bf16* __restrict__ R, int ldr, __bf16* __restrict__ C,
@@ -100,6 +103,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
 
   // half-tile loads: 0 = A rows [0, WTM), 1 = A rows [WTM, BM), 2 = W rows [0, 128), 3 = W [128, 256)
   auto load = [&](int which, int kt) {
+    if (ABL >= 2 && kt > 1) return;
     char* buf = smem + (kt & 1) * BUFB;
     if (which < 2)
       stage_half<WTM>(A, lda, m0 + which * WTM, M, kt, buf + which * AH, tid, wave);
@@ -149,6 +153,77 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
     __builtin_amdgcn_sched_barrier(0);
   };
 
+  if constexpr (RING) {
+    // v2: ten 16 KiB half-tile slots (the whole 160 KiB LDS) instead of two k-tile buffers.
+    // Half-tile h = 4 kt + j (j: A rows 0..127, A rows 128.., W rows 0..127, W rows 128..) lives in
+    // slot h % 10 and is issued at global phase h - 7 (one half per phase, the same one-half DMA
+    // slice per phase as v1), so three half-tiles are always in flight across the once-per-k-tile
+    // counted vmcnt (v1: one, which the waves then stalled on).  The slot h reuses held half h - 10,
+    // whose last reads (A: phase c of its tile, by one wave row; W: phase b, both rows) lie >= 1
+    // section before the DMA is issued, wave-row offset included (the table above, shifted: A half
+    // g of tile t is re-filled at d of t (g = 0) / a of t+1 (g = 1), W halves at b / c of t+1).
+    static_assert(BM == 256 && AH == BH, "ring slots are one half-tile");
+    constexpr int SLOT = BH, NSLOT = 10, LEAD = 7;
+    const int NH = 4 * KT;
+    auto issue = [&](int h) {
+      if (h >= NH) return;
+      const int kt = h >> 2, j = h & 3;
+      char* dst = smem + (h % NSLOT) * SLOT;
+      if (j < 2)
+        stage_half<WTM>(A, lda, m0 + j * WTM, M, kt, dst, tid, wave);
+      else
+        stage_half<128>(W, ldw, n0 + (j - 2) * 128, N, kt, dst, tid, wave);
+    };
+    auto read_a2 = [&](const char* base, int qm) {
+#pragma unroll
+      for (int b = 0; b < QB; ++b)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+          af[b][ks] = *reinterpret_cast<const bf16x8*>(base + swz((qm * QB + b) * 32 + fr, 2 * ks + fh));
+    };
+    auto read_b2 = [&](const char* base, int qn, bf16x8 (&bq)[4]) {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+        bq[ks] = *reinterpret_cast<const bf16x8*>(base + swz((wc & 1) * 64 + qn * 32 + fr, 2 * ks + fh));
+    };
+    for (int h = 0; h < LEAD; ++h) issue(h);
+    if (KT > 1)
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // tile 1's first three halves in flight
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ggp::pp_barrier();
+    if (wr == 1) ggp::pp_barrier();
+    for (int kt = 0; kt < KT; ++kt) {
+      const int hb = 4 * kt;
+      const char* sa = smem + ((hb + wr) % NSLOT) * SLOT;
+      const char* sb = smem + ((hb + 2 + (wc >> 1)) % NSLOT) * SLOT;
+      read_a2(sa, 0);
+      read_b2(sb, 0, bq0);
+      issue(hb + LEAD);
+      mfma_gate();
+      mfma_q(0, 0, bq0);
+      ggp::pp_barrier();
+      read_b2(sb, 1, bq1);
+      issue(hb + 1 + LEAD);
+      mfma_gate();
+      mfma_q(0, 1, bq1);
+      ggp::pp_barrier();
+      read_a2(sa, 1);
+      issue(hb + 2 + LEAD);
+      mfma_gate();
+      mfma_q(1, 1, bq1);
+      ggp::pp_barrier();
+      issue(hb + 3 + LEAD);
+      // tile kt + 1 complete: all but the halves issued in b, c, d of this tile (2 DMAs each)
+      if (kt + 2 < KT)
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      mfma_gate();
+      mfma_q(1, 0, bq0);
+      ggp::pp_barrier();
+    }
+  } else {
   // Schedule (tile T in buffer T & 1; one row of the table per phase, both wave rows):
   //   phase  reads (memory section)        DMA issued               MFMA quadrant
   //   a      A quadrant row 0, W column 0  W half 1 of T+1          (0, 0)
@@ -200,8 +275,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
     // d
     if (kt + 2 < KT) {
       load(2, kt + 2);
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");   // (W half: 2 DMAs per thread)
-    } else {
+      if (ABL == 0) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");   // (W half: 2 DMAs per thread)
+    } else if (ABL == 0) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     mfma_gate();
@@ -212,6 +287,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
     k_tile(kt, std::integral_constant<int, 0>());
     if (kt + 1 < KT) k_tile(kt + 1, std::integral_constant<int, 1>());
   }
+  }   // (v1)
   if (wr == 0) ggp::pp_barrier();   // rows back in step
   __syncthreads();
 
@@ -276,17 +352,17 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
   }
 }
 
-template <int BM, int EPI>
+template <int BM, int EPI, int ABL = 0, int RING = 0>
 static int launch_pp(const void* A, int lda, const void* W, int ldw, const float* bias,
                      const void* R, int ldr, void* C, int ldc, int M, int N, int K, int group_m,
                      int gelu_poly, hipStream_t st) {
-  constexpr int main_bytes = 2 * (BM * 128 + 2 * ggp::BH);
+  constexpr int main_bytes = RING ? 10 * ggp::BH : 2 * (BM * 128 + 2 * ggp::BH);
   constexpr int full = BM * (ggp::BN + 4) * 4;
   constexpr int epi_bytes = full > 160 * 1024 ? full / 2 : full;
   constexpr int lds = main_bytes > epi_bytes ? main_bytes : epi_bytes;
-  set_max_lds<gemm_pp_kernel<BM, EPI>>(lds);
+  set_max_lds<gemm_pp_kernel<BM, EPI, ABL, RING>>(lds);
   const int nwg = ((M + BM - 1) / BM) * (N / ggp::BN);
-  hipLaunchKernelGGL((gemm_pp_kernel<BM, EPI>), dim3(nwg), dim3(ggp::NT), lds, st,
+  hipLaunchKernelGGL((gemm_pp_kernel<BM, EPI, ABL, RING>), dim3(nwg), dim3(ggp::NT), lds, st,
                      (const __bf16*)A, lda, (const __bf16*)W, ldw, bias, (const __bf16*)R, ldr,
                      (__bf16*)C, ldc, M, N, K, group_m, gelu_poly);
   return (int)hipGetLastError();
@@ -296,11 +372,21 @@ static int launch_pp(const void* A, int lda, const void* W, int ldw, const float
 
 using namespace symb;
 
-// Tile rows: 0 = auto (pp_pick_bm), 256 or 128 forced (A/B sweeps).
-static int g_pp_bm = 0;
+// Tile rows: 0 = auto (pp_pick_bm), 256 or 128 forced (A/B sweeps); bm + 1 / + 2: the 256-row
+// bias kernel's timing ablations (ABL above).
+static int g_pp_bm = 0, g_pp_abl = 0, g_pp_ring = 1;
+// 256-row tiles on the half-tile ring (1, default) or the two k-tile buffers (0, v1)
+int symb_gemm_pp_ring(int ring) {
+  if (ring != 0 && ring != 1) return -1;
+  g_pp_ring = ring;
+  return 0;
+}
 int symb_gemm_pp_config(int bm) {
+  const int abl = bm & 3;
+  bm &= ~3;
   if (bm != 0 && bm != 128 && bm != 256) return -1;
   g_pp_bm = bm;
+  g_pp_abl = abl;
   return 0;
 }
 
@@ -326,6 +412,12 @@ int symb_gemm_pp(int epi, const void* A, int lda, const void* W, int ldw, const 
   if (!symb_gemm_pp_supported(epi, M, N, K)) return -1;
   if (lda % 8 || ldw % 8 || ldc % 8 || (epi == ggp::EPI_RES && (R == nullptr || ldr % 8))) return -1;
   const int bm = pp_pick_bm(M, N);
+  if (g_pp_abl == 1 && bm == 256 && epi == ggp::EPI_BIAS)
+    return launch_pp<256, ggp::EPI_BIAS, 1>(A, lda, W, ldw, bias, R, ldr, C, ldc, M, N, K, group_m,
+                                            gelu_poly, st);
+  if (g_pp_abl == 2 && bm == 256 && epi == ggp::EPI_BIAS)
+    return launch_pp<256, ggp::EPI_BIAS, 2>(A, lda, W, ldw, bias, R, ldr, C, ldc, M, N, K, group_m,
+                                            gelu_poly, st);
 #define L(BM_, E_) launch_pp<BM_, E_>(A, lda, W, ldw, bias, R, ldr, C, ldc, M, N, K, group_m, \
                                       gelu_poly, st)
   if (bm == 128) {
@@ -334,6 +426,16 @@ int symb_gemm_pp(int epi, const void* A, int lda, const void* W, int ldw, const 
       case ggp::EPI_GELU: return L(128, ggp::EPI_GELU);
       default: return L(128, ggp::EPI_RES);
     }
+  }
+  if (g_pp_ring) {
+#define LR(E_) launch_pp<256, E_, 0, 1>(A, lda, W, ldw, bias, R, ldr, C, ldc, M, N, K, group_m, \
+                                        gelu_poly, st)
+    switch (epi) {
+      case ggp::EPI_BIAS: return LR(ggp::EPI_BIAS);
+      case ggp::EPI_GELU: return LR(ggp::EPI_GELU);
+      default: return LR(ggp::EPI_RES);
+    }
+#undef LR
   }
   switch (epi) {
     case ggp::EPI_BIAS: return L(256, ggp::EPI_BIAS);

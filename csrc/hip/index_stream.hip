@@ -61,15 +61,23 @@ template <int FMT, int D, int V = 0>
 struct SGeo {
   static constexpr int NKS = SDim<FMT, D>::NKS;
   // MX-fp4 384: 256 queries per wave (V 0) or 128 per wave, two waves per workgroup (V 1); the
-  // wider rows hold fewer resident sets (1024: int8 one set, 4 waves = 128 queries per workgroup)
-  static constexpr int SETS = FMT == SF_MX4 ? (D == 384 && V == 0 ? 8 : D == 1024 ? 2 : 4)
+  // wider rows hold fewer resident sets (1024: int8 one set, 4 waves = 128 queries per workgroup).
+  // V 2 / 3: the default form one sub-tile deeper / shallower in flight (A/B).
+  static constexpr int SETS = FMT == SF_MX4 ? (D == 384 && V != 1 ? 8 : D == 1024 ? 2 : 4)
                                             : (D == 384 ? 4 : D == 768 ? 2 : 1);
   static constexpr int NW0 = 256 / (SETS * 32) > 0 ? 256 / (SETS * 32) : 1;
   static constexpr int NW = NW0 > 4 ? 4 : NW0;
-  static constexpr int DEPTH = FMT == SF_MX4 ? 3 : 2;
+  static constexpr int DEPTH0 = FMT == SF_MX4 ? 3 : 2;
+  static constexpr int DEPTH = V == 2 ? DEPTH0 + 1 : (V == 3 && DEPTH0 > 2 ? DEPTH0 - 1 : DEPTH0);
   static constexpr int QPB = SETS * 32 * NW;                      // queries per workgroup
   static constexpr int STW = 512;                                 // staged candidates per wave
   static constexpr int STAGE = STW * 10;
+  // the LDS-landing form (LAND): each wave's sub-tiles arrive by LDS-DMA into a private ring of
+  // LDEPTH slots (no loop-carried fragment registers); sized for 2 workgroups of 2 waves (int8 /
+  // MX-fp4 768) or 4 of one wave (MX-fp4 384) per CU
+  static constexpr int SLOT = (SDim<FMT, D>::REC + 1023) / 1024 * 1024;
+  static constexpr int LDEPTH = FMT == SF_MX4 && D == 384 ? 4 : 2;
+  static constexpr bool LAND_OK = D == 384 || (D == 768 && FMT == SF_MX4);
   static_assert(SETS * NKS * 4 <= 192, "resident query operands");
   static_assert(NW >= 1 && NW <= 4, "waves per workgroup");
 };
@@ -81,13 +89,6 @@ __device__ __forceinline__ void static_for(F&& f) {
     f(std::integral_constant<int, I>());
     static_for<I + 1, N>(f);
   }
-}
-
-__device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b), c); }
-__device__ __forceinline__ int max16i(const i32x16s& v) {   // v_max3_i32 chains
-  const int a = max3i(v[0], v[1], v[2]), b = max3i(v[3], v[4], v[5]), c = max3i(v[6], v[7], v[8]);
-  const int d = max3i(v[9], v[10], v[11]), e = max3i(v[12], v[13], v[14]);
-  return max3i(max3i(a, b, c), max3i(d, e, v[15]), v[15]);
 }
 
 __device__ __forceinline__ float max16(const float (&v)[16]) {
@@ -106,7 +107,14 @@ __device__ __forceinline__ float max16(const float (&v)[16]) {
 // qsc = its scale record [NQ][2 NSC] dwords); thr[q]: emit a row iff its estimate >= thr (int8:
 // (q8 . x8) * sx >= thr, thr already divided by the query's scale; MX-fp4: the scaled dot).
 // Workgroup lb = (row block rb, query block qb); cand_n must be zeroed by the caller.
-template <int FMT, int D, int V>
+// ABL (timing ablations, wrong results): 1 = no emission test (the accumulators kept live),
+// 2 = no sub-tile loads after the prologue (the first DEPTH sub-tiles re-used).
+// LAND: sub-tiles land in LDS by LDS-DMA (a per-wave ring, counted vmcnt, no barriers) and each is
+// read into ONE set of fragment registers right before its MFMAs -- the register ring's
+// loop-carried fragments made hipcc copy freshly loaded registers at the back edge, which waits
+// for the loads and serialised the prefetch (MX-fp4 scan 5.1 ms with loads vs 3.35 without,
+// profiles/r5_scan/).
+template <int FMT, int D, int V, int ABL = 0, int LAND = 0>
 __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_kernel(
     const uint8_t* __restrict__ img, int n_valid, int rows_per_blk, const uint8_t* __restrict__ Q,
     const uint32_t* __restrict__ qsc, int NQ, int n_qblk, int xcd, const float* __restrict__ thr_in,
@@ -169,6 +177,8 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
       }
     }
     nst = 0;
+    // (vmcnt counts these stores too: the landing ring's counted waits assume only DMAs pending)
+    if constexpr (LAND) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
 
   // ---- the sub-tile ring: fragments (+ row scales / block scales) of DEPTH sub-tiles ----
@@ -219,34 +229,21 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
     }
   };
 
-  // int8 pre-test: max_r acc[r] sx[r] <= imax * (imax >= 0 ? max sx : min sx) over this lane's 16
-  // rows -- 8 integer max3 + 4 ops per set instead of 16 cvt + 16 mul + 8 max3 (the VALU that
-  // competed with the MFMA issue); a block that passes it is re-tested exactly row by row below
-  auto block_raw = [&](auto dc, auto sc) {
-    constexpr int d = decltype(dc)::value, s = decltype(sc)::value;
-    i32x16s acc = {};
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks)
-      acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(fk[d][ks], qf[s][ks], acc, 0, 0, 0);
-    return acc;
-  };
-
+  // (a conservative integer pre-test -- max_r acc[r] times the largest of the 16 row scales --
+  // was measured 1.8x slower: the row scales spread +-30 %, so it let through most blocks and
+  // their exact re-test recomputed the MFMAs; profiles/r5_scan/)
   auto process = [&](auto dc, int i) {
     constexpr int d = decltype(dc)::value;
     const int row0 = (g0 + i) * 32 + 4 * h;   // + (r & 3) + 8 (r >> 2)
     uint32_t hm = 0;                          // sets with a hit in this lane
-    if constexpr (FMT == SF_I8) {
-      float smax = frs[d][0][0], smin = smax;
-#pragma unroll
-      for (int r = 1; r < 16; ++r) {
-        smax = fmaxf(smax, frs[d][r >> 2][r & 3]);
-        smin = fminf(smin, frs[d][r >> 2][r & 3]);
-      }
+    if constexpr (ABL == 1) {
       static_for<0, SETS>([&](auto sc) {
-        constexpr int s = decltype(sc)::value;
-        const int im = max16i(block_raw(dc, sc));
-        hm |= ((float)im * (im >= 0 ? smax : smin) >= thr[s] ? 1u : 0u) << s;
+        float v[16];
+        block(dc, sc, v);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) asm volatile("" ::"v"(v[r]));
       });
+      return;
     } else {
       static_for<0, SETS>([&](auto sc) {
         constexpr int s = decltype(sc)::value;
@@ -282,6 +279,56 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
     }
   };
 
+  if constexpr (LAND) {
+    static_assert(G::LAND_OK, "landing ring sized for this form");
+    constexpr int SLOT = G::SLOT, LD = G::LDEPTH;
+    constexpr int NDMA = NKS + (FMT == SF_I8 ? 1 : NSC);   // DMA instructions per sub-tile
+    char* ring = smem + G::NW * G::STAGE + wave * (LD * SLOT);
+    // (asm DMAs: the builtin's LDS-DMA made hipcc wait vmcnt(0) before every ds_read of the ring,
+    // as it cannot tell the slots apart -- that serialised the prefetch again)
+    auto dma = [&](int i, int slot) {   // sub-tile i (past the end: the last again) into slot
+      const uint8_t* r = rec0 + (size_t)min(i, ns - 1) * REC;
+      const uint32_t dst = lds_addr(ring) + slot * SLOT;
+      if constexpr (FMT == SF_I8) dma2_asm(r + 2 * lane, dst);   // the 128-byte row-scale header
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) dma16_asm(r + S::HDR + 1024 * ks + 16 * lane, dst + S::HDR + 1024 * ks);
+      if constexpr (FMT == SF_MX4) {
+#pragma unroll
+        for (int j = 0; j < NSC; ++j) dma4_asm(r + S::FRAG + 256 * j + 4 * lane, dst + S::FRAG + 256 * j);
+      }
+    };
+    auto fetch = [&](int slot) {
+      const char* src = ring + slot * SLOT;
+      if constexpr (FMT == SF_I8) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) frs[0][c] = *reinterpret_cast<const f32x4*>(src + 64 * h + 16 * c);
+      }
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks)
+        fk[0][ks] = *reinterpret_cast<const i32x4s*>(src + S::HDR + 1024 * ks + 16 * lane);
+      if constexpr (FMT == SF_MX4) {
+#pragma unroll
+        for (int j = 0; j < NSC; ++j)
+          fsc[0][j] = *reinterpret_cast<const uint32_t*>(src + S::FRAG + 256 * j + 4 * lane);
+      }
+    };
+    // the queries (and thresholds) landed before any DMA -- as the builtin, so that hipcc's own
+    // wait bookkeeping sees it (else it keeps the query loads "pending" into the loop and its
+    // counted waits for them drain the DMAs every sub-tile)
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) expcnt(7) lgkmcnt(15)
+    for (int d = 0; d < LD; ++d) dma(d, d);
+    for (int i = 0; i < ns; ++i) {
+      const int slot = i % LD;
+      // sub-tile i landed: only the LD - 1 younger sub-tiles' DMAs may still be in flight
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NDMA * (LD - 1)) : "memory");
+      fetch(slot);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // (slot read: refill it)
+      if (ABL != 2) dma(i + LD, slot);
+      process(std::integral_constant<int, 0>(), i);
+    }
+    if (nst) flush();
+    return;
+  }
   // prologue: DEPTH sub-tiles in flight, then use one / refill its slot
   static_for<0, DEPTH>([&](auto dc) { load(dc, decltype(dc)::value); });
   // (the last round may run past ns: those slots re-read the last sub-tile and emit nothing, as
@@ -290,7 +337,7 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
     static_for<0, DEPTH>([&](auto dc) {
       constexpr int d = decltype(dc)::value;
       process(dc, i0 + d);
-      load(dc, i0 + d + DEPTH);
+      if (ABL != 2) load(dc, i0 + d + DEPTH);
     });
   }
   if (nst) flush();
@@ -521,9 +568,43 @@ __global__ __launch_bounds__(256) void append_rows_kernel(const __bf16* __restri
   if (b4) raise_bounds2(b4, e4, n4);
 }
 
+// Probe of one v_mfma_scale_f32_32x32x64_f8f6f4 (tests: the operand bit layouts of the f8f6f4
+// formats): a / b [64 lanes][8] dwords, sa / sb [64] e8m0 scale bytes (one dword each, byte 0),
+// out [64][16] = the accumulator.  F: 0 fp8 e4m3, 2 fp6 e2m3, 3 fp6 e3m2, 4 fp4 e2m1.
+template <int F>
+__global__ __launch_bounds__(64) void mfma_f8f6f4_probe_kernel(const int* __restrict__ a,
+                                                              const int* __restrict__ b,
+                                                              const int* __restrict__ sa,
+                                                              const int* __restrict__ sb,
+                                                              float* __restrict__ out) {
+  const int l = threadIdx.x;
+  i32x8s av, bv;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    av[i] = a[l * 8 + i];
+    bv[i] = b[l * 8 + i];
+  }
+  f32x16s acc = {};
+  acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(av, bv, acc, F, F, 0, sa[l], 0, sb[l]);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) out[l * 16 + r] = acc[r];
+}
+
 }  // namespace symb
 
 using namespace symb;
+
+int symb_mfma_f8f6f4_probe(const int* a, const int* b, const int* sa, const int* sb, float* out,
+                           int fmt, hipStream_t st) {
+#define L(F_) hipLaunchKernelGGL(mfma_f8f6f4_probe_kernel<F_>, dim3(1), dim3(64), 0, st, a, b, sa, sb, out)
+  if (fmt == 0) L(0);
+  else if (fmt == 2) L(2);
+  else if (fmt == 3) L(3);
+  else if (fmt == 4) L(4);
+  else return -1;
+#undef L
+  return (int)hipGetLastError();
+}
 
 // bytes per 32-row sub-tile of the stream image (form 0 = int8, 1 = MX-fp4); 0 = unsupported
 int symb_stream_rec_bytes(int dim, int form) {
@@ -533,11 +614,19 @@ int symb_stream_rec_bytes(int dim, int form) {
   return 0;
 }
 
-// the MX-fp4 384 form (symb_stream_config): 0 = 256 queries per wave, 1 = 128 per wave x 2
-static int g_stream_mx4_v = 0;
-int symb_stream_config(int mx4_variant) {
-  if (mx4_variant != 0 && mx4_variant != 1) return -1;
+// scan forms (symb_stream_config, A/B): variant 0 = default, 1 = MX-fp4 384 with 128 queries per
+// wave x 2 waves, 2 / 3 = one sub-tile deeper / shallower in flight (register ring, D = 384);
+// abl: the kernel's timing ablations (ABL above; wrong results); land: the LDS-landing form where
+// it is sized (int8 / MX-fp4 384, MX-fp4 768; variant 0)
+static int g_stream_mx4_v = 0, g_stream_i8_v = 0, g_stream_abl = 0, g_stream_land = 1;
+int symb_stream_config(int mx4_variant, int i8_variant, int abl, int land) {
+  if (mx4_variant < 0 || mx4_variant > 3 || (i8_variant != 0 && i8_variant != 2 && i8_variant != 3) ||
+      abl < 0 || abl > 2 || land < 0 || land > 1)
+    return -1;
   g_stream_mx4_v = mx4_variant;
+  g_stream_i8_v = i8_variant;
+  g_stream_abl = abl;
+  g_stream_land = land;
   return 0;
 }
 
@@ -550,7 +639,7 @@ int symb_stream_geometry(int dim, int form, int* qpb, int* wgs_per_cu) {
     return 0;                                        \
   } while (0)
   if (dim == 384) {
-    if (form && g_stream_mx4_v) G_(SF_MX4, 384, 1);
+    if (form && g_stream_mx4_v == 1) G_(SF_MX4, 384, 1);
     if (form) G_(SF_MX4, 384, 0);
     G_(SF_I8, 384, 0);
   }
@@ -566,15 +655,16 @@ int symb_stream_geometry(int dim, int form, int* qpb, int* wgs_per_cu) {
   return -1;
 }
 
-template <int F, int D, int V>
+template <int F, int D, int V, int ABL = 0, int LAND = 0>
 static int launch_stream(const void* img, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                          const void* qsc, int NQ, const float* thr, float* cand_s, int* cand_i,
                          int* cand_n, int cap, int xcd, hipStream_t st, const int* skip,
                          const int* gate, int gate_want, int* runs) {
   using G = SGeo<F, D, V>;
   const int n_qblk = (NQ + G::QPB - 1) / G::QPB;
-  constexpr int lds = G::STAGE * G::NW;
-  hipLaunchKernelGGL((scan_stream_kernel<F, D, V>), dim3(n_rblk * n_qblk), dim3(64 * G::NW), lds,
+  constexpr int lds = G::STAGE * G::NW + (LAND ? G::NW * G::LDEPTH * G::SLOT : 0);
+  if (lds > 64 * 1024) set_max_lds<scan_stream_kernel<F, D, V, ABL, LAND>>(lds);
+  hipLaunchKernelGGL((scan_stream_kernel<F, D, V, ABL, LAND>), dim3(n_rblk * n_qblk), dim3(64 * G::NW), lds,
                      st, (const uint8_t*)img, n_valid, rows_per_blk, (const uint8_t*)Q,
                      (const uint32_t*)qsc, NQ, n_qblk, xcd, thr, cand_s, cand_i, cand_n, cap, skip,
                      gate, gate_want, runs);
@@ -605,12 +695,36 @@ int symb_index_scan_stream(const void* img, int n_valid, int alloc_rows, int row
 #define L(F, D_, V_) launch_stream<F, D_, V_>(img, n_valid, rows_per_blk, n_rblk, Q, qsc, NQ, thr, \
                                               cand_s, cand_i, cand_n, cap, xcd, st, skip, gate,   \
                                               gate_want, runs)
+  const bool land = g_stream_land && (form == 0 ? g_stream_i8_v == 0 : g_stream_mx4_v == 0);
+#define LA(F, D_, A_, L_) launch_stream<F, D_, 0, A_, L_>(img, n_valid, rows_per_blk, n_rblk, Q, qsc, \
+                                                          NQ, thr, cand_s, cand_i, cand_n, cap, xcd, \
+                                                          st, skip, gate, gate_want, runs)
+  if (dim == 768 && form == 1 && land) return LA(SF_MX4, 768, 0, 1);
   if (dim == 384) {
-    if (form && g_stream_mx4_v) return L(SF_MX4, 384, 1);
-    return form ? L(SF_MX4, 384, 0) : L(SF_I8, 384, 0);
+    if (g_stream_abl == 1)
+      return form ? (land ? LA(SF_MX4, 384, 1, 1) : LA(SF_MX4, 384, 1, 0))
+                  : (land ? LA(SF_I8, 384, 1, 1) : LA(SF_I8, 384, 1, 0));
+    if (g_stream_abl == 2)
+      return form ? (land ? LA(SF_MX4, 384, 2, 1) : LA(SF_MX4, 384, 2, 0))
+                  : (land ? LA(SF_I8, 384, 2, 1) : LA(SF_I8, 384, 2, 0));
+    if (land) return form ? LA(SF_MX4, 384, 0, 1) : LA(SF_I8, 384, 0, 1);
+    if (form) {
+      switch (g_stream_mx4_v) {
+        case 1: return L(SF_MX4, 384, 1);
+        case 2: return L(SF_MX4, 384, 2);
+        case 3: return L(SF_MX4, 384, 3);
+        default: return L(SF_MX4, 384, 0);
+      }
+    }
+    switch (g_stream_i8_v) {
+      case 2: return L(SF_I8, 384, 2);
+      case 3: return L(SF_I8, 384, 3);
+      default: return L(SF_I8, 384, 0);
+    }
   }
   if (dim == 768) return form ? L(SF_MX4, 768, 0) : L(SF_I8, 768, 0);
   return form ? L(SF_MX4, 1024, 0) : L(SF_I8, 1024, 0);
+#undef LA
 #undef L
 }
 
