@@ -7,7 +7,8 @@ the target of timing A/Bs and rocprofv3 --pmc passes (benchmarks/pmc_kernel.py -
 
 The shard's scan is the stream scan (index_stream.hip) unless SYMB_PRUNE_STREAM=0 (the round-4
 LDS-ring scan, index_i8.hip).  --tier mx4 times the MX-fp4 first tier on the same block grid with
-the thresholds the tier choice computed (--queries self: stored rows as queries, at the headline's fp4 threshold 0.74).
+the thresholds the tier choice computed (--queries self: stored rows as queries; near: near-duplicate queries, whose sets the centroid
+test skips; both at the headline's fp4 threshold 0.74).
 """
 from __future__ import annotations
 
@@ -30,11 +31,11 @@ def main() -> None:
     ap.add_argument("--corpus", default="random")
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--tier", choices=["i8", "mx4"], default="i8")
-    ap.add_argument("--queries", choices=["heldout", "self"], default="heldout")
+    ap.add_argument("--queries", choices=["heldout", "self", "near"], default="heldout")
     ap.add_argument("--variant", type=int, default=-1, help="stream MX-fp4 form (stream_config)")
     ap.add_argument("--ab", default="",
                     help="stream forms timed in one process, interleaved: comma list of "
-                         "mx4variant:i8variant:ablation[:land] (e.g. 0:0:0:1,0:0:0:0,0:0:1)")
+                         "mx4variant:i8variant:ablation[:land[:centroid]] (e.g. 0:0:0:1:1,0:0:0:1:0)")
     ap.add_argument("--rounds", type=int, default=3)
     a = ap.parse_args()
     from codename_symbiont_amd.index.shard import STREAM_SUB, HbmIndexShard
@@ -53,6 +54,11 @@ def main() -> None:
     if a.queries == "self":
         idx = torch.randint(0, a.rows, (a.nq,), device="cuda")
         q = shard.rows[idx].clone()
+    elif a.queries == "near":   # near-duplicate queries (cos ~0.99), like the headline's embeddings
+        g = torch.Generator(device="cuda").manual_seed(7)
+        c = torch.nn.functional.normalize(torch.randn(a.dim, device="cuda", generator=g), dim=0)
+        q = torch.nn.functional.normalize(
+            c + 0.1 * torch.randn(a.nq, a.dim, device="cuda", generator=g) / a.dim ** 0.5, dim=-1).bfloat16()
     else:
         q = gen.unit(a.nq, seed=7).bfloat16()
     shard.mq_stats = True
@@ -64,7 +70,7 @@ def main() -> None:
     m4 = P["m4"]
     if a.tier == "mx4" and m4 is None:
         raise SystemExit("no MX-fp4 tier on this shard")
-    if a.tier == "mx4" and a.queries == "self":
+    if a.tier == "mx4" and a.queries in ("self", "near"):
         # the headline's batches take the fp4 tier because their k-th scores sit near 0.99 (fresh
         # near-duplicate embeddings): T - margin4 ~ 0.74.  Stored random rows as queries have
         # k-th scores ~0.2 (only the row itself scores high), for which the tier is never chosen;
@@ -80,7 +86,8 @@ def main() -> None:
                                     P["rows_per_blk"], P["n_rblk"], m4["q4"].data_ptr(),
                                     m4["qs4"].data_ptr(), a.nq, m4["thr4"].data_ptr(),
                                     P["cs"].data_ptr(), P["ci"].data_ptr(), P["cnt"].data_ptr(),
-                                    P["cap"], 1, st, dim=a.dim, form=1)
+                                    P["cap"], 1, st, dim=a.dim, form=1,
+                                    **(shard._cent_args(m4) if cent[0] else {}))
             else:
                 h.index_scan_i8(shard.rows_mx4.data_ptr(), shard.sc_mx4.data_ptr(), n,
                                 shard.rows_mx4.shape[0], P["rows_per_blk"], P["n_rblk"],
@@ -108,11 +115,13 @@ def main() -> None:
     else:
         nbytes, kernel = shard.rows_i8.shape[1] + 4, "ldsring-" + ("split" if heavy else "i8")
     forms = [tuple(int(x) for x in f.split(":")) for f in a.ab.split(",")] if a.ab else [None]
+    cent = [True]   # the MX-fp4 centroid test (a 5th form field: 0 = off)
     times = {f: [] for f in forms}
     for _ in range(a.rounds if a.ab else 1):
         for f in forms:
             if f is not None:
-                h.stream_config(*f)
+                h.stream_config(*f[:4])
+                cent[0] = len(f) < 5 or bool(f[4])
             scan()
             torch.cuda.synchronize()
             t0 = time.perf_counter()

@@ -1,4 +1,5 @@
-"""What runs between consecutive int8 scans of the headline (rocprofv3 kernel trace CSV): for the
+"""What runs between consecutive full-shard first-pass scans (the stream scan, or the round-4
+LDS-ring int8 / MX-fp4 scan) of the headline (rocprofv3 kernel trace CSV): for the
 gaps of the last steps, every kernel that overlaps the gap, its queue, how much of the gap it
 covers, and the gap time with NO kernel running (idle).
 
@@ -26,7 +27,8 @@ def main():
           for r in rows]
     ks.sort()
     # the full-shard scans (a gated launch that returned at once is not one)
-    scans = [k for k in ks if k[2] == "index_scan_i8_kernel" and k[1] - k[0] > 200_000]
+    scans = [k for k in ks if k[2] in ("index_scan_i8_kernel", "scan_stream_kernel")
+             and k[1] - k[0] > 200_000]
     gaps = list(zip(scans[:-1], scans[1:]))[-a.steps:]
     agg = collections.defaultdict(float)
     tot_gap = tot_idle = 0.0

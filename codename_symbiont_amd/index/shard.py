@@ -1247,12 +1247,34 @@ class HbmIndexShard:
                          thr4.data_ptr(), nvf.data_ptr(), st, ld=ld, tile_stride=4, tail_ld=ld,
                          nv_zeroed=True)
             ctx["mx4"] = dict(q4=q4, qs4=qs4, thr4=thr4, nv=nvf)
+            if self.img_mx4 is not None and self.mx4_centroid:
+                # the query-side bound (index_stream.hip mx4_centroids_kernel): per 32-query set
+                # the centroid image and radius R, so the scan skips a set's MFMAs on sub-tiles
+                # where c~ . x~ + R X4 stays below every threshold of the set
+                n_sets = -(-NQ // 32)
+                c4 = torch.empty(n_sets, self.dim // 2, dtype=torch.uint8, device=dev)
+                cqs = torch.empty(n_sets, qs4.shape[1], dtype=torch.int32, device=dev)
+                cR = torch.empty(n_sets, dtype=torch.float32, device=dev)
+                h.mx4_centroids(q4.data_ptr(), qs4.data_ptr(), NQ, self.dim, c4.data_ptr(),
+                                cqs.data_ptr(), cR.data_ptr(), st)
+                ctx["mx4"].update(c4=c4, cqs=cqs, cR=cR)
         return ctx
 
     # the search workspace's flag slots (_pruned_begin): route "every block dense", the MX-fp4
     # tier's "not viable" flag, the sample's and the final select's overflow flags, and a slot
     # the dense selects may write (they never overflow)
     WS_DENSE, WS_NV, WS_SAMPLE_OVF, WS_OVF, WS_SCRATCH, WS_FLAGS = 0, 1, 2, 3, 4, 8
+
+    # the MX-fp4 tier's query-side centroid test (SYMB_MX4_CENTROID=0: off, A/B)
+    mx4_centroid = os.environ.get("SYMB_MX4_CENTROID", "1") not in ("", "0")
+
+    def _cent_args(self, m4) -> dict:
+        """index_scan_stream's centroid-test arguments for an MX-fp4 query context (none when the
+        context has no centroids)."""
+        if m4 is None or "c4" not in m4:
+            return {}
+        return dict(cent4=m4["c4"].data_ptr(), centqs=m4["cqs"].data_ptr(),
+                    centR=m4["cR"].data_ptr(), bounds4=self.mx4_bounds.data_ptr())
 
     def _i8_geometry(self, n: int, NQ: int, n_cus: int):
         """(rsplit, rows_per_blk, n_rblk) of the int8 scan over n rows: ~one workgroup per CU
@@ -1336,8 +1358,9 @@ class HbmIndexShard:
         skip = blk[2 + n_rblk:].data_ptr() if self.prune_route else 0
         m4 = ctx.get("mx4")
         if m4 is not None:   # both tiers enqueued, gated on the flag: exactly one runs
-            for t in ("q4", "qs4", "thr4"):
-                m4[t].record_stream(cur)
+            for t in ("q4", "qs4", "thr4", "c4", "cqs", "cR"):
+                if t in m4:
+                    m4[t].record_stream(cur)
         gate, want = (m4["nv"].data_ptr(), 1) if m4 is not None else (0, 0)
         if self.img_i8 is not None and not ctx["heavy"]:   # the stream scan (index_stream.hip)
             h.index_scan_stream(self.img_i8.data_ptr(), n, self.img_i8.shape[0] * STREAM_SUB,
@@ -1364,7 +1387,7 @@ class HbmIndexShard:
                                 NQ, m4["thr4"].data_ptr(), cs.data_ptr(), ci.data_ptr(),
                                 cnt.data_ptr(), cap, self.scan_xcd, st, skip=skip, dim=self.dim,
                                 form=1, gate=m4["nv"].data_ptr(), gate_want=0, zero_cnt=0,
-                                runs=runs)
+                                runs=runs, **self._cent_args(m4))
         elif m4 is not None:
             h.index_scan_i8(self.rows_mx4.data_ptr(), self.sc_mx4.data_ptr(), n,
                             self.rows_mx4.shape[0], rows_per_blk, n_rblk, m4["q4"].data_ptr(), NQ,

@@ -94,7 +94,10 @@ int symb_index_scan_stream(const void* img, int n_valid, int alloc_rows, int row
                            int n_rblk, const void* Q, const void* qsc, int NQ, const float* thr,
                            float* cand_s, int* cand_i, int* cand_n, int cap, int xcd,
                            hipStream_t st, const int* skip, int dim, int form, const int* gate,
-                           int gate_want, int zero_cnt, int* runs);
+                           int gate_want, int zero_cnt, int* runs, const void* cent4,
+                           const void* centqs, const float* centR, const float* bounds4);
+int symb_mx4_centroids(const void* Xq, const void* QS, int NQ, int dim, void* C4, void* CS,
+                       float* R, hipStream_t st);
 int symb_append_rows(const void* src, int n, int dim, void* rows, int r0, void* img8, float* b8,
                      void* img4, float* b4, hipStream_t st);
 int symb_dense_scores(const void* X, int dim, const int* rows, int n_list, int ts, int div,
@@ -497,18 +500,27 @@ PYBIND11_MODULE(_hip, m) {
   m.def("index_scan_stream", [](uptr img, int n_valid, int alloc_rows, int rows_per_blk, int n_rblk,
                                 uptr Q, uptr qsc, int NQ, uptr thr, uptr cand_s, uptr cand_i,
                                 uptr cand_n, int cap, int xcd, uptr st, uptr skip, int dim,
-                                int form, uptr gate, int gate_want, int zero_cnt, uptr runs) {
+                                int form, uptr gate, int gate_want, int zero_cnt, uptr runs,
+                                uptr cent4, uptr centqs, uptr centR, uptr bounds4) {
     check(symb_index_scan_stream(P<void>(img), n_valid, alloc_rows, rows_per_blk, n_rblk,
                                  P<void>(Q), P<void>(qsc), NQ, P<const float>(thr),
                                  P<float>(cand_s), P<int>(cand_i), P<int>(cand_n), cap, xcd, S(st),
                                  P<const int>(skip), dim, form, P<const int>(gate), gate_want,
-                                 zero_cnt, P<int>(runs)),
+                                 zero_cnt, P<int>(runs), P<void>(cent4), P<void>(centqs),
+                                 P<const float>(centR), P<const float>(bounds4)),
           "index_scan_stream");
   }, py::arg("img"), py::arg("n_valid"), py::arg("alloc_rows"), py::arg("rows_per_blk"),
      py::arg("n_rblk"), py::arg("Q"), py::arg("qsc"), py::arg("NQ"), py::arg("thr"),
      py::arg("cand_s"), py::arg("cand_i"), py::arg("cand_n"), py::arg("cap"), py::arg("xcd"),
      py::arg("stream"), py::arg("skip") = 0, py::arg("dim") = 384, py::arg("form") = 0,
-     py::arg("gate") = 0, py::arg("gate_want") = 0, py::arg("zero_cnt") = 1, py::arg("runs") = 0);
+     py::arg("gate") = 0, py::arg("gate_want") = 0, py::arg("zero_cnt") = 1, py::arg("runs") = 0,
+     py::arg("cent4") = 0, py::arg("centqs") = 0, py::arg("centR") = 0, py::arg("bounds4") = 0);
+  m.def("mx4_centroids", [](uptr Xq, uptr QS, int NQ, int dim, uptr C4, uptr CS, uptr R, uptr st) {
+    check(symb_mx4_centroids(P<void>(Xq), P<void>(QS), NQ, dim, P<void>(C4), P<void>(CS),
+                             P<float>(R), S(st)),
+          "mx4_centroids");
+  }, py::arg("Xq"), py::arg("QS"), py::arg("NQ"), py::arg("dim"), py::arg("C4"), py::arg("CS"),
+     py::arg("R"), py::arg("stream"));
   m.def("append_rows", [](uptr src, int n, int dim, uptr rows, int r0, uptr img8, uptr b8,
                           uptr img4, uptr b4, uptr st) {
     check(symb_append_rows(P<void>(src), n, dim, P<void>(rows), r0, P<void>(img8), P<float>(b8),

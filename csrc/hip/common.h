@@ -114,7 +114,7 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
 }
 
-// LDS-DMA issued as inline asm (16 / 4 / 2 bytes per lane; lane l lands at lds + size * l, lds a
+// LDS-DMA issued as inline asm (16 / 4 bytes per lane; lane l lands at lds + size * l, lds a
 // wave-uniform LDS byte address).  hipcc neither counts these loads nor inserts its conservative
 // "any pending LDS-DMA may alias this ds_read" vmcnt(0): the caller retires them with its own
 // counted s_waitcnt vmcnt before reading the data (same wave; other waves also need a barrier).
@@ -130,7 +130,6 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   }
 SYMB_DMA_ASM(dma16_asm, "global_load_lds_dwordx4")
 SYMB_DMA_ASM(dma4_asm, "global_load_lds_dword")
-SYMB_DMA_ASM(dma2_asm, "global_load_lds_ushort")
 #undef SYMB_DMA_ASM
 
 // Raise a kernel's dynamic-LDS limit (hipFuncAttributeMaxDynamicSharedMemorySize) before its

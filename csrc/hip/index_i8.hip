@@ -1247,6 +1247,24 @@ __global__ __launch_bounds__(256) void prune_route_kernel(
   }
 }
 
+// What each query would still emit in the int8 scan after the flooded blocks leave it: one wave per
+// query over the blocks (coalesced); any query above `limit` ORs *dense (every block then goes to
+// the bf16 scan).  (This loop ran inside the single-workgroup final kernel, one thread per query
+// striding its own row of est: 121 us per search at 1024 blocks, profiles/r5_step/.)
+__global__ __launch_bounds__(256) void prune_route_sum_kernel(int NQ, int n_rblk,
+                                                              const float* __restrict__ est,
+                                                              const int* __restrict__ blkmax,
+                                                              float blk_limit, float limit,
+                                                              int* __restrict__ dense) {
+  const int lane = threadIdx.x & 63, q = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= NQ) return;
+  const float* e = est + (size_t)q * n_rblk;
+  float s = 0.f;
+  for (int b = lane; b < n_rblk; b += 64) s += __int_as_float(blkmax[b]) > blk_limit ? 0.f : e[b];
+  s = wave_sum(s);
+  if (lane == 0 && s > limit) atomicOr(dense, 1);
+}
+
 // One workgroup: the per-block decision of prune_route_kernel.  blk: [0] = listed blocks, [1] =
 // n_rblk, [2 .. 2 + n_rblk) = the listed blocks in order, [2 + n_rblk .. 2 + 2 n_rblk) = skip
 // flags of the int8 scan.  *dense ends as 1 iff every block went to the bf16 scan.
@@ -1259,14 +1277,7 @@ __global__ __launch_bounds__(1024) void prune_route_final_kernel(
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   if (tid == 0) all = *dense;
   for (int b = tid; b < n_rblk; b += 1024) flag[b] = __int_as_float(blkmax[b]) > blk_limit;
-  __syncthreads();
-  for (int q = tid; q < NQ; q += 1024) {   // what each query would still emit in the int8 scan
-    const float* e = est + (size_t)q * n_rblk;
-    float s = 0.f;
-    for (int b = 0; b < n_rblk; ++b) s += flag[b] ? 0.f : e[b];
-    if (s > limit) atomicOr(&all, 1);
-  }
-  __syncthreads();
+  __syncthreads();   // (all: prune_route_sum_kernel's verdict, read above)
   // listed blocks in order: one bin per thread (n_rblk <= 1024), ballot prefix per wave
   const int f = tid < n_rblk && (all || flag[tid]);
   const unsigned long long bal = __ballot(f);
@@ -1591,6 +1602,8 @@ int symb_prune_route(int NQ, const float* pre_s, const float* tail_s, int k, flo
                      k, thr_margin, sq, margin, thr0, cs_p, ci_p, cnt_p, cap_p, tshift,
                      rows_per_blk, n_rblk, T, thr, dense, est, blkmax,
                      RouteTail{tail_cs, tail_ci, tail_cnt, tail_cap, tail_off, tail_ld});
+  hipLaunchKernelGGL(prune_route_sum_kernel, dim3((NQ + 3) / 4), dim3(256), 0, st, NQ, n_rblk, est,
+                     blkmax, blk_limit, limit, dense);
   hipLaunchKernelGGL(prune_route_final_kernel, dim3(1), dim3(1024), 0, st, NQ, n_rblk, est, blkmax,
                      blk_limit, limit, max_list, dense, blk);
   return (int)hipGetLastError();

@@ -75,7 +75,8 @@ struct SGeo {
   // the LDS-landing form (LAND): each wave's sub-tiles arrive by LDS-DMA into a private ring of
   // LDEPTH slots (no loop-carried fragment registers); sized for 2 workgroups of 2 waves (int8 /
   // MX-fp4 768) or 4 of one wave (MX-fp4 384) per CU
-  static constexpr int SLOT = (SDim<FMT, D>::REC + 1023) / 1024 * 1024;
+  static constexpr int LHDR = FMT == SF_I8 ? 256 : 0;   // the header's LDS bytes (DMA: 4 B x 64 lanes)
+  static constexpr int SLOT = (SDim<FMT, D>::REC - SDim<FMT, D>::HDR + LHDR + 1023) / 1024 * 1024;
   static constexpr int LDEPTH = FMT == SF_MX4 && D == 384 ? 4 : 2;
   static constexpr bool LAND_OK = D == 384 || (D == 768 && FMT == SF_MX4);
   static_assert(SETS * NKS * 4 <= 192, "resident query operands");
@@ -120,7 +121,8 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
     const uint32_t* __restrict__ qsc, int NQ, int n_qblk, int xcd, const float* __restrict__ thr_in,
     float* __restrict__ cand_s, int* __restrict__ cand_i, int* __restrict__ cand_n, int cap,
     const int* __restrict__ skip, const int* __restrict__ gate, int gate_want,
-    int* __restrict__ runs) {
+    int* __restrict__ runs, const uint8_t* __restrict__ cent4, const uint32_t* __restrict__ centqs,
+    const float* __restrict__ centR, const float* __restrict__ bounds4) {
   using S = SDim<FMT, D>;
   using G = SGeo<FMT, D, V>;
   constexpr int NKS = S::NKS, NSC = S::NSC ? S::NSC : 1, REC = S::REC;
@@ -159,6 +161,36 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
         qs[s][j] = 0u;
     }
     thr[s] = q < NQ ? thr_in[q] : INFINITY;
+  }
+
+  // ---- the centroid test (MX-fp4, optional; mx4_centroids_kernel): one extra B operand holding
+  //      the centroids of the wave's SETS query sets (lane j: centroid j), each set's bound
+  //      R_s X4 and smallest threshold.  A sub-tile whose rows all satisfy
+  //      c~_s . x~ + R_s X4 < min_q thr[q] cannot emit for set s, whose MFMAs are then skipped --
+  //      near-duplicate query batches (the headline's) skip every set on almost every sub-tile ----
+  const bool cent_on = FMT == SF_MX4 && cent4 != nullptr;
+  i32x4s cf[FMT == SF_MX4 ? NKS : 1];
+  uint32_t cqs[NSC];
+  float cbound[SETS], tmin[SETS];
+  if constexpr (FMT == SF_MX4) {
+    if (cent_on) {
+      const int gs0 = (qb * G::NW + wave) * SETS, n_sets = (NQ + 31) / 32;
+      const int gs = min(gs0 + min(lane & 31, SETS - 1), n_sets - 1);
+      const uint8_t* cp = cent4 + (size_t)gs * S::RB + 16 * h;
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) cf[ks] = *reinterpret_cast<const i32x4s*>(cp + 32 * ks);
+#pragma unroll
+      for (int j = 0; j < NSC; ++j) cqs[j] = centqs[(size_t)gs * 2 * NSC + h * NSC + j];
+      const float x4 = bounds4[1];
+#pragma unroll
+      for (int s = 0; s < SETS; ++s) {
+        cbound[s] = centR[min(gs0 + s, n_sets - 1)] * x4 * 1.0001f + 1e-4f;
+        float t = thr[s];
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) t = fminf(t, __shfl_xor(t, o));
+        tmin[s] = t;
+      }
+    }
   }
 
   // ---- per-wave candidate stage (LDS) ----
@@ -236,8 +268,36 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
     constexpr int d = decltype(dc)::value;
     const int row0 = (g0 + i) * 32 + 4 * h;   // + (r & 3) + 8 (r >> 2)
     uint32_t hm = 0;                          // sets with a hit in this lane
+    uint32_t pass = ~0u;                      // sets the centroid test could not rule out
+    if constexpr (FMT == SF_MX4) {
+      if (cent_on) {
+        f32x16s acc = {};
+        static_for<0, NKS>([&](auto kc) {
+          constexpr int ks = decltype(kc)::value;
+          const i32x8s a = __builtin_shufflevector(fk[d][ks], (i32x4s){0, 0, 0, 0}, 0, 1, 2, 3, 4, 5, 6, 7);
+          const i32x8s b = __builtin_shufflevector(cf[ks], (i32x4s){0, 0, 0, 0}, 0, 1, 2, 3, 4, 5, 6, 7);
+          acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, acc, 4, 4, ks & 3,
+                                                                (int)fsc[d][ks >> 2], ks & 3,
+                                                                (int)cqs[ks >> 2]);
+        });
+        float v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = acc[r];
+        float m = max16(v);
+        m = fmaxf(m, __shfl_xor(m, 32));      // lane j: centroid j over the 32 rows
+        pass = 0u;
+#pragma unroll
+        for (int s = 0; s < SETS; ++s)
+          pass |= (__int_as_float(__builtin_amdgcn_readlane(__float_as_int(m), s)) + cbound[s] >=
+                           tmin[s]
+                       ? 1u
+                       : 0u)
+                  << s;
+      }
+    }
     if constexpr (ABL == 1) {
       static_for<0, SETS>([&](auto sc) {
+        if (!((pass >> decltype(sc)::value) & 1u)) return;
         float v[16];
         block(dc, sc, v);
 #pragma unroll
@@ -247,6 +307,7 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
     } else {
       static_for<0, SETS>([&](auto sc) {
         constexpr int s = decltype(sc)::value;
+        if (!((pass >> s) & 1u)) return;
         float v[16];
         block(dc, sc, v);
         hm |= (max16(v) >= thr[s] ? 1u : 0u) << s;
@@ -289,9 +350,12 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
     auto dma = [&](int i, int slot) {   // sub-tile i (past the end: the last again) into slot
       const uint8_t* r = rec0 + (size_t)min(i, ns - 1) * REC;
       const uint32_t dst = lds_addr(ring) + slot * SLOT;
-      if constexpr (FMT == SF_I8) dma2_asm(r + 2 * lane, dst);   // the 128-byte row-scale header
+      // the 128-byte row-scale header: 4 bytes per lane, lanes 32-63 repeating 0-31 into LDS bytes
+      // 128..255 (an LDS-DMA lands lane l at base + 4 l; the 2-byte form did not pack by 2)
+      if constexpr (FMT == SF_I8) dma4_asm(r + 4 * (lane & 31), dst);
 #pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) dma16_asm(r + S::HDR + 1024 * ks + 16 * lane, dst + S::HDR + 1024 * ks);
+      for (int ks = 0; ks < NKS; ++ks)
+        dma16_asm(r + S::HDR + 1024 * ks + 16 * lane, dst + G::LHDR + 1024 * ks);
       if constexpr (FMT == SF_MX4) {
 #pragma unroll
         for (int j = 0; j < NSC; ++j) dma4_asm(r + S::FRAG + 256 * j + 4 * lane, dst + S::FRAG + 256 * j);
@@ -305,7 +369,7 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
       }
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks)
-        fk[0][ks] = *reinterpret_cast<const i32x4s*>(src + S::HDR + 1024 * ks + 16 * lane);
+        fk[0][ks] = *reinterpret_cast<const i32x4s*>(src + G::LHDR + 1024 * ks + 16 * lane);
       if constexpr (FMT == SF_MX4) {
 #pragma unroll
         for (int j = 0; j < NSC; ++j)
@@ -485,6 +549,91 @@ __device__ __forceinline__ void mx4_stream_row(const __bf16* __restrict__ xrow, 
   }
 }
 
+__device__ __forceinline__ float e2m1_value(int c) {   // 4-bit code (sign bit 3) -> value
+  const int m = c & 7;
+  const float v = m < 5 ? 0.5f * m : (m == 5 ? 3.f : m == 6 ? 4.f : 6.f);
+  return (c & 8) ? -v : v;
+}
+
+// Element d of an MX-fp4 query image (quant_stream_mx4 query mode: row-major nibbles Xq [.][D/2],
+// scale record QS [.][2 NSC] dwords, dword h NSC + j byte b = block 2 (4 j + b) + h).
+template <int D>
+__device__ __forceinline__ float mx4_query_elem(const uint8_t* __restrict__ Xq,
+                                                const uint32_t* __restrict__ QS, int q, int d) {
+  constexpr int NSC = SDim<SF_MX4, D>::NSC;
+  const int byte = Xq[(size_t)q * (D / 2) + (d >> 1)];
+  const int nib = (d & 1) ? byte >> 4 : byte & 15;
+  const int k = d >> 5, jb = k >> 1;
+  const int e8 = (QS[(size_t)q * 2 * NSC + (k & 1) * NSC + (jb >> 2)] >> (8 * (jb & 3))) & 255;
+  return e2m1_value(nib) * ldexpf(1.f, e8 - 127);
+}
+
+// The query-side bound of the MX-fp4 tier (scan_stream_kernel's centroid test): for each set of
+// 32 consecutive queries, the MX-fp4 image c~ of the mean of their decoded images and
+// R = max_q |q~ - c~|, so that every query q of the set and every row x satisfy
+//   q~ . x~ = c~ . x~ + (q~ - c~) . x~ <= c~ . x~ + R |x~| <= c~ . x~ + R X4.
+// One wave per set; C4 / CS: the centroids' image in the query layout, R [n_sets].
+template <int D>
+__global__ __launch_bounds__(64) void mx4_centroids_kernel(const uint8_t* __restrict__ Xq,
+                                                           const uint32_t* __restrict__ QS, int NQ,
+                                                           uint8_t* __restrict__ C4,
+                                                           uint32_t* __restrict__ CS,
+                                                           float* __restrict__ R) {
+  constexpr int M = D / 64, NSC = SDim<SF_MX4, D>::NSC;
+  const int set = blockIdx.x, lane = threadIdx.x;
+  const int q0 = set * 32, nq = min(32, NQ - q0);
+  float c[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) c[m] = 0.f;
+  for (int i = 0; i < nq; ++i)
+#pragma unroll
+    for (int m = 0; m < M; ++m) c[m] += mx4_query_elem<D>(Xq, QS, q0 + i, lane + 64 * m);
+  uint32_t scw[NSC];
+#pragma unroll
+  for (int i = 0; i < NSC; ++i) scw[i] = 0u;
+  float ct[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const float x = c[m] / (float)max(nq, 1);
+    const float amax = half_max32(fabsf(x));
+    int e = -127;
+    if (amax > 0.f) {
+      int k;
+      frexpf(amax / 6.f, &k);
+      e = k;
+      if (amax <= 6.f * ldexpf(1.f, k - 1)) e = k - 1;
+      if (amax > 6.f * ldexpf(1.f, e)) ++e;
+      e = max(e, -127);
+    }
+    float qv;
+    const int cd = amax > 0.f ? e2m1_code_s(fabsf(x) * ldexpf(1.f, -e), qv) : (qv = 0.f, 0);
+    const int code = cd | (x < 0.f && cd ? 8 : 0);
+    ct[m] = e2m1_value(code) * ldexpf(1.f, e);   // (the value the image holds)
+    const int hi = __shfl_down(code, 1);
+    if ((lane & 1) == 0) C4[(size_t)set * (D / 2) + (lane >> 1) + 32 * m] = (uint8_t)(code | (hi << 4));
+    scw[m >> 2] |= (uint32_t)(e + 127) << (8 * (m & 3));
+  }
+#pragma unroll
+  for (int i = 0; i < NSC; ++i) {
+    const uint32_t lo = (uint32_t)__shfl((int)scw[i], 0), hi = (uint32_t)__shfl((int)scw[i], 32);
+    if (lane == 0) {
+      CS[(size_t)set * 2 * NSC + i] = lo;
+      CS[(size_t)set * 2 * NSC + NSC + i] = hi;
+    }
+  }
+  float r2 = 0.f;
+  for (int i = 0; i < nq; ++i) {
+    float d2 = 0.f;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const float d = mx4_query_elem<D>(Xq, QS, q0 + i, lane + 64 * m) - ct[m];
+      d2 += d * d;
+    }
+    r2 = fmaxf(r2, wave_sum(d2));
+  }
+  if (lane == 0) R[set] = sqrtf(r2) * 1.0001f + 1e-6f;   // (rounding of the sums above)
+}
+
 // raise bounds[0..1] to the maxima of (a, b) over the workgroup's 4 waves (idle waves pass 0)
 __device__ __forceinline__ void raise_bounds2(float* bounds, float a, float b) {
   __shared__ float red[2][4];
@@ -655,11 +804,18 @@ int symb_stream_geometry(int dim, int form, int* qpb, int* wgs_per_cu) {
   return -1;
 }
 
+struct CentArgs {   // the MX-fp4 centroid test's inputs (all nullptr: off)
+  const void* c4;
+  const void* cqs;
+  const float* R;
+  const float* b4;
+};
+
 template <int F, int D, int V, int ABL = 0, int LAND = 0>
 static int launch_stream(const void* img, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                          const void* qsc, int NQ, const float* thr, float* cand_s, int* cand_i,
                          int* cand_n, int cap, int xcd, hipStream_t st, const int* skip,
-                         const int* gate, int gate_want, int* runs) {
+                         const int* gate, int gate_want, int* runs, CentArgs ca) {
   using G = SGeo<F, D, V>;
   const int n_qblk = (NQ + G::QPB - 1) / G::QPB;
   constexpr int lds = G::STAGE * G::NW + (LAND ? G::NW * G::LDEPTH * G::SLOT : 0);
@@ -667,7 +823,8 @@ static int launch_stream(const void* img, int n_valid, int rows_per_blk, int n_r
   hipLaunchKernelGGL((scan_stream_kernel<F, D, V, ABL, LAND>), dim3(n_rblk * n_qblk), dim3(64 * G::NW), lds,
                      st, (const uint8_t*)img, n_valid, rows_per_blk, (const uint8_t*)Q,
                      (const uint32_t*)qsc, NQ, n_qblk, xcd, thr, cand_s, cand_i, cand_n, cap, skip,
-                     gate, gate_want, runs);
+                     gate, gate_want, runs, (const uint8_t*)ca.c4, (const uint32_t*)ca.cqs, ca.R,
+                     ca.b4);
   return (int)hipGetLastError();
 }
 
@@ -681,8 +838,12 @@ int symb_index_scan_stream(const void* img, int n_valid, int alloc_rows, int row
                            int n_rblk, const void* Q, const void* qsc, int NQ, const float* thr,
                            float* cand_s, int* cand_i, int* cand_n, int cap, int xcd,
                            hipStream_t st, const int* skip, int dim, int form, const int* gate,
-                           int gate_want, int zero_cnt, int* runs) {
+                           int gate_want, int zero_cnt, int* runs, const void* cent4,
+                           const void* centqs, const float* centR, const float* bounds4) {
   if (NQ <= 0) return 0;
+  if (cent4 != nullptr && (form != 1 || centqs == nullptr || centR == nullptr || bounds4 == nullptr))
+    return -1;
+  const CentArgs ca{cent4, centqs, centR, bounds4};
   if ((dim != 384 && dim != 768 && dim != 1024) || (form != 0 && form != 1)) return -1;
   if (form == 1 && qsc == nullptr) return -1;
   if (rows_per_blk % 32 || n_rblk <= 0 || thr == nullptr || cap <= 0 || n_valid <= 0) return -1;
@@ -694,11 +855,11 @@ int symb_index_scan_stream(const void* img, int n_valid, int alloc_rows, int row
   }
 #define L(F, D_, V_) launch_stream<F, D_, V_>(img, n_valid, rows_per_blk, n_rblk, Q, qsc, NQ, thr, \
                                               cand_s, cand_i, cand_n, cap, xcd, st, skip, gate,   \
-                                              gate_want, runs)
+                                              gate_want, runs, ca)
   const bool land = g_stream_land && (form == 0 ? g_stream_i8_v == 0 : g_stream_mx4_v == 0);
 #define LA(F, D_, A_, L_) launch_stream<F, D_, 0, A_, L_>(img, n_valid, rows_per_blk, n_rblk, Q, qsc, \
                                                           NQ, thr, cand_s, cand_i, cand_n, cap, xcd, \
-                                                          st, skip, gate, gate_want, runs)
+                                                          st, skip, gate, gate_want, runs, ca)
   if (dim == 768 && form == 1 && land) return LA(SF_MX4, 768, 0, 1);
   if (dim == 384) {
     if (g_stream_abl == 1)
@@ -726,6 +887,23 @@ int symb_index_scan_stream(const void* img, int n_valid, int alloc_rows, int row
   return form ? L(SF_MX4, 1024, 0) : L(SF_I8, 1024, 0);
 #undef LA
 #undef L
+}
+
+// The MX-fp4 tier's query-set centroids (mx4_centroids_kernel) of an MX-fp4 query image: C4
+// [ceil(NQ / 32)][dim / 2], CS [.][2 NSC] dwords, R [.].
+int symb_mx4_centroids(const void* Xq, const void* QS, int NQ, int dim, void* C4, void* CS,
+                       float* R, hipStream_t st) {
+  if (NQ <= 0) return 0;
+  const int n_sets = (NQ + 31) / 32;
+#define L(D_) hipLaunchKernelGGL(mx4_centroids_kernel<D_>, dim3(n_sets), dim3(64), 0, st,             \
+                                 (const uint8_t*)Xq, (const uint32_t*)QS, NQ, (uint8_t*)C4,         \
+                                 (uint32_t*)CS, R)
+  if (dim == 384) L(384);
+  else if (dim == 768) L(768);
+  else if (dim == 1024) L(1024);
+  else return -1;
+#undef L
+  return (int)hipGetLastError();
 }
 
 // Append n unit bf16 rows (src) at row r0 of the shard: rows, int8 stream image (img8 / b8) and

@@ -949,6 +949,66 @@ def test_index_scan_stream_emits_the_bound_set(form, D):
 
 
 @pytest.mark.parametrize("D", [384, 768])
+def test_mx4_centroid_test_is_exact(D):
+    """The MX-fp4 scan's query-side bound (mx4_centroids_kernel + the scan's centroid test):
+    with two near-duplicate query clusters and planted rows near each, the scan with the test
+    emits exactly the rows it emits without it (the bound c~ . x~ + R X4 only skips sets that
+    cannot emit), and the radii bound every query's distance to its set's centroid image."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+    from codename_symbiont_amd.ops._ext import hip, stream_handle
+
+    n, nq = 150_000 + 33, 256
+    g = torch.Generator(device=DEV).manual_seed(81)
+    shard = HbmIndexShard(D, n + 4096, prune="i8")
+    shard.fill_random(n - 2000, seed=9)
+    cs_ = torch.nn.functional.normalize(torch.randn(2, D, device=DEV, generator=g), dim=-1)
+    near = lambda c, m, e: torch.nn.functional.normalize(
+        c + e * torch.randn(m, D, device=DEV, generator=g) / math.sqrt(D), dim=-1)
+    shard.append_f32(torch.cat([near(cs_[0], 1000, 0.3), near(cs_[1], 1000, 0.3)]))
+    q = torch.cat([near(cs_[0], 128, 0.1), near(cs_[1], 100, 0.1)]).bfloat16()
+    nq = q.shape[0]          # (228: a partial last set)
+    h, st = hip(), stream_handle(shard.device)
+    q4, qs4, _ = shard.mx4_query_image(q)
+    n_sets = -(-nq // 32)
+    c4 = torch.empty(n_sets, D // 2, dtype=torch.uint8, device=DEV)
+    cqs = torch.empty(n_sets, qs4.shape[1], dtype=torch.int32, device=DEV)
+    cR = torch.empty(n_sets, device=DEV)
+    h.mx4_centroids(q4.data_ptr(), qs4.data_ptr(), nq, D, c4.data_ptr(), cqs.data_ptr(),
+                    cR.data_ptr(), st)
+    qt = R.stream_mx4_query_decode(q4, qs4)
+    ct = R.stream_mx4_query_decode(c4, cqs)
+    torch.cuda.synchronize()
+    for s in range(n_sets):
+        d = (qt[32 * s:32 * s + 32] - ct[s]).norm(dim=1).max()
+        assert float(d) <= float(cR[s]) + 1e-6, (s, float(d), float(cR[s]))
+    xt = R.stream_mx4_decode(shard.img_mx4[:(n + 31) // 32], n, D)
+    est = qt @ xt.t()
+    t = (est.topk(30, dim=1).values[:, -1] - 0.02).contiguous()
+    _, rows_per_blk, n_rblk = shard._i8_geometry(n, nq, shard._n_cus())
+    got = []
+    for cent in (False, True):
+        cap = 8192
+        cs = torch.empty(nq, cap, device=DEV)
+        ci = torch.empty(nq, cap, dtype=torch.int32, device=DEV)
+        cnt = torch.empty(nq, dtype=torch.int32, device=DEV)
+        kw = dict(cent4=c4.data_ptr(), centqs=cqs.data_ptr(), centR=cR.data_ptr(),
+                  bounds4=shard.mx4_bounds.data_ptr()) if cent else {}
+        h.index_scan_stream(shard.img_mx4.data_ptr(), n, shard.img_mx4.shape[0] * 32, rows_per_blk,
+                            n_rblk, q4.data_ptr(), qs4.data_ptr(), nq, t.data_ptr(), cs.data_ptr(),
+                            ci.data_ptr(), cnt.data_ptr(), cap, 1, st, dim=D, form=1, **kw)
+        torch.cuda.synchronize()
+        assert int(cnt.max()) <= cap
+        m = torch.zeros(nq, n, dtype=torch.bool, device=DEV)
+        for i in range(nq):
+            m[i, ci[i, :int(cnt[i])].long()] = True
+        got.append(m)
+    assert torch.equal(got[0], got[1]), "the centroid test changed the emitted set"
+    want = est >= t[:, None]
+    near_t = (est - t[:, None]).abs() <= 1e-5
+    assert not ((got[1] != want) & ~near_t).any()
+
+
+@pytest.mark.parametrize("D", [384, 768])
 @pytest.mark.parametrize("k", [1, 10, 16])
 def test_prune_qprep_matches_torch_composition(k, D):
     """index_i8.hip prune_qprep (T = k-th best of the two lists, int8 query image, emission
