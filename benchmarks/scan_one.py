@@ -3,12 +3,13 @@
 the target of timing A/Bs and rocprofv3 --pmc passes (benchmarks/pmc_kernel.py --match scan).
 
     python benchmarks/scan_one.py [--rows 25000000] [--nq 256] [--corpus random] [--iters 10]
-                                  [--tier i8|mx4] [--queries heldout|self]
+                                  [--tier i8|mx4|mx6] [--queries heldout|self]
 
 The shard's scan is the stream scan (index_stream.hip) unless SYMB_PRUNE_STREAM=0 (the round-4
 LDS-ring scan, index_i8.hip).  --tier mx4 times the MX-fp4 first tier on the same block grid with
 the thresholds the tier choice computed (--queries self: stored rows as queries; near: near-duplicate queries, whose sets the centroid
-test skips; both at the headline's fp4 threshold 0.74).
+test skips; both at the headline's fp4 threshold 0.74).  --tier mx6 times the MX-fp6 middle tier
+(SYMB_PRUNE_MX6) at the thresholds its tier choice computed.
 """
 from __future__ import annotations
 
@@ -30,7 +31,7 @@ def main() -> None:
     ap.add_argument("--dim", type=int, default=384)
     ap.add_argument("--corpus", default="random")
     ap.add_argument("--iters", type=int, default=10)
-    ap.add_argument("--tier", choices=["i8", "mx4"], default="i8")
+    ap.add_argument("--tier", choices=["i8", "mx4", "mx6"], default="i8")
     ap.add_argument("--queries", choices=["heldout", "self", "near"], default="heldout")
     ap.add_argument("--variant", type=int, default=-1, help="stream MX-fp4 form (stream_config)")
     ap.add_argument("--ab", default="",
@@ -67,9 +68,11 @@ def main() -> None:
     P, n = shard._pruned_last, shard.visible
     rsplit = 2 if a.nq < 512 else 1
     heavy = P["heavy"]
-    m4 = P["m4"]
+    m4, m6 = P["m4"], P.get("m6")
     if a.tier == "mx4" and m4 is None:
         raise SystemExit("no MX-fp4 tier on this shard")
+    if a.tier == "mx6" and m6 is None:
+        raise SystemExit("no MX-fp6 tier on this shard")
     if a.tier == "mx4" and a.queries in ("self", "near"):
         # the headline's batches take the fp4 tier because their k-th scores sit near 0.99 (fresh
         # near-duplicate embeddings): T - margin4 ~ 0.74.  Stored random rows as queries have
@@ -79,7 +82,14 @@ def main() -> None:
     nbytes = 0
 
     def scan():
-        if a.tier == "mx4":
+        if a.tier == "mx6":
+            P["cnt"].zero_()
+            h.index_scan_stream(shard.img_mx6.data_ptr(), n, shard.img_mx6.shape[0] * STREAM_SUB,
+                                P["rows_per_blk"], P["n_rblk"], m6["q6"].data_ptr(),
+                                m6["qs6"].data_ptr(), a.nq, m6["thr6"].data_ptr(),
+                                P["cs"].data_ptr(), P["ci"].data_ptr(), P["cnt"].data_ptr(),
+                                P["cap"], 1, st, dim=a.dim, form=2)
+        elif a.tier == "mx4":
             P["cnt"].zero_()
             if shard.img_mx4 is not None:
                 h.index_scan_stream(shard.img_mx4.data_ptr(), n, shard.img_mx4.shape[0] * STREAM_SUB,
@@ -106,7 +116,9 @@ def main() -> None:
                             P["ci"].data_ptr(), P["cnt"].data_ptr(), P["cap"], 1, st, rsplit,
                             dim=a.dim, heavy=heavy, sq=P["sq"].data_ptr() if heavy else 0)
 
-    if a.tier == "mx4":
+    if a.tier == "mx6":
+        nbytes, kernel = shard.img_mx6.shape[1] / STREAM_SUB, "stream-mx6"
+    elif a.tier == "mx4":
         nbytes = (shard.img_mx4.shape[1] / STREAM_SUB if shard.img_mx4 is not None
                   else a.dim // 2 + 16)
         kernel = "stream-mx4" if shard.img_mx4 is not None else "ldsring-mx4"
@@ -130,7 +142,7 @@ def main() -> None:
             torch.cuda.synchronize()
             times[f].append((time.perf_counter() - t0) * 1e3 / a.iters)
     if a.ab:
-        h.stream_config(0, 0, 0, 1)
+        h.stream_config(0, 0, 0, 0)
     for f, ts in times.items():
         ms = sorted(ts)[len(ts) // 2]
         print(json.dumps({"bench": "scan_one", "kernel": kernel, "form": f, "rows": n, "nq": a.nq,
@@ -139,7 +151,9 @@ def main() -> None:
                           "ms": round(ms, 3), "TBps": round(n * nbytes / ms / 1e9, 2),
                           "n_rblk": P["n_rblk"], "rows_per_blk": P["rows_per_blk"],
                           "cand_mean": round(float(P["cnt"].float().mean()), 1),
-                          "cand_max": int(P["cnt"].max()), "fill_s": round(fill_s, 1)}), flush=True)
+                          "cand_max": int(P["cnt"].max()), "fill_s": round(fill_s, 1),
+                          "tier_flag": None if shard._tier_last is None else int(shard._tier_last.item())}),
+              flush=True)
 
 
 if __name__ == "__main__":

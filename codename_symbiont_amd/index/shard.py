@@ -144,6 +144,11 @@ MX4_DIMS = (384, 768, 1024)             # ... the MX-fp4 first tier (384-only on
 # 384 / 768 only)
 STREAM_DIMS = (384, 768, 1024)
 STREAM_SUB = 32                         # rows per sub-tile record of the stream images
+# widths of the MX-fp6 (e2m3) middle tier (stream scan only) and where SYMB_PRUNE_MX6=auto keeps
+# it: 0.75 bytes per element, so a 100M x 768 shard (bf16 + int8 + fp4 images ~270 GB) has no
+# room for it by default
+MX6_DIMS = (384, 768)
+AUTO_MX6_DIMS = (384,)
 
 
 class HbmIndexShard:
@@ -224,6 +229,16 @@ class HbmIndexShard:
         # the MX-fp4 image (a first tier below the int8 one, _pruned_end): 192 bytes of e2m1
         # nibbles + 16 bytes of block scales per 384-wide row, and its (E4, X4) maxima
         self.rows_mx4 = self.sc_mx4 = self.mx4_bounds = None
+        # the MX-fp6 image (a tier between the fp4 and int8 ones, _pruned_begin): e2m3 codes + e8m0
+        # block scales, 300 bytes per 384-wide row, and its (E6, X6) maxima
+        self.img_mx6 = self.mx6_bounds = None
+        mx6 = os.environ.get("SYMB_PRUNE_MX6", "auto").strip().lower()
+        if (prune and self.stream and dim in MX6_DIMS and mx6 not in ("", "0", "off")
+                and (mx6 != "auto" or dim in AUTO_MX6_DIMS)):
+            n_alloc = _round_up(self.rows.shape[0], 128)
+            self.img_mx6 = torch.zeros(n_alloc // STREAM_SUB, self._stream_rec(2),
+                                       dtype=torch.uint8, device=self.device)
+            self.mx6_bounds = torch.zeros(2, dtype=torch.float32, device=self.device)
         if (prune and dim in (MX4_DIMS if self.stream else (384,))
                 and os.environ.get("SYMB_PRUNE_MX4", "1") not in ("", "0")):
             n_alloc = _round_up(self.rows.shape[0], 128)
@@ -272,8 +287,10 @@ class HbmIndexShard:
         self.i8_rsplit2 = False
         self._mq_tot = None
         self._mx4_tot = None     # searches whose first tier was the MX-fp4 scan (mq_stats)
+        self._mx6_tot = None     # ... the MX-fp6 scan
         self.tier_stats = True   # ... counted even without mq_stats (one tiny add per search)
         self._mx4_last = None
+        self._tier_last = None
         # the tier recent searches took, read back without a sync: (pinned int, event) of each
         # search's MX-fp4 flag, and the last one known to have landed (True: the fp4 tier ran)
         self._tier_pending = collections.deque()
@@ -287,10 +304,10 @@ class HbmIndexShard:
 
     # ------------------------------------------------------------------ pruning images
     def _stream_rec(self, form: int) -> int:
-        """Bytes per 32-row sub-tile of the stream image (form 0 = int8, 1 = MX-fp4); the same
-        numbers as index_stream.hip SDim (checked against the extension on a GPU)."""
+        """Bytes per 32-row sub-tile of the stream image (form 0 = int8, 1 = MX-fp4, 2 = MX-fp6);
+        the same numbers as index_stream.hip SDim (checked against the extension on a GPU)."""
         nks = self.dim // (64 if form else 32)
-        return nks * 1024 + ((nks + 3) // 4 * 256 if form else 128)
+        return nks * (1536 if form == 2 else 1024) + ((nks + 3) // 4 * 256 if form else 128)
 
     def _set_i8_view(self, heavy: int) -> None:
         """Views of the flat int8 store for the form: the stream image (plain form on a stream
@@ -316,6 +333,11 @@ class HbmIndexShard:
         """The shard keeps the MX-fp4 first-tier image."""
         return self.mx4_bounds is not None
 
+    @property
+    def mx6_on(self) -> bool:
+        """The shard keeps the MX-fp6 middle-tier image."""
+        return self.mx6_bounds is not None
+
     def _stream_subtiles_cpu(self, img, form: int, r0: int, r1: int) -> None:
         """CPU backend: recompute the stream records of the sub-tiles covering rows [r0, r1) from
         the bf16 rows (per-row images: the other rows' bytes come out unchanged)."""
@@ -325,9 +347,10 @@ class HbmIndexShard:
         hi = min(g1 * STREAM_SUB, self.count)
         src = self.rows[g0 * STREAM_SUB:hi]
         if form:
-            rec, nr = R.stream_mx4_ref(src)
+            rec, nr = (R.stream_mx6_ref if form == 2 else R.stream_mx4_ref)(src)
             w = nr[r0 - g0 * STREAM_SUB:r1 - g0 * STREAM_SUB]
-            torch.maximum(self.mx4_bounds, w[:, :2].amax(0), out=self.mx4_bounds)
+            b = self.mx6_bounds if form == 2 else self.mx4_bounds
+            torch.maximum(b, w[:, :2].amax(0), out=b)
         else:
             rec, err, xtn = R.stream_i8_ref(src)
             a, b = r0 - g0 * STREAM_SUB, r1 - g0 * STREAM_SUB
@@ -390,6 +413,15 @@ class HbmIndexShard:
                 self._mx4_image(self.rows[ri], img4, sc4, self.mx4_bounds)
                 self.rows_mx4.index_copy_(0, ri, img4)
                 self.sc_mx4.index_copy_(0, ri, sc4)
+        if self.mx6_on:
+            if gpu:
+                h.quant_stream_mx6(self.rows.data_ptr(), r0, rp, n, self.dim,
+                                   self.img_mx6.data_ptr(), 0, 0, self.mx6_bounds.data_ptr(), 0, st)
+            elif rows is None:
+                self._stream_subtiles_cpu(self.img_mx6, 2, r0, r0 + n)
+            else:
+                for r in rows.tolist():
+                    self._stream_subtiles_cpu(self.img_mx6, 2, r, r + 1)
 
     def mx4_query_image(self, q_unit: torch.Tensor):
         """(nibbles, scale record, margin) of unit queries for the MX-fp4 tier: the stream form
@@ -418,6 +450,28 @@ class HbmIndexShard:
         qs4.copy_(qs)
         m4.copy_(nr[:, 2] * self.mx4_bounds[0] + nr[:, 0] * self.mx4_bounds[1] + 1e-5)
         return q4, qs4, m4
+
+    def mx6_query_image(self, q_unit: torch.Tensor):
+        """(codes, scale record, margin) of unit queries for the MX-fp6 tier (quant_stream_mx6:
+        [NQ][3 D / 4] bytes, [NQ][2 NSC] dwords); margin = |q| E6 + |q - q~| X6 + 1e-5."""
+        NQ, dev = q_unit.shape[0], self.device
+        q6 = torch.empty(NQ, 3 * self.dim // 4, dtype=torch.uint8, device=dev)
+        qs6 = torch.empty(NQ, 2 * ((self.dim // 64 + 3) // 4), dtype=torch.int32, device=dev)
+        m6 = torch.empty(NQ, dtype=torch.float32, device=dev)
+        if dev.type == "cuda":
+            from ..ops._ext import hip, stream_handle
+
+            hip().quant_stream_mx6(q_unit.data_ptr(), 0, 0, NQ, self.dim, 0, q6.data_ptr(),
+                                   qs6.data_ptr(), self.mx6_bounds.data_ptr(), m6.data_ptr(),
+                                   stream_handle(dev))
+            return q6, qs6, m6
+        from ..ops.reference import stream_mx6_query_ref
+
+        img, qs, _, nr = stream_mx6_query_ref(q_unit)
+        q6.copy_(img)
+        qs6.copy_(qs)
+        m6.copy_(nr[:, 2] * self.mx6_bounds[0] + nr[:, 0] * self.mx6_bounds[1] + 1e-5)
+        return q6, qs6, m6
 
     # ------------------------------------------------------------------ inserts
     def _reserve(self, n: int) -> int:
@@ -476,11 +530,13 @@ class HbmIndexShard:
             return False
         from ..ops._ext import hip, stream_handle
 
-        m4 = self.img_mx4 is not None
+        m4, m6 = self.img_mx4 is not None, self.img_mx6 is not None
         hip().append_rows(src.data_ptr(), n, self.dim, self.rows.data_ptr(), r0,
                           self.img_i8.data_ptr(), self.i8_bounds.data_ptr(),
                           self.img_mx4.data_ptr() if m4 else 0,
-                          self.mx4_bounds.data_ptr() if m4 else 0, stream_handle(self.device))
+                          self.mx4_bounds.data_ptr() if m4 else 0, stream_handle(self.device),
+                          img6=self.img_mx6.data_ptr() if m6 else 0,
+                          b6=self.mx6_bounds.data_ptr() if m6 else 0)
         return True
 
     def rows_written(self, r0: int, n: int) -> None:
@@ -493,7 +549,7 @@ class HbmIndexShard:
                 # (re-images every row below r0 + n when the image's form changes; the new
                 # rows' MX-fp4 image below)
                 self.calibrate_prune(r0 + n, lo=r0)
-                if self.mx4_on:
+                if self.mx4_on or self.mx6_on:
                     saved, self.i8_bounds = self.i8_bounds, None
                     try:
                         self._image_rows(r0, n)
@@ -501,7 +557,7 @@ class HbmIndexShard:
                         self.i8_bounds = saved
             else:
                 self._image_rows(r0, n)
-        elif self.mx4_on and n > 0:
+        elif (self.mx4_on or self.mx6_on) and n > 0:
             self._image_rows(r0, n)
         if self.rows8 is None or n <= 0:
             return
@@ -556,7 +612,9 @@ class HbmIndexShard:
             share = float(ev[:SPLIT_HEAVY].sum() / ev.sum().clamp_min(1e-30))
             if self.i8_split == "on" or share >= self.SPLIT_MIN_SHARE:
                 heavy, rot = SPLIT_HEAVY, vec.t().contiguous()
-        mx4_saved, self.mx4_bounds = self.mx4_bounds, None   # (the int8 / split image only)
+        # (the int8 / split image only)
+        mx4_saved, self.mx4_bounds = self.mx4_bounds, None
+        mx6_saved, self.mx6_bounds = self.mx6_bounds, None
         try:
             if heavy == 0 and self._i8_heavy == 0 and lo is not None:
                 self.calib_share = share
@@ -570,7 +628,7 @@ class HbmIndexShard:
             for s in range(0, hi, chunk):
                 self._image_rows(s, min(hi, s + chunk) - s)
         finally:
-            self.mx4_bounds = mx4_saved
+            self.mx4_bounds, self.mx6_bounds = mx4_saved, mx6_saved
         self._calib_gen += 1
         self._calib_next = max(hi * self.CALIB_GROWTH, self.CALIB_MIN_ROWS)
 
@@ -1101,6 +1159,7 @@ class HbmIndexShard:
     # the MX-fp4 first tier runs when every query's estimated fp4 band holds at most this share
     # of PRUNE_CAP (its candidates are re-scored exactly like the int8 ones)
     MX4_LIMIT_FRAC = 0.25
+    MX6_LIMIT_FRAC = 0.25
     prune_route = True   # False: always take the int8 pass (tests of the overflow fallback)
 
     def _search_pruned(self, q_unit, k: int, n_cus):
@@ -1228,7 +1287,7 @@ class HbmIndexShard:
                       tail_cnt=0 if tcnt is None else tcnt.data_ptr(), tail_cap=tcap, tail_off=t0,
                       tail_ld=tail_ld, zeroed=True)
         ctx = dict(q=q_unit, k=k, n=n, n_cus=n_cus, q8=q8, sq=sq, thr=thr, T=T, dense=dense,
-                   blk=blk, geo=geo, heavy=heavy, gen=self._calib_gen, mx4=None, ws=ws)
+                   blk=blk, geo=geo, heavy=heavy, gen=self._calib_gen, mx4=None, mx6=None, ws=ws)
         # 3. the MX-fp4 first tier (mx4_select): when every query's k-th score sits so far above
         #    the corpus bulk that even the coarse fp4 bound (|q| E4 + |q - q~| X4, ~0.25 on unit
         #    rows) leaves few rows in its band -- self / near-duplicate queries, such as the
@@ -1237,11 +1296,11 @@ class HbmIndexShard:
         #    exact scores (the probe: every 4th seed tile, read in place; the band must lie above
         #    the sample's seed threshold, so the sample counted it): the int8 / split scan and
         #    the fp4 scan are both enqueued, each gated on the flag, and exactly one runs.
+        nvf = flags[self.WS_NV:self.WS_NV + 1]
+        n_probe = TILE_ROWS * -(-(m_seed // TILE_ROWS) // 4)
         if self.mx4_on and self.prune_route and dense_tail:
             q4, qs4, m4 = self.mx4_query_image(q_unit)
             thr4 = torch.empty(NQ, dtype=torch.float32, device=dev)
-            nvf = flags[self.WS_NV:self.WS_NV + 1]
-            n_probe = TILE_ROWS * -(-(m_seed // TILE_ROWS) // 4)
             h.mx4_select(NQ, T.data_ptr(), m4.data_ptr(), margin.data_ptr(), S.data_ptr(), m_seed,
                          float(t0) / n_probe, tcs_p, tcap, self.MX4_LIMIT_FRAC * cap,
                          thr4.data_ptr(), nvf.data_ptr(), st, ld=ld, tile_stride=4, tail_ld=ld,
@@ -1258,6 +1317,18 @@ class HbmIndexShard:
                 h.mx4_centroids(q4.data_ptr(), qs4.data_ptr(), NQ, self.dim, c4.data_ptr(),
                                 cqs.data_ptr(), cR.data_ptr(), st)
                 ctx["mx4"].update(c4=c4, cqs=cqs, cR=cR)
+        # 4. the MX-fp6 middle tier, chosen the same way when the fp4 one is not viable: e2m3
+        #    carries ~4x the int8 rounding error, so its band fits held-out queries whose k-th score
+        #    sits a few sigma above the bulk (the fp4 band does not), at the fp4 MFMA rate and 3/4
+        #    of the int8 image's bytes.  The flag then reads 0 (fp4), 1 (fp6) or 3 (int8 / split).
+        if self.mx6_on and self.prune_route and dense_tail:
+            q6, qs6, m6 = self.mx6_query_image(q_unit)
+            thr6 = torch.empty(NQ, dtype=torch.float32, device=dev)
+            h.mx4_select(NQ, T.data_ptr(), m6.data_ptr(), margin.data_ptr(), S.data_ptr(), m_seed,
+                         float(t0) / n_probe, tcs_p, tcap, self.MX6_LIMIT_FRAC * cap,
+                         thr6.data_ptr(), nvf.data_ptr(), st, ld=ld, tile_stride=4, tail_ld=ld,
+                         nv_zeroed=True, stage=1 if ctx["mx4"] is not None else 2, wa=1.0, wb=1.0)
+            ctx["mx6"] = dict(q6=q6, qs6=qs6, thr6=thr6, nv=nvf, m6=m6)
         return ctx
 
     # the search workspace's flag slots (_pruned_begin): route "every block dense", the MX-fp4
@@ -1294,9 +1365,10 @@ class HbmIndexShard:
             else:
                 qpb, wpc = h.stream_geometry(self.dim, 0)
                 n_qblk = math.ceil(NQ / qpb)
-            if self.mx4_on:
-                qpb4, wpc4 = h.stream_geometry(self.dim, 1)
-                n_qblk, wpc = max(n_qblk, math.ceil(NQ / qpb4)), max(wpc, wpc4)
+            for form, on in ((1, self.mx4_on), (2, self.mx6_on)):
+                if on:
+                    qpbf, wpcf = h.stream_geometry(self.dim, form)
+                    n_qblk, wpc = max(n_qblk, math.ceil(NQ / qpbf)), max(wpc, wpcf)
             # (>= 8192 rows per block: the route estimates each block from the exact sample's
             # 1-in-2^5 tiles, so a block needs a few sampled tiles -- ~1k-row blocks saw 0 or 1
             # and left crowded blocks to the int8 scan)
@@ -1356,12 +1428,14 @@ class HbmIndexShard:
         out_s = torch.empty(NQ, k, device=dev)
         out_i = torch.empty(NQ, k, dtype=torch.int32, device=dev)
         skip = blk[2 + n_rblk:].data_ptr() if self.prune_route else 0
-        m4 = ctx.get("mx4")
-        if m4 is not None:   # both tiers enqueued, gated on the flag: exactly one runs
-            for t in ("q4", "qs4", "thr4", "c4", "cqs", "cR"):
-                if t in m4:
-                    m4[t].record_stream(cur)
-        gate, want = (m4["nv"].data_ptr(), 1) if m4 is not None else (0, 0)
+        m4, m6 = ctx.get("mx4"), ctx.get("mx6")
+        for m in (m4, m6):   # every tier enqueued, gated on the flag: exactly one runs
+            if m is not None:
+                for t in ("q4", "qs4", "thr4", "c4", "cqs", "cR", "q6", "qs6", "thr6"):
+                    if t in m:
+                        m[t].record_stream(cur)
+        tier = (m4 or m6 or {}).get("nv")
+        gate, want = (0, 0) if tier is None else (tier.data_ptr(), 3 if m6 is not None else 1)
         if self.img_i8 is not None and not ctx["heavy"]:   # the stream scan (index_stream.hip)
             h.index_scan_stream(self.img_i8.data_ptr(), n, self.img_i8.shape[0] * STREAM_SUB,
                                 rows_per_blk, n_rblk, q8.data_ptr(), 0, NQ, thr.data_ptr(),
@@ -1395,6 +1469,18 @@ class HbmIndexShard:
                             cap, self.scan_xcd, st, rsplit, skip=skip, dim=self.dim,
                             sq=m4["qs4"].data_ptr(), form=1, gate=m4["nv"].data_ptr(),
                             gate_want=0)
+        if m6 is not None:
+            runs = 0
+            if self.mq_stats or self.tier_stats:
+                if self._mx6_tot is None:
+                    self._mx6_tot = torch.zeros(1, dtype=torch.int32, device=dev)
+                runs = self._mx6_tot.data_ptr()
+            h.index_scan_stream(self.img_mx6.data_ptr(), n, self.img_mx6.shape[0] * STREAM_SUB,
+                                rows_per_blk, n_rblk, m6["q6"].data_ptr(), m6["qs6"].data_ptr(),
+                                NQ, m6["thr6"].data_ptr(), cs.data_ptr(), ci.data_ptr(),
+                                cnt.data_ptr(), cap, self.scan_xcd, st, skip=skip, dim=self.dim,
+                                form=2, gate=m6["nv"].data_ptr(), gate_want=1, zero_cnt=0,
+                                runs=runs)
         # 3'. the bf16 emitting scan of the blocks the route listed, at the exact threshold T,
         #     into the same candidate buffers (no launch work when none is listed)
         if self.prune_route:
@@ -1414,9 +1500,10 @@ class HbmIndexShard:
         self._mq_last = (cnt, ovf)
         self._route_last = dense
         self._mx4_last = None if m4 is None else m4["nv"]   # 0: the MX-fp4 tier ran
-        if m4 is not None and dev.type == "cuda":
+        self._tier_last = tier   # 0 fp4, 1 fp6, 3 int8 (1 without the fp6 tier)
+        if tier is not None and dev.type == "cuda":
             flag = torch.empty(1, dtype=torch.int32, pin_memory=True)
-            flag.copy_(m4["nv"], non_blocking=True)
+            flag.copy_(tier, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(cur)
             with self._tier_lock:
@@ -1431,7 +1518,7 @@ class HbmIndexShard:
         if self.mq_stats:   # (diagnostics / benchmarks/micro.py scani8abl: inputs and grid)
             self._pruned_last = dict(q8=q8, thr=thr, sq=ctx["sq"], rows_per_blk=rows_per_blk,
                                      n_rblk=n_rblk, cap=cap, cs=cs, ci=ci, cnt=cnt, q=q_unit,
-                                     m4=m4, heavy=ctx["heavy"])
+                                     m4=m4, m6=m6, heavy=ctx["heavy"])
         self._stats(ovf, cnt, dense, blk)
         return out_s, out_i
 

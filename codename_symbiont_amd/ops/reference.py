@@ -304,6 +304,129 @@ def stream_mx4_decode(rec: torch.Tensor, n: int, d: int) -> torch.Tensor:
     return mx4_decode_codes(img, e)
 
 
+# OCP e2m3 magnitudes by 5-bit code 8 E + m (bias 1; E = 0: subnormal m / 8)
+E2M3 = tuple(m / 8 if e == 0 else 2.0 ** (e - 1) * (1 + m / 8) for e in range(4) for m in range(8))
+
+
+def mx6_codes_ref(x: torch.Tensor):
+    """MX-fp6 (e2m3) quantisation of rows (index_stream.hip mx_stream_row, SF_MX6): per 32-dim
+    block the scale 2^ceil(log2(max|x| / 7.5)) (exponent e), each element the nearest e2m3 value of
+    x / s (sign bit 5).  Returns (codes int32 [n, D], exponents [n, D / 32], decoded x~ f32 [n, D],
+    norms [n, 3] = (|x - x~|, |x~|, |x|))."""
+    xf = x.float()
+    n, d = xf.shape
+    blk = xf.view(n, d // 32, 32)
+    amax = blk.abs().amax(-1)
+    one = torch.ones_like(amax)
+    _, k = torch.frexp(amax / 7.5)
+    e = torch.where(amax <= 7.5 * torch.ldexp(one, k - 1), k - 1, k)
+    e = torch.where(amax > 7.5 * torch.ldexp(one, e), e + 1, e)
+    e = torch.where(amax > 0, e, torch.full_like(e, -127)).clamp_(min=-127)
+    a = blk.abs() * torch.ldexp(one, -e)[..., None]
+    q = torch.where(a < 2.0, torch.round(a * 8.0) / 8.0,
+                    torch.where(a < 4.0, torch.round(a * 4.0) / 4.0,
+                                torch.clamp(torch.round(a * 2.0) / 2.0, max=7.5)))
+    code = torch.where(a < 2.0, q * 8.0, torch.where(a < 4.0, q * 4.0 + 8.0, q * 2.0 + 16.0))
+    code = code.to(torch.int32)
+    code = code | torch.where((blk < 0) & (code != 0), 32, 0).to(torch.int32)
+    xt = (torch.where(blk < 0, -q, q) * torch.ldexp(one, e)[..., None]).view(n, d)
+    norms = torch.stack([(xf - xt).norm(dim=1), xt.norm(dim=1), xf.norm(dim=1)], 1)
+    return code.view(n, d), e, xt, norms
+
+
+def _mx6_pack(codes: torch.Tensor) -> torch.Tensor:
+    """6-bit codes [n, D] -> bytes [n, 3 D / 4]: each 32-element block a 24-byte piece, element j
+    at bits [6 j, 6 j + 6) little-endian."""
+    n, d = codes.shape
+    c = codes.view(n, d // 4, 4).to(torch.int64)
+    v = c[..., 0] | (c[..., 1] << 6) | (c[..., 2] << 12) | (c[..., 3] << 18)
+    return torch.stack([v & 255, (v >> 8) & 255, (v >> 16) & 255], -1).view(n, 3 * d // 4).to(torch.uint8)
+
+
+def _mx6_unpack(img: torch.Tensor) -> torch.Tensor:
+    n, nb = img.shape
+    b = img.view(n, nb // 3, 3).to(torch.int64)
+    v = b[..., 0] | (b[..., 1] << 8) | (b[..., 2] << 16)
+    return torch.stack([(v >> (6 * i)) & 63 for i in range(4)], -1).view(n, 4 * nb // 3)
+
+
+def _mx_scale_record(e: torch.Tensor, n_sub: int) -> torch.Tensor:
+    """The stream image's scale dwords [n_sub, NSC * 256] of exponents e [n, D / 32] (dword j of
+    lane l = 32 hh + rr: the e8m0 bytes of k-steps 4j .. 4j + 3 of row rr, block 2 ks + hh)."""
+    n, nb = e.shape
+    nks = nb // 2
+    nsc = (nks + 3) // 4
+    sc = torch.zeros(n_sub * 32, nsc, 2, 4, dtype=torch.uint8, device=e.device)
+    for b in range(nb):
+        ks, hh = b // 2, b % 2
+        sc[:n, ks // 4, hh, ks % 4] = (e[:, b] + 127).to(torch.uint8)
+    return sc.view(n_sub, 32, nsc, 2, 4).permute(0, 2, 3, 1, 4).reshape(n_sub, nsc * 256)
+
+
+def _mx_scale_exps(rec_sc: torch.Tensor, n: int, nb: int) -> torch.Tensor:
+    n_sub = rec_sc.shape[0]
+    nsc = (nb // 2 + 3) // 4
+    sc = rec_sc.reshape(n_sub, nsc, 2, 32, 4).permute(0, 3, 1, 2, 4).reshape(n_sub * 32, nsc, 2, 4)[:n]
+    return torch.stack([sc[:, (b // 2) // 4, b % 2, (b // 2) % 4].to(torch.int32) - 127
+                        for b in range(nb)], 1)
+
+
+def _mx6_values(codes: torch.Tensor, e: torch.Tensor) -> torch.Tensor:
+    n, d = codes.shape
+    grid = torch.tensor(E2M3, dtype=torch.float32, device=codes.device)
+    v = grid[codes & 31] * torch.where(codes & 32 != 0, -1.0, 1.0)
+    return (v.view(n, d // 32, 32) * torch.ldexp(torch.ones_like(e, dtype=torch.float32),
+                                                  e.to(torch.int32))[..., None]).view(n, d)
+
+
+def stream_mx6_ref(x: torch.Tensor):
+    """MX-fp6 stream image of bf16 rows (quant_stream_mx6, rows): records uint8 [n_sub, 1536 NKS
+    + NSC * 256]: per k-step two 768-byte planes, lane l = 32 hh + rr holding bytes 0-11 / 12-23
+    of row rr's 24-byte piece of block 2 ks + hh at 12 l; then the scale dwords as MX-fp4."""
+    codes, e, _, norms = mx6_codes_ref(x)
+    n, d = x.shape
+    nks = d // 64
+    n_sub = (n + 31) // 32
+    pad = torch.zeros(n_sub * 32, 3 * d // 4, dtype=torch.uint8, device=x.device)
+    pad[:n] = _mx6_pack(codes)
+    # [sub][rr][ks][hh][plane][12] -> [sub][ks][plane][hh][rr][12]
+    frags = pad.view(n_sub, 32, nks, 2, 2, 12).permute(0, 2, 4, 3, 1, 5).reshape(n_sub, nks * 1536)
+    return torch.cat([frags, _mx_scale_record(e, n_sub)], 1), norms
+
+
+def stream_mx6_decode(rec: torch.Tensor, n: int, d: int) -> torch.Tensor:
+    """Decoded f32 rows [n, d] of an MX-fp6 stream image."""
+    nks = d // 64
+    n_sub = rec.shape[0]
+    fr = rec[:, :nks * 1536].reshape(n_sub, nks, 2, 2, 32, 12).permute(0, 4, 1, 3, 2, 5)
+    img = fr.reshape(n_sub * 32, 3 * d // 4)[:n]
+    return _mx6_values(_mx6_unpack(img), _mx_scale_exps(rec[:, nks * 1536:], n, d // 32))
+
+
+def stream_mx6_query_ref(x: torch.Tensor):
+    """The MX-fp6 query image (quant_stream_mx6, queries): bytes [n, 3 D / 4] row-major (block b's
+    24-byte piece at 24 b) and the scale record int32 [n, 2 NSC] as the MX-fp4 one, plus the
+    decoded x~ and norms."""
+    codes, e, xt, norms = mx6_codes_ref(x)
+    n, d = x.shape
+    nsc = (d // 64 + 3) // 4
+    qs = torch.zeros(n, 2, nsc, 4, dtype=torch.uint8, device=x.device)
+    for b in range(d // 32):
+        ks, hh = b // 2, b % 2
+        qs[:, hh, ks // 4, ks % 4] = (e[:, b] + 127).to(torch.uint8)
+    return _mx6_pack(codes), qs.view(n, 2 * nsc * 4).view(torch.int32), xt, norms
+
+
+def stream_mx6_query_decode(q6: torch.Tensor, qs: torch.Tensor) -> torch.Tensor:
+    """Decoded f32 queries of a stream MX-fp6 query image."""
+    n, d = q6.shape[0], q6.shape[1] * 4 // 3
+    nsc = (d // 64 + 3) // 4
+    b = qs.contiguous().view(torch.uint8).view(n, 2, nsc, 4)
+    e = torch.stack([b[:, blk % 2, (blk // 2) // 4, (blk // 2) % 4].to(torch.int32) - 127
+                     for blk in range(d // 32)], 1)
+    return _mx6_values(_mx6_unpack(q6), e)
+
+
 def quant_rows_mx4_ref(x: torch.Tensor):
     """MX-fp4 image of 384-wide rows (index_i8.hip quant_rows_mx4): per 32-dim block the scale
     2^ceil(log2(max|x| / 6)) (e8m0 byte e + 127), each element the nearest e2m1 value of x / s,

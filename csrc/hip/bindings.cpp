@@ -84,7 +84,7 @@ int symb_quant_rows_mx4(const void* X, int n, int dim, void* X4, void* SC, float
 int symb_mx4_select(int NQ, const float* T, const float* margin4, const float* margin8,
                     const float* probe_s, int n_cols, int ld, int tile_stride, float rate,
                     const float* tail_cs, int tail_cap, int tail_ld, float limit, float* thr4,
-                    int* nv, hipStream_t st, int nv_zeroed);
+                    int* nv, hipStream_t st, int nv_zeroed, int stage, float wa, float wb);
 int symb_i8_tile_rows_for(int dim, int heavy);
 // the streaming pruning scan (index_stream.hip)
 int symb_stream_rec_bytes(int dim, int form);
@@ -99,13 +99,15 @@ int symb_index_scan_stream(const void* img, int n_valid, int alloc_rows, int row
 int symb_mx4_centroids(const void* Xq, const void* QS, int NQ, int dim, void* C4, void* CS,
                        float* R, hipStream_t st);
 int symb_append_rows(const void* src, int n, int dim, void* rows, int r0, void* img8, float* b8,
-                     void* img4, float* b4, hipStream_t st);
+                     void* img4, float* b4, void* img6, float* b6, hipStream_t st);
 int symb_dense_scores(const void* X, int dim, const int* rows, int n_list, int ts, int div,
                       int r_lo, int n_range, const void* Q, int NQ, float* out, int ld,
                       hipStream_t st);
 int symb_quant_stream_i8(const void* X, int r0, const int* rows, int n, int dim, void* img,
                          float* bounds, hipStream_t st);
 int symb_quant_stream_mx4(const void* X, int r0, const int* rows, int n, int dim, void* img,
+                          void* Xq, void* QS, float* bounds, float* margin, hipStream_t st);
+int symb_quant_stream_mx6(const void* X, int r0, const int* rows, int n, int dim, void* img,
                           void* Xq, void* QS, float* bounds, float* margin, hipStream_t st);
 int symb_i8_split_queries_per_blk(int rsplit);
 int symb_mx4_config(int tile_rows);
@@ -491,7 +493,7 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("dim"), py::arg("form"));
   m.def("stream_config", [](int mx4_variant, int i8_variant, int abl, int land) {
     check(symb_stream_config(mx4_variant, i8_variant, abl, land), "stream_config");
-  }, py::arg("mx4_variant"), py::arg("i8_variant") = 0, py::arg("abl") = 0, py::arg("land") = 1);
+  }, py::arg("mx4_variant"), py::arg("i8_variant") = 0, py::arg("abl") = 0, py::arg("land") = 0);
   m.def("stream_geometry", [](int dim, int form) {
     int qpb = 0, wpc = 0;
     check(symb_stream_geometry(dim, form, &qpb, &wpc), "stream_geometry");
@@ -522,12 +524,13 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("Xq"), py::arg("QS"), py::arg("NQ"), py::arg("dim"), py::arg("C4"), py::arg("CS"),
      py::arg("R"), py::arg("stream"));
   m.def("append_rows", [](uptr src, int n, int dim, uptr rows, int r0, uptr img8, uptr b8,
-                          uptr img4, uptr b4, uptr st) {
+                          uptr img4, uptr b4, uptr st, uptr img6, uptr b6) {
     check(symb_append_rows(P<void>(src), n, dim, P<void>(rows), r0, P<void>(img8), P<float>(b8),
-                           P<void>(img4), P<float>(b4), S(st)),
+                           P<void>(img4), P<float>(b4), P<void>(img6), P<float>(b6), S(st)),
           "append_rows");
   }, py::arg("src"), py::arg("n"), py::arg("dim"), py::arg("rows"), py::arg("r0"),
-     py::arg("img8"), py::arg("b8"), py::arg("img4"), py::arg("b4"), py::arg("stream"));
+     py::arg("img8"), py::arg("b8"), py::arg("img4"), py::arg("b4"), py::arg("stream"),
+     py::arg("img6") = 0, py::arg("b6") = 0);
   m.def("dense_scores", [](uptr X, int dim, uptr rows, int n_list, int r_lo, int n_range, uptr Q,
                            int NQ, uptr out, int ld, uptr st, int ts, int div) {
     check(symb_dense_scores(P<void>(X), dim, P<const int>(rows), n_list, ts, div, r_lo, n_range,
@@ -551,6 +554,14 @@ PYBIND11_MODULE(_hip, m) {
           "quant_stream_mx4");
   }, py::arg("X"), py::arg("r0"), py::arg("rows"), py::arg("n"), py::arg("dim"), py::arg("img"),
      py::arg("Xq"), py::arg("QS"), py::arg("bounds"), py::arg("margin"), py::arg("stream"));
+  m.def("quant_stream_mx6", [](uptr X, int r0, uptr rows, int n, int dim, uptr img, uptr Xq,
+                               uptr QS, uptr bounds, uptr margin, uptr st) {
+    check(symb_quant_stream_mx6(P<void>(X), r0, P<const int>(rows), n, dim, P<void>(img),
+                                P<void>(Xq), P<void>(QS), P<float>(bounds), P<float>(margin),
+                                S(st)),
+          "quant_stream_mx6");
+  }, py::arg("X"), py::arg("r0"), py::arg("rows"), py::arg("n"), py::arg("dim"), py::arg("img"),
+     py::arg("Xq"), py::arg("QS"), py::arg("bounds"), py::arg("margin"), py::arg("stream"));
   m.def("quant_rows_mx4", [](uptr X, int n, int dim, uptr X4, uptr SC, uptr bounds, uptr margin,
                              uptr st) {
     check(symb_quant_rows_mx4(P<void>(X), n, dim, P<void>(X4), P<void>(SC), P<float>(bounds),
@@ -560,16 +571,18 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("margin"), py::arg("stream"));
   m.def("mx4_select", [](int NQ, uptr T, uptr margin4, uptr margin8, uptr probe_s, int n_cols,
                          float rate, uptr tail_cs, int tail_cap, float limit, uptr thr4, uptr nv,
-                         uptr st, int ld, int tile_stride, int tail_ld, bool nv_zeroed) {
+                         uptr st, int ld, int tile_stride, int tail_ld, bool nv_zeroed, int stage,
+                         float wa, float wb) {
     check(symb_mx4_select(NQ, P<const float>(T), P<const float>(margin4), P<const float>(margin8),
                           P<const float>(probe_s), n_cols, ld, tile_stride, rate,
                           P<const float>(tail_cs), tail_cap, tail_ld, limit, P<float>(thr4),
-                          P<int>(nv), S(st), nv_zeroed ? 1 : 0),
+                          P<int>(nv), S(st), nv_zeroed ? 1 : 0, stage, wa, wb),
           "mx4_select");
   }, py::arg("NQ"), py::arg("T"), py::arg("margin4"), py::arg("margin8"), py::arg("probe_s"),
      py::arg("n_cols"), py::arg("rate"), py::arg("tail_cs"), py::arg("tail_cap"), py::arg("limit"),
      py::arg("thr4"), py::arg("nv"), py::arg("stream"), py::arg("ld") = 0,
-     py::arg("tile_stride") = 1, py::arg("tail_ld") = 0, py::arg("nv_zeroed") = false);
+     py::arg("tile_stride") = 1, py::arg("tail_ld") = 0, py::arg("nv_zeroed") = false,
+     py::arg("stage") = 0, py::arg("wa") = 2.f, py::arg("wb") = 0.f);
   m.def("prune_qquant", [](uptr Q, int NQ, int dim, uptr bounds, uptr Q8, uptr sq, uptr margin,
                            uptr st, uptr zero, int zero_n) {
     check(symb_prune_qquant(P<void>(Q), NQ, dim, P<const float>(bounds), P<void>(Q8), P<float>(sq),

@@ -1113,17 +1113,27 @@ __global__ __launch_bounds__(256) void quant_rows_mx4_kernel(const __bf16* __res
 // runs at thr4 = T - margin4).  Exactness never depends on the choice.
 // probe_s: [NQ][ld] exact scores; the probe is columns c < n_cols whose 64-row tile c / 64 is a
 // multiple of tile_stride (1: every column), scaled by `rate`; tail_cs: [NQ][tail_ld].
+// stage (the MX-fp6 tier between the two, margin4 then being the fp6 margin): 0 = the fp4 choice
+// (bit 0 of *nv: fp4 not viable); 1 = the fp6 choice after the fp4 one (nothing when fp4 runs,
+// else bit 1: fp6 not viable); 2 = the fp6 choice alone (bit 0 always, bit 1 as in 1).  The
+// gated scans then want *nv == 0 (fp4), 1 (fp6), 3 (int8).
+// The band counted is [T - wa margin4 - wb margin8, T - margin8): (2, 0) -- the fp4 tier's
+// worst case -- or (1, 1) for the fp6 tier, whose rounding error on a pair is typically ~1/30 of
+// its Cauchy-Schwarz bound (the int8 margin as the allowance: an underestimate only costs the
+// overflow fallback, never exactness).
 __global__ __launch_bounds__(256) void mx4_select_kernel(
     int NQ, const float* __restrict__ T, const float* __restrict__ margin4,
     const float* __restrict__ margin8, const float* __restrict__ probe_s, int n_cols, int ld,
     int tile_stride, float rate, const float* __restrict__ tail_cs, int tail_cap, int tail_ld,
-    float limit, float* __restrict__ thr4, int* __restrict__ nv) {
+    float limit, float* __restrict__ thr4, int* __restrict__ nv, int stage, float wa, float wb) {
   // one 256-thread workgroup per query (a wave per query took 146 us for 256 queries)
   __shared__ float red[2][4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int q = blockIdx.x;
+  if (stage == 1 && (*nv & 1) == 0) return;   // (bit 0 is final: the fp4 choice ran before)
+  if (stage == 2 && q == 0 && threadIdx.x == 0) atomicOr(nv, 1);
   const float t = T[q];
-  const float lo = t - 2.f * margin4[q], hi = t - margin8[q];
+  const float lo = t - wa * margin4[q] - wb * margin8[q], hi = t - margin8[q];
   float c = 0.f;
   const float* ps = probe_s + (size_t)q * ld;
   for (int i = threadIdx.x; i < n_cols; i += 256)
@@ -1142,7 +1152,7 @@ __global__ __launch_bounds__(256) void mx4_select_kernel(
     c = red[0][0] + red[0][1] + red[0][2] + red[0][3];
     tc = red[1][0] + red[1][1] + red[1][2] + red[1][3];
     thr4[q] = t - margin4[q];
-    if (!(c * rate + tc <= limit)) atomicOr(nv, 1);
+    if (!(c * rate + tc <= limit)) atomicOr(nv, stage ? 2 : 1);
   }
 }
 
@@ -1530,8 +1540,9 @@ int symb_quant_rows_mx4(const void* X, int n, int dim, void* X4, void* SC, float
 int symb_mx4_select(int NQ, const float* T, const float* margin4, const float* margin8,
                     const float* probe_s, int n_cols, int ld, int tile_stride, float rate,
                     const float* tail_cs, int tail_cap, int tail_ld, float limit, float* thr4,
-                    int* nv, hipStream_t st, int nv_zeroed) {
+                    int* nv, hipStream_t st, int nv_zeroed, int stage, float wa, float wb) {
   if (NQ <= 0) return 0;
+  if (stage < 0 || stage > 2 || (stage == 1 && !nv_zeroed)) return -1;
   if (ld <= 0) ld = n_cols;
   if (tail_ld <= 0) tail_ld = tail_cap;
   if (n_cols <= 0 || ld < n_cols || tile_stride < 1 || tail_cap < 0 || tail_ld < tail_cap ||
@@ -1543,7 +1554,7 @@ int symb_mx4_select(int NQ, const float* T, const float* margin4, const float* m
   }
   hipLaunchKernelGGL(mx4_select_kernel, dim3(NQ), dim3(256), 0, st, NQ, T, margin4, margin8,
                      probe_s, n_cols, ld, tile_stride, rate, tail_cs, tail_cap, tail_ld, limit,
-                     thr4, nv);
+                     thr4, nv, stage, wa, wb);
   return (int)hipGetLastError();
 }
 

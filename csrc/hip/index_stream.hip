@@ -35,21 +35,25 @@
 
 namespace symb {
 
-enum : int { SF_I8 = 0, SF_MX4 = 1 };
+enum : int { SF_I8 = 0, SF_MX4 = 1, SF_MX6 = 2 };
 
 typedef __attribute__((ext_vector_type(4))) int i32x4s;
+typedef __attribute__((ext_vector_type(6))) int i32x6s;
+typedef int i32x3a __attribute__((ext_vector_type(3), aligned(4)));   // a 12-byte, dword-aligned piece
 typedef __attribute__((ext_vector_type(8))) int i32x8s;
 typedef __attribute__((ext_vector_type(16))) int i32x16s;
 typedef __attribute__((ext_vector_type(16))) float f32x16s;
 
 template <int FMT, int D>
 struct SDim {
-  static constexpr int KE = FMT == SF_MX4 ? 64 : 32;            // k elements per 32-byte k-step
+  static constexpr int KE = FMT == SF_I8 ? 32 : 64;             // k elements per MFMA k-step
   static constexpr int NKS = D / KE;                             // k-steps per row
-  static constexpr int RB = NKS * 32;                            // image bytes per row
-  static constexpr int NSC = FMT == SF_MX4 ? (NKS + 3) / 4 : 0;  // block-scale dwords per lane
+  static constexpr int LB = FMT == SF_MX6 ? 24 : 16;              // bytes per lane per k-step
+  static constexpr int RB = NKS * 2 * LB;                        // (query) image bytes per row
+  static constexpr int NSC = FMT == SF_I8 ? 0 : (NKS + 3) / 4;   // block-scale dwords per lane
   static constexpr int HDR = FMT == SF_I8 ? 128 : 0;             // row scales (int8)
-  static constexpr int FRAG = NKS * 1024;
+  // per k-step 64 lanes x LB bytes; MX-fp6: two 768-byte planes of 12 bytes per lane
+  static constexpr int FRAG = NKS * 64 * LB;
   static constexpr int REC = HDR + FRAG + NSC * 256;             // bytes per 32-row sub-tile
   static_assert(D % KE == 0 && (D == 384 || D == 768 || D == 1024), "stream image row width");
 };
@@ -64,6 +68,7 @@ struct SGeo {
   // wider rows hold fewer resident sets (1024: int8 one set, 4 waves = 128 queries per workgroup).
   // V 2 / 3: the default form one sub-tile deeper / shallower in flight (A/B).
   static constexpr int SETS = FMT == SF_MX4 ? (D == 384 && V != 1 ? 8 : D == 1024 ? 2 : 4)
+                            : FMT == SF_MX6 ? (D == 384 ? 4 : 2)
                                             : (D == 384 ? 4 : D == 768 ? 2 : 1);
   static constexpr int NW0 = 256 / (SETS * 32) > 0 ? 256 / (SETS * 32) : 1;
   static constexpr int NW = NW0 > 4 ? 4 : NW0;
@@ -78,8 +83,8 @@ struct SGeo {
   static constexpr int LHDR = FMT == SF_I8 ? 256 : 0;   // the header's LDS bytes (DMA: 4 B x 64 lanes)
   static constexpr int SLOT = (SDim<FMT, D>::REC - SDim<FMT, D>::HDR + LHDR + 1023) / 1024 * 1024;
   static constexpr int LDEPTH = FMT == SF_MX4 && D == 384 ? 4 : 2;
-  static constexpr bool LAND_OK = D == 384 || (D == 768 && FMT == SF_MX4);
-  static_assert(SETS * NKS * 4 <= 192, "resident query operands");
+  static constexpr bool LAND_OK = FMT != SF_MX6 && (D == 384 || (D == 768 && FMT == SF_MX4));
+  static_assert(SETS * NKS * SDim<FMT, D>::LB / 4 <= 192, "resident query operands");
   static_assert(NW >= 1 && NW <= 4, "waves per workgroup");
 };
 
@@ -143,19 +148,31 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
 
   // ---- resident queries: B operand of set s, k-step ks = query qw + 32 s + (lane & 31), bytes
   //      32 ks + 16 h .. + 16 of its row-major image ----
-  i32x4s qf[SETS][NKS];
+  using FragT = std::conditional_t<FMT == SF_MX6, i32x6s, i32x4s>;
+  // a k-step's lane piece: 16 bytes, or (MX-fp6) 24 bytes as two dword-aligned 12-byte halves
+  auto frag_at = [](const uint8_t* p, int second) -> FragT {
+    if constexpr (FMT == SF_MX6) {
+      const i32x3a a = *reinterpret_cast<const i32x3a*>(p);
+      const i32x3a b = *reinterpret_cast<const i32x3a*>(p + second);
+      return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5);
+    } else {
+      (void)second;
+      return *reinterpret_cast<const i32x4s*>(p);
+    }
+  };
+  FragT qf[SETS][NKS];
   uint32_t qs[SETS][NSC];
   float thr[SETS];
 #pragma unroll
   for (int s = 0; s < SETS; ++s) {
     const int q = qw + 32 * s + (lane & 31);
     const int qq = min(q, NQ - 1);
-    const uint8_t* qp = Q + (size_t)qq * S::RB + 16 * h;
+    const uint8_t* qp = Q + (size_t)qq * S::RB + S::LB * h;
 #pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) qf[s][ks] = *reinterpret_cast<const i32x4s*>(qp + 32 * ks);
+    for (int ks = 0; ks < NKS; ++ks) qf[s][ks] = frag_at(qp + 2 * S::LB * ks, 12);
 #pragma unroll
     for (int j = 0; j < NSC; ++j) {
-      if constexpr (FMT == SF_MX4)
+      if constexpr (FMT != SF_I8)
         qs[s][j] = qsc[(size_t)qq * 2 * NSC + h * NSC + j];
       else
         qs[s][j] = 0u;
@@ -215,7 +232,7 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
 
   // ---- the sub-tile ring: fragments (+ row scales / block scales) of DEPTH sub-tiles ----
   const uint8_t* rec0 = img + (size_t)g0 * REC;
-  i32x4s fk[DEPTH][NKS];
+  FragT fk[DEPTH][NKS];
   uint32_t fsc[DEPTH][NSC];
   f32x4 frs[DEPTH][FMT == SF_I8 ? 4 : 1];
   auto load = [&](auto dc, int i) {
@@ -226,10 +243,11 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
 #pragma unroll
       for (int c = 0; c < 4; ++c) frs[d][c] = sp[c];
     }
-    const uint8_t* f = r + S::HDR + 16 * lane;
+    // (MX-fp6: lane l's 24 bytes are 12 in the k-step's first 768-byte plane and 12 in its second)
+    const uint8_t* f = r + S::HDR + (FMT == SF_MX6 ? 12 : 16) * lane;
 #pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) fk[d][ks] = *reinterpret_cast<const i32x4s*>(f + 1024 * ks);
-    if constexpr (FMT == SF_MX4) {
+    for (int ks = 0; ks < NKS; ++ks) fk[d][ks] = frag_at(f + 64 * S::LB * ks, 768);
+    if constexpr (FMT != SF_I8) {
 #pragma unroll
       for (int j = 0; j < NSC; ++j)
         fsc[d][j] = *reinterpret_cast<const uint32_t*>(r + S::FRAG + 256 * j + 4 * lane);
@@ -246,6 +264,18 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
         const i32x8s a = __builtin_shufflevector(fk[d][ks], (i32x4s){0, 0, 0, 0}, 0, 1, 2, 3, 4, 5, 6, 7);
         const i32x8s b = __builtin_shufflevector(qf[s][ks], (i32x4s){0, 0, 0, 0}, 0, 1, 2, 3, 4, 5, 6, 7);
         acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, acc, 4, 4, ks & 3,
+                                                              (int)fsc[d][ks >> 2], ks & 3,
+                                                              (int)qs[s][ks >> 2]);
+      });
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = acc[r];
+    } else if constexpr (FMT == SF_MX6) {   // e2m3 x e2m3 (cbsz / blgp 2), six-dword operands
+      f32x16s acc = {};
+      static_for<0, NKS>([&](auto kc) {
+        constexpr int ks = decltype(kc)::value;
+        const i32x8s a = __builtin_shufflevector(fk[d][ks], fk[d][ks], 0, 1, 2, 3, 4, 5, -1, -1);
+        const i32x8s b = __builtin_shufflevector(qf[s][ks], qf[s][ks], 0, 1, 2, 3, 4, 5, -1, -1);
+        acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, acc, 2, 2, ks & 3,
                                                               (int)fsc[d][ks >> 2], ks & 3,
                                                               (int)qs[s][ks >> 2]);
       });
@@ -477,21 +507,58 @@ __device__ __forceinline__ int e2m1_code_s(float a, float& q) {   // a = |x| / s
   return c;
 }
 
-// One row's MX-fp4 image: every 32-dim block b gets s_b = 2^ceil(log2(max |x_b| / 6)) (an e8m0
-// byte) and each element the nearest OCP e2m1 value of x / s_b, two per byte (element 2 j in the
-// low nibble of byte j) -- quant_rows_mx4_kernel's numbers.  One wave, lane l holds dims l + 64 m.
-// Xq == nullptr: into the stream image img at row `row`; else the query layout: row-major nibbles
-// Xq [.][D / 2] and the scale record QS [.][2 NSC] dwords (dword h NSC + j, byte b = block
-// 2 (4 j + b) + h: the scan's per-lane B scales).  en / nn / xn = |x - x~| / |x~| / |x|.
-template <int D>
-__device__ __forceinline__ void mx4_stream_row(const __bf16* __restrict__ xrow, int row,
-                                               uint8_t* __restrict__ img, uint8_t* __restrict__ Xq,
-                                               uint32_t* __restrict__ QS, float& en, float& nn,
-                                               float& xn) {
-  using S = SDim<SF_MX4, D>;
+__device__ __forceinline__ void store3(uint8_t* p, uint32_t v) {   // bytes 0-2 of v, little-endian
+  p[0] = (uint8_t)v;
+  p[1] = (uint8_t)(v >> 8);
+  p[2] = (uint8_t)(v >> 16);
+}
+
+__device__ __forceinline__ int e2m3_code_s(float a, float& q) {   // a = |x| / s <= 7.5
+  // OCP e2m3 (bias 1): code 8 E + m; steps 1/8 below 2, 1/4 below 4, 1/2 up to 7.5
+  if (a < 2.f) {
+    q = rintf(a * 8.f) * 0.125f;
+    return (int)(q * 8.f);               // 0 .. 16 (16 = 2.0)
+  }
+  if (a < 4.f) {
+    q = rintf(a * 4.f) * 0.25f;
+    return (int)(q * 4.f) + 8;           // 16 .. 24
+  }
+  q = fminf(rintf(a * 2.f) * 0.5f, 7.5f);
+  return (int)(q * 2.f) + 16;            // 24 .. 31
+}
+
+// e8m0 exponent of an MX block: the smallest e with amax <= top 2^e (top = the element format's
+// largest value: 6 for e2m1, 7.5 for e2m3); -127 for an all-zero block
+__device__ __forceinline__ int mx_block_exp(float amax, float top) {
+  if (!(amax > 0.f)) return -127;
+  int k;
+  frexpf(amax / top, &k);                // amax / top in [2^(k-1), 2^k)
+  int e = k;
+  if (amax <= top * ldexpf(1.f, k - 1)) e = k - 1;
+  if (amax > top * ldexpf(1.f, e)) ++e;  // (guard the division's rounding)
+  return max(e, -127);
+}
+
+// One row's MX image (FMT SF_MX4: OCP e2m1 nibbles, SF_MX6: OCP e2m3 6-bit codes): every 32-dim
+// block b gets s_b = 2^ceil(log2(max |x_b| / top)) (an e8m0 byte) and each element the nearest
+// code of x / s_b -- quant_rows_mx4_kernel's numbers for fp4.  Codes are packed little-endian per
+// lane piece (element j of a block at bits [w j, w j + w), w = 4 / 6).  One wave, lane l holds
+// dims l + 64 m (block 2 m + (l >> 5), element l & 31).
+// Xq == nullptr: into the stream image img at row `row` (fp6: the piece's bytes 0-11 in the
+// k-step's first 768-byte plane, 12-23 in its second); else the query layout: row-major pieces
+// Xq [.][RB] (RB = D / 2 or 3 D / 4 bytes) and the scale record QS [.][2 NSC] dwords (dword
+// h NSC + j, byte b = block 2 (4 j + b) + h: the scan's per-lane B scales).
+// en / nn / xn = |x - x~| / |x~| / |x|.
+template <int FMT, int D, bool QUERY>
+__device__ __forceinline__ void mx_stream_row(const __bf16* __restrict__ xrow, int row,
+                                              uint8_t* __restrict__ img, uint8_t* __restrict__ Xq,
+                                              uint32_t* __restrict__ QS, float& en, float& nn,
+                                              float& xn) {
+  using S = SDim<FMT, D>;
   constexpr int M = D / 64, NSC = S::NSC;
-  const int lane = threadIdx.x & 63;
-  const bool query = Xq != nullptr;
+  constexpr float TOP = FMT == SF_MX6 ? 7.5f : 6.f;
+  const int lane = threadIdx.x & 63, j = lane & 31, hh = lane >> 5;
+  constexpr bool query = QUERY;
   const uint16_t* xp = reinterpret_cast<const uint16_t*>(xrow);
   // this row's scale record (queries): half 0's words built in lanes 0-31, half 1's in 32-63
   uint32_t scw[NSC];
@@ -502,41 +569,54 @@ __device__ __forceinline__ void mx4_stream_row(const __bf16* __restrict__ xrow, 
   for (int m = 0; m < M; ++m) {
     const float x = __uint_as_float((uint32_t)xp[lane + 64 * m] << 16);
     const float amax = half_max32(fabsf(x));
-    int e = -127;
-    if (amax > 0.f) {
-      int k;
-      frexpf(amax / 6.f, &k);              // amax / 6 in [2^(k-1), 2^k)
-      e = k;
-      if (amax <= 6.f * ldexpf(1.f, k - 1)) e = k - 1;
-      if (amax > 6.f * ldexpf(1.f, e)) ++e;   // (guard the division's rounding)
-      e = max(e, -127);
-    }
+    const int e = mx_block_exp(amax, TOP);
     const float sc = ldexpf(1.f, e);
-    float qv;
-    const int c = amax > 0.f ? e2m1_code_s(fabsf(x) * ldexpf(1.f, -e), qv) : (qv = 0.f, 0);
-    const int code = c | (x < 0.f && c ? 8 : 0);
+    float qv = 0.f;
+    int c = 0;
+    if (amax > 0.f) {
+      if constexpr (FMT == SF_MX6) c = e2m3_code_s(fabsf(x) * ldexpf(1.f, -e), qv);
+      else c = e2m1_code_s(fabsf(x) * ldexpf(1.f, -e), qv);
+    }
+    const int code = c | (x < 0.f && c ? (FMT == SF_MX6 ? 32 : 8) : 0);
     const float xt = (x < 0.f ? -qv : qv) * sc;
     e2 += (x - xt) * (x - xt);
     n2 += xt * xt;
     x2 += x * x;
-    const int hi = __shfl_down(code, 1);
-    const int hh = lane >> 5;                // this half-wave's block 2 m + hh: k-step m
-    const uint8_t byte = (uint8_t)(code | (hi << 4));
-    const int bj = (lane >> 1) + 32 * m;     // row byte of the even lane's pair
-    if (query) {
-      if ((lane & 1) == 0) Xq[(size_t)row * (D / 2) + bj] = byte;
-      scw[m >> 2] |= (uint32_t)(e + 127) << (8 * (m & 3));
+    if constexpr (FMT == SF_MX6) {
+      // 4 codes = 3 bytes, written by the group's first lane (byte 3 (j / 4) of the piece)
+      const uint32_t v = (uint32_t)code | ((uint32_t)__shfl_down(code, 1) << 6) |
+                         ((uint32_t)__shfl_down(code, 2) << 12) |
+                         ((uint32_t)__shfl_down(code, 3) << 18);
+      // (QUERY a template argument: both stores in one function crashed hipcc's inliner)
+      if ((j & 3) == 0) {
+        const int g = j >> 2;
+        if constexpr (query)
+          store3(Xq + (size_t)row * S::RB + 48 * m + 24 * hh + 3 * g, v);
+        else
+          store3(img + (size_t)(row >> 5) * S::REC + 1536 * m + 768 * (g >> 2) +
+                     12 * (32 * hh + (row & 31)) + 3 * (g & 3),
+                 v);
+      }
     } else {
-      if ((lane & 1) == 0) img[stream_frag_off(S::REC, 0, row, bj)] = byte;
-      if ((lane & 31) == 0)
-        img[(size_t)(row >> 5) * S::REC + S::FRAG + 256 * (m >> 2) + 4 * (32 * hh + (row & 31)) +
-            (m & 3)] = (uint8_t)(e + 127);
+      const int hi = __shfl_down(code, 1);
+      const uint8_t byte = (uint8_t)(code | (hi << 4));
+      const int bj = (lane >> 1) + 32 * m;     // row byte of the even lane's pair
+      if ((lane & 1) == 0) {
+        if constexpr (query) Xq[(size_t)row * (D / 2) + bj] = byte;
+        else img[stream_frag_off(S::REC, 0, row, bj)] = byte;
+      }
+    }
+    if constexpr (query) {
+      scw[m >> 2] |= (uint32_t)(e + 127) << (8 * (m & 3));
+    } else if (j == 0) {
+      img[(size_t)(row >> 5) * S::REC + S::FRAG + 256 * (m >> 2) + 4 * (32 * hh + (row & 31)) +
+          (m & 3)] = (uint8_t)(e + 127);
     }
   }
   en = sqrtf(wave_sum(e2));
   nn = sqrtf(wave_sum(n2));
   xn = sqrtf(wave_sum(x2));
-  if (query) {
+  if constexpr (query) {
     // lanes 0 and 32 built the two halves' scale words (identical within a half-wave)
 #pragma unroll
     for (int i = 0; i < NSC; ++i) {
@@ -547,6 +627,15 @@ __device__ __forceinline__ void mx4_stream_row(const __bf16* __restrict__ xrow, 
       }
     }
   }
+}
+
+template <int D>
+__device__ __forceinline__ void mx4_stream_row(const __bf16* __restrict__ xrow, int row,
+                                               uint8_t* __restrict__ img, uint8_t* __restrict__ Xq,
+                                               uint32_t* __restrict__ QS, float& en, float& nn,
+                                               float& xn) {
+  if (Xq != nullptr) mx_stream_row<SF_MX4, D, true>(xrow, row, img, Xq, QS, en, nn, xn);
+  else mx_stream_row<SF_MX4, D, false>(xrow, row, img, Xq, QS, en, nn, xn);
 }
 
 __device__ __forceinline__ float e2m1_value(int c) {   // 4-bit code (sign bit 3) -> value
@@ -596,15 +685,7 @@ __global__ __launch_bounds__(64) void mx4_centroids_kernel(const uint8_t* __rest
   for (int m = 0; m < M; ++m) {
     const float x = c[m] / (float)max(nq, 1);
     const float amax = half_max32(fabsf(x));
-    int e = -127;
-    if (amax > 0.f) {
-      int k;
-      frexpf(amax / 6.f, &k);
-      e = k;
-      if (amax <= 6.f * ldexpf(1.f, k - 1)) e = k - 1;
-      if (amax > 6.f * ldexpf(1.f, e)) ++e;
-      e = max(e, -127);
-    }
+    const int e = mx_block_exp(amax, 6.f);
     float qv;
     const int cd = amax > 0.f ? e2m1_code_s(fabsf(x) * ldexpf(1.f, -e), qv) : (qv = 0.f, 0);
     const int code = cd | (x < 0.f && cd ? 8 : 0);
@@ -666,11 +747,11 @@ __global__ __launch_bounds__(256) void quant_stream_i8_kernel(const __bf16* __re
   raise_bounds2(bounds, en, nn);
 }
 
-// MX-fp4 stream image of bf16 rows (margin == nullptr: rows [r0, r0 + n) or the listed rows into
-// img, bounds[0..1] raised to (E4, X4)) or the query image (margin != nullptr: Xq / QS for rows
-// 0 .. n - 1 and margin = |q| E4 + |q - q~| X4 + 1e-5 from bounds).  One wave per row.
-template <int D>
-__global__ __launch_bounds__(256) void quant_stream_mx4_kernel(
+// MX-fp4 / MX-fp6 stream image of bf16 rows (margin == nullptr: rows [r0, r0 + n) or the listed
+// rows into img, bounds[0..1] raised to (E, X)) or the query image (margin != nullptr: Xq / QS for
+// rows 0 .. n - 1 and margin = |q| E + |q - q~| X + 1e-5 from bounds).  One wave per row.
+template <int FMT, int D>
+__global__ __launch_bounds__(256) void quant_stream_mx_kernel(
     const __bf16* __restrict__ X, int r0, const int* __restrict__ rows, int n,
     uint8_t* __restrict__ img, uint8_t* __restrict__ Xq, uint32_t* __restrict__ QS,
     float* __restrict__ bounds, float* __restrict__ margin) {
@@ -679,29 +760,31 @@ __global__ __launch_bounds__(256) void quant_stream_mx4_kernel(
   float en = 0.f, nn = 0.f, xn = 0.f;
   if (query) {
     if (j >= n) return;   // (no barrier on the query path)
-    mx4_stream_row<D>(X + (size_t)j * D, j, nullptr, Xq, QS, en, nn, xn);
+    mx_stream_row<FMT, D, true>(X + (size_t)j * D, j, nullptr, Xq, QS, en, nn, xn);
     if ((threadIdx.x & 63) == 0) margin[j] = xn * bounds[0] + en * bounds[1] + 1e-5f;
     return;
   }
   if (j < n) {
     const int row = rows ? rows[j] : r0 + j;
-    mx4_stream_row<D>(X + (size_t)row * D, row, img, nullptr, nullptr, en, nn, xn);
+    mx_stream_row<FMT, D, false>(X + (size_t)row * D, row, img, nullptr, nullptr, en, nn, xn);
   }
   raise_bounds2(bounds, en, nn);
 }
 
 // An append of n unit bf16 rows at row r0 in one launch: the rows themselves (src -> rows), their
-// int8 stream image (img8, bounds b8[0..1]) and their MX-fp4 stream image (img4, bounds b4[0..1])
-// -- either image may be absent (nullptr).  One wave per row.
-template <int D>
+// int8 stream image (img8, bounds b8[0..1]), MX-fp4 stream image (img4, bounds b4[0..1]) and
+// MX-fp6 stream image (img6, b6) -- any image may be absent (nullptr).  One wave per row.
+template <int D, bool FP6>
 __global__ __launch_bounds__(256) void append_rows_kernel(const __bf16* __restrict__ src, int n,
                                                           __bf16* __restrict__ rows, int r0,
                                                           uint8_t* __restrict__ img8,
                                                           float* __restrict__ b8,
                                                           uint8_t* __restrict__ img4,
-                                                          float* __restrict__ b4) {
+                                                          float* __restrict__ b4,
+                                                          uint8_t* __restrict__ img6,
+                                                          float* __restrict__ b6) {
   const int j = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  float e8 = 0.f, n8 = 0.f, e4 = 0.f, n4 = 0.f, x4 = 0.f;
+  float e8 = 0.f, n8 = 0.f, e4 = 0.f, n4 = 0.f, x4 = 0.f, e6 = 0.f, n6 = 0.f;
   if (j < n) {
     const __bf16* xr = src + (size_t)j * D;
     // the bf16 row: D * 2 bytes as 4-byte words, D / 128 per lane
@@ -711,10 +794,15 @@ __global__ __launch_bounds__(256) void append_rows_kernel(const __bf16* __restri
     for (int i = 0; i < D / 128; ++i) dp[lane + 64 * i] = sp[lane + 64 * i];
     if (img8) i8_stream_row<D>(xr, r0 + j, img8, e8, n8);
     if (img4) mx4_stream_row<D>(xr, r0 + j, img4, nullptr, nullptr, e4, n4, x4);
+    if constexpr (FP6) mx_stream_row<SF_MX6, D, false>(xr, r0 + j, img6, nullptr, nullptr, e6, n6, x4);
   }
   if (b8) raise_bounds2(b8, e8, n8);
   __syncthreads();   // (raise_bounds2's LDS reused)
   if (b4) raise_bounds2(b4, e4, n4);
+  if constexpr (FP6) {
+    __syncthreads();
+    raise_bounds2(b6, e6, n6);
+  }
 }
 
 // Probe of one v_mfma_scale_f32_32x32x64_f8f6f4 (tests: the operand bit layouts of the f8f6f4
@@ -755,11 +843,15 @@ int symb_mfma_f8f6f4_probe(const int* a, const int* b, const int* sa, const int*
   return (int)hipGetLastError();
 }
 
-// bytes per 32-row sub-tile of the stream image (form 0 = int8, 1 = MX-fp4); 0 = unsupported
+// bytes per 32-row sub-tile of the stream image (form 0 = int8, 1 = MX-fp4, 2 = MX-fp6);
+// 0 = unsupported
 int symb_stream_rec_bytes(int dim, int form) {
-  if (dim == 384) return form ? SDim<SF_MX4, 384>::REC : SDim<SF_I8, 384>::REC;
-  if (dim == 768) return form ? SDim<SF_MX4, 768>::REC : SDim<SF_I8, 768>::REC;
-  if (dim == 1024) return form ? SDim<SF_MX4, 1024>::REC : SDim<SF_I8, 1024>::REC;
+#define R_(D_) (form == 2 ? SDim<SF_MX6, D_>::REC : form ? SDim<SF_MX4, D_>::REC : SDim<SF_I8, D_>::REC)
+  if (form < 0 || form > 2) return 0;
+  if (dim == 384) return R_(384);
+  if (dim == 768) return R_(768);
+  if (dim == 1024) return form == 2 ? 0 : R_(1024);
+#undef R_
   return 0;
 }
 
@@ -767,7 +859,7 @@ int symb_stream_rec_bytes(int dim, int form) {
 // wave x 2 waves, 2 / 3 = one sub-tile deeper / shallower in flight (register ring, D = 384);
 // abl: the kernel's timing ablations (ABL above; wrong results); land: the LDS-landing form where
 // it is sized (int8 / MX-fp4 384, MX-fp4 768; variant 0)
-static int g_stream_mx4_v = 0, g_stream_i8_v = 0, g_stream_abl = 0, g_stream_land = 1;
+static int g_stream_mx4_v = 0, g_stream_i8_v = 0, g_stream_abl = 0, g_stream_land = 0;
 int symb_stream_config(int mx4_variant, int i8_variant, int abl, int land) {
   if (mx4_variant < 0 || mx4_variant > 3 || (i8_variant != 0 && i8_variant != 2 && i8_variant != 3) ||
       abl < 0 || abl > 2 || land < 0 || land > 1)
@@ -788,14 +880,17 @@ int symb_stream_geometry(int dim, int form, int* qpb, int* wgs_per_cu) {
     return 0;                                        \
   } while (0)
   if (dim == 384) {
+    if (form == 2) G_(SF_MX6, 384, 0);
     if (form && g_stream_mx4_v == 1) G_(SF_MX4, 384, 1);
     if (form) G_(SF_MX4, 384, 0);
     G_(SF_I8, 384, 0);
   }
   if (dim == 768) {
+    if (form == 2) G_(SF_MX6, 768, 0);
     if (form) G_(SF_MX4, 768, 0);
     G_(SF_I8, 768, 0);
   }
+  if (form == 2) return -1;
   if (dim == 1024) {
     if (form) G_(SF_MX4, 1024, 0);
     G_(SF_I8, 1024, 0);
@@ -844,8 +939,9 @@ int symb_index_scan_stream(const void* img, int n_valid, int alloc_rows, int row
   if (cent4 != nullptr && (form != 1 || centqs == nullptr || centR == nullptr || bounds4 == nullptr))
     return -1;
   const CentArgs ca{cent4, centqs, centR, bounds4};
-  if ((dim != 384 && dim != 768 && dim != 1024) || (form != 0 && form != 1)) return -1;
-  if (form == 1 && qsc == nullptr) return -1;
+  if ((dim != 384 && dim != 768 && dim != 1024) || form < 0 || form > 2) return -1;
+  if (form == 2 && dim == 1024) return -1;
+  if (form != 0 && qsc == nullptr) return -1;
   if (rows_per_blk % 32 || n_rblk <= 0 || thr == nullptr || cap <= 0 || n_valid <= 0) return -1;
   if ((long long)n_rblk * rows_per_blk < n_valid) return -1;
   if (alloc_rows % 32 || (long long)(n_valid + 31) / 32 * 32 > alloc_rows) return -1;
@@ -860,6 +956,7 @@ int symb_index_scan_stream(const void* img, int n_valid, int alloc_rows, int row
 #define LA(F, D_, A_, L_) launch_stream<F, D_, 0, A_, L_>(img, n_valid, rows_per_blk, n_rblk, Q, qsc, \
                                                           NQ, thr, cand_s, cand_i, cand_n, cap, xcd, \
                                                           st, skip, gate, gate_want, runs, ca)
+  if (form == 2) return dim == 384 ? L(SF_MX6, 384, 0) : L(SF_MX6, 768, 0);
   if (dim == 768 && form == 1 && land) return LA(SF_MX4, 768, 0, 1);
   if (dim == 384) {
     if (g_stream_abl == 1)
@@ -906,18 +1003,25 @@ int symb_mx4_centroids(const void* Xq, const void* QS, int NQ, int dim, void* C4
   return (int)hipGetLastError();
 }
 
-// Append n unit bf16 rows (src) at row r0 of the shard: rows, int8 stream image (img8 / b8) and
-// MX-fp4 stream image (img4 / b4); an image pointer may be nullptr (then its bounds too).
+// Append n unit bf16 rows (src) at row r0 of the shard: rows, int8 stream image (img8 / b8),
+// MX-fp4 stream image (img4 / b4) and MX-fp6 stream image (img6 / b6, not at 1024); an image
+// pointer may be nullptr (then its bounds too).
 int symb_append_rows(const void* src, int n, int dim, void* rows, int r0, void* img8, float* b8,
-                     void* img4, float* b4, hipStream_t st) {
+                     void* img4, float* b4, void* img6, float* b6, hipStream_t st) {
   if (n <= 0) return 0;
-  if (r0 < 0 || rows == nullptr || src == nullptr || (img8 && !b8) || (img4 && !b4)) return -1;
-#define L(D_) hipLaunchKernelGGL(append_rows_kernel<D_>, dim3((n + 3) / 4), dim3(256), 0, st,      \
-                                 (const __bf16*)src, n, (__bf16*)rows, r0, (uint8_t*)img8, b8,    \
-                                 (uint8_t*)img4, b4)
-  if (dim == 384) L(384);
-  else if (dim == 768) L(768);
-  else if (dim == 1024) L(1024);
+  if (r0 < 0 || rows == nullptr || src == nullptr || (img8 && !b8) || (img4 && !b4) ||
+      (img6 && !b6) || (img6 && dim == 1024))
+    return -1;
+#define L(D_, F_) hipLaunchKernelGGL((append_rows_kernel<D_, F_>), dim3((n + 3) / 4), dim3(256), 0,  \
+                                     st, (const __bf16*)src, n, (__bf16*)rows, r0, (uint8_t*)img8, \
+                                     b8, (uint8_t*)img4, b4, (uint8_t*)img6, b6)
+  if (dim == 384) {
+    if (img6) L(384, true);
+    else L(384, false);
+  } else if (dim == 768) {
+    if (img6) L(768, true);
+    else L(768, false);
+  } else if (dim == 1024) L(1024, false);
   else return -1;
 #undef L
   return (int)hipGetLastError();
@@ -947,12 +1051,31 @@ int symb_quant_stream_mx4(const void* X, int r0, const int* rows, int n, int dim
   if (margin == nullptr ? (img == nullptr || (rows == nullptr && r0 < 0))
                         : (Xq == nullptr || QS == nullptr))
     return -1;
-#define L(D_) hipLaunchKernelGGL(quant_stream_mx4_kernel<D_>, dim3((n + 3) / 4), dim3(256), 0, st, \
-                                 (const __bf16*)X, r0, rows, n, (uint8_t*)img, (uint8_t*)Xq,       \
+#define L(D_) hipLaunchKernelGGL((quant_stream_mx_kernel<SF_MX4, D_>), dim3((n + 3) / 4), dim3(256), \
+                                 0, st, (const __bf16*)X, r0, rows, n, (uint8_t*)img, (uint8_t*)Xq, \
                                  (uint32_t*)QS, bounds, margin)
   if (dim == 384) L(384);
   else if (dim == 768) L(768);
   else if (dim == 1024) L(1024);
+  else return -1;
+#undef L
+  return (int)hipGetLastError();
+}
+
+// MX-fp6 (e2m3) stream image, as symb_quant_stream_mx4 (query image Xq [n][3 dim / 4] bytes; the
+// row image's 24-byte lane pieces split over two 768-byte planes per k-step; dim 384 / 768).
+int symb_quant_stream_mx6(const void* X, int r0, const int* rows, int n, int dim, void* img,
+                          void* Xq, void* QS, float* bounds, float* margin, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (bounds == nullptr) return -1;
+  if (margin == nullptr ? (img == nullptr || (rows == nullptr && r0 < 0))
+                        : (Xq == nullptr || QS == nullptr))
+    return -1;
+#define L(D_) hipLaunchKernelGGL((quant_stream_mx_kernel<SF_MX6, D_>), dim3((n + 3) / 4), dim3(256), \
+                                 0, st, (const __bf16*)X, r0, rows, n, (uint8_t*)img, (uint8_t*)Xq, \
+                                 (uint32_t*)QS, bounds, margin)
+  if (dim == 384) L(384);
+  else if (dim == 768) L(768);
   else return -1;
 #undef L
   return (int)hipGetLastError();

@@ -607,6 +607,69 @@ def test_mx4_image_follows_writes_and_bounds_every_pair(stream, D, monkeypatch):
     assert ((s - est).abs() <= m4[:, None]).all()
 
 
+def test_e2m3_grid_and_codes():
+    """The e2m3 value table (OCP MX: bias 1, 3 mantissa bits, max 7.5) and the quantiser's rounding:
+    every code decodes back to itself, x / s lands on the nearest grid value."""
+    from codename_symbiont_amd.ops import reference as R
+
+    grid = torch.tensor(R.E2M3)
+    assert grid[0] == 0 and grid[7] == 0.875 and grid[8] == 1.0 and grid[16] == 2.0
+    assert grid[24] == 4.0 and grid[31] == 7.5 and bool((grid[1:] > grid[:-1]).all())
+    x = torch.randn(64, 384, generator=torch.Generator().manual_seed(1))
+    codes, e, xt, nr = R.mx6_codes_ref(x)
+    assert int(codes.max()) < 64 and torch.equal(R._mx6_unpack(R._mx6_pack(codes)), codes.long())
+    s = torch.ldexp(torch.ones_like(e, dtype=torch.float32), e).repeat_interleave(32, 1)
+    a = (x / s).abs()
+    assert float(a.max()) <= 7.5
+    near = (a[..., None] - grid).abs().min(-1).values
+    assert bool(((xt / s).abs() - a).abs().le(near + 1e-6).all())
+    # ~4x finer than MX-fp4, ~4x coarser than per-row int8 on gaussian rows
+    e4 = R.mx4_codes_ref(x)[3][:, 0] / nr[:, 2]
+    e8 = R.quant_rows_i8_ref(x)[2] / nr[:, 2]
+    e6 = nr[:, 0] / nr[:, 2]
+    assert 2.5 < float(e4.mean() / e6.mean()) < 6 and 2 < float(e6.mean() / e8.mean()) < 8
+
+
+@pytest.mark.parametrize("D", [384, 768])
+def test_mx6_image_follows_writes_and_bounds_every_pair(D, monkeypatch):
+    """The MX-fp6 middle-tier stream image (e2m3 codes in two 768-byte planes per k-step + e8m0
+    block scales) follows appends and scattered overwrites, its (E6, X6) cover every row written,
+    and |q.x - q~.x~| stays within |q| E6 + |q - q~| X6 for every (query, row) pair."""
+    from codename_symbiont_amd.ops import reference as R
+
+    monkeypatch.setenv("SYMB_PRUNE_STREAM", "1")
+    monkeypatch.setenv("SYMB_PRUNE_MX6", "1")
+    g = torch.Generator().manual_seed(19)
+    sh = HbmIndexShard(D, 3000, device="cpu", prune="i8")
+    assert sh.mx6_on and sh.img_mx6.shape[1] == sh._stream_rec(2)
+    sh.append_f32(torch.randn(2000, D, generator=g))
+    sh.upsert(["a", "b"], torch.randn(2, D, generator=g), [Payload("da"), Payload("db")])
+    sh.write_rows_f32([3, 100, 1999], torch.randn(3, D, generator=g))
+    n = sh.count
+    _, _, xt, nr = R.mx6_codes_ref(sh.rows[:n])
+    assert torch.equal(R.stream_mx6_decode(sh.img_mx6[:(n + 31) // 32], n, D), xt)
+    E6, X6 = sh.mx6_bounds.tolist()
+    assert E6 >= float(nr[:, 0].max()) - 1e-7 and X6 >= float(nr[:, 1].max()) - 1e-7
+    q = torch.nn.functional.normalize(torch.randn(32, D, generator=g), dim=-1).bfloat16()
+    q6, qs6, m6 = sh.mx6_query_image(q)
+    qt = R.stream_mx6_query_decode(q6, qs6)
+    assert torch.equal(qt, R.mx6_codes_ref(q)[2])
+    est = qt @ xt.t()
+    s = q.float() @ sh.rows[:n].float().t()
+    assert ((s - est).abs() <= m6[:, None]).all()
+    # the fp6 margin sits between the int8 and fp4 ones
+    _, _, m8 = sh.prune_query_image(q)
+    _, _, m4 = sh.mx4_query_image(q)
+    assert bool((m8 < m6).all()) and bool((m6 < m4).all())
+
+
+def test_mx6_tier_defaults():
+    """SYMB_PRUNE_MX6=auto keeps the fp6 image at 384 only (100M x 768 has no HBM left for it)."""
+    a = HbmIndexShard(384, 256, device="cpu", prune="i8")
+    b = HbmIndexShard(768, 256, device="cpu", prune="i8")
+    assert a.mx6_on == a.stream and not b.mx6_on
+
+
 def test_rwlock_prefers_a_waiting_writer():
     """Once a writer waits, new readers queue behind it (a stream of searches could
     starve upserts)."""

@@ -809,6 +809,36 @@ def test_quant_stream_images_match_reference(D):
             assert torch.equal(R.stream_mx4_query_decode(q4, qs), qt)
             _close(mg, qn[:, 2] * b[0] + qn[:, 0] * b[1] + 1e-5, atol=1e-6, rtol=1e-4,
                    what="stream mx4 margin")
+    if D == 1024:
+        return
+    # the MX-fp6 (e2m3) image: rows (range + scattered list), query image, margin
+    rec = h.stream_rec_bytes(D, 2)
+    nks = D // 64
+    assert rec == nks * 1536 + (nks + 3) // 4 * 256
+    img = torch.zeros(n_sub, rec, dtype=torch.uint8, device=DEV)
+    b = torch.zeros(2, device=DEV)
+    rows = torch.arange(n - 1, 999, -1, dtype=torch.int32, device=DEV)
+    h.quant_stream_mx6(x.data_ptr(), 0, 0, 1000, D, img.data_ptr(), 0, 0, b.data_ptr(), 0, st)
+    h.quant_stream_mx6(x.data_ptr(), 0, rows.data_ptr(), rows.numel(), D, img.data_ptr(), 0, 0,
+                       b.data_ptr(), 0, st)
+    ref, nr = R.stream_mx6_ref(x)
+    torch.cuda.synchronize()
+    assert torch.equal(img[:, :nks * 1536], ref[:, :nks * 1536]), "MX-fp6 stream codes"
+    assert torch.equal(R.stream_mx6_decode(img, n, D), R.stream_mx6_decode(ref, n, D))
+    _close(b, nr[:, :2].amax(0), atol=1e-6, rtol=1e-4, what="stream mx6 bounds")
+    nsc = (nks + 3) // 4
+    q = torch.nn.functional.normalize(_f(300, D, seed=65), dim=-1).bfloat16()
+    q6 = torch.empty(300, 3 * D // 4, dtype=torch.uint8, device=DEV)
+    qs = torch.empty(300, 2 * nsc, dtype=torch.int32, device=DEV)
+    mg = torch.empty(300, device=DEV)
+    h.quant_stream_mx6(q.data_ptr(), 0, 0, 300, D, 0, q6.data_ptr(), qs.data_ptr(), b.data_ptr(),
+                       mg.data_ptr(), st)
+    rq6, rqs, qt, qn = R.stream_mx6_query_ref(q)
+    torch.cuda.synchronize()
+    assert torch.equal(q6, rq6)
+    assert torch.equal(R.stream_mx6_query_decode(q6, qs), qt)
+    _close(mg, qn[:, 2] * b[0] + qn[:, 0] * b[1] + 1e-5, atol=1e-6, rtol=1e-4,
+           what="stream mx6 margin")
 
 
 @pytest.mark.parametrize("D", [384, 768, 1024])
@@ -889,10 +919,26 @@ def test_append_rows_writes_rows_and_both_images(D):
     assert torch.equal(R.stream_mx4_decode(imgs[1][0], cap, D), R.stream_mx4_decode(imgs[1][1], cap, D))
     for b in bs:
         _close(b[0], b[1], atol=0, rtol=1e-6, what="append bounds")
+    if D == 1024:
+        return
+    # with the MX-fp6 image as well (the append_rows_kernel FP6 form)
+    img6 = torch.zeros(2, n_sub, h.stream_rec_bytes(D, 2), dtype=torch.uint8, device=DEV)
+    b6 = torch.zeros(2, 2, device=DEV)
+    rows.zero_()
+    h.append_rows(x.data_ptr(), n, D, rows[0].data_ptr(), r0, imgs[0][0].data_ptr(),
+                  bs[0][0].data_ptr(), imgs[1][0].data_ptr(), bs[1][0].data_ptr(), st,
+                  img6=img6[0].data_ptr(), b6=b6[0].data_ptr())
+    h.quant_stream_mx6(rows[1].data_ptr(), r0, 0, n, D, img6[1].data_ptr(), 0, 0,
+                       b6[1].data_ptr(), 0, st)
+    torch.cuda.synchronize()
+    assert torch.equal(rows[0, r0:r0 + n], x)
+    assert torch.equal(img6[0], img6[1]), "MX-fp6 stream image"
+    _close(b6[0], b6[1], atol=0, rtol=1e-6, what="append fp6 bounds")
 
 
-@pytest.mark.parametrize("form,D", [(0, 384), (1, 384), (0, 768), (1, 768), (0, 1024), (1, 1024)])
-def test_index_scan_stream_emits_the_bound_set(form, D):
+@pytest.mark.parametrize("form,D", [(0, 384), (1, 384), (0, 768), (1, 768), (0, 1024), (1, 1024),
+                                    (2, 384), (2, 768)])
+def test_index_scan_stream_emits_the_bound_set(form, D, monkeypatch):
     """index_stream.hip scan_stream_kernel (v_mfma_i32_32x32x32_i8 / v_mfma_scale_f32_32x32x64
     on fragment-major images, one wave per SIMD): exactly the rows whose estimate (int8: (q8 .
     x8) sx, MX-fp4: the decoded dot) reaches the threshold, for 1, 2 and 3 query blocks, a ragged
@@ -902,6 +948,7 @@ def test_index_scan_stream_emits_the_bound_set(form, D):
     from codename_symbiont_amd.ops._ext import hip, stream_handle
 
     n = 200_000 + 77
+    monkeypatch.setenv("SYMB_PRUNE_MX6", "1" if form == 2 else "0")
     shard = HbmIndexShard(D, n + 4096, prune="i8")
     shard.fill_random(n, seed=5)
     assert shard.stream and (shard.img_i8 is not None) and (shard.img_mx4 is not None)
@@ -909,6 +956,9 @@ def test_index_scan_stream_emits_the_bound_set(form, D):
     if form == 0:
         x8, sx = R.stream_i8_decode(shard.img_i8[:(n + 31) // 32], n, D)
         img = shard.img_i8
+    elif form == 2:
+        xt = R.stream_mx6_decode(shard.img_mx6[:(n + 31) // 32], n, D)
+        img = shard.img_mx6
     else:
         xt = R.stream_mx4_decode(shard.img_mx4[:(n + 31) // 32], n, D)
         img = shard.img_mx4
@@ -918,6 +968,9 @@ def test_index_scan_stream_emits_the_bound_set(form, D):
             q8, sq, _ = shard.prune_query_image(q)
             est = (q8.float() @ x8.float().t()) * sx[None, :]        # (acc * sx: thr / sq units)
             qa, qs = q8, None
+        elif form == 2:
+            qa, qs, _ = shard.mx6_query_image(q)
+            est = R.stream_mx6_query_decode(qa, qs) @ xt.t()
         else:
             qa, qs, _ = shard.mx4_query_image(q)
             est = R.stream_mx4_query_decode(qa, qs) @ xt.t()
@@ -1409,7 +1462,8 @@ def test_index_pruned_search_mx4_tier_is_exact(nq, stream, D, monkeypatch):
         nv = shard._mx4_last
         ts, _ = R.topk_ref(rows, q, k)
         torch.cuda.synchronize()
-        assert nv is not None and int(nv.item()) == (0 if kind == "near" else 1), kind
+        # (random: the int8 tier, 1, or with the fp6 image the fp6 tier, 1, or int8, 3)
+        assert nv is not None and (int(nv.item()) == 0) == (kind == "near"), kind
         _close(s1, ts, atol=2e-5, what=f"mx4 tier {kind} scores")
         _close(R.row_scores_ref(rows, q, r1), ts, atol=2e-5, what=f"mx4 tier {kind} rows")
         # the next search samples 1 tile in 2^7 after an fp4-tier search (its flag has landed by
@@ -1419,6 +1473,42 @@ def test_index_pruned_search_mx4_tier_is_exact(nq, stream, D, monkeypatch):
         want = shard.PRUNE_TILE_SHIFT_MX4 if kind == "near" else shard.PRUNE_TILE_SHIFT
         assert shard._sample_shift_last == want, (kind, shard._sample_shift_last)
         _close(s2, ts, atol=2e-5, what=f"mx4 tier {kind} scores, second search")
+
+
+@pytest.mark.parametrize("D,mx4", [(384, "1"), (384, "0"), (768, "1")])
+def test_index_pruned_search_mx6_tier_is_exact(D, mx4, monkeypatch):
+    """The MX-fp6 middle tier: random held-out queries (k-th score a few sigma above the bulk: the
+    fp4 band too wide, the fp6 one narrow enough) take it -- flag 1 -- and get the exact bf16
+    results; near-duplicate queries still take the fp4 tier (flag 0) when it is kept, the fp6 one
+    otherwise; with the fp6 select's limit at 0 every batch falls through to int8 (flag 3)."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+
+    monkeypatch.setenv("SYMB_PRUNE_MX6", "1")
+    monkeypatch.setenv("SYMB_PRUNE_MX4", mx4)
+    n, k, nq = (1 << 20) + 555, 10, 256
+    g = torch.Generator(device=DEV).manual_seed(13)
+    shard = HbmIndexShard(D, n + 8192, prune="i8")
+    assert shard.mx6_on and shard.mx4_on == (mx4 == "1")
+    shard.fill_random(n, seed=7)
+    c = torch.nn.functional.normalize(torch.randn(D, device=DEV, generator=g), dim=0)
+    shard.append_f32(c + 0.1 * torch.randn(3000, D, device=DEV, generator=g) / math.sqrt(D))
+    rows = shard.unit_rows().float()
+    shard.mq_stats = True
+    for kind, want in (("random", 1), ("near", 0 if mx4 == "1" else 1), ("int8", 3)):
+        if kind == "near":
+            q = c + 0.1 * torch.randn(nq, D, device=DEV, generator=g) / math.sqrt(D)
+        else:
+            q = torch.randn(nq, D, device=DEV, generator=g)
+        q = torch.nn.functional.normalize(q, dim=-1).bfloat16()
+        if kind == "int8":
+            monkeypatch.setattr(shard, "MX6_LIMIT_FRAC", 0.0)
+        s1, r1 = shard.search(q, k)
+        ts, _ = R.topk_ref(rows, q, k)
+        torch.cuda.synchronize()
+        assert int(shard._tier_last.item()) == want, (kind, int(shard._tier_last.item()))
+        _close(s1, ts, atol=2e-5, what=f"mx6 tier {kind} scores")
+        _close(R.row_scores_ref(rows, q, r1), ts, atol=2e-5, what=f"mx6 tier {kind} rows")
+    assert shard._mx6_tot is not None and int(shard._mx6_tot.item()) == (1 if mx4 == "1" else 2)
 
 
 def test_prune_qquant_and_route_match_torch():
