@@ -38,6 +38,8 @@ def main() -> None:
                     help="stream forms timed in one process, interleaved: comma list of "
                          "mx4variant:i8variant:ablation[:land[:centroid]] (e.g. 0:0:0:1:1,0:0:0:1:0)")
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--thr-add", type=float, default=0.0,
+                    help="added to the scan's thresholds (e.g. 10: no row emits -- kernel-only timing)")
     a = ap.parse_args()
     from codename_symbiont_amd.index.shard import STREAM_SUB, HbmIndexShard
     from codename_symbiont_amd.index.synth import CorpusGen, fill_corpus
@@ -79,6 +81,12 @@ def main() -> None:
         # k-th scores ~0.2 (only the row itself scores high), for which the tier is never chosen;
         # time the kernel at the headline's threshold instead
         m4["thr4"].fill_(0.74)
+    if a.tier == "mx6" and a.queries in ("self", "near"):
+        m6["thr6"].fill_(0.74)   # (kernel timing at the headline's threshold, as for mx4)
+    if a.thr_add:
+        for t in (P["thr"], m4 and m4.get("thr4"), m6 and m6.get("thr6")):
+            if t is not None:
+                t.add_(a.thr_add)
     nbytes = 0
 
     def scan():

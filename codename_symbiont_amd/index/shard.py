@@ -190,7 +190,9 @@ class HbmIndexShard:
         if self.device.type == "cuda" and self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
         self.capacity = int(capacity)
-        self.rows = torch.empty(_round_up(max(self.capacity, 1), TILE_ROWS), dim,
+        # (zeroed: the int8 stream image quantises whole 32-row sub-tiles with one shared scale, so
+        # the not-yet-written rows of a sub-tile enter its scale)
+        self.rows = torch.zeros(_round_up(max(self.capacity, 1), TILE_ROWS), dim,
                                 dtype=torch.uint8 if dtype == "fp8" else torch.bfloat16,
                                 device=self.device)
         # e4m3 image of the bf16 rows for the prefilter scan (kept in step by every write)
@@ -307,7 +309,7 @@ class HbmIndexShard:
         """Bytes per 32-row sub-tile of the stream image (form 0 = int8, 1 = MX-fp4, 2 = MX-fp6);
         the same numbers as index_stream.hip SDim (checked against the extension on a GPU)."""
         nks = self.dim // (64 if form else 32)
-        return nks * (1536 if form == 2 else 1024) + ((nks + 3) // 4 * 256 if form else 128)
+        return nks * (1536 if form == 2 else 1024) + ((nks + 3) // 4 * 256 if form else 16)
 
     def _set_i8_view(self, heavy: int) -> None:
         """Views of the flat int8 store for the form: the stream image (plain form on a stream
@@ -353,8 +355,8 @@ class HbmIndexShard:
             torch.maximum(b, w[:, :2].amax(0), out=b)
         else:
             rec, err, xtn = R.stream_i8_ref(src)
-            a, b = r0 - g0 * STREAM_SUB, r1 - g0 * STREAM_SUB
-            torch.maximum(self.i8_bounds[:2], torch.stack([err[a:b].max(), xtn[a:b].max()]),
+            # (every row of the re-imaged sub-tiles: their shared scale may have changed)
+            torch.maximum(self.i8_bounds[:2], torch.stack([err.max(), xtn.max()]),
                           out=self.i8_bounds[:2])
         img[g0:g0 + rec.shape[0]] = rec
 
@@ -1327,7 +1329,7 @@ class HbmIndexShard:
             h.mx4_select(NQ, T.data_ptr(), m6.data_ptr(), margin.data_ptr(), S.data_ptr(), m_seed,
                          float(t0) / n_probe, tcs_p, tcap, self.MX6_LIMIT_FRAC * cap,
                          thr6.data_ptr(), nvf.data_ptr(), st, ld=ld, tile_stride=4, tail_ld=ld,
-                         nv_zeroed=True, stage=1 if ctx["mx4"] is not None else 2, wa=1.0, wb=1.0)
+                         nv_zeroed=True, stage=1 if ctx["mx4"] is not None else 2, wa=1.0, wb=0.0)
             ctx["mx6"] = dict(q6=q6, qs6=qs6, thr6=thr6, nv=nvf, m6=m6)
         return ctx
 

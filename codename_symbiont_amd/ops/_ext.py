@@ -11,6 +11,9 @@ from __future__ import annotations
 
 import functools
 import importlib
+import importlib.util
+import os
+import sys
 
 import torch  # noqa: F401  -- must load torch's libamdhip64.so.7 before _hip (shared HIP runtime)
 
@@ -22,7 +25,14 @@ class ExtensionMissing(RuntimeError):
 @functools.lru_cache(maxsize=None)
 def hip():
     try:
-        mod = importlib.import_module("codename_symbiont_amd._hip")
+        alt = os.environ.get("SYMB_HIP_SO", "")
+        if alt:   # an A/B build of the kernels (csrc/build.py SYMB_BUILD_TAG), same module name
+            spec = importlib.util.spec_from_file_location("codename_symbiont_amd._hip", alt)
+            mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+            sys.modules["codename_symbiont_amd._hip"] = mod
+        else:
+            mod = importlib.import_module("codename_symbiont_amd._hip")
     except ImportError as e:  # pragma: no cover - exercised only on broken installs
         raise ExtensionMissing(
             "codename_symbiont_amd._hip is not built; run `python csrc/build.py` "

@@ -212,27 +212,41 @@ def _stream_rows(frags: torch.Tensor, n: int, rb: int) -> torch.Tensor:
     return frags.reshape(n_sub, nks, 2, 32, 16).permute(0, 3, 1, 2, 4).reshape(n_sub * 32, rb)[:n]
 
 
-STREAM_HDR_POS = [16 * ((r >> 2) & 1) + (r & 3) + 4 * (r >> 3) for r in range(32)]
+def stream_i8_tile_codes_ref(x: torch.Tensor):
+    """int8 codes of rows with ONE scale per 32-row sub-tile (index_stream.hip i8_stream_tile):
+    s = max |x| / 127 over the tile's rows (rows past n count as zeros; an all-zero tile: 1),
+    x8 = round(x * (1 / s)).  Returns (x8 int8 [n, D], per-row scale f32 [n] (the tile's),
+    |x - x~| [n], |x~| [n])."""
+    xf = x.float()
+    n, d = xf.shape
+    n_sub = (n + 31) // 32
+    pad = torch.zeros(n_sub * 32, d, dtype=torch.float32, device=xf.device)
+    pad[:n] = xf
+    amax = pad.view(n_sub, 32 * d).abs().amax(1)
+    s = torch.where(amax > 0, amax / 127.0, torch.ones_like(amax))
+    sr = s.repeat_interleave(32)[:n]
+    inv = 1.0 / sr
+    x8 = torch.round(xf * inv[:, None]).clamp_(-127, 127)
+    xt = x8 * sr[:, None]
+    return x8.to(torch.int8), sr, (xf - xt).norm(dim=1), xt.norm(dim=1)
 
 
 def stream_i8_ref(x: torch.Tensor):
-    """int8 stream image of bf16 rows (quant_stream_i8): records uint8 [n_sub, 128 + D * 32]
-    (the 32 row scales as f32 at STREAM_HDR_POS, then the fragments), plus (|x - x~|, |x~|)."""
-    q8, sc, err, xtn = quant_rows_i8_ref(x)
-    n, d = q8.shape
+    """int8 stream image of bf16 rows (quant_stream_i8): records uint8 [n_sub, 16 + D * 32] (the
+    sub-tile's scale as f32 at byte 0 of a 16-byte header, then the fragments), plus (|x - x~|,
+    |x~|) per row."""
+    q8, sr, err, xtn = stream_i8_tile_codes_ref(x)
     frags = _stream_frags(q8.view(torch.uint8))
     n_sub = frags.shape[0]
-    hdr = torch.zeros(n_sub * 32, dtype=torch.float32, device=x.device)
-    hdr[:n] = sc
-    h2 = torch.zeros(n_sub, 32, dtype=torch.float32, device=x.device)
-    h2[:, STREAM_HDR_POS] = hdr.view(n_sub, 32)
-    return torch.cat([h2.view(torch.uint8), frags], 1), err, xtn
+    hdr = torch.zeros(n_sub, 4, dtype=torch.float32, device=x.device)
+    hdr[:, 0] = sr[::32]
+    return torch.cat([hdr.view(torch.uint8), frags], 1), err, xtn
 
 
 def stream_i8_decode(rec: torch.Tensor, n: int, d: int):
-    """(x8 int8 [n, d], sx f32 [n]) of an int8 stream image."""
-    hdr = rec[:, :128].contiguous().view(torch.float32)[:, STREAM_HDR_POS].reshape(-1)[:n]
-    x8 = _stream_rows(rec[:, 128:], n, d).contiguous().view(torch.int8)
+    """(x8 int8 [n, d], per-row scale f32 [n] -- its sub-tile's) of an int8 stream image."""
+    hdr = rec[:, :16].contiguous().view(torch.float32)[:, 0].repeat_interleave(32)[:n]
+    x8 = _stream_rows(rec[:, 16:], n, d).contiguous().view(torch.int8)
     return x8, hdr
 
 

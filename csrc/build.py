@@ -9,6 +9,10 @@ files live in the source tree and travel with the repository snapshot to the GPU
 incremental (object mtime vs. source + header mtimes) and parallel.
 
 Usage:  python csrc/build.py [--hip-only|--native-only] [--force] [-j N]
+
+A/B builds of the kernels: SYMB_HIP_CXXFLAGS adds flags to every .hip compile and SYMB_BUILD_TAG
+names a separate object directory and output ``_hip_<tag>.so`` (loaded instead of ``_hip`` when
+SYMB_HIP_SO points at it, ops/_ext.py).
 """
 from __future__ import annotations
 
@@ -63,21 +67,30 @@ def _compile_all(jobs: list[tuple[list[str], Path, Path, float]], nproc: int, fo
     return bool(todo)
 
 
+# per-file code-generation flags.  The stream scans keep their MFMA accumulators in VGPRs
+# (`-amdgpu-mfma-vgpr-form`): the default AGPR form copied operands and results through
+# v_accvgpr moves in the hot loop -- 100M x 384 int8 scan 11.36 -> 10.94 ms, MX-fp4 5.59 -> 5.05,
+# MX-fp6 7.26 -> 6.67 (profiles/r5_scan/ab_vgpr_form.jsonl)
+FILE_FLAGS = {"index_stream.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+
+
 def build_hip(force: bool = False, nproc: int = 8) -> Path:
     src_dir = CSRC / "hip"
-    obj_dir = BUILD / "hip"
+    tag = os.environ.get("SYMB_BUILD_TAG", "")
+    obj_dir = BUILD / ("hip_" + tag if tag else "hip")
     obj_dir.mkdir(parents=True, exist_ok=True)
     headers = list(src_dir.glob("*.h"))
     hdr_mtime = _newest(headers)
     common = [
         HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden",
-        "-Wno-unused-result", f"-I{src_dir}",
+        "-Wno-unused-result", f"-I{src_dir}", *os.environ.get("SYMB_HIP_CXXFLAGS", "").split(),
     ]
     jobs = []
     objs = []
     for src in sorted(src_dir.glob("*.hip")):
         obj = obj_dir / (src.stem + ".o")
-        jobs.append((common + ["-c", str(src), "-o", str(obj)], src, obj, hdr_mtime))
+        jobs.append((common + FILE_FLAGS.get(src.name, []) + ["-c", str(src), "-o", str(obj)], src,
+                     obj, max(hdr_mtime, Path(__file__).stat().st_mtime)))
         objs.append(obj)
     # host-only C++ (the hipBLASLt plan cache for the plain projections)
     lt = src_dir / "gemm_lt.cpp"
@@ -97,7 +110,7 @@ def build_hip(force: bool = False, nproc: int = 8) -> Path:
     )
     objs.append(bind_obj)
     changed = _compile_all(jobs, nproc, force)
-    out = PKG / f"_hip{EXT_SUFFIX}"
+    out = PKG / (f"_hip_{tag}.so" if tag else f"_hip{EXT_SUFFIX}")
     if changed or force or not out.exists() or out.stat().st_mtime < _newest(objs):
         _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs),
               f"-L{ROCM}/lib", "-lhipblaslt", f"-Wl,-rpath,{ROCM}/lib", "-o", str(out)])

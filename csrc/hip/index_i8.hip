@@ -1118,9 +1118,9 @@ __global__ __launch_bounds__(256) void quant_rows_mx4_kernel(const __bf16* __res
 // else bit 1: fp6 not viable); 2 = the fp6 choice alone (bit 0 always, bit 1 as in 1).  The
 // gated scans then want *nv == 0 (fp4), 1 (fp6), 3 (int8).
 // The band counted is [T - wa margin4 - wb margin8, T - margin8): (2, 0) -- the fp4 tier's
-// worst case -- or (1, 1) for the fp6 tier, whose rounding error on a pair is typically ~1/30 of
-// its Cauchy-Schwarz bound (the int8 margin as the allowance: an underestimate only costs the
-// overflow fallback, never exactness).
+// worst case -- or (1, 0) for the fp6 tier, whose rounding error on a pair is typically ~1/30 of
+// its Cauchy-Schwarz bound, so its emissions are ~ the rows above T - margin6 (an underestimate
+// only costs the overflow fallback, never exactness; the limit leaves 4x headroom to the cap).
 __global__ __launch_bounds__(256) void mx4_select_kernel(
     int NQ, const float* __restrict__ T, const float* __restrict__ margin4,
     const float* __restrict__ margin8, const float* __restrict__ probe_s, int n_cols, int ld,

@@ -51,7 +51,11 @@ struct SDim {
   static constexpr int LB = FMT == SF_MX6 ? 24 : 16;              // bytes per lane per k-step
   static constexpr int RB = NKS * 2 * LB;                        // (query) image bytes per row
   static constexpr int NSC = FMT == SF_I8 ? 0 : (NKS + 3) / 4;   // block-scale dwords per lane
-  static constexpr int HDR = FMT == SF_I8 ? 128 : 0;             // row scales (int8)
+  // int8: ONE scale per 32-row sub-tile (f32 at byte 0 of a 16-byte header): the hit test takes
+  // max_r acc[r] before its single multiply (per-row scales cost 16 cvt + 16 mul per set and
+  // sub-tile, 8 % of the 100M x 384 scan; profiles/r5_scan/ab_i8_tile_scale.jsonl).  The bound
+  // E = max |x - x~| is a maximum over rows either way, so pruning keeps its power.
+  static constexpr int HDR = FMT == SF_I8 ? 16 : 0;
   // per k-step 64 lanes x LB bytes; MX-fp6: two 768-byte planes of 12 bytes per lane
   static constexpr int FRAG = NKS * 64 * LB;
   static constexpr int REC = HDR + FRAG + NSC * 256;             // bytes per 32-row sub-tile
@@ -234,15 +238,11 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
   const uint8_t* rec0 = img + (size_t)g0 * REC;
   FragT fk[DEPTH][NKS];
   uint32_t fsc[DEPTH][NSC];
-  f32x4 frs[DEPTH][FMT == SF_I8 ? 4 : 1];
+  float fts[DEPTH];   // (int8) the sub-tile's scale
   auto load = [&](auto dc, int i) {
     constexpr int d = decltype(dc)::value;
     const uint8_t* r = rec0 + (size_t)min(i, ns - 1) * REC;   // (past the end: the last again)
-    if constexpr (FMT == SF_I8) {
-      const f32x4* sp = reinterpret_cast<const f32x4*>(r + 64 * h);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) frs[d][c] = sp[c];
-    }
+    if constexpr (FMT == SF_I8) fts[d] = *reinterpret_cast<const float*>(r);
     // (MX-fp6: lane l's 24 bytes are 12 in the k-step's first 768-byte plane and 12 in its second)
     const uint8_t* f = r + S::HDR + (FMT == SF_MX6 ? 12 : 16) * lane;
 #pragma unroll
@@ -254,6 +254,17 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
     }
   };
 
+  // int8: the 32 x 32 block's integer dot products (16 rows of one query per lane)
+  auto acc_i8 = [&](auto dc, auto sc) {
+    constexpr int d = decltype(dc)::value, s = decltype(sc)::value;
+    i32x16s acc = {};
+    if constexpr (FMT == SF_I8) {
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks)
+        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(fk[d][ks], qf[s][ks], acc, 0, 0, 0);
+    }
+    return acc;
+  };
   // the 32 x 32 block of set s over sub-tile slot d, as estimates (16 rows of one query)
   auto block = [&](auto dc, auto sc, float (&v)[16]) {
     constexpr int d = decltype(dc)::value, s = decltype(sc)::value;
@@ -282,12 +293,9 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
 #pragma unroll
       for (int r = 0; r < 16; ++r) v[r] = acc[r];
     } else {
-      i32x16s acc = {};
+      const i32x16s acc = acc_i8(dc, sc);
 #pragma unroll
-      for (int ks = 0; ks < NKS; ++ks)
-        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(fk[d][ks], qf[s][ks], acc, 0, 0, 0);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = (float)acc[r] * frs[d][r >> 2][r & 3];
+      for (int r = 0; r < 16; ++r) v[r] = (float)acc[r] * fts[d];
     }
   };
 
@@ -338,9 +346,18 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
       static_for<0, SETS>([&](auto sc) {
         constexpr int s = decltype(sc)::value;
         if (!((pass >> s) & 1u)) return;
-        float v[16];
-        block(dc, sc, v);
-        hm |= (max16(v) >= thr[s] ? 1u : 0u) << s;
+        if constexpr (FMT == SF_I8) {   // (the sub-tile's scale > 0 keeps the order)
+          const i32x16s acc = acc_i8(dc, sc);
+          int m = max(max(acc[0], acc[1]), acc[2]);
+#pragma unroll
+          for (int r = 3; r < 15; r += 2) m = max(max(m, acc[r]), acc[r + 1]);
+          m = max(m, acc[15]);
+          hm |= ((float)m * fts[d] >= thr[s] ? 1u : 0u) << s;
+        } else {
+          float v[16];
+          block(dc, sc, v);
+          hm |= (max16(v) >= thr[s] ? 1u : 0u) << s;
+        }
       });
     }
     if (__builtin_amdgcn_ballot_w64(hm != 0)) {   // rare: recompute the hit sets, emit per row
@@ -380,9 +397,9 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
     auto dma = [&](int i, int slot) {   // sub-tile i (past the end: the last again) into slot
       const uint8_t* r = rec0 + (size_t)min(i, ns - 1) * REC;
       const uint32_t dst = lds_addr(ring) + slot * SLOT;
-      // the 128-byte row-scale header: 4 bytes per lane, lanes 32-63 repeating 0-31 into LDS bytes
-      // 128..255 (an LDS-DMA lands lane l at base + 4 l; the 2-byte form did not pack by 2)
-      if constexpr (FMT == SF_I8) dma4_asm(r + 4 * (lane & 31), dst);
+      // the 16-byte scale header: 4 bytes per lane (an LDS-DMA lands lane l at base + 4 l), the
+      // 64 lanes repeating it over LDS bytes 0..255
+      if constexpr (FMT == SF_I8) dma4_asm(r + 4 * (lane & 3), dst);
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks)
         dma16_asm(r + S::HDR + 1024 * ks + 16 * lane, dst + G::LHDR + 1024 * ks);
@@ -393,10 +410,7 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
     };
     auto fetch = [&](int slot) {
       const char* src = ring + slot * SLOT;
-      if constexpr (FMT == SF_I8) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) frs[0][c] = *reinterpret_cast<const f32x4*>(src + 64 * h + 16 * c);
-      }
+      if constexpr (FMT == SF_I8) fts[0] = *reinterpret_cast<const float*>(src);
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks)
         fk[0][ks] = *reinterpret_cast<const i32x4s*>(src + G::LHDR + 1024 * ks + 16 * lane);
@@ -446,44 +460,70 @@ __device__ __forceinline__ size_t stream_frag_off(int rec, int hdr, int r, int b
   return (size_t)(r >> 5) * rec + hdr + 1024 * (b >> 5) + 16 * (32 * ((b >> 4) & 1) + rr) + (b & 15);
 }
 
-// One row's int8 stream image (quant_rows_i8_kernel's numbers: sx = max|x| / 127, x8 =
-// round(x / sx)): codes at row `row` of img, its scale in the sub-tile header; en / nn =
-// |x - x~| / |x~| in every lane.  One wave; lane l holds elements PER l .. PER l + PER - 1.
+// The int8 stream image of one whole 32-row sub-tile g of the bf16 rows X: the tile's scale
+// s = max |x| / 127 over its 32 rows (an all-zero tile: 1) at header byte 0, every row's codes
+// round(x / s); returns (max_r |x_r - x~_r|, max_r |x~_r|) in every thread.  One 512-thread
+// workgroup: wave w quantises rows w, w + 8, w + 16, w + 24; lane l holds elements PER l ..
+// PER l + PER - 1 of a row.
 template <int D>
-__device__ __forceinline__ void i8_stream_row(const __bf16* __restrict__ xrow, int row,
-                                              uint8_t* __restrict__ img, float& en, float& nn) {
+__device__ __forceinline__ void i8_stream_tile(const __bf16* __restrict__ X, int g,
+                                               uint8_t* __restrict__ img, float& en_max,
+                                               float& nn_max) {
   using S = SDim<SF_I8, D>;
   constexpr int PER = D / 64;
-  const int lane = threadIdx.x & 63;
-  float x[PER];
-  const uint32_t* xp = reinterpret_cast<const uint32_t*>(xrow + PER * lane);
-#pragma unroll
-  for (int i = 0; i < PER / 2; ++i) {
-    const uint32_t u = xp[i];
-    x[2 * i] = __uint_as_float(u << 16);
-    x[2 * i + 1] = __uint_as_float(u & 0xffff0000u);
-  }
+  __shared__ float red[3][8];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float x[4][PER];
   float amax = 0.f;
 #pragma unroll
-  for (int i = 0; i < PER; ++i) amax = fmaxf(amax, fabsf(x[i]));
-  amax = wave_max(amax);
-  const float s = amax > 0.f ? amax / 127.f : 1.f;
-  const float inv = 1.f / s;
-  float e2 = 0.f, n2 = 0.f;
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t* xp =
+        reinterpret_cast<const uint32_t*>(X + (size_t)(32 * g + w + 8 * k) * D + PER * lane);
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int qv = max(-127, min(127, (int)rintf(x[i] * inv)));
-    const float xt = (float)qv * s;
-    e2 += (x[i] - xt) * (x[i] - xt);
-    n2 += xt * xt;
-    img[stream_frag_off(S::REC, S::HDR, row, PER * lane + i)] = (uint8_t)(qv & 0xff);
+    for (int i = 0; i < PER / 2; ++i) {
+      const uint32_t u = xp[i];
+      x[k][2 * i] = __uint_as_float(u << 16);
+      x[k][2 * i + 1] = __uint_as_float(u & 0xffff0000u);
+      amax = fmaxf(amax, fmaxf(fabsf(x[k][2 * i]), fabsf(x[k][2 * i + 1])));
+    }
   }
-  en = sqrtf(wave_sum(e2));
-  nn = sqrtf(wave_sum(n2));
+  amax = wave_max(amax);
+  if (lane == 0) red[0][w] = amax;
+  __syncthreads();
+  amax = red[0][0];
+#pragma unroll
+  for (int i = 1; i < 8; ++i) amax = fmaxf(amax, red[0][i]);
+  const float sc = amax > 0.f ? amax / 127.f : 1.f;
+  const float inv = 1.f / sc;
+  float em = 0.f, nm = 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int row = 32 * g + w + 8 * k;
+    float e2 = 0.f, n2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int qv = max(-127, min(127, (int)rintf(x[k][i] * inv)));
+      const float xt = (float)qv * sc;
+      e2 += (x[k][i] - xt) * (x[k][i] - xt);
+      n2 += xt * xt;
+      img[stream_frag_off(S::REC, S::HDR, row, PER * lane + i)] = (uint8_t)(qv & 0xff);
+    }
+    em = fmaxf(em, sqrtf(wave_sum(e2)));
+    nm = fmaxf(nm, sqrtf(wave_sum(n2)));
+  }
+  if (threadIdx.x < 4)
+    reinterpret_cast<float*>(img + (size_t)g * S::REC)[threadIdx.x] = threadIdx.x ? 0.f : sc;
   if (lane == 0) {
-    const int rr = row & 31;
-    float* hdr = reinterpret_cast<float*>(img + (size_t)(row >> 5) * S::REC);
-    hdr[16 * ((rr >> 2) & 1) + (rr & 3) + 4 * (rr >> 3)] = s;
+    red[1][w] = em;
+    red[2][w] = nm;
+  }
+  __syncthreads();
+  en_max = red[1][0];
+  nn_max = red[2][0];
+#pragma unroll
+  for (int i = 1; i < 8; ++i) {
+    en_max = fmaxf(en_max, red[1][i]);
+    nn_max = fmaxf(nn_max, red[2][i]);
   }
 }
 
@@ -731,20 +771,18 @@ __device__ __forceinline__ void raise_bounds2(float* bounds, float a, float b) {
   }
 }
 
-// int8 stream image of bf16 rows [r0, r0 + n) (or of the rows listed in `rows`, n of them);
-// bounds (2 floats) raised to (max |x - x~|, max |x~|).  One wave per row.
+// int8 stream image of whole sub-tiles of the bf16 rows X (i8_stream_tile): tiles g_lo +
+// blockIdx.x, or (rows != nullptr) the tile of listed row rows[blockIdx.x] -- a tile listed twice
+// is written twice with the same bytes; bounds (2 floats) raised to (max |x - x~|, max |x~|).
 template <int D>
-__global__ __launch_bounds__(256) void quant_stream_i8_kernel(const __bf16* __restrict__ X, int r0,
-                                                              const int* __restrict__ rows, int n,
+__global__ __launch_bounds__(512) void quant_stream_i8_kernel(const __bf16* __restrict__ X, int g_lo,
+                                                              const int* __restrict__ rows,
                                                               uint8_t* __restrict__ img,
                                                               float* __restrict__ bounds) {
-  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
-  float en = 0.f, nn = 0.f;
-  if (j < n) {   // (block-uniform barrier in raise_bounds2: idle waves report zeros)
-    const int row = rows ? rows[j] : r0 + j;
-    i8_stream_row<D>(X + (size_t)row * D, row, img, en, nn);
-  }
-  raise_bounds2(bounds, en, nn);
+  const int g = rows ? rows[blockIdx.x] >> 5 : g_lo + blockIdx.x;
+  float en, nn;
+  i8_stream_tile<D>(X, g, img, en, nn);
+  if (threadIdx.x < 2) atomicMax(reinterpret_cast<int*>(bounds) + threadIdx.x, __float_as_int(threadIdx.x ? nn : en));
 }
 
 // MX-fp4 / MX-fp6 stream image of bf16 rows (margin == nullptr: rows [r0, r0 + n) or the listed
@@ -771,20 +809,19 @@ __global__ __launch_bounds__(256) void quant_stream_mx_kernel(
   raise_bounds2(bounds, en, nn);
 }
 
-// An append of n unit bf16 rows at row r0 in one launch: the rows themselves (src -> rows), their
-// int8 stream image (img8, bounds b8[0..1]), MX-fp4 stream image (img4, bounds b4[0..1]) and
-// MX-fp6 stream image (img6, b6) -- any image may be absent (nullptr).  One wave per row.
+// An append of n unit bf16 rows at row r0: the rows themselves (src -> rows), their MX-fp4 stream
+// image (img4, bounds b4[0..1]) and MX-fp6 stream image (img6, b6) -- either image may be absent
+// (nullptr).  One wave per row.  (The int8 image's sub-tiles follow in a second launch: their
+// shared scale needs every row of the tile written first.)
 template <int D, bool FP6>
 __global__ __launch_bounds__(256) void append_rows_kernel(const __bf16* __restrict__ src, int n,
                                                           __bf16* __restrict__ rows, int r0,
-                                                          uint8_t* __restrict__ img8,
-                                                          float* __restrict__ b8,
                                                           uint8_t* __restrict__ img4,
                                                           float* __restrict__ b4,
                                                           uint8_t* __restrict__ img6,
                                                           float* __restrict__ b6) {
   const int j = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  float e8 = 0.f, n8 = 0.f, e4 = 0.f, n4 = 0.f, x4 = 0.f, e6 = 0.f, n6 = 0.f;
+  float e4 = 0.f, n4 = 0.f, x4 = 0.f, e6 = 0.f, n6 = 0.f;
   if (j < n) {
     const __bf16* xr = src + (size_t)j * D;
     // the bf16 row: D * 2 bytes as 4-byte words, D / 128 per lane
@@ -792,12 +829,9 @@ __global__ __launch_bounds__(256) void append_rows_kernel(const __bf16* __restri
     uint32_t* dp = reinterpret_cast<uint32_t*>(rows + (size_t)(r0 + j) * D);
 #pragma unroll
     for (int i = 0; i < D / 128; ++i) dp[lane + 64 * i] = sp[lane + 64 * i];
-    if (img8) i8_stream_row<D>(xr, r0 + j, img8, e8, n8);
     if (img4) mx4_stream_row<D>(xr, r0 + j, img4, nullptr, nullptr, e4, n4, x4);
     if constexpr (FP6) mx_stream_row<SF_MX6, D, false>(xr, r0 + j, img6, nullptr, nullptr, e6, n6, x4);
   }
-  if (b8) raise_bounds2(b8, e8, n8);
-  __syncthreads();   // (raise_bounds2's LDS reused)
   if (b4) raise_bounds2(b4, e4, n4);
   if constexpr (FP6) {
     __syncthreads();
@@ -1006,6 +1040,9 @@ int symb_mx4_centroids(const void* Xq, const void* QS, int NQ, int dim, void* C4
 // Append n unit bf16 rows (src) at row r0 of the shard: rows, int8 stream image (img8 / b8),
 // MX-fp4 stream image (img4 / b4) and MX-fp6 stream image (img6 / b6, not at 1024); an image
 // pointer may be nullptr (then its bounds too).
+int symb_quant_stream_i8(const void* X, int r0, const int* rows, int n, int dim, void* img,
+                         float* bounds, hipStream_t st);
+
 int symb_append_rows(const void* src, int n, int dim, void* rows, int r0, void* img8, float* b8,
                      void* img4, float* b4, void* img6, float* b6, hipStream_t st) {
   if (n <= 0) return 0;
@@ -1013,8 +1050,8 @@ int symb_append_rows(const void* src, int n, int dim, void* rows, int r0, void* 
       (img6 && !b6) || (img6 && dim == 1024))
     return -1;
 #define L(D_, F_) hipLaunchKernelGGL((append_rows_kernel<D_, F_>), dim3((n + 3) / 4), dim3(256), 0,  \
-                                     st, (const __bf16*)src, n, (__bf16*)rows, r0, (uint8_t*)img8, \
-                                     b8, (uint8_t*)img4, b4, (uint8_t*)img6, b6)
+                                     st, (const __bf16*)src, n, (__bf16*)rows, r0, (uint8_t*)img4, \
+                                     b4, (uint8_t*)img6, b6)
   if (dim == 384) {
     if (img6) L(384, true);
     else L(384, false);
@@ -1024,16 +1061,19 @@ int symb_append_rows(const void* src, int n, int dim, void* rows, int r0, void* 
   } else if (dim == 1024) L(1024, false);
   else return -1;
 #undef L
+  if (img8) return symb_quant_stream_i8(rows, r0, nullptr, n, dim, img8, b8, st);
   return (int)hipGetLastError();
 }
 
-// int8 stream image of bf16 rows X: rows [r0, r0 + n) (rows == nullptr) or the n listed rows.
+// int8 stream image of the sub-tiles covering bf16 rows [r0, r0 + n) of X (rows == nullptr) or
+// the n listed rows -- whole 32-row tiles (their shared scale), so X holds the shard's every row.
 int symb_quant_stream_i8(const void* X, int r0, const int* rows, int n, int dim, void* img,
                          float* bounds, hipStream_t st) {
   if (n <= 0) return 0;
   if (bounds == nullptr || (rows == nullptr && r0 < 0)) return -1;
-#define L(D_) hipLaunchKernelGGL(quant_stream_i8_kernel<D_>, dim3((n + 3) / 4), dim3(256), 0, st, \
-                                 (const __bf16*)X, r0, rows, n, (uint8_t*)img, bounds)
+  const int g_lo = r0 >> 5, n_wg = rows ? n : ((r0 + n - 1) >> 5) - g_lo + 1;
+#define L(D_) hipLaunchKernelGGL(quant_stream_i8_kernel<D_>, dim3(n_wg), dim3(512), 0, st,          \
+                                 (const __bf16*)X, g_lo, rows, (uint8_t*)img, bounds)
   if (dim == 384) L(384);
   else if (dim == 768) L(768);
   else if (dim == 1024) L(1024);

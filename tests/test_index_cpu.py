@@ -488,7 +488,8 @@ def test_int8_pruning_bound_holds_and_image_follows_writes(stream, D, monkeypatc
     int8 image (the stream image, or the row-major one with SYMB_PRUNE_STREAM=0) and its (E, X)
     follow appends, scattered overwrites and snapshot loads (1024: stream scan only)."""
     from codename_symbiont_amd.index.shard import resolve_prune
-    from codename_symbiont_amd.ops.reference import quant_rows_i8_ref, stream_i8_decode
+    from codename_symbiont_amd.ops.reference import (quant_rows_i8_ref, stream_i8_decode,
+                                                      stream_i8_tile_codes_ref)
 
     monkeypatch.setenv("SYMB_PRUNE_STREAM", stream)
     g = torch.Generator().manual_seed(5)
@@ -501,7 +502,8 @@ def test_int8_pruning_bound_holds_and_image_follows_writes(stream, D, monkeypatc
     sh.write_rows_f32([40, 7, 1999], x[2600:2603])   # scattered overwrites too
     sh.append_f32(x[2000:])
     xb = sh.rows[:sh.count]
-    x8, sx, err, xtn = quant_rows_i8_ref(xb)
+    # (the stream image: one scale per 32-row sub-tile; the row-major one: per row)
+    x8, sx, err, xtn = (stream_i8_tile_codes_ref if sh.stream else quant_rows_i8_ref)(xb)
     if sh.stream:
         y8, ysx = stream_i8_decode(sh.img_i8[:(sh.count + 31) // 32], sh.count, D)
         assert torch.equal(y8, x8) and torch.allclose(ysx, sx)

@@ -750,8 +750,8 @@ def test_quant_rows_i8_matches_reference(D):
 
 @pytest.mark.parametrize("D", [384, 768, 1024])
 def test_quant_stream_images_match_reference(D):
-    """index_stream.hip's image writers == the torch references: the int8 stream image (per-row
-    scale header + fragment-major codes) and the MX-fp4 one (fragment-major nibbles + per-lane
+    """index_stream.hip's image writers == the torch references: the int8 stream image (one scale
+    per 32-row sub-tile + fragment-major codes) and the MX-fp4 one (fragment-major nibbles + per-lane
     block-scale dwords), written for a contiguous range and for scattered rows, with (E, X) /
     (E4, X4) raised; the MX-fp4 query image (row-major nibbles + scale record) and its margin."""
     from codename_symbiont_amd.ops._ext import hip, stream_handle
@@ -769,8 +769,11 @@ def test_quant_stream_images_match_reference(D):
         # rows [0, 1000) as a range, the rest as a scattered list (reversed order)
         rows = torch.arange(n - 1, 999, -1, dtype=torch.int32, device=DEV)
         if form == 0:
-            h.quant_stream_i8(x.data_ptr(), 0, 0, 1000, D, img.data_ptr(), b.data_ptr(), st)
-            h.quant_stream_i8(x.data_ptr(), 0, rows.data_ptr(), rows.numel(), D, img.data_ptr(),
+            # (whole 32-row sub-tiles: the writer reads the padded tail rows, zeros here)
+            xp = torch.zeros(n_sub * 32, D, dtype=torch.bfloat16, device=DEV)
+            xp[:n] = x
+            h.quant_stream_i8(xp.data_ptr(), 0, 0, 1000, D, img.data_ptr(), b.data_ptr(), st)
+            h.quant_stream_i8(xp.data_ptr(), 0, rows.data_ptr(), rows.numel(), D, img.data_ptr(),
                               b.data_ptr(), st)
             ref, err, xtn = R.stream_i8_ref(x)
             torch.cuda.synchronize()
@@ -924,7 +927,7 @@ def test_append_rows_writes_rows_and_both_images(D):
     # with the MX-fp6 image as well (the append_rows_kernel FP6 form)
     img6 = torch.zeros(2, n_sub, h.stream_rec_bytes(D, 2), dtype=torch.uint8, device=DEV)
     b6 = torch.zeros(2, 2, device=DEV)
-    rows.zero_()
+    rows[0].zero_()
     h.append_rows(x.data_ptr(), n, D, rows[0].data_ptr(), r0, imgs[0][0].data_ptr(),
                   bs[0][0].data_ptr(), imgs[1][0].data_ptr(), bs[1][0].data_ptr(), st,
                   img6=img6[0].data_ptr(), b6=b6[0].data_ptr())
@@ -1475,12 +1478,13 @@ def test_index_pruned_search_mx4_tier_is_exact(nq, stream, D, monkeypatch):
         _close(s2, ts, atol=2e-5, what=f"mx4 tier {kind} scores, second search")
 
 
-@pytest.mark.parametrize("D,mx4", [(384, "1"), (384, "0"), (768, "1")])
+@pytest.mark.parametrize("D,mx4", [(384, "1"), (384, "0"), (768, "0")])
 def test_index_pruned_search_mx6_tier_is_exact(D, mx4, monkeypatch):
-    """The MX-fp6 middle tier: random held-out queries (k-th score a few sigma above the bulk: the
-    fp4 band too wide, the fp6 one narrow enough) take it -- flag 1 -- and get the exact bf16
-    results; near-duplicate queries still take the fp4 tier (flag 0) when it is kept, the fp6 one
-    otherwise; with the fp6 select's limit at 0 every batch falls through to int8 (flag 3)."""
+    """The MX-fp6 middle tier and the three-way tier flag: near-duplicate queries (their k-th score
+    far above the bulk) take the fp4 tier (flag 0) when the shard keeps it, else the fp6 one
+    (flag 1); random held-out queries, whose sample threshold T sits a few sigma above the bulk,
+    leave too many rows in the fp6 band and take int8 (flag 3); with the fp6 select's limit at 0
+    near queries fall through to int8 too.  Every search gives the exact bf16 results."""
     from codename_symbiont_amd.index.shard import HbmIndexShard
 
     monkeypatch.setenv("SYMB_PRUNE_MX6", "1")
@@ -1494,21 +1498,22 @@ def test_index_pruned_search_mx6_tier_is_exact(D, mx4, monkeypatch):
     shard.append_f32(c + 0.1 * torch.randn(3000, D, device=DEV, generator=g) / math.sqrt(D))
     rows = shard.unit_rows().float()
     shard.mq_stats = True
-    for kind, want in (("random", 1), ("near", 0 if mx4 == "1" else 1), ("int8", 3)):
-        if kind == "near":
+    for kind, want in (("near", 0 if mx4 == "1" else 1), ("random", 3), ("near-int8", 3)):
+        if kind.startswith("near"):
             q = c + 0.1 * torch.randn(nq, D, device=DEV, generator=g) / math.sqrt(D)
         else:
             q = torch.randn(nq, D, device=DEV, generator=g)
         q = torch.nn.functional.normalize(q, dim=-1).bfloat16()
-        if kind == "int8":
-            monkeypatch.setattr(shard, "MX6_LIMIT_FRAC", 0.0)
+        if kind == "near-int8":
+            monkeypatch.setattr(shard, "MX6_LIMIT_FRAC", -1.0)
+            monkeypatch.setattr(shard, "MX4_LIMIT_FRAC", -1.0)
         s1, r1 = shard.search(q, k)
         ts, _ = R.topk_ref(rows, q, k)
         torch.cuda.synchronize()
         assert int(shard._tier_last.item()) == want, (kind, int(shard._tier_last.item()))
         _close(s1, ts, atol=2e-5, what=f"mx6 tier {kind} scores")
         _close(R.row_scores_ref(rows, q, r1), ts, atol=2e-5, what=f"mx6 tier {kind} rows")
-    assert shard._mx6_tot is not None and int(shard._mx6_tot.item()) == (1 if mx4 == "1" else 2)
+    assert shard._mx6_tot is not None and int(shard._mx6_tot.item()) == (0 if mx4 == "1" else 1)
 
 
 def test_prune_qquant_and_route_match_torch():
