@@ -88,8 +88,8 @@ def test_rccl_index_group_store_roundtrip(rccl):
 
 
 def test_rccl_embed_group_matches_encoder(rccl):
-    """DP embedding (EmbedGroup: int64 header + int32 batch broadcasts, f32 all_gather of the
-    pooled rows over RCCL) == the encoder run directly."""
+    """DP embedding (EmbedGroup: int64 header + int32 batch broadcasts, all_gather of the pooled
+    rows over RCCL in the wire dtype) == the encoder run directly, rounded to that dtype."""
     from codename_symbiont_amd.models import get_config
     from codename_symbiont_amd.models.encoder import HipEncoder, synthetic_batch
     from codename_symbiont_amd.parallel.embed_group import EmbedGroup
@@ -101,5 +101,6 @@ def test_rccl_embed_group_matches_encoder(rccl):
     b = synthetic_batch(cfg, 37, 48, seed=5, varlen=True).to(rccl.device)
     got = grp.embed(b)
     want, _ = enc.forward_packed(b)
+    want = want.to(grp.wire_dtype).float()   # (the pooled rows cross the wire in its dtype)
     torch.cuda.synchronize()
     assert got.shape == want.shape and torch.equal(got, want)
