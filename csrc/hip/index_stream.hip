@@ -70,7 +70,8 @@ struct SGeo {
   static constexpr int NKS = SDim<FMT, D>::NKS;
   // MX-fp4 384: 256 queries per wave (V 0) or 128 per wave, two waves per workgroup (V 1); the
   // wider rows hold fewer resident sets (1024: int8 one set, 4 waves = 128 queries per workgroup).
-  // V 2 / 3: the default form one sub-tile deeper / shallower in flight (A/B).
+  // V 2 / 3: the default form one sub-tile deeper / shallower in flight (A/B); V 4 (int8): the
+  // 16 x 16 x 64 MFMA shape on the same image (see scan_stream_kernel I16).
   static constexpr int SETS = FMT == SF_MX4 ? (D == 384 && V != 1 ? 8 : D == 1024 ? 2 : 4)
                             : FMT == SF_MX6 ? (D == 384 ? 4 : 2)
                                             : (D == 384 ? 4 : D == 768 ? 2 : 1);
@@ -87,7 +88,8 @@ struct SGeo {
   static constexpr int LHDR = FMT == SF_I8 ? 256 : 0;   // the header's LDS bytes (DMA: 4 B x 64 lanes)
   static constexpr int SLOT = (SDim<FMT, D>::REC - SDim<FMT, D>::HDR + LHDR + 1023) / 1024 * 1024;
   static constexpr int LDEPTH = FMT == SF_MX4 && D == 384 ? 4 : 2;
-  static constexpr bool LAND_OK = FMT != SF_MX6 && (D == 384 || (D == 768 && FMT == SF_MX4));
+  static constexpr bool LAND_OK =
+      FMT != SF_MX6 && V != 4 && (D == 384 || (D == 768 && FMT == SF_MX4));
   static_assert(SETS * NKS * SDim<FMT, D>::LB / 4 <= 192, "resident query operands");
   static_assert(NW >= 1 && NW <= 4, "waves per workgroup");
 };
@@ -164,16 +166,35 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
       return *reinterpret_cast<const i32x4s*>(p);
     }
   };
+  // I16 (int8, V 4): v_mfma_i32_16x16x64_i8 on the same image -- per set and sub-tile four 16 x 16
+  // blocks (row half rh, query half qh) of NKS / 2 64-deep k-steps: the A operand of lane l is
+  // row 16 rh + (l & 15), bytes 64 K + 16 (l >> 4), i.e. 16 bytes at 1024 (2 K + (l >> 5)) +
+  // 16 (32 ((l >> 4) & 1) + 16 rh + (l & 15)) of the record; the result of lane l is query
+  // 16 qh + (l & 15), rows 16 rh + 4 (l >> 4) + r.  qf[s][2 K + qh], fk[d][2 K + rh]; a lane's
+  // 16 values e = 8 rh + 4 qh + r.
+  constexpr bool I16 = FMT == SF_I8 && V == 4;
   FragT qf[SETS][NKS];
   uint32_t qs[SETS][NSC];
   float thr[SETS];
+  float thr2[SETS][2];   // (I16) the thresholds of the lane's two queries
 #pragma unroll
   for (int s = 0; s < SETS; ++s) {
     const int q = qw + 32 * s + (lane & 31);
     const int qq = min(q, NQ - 1);
     const uint8_t* qp = Q + (size_t)qq * S::RB + S::LB * h;
+    if constexpr (I16) {
 #pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) qf[s][ks] = frag_at(qp + 2 * S::LB * ks, 12);
+      for (int qh = 0; qh < 2; ++qh) {
+        const int q2 = qw + 32 * s + 16 * qh + (lane & 15);
+        const uint8_t* qp2 = Q + (size_t)min(q2, NQ - 1) * S::RB + 16 * (lane >> 4);
+#pragma unroll
+        for (int K = 0; K < NKS / 2; ++K) qf[s][2 * K + qh] = *reinterpret_cast<const i32x4s*>(qp2 + 64 * K);
+        thr2[s][qh] = q2 < NQ ? thr_in[q2] : INFINITY;
+      }
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) qf[s][ks] = frag_at(qp + 2 * S::LB * ks, 12);
+    }
 #pragma unroll
     for (int j = 0; j < NSC; ++j) {
       if constexpr (FMT != SF_I8)
@@ -244,9 +265,18 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
     const uint8_t* r = rec0 + (size_t)min(i, ns - 1) * REC;   // (past the end: the last again)
     if constexpr (FMT == SF_I8) fts[d] = *reinterpret_cast<const float*>(r);
     // (MX-fp6: lane l's 24 bytes are 12 in the k-step's first 768-byte plane and 12 in its second)
-    const uint8_t* f = r + S::HDR + (FMT == SF_MX6 ? 12 : 16) * lane;
+    if constexpr (I16) {
+      const uint8_t* f = r + S::HDR + 1024 * (lane >> 5) + 16 * (32 * ((lane >> 4) & 1) + (lane & 15));
 #pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) fk[d][ks] = frag_at(f + 64 * S::LB * ks, 768);
+      for (int K = 0; K < NKS / 2; ++K)
+#pragma unroll
+        for (int rh = 0; rh < 2; ++rh)
+          fk[d][2 * K + rh] = *reinterpret_cast<const i32x4s*>(f + 2048 * K + 256 * rh);
+    } else {
+      const uint8_t* f = r + S::HDR + (FMT == SF_MX6 ? 12 : 16) * lane;
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) fk[d][ks] = frag_at(f + 64 * S::LB * ks, 768);
+    }
     if constexpr (FMT != SF_I8) {
 #pragma unroll
       for (int j = 0; j < NSC; ++j)
@@ -258,7 +288,19 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
   auto acc_i8 = [&](auto dc, auto sc) {
     constexpr int d = decltype(dc)::value, s = decltype(sc)::value;
     i32x16s acc = {};
-    if constexpr (FMT == SF_I8) {
+    if constexpr (I16) {
+      i32x4s c[2][2] = {};
+#pragma unroll
+      for (int K = 0; K < NKS / 2; ++K)
+#pragma unroll
+        for (int rh = 0; rh < 2; ++rh)
+#pragma unroll
+          for (int qh = 0; qh < 2; ++qh)
+            c[rh][qh] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fk[d][2 * K + rh], qf[s][2 * K + qh],
+                                                             c[rh][qh], 0, 0, 0);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e] = c[e >> 3][(e >> 2) & 1][e & 3];
+    } else if constexpr (FMT == SF_I8) {
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks)
         acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(fk[d][ks], qf[s][ks], acc, 0, 0, 0);
@@ -346,7 +388,14 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
       static_for<0, SETS>([&](auto sc) {
         constexpr int s = decltype(sc)::value;
         if (!((pass >> s) & 1u)) return;
-        if constexpr (FMT == SF_I8) {   // (the sub-tile's scale > 0 keeps the order)
+        if constexpr (I16) {   // each query half against its own threshold
+          const i32x16s acc = acc_i8(dc, sc);
+          const int m0 = max(max(max(acc[0], acc[1]), max(acc[2], acc[3])),
+                             max(max(acc[8], acc[9]), max(acc[10], acc[11])));
+          const int m1 = max(max(max(acc[4], acc[5]), max(acc[6], acc[7])),
+                             max(max(acc[12], acc[13]), max(acc[14], acc[15])));
+          hm |= ((float)m0 * fts[d] >= thr2[s][0] || (float)m1 * fts[d] >= thr2[s][1] ? 1u : 0u) << s;
+        } else if constexpr (FMT == SF_I8) {   // (the sub-tile's scale > 0 keeps the order)
           const i32x16s acc = acc_i8(dc, sc);
           int m = max(max(acc[0], acc[1]), acc[2]);
 #pragma unroll
@@ -368,8 +417,18 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
         block(dc, sc, v);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int row = row0 + (r & 3) + 8 * (r >> 2);
-          const bool p = v[r] >= thr[s] && row < row_end;
+          int row, ql;
+          float t;
+          if constexpr (I16) {
+            row = (g0 + i) * 32 + 16 * (r >> 3) + 4 * (lane >> 4) + (r & 3);
+            ql = 32 * s + 16 * ((r >> 2) & 1) + (lane & 15);
+            t = thr2[s][(r >> 2) & 1];
+          } else {
+            row = row0 + (r & 3) + 8 * (r >> 2);
+            ql = 32 * s + (lane & 31);
+            t = thr[s];
+          }
+          const bool p = v[r] >= t && row < row_end;
           const uint64_t m = __builtin_amdgcn_ballot_w64(p);
           if (m) {
             if (nst > STW - 64) flush();
@@ -378,7 +437,7 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
             if (p) {
               st_s[idx] = v[r];
               st_r[idx] = row;
-              st_q[idx] = (uint16_t)(32 * s + (lane & 31));
+              st_q[idx] = (uint16_t)ql;
             }
             nst += __builtin_popcountll(m);
           }
@@ -895,7 +954,7 @@ int symb_stream_rec_bytes(int dim, int form) {
 // it is sized (int8 / MX-fp4 384, MX-fp4 768; variant 0)
 static int g_stream_mx4_v = 0, g_stream_i8_v = 0, g_stream_abl = 0, g_stream_land = 0;
 int symb_stream_config(int mx4_variant, int i8_variant, int abl, int land) {
-  if (mx4_variant < 0 || mx4_variant > 3 || (i8_variant != 0 && i8_variant != 2 && i8_variant != 3) ||
+  if (mx4_variant < 0 || mx4_variant > 3 || i8_variant < 0 || i8_variant > 4 || i8_variant == 1 ||
       abl < 0 || abl > 2 || land < 0 || land > 1)
     return -1;
   g_stream_mx4_v = mx4_variant;
@@ -1011,6 +1070,7 @@ int symb_index_scan_stream(const void* img, int n_valid, int alloc_rows, int row
     switch (g_stream_i8_v) {
       case 2: return L(SF_I8, 384, 2);
       case 3: return L(SF_I8, 384, 3);
+      case 4: return L(SF_I8, 384, 4);
       default: return L(SF_I8, 384, 0);
     }
   }

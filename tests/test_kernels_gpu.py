@@ -939,14 +939,16 @@ def test_append_rows_writes_rows_and_both_images(D):
     _close(b6[0], b6[1], atol=0, rtol=1e-6, what="append fp6 bounds")
 
 
-@pytest.mark.parametrize("form,D", [(0, 384), (1, 384), (0, 768), (1, 768), (0, 1024), (1, 1024),
-                                    (2, 384), (2, 768)])
-def test_index_scan_stream_emits_the_bound_set(form, D, monkeypatch):
+@pytest.mark.parametrize("form,D,i8v", [(0, 384, 0), (1, 384, 0), (0, 768, 0), (1, 768, 0),
+                                        (0, 1024, 0), (1, 1024, 0), (2, 384, 0), (2, 768, 0),
+                                        (0, 384, 4)])
+def test_index_scan_stream_emits_the_bound_set(form, D, i8v, monkeypatch, request):
     """index_stream.hip scan_stream_kernel (v_mfma_i32_32x32x32_i8 / v_mfma_scale_f32_32x32x64
     on fragment-major images, one wave per SIMD): exactly the rows whose estimate (int8: (q8 .
     x8) sx, MX-fp4: the decoded dot) reaches the threshold, for 1, 2 and 3 query blocks, a ragged
     row count and skipped row blocks -- pins the fragment layout, the accumulator row map, the
-    row-scale header and the block-scale bytes' lane / k-step mapping."""
+    row-scale header and the block-scale bytes' lane / k-step mapping.  i8v 4: the int8 scan on
+    the 16 x 16 x 64 MFMA shape (stream_config i8 variant 4) over the same image."""
     from codename_symbiont_amd.index.shard import HbmIndexShard
     from codename_symbiont_amd.ops._ext import hip, stream_handle
 
@@ -956,6 +958,8 @@ def test_index_scan_stream_emits_the_bound_set(form, D, monkeypatch):
     shard.fill_random(n, seed=5)
     assert shard.stream and (shard.img_i8 is not None) and (shard.img_mx4 is not None)
     h, st = hip(), stream_handle(shard.device)
+    h.stream_config(0, i8v)
+    request.addfinalizer(lambda: h.stream_config(0, 0))
     if form == 0:
         x8, sx = R.stream_i8_decode(shard.img_i8[:(n + 31) // 32], n, D)
         img = shard.img_i8
