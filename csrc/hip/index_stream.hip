@@ -94,15 +94,6 @@ struct SGeo {
   static_assert(NW >= 1 && NW <= 4, "waves per workgroup");
 };
 
-// compile-time loop: f(integral_constant<int, i>) for i = I .. N - 1
-template <int I, int N, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (I < N) {
-    f(std::integral_constant<int, I>());
-    static_for<I + 1, N>(f);
-  }
-}
-
 __device__ __forceinline__ float max16(const float (&v)[16]) {
   float a = __builtin_fmaxf(__builtin_fmaxf(v[0], v[1]), v[2]);   // v_max3_f32 chains
   float b = __builtin_fmaxf(__builtin_fmaxf(v[3], v[4]), v[5]);
@@ -949,12 +940,13 @@ int symb_stream_rec_bytes(int dim, int form) {
 }
 
 // scan forms (symb_stream_config, A/B): variant 0 = default, 1 = MX-fp4 384 with 128 queries per
-// wave x 2 waves, 2 / 3 = one sub-tile deeper / shallower in flight (register ring, D = 384);
+// wave x 2 waves, 2 / 3 = one sub-tile deeper / shallower in flight (register ring, D = 384),
+// int8 4 = the 16 x 16 x 64 MFMA shape, int8 5 .. 9 = the LDS-query scan's forms (index_lq.hip);
 // abl: the kernel's timing ablations (ABL above; wrong results); land: the LDS-landing form where
 // it is sized (int8 / MX-fp4 384, MX-fp4 768; variant 0)
 static int g_stream_mx4_v = 0, g_stream_i8_v = 0, g_stream_abl = 0, g_stream_land = 0;
 int symb_stream_config(int mx4_variant, int i8_variant, int abl, int land) {
-  if (mx4_variant < 0 || mx4_variant > 3 || i8_variant < 0 || i8_variant > 4 || i8_variant == 1 ||
+  if (mx4_variant < 0 || mx4_variant > 3 || i8_variant < 0 || i8_variant > 9 || i8_variant == 1 ||
       abl < 0 || abl > 2 || land < 0 || land > 1)
     return -1;
   g_stream_mx4_v = mx4_variant;
@@ -964,8 +956,23 @@ int symb_stream_config(int mx4_variant, int i8_variant, int abl, int land) {
   return 0;
 }
 
+// the LDS-query int8 scan (index_lq.hip): i8 variants 5 .. 9 = its forms 0 .. 4
+int symb_lq_qpb(int dim);
+int symb_index_scan_lq(const void* img, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
+                       int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
+                       hipStream_t st, const int* skip, int dim, const int* gate, int gate_want,
+                       int* runs, int form);
+static bool lq_on(int dim, int form) {
+  return form == 0 && g_stream_i8_v >= 5 && symb_lq_qpb(dim) > 0;
+}
+
 // queries per workgroup and workgroups per CU (one wave per SIMD) of the stream scan
 int symb_stream_geometry(int dim, int form, int* qpb, int* wgs_per_cu) {
+  if (lq_on(dim, form)) {
+    *qpb = symb_lq_qpb(dim);
+    *wgs_per_cu = 1;
+    return 0;
+  }
 #define G_(F, D_, V_)                                \
   do {                                               \
     *qpb = SGeo<F, D_, V_>::QPB;                     \
@@ -1049,6 +1056,10 @@ int symb_index_scan_stream(const void* img, int n_valid, int alloc_rows, int row
 #define LA(F, D_, A_, L_) launch_stream<F, D_, 0, A_, L_>(img, n_valid, rows_per_blk, n_rblk, Q, qsc, \
                                                           NQ, thr, cand_s, cand_i, cand_n, cap, xcd, \
                                                           st, skip, gate, gate_want, runs, ca)
+  if (lq_on(dim, form))
+    return symb_index_scan_lq(img, n_valid, rows_per_blk, n_rblk, Q, NQ, thr, cand_s, cand_i,
+                              cand_n, cap, st, skip, dim, gate, gate_want, runs,
+                              g_stream_i8_v - 5);
   if (form == 2) return dim == 384 ? L(SF_MX6, 384, 0) : L(SF_MX6, 768, 0);
   if (dim == 768 && form == 1 && land) return LA(SF_MX4, 768, 0, 1);
   if (dim == 384) {

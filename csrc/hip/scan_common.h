@@ -18,6 +18,15 @@ __device__ __forceinline__ void glds16_aux(const void* gsrc, void* lds_wave_base
       (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, AUX);
 }
 
+// compile-time loop: f(integral_constant<int, i>) for i = I .. N - 1
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>());
+    static_for<I + 1, N>(f);
+  }
+}
+
 // no-op DMA functor for MFMA chains that issue no LDS-DMA pieces
 struct NoDma {
   __device__ __forceinline__ void operator()(int) const {}
