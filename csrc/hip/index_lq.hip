@@ -38,10 +38,9 @@ struct LqGeo {
   static_assert(LDS <= 160 * 1024, "LDS");
 };
 
-// CH: independent accumulation chains per set (the 12 k-steps split round-robin, summed for the
-// test); timing ablations (wrong results): ABL 2 = no sub-tile loads after the prologue, 3 = that
-// and no LDS fragment reads either (every set multiplies the registers of set 0).
-template <int D, int DEPTH, int CH = 1, int ABL = 0>
+// NP: sub-tiles (ring slots) each LDS query fragment feeds -- 2 halves the LDS read bytes per
+// MFMA; timing ablation ABL 2 (wrong results): no sub-tile loads after the prologue.
+template <int D, int DEPTH, int NP = 1, int ABL = 0>
 __global__ __launch_bounds__(256, 1) void scan_lq_i8_kernel(
     const uint8_t* __restrict__ img, int n_valid, int rows_per_blk, const uint8_t* __restrict__ Q,
     int NQ, int n_qblk, const float* __restrict__ thr_in, float* __restrict__ cand_s,
@@ -119,19 +118,17 @@ __global__ __launch_bounds__(256, 1) void scan_lq_i8_kernel(
     return *reinterpret_cast<const i32x4q*>(smem + 1024 * (s * NKS + ks) + 16 * lane);
   };
 
-  // Query fragments double-buffered in registers: while set s's 12 MFMAs run from qf2[s & 1],
-  // the 12 ds_read_b128 of set s + 1 (set 0 of the NEXT sub-tile after set 7) fill qf2[~s & 1],
-  // one read per MFMA (sched_group_barrier pins the pairing: left to itself hipcc issued each
+  // Query fragments double-buffered in registers: while set s's MFMAs run from qf2[s & 1], the
+  // 12 ds_read_b128 of set s + 1 (set 0 of the NEXT slot group after set 7) fill qf2[~s & 1], one
+  // read per NP MFMAs (sched_group_barrier pins the pairing: left to itself hipcc issued each
   // read right before its MFMA and waited lgkmcnt(0) on it, one LDS round trip per MFMA), and the
-  // hit test of set s - 1 rides in the VALU gaps of set s's MFMAs (two accumulators).
+  // hit test of set s - 1 rides in the VALU gaps of set s's MFMAs (two accumulator sets).
+  static_assert(DEPTH % NP == 0, "slot groups");
   i32x4q qf2[2][NKS];
 #pragma unroll
   for (int ks = 0; ks < NKS; ++ks) qf2[0][ks] = qfrag(0, ks);
-  i32x16q acc[2][CH];
-  auto hit_test = [&](const i32x16q (&a)[CH], float ts, float t) -> bool {
-    i32x16q x = a[0];
-#pragma unroll
-    for (int c = 1; c < CH; ++c) x += a[c];
+  i32x16q acc[2][NP];
+  auto hit_test = [&](const i32x16q& x, float ts, float t) -> bool {
     int m = max(max(x[0], x[1]), x[2]);
 #pragma unroll
     for (int r = 3; r < 15; r += 2) m = max(max(m, x[r]), x[r + 1]);
@@ -139,33 +136,44 @@ __global__ __launch_bounds__(256, 1) void scan_lq_i8_kernel(
     return (float)m * ts >= t;   // (the sub-tile's scale > 0 keeps the order)
   };
 
-  auto process = [&](auto dc, int j) {
-    constexpr int d = decltype(dc)::value;
-    uint32_t hm = 0;   // sets with a hit in this lane
+  // slots d0 .. d0 + NP - 1 hold the wave's sub-tiles j0 .. j0 + NP - 1
+  auto process = [&](auto dc, int j0) {
+    constexpr int d0 = decltype(dc)::value;
+    uint32_t hm[NP] = {};   // per slot: sets with a hit in this lane
     static_for<0, SETS>([&](auto sc) {
       constexpr int s = decltype(sc)::value, b = s & 1, nb = b ^ 1;
       constexpr int sn = s + 1 < SETS ? s + 1 : 0;
 #pragma unroll
-      for (int c = 0; c < CH; ++c) acc[b][c] = i32x16q{};
+      for (int p = 0; p < NP; ++p) acc[b][p] = i32x16q{};
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
-        acc[b][ks % CH] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fk[d][ks], qf2[b][ks],
-                                                               acc[b][ks % CH], 0, 0, 0);
-        if constexpr (ABL != 3) qf2[nb][ks] = qfrag(sn, ks);
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+          acc[b][p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fk[d0 + p][ks], qf2[b][ks], acc[b][p],
+                                                           0, 0, 0);
+        qf2[nb][ks] = qfrag(sn, ks);
       }
-      if constexpr (s > 0) hm |= (hit_test(acc[nb], fts[d], thr[s - 1]) ? 1u : 0u) << (s - 1);
+      if constexpr (s > 0) {
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+          hm[p] |= (hit_test(acc[nb][p], fts[d0 + p], thr[s - 1]) ? 1u : 0u) << (s - 1);
+      }
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA ...
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // ... one LDS read
+        __builtin_amdgcn_sched_group_barrier(0x008, NP, 0);   // NP MFMAs ...
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);    // ... one LDS read
       }
     });
-    hm |= (hit_test(acc[(SETS - 1) & 1], fts[d], thr[SETS - 1]) ? 1u : 0u) << (SETS - 1);
-    if (__builtin_amdgcn_ballot_w64(hm != 0)) {   // rare: recompute the hit sets, emit per row
-      const int row0 = (g0 + wave + 4 * j) * 32 + 4 * h;   // + (r & 3) + 8 (r >> 2)
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+      hm[p] |= (hit_test(acc[(SETS - 1) & 1][p], fts[d0 + p], thr[SETS - 1]) ? 1u : 0u) << (SETS - 1);
+    static_for<0, NP>([&](auto pc) {
+      constexpr int p = decltype(pc)::value, d = d0 + p;
+      if (!__builtin_amdgcn_ballot_w64(hm[p] != 0)) return;   // rare: recompute the hit sets
+      const int row0 = (g0 + wave + 4 * (j0 + p)) * 32 + 4 * h;   // + (r & 3) + 8 (r >> 2)
       static_for<0, SETS>([&](auto sc) {
         constexpr int s = decltype(sc)::value;
-        if (!__builtin_amdgcn_ballot_w64((hm >> s) & 1)) return;
+        if (!__builtin_amdgcn_ballot_w64((hm[p] >> s) & 1)) return;
         i32x16q a = {};
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks)
@@ -174,13 +182,13 @@ __global__ __launch_bounds__(256, 1) void scan_lq_i8_kernel(
         for (int r = 0; r < 16; ++r) {
           const float v = (float)a[r] * fts[d];
           const int row = row0 + (r & 3) + 8 * (r >> 2);
-          const bool p = v >= thr[s] && row < row_end;
-          const uint64_t mk = __builtin_amdgcn_ballot_w64(p);
+          const bool pr = v >= thr[s] && row < row_end;
+          const uint64_t mk = __builtin_amdgcn_ballot_w64(pr);
           if (mk) {
             if (nst > STW - 64) flush();
             const int idx = nst + (int)__builtin_amdgcn_mbcnt_hi(
                                       (uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0));
-            if (p) {
+            if (pr) {
               st_s[idx] = v;
               st_r[idx] = row;
               st_q[idx] = (uint16_t)(32 * s + (lane & 31));
@@ -189,7 +197,7 @@ __global__ __launch_bounds__(256, 1) void scan_lq_i8_kernel(
           }
         }
       });
-    }
+    });
   };
 
   // prologue: DEPTH sub-tiles in flight; then use one / refill its slot (the last round may run
@@ -197,23 +205,27 @@ __global__ __launch_bounds__(256, 1) void scan_lq_i8_kernel(
   // emit nothing -- a branch-free body keeps the loads' waits counted)
   static_for<0, DEPTH>([&](auto dc) { load(dc, decltype(dc)::value); });
   for (int j0 = 0; j0 < nsw; j0 += DEPTH) {
-    static_for<0, DEPTH>([&](auto dc) {
-      constexpr int d = decltype(dc)::value;
-      process(dc, j0 + d);
-      if constexpr (ABL < 2) load(dc, j0 + d + DEPTH);
+    static_for<0, DEPTH / NP>([&](auto gc) {
+      constexpr int d0 = decltype(gc)::value * NP;
+      process(std::integral_constant<int, d0>(), j0 + d0);
+      if constexpr (ABL < 2)
+        static_for<0, NP>([&](auto pc) {
+          constexpr int d = d0 + decltype(pc)::value;
+          load(std::integral_constant<int, d>(), j0 + d + DEPTH);
+        });
     });
   }
   if (nst) flush();
 }
 
-template <int D, int DEPTH, int CH = 1, int ABL = 0>
+template <int D, int DEPTH, int NP = 1, int ABL = 0>
 static int launch_lq(const void* img, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                      int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
                      hipStream_t st, const int* skip, const int* gate, int gate_want, int* runs) {
   using G = LqGeo<D>;
   const int n_qblk = (NQ + G::QPB - 1) / G::QPB;
-  set_max_lds<scan_lq_i8_kernel<D, DEPTH, CH, ABL>>(G::LDS);
-  hipLaunchKernelGGL((scan_lq_i8_kernel<D, DEPTH, CH, ABL>), dim3(n_rblk * n_qblk), dim3(64 * G::NW), G::LDS,
+  set_max_lds<scan_lq_i8_kernel<D, DEPTH, NP, ABL>>(G::LDS);
+  hipLaunchKernelGGL((scan_lq_i8_kernel<D, DEPTH, NP, ABL>), dim3(n_rblk * n_qblk), dim3(64 * G::NW), G::LDS,
                      st, (const uint8_t*)img, n_valid, rows_per_blk, (const uint8_t*)Q, NQ, n_qblk,
                      thr, cand_s, cand_i, cand_n, cap, skip, gate, gate_want, runs);
   return (int)hipGetLastError();
@@ -227,9 +239,8 @@ using namespace symb;
 int symb_lq_qpb(int dim) { return dim == 384 ? LqGeo<384>::QPB : dim == 768 ? LqGeo<768>::QPB : 0; }
 
 // The LDS-query int8 scan over rows [0, n_valid) of an int8 stream image (the arguments of
-// symb_index_scan_stream, form 0); form (A/B): 0 = the default, 1 = two accumulation chains per
-// set, 2 / 3 = those two with the no-refill timing ablation, 4 = no refills and no LDS reads
-// (ablations: wrong results).
+// symb_index_scan_stream, form 0); form (A/B): 0 = the default (3 slots), 1 = its no-refill
+// timing ablation (wrong results).  (NP = 2 with 4 slots spills at 512 VGPRs.)
 int symb_index_scan_lq(const void* img, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                        int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
                        hipStream_t st, const int* skip, int dim, const int* gate, int gate_want,
@@ -239,10 +250,7 @@ int symb_index_scan_lq(const void* img, int n_valid, int rows_per_blk, int n_rbl
                             cap, st, skip, gate, gate_want, runs)
   if (dim == 384) {
     switch (form) {
-      case 1: return L(384, 3, 2, 0);
-      case 2: return L(384, 3, 1, 2);
-      case 3: return L(384, 3, 2, 2);
-      case 4: return L(384, 3, 1, 3);
+      case 1: return L(384, 3, 1, 2);
       default: return L(384, 3, 1, 0);
     }
   }

@@ -941,12 +941,12 @@ int symb_stream_rec_bytes(int dim, int form) {
 
 // scan forms (symb_stream_config, A/B): variant 0 = default, 1 = MX-fp4 384 with 128 queries per
 // wave x 2 waves, 2 / 3 = one sub-tile deeper / shallower in flight (register ring, D = 384),
-// int8 4 = the 16 x 16 x 64 MFMA shape, int8 5 .. 9 = the LDS-query scan's forms (index_lq.hip);
+// int8 4 = the 16 x 16 x 64 MFMA shape, int8 5 / 6 = the LDS-query scan's forms (index_lq.hip);
 // abl: the kernel's timing ablations (ABL above; wrong results); land: the LDS-landing form where
 // it is sized (int8 / MX-fp4 384, MX-fp4 768; variant 0)
 static int g_stream_mx4_v = 0, g_stream_i8_v = 0, g_stream_abl = 0, g_stream_land = 0;
 int symb_stream_config(int mx4_variant, int i8_variant, int abl, int land) {
-  if (mx4_variant < 0 || mx4_variant > 3 || i8_variant < 0 || i8_variant > 9 || i8_variant == 1 ||
+  if (mx4_variant < 0 || mx4_variant > 3 || i8_variant < 0 || i8_variant > 6 || i8_variant == 1 ||
       abl < 0 || abl > 2 || land < 0 || land > 1)
     return -1;
   g_stream_mx4_v = mx4_variant;
@@ -956,7 +956,7 @@ int symb_stream_config(int mx4_variant, int i8_variant, int abl, int land) {
   return 0;
 }
 
-// the LDS-query int8 scan (index_lq.hip): i8 variants 5 .. 9 = its forms 0 .. 4
+// the LDS-query int8 scan (index_lq.hip): i8 variants 5 / 6 = its forms 0 / 1
 int symb_lq_qpb(int dim);
 int symb_index_scan_lq(const void* img, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                        int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,

@@ -940,7 +940,7 @@ def test_append_rows_writes_rows_and_both_images(D):
 
 
 @pytest.mark.parametrize("form,D,i8v", [(0, 384, 0), (1, 384, 0), (0, 768, 0), (1, 768, 0),
-                                        (0, 384, 5), (0, 384, 6), (0, 768, 5),
+                                        (0, 384, 5), (0, 768, 5),
                                         (0, 1024, 0), (1, 1024, 0), (2, 384, 0), (2, 768, 0),
                                         (0, 384, 4)])
 def test_index_scan_stream_emits_the_bound_set(form, D, i8v, monkeypatch, request):
