@@ -5,7 +5,7 @@
     tile: symb_gemm_config tile mode (3 = auto with the 256x192 tile, 10 = round-3 auto,
     2 = 256x256 wherever N % 256 == 0);
     --torch runs torch.matmul (hipBLASLt) on the same operands instead; --pp 256 the ping-pong
-    kernel (gemm_pp.hip) with 256-row tiles.
+    kernel (gemm_pp.hip) with 256-row tiles; --vs 0 the VGPR-staged 4-wave kernel (gemm_vs.hip).
 Prints one JSON line: ms per call and TFLOP/s.
 """
 from __future__ import annotations
@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--ring", type=int, default=1, help="ping-pong 256-row tiles on the half-tile ring")
     ap.add_argument("--pp", type=int, default=-1,
                     help="ping-pong kernel tile rows (gemm_pp.hip: 0 auto, 256, 128; -1 off)")
+    ap.add_argument("--vs", type=int, default=-1,
+                    help="VGPR-staged 4-wave kernel (gemm_vs.hip) tile columns: 0 auto, 256, 192; -1 off")
     a = ap.parse_args()
     from codename_symbiont_amd.ops import kernels as K
     from codename_symbiont_amd.ops._ext import hip
@@ -49,6 +51,7 @@ def main():
     hip().gemm_lt_config(a.lt)
     hip().gemm_pp_config(0 if a.pp < 0 else 2, max(a.pp, 0))
     hip().gemm_pp_ring(a.ring)
+    hip().gemm_vs_config(0 if a.vs < 0 else 2, max(a.vs, 0))
     f = (lambda: torch.matmul(x, w.t(), out=y)) if a.torch else (lambda: K.gemm(x, w, b, a.epi, r, out=y))
     for _ in range(3):
         f()

@@ -3,7 +3,8 @@
 
     python benchmarks/gemm_sweep.py [--models bge-base,e5-large] [--variants t3,t9,lt,torch]
 
-Variants: pp / pp256 / pp128 = the ping-pong kernel (gemm_pp.hip; auto / forced tile rows; a
+Variants: vs / vs256 / vs192 = the VGPR-staged 4-wave kernel (gemm_vs.hip; auto / forced tile
+columns); pp / pp256 / pp128 = the ping-pong kernel (gemm_pp.hip; auto / forced tile rows; a
 "v1" suffix: two k-tile buffers instead of the half-tile ring);
 tN = symb_gemm with tile mode N (3 = auto with the 256x192 tile, 10 = the round-3
 auto rule, 2 = the 256x256 tile wherever N % 256 == 0), hipBLASLt route off; lt = the hipBLASLt
@@ -63,6 +64,11 @@ def main():
                     return lambda: (hip().gemm_config(128, 10, 8), hip().gemm_pp_config(0),
                                     hip().gemm_lt_config(1), K.gemm(x, w, b, epi, r, out=y),
                                     hip().gemm_lt_config(0))
+                if v.startswith("vs"):   # vs / vs256 / vs192: gemm_vs.hip (auto / forced width)
+                    bn = int(v[2:] or 0)
+                    return lambda: (hip().gemm_config(128, 3, 8), hip().gemm_lt_config(0),
+                                    hip().gemm_pp_config(0), hip().gemm_vs_config(2, bn),
+                                    K.gemm(x, w, b, epi, r, out=y), hip().gemm_vs_config(0))
                 if v.startswith("pp"):
                     ring = 0 if v.endswith("v1") else 1
                     bm = int(v[2:].replace("v1", "") or 0)

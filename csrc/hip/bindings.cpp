@@ -140,6 +140,7 @@ int symb_prune_qprep(const void* Q, int NQ, int dim, const float* pre_s, const f
 int symb_gemm_lt_config(int mode);
 int symb_gemm_pp_mode(int mode, int bm);
 int symb_gemm_pp_ring(int ring);
+int symb_gemm_vs_mode(int mode, int bn);
 int symb_mfma_f8f6f4_probe(const int* a, const int* b, const int* sa, const int* sb, float* out,
                            int fmt, hipStream_t st);
 int symb_gemm_lt_plans();
@@ -647,6 +648,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gemm_pp_config", [](int mode, int bm) { check(symb_gemm_pp_mode(mode, bm), "gemm_pp_config"); },
         py::arg("mode"), py::arg("bm") = 0);
   m.def("gemm_pp_ring", [](int ring) { check(symb_gemm_pp_ring(ring), "gemm_pp_ring"); });
+  m.def("gemm_vs_config", [](int mode, int bn) { check(symb_gemm_vs_mode(mode, bn), "gemm_vs_config"); },
+        py::arg("mode"), py::arg("bn") = 0);
   m.def("mfma_f8f6f4_probe", [](uptr a, uptr b, uptr sa, uptr sb, uptr out, int fmt, uptr st) {
     check(symb_mfma_f8f6f4_probe(P<const int>(a), P<const int>(b), P<const int>(sa),
                                  P<const int>(sb), P<float>(out), fmt, S(st)),

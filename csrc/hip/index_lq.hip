@@ -51,9 +51,12 @@ __global__ __launch_bounds__(256, 1) void scan_lq_i8_kernel(
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // (wave-uniform: scalar loop control)
-  const int qb = blockIdx.x % n_qblk, rb = blockIdx.x / n_qblk;
+  // (XCD-contiguous block order: the query blocks of one row block -- two at D = 768 -- run on
+  // one XCD, so the second read of each row hits that XCD's L2 / the Infinity Cache)
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int qb = lb % n_qblk, rb = lb / n_qblk;
   if (gate != nullptr && *gate != gate_want) return;   // (workgroup-uniform exits only)
-  if (runs != nullptr && blockIdx.x == 0 && tid == 0) atomicAdd(runs, 1);
+  if (runs != nullptr && lb == 0 && tid == 0) atomicAdd(runs, 1);
   if (skip != nullptr && skip[rb] != 0) return;
   const int row_begin = rb * rows_per_blk;
   const int row_end = min(row_begin + rows_per_blk, n_valid);

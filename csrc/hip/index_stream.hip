@@ -962,8 +962,10 @@ int symb_index_scan_lq(const void* img, int n_valid, int rows_per_blk, int n_rbl
                        int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
                        hipStream_t st, const int* skip, int dim, const int* gate, int gate_want,
                        int* runs, int form);
+// (the default int8 form at D = 768: 100M x 768 held-out 37.8 -> 25.1 ms, profiles/r5_lq/)
 static bool lq_on(int dim, int form) {
-  return form == 0 && g_stream_i8_v >= 5 && symb_lq_qpb(dim) > 0;
+  return form == 0 && (g_stream_i8_v >= 5 || (g_stream_i8_v == 0 && dim == 768)) &&
+         symb_lq_qpb(dim) > 0;
 }
 
 // queries per workgroup and workgroups per CU (one wave per SIMD) of the stream scan
@@ -1059,7 +1061,7 @@ int symb_index_scan_stream(const void* img, int n_valid, int alloc_rows, int row
   if (lq_on(dim, form))
     return symb_index_scan_lq(img, n_valid, rows_per_blk, n_rblk, Q, NQ, thr, cand_s, cand_i,
                               cand_n, cap, st, skip, dim, gate, gate_want, runs,
-                              g_stream_i8_v - 5);
+                              g_stream_i8_v >= 5 ? g_stream_i8_v - 5 : 0);
   if (form == 2) return dim == 384 ? L(SF_MX6, 384, 0) : L(SF_MX6, 768, 0);
   if (dim == 768 && form == 1 && land) return LA(SF_MX4, 768, 0, 1);
   if (dim == 384) {

@@ -141,6 +141,35 @@ def test_gemm_pingpong(M, N, K, epi, bm, ring):
     _close(out, ref, atol=4e-2, rtol=2e-2, what=f"pingpong gemm bm={bm} epi={epi}")
 
 
+@pytest.mark.parametrize("bn", [0, 256, 192])
+@pytest.mark.parametrize("M,N,K,epi", [
+    (300, 768, 128, 0), (1000, 768, 768, 2), (2049, 2304, 768, 0), (4353, 768, 3072, 2),
+    (777, 3072, 768, 1), (5000, 1024, 4096, 2), (257, 768, 320, 1), (32768, 768, 768, 0),
+    (130, 4608, 1024, 1), (600, 1536, 64, 0),
+])
+def test_gemm_vgpr_staged(M, N, K, epi, bn):
+    """gemm_vs.hip (the wide projections' 4-wave kernel: 128 x 128 / 96 wave tiles, operands
+    staged global -> VGPR -> LDS by buffer loads) == the fp32 oracle on every epilogue, both tile
+    widths, ragged M (rows past M read as zeros through the descriptor), single- and odd-count
+    k-tiles (K = 64, 320)."""
+    from codename_symbiont_amd.ops._ext import hip
+    from codename_symbiont_amd.ops.kernels import gemm
+
+    if bn and N % bn:
+        pytest.skip("tile width does not divide N")
+    hip().gemm_vs_config(2, bn)
+    hip().gemm_skinny_config(0)
+    try:
+        out = gemm(a := _bf(M, K, seed=1), w := _bf(N, K, scale=1.0 / math.sqrt(K), seed=2),
+                   bias := _f(N, scale=0.5, seed=3), epi,
+                   res := (_bf(M, N, seed=4) if epi == 2 else None))
+    finally:
+        hip().gemm_vs_config(0)
+        hip().gemm_skinny_config(256)
+    ref = R.gemm_ref(a, w, bias, epi, res, None, None, 1e-12)
+    _close(out, ref, atol=4e-2, rtol=2e-2, what=f"vgpr-staged gemm bn={bn} epi={epi}")
+
+
 @pytest.mark.parametrize("M,N,K,epi", [(300, 1152, 384, 0), (4100, 768, 3072, 2), (999, 2304, 768, 0),
                                       (77, 1024, 4096, 2)])
 def test_gemm_hipblaslt_route(M, N, K, epi):
@@ -940,7 +969,7 @@ def test_append_rows_writes_rows_and_both_images(D):
 
 
 @pytest.mark.parametrize("form,D,i8v", [(0, 384, 0), (1, 384, 0), (0, 768, 0), (1, 768, 0),
-                                        (0, 384, 5), (0, 768, 5),
+                                        (0, 384, 5), (0, 768, 2),
                                         (0, 1024, 0), (1, 1024, 0), (2, 384, 0), (2, 768, 0),
                                         (0, 384, 4)])
 def test_index_scan_stream_emits_the_bound_set(form, D, i8v, monkeypatch, request):
@@ -949,7 +978,9 @@ def test_index_scan_stream_emits_the_bound_set(form, D, i8v, monkeypatch, reques
     x8) sx, MX-fp4: the decoded dot) reaches the threshold, for 1, 2 and 3 query blocks, a ragged
     row count and skipped row blocks -- pins the fragment layout, the accumulator row map, the
     row-scale header and the block-scale bytes' lane / k-step mapping.  i8v 4: the int8 scan on
-    the 16 x 16 x 64 MFMA shape (stream_config i8 variant 4) over the same image."""
+    the 16 x 16 x 64 MFMA shape (stream_config i8 variant 4) over the same image; i8v 5 at 384
+    and the default at 768: the LDS-query int8 scan (index_lq.hip); i8v 2 at 768: the
+    register-resident stream scan."""
     from codename_symbiont_amd.index.shard import HbmIndexShard
     from codename_symbiont_amd.ops._ext import hip, stream_handle
 
