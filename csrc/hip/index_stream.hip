@@ -751,22 +751,43 @@ __device__ __forceinline__ float mx4_query_elem(const uint8_t* __restrict__ Xq,
 // 32 consecutive queries, the MX-fp4 image c~ of the mean of their decoded images and
 // R = max_q |q~ - c~|, so that every query q of the set and every row x satisfy
 //   q~ . x~ = c~ . x~ + (q~ - c~) . x~ <= c~ . x~ + R |x~| <= c~ . x~ + R X4.
-// One wave per set; C4 / CS: the centroids' image in the query layout, R [n_sets].
+// Four waves per set, wave w decoding queries w, w + 4, .. of it (8 independent loads each,
+// kept in registers for the radius pass; one wave walking all 32 serially took 66 us per search
+// beside the encoder, profiles/r5_step/); C4 / CS: the centroids' image in the query layout,
+// R [n_sets].
 template <int D>
-__global__ __launch_bounds__(64) void mx4_centroids_kernel(const uint8_t* __restrict__ Xq,
-                                                           const uint32_t* __restrict__ QS, int NQ,
-                                                           uint8_t* __restrict__ C4,
-                                                           uint32_t* __restrict__ CS,
-                                                           float* __restrict__ R) {
-  constexpr int M = D / 64, NSC = SDim<SF_MX4, D>::NSC;
-  const int set = blockIdx.x, lane = threadIdx.x;
+__global__ __launch_bounds__(256) void mx4_centroids_kernel(const uint8_t* __restrict__ Xq,
+                                                            const uint32_t* __restrict__ QS, int NQ,
+                                                            uint8_t* __restrict__ C4,
+                                                            uint32_t* __restrict__ CS,
+                                                            float* __restrict__ R) {
+  constexpr int M = D / 64, NSC = SDim<SF_MX4, D>::NSC, QW = 8;
+  __shared__ float part[4][D];
+  __shared__ float rmax[4];
+  const int set = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int q0 = set * 32, nq = min(32, NQ - q0);
+  float xv[QW][M];
   float c[M];
 #pragma unroll
   for (int m = 0; m < M; ++m) c[m] = 0.f;
-  for (int i = 0; i < nq; ++i)
 #pragma unroll
-    for (int m = 0; m < M; ++m) c[m] += mx4_query_elem<D>(Xq, QS, q0 + i, lane + 64 * m);
+  for (int i = 0; i < QW; ++i) {
+    const int q = w + 4 * i;
+    const int qq = q0 + min(q, nq - 1);
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      xv[i][m] = mx4_query_elem<D>(Xq, QS, qq, lane + 64 * m);
+      if (q < nq) c[m] += xv[i][m];
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < M; ++m) part[w][lane + 64 * m] = c[m];
+  __syncthreads();
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const int d = lane + 64 * m;
+    c[m] = (part[0][d] + part[1][d]) + (part[2][d] + part[3][d]);   // (the same sum in every wave)
+  }
   uint32_t scw[NSC];
 #pragma unroll
   for (int i = 0; i < NSC; ++i) scw[i] = 0u;
@@ -781,28 +802,34 @@ __global__ __launch_bounds__(64) void mx4_centroids_kernel(const uint8_t* __rest
     const int code = cd | (x < 0.f && cd ? 8 : 0);
     ct[m] = e2m1_value(code) * ldexpf(1.f, e);   // (the value the image holds)
     const int hi = __shfl_down(code, 1);
-    if ((lane & 1) == 0) C4[(size_t)set * (D / 2) + (lane >> 1) + 32 * m] = (uint8_t)(code | (hi << 4));
+    if (w == 0 && (lane & 1) == 0)
+      C4[(size_t)set * (D / 2) + (lane >> 1) + 32 * m] = (uint8_t)(code | (hi << 4));
     scw[m >> 2] |= (uint32_t)(e + 127) << (8 * (m & 3));
   }
 #pragma unroll
   for (int i = 0; i < NSC; ++i) {
     const uint32_t lo = (uint32_t)__shfl((int)scw[i], 0), hi = (uint32_t)__shfl((int)scw[i], 32);
-    if (lane == 0) {
+    if (w == 0 && lane == 0) {
       CS[(size_t)set * 2 * NSC + i] = lo;
       CS[(size_t)set * 2 * NSC + NSC + i] = hi;
     }
   }
   float r2 = 0.f;
-  for (int i = 0; i < nq; ++i) {
+#pragma unroll
+  for (int i = 0; i < QW; ++i) {
     float d2 = 0.f;
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-      const float d = mx4_query_elem<D>(Xq, QS, q0 + i, lane + 64 * m) - ct[m];
+      const float d = xv[i][m] - ct[m];
       d2 += d * d;
     }
-    r2 = fmaxf(r2, wave_sum(d2));
+    d2 = wave_sum(d2);
+    if (w + 4 * i < nq) r2 = fmaxf(r2, d2);
   }
-  if (lane == 0) R[set] = sqrtf(r2) * 1.0001f + 1e-6f;   // (rounding of the sums above)
+  if (lane == 0) rmax[w] = r2;
+  __syncthreads();
+  if (threadIdx.x == 0)   // (rounding of the sums above)
+    R[set] = sqrtf(fmaxf(fmaxf(rmax[0], rmax[1]), fmaxf(rmax[2], rmax[3]))) * 1.0001f + 1e-6f;
 }
 
 // raise bounds[0..1] to the maxima of (a, b) over the workgroup's 4 waves (idle waves pass 0)
@@ -1099,7 +1126,7 @@ int symb_mx4_centroids(const void* Xq, const void* QS, int NQ, int dim, void* C4
                        float* R, hipStream_t st) {
   if (NQ <= 0) return 0;
   const int n_sets = (NQ + 31) / 32;
-#define L(D_) hipLaunchKernelGGL(mx4_centroids_kernel<D_>, dim3(n_sets), dim3(64), 0, st,             \
+#define L(D_) hipLaunchKernelGGL(mx4_centroids_kernel<D_>, dim3(n_sets), dim3(256), 0, st,             \
                                  (const uint8_t*)Xq, (const uint32_t*)QS, NQ, (uint8_t*)C4,         \
                                  (uint32_t*)CS, R)
   if (dim == 384) L(384);
