@@ -138,8 +138,6 @@ int symb_prune_qprep(const void* Q, int NQ, int dim, const float* pre_s, const f
                      float thr_margin, const float* bounds, void* Q8, float* sq, float* T,
                      float* thr, hipStream_t st);
 int symb_gemm_lt_config(int mode);
-int symb_gemm_pp_mode(int mode, int bm);
-int symb_gemm_pp_ring(int ring);
 int symb_gemm_vs_mode(int mode, int bn);
 int symb_mfma_f8f6f4_probe(const int* a, const int* b, const int* sa, const int* sb, float* out,
                            int fmt, hipStream_t st);
@@ -645,9 +643,6 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("Q"), py::arg("NQ"), py::arg("dim"), py::arg("pre_s"), py::arg("tail_s"),
      py::arg("k"), py::arg("thr_margin"), py::arg("bounds"), py::arg("Q8"), py::arg("sq"),
      py::arg("T"), py::arg("thr"), py::arg("stream"));
-  m.def("gemm_pp_config", [](int mode, int bm) { check(symb_gemm_pp_mode(mode, bm), "gemm_pp_config"); },
-        py::arg("mode"), py::arg("bm") = 0);
-  m.def("gemm_pp_ring", [](int ring) { check(symb_gemm_pp_ring(ring), "gemm_pp_ring"); });
   m.def("gemm_vs_config", [](int mode, int bn) { check(symb_gemm_vs_mode(mode, bn), "gemm_vs_config"); },
         py::arg("mode"), py::arg("bn") = 0);
   m.def("mfma_f8f6f4_probe", [](uptr a, uptr b, uptr sa, uptr sb, uptr out, int fmt, uptr st) {

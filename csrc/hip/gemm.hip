@@ -502,25 +502,9 @@ int symb_gemm_lt_config(int mode) {
   return 0;
 }
 
-// The ping-pong kernel (gemm_pp.hip) for the wide projections: 0 = off (default: it measured
-// 0.78-0.92x the round-4 tiles, profiles/r5_gemm/), 1 = auto (K >= 768, N >= 768, M >= 2048),
-// 2 = wherever it supports the shape.  It runs before the hipBLASLt route.
-int symb_gemm_pp(int epi, const void* A, int lda, const void* W, int ldw, const float* bias,
-                 const void* R, int ldr, void* C, int ldc, int M, int N, int K, int group_m,
-                 int gelu_poly, hipStream_t st);
-bool symb_gemm_pp_supported(int epi, int M, int N, int K);
-int symb_gemm_pp_config(int bm);
-static int g_pp = 0;
-int symb_gemm_pp_mode(int mode, int bm) {
-  if (mode < 0 || mode > 2) return -1;
-  if (symb_gemm_pp_config(bm) != 0) return -1;
-  g_pp = mode;
-  return 0;
-}
-
 // The VGPR-staged 4-wave kernel (gemm_vs.hip, hipBLASLt's geometry) for the wide projections:
 // 0 = off, 1 = auto (K >= 768, N >= 768, M >= 2048), 2 = wherever it supports the shape.  It
-// runs before the ping-pong kernel and the hipBLASLt route.
+// runs before the hipBLASLt route (off by default: 0.77-0.80x this file's tiles, profiles/r5_gemm/).
 int symb_gemm_vs(int epi, const void* A, int lda, const void* W, int ldw, const float* bias,
                  const void* R, int ldr, void* C, int ldc, int M, int N, int K, int group_m,
                  int gelu_poly, hipStream_t st);
@@ -573,12 +557,6 @@ int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const flo
   if (g_vs && symb_gemm_vs_supported(epi, M, N, K) &&
       (g_vs == 2 || (K >= 768 && N >= 768 && M >= 2048))) {
     const int rc = symb_gemm_vs(epi, A, lda, W, ldw, bias, R, ldr, C, ldc, M, N, K, g_group_m,
-                                g_gelu_poly, st);
-    if (rc != -1) return rc;
-  }
-  if (g_pp && symb_gemm_pp_supported(epi, M, N, K) &&
-      (g_pp == 2 || (K >= 768 && N >= 768 && M >= 2048))) {
-    const int rc = symb_gemm_pp(epi, A, lda, W, ldw, bias, R, ldr, C, ldc, M, N, K, g_group_m,
                                 g_gelu_poly, st);
     if (rc != -1) return rc;
   }

@@ -96,7 +96,6 @@ def test_gemm(M, N, K, epi, tile):
     # the M <= 256 shapes exercise the tiled kernels' ragged small-M handling (test_gemm_skinny
     # covers the skinny path)
     hip().gemm_skinny_config(0)
-    hip().gemm_pp_config(0)   # (the ping-pong kernel: test_gemm_pingpong)
     try:
         out = gemm(a := _bf(M, K, seed=1), w := _bf(N, K, scale=1.0 / math.sqrt(K), seed=2),
                    bias := _f(N, scale=0.5, seed=3), epi,
@@ -108,37 +107,8 @@ def test_gemm(M, N, K, epi, tile):
         hip().gemm_resln_config(16)
         hip().gemm_lt_config(1)
         hip().gemm_skinny_config(256)
-        hip().gemm_pp_config(0)
     ref = R.gemm_ref(a, w, bias, epi, res, g, b, 1e-12)
     _close(out, ref, atol=4e-2, rtol=2e-2, what=f"gemm epi={epi}")
-
-
-@pytest.mark.parametrize("bm,ring", [(256, 1), (256, 0), (128, 0)])
-@pytest.mark.parametrize("M,N,K,epi", [
-    (300, 256, 128, 0), (1000, 768, 768, 2), (2049, 2304, 768, 0), (4353, 768, 3072, 2),
-    (777, 3072, 768, 1), (5000, 1024, 4096, 2), (257, 512, 320, 1), (32768, 768, 768, 0),
-    (130, 4096, 1024, 1), (600, 1024, 192, 0),
-])
-def test_gemm_pingpong(M, N, K, epi, bm, ring):
-    """gemm_pp.hip (the wide projections' kernel: two wave rows half a phase apart, LDS-DMA
-    half-tiles; ring = the 10-slot half-tile ring) == the fp32 oracle on every epilogue, both tile
-    heights, ragged M, odd numbers of 64-deep k-tiles (K = 192, 320) and two-tile K (128)."""
-    from codename_symbiont_amd.ops._ext import hip
-    from codename_symbiont_amd.ops.kernels import gemm
-
-    hip().gemm_pp_config(2, bm)
-    hip().gemm_pp_ring(ring)
-    hip().gemm_skinny_config(0)
-    try:
-        out = gemm(a := _bf(M, K, seed=1), w := _bf(N, K, scale=1.0 / math.sqrt(K), seed=2),
-                   bias := _f(N, scale=0.5, seed=3), epi,
-                   res := (_bf(M, N, seed=4) if epi == 2 else None))
-    finally:
-        hip().gemm_pp_config(0)
-        hip().gemm_pp_ring(1)
-        hip().gemm_skinny_config(256)
-    ref = R.gemm_ref(a, w, bias, epi, res, None, None, 1e-12)
-    _close(out, ref, atol=4e-2, rtol=2e-2, what=f"pingpong gemm bm={bm} epi={epi}")
 
 
 @pytest.mark.parametrize("bn", [0, 256, 192])
