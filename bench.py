@@ -257,6 +257,7 @@ def main(argv=None) -> int:
         # plain `python bench.py --gpus N`: launch the N ranks (nothing has touched the GPU yet)
         return self_launch(args.gpus, sys.argv[1:] if argv is None else list(argv))
 
+    _claim_stdout()
     from codename_symbiont_amd.parallel import dist as D
 
     info = D.init(device_type=None if args.device == "auto" else args.device,
@@ -274,6 +275,26 @@ def main(argv=None) -> int:
         rc = run_gpu(args, info, comm)
     D.shutdown(info)
     return rc
+
+
+# stdout carries exactly one line, rank 0's JSON result: everything else a rank process writes
+# to fd 1 -- e.g. the version banner RCCL prints when it creates a communicator ("RCCL version :
+# ...", one per rank and group) -- goes to stderr, so the driver's parse of stdout sees only the
+# result.  (Set in each rank process before torch.distributed initialises.)
+_RESULT_OUT = None
+
+
+def _claim_stdout() -> None:
+    global _RESULT_OUT
+    if _RESULT_OUT is not None:
+        return
+    sys.stdout.flush()
+    _RESULT_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
+
+def _emit_result(line: str) -> None:
+    print(line, file=_RESULT_OUT or sys.stdout, flush=True)
 
 
 def metric_and_config(args, info, cfg, prune, prefilter, extra_cfg: dict):
@@ -469,9 +490,9 @@ def run_cpu(args, info, comm) -> int:
                  "heldout_ms_per_search": round(el_h * 1000.0 / H, 3), "heldout_searches": H}
     metric, config, unit = metric_and_config(args, info, cfg, None, None, {"device": "cpu"})
     if info.rank == 0:
-        print(result_line(args, info, comm, metric, unit, config, total, ms, None, None,
-                          _data_txt(args) + " (CPU rehearsal: not a performance number)", extra),
-              flush=True)
+        _emit_result(result_line(args, info, comm, metric, unit, config, total, ms, None, None,
+                                 _data_txt(args) + " (CPU rehearsal: not a performance number)",
+                                 extra))
     return 0
 
 
@@ -872,8 +893,8 @@ def run_gpu(args, info, comm) -> int:
     metric, config, unit = metric_and_config(args, info, cfg, prune, prefilter,
                                              dict(cfg_extra, _group_dp=group_dp))
     if info.rank == 0:
-        print(result_line(args, info, comm, metric, unit, config, total, ms, prune, prefilter,
-                          _data_txt(args), extra_out), flush=True)
+        _emit_result(result_line(args, info, comm, metric, unit, config, total, ms, prune,
+                                 prefilter, _data_txt(args), extra_out))
     return 0
 
 

@@ -27,7 +27,8 @@ def _run(args, env_extra=None, drop=("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER
 def test_bench_self_launches_n_ranks():
     p, out = _run(["--gpus", "2"] + TINY)
     assert p.returncode == 0, p.stderr[-2000:]
-    assert len(out) == 1, p.stdout          # exactly one JSON line, from rank 0
+    assert len(out) == 1, p.stdout          # exactly one JSON line, from rank 0 ...
+    assert p.stdout.strip().splitlines() == [json.dumps(out[0])], p.stdout   # ... and nothing else
     r = out[0]
     assert r["n_gpus"] == 2 and r["world"] == 2 and r["backend"] == "gloo"
     assert r["comm_check"]["collective"].startswith("all_gather ok")
