@@ -1,7 +1,7 @@
 // int8 pruning scan with the QUERIES in LDS and the rows streamed through a deep VGPR ring
 // (the first pass of the exact pruned search; reference hot path
-// services/vector_memory_service/src/main.rs:261-286).  Stream-config int8 variant 5 of
-// index_stream.hip's scan over the same fragment-major int8 image.
+// services/vector_memory_service/src/main.rs:261-286), over index_stream.hip's fragment-major
+// int8 image: the default int8 form at D = 768, stream-config int8 variant 5 at D = 384.
 //
 // Why (profiles/r5_scan/): scan_stream_kernel keeps 128 queries per wave as resident B operands
 // (192 VGPRs) and pairs two waves on the same rows.  What is left for the row ring is two
@@ -16,6 +16,11 @@
 // Per sub-tile a wave issues 96 v_mfma_i32_32x32x32_i8 (8 sets x 12 k-steps, B operand from one
 // ds_read_b128 each: 128 B/clk/CU of LDS at the MFMA rate, half the array's 256) and the same
 // integer-max hit test as scan_stream_kernel; only a block with a hit recomputes and emits.
+//
+// Measured (profiles/r5_lq/): at D = 384 the stall is gone (waves parked 41 -> 16 %) and the time
+// is not -- the chip holds 1.22 GHz with the MFMA pipes 76 % busy, the power limit -- so the
+// register-resident stream scan stays the default there.  At D = 768 (two query blocks per row
+// block, run on one XCD) it is 23.6 ms against the stream scan's 41.1 ms for 100M held-out rows.
 #include "scan_common.h"
 
 namespace symb {
@@ -38,8 +43,9 @@ struct LqGeo {
   static_assert(LDS <= 160 * 1024, "LDS");
 };
 
-// NP: sub-tiles (ring slots) each LDS query fragment feeds -- 2 halves the LDS read bytes per
-// MFMA; timing ablation ABL 2 (wrong results): no sub-tile loads after the prologue.
+// NP: sub-tiles (ring slots) each LDS query fragment feeds -- 2 would halve the LDS read bytes per
+// MFMA, but NP = 2 with 4 slots spills at 512 VGPRs, so only NP = 1 is instantiated; timing
+// ablation ABL 2 (wrong results): no sub-tile loads after the prologue.
 template <int D, int DEPTH, int NP = 1, int ABL = 0>
 __global__ __launch_bounds__(256, 1) void scan_lq_i8_kernel(
     const uint8_t* __restrict__ img, int n_valid, int rows_per_blk, const uint8_t* __restrict__ Q,
