@@ -1238,10 +1238,18 @@ class HbmIndexShard:
         thr0 = torch.empty(NQ, dtype=torch.float32, device=dev)
         seed_s = torch.empty(NQ, k, device=dev)
         seed_i = torch.empty(NQ, k, dtype=torch.int32, device=dev)
+        # (a dense tail is selected in the same launch: its columns follow the seed tiles' in S)
+        tail_s = torch.empty(NQ, k, device=dev)
+        tail_i = torch.empty(NQ, k, dtype=torch.int32, device=dev) if dense_tail else None
+        fuse_tail = dense_tail and tcap > 0
+        tcs_p = S.data_ptr() + 4 * m_seed
         h.topk_select_counted(S.data_ptr(), 0, 0, m_seed, NQ, kmax, k, seed_s.data_ptr(),
                               seed_i.data_ptr(), flags[self.WS_SCRATCH].data_ptr(), st,
                               reset_ovf=False, ld=ld, kth_out=thr0.data_ptr(),
-                              kth_margin=self.MQ_THR_MARGIN)
+                              kth_margin=self.MQ_THR_MARGIN,
+                              seg2_s=tcs_p if fuse_tail else 0, seg2_cap=tcap if fuse_tail else 0,
+                              seg2_out_s=tail_s.data_ptr() if fuse_tail else 0,
+                              seg2_out_i=tail_i.data_ptr() if fuse_tail else 0)
         pm = self.prepass_min_tiles
         pre_s, _, cs_p, ci_p, cnt_p = self._scan_mq(
             nv * TILE_ROWS, q_unit, kmax, k, thr0, n_cus, tshift=ts, fallback=False, cand=True,
@@ -1254,13 +1262,11 @@ class HbmIndexShard:
         # atomic on the query's counter: with a fresh near-duplicate crowd in the tail every
         # (query, row) pair emitted and the counters serialized (0.6 ms per headline step,
         # profiles/r3_step_trace/)
-        tail_s = torch.empty(NQ, k, device=dev)
         if dense_tail:
-            tail_i = torch.empty(NQ, k, dtype=torch.int32, device=dev)
-            tcs_p = S.data_ptr() + 4 * m_seed
-            h.topk_select_counted(tcs_p, 0, 0, tcap, NQ, kmax, k, tail_s.data_ptr(),
-                                  tail_i.data_ptr(), flags[self.WS_SCRATCH].data_ptr(), st,
-                                  reset_ovf=False, ld=ld)
+            if not fuse_tail:
+                h.topk_select_counted(tcs_p, 0, 0, tcap, NQ, kmax, k, tail_s.data_ptr(),
+                                      tail_i.data_ptr(), flags[self.WS_SCRATCH].data_ptr(), st,
+                                      reset_ovf=False, ld=ld)
             tci = tcnt = None
             tail_ld = ld
         else:

@@ -160,7 +160,9 @@ int symb_index_scan_mq_ablate(const void* X, int n_valid, int rows_per_blk, int 
 int symb_topk_select_counted(const float* cand_s, const int* cand_i, const int* cand_n, int cap,
                              int NQ, int kmax, int k, float* out_s, int* out_i, int* ovf,
                              hipStream_t st, const int* gate, int reset_ovf, int ld = 0,
-                             float* kth_out = nullptr, float kth_margin = 0.f);
+                             float* kth_out = nullptr, float kth_margin = 0.f,
+                             const float* seg2_s = nullptr, int seg2_cap = 0,
+                             float* seg2_out_s = nullptr, int* seg2_out_i = nullptr);
 
 namespace {
 
@@ -685,16 +687,20 @@ PYBIND11_MODULE(_hip, m) {
   m.def("topk_select_counted", [](uptr cand_s, uptr cand_i, uptr cand_n, int cap, int NQ,
                                   int kmax, int k, uptr out_s, uptr out_i, uptr ovf, uptr st,
                                   uptr gate, bool reset_ovf, int ld, uptr kth_out,
-                                  float kth_margin) {
+                                  float kth_margin, uptr seg2_s, int seg2_cap, uptr seg2_out_s,
+                                  uptr seg2_out_i) {
     check(symb_topk_select_counted(P<const float>(cand_s), P<const int>(cand_i),
                                    P<const int>(cand_n), cap, NQ, kmax, k, P<float>(out_s),
                                    P<int>(out_i), P<int>(ovf), S(st), P<const int>(gate),
-                                   reset_ovf ? 1 : 0, ld, P<float>(kth_out), kth_margin),
+                                   reset_ovf ? 1 : 0, ld, P<float>(kth_out), kth_margin,
+                                   P<const float>(seg2_s), seg2_cap, P<float>(seg2_out_s),
+                                   P<int>(seg2_out_i)),
           "topk_select_counted");
   }, py::arg("cand_s"), py::arg("cand_i"), py::arg("cand_n"), py::arg("cap"), py::arg("NQ"),
      py::arg("kmax"), py::arg("k"), py::arg("out_s"), py::arg("out_i"), py::arg("ovf"),
      py::arg("stream"), py::arg("gate") = 0, py::arg("reset_ovf") = true, py::arg("ld") = 0,
-     py::arg("kth_out") = 0, py::arg("kth_margin") = 0.f);
+     py::arg("kth_out") = 0, py::arg("kth_margin") = 0.f, py::arg("seg2_s") = 0,
+     py::arg("seg2_cap") = 0, py::arg("seg2_out_s") = 0, py::arg("seg2_out_i") = 0);
   m.def("index_scan_ablate", [](uptr X, int n_valid, int rows_per_blk, int n_rblk, uptr Q, int NQ,
                                 uptr cs, uptr ci, uptr st, int abl, uptr thr) {
     check(symb_index_scan_ablate(P<void>(X), n_valid, rows_per_blk, n_rblk, P<void>(Q), NQ,

@@ -1169,6 +1169,9 @@ struct RouteTail {
   int ld;    // row stride of cs (dense form; = cap unless the tail shares a wider score matrix)
 };
 
+// One 256-thread workgroup per query (was one wave per query, 4 per workgroup: 64 workgroups
+// for a 256-query batch on a 256-CU chip, the longest kernel of the pre-pass chain beside the
+// encoder); the four waves split its candidate list and tail and share its LDS histograms.
 __global__ __launch_bounds__(256) void prune_route_kernel(
     int NQ, const float* __restrict__ pre_s, const float* __restrict__ tail_s, int k,
     float thr_margin, const float* __restrict__ sq, const float* __restrict__ margin,
@@ -1176,12 +1179,12 @@ __global__ __launch_bounds__(256) void prune_route_kernel(
     const int* __restrict__ cnt_p, int cap_p, int tshift, int rows_per_blk, int n_rblk,
     float* __restrict__ T_out, float* __restrict__ thr, int* __restrict__ dense,
     float* __restrict__ est, int* __restrict__ blkmax, RouteTail tail) {
-  __shared__ int hist[4][ROUTE_MAX_BLOCKS];
-  __shared__ int thist[4][ROUTE_MAX_BLOCKS];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int q = blockIdx.x * 4 + w;
-  if (q >= NQ) return;   // (no barrier in this kernel: each wave bins its own query)
-  // k-th best of 2k values (prune_qprep_kernel)
+  __shared__ int h[ROUTE_MAX_BLOCKS];
+  __shared__ int th[ROUTE_MAX_BLOCKS];
+  __shared__ float wc[4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int q = blockIdx.x;
+  // k-th best of 2k values (prune_qprep_kernel), every wave alike
   float v = -INFINITY;
   if (lane < k) v = pre_s[(size_t)q * k + lane];
   else if (lane < 2 * k) v = tail_s[(size_t)q * k + lane - k];
@@ -1199,15 +1202,13 @@ __global__ __launch_bounds__(256) void prune_route_kernel(
   const float t0 = thr0[q];
   const float* cs = cs_p + (size_t)q * cap_p;
   const int* ci = ci_p + (size_t)q * cap_p;
-  int* h = hist[w];
-  int* th = thist[w];
-  for (int b = lane; b < n_rblk; b += 64) {
+  for (int b = tid; b < n_rblk; b += 256) {
     h[b] = 0;
     th[b] = 0;
   }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __syncthreads();
   float c = 0.f;
-  for (int i = lane; i < n; i += 64) {
+  for (int i = tid; i < n; i += 256) {
     if (cs[i] >= band) {
       c += 1.f;
       atomicAdd(&h[min(ci[i] / rows_per_blk, n_rblk - 1)], 1);
@@ -1216,7 +1217,7 @@ __global__ __launch_bounds__(256) void prune_route_kernel(
   const bool tail_dense = tail.cs != nullptr && tail.ci == nullptr;
   if (tail_dense) {   // the exact tail as dense scores [NQ][cap] (row i = tail.off + i)
     const float* tcs = tail.cs + (size_t)q * tail.ld;
-    for (int i0 = 0; i0 < tail.cap; i0 += 64) {
+    for (int i0 = w * 64; i0 < tail.cap; i0 += 256) {
       const int i = i0 + lane;
       const bool hit = i < tail.cap && tcs[i] >= band;
       const int b = min((min(i, tail.cap - 1) + tail.off) / rows_per_blk, n_rblk - 1);
@@ -1232,10 +1233,13 @@ __global__ __launch_bounds__(256) void prune_route_kernel(
     const int tn = min(tail.cnt[q], tail.cap);
     const float* tcs = tail.cs + (size_t)q * tail.cap;
     const int* tci = tail.ci + (size_t)q * tail.cap;
-    for (int i = lane; i < tn; i += 64)
+    for (int i = tid; i < tn; i += 256)
       if (tcs[i] >= band) atomicAdd(&th[min((tci[i] + tail.off) / rows_per_blk, n_rblk - 1)], 1);
   }
   c = wave_sum(c);
+  if (lane == 0) wc[w] = c;
+  __syncthreads();   // (the histograms and the waves' counts)
+  c = wc[0] + wc[1] + wc[2] + wc[3];
   const float binned = c;
   float tscale = 1.f;
   if (band < t0) {   // the band reaches below what the sample emitted: extrapolate (see above)
@@ -1243,14 +1247,13 @@ __global__ __launch_bounds__(256) void prune_route_kernel(
     // (an emitting tail scan kept only rows >= thr0 too; a dense tail counted every row)
     tscale = tail_dense ? 1.f : binned > 0.f ? fmaxf(1.f, c / binned) : 1.f;
   }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   const float scale = (binned > 0.f ? c / binned : 0.f) * (float)(1 << tshift);
-  for (int b = lane; b < n_rblk; b += 64) {
+  for (int b = tid; b < n_rblk; b += 256) {
     const float e = (float)h[b] * scale + (float)th[b] * tscale;
     est[(size_t)q * n_rblk + b] = e;
     if (e > 0.f) atomicMax(blkmax + b, __float_as_int(e));   // (non-negative floats order as ints)
   }
-  if (lane == 0) {
+  if (tid == 0) {
     T_out[q] = T;
     thr[q] = (T - m) / sq[q];
     if (cnt > cap_p) atomicOr(dense, 1);
@@ -1609,7 +1612,7 @@ int symb_prune_route(int NQ, const float* pre_s, const float* tail_s, int k, flo
     if (e == hipSuccess) e = hipMemsetAsync(blkmax, 0, sizeof(int) * (size_t)n_rblk, st);
     if (e != hipSuccess) return (int)e;
   }
-  hipLaunchKernelGGL(prune_route_kernel, dim3((NQ + 3) / 4), dim3(256), 0, st, NQ, pre_s, tail_s,
+  hipLaunchKernelGGL(prune_route_kernel, dim3(NQ), dim3(256), 0, st, NQ, pre_s, tail_s,
                      k, thr_margin, sq, margin, thr0, cs_p, ci_p, cnt_p, cap_p, tshift,
                      rows_per_blk, n_rblk, T, thr, dense, est, blkmax,
                      RouteTail{tail_cs, tail_ci, tail_cnt, tail_cap, tail_off, tail_ld});

@@ -426,19 +426,86 @@ __global__ __launch_bounds__(512, 1) void index_scan_mq_kernel(
   }
 }
 
-// Top-k of each query's emitted candidates.  One workgroup per query: strided local top-KMAX,
-// then an LDS tree of pairwise merges.  A query whose buffer overflowed raises *ovf (the gated
-// 256-query kernel then recomputes the batch).
+// Wave-wide max of a float, valid in lane 63: DPP row shifts fold each 16-lane row, then two row
+// broadcasts fold the rows (max is idempotent, so lanes whose DPP source is out of range simply
+// keep their own value).
+__device__ __forceinline__ float wave_max63(float v) {
+  int x = __float_as_int(v);
+  x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x111, 0xf, 0xf, false))));
+  x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x112, 0xf, 0xf, false))));
+  x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x114, 0xf, 0xf, false))));
+  x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x118, 0xf, 0xf, false))));
+  x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x142, 0xa, 0xf, false))));
+  x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x143, 0xc, 0xf, false))));
+  return __int_as_float(__builtin_amdgcn_readlane(x, 63));
+}
+
+// KMAX rounds of a wave-wide "pop the best head": every lane holds a descending list of L
+// candidates; each round the wave max of the heads (DPP, no LDS), the lowest lane holding it gives
+// up its head (its list shifts by one) and lane r keeps round r's winner.  Replaces the LDS tree
+// of pairwise merges (8 rounds x 2 barriers x a 16-step serial merge per level).
+template <int KMAX, int L>
+__device__ __forceinline__ void wave_pop_topk(float (&tv)[L], int (&ti)[L], int lane, float& rv,
+                                              int& ri) {
+  rv = -INFINITY;
+  ri = -1;
+#pragma unroll
+  for (int r = 0; r < KMAX; ++r) {
+    const float mx = wave_max63(tv[0]);
+    const uint64_t hit = __ballot(tv[0] == mx);
+    const int win = hit ? (int)__builtin_ctzll(hit) : 0;
+    const int id = __builtin_amdgcn_readlane(ti[0], win);
+    if (lane == r) {
+      rv = mx;
+      ri = id;
+    }
+    if (lane == win) {
+#pragma unroll
+      for (int i = 0; i + 1 < L; ++i) {
+        tv[i] = tv[i + 1];
+        ti[i] = ti[i + 1];
+      }
+      tv[L - 1] = -INFINITY;
+      ti[L - 1] = -1;
+    }
+  }
+}
+
+// A second, dense segment of the same select launch (blockIdx.y == 1): the pruned search's
+// exact fresh-row tail, selected in the seed select's launch instead of a serial one of its own.
+struct SelSeg2 {
+  const float* s;   // [NQ, ld] scores (the same stride as the first segment)
+  int cap;          // columns
+  float* out_s;     // [NQ, k]
+  int* out_i;
+};
+
+// Top-k of each query's emitted candidates (or of a dense score row).  One workgroup per query:
+// every thread keeps a register top-KMAX over a strided walk (4 independent loads in flight per
+// thread), each wave reduces its 64 lists with wave_pop_topk, and wave 0 reduces the waves'
+// lists the same way.  A query whose buffer overflowed raises *ovf (the gated 256-query kernel
+// then recomputes the batch).
 template <int KMAX, int NTH>
 __global__ __launch_bounds__(NTH) void topk_select_counted_kernel(
     const float* __restrict__ cand_s, const int* __restrict__ cand_i,
     const int* __restrict__ cand_n, int cap, int k, float* __restrict__ out_s,
     int* __restrict__ out_i, int* __restrict__ ovf, const int* __restrict__ gate, int ld,
-    float* __restrict__ kth_out, float kth_margin) {
+    float* __restrict__ kth_out, float kth_margin, SelSeg2 seg2) {
+  constexpr int NW = NTH / 64, P = NW * KMAX / 64;   // waves; wave 0's list length per lane
+  static_assert(NW * KMAX % 64 == 0 && P >= 1, "wave lists must tile wave 0's lanes");
   if (gate != nullptr && *gate == 0) return;   // (grid-uniform, before any barrier)
-  __shared__ float ls[NTH * KMAX];
-  __shared__ int li[NTH * KMAX];
-  const int q = blockIdx.x, tid = threadIdx.x;
+  __shared__ float ls[NW * KMAX];
+  __shared__ int li[NW * KMAX];
+  const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (blockIdx.y == 1) {   // (block-uniform) the dense second segment
+    cand_s = seg2.s;
+    cand_i = cand_n = nullptr;
+    cap = seg2.cap;
+    out_s = seg2.out_s;
+    out_i = seg2.out_i;
+    kth_out = nullptr;
+  }
   // cand_n == nullptr: every row holds cap candidates; cand_i == nullptr: a candidate's id is
   // its position (dense score rows, e.g. the pruned search's exact tail)
   const int cnt = cand_n != nullptr ? cand_n[q] : cap;
@@ -453,50 +520,48 @@ __global__ __launch_bounds__(NTH) void topk_select_counted_kernel(
     tv[i] = -INFINITY;
     ti[i] = -1;
   }
-  for (int c = tid; c < n; c += NTH) {
+  int c = tid;
+  for (; c + 3 * NTH < n; c += 4 * NTH) {
+    float s[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) s[u] = cs[c + u * NTH];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (s[u] > tv[KMAX - 1])
+        topk_insert<KMAX>(tv, ti, s[u], ci != nullptr ? ci[c + u * NTH] : c + u * NTH);
+  }
+  for (; c < n; c += NTH) {
     const float s = cs[c];
     if (s > tv[KMAX - 1]) topk_insert<KMAX>(tv, ti, s, ci != nullptr ? ci[c] : c);
   }
-#pragma unroll
-  for (int i = 0; i < KMAX; ++i) {
-    ls[tid * KMAX + i] = tv[i];
-    li[tid * KMAX + i] = ti[i];
+  float rv;
+  int ri;
+  wave_pop_topk<KMAX, KMAX>(tv, ti, lane, rv, ri);
+  if (lane < KMAX) {
+    ls[wave * KMAX + lane] = rv;
+    li[wave * KMAX + lane] = ri;
   }
   __syncthreads();
-  for (int half = NTH / 2; half >= 1; half >>= 1) {
-    if (tid < half) {
-      const float* as = ls + tid * KMAX;
-      const int* ai = li + tid * KMAX;
-      const float* bs = ls + (tid + half) * KMAX;
-      const int* bi = li + (tid + half) * KMAX;
-      int pa = 0, pb = 0;
+  if (wave != 0) return;
+  float pv[P];
+  int pi[P];
 #pragma unroll
-      for (int i = 0; i < KMAX; ++i) {
-        const bool take_a = as[pa] >= bs[pb];
-        tv[i] = take_a ? as[pa] : bs[pb];
-        ti[i] = take_a ? ai[pa] : bi[pb];
-        pa += take_a ? 1 : 0;
-        pb += take_a ? 0 : 1;
-        pa = min(pa, KMAX - 1);
-        pb = min(pb, KMAX - 1);
-      }
-    }
-    __syncthreads();
-    if (tid < half) {
-#pragma unroll
-      for (int i = 0; i < KMAX; ++i) {
-        ls[tid * KMAX + i] = tv[i];
-        li[tid * KMAX + i] = ti[i];
-      }
-    }
-    __syncthreads();
+  for (int j = 0; j < P; ++j) {
+    pv[j] = -INFINITY;
+    pi[j] = -1;
   }
-  if (tid < k) {
-    out_s[(size_t)q * k + tid] = tid < KMAX ? ls[tid] : -INFINITY;
-    out_i[(size_t)q * k + tid] = tid < KMAX ? li[tid] : -1;
+#pragma unroll
+  for (int j = 0; j < P; ++j) {
+    const float v = ls[lane + 64 * j];
+    if (v > pv[P - 1]) topk_insert<P>(pv, pi, v, li[lane + 64 * j]);
+  }
+  wave_pop_topk<KMAX, P>(pv, pi, lane, rv, ri);
+  if (lane < k) {
+    out_s[(size_t)q * k + lane] = rv;
+    out_i[(size_t)q * k + lane] = ri;
   }
   // (optional) the k-th best minus a margin: a seed threshold for the next scan, no torch op
-  if (kth_out != nullptr && tid == 0) kth_out[q] = (k <= KMAX ? ls[k - 1] : -INFINITY) - kth_margin;
+  if (kth_out != nullptr && lane == k - 1) kth_out[q] = rv - kth_margin;
 }
 
 // Top-k of each query's emitted candidates for ANY k <= SEL_MAX (the reference passes top_k
@@ -761,11 +826,17 @@ int symb_index_scan_mq_ablate(const void* X, int n_valid, int rows_per_blk, int 
 int symb_topk_select_counted(const float* cand_s, const int* cand_i, const int* cand_n, int cap,
                              int NQ, int kmax, int k, float* out_s, int* out_i, int* ovf,
                              hipStream_t st, const int* gate, int reset_ovf, int ld,
-                             float* kth_out, float kth_margin) {
+                             float* kth_out, float kth_margin, const float* seg2_s, int seg2_cap,
+                             float* seg2_out_s, int* seg2_out_i) {
   if (NQ <= 0) return 0;
   if (k > kmax) return -1;
   if (ld <= 0) ld = cap;
   if (ld < cap) return -1;
+  const SelSeg2 seg2{seg2_s, seg2_cap, seg2_out_s, seg2_out_i};
+  const dim3 grid(NQ, seg2_s != nullptr ? 2 : 1);
+  if (seg2_s != nullptr && (kmax == sel::SEL_MAX || seg2_cap <= 0 || seg2_cap > ld ||
+                            seg2_out_s == nullptr || seg2_out_i == nullptr))
+    return -1;
   if (kmax == sel::SEL_MAX && (cand_i == nullptr || cand_n == nullptr)) return -1;   // (dense rows: KMAX 16 / 32 forms)
   if (kmax == sel::SEL_MAX && (ld != cap || kth_out != nullptr)) return -1;
   if (reset_ovf) {
@@ -775,12 +846,15 @@ int symb_topk_select_counted(const float* cand_s, const int* cand_i, const int* 
   if (kmax == sel::SEL_MAX)   // any k <= 128: radix select + bitonic sort
     hipLaunchKernelGGL(topk_select_radix_kernel, dim3(NQ), dim3(sel::NTH), 0, st, cand_s, cand_i,
                        cand_n, cap, k, out_s, out_i, ovf, gate);
+  else if (kmax == 16 && cand_n == nullptr && cap >= 8192)   // long dense rows: 16 waves
+    hipLaunchKernelGGL((topk_select_counted_kernel<16, 1024>), grid, dim3(1024), 0, st, cand_s,
+                       cand_i, cand_n, cap, k, out_s, out_i, ovf, gate, ld, kth_out, kth_margin, seg2);
   else if (kmax == 16)
-    hipLaunchKernelGGL((topk_select_counted_kernel<16, 256>), dim3(NQ), dim3(256), 0, st, cand_s,
-                       cand_i, cand_n, cap, k, out_s, out_i, ovf, gate, ld, kth_out, kth_margin);
+    hipLaunchKernelGGL((topk_select_counted_kernel<16, 256>), grid, dim3(256), 0, st, cand_s,
+                       cand_i, cand_n, cap, k, out_s, out_i, ovf, gate, ld, kth_out, kth_margin, seg2);
   else if (kmax == 32)
-    hipLaunchKernelGGL((topk_select_counted_kernel<32, 128>), dim3(NQ), dim3(128), 0, st, cand_s,
-                       cand_i, cand_n, cap, k, out_s, out_i, ovf, gate, ld, kth_out, kth_margin);
+    hipLaunchKernelGGL((topk_select_counted_kernel<32, 128>), grid, dim3(128), 0, st, cand_s,
+                       cand_i, cand_n, cap, k, out_s, out_i, ovf, gate, ld, kth_out, kth_margin, seg2);
   else
     return -1;
   return (int)hipGetLastError();

@@ -1782,6 +1782,90 @@ def test_topk_select_radix_matches_torch(k):
     assert (out_s == 7.0).all()
 
 
+@pytest.mark.parametrize("kmax,k,dense,cap", [(16, 1, False, 3000), (16, 10, False, 3000),
+                                               (16, 16, False, 20000), (32, 32, False, 3000),
+                                               (32, 17, True, 5000), (16, 10, True, 4097),
+                                               (16, 10, True, 70001), (16, 16, True, 65536),
+                                               (16, 16, True, 8192)])
+def test_topk_select_counted_matches_torch(kmax, k, dense, cap):
+    """topk_select_counted_kernel (the KMAX 16 / 32 forms: register lists, DPP wave pops, the
+    16-wave form for long dense rows) vs torch.topk -- coarse values (many ties: every id must
+    still be distinct and point at its score), counted lists that are empty / shorter than k /
+    overflowed, dense score rows with a padded stride, the k-th-best output, a gated-off launch."""
+    from codename_symbiont_amd.ops._ext import hip, stream_handle
+
+    nq, ld = 37, cap + (3 if dense else 0)
+    cs = _f(nq, ld, seed=103).round(decimals=2)
+    ci = None if dense else (torch.arange(nq * ld, dtype=torch.int32, device=DEV).view(nq, ld) * 3)
+    cnt = None
+    if not dense:
+        cnt = torch.randint(0, cap, (nq,), dtype=torch.int32, device=DEV)
+        cnt[0], cnt[1], cnt[2] = 0, min(k, 5), cap + 7
+    out_s = torch.empty(nq, k, device=DEV)
+    out_i = torch.empty(nq, k, dtype=torch.int32, device=DEV)
+    kth = torch.empty(nq, device=DEV)
+    ovf = torch.zeros(1, dtype=torch.int32, device=DEV)
+    hip().topk_select_counted(cs.data_ptr(), 0 if dense else ci.data_ptr(),
+                              0 if dense else cnt.data_ptr(), cap, nq, kmax, k, out_s.data_ptr(),
+                              out_i.data_ptr(), ovf.data_ptr(), stream_handle(), reset_ovf=False,
+                              ld=ld, kth_out=kth.data_ptr(), kth_margin=0.25)
+    torch.cuda.synchronize()
+    assert int(ovf.item()) == (0 if dense else 1)
+    for q in range(nq):
+        n = cap if dense else min(int(cnt[q]), cap)
+        ref = torch.full((k,), -math.inf, device=DEV)
+        if n:
+            v = torch.topk(cs[q, :n], min(k, n)).values
+            ref[:v.numel()] = v
+        assert torch.equal(out_s[q], ref), q
+        assert torch.equal(kth[q], ref[k - 1] - 0.25), q              # (fp32 arithmetic)
+        fin = torch.isfinite(ref)
+        ids = out_i[q][fin].long()
+        pos = ids if dense else ids // 3 - q * ld
+        assert ((pos >= 0) & (pos < n)).all(), q
+        assert torch.equal(cs[q][pos], ref[fin]), q                 # ids point at their scores
+        assert ids.unique().numel() == ids.numel(), q
+        assert (out_i[q][~fin] == -1).all()
+    gate = torch.zeros(1, dtype=torch.int32, device=DEV)
+    out_s.fill_(7.0)
+    hip().topk_select_counted(cs.data_ptr(), 0 if dense else ci.data_ptr(),
+                              0 if dense else cnt.data_ptr(), cap, nq, kmax, k, out_s.data_ptr(),
+                              out_i.data_ptr(), ovf.data_ptr(), stream_handle(), gate=gate.data_ptr(),
+                              reset_ovf=False, ld=ld)
+    torch.cuda.synchronize()
+    assert (out_s == 7.0).all()
+
+
+@pytest.mark.parametrize("m,tcap", [(2048, 4096), (70000, 8191), (64, 1)])
+def test_topk_select_counted_second_segment(m, tcap):
+    """The pruned search's seed select with the dense fresh-row tail as the launch's second
+    segment (blockIdx.y == 1): both == torch.topk of their own columns of one score matrix; the
+    k-th-best output comes from the first segment only."""
+    from codename_symbiont_amd.ops._ext import hip, stream_handle
+
+    nq, k, ld = 29, 10, m + tcap + 3
+    S = _f(nq, ld, seed=107).round(decimals=2)
+    o = [torch.empty(nq, k, device=DEV) for _ in range(2)]
+    oi = [torch.empty(nq, k, dtype=torch.int32, device=DEV) for _ in range(2)]
+    kth = torch.empty(nq, device=DEV)
+    flag = torch.zeros(1, dtype=torch.int32, device=DEV)
+    hip().topk_select_counted(S.data_ptr(), 0, 0, m, nq, 16, k, o[0].data_ptr(), oi[0].data_ptr(),
+                              flag.data_ptr(), stream_handle(), reset_ovf=False, ld=ld,
+                              kth_out=kth.data_ptr(), kth_margin=0.5,
+                              seg2_s=S.data_ptr() + 4 * m, seg2_cap=tcap,
+                              seg2_out_s=o[1].data_ptr(), seg2_out_i=oi[1].data_ptr())
+    torch.cuda.synchronize()
+    for seg, (lo, n) in enumerate([(0, m), (m, tcap)]):
+        ref = torch.full((nq, k), -math.inf, device=DEV)
+        v = torch.topk(S[:, lo:lo + n], min(k, n), dim=1).values
+        ref[:, :v.shape[1]] = v
+        assert torch.equal(o[seg], ref), seg
+        fin = torch.isfinite(ref)
+        got = torch.gather(S[:, lo:lo + n], 1, oi[seg].clamp_min(0).long())
+        assert torch.equal(got[fin], ref[fin]), seg
+    assert torch.equal(kth, o[0][:, k - 1] - 0.5) and int(flag) == 0
+
+
 @pytest.mark.parametrize("k", [17, 32, 64, 100, 128])
 @pytest.mark.parametrize("data", ["random", "clustered"])
 def test_index_large_k_search_is_exact(k, data):
