@@ -1134,13 +1134,40 @@ __global__ __launch_bounds__(256) void mx4_select_kernel(
   if (stage == 2 && q == 0 && threadIdx.x == 0) atomicOr(nv, 1);
   const float t = T[q];
   const float lo = t - wa * margin4[q] - wb * margin8[q], hi = t - margin8[q];
+  // the probe's columns enumerated directly (probe tile j = tile j * tile_stride), four
+  // independent loads in flight per thread: the walk over every column with a per-element tile
+  // test waited out one load round trip per probe column (97 us per held-out search)
   float c = 0.f;
   const float* ps = probe_s + (size_t)q * ld;
-  for (int i = threadIdx.x; i < n_cols; i += 256)
-    if (((i >> 6) % tile_stride) == 0) c += (ps[i] >= lo && ps[i] < hi) ? 1.f : 0.f;
+  const int n_probe = ((n_cols + 63) / 64 + tile_stride - 1) / tile_stride * 64;
+  auto pcol = [&](int j) { return ((j >> 6) * tile_stride << 6) + (j & 63); };
+  int j = threadIdx.x;
+  for (; j + 3 * 256 < n_probe; j += 4 * 256) {
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int col = pcol(j + u * 256);
+      v[u] = col < n_cols ? ps[col] : -INFINITY;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) c += (v[u] >= lo && v[u] < hi) ? 1.f : 0.f;
+  }
+  for (; j < n_probe; j += 256) {
+    const int col = pcol(j);
+    const float v = col < n_cols ? ps[col] : -INFINITY;
+    c += (v >= lo && v < hi) ? 1.f : 0.f;
+  }
   float tc = 0.f;
   const float* tcs = tail_cs + (size_t)q * tail_ld;
-  for (int i = threadIdx.x; i < tail_cap; i += 256) tc += (tcs[i] >= lo && tcs[i] < hi) ? 1.f : 0.f;
+  int i = threadIdx.x;
+  for (; i + 3 * 256 < tail_cap; i += 4 * 256) {
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = tcs[i + u * 256];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) tc += (v[u] >= lo && v[u] < hi) ? 1.f : 0.f;
+  }
+  for (; i < tail_cap; i += 256) tc += (tcs[i] >= lo && tcs[i] < hi) ? 1.f : 0.f;
   c = wave_sum(c);
   tc = wave_sum(tc);
   if (lane == 0) {

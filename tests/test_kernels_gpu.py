@@ -1836,6 +1836,42 @@ def test_topk_select_counted_matches_torch(kmax, k, dense, cap):
     assert (out_s == 7.0).all()
 
 
+@pytest.mark.parametrize("n_cols,stride,tcap", [(48832, 4, 5000), (12224, 4, 8191), (1000, 1, 0),
+                                                (777, 3, 64), (300000, 4, 4096)])
+def test_mx4_select_counts_the_probe_band(n_cols, stride, tcap):
+    """index_i8.hip mx4_select_kernel: per query, the probe columns (64-column tiles t with
+    t % stride == 0, c < n_cols) and the dense tail scoring in [T - 2 m4, T - m8), the probe
+    count scaled by rate -- the tier is not viable (nv = 1) iff some query's estimate exceeds the
+    limit; thr4 = T - m4.  Pinned at the largest estimate (limit = it: viable; just below: not)."""
+    from codename_symbiont_amd.ops._ext import hip, stream_handle
+
+    nq = 33
+    ld, tld = n_cols + 5, max(tcap, 1) + 2
+    g = torch.Generator(device="cpu").manual_seed(n_cols + tcap)
+    S = (torch.rand(nq, ld, generator=g) * 0.4).to(DEV)
+    tail = (torch.rand(nq, tld, generator=g) * 0.4).to(DEV)
+    T = (torch.rand(nq, generator=g) * 0.2 + 0.25).to(DEV)
+    m4 = (torch.rand(nq, generator=g) * 0.05 + 0.02).to(DEV)
+    m8 = (torch.rand(nq, generator=g) * 0.01).to(DEV)
+    rate = 37.0
+    lo, hi = (T - 2 * m4)[:, None], (T - m8)[:, None]
+    col = torch.arange(n_cols, device=DEV)
+    probe = ((col // 64) % stride) == 0
+    band = (S[:, :n_cols] >= lo) & (S[:, :n_cols] < hi) & probe[None]
+    tband = (tail[:, :tcap] >= lo) & (tail[:, :tcap] < hi)
+    est = band.sum(1).float() * rate + tband.sum(1).float()
+    top = float(est.max())
+    thr4 = torch.empty(nq, device=DEV)
+    for limit, want in ((top, 0), (top - 0.5, 1)):
+        nv = torch.zeros(1, dtype=torch.int32, device=DEV)
+        hip().mx4_select(nq, T.data_ptr(), m4.data_ptr(), m8.data_ptr(), S.data_ptr(), n_cols, rate,
+                         tail.data_ptr(), tcap, limit, thr4.data_ptr(), nv.data_ptr(),
+                         stream_handle(), ld=ld, tile_stride=stride, tail_ld=tld, nv_zeroed=True)
+        torch.cuda.synchronize()
+        assert int(nv) == want, (limit, top)
+    assert torch.equal(thr4, T - m4)
+
+
 @pytest.mark.parametrize("m,tcap", [(2048, 4096), (70000, 8191), (64, 1)])
 def test_topk_select_counted_second_segment(m, tcap):
     """The pruned search's seed select with the dense fresh-row tail as the launch's second
