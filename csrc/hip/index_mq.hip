@@ -520,6 +520,48 @@ __global__ __launch_bounds__(NTH) void topk_select_counted_kernel(
     tv[i] = -INFINITY;
     ti[i] = -1;
   }
+  float rv;
+  int ri;
+  // Long lists: a first pass takes each thread's max; the KMAX-th largest of those maxima is at
+  // most the list's KMAX-th largest entry (the KMAX largest maxima are KMAX distinct entries), so
+  // the second pass inserts only entries reaching it.  Without it a dense row of random scores
+  // inserts most of each thread's first ~3 KMAX entries, a serial 16-step chain each.
+  __shared__ float floor_s;
+  float floor_v = -INFINITY;
+  if (n >= 8 * NTH) {   // (block-uniform)
+    float mx = -INFINITY;
+    int c = tid;
+    for (; c + 3 * NTH < n; c += 4 * NTH) {
+      float s[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s[u] = cs[c + u * NTH];
+      mx = fmaxf(fmaxf(mx, fmaxf(s[0], s[1])), fmaxf(s[2], s[3]));
+    }
+    for (; c < n; c += NTH) mx = fmaxf(mx, cs[c]);
+    float mv[1] = {mx};
+    int mi[1] = {0};
+    wave_pop_topk<KMAX, 1>(mv, mi, lane, rv, ri);
+    if (lane < KMAX) ls[wave * KMAX + lane] = rv;
+    __syncthreads();
+    if (wave == 0) {
+      float pv[P];
+      int pi[P];
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        pv[j] = -INFINITY;
+        pi[j] = 0;
+      }
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        const float v = ls[lane + 64 * j];
+        if (v > pv[P - 1]) topk_insert<P>(pv, pi, v, 0);
+      }
+      wave_pop_topk<KMAX, P>(pv, pi, lane, rv, ri);
+      if (lane == KMAX - 1) floor_s = rv;
+    }
+    __syncthreads();
+    floor_v = floor_s;
+  }
   int c = tid;
   for (; c + 3 * NTH < n; c += 4 * NTH) {
     float s[4];
@@ -527,15 +569,13 @@ __global__ __launch_bounds__(NTH) void topk_select_counted_kernel(
     for (int u = 0; u < 4; ++u) s[u] = cs[c + u * NTH];
 #pragma unroll
     for (int u = 0; u < 4; ++u)
-      if (s[u] > tv[KMAX - 1])
+      if (s[u] >= floor_v && s[u] > tv[KMAX - 1])
         topk_insert<KMAX>(tv, ti, s[u], ci != nullptr ? ci[c + u * NTH] : c + u * NTH);
   }
   for (; c < n; c += NTH) {
     const float s = cs[c];
-    if (s > tv[KMAX - 1]) topk_insert<KMAX>(tv, ti, s, ci != nullptr ? ci[c] : c);
+    if (s >= floor_v && s > tv[KMAX - 1]) topk_insert<KMAX>(tv, ti, s, ci != nullptr ? ci[c] : c);
   }
-  float rv;
-  int ri;
   wave_pop_topk<KMAX, KMAX>(tv, ti, lane, rv, ri);
   if (lane < KMAX) {
     ls[wave * KMAX + lane] = rv;
