@@ -1110,8 +1110,19 @@ class HbmIndexShard:
         if not self.mq_stats:
             return
         if self._mq_tot is None:
-            self._mq_tot = tuple(torch.zeros(1, dtype=torch.int32, device=self.device)
-                                 for _ in range(5))
+            self._mq_tot_buf = torch.zeros(5, dtype=torch.int32, device=self.device)
+            self._mq_tot = tuple(self._mq_tot_buf[i:i + 1] for i in range(5))
+        if (self.device.type == "cuda" and ovf.dtype == torch.int32 and cnt.dtype == torch.int32
+                and cnt.is_contiguous() and (dense is None or dense.dtype == torch.int32)
+                and (blk is None or blk.dtype == torch.int32)):
+            from ..ops._ext import hip, stream_handle
+
+            # (one launch: prepass statistics kernel, index_i8.hip prune_stats_kernel)
+            hip().prune_stats(ovf.data_ptr(), cnt.data_ptr(), cnt.numel(),
+                              0 if dense is None else dense.data_ptr(),
+                              0 if blk is None else blk.data_ptr(), self._mq_tot_buf.data_ptr(),
+                              stream_handle(self.device))
+            return
         self._mq_tot[0].add_(ovf)
         torch.maximum(self._mq_tot[1], cnt.max().view(1), out=self._mq_tot[1])
         if dense is not None:

@@ -157,6 +157,8 @@ int symb_index_scan_mq_ablate(const void* X, int n_valid, int rows_per_blk, int 
                               const void* Q, int NQ, const float* thr, float* cand_s, int* cand_i,
                               int* cand_n, int cap, int xcd, hipStream_t st, int abl, int sets,
                               int rsplit);
+int symb_prune_stats(const int* ovf, const int* cnt, int NQ, const int* dense, const int* blk,
+                     int* tot, hipStream_t st);
 int symb_topk_select_counted(const float* cand_s, const int* cand_i, const int* cand_n, int cap,
                              int NQ, int kmax, int k, float* out_s, int* out_i, int* ovf,
                              hipStream_t st, const int* gate, int reset_ovf, int ld = 0,
@@ -684,6 +686,12 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("NQ"), py::arg("thr"), py::arg("cand_s"), py::arg("cand_i"), py::arg("cand_n"),
      py::arg("cap"), py::arg("xcd"), py::arg("stream"), py::arg("abl"), py::arg("sets") = 4,
      py::arg("rsplit") = 1);
+  m.def("prune_stats", [](uptr ovf, uptr cnt, int NQ, uptr dense, uptr blk, uptr tot, uptr st) {
+    check(symb_prune_stats(P<const int>(ovf), P<const int>(cnt), NQ, P<const int>(dense),
+                           P<const int>(blk), P<int>(tot), S(st)),
+          "prune_stats");
+  }, py::arg("ovf"), py::arg("cnt"), py::arg("NQ"), py::arg("dense"), py::arg("blk"),
+     py::arg("tot"), py::arg("stream"));
   m.def("topk_select_counted", [](uptr cand_s, uptr cand_i, uptr cand_n, int cap, int NQ,
                                   int kmax, int k, uptr out_s, uptr out_i, uptr ovf, uptr st,
                                   uptr gate, bool reset_ovf, int ld, uptr kth_out,

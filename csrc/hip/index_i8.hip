@@ -1305,6 +1305,38 @@ __global__ __launch_bounds__(256) void prune_route_sum_kernel(int NQ, int n_rblk
   if (lane == 0 && s > limit) atomicOr(dense, 1);
 }
 
+// The search statistics of HbmIndexShard.mq_stats in one launch (they were ~10 framework
+// kernels per search): tot[0] += *ovf; tot[1] = max(tot[1], max of cnt[0 .. NQ)); with dense:
+// tot[2] += *dense; with blk too: part = (blk[0] > 0) && !*dense, tot[3] += part,
+// tot[4] += blk[0] * part.  One workgroup; stream order makes the read-modify-writes safe.
+__global__ __launch_bounds__(256) void prune_stats_kernel(const int* __restrict__ ovf,
+                                                          const int* __restrict__ cnt, int NQ,
+                                                          const int* __restrict__ dense,
+                                                          const int* __restrict__ blk,
+                                                          int* __restrict__ tot) {
+  __shared__ int wm[4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int m = 0;
+  for (int i = tid; i < NQ; i += 256) m = max(m, cnt[i]);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
+  if (lane == 0) wm[w] = m;
+  __syncthreads();
+  if (tid != 0) return;
+  m = max(max(wm[0], wm[1]), max(wm[2], wm[3]));
+  tot[0] += *ovf;
+  tot[1] = max(tot[1], m);
+  if (dense != nullptr) {
+    const int d = *dense;
+    tot[2] += d;
+    if (blk != nullptr) {
+      const int part = (blk[0] > 0 ? 1 : 0) * (1 - d);
+      tot[3] += part;
+      tot[4] += blk[0] * part;
+    }
+  }
+}
+
 // One workgroup: the per-block decision of prune_route_kernel.  blk: [0] = listed blocks, [1] =
 // n_rblk, [2 .. 2 + n_rblk) = the listed blocks in order, [2 + n_rblk .. 2 + 2 n_rblk) = skip
 // flags of the int8 scan.  *dense ends as 1 iff every block went to the bf16 scan.
@@ -1567,6 +1599,13 @@ int symb_quant_rows_mx4(const void* X, int n, int dim, void* X4, void* SC, float
 
 // The MX-fp4 tier choice (mx4_select_kernel); nv (one int) is zeroed here.  probe_s: [NQ][n_probe]
 // exact scores of the probe rows, tail_cs: [NQ][tail_cap] exact scores of the tail rows.
+int symb_prune_stats(const int* ovf, const int* cnt, int NQ, const int* dense, const int* blk,
+                     int* tot, hipStream_t st) {
+  if (NQ <= 0 || ovf == nullptr || cnt == nullptr || tot == nullptr) return -1;
+  hipLaunchKernelGGL(prune_stats_kernel, dim3(1), dim3(256), 0, st, ovf, cnt, NQ, dense, blk, tot);
+  return (int)hipGetLastError();
+}
+
 int symb_mx4_select(int NQ, const float* T, const float* margin4, const float* margin8,
                     const float* probe_s, int n_cols, int ld, int tile_stride, float rate,
                     const float* tail_cs, int tail_cap, int tail_ld, float limit, float* thr4,

@@ -1872,6 +1872,38 @@ def test_mx4_select_counts_the_probe_band(n_cols, stride, tcap):
     assert torch.equal(thr4, T - m4)
 
 
+def test_prune_stats_matches_torch():
+    """index_i8.hip prune_stats_kernel (HbmIndexShard.mq_stats in one launch) == the torch
+    composition it replaced, accumulated over several searches (with and without the route's
+    dense flag / block list)."""
+    from codename_symbiont_amd.ops._ext import hip, stream_handle
+
+    g = torch.Generator(device="cpu").manual_seed(5)
+    tot = torch.zeros(5, dtype=torch.int32, device=DEV)
+    ref = torch.zeros(5, dtype=torch.int64)
+    for it, (nq, with_dense, with_blk) in enumerate([(256, True, True), (1000, True, False),
+                                                     (7, False, False), (2048, True, True),
+                                                     (300, True, True)]):
+        ovf = torch.randint(0, 2, (1,), generator=g, dtype=torch.int32)
+        cnt = torch.randint(0, 40000, (nq,), generator=g, dtype=torch.int32)
+        dense = torch.tensor([it % 2], dtype=torch.int32)
+        blk = torch.tensor([it * 3 % 5, 9], dtype=torch.int32)
+        o, c, d, b = ovf.to(DEV), cnt.to(DEV), dense.to(DEV), blk.to(DEV)
+        hip().prune_stats(o.data_ptr(), c.data_ptr(), nq, d.data_ptr() if with_dense else 0,
+                          b.data_ptr() if with_blk and with_dense else 0, tot.data_ptr(),
+                          stream_handle())
+        ref[0] += int(ovf)
+        ref[1] = max(int(ref[1]), int(cnt.max()))
+        if with_dense:
+            ref[2] += int(dense)
+            if with_blk:
+                part = int(blk[0] > 0) * (1 - int(dense))
+                ref[3] += part
+                ref[4] += int(blk[0]) * part
+    torch.cuda.synchronize()
+    assert tot.cpu().long().tolist() == ref.tolist()
+
+
 @pytest.mark.parametrize("m,tcap", [(2048, 4096), (70000, 8191), (64, 1)])
 def test_topk_select_counted_second_segment(m, tcap):
     """The pruned search's seed select with the dense fresh-row tail as the launch's second
