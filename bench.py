@@ -376,7 +376,8 @@ def result_line(args, info, comm, metric, unit, config, total, ms, prune, prefil
         "dtype": args.encoder_dtype,
         "index_dtype": args.index_dtype,
         "index_prefilter": prefilter,
-        "index_search": ("exact: bound-pruned scan + bf16 re-score" if prune
+        "index_search": None if args.mode == "embed" else (
+                        "exact: bound-pruned scan + bf16 re-score" if prune
                          else ("fp8 prefilter + bf16 re-score" if prefilter
                                else ("exact scan of the e4m3 rows" if args.index_dtype == "fp8"
                                      else "exact bf16 scan"))),
@@ -496,6 +497,98 @@ def run_cpu(args, info, comm) -> int:
     return 0
 
 
+def _framing(cfg):
+    """[CLS] / [SEP] ids of the synthetic batches (encoder.synthetic_batch's framing)."""
+    return (101, 102) if cfg.vocab_size > 30000 and cfg.pad_token_id == 0 else (0, 2)
+
+
+def run_embed(args, info, comm, enc, cfg, t_setup: float) -> int:
+    """--mode embed (BASELINE configs #2 / #4, replica DP: every rank embeds its own batch).
+
+    One step = B full-length sentences of S tokens through the HIP encoder.  Every step's token
+    ids are NEW: drawn on the GPU by torch.randint inside the replayed hipGraph (the graph-safe
+    default generator advances its Philox offset on every replay) and framed with [CLS] / [SEP]
+    at the sentence bounds; positions and cu_seqlens keep the fixed full-length layout.  No index
+    shard is allocated and nothing is upserted (the reference's batch loop,
+    preprocessing_service/src/embedding_generator.rs:146-214, only embeds).  The graph holds the
+    token draw and the whole forward, so the host enqueues one replay per step."""
+    from codename_symbiont_amd.models.encoder import synthetic_batch
+    from codename_symbiont_amd.parallel import dist as D
+    from codename_symbiont_amd.utils.gpu_debug import debug_enabled
+
+    dev = info.device
+    B, S, K, W = args.batch, args.seq, args.steps, args.warmup
+    torch.manual_seed(4321 + info.rank)
+    batch = synthetic_batch(cfg, B, S, seed=1000 * info.rank).to(dev)
+    T = batch.num_tokens
+    cls, sep = _framing(cfg)
+    cls_at = batch.cu_seqlens[:-1].long()
+    sep_at = (batch.cu_seqlens[1:] - 1).long()
+    out32 = torch.empty(B, cfg.hidden, device=dev)
+    outu = torch.empty(B, cfg.hidden, dtype=torch.bfloat16, device=dev)
+
+    def draw_and_encode() -> None:
+        torch.randint(1000, cfg.vocab_size, (T,), device=dev, dtype=torch.int32, out=batch.ids)
+        batch.ids.index_fill_(0, cls_at, cls)
+        batch.ids.index_fill_(0, sep_at, sep)
+        enc.forward_packed(batch, out32, outu)
+
+    draw_and_encode()   # kernel attributes, workspace
+    torch.cuda.synchronize(dev)
+    use_graph = not args.no_graph and not debug_enabled()
+    run = draw_and_encode
+    if use_graph:
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
+            draw_and_encode()
+        run = graph.replay
+    log(info, f"[bench] setup {time.time() - t_setup:.1f}s: {cfg.model_name} embed, {B} x {S} "
+              f"tokens per step, no index shard; graph={use_graph}")
+    ids_seen = []
+    for i in range(max(W, 2)):
+        run()
+        if i < 2:
+            ids_seen.append(batch.ids.clone())
+    fresh = not torch.equal(ids_seen[0], ids_seen[1])
+    torch.cuda.synchronize(dev)
+    D.barrier(info)
+    torch.cuda.synchronize(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(K)]
+    cur = torch.cuda.current_stream(dev)
+    t_start = time.perf_counter()
+    for j in range(K):
+        evs[j][0].record(cur)
+        run()
+        evs[j][1].record(cur)
+    host_ms = (time.perf_counter() - t_start) * 1000.0 / K
+    torch.cuda.synchronize(dev)
+    D.barrier(info)
+    torch.cuda.synchronize(dev)
+    elapsed = D.allreduce_max(info, time.perf_counter() - t_start)
+    ms = elapsed * 1000.0 / K
+    total = B * info.world * K / elapsed
+    extra_out = {
+        "embed_ms_per_step_rank0": round(sum(a.elapsed_time(b) for a, b in evs) / K, 3),
+        "host_enqueue_ms_per_step_rank0": round(host_ms, 3),
+        "token_ids": "drawn on the GPU every step inside the replayed graph",
+        "token_ids_fresh_per_step": fresh,
+        "index_shard": None,
+    }
+    cfg_extra = dict(args.opts_changed)
+    cfg_extra.pop("timeline", None)
+    if use_graph:
+        cfg_extra["encoder_hipgraph"] = True
+    metric, config, unit = metric_and_config(args, info, cfg, None, None, cfg_extra)
+    config["parallelism"] = f"dp{info.world} (replica: one batch per rank)"
+    if info.rank == 0:
+        data = (f"synthetic token ids (fresh every step, {S}-token sentences), random-init "
+                f"weights; no index")
+        _emit_result(result_line(args, info, comm, metric, unit, config, total, ms, None, None,
+                                 data, extra_out))
+    return 0
+
+
 def run_gpu(args, info, comm) -> int:
     from codename_symbiont_amd.index.shard import MQ_DIMS, HbmIndexShard, resolve_prune
     from codename_symbiont_amd.index.synth import CorpusGen, fill_corpus
@@ -518,27 +611,33 @@ def run_gpu(args, info, comm) -> int:
     # exact either way; i8 applies to 384-wide bf16 shards without a prefilter (else: plain scan)
     prune = resolve_prune("auto" if args.index_prune == "i8" and args.mode != "embed" else "none",
                           args.index_dtype, cfg.hidden, prefilter, device=dev)
-    shard = HbmIndexShard(cfg.hidden, rows_per_rank + extra, device=dev, dtype=args.index_dtype,
-                          prefilter=prefilter, prune=prune)
+    group_dp = args.mode == "embed" and args.embed_dp == "group" and info.world > 1
+    if args.mode == "embed" and not group_dp:
+        # config #2 / #4: the encoder alone -- no index shard, no upserts, token ids drawn on
+        # the GPU inside the replayed graph (run_embed)
+        return run_embed(args, info, comm, enc, cfg, t0)
     gen = CorpusGen(args.corpus, cfg.hidden, dev, clusters=args.clusters,
                     spread=args.cluster_spread)
+    shard = searcher = None
     if args.mode != "embed":
+        shard = HbmIndexShard(cfg.hidden, rows_per_rank + extra, device=dev,
+                              dtype=args.index_dtype, prefilter=prefilter, prune=prune)
         fill_corpus(shard, gen, rows_per_rank, seed=100 + info.rank)
-    searcher = _make_searcher(args, shard, info, lambda n, seed: enc.forward_packed(
-        synthetic_batch(cfg, n, S, seed=seed).to(dev))[1].clone())
-    shard.mq_stats = os.environ.get("SYMB_MQ_STATS", "0") not in ("", "0") or args.mode == "search"
-    if args.prune_sample_shift:
-        shard.PRUNE_TILE_SHIFT = shard.PRUNE_TILE_SHIFT_SPLIT = args.prune_sample_shift
-        shard.PRUNE_TILE_SHIFT_MX4 = args.prune_sample_shift
-    if args.prune_block_frac:
-        shard.PRUNE_BLOCK_FRAC = args.prune_block_frac
+        searcher = _make_searcher(args, shard, info, lambda n, seed: enc.forward_packed(
+            synthetic_batch(cfg, n, S, seed=seed).to(dev))[1].clone())
+        shard.mq_stats = (os.environ.get("SYMB_MQ_STATS", "0") not in ("", "0")
+                          or args.mode == "search")
+        if args.prune_sample_shift:
+            shard.PRUNE_TILE_SHIFT = shard.PRUNE_TILE_SHIFT_SPLIT = args.prune_sample_shift
+            shard.PRUNE_TILE_SHIFT_MX4 = args.prune_sample_shift
+        if args.prune_block_frac:
+            shard.PRUNE_BLOCK_FRAC = args.prune_block_frac
     torch.cuda.synchronize(dev)
     row_bytes = cfg.hidden * (1 if args.index_dtype == "fp8" else 2)
-    log(info, f"[bench] setup {time.time() - t0:.1f}s: {cfg.model_name}, shard {rows_per_rank} "
-              f"rows x {cfg.hidden} {args.index_dtype} ({args.corpus}) = "
-              f"{rows_per_rank * row_bytes / 1e9:.1f} GB/rank; comm {comm}")
-
-    group_dp = args.mode == "embed" and args.embed_dp == "group" and info.world > 1
+    log(info, f"[bench] setup {time.time() - t0:.1f}s: {cfg.model_name}, "
+              + (f"shard {rows_per_rank} rows x {cfg.hidden} {args.index_dtype} ({args.corpus}) = "
+                 f"{rows_per_rank * row_bytes / 1e9:.1f} GB/rank" if shard is not None
+                 else "no index shard (embed mode)") + f"; comm {comm}")
     if group_dp:
         from codename_symbiont_amd.parallel.embed_group import EmbedGroup
 
@@ -579,7 +678,7 @@ def run_gpu(args, info, comm) -> int:
     # inserted); self queries are stored rows (each query's best match is itself)
     if args.queries == "heldout":
         qsets = [gen.unit(B, 5000 + 10 * info.rank + i).bfloat16() for i in range(NB)]
-    else:
+    elif shard is not None:
         stride = max(1, rows_per_rank // (NB * B))
         qsets = [shard.rows[torch.arange(B, device=dev) * stride + i].clone() for i in range(NB)]
 
@@ -743,7 +842,7 @@ def run_gpu(args, info, comm) -> int:
             run_encoder(slot, out_f32, out_unit)
             consumed[slot].record(compute)
             prefetch(i + 1)
-            if args.queries == "self":
+            if args.queries == "self" and shard is not None:
                 shard.append_unit(out_unit)
             q = out_unit
         else:
@@ -769,10 +868,10 @@ def run_gpu(args, info, comm) -> int:
     torch.cuda.synchronize(dev)
     D.barrier(info)
     torch.cuda.synchronize(dev)
-    if shard._mq_tot is not None:   # count overflows of the timed steps only
+    if shard is not None and shard._mq_tot is not None:   # overflows of the timed steps only
         for t in shard._mq_tot:
             t.zero_()
-    if shard._mx4_tot is not None:
+    if shard is not None and shard._mx4_tot is not None:
         shard._mx4_tot.zero_()
     for kph in hph:
         hph[kph] = 0.0
@@ -799,6 +898,8 @@ def run_gpu(args, info, comm) -> int:
         "host_enqueue_ms_per_step_rank0": round(host_ms, 3),
         "host_phase_ms_per_step_rank0": {kph: round(v * 1000.0 / K, 3) for kph, v in hph.items()},
     }
+    if group_dp:   # ranks 1..N-1's pooled rows cross the wire in this dtype
+        extra_out["embed_wire"] = egroup.wire
     if sampler is not None:
         clocks = sampler.stop()
         # step boundaries: the search-end events, relative to the first step's start
@@ -816,9 +917,9 @@ def run_gpu(args, info, comm) -> int:
         extra_out["step_ms_last_decile"] = round((ends[-1] - ends[-q - 1]) / q, 3) if K > q else None
         if clocks:
             extra_out["sclk_mhz_samples"] = [c[1] for c in clocks][:: max(1, len(clocks) // 20)]
-    if shard._mx4_tot is not None and args.mode != "embed":   # batches the MX-fp4 tier served
+    if shard is not None and shard._mx4_tot is not None:   # batches the MX-fp4 tier served
         extra_out["search_mx4_tier_batches"] = int(shard._mx4_tot.item())
-    if shard._mq_tot is not None and args.mode != "embed":
+    if shard is not None and shard._mq_tot is not None:
         ovf = int(shard._mq_tot[0].item())
         extra_out["search_overflow_batches"] = ovf
         extra_out["search_max_candidates"] = int(shard._mq_tot[1].item())

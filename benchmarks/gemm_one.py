@@ -4,8 +4,7 @@
     python benchmarks/gemm_one.py --m 32768 --n 3072 --k 768 --epi 1 --tile 3 --iters 50
     tile: symb_gemm_config tile mode (3 = auto with the 256x192 tile, 10 = round-3 auto,
     2 = 256x256 wherever N % 256 == 0);
-    --torch runs torch.matmul (hipBLASLt) on the same operands instead; --vs 0 the VGPR-staged
-    4-wave kernel (gemm_vs.hip).
+    --torch runs torch.matmul (hipBLASLt) on the same operands instead.
 Prints one JSON line: ms per call and TFLOP/s.
 """
 from __future__ import annotations
@@ -32,8 +31,6 @@ def main():
     ap.add_argument("--torch", action="store_true")
     ap.add_argument("--lt", type=int, default=0,
                     help="hipBLASLt route for plain projections (gemm_lt_config: 0 off, 1 auto)")
-    ap.add_argument("--vs", type=int, default=-1,
-                    help="VGPR-staged 4-wave kernel (gemm_vs.hip) tile columns: 0 auto, 256, 192; -1 off")
     a = ap.parse_args()
     from codename_symbiont_amd.ops import kernels as K
     from codename_symbiont_amd.ops._ext import hip
@@ -46,7 +43,6 @@ def main():
     y = torch.empty(a.m, a.n, device="cuda", dtype=torch.bfloat16)
     hip().gemm_config(128, a.tile, 8)
     hip().gemm_lt_config(a.lt)
-    hip().gemm_vs_config(0 if a.vs < 0 else 2, max(a.vs, 0))
     f = (lambda: torch.matmul(x, w.t(), out=y)) if a.torch else (lambda: K.gemm(x, w, b, a.epi, r, out=y))
     for _ in range(3):
         f()

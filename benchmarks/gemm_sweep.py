@@ -3,9 +3,7 @@
 
     python benchmarks/gemm_sweep.py [--models bge-base,e5-large] [--variants t3,t9,lt,torch]
 
-Variants: vs / vs256 / vs192 = the VGPR-staged 4-wave kernel (gemm_vs.hip; auto / forced tile
-columns);
-tN = symb_gemm with tile mode N (3 = auto with the 256x192 tile, 10 = the round-3
+Variants: tN = symb_gemm with tile mode N (3 = auto with the 256x192 tile, 10 = the round-3
 auto rule, 2 = the 256x256 tile wherever N % 256 == 0), hipBLASLt route off; lt = the hipBLASLt
 route for the plain projections (round-3 default);
 torch = torch.matmul (hipBLASLt, no epilogue).
@@ -63,11 +61,6 @@ def main():
                     return lambda: (hip().gemm_config(128, 10, 8),
                                     hip().gemm_lt_config(1), K.gemm(x, w, b, epi, r, out=y),
                                     hip().gemm_lt_config(0))
-                if v.startswith("vs"):   # vs / vs256 / vs192: gemm_vs.hip (auto / forced width)
-                    bn = int(v[2:] or 0)
-                    return lambda: (hip().gemm_config(128, 3, 8), hip().gemm_lt_config(0),
-                                    hip().gemm_vs_config(2, bn),
-                                    K.gemm(x, w, b, epi, r, out=y), hip().gemm_vs_config(0))
                 t = int(v[1:])
                 return lambda: (hip().gemm_config(128, t, 8), hip().gemm_lt_config(0),
                                 K.gemm(x, w, b, epi, r, out=y))
@@ -95,7 +88,6 @@ def main():
                                   "TFLOPs": round(2 * a.m * n * k / med / 1e6)}), flush=True)
     hip().gemm_config(128, 3, 8)
     hip().gemm_lt_config(1)
-    hip().gemm_vs_config(0)
 
 
 if __name__ == "__main__":

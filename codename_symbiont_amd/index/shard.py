@@ -145,10 +145,12 @@ MX4_DIMS = (384, 768, 1024)             # ... the MX-fp4 first tier (384-only on
 STREAM_DIMS = (384, 768, 1024)
 STREAM_SUB = 32                         # rows per sub-tile record of the stream images
 # widths of the MX-fp6 (e2m3) middle tier (stream scan only) and where SYMB_PRUNE_MX6=auto keeps
-# it: 0.75 bytes per element, so a 100M x 768 shard (bf16 + int8 + fp4 images ~270 GB) has no
-# room for it by default
+# it: nowhere -- measured, it never applies (held-out queries leave ~70.8k candidates in its band
+# against a 32k cap, and self / near-duplicate queries take the fp4 tier: profiles/r5_lq/), so a
+# default shard allocates no fp6 image and runs no fp6 quantiser, select or gated scan.
+# SYMB_PRUNE_MX6=on keeps it (0.75 bytes per element) for A/B runs.
 MX6_DIMS = (384, 768)
-AUTO_MX6_DIMS = (384,)
+AUTO_MX6_DIMS = ()
 
 
 class HbmIndexShard:
@@ -1447,6 +1449,14 @@ class HbmIndexShard:
         out_s = torch.empty(NQ, k, device=dev)
         out_i = torch.empty(NQ, k, dtype=torch.int32, device=dev)
         skip = blk[2 + n_rblk:].data_ptr() if self.prune_route else 0
+        # The scans stop at the last whole 32-row sub-tile: an append into a partly filled one
+        # re-quantises its rows under a new shared int8 scale (and raises E past what this
+        # search's margins assumed), and a pipelined caller appends batch i + 1 while batch i's
+        # scan runs.  The < 32 rows past the boundary enter every query's candidate list
+        # unconditionally (prefill_candidates) and are re-scored exactly like any candidate.
+        n_scan = n - n % STREAM_SUB if self.stream else n
+        if n_scan < n:
+            h.prefill_candidates(NQ, n_scan, n - n_scan, ci.data_ptr(), cnt.data_ptr(), cap, st)
         m4, m6 = ctx.get("mx4"), ctx.get("mx6")
         for m in (m4, m6):   # every tier enqueued, gated on the flag: exactly one runs
             if m is not None:
@@ -1456,13 +1466,13 @@ class HbmIndexShard:
         tier = (m4 or m6 or {}).get("nv")
         gate, want = (0, 0) if tier is None else (tier.data_ptr(), 3 if m6 is not None else 1)
         if self.img_i8 is not None and not ctx["heavy"]:   # the stream scan (index_stream.hip)
-            h.index_scan_stream(self.img_i8.data_ptr(), n, self.img_i8.shape[0] * STREAM_SUB,
+            h.index_scan_stream(self.img_i8.data_ptr(), n_scan, self.img_i8.shape[0] * STREAM_SUB,
                                 rows_per_blk, n_rblk, q8.data_ptr(), 0, NQ, thr.data_ptr(),
                                 cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(), cap, self.scan_xcd,
                                 st, skip=skip, dim=self.dim, form=0, gate=gate, gate_want=want,
                                 zero_cnt=0)
         else:
-            h.index_scan_i8(self.rows_i8.data_ptr(), self.sx_i8.data_ptr(), n,
+            h.index_scan_i8(self.rows_i8.data_ptr(), self.sx_i8.data_ptr(), n_scan,
                             self.rows_i8.shape[0], rows_per_blk, n_rblk,
                             q8.data_ptr(), NQ, thr.data_ptr(), cs.data_ptr(), ci.data_ptr(),
                             cnt.data_ptr(), cap, self.scan_xcd, st, rsplit, skip=skip,
@@ -1475,14 +1485,14 @@ class HbmIndexShard:
                 if self._mx4_tot is None:
                     self._mx4_tot = torch.zeros(1, dtype=torch.int32, device=dev)
                 runs = self._mx4_tot.data_ptr()
-            h.index_scan_stream(self.img_mx4.data_ptr(), n, self.img_mx4.shape[0] * STREAM_SUB,
+            h.index_scan_stream(self.img_mx4.data_ptr(), n_scan, self.img_mx4.shape[0] * STREAM_SUB,
                                 rows_per_blk, n_rblk, m4["q4"].data_ptr(), m4["qs4"].data_ptr(),
                                 NQ, m4["thr4"].data_ptr(), cs.data_ptr(), ci.data_ptr(),
                                 cnt.data_ptr(), cap, self.scan_xcd, st, skip=skip, dim=self.dim,
                                 form=1, gate=m4["nv"].data_ptr(), gate_want=0, zero_cnt=0,
                                 runs=runs, **self._cent_args(m4))
         elif m4 is not None:
-            h.index_scan_i8(self.rows_mx4.data_ptr(), self.sc_mx4.data_ptr(), n,
+            h.index_scan_i8(self.rows_mx4.data_ptr(), self.sc_mx4.data_ptr(), n_scan,
                             self.rows_mx4.shape[0], rows_per_blk, n_rblk, m4["q4"].data_ptr(), NQ,
                             m4["thr4"].data_ptr(), cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(),
                             cap, self.scan_xcd, st, rsplit, skip=skip, dim=self.dim,
@@ -1494,7 +1504,7 @@ class HbmIndexShard:
                 if self._mx6_tot is None:
                     self._mx6_tot = torch.zeros(1, dtype=torch.int32, device=dev)
                 runs = self._mx6_tot.data_ptr()
-            h.index_scan_stream(self.img_mx6.data_ptr(), n, self.img_mx6.shape[0] * STREAM_SUB,
+            h.index_scan_stream(self.img_mx6.data_ptr(), n_scan, self.img_mx6.shape[0] * STREAM_SUB,
                                 rows_per_blk, n_rblk, m6["q6"].data_ptr(), m6["qs6"].data_ptr(),
                                 NQ, m6["thr6"].data_ptr(), cs.data_ptr(), ci.data_ptr(),
                                 cnt.data_ptr(), cap, self.scan_xcd, st, skip=skip, dim=self.dim,
@@ -1504,7 +1514,7 @@ class HbmIndexShard:
         #     into the same candidate buffers (no launch work when none is listed)
         if self.prune_route:
             sets, mrs, _, slots = self._mq_slots(NQ, n_cus)
-            h.index_scan_mq(self.rows.data_ptr(), n, TILE_ROWS, slots, q_unit.data_ptr(), NQ,
+            h.index_scan_mq(self.rows.data_ptr(), n_scan, TILE_ROWS, slots, q_unit.data_ptr(), NQ,
                             T.data_ptr(), cs.data_ptr(), ci.data_ptr(), cnt.data_ptr(), cap,
                             self.scan_xcd, st, sets, 0, mrs, blist=blk.data_ptr(),
                             list_tiles=rows_per_blk // TILE_ROWS, zero_cnt=False, dim=self.dim)

@@ -15,10 +15,17 @@ token batch to the group and every GPU of the node encodes a share of it:
 Messages are tiny next to the work (a 256 x 128-token batch is 256 KB of ids in, 256 x H x 2 B of
 embeddings out), so one broadcast + one all_gather per batch keeps every link's share small.  The
 slice each rank encodes runs on its own compute stream; rank 0's H2D of the next batch overlaps
-through the embed batcher's copy stream (services/batcher.py).  Ranks 1..N-1 run ``serve()``; the
-header is the only host read a batch costs them (they must learn its shapes to receive it).
-The bf16 wire rounds each pooled value once (relative 2^-9; cosine to the f32 rows >= 0.99999,
-tests/test_parallel_cpu.py); ``wire_dtype`` = torch.float32 keeps the f32 values exactly.
+through the embed batcher's copy stream (services/batcher.py).  Ranks 1..N-1 run ``serve()``.
+
+Control plane: on RCCL the fixed-size header travels over a gloo (host TCP) group of the same
+ranks, so learning a batch's shapes is a host receive that never synchronises a GPU stream --
+a rank enqueues batch i + 1's receives and forward while batch i's are still running (a header
+broadcast over RCCL would need a device read-back, which waits for everything queued before it).
+
+The bf16 wire rounds each pooled value of ranks 1..N-1 once (relative 2^-9; cosine to the f32
+rows >= 0.99999, tests/test_parallel_cpu.py); rank 0's own slice never crosses the wire and keeps
+its f32 values.  ``wire_dtype`` = torch.float32 keeps every value exactly (the bench and the
+service report which wire ran).
 """
 from __future__ import annotations
 
@@ -66,6 +73,17 @@ class EmbedGroup:
             wire_dtype = torch.bfloat16 if info.backend == "nccl" else torch.float32
         self.wire_dtype = wire_dtype
         self.hdr_len = HDR_FIXED + HDR_RANK * info.world
+        # the header's group: gloo beside RCCL (host-only receive), else the data group itself
+        self.ctrl = group
+        if self.collective and info.backend == "nccl" and group is None:
+            self.ctrl = dist.new_group(backend="gloo")
+        self.ctrl_device = (torch.device("cpu") if self.ctrl is not group
+                            else self.comm_device)
+
+    @property
+    def wire(self) -> str:
+        """The embeddings' wire dtype (``bf16`` | ``f32``), for result records."""
+        return "bf16" if self.wire_dtype == torch.bfloat16 else "f32"
 
     # ------------------------------------------------------------------ plumbing
     def _bcast(self, t: torch.Tensor) -> torch.Tensor:
@@ -75,12 +93,14 @@ class EmbedGroup:
 
     def _header(self, vals=None) -> list[int]:
         """Broadcast the op header from rank 0 (vals) / receive it (vals None); host ints."""
-        t = torch.zeros(self.hdr_len, dtype=torch.int64, device=self.comm_device)
         if vals is not None:
-            t.copy_(torch.tensor(vals + [0] * (self.hdr_len - len(vals)), dtype=torch.int64))
-            self._bcast(t)
-            return vals
-        return self._bcast(t).tolist()
+            t = torch.tensor(vals + [0] * (self.hdr_len - len(vals)), dtype=torch.int64)
+        else:
+            t = torch.zeros(self.hdr_len, dtype=torch.int64)
+        t = t.to(self.ctrl_device)
+        if self.collective:
+            dist.broadcast(t, src=0, group=self.ctrl)
+        return vals if vals is not None else t.tolist()
 
     def _plan(self, cu_host: np.ndarray) -> list[int]:
         """Rank 0: the EMBED header for a batch with these (host) cu_seqlens."""
@@ -103,6 +123,7 @@ class EmbedGroup:
         ranges = [tuple(part(r)[:2]) for r in range(info.world)]
         s, e, t0, t1, max_len = part(info.rank)
         out = torch.zeros(maxb, self.H, dtype=wdt, device=self.comm_device)
+        pooled = None
         if e > s:
             dev = getattr(self.enc, "device", torch.device("cpu"))
             # the slice's sentences and tokens by the header's host offsets: no device read
@@ -116,8 +137,11 @@ class EmbedGroup:
         dist.all_gather_into_tensor(gathered, out, group=self.group)
         if not info.is_root:
             return None
-        return torch.cat([gathered[r * maxb: r * maxb + (b - a)] for r, (a, b) in
-                          enumerate(ranges)]).float()
+        # rank 0's own rows straight from its f32 output (they never crossed the wire)
+        own = (pooled.float().to(self.comm_device) if pooled is not None
+               else gathered[:0].float())
+        return torch.cat([own] + [gathered[r * maxb: r * maxb + (b - a)].float()
+                                  for r, (a, b) in enumerate(ranges) if r > 0])
 
     # ------------------------------------------------------------------ collective entry points
     def embed(self, b: PackedBatch | None, cu_host=None) -> torch.Tensor | None:

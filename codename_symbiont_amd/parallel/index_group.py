@@ -10,13 +10,20 @@ a short, fixed sequence of collectives, so all ranks stay in lockstep:
            (counted in ``comm_stats``); rank 0's op lock covers only their ENQUEUE, so the
            header / query broadcast / scan of search i+1 queue behind search i's exchange while
            the caller of search i waits for its result outside the lock.
-  UPSERT : header -> broadcast vectors [n, D] f32 + (owner rank, target row) -> owners write rows.
+  UPSERT : header -> scatter each owner ITS rows only: the per-rank (count, new-row count,
+           overwrite targets) over the control group, the vectors [m, D] f32 (padded to the
+           largest share m) over RCCL -> every rank writes its share.  A broadcast of every
+           vector to every rank sent N times the bytes, and each rank had to find its rows with
+           a device read-back.
   SNAPSHOT / LOAD : header -> every rank saves / loads its own shard under <dir>/rank<r>/
            (index/persist.py: incremental segments of the rows written since the previous
            snapshot); rank 0 adds group.json (world, per-rank counts) and a DELTA of the
            gid -> (point id, payload) table (the gids upserted since, merged geometrically with
            earlier deltas).  A load requires the same world size.
   STOP   : header only.
+Control plane: on RCCL the 4-word op header (and an upsert's per-rank plan) travels over a gloo
+(host TCP) group of the same ranks, so ranks 1..N-1 learn each op with a host receive that never
+synchronises a GPU stream -- they enqueue op i + 1's collectives while op i's still run.
 Owner assignment is least-loaded-first, so shards stay balanced (the reference's Qdrant has a
 single shard: vector_memory_service/src/main.rs:50).  Global id = rank << 40 | row.
 Payloads (and the point-id -> gid map) live on rank 0 only; other ranks hold vectors only.
@@ -73,6 +80,12 @@ class IndexGroup:
         self.wire_dtype = torch.bfloat16 if info.backend == "nccl" else torch.float32
         # a single-rank process group still runs every collective (RCCL tests on one GPU)
         self.collective = info.world > 1 or info.backend != "none"
+        # the op headers' group: gloo beside RCCL (host-only receive), else the data group itself
+        self.ctrl = group
+        if self.collective and info.backend == "nccl" and group is None:
+            self.ctrl = dist.new_group(backend="gloo")
+        self.ctrl_device = (torch.device("cpu") if self.ctrl is not group
+                            else self.comm_device)
         # per-op collective accounting: {op: [ops, collectives, bytes this rank sent]}
         self.comm_stats: dict[str, list[int]] = {}
         # rank-0 bookkeeping; ops may arrive from several executor threads, but the collective
@@ -101,12 +114,23 @@ class IndexGroup:
         return t
 
     def _header(self, op: int, a: int = 0, b: int = 0) -> torch.Tensor:
-        # pinned + non_blocking: building the header on the GPU must not wait for the stream
-        # (a pageable H2D copy would block the host until the previous search had finished)
+        # (a GPU-resident header -- only when the control group is the data group -- is built
+        # pinned + non_blocking: it must not wait for the stream)
         h = torch.tensor([op, a, b, 0], dtype=torch.int64)
-        if self.comm_device.type == "cuda":
-            h = h.pin_memory().to(self.comm_device, non_blocking=True)
-        return self._bcast(h)
+        if self.ctrl_device.type == "cuda":
+            h = h.pin_memory().to(self.ctrl_device, non_blocking=True)
+        if self.collective:
+            dist.broadcast(h, src=0, group=self.ctrl)
+        return h
+
+    def _scatter(self, out: torch.Tensor, parts, group) -> torch.Tensor:
+        """Rank 0's parts[r] -> rank r's ``out`` (``parts`` None on ranks 1..N-1)."""
+        if self.collective:
+            dist.scatter(out, scatter_list=list(parts) if parts is not None else None, src=0,
+                         group=group)
+        else:
+            out.copy_(parts[0])
+        return out
 
     def _count(self, op: str, collectives: int, nbytes: int) -> None:
         c = self.comm_stats.setdefault(op, [0, 0, 0])
@@ -136,20 +160,26 @@ class IndexGroup:
         allp = allp.view(info.world, nq, k, 2).to(self.shard.device, non_blocking=True)
         return merge_ranked(allp[..., 0].float(), allp[..., 1].long(), k)
 
-    def _do_upsert(self, vecs: torch.Tensor, owner: torch.Tensor, target: torch.Tensor) -> None:
-        """This rank's share of an upsert: new rows appended in one call, overwrites written in
-        one batched scatter (HbmIndexShard.write_rows_f32)."""
-        mine = (owner == self.info.rank).nonzero().flatten()
-        if mine.numel() == 0:
+    def _do_upsert(self, m: int, vparts=None, mparts=None) -> None:
+        """Receive and write this rank's share of an upsert: ``m`` = the largest share (rows);
+        rank 0 passes the per-rank parts (vectors [W, m, D] f32 on the comm device, plan [W,
+        2 + m] int64 on the control device: count, new rows first, then the overwrite targets).
+        New rows are appended in one call, overwrites written in one batched scatter
+        (HbmIndexShard.write_rows_f32)."""
+        plan = self._scatter(torch.empty(2 + m, dtype=torch.int64, device=self.ctrl_device),
+                             mparts, self.ctrl)
+        v = self._scatter(torch.empty(m, self.dim, dtype=torch.float32, device=self.comm_device),
+                          vparts, self.group)
+        p = plan.tolist()   # (host-resident over the gloo control group: no device sync)
+        cnt, n_new = p[0], p[1]
+        if cnt == 0:
             return
-        v = vecs[mine].to(self.shard.device, torch.float32)
-        tg = target[mine]
-        new = (tg < 0).nonzero().flatten()
-        old = (tg >= 0).nonzero().flatten()
-        if new.numel():
-            self.shard.append_f32(v[new.to(v.device)])
-        if old.numel():
-            self.shard.write_rows_f32(tg[old].cpu(), v[old.to(v.device)])
+        v = v[:cnt].to(self.shard.device)
+        if n_new:
+            self.shard.append_f32(v[:n_new])
+        if cnt > n_new:
+            self.shard.write_rows_f32(torch.tensor(p[2 + n_new:2 + cnt], dtype=torch.int64),
+                                      v[n_new:cnt])
 
     def _rank_dir(self, directory: str) -> str:
         return os.path.join(directory, f"rank{self.info.rank}")
@@ -351,10 +381,21 @@ class IndexGroup:
                 owner[i] = r
                 gids.append((r << RANK_SHIFT) | counts[r])
                 counts[r] += 1
-        self._header(OP_UPSERT, n)
-        v = self._bcast(vecs.to(self.comm_device, torch.float32).contiguous())
-        ot = self._bcast(torch.from_numpy(np.stack([owner, target])).to(self.comm_device))
-        self._do_upsert(v, ot[0], ot[1])
+        # per-owner shares, each ordered new rows first (appended in input order) then overwrites
+        W = self.info.world
+        share = [np.concatenate([np.nonzero((owner == r) & (target < 0))[0],
+                                 np.nonzero((owner == r) & (target >= 0))[0]]) for r in range(W)]
+        m = max(1, max(len(x) for x in share))
+        plan = np.zeros((W, 2 + m), np.int64)
+        vsrc = vecs.to(self.comm_device, torch.float32)
+        vparts = torch.zeros(W, m, self.dim, dtype=torch.float32, device=self.comm_device)
+        for r, idx in enumerate(share):
+            plan[r, 0], plan[r, 1] = len(idx), int((target[idx] < 0).sum())
+            plan[r, 2:2 + len(idx)] = target[idx]
+            if len(idx):
+                vparts[r, :len(idx)] = vsrc[torch.from_numpy(idx).to(vsrc.device)]
+        self._header(OP_UPSERT, m)
+        self._do_upsert(m, vparts, torch.from_numpy(plan).to(self.ctrl_device))
         self.counts = counts
         for pid, g, p in zip(point_ids, gids, payloads):
             self.payload_by_gid[g] = (pid, p)
@@ -387,9 +428,7 @@ class IndexGroup:
             q = self._bcast(torch.empty(a, self.dim, dtype=self.wire_dtype, device=self.comm_device))
             self._do_search(q, b)
         elif op == OP_UPSERT:
-            v = self._bcast(torch.empty(a, self.dim, dtype=torch.float32, device=self.comm_device))
-            ot = self._bcast(torch.empty(2, a, dtype=torch.int64, device=self.comm_device))
-            self._do_upsert(v, ot[0], ot[1])
+            self._do_upsert(a)
         elif op in (OP_SNAPSHOT, OP_LOAD):
             if self.snapshot_root is None:
                 raise RuntimeError("index rank has no snapshot directory (SYMB_SNAPSHOT_DIR)")

@@ -105,6 +105,8 @@ int symb_dense_scores(const void* X, int dim, const int* rows, int n_list, int t
                       hipStream_t st);
 int symb_quant_stream_i8(const void* X, int r0, const int* rows, int n, int dim, void* img,
                          float* bounds, hipStream_t st);
+int symb_prefill_candidates(int NQ, int r_lo, int n, int* cand_i, int* cand_n, int cap,
+                            hipStream_t st);
 int symb_quant_stream_mx4(const void* X, int r0, const int* rows, int n, int dim, void* img,
                           void* Xq, void* QS, float* bounds, float* margin, hipStream_t st);
 int symb_quant_stream_mx6(const void* X, int r0, const int* rows, int n, int dim, void* img,
@@ -138,7 +140,6 @@ int symb_prune_qprep(const void* Q, int NQ, int dim, const float* pre_s, const f
                      float thr_margin, const float* bounds, void* Q8, float* sq, float* T,
                      float* thr, hipStream_t st);
 int symb_gemm_lt_config(int mode);
-int symb_gemm_vs_mode(int mode, int bn);
 int symb_mfma_f8f6f4_probe(const int* a, const int* b, const int* sa, const int* sb, float* out,
                            int fmt, hipStream_t st);
 int symb_gemm_lt_plans();
@@ -549,6 +550,12 @@ PYBIND11_MODULE(_hip, m) {
           "quant_stream_i8");
   }, py::arg("X"), py::arg("r0"), py::arg("rows"), py::arg("n"), py::arg("dim"), py::arg("img"),
      py::arg("bounds"), py::arg("stream"));
+  m.def("prefill_candidates", [](int NQ, int r_lo, int n, uptr cand_i, uptr cand_n, int cap,
+                                 uptr st) {
+    check(symb_prefill_candidates(NQ, r_lo, n, P<int>(cand_i), P<int>(cand_n), cap, S(st)),
+          "prefill_candidates");
+  }, py::arg("NQ"), py::arg("r_lo"), py::arg("n"), py::arg("cand_i"), py::arg("cand_n"),
+     py::arg("cap"), py::arg("stream"));
   m.def("quant_stream_mx4", [](uptr X, int r0, uptr rows, int n, int dim, uptr img, uptr Xq,
                                uptr QS, uptr bounds, uptr margin, uptr st) {
     check(symb_quant_stream_mx4(P<void>(X), r0, P<const int>(rows), n, dim, P<void>(img),
@@ -647,8 +654,6 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("Q"), py::arg("NQ"), py::arg("dim"), py::arg("pre_s"), py::arg("tail_s"),
      py::arg("k"), py::arg("thr_margin"), py::arg("bounds"), py::arg("Q8"), py::arg("sq"),
      py::arg("T"), py::arg("thr"), py::arg("stream"));
-  m.def("gemm_vs_config", [](int mode, int bn) { check(symb_gemm_vs_mode(mode, bn), "gemm_vs_config"); },
-        py::arg("mode"), py::arg("bn") = 0);
   m.def("mfma_f8f6f4_probe", [](uptr a, uptr b, uptr sa, uptr sb, uptr out, int fmt, uptr st) {
     check(symb_mfma_f8f6f4_probe(P<const int>(a), P<const int>(b), P<const int>(sa),
                                  P<const int>(sb), P<float>(out), fmt, S(st)),

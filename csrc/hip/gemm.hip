@@ -502,22 +502,6 @@ int symb_gemm_lt_config(int mode) {
   return 0;
 }
 
-// The VGPR-staged 4-wave kernel (gemm_vs.hip, hipBLASLt's geometry) for the wide projections:
-// 0 = off, 1 = auto (K >= 768, N >= 768, M >= 2048), 2 = wherever it supports the shape.  It
-// runs before the hipBLASLt route (off by default: 0.77-0.80x this file's tiles, profiles/r5_gemm/).
-int symb_gemm_vs(int epi, const void* A, int lda, const void* W, int ldw, const float* bias,
-                 const void* R, int ldr, void* C, int ldc, int M, int N, int K, int group_m,
-                 int gelu_poly, hipStream_t st);
-bool symb_gemm_vs_supported(int epi, int M, int N, int K);
-int symb_gemm_vs_config(int bn);
-static int g_vs = 0;
-int symb_gemm_vs_mode(int mode, int bn) {
-  if (mode < 0 || mode > 2) return -1;
-  if (symb_gemm_vs_config(bn) != 0) return -1;
-  g_vs = mode;
-  return 0;
-}
-
 // Small-M split-K path (gemm_skinny.hip): M <= symb_gemm_skinny_max_m() (default 256, the
 // query-path batches) goes there first.
 int symb_gemm_skinny_max_m();
@@ -554,12 +538,6 @@ int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const flo
     return -1;  // wider rows: EPI_RES + symb_add_ln
   }
   if (N % 128 != 0) return -1;
-  if (g_vs && symb_gemm_vs_supported(epi, M, N, K) &&
-      (g_vs == 2 || (K >= 768 && N >= 768 && M >= 2048))) {
-    const int rc = symb_gemm_vs(epi, A, lda, W, ldw, bias, R, ldr, C, ldc, M, N, K, g_group_m,
-                                g_gelu_poly, st);
-    if (rc != -1) return rc;
-  }
   if ((epi == EPI_BIAS || epi == EPI_RES) &&
       (g_gemm_lt == 2 || (g_gemm_lt == 1 && K >= 768 && N >= 768 && M >= 4096))) {
     const int rc = symb_gemm_lt(epi, A, lda, W, ldw, bias, R, ldr, C, ldc, M, N, K, st);

@@ -1308,7 +1308,8 @@ __global__ __launch_bounds__(256) void prune_route_sum_kernel(int NQ, int n_rblk
 // The search statistics of HbmIndexShard.mq_stats in one launch (they were ~10 framework
 // kernels per search): tot[0] += *ovf; tot[1] = max(tot[1], max of cnt[0 .. NQ)); with dense:
 // tot[2] += *dense; with blk too: part = (blk[0] > 0) && !*dense, tot[3] += part,
-// tot[4] += blk[0] * part.  One workgroup; stream order makes the read-modify-writes safe.
+// tot[4] += blk[0] * part.  One workgroup; the updates are device atomics, so searches whose end
+// halves run on different streams (a pipelined loop beside a plain one) never lose a count.
 __global__ __launch_bounds__(256) void prune_stats_kernel(const int* __restrict__ ovf,
                                                           const int* __restrict__ cnt, int NQ,
                                                           const int* __restrict__ dense,
@@ -1324,15 +1325,15 @@ __global__ __launch_bounds__(256) void prune_stats_kernel(const int* __restrict_
   __syncthreads();
   if (tid != 0) return;
   m = max(max(wm[0], wm[1]), max(wm[2], wm[3]));
-  tot[0] += *ovf;
-  tot[1] = max(tot[1], m);
+  atomicAdd(tot + 0, *ovf);
+  atomicMax(tot + 1, m);
   if (dense != nullptr) {
     const int d = *dense;
-    tot[2] += d;
+    atomicAdd(tot + 2, d);
     if (blk != nullptr) {
       const int part = (blk[0] > 0 ? 1 : 0) * (1 - d);
-      tot[3] += part;
-      tot[4] += blk[0] * part;
+      atomicAdd(tot + 3, part);
+      atomicAdd(tot + 4, blk[0] * part);
     }
   }
 }

@@ -29,8 +29,11 @@
 //   MX-fp4: [NKS x 1 KiB, the same byte map over the 192 nibble bytes of a 384-wide row]
 //           [NSC x 256 B: dword j of lane l = the e8m0 scales of k-steps 4 j .. 4 j + 3 (byte
 //            ks % 4) of row l & 31, block 2 ks + (l >> 5)]
-// Each row's bytes depend only on that row (per-row scales), so appending rows into a partly
-// filled sub-tile never rewrites bytes a concurrent scan may be reading.
+// The int8 image keeps ONE scale per sub-tile (SDim::HDR), so an append into a partly filled
+// sub-tile re-quantises the rows already there (and may raise E).  The pruned search therefore
+// scans only whole sub-tiles below its visible count and lists the partial sub-tile's rows as
+// candidates of every query (prepass.hip prefill_candidates; index/shard.py _pruned_end): a scan
+// in flight never reads a sub-tile a concurrent append rewrites.  The MX images are per row.
 #include "scan_common.h"
 
 namespace symb {

@@ -100,9 +100,33 @@ __global__ __launch_bounds__(256) void dense_scores_kernel(const __bf16* __restr
   }
 }
 
+// Every query's candidate list starts as rows [r_lo, r_lo + n) (n < 64): cand_n[q] = n and
+// cand_i[q * cap + j] = r_lo + j (their scores are written by the re-score).  The pruned search
+// lists the rows of a partly filled last 32-row sub-tile this way and its scans stop at the
+// sub-tile boundary: an append into that sub-tile re-quantises its rows under a new shared int8
+// scale, so a scan in flight beside the append must not read it (index/shard.py _pruned_end).
+__global__ __launch_bounds__(256) void prefill_candidates_kernel(int NQ, int r_lo, int n,
+                                                                 int* __restrict__ cand_i,
+                                                                 int* __restrict__ cand_n,
+                                                                 int cap) {
+  const int q = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (q >= NQ) return;
+  if (lane < n) cand_i[(size_t)q * cap + lane] = r_lo + lane;
+  if (lane == 0) cand_n[q] = n;
+}
+
 }  // namespace symb
 
 using namespace symb;
+
+int symb_prefill_candidates(int NQ, int r_lo, int n, int* cand_i, int* cand_n, int cap,
+                            hipStream_t st) {
+  if (NQ <= 0) return 0;
+  if (n < 0 || n >= 64 || n > cap || r_lo < 0) return -1;
+  hipLaunchKernelGGL(prefill_candidates_kernel, dim3((NQ + 3) / 4), dim3(256), 0, st, NQ, r_lo, n,
+                     cand_i, cand_n, cap);
+  return (int)hipGetLastError();
+}
 
 // 32-row tiles per wave of the 384-wide dense scores (query fragments resident across them)
 #ifndef SYMB_DS_TPW

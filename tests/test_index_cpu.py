@@ -665,11 +665,15 @@ def test_mx6_image_follows_writes_and_bounds_every_pair(D, monkeypatch):
     assert bool((m8 < m6).all()) and bool((m6 < m4).all())
 
 
-def test_mx6_tier_defaults():
-    """SYMB_PRUNE_MX6=auto keeps the fp6 image at 384 only (100M x 768 has no HBM left for it)."""
+def test_mx6_tier_defaults(monkeypatch):
+    """SYMB_PRUNE_MX6=auto keeps no fp6 image (measured never to apply, profiles/r5_lq/), so a
+    100M x 384 shard allocates none; SYMB_PRUNE_MX6=1 keeps it at 384 / 768 for A/B runs."""
     a = HbmIndexShard(384, 256, device="cpu", prune="i8")
     b = HbmIndexShard(768, 256, device="cpu", prune="i8")
-    assert a.mx6_on == a.stream and not b.mx6_on
+    assert not a.mx6_on and a.img_mx6 is None and not b.mx6_on
+    monkeypatch.setenv("SYMB_PRUNE_MX6", "1")
+    c = HbmIndexShard(384, 256, device="cpu", prune="i8")
+    assert c.mx6_on == c.stream
 
 
 def test_rwlock_prefers_a_waiting_writer():

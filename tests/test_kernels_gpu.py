@@ -111,35 +111,6 @@ def test_gemm(M, N, K, epi, tile):
     _close(out, ref, atol=4e-2, rtol=2e-2, what=f"gemm epi={epi}")
 
 
-@pytest.mark.parametrize("bn", [0, 256, 192])
-@pytest.mark.parametrize("M,N,K,epi", [
-    (300, 768, 128, 0), (1000, 768, 768, 2), (2049, 2304, 768, 0), (4353, 768, 3072, 2),
-    (777, 3072, 768, 1), (5000, 1024, 4096, 2), (257, 768, 320, 1), (32768, 768, 768, 0),
-    (130, 4608, 1024, 1), (600, 1536, 64, 0),
-])
-def test_gemm_vgpr_staged(M, N, K, epi, bn):
-    """gemm_vs.hip (the wide projections' 4-wave kernel: 128 x 128 / 96 wave tiles, operands
-    staged global -> VGPR -> LDS by buffer loads) == the fp32 oracle on every epilogue, both tile
-    widths, ragged M (rows past M read as zeros through the descriptor), single- and odd-count
-    k-tiles (K = 64, 320)."""
-    from codename_symbiont_amd.ops._ext import hip
-    from codename_symbiont_amd.ops.kernels import gemm
-
-    if bn and N % bn:
-        pytest.skip("tile width does not divide N")
-    hip().gemm_vs_config(2, bn)
-    hip().gemm_skinny_config(0)
-    try:
-        out = gemm(a := _bf(M, K, seed=1), w := _bf(N, K, scale=1.0 / math.sqrt(K), seed=2),
-                   bias := _f(N, scale=0.5, seed=3), epi,
-                   res := (_bf(M, N, seed=4) if epi == 2 else None))
-    finally:
-        hip().gemm_vs_config(0)
-        hip().gemm_skinny_config(256)
-    ref = R.gemm_ref(a, w, bias, epi, res, None, None, 1e-12)
-    _close(out, ref, atol=4e-2, rtol=2e-2, what=f"vgpr-staged gemm bn={bn} epi={epi}")
-
-
 @pytest.mark.parametrize("M,N,K,epi", [(300, 1152, 384, 0), (4100, 768, 3072, 2), (999, 2304, 768, 0),
                                       (77, 1024, 4096, 2)])
 def test_gemm_hipblaslt_route(M, N, K, epi):
@@ -1741,6 +1712,47 @@ def test_pruned_search_split_across_streams_matches_search():
         s1, r1 = shard.search_end(ctx)
     torch.cuda.synchronize()
     assert torch.equal(r0, r1) and torch.equal(s0, s1)
+
+
+def test_pruned_search_append_into_partial_subtile_between_halves():
+    """A shard whose row count is not a multiple of the int8 image's 32-row sub-tile: an append
+    between search_begin and search_end re-quantises that sub-tile under a new (larger) shared
+    scale.  The search must still return exactly what a full bf16 scan of the rows begin saw
+    returns -- including the partial sub-tile's own rows, which self queries must find."""
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+
+    n, k = (1 << 20) + 4011, 10
+    shard = HbmIndexShard(384, n + 1024, prune="i8")
+    shard.fill_random(n, seed=23)
+    ref = HbmIndexShard(384, n, prune=None)
+    ref.rows[:n].copy_(shard.rows[:n])
+    ref.count = ref.visible = n
+    ref.scan_mq = False
+    assert n % 32 != 0
+    # self queries on the partial sub-tile's rows (their best match is themselves), plus held-out
+    q = torch.cat([shard.rows[n - 11:n].clone(),
+                   torch.nn.functional.normalize(_f(245, 384, seed=24), dim=-1).bfloat16()])
+    s0, r0 = ref.search(q, k)
+    # spiky unit rows: one large coordinate each, so the sub-tile's shared scale must grow
+    spike = torch.zeros(64, 384, device=DEV)
+    spike[torch.arange(64), torch.arange(64) * 5] = 1.0
+    spike = (spike + 0.01 * _f(64, 384, seed=25))
+    spike = torch.nn.functional.normalize(spike, dim=-1).bfloat16()
+    a, b = torch.cuda.Stream(), torch.cuda.Stream()
+    a.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(a):
+        ctx = shard.search_begin(q, k)
+        assert "full" not in ctx and ctx["n"] == n
+        shard.append_unit(spike)      # rewrites sub-tile n >> 5 in place
+        done = torch.cuda.Event()
+        done.record(a)
+    b.wait_event(done)
+    with torch.cuda.stream(b):
+        s1, r1 = shard.search_end(ctx)
+    torch.cuda.synchronize()
+    assert (r1[:11, 0] == torch.arange(n - 11, n, device=DEV, dtype=torch.int32)).all()
+    assert torch.equal(r0, r1), "ids differ from the full bf16 scan of the rows begin saw"
+    _close(s1, s0, atol=2e-5, what="partial sub-tile pruned vs exact scores")
 
 
 @pytest.mark.parametrize("k", [1, 10, 17, 64, 100, 128])

@@ -356,9 +356,7 @@ def _dead_rank_worker(rank, world, port, out):
     grp = IndexGroup(info, dim=8, capacity_per_rank=100)
     if rank == 1:
         h = grp._header(0).tolist()          # the UPSERT op runs normally ...
-        v = grp._bcast(torch.empty(h[1], 8))
-        ot = grp._bcast(torch.empty(2, h[1], dtype=torch.int64))
-        grp._do_upsert(v, ot[0], ot[1])
+        grp._do_upsert(h[1])
         grp._header(0)                       # ... then the SEARCH header arrives and the rank dies
         os._exit(3)
     from codename_symbiont_amd.index.shard import Payload
