@@ -159,6 +159,26 @@ class HipEncoder:
                 scales.append(s)
             self._fp8.append((q, scales))      # keep the e4m3 weights and scales alive
             self.rt.add_layer_fp8([q[k].data_ptr() for k in keys] + [s.data_ptr() for s in scales])
+        # deferred LayerNorm for the wide (H >= 768) bf16 encoders (EncoderRuntime's
+        # deferred_forward): the QKV weight folded with the previous layer's ln2 and the FFN1
+        # weight with this layer's ln1 (ops.kernels.fold_ln), so no add_ln pass and no hipBLASLt
+        # projection runs above the small-M limit.  SYMB_DEFERRED_LN=0: the add_ln path (A/B).
+        self._folds = []
+        if precision == "bf16" and cfg.hidden != 384 and cfg.hidden % 64 == 0:
+            import os
+
+            from ..ops.kernels import fold_ln
+
+            for li, L in enumerate(p["layers"]):
+                fq = (None, None, None)
+                if li > 0:
+                    prev = p["layers"][li - 1]
+                    fq = fold_ln(L["wqkv"], L["bqkv"], prev["ln2_g"], prev["ln2_b"])
+                fi = fold_ln(L["wi"], L["bi"], L["ln1_g"], L["ln1_b"])
+                self._folds.append((fq, fi))
+                self.rt.set_fold(li, [0 if t is None else t.data_ptr() for t in fq + fi])
+            self.rt.set_deferred_ln(0 if os.environ.get("SYMB_DEFERRED_LN", "1") in ("", "0")
+                                    else 1)
         self._ws_tokens = 0
         self._ws: list[torch.Tensor] = []
 

@@ -12,7 +12,56 @@ import torch
 from ._ext import hip, stream_handle
 
 EPI_BIAS, EPI_GELU, EPI_RES, EPI_RES_LN = 0, 1, 2, 3
+LNF_FOLD, LNF_RESLN, LNF_STATS = 1, 2, 4    # deferred-LayerNorm epilogue modes (gemm.hip)
 SUPPORTED_H = (384, 768, 1024)
+
+
+def fold_ln(w: torch.Tensor, b: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor):
+    """Fold a LayerNorm that precedes a linear layer into it (the deferred LayerNorm, gemm.hip
+    LNF_FOLD): LN(y) W^T + b = rstd (y W'^T - mean cs) + b' with W' = W o gamma (bf16 [N, K]),
+    cs = rowsum(W') (f32 [N], from the rounded W'), b' = b + W beta (f32 [N])."""
+    wf = w.float()
+    wg = (wf * gamma.float()[None, :]).to(torch.bfloat16).contiguous()
+    cs = wg.float().sum(1).contiguous()
+    bf = (b.float() + wf @ beta.float()).contiguous()
+    return wg, bf, cs
+
+
+def gemm_ln(a, w, bias, epi, lnf, residual=None, gamma=None, beta=None, ln_eps=1e-12, cs=None,
+            st_in=None, st_out=None, out=None):
+    """Deferred-LayerNorm GEMM (gemm.hip symb_gemm_ln): st_in / st_out are float32 [M, N / 64, 2]
+    row-statistics partials (chunk mean, squared deviations); see gemm_bf16_kernel's LNF modes."""
+    _chk(a, torch.bfloat16, "a", 2)
+    _chk(w, torch.bfloat16, "w", 2)
+    _chk(bias, torch.float32, "bias", 1)
+    M, K = a.shape
+    N = w.shape[0]
+    if w.shape[1] != K or bias.numel() != N or K % 64 or N % 128:
+        raise ValueError("gemm_ln: shapes")
+    np_in = 0
+    if lnf & (LNF_FOLD | LNF_RESLN):
+        _chk(st_in, torch.float32, "st_in", 3)
+        if st_in.shape[0] != M or st_in.shape[2] != 2:
+            raise ValueError("st_in: [M, np, 2]")
+        np_in = st_in.shape[1]
+    if lnf & LNF_FOLD:
+        _chk(cs, torch.float32, "cs", 1)
+        if cs.numel() != N:
+            raise ValueError("cs: [N]")
+    if lnf & LNF_RESLN or epi == EPI_RES:
+        _chk(residual, torch.bfloat16, "residual", 2)
+        if residual.shape != (M, N):
+            raise ValueError("residual: [M, N]")
+    if lnf & LNF_STATS:
+        _chk(st_out, torch.float32, "st_out", 3)
+        if st_out.shape != (M, N // 64, 2):
+            raise ValueError("st_out: [M, N / 64, 2]")
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
+    hip().gemm_ln(epi, lnf, _ptr(a), K, _ptr(w), K, _ptr(bias), _ptr(residual), N, _ptr(gamma),
+                  _ptr(beta), float(ln_eps), _ptr(cs), _ptr(st_in), np_in, _ptr(st_out), _ptr(out),
+                  N, M, N, K, stream_handle())
+    return out
 
 
 def _ptr(t: torch.Tensor | None) -> int:

@@ -37,6 +37,15 @@ def gemm_ref(a, w, bias, epi=0, residual=None, gamma=None, beta=None, eps=1e-12)
     return y
 
 
+def ln_chunk_stats_ref(y: torch.Tensor, chunk: int = 64) -> torch.Tensor:
+    """Per-row partial statistics of y [M, N] over `chunk`-column chunks: [M, N / chunk, 2] of
+    (chunk mean, sum of squared deviations from it) in fp32 -- the deferred LayerNorm's LNF_STATS
+    output (gemm.hip)."""
+    yc = y.float().view(y.shape[0], -1, chunk)
+    m = yc.mean(-1)
+    return torch.stack([m, ((yc - m[..., None]) ** 2).sum(-1)], -1)
+
+
 def attention_ref(qkv, cu_seqlens, n_heads, head_dim):
     """Varlen bidirectional attention over packed [T, 3H] rows -> [T, H] (fp32)."""
     H = n_heads * head_dim

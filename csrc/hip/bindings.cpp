@@ -28,7 +28,12 @@ int symb_add_ln(const void* x, const void* res, const float* g, const float* b, 
                 void* out, int T, int H, hipStream_t st, void* out8 = nullptr,
                 float* scale8 = nullptr);
 int symb_pool(const void* hidden, const int32_t* cu, int B, int H, int mode, int normalize_f32,
-              float* out_f32, void* out_norm, hipStream_t st);
+              float* out_f32, void* out_norm, hipStream_t st, const float* gamma = nullptr,
+              const float* beta = nullptr, float eps = 0.f);
+int symb_gemm_ln(int epi, int lnf, const void* A, int lda, const void* W, int ldw,
+                 const float* bias, const void* R, int ldr, const float* gamma, const float* beta,
+                 float ln_eps, const float* cs, const void* st_in, int np_in, void* st_out,
+                 void* C, int ldc, int M, int N, int K, hipStream_t st);
 int symb_l2norm_cast(const float* x, void* out, int n, int D, int ld_out, hipStream_t st);
 int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const float* bias,
               const void* R, int ldr, const float* gamma, const float* beta, float eps, void* C,
@@ -200,6 +205,11 @@ struct LayerWeights {
   // channel scales (f32 [N]); activations are quantised per token right before each GEMM
   bool fp8 = false;
   uptr sw_qkv = 0, sw_o = 0, sw_i = 0, sw_o2 = 0;
+  // deferred LayerNorm (set_fold): the QKV weight folded with the PREVIOUS layer's ln2 gamma and
+  // the FFN1 weight folded with this layer's ln1 gamma, their biases b + W beta and the folded
+  // weights' row sums (0 for layer 0's QKV, whose input the embedding LayerNorm normalised)
+  uptr fq_w = 0, fq_b = 0, fq_cs = 0, fi_w = 0, fi_b = 0, fi_cs = 0;
+  bool folded = false;
 };
 
 class EncoderRuntime {
@@ -228,6 +238,27 @@ class EncoderRuntime {
     any_fp8_ = true;
   }
   int num_layers() const { return (int)layers_.size(); }
+  // The deferred-LayerNorm operands of bf16 layer li (gemm.hip LNF): pointers 0 for layer 0's QKV.
+  void set_fold(int li, const std::vector<uptr>& w) {
+    if (li < 0 || li >= (int)layers_.size() || w.size() != 6)
+      throw std::invalid_argument("set_fold: layer index and 6 pointers");
+    auto& L = layers_[li];
+    if (L.fp8) throw std::invalid_argument("set_fold: bf16 layers only");
+    if ((li == 0) != (w[0] == 0)) throw std::invalid_argument("set_fold: QKV fold from layer 1 on");
+    L.fq_w = w[0]; L.fq_b = w[1]; L.fq_cs = w[2]; L.fi_w = w[3]; L.fi_b = w[4]; L.fi_cs = w[5];
+    L.folded = true;
+  }
+  // 0 = the add_ln path for wide rows, 1 = deferred LayerNorm where every layer is folded
+  void set_deferred_ln(int mode) {
+    if (mode != 0 && mode != 1) throw std::invalid_argument("deferred_ln: 0 or 1");
+    deferred_ln_ = mode;
+  }
+  bool deferred_ln_ready() const {
+    if (layers_.empty()) return false;
+    for (const auto& L : layers_)
+      if (L.fp8 || !L.folded) return false;
+    return true;
+  }
 
   // Split-partial buffer the bf16 layers' small-M (query-path) GEMMs need: skinny_ws_bytes().
   size_t skinny_ws_bytes() const {
@@ -269,6 +300,10 @@ class EncoderRuntime {
                          (ws_in.size() > base && T <= symb_gemm_skinny_max_m() &&
                           symb_gemm_skinny_scratch_bytes(EPI_RES_LN, T, H, H) > 0 &&
                           symb_gemm_skinny_scratch_bytes(EPI_RES_LN, T, H, FF_) > 0);
+    if (!fuse_ln && H % 64 == 0 && deferred_ln_ && deferred_ln_ready()) {
+      deferred_forward(ws, T, B, max_len, cu, st, pool_mode, normalize_f32, out_f32, out_norm);
+      return;
+    }
     bool h_quantized = false;  // a8/sa hold the per-token e4m3 image of h (fp8 layers)
     for (size_t li = 0; li < layers_.size(); ++li) {
       const auto& L = layers_[li];
@@ -332,6 +367,69 @@ class EncoderRuntime {
   }
 
  private:
+  // Deferred-LayerNorm forward (bf16 layers at H >= 768, above the small-M limit): no add_ln pass
+  // and no hipBLASLt.  Per layer, with y2 = the previous layer's pre-LN output in h (layer 0: the
+  // embedding LayerNorm's normalised output) and its row statistics in s2:
+  //   qkv = LN2(y2) Wqkv^T + b       QKV GEMM on the folded weight, LNF_FOLD epilogue (s2)
+  //   y1  = ctx Wo^T + bo + LN2(y2)  out-proj, LNF_RESLN | LNF_STATS epilogue (reads s2, writes s1)
+  //   ff  = GELU(LN1(y1) W1^T + b1)  FFN1 on the folded weight, LNF_FOLD epilogue (s1)
+  //   y2' = ff W2^T + b2 + LN1(y1)   FFN2, LNF_RESLN | LNF_STATS epilogue (reads s1, writes s2)
+  // and the pool kernel applies the last ln2 to every token row before pooling.
+  void deferred_forward(const std::vector<uptr>& ws, int T, int B, int max_len, uptr cu,
+                        hipStream_t st, int pool_mode, int normalize_f32, uptr out_f32,
+                        uptr out_norm) {
+    const int H = H_, NP = H / 64;
+    uptr h = ws[0], y1 = ws[1], qkv = ws[2], ctx = ws[3], ff = ws[4];
+    // the row statistics live in the add_ln path's tmp buffer (T x H bf16 = 2 T H bytes; the two
+    // float2 [T][H / 64] sets need T H / 4)
+    void* s1 = P<void>(ws[5]);
+    void* s2 = P<void>(ws[5] + (uptr)T * NP * 8);
+    const float *g2 = nullptr, *b2 = nullptr;   // the previous layer's ln2 (h is pre-LN)
+    for (size_t li = 0; li < layers_.size(); ++li) {
+      const auto& L = layers_[li];
+      const bool pre = li > 0;
+      if (pre)
+        check(symb_gemm_ln(EPI_BIAS, 1, P<void>(h), H, P<void>(L.fq_w), H, P<float>(L.fq_b),
+                           nullptr, 0, nullptr, nullptr, eps_, P<float>(L.fq_cs), s2, NP, nullptr,
+                           P<void>(qkv), 3 * H, T, 3 * H, H, st),
+              "qkv gemm (folded ln2)");
+      else
+        check(symb_gemm_ln_plain(EPI_BIAS, h, L.wqkv, L.bqkv, 0, qkv, T, 3 * H, H, st),
+              "qkv gemm");
+      check(symb_attention(P<void>(qkv), 3 * H, P<int32_t>(cu), B, max_len, nh_, hd_,
+                           P<void>(ctx), H, st),
+            "attention");
+      check(symb_gemm_ln(EPI_RES, pre ? 2 | 4 : 4, P<void>(ctx), H, P<void>(L.wo), H,
+                         P<float>(L.bo), P<void>(h), H, g2, b2, eps_, nullptr, pre ? s2 : nullptr,
+                         NP, s1, P<void>(y1), H, T, H, H, st),
+            "out-proj gemm (+ln2, stats)");
+      check(symb_gemm_ln(EPI_GELU, 1, P<void>(y1), H, P<void>(L.fi_w), H, P<float>(L.fi_b),
+                         nullptr, 0, nullptr, nullptr, eps_, P<float>(L.fi_cs), s1, NP, nullptr,
+                         P<void>(ff), FF_, T, FF_, H, st),
+            "ffn1 gemm (folded ln1)");
+      check(symb_gemm_ln(EPI_RES, 2 | 4, P<void>(ff), FF_, P<void>(L.wo2), FF_, P<float>(L.bo2),
+                         P<void>(y1), H, P<float>(L.ln1_g), P<float>(L.ln1_b), eps_, nullptr, s1,
+                         NP, s2, P<void>(h), H, T, H, FF_, st),
+            "ffn2 gemm (+ln1, stats)");
+      g2 = P<float>(L.ln2_g);
+      b2 = P<float>(L.ln2_b);
+    }
+    if (out_f32)
+      check(symb_pool(P<void>(h), P<int32_t>(cu), B, H, pool_mode, normalize_f32, P<float>(out_f32),
+                      P<void>(out_norm), st, g2, b2, eps_),
+            "pool (+ln2)");
+    else   // token states requested: normalise h in place (one pass, last layer only)
+      check(symb_add_ln(P<void>(h), nullptr, g2, b2, eps_, P<void>(h), T, H, st), "final ln2");
+  }
+
+  // plain bias GEMM on this repo's tiles (layer 0's QKV of the deferred forward: never hipBLASLt)
+  static int symb_gemm_ln_plain(int epi, uptr A, uptr W, uptr b, uptr R, uptr C, int M, int N,
+                                int K, hipStream_t st) {
+    (void)R;
+    return symb_gemm_ln(epi, 0, P<void>(A), K, P<void>(W), K, P<float>(b), nullptr, 0, nullptr,
+                        nullptr, 0.f, nullptr, nullptr, 0, nullptr, P<void>(C), N, M, N, K, st);
+  }
+
   // e4m3 layer: every projection is an fp8 MFMA GEMM with its scales folded into the epilogue.
   // Activation hand-offs (no separate quantiser pass inside a run of fp8 layers):
   //   h   --(previous layer's ln2, fused per-token quant, or quant_rows here)--> QKV
@@ -383,6 +481,7 @@ class EncoderRuntime {
   }
 
   bool any_fp8_ = false;
+  int deferred_ln_ = 1;
   int H_, nh_, hd_, FF_;
   float eps_;
   uptr wemb_, pemb_, temb_, eln_g_, eln_b_;
@@ -419,11 +518,13 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("x"), py::arg("res"), py::arg("g"), py::arg("b"), py::arg("eps"), py::arg("out"),
      py::arg("T"), py::arg("H"), py::arg("st"), py::arg("out8") = 0, py::arg("scale8") = 0);
   m.def("pool", [](uptr hidden, uptr cu, int B, int H, int mode, int normalize_f32, uptr out_f32,
-                   uptr out_norm, uptr st) {
+                   uptr out_norm, uptr st, uptr g, uptr b, float eps) {
     check(symb_pool(P<void>(hidden), P<int32_t>(cu), B, H, mode, normalize_f32, P<float>(out_f32),
-                    P<void>(out_norm), S(st)),
+                    P<void>(out_norm), S(st), P<float>(g), P<float>(b), eps),
           "pool");
-  });
+  }, py::arg("hidden"), py::arg("cu"), py::arg("B"), py::arg("H"), py::arg("mode"),
+     py::arg("normalize_f32"), py::arg("out_f32"), py::arg("out_norm"), py::arg("st"),
+     py::arg("g") = 0, py::arg("b") = 0, py::arg("eps") = 0.f);
   m.def("l2norm_cast", [](uptr x, uptr out, int n, int D, int ld_out, uptr st) {
     check(symb_l2norm_cast(P<float>(x), P<void>(out), n, D, ld_out, S(st)), "l2norm_cast");
   });
@@ -432,6 +533,14 @@ PYBIND11_MODULE(_hip, m) {
     check(symb_gemm(epi, P<void>(A), lda, P<void>(W), ldw, P<float>(bias), P<void>(R), ldr,
                     P<float>(g), P<float>(b), eps, P<void>(C), ldc, M, N, K, S(st)),
           "gemm");
+  });
+  m.def("gemm_ln", [](int epi, int lnf, uptr A, int lda, uptr W, int ldw, uptr bias, uptr R,
+                      int ldr, uptr g, uptr b, float ln_eps, uptr cs, uptr st_in, int np_in,
+                      uptr st_out, uptr C, int ldc, int M, int N, int K, uptr st) {
+    check(symb_gemm_ln(epi, lnf, P<void>(A), lda, P<void>(W), ldw, P<float>(bias), P<void>(R), ldr,
+                       P<float>(g), P<float>(b), ln_eps, P<float>(cs), P<void>(st_in), np_in,
+                       P<void>(st_out), P<void>(C), ldc, M, N, K, S(st)),
+          "gemm_ln");
   });
   m.def("attention", [](uptr qkv, int ld_qkv, uptr cu, int B, int max_len, int n_heads,
                         int head_dim, uptr out, int ld_out, uptr st, uptr oscale) {
@@ -801,5 +910,8 @@ PYBIND11_MODULE(_hip, m) {
       .def("add_layer_fp8", &EncoderRuntime::add_layer_fp8)
       .def("num_layers", &EncoderRuntime::num_layers)
       .def("skinny_ws_bytes", &EncoderRuntime::skinny_ws_bytes)
+      .def("set_fold", &EncoderRuntime::set_fold)
+      .def("set_deferred_ln", &EncoderRuntime::set_deferred_ln)
+      .def("deferred_ln_ready", &EncoderRuntime::deferred_ln_ready)
       .def("forward", &EncoderRuntime::forward);
 }

@@ -74,15 +74,40 @@ __device__ __forceinline__ int2 pack_e4m3x8(const float (&y)[8], int ex) {
 // EPI_GELU_MX8 (F8 only): GELU(+ bias) emitted as MX fp8 -- e4m3 bytes in C plus one E8M0 scale
 // per 32 output columns in cscale -- which is the A operand format AMX consumes.  The FFN1 -> FFN2
 // hand-off then needs no separate quantiser pass over the 4H-wide activation.
+//
+// Deferred LayerNorm (LNF, bf16 only; the H >= 768 encoders -- VERDICT r5 item 1).  A post-LN
+// BERT layer normalises every residual sum y = x + f(x) before two consumers read it: the next
+// projection (as its A operand) and the next residual add.  Rather than a separate pass that
+// reads y and writes LN(y) (add_ln, twice per layer), the producer's epilogue also writes
+// per-row partial statistics of the y it stores, and the consumers normalise algebraically:
+//   LNF_STATS : the epilogue writes, per row and 64-column chunk of its output, (chunk mean,
+//               sum of squared deviations from it) as float2 into st_out [M][N / 64] -- from the
+//               bf16-rounded values it stores, so the statistics describe exactly the tensor the
+//               consumers read.
+//   LNF_FOLD  : A is a pre-LN y with statistics st_in [M][np_in].  Since
+//                 LN(y) W^T + b = rstd (y (W o gamma)^T - mean cs) + (b + W beta),
+//               cs = rowsum(W o gamma), the kernel runs on the folded weight W o gamma and the
+//               epilogue applies rstd (acc - mean cs[n]) + b'[n] (b' = b + W beta: `bias`).
+//   LNF_RESLN : the residual R is a pre-LN y with statistics st_in: the epilogue adds
+//               (R - mean) rstd gamma + beta instead of R.
+// Row statistics combine the np_in chunk partials (Chan et al.'s pairwise update) once per tile
+// row into LDS; ln_eps is the LayerNorm epsilon.
+enum { LNF_FOLD = 1, LNF_RESLN = 2, LNF_STATS = 4 };
+
 template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, int NSTAGE = 2, bool F8 = false,
-          bool AMX = false>
+          bool AMX = false, int LNF = 0>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
     const void* __restrict__ Av, int lda, const void* __restrict__ Wv, int ldw,
     const float* __restrict__ bias, const __bf16* __restrict__ R, int ldr,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
     __bf16* __restrict__ C, int ldc, int M, int N, int K, const float* __restrict__ sa,
     const float* __restrict__ sw, int group_m, const uint8_t* __restrict__ ascale,
-    uint8_t* __restrict__ cscale) {
+    uint8_t* __restrict__ cscale, const float2* __restrict__ st_in, int np_in,
+    const float* __restrict__ cs, float2* __restrict__ st_out, float ln_eps) {
+  static_assert(LNF == 0 || (!F8 && EPI != EPI_RES_LN && EPI != EPI_GELU_MX8), "deferred LN: bf16");
+  static_assert(!(LNF & LNF_FOLD) || !(LNF & LNF_RESLN), "one statistics input per kernel");
+  static_assert(!(LNF & LNF_RESLN) || EPI == EPI_RES, "a normalised residual needs EPI_RES");
+  static_assert(!(LNF & LNF_STATS) || BN % 64 == 0, "statistics chunks of 64 columns");
   static_assert(!AMX || (F8 && NSTAGE == 2), "MX activations are an fp8 2-stage mode");
   static_assert(NSTAGE >= 2 && NSTAGE <= 4, "LDS ring depth");
   static_assert(EPI != EPI_GELU_MX8 || (F8 && BN % 32 == 0), "MX output is an fp8 mode");
@@ -310,11 +335,29 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
   // one wave-row band per pass.
   constexpr int CS = BN + 4;
   constexpr int PROWS = BM / EPI_PASSES;
+  constexpr bool NEED_RS = (LNF & (LNF_FOLD | LNF_RESLN)) != 0;
   float* Cs = reinterpret_cast<float*>(smem);
+  // this pass's row statistics (mean, rstd) for LNF_FOLD / LNF_RESLN, after the fp32 tile
+  float2* rs = reinterpret_cast<float2*>(smem + PROWS * CS * 4);
   __syncthreads();
 #pragma unroll 1
   for (int p = 0; p < EPI_PASSES; ++p) {
     const int band0 = m0 + p * PROWS;  // first global row of this pass
+    if constexpr (NEED_RS) {
+      for (int t = tid; t < PROWS; t += NT) {
+        const float2* sp = st_in + (size_t)min(band0 + t, M - 1) * np_in;
+        float msum = 0.f;
+        for (int i = 0; i < np_in; ++i) msum += sp[i].x;
+        const float mean = msum / (float)np_in;
+        float m2 = 0.f;
+        for (int i = 0; i < np_in; ++i) {
+          const float2 v = sp[i];
+          const float d = v.x - mean;
+          m2 += v.y + 64.f * d * d;
+        }
+        rs[t] = make_float2(mean, rsqrtf(m2 / (64.f * (float)np_in) + ln_eps));
+      }
+    }
     if (EPI_PASSES == 1 || wm == p) {
 #pragma unroll
       for (int i = 0; i < RM; ++i)
@@ -346,10 +389,21 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
         const f32x4 b0 = *reinterpret_cast<const f32x4*>(bias + n0 + c8);
         const f32x4 b1 = *reinterpret_cast<const f32x4*>(bias + n0 + c8 + 4);
         float y[8];
+        if constexpr ((LNF & LNF_FOLD) != 0) {
+          const float2 st = rs[row];
+          const f32x4 c0 = *reinterpret_cast<const f32x4*>(cs + n0 + c8);
+          const f32x4 c1 = *reinterpret_cast<const f32x4*>(cs + n0 + c8 + 4);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          y[e] = x0[e] + b0[e];
-          y[e + 4] = x1[e] + b1[e];
+          for (int e = 0; e < 4; ++e) {
+            y[e] = st.y * (x0[e] - st.x * c0[e]) + b0[e];
+            y[e + 4] = st.y * (x1[e] - st.x * c1[e]) + b1[e];
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            y[e] = x0[e] + b0[e];
+            y[e + 4] = x1[e] + b1[e];
+          }
         }
         if constexpr (EPI == EPI_GELU || EPI == EPI_GELU_MX8) {
           if (eps != 0.f) {   // GELU epilogues take eps (LayerNorm-only) as the form switch
@@ -375,8 +429,34 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
         if constexpr (EPI == EPI_RES) {
           float r[8];
           load8(R + (size_t)grow * ldr + n0 + c8, r);
+          if constexpr ((LNF & LNF_RESLN) != 0) {
+            const float2 st = rs[row];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) y[e] += r[e];
+            for (int e = 0; e < 8; ++e)
+              y[e] += (r[e] - st.x) * st.y * gamma[n0 + c8 + e] + beta[n0 + c8 + e];
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) y[e] += r[e];
+          }
+        }
+        if constexpr ((LNF & LNF_STATS) != 0) {
+          // the 8 lanes (tid & 7) of this row's 64-column chunk: statistics of the stored values
+#pragma unroll
+          for (int e = 0; e < 8; ++e) y[e] = (float)(__bf16)y[e];
+          float sm = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) sm += y[e];
+          sm += __shfl_xor(sm, 1, 64);
+          sm += __shfl_xor(sm, 2, 64);
+          sm += __shfl_xor(sm, 4, 64);
+          const float mc = sm * (1.f / 64.f);
+          float d2 = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) d2 += (y[e] - mc) * (y[e] - mc);
+          d2 += __shfl_xor(d2, 1, 64);
+          d2 += __shfl_xor(d2, 2, 64);
+          d2 += __shfl_xor(d2, 4, 64);
+          if ((tid & 7) == 0) st_out[(size_t)grow * (N / 64) + (n0 + c8) / 64] = make_float2(mc, d2);
         }
         store8(C + (size_t)grow * ldc + n0 + c8, y);
       }
@@ -397,22 +477,36 @@ static int g_fp8_waves = 8;
 // 123.9 us (bias-only epilogue: 40.3 / 111.4), same max error vs the fp32 oracle (bf16-bound).
 static int g_gelu_poly = 1;
 
+// Deferred-LayerNorm operands of a launch (LNF kernels; see gemm_bf16_kernel).
+struct LnArgs {
+  const float2* st_in = nullptr;
+  int np_in = 0;
+  const float* cs = nullptr;
+  float2* st_out = nullptr;
+  float ln_eps = 0.f;
+};
+
 template <int BM, int BN, int WM, int WN, int EPI, int NSTAGE = 2, bool F8 = false,
-          bool AMX = false>
+          bool AMX = false, int LNF = 0>
 static int launch_cfg(const void* A, int lda, const void* W, int ldw, const float* bias,
                       const __bf16* R, int ldr, const float* g, const float* b, float eps,
                       __bf16* C, int ldc, int M, int N, int K, hipStream_t st,
                       const float* sa = nullptr, const float* sw = nullptr,
-                      const uint8_t* ascale = nullptr, uint8_t* cscale = nullptr) {
-  auto kern = gemm_bf16_kernel<BM, BN, WM, WN, EPI, NSTAGE, F8, AMX>;
+                      const uint8_t* ascale = nullptr, uint8_t* cscale = nullptr,
+                      const LnArgs& ln = LnArgs()) {
+  auto kern = gemm_bf16_kernel<BM, BN, WM, WN, EPI, NSTAGE, F8, AMX, LNF>;
   constexpr int main_bytes = NSTAGE * ((BM + BN) * 128 + (AMX ? BM * 4 : 0));
   constexpr int full_epi = BM * (BN + 4) * 4;
-  constexpr int epi_bytes = full_epi > 160 * 1024 ? (BM / WM) * (BN + 4) * 4 : full_epi;
+  constexpr int passes = full_epi > 160 * 1024 ? WM : 1;
+  constexpr int epi_bytes = (BM / passes) * (BN + 4) * 4 +
+                            ((LNF & (LNF_FOLD | LNF_RESLN)) ? (BM / passes) * 8 : 0);
   constexpr int lds = main_bytes > epi_bytes ? main_bytes : epi_bytes;
-  set_max_lds<gemm_bf16_kernel<BM, BN, WM, WN, EPI, NSTAGE, F8, AMX>>(lds);
+  static_assert(lds <= 160 * 1024, "LDS");
+  set_max_lds<gemm_bf16_kernel<BM, BN, WM, WN, EPI, NSTAGE, F8, AMX, LNF>>(lds);
   const int nwg = ((M + BM - 1) / BM) * (N / BN);
   hipLaunchKernelGGL(kern, dim3(nwg), dim3(64 * WM * WN), lds, st, A, lda, W, ldw, bias, R, ldr,
-                     g, b, eps, C, ldc, M, N, K, sa, sw, g_group_m, ascale, cscale);
+                     g, b, eps, C, ldc, M, N, K, sa, sw, g_group_m, ascale, cscale, ln.st_in,
+                     ln.np_in, ln.cs, ln.st_out, ln.ln_eps);
   return (int)hipGetLastError();
 }
 
@@ -590,6 +684,77 @@ int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const flo
       return launch_cfg<128, 128, 2, 2, EPI_RES>(a, lda, w, ldw, bias, r, ldr, gamma, beta, eps, c,
                                                  ldc, M, N, K, st);
   }
+  return -1;
+}
+
+// Deferred-LayerNorm GEMMs (gemm_bf16_kernel's LNF modes) on the same tiles symb_gemm picks for
+// the shape (never hipBLASLt or the small-M path): lnf = LNF_FOLD with EPI_BIAS / EPI_GELU (A a
+// pre-LN y, W the gamma-folded weight, bias b' = b + W beta, cs = rowsum of the folded weight),
+// LNF_STATS with EPI_RES (the residual R already normalised), LNF_RESLN | LNF_STATS with EPI_RES
+// (R a pre-LN y normalised on the fly with gamma / beta).  st_in: float2 [M][np_in] partials of
+// the pre-LN input; st_out: float2 [M][N / 64] partials of C.
+template <int EPI, int LNF>
+static int launch_ln(int bn, bool small, const void* A, int lda, const void* W, int ldw,
+                     const float* bias, const __bf16* R, int ldr, const float* g, const float* b,
+                     float eps, __bf16* C, int ldc, int M, int N, int K, hipStream_t st,
+                     const LnArgs& ln) {
+  if (bn == 256)
+    return launch_cfg<256, 256, 2, 4, EPI, 2, false, false, LNF>(A, lda, W, ldw, bias, R, ldr, g, b,
+                                                                 eps, C, ldc, M, N, K, st, nullptr,
+                                                                 nullptr, nullptr, nullptr, ln);
+  if (bn == 192)
+    return launch_cfg<256, 192, 2, 4, EPI, 2, false, false, LNF>(A, lda, W, ldw, bias, R, ldr, g, b,
+                                                                 eps, C, ldc, M, N, K, st, nullptr,
+                                                                 nullptr, nullptr, nullptr, ln);
+  if (small)
+    return launch_cfg<128, 128, 2, 4, EPI, 4, false, false, LNF>(A, lda, W, ldw, bias, R, ldr, g, b,
+                                                                 eps, C, ldc, M, N, K, st, nullptr,
+                                                                 nullptr, nullptr, nullptr, ln);
+  return launch_cfg<128, 128, 2, 4, EPI, 2, false, false, LNF>(A, lda, W, ldw, bias, R, ldr, g, b,
+                                                               eps, C, ldc, M, N, K, st, nullptr,
+                                                               nullptr, nullptr, nullptr, ln);
+}
+
+int symb_gemm_ln(int epi, int lnf, const void* A, int lda, const void* W, int ldw,
+                 const float* bias, const void* R, int ldr, const float* gamma, const float* beta,
+                 float ln_eps, const float* cs, const void* st_in, int np_in, void* st_out,
+                 void* C, int ldc, int M, int N, int K, hipStream_t st) {
+  if (M <= 0) return 0;
+  if (K % GEMM_BK != 0 || N % 128 != 0) return -1;
+  const bool fold = lnf & LNF_FOLD, resln = lnf & LNF_RESLN, stats = lnf & LNF_STATS;
+  if ((fold || resln) && (st_in == nullptr || np_in < 1 || np_in > 64)) return -1;
+  if (fold && cs == nullptr) return -1;
+  if (resln && (gamma == nullptr || beta == nullptr || R == nullptr)) return -1;
+  if (stats && st_out == nullptr) return -1;
+  LnArgs ln;
+  ln.st_in = (const float2*)st_in;
+  ln.np_in = np_in;
+  ln.cs = cs;
+  ln.st_out = (float2*)st_out;
+  ln.ln_eps = ln_eps;
+  // the tile symb_gemm's auto rule (g_tile 3) picks for the shape
+  const int bn = big_tile_bn(3, M, N, K);
+  const bool small = !bn && ((M + 127) / 128) * (N / 128) < 256;
+  auto a = (const __bf16*)A;
+  auto w = (const __bf16*)W;
+  auto r = (const __bf16*)R;
+  auto c = (__bf16*)C;
+  const float geps = g_gelu_poly ? 1.f : 0.f;   // the GELU epilogue's form switch
+  if (epi == EPI_BIAS && lnf == 0)
+    return launch_ln<EPI_BIAS, 0>(bn, small, a, lda, w, ldw, bias, r, ldr, gamma, beta, 0.f, c, ldc,
+                                  M, N, K, st, ln);
+  if (epi == EPI_BIAS && lnf == LNF_FOLD)
+    return launch_ln<EPI_BIAS, LNF_FOLD>(bn, small, a, lda, w, ldw, bias, r, ldr, gamma, beta, 0.f,
+                                         c, ldc, M, N, K, st, ln);
+  if (epi == EPI_GELU && lnf == LNF_FOLD)
+    return launch_ln<EPI_GELU, LNF_FOLD>(bn, small, a, lda, w, ldw, bias, r, ldr, gamma, beta, geps,
+                                         c, ldc, M, N, K, st, ln);
+  if (epi == EPI_RES && lnf == LNF_STATS)
+    return launch_ln<EPI_RES, LNF_STATS>(bn, small, a, lda, w, ldw, bias, r, ldr, gamma, beta, 0.f,
+                                         c, ldc, M, N, K, st, ln);
+  if (epi == EPI_RES && lnf == (LNF_RESLN | LNF_STATS))
+    return launch_ln<EPI_RES, LNF_RESLN | LNF_STATS>(bn, small, a, lda, w, ldw, bias, r, ldr, gamma,
+                                                     beta, 0.f, c, ldc, M, N, K, st, ln);
   return -1;
 }
 

@@ -170,13 +170,18 @@ __global__ __launch_bounds__(256) void add_ln_kernel(
 //   mode 0 = masked mean (reference: sum / (count + 1e-9)), mode 1 = CLS (first token).
 //   out_f32  : [B,H] pooled (un-normalised, what the wire format carries)
 //   out_norm : [B,H] bf16 L2-normalised copy (what the HBM index / query path consumes), optional
+//   gamma / beta (optional): `hidden` is the last layer's PRE-LayerNorm residual sum (the deferred
+//            LayerNorm of the H >= 768 encoders, gemm.hip LNF): every token row is normalised
+//            here, from its own values (the wave holds the whole row), before it is pooled.
 // ---------------------------------------------------------------------------------------------
 template <int H>
 __global__ __launch_bounds__(256) void pool_kernel(const __bf16* __restrict__ hidden,
                                                    const int32_t* __restrict__ cu_seqlens,
                                                    int mode, int normalize_f32,
                                                    float* __restrict__ out_f32,
-                                                   __bf16* __restrict__ out_norm) {
+                                                   __bf16* __restrict__ out_norm,
+                                                   const float* __restrict__ gamma,
+                                                   const float* __restrict__ beta, float eps) {
   constexpr int NV = H / 8;
   constexpr int PER = (NV + 63) / 64;
   __shared__ float part[4][H];
@@ -191,16 +196,41 @@ __global__ __launch_bounds__(256) void pool_kernel(const __bf16* __restrict__ hi
     for (int e = 0; e < 8; ++e) acc[i][e] = 0.f;
   const int t_end = mode == 1 ? (L > 0 ? 1 : 0) : L;
   for (int t = wave; t < t_end; t += 4) {
+    float r[PER][8];
+    float sm = 0.f;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int v = lane + 64 * i;
-      if (v < NV) {
-        float r[8];
-        load8(hidden + (size_t)(s0 + t) * H + v * 8, r);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) acc[i][e] += r[e];
+      for (int e = 0; e < 8; ++e) r[i][e] = 0.f;
+      if (v < NV) {
+        load8(hidden + (size_t)(s0 + t) * H + v * 8, r[i]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sm += r[i][e];
       }
     }
+    if (gamma != nullptr) {
+      const float mean = wave_sum(sm) * (1.0f / H);
+      float ss = 0.f;
+#pragma unroll
+      for (int i = 0; i < PER; ++i)
+        if (lane + 64 * i < NV)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ss += (r[i][e] - mean) * (r[i][e] - mean);
+      const float rstd = rsqrtf(wave_sum(ss) * (1.0f / H) + eps);
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int v = lane + 64 * i;
+        if (v < NV)
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            r[i][e] = (r[i][e] - mean) * rstd * gamma[v * 8 + e] + beta[v * 8 + e];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[i][e] += r[i][e];
   }
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
@@ -305,11 +335,13 @@ int symb_add_ln(const void* x, const void* res, const float* g, const float* b, 
 }
 
 int symb_pool(const void* hidden, const int32_t* cu, int B, int H, int mode, int normalize_f32,
-              float* out_f32, void* out_norm, hipStream_t st) {
+              float* out_f32, void* out_norm, hipStream_t st, const float* gamma,
+              const float* beta, float eps) {
   if (B <= 0) return 0;
+  if ((gamma == nullptr) != (beta == nullptr)) return -1;
   SYMB_H_DISPATCH(H, hipLaunchKernelGGL(pool_kernel<HH>, dim3(B), dim3(256), 0, st,
                                         (const __bf16*)hidden, cu, mode, normalize_f32, out_f32,
-                                        (__bf16*)out_norm));
+                                        (__bf16*)out_norm, gamma, beta, eps));
   return (int)hipGetLastError();
 }
 

@@ -388,6 +388,98 @@ def test_encoder_matches_fp32_oracle(model):
             assert cos2.min().item() > 0.9999, (mode, cos2)
 
 
+@pytest.mark.parametrize("M", [300, 4353, 32768])
+@pytest.mark.parametrize("N,K,epi,lnf", [
+    (2304, 768, 0, 1), (3072, 768, 1, 1), (768, 768, 2, 6), (768, 3072, 2, 6), (768, 768, 2, 4),
+    (3072, 1024, 0, 1), (4096, 1024, 1, 1), (1024, 4096, 2, 6), (1024, 1024, 2, 4),
+])
+def test_gemm_deferred_ln_matches_oracle(M, N, K, epi, lnf):
+    """gemm.hip's deferred-LayerNorm epilogues (symb_gemm_ln) against fp32 oracles, on every tile
+    the shapes pick (256 x 256 / 256 x 192 / 128 x 128, 2- and 4-deep rings) and ragged M:
+    LNF_FOLD: epi(LN(y) W^T + b) computed from the pre-LN y, its chunk statistics and the
+    gamma-folded weight; LNF_RESLN: + LN(R) from the pre-LN residual; LNF_STATS: the chunk
+    statistics of the stored (bf16) output."""
+    from codename_symbiont_amd.ops.kernels import LNF_FOLD, LNF_RESLN, LNF_STATS, fold_ln, gemm_ln
+
+    eps = 1e-12
+    gamma = _f(K if lnf & LNF_FOLD else N, scale=0.3, seed=7, offset=1.0)
+    beta = _f(K if lnf & LNF_FOLD else N, scale=0.2, seed=8)
+    w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=2)
+    bias = _f(N, scale=0.5, seed=3)
+    if lnf & LNF_FOLD:
+        y = (_f(M, K, scale=1.5, seed=1, offset=0.3)).bfloat16()
+        wg, bf, cs = fold_ln(w, bias, gamma, beta)
+        out = gemm_ln(y, wg, bf, epi, lnf, ln_eps=eps, cs=cs, st_in=R.ln_chunk_stats_ref(y))
+        ref = R.gemm_ref(R.add_ln_ref(y, None, gamma, beta, eps), w, bias, epi)
+        _close(out, ref, atol=5e-2, rtol=2e-2, what=f"folded-LN gemm epi={epi}")
+        return
+    x = _bf(M, K, seed=1)
+    st_out = torch.empty(M, N // 64, 2, device=DEV)
+    if lnf & LNF_RESLN:
+        r = (_f(M, N, scale=1.5, seed=4, offset=-0.2)).bfloat16()
+        out = gemm_ln(x, w, bias, epi, lnf, residual=r, gamma=gamma, beta=beta, ln_eps=eps,
+                      st_in=R.ln_chunk_stats_ref(r), st_out=st_out)
+        ref = R.gemm_ref(x, w, bias, 0) + R.add_ln_ref(r, None, gamma, beta, eps)
+    else:
+        r = _bf(M, N, seed=4)
+        out = gemm_ln(x, w, bias, epi, lnf, residual=r, st_out=st_out)
+        ref = R.gemm_ref(x, w, bias, 2, r)
+    _close(out, ref, atol=5e-2, rtol=2e-2, what=f"deferred-LN gemm lnf={lnf}")
+    _close(st_out, R.ln_chunk_stats_ref(out), atol=1e-4, rtol=1e-4, what="output chunk statistics")
+
+
+@pytest.mark.parametrize("H,mode", [(768, "mean"), (1024, "mean"), (768, "cls")])
+def test_pool_applies_deferred_layernorm(H, mode):
+    """pool_kernel with gamma / beta: every token row of the pre-LN hidden state is normalised
+    before pooling == pool_ref(LN(y))."""
+    from codename_symbiont_amd.ops._ext import hip, stream_handle
+
+    lens = [5, 1, 128, 37, 0, 64]
+    cu = torch.tensor([0] + lens).cumsum(0).to(torch.int32).to(DEV)
+    T, B = int(cu[-1]), len(lens)
+    y = _f(T, H, scale=2.0, seed=3, offset=0.4).bfloat16()
+    g, b = _f(H, scale=0.3, seed=4, offset=1.0), _f(H, scale=0.2, seed=5)
+    out = torch.empty(B, H, device=DEV)
+    nrm = torch.empty(B, H, dtype=torch.bfloat16, device=DEV)
+    hip().pool(y.data_ptr(), cu.data_ptr(), B, H, 0 if mode == "mean" else 1, 0, out.data_ptr(),
+               nrm.data_ptr(), stream_handle(), g=g.data_ptr(), b=b.data_ptr(), eps=1e-12)
+    ref = R.pool_ref(R.add_ln_ref(y, None, g, b, 1e-12), cu, mode, False)
+    _close(out, ref, atol=2e-4, rtol=1e-4, what="pool of LN(y)")
+
+
+@pytest.mark.parametrize("model", ["bge-base", "e5-large"])
+def test_encoder_deferred_ln_matches_oracle(model, monkeypatch):
+    """The wide encoders' deferred-LayerNorm forward (EncoderRuntime::deferred_forward: folded
+    QKV / FFN1 weights, residual LayerNorms in the out-proj / FFN2 epilogues, the last one in the
+    pool) on LayerNorm parameters away from (1, 0) == the fp32 oracle, and == the add_ln path."""
+    from codename_symbiont_amd.models import get_config
+    from codename_symbiont_amd.models.encoder import HipEncoder, TorchEncoder, synthetic_batch
+    from codename_symbiont_amd.models.weights import random_params
+
+    cfg = get_config(model)
+    params = random_params(cfg, seed=3)
+    gen = torch.Generator().manual_seed(9)
+    for L in params["layers"]:
+        for k in ("ln1_g", "ln2_g"):
+            L[k] = (1.0 + 0.3 * torch.randn(L[k].shape, generator=gen)).to(L[k].device)
+        for k in ("ln1_b", "ln2_b"):
+            L[k] = (0.2 * torch.randn(L[k].shape, generator=gen)).to(L[k].device)
+    hip_enc = HipEncoder(cfg, params=params)
+    assert hip_enc.rt.deferred_ln_ready()
+    b = synthetic_batch(cfg, 24, 96, seed=1, varlen=True)
+    out = hip_enc.forward_packed(b.to(DEV))[0].clone()
+    hip_enc.rt.set_deferred_ln(0)
+    try:
+        old = hip_enc.forward_packed(b.to(DEV))[0].clone()
+    finally:
+        hip_enc.rt.set_deferred_ln(1)
+    ref, _ = TorchEncoder(cfg, params=params).forward_packed(b)
+    cos = torch.nn.functional.cosine_similarity(out.float().cpu(), ref.float(), dim=-1)
+    assert cos.min().item() > 0.999, cos
+    cos2 = torch.nn.functional.cosine_similarity(out.float(), old.float(), dim=-1)
+    assert cos2.min().item() > 0.9995, cos2
+
+
 @pytest.mark.parametrize("D,k,n,nq", [(384, 10, 10_007, 300), (384, 20, 5000, 17),
                                       (768, 5, 9000, 130), (1024, 16, 4133, 64)])
 def test_index_scan_topk_exact(D, k, n, nq):

@@ -88,8 +88,10 @@ def test_rccl_index_group_store_roundtrip(rccl):
 
 
 def test_rccl_embed_group_matches_encoder(rccl):
-    """DP embedding (EmbedGroup: int64 header + int32 batch broadcasts, all_gather of the pooled
-    rows over RCCL in the wire dtype) == the encoder run directly, rounded to that dtype."""
+    """DP embedding (EmbedGroup: int64 header over the gloo control group, int32 batch
+    broadcasts and the all_gather of the pooled rows over RCCL in the wire dtype) == the encoder
+    run directly.  World 1: every row is rank 0's own slice, which never crosses the wire and
+    keeps its f32 values (ranks 1..N-1's rows are rounded to the wire dtype once)."""
     from codename_symbiont_amd.models import get_config
     from codename_symbiont_amd.models.encoder import HipEncoder, synthetic_batch
     from codename_symbiont_amd.parallel.embed_group import EmbedGroup
@@ -101,6 +103,6 @@ def test_rccl_embed_group_matches_encoder(rccl):
     b = synthetic_batch(cfg, 37, 48, seed=5, varlen=True).to(rccl.device)
     got = grp.embed(b)
     want, _ = enc.forward_packed(b)
-    want = want.to(grp.wire_dtype).float()   # (the pooled rows cross the wire in its dtype)
     torch.cuda.synchronize()
+    assert grp.wire == "bf16" and grp.ctrl is not None
     assert got.shape == want.shape and torch.equal(got, want)
