@@ -336,26 +336,27 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
   constexpr int CS = BN + 4;
   constexpr int PROWS = BM / EPI_PASSES;
   constexpr bool NEED_RS = (LNF & (LNF_FOLD | LNF_RESLN)) != 0;
+  constexpr int NP_MAX = 16;                        // statistics chunks per row (N <= 1024)
+  constexpr int PV = NEED_RS ? (PROWS * NP_MAX + NT - 1) / NT : 1;
   float* Cs = reinterpret_cast<float*>(smem);
-  // this pass's row statistics (mean, rstd) for LNF_FOLD / LNF_RESLN, after the fp32 tile
+  // this pass's row statistics (mean, rstd) for LNF_FOLD / LNF_RESLN, after the fp32 tile, and
+  // the raw chunk partials they are combined from
   float2* rs = reinterpret_cast<float2*>(smem + PROWS * CS * 4);
+  float2* rsraw = rs + PROWS;
   __syncthreads();
 #pragma unroll 1
   for (int p = 0; p < EPI_PASSES; ++p) {
     const int band0 = m0 + p * PROWS;  // first global row of this pass
+    // the band's partials are ONE contiguous block of st_in: issue every load now (coalesced,
+    // all in flight while the accumulators are staged), combine after the staging barrier
+    float2 pv[PV];
     if constexpr (NEED_RS) {
-      for (int t = tid; t < PROWS; t += NT) {
-        const float2* sp = st_in + (size_t)min(band0 + t, M - 1) * np_in;
-        float msum = 0.f;
-        for (int i = 0; i < np_in; ++i) msum += sp[i].x;
-        const float mean = msum / (float)np_in;
-        float m2 = 0.f;
-        for (int i = 0; i < np_in; ++i) {
-          const float2 v = sp[i];
-          const float d = v.x - mean;
-          m2 += v.y + 64.f * d * d;
-        }
-        rs[t] = make_float2(mean, rsqrtf(m2 / (64.f * (float)np_in) + ln_eps));
+      const int nv = max(0, min(PROWS, M - band0)) * np_in;
+      const float2* sp = st_in + (size_t)band0 * np_in;
+#pragma unroll
+      for (int u = 0; u < PV; ++u) {
+        const int idx = u * NT + tid;
+        pv[u] = idx < nv ? sp[idx] : make_float2(0.f, 0.f);
       }
     }
     if (EPI_PASSES == 1 || wm == p) {
@@ -374,6 +375,25 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
             else
               Cs[row * CS + col] = acc[i][j][r];
           }
+    }
+    if constexpr (NEED_RS) {
+#pragma unroll
+      for (int u = 0; u < PV; ++u)
+        if (u * NT + tid < PROWS * np_in) rsraw[u * NT + tid] = pv[u];
+      __syncthreads();
+      for (int t = tid; t < PROWS; t += NT) {
+        const float2* sp = rsraw + t * np_in;
+        float msum = 0.f;
+        for (int i = 0; i < np_in; ++i) msum += sp[i].x;
+        const float mean = msum / (float)np_in;
+        float m2 = 0.f;
+        for (int i = 0; i < np_in; ++i) {
+          const float2 v = sp[i];
+          const float d = v.x - mean;
+          m2 += v.y + 64.f * d * d;
+        }
+        rs[t] = make_float2(mean, rsqrtf(m2 / (64.f * (float)np_in) + ln_eps));
+      }
     }
     __syncthreads();
     if constexpr (EPI == EPI_RES_LN) {
@@ -431,9 +451,15 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
           load8(R + (size_t)grow * ldr + n0 + c8, r);
           if constexpr ((LNF & LNF_RESLN) != 0) {
             const float2 st = rs[row];
+            const f32x4 g0 = *reinterpret_cast<const f32x4*>(gamma + n0 + c8);
+            const f32x4 g1 = *reinterpret_cast<const f32x4*>(gamma + n0 + c8 + 4);
+            const f32x4 e0 = *reinterpret_cast<const f32x4*>(beta + n0 + c8);
+            const f32x4 e1 = *reinterpret_cast<const f32x4*>(beta + n0 + c8 + 4);
 #pragma unroll
-            for (int e = 0; e < 8; ++e)
-              y[e] += (r[e] - st.x) * st.y * gamma[n0 + c8 + e] + beta[n0 + c8 + e];
+            for (int e = 0; e < 4; ++e) {
+              y[e] += (r[e] - st.x) * st.y * g0[e] + e0[e];
+              y[e + 4] += (r[e + 4] - st.x) * st.y * g1[e] + e1[e];
+            }
           } else {
 #pragma unroll
             for (int e = 0; e < 8; ++e) y[e] += r[e];
@@ -499,7 +525,7 @@ static int launch_cfg(const void* A, int lda, const void* W, int ldw, const floa
   constexpr int full_epi = BM * (BN + 4) * 4;
   constexpr int passes = full_epi > 160 * 1024 ? WM : 1;
   constexpr int epi_bytes = (BM / passes) * (BN + 4) * 4 +
-                            ((LNF & (LNF_FOLD | LNF_RESLN)) ? (BM / passes) * 8 : 0);
+                            ((LNF & (LNF_FOLD | LNF_RESLN)) ? (BM / passes) * 8 * 17 : 0);
   constexpr int lds = main_bytes > epi_bytes ? main_bytes : epi_bytes;
   static_assert(lds <= 160 * 1024, "LDS");
   set_max_lds<gemm_bf16_kernel<BM, BN, WM, WN, EPI, NSTAGE, F8, AMX, LNF>>(lds);
@@ -722,7 +748,7 @@ int symb_gemm_ln(int epi, int lnf, const void* A, int lda, const void* W, int ld
   if (M <= 0) return 0;
   if (K % GEMM_BK != 0 || N % 128 != 0) return -1;
   const bool fold = lnf & LNF_FOLD, resln = lnf & LNF_RESLN, stats = lnf & LNF_STATS;
-  if ((fold || resln) && (st_in == nullptr || np_in < 1 || np_in > 64)) return -1;
+  if ((fold || resln) && (st_in == nullptr || np_in < 1 || np_in > 16)) return -1;
   if (fold && cs == nullptr) return -1;
   if (resln && (gamma == nullptr || beta == nullptr || R == nullptr)) return -1;
   if (stats && st_out == nullptr) return -1;
