@@ -351,6 +351,9 @@ def scan_label(args, shard, prune, prefilter, dim: int, nq: int) -> str:
         return ("bf16 emitting scan + radix select (exact, large k)" if dim in MQ_DIMS
                 else "bf16 list scan (exact)")
     if prune:
+        if shard.stream and shard.i8_ring and not shard._i8_heavy:
+            return ("exact pruned: MX-fp4 stream scan (index_stream.hip) / int8 LDS-ring scan "
+                    "(index_i8.hip) of bound-checked images + bf16 re-score")
         if shard.stream and not shard._i8_heavy:
             return ("exact pruned: int8 / MX-fp4 stream scan (index_stream.hip) of bound-checked "
                     "images + bf16 re-score")

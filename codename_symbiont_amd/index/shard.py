@@ -144,6 +144,7 @@ MX4_DIMS = (384, 768, 1024)             # ... the MX-fp4 first tier (384-only on
 # 384 / 768 only)
 STREAM_DIMS = (384, 768, 1024)
 STREAM_SUB = 32                         # rows per sub-tile record of the stream images
+I8_RING_DIMS = ()                       # ... where the int8 tier runs the LDS-ring scan instead
 # widths of the MX-fp6 (e2m3) middle tier (stream scan only) and where SYMB_PRUNE_MX6=auto keeps
 # it: nowhere -- measured, it never applies (held-out queries leave ~70.8k candidates in its band
 # against a 32k cap, and self / near-duplicate queries take the fp4 tier: profiles/r5_lq/), so a
@@ -216,6 +217,14 @@ class HbmIndexShard:
         # [n_sub, REC] bytes, 32-row sub-tiles in fragment-major order (img_i8 / img_mx4)
         self.stream = bool(prune) and dim in STREAM_DIMS and os.environ.get(
             "SYMB_PRUNE_STREAM", "1") not in ("", "0")
+        # the int8 tier's kernel, chosen apart from the fp4 tier's: "stream"
+        # = the fragment-major image (index_stream.hip, or its LDS-query form index_lq.hip at 768)
+        # or "ring" = the row-major image with per-row scales on the LDS-ring scan (index_i8.hip,
+        # round 4's I8Dim<768>); the MX-fp4 tier keeps its stream image either way.
+        # SYMB_PRUNE_I8=auto takes I8_RING_DIMS.
+        i8k = os.environ.get("SYMB_PRUNE_I8", "auto").strip().lower()
+        self.i8_ring = bool(self.stream and dim in (384, 768) and (
+            i8k == "ring" or (i8k == "auto" and dim in I8_RING_DIMS)))
         self.img_i8 = self.img_mx4 = None
         if prune:
             # padded to whole 128-row tiles: the int8 scan's DMA reads whole tiles; one flat byte
@@ -223,7 +232,7 @@ class HbmIndexShard:
             n_alloc = _round_up(self.rows.shape[0], 128)
             rb = dim + SPLIT_HEAVY if dim in SPLIT_DIMS else dim
             nbytes = n_alloc * rb
-            if self.stream:
+            if self.stream and not self.i8_ring:
                 nbytes = max(nbytes, n_alloc // STREAM_SUB * self._stream_rec(0))
             self._i8_store = torch.zeros(nbytes, dtype=torch.int8, device=self.device)
             self.sx_i8 = torch.ones(n_alloc, dtype=torch.float32, device=self.device)
@@ -317,7 +326,7 @@ class HbmIndexShard:
         """Views of the flat int8 store for the form: the stream image (plain form on a stream
         shard) or the row-major image [n_alloc, D + heavy] (split form, or stream off)."""
         n_alloc = self.sx_i8.shape[0]
-        if self.stream and not heavy:
+        if self.stream and not heavy and not self.i8_ring:
             rec = self._stream_rec(0)
             self.img_i8 = self._i8_store[:n_alloc // STREAM_SUB * rec].view(torch.uint8).view(
                 n_alloc // STREAM_SUB, rec)
@@ -1383,6 +1392,8 @@ class HbmIndexShard:
             # on the LDS-ring kernel: 64-row tiles there too.
             if heavy:
                 n_qblk, wpc = math.ceil(NQ / h.i8_split_queries_per_blk(rsplit)), 1
+            elif self.i8_ring:   # (the LDS-ring int8 scan beside the stream fp4 tier)
+                n_qblk, wpc = math.ceil(NQ / h.i8_queries_per_blk(rsplit)), h.i8_wgs_per_cu()
             else:
                 qpb, wpc = h.stream_geometry(self.dim, 0)
                 n_qblk = math.ceil(NQ / qpb)

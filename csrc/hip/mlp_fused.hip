@@ -282,7 +282,9 @@ __global__ __launch_bounds__(MF_NT) void mlp_fused_kernel(
 //  * LDS holds only the weight stream: a 3-slot ring of 48 KiB steps (W1_c in 2 steps of 3
 //    k-tiles, W2_c in 2 steps of one 384-row k-tile), each step's LDS-DMA issued two steps ahead.
 constexpr int MR_BM = 128, MR_NW = 4, MR_NT = 64 * MR_NW;
-constexpr int MR_SLOT = 48 * 1024, MR_NSLOT = 3, MR_LDS = MR_SLOT * MR_NSLOT;
+constexpr int MR_SLOT = 48 * 1024, MR_NSLOT = 3;
+constexpr int MR_B1 = MR_SLOT * MR_NSLOT;            // b1 (1536 floats) parked in LDS
+constexpr int MR_LDS = MR_B1 + MF_FF * 4;
 constexpr int MR_SPC = 4;                            // ring steps per 128-column chunk
 constexpr int MR_NSTEP = (MF_FF / MF_FC) * MR_SPC;   // 48
 constexpr int MR_DMA = 12;                           // LDS-DMA pieces per lane per step
@@ -323,8 +325,11 @@ void mlp_reg_kernel(const __bf16* X, const __bf16* __restrict__ W1, const float*
     }
   };
 
-  stage(0);
-  stage(1);
+  // b1 into LDS (read per chunk with ds_read: a global load there would be counted in vmcnt
+  // behind the ring's LDS-DMA and its wait would drain the prefetch)
+  float* b1s = reinterpret_cast<float*>(smem + MR_B1);
+  for (int i = tid; i < MF_FF / 4; i += MR_NT)
+    reinterpret_cast<f32x4*>(b1s)[i] = reinterpret_cast<const f32x4*>(b1)[i];
   // the wave's 32 X rows as B fragments: token 16i + r16, k 32ks + 8g4 .. + 7
   bf16x8 xf[2][12];
 #pragma unroll
@@ -333,6 +338,9 @@ void mlp_reg_kernel(const __bf16* X, const __bf16* __restrict__ W1, const float*
 #pragma unroll
     for (int ks = 0; ks < 12; ++ks) xf[i][ks] = *reinterpret_cast<const bf16x8*>(xr + 32 * ks);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (X and b1 landed before the ring starts)
+  stage(0);
+  stage(1);
 
   f32x4 acc[2][24];     // out^T: token 16i + r16, output columns 16j + 4g4 + e
 #pragma unroll
@@ -342,12 +350,16 @@ void mlp_reg_kernel(const __bf16* X, const __bf16* __restrict__ W1, const float*
 
   // step q's pieces landed (this wave: all but the next step's MR_DMA; every wave: the
   // barrier); slot (q + 2) % 3 was last read in step q - 1, so it is free to refill
+  // (a raw s_barrier: __syncthreads would drain vmcnt to 0 -- the next step's pieces too --
+  // which serialised the ring; every wave's reads of the slot being refilled retired with its
+  // lgkmcnt(0) before the barrier)
   auto step_begin = [&](int q) {
     if (q + 1 < MR_NSTEP)
       asm volatile("s_waitcnt vmcnt(%0)" ::"i"(MR_DMA) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
     if (q + 2 < MR_NSTEP) stage(q + 2);
   };
 
@@ -384,7 +396,7 @@ void mlp_reg_kernel(const __bf16* X, const __bf16* __restrict__ W1, const float*
     bf16x8 hb[2][4];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const f32x4 bb = *reinterpret_cast<const f32x4*>(b1 + c * MF_FC + 16 * j + 4 * g4);
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(b1s + c * MF_FC + 16 * j + 4 * g4);
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         f32x2 y0{ha[i][j][0] + bb[0], ha[i][j][1] + bb[1]};

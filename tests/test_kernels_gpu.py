@@ -1279,14 +1279,21 @@ def test_wide_index_topk_exact_vs_torch_topk(D, k):
     assert r[:8, 0].tolist() == list(range(n, n + 8))
 
 
-@pytest.mark.parametrize("nq,data,D", [(256, "random", 768), (300, "near", 768),
-                                       (512, "random", 768), (256, "clustered", 768),
-                                       (256, "random", 1024), (300, "near", 1024)])
-def test_index_pruned_search_768_is_exact(nq, data, D):
+@pytest.mark.parametrize("nq,data,D,i8k", [(256, "random", 768, "stream"), (300, "near", 768, "stream"),
+                                           (512, "random", 768, "stream"),
+                                           (256, "clustered", 768, "stream"),
+                                           (256, "random", 768, "ring"), (300, "near", 768, "ring"),
+                                           (512, "random", 768, "ring"),
+                                           (256, "random", 1024, "stream"),
+                                           (300, "near", 1024, "stream")])
+def test_index_pruned_search_768_is_exact(nq, data, D, i8k, monkeypatch):
     """The int8-pruned search at the reference's 768-d collection (12 i8 k-steps, 192 query
     registers) and at 1024 (the stream scan's one-set form): the rows and scores of the exact
-    bf16 scan."""
+    bf16 scan.  i8k ring: the int8 tier on the row-major LDS-ring scan (index_i8.hip) beside the
+    MX-fp4 tier's stream image (SYMB_PRUNE_I8=ring)."""
     from codename_symbiont_amd.index.shard import HbmIndexShard
+
+    monkeypatch.setenv("SYMB_PRUNE_I8", i8k)
 
     n, k = (1 << 20) + 777, 10
     g = torch.Generator(device=DEV).manual_seed(72)
@@ -1298,6 +1305,8 @@ def test_index_pruned_search_768_is_exact(nq, data, D):
         x = torch.randn(n, D, device=DEV, generator=g)
     ref = HbmIndexShard(D, n + 4096)
     shard = HbmIndexShard(D, n + 4096, prune="i8")
+    assert shard.i8_ring == (i8k == "ring") and shard.mx4_on
+    assert (shard.img_i8 is None) == (i8k == "ring") and (shard.img_mx4 is not None)
     for sh in (ref, shard):
         sh.append_f32(x)
     del x
