@@ -465,7 +465,7 @@ def cmd_encoder(a):
     _hip().gemm_config(128, 3, 8)
     _hip().gemm_lt_config(1)
     _hip().gemm_fp8_config(8)
-    _hip().mlp_fused_config(2)
+    _hip().mlp_fused_config(1)
     toks = a.batch * a.seq
     fl = cfg.flops_per_token(a.seq) * toks
     out = {p: dict(ms=round(m, 3), embeds_per_s=round(a.batch / (m / 1e3)),

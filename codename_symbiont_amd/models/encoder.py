@@ -162,7 +162,11 @@ class HipEncoder:
         # deferred LayerNorm for the wide (H >= 768) bf16 encoders (EncoderRuntime's
         # deferred_forward): the QKV weight folded with the previous layer's ln2 and the FFN1
         # weight with this layer's ln1 (ops.kernels.fold_ln), so no add_ln pass and no hipBLASLt
-        # projection runs above the small-M limit.  SYMB_DEFERRED_LN=0: the add_ln path (A/B).
+        # projection runs above the small-M limit.  Opt-in (SYMB_DEFERRED_LN=1): this repo's
+        # GEMM main loops trail hipBLASLt's on the plain QKV / FFN2 shapes by more than the two
+        # add_ln passes the fusion removes -- bge 7.65 vs 6.75 ms, e5 23.4 vs 20.7 ms per
+        # 256 x 128 batch on one box (profiles/r6_gemm/) -- so the default keeps the hipBLASLt
+        # route for the plain projections.
         self._folds = []
         if precision == "bf16" and cfg.hidden != 384 and cfg.hidden % 64 == 0:
             import os
@@ -177,7 +181,7 @@ class HipEncoder:
                 fi = fold_ln(L["wi"], L["bi"], L["ln1_g"], L["ln1_b"])
                 self._folds.append((fq, fi))
                 self.rt.set_fold(li, [0 if t is None else t.data_ptr() for t in fq + fi])
-            self.rt.set_deferred_ln(0 if os.environ.get("SYMB_DEFERRED_LN", "1") in ("", "0")
+            self.rt.set_deferred_ln(0 if os.environ.get("SYMB_DEFERRED_LN", "0") in ("", "0")
                                     else 1)
         self._ws_tokens = 0
         self._ws: list[torch.Tensor] = []

@@ -42,11 +42,6 @@ def hip():
 
     # SYMB_GPU_DEBUG=1: every kernel launch is synchronized and checked (fault attribution)
     mod.set_debug(debug_enabled())
-    # SYMB_MLP_FORM (A/B): the 384-wide FFN block as 0 = two GEMMs, 1 = the LDS-staged fused
-    # kernel, 2 = the register-resident fused kernel (default)
-    form = os.environ.get("SYMB_MLP_FORM", "")
-    if form:
-        mod.mlp_fused_config(int(form))
     return mod
 
 

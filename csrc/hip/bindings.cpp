@@ -55,7 +55,6 @@ int symb_gemm_fp8_config(int waves, int big);
 int symb_gemm_resln_config(int waves);
 int symb_gemm_gelu_config(int poly);
 int symb_gemm_gelu_poly();
-int symb_mlp_fused_form(int form);   // 1 / 2 set the fused form; 0 returns the current one
 int symb_mlp_fused(const void* X, const void* W1, const float* b1, const void* W2, const float* b2,
                    const float* gamma, const float* beta, float eps, int gelu_poly, void* C, int M,
                    int H, int FF, hipStream_t st);
@@ -482,7 +481,7 @@ class EncoderRuntime {
   }
 
   bool any_fp8_ = false;
-  int deferred_ln_ = 1;
+  int deferred_ln_ = 0;
   int H_, nh_, hd_, FF_;
   float eps_;
   uptr wemb_, pemb_, temb_, eln_g_, eln_b_;
@@ -854,13 +853,10 @@ PYBIND11_MODULE(_hip, m) {
                          S(st)),
           "mlp_fused");
   });
-  // 0: two GEMMs, 1: the LDS-staged fused FFN block, 2: the register-resident one (default)
-  m.def("mlp_fused_config", [](int mode) {
-    if (mode < 0 || mode > 2) throw std::invalid_argument("mlp_fused_config: mode 0, 1 or 2");
-    g_mlp_fused = mode ? 1 : 0;
-    if (mode) check(symb_mlp_fused_form(mode), "mlp_fused_form");
+  m.def("mlp_fused_config", [](int mode) {   // 0: two GEMMs, 1: the fused FFN block (default)
+    if (mode < 0 || mode > 1) throw std::invalid_argument("mlp_fused_config: mode 0 or 1");
+    g_mlp_fused = mode;
   });
-  m.def("mlp_fused_mode", []() { return g_mlp_fused ? symb_mlp_fused_form(0) : 0; });
   m.def("gemm_gelu_config", [](int poly) { check(symb_gemm_gelu_config(poly), "gemm_gelu_config"); },
         py::arg("poly"));
   m.def("gemm_fp8_config", [](int waves, int big) {

@@ -578,8 +578,7 @@ static int big_tile_bn(int tile, int M, int N, int K) {
 }
 int symb_gemm_config(int resln_bm, int tile, int group_m) {
   if (resln_bm != 64 && resln_bm != 128) return -1;
-  if (tile != 0 && tile != 2 && tile != 3 && tile != 10 && tile != 20 && tile != 21)
-    return -1;   // (see g_tile)
+  if (tile != 0 && tile != 2 && tile != 3 && tile != 10) return -1;   // (see g_tile)
   if (group_m < 0 || group_m > 64) return -1;
   g_resln_bm = resln_bm;
   g_tile = tile;
@@ -663,21 +662,6 @@ int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const flo
       (g_gemm_lt == 2 || (g_gemm_lt == 1 && K >= 768 && N >= 768 && M >= 4096))) {
     const int rc = symb_gemm_lt(epi, A, lda, W, ldw, bias, R, ldr, C, ldc, M, N, K, st);
     if (rc != -1 && rc != -2) return rc;   // 0, or a HIP error; else this file's kernels
-  }
-  if (g_tile == 20 || g_tile == 21) {
-    // (A/B) 256 x 128 tiles with a 3-deep LDS-DMA ring (144 KiB): 20 = 4 x 2 waves of 64 x 64,
-    // 21 = 2 x 4 waves of 128 x 32
-#define SYMB_G(E) (g_tile == 20 ? launch_cfg<256, 128, 4, 2, E, 3>(a, lda, w, ldw, bias, r, ldr, gamma, \
-                                                                 beta, eps, c, ldc, M, N, K, st)     \
-                               : launch_cfg<256, 128, 2, 4, E, 3>(a, lda, w, ldw, bias, r, ldr, gamma, \
-                                                                 beta, eps, c, ldc, M, N, K, st))
-    switch (epi) {
-      case EPI_BIAS: return SYMB_G(EPI_BIAS);
-      case EPI_GELU: return SYMB_G(EPI_GELU);
-      case EPI_RES: return SYMB_G(EPI_RES);
-    }
-#undef SYMB_G
-    return -1;
   }
   if (const int bn = big_tile_bn(g_tile, M, N, K)) {
 #define SYMB_G(E, BN_) launch_cfg<256, BN_, 2, 4, E>(a, lda, w, ldw, bias, r, ldr, gamma, beta, eps, \

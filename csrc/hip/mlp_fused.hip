@@ -52,7 +52,11 @@ __device__ __forceinline__ int mf_swz(int row, int chunk) {
 }
 
 // (Round 4 also built a form that ran the attention out-projection + LayerNorm first in the same
-// workgroup; it measured parity-to-slower and was removed in round 5.)
+// workgroup; it measured parity-to-slower and was removed in round 5.  Round 6 built a register-
+// resident form -- 4 waves of 512 registers, X and the GELU intermediate in VGPRs, k-permuted W2
+// fragments, LayerNorm across the 4 lanes of a token, only the weights through a 3-slot LDS ring:
+// exact, but 1.56-1.60 ms per MiniLM forward against 1.25-1.27 with this kernel (24 VGPRs
+// spilled, reloads draining the ring), so it was removed: profiles/r6_gemm/README.md.)
 __global__ __launch_bounds__(MF_NT) void mlp_fused_kernel(
     const __bf16* X, const __bf16* __restrict__ W1, const float* __restrict__ b1,
     const __bf16* __restrict__ W2, const float* __restrict__ b2, const float* __restrict__ gamma,
@@ -266,239 +270,11 @@ __global__ __launch_bounds__(MF_NT) void mlp_fused_kernel(
   ln_store(b2, X, gamma, beta, C);
 }
 
-// ---------------------------------------------------------------------------------------------
-// Register-resident form (the MiniLM forward's FFN blocks were ~53 % of it).
-// Four waves, ONE per SIMD (512 registers each), 32 token rows per wave, 128 per workgroup:
-//  * the wave's X rows (32 x 384) are loaded ONCE into VGPRs as B-operand fragments (96 VGPRs)
-//    instead of being re-streamed through LDS for each of the 12 chunks (1.1 MiB of the 3.5 MiB
-//    the LDS form moved per workgroup);
-//  * H_c never touches LDS: phase A computes H_c^T (W1_c rows as the A operand), so a lane holds
-//    4 consecutive intermediate columns of one token -- after GELU and the bf16 rounding, two of
-//    those tiles ARE the B operand of phase B under a fixed permutation of the k index, and the
-//    W2 fragments are read with the same permutation (two 8-byte reads per fragment);
-//  * phase B accumulates out^T (W2 rows as the A operand): a lane ends with 4 consecutive output
-//    columns of one token, so the residual add, the LayerNorm (row sums over the 4 lanes of a
-//    token: two shuffles) and the 8-byte bf16 stores need no LDS staging at all;
-//  * LDS holds only the weight stream: a 3-slot ring of 48 KiB steps (W1_c in 2 steps of 3
-//    k-tiles, W2_c in 2 steps of one 384-row k-tile), each step's LDS-DMA issued two steps ahead.
-constexpr int MR_BM = 128, MR_NW = 4, MR_NT = 64 * MR_NW;
-constexpr int MR_SLOT = 48 * 1024, MR_NSLOT = 3;
-constexpr int MR_B1 = MR_SLOT * MR_NSLOT;            // b1 (1536 floats) parked in LDS
-constexpr int MR_LDS = MR_B1 + MF_FF * 4;
-constexpr int MR_SPC = 4;                            // ring steps per 128-column chunk
-constexpr int MR_NSTEP = (MF_FF / MF_FC) * MR_SPC;   // 48
-constexpr int MR_DMA = 12;                           // LDS-DMA pieces per lane per step
-
-__global__ __launch_bounds__(MR_NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
-void mlp_reg_kernel(const __bf16* X, const __bf16* __restrict__ W1, const float* __restrict__ b1,
-                    const __bf16* __restrict__ W2, const float* __restrict__ b2,
-                    const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
-                    int gelu_poly, __bf16* C, int M) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r16 = lane & 15, g4 = lane >> 4;
-  const int m0 = xcd_remap(blockIdx.x, gridDim.x) * MR_BM + wave * 32;   // this wave's rows
-
-  // ring step q -> slot q % 3.  s = q % 4: 0, 1 = W1_c (rows 128c ..) k-tiles 3s .. 3s + 2;
-  // 2, 3 = W2 (all 384 rows) k-tile 2c + s - 2 of its 1536 columns.  Piece v = i * 256 + tid is
-  // row 32i + (tid >> 3) of a tile; its swizzled chunk (tid & 7) ^ ((tid >> 4) & 7) does not
-  // depend on i, so a lane keeps ONE base address per matrix and every piece adds a uniform
-  // offset (per-piece 64-bit addresses held across the loop spilled registers)
-  const int lrow = tid >> 3, lch = (tid & 7) ^ ((tid >> 4) & 7);
-  const char* w1p = reinterpret_cast<const char*>(W1) + (size_t)lrow * MF_H * 2 + lch * 16;
-  const char* w2p = reinterpret_cast<const char*>(W2) + (size_t)lrow * MF_FF * 2 + lch * 16;
-  auto stage = [&](int q) {
-    const int c = q / MR_SPC, s = q % MR_SPC;
-    char* base = smem + (q % MR_NSLOT) * MR_SLOT + wave * 64 * 16;
-    if (s < 2) {
-#pragma unroll
-      for (int t = 0; t < 3; ++t)
-#pragma unroll
-        for (int i = 0; i < (MF_FC * 8) / MR_NT; ++i)
-          glds16(w1p + (size_t)(c * MF_FC + 32 * i) * MF_H * 2 + (3 * s + t) * 128,
-                 base + t * (MF_FC * 128) + i * MR_NT * 16);
-    } else {
-      const int kt = 2 * c + s - 2;
-#pragma unroll
-      for (int i = 0; i < (MF_H * 8) / MR_NT; ++i)
-        glds16(w2p + (size_t)(32 * i) * MF_FF * 2 + kt * 128, base + i * MR_NT * 16);
-    }
-  };
-
-  // b1 into LDS (read per chunk with ds_read: a global load there would be counted in vmcnt
-  // behind the ring's LDS-DMA and its wait would drain the prefetch)
-  float* b1s = reinterpret_cast<float*>(smem + MR_B1);
-  for (int i = tid; i < MF_FF / 4; i += MR_NT)
-    reinterpret_cast<f32x4*>(b1s)[i] = reinterpret_cast<const f32x4*>(b1)[i];
-  // the wave's 32 X rows as B fragments: token 16i + r16, k 32ks + 8g4 .. + 7
-  bf16x8 xf[2][12];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const __bf16* xr = X + (size_t)min(m0 + 16 * i + r16, M - 1) * MF_H + 8 * g4;
-#pragma unroll
-    for (int ks = 0; ks < 12; ++ks) xf[i][ks] = *reinterpret_cast<const bf16x8*>(xr + 32 * ks);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (X and b1 landed before the ring starts)
-  stage(0);
-  stage(1);
-
-  f32x4 acc[2][24];     // out^T: token 16i + r16, output columns 16j + 4g4 + e
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 24; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // step q's pieces landed (this wave: all but the next step's MR_DMA; every wave: the
-  // barrier); slot (q + 2) % 3 was last read in step q - 1, so it is free to refill
-  // (a raw s_barrier: __syncthreads would drain vmcnt to 0 -- the next step's pieces too --
-  // which serialised the ring; every wave's reads of the slot being refilled retired with its
-  // lgkmcnt(0) before the barrier)
-  auto step_begin = [&](int q) {
-    if (q + 1 < MR_NSTEP)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(MR_DMA) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (q + 2 < MR_NSTEP) stage(q + 2);
-  };
-
-#pragma unroll 1
-  for (int c = 0; c < MF_FF / MF_FC; ++c) {
-    // ---- phase A: H_c^T = W1_c X^T (lane: token 16i + r16, H_c columns 16j + 4g4 + e) ----
-    f32x4 ha[2][8];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) ha[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int q = c * MR_SPC + s;
-      step_begin(q);
-      const char* base = smem + (q % MR_NSLOT) * MR_SLOT;
-#pragma unroll
-      for (int t = 0; t < 3; ++t)
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          const int ks = (3 * s + t) * 2 + kk;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const bf16x8 wf = *reinterpret_cast<const bf16x8*>(
-                base + t * (MF_FC * 128) + mf_swz(16 * j + r16, 4 * kk + g4));
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-              ha[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xf[i][ks], ha[i][j], 0, 0, 0);
-          }
-        }
-    }
-    // ---- GELU(+ b1) -> bf16 B fragments of phase B: hb[i][kb] positions 0..3 = H_c columns
-    //      32kb + 4g4 + e, positions 4..7 = 32kb + 16 + 4g4 + e (tiles 2kb, 2kb + 1) ----
-    bf16x8 hb[2][4];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const f32x4 bb = *reinterpret_cast<const f32x4*>(b1s + c * MF_FC + 16 * j + 4 * g4);
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        f32x2 y0{ha[i][j][0] + bb[0], ha[i][j][1] + bb[1]};
-        f32x2 y1{ha[i][j][2] + bb[2], ha[i][j][3] + bb[3]};
-        if (gelu_poly) {
-          y0 = gelu2_poly(y0);
-          y1 = gelu2_poly(y1);
-        } else {
-          y0.x = gelu_erf(y0.x);
-          y0.y = gelu_erf(y0.y);
-          y1.x = gelu_erf(y1.x);
-          y1.y = gelu_erf(y1.y);
-        }
-        const int p = (j & 1) * 4;
-        hb[i][j >> 1][p + 0] = (__bf16)y0.x;
-        hb[i][j >> 1][p + 1] = (__bf16)y0.y;
-        hb[i][j >> 1][p + 2] = (__bf16)y1.x;
-        hb[i][j >> 1][p + 3] = (__bf16)y1.y;
-      }
-    }
-    // ---- phase B: out^T += W2_c H_c^T, k in the permuted order of hb ----
-    typedef short s16x4 __attribute__((ext_vector_type(4)));
-#pragma unroll
-    for (int s = 2; s < 4; ++s) {
-      const int q = c * MR_SPC + s;
-      step_begin(q);
-      const char* base = smem + (q % MR_NSLOT) * MR_SLOT;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int kb = (s - 2) * 2 + kk;
-        const int ch = 4 * kk + (g4 >> 1), off = (g4 & 1) * 8;
-#pragma unroll
-        for (int j = 0; j < 24; ++j) {
-          const int row = 16 * j + r16;
-          const s16x4 lo = *reinterpret_cast<const s16x4*>(base + mf_swz(row, ch) + off);
-          const s16x4 hi = *reinterpret_cast<const s16x4*>(base + mf_swz(row, ch + 2) + off);
-          const bf16x8 wf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, hb[i][kb], acc[i][j], 0, 0, 0);
-        }
-      }
-    }
-  }
-
-  // ---- epilogue: + b2 + X, LayerNorm over the token's 384 columns (4 lanes), bf16 stores ----
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int t = m0 + 16 * i + r16;
-    const __bf16* xr = X + (size_t)min(t, M - 1) * MF_H + 4 * g4;
-    float sm = 0.f;
-#pragma unroll
-    for (int j = 0; j < 24; ++j) {
-      const f32x4 bb = *reinterpret_cast<const f32x4*>(b2 + 16 * j + 4 * g4);
-      const bf16x4 rr = *reinterpret_cast<const bf16x4*>(xr + 16 * j);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        acc[i][j][e] += bb[e] + (float)rr[e];
-        sm += acc[i][j][e];
-      }
-    }
-    sm += __shfl_xor(sm, 16, 64);
-    sm += __shfl_xor(sm, 32, 64);
-    const float mean = sm * (1.0f / MF_H);
-    float ss = 0.f;
-#pragma unroll
-    for (int j = 0; j < 24; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) ss += (acc[i][j][e] - mean) * (acc[i][j][e] - mean);
-    ss += __shfl_xor(ss, 16, 64);
-    ss += __shfl_xor(ss, 32, 64);
-    const float rstd = rsqrtf(ss * (1.0f / MF_H) + eps);
-    if (t < M) {
-      __bf16* o = C + (size_t)t * MF_H + 4 * g4;
-#pragma unroll
-      for (int j = 0; j < 24; ++j) {
-        const f32x4 gg = *reinterpret_cast<const f32x4*>(gamma + 16 * j + 4 * g4);
-        const f32x4 be = *reinterpret_cast<const f32x4*>(beta + 16 * j + 4 * g4);
-        bf16x4 v;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = (__bf16)((acc[i][j][e] - mean) * rstd * gg[e] + be[e]);
-        *reinterpret_cast<bf16x4*>(o + 16 * j) = v;
-      }
-    }
-  }
-}
-
 }  // namespace
 
 }  // namespace symb
 
 using namespace symb;
-
-// FFN block form: 1 = the LDS-staged kernel (mlp_fused_kernel), 2 = the register-resident one
-// (mlp_reg_kernel); see symb_mlp_fused_form.
-static int g_mlp_form = 2;
-int symb_mlp_fused_form(int form) {
-  if (form == 0) return g_mlp_form;
-  if (form != 1 && form != 2) return -1;
-  g_mlp_form = form;
-  return 0;
-}
 
 // The whole FFN block of a 384-wide layer in one launch (X, C: [M, 384] bf16, row stride 384;
 // C must not alias X).  Returns 0, a HIP error, or -1 (shape not supported).
@@ -507,13 +283,6 @@ int symb_mlp_fused(const void* X, const void* W1, const float* b1, const void* W
                    int H, int FF, hipStream_t st) {
   if (M <= 0) return 0;
   if (H != MF_H || FF != MF_FF || X == C) return -1;
-  if (g_mlp_form == 2) {
-    set_max_lds<mlp_reg_kernel>(MR_LDS);
-    hipLaunchKernelGGL(mlp_reg_kernel, dim3((M + MR_BM - 1) / MR_BM), dim3(MR_NT), MR_LDS, st,
-                       (const __bf16*)X, (const __bf16*)W1, b1, (const __bf16*)W2, b2, gamma, beta,
-                       eps, gelu_poly, (__bf16*)C, M);
-    return (int)hipGetLastError();
-  }
   const dim3 grid((M + MF_BM - 1) / MF_BM), block(MF_NT);
   set_max_lds<mlp_fused_kernel>(MF_LDS);
   hipLaunchKernelGGL(mlp_fused_kernel, grid, block, MF_LDS, st, (const __bf16*)X,
