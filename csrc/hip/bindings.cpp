@@ -55,6 +55,7 @@ int symb_gemm_fp8_config(int waves, int big);
 int symb_gemm_resln_config(int waves);
 int symb_gemm_gelu_config(int poly);
 int symb_gemm_gelu_poly();
+int symb_mlp_fused_vs(int vs);   // fused FFN ring fill: 0 LDS-DMA, 1 register staging; -1 query
 int symb_mlp_fused(const void* X, const void* W1, const float* b1, const void* W2, const float* b2,
                    const float* gamma, const float* beta, float eps, int gelu_poly, void* C, int M,
                    int H, int FF, hipStream_t st);
@@ -857,6 +858,7 @@ PYBIND11_MODULE(_hip, m) {
     if (mode < 0 || mode > 1) throw std::invalid_argument("mlp_fused_config: mode 0 or 1");
     g_mlp_fused = mode;
   });
+  m.def("mlp_fused_vs", [](int vs) { return symb_mlp_fused_vs(vs); }, py::arg("vs") = -1);
   m.def("gemm_gelu_config", [](int poly) { check(symb_gemm_gelu_config(poly), "gemm_gelu_config"); },
         py::arg("poly"));
   m.def("gemm_fp8_config", [](int waves, int big) {

@@ -255,12 +255,19 @@ def test_gemm_skinny_nw8_multi_split(M, N, K, epi):
     _close(eight, four, atol=2e-2, rtol=1e-2, what="8-wave vs 4-wave skinny")
 
 
+@pytest.mark.parametrize("vs", [0, 1])
 @pytest.mark.parametrize("M", [128, 1000, 4173, 32768])
-def test_mlp_fused(M):
+def test_mlp_fused(M, vs, request):
     """mlp_fused.hip (the whole 384-wide FFN block in one launch: 12 chunks of 128 intermediate
     columns through LDS, ragged last row block) == the fp32 oracle with the intermediate rounded
-    to bf16, and == the two-GEMM path it replaces, bit-exact on repeat."""
+    to bf16, and == the two-GEMM path it replaces, bit-exact on repeat.  vs: the ring filled by
+    LDS-DMA (0) or by register staging (1)."""
+    from codename_symbiont_amd.ops._ext import hip
     from codename_symbiont_amd.ops.kernels import EPI_GELU, EPI_RES_LN, gemm, mlp_fused
+
+    old = hip().mlp_fused_vs()
+    hip().mlp_fused_vs(vs)
+    request.addfinalizer(lambda: hip().mlp_fused_vs(old))
 
     x = torch.nn.functional.layer_norm(_f(M, 384, seed=21), (384,)).bfloat16()
     w1 = _bf(1536, 384, scale=1.0 / math.sqrt(384), seed=22)
