@@ -33,10 +33,10 @@ def main() -> None:
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--tier", choices=["i8", "mx4", "mx6"], default="i8")
     ap.add_argument("--queries", choices=["heldout", "self", "near"], default="heldout")
-    ap.add_argument("--variant", type=int, default=-1, help="stream MX-fp4 form (stream_config)")
     ap.add_argument("--ab", default="",
                     help="stream forms timed in one process, interleaved: comma list of "
-                         "mx4variant:i8variant:ablation[:land[:centroid]] (e.g. 0:0:0:1:1,0:0:0:1:0)")
+                         "ablation[:centroid] (ablation: stream_config; centroid 0 = the MX-fp4 "
+                         "centroid test off), e.g. 0:1,0:0")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--thr-add", type=float, default=0.0,
                     help="added to the scan's thresholds (e.g. 10: no row emits -- kernel-only timing)")
@@ -46,8 +46,6 @@ def main() -> None:
     from codename_symbiont_amd.ops._ext import hip, stream_handle
 
     h, st = hip(), stream_handle()
-    if a.variant >= 0:
-        h.stream_config(a.variant)
     gen = CorpusGen(a.corpus, a.dim, "cuda")
     shard = HbmIndexShard(a.dim, a.rows + 8192, device="cuda", prune="i8")
     t0 = time.perf_counter()
@@ -140,8 +138,8 @@ def main() -> None:
     for _ in range(a.rounds if a.ab else 1):
         for f in forms:
             if f is not None:
-                h.stream_config(*f[:4])
-                cent[0] = len(f) < 5 or bool(f[4])
+                h.stream_config(f[0])
+                cent[0] = len(f) < 2 or bool(f[1])
             scan()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -150,7 +148,7 @@ def main() -> None:
             torch.cuda.synchronize()
             times[f].append((time.perf_counter() - t0) * 1e3 / a.iters)
     if a.ab:
-        h.stream_config(0, 0, 0, 0)
+        h.stream_config(0)
     for f, ts in times.items():
         ms = sorted(ts)[len(ts) // 2]
         print(json.dumps({"bench": "scan_one", "kernel": kernel, "form": f, "rows": n, "nq": a.nq,

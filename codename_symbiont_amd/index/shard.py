@@ -144,7 +144,9 @@ MX4_DIMS = (384, 768, 1024)             # ... the MX-fp4 first tier (384-only on
 # 384 / 768 only)
 STREAM_DIMS = (384, 768, 1024)
 STREAM_SUB = 32                         # rows per sub-tile record of the stream images
-I8_RING_DIMS = ()                       # ... where the int8 tier runs the LDS-ring scan instead
+# ... where the int8 tier runs the LDS-ring scan (index_i8.hip) beside the stream fp4 tier: 100M x
+# 768 held-out 21.6 ms against 25.4 ms for the LDS-query stream form (profiles/r6_768/)
+I8_RING_DIMS = (768,)
 # widths of the MX-fp6 (e2m3) middle tier (stream scan only) and where SYMB_PRUNE_MX6=auto keeps
 # it: nowhere -- measured, it never applies (held-out queries leave ~70.8k candidates in its band
 # against a 32k cap, and self / near-duplicate queries take the fp4 tier: profiles/r5_lq/), so a
@@ -218,9 +220,9 @@ class HbmIndexShard:
         self.stream = bool(prune) and dim in STREAM_DIMS and os.environ.get(
             "SYMB_PRUNE_STREAM", "1") not in ("", "0")
         # the int8 tier's kernel, chosen apart from the fp4 tier's: "stream"
-        # = the fragment-major image (index_stream.hip, or its LDS-query form index_lq.hip at 768)
-        # or "ring" = the row-major image with per-row scales on the LDS-ring scan (index_i8.hip,
-        # round 4's I8Dim<768>); the MX-fp4 tier keeps its stream image either way.
+        # = the fragment-major image (index_stream.hip) or "ring" = the row-major image with
+        # per-row scales on the LDS-ring scan (index_i8.hip, round 4's I8Dim<768>); the MX-fp4
+        # tier keeps its stream image either way.
         # SYMB_PRUNE_I8=auto takes I8_RING_DIMS.
         i8k = os.environ.get("SYMB_PRUNE_I8", "auto").strip().lower()
         self.i8_ring = bool(self.stream and dim in (384, 768) and (

@@ -42,8 +42,6 @@ def hip():
 
     # SYMB_GPU_DEBUG=1: every kernel launch is synchronized and checked (fault attribution)
     mod.set_debug(debug_enabled())
-    if os.environ.get("SYMB_MLP_VS", ""):   # (A/B) the fused FFN block's ring fill
-        mod.mlp_fused_vs(int(os.environ["SYMB_MLP_VS"]))
     return mod
 
 

@@ -55,7 +55,6 @@ int symb_gemm_fp8_config(int waves, int big);
 int symb_gemm_resln_config(int waves);
 int symb_gemm_gelu_config(int poly);
 int symb_gemm_gelu_poly();
-int symb_mlp_fused_vs(int vs);   // fused FFN ring fill: 0 LDS-DMA, 1 register staging; -1 query
 int symb_mlp_fused(const void* X, const void* W1, const float* b1, const void* W2, const float* b2,
                    const float* gamma, const float* beta, float eps, int gelu_poly, void* C, int M,
                    int H, int FF, hipStream_t st);
@@ -94,7 +93,7 @@ int symb_mx4_select(int NQ, const float* T, const float* margin4, const float* m
 int symb_i8_tile_rows_for(int dim, int heavy);
 // the streaming pruning scan (index_stream.hip)
 int symb_stream_rec_bytes(int dim, int form);
-int symb_stream_config(int mx4_variant, int i8_variant, int abl, int land);
+int symb_stream_config(int abl);
 int symb_stream_geometry(int dim, int form, int* qpb, int* wgs_per_cu);
 int symb_index_scan_stream(const void* img, int n_valid, int alloc_rows, int rows_per_blk,
                            int n_rblk, const void* Q, const void* qsc, int NQ, const float* thr,
@@ -605,9 +604,8 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("gate_want") = 0);
   m.def("stream_rec_bytes", [](int dim, int form) { return symb_stream_rec_bytes(dim, form); },
         py::arg("dim"), py::arg("form"));
-  m.def("stream_config", [](int mx4_variant, int i8_variant, int abl, int land) {
-    check(symb_stream_config(mx4_variant, i8_variant, abl, land), "stream_config");
-  }, py::arg("mx4_variant"), py::arg("i8_variant") = 0, py::arg("abl") = 0, py::arg("land") = 0);
+  m.def("stream_config", [](int abl) { check(symb_stream_config(abl), "stream_config"); },
+        py::arg("abl") = 0);
   m.def("stream_geometry", [](int dim, int form) {
     int qpb = 0, wpc = 0;
     check(symb_stream_geometry(dim, form, &qpb, &wpc), "stream_geometry");
@@ -858,7 +856,6 @@ PYBIND11_MODULE(_hip, m) {
     if (mode < 0 || mode > 1) throw std::invalid_argument("mlp_fused_config: mode 0 or 1");
     g_mlp_fused = mode;
   });
-  m.def("mlp_fused_vs", [](int vs) { return symb_mlp_fused_vs(vs); }, py::arg("vs") = -1);
   m.def("gemm_gelu_config", [](int poly) { check(symb_gemm_gelu_config(poly), "gemm_gelu_config"); },
         py::arg("poly"));
   m.def("gemm_fp8_config", [](int waves, int big) {

@@ -66,33 +66,23 @@ struct SDim {
 };
 
 // Scan geometry: SETS 32-query sets per wave (resident B operands: SETS x NKS x 4 VGPRs), NW
-// waves per workgroup on the same rows, DEPTH sub-tiles in flight per wave.  V selects among the
-// measured forms (symb_stream_config): V = 0 the default of each (format, width).
-template <int FMT, int D, int V = 0>
+// waves per workgroup on the same rows, DEPTH sub-tiles in flight per wave.  MX-fp4 384: 256
+// queries per wave; the wider rows hold fewer resident sets (1024: int8 one set, 4 waves = 128
+// queries per workgroup).  (Round 5's A/B forms -- a 128-query MX-fp4 form, one sub-tile
+// deeper / shallower in flight, the 16 x 16 x 64 int8 MFMA shape and an LDS-landing ring --
+// measured slower or equal and were removed in round 6.)
+template <int FMT, int D>
 struct SGeo {
   static constexpr int NKS = SDim<FMT, D>::NKS;
-  // MX-fp4 384: 256 queries per wave (V 0) or 128 per wave, two waves per workgroup (V 1); the
-  // wider rows hold fewer resident sets (1024: int8 one set, 4 waves = 128 queries per workgroup).
-  // V 2 / 3: the default form one sub-tile deeper / shallower in flight (A/B); V 4 (int8): the
-  // 16 x 16 x 64 MFMA shape on the same image (see scan_stream_kernel I16).
-  static constexpr int SETS = FMT == SF_MX4 ? (D == 384 && V != 1 ? 8 : D == 1024 ? 2 : 4)
+  static constexpr int SETS = FMT == SF_MX4 ? (D == 384 ? 8 : D == 1024 ? 2 : 4)
                             : FMT == SF_MX6 ? (D == 384 ? 4 : 2)
                                             : (D == 384 ? 4 : D == 768 ? 2 : 1);
   static constexpr int NW0 = 256 / (SETS * 32) > 0 ? 256 / (SETS * 32) : 1;
   static constexpr int NW = NW0 > 4 ? 4 : NW0;
-  static constexpr int DEPTH0 = FMT == SF_MX4 ? 3 : 2;
-  static constexpr int DEPTH = V == 2 ? DEPTH0 + 1 : (V == 3 && DEPTH0 > 2 ? DEPTH0 - 1 : DEPTH0);
+  static constexpr int DEPTH = FMT == SF_MX4 ? 3 : 2;
   static constexpr int QPB = SETS * 32 * NW;                      // queries per workgroup
   static constexpr int STW = 512;                                 // staged candidates per wave
   static constexpr int STAGE = STW * 10;
-  // the LDS-landing form (LAND): each wave's sub-tiles arrive by LDS-DMA into a private ring of
-  // LDEPTH slots (no loop-carried fragment registers); sized for 2 workgroups of 2 waves (int8 /
-  // MX-fp4 768) or 4 of one wave (MX-fp4 384) per CU
-  static constexpr int LHDR = FMT == SF_I8 ? 256 : 0;   // the header's LDS bytes (DMA: 4 B x 64 lanes)
-  static constexpr int SLOT = (SDim<FMT, D>::REC - SDim<FMT, D>::HDR + LHDR + 1023) / 1024 * 1024;
-  static constexpr int LDEPTH = FMT == SF_MX4 && D == 384 ? 4 : 2;
-  static constexpr bool LAND_OK =
-      FMT != SF_MX6 && V != 4 && (D == 384 || (D == 768 && FMT == SF_MX4));
   static_assert(SETS * NKS * SDim<FMT, D>::LB / 4 <= 192, "resident query operands");
   static_assert(NW >= 1 && NW <= 4, "waves per workgroup");
 };
@@ -115,13 +105,8 @@ __device__ __forceinline__ float max16(const float (&v)[16]) {
 // Workgroup lb = (row block rb, query block qb); cand_n must be zeroed by the caller.
 // ABL (timing ablations, wrong results): 1 = no emission test (the accumulators kept live),
 // 2 = no sub-tile loads after the prologue (the first DEPTH sub-tiles re-used).
-// LAND: sub-tiles land in LDS by LDS-DMA (a per-wave ring, counted vmcnt, no barriers) and each is
-// read into ONE set of fragment registers right before its MFMAs -- the register ring's
-// loop-carried fragments made hipcc copy freshly loaded registers at the back edge, which waits
-// for the loads and serialised the prefetch (MX-fp4 scan 5.1 ms with loads vs 3.35 without,
-// profiles/r5_scan/).
-template <int FMT, int D, int V, int ABL = 0, int LAND = 0>
-__global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_kernel(
+template <int FMT, int D, int ABL = 0>
+__global__ __launch_bounds__((64 * SGeo<FMT, D>::NW), 1) void scan_stream_kernel(
     const uint8_t* __restrict__ img, int n_valid, int rows_per_blk, const uint8_t* __restrict__ Q,
     const uint32_t* __restrict__ qsc, int NQ, int n_qblk, int xcd, const float* __restrict__ thr_in,
     float* __restrict__ cand_s, int* __restrict__ cand_i, int* __restrict__ cand_n, int cap,
@@ -129,7 +114,7 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
     int* __restrict__ runs, const uint8_t* __restrict__ cent4, const uint32_t* __restrict__ centqs,
     const float* __restrict__ centR, const float* __restrict__ bounds4) {
   using S = SDim<FMT, D>;
-  using G = SGeo<FMT, D, V>;
+  using G = SGeo<FMT, D>;
   constexpr int NKS = S::NKS, NSC = S::NSC ? S::NSC : 1, REC = S::REC;
   constexpr int SETS = G::SETS, DEPTH = G::DEPTH, STW = G::STW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -160,35 +145,16 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
       return *reinterpret_cast<const i32x4s*>(p);
     }
   };
-  // I16 (int8, V 4): v_mfma_i32_16x16x64_i8 on the same image -- per set and sub-tile four 16 x 16
-  // blocks (row half rh, query half qh) of NKS / 2 64-deep k-steps: the A operand of lane l is
-  // row 16 rh + (l & 15), bytes 64 K + 16 (l >> 4), i.e. 16 bytes at 1024 (2 K + (l >> 5)) +
-  // 16 (32 ((l >> 4) & 1) + 16 rh + (l & 15)) of the record; the result of lane l is query
-  // 16 qh + (l & 15), rows 16 rh + 4 (l >> 4) + r.  qf[s][2 K + qh], fk[d][2 K + rh]; a lane's
-  // 16 values e = 8 rh + 4 qh + r.
-  constexpr bool I16 = FMT == SF_I8 && V == 4;
   FragT qf[SETS][NKS];
   uint32_t qs[SETS][NSC];
   float thr[SETS];
-  float thr2[SETS][2];   // (I16) the thresholds of the lane's two queries
 #pragma unroll
   for (int s = 0; s < SETS; ++s) {
     const int q = qw + 32 * s + (lane & 31);
     const int qq = min(q, NQ - 1);
     const uint8_t* qp = Q + (size_t)qq * S::RB + S::LB * h;
-    if constexpr (I16) {
 #pragma unroll
-      for (int qh = 0; qh < 2; ++qh) {
-        const int q2 = qw + 32 * s + 16 * qh + (lane & 15);
-        const uint8_t* qp2 = Q + (size_t)min(q2, NQ - 1) * S::RB + 16 * (lane >> 4);
-#pragma unroll
-        for (int K = 0; K < NKS / 2; ++K) qf[s][2 * K + qh] = *reinterpret_cast<const i32x4s*>(qp2 + 64 * K);
-        thr2[s][qh] = q2 < NQ ? thr_in[q2] : INFINITY;
-      }
-    } else {
-#pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) qf[s][ks] = frag_at(qp + 2 * S::LB * ks, 12);
-    }
+    for (int ks = 0; ks < NKS; ++ks) qf[s][ks] = frag_at(qp + 2 * S::LB * ks, 12);
 #pragma unroll
     for (int j = 0; j < NSC; ++j) {
       if constexpr (FMT != SF_I8)
@@ -245,8 +211,6 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
       }
     }
     nst = 0;
-    // (vmcnt counts these stores too: the landing ring's counted waits assume only DMAs pending)
-    if constexpr (LAND) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
 
   // ---- the sub-tile ring: fragments (+ row scales / block scales) of DEPTH sub-tiles ----
@@ -259,18 +223,9 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
     const uint8_t* r = rec0 + (size_t)min(i, ns - 1) * REC;   // (past the end: the last again)
     if constexpr (FMT == SF_I8) fts[d] = *reinterpret_cast<const float*>(r);
     // (MX-fp6: lane l's 24 bytes are 12 in the k-step's first 768-byte plane and 12 in its second)
-    if constexpr (I16) {
-      const uint8_t* f = r + S::HDR + 1024 * (lane >> 5) + 16 * (32 * ((lane >> 4) & 1) + (lane & 15));
+    const uint8_t* f = r + S::HDR + (FMT == SF_MX6 ? 12 : 16) * lane;
 #pragma unroll
-      for (int K = 0; K < NKS / 2; ++K)
-#pragma unroll
-        for (int rh = 0; rh < 2; ++rh)
-          fk[d][2 * K + rh] = *reinterpret_cast<const i32x4s*>(f + 2048 * K + 256 * rh);
-    } else {
-      const uint8_t* f = r + S::HDR + (FMT == SF_MX6 ? 12 : 16) * lane;
-#pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) fk[d][ks] = frag_at(f + 64 * S::LB * ks, 768);
-    }
+    for (int ks = 0; ks < NKS; ++ks) fk[d][ks] = frag_at(f + 64 * S::LB * ks, 768);
     if constexpr (FMT != SF_I8) {
 #pragma unroll
       for (int j = 0; j < NSC; ++j)
@@ -282,19 +237,7 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
   auto acc_i8 = [&](auto dc, auto sc) {
     constexpr int d = decltype(dc)::value, s = decltype(sc)::value;
     i32x16s acc = {};
-    if constexpr (I16) {
-      i32x4s c[2][2] = {};
-#pragma unroll
-      for (int K = 0; K < NKS / 2; ++K)
-#pragma unroll
-        for (int rh = 0; rh < 2; ++rh)
-#pragma unroll
-          for (int qh = 0; qh < 2; ++qh)
-            c[rh][qh] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fk[d][2 * K + rh], qf[s][2 * K + qh],
-                                                             c[rh][qh], 0, 0, 0);
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[e] = c[e >> 3][(e >> 2) & 1][e & 3];
-    } else if constexpr (FMT == SF_I8) {
+    if constexpr (FMT == SF_I8) {
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks)
         acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(fk[d][ks], qf[s][ks], acc, 0, 0, 0);
@@ -382,14 +325,7 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
       static_for<0, SETS>([&](auto sc) {
         constexpr int s = decltype(sc)::value;
         if (!((pass >> s) & 1u)) return;
-        if constexpr (I16) {   // each query half against its own threshold
-          const i32x16s acc = acc_i8(dc, sc);
-          const int m0 = max(max(max(acc[0], acc[1]), max(acc[2], acc[3])),
-                             max(max(acc[8], acc[9]), max(acc[10], acc[11])));
-          const int m1 = max(max(max(acc[4], acc[5]), max(acc[6], acc[7])),
-                             max(max(acc[12], acc[13]), max(acc[14], acc[15])));
-          hm |= ((float)m0 * fts[d] >= thr2[s][0] || (float)m1 * fts[d] >= thr2[s][1] ? 1u : 0u) << s;
-        } else if constexpr (FMT == SF_I8) {   // (the sub-tile's scale > 0 keeps the order)
+        if constexpr (FMT == SF_I8) {   // (the sub-tile's scale > 0 keeps the order)
           const i32x16s acc = acc_i8(dc, sc);
           int m = max(max(acc[0], acc[1]), acc[2]);
 #pragma unroll
@@ -411,18 +347,9 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
         block(dc, sc, v);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          int row, ql;
-          float t;
-          if constexpr (I16) {
-            row = (g0 + i) * 32 + 16 * (r >> 3) + 4 * (lane >> 4) + (r & 3);
-            ql = 32 * s + 16 * ((r >> 2) & 1) + (lane & 15);
-            t = thr2[s][(r >> 2) & 1];
-          } else {
-            row = row0 + (r & 3) + 8 * (r >> 2);
-            ql = 32 * s + (lane & 31);
-            t = thr[s];
-          }
-          const bool p = v[r] >= t && row < row_end;
+          const int row = row0 + (r & 3) + 8 * (r >> 2);
+          const int ql = 32 * s + (lane & 31);
+          const bool p = v[r] >= thr[s] && row < row_end;
           const uint64_t m = __builtin_amdgcn_ballot_w64(p);
           if (m) {
             if (nst > STW - 64) flush();
@@ -440,56 +367,6 @@ __global__ __launch_bounds__((64 * SGeo<FMT, D, V>::NW), 1) void scan_stream_ker
     }
   };
 
-  if constexpr (LAND) {
-    static_assert(G::LAND_OK, "landing ring sized for this form");
-    constexpr int SLOT = G::SLOT, LD = G::LDEPTH;
-    constexpr int NDMA = NKS + (FMT == SF_I8 ? 1 : NSC);   // DMA instructions per sub-tile
-    char* ring = smem + G::NW * G::STAGE + wave * (LD * SLOT);
-    // (asm DMAs: the builtin's LDS-DMA made hipcc wait vmcnt(0) before every ds_read of the ring,
-    // as it cannot tell the slots apart -- that serialised the prefetch again)
-    auto dma = [&](int i, int slot) {   // sub-tile i (past the end: the last again) into slot
-      const uint8_t* r = rec0 + (size_t)min(i, ns - 1) * REC;
-      const uint32_t dst = lds_addr(ring) + slot * SLOT;
-      // the 16-byte scale header: 4 bytes per lane (an LDS-DMA lands lane l at base + 4 l), the
-      // 64 lanes repeating it over LDS bytes 0..255
-      if constexpr (FMT == SF_I8) dma4_asm(r + 4 * (lane & 3), dst);
-#pragma unroll
-      for (int ks = 0; ks < NKS; ++ks)
-        dma16_asm(r + S::HDR + 1024 * ks + 16 * lane, dst + G::LHDR + 1024 * ks);
-      if constexpr (FMT == SF_MX4) {
-#pragma unroll
-        for (int j = 0; j < NSC; ++j) dma4_asm(r + S::FRAG + 256 * j + 4 * lane, dst + S::FRAG + 256 * j);
-      }
-    };
-    auto fetch = [&](int slot) {
-      const char* src = ring + slot * SLOT;
-      if constexpr (FMT == SF_I8) fts[0] = *reinterpret_cast<const float*>(src);
-#pragma unroll
-      for (int ks = 0; ks < NKS; ++ks)
-        fk[0][ks] = *reinterpret_cast<const i32x4s*>(src + G::LHDR + 1024 * ks + 16 * lane);
-      if constexpr (FMT == SF_MX4) {
-#pragma unroll
-        for (int j = 0; j < NSC; ++j)
-          fsc[0][j] = *reinterpret_cast<const uint32_t*>(src + S::FRAG + 256 * j + 4 * lane);
-      }
-    };
-    // the queries (and thresholds) landed before any DMA -- as the builtin, so that hipcc's own
-    // wait bookkeeping sees it (else it keeps the query loads "pending" into the loop and its
-    // counted waits for them drain the DMAs every sub-tile)
-    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) expcnt(7) lgkmcnt(15)
-    for (int d = 0; d < LD; ++d) dma(d, d);
-    for (int i = 0; i < ns; ++i) {
-      const int slot = i % LD;
-      // sub-tile i landed: only the LD - 1 younger sub-tiles' DMAs may still be in flight
-      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NDMA * (LD - 1)) : "memory");
-      fetch(slot);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // (slot read: refill it)
-      if (ABL != 2) dma(i + LD, slot);
-      process(std::integral_constant<int, 0>(), i);
-    }
-    if (nst) flush();
-    return;
-  }
   // prologue: DEPTH sub-tiles in flight, then use one / refill its slot
   static_for<0, DEPTH>([&](auto dc) { load(dc, decltype(dc)::value); });
   // (the last round may run past ns: those slots re-read the last sub-tile and emit nothing, as
@@ -969,63 +846,36 @@ int symb_stream_rec_bytes(int dim, int form) {
   return 0;
 }
 
-// scan forms (symb_stream_config, A/B): variant 0 = default, 1 = MX-fp4 384 with 128 queries per
-// wave x 2 waves, 2 / 3 = one sub-tile deeper / shallower in flight (register ring, D = 384),
-// int8 4 = the 16 x 16 x 64 MFMA shape, int8 5 / 6 = the LDS-query scan's forms (index_lq.hip);
-// abl: the kernel's timing ablations (ABL above; wrong results); land: the LDS-landing form where
-// it is sized (int8 / MX-fp4 384, MX-fp4 768; variant 0)
-static int g_stream_mx4_v = 0, g_stream_i8_v = 0, g_stream_abl = 0, g_stream_land = 0;
-int symb_stream_config(int mx4_variant, int i8_variant, int abl, int land) {
-  if (mx4_variant < 0 || mx4_variant > 3 || i8_variant < 0 || i8_variant > 6 || i8_variant == 1 ||
-      abl < 0 || abl > 2 || land < 0 || land > 1)
-    return -1;
-  g_stream_mx4_v = mx4_variant;
-  g_stream_i8_v = i8_variant;
+// the kernel's timing ablations (ABL above; wrong results) for benchmarks (symb_stream_config)
+static int g_stream_abl = 0;
+int symb_stream_config(int abl) {
+  if (abl < 0 || abl > 2) return -1;
   g_stream_abl = abl;
-  g_stream_land = land;
   return 0;
-}
-
-// the LDS-query int8 scan (index_lq.hip): i8 variants 5 / 6 = its forms 0 / 1
-int symb_lq_qpb(int dim);
-int symb_index_scan_lq(const void* img, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
-                       int NQ, const float* thr, float* cand_s, int* cand_i, int* cand_n, int cap,
-                       hipStream_t st, const int* skip, int dim, const int* gate, int gate_want,
-                       int* runs, int form);
-// (the default int8 form at D = 768: 100M x 768 held-out 37.8 -> 25.1 ms, profiles/r5_lq/)
-static bool lq_on(int dim, int form) {
-  return form == 0 && (g_stream_i8_v >= 5 || (g_stream_i8_v == 0 && dim == 768)) &&
-         symb_lq_qpb(dim) > 0;
 }
 
 // queries per workgroup and workgroups per CU (one wave per SIMD) of the stream scan
 int symb_stream_geometry(int dim, int form, int* qpb, int* wgs_per_cu) {
-  if (lq_on(dim, form)) {
-    *qpb = symb_lq_qpb(dim);
-    *wgs_per_cu = 1;
-    return 0;
-  }
-#define G_(F, D_, V_)                                \
+#define G_(F, D_)                                    \
   do {                                               \
-    *qpb = SGeo<F, D_, V_>::QPB;                     \
-    *wgs_per_cu = 4 / SGeo<F, D_, V_>::NW;           \
+    *qpb = SGeo<F, D_>::QPB;                         \
+    *wgs_per_cu = 4 / SGeo<F, D_>::NW;               \
     return 0;                                        \
   } while (0)
   if (dim == 384) {
-    if (form == 2) G_(SF_MX6, 384, 0);
-    if (form && g_stream_mx4_v == 1) G_(SF_MX4, 384, 1);
-    if (form) G_(SF_MX4, 384, 0);
-    G_(SF_I8, 384, 0);
+    if (form == 2) G_(SF_MX6, 384);
+    if (form) G_(SF_MX4, 384);
+    G_(SF_I8, 384);
   }
   if (dim == 768) {
-    if (form == 2) G_(SF_MX6, 768, 0);
-    if (form) G_(SF_MX4, 768, 0);
-    G_(SF_I8, 768, 0);
+    if (form == 2) G_(SF_MX6, 768);
+    if (form) G_(SF_MX4, 768);
+    G_(SF_I8, 768);
   }
   if (form == 2) return -1;
   if (dim == 1024) {
-    if (form) G_(SF_MX4, 1024, 0);
-    G_(SF_I8, 1024, 0);
+    if (form) G_(SF_MX4, 1024);
+    G_(SF_I8, 1024);
   }
 #undef G_
   return -1;
@@ -1038,16 +888,16 @@ struct CentArgs {   // the MX-fp4 centroid test's inputs (all nullptr: off)
   const float* b4;
 };
 
-template <int F, int D, int V, int ABL = 0, int LAND = 0>
+template <int F, int D, int ABL = 0>
 static int launch_stream(const void* img, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                          const void* qsc, int NQ, const float* thr, float* cand_s, int* cand_i,
                          int* cand_n, int cap, int xcd, hipStream_t st, const int* skip,
                          const int* gate, int gate_want, int* runs, CentArgs ca) {
-  using G = SGeo<F, D, V>;
+  using G = SGeo<F, D>;
   const int n_qblk = (NQ + G::QPB - 1) / G::QPB;
-  constexpr int lds = G::STAGE * G::NW + (LAND ? G::NW * G::LDEPTH * G::SLOT : 0);
-  if (lds > 64 * 1024) set_max_lds<scan_stream_kernel<F, D, V, ABL, LAND>>(lds);
-  hipLaunchKernelGGL((scan_stream_kernel<F, D, V, ABL, LAND>), dim3(n_rblk * n_qblk), dim3(64 * G::NW), lds,
+  constexpr int lds = G::STAGE * G::NW;
+  if (lds > 64 * 1024) set_max_lds<scan_stream_kernel<F, D, ABL>>(lds);
+  hipLaunchKernelGGL((scan_stream_kernel<F, D, ABL>), dim3(n_rblk * n_qblk), dim3(64 * G::NW), lds,
                      st, (const uint8_t*)img, n_valid, rows_per_blk, (const uint8_t*)Q,
                      (const uint32_t*)qsc, NQ, n_qblk, xcd, thr, cand_s, cand_i, cand_n, cap, skip,
                      gate, gate_want, runs, (const uint8_t*)ca.c4, (const uint32_t*)ca.cqs, ca.R,
@@ -1081,45 +931,14 @@ int symb_index_scan_stream(const void* img, int n_valid, int alloc_rows, int row
     hipError_t e = hipMemsetAsync(cand_n, 0, sizeof(int) * (size_t)NQ, st);
     if (e != hipSuccess) return (int)e;
   }
-#define L(F, D_, V_) launch_stream<F, D_, V_>(img, n_valid, rows_per_blk, n_rblk, Q, qsc, NQ, thr, \
+#define L(F, D_, A_) launch_stream<F, D_, A_>(img, n_valid, rows_per_blk, n_rblk, Q, qsc, NQ, thr, \
                                               cand_s, cand_i, cand_n, cap, xcd, st, skip, gate,   \
                                               gate_want, runs, ca)
-  const bool land = g_stream_land && (form == 0 ? g_stream_i8_v == 0 : g_stream_mx4_v == 0);
-#define LA(F, D_, A_, L_) launch_stream<F, D_, 0, A_, L_>(img, n_valid, rows_per_blk, n_rblk, Q, qsc, \
-                                                          NQ, thr, cand_s, cand_i, cand_n, cap, xcd, \
-                                                          st, skip, gate, gate_want, runs, ca)
-  if (lq_on(dim, form))
-    return symb_index_scan_lq(img, n_valid, rows_per_blk, n_rblk, Q, NQ, thr, cand_s, cand_i,
-                              cand_n, cap, st, skip, dim, gate, gate_want, runs,
-                              g_stream_i8_v >= 5 ? g_stream_i8_v - 5 : 0);
-  if (form == 2) return dim == 384 ? L(SF_MX6, 384, 0) : L(SF_MX6, 768, 0);
-  if (dim == 768 && form == 1 && land) return LA(SF_MX4, 768, 0, 1);
-  if (dim == 384) {
-    if (g_stream_abl == 1)
-      return form ? (land ? LA(SF_MX4, 384, 1, 1) : LA(SF_MX4, 384, 1, 0))
-                  : (land ? LA(SF_I8, 384, 1, 1) : LA(SF_I8, 384, 1, 0));
-    if (g_stream_abl == 2)
-      return form ? (land ? LA(SF_MX4, 384, 2, 1) : LA(SF_MX4, 384, 2, 0))
-                  : (land ? LA(SF_I8, 384, 2, 1) : LA(SF_I8, 384, 2, 0));
-    if (land) return form ? LA(SF_MX4, 384, 0, 1) : LA(SF_I8, 384, 0, 1);
-    if (form) {
-      switch (g_stream_mx4_v) {
-        case 1: return L(SF_MX4, 384, 1);
-        case 2: return L(SF_MX4, 384, 2);
-        case 3: return L(SF_MX4, 384, 3);
-        default: return L(SF_MX4, 384, 0);
-      }
-    }
-    switch (g_stream_i8_v) {
-      case 2: return L(SF_I8, 384, 2);
-      case 3: return L(SF_I8, 384, 3);
-      case 4: return L(SF_I8, 384, 4);
-      default: return L(SF_I8, 384, 0);
-    }
-  }
-  if (dim == 768) return form ? L(SF_MX4, 768, 0) : L(SF_I8, 768, 0);
-  return form ? L(SF_MX4, 1024, 0) : L(SF_I8, 1024, 0);
-#undef LA
+#define LD(F, D_) (g_stream_abl == 1 ? L(F, D_, 1) : g_stream_abl == 2 ? L(F, D_, 2) : L(F, D_, 0))
+  if (dim == 384) return form == 2 ? LD(SF_MX6, 384) : form ? LD(SF_MX4, 384) : LD(SF_I8, 384);
+  if (dim == 768) return form == 2 ? LD(SF_MX6, 768) : form ? LD(SF_MX4, 768) : LD(SF_I8, 768);
+  return form ? LD(SF_MX4, 1024) : LD(SF_I8, 1024);
+#undef LD
 #undef L
 }
 

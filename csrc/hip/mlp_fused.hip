@@ -57,10 +57,6 @@ __device__ __forceinline__ int mf_swz(int row, int chunk) {
 // fragments, LayerNorm across the 4 lanes of a token, only the weights through a 3-slot LDS ring:
 // exact, but 1.56-1.60 ms per MiniLM forward against 1.25-1.27 with this kernel (24 VGPRs
 // spilled, reloads draining the ring), so it was removed: profiles/r6_gemm/README.md.)
-// VS = true: the ring is filled by register staging (global_load_dwordx4 of step q + 1 issued
-// before step q's MFMAs, ds_write_b128 after them) instead of LDS-DMA, whose issue cost (~60-185
-// cycles per 1 KiB piece beside MFMAs, MI355X_MICROARCH.md) is paid by the computing waves.
-template <bool VS>
 __global__ __launch_bounds__(MF_NT) void mlp_fused_kernel(
     const __bf16* X, const __bf16* __restrict__ W1, const float* __restrict__ b1,
     const __bf16* __restrict__ W2, const float* __restrict__ b2, const float* __restrict__ gamma,
@@ -76,11 +72,11 @@ __global__ __launch_bounds__(MF_NT) void mlp_fused_kernel(
   char* hc = smem + MF_HC;
 
   // step q of the whole sequence -> (chunk, phase step) into slot q & 1: piece p of the step (a
-  // 16-byte swizzled chunk per lane, global source src(p), lane-linear LDS position dst(p)).
-  // DMA form: one global_load_lds per piece; VS form: gl[p] = *src(p) now, *dst(p) = gl[p] later
-  constexpr int NPA = 2 * MF_KA * (MF_BM * 8) / MF_NT;   // phase-A pieces per lane (8)
+  // 16-byte swizzled chunk per lane, global source src(p), lane-linear LDS position dst(p)), one
+  // global_load_lds each.  (Register staging -- global_load_dwordx4 of step q + 1 before step
+  // q's MFMAs, ds_write_b128 after them -- measured slower: MiniLM forward 1.32-1.33 vs
+  // 1.26-1.27 ms, profiles/r6_gemm/README.md.)
   constexpr int NPB = (MF_H * 8) / MF_NT;                // phase-B pieces per lane (6)
-  u32x4 gl[VS ? NPA : 1];
   auto piece = [&](int q, auto fn) {
     const int c = q / STEPS, s = q % STEPS;
     char* base = smem + (q & 1) * MF_SLOT;
@@ -117,16 +113,8 @@ __global__ __launch_bounds__(MF_NT) void mlp_fused_kernel(
       }
     }
   };
-  auto stage = [&](int q) {   // DMA form: issue step q's pieces
+  auto stage = [&](int q) {
     piece(q, [&](int, const char* src, char* dst) { glds16(src, dst); });
-  };
-  auto gload = [&](int q) {   // VS form: step q's pieces into registers
-    piece(q, [&](int p, const char* src, char*) { gl[p] = *reinterpret_cast<const u32x4*>(src); });
-  };
-  auto gstore = [&](int q) {  // ... and from registers into the slot
-    piece(q, [&](int p, const char*, char* dst) {
-      *reinterpret_cast<u32x4*>(dst + lane * 16) = gl[p];
-    });
   };
 
   f32x4 acc[2][12];                                  // out rows wm*32 + 16i, cols wn*192 + 16j
@@ -136,21 +124,11 @@ __global__ __launch_bounds__(MF_NT) void mlp_fused_kernel(
     for (int j = 0; j < 12; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int r16 = lane & 15, g4 = lane >> 4;
-  // step q landed; every wave is done with slot (q+1)&1 and with H_c's writes / reads.  VS: the
-  // next step's loads go out now and are written to LDS by step_end after this step's MFMAs
+  // step q landed; every wave is done with slot (q+1)&1 and with H_c's writes / reads
   auto step_begin = [&](int q) {
-    if constexpr (!VS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (q + 1 < NCHUNK * STEPS) {
-      if constexpr (VS)
-        gload(q + 1);
-      else
-        stage(q + 1);
-    }
-  };
-  auto step_end = [&](int q) {
-    if constexpr (VS)
-      if (q + 1 < NCHUNK * STEPS) gstore(q + 1);
+    if (q + 1 < NCHUNK * STEPS) stage(q + 1);
   };
   // LayerNorm(acc + bias + R) of the block's 128 rows -> out (bf16); the fp32 tile is staged
   // through LDS (all of it may be overwritten) in two 64-row passes
@@ -204,12 +182,7 @@ __global__ __launch_bounds__(MF_NT) void mlp_fused_kernel(
   }
   };
 
-  if constexpr (VS) {
-    gload(0);
-    gstore(0);
-  } else {
-    stage(0);
-  }
+  stage(0);
   int q = 0;
 #pragma unroll 1
   for (int c = 0; c < NCHUNK; ++c) {
@@ -241,7 +214,6 @@ __global__ __launch_bounds__(MF_NT) void mlp_fused_kernel(
           for (int j = 0; j < 4; ++j)
             ha[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], ha[i][j], 0, 0, 0);
       }
-      step_end(q);
     }
     // H_c = GELU(. + b1) -> bf16 into the swizzled 2-k-tile image.  The MFMA operands are
     // swapped (W1_c rows first), so accumulator (i, j) holds H_c^T: lane element e is token row
@@ -299,7 +271,6 @@ __global__ __launch_bounds__(MF_NT) void mlp_fused_kernel(
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b, acc[i][j], 0, 0, 0);
         }
       }
-      step_end(q);
     }
   }
 
@@ -313,15 +284,6 @@ __global__ __launch_bounds__(MF_NT) void mlp_fused_kernel(
 
 using namespace symb;
 
-// Ring fill of the fused FFN block: 0 = LDS-DMA, 1 = register staging (mlp_fused_kernel VS).
-static int g_mlp_vs = 0;
-int symb_mlp_fused_vs(int vs) {
-  if (vs < 0) return g_mlp_vs;
-  if (vs > 1) return -1;
-  g_mlp_vs = vs;
-  return 0;
-}
-
 // The whole FFN block of a 384-wide layer in one launch (X, C: [M, 384] bf16, row stride 384;
 // C must not alias X).  Returns 0, a HIP error, or -1 (shape not supported).
 int symb_mlp_fused(const void* X, const void* W1, const float* b1, const void* W2, const float* b2,
@@ -330,15 +292,8 @@ int symb_mlp_fused(const void* X, const void* W1, const float* b1, const void* W
   if (M <= 0) return 0;
   if (H != MF_H || FF != MF_FF || X == C) return -1;
   const dim3 grid((M + MF_BM - 1) / MF_BM), block(MF_NT);
-  if (g_mlp_vs) {
-    set_max_lds<mlp_fused_kernel<true>>(MF_LDS);
-    hipLaunchKernelGGL(mlp_fused_kernel<true>, grid, block, MF_LDS, st, (const __bf16*)X,
-                       (const __bf16*)W1, b1, (const __bf16*)W2, b2, gamma, beta, eps, gelu_poly,
-                       (__bf16*)C, M);
-    return (int)hipGetLastError();
-  }
-  set_max_lds<mlp_fused_kernel<false>>(MF_LDS);
-  hipLaunchKernelGGL(mlp_fused_kernel<false>, grid, block, MF_LDS, st, (const __bf16*)X,
+  set_max_lds<mlp_fused_kernel>(MF_LDS);
+  hipLaunchKernelGGL(mlp_fused_kernel, grid, block, MF_LDS, st, (const __bf16*)X,
                      (const __bf16*)W1, b1, (const __bf16*)W2, b2, gamma, beta, eps, gelu_poly,
                      (__bf16*)C, M);
   return (int)hipGetLastError();

@@ -255,19 +255,12 @@ def test_gemm_skinny_nw8_multi_split(M, N, K, epi):
     _close(eight, four, atol=2e-2, rtol=1e-2, what="8-wave vs 4-wave skinny")
 
 
-@pytest.mark.parametrize("vs", [0, 1])
 @pytest.mark.parametrize("M", [128, 1000, 4173, 32768])
-def test_mlp_fused(M, vs, request):
+def test_mlp_fused(M):
     """mlp_fused.hip (the whole 384-wide FFN block in one launch: 12 chunks of 128 intermediate
     columns through LDS, ragged last row block) == the fp32 oracle with the intermediate rounded
-    to bf16, and == the two-GEMM path it replaces, bit-exact on repeat.  vs: the ring filled by
-    LDS-DMA (0) or by register staging (1)."""
-    from codename_symbiont_amd.ops._ext import hip
+    to bf16, and == the two-GEMM path it replaces, bit-exact on repeat."""
     from codename_symbiont_amd.ops.kernels import EPI_GELU, EPI_RES_LN, gemm, mlp_fused
-
-    old = hip().mlp_fused_vs()
-    hip().mlp_fused_vs(vs)
-    request.addfinalizer(lambda: hip().mlp_fused_vs(old))
 
     x = torch.nn.functional.layer_norm(_f(M, 384, seed=21), (384,)).bfloat16()
     w1 = _bf(1536, 384, scale=1.0 / math.sqrt(384), seed=22)
@@ -1008,30 +1001,25 @@ def test_append_rows_writes_rows_and_both_images(D):
     _close(b6[0], b6[1], atol=0, rtol=1e-6, what="append fp6 bounds")
 
 
-@pytest.mark.parametrize("form,D,i8v", [(0, 384, 0), (1, 384, 0), (0, 768, 0), (1, 768, 0),
-                                        (0, 384, 5), (0, 768, 2),
-                                        (0, 1024, 0), (1, 1024, 0), (2, 384, 0), (2, 768, 0),
-                                        (0, 384, 4)])
-def test_index_scan_stream_emits_the_bound_set(form, D, i8v, monkeypatch, request):
+@pytest.mark.parametrize("form,D", [(0, 384), (1, 384), (0, 768), (1, 768), (0, 1024), (1, 1024),
+                                    (2, 384), (2, 768)])
+def test_index_scan_stream_emits_the_bound_set(form, D, monkeypatch):
     """index_stream.hip scan_stream_kernel (v_mfma_i32_32x32x32_i8 / v_mfma_scale_f32_32x32x64
     on fragment-major images, one wave per SIMD): exactly the rows whose estimate (int8: (q8 .
     x8) sx, MX-fp4: the decoded dot) reaches the threshold, for 1, 2 and 3 query blocks, a ragged
     row count and skipped row blocks -- pins the fragment layout, the accumulator row map, the
-    row-scale header and the block-scale bytes' lane / k-step mapping.  i8v 4: the int8 scan on
-    the 16 x 16 x 64 MFMA shape (stream_config i8 variant 4) over the same image; i8v 5 at 384
-    and the default at 768: the LDS-query int8 scan (index_lq.hip); i8v 2 at 768: the
-    register-resident stream scan."""
+    row-scale header and the block-scale bytes' lane / k-step mapping (at 768 the int8 stream
+    image is the SYMB_PRUNE_I8=stream form; the default there is the LDS-ring scan)."""
     from codename_symbiont_amd.index.shard import HbmIndexShard
     from codename_symbiont_amd.ops._ext import hip, stream_handle
 
     n = 200_000 + 77
     monkeypatch.setenv("SYMB_PRUNE_MX6", "1" if form == 2 else "0")
+    monkeypatch.setenv("SYMB_PRUNE_I8", "stream")
     shard = HbmIndexShard(D, n + 4096, prune="i8")
     shard.fill_random(n, seed=5)
     assert shard.stream and (shard.img_i8 is not None) and (shard.img_mx4 is not None)
     h, st = hip(), stream_handle(shard.device)
-    h.stream_config(0, i8v)
-    request.addfinalizer(lambda: h.stream_config(0, 0))
     if form == 0:
         x8, sx = R.stream_i8_decode(shard.img_i8[:(n + 31) // 32], n, D)
         img = shard.img_i8
