@@ -141,9 +141,9 @@ OPTS = {
     "search_pipeline": (1, int, "--mode full: run batch i+1's query-side search work under "
                                 "batch i's scan on a third stream"),
     "encode_ahead": (2, int, "pipelined step: batch i + AHEAD is encoded during step i (1 | 2)"),
-    "scan_after_encode": (1, int, "pipelined step (AHEAD 2): batch i's scan waits for batch i + 1's "
-                                  "encoder, so the scan never starves an encoder that batch "
-                                  "i + 1's pre-pass waits on (0: the round-5 order, A/B)"),
+    "scan_after_encode": (0, int, "pipelined step (AHEAD 2): 1 = batch i's scan waits for batch "
+                                  "i + 1's encoder (measured slower: 49.0k vs 50.2k at N = 1, "
+                                  "equal at simulate_world=8, profiles/r6_step/)"),
     "graph": (1, int, "--mode embed: replay a captured hipGraph of the encoder forward"),
     "prune_sample_shift": (0, int, "exact pruned search: threshold sample = 1 tile in 2^shift "
                                    "(0 = the shard default)"),
@@ -798,10 +798,8 @@ def run_gpu(args, info, comm) -> int:
         t2 = time.perf_counter()
         compute.wait_event(pre_done[slot])
         if AHEAD == 2 and args.scan_after_encode:
-            # batch i + 1's encoder (enqueued a step ago) finishes BEFORE batch i's scan holds
-            # every SIMD: its pre-pass then runs at the start of the next gap beside batch i + 2's
-            # encoder, instead of after the remainder of its own encoder (the round-5 critical
-            # path: encoder remainder + pre-pass, profiles/r6_step/)
+            # (A/B) batch i + 1's encoder finishes before batch i's scan holds every SIMD; measured
+            # slower than letting the scan start first (profiles/r6_step/)
             compute.wait_event(enc_done[(i + 1) % NO])
         if ev:
             ev[2].record(compute)

@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""Repeat the fp8 (e4m3) list scan of config #5 (index_fp8.hip) on one shard -- the target of
+rocprofv3 --pmc passes (benchmarks/pmc_kernel.py --match index_scan_fp8).
+
+    python benchmarks/fp8_one.py [--rows 25000000] [--dim 1024] [--nq 256] [--variant 0] [--iters 10]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=25_000_000)
+    ap.add_argument("--dim", type=int, default=1024)
+    ap.add_argument("--nq", type=int, default=256)
+    ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--seed-threshold", type=int, default=1)
+    ap.add_argument("--iters", type=int, default=10)
+    a = ap.parse_args()
+    from codename_symbiont_amd.index.shard import HbmIndexShard
+
+    shard = HbmIndexShard(a.dim, a.rows, device="cuda", dtype="fp8")
+    shard.fill_random(a.rows, seed=1)
+    shard.scan_variant, shard.seed_threshold = a.variant, bool(a.seed_threshold)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    q = torch.nn.functional.normalize(torch.randn(a.nq, a.dim, device="cuda", generator=g),
+                                      dim=-1).bfloat16()
+    shard.search(q, 10)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.iters):
+        shard.search(q, 10)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / a.iters * 1e3
+    print(json.dumps({"bench": "fp8_one", "rows": a.rows, "dim": a.dim, "nq": a.nq,
+                      "variant": a.variant, "ms": round(ms, 3),
+                      "GBps": round(a.rows * a.dim / (ms / 1e3) / 1e9)}))
+
+
+if __name__ == "__main__":
+    main()

@@ -36,6 +36,10 @@ def main():
                 waits.append((s - max(p[1] for p in prev)) / 1e3)
     out = {"scans": len(scans), "collective_kernels": len(coll),
            "started_during_a_scan": inside, "started_outside_scans": after,
+           # start of each outside-scan collective after the last scan ended (a few us: it was
+           # issued under the scan and waited for it)
+           "start_after_scan_end_us": [round(w, 1) for w in waits],
+           "collective_us": [round((e - s) / 1e3, 1) for s, e, _ in coll],
            "collective_us_mean": round(sum(e - s for s, e, _ in coll) / max(1, len(coll)) / 1e3, 2),
            "names": sorted({re.sub(r"\(.*", "", n)[:80] for _, _, n in coll})}
     print(json.dumps(out, indent=1))

@@ -103,20 +103,35 @@ class Subscription:
             raise StopAsyncIteration
         return m
 
-    async def next_batch(self, max_n: int = 256, align: int = 0) -> list[Msg] | None:
+    async def next_batch(self, max_n: int = 256, align: int = 0, fill: int = 0,
+                         fill_until=None) -> list[Msg] | None:
         """Wait for one message, then take whatever else is already queued (up to ``max_n``);
         None once the subscription has ended.
 
         ``align`` > 0: when more than ``align`` messages are ready, take a whole multiple of it
         and leave the rest queued for the next call -- a consumer whose unit of work is a block
         of ``align`` items (the index scan's 256-query block) then never pays a whole extra
-        block for a few stragglers; a burst of ``align`` or fewer is taken whole (latency)."""
+        block for a few stragglers; a burst of ``align`` or fewer is taken whole (latency).
+
+        ``fill`` > 0 with ``fill_until`` (a callable returning a loop-clock deadline or None):
+        after the first message, keep waiting until ``fill`` messages are ready or the deadline
+        passes -- a consumer whose device is busy anyway (a scan in flight) collects a full
+        block instead of launching a partial one that costs as much."""
         if self._closed and self._q.empty():
             return None
         m = await self._q.get()
         if m is None:
             return None
         batch = [m]
+        if fill > 1 and fill_until is not None and 1 + self._q.qsize() < fill:
+            deadline = fill_until()
+            loop = asyncio.get_running_loop()
+            while deadline is not None and 1 + self._q.qsize() < fill:
+                left = deadline - loop.time()
+                if left <= 0:
+                    break
+                # (poll: a waiter on the queue would take a message out of order)
+                await asyncio.sleep(min(left, 0.0005))
         if align > 0:
             ready = 1 + self._q.qsize()   # (may count an end marker: at worst one short batch)
             if ready > align:

@@ -140,18 +140,23 @@ class Service:
         self._loops.append(asyncio.create_task(loop()))
 
     async def subscribe_batches(self, subject: str, handler, max_batch: int = 256,
-                                queue: str | None = None, align: int = 0) -> None:
+                                queue: str | None = None, align: int = 0, gate=None,
+                                fill: int = 0, fill_until=None) -> None:
         """Subscribe and call ``await handler(list_of_msgs)`` with everything queued at once (one
         message at least): under load a handler sees whole bursts, so per-message Python costs
         (decode, task, reply write) become per-batch costs.  The handler runs in this loop; it
-        may hand work off (spawn) to overlap the next batch with the current one.  ``align``:
-        see ``Subscription.next_batch``."""
+        may hand work off (spawn) to overlap the next batch with the current one.  ``gate``: an
+        async callable awaited before each batch is drawn (a free in-flight slot: messages keep
+        queueing meanwhile).  ``align`` / ``fill`` / ``fill_until``: see
+        ``Subscription.next_batch``."""
         sub = await self.nc.subscribe(subject, queue=queue or (self.cfg.queue_group or None))
         self.log.info("Subscribed to subject: %s", subject)
 
         async def loop():
             while True:
-                batch = await sub.next_batch(max_batch, align)
+                if gate is not None:
+                    await gate()
+                batch = await sub.next_batch(max_batch, align, fill, fill_until)
                 if batch is None:
                     break
                 self.metrics.inc(f"received.{subject}", len(batch))

@@ -52,18 +52,31 @@ async def _collect(q: asyncio.Queue, first, window: float, last_end: float, full
 
 
 class EmbedBatcher:
+    """``depth`` launch groups in flight: group i + 1 is collected and tokenized (native, GIL
+    released) while group i runs on the GPU, and only the enqueue of a group's kernels is
+    serialized (``_gpu_lock``: the encoder's workspaces and captured graphs are shared); each
+    group then waits on its OWN completion event, not on the stream (profiles/r5_e2e/: the serial
+    loop left the mpnet query hop at 204 ms p50, tokenize + enqueue + a full-stream sync per
+    group back to back)."""
+
     def __init__(self, encoder, tokenizer, token_budget: int = 65536, window_ms: float = 2.0,
-                 max_seqs: int = 4096, metrics=None):
+                 max_seqs: int = 4096, metrics=None, depth: int = 2):
+        import threading
+
         self.encoder = encoder
         self.tok = tokenizer
         self.token_budget = token_budget
         self.window = window_ms / 1000.0
         self.max_seqs = max_seqs
         self.metrics = metrics
+        self.depth = max(1, int(depth))
         self._q: asyncio.Queue = asyncio.Queue()
         self._task: asyncio.Task | None = None
         self._lock = asyncio.Lock()
+        self._gpu_lock = threading.Lock()
         self._last_end = float("-inf")   # loop time the last launch finished
+        self._inflight = 0
+        self._finishing: set = set()
 
     def start(self) -> None:
         if self._task is None:
@@ -80,30 +93,44 @@ class EmbedBatcher:
 
     async def _run(self) -> None:
         loop = asyncio.get_running_loop()
+        slots = asyncio.Semaphore(self.depth)
         while True:
+            await slots.acquire()        # (requests keep queueing while every slot is busy)
             first = await self._q.get()
-            batch = await _collect(self._q, first, self.window, self._last_end,
+            # a group in flight counts as busy: collect for the window
+            busy_since = loop.time() if self._inflight else self._last_end
+            batch = await _collect(self._q, first, self.window, busy_since,
                                    lambda b: sum(len(r.texts) for r in b) >= self.max_seqs)
             texts = [t for r in batch for t in r.texts]
-            try:
-                out = await loop.run_in_executor(None, self._encode_all, texts)
-            except Exception as e:  # propagate to every waiter
-                self._last_end = loop.time()
-                for r in batch:
-                    if not r.fut.done():
-                        r.fut.set_exception(e)
-                continue
-            self._last_end = loop.time()
-            o = 0
+            self._inflight += 1
+            fut = loop.run_in_executor(None, self._encode_all, texts)
+            t = asyncio.create_task(self._finish(batch, texts, fut, slots))
+            self._finishing.add(t)          # (a strong reference until it is done)
+            t.add_done_callback(self._finishing.discard)
+
+    async def _finish(self, batch, texts, fut, slots) -> None:
+        loop = asyncio.get_running_loop()
+        try:
+            out = await fut
+        except Exception as e:  # propagate to every waiter
             for r in batch:
                 if not r.fut.done():
-                    r.fut.set_result(out[o:o + len(r.texts)])
-                o += len(r.texts)
-                if self.metrics is not None:
-                    self.metrics.observe("embed.request", (time.perf_counter() - r.t0) * 1e3)
+                    r.fut.set_exception(e)
+            return
+        finally:
+            self._inflight -= 1
+            self._last_end = loop.time()
+            slots.release()
+        o = 0
+        for r in batch:
+            if not r.fut.done():
+                r.fut.set_result(out[o:o + len(r.texts)])
+            o += len(r.texts)
             if self.metrics is not None:
-                self.metrics.inc("embed.sentences", len(texts))
-                self.metrics.inc("embed.launch_groups")
+                self.metrics.observe("embed.request", (time.perf_counter() - r.t0) * 1e3)
+        if self.metrics is not None:
+            self.metrics.inc("embed.sentences", len(texts))
+            self.metrics.inc("embed.launch_groups")
 
     def _encode_all(self, texts: list[str]) -> np.ndarray:
         """Tokenize (native, GIL released) and run token-budgeted packed forwards."""
@@ -113,11 +140,18 @@ class EmbedBatcher:
         with stage("tokenize", self.metrics, n=len(texts)):
             ids, cu = self.tok.encode_packed(texts)
         lens = np.diff(cu)
-        outs = []
-        s = 0
         dev = getattr(self.encoder, "device", torch.device("cpu"))
         if dev.type == "cuda":
             return self._encode_all_gpu(ids, cu, lens, dev)
+        with self._gpu_lock:
+            return self._encode_all_cpu(texts, ids, cu, lens, dev)
+
+    def _encode_all_cpu(self, texts, ids, cu, lens, dev) -> np.ndarray:
+        from ..models.encoder import PackedBatch
+
+        cfg = self.encoder.cfg
+        outs = []
+        s = 0
         while s < len(texts):
             e, tok = s, 0
             while e < len(texts) and (e == s or tok + lens[e] <= self.token_budget):
@@ -147,9 +181,19 @@ class EmbedBatcher:
         cfg = self.encoder.cfg
         n = len(lens)
         out = torch.empty((n, cfg.hidden), dtype=torch.float32, pin_memory=True)
+        keep = []   # host/device tensors that must outlive their async copies
+        with self._gpu_lock:
+            done = self._enqueue_gpu(ids, cu, lens, dev, cfg, out, keep)
+        with stage("encode_d2h_sync", self.metrics):
+            done.synchronize()   # this group's copies only, not a later group's kernels
+        return out.numpy()
+
+    def _enqueue_gpu(self, ids, cu, lens, dev, cfg, out, keep):
+        from ..models.encoder import PackedBatch
+
+        n = len(lens)
         compute = torch.cuda.current_stream(dev)
         copy = self._copy_stream(dev)
-        keep = []   # host/device tensors that must outlive their async copies
         s = 0
         while s < n:
             e, tok = s, 0
@@ -177,9 +221,9 @@ class EmbedBatcher:
             out[s:e].copy_(pooled.float(), non_blocking=True)
             keep.append((host, pooled))
             s = e
-        with stage("encode_d2h_sync", self.metrics):
-            compute.synchronize()
-        return out.numpy()
+        done = torch.cuda.Event()
+        done.record(compute)
+        return done
 
     def _copy_stream(self, dev):
         st = getattr(self, "_cs", None)

@@ -81,6 +81,9 @@ class Config:
     # bursts larger than this take a whole multiple of it (the int8 scan's 256-query block: a
     # 369-query burst would cost two full scans of the shard; 0 = take whatever is queued)
     search_align: int = field(default_factory=lambda: _int("SYMB_SEARCH_ALIGN", 256))
+    # while a scan runs, the next burst collects until it fills a search_align block or the
+    # running scan is due to end (services/vector_memory.py _fill_deadline); 0 = launch at once
+    search_fill: int = field(default_factory=lambda: _int("SYMB_SEARCH_FILL", 1))
     # CUs the index scans may occupy (0 = all): leave some to an encoder sharing the GPU
     scan_cus: int = field(default_factory=lambda: _int("SYMB_SCAN_CUS", 0))
     collection: str = "symbiont_document_embeddings"

@@ -132,7 +132,7 @@ struct Fp8Chain {
   }
 };
 
-template <int D, int KMAX, int NS, int SUBS, int AUX>
+template <int D, int KMAX, int NS, int SUBS, int AUX, bool L2SRC = false>
 __global__ __launch_bounds__(256, 1) void index_scan_fp8_kernel(
     const uint8_t* __restrict__ X, int n_valid, int rows_per_blk, const uint8_t* __restrict__ Q,
     int NQ, int n_qblk, int xcd, const float* __restrict__ thr_init, float* __restrict__ cand_s,
@@ -168,18 +168,27 @@ __global__ __launch_bounds__(256, 1) void index_scan_fp8_kernel(
       q1[ks] = *reinterpret_cast<const i32x8*>(p1 + ks * 64);
     }
   }
-  uint32_t goff[LOADS];
+  // per-piece source offsets: piece i + GP repeats piece i's swizzle GP * RPS rows further down,
+  // so only GP offsets stay live (D = 1024: 4 registers instead of 16); GP = LOADS where the
+  // pattern does not repeat
+  constexpr int RPS = (NW * 64) % CPR == 0 ? NW * 64 / CPR : 0;   // rows per piece step
+  constexpr int GP = (G == 16 && RPS > 0 && 16 % RPS == 0 && LOADS % (16 / RPS) == 0)
+                         ? 16 / RPS : LOADS;
+  uint32_t goff[GP];
 #pragma unroll
-  for (int i = 0; i < LOADS; ++i) {
+  for (int i = 0; i < GP; ++i) {
     const int s = (i * NW + wave) * 64 + lane;  // 16-byte LDS slot this lane fills
     const int row = s / CPR, pc = s % CPR;
     goff[i] = (uint32_t)(row * D + (Swz::phys(pc, row) << 4));   // the swizzle is an involution
   }
   auto issue_piece = [&](int t, int i) {
-    const int tt = min(t, n_tiles - 1);  // past the end: re-load the last tile (keeps vmcnt exact)
+    // past the end: re-load the last tile (keeps vmcnt exact); L2SRC (diagnostic): every tile
+    // reads the block's first 8 tiles, an L2-resident source -- the kernel's compute ceiling
+    const int tt = L2SRC ? (t & 7) % n_tiles : min(t, n_tiles - 1);
     const uint8_t* base = X + (size_t)(row_begin + tt * TR) * D;
     char* dst = smem + (t % NS) * TILE_BYTES;
-    glds16_aux<AUX>(base + goff[i], dst + (i * NW + wave) * 1024);
+    glds16_aux<AUX>(base + (size_t)(i / GP) * (GP * RPS * D) + goff[i % GP],
+                    dst + (i * NW + wave) * 1024);
   };
   const uint32_t lds_smem = lds_addr(smem);
   uint32_t voff[8];
@@ -293,13 +302,13 @@ int symb_quant_fp8(const void* in, int in_f32, int ld_in, uint8_t* out, int ld_o
   return (int)hipGetLastError();
 }
 
-template <int D, int KMAX, int NS, int SUBS, int AUX>
+template <int D, int KMAX, int NS, int SUBS, int AUX, bool L2SRC = false>
 static int launch_fp8(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                       int NQ, int n_qblk, int xcd, const float* thr, float* cs, int* ci,
                       hipStream_t st) {
-  auto kern = index_scan_fp8_kernel<D, KMAX, NS, SUBS, AUX>;
+  auto kern = index_scan_fp8_kernel<D, KMAX, NS, SUBS, AUX, L2SRC>;
   constexpr int lds = NS * 32 * SUBS * D;
-  set_max_lds<index_scan_fp8_kernel<D, KMAX, NS, SUBS, AUX>>(lds);
+  set_max_lds<index_scan_fp8_kernel<D, KMAX, NS, SUBS, AUX, L2SRC>>(lds);
   hipLaunchKernelGGL(kern, dim3(n_rblk * n_qblk), dim3(256), lds, st, (const uint8_t*)X, n_valid,
                      rows_per_blk, (const uint8_t*)Q, NQ, n_qblk, xcd, thr, cs, ci);
   return (int)hipGetLastError();
@@ -320,8 +329,13 @@ static int dispatch_fp8(int kmax, int aux, int variant, const void* X, int n_val
   constexpr int SUBS = Fp8Cfg<D>::SUBS, NS = Fp8Cfg<D>::NS;
 #define SYMB_F(K, NS_, SUBS_, A) \
   launch_fp8<D, K, NS_, SUBS_, A>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, n_qblk, xcd, thr, cs, ci, st)
-  if constexpr (D == 1024)  // variant 1: one sub-tile per barrier, 4-deep ring (-4 % at 100M rows)
-    if (variant == 1) return aux ? SYMB_F(16, 4, 1, 2) : SYMB_F(16, 4, 1, 0);
+  // (round 6: one sub-tile per barrier with a 4- or 5-deep ring measured 4 % slower at 100M x
+  // 1024 -- profiles/r6_fp8/ -- and was removed.)  variant 9, diagnostic: the default geometry
+  // re-reading 8 tiles per row block from L2, the kernel's compute ceiling (not a search result)
+  if constexpr (D == 1024)
+    if (variant == 9)
+      return launch_fp8<D, 16, NS, SUBS, 0, true>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, n_qblk,
+                                                  xcd, thr, cs, ci, st);
   if (kmax == 16) return aux ? SYMB_F(16, NS, SUBS, 2) : SYMB_F(16, NS, SUBS, 0);
   if (kmax == 32) return aux ? SYMB_F(32, NS, SUBS, 2) : SYMB_F(32, NS, SUBS, 0);
 #undef SYMB_F
@@ -330,7 +344,7 @@ static int dispatch_fp8(int kmax, int aux, int variant, const void* X, int n_val
 
 // X: [>= round_up(n_valid, 64), D] e4m3 rows (scale S), Q: [NQ, D] e4m3 queries (scale S).
 // Candidates: [NQ][n_rblk][2][kmax] raw accumulators (S^2 * cosine); thr_init in the same units.
-// variant: 0 = default ring geometry, 1 = D=1024 with 1 sub-tile/barrier and a 4-deep ring.
+// variant: 0 = the ring geometry of Fp8Cfg; 9 (D = 1024) = the L2-source diagnostic.
 int symb_index_scan_fp8(const void* X, int n_valid, int D, int rows_per_blk, int n_rblk,
                         const void* Q, int NQ, int kmax, float* cand_s, int* cand_i,
                         hipStream_t st, int aux, const float* thr_init, int variant, int xcd) {

@@ -156,3 +156,39 @@ def test_idle_request_skips_window_busy_requests_coalesce():
     idle_s = asyncio.run(asyncio.wait_for(main(), 10))
     assert idle_s < 0.2
     assert launches == [1, 3]
+
+
+def test_embed_batcher_overlaps_groups():
+    """depth 2: group 2 is collected and tokenized while group 1 is still in its (slow) encode,
+    and each caller still gets its own rows."""
+    import threading
+    import time
+
+    events = []
+    lock = threading.Lock()
+
+    class SlowTok(_ToyTokenizer):
+        def encode_packed(self, texts):
+            with lock:
+                events.append(("tok", texts[0].split()[0], time.perf_counter()))
+            return super().encode_packed(texts)
+
+    class SlowEnc(_ToyEncoder):
+        def forward_packed(self, b):
+            time.sleep(0.4)
+            return super().forward_packed(b)
+
+    async def main():
+        b = EmbedBatcher(SlowEnc(), SlowTok(), token_budget=64, window_ms=0.0, depth=2)
+        first = asyncio.create_task(b.embed(["aa bb"]))
+        await asyncio.sleep(0.05)              # group 1 is in its encode now
+        second = asyncio.create_task(b.embed(["cc dd"]))
+        outs = await asyncio.gather(first, second)
+        b._task.cancel()
+        return outs
+    outs = asyncio.run(asyncio.wait_for(main(), 10))
+    np.testing.assert_array_equal(outs[0], _expected(["aa bb"]))
+    np.testing.assert_array_equal(outs[1], _expected(["cc dd"]))
+    t = {name: ts for _, name, ts in events}
+    # group 2 tokenized ~50 ms after group 1, i.e. during group 1's 400 ms encode
+    assert t["cc"] - t["aa"] < 0.35

@@ -324,3 +324,39 @@ def test_next_batch_align():
         assert len(await sub.next_batch(200, align=256)) == 100
 
     asyncio.run(with_timeout())
+
+
+def test_next_batch_fill_until_deadline():
+    """next_batch(fill=F, fill_until=f): with fewer than F ready it keeps collecting until F are
+    ready or f()'s deadline passes; a None deadline (nothing in flight) launches at once."""
+    from codename_symbiont_amd.bus.client import Msg, Subscription
+
+    async def main():
+        loop = asyncio.get_running_loop()
+        sub = Subscription(None, "1", "s", None)
+        sub._deliver(Msg("s", None, b"0"))
+        t0 = loop.time()
+        assert len(await sub.next_batch(512, 256, fill=256, fill_until=lambda: None)) == 1
+        assert loop.time() - t0 < 0.1
+
+        async def trickle(n, gap):
+            for i in range(n):
+                await asyncio.sleep(gap)
+                sub._deliver(Msg("s", None, b"%d" % i))
+        # the block fills before the deadline: exactly 256 taken, the rest stays queued
+        sub._deliver(Msg("s", None, b"x"))
+        feed = asyncio.create_task(trickle(300, 0.0))
+        b = await sub.next_batch(512, 256, fill=256, fill_until=lambda: loop.time() + 5.0)
+        await feed
+        assert len(b) == 256
+        rest = await sub.next_batch(512, 256)
+        assert len(rest) == 301 - 256
+        # the deadline passes first: whatever arrived by then
+        sub._deliver(Msg("s", None, b"y"))
+        feed = asyncio.create_task(trickle(5, 0.01))
+        t0 = loop.time()
+        b = await sub.next_batch(512, 256, fill=256, fill_until=lambda: loop.time() + 0.2)
+        assert 0.15 < loop.time() - t0 < 1.5 and 2 <= len(b) <= 6
+        await feed
+
+    asyncio.run(asyncio.wait_for(main(), 10))
