@@ -23,6 +23,11 @@ def main():
     scans = [(s, e) for s, e, n, _ in ks
              if re.search(r"scan_stream_kernel|index_scan_i8_kernel", n) and e - s > 200_000]
     coll = [(s, e, n) for s, e, n, _ in ks if re.search(r"nccl|rccl", n, re.I)]
+    # hardware queues: HIP maps streams round-robin onto GPU_MAX_HW_QUEUES queues, and kernels
+    # of two streams on one queue run in FIFO order whatever their dependencies
+    scan_q = {q for s, e, n, q in ks
+              if re.search(r"scan_stream_kernel|index_scan_i8_kernel", n) and e - s > 200_000}
+    coll_q = {q for s, e, n, q in ks if re.search(r"nccl|rccl", n, re.I)}
     inside = after = 0
     waits = []
     for s, e, n in coll:
@@ -41,6 +46,7 @@ def main():
            "start_after_scan_end_us": [round(w, 1) for w in waits],
            "collective_us": [round((e - s) / 1e3, 1) for s, e, _ in coll],
            "collective_us_mean": round(sum(e - s for s, e, _ in coll) / max(1, len(coll)) / 1e3, 2),
+           "scan_hw_queues": sorted(scan_q), "collective_hw_queues": sorted(coll_q),
            "names": sorted({re.sub(r"\(.*", "", n)[:80] for _, _, n in coll})}
     print(json.dumps(out, indent=1))
 
