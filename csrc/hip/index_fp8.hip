@@ -132,7 +132,12 @@ struct Fp8Chain {
   }
 };
 
-template <int D, int KMAX, int NS, int SUBS, int AUX, bool L2SRC = false>
+// DIAG (timing diagnostics only -- results are not a search's): DG_L2 every tile re-reads the
+// block's first 8 tiles (an L2-resident source); DG_NODMA no loads after the prologue (stale
+// LDS); DG_NOUPD no top-k test; DG_NOBAR no per-tile barrier.
+enum { DG_L2 = 1, DG_NODMA = 2, DG_NOUPD = 4, DG_NOBAR = 8 };
+
+template <int D, int KMAX, int NS, int SUBS, int AUX, int DIAG = 0>
 __global__ __launch_bounds__(256, 1) void index_scan_fp8_kernel(
     const uint8_t* __restrict__ X, int n_valid, int rows_per_blk, const uint8_t* __restrict__ Q,
     int NQ, int n_qblk, int xcd, const float* __restrict__ thr_init, float* __restrict__ cand_s,
@@ -182,9 +187,8 @@ __global__ __launch_bounds__(256, 1) void index_scan_fp8_kernel(
     goff[i] = (uint32_t)(row * D + (Swz::phys(pc, row) << 4));   // the swizzle is an involution
   }
   auto issue_piece = [&](int t, int i) {
-    // past the end: re-load the last tile (keeps vmcnt exact); L2SRC (diagnostic): every tile
-    // reads the block's first 8 tiles, an L2-resident source -- the kernel's compute ceiling
-    const int tt = L2SRC ? (t & 7) % n_tiles : min(t, n_tiles - 1);
+    // past the end: re-load the last tile (keeps vmcnt exact)
+    const int tt = (DIAG & DG_L2) ? (t & 7) % n_tiles : min(t, n_tiles - 1);
     const uint8_t* base = X + (size_t)(row_begin + tt * TR) * D;
     char* dst = smem + (t % NS) * TILE_BYTES;
     glds16_aux<AUX>(base + (size_t)(i / GP) * (GP * RPS * D) + goff[i % GP],
@@ -239,8 +243,10 @@ __global__ __launch_bounds__(256, 1) void index_scan_fp8_kernel(
   i32x4 lo[R], hi[R];
   for (int t = 0; t < n_tiles; ++t) {
     wait_vmcnt<LOADS * (NS - 2)>();  // tile t landed for this wave
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    if constexpr (!(DIAG & DG_NOBAR)) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
     const uint32_t tbase = lds_smem + (uint32_t)((t % NS) * TILE_BYTES);
     const int row0 = row_begin + t * TR;
     const int tnext = t + NS - 1;
@@ -251,7 +257,10 @@ __global__ __launch_bounds__(256, 1) void index_scan_fp8_kernel(
       f32x16 acc0, acc1;
       if (sub == 0) {
         fp8_prologue<0, PF, R, G>(lo, hi, voff, base);
-        Fp8Chain<0, NKS, PF, LOADS, G>::run(acc0, acc1, lo, hi, q0, q1, voff, base, dma);
+        if constexpr (DIAG & DG_NODMA)
+          Fp8Chain<0, NKS, PF, 0, G>::run(acc0, acc1, lo, hi, q0, q1, voff, base, NoDma());
+        else
+          Fp8Chain<0, NKS, PF, LOADS, G>::run(acc0, acc1, lo, hi, q0, q1, voff, base, dma);
       } else {
         Fp8Chain<0, NKS, PF, 0, G>::run(acc0, acc1, lo, hi, q0, q1, voff, base, NoDma());
       }
@@ -259,8 +268,10 @@ __global__ __launch_bounds__(256, 1) void index_scan_fp8_kernel(
         fp8_prologue<0, PF, R, G>(lo, hi, voff, base + SUB_BYTES);
       // (reads of the asm MFMA results stay below the chain-end s_nops: index_i8.hip emit)
       asm volatile("" : "+v"(acc0), "+v"(acc1));
-      update(acc0, tv0, ti0, thr0, row0 + sub * SUB);
-      update(acc1, tv1, ti1, thr1, row0 + sub * SUB);
+      if constexpr (!(DIAG & DG_NOUPD)) {
+        update(acc0, tv0, ti0, thr0, row0 + sub * SUB);
+        update(acc1, tv1, ti1, thr1, row0 + sub * SUB);
+      }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the tail prefetches before exit
@@ -302,13 +313,13 @@ int symb_quant_fp8(const void* in, int in_f32, int ld_in, uint8_t* out, int ld_o
   return (int)hipGetLastError();
 }
 
-template <int D, int KMAX, int NS, int SUBS, int AUX, bool L2SRC = false>
+template <int D, int KMAX, int NS, int SUBS, int AUX, int DIAG = 0>
 static int launch_fp8(const void* X, int n_valid, int rows_per_blk, int n_rblk, const void* Q,
                       int NQ, int n_qblk, int xcd, const float* thr, float* cs, int* ci,
                       hipStream_t st) {
-  auto kern = index_scan_fp8_kernel<D, KMAX, NS, SUBS, AUX, L2SRC>;
+  auto kern = index_scan_fp8_kernel<D, KMAX, NS, SUBS, AUX, DIAG>;
   constexpr int lds = NS * 32 * SUBS * D;
-  set_max_lds<index_scan_fp8_kernel<D, KMAX, NS, SUBS, AUX, L2SRC>>(lds);
+  set_max_lds<index_scan_fp8_kernel<D, KMAX, NS, SUBS, AUX, DIAG>>(lds);
   hipLaunchKernelGGL(kern, dim3(n_rblk * n_qblk), dim3(256), lds, st, (const uint8_t*)X, n_valid,
                      rows_per_blk, (const uint8_t*)Q, NQ, n_qblk, xcd, thr, cs, ci);
   return (int)hipGetLastError();
@@ -330,12 +341,21 @@ static int dispatch_fp8(int kmax, int aux, int variant, const void* X, int n_val
 #define SYMB_F(K, NS_, SUBS_, A) \
   launch_fp8<D, K, NS_, SUBS_, A>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, n_qblk, xcd, thr, cs, ci, st)
   // (round 6: one sub-tile per barrier with a 4- or 5-deep ring measured 4 % slower at 100M x
-  // 1024 -- profiles/r6_fp8/ -- and was removed.)  variant 9, diagnostic: the default geometry
-  // re-reading 8 tiles per row block from L2, the kernel's compute ceiling (not a search result)
-  if constexpr (D == 1024)
-    if (variant == 9)
-      return launch_fp8<D, 16, NS, SUBS, 0, true>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, n_qblk,
-                                                  xcd, thr, cs, ci, st);
+  // 1024 -- profiles/r6_fp8/ -- and was removed.)  Variants 9-14 (D = 1024): timing diagnostics
+  // of the default geometry, not search results -- 9 L2-resident source, 11 no loads after the
+  // prologue, 12 no top-k test, 13 no barrier, 14 = 11 + 12 + 13 (the bare MFMA chains)
+  if constexpr (D == 1024) {
+#define SYMB_DG(DG) launch_fp8<D, 16, NS, SUBS, 0, DG>(X, n_valid, rows_per_blk, n_rblk, Q, NQ, \
+                                                      n_qblk, xcd, thr, cs, ci, st)
+    switch (variant) {
+      case 9: return SYMB_DG(DG_L2);
+      case 11: return SYMB_DG(DG_NODMA);
+      case 12: return SYMB_DG(DG_NOUPD);
+      case 13: return SYMB_DG(DG_NOBAR);
+      case 14: return SYMB_DG(DG_NODMA | DG_NOUPD | DG_NOBAR);
+    }
+#undef SYMB_DG
+  }
   if (kmax == 16) return aux ? SYMB_F(16, NS, SUBS, 2) : SYMB_F(16, NS, SUBS, 0);
   if (kmax == 32) return aux ? SYMB_F(32, NS, SUBS, 2) : SYMB_F(32, NS, SUBS, 0);
 #undef SYMB_F
@@ -344,7 +364,7 @@ static int dispatch_fp8(int kmax, int aux, int variant, const void* X, int n_val
 
 // X: [>= round_up(n_valid, 64), D] e4m3 rows (scale S), Q: [NQ, D] e4m3 queries (scale S).
 // Candidates: [NQ][n_rblk][2][kmax] raw accumulators (S^2 * cosine); thr_init in the same units.
-// variant: 0 = the ring geometry of Fp8Cfg; 9 (D = 1024) = the L2-source diagnostic.
+// variant: 0 = the ring geometry of Fp8Cfg; 9, 11-14 (D = 1024) = timing diagnostics.
 int symb_index_scan_fp8(const void* X, int n_valid, int D, int rows_per_blk, int n_rblk,
                         const void* Q, int NQ, int kmax, float* cand_s, int* cand_i,
                         hipStream_t st, int aux, const float* thr_init, int variant, int xcd) {
