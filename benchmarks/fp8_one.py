@@ -25,15 +25,24 @@ def main() -> None:
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--seed-threshold", type=int, default=1)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--check", type=int, default=0, help="compare ids / scores with variant 0")
     a = ap.parse_args()
     from codename_symbiont_amd.index.shard import HbmIndexShard
 
     shard = HbmIndexShard(a.dim, a.rows, device="cuda", dtype="fp8")
     shard.fill_random(a.rows, seed=1)
-    shard.scan_variant, shard.seed_threshold = a.variant, bool(a.seed_threshold)
+    shard.seed_threshold = bool(a.seed_threshold)
     g = torch.Generator(device="cuda").manual_seed(5)
     q = torch.nn.functional.normalize(torch.randn(a.nq, a.dim, device="cuda", generator=g),
                                       dim=-1).bfloat16()
+    match = None
+    if a.check:   # the default kernel's answer, for the exact A/B forms
+        shard.scan_variant = 0
+        ref = shard.search(q, 10)
+        shard.scan_variant = a.variant
+        got = shard.search(q, 10)
+        match = bool(torch.equal(ref[1], got[1]) and torch.equal(ref[0], got[0]))
+    shard.scan_variant = a.variant
     shard.search(q, 10)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -42,7 +51,7 @@ def main() -> None:
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / a.iters * 1e3
     print(json.dumps({"bench": "fp8_one", "rows": a.rows, "dim": a.dim, "nq": a.nq,
-                      "variant": a.variant, "ms": round(ms, 3),
+                      "variant": a.variant, "ms": round(ms, 3), "matches_v0": match,
                       "GBps": round(a.rows * a.dim / (ms / 1e3) / 1e9)}))
 
 
