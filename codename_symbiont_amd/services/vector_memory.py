@@ -150,7 +150,9 @@ class VectorMemoryService(Service):
         one [n, D] query matrix and answered from one scan; irregular ones (decode errors, wrong
         dimension, extra keys) take ``handle_search``, which produces the reference's error
         replies.  The scan runs in an executor thread while this loop goes back for the next
-        burst (at most SEARCH_MAX_INFLIGHT scans in flight)."""
+        burst (at most SEARCH_MAX_INFLIGHT scans in flight: the subscription's gate,
+        ``_search_slot``, took a slot before this burst was drawn; ``_finish_search_batch``
+        returns it)."""
         with stage("search_decode", self.metrics, n=len(msgs)):
             ok, ids, topk, q = native().search_tasks_batch([bytes(m.data) for m in msgs],
                                                            self.store.dim)
@@ -158,10 +160,8 @@ class VectorMemoryService(Service):
         if len(good) < len(msgs):
             for i in np.flatnonzero(~ok):
                 self.spawn(self.handle_search(msgs[int(i)]))
-        if self._inflight is None:   # (a caller that did not pass through _search_slot)
-            await self._search_slot()
         if not len(good):
-            self._inflight.release()
+            self._inflight.release()   # (the scan slot _search_slot took for this burst)
             return
         ks = topk[good]
         loop = asyncio.get_running_loop()
