@@ -12,6 +12,7 @@ Here:
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -169,8 +170,6 @@ class HipEncoder:
         # route for the plain projections.
         self._folds = []
         if precision == "bf16" and cfg.hidden != 384 and cfg.hidden % 64 == 0:
-            import os
-
             from ..ops.kernels import fold_ln
 
             for li, L in enumerate(p["layers"]):
@@ -183,6 +182,9 @@ class HipEncoder:
                 self.rt.set_fold(li, [0 if t is None else t.data_ptr() for t in fq + fi])
             self.rt.set_deferred_ln(0 if os.environ.get("SYMB_DEFERRED_LN", "0") in ("", "0")
                                     else 1)
+        # (A/B) SYMB_QKV_ATTN=0: the QKV GEMM + attention pair instead of the fused kernel
+        if os.environ.get("SYMB_QKV_ATTN", "") in ("0", "1"):
+            hip().qkv_attn_config(int(os.environ["SYMB_QKV_ATTN"]))
         self._ws_tokens = 0
         self._ws: list[torch.Tensor] = []
 

@@ -182,6 +182,25 @@ def attention(qkv, cu_seqlens, max_len, n_heads, head_dim, out=None):
     return out
 
 
+def qkv_attention(x, wqkv, bqkv, cu_seqlens, max_len, n_heads, head_dim, out=None):
+    """The QKV projection fused into varlen attention (attention.hip qkv_attn_kernel): x [T, H]
+    bf16, wqkv [3H, H] bf16, bqkv [3H] f32 -> [T, H].  head_dim 32 / 12 heads, sentences of at
+    most 128 tokens (the kernel raises otherwise)."""
+    _chk(x, torch.bfloat16, "x", 2)
+    _chk(wqkv, torch.bfloat16, "wqkv", 2)
+    _chk(bqkv, torch.float32, "bqkv", 1)
+    _chk(cu_seqlens, torch.int32, "cu_seqlens", 1)
+    T, H = x.shape
+    if wqkv.shape != (3 * H, H) or bqkv.numel() != 3 * H or H != n_heads * head_dim:
+        raise ValueError("bad qkv_attention geometry")
+    B = cu_seqlens.numel() - 1
+    if out is None:
+        out = torch.empty(T, H, dtype=torch.bfloat16, device=x.device)
+    hip().qkv_attention(_ptr(x), _ptr(wqkv), _ptr(bqkv), _ptr(cu_seqlens), B, int(max_len),
+                        n_heads, head_dim, _ptr(out), stream_handle())
+    return out
+
+
 def pool(hidden, cu_seqlens, mode="mean", normalize=False, want_normed_bf16=True):
     """Returns (pooled_f32 [B,H], unit_bf16 [B,H] or None)."""
     _chk(hidden, torch.bfloat16, "hidden", 2)

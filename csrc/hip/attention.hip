@@ -198,9 +198,234 @@ __global__ __launch_bounds__(64 * NWAVE) void attn_varlen_kernel(const __bf16* _
   }
 }
 
+// ---- QKV projection fused into attention (head_dim 32, sentences of <= 128 tokens) ------------
+//
+// The unfused layer writes the [T, 3H] QKV activation (75 MB at 32768 tokens, H = 384) and the
+// attention kernel reads it back; both kernels run far from their MFMA floors (QKV GEMM ~47 us,
+// attention ~31 us per MiniLM layer, profiles/r6_step/).  Here ONE workgroup per sentence walks
+// the heads, and the activation never leaves the CU:
+//  * the sentence's X rows are read once: wave w owns tokens 16w .. 16w + 15 and keeps their
+//    rows as resident B fragments (12 k-steps x 4 VGPRs);
+//  * per head, the projection computes OUT^T = W_h X^T (v_mfma_f32_16x16x32_bf16; A = the
+//    head's 96 Q / K / V weight rows, staged in LDS with 16-byte chunks XOR-swizzled by the row's
+//    low 4 bits: conflict-free A-fragment reads; k-step outer, the next k-step's six fragments
+//    read under the current six independent MFMAs), so a lane ends with dims 4g .. 4g + 3 and
+//    16 + 4g .. of ONE token (c16) for each of Q, K, V;
+//  * the k index of the attention's QK^T product is permuted to match: chunk g of a head row is
+//    dims {4g..4g+3, 16+4g..16+4g+3}.  A lane's Q values ARE its B fragment (no exchange), its K
+//    values are one 16-byte store into the attention's swizzled K row; V rows are stored in
+//    natural order (read transposed with ds_read_b64_tr_b16 as in attn_varlen_kernel);
+//  * software pipeline over heads: head h + 1's projection (MFMA-bound) and head h's attention
+//    (latency-bound softmax VALU and small MFMAs) share one barrier interval, with K / V in two
+//    LDS buffers; the two waves of a SIMD (w, w + 4) run them in opposite orders, so one's
+//    projection overlaps the other's softmax; head h + 2's weight rows are loaded into registers
+//    at the top of the interval and stored to LDS after its barrier;
+//  * the attention scores a sentence's (<= 128) keys in one pass: 8 S tiles, one max, one
+//    exp2 pass, no online rescaling (keys past the sentence masked).
+// Measured forms (the GEMM + attention pair: ~78 us per MiniLM layer): one workgroup per
+// (sentence, head), re-reading X per head with every head's weight staging exposed -- 91 us;
+// one per sentence with the phases in series -- 73.4 us, of which the attention 36 us (its two
+// waves per SIMD could not hide the softmax's latency).
+// Tokens past the sentence are clamped to its last row (finite values), as there.
+template <int NH>
+__global__ __launch_bounds__(512, 1) void qkv_attn_kernel(const __bf16* __restrict__ X,
+                                                          const __bf16* __restrict__ Wqkv,
+                                                          const float* __restrict__ bqkv,
+                                                          const int32_t* __restrict__ cu,
+                                                          float scale_log2,
+                                                          __bf16* __restrict__ out, int B) {
+  constexpr int D = 32, H = NH * D, NKX = H / 32;   // k-steps of the projection
+  constexpr int WROW = H * 2;                       // weight row bytes in LDS
+  constexpr int NCH = WROW / 16;                    // 16-byte chunks per weight row
+  constexpr int WPL = 96 * NCH / 512;               // weight chunks per lane per head
+  constexpr int KRB = D * 2, VRB = D * 2 + 32, KVB = 128 * KRB + 128 * VRB;
+  static_assert((H * 2) % 256 == 0 && (96 * NCH) % 512 == 0, "weight rows of whole 256-byte groups");
+  static_assert(NH >= 2, "the head pipeline peels the last head");
+  typedef short s16x4 __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) char sW[96 * WROW];
+  __shared__ __attribute__((aligned(16))) char sKV[2 * KVB];   // K | V of heads h, h + 1
+
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int s0 = cu[b], L = cu[b + 1] - s0;
+  if (L <= 0) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c16 = lane & 15, g = lane >> 4;
+  const int row = wave * 16 + c16;   // this lane's token: query of the attention, key of K / V
+
+  bf16x8 wst[WPL];
+  auto load_w = [&](int h) {   // head h's Q / K / V weight rows (row = 32 * section + dim)
+#pragma unroll
+    for (int k = 0; k < WPL; ++k) {
+      const int i = tid + k * 512, wr = i / NCH, c = i % NCH;
+      const int grow = (wr >> 5) * H + h * D + (wr & 31);
+      wst[k] = *reinterpret_cast<const bf16x8*>(Wqkv + (size_t)grow * H + c * 8);
+    }
+  };
+  auto store_w = [&]() {
+#pragma unroll
+    for (int k = 0; k < WPL; ++k) {
+      const int i = tid + k * 512, wr = i / NCH, c = i % NCH;
+      *reinterpret_cast<bf16x8*>(sW + wr * WROW + ((c ^ (wr & 15)) << 4)) = wst[k];
+    }
+  };
+  load_w(0);
+  const __bf16* xp = X + (size_t)(s0 + min(row, L - 1)) * H + g * 8;
+  bf16x8 xf[NKX];
+#pragma unroll
+  for (int ks = 0; ks < NKX; ++ks) xf[ks] = *reinterpret_cast<const bf16x8*>(xp + ks * 32);
+  store_w();
+  load_w(1);
+  __syncthreads();
+
+  // projection of head h from the weight slab: Q as this lane's B fragment, K / V to buffer kb
+  auto project = [&](int h, bf16x8& qf, int kb) {
+    f32x4 acc[6];
+    bf16x8 wf[2][6];
+    auto rd = [&](int buf, int ks) {
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        const int wr = j * 16 + c16;
+        wf[buf][j] = *reinterpret_cast<const bf16x8*>(sW + wr * WROW +
+                                                      (((ks * 4 + g) ^ (wr & 15)) << 4));
+      }
+    };
+#pragma unroll
+    for (int j = 0; j < 6; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    rd(0, 0);
+#pragma unroll
+    for (int ks = 0; ks < NKX; ++ks) {
+      if (ks + 1 < NKX) rd((ks + 1) & 1, ks + 1);
+#pragma unroll
+      for (int j = 0; j < 6; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks & 1][j], xf[ks], acc[j], 0, 0, 0);
+    }
+    // + bias; lane holds dims (j & 1) * 16 + 4g + r of section j >> 1 for its token
+    bf16x8 kv;
+    bf16x4 v0, v1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int d0 = h * D + 4 * g + r, d1 = d0 + 16;
+      qf[r] = (__bf16)(acc[0][r] + bqkv[d0]);
+      qf[4 + r] = (__bf16)(acc[1][r] + bqkv[d1]);
+      kv[r] = (__bf16)(acc[2][r] + bqkv[H + d0]);
+      kv[4 + r] = (__bf16)(acc[3][r] + bqkv[H + d1]);
+      v0[r] = (__bf16)(acc[4][r] + bqkv[2 * H + d0]);
+      v1[r] = (__bf16)(acc[5][r] + bqkv[2 * H + d1]);
+    }
+    char* Ks = sKV + kb * KVB;
+    char* Vs = Ks + 128 * KRB;
+    *reinterpret_cast<bf16x8*>(Ks + row * KRB + ((g ^ ((row >> 1) & 3)) << 4)) = kv;
+    *reinterpret_cast<bf16x4*>(Vs + row * VRB + (4 * g) * 2) = v0;
+    *reinterpret_cast<bf16x4*>(Vs + row * VRB + (16 + 4 * g) * 2) = v1;
+  };
+
+  // attention of head h (queries: this wave's 16 tokens) over K / V buffer kb
+  uint32_t koff[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const int r = n * 16 + c16;
+    koff[n] = (uint32_t)(r * KRB + ((g ^ ((r >> 1) & 3)) << 4));
+  }
+  const uint32_t vbase = (uint32_t)((4 * g + (c16 >> 2)) * VRB + (c16 & 3) * 8);
+  const uint32_t lds_kv = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)sKV);
+  auto attend = [&](int h, const bf16x8& qf, int kb) {
+    const char* Ks = sKV + kb * KVB;
+    f32x4 sc[8];
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+      const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + (n >> 2) * 64 * KRB + koff[n & 3]);
+      sc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int n = 0; n < 8; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = (n * 16 + 4 * g + r) < L ? sc[n][r] * scale_log2 : -INFINITY;
+        sc[n][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float lsum = 0.f;
+    bf16x8 pb[4];
+#pragma unroll
+    for (int n = 0; n < 8; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = exp2f(sc[n][r] - mx);
+        lsum += p;
+        pb[n >> 1][(n & 1) * 4 + r] = (__bf16)p;
+      }
+    f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    const uint32_t vb = lds_kv + (uint32_t)(kb * KVB + 128 * KRB) + vbase;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        const uint32_t a0 = vb + (uint32_t)(t * 32 * VRB + d * 32);
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(uintptr_t)a0);
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(uintptr_t)(a0 + 16 * VRB));
+        const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        o[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[t], o[d], 0, 0, 0);
+      }
+    lsum += __shfl_xor(lsum, 16, 64);
+    lsum += __shfl_xor(lsum, 32, 64);
+    if (row < L) {
+      const float inv = 1.0f / lsum;
+      __bf16* op = out + (size_t)(s0 + row) * H + h * D + 4 * g;
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        bf16x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (__bf16)(o[d][r] * inv);
+        *reinterpret_cast<bf16x4*>(op + d * 16) = v;
+      }
+    }
+  };
+
+  bf16x8 q_cur, q_next;
+  project(0, q_cur, 0);
+  __syncthreads();    // head 0's K / V visible; every wave done with head 0's weights
+  store_w();          // head 1's weights
+  __syncthreads();
+  for (int h = 0; h + 1 < NH; ++h) {
+    load_w(min(h + 2, NH - 1));       // (the last head's rows again at the end: harmless)
+    // the two waves of a SIMD (w, w + 4) take the two phases in opposite orders, so one's
+    // MFMA-bound projection runs under the other's softmax
+    if (wave & 4) {
+      attend(h, q_cur, h & 1);
+      project(h + 1, q_next, (h + 1) & 1);
+    } else {
+      project(h + 1, q_next, (h + 1) & 1);
+      attend(h, q_cur, h & 1);
+    }
+    q_cur = q_next;
+    __syncthreads();  // head h + 1's K / V visible; the weight slab and buffer h & 1 are free
+    store_w();
+    __syncthreads();
+  }
+  attend(NH - 1, q_cur, (NH - 1) & 1);
+}
+
 }  // namespace symb
 
 using namespace symb;
+
+// X [T, H] bf16 rows (packed sentences, cu_seqlens), Wqkv [3H, H], bqkv [3H] -> out [T, H]: the
+// QKV projection and the attention in one launch.  head_dim 32, H = 384 (12 heads), every
+// sentence <= 128 tokens; -1 otherwise (the caller runs the GEMM + attention pair).
+int symb_qkv_attention(const void* X, const void* Wqkv, const float* bqkv, const int32_t* cu, int B,
+                       int max_len, int n_heads, int head_dim, void* out, hipStream_t st) {
+  if (B <= 0) return 0;
+  if (head_dim != 32 || n_heads != 12 || max_len > 128 || max_len <= 0) return -1;
+  const float scale_log2 = 1.4426950408889634f / sqrtf((float)head_dim);
+hipLaunchKernelGGL((qkv_attn_kernel<12>), dim3(B), dim3(512), 0, st, (const __bf16*)X,
+                     (const __bf16*)Wqkv, bqkv, cu, scale_log2, (__bf16*)out, B);
+  return (int)hipGetLastError();
+}
 
 // 8 waves (one workgroup per <=128-token sentence and head) with 64-key tiles: 256 x 128 tokens,
 // 12 heads: D=32 40.5 -> 34.0 us, D=64 52.2 -> 43.1 us vs 4 waves (profiles/r1_attn/attn_waves.json)

@@ -43,6 +43,12 @@ int symb_attention(const void* qkv, int ld_qkv, const int32_t* cu, int B, int ma
                    void* oscale = nullptr);
 int symb_topk_geometry(int D, int kmax, int* lists, int* queries_per_blk);
 int symb_attention_config(int waves, int kvt, int xcd);
+int symb_qkv_attention(const void* X, const void* Wqkv, const float* bqkv, const int32_t* cu, int B,
+                       int max_len, int n_heads, int head_dim, void* out, hipStream_t st);
+// The QKV projection fused into the attention (attention.hip qkv_attn_kernel) for 384-wide,
+// 32-dim-head bf16 layers whose sentences fit 128 tokens, above the small-M limit (1, default);
+// 0: the QKV GEMM + attention pair.
+static int g_qkv_attn = 1;
 int symb_index_scan(const void* X, int n_valid, int D, int rows_per_blk, int n_rblk,
                     const void* Q, int NQ, int kmax, float* cand_s, int* cand_i, hipStream_t st,
                     int ns, int aux, const float* thr_init, int xcd,
@@ -314,12 +320,21 @@ class EncoderRuntime {
         continue;
       }
       h_quantized = false;
-      check(symb_gemm(EPI_BIAS, P<void>(h), H, P<void>(L.wqkv), H, P<float>(L.bqkv), nullptr, 0,
-                      nullptr, nullptr, 0.f, P<void>(qkv), 3 * H, T, 3 * H, H, st),
-            "qkv gemm");
-      check(symb_attention(P<void>(qkv), 3 * H, P<int32_t>(cu), B, max_len, nh_, hd_,
-                           P<void>(ctx), H, st),
-            "attention");
+      // the QKV activation never leaves the CU: one launch per layer for short-sentence batches
+      const bool fused_qkv = g_qkv_attn && H == 384 && hd_ == 32 && nh_ == 12 && max_len <= 128 &&
+                             T > symb_gemm_skinny_max_m();
+      if (fused_qkv) {
+        check(symb_qkv_attention(P<void>(h), P<void>(L.wqkv), P<float>(L.bqkv), P<int32_t>(cu), B,
+                                 max_len, nh_, hd_, P<void>(ctx), st),
+              "qkv+attention");
+      } else {
+        check(symb_gemm(EPI_BIAS, P<void>(h), H, P<void>(L.wqkv), H, P<float>(L.bqkv), nullptr,
+                        0, nullptr, nullptr, 0.f, P<void>(qkv), 3 * H, T, 3 * H, H, st),
+              "qkv gemm");
+        check(symb_attention(P<void>(qkv), 3 * H, P<int32_t>(cu), B, max_len, nh_, hd_,
+                             P<void>(ctx), H, st),
+              "attention");
+      }
       // the fused FFN block (mlp_fused.hip) for 384 x 1536 layers above the small-M limit
       const bool fused_ffn = g_mlp_fused && H == 384 && FF_ == 1536 && T > symb_gemm_skinny_max_m();
       if (fuse_ln) {
@@ -550,6 +565,17 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("qkv"), py::arg("ld_qkv"), py::arg("cu"), py::arg("B"), py::arg("max_len"),
      py::arg("n_heads"), py::arg("head_dim"), py::arg("out"), py::arg("ld_out"), py::arg("st"),
      py::arg("oscale") = 0);
+  m.def("qkv_attention", [](uptr X, uptr Wqkv, uptr bqkv, uptr cu, int B, int max_len,
+                            int n_heads, int head_dim, uptr out, uptr st) {
+    check(symb_qkv_attention(P<void>(X), P<void>(Wqkv), P<float>(bqkv), P<int32_t>(cu), B, max_len,
+                             n_heads, head_dim, P<void>(out), S(st)),
+          "qkv_attention");
+  }, py::arg("X"), py::arg("Wqkv"), py::arg("bqkv"), py::arg("cu"), py::arg("B"),
+     py::arg("max_len"), py::arg("n_heads"), py::arg("head_dim"), py::arg("out"), py::arg("st"));
+  m.def("qkv_attn_config", [](int mode) {   // 0: QKV GEMM + attention, 1: fused (default)
+    if (mode < 0 || mode > 1) throw std::invalid_argument("qkv_attn_config: mode 0 or 1");
+    g_qkv_attn = mode;
+  });
   m.def("topk_geometry", [](int D, int kmax) {
     int lists = 0, qpb = 0;
     check(symb_topk_geometry(D, kmax, &lists, &qpb), "topk_geometry");

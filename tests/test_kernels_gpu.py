@@ -332,6 +332,45 @@ def test_attention_varlen(D, nh, lens, waves, kvt, xcd):
     _close(out, ref, atol=2e-2, rtol=2e-2, what="attention")
 
 
+@pytest.mark.parametrize("lens", [[1, 7, 64, 65, 100, 128, 3, 128, 17],   # every tile shape
+                                  [128] * 40,                              # full sentences
+                                  [2, 1, 3]])
+def test_qkv_attention_fused_matches_oracle(lens):
+    """attention.hip qkv_attn_kernel (the MiniLM layer's QKV projection inside the attention)
+    against the fp32 oracle of projection + attention and against the unfused GEMM + attention
+    pair."""
+    from codename_symbiont_amd.ops.kernels import attention, gemm, qkv_attention, EPI_BIAS
+
+    nh, D = 12, 32
+    H = nh * D
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
+    T = int(cu[-1])
+    x = _bf(T, H, seed=11)
+    w = (torch.randn(3 * H, H, generator=torch.Generator().manual_seed(12)) / H ** 0.5).bfloat16().to(DEV)
+    b = (torch.randn(3 * H, generator=torch.Generator().manual_seed(13)) * 0.1).to(DEV)
+    out = qkv_attention(x, w, b, cu, max(lens), nh, D)
+    torch.cuda.synchronize()
+    qkv32 = x.float() @ w.float().t() + b
+    ref = R.attention_ref(qkv32.bfloat16(), cu, nh, D)
+    _close(out, ref, atol=2e-2, rtol=2e-2, what="qkv_attention vs oracle")
+    qkv = gemm(x, w, b, EPI_BIAS)
+    pair = attention(qkv, cu, max(lens), nh, D)
+    _close(out, pair.float(), atol=2e-2, rtol=2e-2, what="qkv_attention vs the unfused pair")
+
+
+def test_qkv_attention_rejects_long_sentences():
+    from codename_symbiont_amd.ops.kernels import qkv_attention
+
+    nh, D = 12, 32
+    H = nh * D
+    cu = torch.tensor([0, 129], dtype=torch.int32, device=DEV)
+    x = _bf(129, H, seed=1)
+    w = _bf(3 * H, H, seed=2)
+    b = torch.zeros(3 * H, device=DEV)
+    with pytest.raises(ValueError):   # (the kernel's -1: the caller runs the unfused pair)
+        qkv_attention(x, w, b, cu, 129, nh, D)
+
+
 @pytest.mark.parametrize("H,mode,norm", [(384, "mean", True), (768, "cls", True),
                                          (1024, "mean", False)])
 def test_pool(H, mode, norm):
@@ -2187,8 +2226,11 @@ def test_encoder_graph_replay_matches_eager():
     cfg = get_config("minilm-l6")
     enc = HipEncoder(cfg, seed=4)
     # padding to the token bucket can move a batch across the skinny path's M <= 64 bound, which
-    # changes the fp32 summation order: compare like with like (the skinny path has its own tests)
+    # changes the fp32 summation order: compare like with like (the skinny path has its own tests);
+    # likewise the fused QKV + attention kernel, which the bucketed graph (max_len = its token
+    # bucket) never takes
     hip().gemm_skinny_config(0)
+    hip().qkv_attn_config(0)
     try:
         for B, S, seed in [(1, 9, 0), (3, 40, 1), (1, 200, 2), (8, 30, 3), (3, 17, 4), (32, 50, 5)]:
             b = synthetic_batch(cfg, B, S, seed=seed, varlen=True).to(DEV)
@@ -2201,6 +2243,7 @@ def test_encoder_graph_replay_matches_eager():
             assert torch.equal(gu, eu)
     finally:
         hip().gemm_skinny_config(256)
+        hip().qkv_attn_config(1)
     assert len(enc._graphs) >= 4
 
 
