@@ -20,6 +20,9 @@
 //    D*2 + 32 bytes.  Both layouts are conflict-free for their reads (checked with the LDS lane-
 //    group rules, then SQ_LDS_BANK_CONFLICT).
 //  * Output O^T: a lane holds 4 consecutive head dims of one query -> 8-byte stores.
+//  * exp2 is the raw v_exp_f32 (__builtin_amdgcn_exp2f): its arguments are <= 0 (or -inf for a
+//    masked key, which it maps to 0), so exp2f's range handling (v_cmp / v_cndmask / v_ldexp
+//    around every exp) is dead weight.
 //  * MX8 (fp8 encoder): the output is emitted as MX fp8 for the out-projection's block-scaled
 //    MFMA -- e4m3 bytes plus one E8M0 exponent per 32 head dims, computed across the 4 lanes that
 //    share a query (a 32-dim block is 2 of a lane's 16-dim output tiles) -- instead of bf16 rows
@@ -126,7 +129,7 @@ __global__ __launch_bounds__(64 * NWAVE) void attn_varlen_kernel(const __bf16* _
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float mn = fmaxf(m, mx);
-    const float alpha = exp2f(m - mn);
+    const float alpha = __builtin_amdgcn_exp2f(m - mn);
     m = mn;
     lsum *= alpha;
 #pragma unroll
@@ -136,7 +139,7 @@ __global__ __launch_bounds__(64 * NWAVE) void attn_varlen_kernel(const __bf16* _
     for (int n = 0; n < NT; ++n)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = exp2f(s[n][r] - mn);
+        const float p = __builtin_amdgcn_exp2f(s[n][r] - mn);
         lsum += p;
         pb[n >> 1][(n & 1) * 4 + r] = (__bf16)p;
       }
@@ -329,6 +332,9 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(const __bf16* __restri
   const uint32_t vbase = (uint32_t)((4 * g + (c16 >> 2)) * VRB + (c16 & 3) * 8);
   const uint32_t lds_kv = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)sKV);
   auto attend = [&](int h, const bf16x8& qf, int kb) {
+    // (the latency-bound half of the interval: its instructions go first on the SIMD, the other
+    // wave's projection MFMAs fill the gaps)
+    __builtin_amdgcn_s_setprio(1);
     const char* Ks = sKV + kb * KVB;
     f32x4 sc[8];
 #pragma unroll
@@ -336,24 +342,26 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(const __bf16* __restri
       const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + (n >> 2) * 64 * KRB + koff[n & 3]);
       sc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
     }
+    if (L < 128) {   // (block-uniform) keys past the sentence
+#pragma unroll
+      for (int n = 0; n < 8; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (n * 16 + 4 * g + r >= L) sc[n][r] = -INFINITY;
+    }
     float mx = -INFINITY;
 #pragma unroll
-    for (int n = 0; n < 8; ++n)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float v = (n * 16 + 4 * g + r) < L ? sc[n][r] * scale_log2 : -INFINITY;
-        sc[n][r] = v;
-        mx = fmaxf(mx, v);
-      }
+    for (int n = 0; n < 8; ++n) mx = fmaxf(mx, fmaxf(fmaxf(sc[n][0], sc[n][1]), fmaxf(sc[n][2], sc[n][3])));
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mxs = mx * scale_log2;
     float lsum = 0.f;
     bf16x8 pb[4];
 #pragma unroll
     for (int n = 0; n < 8; ++n)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = exp2f(sc[n][r] - mx);
+        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[n][r], scale_log2, -mxs));
         lsum += p;
         pb[n >> 1][(n & 1) * 4 + r] = (__bf16)p;
       }
@@ -384,6 +392,7 @@ __global__ __launch_bounds__(512, 1) void qkv_attn_kernel(const __bf16* __restri
         *reinterpret_cast<bf16x4*>(op + d * 16) = v;
       }
     }
+    __builtin_amdgcn_s_setprio(0);
   };
 
   bf16x8 q_cur, q_next;
