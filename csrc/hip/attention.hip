@@ -431,7 +431,7 @@ int symb_qkv_attention(const void* X, const void* Wqkv, const float* bqkv, const
   if (B <= 0) return 0;
   if (head_dim != 32 || n_heads != 12 || max_len > 128 || max_len <= 0) return -1;
   const float scale_log2 = 1.4426950408889634f / sqrtf((float)head_dim);
-hipLaunchKernelGGL((qkv_attn_kernel<12>), dim3(B), dim3(512), 0, st, (const __bf16*)X,
+  hipLaunchKernelGGL((qkv_attn_kernel<12>), dim3(B), dim3(512), 0, st, (const __bf16*)X,
                      (const __bf16*)Wqkv, bqkv, cu, scale_log2, (__bf16*)out, B);
   return (int)hipGetLastError();
 }
