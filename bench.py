@@ -145,6 +145,8 @@ OPTS = {
                                   "i + 1's encoder (measured slower: 49.0k vs 50.2k at N = 1, "
                                   "equal at simulate_world=8, profiles/r6_step/)"),
     "graph": (1, int, "--mode embed: replay a captured hipGraph of the encoder forward"),
+    "prune_shift_mx4": (0, int, "exact pruned search: the sample density while the MX-fp4 tier "
+                                "applies (0 = the shard default, 2^7)"),
     "prune_sample_shift": (0, int, "exact pruned search: threshold sample = 1 tile in 2^shift "
                                    "(0 = the shard default)"),
     "prune_block_frac": (0.0, float, "exact pruned search: route a row block to the bf16 scan "
@@ -633,6 +635,8 @@ def run_gpu(args, info, comm) -> int:
             synthetic_batch(cfg, n, S, seed=seed).to(dev))[1].clone())
         shard.mq_stats = (os.environ.get("SYMB_MQ_STATS", "0") not in ("", "0")
                           or args.mode == "search")
+        if args.prune_shift_mx4:
+            shard.PRUNE_TILE_SHIFT_MX4 = args.prune_shift_mx4
         if args.prune_sample_shift:
             shard.PRUNE_TILE_SHIFT = shard.PRUNE_TILE_SHIFT_SPLIT = args.prune_sample_shift
             shard.PRUNE_TILE_SHIFT_MX4 = args.prune_sample_shift
