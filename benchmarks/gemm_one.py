@@ -29,7 +29,6 @@ def main():
     ap.add_argument("--tile", type=int, default=3)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--torch", action="store_true")
-    ap.add_argument("--pp", type=int, default=0, help="256-row tiles main loop: 0 8-wave 2-stage, 1 ping-pong, 2 4-wave 2-stage")
     ap.add_argument("--lt", type=int, default=0,
                     help="hipBLASLt route for plain projections (gemm_lt_config: 0 off, 1 auto)")
     a = ap.parse_args()
@@ -44,7 +43,6 @@ def main():
     y = torch.empty(a.m, a.n, device="cuda", dtype=torch.bfloat16)
     hip().gemm_config(128, a.tile, 8)
     hip().gemm_lt_config(a.lt)
-    hip().gemm_pp_config(a.pp)
     f = (lambda: torch.matmul(x, w.t(), out=y)) if a.torch else (lambda: K.gemm(x, w, b, a.epi, r, out=y))
     for _ in range(3):
         f()
@@ -56,7 +54,7 @@ def main():
     e.record()
     torch.cuda.synchronize()
     ms = s.elapsed_time(e) / a.iters
-    print(json.dumps({"lt": a.lt, "pp": a.pp, "m": a.m, "n": a.n, "k": a.k, "epi": a.epi, "tile": a.tile, "torch": a.torch,
+    print(json.dumps({"lt": a.lt, "m": a.m, "n": a.n, "k": a.k, "epi": a.epi, "tile": a.tile, "torch": a.torch,
                       "ms": round(ms, 4), "TFLOPs": round(2 * a.m * a.n * a.k / ms / 1e9)}))
 
 

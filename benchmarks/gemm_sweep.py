@@ -3,10 +3,9 @@
 
     python benchmarks/gemm_sweep.py [--models bge-base,e5-large] [--variants t3,t9,lt,torch]
 
-Variants: tN / pN / qN = symb_gemm with tile mode N (3 = auto with the 256x192 tile, 10 = the
-round-3 auto rule, 2 = the 256x256 tile wherever N % 256 == 0), hipBLASLt route off, and for the
-256-row tiles the 8-wave 2-stage / 8-wave ping-pong / 4-wave 2-stage main loop (gemm_pp_config
-0 / 1 / 2); lt = the hipBLASLt route for the plain projections (the default);
+Variants: tN = symb_gemm with tile mode N (3 = auto with the 256x192 tile, 10 = the round-3
+auto rule, 2 = the 256x256 tile wherever N % 256 == 0), hipBLASLt route off; lt = the hipBLASLt
+route for the plain projections (round-3 default);
 torch = torch.matmul (hipBLASLt, no epilogue).
 Operands are random (the clock the chip holds depends on the data).  One JSON line per
 (shape, variant): median / min us over the rounds and TFLOP/s at the median.
@@ -62,9 +61,9 @@ def main():
                     return lambda: (hip().gemm_config(128, 10, 8),
                                     hip().gemm_lt_config(1), K.gemm(x, w, b, epi, r, out=y),
                                     hip().gemm_lt_config(0))
-                t, pp = int(v[1:]), {"t": 0, "p": 1, "q": 2}[v[0]]
+                t = int(v[1:])
                 return lambda: (hip().gemm_config(128, t, 8), hip().gemm_lt_config(0),
-                                hip().gemm_pp_config(pp), K.gemm(x, w, b, epi, r, out=y))
+                                K.gemm(x, w, b, epi, r, out=y))
 
             fns = {v: mk(v) for v in a.variants.split(",")}
             times = {v: [] for v in fns}
@@ -89,7 +88,6 @@ def main():
                                   "TFLOPs": round(2 * a.m * n * k / med / 1e6)}), flush=True)
     hip().gemm_config(128, 3, 8)
     hip().gemm_lt_config(1)
-    hip().gemm_pp_config(0)
 
 
 if __name__ == "__main__":

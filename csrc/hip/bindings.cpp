@@ -151,7 +151,6 @@ int symb_prune_qprep(const void* Q, int NQ, int dim, const float* pre_s, const f
                      float thr_margin, const float* bounds, void* Q8, float* sq, float* T,
                      float* thr, hipStream_t st);
 int symb_gemm_lt_config(int mode);
-int symb_gemm_pp_config(int mode);
 int symb_mfma_f8f6f4_probe(const int* a, const int* b, const int* sa, const int* sb, float* out,
                            int fmt, hipStream_t st);
 int symb_gemm_lt_plans();
@@ -797,8 +796,6 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gemm_lt_config", [](int mode) { check(symb_gemm_lt_config(mode), "gemm_lt_config"); },
         py::arg("mode"));
   m.def("gemm_lt_plans", []() { return symb_gemm_lt_plans(); });
-  m.def("gemm_pp_config", [](int mode) { check(symb_gemm_pp_config(mode), "gemm_pp_config"); },
-        py::arg("mode"));
   m.def("mq_config", [](int aux) { check(symb_mq_config(aux), "mq_config"); }, py::arg("aux"));
   m.def("mq_queries_per_blk", [](int sets, int rsplit) { return symb_mq_queries_per_blk(sets, rsplit); },
         py::arg("sets") = 4, py::arg("rsplit") = 1);

@@ -132,17 +132,6 @@ SYMB_DMA_ASM(dma16_asm, "global_load_lds_dwordx4")
 SYMB_DMA_ASM(dma4_asm, "global_load_lds_dword")
 #undef SYMB_DMA_ASM
 
-// dma16_asm with a wave-uniform 64-bit base in SGPRs and a 32-bit per-lane byte offset (the
-// SADDR form): one VGPR per piece instead of a 64-bit address pair.
-__device__ __forceinline__ void dma16_saddr(const void* base, uint32_t voff, uint32_t lds) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
-               "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(voff), "s"(base), "s"(__builtin_amdgcn_readfirstlane(lds))
-               : "memory");
-}
-
 // Raise a kernel's dynamic-LDS limit (hipFuncAttributeMaxDynamicSharedMemorySize) before its
 // first launch ON EACH DEVICE: the attribute is per device, so a process driving several GPUs
 // must set it once per device, not once per process.  One bit per device id per kernel.

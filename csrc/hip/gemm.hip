@@ -94,19 +94,8 @@ __device__ __forceinline__ int2 pack_e4m3x8(const float (&y)[8], int ex) {
 // row into LDS; ln_eps is the LayerNorm epsilon.
 enum { LNF_FOLD = 1, LNF_RESLN = 2, LNF_STATS = 4 };
 
-// PP = true (bf16 256-row tiles, 8 waves as 2 x 4): the ping-pong main loop.  The 2-stage loop
-// below drains its LDS-DMA (vmcnt(0) + __syncthreads) once per k-tile, so every k-tile waits a
-// full L2 round trip for a 48-64 KiB stage with the MFMA pipes idle (~1.9 us per k-tile against
-// ~0.7 us of MFMA work at M = 32768, profiles/r6_gemm).  In the ping-pong form the two wave rows
-// (wm = 0: waves 0-3, wm = 1: waves 4-7 -- one of each on every SIMD) run one barrier slot apart:
-// in every slot one wave of each SIMD issues its k-tile's 64 MFMAs while the other reads its
-// next k-tile's fragments from LDS, so the SIMD's MFMA pipe never waits for LDS reads.  Each
-// row's A half is private to it, so a row refills its own A half of buffer t & 1 one slot after
-// reading it; W sits in a 3-deep ring that row 1 refills in its read slots.  Every refill goes
-// out about three slots before its first reader, and every wait inside the k-loop is counted:
-// the pieces issued after the one a slot needs stay in flight.
 template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, int NSTAGE = 2, bool F8 = false,
-          bool AMX = false, int LNF = 0, bool PP = false>
+          bool AMX = false, int LNF = 0>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
     const void* __restrict__ Av, int lda, const void* __restrict__ Wv, int ldw,
     const float* __restrict__ bias, const __bf16* __restrict__ R, int ldr,
@@ -244,141 +233,6 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
     for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   constexpr int LOADS = (BM * 8) / NT + (BN * 8) / NT;  // glds per thread per stage
-  if constexpr (PP) {
-    static_assert(BM == 256 && WAVES_M == 2 && WAVES_N == 4 && NSTAGE == 2 && !F8,
-                  "ping-pong: 256-row bf16 tiles, 8 waves as 2 x 4");
-    static_assert(BN % 32 == 0 && (2 * BM + 3 * BN) * 128 <= 160 * 1024, "ping-pong LDS");
-    constexpr int NB = BN / 32;                      // W pieces per thread of one wave row
-    // LDS: A k-tiles in 2 buffers (each wave row's half private to it), W k-tiles in 3
-    char* const sAbase = smem;
-    char* const sBbase = smem + 2 * BM * 128;
-    // barrier that no memory access or MFMA is scheduled across
-    auto bar = [&]() {
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    const int gtid = tid & 255, gw = wave & 3;       // thread / wave within the wave row
-    // the wave row as a scalar: every branch on it below is a uniform (SCC) branch, never an
-    // exec mask -- a masked s_barrier / s_waitcnt would still execute
-    const int prow = __builtin_amdgcn_readfirstlane(wm);
-    // (inline-asm DMA throughout: hipcc neither counts it nor puts its conservative vmcnt(0) in
-    // front of the ds_reads, which would drain the refills in flight.  32-bit per-lane offsets
-    // off an SGPR base -- the host keeps M * lda and N * ldw under 2^31 bytes -- hold the pieces'
-    // addresses in one VGPR each)
-    // A rows half*128 .. +128 of k-tile kt (one wave row: 4 pieces per thread)
-    auto issue_a = [&](int kt, int half) {
-      char* sA = sAbase + (kt & 1) * (BM * 128) + half * (128 * 128);
-      const size_t k0 = (size_t)kt * 128;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int s = i * 256 + gtid;
-        const int row = s >> 3, pc = s & 7, c = pc ^ ((row >> 1) & 7);
-        const int grow = min(m0 + half * 128 + row, M - 1);
-        dma16_saddr(A + k0, (uint32_t)(grow * lda * ES + c * 16), lds_addr(sA + (i * 256 + gw * 64) * 16));
-      }
-    };
-    // all BN rows of W for k-tile kt into W buffer kt % 3 (one wave row: NB pieces per thread)
-    auto issue_b = [&](int kt) {
-      char* sB = sBbase + (kt % 3) * (BN * 128);
-      const size_t k0 = (size_t)kt * 128;
-#pragma unroll
-      for (int i = 0; i < NB; ++i) {
-        const int s = i * 256 + gtid;
-        const int row = s >> 3, pc = s & 7, c = pc ^ ((row >> 1) & 7);
-        dma16_saddr(W + k0, (uint32_t)((n0 + row) * ldw * ES + c * 16), lds_addr(sB + (i * 256 + gw * 64) * 16));
-      }
-    };
-    // Issue order and waits.  Row 0 owns A rows 0-127: A0(t + 2) in its compute slot t, and at
-    // the end of that slot vmcnt(4) retires A0(t + 1).  Row 1 owns A rows 128-255 and W:
-    // B(s + 2) in its read slot s (W buffer (s - 1) % 3, whose last reader was row 1's read slot
-    // s - 1), A1(s + 2) in its compute slot s.  So row 1's pieces go out as ... B(s + 1),
-    // A1(s + 1), B(s + 2), A1(s + 2) ..., and at the end of read slot s it retires B(s + 1) (row
-    // 0 reads k-tile s + 1 in the next slot), at the end of compute slot s A1(s + 1) (its own
-    // next read), each time with the younger A1 / B pieces left in flight.
-    // prologue: row 0 A0(0), A0(1); row 1 A1(0), B(0), B(1), A1(1); k-tile 0 retired
-    if (prow == 0) {
-      issue_a(0, 0);
-      if (KT > 1) {
-        issue_a(1, 0);
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-    } else {
-      issue_a(0, 1);
-      issue_b(0);
-      if (KT > 1) {
-        issue_b(1);
-        issue_a(1, 1);
-        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(4 + NB) : "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-    }
-    bar();
-    if (prow == 1) bar();                            // row 1 runs one slot behind
-#pragma unroll 1
-    for (int kt = 0; kt < KT; ++kt) {
-      // read slot: row 1 first refills W two k-tiles ahead; this k-tile's fragments (both k
-      // halves) into registers
-      if (prow == 1 && kt + 2 < KT) issue_b(kt + 2);
-      const char* sA = sAbase + (kt & 1) * (BM * 128);
-      const char* sB = sBbase + (kt % 3) * (BN * 128);
-      bf16x8 a[2][RM], b[2][RN];
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int chunk = kk * 4 + (lane >> 4);
-#pragma unroll
-        for (int j = 0; j < RN; ++j)
-          b[kk][j] = *reinterpret_cast<const bf16x8*>(sB + swz_off(wn * WTN + j * 16 + (lane & 15), chunk));
-#pragma unroll
-        for (int i = 0; i < RM; ++i)
-          a[kk][i] = *reinterpret_cast<const bf16x8*>(sA + swz_off(wm * WTM + i * 16 + (lane & 15), chunk));
-      }
-      // the reads are done before the slot ends (refills of these buffers follow it); row 1
-      // retires B(kt + 1), leaving A1(kt + 1) and B(kt + 2) in flight
-      if (prow == 1) {
-        if (kt + 2 < KT)
-          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(4 + NB) : "memory");
-        else if (kt + 1 < KT)
-          asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-        else
-          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      }
-      bar();
-      // compute slot: refill this A buffer's half with k-tile kt + 2, then the k-tile's MFMAs
-      const bool refill = kt + 2 < KT;
-      if (refill) issue_a(kt + 2, prow);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int i = 0; i < RM; ++i)
-#pragma unroll
-          for (int j = 0; j < RN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kk][i], b[kk][j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_sched_barrier(0);
-      // retire this row's A half of k-tile kt + 1 (row 1: with B(kt + 2), leaving the pieces
-      // issued this slot in flight)
-      if (refill) {
-        if (prow == 0)
-          asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else
-          asm volatile("s_waitcnt vmcnt(%0)" ::"i"(4 + NB) : "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      bar();
-    }
-    if (prow == 0) bar();                            // every wave ends on the same barrier count
-  } else {
   stage(0, 0);
 #pragma unroll
   for (int p = 1; p < NSTAGE - 1; ++p)
@@ -475,7 +329,6 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_kernel(
       }
     }
   }
-  }  // (PP)
 
   // ---- epilogue: fp32 tile -> LDS (padded rows) -> row-contiguous 16-byte stores ----
   // A tile whose fp32 image does not fit LDS (256-row tiles, row-complete LN tiles) is emitted
@@ -660,23 +513,22 @@ struct LnArgs {
 };
 
 template <int BM, int BN, int WM, int WN, int EPI, int NSTAGE = 2, bool F8 = false,
-          bool AMX = false, int LNF = 0, bool PP = false>
+          bool AMX = false, int LNF = 0>
 static int launch_cfg(const void* A, int lda, const void* W, int ldw, const float* bias,
                       const __bf16* R, int ldr, const float* g, const float* b, float eps,
                       __bf16* C, int ldc, int M, int N, int K, hipStream_t st,
                       const float* sa = nullptr, const float* sw = nullptr,
                       const uint8_t* ascale = nullptr, uint8_t* cscale = nullptr,
                       const LnArgs& ln = LnArgs()) {
-  auto kern = gemm_bf16_kernel<BM, BN, WM, WN, EPI, NSTAGE, F8, AMX, LNF, PP>;
-  constexpr int main_bytes = PP ? (2 * BM + 3 * BN) * 128
-                                : NSTAGE * ((BM + BN) * 128 + (AMX ? BM * 4 : 0));
+  auto kern = gemm_bf16_kernel<BM, BN, WM, WN, EPI, NSTAGE, F8, AMX, LNF>;
+  constexpr int main_bytes = NSTAGE * ((BM + BN) * 128 + (AMX ? BM * 4 : 0));
   constexpr int full_epi = BM * (BN + 4) * 4;
   constexpr int passes = full_epi > 160 * 1024 ? WM : 1;
   constexpr int epi_bytes = (BM / passes) * (BN + 4) * 4 +
                             ((LNF & (LNF_FOLD | LNF_RESLN)) ? (BM / passes) * 8 * 17 : 0);
   constexpr int lds = main_bytes > epi_bytes ? main_bytes : epi_bytes;
   static_assert(lds <= 160 * 1024, "LDS");
-  set_max_lds<gemm_bf16_kernel<BM, BN, WM, WN, EPI, NSTAGE, F8, AMX, LNF, PP>>(lds);
+  set_max_lds<gemm_bf16_kernel<BM, BN, WM, WN, EPI, NSTAGE, F8, AMX, LNF>>(lds);
   const int nwg = ((M + BM - 1) / BM) * (N / BN);
   hipLaunchKernelGGL(kern, dim3(nwg), dim3(64 * WM * WN), lds, st, A, lda, W, ldw, bias, R, ldr,
                      g, b, eps, C, ldc, M, N, K, sa, sw, g_group_m, ascale, cscale, ln.st_in,
@@ -705,15 +557,6 @@ static int g_resln_bm = 128;
 // without partials or a fix-up (a deep-ring kernel with last-wave split-K was built and measured
 // slower on every shape: profiles/r4_gemm/).
 static int g_tile = 3;
-// Main loop of the 256-row big tiles: 0 = the 2-stage loop, 8 waves of 128 x BN/4; 1 = ping-pong
-// (gemm_bf16_kernel PP), 8 waves; 2 = the 2-stage loop with 4 waves of 128 x BN/2 (one
-// 512-register wave per SIMD, accumulators in AGPRs).
-static int g_gemm_pp = 0;
-int symb_gemm_pp_config(int mode) {
-  if (mode < 0 || mode > 2) return -1;
-  g_gemm_pp = mode;
-  return 0;
-}
 static int big_tile_bn(int tile, int M, int N, int K) {
   if (tile == 2) return N % 256 == 0 ? 256 : 0;
   if (tile != 3 && tile != 10) return 0;
@@ -820,19 +663,9 @@ int symb_gemm(int epi, const void* A, int lda, const void* W, int ldw, const flo
     const int rc = symb_gemm_lt(epi, A, lda, W, ldw, bias, R, ldr, C, ldc, M, N, K, st);
     if (rc != -1 && rc != -2) return rc;   // 0, or a HIP error; else this file's kernels
   }
-  // (the ping-pong loop addresses A and W with 32-bit byte offsets)
-  const bool pp_ok = (long)M * lda * 2 < (1l << 31) && (long)N * ldw * 2 < (1l << 31);
   if (const int bn = big_tile_bn(g_tile, M, N, K)) {
-#define SYMB_G(E, BN_)                                                                           \
-  (g_gemm_pp == 1 && pp_ok                                                                        \
-       ? launch_cfg<256, BN_, 2, 4, E, 2, false, false, 0, true>(a, lda, w, ldw, bias, r, ldr,     \
-                                                                 gamma, beta, eps, c, ldc, M, N, \
-                                                                 K, st)                          \
-   : g_gemm_pp == 2                                                                              \
-       ? launch_cfg<256, BN_, 2, 2, E>(a, lda, w, ldw, bias, r, ldr, gamma, beta, eps, c, ldc, M, \
-                                       N, K, st)                                                 \
-       : launch_cfg<256, BN_, 2, 4, E>(a, lda, w, ldw, bias, r, ldr, gamma, beta, eps, c, ldc, M, \
-                                       N, K, st))
+#define SYMB_G(E, BN_) launch_cfg<256, BN_, 2, 4, E>(a, lda, w, ldw, bias, r, ldr, gamma, beta, eps, \
+                                                    c, ldc, M, N, K, st)
     switch (epi) {
       case EPI_BIAS: return bn == 256 ? SYMB_G(EPI_BIAS, 256) : SYMB_G(EPI_BIAS, 192);
       case EPI_GELU: return bn == 256 ? SYMB_G(EPI_GELU, 256) : SYMB_G(EPI_GELU, 192);
@@ -891,23 +724,6 @@ static int launch_ln(int bn, bool small, const void* A, int lda, const void* W, 
                      const float* bias, const __bf16* R, int ldr, const float* g, const float* b,
                      float eps, __bf16* C, int ldc, int M, int N, int K, hipStream_t st,
                      const LnArgs& ln) {
-  const bool pp = g_gemm_pp == 1 && (long)M * lda * 2 < (1l << 31) && (long)N * ldw * 2 < (1l << 31);
-  if (bn == 256 && g_gemm_pp == 2)
-    return launch_cfg<256, 256, 2, 2, EPI, 2, false, false, LNF>(A, lda, W, ldw, bias, R, ldr, g, b,
-                                                                 eps, C, ldc, M, N, K, st, nullptr,
-                                                                 nullptr, nullptr, nullptr, ln);
-  if (bn == 192 && g_gemm_pp == 2)
-    return launch_cfg<256, 192, 2, 2, EPI, 2, false, false, LNF>(A, lda, W, ldw, bias, R, ldr, g, b,
-                                                                 eps, C, ldc, M, N, K, st, nullptr,
-                                                                 nullptr, nullptr, nullptr, ln);
-  if (bn == 256 && pp)
-    return launch_cfg<256, 256, 2, 4, EPI, 2, false, false, LNF, true>(
-        A, lda, W, ldw, bias, R, ldr, g, b, eps, C, ldc, M, N, K, st, nullptr, nullptr, nullptr,
-        nullptr, ln);
-  if (bn == 192 && pp)
-    return launch_cfg<256, 192, 2, 4, EPI, 2, false, false, LNF, true>(
-        A, lda, W, ldw, bias, R, ldr, g, b, eps, C, ldc, M, N, K, st, nullptr, nullptr, nullptr,
-        nullptr, ln);
   if (bn == 256)
     return launch_cfg<256, 256, 2, 4, EPI, 2, false, false, LNF>(A, lda, W, ldw, bias, R, ldr, g, b,
                                                                  eps, C, ldc, M, N, K, st, nullptr,
