@@ -2,6 +2,7 @@
 # Round 6, run y: the ping-pong main loop of the 256-row GEMM tiles -- exactness (oracle and
 # bit-identity with the 2-stage loop), then the bge / e5 shapes: 2-stage (t3), ping-pong (p3),
 # 256 x 256 ping-pong (p2), hipBLASLt (lt), interleaved in one process.
+# (Ran against commit d5ba24c; gemm_pp_config and the p / q sweep variants were removed after it.)
 set -o pipefail
 O=gpurun_out/r6_y
 mkdir -p $O

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round 6, run z: counters of the 256-row GEMM tiles' 2-stage vs ping-pong main loops and of
 # hipBLASLt on e5-large FFN2 (M 32768, N 1024, K 4096: the longest k-loop).
+# (Ran against commit d5ba24c; gemm_pp_config and the p / q sweep variants were removed after it.)
 set -o pipefail
 O=gpurun_out/r6_z
 mkdir -p $O
