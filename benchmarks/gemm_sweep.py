@@ -4,8 +4,9 @@
     python benchmarks/gemm_sweep.py [--models bge-base,e5-large] [--variants t3,t9,lt,torch]
 
 Variants: tN = symb_gemm with tile mode N (3 = auto with the 256x192 tile, 10 = the round-3
-auto rule, 2 = the 256x256 tile wherever N % 256 == 0), hipBLASLt route off; lt = the hipBLASLt
-route for the plain projections (round-3 default);
+auto rule, 2 = the 256x256 tile wherever N % 256 == 0), hipBLASLt route off; tNgG = the same with
+a G-row grouped tile order (default 8); lt = the hipBLASLt route for the plain projections (the
+default);
 torch = torch.matmul (hipBLASLt, no epilogue).
 Operands are random (the clock the chip holds depends on the data).  One JSON line per
 (shape, variant): median / min us over the rounds and TFLOP/s at the median.
@@ -61,8 +62,9 @@ def main():
                     return lambda: (hip().gemm_config(128, 10, 8),
                                     hip().gemm_lt_config(1), K.gemm(x, w, b, epi, r, out=y),
                                     hip().gemm_lt_config(0))
-                t = int(v[1:])
-                return lambda: (hip().gemm_config(128, t, 8), hip().gemm_lt_config(0),
+                t, _, gm = v[1:].partition("g")     # tN or tNgG (grouped tile order, G rows)
+                t, gm = int(t), int(gm or 8)
+                return lambda: (hip().gemm_config(128, t, gm), hip().gemm_lt_config(0),
                                 K.gemm(x, w, b, epi, r, out=y))
 
             fns = {v: mk(v) for v in a.variants.split(",")}
